@@ -1,0 +1,653 @@
+// Classification hot paths for gfx950 (SURVEY §2.10 kernels K1, K2, K4, K5, K6, K8).
+//
+//  * tmx::range_flag          — device-side "any value outside [0,1] (or NaN)" flag; replaces the reference's
+//                               host-synchronising `if not torch.all((p>=0)*(p<=1))` (stat_scores.py:104).
+//  * tmx::bincount            — LDS-privatised int32 histogram, one int64 global atomic per non-empty bin per
+//                               workgroup (replaces the deterministic-mode per-bin Python loop, data.py:194).
+//  * tmx::mc_confmat_update   — fused argmax-over-C + (target, pred) histogram into an int64 [C, C] state
+//                               (stat_scores.py:405-418, confusion_matrix.py:306-337).  One wave per row for
+//                               large C (16-B vector loads), one thread per row for small C; LDS-privatised
+//                               confusion matrix when C*C int32 counters fit in 64 KiB.
+//  * tmx::binary_stats_update — one-pass tp/fp/tn/fn per label with the sigmoid-if-needed + threshold rule
+//                               evaluated in the input dtype (stat_scores.py:95-131, 650-681).
+//  * tmx::curve_hist_update   — exact score histogram for 16-bit scores: each (class, label, score-code) is
+//                               counted in an int64 [C, 2, 16384] state.  A bf16/fp16 value in [0, 1] has at
+//                               most 16257 codes and code order == value order, so this reproduces the
+//                               reference's sort-based `_binary_clf_curve` (precision_recall_curve.py:28-80)
+//                               exactly, with a fixed-size, all-reducible state instead of a growing `cat` list.
+//  * tmx::curve_hist_reduce   — per-class AUROC / AP / positive / negative totals from that histogram: one
+//                               workgroup per class, block scan over codes in descending order (K8).
+//  * tmx::binned_curve_update — bucketize (binary search over T thresholds in LDS) + per-(class, label,
+//                               bucket) histogram, then a suffix scan into the reference's [T, C, 2, 2]
+//                               multi-threshold confusion matrix (K5) — O(N*C*log T) instead of O(N*C*T).
+#include "common.h"
+
+namespace tmx {
+
+// =========================================================================================================
+// range flag
+// =========================================================================================================
+template <typename T>
+__global__ void range_flag_kernel(const T* __restrict__ x, int64_t n, int* __restrict__ flag) {
+  bool bad = false;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    float v = to_f32<T>(x[i]);
+    bad |= !(v >= 0.f && v <= 1.f);
+  }
+  unsigned long long m = __ballot(bad);
+  if (m && (threadIdx.x & (kWave - 1)) == 0) atomicOr(flag, 1);
+}
+
+at::Tensor range_flag(const at::Tensor& x_) {
+  auto x = x_.contiguous();
+  auto flag = at::zeros({1}, x.options().dtype(at::kInt));
+  const int64_t n = x.numel();
+  if (n == 0) return flag;
+  const int block = 256;
+  TMX_DISPATCH_FLOAT(x.scalar_type(), "range_flag", [&] {
+    hipLaunchKernelGGL(range_flag_kernel<scalar_t>, grid_for(n, block), block, 0, stream(),
+                       reinterpret_cast<const scalar_t*>(x.data_ptr()), n, flag.data_ptr<int>());
+  });
+  TMX_LAUNCH_CHECK();
+  return flag;
+}
+
+// =========================================================================================================
+// bincount
+// =========================================================================================================
+__global__ void bincount_lds_kernel(const int64_t* __restrict__ x, int64_t n, int nbins, int64_t* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) int s_bins[];
+  for (int b = threadIdx.x; b < nbins; b += blockDim.x) s_bins[b] = 0;
+  __syncthreads();
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t v = x[i];
+    if (v >= 0 && v < nbins) atomicAdd(&s_bins[v], 1);
+  }
+  __syncthreads();
+  for (int b = threadIdx.x; b < nbins; b += blockDim.x) {
+    int c = s_bins[b];
+    if (c) atomic_add_i64(out + b, c);
+  }
+}
+
+__global__ void bincount_global_kernel(const int64_t* __restrict__ x, int64_t n, int64_t nbins, int64_t* __restrict__ out) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t v = x[i];
+    if (v >= 0 && v < nbins) atomic_add_i64(out + v, 1);
+  }
+}
+
+at::Tensor bincount(const at::Tensor& x_, int64_t minlength) {
+  auto x = x_.contiguous().to(at::kLong);
+  auto out = at::zeros({minlength}, x.options().dtype(at::kLong));
+  const int64_t n = x.numel();
+  if (n == 0 || minlength == 0) return out;
+  const int block = 256;
+  if (minlength <= 16384) {
+    const int grid = grid_for(n, block * 8, 1024);
+    hipLaunchKernelGGL(bincount_lds_kernel, grid, block, minlength * sizeof(int), stream(), x.data_ptr<int64_t>(), n,
+                       (int)minlength, out.data_ptr<int64_t>());
+  } else {
+    hipLaunchKernelGGL(bincount_global_kernel, grid_for(n, block), block, 0, stream(), x.data_ptr<int64_t>(), n,
+                       minlength, out.data_ptr<int64_t>());
+  }
+  TMX_LAUNCH_CHECK();
+  return out;
+}
+
+// =========================================================================================================
+// multiclass confusion matrix (labels or argmax of scores)
+// =========================================================================================================
+__device__ __forceinline__ void confmat_add(int* s_cm, int64_t* g_cm, bool use_lds, int C, int64_t t, int64_t p) {
+  if (t < 0 || t >= C || p < 0 || p >= C) return;
+  int64_t idx = t * C + p;
+  if (use_lds) atomicAdd(&s_cm[idx], 1);
+  else atomic_add_i64(g_cm + idx, 1);
+}
+
+__device__ __forceinline__ void confmat_flush(int* s_cm, int64_t* g_cm, int C) {
+  __syncthreads();
+  for (int b = threadIdx.x; b < C * C; b += blockDim.x) {
+    int c = s_cm[b];
+    if (c) atomic_add_i64(g_cm + b, c);
+  }
+}
+
+__global__ void mc_confmat_labels_kernel(const int64_t* __restrict__ preds, const int64_t* __restrict__ target, int64_t n,
+                                         int C, int64_t ignore_index, bool has_ignore, bool use_lds, int64_t* __restrict__ cm) {
+  extern __shared__ __attribute__((aligned(16))) int s_cm[];
+  if (use_lds) {
+    for (int b = threadIdx.x; b < C * C; b += blockDim.x) s_cm[b] = 0;
+    __syncthreads();
+  }
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t t = target[i];
+    if (has_ignore && t == ignore_index) continue;
+    confmat_add(s_cm, cm, use_lds, C, t, preds[i]);
+  }
+  if (use_lds) confmat_flush(s_cm, cm, C);
+}
+
+// one thread per row (small C)
+template <typename T>
+__global__ void mc_confmat_argmax_thread_kernel(const T* __restrict__ preds, const int64_t* __restrict__ target, int64_t n,
+                                                int C, int64_t ignore_index, bool has_ignore, bool use_lds,
+                                                int64_t* __restrict__ cm) {
+  extern __shared__ __attribute__((aligned(16))) int s_cm[];
+  if (use_lds) {
+    for (int b = threadIdx.x; b < C * C; b += blockDim.x) s_cm[b] = 0;
+    __syncthreads();
+  }
+  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
+    int64_t t = target[r];
+    if (has_ignore && t == ignore_index) continue;
+    const T* row = preds + r * C;
+    float best = to_f32<T>(row[0]);
+    int bi = 0;
+    for (int c = 1; c < C; ++c) {
+      float v = to_f32<T>(row[c]);
+      if (argmax_better(v, c, best, bi)) { best = v; bi = c; }
+    }
+    confmat_add(s_cm, cm, use_lds, C, t, bi);
+  }
+  if (use_lds) confmat_flush(s_cm, cm, C);
+}
+
+// one wave per row (large C)
+template <typename T>
+__global__ void mc_confmat_argmax_wave_kernel(const T* __restrict__ preds, const int64_t* __restrict__ target, int64_t n,
+                                              int C, int64_t ignore_index, bool has_ignore, bool use_lds,
+                                              int64_t* __restrict__ cm) {
+  extern __shared__ __attribute__((aligned(16))) int s_cm[];
+  if (use_lds) {
+    for (int b = threadIdx.x; b < C * C; b += blockDim.x) s_cm[b] = 0;
+    __syncthreads();
+  }
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / kWave;
+  const int64_t nwaves = (int64_t)gridDim.x * blockDim.x / kWave;
+  for (int64_t r = wave; r < n; r += nwaves) {
+    int64_t t = target[r];
+    if (has_ignore && t == ignore_index) continue;
+    const T* row = preds + r * C;
+    float best = -INFINITY;
+    int bi = C;  // sentinel larger than any index
+    for (int c = lane; c < C; c += kWave) {
+      float v = to_f32<T>(row[c]);
+      if (argmax_better(v, c, best, bi)) { best = v; bi = c; }
+    }
+    wave_argmax(best, bi);
+    if (lane == 0) confmat_add(s_cm, cm, use_lds, C, t, bi);
+  }
+  if (use_lds) confmat_flush(s_cm, cm, C);
+}
+
+// confmat: int64 [C, C] updated in place.  preds: [N] int64 labels or [N, C] float scores.
+void mc_confmat_update(const at::Tensor& preds_, const at::Tensor& target_, at::Tensor& confmat, int64_t ignore_index,
+                       bool has_ignore) {
+  TORCH_CHECK(confmat.is_contiguous() && confmat.scalar_type() == at::kLong, "confmat must be contiguous int64");
+  const int C = static_cast<int>(confmat.size(0));
+  auto target = target_.contiguous().to(at::kLong);
+  const int64_t n = target.numel();
+  if (n == 0) return;
+  const bool use_lds = (int64_t)C * C * 4 <= 64 * 1024;
+  const size_t shm = use_lds ? (size_t)C * C * sizeof(int) : 0;
+  const int block = 256;
+  if (!preds_.is_floating_point()) {
+    auto preds = preds_.contiguous().to(at::kLong);
+    TORCH_CHECK(preds.numel() == n, "preds/target size mismatch");
+    hipLaunchKernelGGL(mc_confmat_labels_kernel, grid_for(n, block * 4, 1024), block, shm, stream(), preds.data_ptr<int64_t>(),
+                       target.data_ptr<int64_t>(), n, C, ignore_index, has_ignore, use_lds, confmat.data_ptr<int64_t>());
+  } else {
+    auto preds = preds_.contiguous();
+    TORCH_CHECK(preds.numel() == n * C, "preds must be [N, C] with C = confmat.size(0)");
+    TMX_DISPATCH_FLOAT(preds.scalar_type(), "mc_confmat_update", [&] {
+      const scalar_t* p = reinterpret_cast<const scalar_t*>(preds.data_ptr());
+      if (C <= 32) {
+        hipLaunchKernelGGL(mc_confmat_argmax_thread_kernel<scalar_t>, grid_for(n, block, 2048), block, shm, stream(), p,
+                           target.data_ptr<int64_t>(), n, C, ignore_index, has_ignore, use_lds, confmat.data_ptr<int64_t>());
+      } else {
+        hipLaunchKernelGGL(mc_confmat_argmax_wave_kernel<scalar_t>, grid_for(n * kWave, block, 2048), block, shm, stream(), p,
+                           target.data_ptr<int64_t>(), n, C, ignore_index, has_ignore, use_lds, confmat.data_ptr<int64_t>());
+      }
+    });
+  }
+  TMX_LAUNCH_CHECK();
+}
+
+// =========================================================================================================
+// binary / multilabel stat scores: counts[L, 4] = (tp, fp, tn, fn) per label
+// preds/target viewed as [N, L, S] (S = flattened extra dims), reduced over N and S.
+// =========================================================================================================
+template <typename T, bool FLOAT_PREDS>
+__global__ void binary_stats_kernel(const T* __restrict__ preds, const int64_t* __restrict__ target, int64_t N, int L,
+                                    int64_t S, float threshold, const int* __restrict__ sigmoid_flag,
+                                    int64_t ignore_index, bool has_ignore, int64_t* __restrict__ counts) {
+  extern __shared__ __attribute__((aligned(16))) int s_cnt[];  // [L][4]
+  for (int b = threadIdx.x; b < 4 * L; b += blockDim.x) s_cnt[b] = 0;
+  __syncthreads();
+  const bool do_sigmoid = FLOAT_PREDS && sigmoid_flag != nullptr && sigmoid_flag[0] != 0;
+  const float thr_rt = round_trip<T>(threshold);
+  const int64_t total = N * L * S;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t t = target[i];
+    if (has_ignore && t == ignore_index) continue;
+    const int l = static_cast<int>((i / S) % L);
+    int p;
+    if constexpr (FLOAT_PREDS) {
+      float v = to_f32<T>(preds[i]);
+      if (do_sigmoid) v = round_trip<T>(1.f / (1.f + expf(-v)));
+      p = v > thr_rt ? 1 : 0;
+    } else {
+      p = static_cast<int>(to_f32<T>(preds[i]) != 0.f);
+    }
+    // (tp, fp, tn, fn)
+    int slot = (t == 1) ? (p ? 0 : 3) : (p ? 1 : 2);
+    if (t == 0 || t == 1) atomicAdd(&s_cnt[l * 4 + slot], 1);
+  }
+  __syncthreads();
+  for (int b = threadIdx.x; b < 4 * L; b += blockDim.x) {
+    int c = s_cnt[b];
+    if (c) atomic_add_i64(counts + b, c);
+  }
+}
+
+template <bool FLOAT_PREDS>
+__global__ void binary_stats_int_kernel(const int64_t* __restrict__ preds, const int64_t* __restrict__ target, int64_t N,
+                                        int L, int64_t S, int64_t ignore_index, bool has_ignore, int64_t* __restrict__ counts) {
+  extern __shared__ __attribute__((aligned(16))) int s_cnt[];
+  for (int b = threadIdx.x; b < 4 * L; b += blockDim.x) s_cnt[b] = 0;
+  __syncthreads();
+  const int64_t total = N * L * S;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t t = target[i];
+    if (has_ignore && t == ignore_index) continue;
+    const int l = static_cast<int>((i / S) % L);
+    int p = preds[i] != 0;
+    int slot = (t == 1) ? (p ? 0 : 3) : (p ? 1 : 2);
+    if (t == 0 || t == 1) atomicAdd(&s_cnt[l * 4 + slot], 1);
+  }
+  __syncthreads();
+  for (int b = threadIdx.x; b < 4 * L; b += blockDim.x) {
+    int c = s_cnt[b];
+    if (c) atomic_add_i64(counts + b, c);
+  }
+}
+
+// counts: int64 [L, 4] updated in place.
+void binary_stats_update(const at::Tensor& preds_, const at::Tensor& target_, at::Tensor& counts, int64_t num_labels,
+                         double threshold, int64_t ignore_index, bool has_ignore) {
+  TORCH_CHECK(counts.is_contiguous() && counts.scalar_type() == at::kLong && counts.numel() == 4 * num_labels);
+  auto target = target_.contiguous().to(at::kLong);
+  const int64_t total = target.numel();
+  if (total == 0) return;
+  const int64_t N = target.size(0);
+  const int L = static_cast<int>(num_labels);
+  const int64_t S = total / (N * L);
+  TORCH_CHECK(N * L * S == total, "target shape incompatible with num_labels");
+  const int block = 256;
+  const size_t shm = 4 * L * sizeof(int);
+  TORCH_CHECK(shm <= 64 * 1024, "too many labels for binary_stats_update");
+  const int grid = grid_for(total, block * 4, 1024);
+  if (preds_.is_floating_point()) {
+    auto preds = preds_.contiguous();
+    auto flag = range_flag(preds);
+    TMX_DISPATCH_FLOAT(preds.scalar_type(), "binary_stats_update", [&] {
+      hipLaunchKernelGGL((binary_stats_kernel<scalar_t, true>), grid, block, shm, stream(),
+                         reinterpret_cast<const scalar_t*>(preds.data_ptr()), target.data_ptr<int64_t>(), N, L, S,
+                         (float)threshold, flag.data_ptr<int>(), ignore_index, has_ignore, counts.data_ptr<int64_t>());
+    });
+  } else {
+    auto preds = preds_.contiguous().to(at::kLong);
+    hipLaunchKernelGGL((binary_stats_int_kernel<false>), grid, block, shm, stream(), preds.data_ptr<int64_t>(),
+                       target.data_ptr<int64_t>(), N, L, S, ignore_index, has_ignore, counts.data_ptr<int64_t>());
+  }
+  TMX_LAUNCH_CHECK();
+}
+
+// =========================================================================================================
+// exact 16-bit score histogram  hist[C][2][kCodes]
+// =========================================================================================================
+constexpr int kCodeBits = 14;
+constexpr int kCodes = 1 << kCodeBits;  // 16384 >= 16257 (bf16 codes in [0,1]) and 15361 (fp16)
+
+template <typename T> __device__ __forceinline__ int score_code(uint16_t b);
+template <> __device__ __forceinline__ int score_code<__hip_bfloat16>(uint16_t b) {
+  if (b == 0x8000) return 0;       // -0.0 == 0.0
+  return b <= 0x3F80 ? b : -1;     // >1, negative or NaN -> dropped
+}
+template <> __device__ __forceinline__ int score_code<__half>(uint16_t b) {
+  if (b == 0x8000) return 0;
+  return b <= 0x3C00 ? b : -1;
+}
+
+__device__ __forceinline__ void hist_add(int64_t* hist, int64_t c, int label, int code) {
+  if (code < 0) return;
+  atomic_add_i64(hist + (((c << 1) + label) << kCodeBits) + code, 1);
+}
+
+// Multiclass: one wave per row.  Softmax (if flagged) is computed in fp32 and rounded to the input dtype,
+// exactly as torch's softmax on a 16-bit tensor stores it; codes are the rounded bit patterns.
+// Optionally also accumulates the argmax confusion matrix (fused AUROC + ConfusionMatrix plan).
+template <typename T, int VPT>
+__global__ void __launch_bounds__(256) curve_hist_mc_kernel(const T* __restrict__ preds, const int64_t* __restrict__ target,
+                                                            int64_t n, int C, const int* __restrict__ softmax_flag,
+                                                            int64_t ignore_index, bool has_ignore, int64_t* __restrict__ hist,
+                                                            int64_t* __restrict__ confmat) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / kWave;
+  const int64_t nwaves = (int64_t)gridDim.x * blockDim.x / kWave;
+  const bool do_softmax = softmax_flag[0] != 0;
+  for (int64_t r = wave; r < n; r += nwaves) {
+    const int64_t t = target[r];
+    if (has_ignore && t == ignore_index) continue;
+    const T* row = preds + r * C;
+    float v[VPT];
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) {
+      int c = lane + j * kWave;
+      v[j] = c < C ? to_f32<T>(row[c]) : -INFINITY;
+    }
+    float m = -INFINITY;
+    int am = C;
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) {
+      int c = lane + j * kWave;
+      if (c < C && argmax_better(v[j], c, m, am)) { m = v[j]; am = c; }
+    }
+    float mx = m;
+    int amx = am;
+    wave_argmax(mx, amx);
+    if (confmat != nullptr && lane == 0 && t >= 0 && t < C && amx < C) atomic_add_i64(confmat + t * C + amx, 1);
+    float inv = 1.f;
+    if (do_softmax) {
+      float s = 0.f;
+#pragma unroll
+      for (int j = 0; j < VPT; ++j) {
+        int c = lane + j * kWave;
+        if (c < C) { v[j] = expf(v[j] - mx); s += v[j]; }
+      }
+      s = wave_sum(s);
+      inv = s;
+    }
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) {
+      int c = lane + j * kWave;
+      if (c < C) {
+        uint16_t b = do_softmax ? round_bits16<T>(v[j] / inv) : bits16<T>(row[c]);
+        hist_add(hist, c, c == t ? 1 : 0, score_code<T>(b));
+      }
+    }
+  }
+}
+
+// Binary / multilabel: element-wise (sigmoid if flagged). preds/target viewed as [N, L, S].
+template <typename T>
+__global__ void curve_hist_ml_kernel(const T* __restrict__ preds, const int64_t* __restrict__ target, int64_t N, int L,
+                                     int64_t S, const int* __restrict__ sigmoid_flag, int64_t ignore_index, bool has_ignore,
+                                     int64_t* __restrict__ hist) {
+  const bool do_sigmoid = sigmoid_flag[0] != 0;
+  const int64_t total = N * L * S;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t t = target[i];
+    if (has_ignore && t == ignore_index) continue;
+    const int l = static_cast<int>((i / S) % L);
+    uint16_t b;
+    if (do_sigmoid) {
+      float x = to_f32<T>(preds[i]);
+      b = round_bits16<T>(1.f / (1.f + expf(-x)));
+    } else {
+      b = bits16<T>(preds[i]);
+    }
+    hist_add(hist, l, t == 1 ? 1 : 0, score_code<T>(b));
+  }
+}
+
+// hist: int64 [C, 2, kCodes] updated in place.
+// task 0 = multiclass (preds [N, C], target [N]); task 1 = binary/multilabel (preds/target [N, L, ...]).
+void curve_hist_update(const at::Tensor& preds_, const at::Tensor& target_, at::Tensor& hist, int64_t task,
+                       int64_t ignore_index, bool has_ignore, c10::optional<at::Tensor> confmat) {
+  TORCH_CHECK(hist.is_contiguous() && hist.scalar_type() == at::kLong && hist.dim() == 3 && hist.size(1) == 2 &&
+              hist.size(2) == kCodes, "hist must be int64 [C, 2, 16384]");
+  auto preds = preds_.contiguous();
+  auto target = target_.contiguous().to(at::kLong);
+  const int C = static_cast<int>(hist.size(0));
+  const int block = 256;
+  auto flag = range_flag(preds);
+  int64_t* cm = nullptr;
+  if (confmat.has_value()) {
+    TORCH_CHECK(confmat->is_contiguous() && confmat->scalar_type() == at::kLong && confmat->numel() == (int64_t)C * C);
+    cm = confmat->data_ptr<int64_t>();
+  }
+  TMX_DISPATCH_HALF(preds.scalar_type(), "curve_hist_update", [&] {
+    const scalar_t* p = reinterpret_cast<const scalar_t*>(preds.data_ptr());
+    if (task == 0) {
+      const int64_t n = target.numel();
+      if (n == 0) return;
+      TORCH_CHECK(preds.numel() == n * C, "preds must be [N, C]");
+      const int grid = grid_for(n * kWave, block, 4096);
+      if (C <= 64 * 4) {
+        hipLaunchKernelGGL((curve_hist_mc_kernel<scalar_t, 4>), grid, block, 0, stream(), p, target.data_ptr<int64_t>(), n, C,
+                           flag.data_ptr<int>(), ignore_index, has_ignore, hist.data_ptr<int64_t>(), cm);
+      } else if (C <= 64 * 16) {
+        hipLaunchKernelGGL((curve_hist_mc_kernel<scalar_t, 16>), grid, block, 0, stream(), p, target.data_ptr<int64_t>(), n, C,
+                           flag.data_ptr<int>(), ignore_index, has_ignore, hist.data_ptr<int64_t>(), cm);
+      } else {
+        TORCH_CHECK(C <= 64 * 64, "curve_hist_update: num_classes > 4096 not supported by the exact histogram path");
+        hipLaunchKernelGGL((curve_hist_mc_kernel<scalar_t, 64>), grid, block, 0, stream(), p, target.data_ptr<int64_t>(), n, C,
+                           flag.data_ptr<int>(), ignore_index, has_ignore, hist.data_ptr<int64_t>(), cm);
+      }
+    } else {
+      const int64_t total = target.numel();
+      if (total == 0) return;
+      TORCH_CHECK(preds.numel() == total, "preds/target size mismatch");
+      const int64_t N = target.size(0);
+      const int64_t S = total / (N * C);
+      TORCH_CHECK(N * C * S == total, "target shape incompatible with num_labels");
+      hipLaunchKernelGGL(curve_hist_ml_kernel<scalar_t>, grid_for(total, block, 4096), block, 0, stream(), p,
+                         target.data_ptr<int64_t>(), N, C, S, flag.data_ptr<int>(), ignore_index, has_ignore,
+                         hist.data_ptr<int64_t>());
+    }
+  });
+  TMX_LAUNCH_CHECK();
+}
+
+// Per-class reduction of the exact histogram (descending code order).
+//   out[c] = {auroc, average_precision, n_pos, n_neg}
+// AUROC = sum_k neg_k * (2*TP_{<k} + pos_k) / (2 * P * N)  (trapezoid over every code; empty codes add 0)
+// AP    = sum_k (pos_k / P) * TP_k / (TP_k + FP_k)
+__global__ void __launch_bounds__(256) curve_hist_reduce_kernel(const int64_t* __restrict__ hist, int K, double* __restrict__ out) {
+  const int c = blockIdx.x;
+  const int64_t* neg = hist + ((int64_t)c * 2 + 0) * K;
+  const int64_t* pos = hist + ((int64_t)c * 2 + 1) * K;
+  const int tid = threadIdx.x;
+  const int per = (K + blockDim.x - 1) / blockDim.x;
+  // thread tid owns descending positions [tid*per, (tid+1)*per) -> codes K-1-pos
+  long long sp = 0, sn = 0;
+  for (int j = 0; j < per; ++j) {
+    int q = tid * per + j;
+    if (q < K) { sp += pos[K - 1 - q]; sn += neg[K - 1 - q]; }
+  }
+  __shared__ long long s_p[256], s_n[256];
+  s_p[tid] = sp; s_n[tid] = sn;
+  __syncthreads();
+  // inclusive Hillis-Steele scan (256 entries)
+  for (int off = 1; off < 256; off <<= 1) {
+    long long ap = tid >= off ? s_p[tid - off] : 0, an = tid >= off ? s_n[tid - off] : 0;
+    __syncthreads();
+    s_p[tid] += ap; s_n[tid] += an;
+    __syncthreads();
+  }
+  const long long P = s_p[255], N = s_n[255];
+  long long tp = tid ? s_p[tid - 1] : 0, fp = tid ? s_n[tid - 1] : 0;
+  double area = 0.0, ap_sum = 0.0;
+  for (int j = 0; j < per; ++j) {
+    int q = tid * per + j;
+    if (q >= K) break;
+    long long pk = pos[K - 1 - q], nk = neg[K - 1 - q];
+    area += (double)nk * (double)(2 * tp + pk);
+    tp += pk; fp += nk;
+    if (pk) ap_sum += (double)pk * ((double)tp / (double)(tp + fp));
+  }
+  __shared__ double s_a[256], s_b[256];
+  s_a[tid] = area; s_b[tid] = ap_sum;
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if (tid < off) { s_a[tid] += s_a[tid + off]; s_b[tid] += s_b[tid + off]; }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    double auc = (P > 0 && N > 0) ? s_a[0] / (2.0 * (double)P * (double)N) : 0.0;
+    double apv = P > 0 ? s_b[0] / (double)P : NAN;
+    out[c * 4 + 0] = auc;
+    out[c * 4 + 1] = apv;
+    out[c * 4 + 2] = (double)P;
+    out[c * 4 + 3] = (double)N;
+  }
+}
+
+at::Tensor curve_hist_reduce(const at::Tensor& hist_) {
+  auto hist = hist_.contiguous();
+  TORCH_CHECK(hist.scalar_type() == at::kLong && hist.dim() == 3 && hist.size(1) == 2);
+  const int C = static_cast<int>(hist.size(0));
+  auto out = at::empty({C, 4}, hist.options().dtype(at::kDouble));
+  if (C == 0) return out;
+  hipLaunchKernelGGL(curve_hist_reduce_kernel, C, 256, 0, stream(), hist.data_ptr<int64_t>(), (int)hist.size(2),
+                     out.data_ptr<double>());
+  TMX_LAUNCH_CHECK();
+  return out;
+}
+
+// =========================================================================================================
+// binned (multi-threshold) curve:  confmat[T, C, 2, 2] += counts
+// bucket b(p) = #thresholds <= p  (p >= thr[i]  <=>  i < b(p));  hist[C][2][T+1] then suffix-sum.
+// =========================================================================================================
+template <typename T, int MODE>  // MODE 0: multiclass rows (softmax), 1: elementwise (sigmoid)
+__global__ void binned_hist_kernel(const T* __restrict__ preds, const int64_t* __restrict__ target, int64_t N, int C,
+                                   int64_t S, const float* __restrict__ thr, int nT, const int* __restrict__ flag,
+                                   int64_t ignore_index, bool has_ignore, int* __restrict__ hist) {
+  extern __shared__ __attribute__((aligned(16))) float s_thr[];
+  for (int i = threadIdx.x; i < nT; i += blockDim.x) s_thr[i] = thr[i];
+  __syncthreads();
+  const bool do_norm = flag[0] != 0;
+  auto bucket = [&](float p) {
+    int lo = 0, hi = nT;  // first index with thr > p
+    while (lo < hi) {
+      int mid = (lo + hi) >> 1;
+      if (s_thr[mid] <= p) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+  };
+  if constexpr (MODE == 0) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / kWave;
+    const int64_t nwaves = (int64_t)gridDim.x * blockDim.x / kWave;
+    for (int64_t r = wave; r < N; r += nwaves) {
+      const int64_t t = target[r];
+      if (has_ignore && t == ignore_index) continue;
+      const T* row = preds + r * C;
+      float mx = -INFINITY, s = 0.f;
+      if (do_norm) {
+        for (int c = lane; c < C; c += kWave) mx = fmaxf(mx, to_f32<T>(row[c]));
+        mx = wave_max(mx);
+        for (int c = lane; c < C; c += kWave) s += expf(to_f32<T>(row[c]) - mx);
+        s = wave_sum(s);
+      }
+      for (int c = lane; c < C; c += kWave) {
+        float v = to_f32<T>(row[c]);
+        if (do_norm) v = round_trip<T>(expf(v - mx) / s);
+        int b = bucket(v);
+        atomicAdd(hist + ((int64_t)c * 2 + (c == t ? 1 : 0)) * (nT + 1) + b, 1);
+      }
+    }
+  } else {
+    const int64_t total = N * C * S;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+      const int64_t t = target[i];
+      if (has_ignore && t == ignore_index) continue;
+      if (t != 0 && t != 1) continue;
+      const int l = static_cast<int>((i / S) % C);
+      float v = to_f32<T>(preds[i]);
+      if (do_norm) v = round_trip<T>(1.f / (1.f + expf(-v)));
+      int b = bucket(v);
+      atomicAdd(hist + ((int64_t)l * 2 + (int)t) * (nT + 1) + b, 1);
+    }
+  }
+}
+
+// confmat[t, c, y, p]: y = target (0/1), p = (score >= thr[t]).  tp=[1][1] fp=[0][1] fn=[1][0] tn=[0][0]
+__global__ void binned_scan_kernel(const int* __restrict__ hist, int C, int nT, int64_t* __restrict__ confmat) {
+  const int c = blockIdx.x;
+  for (int y = 0; y < 2; ++y) {
+    const int* h = hist + ((int64_t)c * 2 + y) * (nT + 1);
+    if (threadIdx.x == 0) {
+      long long total = 0;
+      for (int b = 0; b <= nT; ++b) total += h[b];
+      long long above = 0;  // # with bucket > t  (score >= thr[t])
+      for (int t = nT - 1; t >= 0; --t) {
+        above += h[t + 1];
+        int64_t* cell = confmat + ((int64_t)t * C + c) * 4 + y * 2;
+        cell[1] += above;          // predicted positive
+        cell[0] += total - above;  // predicted negative
+      }
+    }
+  }
+}
+
+void binned_curve_update(const at::Tensor& preds_, const at::Tensor& target_, const at::Tensor& thresholds_,
+                         at::Tensor& confmat, int64_t task, int64_t ignore_index, bool has_ignore) {
+  auto preds = preds_.contiguous();
+  auto target = target_.contiguous().to(at::kLong);
+  auto thr = thresholds_.contiguous().to(at::kFloat);
+  const int nT = static_cast<int>(thr.numel());
+  TORCH_CHECK(confmat.is_contiguous() && confmat.scalar_type() == at::kLong && confmat.dim() == 4 && confmat.size(0) == nT);
+  const int C = static_cast<int>(confmat.size(1));
+  auto hist = at::zeros({C, 2, nT + 1}, preds.options().dtype(at::kInt));
+  auto flag = range_flag(preds);
+  const int block = 256;
+  const size_t shm = nT * sizeof(float);
+  TORCH_CHECK(shm <= 64 * 1024, "too many thresholds");
+  TMX_DISPATCH_FLOAT(preds.scalar_type(), "binned_curve_update", [&] {
+    const scalar_t* p = reinterpret_cast<const scalar_t*>(preds.data_ptr());
+    if (task == 0) {
+      const int64_t n = target.numel();
+      if (n == 0) return;
+      hipLaunchKernelGGL((binned_hist_kernel<scalar_t, 0>), grid_for(n * kWave, block, 4096), block, shm, stream(), p,
+                         target.data_ptr<int64_t>(), n, C, (int64_t)1, thr.data_ptr<float>(), nT, flag.data_ptr<int>(),
+                         ignore_index, has_ignore, hist.data_ptr<int>());
+    } else {
+      const int64_t total = target.numel();
+      if (total == 0) return;
+      const int64_t N = target.size(0);
+      const int64_t S = total / (N * C);
+      hipLaunchKernelGGL((binned_hist_kernel<scalar_t, 1>), grid_for(total, block, 4096), block, shm, stream(), p,
+                         target.data_ptr<int64_t>(), N, C, S, thr.data_ptr<float>(), nT, flag.data_ptr<int>(), ignore_index,
+                         has_ignore, hist.data_ptr<int>());
+    }
+  });
+  TMX_LAUNCH_CHECK();
+  hipLaunchKernelGGL(binned_scan_kernel, C, 64, 0, stream(), hist.data_ptr<int>(), C, nT, confmat.data_ptr<int64_t>());
+  TMX_LAUNCH_CHECK();
+}
+
+}  // namespace tmx
+
+TORCH_LIBRARY_FRAGMENT(tmx, m) {
+  m.def("range_flag(Tensor x) -> Tensor");
+  m.def("bincount(Tensor x, int minlength) -> Tensor");
+  m.def("mc_confmat_update(Tensor preds, Tensor target, Tensor(a!) confmat, int ignore_index, bool has_ignore) -> ()");
+  m.def("binary_stats_update(Tensor preds, Tensor target, Tensor(a!) counts, int num_labels, float threshold, int ignore_index, bool has_ignore) -> ()");
+  m.def("curve_hist_update(Tensor preds, Tensor target, Tensor(a!) hist, int task, int ignore_index, bool has_ignore, Tensor(b!)? confmat) -> ()");
+  m.def("curve_hist_reduce(Tensor hist) -> Tensor");
+  m.def("binned_curve_update(Tensor preds, Tensor target, Tensor thresholds, Tensor(a!) confmat, int task, int ignore_index, bool has_ignore) -> ()");
+}
+
+TORCH_LIBRARY_IMPL(tmx, CUDA, m) {
+  m.impl("range_flag", &tmx::range_flag);
+  m.impl("bincount", &tmx::bincount);
+  m.impl("mc_confmat_update", &tmx::mc_confmat_update);
+  m.impl("binary_stats_update", &tmx::binary_stats_update);
+  m.impl("curve_hist_update", &tmx::curve_hist_update);
+  m.impl("curve_hist_reduce", &tmx::curve_hist_reduce);
+  m.impl("binned_curve_update", &tmx::binned_curve_update);
+}

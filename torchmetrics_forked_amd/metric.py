@@ -1,0 +1,732 @@
+"""The ``Metric`` runtime (behavioural contract: reference ``metric.py:50-1198``).
+
+A metric is an ``nn.Module`` whose *states* (registered with :meth:`Metric.add_state`) live on the metric's
+device and are merged across processes by the coalesced sync engine (:mod:`..parallel.sync`).
+
+MI355X-first choices that differ from the reference while keeping its observable contract:
+
+* ``sync`` uses one ``all_reduce`` per (op, dtype) bucket for sum/mean/min/max states and a single packed
+  all-gather for list/``cat``/``None`` states, instead of barrier + shape-gather + payload-gather per leaf.
+  A user supplied ``dist_sync_fn`` still gets the per-leaf protocol.
+* ``forward`` on the reduce-state path merges batch state into the global state without re-allocating
+  defaults on the host for every step (``_reset_states`` clones device defaults in place).
+* Optional ``sync(async_op=True)`` starts the collectives on the current stream and returns a handle, so the
+  caller can overlap the next step's update kernels with the RCCL traffic (``parallel.streams``).
+"""
+import builtins
+import functools
+import inspect
+from abc import ABC, abstractmethod
+from contextlib import contextmanager
+from copy import deepcopy
+from typing import Any, Callable, ClassVar, Dict, Generator, List, Optional, Sequence, Tuple, Union
+
+import torch
+from torch import Tensor
+from torch.nn import Module
+
+from torchmetrics_forked_amd.parallel.sync import legacy_sync_states, sync_states
+from torchmetrics_forked_amd.utilities.data import (
+    _flatten,
+    _squeeze_if_scalar,
+    apply_to_collection,
+    dim_zero_cat,
+    dim_zero_max,
+    dim_zero_mean,
+    dim_zero_min,
+    dim_zero_sum,
+)
+from torchmetrics_forked_amd.utilities.distributed import gather_all_tensors
+from torchmetrics_forked_amd.utilities.exceptions import TorchMetricsUserError
+from torchmetrics_forked_amd.utilities.plot import _AX_TYPE, _PLOT_OUT_TYPE, plot_single_or_multi_val
+from torchmetrics_forked_amd.utilities.prints import rank_zero_warn
+
+_STR_REDUCTIONS = {
+    "sum": dim_zero_sum,
+    "mean": dim_zero_mean,
+    "max": dim_zero_max,
+    "min": dim_zero_min,
+    "cat": dim_zero_cat,
+}
+_CONST_ATTRS = frozenset(
+    ("higher_is_better", "is_differentiable", "full_state_update", "plot_lower_bound", "plot_upper_bound", "plot_legend_name")
+)
+_BOOL_KWARGS = ("compute_on_cpu", "dist_sync_on_step", "sync_on_compute", "compute_with_cache")
+
+
+def jit_distributed_available() -> bool:
+    return torch.distributed.is_available() and torch.distributed.is_initialized()
+
+
+class Metric(Module, ABC):
+    """Base class of every metric.
+
+    Subclasses register states in ``__init__`` with :meth:`add_state` and implement ``update`` (accumulate a
+    batch into the states) and ``compute`` (final value from the states).
+
+    Keyword Args:
+        compute_on_cpu: move list states to CPU after each ``update`` (saves device memory).
+        dist_sync_on_step: synchronise states on every ``forward`` call.
+        process_group: process group used for synchronisation (default: world).
+        dist_sync_fn: custom per-tensor gather function (switches to the legacy per-leaf protocol).
+        distributed_available_fn: callable deciding whether we run distributed.
+        sync_on_compute: synchronise states when ``compute`` is called (default True).
+        compute_with_cache: cache ``compute`` output until the next ``update`` (default True).
+    """
+
+    __jit_ignored_attributes__: ClassVar[List[str]] = ["device"]
+    __jit_unused_properties__: ClassVar[List[str]] = [
+        "is_differentiable",
+        "higher_is_better",
+        "plot_lower_bound",
+        "plot_upper_bound",
+        "plot_legend_name",
+        "metric_state",
+        "_update_called",
+    ]
+    is_differentiable: Optional[bool] = None
+    higher_is_better: Optional[bool] = None
+    full_state_update: Optional[bool] = None
+
+    plot_lower_bound: Optional[float] = None
+    plot_upper_bound: Optional[float] = None
+    plot_legend_name: Optional[str] = None
+
+    def __init__(self, **kwargs: Any) -> None:
+        super().__init__()
+        torch._C._log_api_usage_once(f"torchmetrics_forked_amd.metric.{self.__class__.__name__}")
+        self._device = torch.device("cpu")
+
+        opts = {
+            "compute_on_cpu": kwargs.pop("compute_on_cpu", False),
+            "dist_sync_on_step": kwargs.pop("dist_sync_on_step", False),
+            "sync_on_compute": kwargs.pop("sync_on_compute", True),
+            "compute_with_cache": kwargs.pop("compute_with_cache", True),
+        }
+        for key in _BOOL_KWARGS:
+            if not isinstance(opts[key], bool):
+                article = "a" if key in ("sync_on_compute", "compute_with_cache") else "an"
+                raise ValueError(f"Expected keyword argument `{key}` to be {article} `bool` but got {opts[key]}")
+            setattr(self, key, opts[key])
+
+        self.process_group = kwargs.pop("process_group", None)
+        self.dist_sync_fn = kwargs.pop("dist_sync_fn", None)
+        if self.dist_sync_fn is not None and not callable(self.dist_sync_fn):
+            raise ValueError(
+                f"Expected keyword argument `dist_sync_fn` to be an callable function but got {self.dist_sync_fn}"
+            )
+        self.distributed_available_fn = kwargs.pop("distributed_available_fn", None) or jit_distributed_available
+        if kwargs:
+            raise ValueError(f"Unexpected keyword arguments: {', '.join(f'`{k}`' for k in sorted(kwargs))}")
+
+        self._update_signature = inspect.signature(self.update)
+        self.update: Callable = self._wrap_update(self.update)  # type: ignore[method-assign]
+        self.compute: Callable = self._wrap_compute(self.compute)  # type: ignore[method-assign]
+        self._computed: Any = None
+        self._forward_cache: Any = None
+        self._update_count = 0
+        self._to_sync = self.sync_on_compute
+        self._should_unsync = True
+        self._enable_grad = False
+        self._dtype_convert = False
+
+        self._defaults: Dict[str, Union[List, Tensor]] = {}
+        self._persistent: Dict[str, bool] = {}
+        self._reductions: Dict[str, Union[str, Callable[..., Any], None]] = {}
+
+        self._is_synced = False
+        self._cache: Optional[Dict[str, Union[List[Tensor], Tensor]]] = None
+
+    # ------------------------------------------------------------------------------------------------ props
+    @property
+    def _update_called(self) -> bool:
+        rank_zero_warn(
+            "This property will be removed in 2.0.0. Use `Metric.updated_called` instead.", DeprecationWarning, stacklevel=2
+        )
+        return self.update_called
+
+    @property
+    def update_called(self) -> bool:
+        return self._update_count > 0
+
+    @property
+    def update_count(self) -> int:
+        return self._update_count
+
+    @property
+    def metric_state(self) -> Dict[str, Union[List[Tensor], Tensor]]:
+        return {name: getattr(self, name) for name in self._defaults}
+
+    @property
+    def device(self) -> "torch.device":
+        return self._device
+
+    # ----------------------------------------------------------------------------------------------- states
+    def add_state(
+        self,
+        name: str,
+        default: Union[list, Tensor],
+        dist_reduce_fx: Optional[Union[str, Callable]] = None,
+        persistent: bool = False,
+    ) -> None:
+        """Register a state: a tensor, or an empty list that ``update`` appends tensors to.
+
+        ``dist_reduce_fx`` is one of ``"sum" | "mean" | "max" | "min" | "cat"``, a callable applied to the
+        stacked ``(world, ...)`` state, or ``None`` (states are gathered, not reduced).
+        """
+        if not isinstance(default, (Tensor, list)) or (isinstance(default, list) and default):
+            raise ValueError("state variable must be a tensor or any empty list (where you can append tensors)")
+        if isinstance(dist_reduce_fx, str) or dist_reduce_fx is None:
+            if dist_reduce_fx is not None and dist_reduce_fx not in _STR_REDUCTIONS:
+                raise ValueError("`dist_reduce_fx` must be callable or one of ['mean', 'sum', 'cat', 'min', 'max', None]")
+            fx = _STR_REDUCTIONS.get(dist_reduce_fx) if dist_reduce_fx is not None else None
+        elif callable(dist_reduce_fx):
+            fx = dist_reduce_fx
+        else:
+            raise ValueError("`dist_reduce_fx` must be callable or one of ['mean', 'sum', 'cat', 'min', 'max', None]")
+        if isinstance(default, Tensor):
+            default = default.contiguous()
+        setattr(self, name, default)
+        self._defaults[name] = deepcopy(default)
+        self._persistent[name] = persistent
+        self._reductions[name] = fx
+
+    # ---------------------------------------------------------------------------------------------- forward
+    @torch.jit.unused
+    def forward(self, *args: Any, **kwargs: Any) -> Any:
+        """Accumulate the batch into the global state and return the metric value on this batch alone."""
+        if self._is_synced:
+            raise TorchMetricsUserError(
+                "The Metric shouldn't be synced when performing ``forward``. HINT: Did you forget to call ``unsync`` ?."
+            )
+        if self.full_state_update or self.full_state_update is None or self.dist_sync_on_step:
+            self._forward_cache = self._forward_full_state_update(*args, **kwargs)
+        else:
+            self._forward_cache = self._forward_reduce_state_update(*args, **kwargs)
+        return self._forward_cache
+
+    def _enter_batch_mode(self) -> bool:
+        self._to_sync = self.dist_sync_on_step
+        self._should_unsync = False
+        saved = self.compute_on_cpu
+        self.compute_on_cpu = False
+        self._enable_grad = True
+        return saved
+
+    def _leave_batch_mode(self, saved_compute_on_cpu: bool) -> None:
+        self._is_synced = False
+        self._should_unsync = True
+        self._to_sync = self.sync_on_compute
+        self._computed = None
+        self._enable_grad = False
+        self.compute_on_cpu = saved_compute_on_cpu
+        if self.compute_on_cpu:
+            self._move_list_states_to_cpu()
+
+    def _forward_full_state_update(self, *args: Any, **kwargs: Any) -> Any:
+        """Two ``update`` calls: one into the global state, one into a fresh state for the batch value."""
+        self.update(*args, **kwargs)
+        count = self._update_count
+        saved = self._enter_batch_mode()
+        snapshot = self.metric_state
+        self.reset()
+        self.update(*args, **kwargs)
+        batch_val = self.compute()
+        for name, val in snapshot.items():
+            setattr(self, name, val)
+        self._update_count = count
+        self._leave_batch_mode(saved)
+        return batch_val
+
+    def _forward_reduce_state_update(self, *args: Any, **kwargs: Any) -> Any:
+        """One ``update`` into a fresh state; the batch state is then merged into the global state."""
+        snapshot = self.metric_state
+        count = self._update_count
+        self.reset()
+        saved = self._enter_batch_mode()
+        self.update(*args, **kwargs)
+        batch_val = self.compute()
+        self._update_count = count + 1
+        with torch.no_grad():
+            self._reduce_states(snapshot)
+        self._leave_batch_mode(saved)
+        return batch_val
+
+    def _reduce_states(self, incoming_state: Dict[str, Any]) -> None:
+        """Merge ``incoming_state`` (global) with the current (batch) state according to each reduction."""
+        for name in self._defaults:
+            local = getattr(self, name)
+            glob = incoming_state[name]
+            fx = self._reductions[name]
+            if fx is dim_zero_sum:
+                merged = glob + local
+            elif fx is dim_zero_mean:
+                merged = ((self._update_count - 1) * glob + local).float() / self._update_count
+            elif fx is dim_zero_max:
+                merged = torch.max(glob, local)
+            elif fx is dim_zero_min:
+                merged = torch.min(glob, local)
+            elif fx is dim_zero_cat:
+                if isinstance(glob, Tensor) and isinstance(local, Tensor):
+                    merged = torch.cat([glob, local])
+                else:
+                    merged = list(glob) + list(local) if isinstance(glob, list) else glob + local
+            elif fx is None and isinstance(glob, Tensor):
+                merged = torch.stack([glob, local])
+            elif fx is None and isinstance(glob, list):
+                merged = _flatten([glob, local])
+            elif callable(fx):
+                merged = fx(torch.stack([glob, local]))
+            else:
+                raise TypeError(f"Unsupported reduce_fn: {fx}")
+            setattr(self, name, merged)
+
+    # ------------------------------------------------------------------------------------------------- sync
+    def _sync_dist(self, dist_sync_fn: Optional[Callable] = None, process_group: Optional[Any] = None) -> None:
+        states = self.metric_state
+        group = process_group or self.process_group
+        if dist_sync_fn is None or dist_sync_fn is gather_all_tensors:
+            synced = sync_states(states, self._reductions, group=group)
+        else:
+            synced = legacy_sync_states(states, self._reductions, dist_sync_fn, group=group)
+        for name, val in synced.items():
+            setattr(self, name, val)
+
+    def _wrap_update(self, update: Callable) -> Callable:
+        @functools.wraps(update)
+        def wrapped_func(*args: Any, **kwargs: Any) -> None:
+            self._computed = None
+            self._update_count += 1
+            with torch.set_grad_enabled(self._enable_grad):
+                try:
+                    update(*args, **kwargs)
+                except RuntimeError as err:
+                    if "Expected all tensors to be on" in str(err):
+                        raise RuntimeError(
+                            "Encountered different devices in metric calculation (see stacktrace for details)."
+                            " This could be due to the metric class not being on the same device as input."
+                            f" Instead of `metric={self.__class__.__name__}(...)` try to do"
+                            f" `metric={self.__class__.__name__}(...).to(device)` where"
+                            " device corresponds to the device of the input."
+                        ) from err
+                    raise err
+            if self.compute_on_cpu:
+                self._move_list_states_to_cpu()
+
+        return wrapped_func
+
+    def _move_list_states_to_cpu(self) -> None:
+        for name in self._defaults:
+            val = getattr(self, name)
+            if isinstance(val, Sequence):
+                setattr(self, name, [v.to("cpu") for v in val])
+
+    def sync(
+        self,
+        dist_sync_fn: Optional[Callable] = None,
+        process_group: Optional[Any] = None,
+        should_sync: bool = True,
+        distributed_available: Optional[Callable] = None,
+    ) -> None:
+        """Replace local states by their cross-process reduction (local copies are cached for ``unsync``)."""
+        if self._is_synced and should_sync:
+            raise TorchMetricsUserError("The Metric has already been synced.")
+        if distributed_available is None and self.distributed_available_fn is not None:
+            distributed_available = self.distributed_available_fn
+        is_distributed = distributed_available() if callable(distributed_available) else None
+        if not should_sync or not is_distributed:
+            return
+        self._cache = self.metric_state
+        self._sync_dist(dist_sync_fn, process_group=process_group)
+        self._is_synced = True
+
+    def unsync(self, should_unsync: bool = True) -> None:
+        """Restore the local (pre-sync) states."""
+        if not should_unsync:
+            return
+        if not self._is_synced:
+            raise TorchMetricsUserError("The Metric has already been un-synced.")
+        if self._cache is None:
+            raise TorchMetricsUserError("The internal cache should exist to unsync the Metric.")
+        for name, val in self._cache.items():
+            setattr(self, name, val)
+        self._is_synced = False
+        self._cache = None
+
+    @contextmanager
+    def sync_context(
+        self,
+        dist_sync_fn: Optional[Callable] = None,
+        process_group: Optional[Any] = None,
+        should_sync: bool = True,
+        should_unsync: bool = True,
+        distributed_available: Optional[Callable] = None,
+    ) -> Generator:
+        """Context manager: synced states inside, local states restored on exit (if we synced)."""
+        self.sync(
+            dist_sync_fn=dist_sync_fn,
+            process_group=process_group,
+            should_sync=should_sync,
+            distributed_available=distributed_available,
+        )
+        yield
+        self.unsync(should_unsync=self._is_synced and should_unsync)
+
+    def _wrap_compute(self, compute: Callable) -> Callable:
+        @functools.wraps(compute)
+        def wrapped_func(*args: Any, **kwargs: Any) -> Any:
+            if self._update_count == 0:
+                rank_zero_warn(
+                    f"The ``compute`` method of metric {self.__class__.__name__}"
+                    " was called before the ``update`` method which may lead to errors,"
+                    " as metric states have not yet been updated.",
+                    UserWarning,
+                )
+            if self._computed is not None:
+                return self._computed
+            with self.sync_context(
+                dist_sync_fn=self.dist_sync_fn, should_sync=self._to_sync, should_unsync=self._should_unsync
+            ):
+                value = _squeeze_if_scalar(compute(*args, **kwargs))
+            if self.compute_with_cache:
+                self._computed = value
+            return value
+
+        return wrapped_func
+
+    @abstractmethod
+    def update(self, *_: Any, **__: Any) -> None:
+        """Accumulate a batch into the metric states."""
+
+    @abstractmethod
+    def compute(self) -> Any:
+        """Compute the final metric value from the (synchronised) states."""
+
+    # ------------------------------------------------------------------------------------------------ misc
+    def plot(self, *_: Any, **__: Any) -> Any:
+        raise NotImplementedError
+
+    def _plot(self, val: Any = None, ax: Optional[_AX_TYPE] = None) -> _PLOT_OUT_TYPE:
+        val = val if val is not None else self.compute()
+        return plot_single_or_multi_val(
+            val,
+            ax=ax,
+            higher_is_better=self.higher_is_better,
+            name=self.__class__.__name__,
+            lower_bound=self.plot_lower_bound,
+            upper_bound=self.plot_upper_bound,
+            legend_name=self.plot_legend_name,
+        )
+
+    def reset(self) -> None:
+        """Restore every state to its default (on the state's current device)."""
+        self._update_count = 0
+        self._forward_cache = None
+        self._computed = None
+        for name, default in self._defaults.items():
+            if isinstance(default, Tensor):
+                current = getattr(self, name)
+                dev = current.device if isinstance(current, Tensor) else default.device
+                setattr(self, name, default.detach().clone().to(dev))
+            else:
+                setattr(self, name, [])
+        self._cache = None
+        self._is_synced = False
+
+    def clone(self) -> "Metric":
+        return deepcopy(self)
+
+    def __getstate__(self) -> Dict[str, Any]:
+        return {k: v for k, v in self.__dict__.items() if k not in ("update", "compute", "_update_signature")}
+
+    def __setstate__(self, state: Dict[str, Any]) -> None:
+        self.__dict__.update(state)
+        self._update_signature = inspect.signature(self.update)
+        self.update: Callable = self._wrap_update(self.update)  # type: ignore[method-assign]
+        self.compute: Callable = self._wrap_compute(self.compute)  # type: ignore[method-assign]
+
+    def __setattr__(self, name: str, value: Any) -> None:
+        if name in _CONST_ATTRS:
+            raise RuntimeError(f"Can't change const `{name}`.")
+        super().__setattr__(name, value)
+
+    # dtype casts are no-ops unless routed through set_dtype (reference metric.py:729-760)
+    def type(self, dst_type: Union[str, torch.dtype]) -> "Metric":  # noqa: A003
+        return self
+
+    def float(self) -> "Metric":  # noqa: A003
+        return self
+
+    def double(self) -> "Metric":
+        return self
+
+    def half(self) -> "Metric":
+        return self
+
+    def set_dtype(self, dst_type: Union[str, torch.dtype]) -> "Metric":
+        """Cast every floating state (and default) to ``dst_type``."""
+        self._dtype_convert = True
+        out = super().type(dst_type)
+        out._dtype_convert = False
+        return out
+
+    def _apply(self, fn: Callable, exclude_state: Sequence[str] = "") -> Module:
+        this = super()._apply(fn)
+        fs = str(fn)
+        is_cast = any(f in fs for f in ("Module.type", "Module.half", "Module.float", "Module.double", "Module.bfloat16"))
+        if not self._dtype_convert and is_cast:
+            return this
+        for key, value in this._defaults.items():
+            if key in exclude_state:
+                continue
+            if isinstance(value, Tensor):
+                this._defaults[key] = fn(value)
+            elif isinstance(value, Sequence):
+                this._defaults[key] = [fn(v) for v in value]
+            current = getattr(this, key)
+            if isinstance(current, Tensor):
+                setattr(this, key, fn(current))
+            elif isinstance(current, Sequence):
+                setattr(this, key, [fn(v) for v in current])
+            else:
+                raise TypeError(
+                    f"Expected metric state to be either a Tensor or a list of Tensor, but encountered {current}"
+                )
+        self._device = fn(torch.zeros(1, device=self.device)).device
+        if this._computed is not None:
+            this._computed = apply_to_collection(this._computed, Tensor, fn)
+        if this._forward_cache is not None:
+            this._forward_cache = apply_to_collection(this._forward_cache, Tensor, fn)
+        return this
+
+    def persistent(self, mode: bool = False) -> None:
+        for key in self._persistent:
+            self._persistent[key] = mode
+
+    def state_dict(  # type: ignore[override]
+        self, destination: Optional[Dict[str, Any]] = None, prefix: str = "", keep_vars: bool = False
+    ) -> Dict[str, Any]:
+        destination = super().state_dict(destination=destination, prefix=prefix, keep_vars=keep_vars)  # type: ignore
+        for key in self._defaults:
+            if not self._persistent[key]:
+                continue
+            val = getattr(self, key)
+            if not keep_vars:
+                if isinstance(val, Tensor):
+                    val = val.detach()
+                elif isinstance(val, list):
+                    val = [v.detach() if isinstance(v, Tensor) else v for v in val]
+            destination[prefix + key] = deepcopy(val)
+        return destination
+
+    def _load_from_state_dict(
+        self,
+        state_dict: dict,
+        prefix: str,
+        local_metadata: dict,
+        strict: bool,
+        missing_keys: List[str],
+        unexpected_keys: List[str],
+        error_msgs: List[str],
+    ) -> None:
+        for key in self._defaults:
+            name = prefix + key
+            if name in state_dict:
+                setattr(self, key, state_dict.pop(name))
+        super()._load_from_state_dict(state_dict, prefix, local_metadata, True, missing_keys, unexpected_keys, error_msgs)
+
+    def _filter_kwargs(self, **kwargs: Any) -> Dict[str, Any]:
+        """Keep only kwargs accepted by ``update`` (all of them if it takes ``**kwargs``)."""
+        params = self._update_signature.parameters
+        var_kinds = (inspect.Parameter.VAR_POSITIONAL, inspect.Parameter.VAR_KEYWORD)
+        has_var_kw = any(p.kind == inspect.Parameter.VAR_KEYWORD for p in params.values())
+        if has_var_kw:
+            return kwargs
+        return {k: v for k, v in kwargs.items() if k in params and params[k].kind not in var_kinds}
+
+    def __hash__(self) -> int:
+        vals: List[Any] = [self.__class__.__name__, id(self)]
+        for key in self._defaults:
+            val = getattr(self, key)
+            if hasattr(val, "__iter__") and not isinstance(val, Tensor):
+                vals.extend(val)
+            else:
+                vals.append(val)
+        return hash(tuple(vals))
+
+    # ------------------------------------------------------------------------------------- operator algebra
+    def __add__(self, other: Any) -> "CompositionalMetric":
+        return CompositionalMetric(torch.add, self, other)
+
+    def __and__(self, other: Any) -> "CompositionalMetric":
+        return CompositionalMetric(torch.bitwise_and, self, other)
+
+    def __eq__(self, other: Any) -> "CompositionalMetric":  # type: ignore[override]
+        return CompositionalMetric(torch.eq, self, other)
+
+    def __floordiv__(self, other: Any) -> "CompositionalMetric":
+        return CompositionalMetric(torch.floor_divide, self, other)
+
+    def __ge__(self, other: Any) -> "CompositionalMetric":
+        return CompositionalMetric(torch.ge, self, other)
+
+    def __gt__(self, other: Any) -> "CompositionalMetric":
+        return CompositionalMetric(torch.gt, self, other)
+
+    def __le__(self, other: Any) -> "CompositionalMetric":
+        return CompositionalMetric(torch.le, self, other)
+
+    def __lt__(self, other: Any) -> "CompositionalMetric":
+        return CompositionalMetric(torch.lt, self, other)
+
+    def __matmul__(self, other: Any) -> "CompositionalMetric":
+        return CompositionalMetric(torch.matmul, self, other)
+
+    def __mod__(self, other: Any) -> "CompositionalMetric":
+        return CompositionalMetric(torch.fmod, self, other)
+
+    def __mul__(self, other: Any) -> "CompositionalMetric":
+        return CompositionalMetric(torch.mul, self, other)
+
+    def __ne__(self, other: Any) -> "CompositionalMetric":  # type: ignore[override]
+        return CompositionalMetric(torch.ne, self, other)
+
+    def __or__(self, other: Any) -> "CompositionalMetric":
+        return CompositionalMetric(torch.bitwise_or, self, other)
+
+    def __pow__(self, other: Any) -> "CompositionalMetric":
+        return CompositionalMetric(torch.pow, self, other)
+
+    def __radd__(self, other: Any) -> "CompositionalMetric":
+        return CompositionalMetric(torch.add, other, self)
+
+    def __rand__(self, other: Any) -> "CompositionalMetric":
+        return CompositionalMetric(torch.bitwise_and, self, other)
+
+    def __rfloordiv__(self, other: Any) -> "CompositionalMetric":
+        return CompositionalMetric(torch.floor_divide, other, self)
+
+    def __rmatmul__(self, other: Any) -> "CompositionalMetric":
+        return CompositionalMetric(torch.matmul, other, self)
+
+    def __rmod__(self, other: Any) -> "CompositionalMetric":
+        return CompositionalMetric(torch.fmod, other, self)
+
+    def __rmul__(self, other: Any) -> "CompositionalMetric":
+        return CompositionalMetric(torch.mul, other, self)
+
+    def __ror__(self, other: Any) -> "CompositionalMetric":
+        return CompositionalMetric(torch.bitwise_or, other, self)
+
+    def __rpow__(self, other: Any) -> "CompositionalMetric":
+        return CompositionalMetric(torch.pow, other, self)
+
+    def __rsub__(self, other: Any) -> "CompositionalMetric":
+        return CompositionalMetric(torch.sub, other, self)
+
+    def __rtruediv__(self, other: Any) -> "CompositionalMetric":
+        return CompositionalMetric(torch.true_divide, other, self)
+
+    def __rxor__(self, other: Any) -> "CompositionalMetric":
+        return CompositionalMetric(torch.bitwise_xor, other, self)
+
+    def __sub__(self, other: Any) -> "CompositionalMetric":
+        return CompositionalMetric(torch.sub, self, other)
+
+    def __truediv__(self, other: Any) -> "CompositionalMetric":
+        return CompositionalMetric(torch.true_divide, self, other)
+
+    def __xor__(self, other: Any) -> "CompositionalMetric":
+        return CompositionalMetric(torch.bitwise_xor, self, other)
+
+    def __abs__(self) -> "CompositionalMetric":
+        return CompositionalMetric(torch.abs, self, None)
+
+    def __inv__(self) -> "CompositionalMetric":
+        return CompositionalMetric(torch.bitwise_not, self, None)
+
+    def __invert__(self) -> "CompositionalMetric":
+        return self.__inv__()
+
+    def __neg__(self) -> "CompositionalMetric":
+        return CompositionalMetric(_neg, self, None)
+
+    def __pos__(self) -> "CompositionalMetric":
+        return CompositionalMetric(torch.abs, self, None)
+
+    def __getitem__(self, idx: int) -> "CompositionalMetric":
+        return CompositionalMetric(lambda x: x[idx], self, None)
+
+    def __getnewargs__(self) -> Tuple:
+        return (Metric.__str__(self),)
+
+    __iter__ = None
+
+
+def _neg(x: Tensor) -> Tensor:
+    return -torch.abs(x)
+
+
+class CompositionalMetric(Metric):
+    """``op(metric_a.compute(), metric_b.compute())``; update/forward/reset are forwarded to the operands."""
+
+    def __init__(self, operator: Callable, metric_a: Union[Metric, builtins.float, Tensor], metric_b: Union[Metric, builtins.float, Tensor, None]) -> None:
+        super().__init__()
+        self.op = operator
+        if isinstance(metric_a, Tensor):
+            self.register_buffer("metric_a", metric_a, persistent=False)
+        else:
+            self.metric_a = metric_a
+        if isinstance(metric_b, Tensor):
+            self.register_buffer("metric_b", metric_b, persistent=False)
+        else:
+            self.metric_b = metric_b
+
+    def _sync_dist(self, dist_sync_fn: Optional[Callable] = None, process_group: Optional[Any] = None) -> None:
+        """Operands synchronise themselves."""
+
+    def update(self, *args: Any, **kwargs: Any) -> None:
+        if isinstance(self.metric_a, Metric):
+            self.metric_a.update(*args, **self.metric_a._filter_kwargs(**kwargs))
+        if isinstance(self.metric_b, Metric):
+            self.metric_b.update(*args, **self.metric_b._filter_kwargs(**kwargs))
+
+    def compute(self) -> Any:
+        val_a = self.metric_a.compute() if isinstance(self.metric_a, Metric) else self.metric_a
+        val_b = self.metric_b.compute() if isinstance(self.metric_b, Metric) else self.metric_b
+        return self.op(val_a) if val_b is None else self.op(val_a, val_b)
+
+    @torch.jit.unused
+    def forward(self, *args: Any, **kwargs: Any) -> Any:
+        val_a = self.metric_a(*args, **self.metric_a._filter_kwargs(**kwargs)) if isinstance(self.metric_a, Metric) else self.metric_a
+        val_b = self.metric_b(*args, **self.metric_b._filter_kwargs(**kwargs)) if isinstance(self.metric_b, Metric) else self.metric_b
+        if val_a is None:
+            self._forward_cache = None
+            return self._forward_cache
+        if val_b is None:
+            if isinstance(self.metric_b, Metric):
+                self._forward_cache = None
+                return self._forward_cache
+            self._forward_cache = self.op(val_a)
+            return self._forward_cache
+        self._forward_cache = self.op(val_a, val_b)
+        return self._forward_cache
+
+    def reset(self) -> None:
+        if isinstance(self.metric_a, Metric):
+            self.metric_a.reset()
+        if isinstance(self.metric_b, Metric):
+            self.metric_b.reset()
+
+    def persistent(self, mode: bool = False) -> None:
+        if isinstance(self.metric_a, Metric):
+            self.metric_a.persistent(mode=mode)
+        if isinstance(self.metric_b, Metric):
+            self.metric_b.persistent(mode=mode)
+
+    def __repr__(self) -> str:
+        _op_metrics = f"(\n  {self.op.__name__}(\n    {self.metric_a!r},\n    {self.metric_b!r}\n  )\n)"
+        return self.__class__.__name__ + _op_metrics
+
+    def _wrap_compute(self, compute: Callable) -> Callable:
+        return compute

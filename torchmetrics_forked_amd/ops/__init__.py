@@ -1,0 +1,69 @@
+"""Native op layer: hand-written gfx950 HIP kernels exposed as ``torch.ops.tmx.*``.
+
+Policy (MI355X-first, no silent fallbacks on the GPU):
+
+* ``load()`` loads ``_tmx_native.so`` (built in-tree by :mod:`.build`).  On a machine with a ROCm GPU the
+  library **must** load: every GPU code path calls :func:`require`, which raises if it is missing, so a GPU run
+  can never quietly degrade to eager PyTorch.
+* CPU tensors (gloo / plumbing configs, unit tests in the CPU container) use the pure-PyTorch reference
+  implementations that live next to each wrapper; these are also the numerics oracles for the kernel tests.
+* Set ``TMX_DISABLE_NATIVE=1`` to force the eager path for A/B comparisons (documented, never implicit).
+"""
+import os
+import threading
+from pathlib import Path
+from typing import Optional
+
+import torch
+
+_LIB = Path(__file__).resolve().parent / "_tmx_native.so"
+_lock = threading.Lock()
+_loaded: Optional[bool] = None
+_error: Optional[str] = None
+
+
+def load() -> bool:
+    """Load the native library once; returns True on success."""
+    global _loaded, _error
+    if _loaded is not None:
+        return _loaded
+    with _lock:
+        if _loaded is not None:
+            return _loaded
+        if os.environ.get("TMX_DISABLE_NATIVE", "0") == "1":
+            _loaded, _error = False, "disabled by TMX_DISABLE_NATIVE=1"
+            return False
+        if not _LIB.exists():
+            _loaded, _error = False, f"{_LIB} not built (run `python -m torchmetrics_forked_amd.ops.build`)"
+            return False
+        try:
+            torch.ops.load_library(str(_LIB))
+            _loaded = True
+        except Exception as err:  # pragma: no cover - surfaced through require()
+            _loaded, _error = False, f"failed to load {_LIB}: {err}"
+    return bool(_loaded)
+
+
+def available() -> bool:
+    return load()
+
+
+def require(tensor: Optional[torch.Tensor] = None) -> None:
+    """Raise unless the native library is loaded (called on every GPU code path)."""
+    if not load():
+        where = f" for a tensor on {tensor.device}" if tensor is not None else ""
+        raise RuntimeError(f"torchmetrics_forked_amd native HIP library required{where}: {_error}")
+
+
+def use_native(t: torch.Tensor) -> bool:
+    """True when ``t`` lives on the GPU; then the native library is mandatory (raises if missing)."""
+    if t.is_cuda:
+        if os.environ.get("TMX_DISABLE_NATIVE", "0") == "1":
+            return False
+        require(t)
+        return True
+    return False
+
+
+def lib_path() -> Path:
+    return _LIB

@@ -1,0 +1,184 @@
+"""Python entry points for the classification kernels in ``csrc/classification.hip``.
+
+Each function dispatches to ``torch.ops.tmx.*`` for GPU tensors (native library mandatory there) and to an
+eager PyTorch implementation for CPU tensors.  The eager implementations follow the reference semantics
+operation-by-operation and double as the numerics oracle in ``tests/test_ops_gpu.py``.
+"""
+from typing import Optional
+
+import torch
+from torch import Tensor
+
+from torchmetrics_forked_amd import ops
+
+N_CODES = 1 << 14
+
+
+def range_flag(x: Tensor) -> Tensor:
+    """int32[1]: 1 when any element is outside [0, 1] (or NaN)."""
+    if ops.use_native(x):
+        return torch.ops.tmx.range_flag(x)
+    return (~((x >= 0) & (x <= 1))).any().reshape(1).int()
+
+
+def mc_confmat_update(preds: Tensor, target: Tensor, confmat: Tensor, ignore_index: Optional[int]) -> None:
+    """``confmat[t, p] += 1`` for every (target, argmax/label pred) pair; rows with ``t == ignore_index`` skipped."""
+    C = confmat.shape[0]
+    if ops.use_native(target):
+        torch.ops.tmx.mc_confmat_update(preds, target, confmat, -1 if ignore_index is None else ignore_index, ignore_index is not None)
+        return
+    p = preds.argmax(dim=1) if preds.is_floating_point() else preds
+    p, t = p.reshape(-1).long(), target.reshape(-1).long()
+    keep = (t >= 0) & (t < C) & (p >= 0) & (p < C)
+    if ignore_index is not None:
+        keep &= t != ignore_index
+    idx = (t * C + p)[keep]
+    confmat += torch.bincount(idx, minlength=C * C).reshape(C, C)
+
+
+def binary_stats_update(
+    preds: Tensor, target: Tensor, counts: Tensor, num_labels: int, threshold: float, ignore_index: Optional[int]
+) -> None:
+    """``counts[L, 4] += (tp, fp, tn, fn)`` per label; preds/target are ``[N, L, ...]`` (``L=1`` for binary)."""
+    if ops.use_native(target):
+        torch.ops.tmx.binary_stats_update(
+            preds, target, counts, num_labels, float(threshold), -1 if ignore_index is None else ignore_index, ignore_index is not None
+        )
+        return
+    if preds.is_floating_point():
+        if not bool(((preds >= 0) & (preds <= 1)).all()):
+            preds = preds.sigmoid()
+        preds = preds > threshold
+    n = target.shape[0]
+    p = preds.reshape(n, num_labels, -1).long()
+    t = target.reshape(n, num_labels, -1).long()
+    valid = (t == 0) | (t == 1)
+    if ignore_index is not None:
+        valid &= t != ignore_index
+    tp = ((p == 1) & (t == 1) & valid).sum((0, 2))
+    fp = ((p == 1) & (t == 0) & valid).sum((0, 2))
+    tn = ((p == 0) & (t == 0) & valid).sum((0, 2))
+    fn = ((p == 0) & (t == 1) & valid).sum((0, 2))
+    counts += torch.stack([tp, fp, tn, fn], dim=1)
+
+
+def _codes(x: Tensor) -> Tensor:
+    """Order-preserving integer code of a 16-bit float in [0, 1]; -1 for values outside (NaN, <0, >1)."""
+    bits = x.contiguous().view(torch.int16).to(torch.int32) & 0xFFFF
+    one = 0x3F80 if x.dtype == torch.bfloat16 else 0x3C00
+    bits = torch.where(bits == 0x8000, torch.zeros_like(bits), bits)
+    return torch.where(bits <= one, bits, torch.full_like(bits, -1))
+
+
+def curve_hist_update(
+    preds: Tensor,
+    target: Tensor,
+    hist: Tensor,
+    task: str,
+    ignore_index: Optional[int],
+    confmat: Optional[Tensor] = None,
+) -> None:
+    """Accumulate the exact 16-bit score histogram ``hist[C, 2, 16384]`` (see csrc/classification.hip).
+
+    ``task="multiclass"``: preds ``[N, C]`` scores (softmax applied if any value outside [0,1]), target ``[N]``;
+    optionally also accumulates the argmax confusion matrix (fused plan).  ``task="multilabel"``/``"binary"``:
+    preds/target ``[N, L, ...]`` (sigmoid if needed), target in {0, 1}.
+    """
+    if preds.dtype not in (torch.bfloat16, torch.float16):
+        raise TypeError(f"curve_hist_update expects bf16/fp16 scores, got {preds.dtype}")
+    tcode = 0 if task == "multiclass" else 1
+    if ops.use_native(target):
+        torch.ops.tmx.curve_hist_update(
+            preds, target, hist, tcode, -1 if ignore_index is None else ignore_index, ignore_index is not None, confmat
+        )
+        return
+    C = hist.shape[0]
+    if task == "multiclass":
+        t = target.reshape(-1).long()
+        p = preds.reshape(t.shape[0], C)
+        keep = torch.ones_like(t, dtype=torch.bool) if ignore_index is None else t != ignore_index
+        p, t = p[keep], t[keep]
+        if confmat is not None:
+            mc_confmat_update(p, t, confmat, None)
+        if not bool(((p >= 0) & (p <= 1)).all()):
+            p = p.softmax(1)
+        code = _codes(p).long()  # [n, C]
+        cls = torch.arange(C, device=p.device).expand_as(code)
+        lab = (t.unsqueeze(1) == cls).long()
+    else:
+        n = target.shape[0]
+        p = preds.reshape(n, C, -1)
+        t = target.reshape(n, C, -1).long()
+        if not bool(((p >= 0) & (p <= 1)).all()):
+            p = p.sigmoid()
+        code = _codes(p).long()
+        cls = torch.arange(C, device=p.device).view(1, C, 1).expand_as(code)
+        lab = t
+        valid = (t == 0) | (t == 1)
+        if ignore_index is not None:
+            valid &= t != ignore_index
+        code = torch.where(valid, code, torch.full_like(code, -1))
+        lab = lab.clamp(0, 1)
+    ok = code >= 0
+    flat = ((cls * 2 + lab) * N_CODES + code)[ok]
+    hist += torch.bincount(flat.reshape(-1), minlength=hist.numel()).reshape(hist.shape)
+
+
+def curve_hist_reduce(hist: Tensor) -> Tensor:
+    """float64 ``[C, 4]`` = (auroc, average_precision, n_pos, n_neg) per class, from ``hist[C, 2, K]``."""
+    if ops.use_native(hist):
+        return torch.ops.tmx.curve_hist_reduce(hist)
+    neg = hist[:, 0].flip(-1).double()
+    pos = hist[:, 1].flip(-1).double()
+    tp = pos.cumsum(-1)
+    fp = neg.cumsum(-1)
+    P, N = tp[:, -1], fp[:, -1]
+    tp_prev = tp - pos
+    area = (neg * (2 * tp_prev + pos)).sum(-1)
+    auroc = torch.where((P > 0) & (N > 0), area / (2 * P * N).clamp_min(1), torch.zeros_like(P))
+    prec = torch.where(tp + fp > 0, tp / (tp + fp).clamp_min(1), torch.zeros_like(tp))
+    ap = torch.where(P > 0, (pos * prec).sum(-1) / P.clamp_min(1), torch.full_like(P, float("nan")))
+    return torch.stack([auroc, ap, P, N], dim=1)
+
+
+def binned_curve_update(
+    preds: Tensor, target: Tensor, thresholds: Tensor, confmat: Tensor, task: str, ignore_index: Optional[int]
+) -> None:
+    """``confmat[T, C, 2, 2] += `` multi-threshold confusion counts (score >= thr[t]) per class/label."""
+    tcode = 0 if task == "multiclass" else 1
+    if ops.use_native(target):
+        torch.ops.tmx.binned_curve_update(
+            preds, target, thresholds, confmat, tcode, -1 if ignore_index is None else ignore_index, ignore_index is not None
+        )
+        return
+    T, C = confmat.shape[0], confmat.shape[1]
+    thr = thresholds.to(torch.float32)
+    if task == "multiclass":
+        t = target.reshape(-1).long()
+        p = preds.reshape(t.shape[0], C)
+        keep = torch.ones_like(t, dtype=torch.bool) if ignore_index is None else t != ignore_index
+        p, t = p[keep], t[keep]
+        if not bool(((p >= 0) & (p <= 1)).all()):
+            p = p.softmax(1)
+        lab = torch.nn.functional.one_hot(t, C).long()  # [n, C]
+        valid = torch.ones_like(lab, dtype=torch.bool)
+    else:
+        n = target.shape[0]
+        p = preds.reshape(n, C, -1)
+        t = target.reshape(n, C, -1).long()
+        if not bool(((p >= 0) & (p <= 1)).all()):
+            p = p.sigmoid()
+        p = p.transpose(1, 2).reshape(-1, C)
+        lab = t.transpose(1, 2).reshape(-1, C)
+        valid = (lab == 0) | (lab == 1)
+        if ignore_index is not None:
+            valid &= lab != ignore_index
+    bucket = torch.bucketize(p.float(), thr, right=True)  # number of thresholds <= p
+    cls = torch.arange(C, device=p.device).expand_as(bucket)
+    idx = ((cls * 2 + lab.clamp(0, 1)) * (T + 1) + bucket)[valid]
+    h = torch.bincount(idx, minlength=C * 2 * (T + 1)).reshape(C, 2, T + 1)
+    total = h.sum(-1, keepdim=True)
+    above = h.flip(-1).cumsum(-1).flip(-1)[..., 1:]  # above[c, y, t] = #(bucket > t)
+    below = total - above
+    upd = torch.stack([below, above], dim=-1)  # [C, 2(y), T, 2(p)]
+    confmat += upd.permute(2, 0, 1, 3)

@@ -1,0 +1,132 @@
+"""State reductions and tensor helpers (parity: reference ``utilities/data.py:25-237``).
+
+Differences from the reference (by design):
+  * ``_bincount`` never falls back to a per-bin Python loop; under deterministic mode it uses a
+    scatter-add of ones (deterministic for integer accumulation) and on ROCm devices it routes to the
+    framework's LDS-privatised histogram kernel (``ops.histogram.bincount``) when the extension is loaded.
+  * ``_cumsum`` never copies to the host: integer / float cumsum on GPU is done in fp64 on device.
+"""
+from typing import Any, Callable, Dict, List, Mapping, Optional, Sequence, Tuple, Union
+
+import torch
+from torch import Tensor
+
+METRIC_EPS = 1e-6
+
+
+def dim_zero_cat(x: Union[Tensor, List[Tensor]]) -> Tensor:
+    """Concatenate a list (or a tensor) along dim 0; 0-d entries are promoted to 1-d."""
+    if isinstance(x, Tensor):
+        return x
+    parts = [y.unsqueeze(0) if y.numel() == 1 and y.ndim == 0 else y for y in x]
+    if not parts:
+        raise ValueError("No samples to concatenate")
+    return torch.cat(parts, dim=0)
+
+
+def dim_zero_sum(x: Tensor) -> Tensor:
+    return torch.sum(x, dim=0)
+
+
+def dim_zero_mean(x: Tensor) -> Tensor:
+    return torch.mean(x, dim=0)
+
+
+def dim_zero_max(x: Tensor) -> Tensor:
+    return torch.max(x, dim=0).values
+
+
+def dim_zero_min(x: Tensor) -> Tensor:
+    return torch.min(x, dim=0).values
+
+
+def _flatten(x: Sequence) -> list:
+    return [item for sub in x for item in sub]
+
+
+def _flatten_dict(x: Dict) -> Tuple[Dict, bool]:
+    """Flatten one level of nested dicts; report whether any key collided."""
+    out: Dict = {}
+    dup = False
+    for key, value in x.items():
+        items = value.items() if isinstance(value, dict) else [(key, value)]
+        for k, v in items:
+            dup = dup or k in out
+            out[k] = v
+    return out, dup
+
+
+def to_onehot(label_tensor: Tensor, num_classes: Optional[int] = None) -> Tensor:
+    """Dense labels ``[N, ...]`` -> one-hot ``[N, C, ...]`` (same dtype as the labels)."""
+    if num_classes is None:
+        num_classes = int(label_tensor.max().item()) + 1
+    out = torch.zeros(
+        label_tensor.shape[0], num_classes, *label_tensor.shape[1:], dtype=label_tensor.dtype, device=label_tensor.device
+    )
+    return out.scatter_(1, label_tensor.long().unsqueeze(1).expand_as(out), 1)
+
+
+def select_topk(prob_tensor: Tensor, topk: int = 1, dim: int = 1) -> Tensor:
+    """Int32 mask with ones at the ``topk`` largest entries along ``dim``."""
+    idx = prob_tensor.argmax(dim=dim, keepdim=True) if topk == 1 else prob_tensor.topk(k=topk, dim=dim).indices
+    return torch.zeros_like(prob_tensor).scatter(dim, idx, 1.0).int()
+
+
+def to_categorical(x: Tensor, argmax_dim: int = 1) -> Tensor:
+    return torch.argmax(x, dim=argmax_dim)
+
+
+def _squeeze_scalar_element_tensor(x: Tensor) -> Tensor:
+    return x.squeeze() if x.numel() == 1 else x
+
+
+def apply_to_collection(data: Any, dtype: Union[type, Tuple[type, ...]], function: Callable, *args: Any, **kwargs: Any) -> Any:
+    """Recursively apply ``function`` to every leaf of ``dtype`` inside dicts / lists / tuples."""
+    if isinstance(data, dtype):
+        return function(data, *args, **kwargs)
+    if isinstance(data, Mapping):
+        return type(data)({k: apply_to_collection(v, dtype, function, *args, **kwargs) for k, v in data.items()})
+    if isinstance(data, tuple) and hasattr(data, "_fields"):  # namedtuple
+        return type(data)(*(apply_to_collection(d, dtype, function, *args, **kwargs) for d in data))
+    if isinstance(data, (list, tuple)):
+        return type(data)(apply_to_collection(d, dtype, function, *args, **kwargs) for d in data)
+    return data
+
+
+def _squeeze_if_scalar(data: Any) -> Any:
+    return apply_to_collection(data, Tensor, _squeeze_scalar_element_tensor)
+
+
+def _bincount(x: Tensor, minlength: Optional[int] = None) -> Tensor:
+    """Deterministic int64 bincount (no per-bin Python loop, no host round-trip when ``minlength`` given)."""
+    if minlength is None:
+        minlength = int(x.max().item()) + 1 if x.numel() else 0
+    x = x.reshape(-1).long()
+    if x.is_cuda:
+        from torchmetrics_forked_amd.ops import histogram as _hist
+
+        if _hist.available():
+            return _hist.bincount(x, minlength)
+    if torch.are_deterministic_algorithms_enabled():
+        out = torch.zeros(minlength, dtype=torch.long, device=x.device)
+        return out.scatter_add_(0, x, torch.ones_like(x))
+    return torch.bincount(x, minlength=minlength)
+
+
+def _cumsum(x: Tensor, dim: Optional[int] = 0, dtype: Optional[torch.dtype] = None) -> Tensor:
+    if torch.are_deterministic_algorithms_enabled() and x.is_cuda and x.is_floating_point():
+        # deterministic on device: accumulate in fp64 (sequential-order independent to ~1e-16)
+        return torch.cumsum(x.double(), dim=dim).to(dtype or x.dtype)
+    return torch.cumsum(x, dim=dim, dtype=dtype)
+
+
+def _flexible_bincount(x: Tensor) -> Tensor:
+    """Counts of each distinct value of ``x`` (in sorted order of the distinct values)."""
+    _, counts = torch.unique(x, return_counts=True)
+    return counts
+
+
+def allclose(tensor1: Tensor, tensor2: Tensor) -> bool:
+    if tensor1.dtype != tensor2.dtype:
+        tensor2 = tensor2.to(dtype=tensor1.dtype)
+    return torch.allclose(tensor1, tensor2)

@@ -1,0 +1,74 @@
+"""Eager vs deferred tensor validation.
+
+The reference validates every ``update`` with host-synchronising checks (``torch.unique`` + Python ``if``,
+SURVEY §0 fact 6).  On MI355X that stalls the HIP stream once or twice per step.  Here a validator receives a
+``sink``:
+
+* ``sink is None`` (functional API, CPU tensors, or ``TMX_VALIDATION=eager``): raise immediately, exactly like the
+  reference (same exception types and messages).
+* ``sink`` is a :class:`DeferredChecks` (module metrics on GPU tensors): each check contributes a device-side
+  boolean flag; flags are OR-ed on device and inspected once, at ``compute`` time (which synchronises anyway),
+  raising the same exception type and message.
+"""
+import os
+from typing import Callable, Dict, List, Optional, Tuple, Type
+
+import torch
+from torch import Tensor
+
+
+def validation_mode() -> str:
+    return os.environ.get("TMX_VALIDATION", "auto")
+
+
+class DeferredChecks:
+    """Accumulates device-side failure flags keyed by (exception type, message)."""
+
+    def __init__(self) -> None:
+        self._flags: Dict[Tuple[Type[Exception], str], Tensor] = {}
+
+    def add(self, bad: Tensor, exc: Type[Exception], message: str) -> None:
+        key = (exc, message)
+        bad = bad.reshape(-1).any().reshape(1)
+        prev = self._flags.get(key)
+        self._flags[key] = bad if prev is None else (prev | bad)
+
+    def check(self) -> None:
+        if not self._flags:
+            return
+        keys = list(self._flags.keys())
+        flags = torch.cat([self._flags[k].to(torch.bool).cpu() for k in keys])  # one host sync
+        self._flags = {}
+        for k, f in zip(keys, flags.tolist()):
+            if f:
+                raise k[0](k[1])
+
+    def clear(self) -> None:
+        self._flags = {}
+
+
+def make_sink(t: Tensor) -> Optional[DeferredChecks]:
+    """Sink for a tensor: deferred on GPU (unless TMX_VALIDATION=eager), eager otherwise."""
+    mode = validation_mode()
+    if mode == "eager" or (mode == "auto" and not t.is_cuda):
+        return None
+    return DeferredChecks()
+
+
+def fail_if(
+    bad: Tensor,
+    exc: Type[Exception],
+    message: Callable[[], str],
+    sink: Optional[DeferredChecks],
+    static_message: Optional[str] = None,
+) -> None:
+    """Raise ``exc(message())`` if ``bad`` (eager) or record it in ``sink`` (deferred).
+
+    ``message`` may read tensor values (only evaluated when raising eagerly); deferred mode uses
+    ``static_message`` (no host access) or a generic description.
+    """
+    if sink is None:
+        if bool(bad.any()):
+            raise exc(message())
+    else:
+        sink.add(bad, exc, static_message or "Invalid input values detected (deferred validation at compute).")
