@@ -1,0 +1,155 @@
+"""Headline benchmark: metric-updates/sec of MulticlassAUROC + MulticlassConfusionMatrix (C=1000, bs=65536, bf16).
+
+BASELINE.json config 2: "MulticlassAUROC + ConfusionMatrix num_classes=1000 bs=65536 bf16, 8xMI355X DDP sync".
+
+One *step* = one ``MetricCollection.update(preds, target)`` on a fresh synthetic batch (bf16 logits
+``[65536, 1000]`` + int64 labels, pre-generated in HBM and cycled, i.e. what a prefetching loader hands over).
+The timed window is exactly K steps followed by ONE ``compute()`` (cross-rank RCCL sync + final AUROC over all
+classes + confusion matrix), bracketed by barrier + device synchronize on both sides; the max over ranks is
+reported.  ``value`` = world_size * K / max_rank_seconds (whole-job aggregate, weak scaling: per-GPU batch fixed).
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]   (N>1 under torch.distributed.run)
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+BASELINE_UPDATES_PER_SEC = None  # filled from BASELINE.json "published" (none published) / measured ref
+
+
+def _baseline() -> "float | None":
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "BASELINE.json")
+    try:
+        with open(path) as f:
+            pub = json.load(f).get("published", {})
+        v = pub.get("metric_updates_per_sec_1gpu") if isinstance(pub, dict) else None
+        return float(v) if v else None
+    except Exception:
+        return None
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--num-classes", type=int, default=1000)
+    ap.add_argument("--batch", type=int, default=65536)
+    ap.add_argument("--pool", type=int, default=4, help="distinct synthetic batches cycled through")
+    ap.add_argument("--no-fuse", action="store_true", help="disable the fused collection update plan (A/B)")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    use_cuda = torch.cuda.is_available()
+    if use_cuda:
+        torch.cuda.set_device(local_rank)
+        device = torch.device("cuda", local_rank)
+    else:
+        device = torch.device("cpu")
+    if world > 1:
+        dist.init_process_group("nccl" if use_cuda else "gloo", device_id=device if use_cuda else None)
+
+    import torchmetrics_forked_amd as tm
+    from torchmetrics_forked_amd import ops
+
+    if use_cuda:
+        ops.require()
+
+    C, B = args.num_classes, args.batch
+    coll = tm.MetricCollection(
+        {
+            "auroc": tm.MulticlassAUROC(num_classes=C),
+            "confmat": tm.MulticlassConfusionMatrix(num_classes=C),
+        }
+    ).to(device)
+    if args.no_fuse:
+        coll._fused_plans = []
+
+    gen = torch.Generator(device=device).manual_seed(1234 + rank)
+    pool = []
+    for _ in range(args.pool):
+        logits = torch.randn(B, C, device=device, generator=gen, dtype=torch.float32).to(torch.bfloat16)
+        target = torch.randint(0, C, (B,), device=device, generator=gen)
+        pool.append((logits, target))
+
+    def sync() -> None:
+        if use_cuda:
+            torch.cuda.synchronize(device)
+
+    def barrier() -> None:
+        if world > 1:
+            dist.barrier()
+
+    # warmup (includes one compute so every kernel / collective path is initialised)
+    for i in range(args.warmup):
+        coll.update(*pool[i % args.pool])
+    if args.warmup:
+        coll.compute()
+    coll.reset()
+    sync()
+    barrier()
+    sync()
+
+    t0 = time.perf_counter()
+    ev_start = torch.cuda.Event(enable_timing=True) if use_cuda else None
+    ev_upd = torch.cuda.Event(enable_timing=True) if use_cuda else None
+    if use_cuda:
+        ev_start.record()
+    for i in range(args.steps):
+        coll.update(*pool[i % args.pool])
+    if use_cuda:
+        ev_upd.record()
+    res = coll.compute()
+    sync()
+    barrier()
+    sync()
+    elapsed = time.perf_counter() - t0
+    upd_ms = ev_start.elapsed_time(ev_upd) if use_cuda else float("nan")
+
+    t = torch.tensor([elapsed, upd_ms], dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed, upd_ms = float(t[0]), float(t[1])
+
+    if rank == 0:
+        value = world * args.steps / elapsed
+        base = _baseline()
+        out = {
+            "metric": "metric-updates/sec (whole node), MulticlassAUROC 1000-cls bs=65536",
+            "value": round(value, 3),
+            "unit": "updates/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1000.0 * elapsed / args.steps, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(value / base, 3) if base else None,
+            "dtype": "bf16",
+            "data": "synthetic (randn bf16 logits [65536,1000] + uniform int64 labels, pre-generated pool in HBM)",
+            "config": {
+                "model": "MulticlassAUROC(num_classes=1000)+MulticlassConfusionMatrix(num_classes=1000)",
+                "global_batch": B * world,
+                "seq_len": 1,
+                "parallelism": f"dp{world}",
+            },
+            "update_only_ms_per_step": round(upd_ms / args.steps, 4) if use_cuda else None,
+            "compute_incl_sync_ms": round(1000.0 * elapsed - (upd_ms if use_cuda else 0.0), 3),
+            "auroc": float(res["auroc"]),
+            "fused_update": not args.no_fuse,
+            "device": torch.cuda.get_device_name(device) if use_cuda else "cpu",
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

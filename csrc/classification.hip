@@ -406,14 +406,15 @@ __global__ void curve_hist_ml_kernel(const T* __restrict__ preds, const int64_t*
 // hist: int64 [C, 2, kCodes] updated in place.
 // task 0 = multiclass (preds [N, C], target [N]); task 1 = binary/multilabel (preds/target [N, L, ...]).
 void curve_hist_update(const at::Tensor& preds_, const at::Tensor& target_, at::Tensor& hist, int64_t task,
-                       int64_t ignore_index, bool has_ignore, c10::optional<at::Tensor> confmat) {
+                       int64_t ignore_index, bool has_ignore, c10::optional<at::Tensor> confmat,
+                       c10::optional<at::Tensor> norm_flag) {
   TORCH_CHECK(hist.is_contiguous() && hist.scalar_type() == at::kLong && hist.dim() == 3 && hist.size(1) == 2 &&
               hist.size(2) == kCodes, "hist must be int64 [C, 2, 16384]");
   auto preds = preds_.contiguous();
   auto target = target_.contiguous().to(at::kLong);
   const int C = static_cast<int>(hist.size(0));
   const int block = 256;
-  auto flag = range_flag(preds);
+  auto flag = norm_flag.has_value() ? norm_flag->to(at::kInt).contiguous() : range_flag(preds);
   int64_t* cm = nullptr;
   if (confmat.has_value()) {
     TORCH_CHECK(confmat->is_contiguous() && confmat->scalar_type() == at::kLong && confmat->numel() == (int64_t)C * C);
@@ -595,7 +596,8 @@ __global__ void binned_scan_kernel(const int* __restrict__ hist, int C, int nT, 
 }
 
 void binned_curve_update(const at::Tensor& preds_, const at::Tensor& target_, const at::Tensor& thresholds_,
-                         at::Tensor& confmat, int64_t task, int64_t ignore_index, bool has_ignore) {
+                         at::Tensor& confmat, int64_t task, int64_t ignore_index, bool has_ignore,
+                         c10::optional<at::Tensor> norm_flag) {
   auto preds = preds_.contiguous();
   auto target = target_.contiguous().to(at::kLong);
   auto thr = thresholds_.contiguous().to(at::kFloat);
@@ -603,7 +605,7 @@ void binned_curve_update(const at::Tensor& preds_, const at::Tensor& target_, co
   TORCH_CHECK(confmat.is_contiguous() && confmat.scalar_type() == at::kLong && confmat.dim() == 4 && confmat.size(0) == nT);
   const int C = static_cast<int>(confmat.size(1));
   auto hist = at::zeros({C, 2, nT + 1}, preds.options().dtype(at::kInt));
-  auto flag = range_flag(preds);
+  auto flag = norm_flag.has_value() ? norm_flag->to(at::kInt).contiguous() : range_flag(preds);
   const int block = 256;
   const size_t shm = nT * sizeof(float);
   TORCH_CHECK(shm <= 64 * 1024, "too many thresholds");
@@ -637,9 +639,9 @@ TORCH_LIBRARY_FRAGMENT(tmx, m) {
   m.def("bincount(Tensor x, int minlength) -> Tensor");
   m.def("mc_confmat_update(Tensor preds, Tensor target, Tensor(a!) confmat, int ignore_index, bool has_ignore) -> ()");
   m.def("binary_stats_update(Tensor preds, Tensor target, Tensor(a!) counts, int num_labels, float threshold, int ignore_index, bool has_ignore) -> ()");
-  m.def("curve_hist_update(Tensor preds, Tensor target, Tensor(a!) hist, int task, int ignore_index, bool has_ignore, Tensor(b!)? confmat) -> ()");
+  m.def("curve_hist_update(Tensor preds, Tensor target, Tensor(a!) hist, int task, int ignore_index, bool has_ignore, Tensor(b!)? confmat, Tensor? norm_flag) -> ()");
   m.def("curve_hist_reduce(Tensor hist) -> Tensor");
-  m.def("binned_curve_update(Tensor preds, Tensor target, Tensor thresholds, Tensor(a!) confmat, int task, int ignore_index, bool has_ignore) -> ()");
+  m.def("binned_curve_update(Tensor preds, Tensor target, Tensor thresholds, Tensor(a!) confmat, int task, int ignore_index, bool has_ignore, Tensor? norm_flag) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(tmx, CUDA, m) {

@@ -1,0 +1,136 @@
+"""Numerics of the gfx950 HIP kernels vs the eager PyTorch (CPU) implementation of the same op.
+
+Every op in ``torchmetrics_forked_amd.ops.classification`` is run on ``cuda:0`` (native library, mandatory) and
+on CPU (eager reference path) with identical inputs; integer states must match exactly, float reductions to
+fp64 rounding.
+"""
+import pytest
+import torch
+
+from torchmetrics_forked_amd import ops
+from torchmetrics_forked_amd.ops import classification as K
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_native(device):
+    ops.require()
+
+
+def _both(fn, *tensors, **kw):
+    """Run ``fn`` on (cuda copies, cpu copies); return the mutated/returned tensors of both."""
+    gpu = [t.cuda() if isinstance(t, torch.Tensor) else t for t in tensors]
+    cpu = [t.clone() if isinstance(t, torch.Tensor) else t for t in tensors]
+    rg = fn(*gpu, **kw)
+    rc = fn(*cpu, **kw)
+    torch.cuda.synchronize()
+    return gpu, cpu, rg, rc
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
+def test_range_flag(dtype):
+    x = torch.rand(10000).to(dtype)
+    assert int(K.range_flag(x.cuda()).item()) == 0
+    x[1234] = 1.5
+    assert int(K.range_flag(x.cuda()).item()) == 1
+    x[1234] = float("nan")
+    assert int(K.range_flag(x.cuda()).item()) == 1
+
+
+@pytest.mark.parametrize("minlength", [7, 1000, 70000])
+def test_bincount(minlength):
+    x = torch.randint(0, minlength, (200000,))
+    out = torch.ops.tmx.bincount(x.cuda(), minlength)
+    assert torch.equal(out.cpu(), torch.bincount(x, minlength=minlength))
+
+
+@pytest.mark.parametrize("C", [5, 33, 1000])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16, torch.int64])
+@pytest.mark.parametrize("ignore_index", [None, 2])
+def test_mc_confmat(C, dtype, ignore_index):
+    N = 5000
+    preds = torch.randint(0, C, (N,)) if dtype == torch.int64 else torch.randn(N, C).to(dtype)
+    target = torch.randint(0, C, (N,))
+    if ignore_index is not None:
+        target[::7] = ignore_index
+    g, c, _, _ = _both(K.mc_confmat_update, preds, target, torch.zeros(C, C, dtype=torch.long), ignore_index)
+    assert torch.equal(g[2].cpu(), c[2])
+
+
+@pytest.mark.parametrize("L", [1, 6])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.int64])
+@pytest.mark.parametrize("logits", [False, True])
+def test_binary_stats(L, dtype, logits):
+    N = 4000
+    if dtype == torch.int64:
+        preds = torch.randint(0, 2, (N, L, 3))
+    else:
+        preds = (torch.randn(N, L, 3) if logits else torch.rand(N, L, 3)).to(dtype)
+    target = torch.randint(0, 2, (N, L, 3))
+    target[::11] = -1
+    g, c, _, _ = _both(K.binary_stats_update, preds, target, torch.zeros(L, 4, dtype=torch.long), L, 0.5, -1)
+    assert torch.equal(g[2].cpu(), c[2])
+
+
+@pytest.mark.parametrize("C", [4, 257, 1000])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("probs", [False, True])
+def test_curve_hist_multiclass(C, dtype, probs):
+    N = 3000
+    x = torch.randn(N, C)
+    preds = (x.softmax(1) if probs else x).to(dtype)
+    target = torch.randint(0, C, (N,))
+    target[::13] = -1
+    hist = torch.zeros(C, 2, K.N_CODES, dtype=torch.long)
+    cm = torch.zeros(C, C, dtype=torch.long)
+    g, c, _, _ = _both(K.curve_hist_update, preds, target, hist, "multiclass", -1, cm)
+    # softmax rounding of the fused fp32 kernel may flip a handful of bf16 roundings vs ATen's softmax
+    diff = (g[2].cpu() - c[2]).abs().sum().item()
+    assert diff <= max(4, int(2e-4 * N * C)), diff
+    assert g[2].sum().item() == c[2].sum().item()
+    assert torch.equal(g[5].cpu(), c[5])  # fused argmax confusion matrix is exact
+    red_g = K.curve_hist_reduce(g[2]).cpu()
+    red_c = K.curve_hist_reduce(g[2].cpu())
+    torch.testing.assert_close(red_g, red_c, rtol=1e-12, atol=1e-12, equal_nan=True)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_curve_hist_multilabel(dtype):
+    N, L = 2000, 7
+    preds = torch.randn(N, L, 2).to(dtype)
+    target = torch.randint(0, 2, (N, L, 2))
+    target[::5, 0] = -1
+    hist = torch.zeros(L, 2, K.N_CODES, dtype=torch.long)
+    g, c, _, _ = _both(K.curve_hist_update, preds, target, hist, "multilabel", -1)
+    assert torch.equal(g[2].cpu(), c[2])
+
+
+@pytest.mark.parametrize("task,C", [("multiclass", 10), ("multilabel", 5), ("binary", 1)])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_binned_curve(task, C, dtype):
+    N, T = 3000, 11
+    thr = torch.linspace(0, 1, T)
+    if task == "multiclass":
+        preds, target = torch.randn(N, C).softmax(1).to(dtype), torch.randint(0, C, (N,))
+    else:
+        preds, target = torch.rand(N, C, 1).to(dtype), torch.randint(0, 2, (N, C, 1))
+    cm = torch.zeros(T, C, 2, 2, dtype=torch.long)
+    g, c, _, _ = _both(K.binned_curve_update, preds, target, thr, cm, task, None)
+    assert torch.equal(g[3].cpu(), c[3])
+
+
+def test_module_auroc_confmat_gpu_matches_cpu():
+    import torchmetrics_forked_amd as tm
+
+    C, N = 100, 8192
+    logits = torch.randn(N, C).bfloat16()
+    target = torch.randint(0, C, (N,))
+    out = []
+    for dev in ("cuda", "cpu"):
+        coll = tm.MetricCollection({"auroc": tm.MulticlassAUROC(num_classes=C), "cm": tm.MulticlassConfusionMatrix(num_classes=C)}).to(dev)
+        for i in range(4):
+            coll.update(logits[i::4].to(dev), target[i::4].to(dev))
+        out.append({k: v.cpu() for k, v in coll.compute().items()})
+    assert torch.equal(out[0]["cm"], out[1]["cm"])
+    assert abs(out[0]["auroc"].item() - out[1]["auroc"].item()) < 1e-4

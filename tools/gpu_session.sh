@@ -1,0 +1,30 @@
+#!/bin/bash
+# One GPU session: gpu tests, headline bench, rocprofv3 kernel stats, reference baseline.
+# Every GPU step has its own timeout; a fault/abort/timeout stops the session (no further GPU work).
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out
+mkdir -p $OUT
+export TMPDIR=/tmp
+stop_if_fatal() {  # $1 = exit code, $2 = step name
+  local rc=$1
+  if [ $rc -ge 124 ] || [ $rc -eq 134 ] || [ $rc -eq 139 ]; then
+    echo "FATAL step '$2' rc=$rc - stopping GPU session" | tee -a $OUT/session.log; exit $rc
+  fi
+  echo "step '$2' rc=$rc" | tee -a $OUT/session.log
+}
+STEPS="${STEPS:-pytest,bench,prof,ref}"
+if [[ $STEPS == *pytest* ]]; then
+  timeout -k 10 600 python -m pytest tests -m gpu -x -q > $OUT/pytest_gpu.log 2>&1; stop_if_fatal $? pytest; tail -5 $OUT/pytest_gpu.log
+fi
+if [[ $STEPS == *bench* ]]; then
+  timeout -k 10 300 python bench.py --steps 50 --warmup 5 > $OUT/bench.json 2> $OUT/bench.err; stop_if_fatal $? bench; cat $OUT/bench.json
+fi
+if [[ $STEPS == *prof* ]]; then
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 > $OUT/prof.log 2>&1; stop_if_fatal $? prof
+  find $OUT/prof -name "*kernel_stats.csv" | head -3
+fi
+if [[ $STEPS == *ref* ]]; then
+  timeout -k 10 900 python tools/ref_bench.py --steps 10 --warmup 2 > $OUT/ref_bench.json 2> $OUT/ref_bench.err; stop_if_fatal $? ref; cat $OUT/ref_bench.json
+fi
+echo "session done"

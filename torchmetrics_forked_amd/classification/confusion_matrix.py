@@ -1,0 +1,174 @@
+"""Confusion-matrix modules (API parity: reference ``classification/confusion_matrix.py:51-531``)."""
+from typing import Any, List, Optional, Tuple, Type
+
+import torch
+from torch import Tensor
+from typing_extensions import Literal
+
+from torchmetrics_forked_amd.classification.base import _ClassificationTaskWrapper
+from torchmetrics_forked_amd.classification.stat_scores import _task_factory
+from torchmetrics_forked_amd.functional.classification.confusion_matrix import (
+    _binary_confusion_matrix_arg_validation,
+    _binary_confusion_matrix_update,
+    _confusion_matrix_reduce,
+    _multiclass_confusion_matrix_arg_validation,
+    _multiclass_confusion_matrix_update,
+    _multilabel_confusion_matrix_arg_validation,
+    _multilabel_confusion_matrix_update,
+)
+from torchmetrics_forked_amd.functional.classification.stat_scores import (
+    _binary_stat_scores_tensor_validation,
+    _multiclass_stat_scores_tensor_validation,
+    _multilabel_stat_scores_tensor_validation,
+)
+from torchmetrics_forked_amd.metric import Metric
+from torchmetrics_forked_amd.utilities.plot import _AX_TYPE, _PLOT_OUT_TYPE, plot_confusion_matrix
+
+
+class _ConfmatPlot:
+    def plot(
+        self,
+        val: Optional[Tensor] = None,
+        ax: Optional[_AX_TYPE] = None,
+        add_text: bool = True,
+        labels: Optional[List[str]] = None,
+    ) -> _PLOT_OUT_TYPE:
+        val = val if val is not None else self.compute()  # type: ignore[attr-defined]
+        if not isinstance(val, Tensor):
+            raise TypeError(f"Expected val to be a single tensor but got {val}")
+        return plot_confusion_matrix(val, ax=ax, add_text=add_text, labels=labels)
+
+
+class BinaryConfusionMatrix(_ConfmatPlot, Metric):
+    """``[2, 2]`` confusion matrix for binary tasks."""
+
+    is_differentiable: bool = False
+    higher_is_better: Optional[bool] = None
+    full_state_update: bool = False
+    confmat: Tensor
+
+    def __init__(
+        self,
+        threshold: float = 0.5,
+        ignore_index: Optional[int] = None,
+        normalize: Optional[Literal["true", "pred", "all", "none"]] = None,
+        validate_args: bool = True,
+        **kwargs: Any,
+    ) -> None:
+        super().__init__(**kwargs)
+        if validate_args:
+            _binary_confusion_matrix_arg_validation(threshold, ignore_index, normalize)
+        self.threshold = threshold
+        self.ignore_index = ignore_index
+        self.normalize = normalize
+        self.validate_args = validate_args
+        self.add_state("confmat", torch.zeros(2, 2, dtype=torch.long), dist_reduce_fx="sum")
+
+    def update(self, preds: Tensor, target: Tensor) -> None:
+        if self.validate_args:
+            _binary_stat_scores_tensor_validation(preds, target, "global", self.ignore_index, self._validation_sink(target))
+        self.confmat += _binary_confusion_matrix_update(preds, target, self.threshold, self.ignore_index)
+
+    def compute(self) -> Tensor:
+        return _confusion_matrix_reduce(self.confmat, self.normalize)
+
+
+class MulticlassConfusionMatrix(_ConfmatPlot, Metric):
+    """``[C, C]`` confusion matrix for multiclass tasks (fused argmax + LDS histogram on device)."""
+
+    is_differentiable: bool = False
+    higher_is_better: Optional[bool] = None
+    full_state_update: bool = False
+    confmat: Tensor
+
+    def __init__(
+        self,
+        num_classes: int,
+        ignore_index: Optional[int] = None,
+        normalize: Optional[Literal["none", "true", "pred", "all"]] = None,
+        validate_args: bool = True,
+        **kwargs: Any,
+    ) -> None:
+        super().__init__(**kwargs)
+        if validate_args:
+            _multiclass_confusion_matrix_arg_validation(num_classes, ignore_index, normalize)
+        self.num_classes = num_classes
+        self.ignore_index = ignore_index
+        self.normalize = normalize
+        self.validate_args = validate_args
+        self.add_state("confmat", torch.zeros(num_classes, num_classes, dtype=torch.long), dist_reduce_fx="sum")
+
+    def _fusion_key(self) -> Optional[Tuple]:
+        return ("multiclass_scores", self.num_classes, self.ignore_index)
+
+    def _validate(self, preds: Tensor, target: Tensor) -> None:
+        if self.validate_args:
+            _multiclass_stat_scores_tensor_validation(
+                preds, target, self.num_classes, "global", self.ignore_index, self._validation_sink(target)
+            )
+
+    def update(self, preds: Tensor, target: Tensor) -> None:
+        self._validate(preds, target)
+        self.confmat += _multiclass_confusion_matrix_update(preds, target, self.num_classes, self.ignore_index)
+
+    def compute(self) -> Tensor:
+        return _confusion_matrix_reduce(self.confmat, self.normalize)
+
+
+class MultilabelConfusionMatrix(_ConfmatPlot, Metric):
+    """``[L, 2, 2]`` per-label confusion matrices."""
+
+    is_differentiable: bool = False
+    higher_is_better: Optional[bool] = None
+    full_state_update: bool = False
+    confmat: Tensor
+
+    def __init__(
+        self,
+        num_labels: int,
+        threshold: float = 0.5,
+        ignore_index: Optional[int] = None,
+        normalize: Optional[Literal["none", "true", "pred", "all"]] = None,
+        validate_args: bool = True,
+        **kwargs: Any,
+    ) -> None:
+        super().__init__(**kwargs)
+        if validate_args:
+            _multilabel_confusion_matrix_arg_validation(num_labels, threshold, ignore_index, normalize)
+        self.num_labels = num_labels
+        self.threshold = threshold
+        self.ignore_index = ignore_index
+        self.normalize = normalize
+        self.validate_args = validate_args
+        self.add_state("confmat", torch.zeros(num_labels, 2, 2, dtype=torch.long), dist_reduce_fx="sum")
+
+    def update(self, preds: Tensor, target: Tensor) -> None:
+        if self.validate_args:
+            _multilabel_stat_scores_tensor_validation(
+                preds, target, self.num_labels, "global", self.ignore_index, self._validation_sink(target)
+            )
+        self.confmat += _multilabel_confusion_matrix_update(preds, target, self.num_labels, self.threshold, self.ignore_index)
+
+    def compute(self) -> Tensor:
+        return _confusion_matrix_reduce(self.confmat, self.normalize)
+
+
+class ConfusionMatrix(_ClassificationTaskWrapper):
+    """Task wrapper returning Binary/Multiclass/MultilabelConfusionMatrix."""
+
+    def __new__(  # type: ignore[misc]
+        cls: Type["ConfusionMatrix"],
+        task: Literal["binary", "multiclass", "multilabel"],
+        threshold: float = 0.5,
+        num_classes: Optional[int] = None,
+        num_labels: Optional[int] = None,
+        normalize: Optional[Literal["true", "pred", "all", "none"]] = None,
+        ignore_index: Optional[int] = None,
+        validate_args: bool = True,
+        **kwargs: Any,
+    ) -> Metric:
+        kwargs.update({"normalize": normalize, "ignore_index": ignore_index, "validate_args": validate_args})
+        return _task_factory(
+            task, BinaryConfusionMatrix, MulticlassConfusionMatrix, MultilabelConfusionMatrix,
+            (threshold,), (num_classes,), (num_labels, threshold), num_classes, num_labels, None, kwargs,
+        )

@@ -1,0 +1,301 @@
+"""Precision-recall-curve modules and the shared curve-state machinery (API parity: reference
+``classification/precision_recall_curve.py:55-675``).
+
+State layout (``thresholds=None``):
+  * ``score_hist`` — exact ``int64 [C, 2, 16384]`` histogram for bf16/fp16 scores, ``"sum"``-reduced (RCCL
+    all-reduce), materialised lazily on the first 16-bit batch so fp32 users pay nothing;
+  * ``preds`` / ``target`` — ``cat`` lists (reference layout) for fp32/fp64 scores.
+With ``thresholds`` given the state is the reference's ``confmat [T, (C,) 2, 2]``.
+"""
+from typing import Any, List, Optional, Sequence, Tuple, Type, Union
+
+import torch
+import torch.distributed as dist
+from torch import Tensor
+from typing_extensions import Literal
+
+from torchmetrics_forked_amd.classification.base import _ClassificationTaskWrapper
+from torchmetrics_forked_amd.functional.classification import _curve_engine as eng
+from torchmetrics_forked_amd.functional.classification.precision_recall_curve import (
+    CurveState,
+    _adjust_threshold_arg,
+    _binary_precision_recall_curve_arg_validation,
+    _binary_precision_recall_curve_tensor_validation,
+    _multiclass_precision_recall_curve_arg_validation,
+    _multiclass_precision_recall_curve_tensor_validation,
+    _multilabel_precision_recall_curve_arg_validation,
+    _multilabel_precision_recall_curve_tensor_validation,
+    binary_curve_update,
+    multiclass_curve_update,
+    multilabel_curve_update,
+    precision_recall_curve_compute,
+)
+from torchmetrics_forked_amd.metric import Metric
+from torchmetrics_forked_amd.ops import classification as cls_ops
+from torchmetrics_forked_amd.utilities.data import dim_zero_cat
+from torchmetrics_forked_amd.utilities.enums import ClassificationTask
+from torchmetrics_forked_amd.utilities.plot import _AX_TYPE, _PLOT_OUT_TYPE, plot_curve
+
+
+class _CurveMetric(Metric):
+    """Owns the curve states; subclasses choose the task and implement ``compute`` from ``_curve_state()``."""
+
+    _task: str = "binary"
+    is_differentiable: bool = False
+    higher_is_better: Optional[bool] = None
+    full_state_update: bool = False
+
+    def _init_curve_states(self, num: int, thresholds: Optional[Union[int, List[float], Tensor]]) -> None:
+        self._num = num
+        self._hist_dtype: Optional[torch.dtype] = None
+        thresholds = _adjust_threshold_arg(thresholds)
+        if thresholds is None:
+            self.thresholds = thresholds
+            self.add_state("preds", default=[], dist_reduce_fx="cat")
+            self.add_state("target", default=[], dist_reduce_fx="cat")
+            self.add_state("score_hist", default=torch.zeros(0, dtype=torch.long), dist_reduce_fx="sum")
+        else:
+            self.register_buffer("thresholds", thresholds, persistent=False)
+            shape = (len(thresholds), 2, 2) if self._task == "binary" else (len(thresholds), num, 2, 2)
+            self.add_state("confmat", default=torch.zeros(*shape, dtype=torch.long), dist_reduce_fx="sum")
+
+    # -------------------------------------------------------------------------------------------- update
+    def _hist_ok(self, preds: Tensor) -> bool:
+        if preds.dtype not in eng.HIST_DTYPES:
+            return False
+        if self._hist_dtype is None or self._hist_dtype == preds.dtype or self.score_hist.numel() == 0:
+            return not (isinstance(self.preds, list) and len(self.preds) > 0)
+        return False
+
+    def _ensure_hist(self, device: torch.device) -> Tensor:
+        if self.score_hist.numel() == 0:
+            self.score_hist = torch.zeros(self._num, 2, eng.N_CODES, dtype=torch.long, device=device)
+        return self.score_hist
+
+    def _curve_update(self, preds: Tensor, target: Tensor, confmat_out: Optional[Tensor] = None) -> None:
+        thr = self.thresholds
+        ii = self.ignore_index
+        if thr is not None:
+            if self._task == "binary":
+                st = binary_curve_update(preds, target, thr, ii)
+                self.confmat += st[1][:, 0]
+            elif self._task == "multiclass":
+                self.confmat += multiclass_curve_update(preds, target, self._num, thr, ii)[1]
+            else:
+                self.confmat += multilabel_curve_update(preds, target, self._num, thr, ii)[1]
+            return
+        if self._hist_ok(preds):
+            hist = self._ensure_hist(preds.device)
+            self._hist_dtype = preds.dtype
+            if self._task == "binary":
+                cls_ops.curve_hist_update(preds.reshape(-1, 1, 1), target.reshape(-1, 1, 1), hist, "binary", ii)
+            elif self._task == "multiclass":
+                p = torch.movedim(preds, 1, -1).reshape(-1, self._num)
+                cls_ops.curve_hist_update(p, target.reshape(-1), hist, "multiclass", ii, confmat_out)
+            else:
+                cls_ops.curve_hist_update(preds, target, hist, "multilabel", ii)
+            return
+        if self.score_hist.numel() > 0:
+            raise NotImplementedError(
+                "Mixing 16-bit (exact-histogram) and 32/64-bit score batches in one curve metric is not supported;"
+                f" got {preds.dtype} after {self._hist_dtype}. Cast the inputs to one dtype."
+            )
+        if self._task == "binary":
+            st = binary_curve_update(preds, target, None, ii, force_samples=True)
+        elif self._task == "multiclass":
+            st = multiclass_curve_update(preds, target, self._num, None, ii, force_samples=True)
+        else:
+            st = multilabel_curve_update(preds, target, self._num, None, ii, force_samples=True)
+        self.preds.append(st[1])
+        self.target.append(st[2])
+
+    # ---------------------------------------------------------------------------------------------- sync
+    def _sync_dist(self, dist_sync_fn: Any = None, process_group: Optional[Any] = None) -> None:
+        if self.thresholds is None:
+            group = process_group or self.process_group
+            used = torch.tensor([1 if self.score_hist.numel() > 0 else 0], dtype=torch.int32)
+            backend = dist.get_backend(group) if group is not None else dist.get_backend()
+            dev = self.score_hist.device if backend != "nccl" or self.score_hist.is_cuda else torch.device("cuda")
+            used = used.to(dev if backend == "nccl" else "cpu")
+            dist.all_reduce(used, op=dist.ReduceOp.MAX, group=group)
+            if int(used.item()) and self.score_hist.numel() == 0:
+                self._ensure_hist(self.device)
+        super()._sync_dist(dist_sync_fn, process_group)
+
+    # ------------------------------------------------------------------------------------------- compute
+    def _curve_state(self) -> CurveState:
+        if self.thresholds is not None:
+            cm = self.confmat.unsqueeze(1) if self._task == "binary" else self.confmat
+            return ("binned", cm)
+        if isinstance(self.score_hist, Tensor) and self.score_hist.numel() > 0:
+            return ("hist", self.score_hist, self._hist_dtype or torch.bfloat16)
+        return ("samples", dim_zero_cat(self.preds), dim_zero_cat(self.target))
+
+    def plot(
+        self, curve: Optional[Tuple] = None, score: Optional[Union[Tensor, bool]] = None, ax: Optional[_AX_TYPE] = None
+    ) -> _PLOT_OUT_TYPE:
+        curve_computed = curve or self.compute()
+        if isinstance(curve_computed, Tensor):
+            return self._plot(curve_computed, ax)
+        score = self._auc_for_plot(curve_computed) if isinstance(score, bool) and score else score
+        return plot_curve(curve_computed, score=score, ax=ax, label_names=self._label_names, name=self.__class__.__name__)
+
+    _label_names = ("Recall", "Precision")
+
+    def _auc_for_plot(self, curve: Tuple) -> Optional[Tensor]:
+        from torchmetrics_forked_amd.utilities.compute import _auc_compute_without_check
+
+        x, y = curve[1], curve[0]
+        if isinstance(x, Tensor) and x.ndim == 1:
+            return _auc_compute_without_check(x, y, -1.0)
+        return torch.stack([_auc_compute_without_check(a, b, -1.0) for a, b in zip(x, y)])
+
+
+class BinaryPrecisionRecallCurve(_CurveMetric):
+    """Precision-recall curve for binary tasks."""
+
+    _task = "binary"
+
+    def __init__(
+        self,
+        thresholds: Optional[Union[int, List[float], Tensor]] = None,
+        ignore_index: Optional[int] = None,
+        validate_args: bool = True,
+        **kwargs: Any,
+    ) -> None:
+        super().__init__(**kwargs)
+        if validate_args:
+            _binary_precision_recall_curve_arg_validation(thresholds, ignore_index)
+        self.ignore_index = ignore_index
+        self.validate_args = validate_args
+        self._init_curve_states(1, thresholds)
+
+    def update(self, preds: Tensor, target: Tensor) -> None:
+        if self.validate_args:
+            _binary_precision_recall_curve_tensor_validation(preds, target, self.ignore_index, self._validation_sink(target))
+        self._curve_update(preds, target)
+
+    def compute(self) -> Tuple[Tensor, Tensor, Tensor]:
+        return precision_recall_curve_compute(self._curve_state(), "binary", 1, self.thresholds)
+
+
+class MulticlassPrecisionRecallCurve(_CurveMetric):
+    """One-vs-rest precision-recall curves for multiclass tasks."""
+
+    _task = "multiclass"
+
+    def __init__(
+        self,
+        num_classes: int,
+        thresholds: Optional[Union[int, List[float], Tensor]] = None,
+        average: Optional[Literal["micro", "macro"]] = None,
+        ignore_index: Optional[int] = None,
+        validate_args: bool = True,
+        **kwargs: Any,
+    ) -> None:
+        super().__init__(**kwargs)
+        if validate_args:
+            _multiclass_precision_recall_curve_arg_validation(num_classes, thresholds, ignore_index, average)
+        self.num_classes = num_classes
+        self.average = average
+        self.ignore_index = ignore_index
+        self.validate_args = validate_args
+        self._init_curve_states(num_classes, thresholds)
+
+    def _fusion_key(self) -> Optional[Tuple]:
+        """Key under which a ``MetricCollection`` may fuse this update with others (see ``ops.fused``)."""
+        if self.thresholds is not None:
+            return None
+        return ("multiclass_scores", self.num_classes, self.ignore_index)
+
+    def update(self, preds: Tensor, target: Tensor) -> None:
+        if self.validate_args:
+            _multiclass_precision_recall_curve_tensor_validation(
+                preds, target, self.num_classes, self.ignore_index, self._validation_sink(target)
+            )
+        self._curve_update(preds, target)
+
+    def compute(self) -> Union[Tuple[Tensor, Tensor, Tensor], Tuple[List[Tensor], List[Tensor], List[Tensor]]]:
+        return precision_recall_curve_compute(
+            self._curve_state(), "multiclass", self.num_classes, self.thresholds, self.ignore_index, self.average
+        )
+
+
+class MultilabelPrecisionRecallCurve(_CurveMetric):
+    """Per-label precision-recall curves."""
+
+    _task = "multilabel"
+
+    def __init__(
+        self,
+        num_labels: int,
+        thresholds: Optional[Union[int, List[float], Tensor]] = None,
+        ignore_index: Optional[int] = None,
+        validate_args: bool = True,
+        **kwargs: Any,
+    ) -> None:
+        super().__init__(**kwargs)
+        if validate_args:
+            _multilabel_precision_recall_curve_arg_validation(num_labels, thresholds, ignore_index)
+        self.num_labels = num_labels
+        self.ignore_index = ignore_index
+        self.validate_args = validate_args
+        self._init_curve_states(num_labels, thresholds)
+
+    def update(self, preds: Tensor, target: Tensor) -> None:
+        if self.validate_args:
+            _multilabel_precision_recall_curve_tensor_validation(
+                preds, target, self.num_labels, self.ignore_index, self._validation_sink(target)
+            )
+        self._curve_update(preds, target)
+
+    def compute(self) -> Union[Tuple[Tensor, Tensor, Tensor], Tuple[List[Tensor], List[Tensor], List[Tensor]]]:
+        return precision_recall_curve_compute(
+            self._curve_state(), "multilabel", self.num_labels, self.thresholds, self.ignore_index
+        )
+
+
+def _curve_task_factory(
+    task: str,
+    binary_cls: Type[Metric],
+    multiclass_cls: Type[Metric],
+    multilabel_cls: Type[Metric],
+    binary_args: tuple,
+    multiclass_args: tuple,
+    multilabel_args: tuple,
+    num_classes: Optional[int],
+    num_labels: Optional[int],
+    kwargs: dict,
+) -> Metric:
+    task = ClassificationTask.from_str(task)
+    if task == ClassificationTask.BINARY:
+        return binary_cls(*binary_args, **kwargs)
+    if task == ClassificationTask.MULTICLASS:
+        if not isinstance(num_classes, int):
+            raise ValueError(f"`num_classes` is expected to be `int` but `{type(num_classes)} was passed.`")
+        return multiclass_cls(*multiclass_args, **kwargs)
+    if task == ClassificationTask.MULTILABEL:
+        if not isinstance(num_labels, int):
+            raise ValueError(f"`num_labels` is expected to be `int` but `{type(num_labels)} was passed.`")
+        return multilabel_cls(*multilabel_args, **kwargs)
+    raise ValueError(f"Task {task} not supported!")
+
+
+class PrecisionRecallCurve(_ClassificationTaskWrapper):
+    """Task wrapper returning Binary/Multiclass/MultilabelPrecisionRecallCurve."""
+
+    def __new__(  # type: ignore[misc]
+        cls: Type["PrecisionRecallCurve"],
+        task: Literal["binary", "multiclass", "multilabel"],
+        thresholds: Optional[Union[int, List[float], Tensor]] = None,
+        num_classes: Optional[int] = None,
+        num_labels: Optional[int] = None,
+        ignore_index: Optional[int] = None,
+        validate_args: bool = True,
+        **kwargs: Any,
+    ) -> Metric:
+        kwargs.update({"thresholds": thresholds, "ignore_index": ignore_index, "validate_args": validate_args})
+        return _curve_task_factory(
+            task, BinaryPrecisionRecallCurve, MulticlassPrecisionRecallCurve, MultilabelPrecisionRecallCurve,
+            (), (num_classes,), (num_labels,), num_classes, num_labels, kwargs,
+        )

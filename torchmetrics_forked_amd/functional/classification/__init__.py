@@ -1,0 +1,35 @@
+"""Functional classification metrics (API parity: reference ``functional/classification/__init__.py``)."""
+from torchmetrics_forked_amd.functional.classification.accuracy import (
+    accuracy, binary_accuracy, multiclass_accuracy, multilabel_accuracy,
+)
+from torchmetrics_forked_amd.functional.classification.auroc import auroc, binary_auroc, multiclass_auroc, multilabel_auroc
+from torchmetrics_forked_amd.functional.classification.average_precision import (
+    average_precision, binary_average_precision, multiclass_average_precision, multilabel_average_precision,
+)
+from torchmetrics_forked_amd.functional.classification.confusion_matrix import (
+    binary_confusion_matrix, confusion_matrix, multiclass_confusion_matrix, multilabel_confusion_matrix,
+)
+from torchmetrics_forked_amd.functional.classification.f_beta import (
+    binary_f1_score, binary_fbeta_score, f1_score, fbeta_score, multiclass_f1_score, multiclass_fbeta_score,
+    multilabel_f1_score, multilabel_fbeta_score,
+)
+from torchmetrics_forked_amd.functional.classification.hamming import (
+    binary_hamming_distance, hamming_distance, multiclass_hamming_distance, multilabel_hamming_distance,
+)
+from torchmetrics_forked_amd.functional.classification.precision_recall import (
+    binary_precision, binary_recall, multiclass_precision, multiclass_recall, multilabel_precision, multilabel_recall,
+    precision, recall,
+)
+from torchmetrics_forked_amd.functional.classification.precision_recall_curve import (
+    binary_precision_recall_curve, multiclass_precision_recall_curve, multilabel_precision_recall_curve,
+    precision_recall_curve,
+)
+from torchmetrics_forked_amd.functional.classification.roc import binary_roc, multiclass_roc, multilabel_roc, roc
+from torchmetrics_forked_amd.functional.classification.specificity import (
+    binary_specificity, multiclass_specificity, multilabel_specificity, specificity,
+)
+from torchmetrics_forked_amd.functional.classification.stat_scores import (
+    binary_stat_scores, multiclass_stat_scores, multilabel_stat_scores, stat_scores,
+)
+
+__all__ = [k for k in dir() if not k.startswith("_")]

@@ -62,6 +62,18 @@ def binary_stats_update(
     counts += torch.stack([tp, fp, tn, fn], dim=1)
 
 
+def _norm_flag(preds: Tensor, target: Tensor, task: str, ignore_index: Optional[int]) -> Optional[Tensor]:
+    """Range flag restricted to non-ignored rows/elements (reference removes ignored data *before* the
+    sigmoid/softmax decision for binary & multiclass curves, ``precision_recall_curve.py:176-184,441-448``)."""
+    if ignore_index is None or task == "multilabel":
+        return None
+    bad = ~((preds >= 0) & (preds <= 1))
+    t = target.reshape(-1)
+    keep = t != ignore_index
+    bad = bad.reshape(t.shape[0], -1) & keep.unsqueeze(1)
+    return bad.any().reshape(1).int()
+
+
 def _codes(x: Tensor) -> Tensor:
     """Order-preserving integer code of a 16-bit float in [0, 1]; -1 for values outside (NaN, <0, >1)."""
     bits = x.contiguous().view(torch.int16).to(torch.int32) & 0xFFFF
@@ -89,7 +101,8 @@ def curve_hist_update(
     tcode = 0 if task == "multiclass" else 1
     if ops.use_native(target):
         torch.ops.tmx.curve_hist_update(
-            preds, target, hist, tcode, -1 if ignore_index is None else ignore_index, ignore_index is not None, confmat
+            preds, target, hist, tcode, -1 if ignore_index is None else ignore_index, ignore_index is not None, confmat,
+            _norm_flag(preds, target, task, ignore_index),
         )
         return
     C = hist.shape[0]
@@ -109,7 +122,10 @@ def curve_hist_update(
         n = target.shape[0]
         p = preds.reshape(n, C, -1)
         t = target.reshape(n, C, -1).long()
-        if not bool(((p >= 0) & (p <= 1)).all()):
+        in_range = (p >= 0) & (p <= 1)
+        if task == "binary" and ignore_index is not None:
+            in_range |= t == ignore_index
+        if not bool(in_range.all()):
             p = p.sigmoid()
         code = _codes(p).long()
         cls = torch.arange(C, device=p.device).view(1, C, 1).expand_as(code)
@@ -148,7 +164,8 @@ def binned_curve_update(
     tcode = 0 if task == "multiclass" else 1
     if ops.use_native(target):
         torch.ops.tmx.binned_curve_update(
-            preds, target, thresholds, confmat, tcode, -1 if ignore_index is None else ignore_index, ignore_index is not None
+            preds, target, thresholds, confmat, tcode, -1 if ignore_index is None else ignore_index, ignore_index is not None,
+            _norm_flag(preds, target, task, ignore_index),
         )
         return
     T, C = confmat.shape[0], confmat.shape[1]
@@ -166,7 +183,10 @@ def binned_curve_update(
         n = target.shape[0]
         p = preds.reshape(n, C, -1)
         t = target.reshape(n, C, -1).long()
-        if not bool(((p >= 0) & (p <= 1)).all()):
+        in_range = (p >= 0) & (p <= 1)
+        if task == "binary" and ignore_index is not None:
+            in_range |= t == ignore_index
+        if not bool(in_range.all()):
             p = p.sigmoid()
         p = p.transpose(1, 2).reshape(-1, C)
         lab = t.transpose(1, 2).reshape(-1, C)

@@ -94,6 +94,8 @@ def interp(x: Tensor, xp: Tensor, fp: Tensor) -> Tensor:
     """
     slope = _safe_divide(fp[1:] - fp[:-1], xp[1:] - xp[:-1])
     intercept = fp[:-1] - slope * xp[:-1]
-    idx = torch.searchsorted(xp.contiguous(), x.contiguous(), right=True) - 1
+    # segment index = #(xp <= x) - 1, which is order independent (identical to the reference even when
+    # xp is not monotone, e.g. macro-averaged PR curves); counted with a sort + binary search.
+    idx = torch.searchsorted(torch.sort(xp).values.contiguous(), x.contiguous(), right=True) - 1
     idx = idx.clamp(0, slope.numel() - 1)
     return slope[idx] * x + intercept[idx]
