@@ -13,11 +13,14 @@ stop_if_fatal() {  # $1 = exit code, $2 = step name
   fi
   echo "step '$2' rc=$rc" | tee -a $OUT/session.log
 }
-STEPS="${STEPS:-pytest,bench,prof,ref}"
+STEPS="${STEPS:-pytest,kbench,bench,prof,ref}"
 if [[ $STEPS == *pytest* ]]; then
   timeout -k 10 600 python -m pytest tests -m gpu -x -q > $OUT/pytest_gpu.log 2>&1; stop_if_fatal $? pytest; tail -5 $OUT/pytest_gpu.log
 fi
-if [[ $STEPS == *bench* ]]; then
+if [[ $STEPS == *kbench* ]]; then
+  timeout -k 10 300 python tools/kbench.py > $OUT/kbench.json 2> $OUT/kbench.err; stop_if_fatal $? kbench; cat $OUT/kbench.json
+fi
+if [[ $STEPS == *,bench* ]] || [[ $STEPS == bench* ]]; then
   timeout -k 10 300 python bench.py --steps 50 --warmup 5 > $OUT/bench.json 2> $OUT/bench.err; stop_if_fatal $? bench; cat $OUT/bench.json
 fi
 if [[ $STEPS == *prof* ]]; then
