@@ -41,7 +41,21 @@ template <typename T>
 __global__ void range_flag16_kernel(const uint4* __restrict__ xv, int64_t nvec, const uint16_t* __restrict__ tail,
                                     int ntail, int* __restrict__ flag) {
   bool bad = false;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * blockDim.x) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  // 4 independent 16-B loads in flight per lane before any compare
+  for (; i + 3 * stride < nvec; i += 4 * stride) {
+    uint4 w[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) w[u] = xv[i + u * stride];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint32_t parts[4] = {w[u].x, w[u].y, w[u].z, w[u].w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) bad |= bad16<T>(parts[k] & 0xFFFFu) | bad16<T>(parts[k] >> 16);
+    }
+  }
+  for (; i < nvec; i += stride) {
     uint4 w = xv[i];
     const uint32_t parts[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
@@ -370,7 +384,7 @@ template <typename T, int VPT>
 __global__ void __launch_bounds__(256) curve_hist_mc_kernel(const T* __restrict__ preds, const int64_t* __restrict__ target,
                                                             int64_t n, int C, const int* __restrict__ softmax_flag,
                                                             int64_t ignore_index, bool has_ignore, int64_t* __restrict__ hist,
-                                                            int64_t* __restrict__ confmat) {
+                                                            int64_t* __restrict__ confmat, int* __restrict__ err) {
   const int lane = threadIdx.x & (kWave - 1);
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / kWave;
   const int64_t nwaves = (int64_t)gridDim.x * blockDim.x / kWave;
@@ -378,6 +392,7 @@ __global__ void __launch_bounds__(256) curve_hist_mc_kernel(const T* __restrict_
   for (int64_t r = wave; r < n; r += nwaves) {
     const int64_t t = target[r];
     if (has_ignore && t == ignore_index) continue;
+    if ((t < 0 || t >= C) && err != nullptr && lane == 0) atomicOr(err, 1);
     const T* row = preds + r * C;
     float v[VPT];
 #pragma unroll
@@ -431,7 +446,7 @@ __global__ void __launch_bounds__(256) curve_hist_mc_kernel(const T* __restrict_
 //       int64 atomic per non-empty bin on flush (consecutive codes -> contiguous atomics).
 // Replaces 1 scattered 64-bit global atomic per score (2.8 ms/update at 65536x1000 on MI355X).
 // ---------------------------------------------------------------------------------------------------------
-constexpr int kTileRows = 64;
+constexpr int kTileRows = 32;   // 16 packed dwords per class -> 64 KiB LDS at C=1024, 2 WGs/CU
 constexpr int kA_Threads = 512;
 
 template <typename T> __device__ __forceinline__ void unpack8(const uint4& w, float* v);
@@ -461,12 +476,12 @@ template <typename T> __device__ __forceinline__ uint16_t raw_bits(const uint4& 
 }
 
 template <typename T>
-__global__ void __launch_bounds__(kA_Threads) mc_codes_kernel(const T* __restrict__ preds, const int64_t* __restrict__ target,
-                                                               int64_t n, int C, const int* __restrict__ softmax_flag,
-                                                               int64_t ignore_index, bool has_ignore,
-                                                               uint32_t* __restrict__ codes, int64_t n_pad,
-                                                               int64_t* __restrict__ confmat) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t s_tile[];  // [C][32]
+__global__ void __launch_bounds__(kA_Threads, 4) mc_codes_kernel(const T* __restrict__ preds, const int64_t* __restrict__ target,
+                                                                  int64_t n, int C, const int* __restrict__ softmax_flag,
+                                                                  int64_t ignore_index, bool has_ignore,
+                                                                  uint32_t* __restrict__ codes, int64_t n_pad,
+                                                                  int64_t* __restrict__ confmat, int* __restrict__ err) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_tile[];  // [C][kTileRows / 2]
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = threadIdx.x / kWave;
   const int nwaves = kA_Threads / kWave;
@@ -485,6 +500,7 @@ __global__ void __launch_bounds__(kA_Threads) mc_codes_kernel(const T* __restric
         bool valid = r < n;
         const int64_t t = valid ? target[r] : -1;
         if (has_ignore && t == ignore_index) valid = false;
+        if (valid && (t < 0 || t >= C) && err != nullptr && lane == 0) atomicOr(err, 1);
         uint4 w[2];
         float v[16];
 #pragma unroll
@@ -538,15 +554,16 @@ __global__ void __launch_bounds__(kA_Threads) mc_codes_kernel(const T* __restric
       for (int j = 0; j < 16; ++j) {
         const int q = lane + kWave * (j >> 3);
         const int c = 8 * q + (j & 7);
-        if (c < C) s_tile[c * 32 + (p ^ (q & 31))] = packed[j];
+        if (c < C) s_tile[c * (kTileRows / 2) + (p ^ (q & (kTileRows / 2 - 1)))] = packed[j];
       }
     }
     __syncthreads();
     const int64_t seg = r0 / 2;  // dword offset of this tile inside a class row
-    for (int idx = threadIdx.x; idx < C * 32; idx += kA_Threads) {
-      const int c = idx >> 5, d = idx & 31;
+    constexpr int kSlots = kTileRows / 2;
+    for (int idx = threadIdx.x; idx < C * kSlots; idx += kA_Threads) {
+      const int c = idx / kSlots, d = idx % kSlots;
       const uint32_t wv = s_tile[idx];
-      const int p = d ^ ((c >> 3) & 31);
+      const int p = d ^ ((c >> 3) & (kSlots - 1));
       codes[(int64_t)c * (n_pad / 2) + seg + p] = wv;
     }
     __syncthreads();
@@ -579,25 +596,34 @@ __global__ void __launch_bounds__(256) class_hist_kernel(const uint16_t* __restr
   }
   __syncthreads();
   int64_t* neg_hist = hist + ((int64_t)c * 2) * kCodes;
-  for (int i = threadIdx.x; i < kCodes; i += blockDim.x) {
-    const uint32_t cnt = s_neg[i];
-    if (cnt) atomic_add_i64(neg_hist + i, cnt);
+  if (splits == 1) {
+    // this workgroup is the only writer of class c's negative bins in this launch: plain read-modify-write
+    for (int i = threadIdx.x; i < kCodes; i += blockDim.x) {
+      const uint32_t cnt = s_neg[i];
+      if (cnt) neg_hist[i] += cnt;
+    }
+  } else {
+    for (int i = threadIdx.x; i < kCodes; i += blockDim.x) {
+      const uint32_t cnt = s_neg[i];
+      if (cnt) atomic_add_i64(neg_hist + i, cnt);
+    }
   }
 }
 
 template <typename T>
 void launch_two_pass(const T* p, const int64_t* target, int64_t n, int C, const int* flag, int64_t ignore_index,
-                     bool has_ignore, int64_t* hist, int64_t* cm, const at::TensorOptions& opts) {
+                     bool has_ignore, int64_t* hist, int64_t* cm, int* err, const at::TensorOptions& opts) {
   const int64_t n_pad = (n + kTileRows - 1) / kTileRows * kTileRows;
   auto codes = at::empty({(int64_t)C * n_pad}, opts.dtype(at::kShort));
   const int64_t ntiles = n_pad / kTileRows;
-  const size_t shm_a = (size_t)C * 32 * sizeof(uint32_t);
-  const int grid_a = static_cast<int>(std::min<int64_t>(ntiles, 256 * 4));
+  const size_t shm_a = (size_t)C * (kTileRows / 2) * sizeof(uint32_t);
+  const int grid_a = static_cast<int>(std::min<int64_t>(ntiles, 256 * 8));
   hipLaunchKernelGGL(mc_codes_kernel<T>, grid_a, kA_Threads, shm_a, stream(), p, target, n, C, flag, ignore_index, has_ignore,
-                     reinterpret_cast<uint32_t*>(codes.data_ptr()), n_pad, cm);
+                     reinterpret_cast<uint32_t*>(codes.data_ptr()), n_pad, cm, err);
   TMX_LAUNCH_CHECK();
+  // row splits only when there are too few classes to fill the chip (exclusive-owner flush when splits == 1)
   int splits = 1;
-  while ((int64_t)C * splits < 2048 && n_pad / (8 * (splits * 2)) >= 1024) splits *= 2;
+  while ((int64_t)C * splits < 512 && n_pad / (8 * (splits * 2)) >= 1024) splits *= 2;
   hipLaunchKernelGGL(class_hist_kernel, C * splits, 256, kCodes * sizeof(uint32_t), stream(),
                      reinterpret_cast<const uint16_t*>(codes.data_ptr()), n_pad, splits, hist);
   TMX_LAUNCH_CHECK();
@@ -629,7 +655,7 @@ __global__ void curve_hist_ml_kernel(const T* __restrict__ preds, const int64_t*
 // task 0 = multiclass (preds [N, C], target [N]); task 1 = binary/multilabel (preds/target [N, L, ...]).
 void curve_hist_update(const at::Tensor& preds_, const at::Tensor& target_, at::Tensor& hist, int64_t task,
                        int64_t ignore_index, bool has_ignore, c10::optional<at::Tensor> confmat,
-                       c10::optional<at::Tensor> norm_flag) {
+                       c10::optional<at::Tensor> norm_flag, c10::optional<at::Tensor> err_flag) {
   TORCH_CHECK(hist.is_contiguous() && hist.scalar_type() == at::kLong && hist.dim() == 3 && hist.size(1) == 2 &&
               hist.size(2) == kCodes, "hist must be int64 [C, 2, 16384]");
   auto preds = preds_.contiguous();
@@ -642,6 +668,11 @@ void curve_hist_update(const at::Tensor& preds_, const at::Tensor& target_, at::
     TORCH_CHECK(confmat->is_contiguous() && confmat->scalar_type() == at::kLong && confmat->numel() == (int64_t)C * C);
     cm = confmat->data_ptr<int64_t>();
   }
+  int* err = nullptr;
+  if (err_flag.has_value()) {
+    TORCH_CHECK(err_flag->scalar_type() == at::kInt && err_flag->is_contiguous(), "err_flag must be int32");
+    err = err_flag->data_ptr<int>();
+  }
   TMX_DISPATCH_HALF(preds.scalar_type(), "curve_hist_update", [&] {
     const scalar_t* p = reinterpret_cast<const scalar_t*>(preds.data_ptr());
     if (task == 0) {
@@ -651,20 +682,20 @@ void curve_hist_update(const at::Tensor& preds_, const at::Tensor& target_, at::
       const bool aligned = (reinterpret_cast<uintptr_t>(p) & 15) == 0;
       if (C % 8 == 0 && C <= 8 * 2 * kWave && aligned) {
         launch_two_pass<scalar_t>(p, target.data_ptr<int64_t>(), n, C, flag.data_ptr<int>(), ignore_index, has_ignore,
-                                  hist.data_ptr<int64_t>(), cm, preds.options());
+                                  hist.data_ptr<int64_t>(), cm, err, preds.options());
         return;
       }
       const int grid = grid_for(n * kWave, block, 4096);
       if (C <= 64 * 4) {
         hipLaunchKernelGGL((curve_hist_mc_kernel<scalar_t, 4>), grid, block, 0, stream(), p, target.data_ptr<int64_t>(), n, C,
-                           flag.data_ptr<int>(), ignore_index, has_ignore, hist.data_ptr<int64_t>(), cm);
+                           flag.data_ptr<int>(), ignore_index, has_ignore, hist.data_ptr<int64_t>(), cm, err);
       } else if (C <= 64 * 16) {
         hipLaunchKernelGGL((curve_hist_mc_kernel<scalar_t, 16>), grid, block, 0, stream(), p, target.data_ptr<int64_t>(), n, C,
-                           flag.data_ptr<int>(), ignore_index, has_ignore, hist.data_ptr<int64_t>(), cm);
+                           flag.data_ptr<int>(), ignore_index, has_ignore, hist.data_ptr<int64_t>(), cm, err);
       } else {
         TORCH_CHECK(C <= 64 * 64, "curve_hist_update: num_classes > 4096 not supported by the exact histogram path");
         hipLaunchKernelGGL((curve_hist_mc_kernel<scalar_t, 64>), grid, block, 0, stream(), p, target.data_ptr<int64_t>(), n, C,
-                           flag.data_ptr<int>(), ignore_index, has_ignore, hist.data_ptr<int64_t>(), cm);
+                           flag.data_ptr<int>(), ignore_index, has_ignore, hist.data_ptr<int64_t>(), cm, err);
       }
     } else {
       const int64_t total = target.numel();
@@ -874,7 +905,7 @@ TORCH_LIBRARY_FRAGMENT(tmx, m) {
   m.def("bincount(Tensor x, int minlength) -> Tensor");
   m.def("mc_confmat_update(Tensor preds, Tensor target, Tensor(a!) confmat, int ignore_index, bool has_ignore) -> ()");
   m.def("binary_stats_update(Tensor preds, Tensor target, Tensor(a!) counts, int num_labels, float threshold, int ignore_index, bool has_ignore) -> ()");
-  m.def("curve_hist_update(Tensor preds, Tensor target, Tensor(a!) hist, int task, int ignore_index, bool has_ignore, Tensor(b!)? confmat, Tensor? norm_flag) -> ()");
+  m.def("curve_hist_update(Tensor preds, Tensor target, Tensor(a!) hist, int task, int ignore_index, bool has_ignore, Tensor(b!)? confmat, Tensor? norm_flag, Tensor(c!)? err_flag) -> ()");
   m.def("curve_hist_reduce(Tensor hist) -> Tensor");
   m.def("binned_curve_update(Tensor preds, Tensor target, Tensor thresholds, Tensor(a!) confmat, int task, int ignore_index, bool has_ignore, Tensor? norm_flag) -> ()");
 }

@@ -101,10 +101,10 @@ class MulticlassConfusionMatrix(_ConfmatPlot, Metric):
     def _fusion_key(self) -> Optional[Tuple]:
         return ("multiclass_scores", self.num_classes, self.ignore_index)
 
-    def _validate(self, preds: Tensor, target: Tensor) -> None:
+    def _validate(self, preds: Tensor, target: Tensor, check_values: bool = True) -> None:
         if self.validate_args:
             _multiclass_stat_scores_tensor_validation(
-                preds, target, self.num_classes, "global", self.ignore_index, self._validation_sink(target)
+                preds, target, self.num_classes, "global", self.ignore_index, self._validation_sink(target), check_values
             )
 
     def update(self, preds: Tensor, target: Tensor) -> None:

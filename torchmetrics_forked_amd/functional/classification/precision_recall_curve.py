@@ -101,9 +101,19 @@ def _multiclass_precision_recall_curve_arg_validation(
     _binary_precision_recall_curve_arg_validation(thresholds, ignore_index)
 
 
+TARGET_RANGE_MSG = "Detected more unique values in `target` than `num_classes`."
+
+
 def _multiclass_precision_recall_curve_tensor_validation(
-    preds: Tensor, target: Tensor, num_classes: int, ignore_index: Optional[int] = None, sink: Optional[DeferredChecks] = None
+    preds: Tensor,
+    target: Tensor,
+    num_classes: int,
+    ignore_index: Optional[int] = None,
+    sink: Optional[DeferredChecks] = None,
+    check_values: bool = True,
 ) -> None:
+    """Shape/dtype checks on the host; the target value check is eager, deferred, or (``check_values=False``)
+    left to a native kernel that ORs into the sink's device flag while it streams the data."""
     if not preds.ndim == target.ndim + 1:
         raise ValueError(f"Expected `preds` to have one more dimension than `target` but got {preds.ndim} and {target.ndim}")
     if target.is_floating_point():
@@ -119,6 +129,8 @@ def _multiclass_precision_recall_curve_tensor_validation(
             "Expected the shape of `preds` should be (N, C, ...) and the shape of `target` should be (N, ...)"
             f" but got {preds.shape} and {target.shape}"
         )
+    if not check_values:
+        return
     if sink is None:
         n_unique = len(torch.unique(target))
         limit = num_classes if ignore_index is None else num_classes + 1
@@ -131,7 +143,7 @@ def _multiclass_precision_recall_curve_tensor_validation(
         bad = (target < 0) | (target >= num_classes)
         if ignore_index is not None:
             bad &= target != ignore_index
-        sink.add(bad, RuntimeError, "Detected more unique values in `target` than `num_classes`.")
+        sink.add(bad, RuntimeError, TARGET_RANGE_MSG)
 
 
 def _multilabel_precision_recall_curve_arg_validation(

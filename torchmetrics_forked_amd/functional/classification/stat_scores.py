@@ -186,6 +186,7 @@ def _multiclass_stat_scores_tensor_validation(
     multidim_average: str = "global",
     ignore_index: Optional[int] = None,
     sink: Optional[DeferredChecks] = None,
+    check_values: bool = True,
 ) -> None:
     if preds.ndim == target.ndim + 1:
         if not preds.is_floating_point():
@@ -221,6 +222,8 @@ def _multiclass_stat_scores_tensor_validation(
             "Either `preds` and `target` both should have the (same) shape (N, ...), or `target` should be (N, ...)"
             " and `preds` should be (N, C, ...)."
         )
+    if not check_values:
+        return
     if sink is None:
         n_unique = len(torch.unique(target))
         limit = num_classes if ignore_index is None else num_classes + 1

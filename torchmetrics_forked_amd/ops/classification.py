@@ -89,6 +89,7 @@ def curve_hist_update(
     task: str,
     ignore_index: Optional[int],
     confmat: Optional[Tensor] = None,
+    err_flag: Optional[Tensor] = None,
 ) -> None:
     """Accumulate the exact 16-bit score histogram ``hist[C, 2, 16384]`` (see csrc/classification.hip).
 
@@ -102,7 +103,7 @@ def curve_hist_update(
     if ops.use_native(target):
         torch.ops.tmx.curve_hist_update(
             preds, target, hist, tcode, -1 if ignore_index is None else ignore_index, ignore_index is not None, confmat,
-            _norm_flag(preds, target, task, ignore_index),
+            _norm_flag(preds, target, task, ignore_index), err_flag,
         )
         return
     C = hist.shape[0]

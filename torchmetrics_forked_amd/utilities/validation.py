@@ -22,29 +22,51 @@ def validation_mode() -> str:
 
 
 class DeferredChecks:
-    """Accumulates device-side failure flags keyed by (exception type, message)."""
+    """Accumulates device-side failure flags keyed by (exception type, message).
+
+    Two ways to contribute: ``add(bad, ...)`` ORs a boolean tensor in (one small reduction kernel), or
+    ``flag(...)`` hands out a persistent ``int32[1]`` device word that native kernels OR into directly while
+    they stream the data anyway (zero extra kernels per update).
+    """
 
     def __init__(self) -> None:
         self._flags: Dict[Tuple[Type[Exception], str], Tensor] = {}
 
     def add(self, bad: Tensor, exc: Type[Exception], message: str) -> None:
         key = (exc, message)
-        bad = bad.reshape(-1).any().reshape(1)
+        bad = bad.reshape(-1).any().reshape(1).to(torch.int32)
         prev = self._flags.get(key)
-        self._flags[key] = bad if prev is None else (prev | bad)
+        if prev is None:
+            self._flags[key] = bad
+        else:
+            prev.bitwise_or_(bad)
+
+    def flag(self, exc: Type[Exception], message: str, device: torch.device) -> Tensor:
+        key = (exc, message)
+        f = self._flags.get(key)
+        if f is None or f.device != device:
+            f = torch.zeros(1, dtype=torch.int32, device=device)
+            self._flags[key] = f
+        return f
+
+    def attach(self, exc: Type[Exception], message: str, flag: Tensor) -> None:
+        """Share another sink's device flag (one kernel writes, several metrics raise)."""
+        self._flags[(exc, message)] = flag
 
     def check(self) -> None:
         if not self._flags:
             return
         keys = list(self._flags.keys())
-        flags = torch.cat([self._flags[k].to(torch.bool).cpu() for k in keys])  # one host sync
-        self._flags = {}
+        flags = torch.cat([self._flags[k].reshape(1).to(torch.int32).cpu() for k in keys])  # one host sync
+        for k in keys:
+            self._flags[k].zero_()
         for k, f in zip(keys, flags.tolist()):
             if f:
                 raise k[0](k[1])
 
     def clear(self) -> None:
-        self._flags = {}
+        for f in self._flags.values():
+            f.zero_()
 
 
 def make_sink(t: Tensor) -> Optional[DeferredChecks]:
