@@ -37,32 +37,33 @@ template <typename T>
 __device__ __forceinline__ bool bad16(uint32_t b) { return b > RangeBits<T>::one && b != RangeBits<T>::neg0; }
 
 // 16-bit floats: 8 elements per 16-B load (vectorised, Guideline 13).
+// The flag only needs ONE witness: blocks poll it (agent-scope relaxed load, served by L2) and stop early, and a
+// block that finds a bad value sets it with a single plain store (idempotent) — no same-address atomics, which
+// serialise at the memory side when every block of a logits batch finds a witness at once.
 template <typename T>
 __global__ void range_flag16_kernel(const uint4* __restrict__ xv, int64_t nvec, const uint16_t* __restrict__ tail,
                                     int ntail, int* __restrict__ flag) {
+  __shared__ int s_done;
+  if (threadIdx.x == 0) s_done = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  if (s_done) return;
   bool bad = false;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  // 4 independent 16-B loads in flight per lane before any compare
-  for (; i + 3 * stride < nvec; i += 4 * stride) {
+  if (blockIdx.x == 0 && threadIdx.x < ntail) bad |= bad16<T>(tail[threadIdx.x]);
+  for (; i < nvec; i += 4 * stride) {
     uint4 w[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) w[u] = xv[i + u * stride];
+    for (int u = 0; u < 4; ++u) w[u] = (i + u * stride < nvec) ? xv[i + u * stride] : make_uint4(0, 0, 0, 0);
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const uint32_t parts[4] = {w[u].x, w[u].y, w[u].z, w[u].w};
 #pragma unroll
       for (int k = 0; k < 4; ++k) bad |= bad16<T>(parts[k] & 0xFFFFu) | bad16<T>(parts[k] >> 16);
     }
+    if (__syncthreads_or(bad)) break;
   }
-  for (; i < nvec; i += stride) {
-    uint4 w = xv[i];
-    const uint32_t parts[4] = {w.x, w.y, w.z, w.w};
-#pragma unroll
-    for (int k = 0; k < 4; ++k) bad |= bad16<T>(parts[k] & 0xFFFFu) | bad16<T>(parts[k] >> 16);
-  }
-  if (blockIdx.x == 0 && threadIdx.x < ntail) bad |= bad16<T>(tail[threadIdx.x]);
-  if (__ballot(bad) && (threadIdx.x & (kWave - 1)) == 0) atomicOr(flag, 1);
+  if (__syncthreads_or(bad) && threadIdx.x == 0) __hip_atomic_store(flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 template <typename T>
@@ -490,27 +491,43 @@ __global__ void __launch_bounds__(kA_Threads, 4) mc_codes_kernel(const T* __rest
   const int64_t ntiles = (n + kTileRows - 1) / kTileRows;
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const int64_t r0 = tile * kTileRows;
-    for (int p = wave; p < kTileRows / 2; p += nwaves) {
+    // every wave owns kPairs row pairs of the tile: issue all their 16-B loads first (latency hiding), then
+    // compute pair by pair.
+    constexpr int kPairs = kTileRows / 2 / (kA_Threads / kWave);
+    uint4 wbuf[kPairs][2][2];
+    int64_t tv[kPairs][2];
+#pragma unroll
+    for (int pp = 0; pp < kPairs; ++pp)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int64_t r = r0 + 2 * (wave + pp * nwaves) + h;
+        tv[pp][h] = r < n ? target[r] : INT64_MIN;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          const int q = lane + kWave * k;
+          wbuf[pp][h][k] = (r < n && q < nvec) ? reinterpret_cast<const uint4*>(preds + r * C)[q] : make_uint4(0, 0, 0, 0);
+        }
+      }
+#pragma unroll
+    for (int pp = 0; pp < kPairs; ++pp) {
+      const int p = wave + pp * nwaves;
       uint32_t packed[16];
 #pragma unroll
       for (int j = 0; j < 16; ++j) packed[j] = 0;
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        const int64_t r = r0 + 2 * p + h;
-        bool valid = r < n;
-        const int64_t t = valid ? target[r] : -1;
+        const int64_t t = tv[pp][h];
+        bool valid = t != INT64_MIN;
         if (has_ignore && t == ignore_index) valid = false;
         if (valid && (t < 0 || t >= C) && err != nullptr && lane == 0) atomicOr(err, 1);
-        uint4 w[2];
+        const uint4* w = wbuf[pp][h];
         float v[16];
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
           const int q = lane + kWave * k;
           if (valid && q < nvec) {
-            w[k] = reinterpret_cast<const uint4*>(preds + r * C)[q];
             unpack8<T>(w[k], v + 8 * k);
           } else {
-            w[k] = make_uint4(0, 0, 0, 0);
 #pragma unroll
             for (int e = 0; e < 8; ++e) v[8 * k + e] = -INFINITY;
           }
@@ -570,7 +587,7 @@ __global__ void __launch_bounds__(kA_Threads, 4) mc_codes_kernel(const T* __rest
   }
 }
 
-__global__ void __launch_bounds__(256) class_hist_kernel(const uint16_t* __restrict__ codes, int64_t n_pad, int splits,
+__global__ void __launch_bounds__(512) class_hist_kernel(const uint16_t* __restrict__ codes, int64_t n_pad, int splits,
                                                          int64_t* __restrict__ hist) {
   extern __shared__ __attribute__((aligned(16))) uint32_t s_neg[];  // [kCodes]
   const int c = blockIdx.x / splits, sp = blockIdx.x % splits;
@@ -582,16 +599,22 @@ __global__ void __launch_bounds__(256) class_hist_kernel(const uint16_t* __restr
   const int64_t chunk = (nv + splits - 1) / splits;
   const int64_t v0 = sp * chunk, v1 = v0 + chunk < nv ? v0 + chunk : nv;
   int64_t* pos_hist = hist + ((int64_t)c * 2 + 1) * kCodes;
-  for (int64_t v = v0 + threadIdx.x; v < v1; v += blockDim.x) {
-    const uint4 w = col[v];
-    const uint32_t parts[4] = {w.x, w.y, w.z, w.w};
+  const int64_t bstride = blockDim.x;
+  for (int64_t v = v0 + threadIdx.x; v < v1; v += 4 * bstride) {
+    uint4 w[4];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const uint32_t x = (k & 1) ? (parts[k >> 1] >> 16) : (parts[k >> 1] & 0xFFFFu);
-      if (x & 0x8000u) continue;
-      const uint32_t code = x & 0x3FFFu;
-      if (x & 0x4000u) atomic_add_i64(pos_hist + code, 1);
-      else atomicAdd(&s_neg[code], 1u);
+    for (int u = 0; u < 4; ++u) w[u] = (v + u * bstride < v1) ? col[v + u * bstride] : make_uint4(0x80008000u, 0x80008000u, 0x80008000u, 0x80008000u);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint32_t parts[4] = {w[u].x, w[u].y, w[u].z, w[u].w};
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const uint32_t x = (k & 1) ? (parts[k >> 1] >> 16) : (parts[k >> 1] & 0xFFFFu);
+        if (x & 0x8000u) continue;
+        const uint32_t code = x & 0x3FFFu;
+        if (x & 0x4000u) atomic_add_i64(pos_hist + code, 1);
+        else atomicAdd(&s_neg[code], 1u);
+      }
     }
   }
   __syncthreads();
@@ -624,7 +647,7 @@ void launch_two_pass(const T* p, const int64_t* target, int64_t n, int C, const 
   // row splits only when there are too few classes to fill the chip (exclusive-owner flush when splits == 1)
   int splits = 1;
   while ((int64_t)C * splits < 512 && n_pad / (8 * (splits * 2)) >= 1024) splits *= 2;
-  hipLaunchKernelGGL(class_hist_kernel, C * splits, 256, kCodes * sizeof(uint32_t), stream(),
+  hipLaunchKernelGGL(class_hist_kernel, C * splits, 512, kCodes * sizeof(uint32_t), stream(),
                      reinterpret_cast<const uint16_t*>(codes.data_ptr()), n_pad, splits, hist);
   TMX_LAUNCH_CHECK();
 }

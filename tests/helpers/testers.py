@@ -97,7 +97,9 @@ def _class_test(
         elif check_batch and not metric.dist_sync_on_step:
             assert_allclose(batch_result, reference_metric(preds[i], target[i]), atol)
     result = metric.compute()
-    ref = reference_metric(_cat(list(preds)), _cat(list(target)))
+    # gathered `cat` states are rank-major: order the oracle input the same way
+    order = [i for r in range(world) for i in range(r, num_batches, world)]
+    ref = reference_metric(_cat([preds[i] for i in order]), _cat([target[i] for i in order]))
     assert_allclose(result, ref, atol)
 
 
@@ -141,3 +143,22 @@ def run_functional_metric_test(
         p = preds[i].to(device) if isinstance(preds[i], Tensor) else preds[i]
         t = target[i].to(device) if isinstance(target[i], Tensor) else target[i]
         assert_allclose(metric_functional(p, t, **metric_args), reference_metric(preds[i], target[i]), atol)
+
+
+class RefFn:
+    """Picklable reference-oracle callable: ``torchmetrics.functional.<...>.<name>(p, t, **kwargs)`` from the
+    read-only reference (imported lazily, also inside spawned DDP workers)."""
+
+    def __init__(self, name: str, domain: str = "classification", **kwargs: Any) -> None:
+        self.name, self.domain, self.kwargs = name, domain, kwargs
+
+    def __call__(self, p: Any, t: Any) -> Any:
+        import sys
+
+        for path in ("/root/repo/tests/_oracle", "/root/reference/src"):
+            if path not in sys.path:
+                sys.path.append(path)
+        import importlib
+
+        mod = importlib.import_module(f"torchmetrics.functional.{self.domain}" if self.domain else "torchmetrics.functional")
+        return getattr(mod, self.name)(p, t, **self.kwargs)

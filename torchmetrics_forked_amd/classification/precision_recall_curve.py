@@ -112,6 +112,17 @@ class _CurveMetric(Metric):
         self.preds.append(st[1])
         self.target.append(st[2])
 
+    def _reduce_states(self, incoming_state: dict) -> None:
+        """``forward`` merge: the lazily materialised histogram may be empty on either side."""
+        if self.thresholds is None:
+            glob, local = incoming_state["score_hist"], self.score_hist
+            if glob.numel() == 0 or local.numel() == 0:
+                merged = local if glob.numel() == 0 else glob
+                incoming_state = dict(incoming_state)
+                incoming_state["score_hist"] = torch.zeros_like(merged)
+                self.score_hist = merged
+        super()._reduce_states(incoming_state)
+
     # ---------------------------------------------------------------------------------------------- sync
     def _sync_dist(self, dist_sync_fn: Any = None, process_group: Optional[Any] = None) -> None:
         if self.thresholds is None:
