@@ -1,0 +1,309 @@
+// Exact-histogram curve kernels (device code only; shared by csrc/classification.hip and the standalone
+// ablation harness tools/kexp/curve_hist_exp.hip).  See classification.hip for the op-level documentation.
+#pragma once
+
+#include "device_common.h"
+
+namespace tmx {
+
+// Bit-level range test: a 16/32-bit float is in [0, 1] iff its pattern is <= bits(1.0) or equals -0.0.
+// NaN / negative / >1 patterns all compare above; no float conversion needed.
+template <typename T> struct RangeBits;
+template <> struct RangeBits<__hip_bfloat16> { static constexpr uint32_t one = 0x3F80, neg0 = 0x8000; };
+template <> struct RangeBits<__half> { static constexpr uint32_t one = 0x3C00, neg0 = 0x8000; };
+
+template <typename T>
+__device__ __forceinline__ bool bad16(uint32_t b) { return b > RangeBits<T>::one && b != RangeBits<T>::neg0; }
+
+// 16-bit floats: 8 elements per 16-B load (vectorised, Guideline 13).
+// The flag only needs ONE witness: blocks poll it (agent-scope relaxed load, served by L2) and stop early, and a
+// block that finds a bad value sets it with a single plain store (idempotent) — no same-address atomics, which
+// serialise at the memory side when every block of a logits batch finds a witness at once.
+template <typename T>
+__global__ void range_flag16_kernel(const uint4* __restrict__ xv, int64_t nvec, const uint16_t* __restrict__ tail,
+                                    int ntail, int* __restrict__ flag) {
+  __shared__ int s_done;
+  if (threadIdx.x == 0) s_done = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  if (s_done) return;
+  bool bad = false;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (blockIdx.x == 0 && threadIdx.x < ntail) bad |= bad16<T>(tail[threadIdx.x]);
+  for (; i < nvec; i += 4 * stride) {
+    uint4 w[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) w[u] = (i + u * stride < nvec) ? xv[i + u * stride] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint32_t parts[4] = {w[u].x, w[u].y, w[u].z, w[u].w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) bad |= bad16<T>(parts[k] & 0xFFFFu) | bad16<T>(parts[k] >> 16);
+    }
+    if (__syncthreads_or(bad)) break;
+  }
+  if (__syncthreads_or(bad) && threadIdx.x == 0) __hip_atomic_store(flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+constexpr int kCodeBits = 14;
+constexpr int kCodes = 1 << kCodeBits;  // 16384 >= 16257 (bf16 codes in [0,1]) and 15361 (fp16)
+
+template <typename T> __device__ __forceinline__ int score_code(uint16_t b);
+template <> __device__ __forceinline__ int score_code<__hip_bfloat16>(uint16_t b) {
+  if (b == 0x8000) return 0;       // -0.0 == 0.0
+  return b <= 0x3F80 ? b : -1;     // >1, negative or NaN -> dropped
+}
+template <> __device__ __forceinline__ int score_code<__half>(uint16_t b) {
+  if (b == 0x8000) return 0;
+  return b <= 0x3C00 ? b : -1;
+}
+
+// ---------------------------------------------------------------------------------------------------------
+// Two-pass multiclass histogram (C % 8 == 0, C <= 1024):
+//   (A) row pass  — one wave per row pair: 16-B vector loads, fp32 softmax (if flagged) rounded to the input
+//       dtype, argmax (fused confusion matrix), 16-bit code per element with flag bits
+//       (bit 14 = positive label, bit 15 = skip).  Codes of a 64-row tile are transposed to class-major
+//       through an LDS tile [C][32 dwords] (two rows packed per dword), XOR-swizzled by class group so both
+//       the scattered writes and the row read-out are bank-conflict free, then stored as 128-B segments of
+//       a class-major scratch codes[C][n_pad].
+//   (B) class pass — one workgroup per (class, row split): negatives counted in an LDS-privatised u32
+//       histogram (64 KiB, two workgroups per CU), positives (1/C of the data) straight to global; one
+//       int64 atomic per non-empty bin on flush (consecutive codes -> contiguous atomics).
+// Replaces 1 scattered 64-bit global atomic per score (2.8 ms/update at 65536x1000 on MI355X).
+// ---------------------------------------------------------------------------------------------------------
+constexpr int kTileRows = 32;   // 16 packed dwords per class -> 64 KiB LDS at C=1024, 2 WGs/CU
+constexpr int kA_Threads = 512;
+
+template <typename T> __device__ __forceinline__ void unpack8(const uint4& w, float* v);
+template <> __device__ __forceinline__ void unpack8<__hip_bfloat16>(const uint4& w, float* v) {
+  const uint32_t p[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    v[2 * k] = __uint_as_float(p[k] << 16);
+    v[2 * k + 1] = __uint_as_float(p[k] & 0xFFFF0000u);
+  }
+}
+template <> __device__ __forceinline__ void unpack8<__half>(const uint4& w, float* v) {
+  const uint32_t p[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    __half lo, hi;
+    uint16_t l16 = p[k] & 0xFFFF, h16 = p[k] >> 16;
+    lo = *reinterpret_cast<__half*>(&l16);
+    hi = *reinterpret_cast<__half*>(&h16);
+    v[2 * k] = __half2float(lo);
+    v[2 * k + 1] = __half2float(hi);
+  }
+}
+template <typename T> __device__ __forceinline__ uint16_t raw_bits(const uint4& w, int e) {
+  const uint32_t p[4] = {w.x, w.y, w.z, w.w};
+  return (e & 1) ? (p[e >> 1] >> 16) : (p[e >> 1] & 0xFFFF);
+}
+
+// Ablation switches (standalone harness only; the library instantiates ABL = 0).
+constexpr int kAblNoStore = 1;    // skip the class-major scratch store
+constexpr int kAblNoNorm = 2;     // skip exp/div (raw codes)
+constexpr int kAblNoLds = 4;      // skip the LDS transpose
+
+// Normalisation mode (sigmoid/softmax-if-any-value-outside-[0,1]) is *speculated*: ``mode[0]`` holds the mode
+// used by this launch (the previous batch's verdict, or the range_flag pre-pass result), the kernel records the
+// real verdict for this batch in ``mode[1]`` (plain store of 1 by any block that saw a witness; only
+// non-ignored rows count, as in the reference).  A FIXUP launch of the same kernel exits immediately unless
+// mode[0] != mode[1], in which case it recomputes the codes with the real mode (confusion matrix and error
+// flags are mode independent and are not touched again).  ``class_hist_kernel`` then rolls the prediction
+// forward (mode[0] = mode[1], mode[1] = 0).  Net effect: no separate 131-MB range pass per update.
+template <typename T, bool FIXUP, int ABL = 0>
+__global__ void __launch_bounds__(kA_Threads, 4) mc_codes_kernel(const T* __restrict__ preds, const int64_t* __restrict__ target,
+                                                                  int64_t n, int C, int* __restrict__ mode,
+                                                                  int64_t ignore_index, bool has_ignore,
+                                                                  uint32_t* __restrict__ codes, int64_t n_pad,
+                                                                  int64_t* __restrict__ confmat, int* __restrict__ err,
+                                                                  bool record_mode) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_tile[];  // [C][kTileRows / 2]
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wave = threadIdx.x / kWave;
+  const int nwaves = kA_Threads / kWave;
+  int use_mode;
+  if constexpr (FIXUP) {
+    const int m0 = __hip_atomic_load(mode, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int m1 = __hip_atomic_load(mode + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (m0 == m1) return;  // speculation was right (the common case): nothing to redo
+    use_mode = m1;
+  } else {
+    use_mode = mode[0];
+  }
+  const bool do_softmax = (ABL & kAblNoNorm) ? false : use_mode != 0;
+  bool saw_bad = false;
+  const int nvec = C / 8;
+  const int64_t ntiles = (n + kTileRows - 1) / kTileRows;
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int64_t r0 = tile * kTileRows;
+    // every wave owns kPairs row pairs of the tile: issue all their 16-B loads first (latency hiding), then
+    // compute pair by pair.
+    constexpr int kPairs = kTileRows / 2 / (kA_Threads / kWave);
+    uint4 wbuf[kPairs][2][2];
+    int64_t tv[kPairs][2];
+#pragma unroll
+    for (int pp = 0; pp < kPairs; ++pp)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int64_t r = r0 + 2 * (wave + pp * nwaves) + h;
+        tv[pp][h] = r < n ? target[r] : INT64_MIN;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          const int q = lane + kWave * k;
+          wbuf[pp][h][k] = (r < n && q < nvec) ? reinterpret_cast<const uint4*>(preds + r * C)[q] : make_uint4(0, 0, 0, 0);
+        }
+      }
+#pragma unroll
+    for (int pp = 0; pp < kPairs; ++pp) {
+      const int p = wave + pp * nwaves;
+      uint32_t packed[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) packed[j] = 0;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int64_t t = tv[pp][h];
+        bool valid = t != INT64_MIN;
+        if (has_ignore && t == ignore_index) valid = false;
+        if (!FIXUP && valid && (t < 0 || t >= C) && err != nullptr && lane == 0) atomicOr(err, 1);
+        const uint4* w = wbuf[pp][h];
+        float v[16];
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          const int q = lane + kWave * k;
+          if (valid && q < nvec) {
+            unpack8<T>(w[k], v + 8 * k);
+            if (!FIXUP && record_mode) {
+#pragma unroll
+              for (int e = 0; e < 8; ++e) saw_bad |= bad16<T>(raw_bits<T>(w[k], e));
+            }
+          } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[8 * k + e] = -INFINITY;
+          }
+        }
+        float mx = -INFINITY;
+        if (!FIXUP || do_softmax) {
+          float m = -INFINITY;
+          int am = C;
+#pragma unroll
+          for (int k = 0; k < 2; ++k)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const int c = 8 * (lane + kWave * k) + e;
+              if (c < C && argmax_better(v[8 * k + e], c, m, am)) { m = v[8 * k + e]; am = c; }
+            }
+          mx = m;
+          int amx = am;
+          wave_argmax(mx, amx);
+          if (!FIXUP && valid && confmat != nullptr && lane == 0 && t >= 0 && t < C && amx < C)
+            atomic_add_i64(confmat + t * C + amx, 1);
+        }
+        float s = 1.f;
+        if (do_softmax) {
+          float acc = 0.f;
+#pragma unroll
+          for (int j = 0; j < 16; ++j) {
+            const int c = 8 * (lane + kWave * (j >> 3)) + (j & 7);
+            if (c < C) { v[j] = expf(v[j] - mx); acc += v[j]; }
+          }
+          s = wave_sum(acc);
+        }
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          const int c = 8 * (lane + kWave * (j >> 3)) + (j & 7);
+          uint32_t code = 0x8000u;
+          if (valid && c < C) {
+            const uint16_t b = do_softmax ? round_bits16<T>(v[j] / s) : raw_bits<T>(w[j >> 3], j & 7);
+            const int sc = score_code<T>(b);
+            code = sc < 0 ? 0x8000u : (uint32_t)sc | (c == t ? 0x4000u : 0u);
+          }
+          packed[j] |= code << (16 * h);
+        }
+      }
+      if constexpr (!(ABL & kAblNoLds)) {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          const int q = lane + kWave * (j >> 3);
+          const int c = 8 * q + (j & 7);
+          if (c < C) s_tile[c * (kTileRows / 2) + (p ^ (q & (kTileRows / 2 - 1)))] = packed[j];
+        }
+      } else {
+        uint32_t acc = 0;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) acc ^= packed[j];
+        if (acc == 0x12345678u) s_tile[threadIdx.x] = acc;  // keep the computation alive
+      }
+    }
+    __syncthreads();
+    if constexpr (!(ABL & kAblNoStore)) {
+      const int64_t seg = r0 / 2;  // dword offset of this tile inside a class row
+      constexpr int kSlots = kTileRows / 2;
+      for (int idx = threadIdx.x; idx < C * kSlots; idx += kA_Threads) {
+        const int c = idx / kSlots, d = idx % kSlots;
+        const uint32_t wv = s_tile[idx];
+        const int p = d ^ ((c >> 3) & (kSlots - 1));
+        codes[(int64_t)c * (n_pad / 2) + seg + p] = wv;
+      }
+    }
+    __syncthreads();
+  }
+  if constexpr (!FIXUP) {
+    if (record_mode && __syncthreads_or(saw_bad) && threadIdx.x == 0)
+      __hip_atomic_store(mode + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+__global__ void __launch_bounds__(512) class_hist_kernel(const uint16_t* __restrict__ codes, int64_t n_pad, int splits,
+                                                         int64_t* __restrict__ hist, int* __restrict__ mode_roll) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_neg[];  // [kCodes]
+  const int c = blockIdx.x / splits, sp = blockIdx.x % splits;
+  if (mode_roll != nullptr && blockIdx.x == 0 && threadIdx.x == 0) {  // previous kernels are complete (stream order)
+    mode_roll[0] = mode_roll[1];
+    mode_roll[1] = 0;
+  }
+  uint4* s4 = reinterpret_cast<uint4*>(s_neg);
+  for (int i = threadIdx.x; i < kCodes / 4; i += blockDim.x) s4[i] = make_uint4(0, 0, 0, 0);
+  __syncthreads();
+  const uint4* col = reinterpret_cast<const uint4*>(codes + (int64_t)c * n_pad);
+  const int64_t nv = n_pad / 8;
+  const int64_t chunk = (nv + splits - 1) / splits;
+  const int64_t v0 = sp * chunk, v1 = v0 + chunk < nv ? v0 + chunk : nv;
+  int64_t* pos_hist = hist + ((int64_t)c * 2 + 1) * kCodes;
+  const int64_t bstride = blockDim.x;
+  for (int64_t v = v0 + threadIdx.x; v < v1; v += 4 * bstride) {
+    uint4 w[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) w[u] = (v + u * bstride < v1) ? col[v + u * bstride] : make_uint4(0x80008000u, 0x80008000u, 0x80008000u, 0x80008000u);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint32_t parts[4] = {w[u].x, w[u].y, w[u].z, w[u].w};
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const uint32_t x = (k & 1) ? (parts[k >> 1] >> 16) : (parts[k >> 1] & 0xFFFFu);
+        if (x & 0x8000u) continue;
+        const uint32_t code = x & 0x3FFFu;
+        if (x & 0x4000u) atomic_add_i64(pos_hist + code, 1);
+        else atomicAdd(&s_neg[code], 1u);
+      }
+    }
+  }
+  __syncthreads();
+  int64_t* neg_hist = hist + ((int64_t)c * 2) * kCodes;
+  if (splits == 1) {
+    // this workgroup is the only writer of class c's negative bins in this launch: plain read-modify-write
+    for (int i = threadIdx.x; i < kCodes; i += blockDim.x) {
+      const uint32_t cnt = s_neg[i];
+      if (cnt) neg_hist[i] += cnt;
+    }
+  } else {
+    for (int i = threadIdx.x; i < kCodes; i += blockDim.x) {
+      const uint32_t cnt = s_neg[i];
+      if (cnt) atomic_add_i64(neg_hist + i, cnt);
+    }
+  }
+}
+
+
+}  // namespace tmx

@@ -1,0 +1,123 @@
+"""Cross-process synchronisation through the coalesced sync engine on a 2-process gloo group."""
+import pytest
+import torch
+
+from tests.helpers.ddp import run_ddp
+from tests.helpers.dummies import DummyCat, DummyList, DummyMinMaxMean, DummyStacked, DummySum
+from torchmetrics_forked_amd import MetricCollection
+from torchmetrics_forked_amd.utilities.distributed import gather_all_tensors
+
+
+def _sum_sync(rank, world):
+    m = DummySum()
+    m.update(torch.tensor(float(rank + 1)))
+    assert m.compute() == 3.0
+    # local state restored after compute
+    assert m.x == rank + 1
+    return True
+
+
+def _cat_uneven(rank, world):
+    m = DummyCat()
+    for i in range(rank + 1):  # rank0: 1 element list, rank1: 2
+        m.update(torch.arange(2) + 10 * rank + i)
+    out = m.compute()
+    assert out.tolist() == [0.0, 1.0, 10.0, 11.0, 11.0, 12.0], out
+    return True
+
+
+def _cat_empty_rank(rank, world):
+    m = DummyCat()
+    if rank == 1:
+        m.update(torch.tensor([5.0, 6.0]))
+    else:
+        m._update_count = 1
+    assert m.compute().tolist() == [5.0, 6.0]
+    return True
+
+
+def _list_interleave(rank, world):
+    m = DummyList()
+    m.update(torch.tensor(rank * 10.0))
+    m.update(torch.tensor(rank * 10.0 + 1))
+    out = [float(t) for t in m.compute()]
+    assert out == [0.0, 10.0, 1.0, 11.0], out  # element-major, rank-interleaved (reference semantics)
+    return True
+
+
+def _minmax_mean(rank, world):
+    m = DummyMinMaxMean()
+    m.update(torch.tensor([rank * 1.0, rank + 3.0]))
+    m.sync()
+    assert m.mn == 0.0 and m.mx == 4.0
+    assert torch.isclose(m.mean, torch.tensor(2.0))
+    st = DummyStacked()
+    st.update(torch.tensor([rank * 1.0, rank + 3.0]))
+    assert st.compute().shape == (2, 2)
+    assert torch.allclose(m.custom, torch.full((3,), 3.0 * 5.0))
+    m.unsync()
+    assert m.mx == rank + 3.0
+    return True
+
+
+def _sync_context_and_state_dict(rank, world):
+    m = DummySum()
+    m.persistent(True)
+    m.update(torch.tensor(float(rank + 1)))
+    with m.sync_context():
+        assert m.state_dict()["x"] == 3.0
+    assert m.state_dict()["x"] == rank + 1
+    return True
+
+
+def _no_sync_on_compute(rank, world):
+    m = DummySum(sync_on_compute=False)
+    m.update(torch.tensor(float(rank + 1)))
+    assert m.compute() == rank + 1
+    return True
+
+
+def _dist_sync_on_step(rank, world):
+    m = DummySum(dist_sync_on_step=True)
+    v = m(torch.tensor(float(rank + 1)))
+    assert v == 3.0
+    return True
+
+
+def _custom_dist_sync_fn(rank, world):
+    calls = []
+
+    def fn(t, group=None):
+        calls.append(1)
+        return gather_all_tensors(t, group)
+
+    m = DummySum(dist_sync_fn=fn)
+    m.update(torch.tensor(1.0))
+    assert m.compute() == 2.0 and calls
+    return True
+
+
+def _gather_uneven(rank, world):
+    t = torch.ones(rank + 1, 2) * rank
+    out = gather_all_tensors(t)
+    assert [o.shape[0] for o in out] == [1, 2]
+    return True
+
+
+def _collection_coalesced(rank, world):
+    coll = MetricCollection({"s": DummySum(), "c": DummyCat(), "m": DummyMinMaxMean()})
+    coll.update(torch.tensor(float(rank + 1)))
+    out = coll.compute()
+    assert out["s"] == 3.0
+    assert sorted(out["c"].tolist()) == [1.0, 2.0]
+    assert coll["s"].x == rank + 1  # unsynced afterwards
+    return True
+
+
+@pytest.mark.parametrize(
+    "fn",
+    [_sum_sync, _cat_uneven, _cat_empty_rank, _list_interleave, _minmax_mean, _sync_context_and_state_dict,
+     _no_sync_on_compute, _dist_sync_on_step, _custom_dist_sync_fn, _gather_uneven, _collection_coalesced],
+)
+def test_ddp(fn):
+    assert all(run_ddp(fn))

@@ -17,6 +17,9 @@ STEPS="${STEPS:-pytest,kbench,bench,prof,ref}"
 if [[ $STEPS == *pytest* ]]; then
   timeout -k 10 600 python -m pytest tests -m gpu -x -q > $OUT/pytest_gpu.log 2>&1; stop_if_fatal $? pytest; tail -5 $OUT/pytest_gpu.log
 fi
+if [[ $STEPS == *kexp* ]]; then
+  timeout -k 10 120 ./build/curve_hist_exp > $OUT/kexp.json 2> $OUT/kexp.err; stop_if_fatal $? kexp; cat $OUT/kexp.json
+fi
 if [[ $STEPS == *kbench* ]]; then
   timeout -k 10 300 python tools/kbench.py > $OUT/kbench.json 2> $OUT/kbench.err; stop_if_fatal $? kbench; cat $OUT/kbench.json
 fi

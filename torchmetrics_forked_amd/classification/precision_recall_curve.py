@@ -68,6 +68,16 @@ class _CurveMetric(Metric):
             return not (isinstance(self.preds, list) and len(self.preds) > 0)
         return False
 
+    def _mode_state(self, preds: Tensor) -> Optional[Tensor]:
+        """Persistent int32[2] speculation word for the GPU kernels' softmax decision (see curve_hist_kernels.h)."""
+        if not preds.is_cuda:
+            return None
+        st = getattr(self, "_spec_mode", None)
+        if st is None or st.device != preds.device:
+            st = torch.zeros(2, dtype=torch.int32, device=preds.device)
+            self._spec_mode = st
+        return st
+
     def _ensure_hist(self, device: torch.device) -> Tensor:
         if self.score_hist.numel() == 0:
             self.score_hist = torch.zeros(self._num, 2, eng.N_CODES, dtype=torch.long, device=device)
@@ -94,7 +104,7 @@ class _CurveMetric(Metric):
                 cls_ops.curve_hist_update(preds.reshape(-1, 1, 1), target.reshape(-1, 1, 1), hist, "binary", ii)
             elif self._task == "multiclass":
                 p = torch.movedim(preds, 1, -1).reshape(-1, self._num)
-                cls_ops.curve_hist_update(p, target.reshape(-1), hist, "multiclass", ii, confmat_out, err_flag)
+                cls_ops.curve_hist_update(p, target.reshape(-1), hist, "multiclass", ii, confmat_out, err_flag, self._mode_state(p))
             else:
                 cls_ops.curve_hist_update(preds, target, hist, "multilabel", ii)
             return

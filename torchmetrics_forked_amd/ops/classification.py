@@ -90,6 +90,7 @@ def curve_hist_update(
     ignore_index: Optional[int],
     confmat: Optional[Tensor] = None,
     err_flag: Optional[Tensor] = None,
+    mode_state: Optional[Tensor] = None,
 ) -> None:
     """Accumulate the exact 16-bit score histogram ``hist[C, 2, 16384]`` (see csrc/classification.hip).
 
@@ -101,9 +102,12 @@ def curve_hist_update(
         raise TypeError(f"curve_hist_update expects bf16/fp16 scores, got {preds.dtype}")
     tcode = 0 if task == "multiclass" else 1
     if ops.use_native(target):
+        # with a persistent ``mode_state`` (int32[2]) the multiclass kernel speculates the softmax decision and
+        # records the real one in-pass (no separate range pass, ignore-aware); otherwise a pre-pass flag is used
+        norm = None if (mode_state is not None and task == "multiclass") else _norm_flag(preds, target, task, ignore_index)
         torch.ops.tmx.curve_hist_update(
             preds, target, hist, tcode, -1 if ignore_index is None else ignore_index, ignore_index is not None, confmat,
-            _norm_flag(preds, target, task, ignore_index), err_flag,
+            norm, err_flag, mode_state,
         )
         return
     C = hist.shape[0]
