@@ -390,7 +390,7 @@ void launch_two_pass(const T* p, const int64_t* target, int64_t n, int C, int* m
   auto codes = at::empty({(int64_t)C * n_pad}, opts.dtype(at::kShort));
   const int64_t ntiles = n_pad / kTileRows;
   const size_t shm_a = (size_t)C * (kTileRows / 2) * sizeof(uint32_t);
-  const int grid_a = static_cast<int>(std::min<int64_t>(ntiles, 256 * 8));
+  const int grid_a = static_cast<int>(std::min<int64_t>(ntiles, 256 * 2));  // persistent: 2 x 64 KiB blocks per CU
   uint32_t* cptr = reinterpret_cast<uint32_t*>(codes.data_ptr());
   hipLaunchKernelGGL((mc_codes_kernel<T, false>), grid_a, kA_Threads, shm_a, stream(), p, target, n, C, mode, ignore_index,
                      has_ignore, cptr, n_pad, cm, err, speculative);

@@ -42,7 +42,8 @@ __global__ void range_flag16_kernel(const uint4* __restrict__ xv, int64_t nvec, 
     }
     if (__syncthreads_or(bad)) break;
   }
-  if (__syncthreads_or(bad) && threadIdx.x == 0) __hip_atomic_store(flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (__syncthreads_or(bad) && threadIdx.x == 0 && __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
+    __hip_atomic_store(flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 constexpr int kCodeBits = 14;
@@ -112,6 +113,115 @@ constexpr int kAblNoLds = 4;      // skip the LDS transpose
 // mode[0] != mode[1], in which case it recomputes the codes with the real mode (confusion matrix and error
 // flags are mode independent and are not touched again).  ``class_hist_kernel`` then rolls the prediction
 // forward (mode[0] = mode[1], mode[1] = 0).  Net effect: no separate 131-MB range pass per update.
+// RNE fp32 -> 16-bit pattern without NaN special-casing (NaN / out-of-range patterns are rejected by score_code).
+template <typename T> __device__ __forceinline__ uint32_t rne16(float f);
+template <> __device__ __forceinline__ uint32_t rne16<__hip_bfloat16>(float f) {
+  const uint32_t u = __float_as_uint(f);
+  return (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;
+}
+template <> __device__ __forceinline__ uint32_t rne16<__half>(float f) { return round_bits16<__half>(f); }
+
+// softmax output code: RNE16(e * (1/s)).  The reciprocal form differs from an IEEE ``e / s`` by <= 1 fp32 ulp,
+// i.e. it moves a value across a 16-bit rounding boundary with probability ~2^-16 — the same order as the
+// summation-order differences every softmax implementation already has (tests bound the flip rate).
+template <typename T> __device__ __forceinline__ uint32_t quot_code(float e, float rinv) { return rne16<T>(e * rinv); }
+
+// LDS tile [C][kSlots] dwords, 2 rows per dword (u16 halves), slot XOR-swizzled by the class group q so the
+// per-lane scattered writes are (2-way at most) conflict free and the row read-out is conflict free.
+template <int ABL>
+__device__ __forceinline__ void lds_put(uint16_t* s_tile16, int c, int C, int q, int p, int h, uint32_t code) {
+  constexpr int kSlots = kTileRows / 2;
+  if constexpr (!(ABL & kAblNoLds)) {
+    if (c < C) s_tile16[2 * (c * kSlots + (p ^ (q & (kSlots - 1)))) + h] = static_cast<uint16_t>(code);
+  } else {
+    if (code == 0x1234u) s_tile16[threadIdx.x] = 0;  // keep the computation alive
+  }
+}
+
+// One row of up to 1024 classes lives in 2 x 16 B per lane: element j of lane -> class 8 * (lane + 64 * (j>>3)) + (j&7).
+template <typename T, int ABL>
+__device__ __forceinline__ void codes_for_row(const uint4 (&w)[2], int64_t t, bool valid, int C, int nvec, int lane,
+                                              bool do_softmax, bool fixup, int64_t* __restrict__ confmat,
+                                              int* __restrict__ err, bool& saw_bad, bool record_mode, int h, int p,
+                                              uint16_t* __restrict__ s_tile16) {
+  float v[16];
+  bool has_nan = false;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int q = lane + kWave * k;
+    const bool ok = valid && q < nvec;
+    float tmp[8];
+    unpack8<T>(w[k], tmp);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      v[8 * k + e] = ok ? tmp[e] : -INFINITY;
+      has_nan |= ok && (tmp[e] != tmp[e]);
+      if (!fixup && record_mode && ok) saw_bad |= bad16<T>(raw_bits<T>(w[k], e));
+    }
+  }
+  float mx = -INFINITY;
+  if (!fixup || do_softmax) {
+    // lane-local arg-max in increasing class order (strict > keeps the first maximum)
+    float m = v[0];
+    int am = 8 * lane;
+#pragma unroll
+    for (int j = 1; j < 16; ++j) {
+      const int c = 8 * (lane + kWave * (j >> 3)) + (j & 7);
+      if (v[j] > m) { m = v[j]; am = c; }
+    }
+    if (m == -INFINITY) am = C;  // nothing valid in this lane (or all -inf): never wins a tie
+    mx = m;
+    int amx = am;
+    wave_argmax(mx, amx);
+    if (__ballot(has_nan)) {  // rare: torch.argmax returns the first NaN
+      int first = C;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int c = 8 * (lane + kWave * (j >> 3)) + (j & 7);
+        if (v[j] != v[j] && c < first) first = c;
+      }
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) first = min(first, __shfl_xor(first, off, kWave));
+      amx = first;
+    }
+    if (!fixup && valid && confmat != nullptr && lane == 0 && t >= 0 && t < C && amx < C) atomic_add_i64(confmat + t * C + amx, 1);
+    if (!fixup && valid && (t < 0 || t >= C) && err != nullptr && lane == 0) atomicOr(err, 1);
+  }
+  if (do_softmax && !(ABL & kAblNoNorm)) {
+    float acc = 0.f;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      v[j] = expf(v[j] - mx);  // -inf (padding) -> 0
+      acc += v[j];
+    }
+    const float s = wave_sum(acc);
+    const float rinv = 1.f / s;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int c = 8 * (lane + kWave * (j >> 3)) + (j & 7);
+      uint32_t code = 0x8000u;
+      if (valid && c < C) {
+        const int sc = score_code<T>(static_cast<uint16_t>(quot_code<T>(v[j], rinv)));
+        code = sc < 0 ? 0x8000u : (uint32_t)sc | (c == t ? 0x4000u : 0u);
+      }
+      lds_put<ABL>(s_tile16, c, C, lane + kWave * (j >> 3), p, h, code);
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int c = 8 * (lane + kWave * (j >> 3)) + (j & 7);
+      uint32_t code = 0x8000u;
+      if (valid && c < C) {
+        const int sc = score_code<T>(raw_bits<T>(w[j >> 3], j & 7));
+        code = sc < 0 ? 0x8000u : (uint32_t)sc | (c == t ? 0x4000u : 0u);
+      }
+      lds_put<ABL>(s_tile16, c, C, lane + kWave * (j >> 3), p, h, code);
+    }
+  }
+}
+
+// Persistent, software-pipelined row pass.  Each wave walks its row pairs (2 per 32-row tile) and always has the
+// NEXT pair's 2 x 2 x 16 B loads in flight while it computes the current pair.
 template <typename T, bool FIXUP, int ABL = 0>
 __global__ void __launch_bounds__(kA_Threads, 4) mc_codes_kernel(const T* __restrict__ preds, const int64_t* __restrict__ target,
                                                                   int64_t n, int C, int* __restrict__ mode,
@@ -120,9 +230,11 @@ __global__ void __launch_bounds__(kA_Threads, 4) mc_codes_kernel(const T* __rest
                                                                   int64_t* __restrict__ confmat, int* __restrict__ err,
                                                                   bool record_mode) {
   extern __shared__ __attribute__((aligned(16))) uint32_t s_tile[];  // [C][kTileRows / 2]
+  constexpr int kSlots = kTileRows / 2;
+  constexpr int kWavesPerBlock = kA_Threads / kWave;
+  constexpr int kPairsPerWave = kSlots / kWavesPerBlock;
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = threadIdx.x / kWave;
-  const int nwaves = kA_Threads / kWave;
   int use_mode;
   if constexpr (FIXUP) {
     const int m0 = __hip_atomic_load(mode, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -132,125 +244,59 @@ __global__ void __launch_bounds__(kA_Threads, 4) mc_codes_kernel(const T* __rest
   } else {
     use_mode = mode[0];
   }
-  const bool do_softmax = (ABL & kAblNoNorm) ? false : use_mode != 0;
+  const bool do_softmax = use_mode != 0;
   bool saw_bad = false;
   const int nvec = C / 8;
   const int64_t ntiles = (n + kTileRows - 1) / kTileRows;
-  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const int64_t r0 = tile * kTileRows;
-    // every wave owns kPairs row pairs of the tile: issue all their 16-B loads first (latency hiding), then
-    // compute pair by pair.
-    constexpr int kPairs = kTileRows / 2 / (kA_Threads / kWave);
-    uint4 wbuf[kPairs][2][2];
-    int64_t tv[kPairs][2];
+
+  // row sequence of this wave inside a tile: local rows {2w, 2w+1, 2w+16, 2w+17, ...} (pairs w, w+8)
+  auto local_row = [&](int i) { return 2 * (wave + (i >> 1) * kWavesPerBlock) + (i & 1); };
+  constexpr int kRowsPerWave = 2 * kPairsPerWave;
+  auto load_row = [&](int64_t tl, int lr, uint4 (&w)[2], int64_t& tv) {
+    const int64_t r = tl * kTileRows + lr;
+    const bool in = tl < ntiles && r < n;
+    tv = in ? target[r] : INT64_MIN;
+    const uint4* row = reinterpret_cast<const uint4*>(preds + (in ? r : 0) * C);
 #pragma unroll
-    for (int pp = 0; pp < kPairs; ++pp)
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int64_t r = r0 + 2 * (wave + pp * nwaves) + h;
-        tv[pp][h] = r < n ? target[r] : INT64_MIN;
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-          const int q = lane + kWave * k;
-          wbuf[pp][h][k] = (r < n && q < nvec) ? reinterpret_cast<const uint4*>(preds + r * C)[q] : make_uint4(0, 0, 0, 0);
-        }
-      }
-#pragma unroll
-    for (int pp = 0; pp < kPairs; ++pp) {
-      const int p = wave + pp * nwaves;
-      uint32_t packed[16];
-#pragma unroll
-      for (int j = 0; j < 16; ++j) packed[j] = 0;
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int64_t t = tv[pp][h];
-        bool valid = t != INT64_MIN;
-        if (has_ignore && t == ignore_index) valid = false;
-        if (!FIXUP && valid && (t < 0 || t >= C) && err != nullptr && lane == 0) atomicOr(err, 1);
-        const uint4* w = wbuf[pp][h];
-        float v[16];
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-          const int q = lane + kWave * k;
-          if (valid && q < nvec) {
-            unpack8<T>(w[k], v + 8 * k);
-            if (!FIXUP && record_mode) {
-#pragma unroll
-              for (int e = 0; e < 8; ++e) saw_bad |= bad16<T>(raw_bits<T>(w[k], e));
-            }
-          } else {
-#pragma unroll
-            for (int e = 0; e < 8; ++e) v[8 * k + e] = -INFINITY;
-          }
-        }
-        float mx = -INFINITY;
-        if (!FIXUP || do_softmax) {
-          float m = -INFINITY;
-          int am = C;
-#pragma unroll
-          for (int k = 0; k < 2; ++k)
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-              const int c = 8 * (lane + kWave * k) + e;
-              if (c < C && argmax_better(v[8 * k + e], c, m, am)) { m = v[8 * k + e]; am = c; }
-            }
-          mx = m;
-          int amx = am;
-          wave_argmax(mx, amx);
-          if (!FIXUP && valid && confmat != nullptr && lane == 0 && t >= 0 && t < C && amx < C)
-            atomic_add_i64(confmat + t * C + amx, 1);
-        }
-        float s = 1.f;
-        if (do_softmax) {
-          float acc = 0.f;
-#pragma unroll
-          for (int j = 0; j < 16; ++j) {
-            const int c = 8 * (lane + kWave * (j >> 3)) + (j & 7);
-            if (c < C) { v[j] = expf(v[j] - mx); acc += v[j]; }
-          }
-          s = wave_sum(acc);
-        }
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-          const int c = 8 * (lane + kWave * (j >> 3)) + (j & 7);
-          uint32_t code = 0x8000u;
-          if (valid && c < C) {
-            const uint16_t b = do_softmax ? round_bits16<T>(v[j] / s) : raw_bits<T>(w[j >> 3], j & 7);
-            const int sc = score_code<T>(b);
-            code = sc < 0 ? 0x8000u : (uint32_t)sc | (c == t ? 0x4000u : 0u);
-          }
-          packed[j] |= code << (16 * h);
-        }
-      }
-      if constexpr (!(ABL & kAblNoLds)) {
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-          const int q = lane + kWave * (j >> 3);
-          const int c = 8 * q + (j & 7);
-          if (c < C) s_tile[c * (kTileRows / 2) + (p ^ (q & (kTileRows / 2 - 1)))] = packed[j];
-        }
-      } else {
-        uint32_t acc = 0;
-#pragma unroll
-        for (int j = 0; j < 16; ++j) acc ^= packed[j];
-        if (acc == 0x12345678u) s_tile[threadIdx.x] = acc;  // keep the computation alive
-      }
+    for (int k = 0; k < 2; ++k) {
+      const int q = lane + kWave * k;
+      w[k] = (in && q < nvec) ? row[q] : make_uint4(0, 0, 0, 0);
+    }
+  };
+
+  uint4 wcur[2], wnext[2];
+  int64_t tcur, tnext;
+  int64_t tile = blockIdx.x;
+  load_row(tile, local_row(0), wcur, tcur);
+  for (; tile < ntiles; tile += gridDim.x) {
+#pragma unroll 1
+    for (int i = 0; i < kRowsPerWave; ++i) {
+      // keep the next row's loads in flight while this row is computed
+      if (i + 1 < kRowsPerWave) load_row(tile, local_row(i + 1), wnext, tnext);
+      else load_row(tile + gridDim.x, local_row(0), wnext, tnext);
+      const bool valid = tcur != INT64_MIN && !(has_ignore && tcur == ignore_index);
+      codes_for_row<T, ABL>(wcur, tcur, valid, C, nvec, lane, do_softmax, FIXUP, confmat, err, saw_bad, record_mode,
+                            i & 1, wave + (i >> 1) * kWavesPerBlock, reinterpret_cast<uint16_t*>(s_tile));
+      tcur = tnext;
+      wcur[0] = wnext[0];
+      wcur[1] = wnext[1];
     }
     __syncthreads();
     if constexpr (!(ABL & kAblNoStore)) {
-      const int64_t seg = r0 / 2;  // dword offset of this tile inside a class row
-      constexpr int kSlots = kTileRows / 2;
+      const int64_t seg = tile * (kTileRows / 2);  // dword offset of this tile inside a class row
+      const int64_t row_dw = n_pad / 2;
       for (int idx = threadIdx.x; idx < C * kSlots; idx += kA_Threads) {
         const int c = idx / kSlots, d = idx % kSlots;
         const uint32_t wv = s_tile[idx];
         const int p = d ^ ((c >> 3) & (kSlots - 1));
-        codes[(int64_t)c * (n_pad / 2) + seg + p] = wv;
+        codes[c * row_dw + seg + p] = wv;
       }
     }
     __syncthreads();
   }
   if constexpr (!FIXUP) {
-    if (record_mode && __syncthreads_or(saw_bad) && threadIdx.x == 0)
+    if (record_mode && __syncthreads_or(saw_bad) && threadIdx.x == 0 &&
+        __hip_atomic_load(mode + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
       __hip_atomic_store(mode + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }

@@ -53,7 +53,7 @@ int main() {
   int hm[2] = {1, 0};
   CK(hipMemcpy(mode, hm, 8, hipMemcpyHostToDevice));
   const int64_t ntiles = n_pad / kTileRows;
-  const int grid = (int)std::min<int64_t>(ntiles, 256 * 8);
+  const int grid = (int)std::min<int64_t>(ntiles, 256 * 2);
   const size_t shm = (size_t)C * (kTileRows / 2) * 4;
 #define RUN_MC(ABL) time_us([&] { hipLaunchKernelGGL((mc_codes_kernel<__hip_bfloat16, false, ABL>), grid, kA_Threads, shm, 0, d, dt, N, C, mode, -1, false, codes, n_pad, cm, err, false); })
   float t_full = RUN_MC(0);
