@@ -23,12 +23,21 @@ BASELINE_UPDATES_PER_SEC = None  # filled from BASELINE.json "published" (none p
 
 
 def _baseline() -> "float | None":
-    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "BASELINE.json")
+    """BASELINE.json publishes no number; BASELINE.md's config-2 row holds the reference measured on MI355X with
+    this same harness (per-GPU updates/s, ``profiles/reference_baseline_mi355x.json``).  Weak scaling: the
+    whole-node baseline for N GPUs is N x the 1-GPU reference rate (the reference cannot do better: its compute
+    gathers every rank's scores and sorts per class on every rank)."""
+    here = os.path.dirname(os.path.abspath(__file__))
     try:
-        with open(path) as f:
+        with open(os.path.join(here, "BASELINE.json")) as f:
             pub = json.load(f).get("published", {})
-        v = pub.get("metric_updates_per_sec_1gpu") if isinstance(pub, dict) else None
-        return float(v) if v else None
+        if isinstance(pub, dict) and pub.get("metric_updates_per_sec_1gpu"):
+            return float(pub["metric_updates_per_sec_1gpu"])
+    except Exception:
+        pass
+    try:
+        with open(os.path.join(here, "profiles", "reference_baseline_mi355x.json")) as f:
+            return float(json.load(f)["ref_updates_per_sec"])
     except Exception:
         return None
 
@@ -131,7 +140,7 @@ def main() -> None:
             "ms_per_step": round(1000.0 * elapsed / args.steps, 4),
             "higher_is_better": True,
             "scaling": "weak",
-            "vs_baseline": round(value / base, 3) if base else None,
+            "vs_baseline": round(value / (base * world), 3) if base else None,
             "dtype": "bf16",
             "data": "synthetic (randn bf16 logits [65536,1000] + uniform int64 labels, pre-generated pool in HBM)",
             "config": {
