@@ -1,17 +1,45 @@
 """Classification metrics (API parity: reference ``classification/__init__.py``)."""
-from torchmetrics_forked_amd.classification.accuracy import Accuracy, BinaryAccuracy, MulticlassAccuracy, MultilabelAccuracy
-from torchmetrics_forked_amd.classification.auroc import AUROC, BinaryAUROC, MulticlassAUROC, MultilabelAUROC
+from torchmetrics_forked_amd.classification.accuracy import (
+    Accuracy,
+    BinaryAccuracy,
+    MulticlassAccuracy,
+    MultilabelAccuracy,
+)
+from torchmetrics_forked_amd.classification.auroc import (
+    AUROC,
+    BinaryAUROC,
+    MulticlassAUROC,
+    MultilabelAUROC,
+)
 from torchmetrics_forked_amd.classification.average_precision import (
     AveragePrecision,
     BinaryAveragePrecision,
     MulticlassAveragePrecision,
     MultilabelAveragePrecision,
 )
+from torchmetrics_forked_amd.classification.calibration_error import (
+    BinaryCalibrationError,
+    CalibrationError,
+    MulticlassCalibrationError,
+)
+from torchmetrics_forked_amd.classification.cohen_kappa import (
+    BinaryCohenKappa,
+    CohenKappa,
+    MulticlassCohenKappa,
+)
 from torchmetrics_forked_amd.classification.confusion_matrix import (
     BinaryConfusionMatrix,
     ConfusionMatrix,
     MulticlassConfusionMatrix,
     MultilabelConfusionMatrix,
+)
+from torchmetrics_forked_amd.classification.dice import (
+    Dice,
+)
+from torchmetrics_forked_amd.classification.exact_match import (
+    ExactMatch,
+    MulticlassExactMatch,
+    MultilabelExactMatch,
 )
 from torchmetrics_forked_amd.classification.f_beta import (
     BinaryF1Score,
@@ -23,11 +51,38 @@ from torchmetrics_forked_amd.classification.f_beta import (
     MultilabelF1Score,
     MultilabelFBetaScore,
 )
+from torchmetrics_forked_amd.classification.group_fairness import (
+    BinaryFairness,
+    BinaryGroupStatRates,
+)
 from torchmetrics_forked_amd.classification.hamming import (
     BinaryHammingDistance,
     HammingDistance,
     MulticlassHammingDistance,
     MultilabelHammingDistance,
+)
+from torchmetrics_forked_amd.classification.hinge import (
+    BinaryHingeLoss,
+    HingeLoss,
+    MulticlassHingeLoss,
+)
+from torchmetrics_forked_amd.classification.jaccard import (
+    BinaryJaccardIndex,
+    JaccardIndex,
+    MulticlassJaccardIndex,
+    MultilabelJaccardIndex,
+)
+from torchmetrics_forked_amd.classification.matthews_corrcoef import (
+    BinaryMatthewsCorrCoef,
+    MatthewsCorrCoef,
+    MulticlassMatthewsCorrCoef,
+    MultilabelMatthewsCorrCoef,
+)
+from torchmetrics_forked_amd.classification.precision_fixed_recall import (
+    BinaryPrecisionAtFixedRecall,
+    MulticlassPrecisionAtFixedRecall,
+    MultilabelPrecisionAtFixedRecall,
+    PrecisionAtFixedRecall,
 )
 from torchmetrics_forked_amd.classification.precision_recall import (
     BinaryPrecision,
@@ -45,12 +100,34 @@ from torchmetrics_forked_amd.classification.precision_recall_curve import (
     MultilabelPrecisionRecallCurve,
     PrecisionRecallCurve,
 )
-from torchmetrics_forked_amd.classification.roc import ROC, BinaryROC, MulticlassROC, MultilabelROC
+from torchmetrics_forked_amd.classification.ranking import (
+    MultilabelCoverageError,
+    MultilabelRankingAveragePrecision,
+    MultilabelRankingLoss,
+)
+from torchmetrics_forked_amd.classification.recall_fixed_precision import (
+    BinaryRecallAtFixedPrecision,
+    MulticlassRecallAtFixedPrecision,
+    MultilabelRecallAtFixedPrecision,
+    RecallAtFixedPrecision,
+)
+from torchmetrics_forked_amd.classification.roc import (
+    ROC,
+    BinaryROC,
+    MulticlassROC,
+    MultilabelROC,
+)
 from torchmetrics_forked_amd.classification.specificity import (
     BinarySpecificity,
     MulticlassSpecificity,
     MultilabelSpecificity,
     Specificity,
+)
+from torchmetrics_forked_amd.classification.specificity_sensitivity import (
+    BinarySpecificityAtSensitivity,
+    MulticlassSpecificityAtSensitivity,
+    MultilabelSpecificityAtSensitivity,
+    SpecificityAtSensitivity,
 )
 from torchmetrics_forked_amd.classification.stat_scores import (
     BinaryStatScores,

@@ -1,0 +1,232 @@
+"""Fixed-operating-point curve metrics: Recall@Precision, Precision@Recall, Specificity@Sensitivity
+(API parity: reference ``classification/recall_fixed_precision.py``, ``precision_fixed_recall.py``,
+``specificity_sensitivity.py``).  They subclass the PR-curve modules, so they share the exact 16-bit histogram /
+sample / binned state machinery and its single-collective sync."""
+from typing import Any, Callable, List, Optional, Tuple, Type, Union
+
+from torch import Tensor
+from typing_extensions import Literal
+
+from torchmetrics_forked_amd.classification.base import _ClassificationTaskWrapper
+from torchmetrics_forked_amd.classification.precision_recall_curve import (
+    BinaryPrecisionRecallCurve,
+    MulticlassPrecisionRecallCurve,
+    MultilabelPrecisionRecallCurve,
+    _curve_task_factory,
+)
+from torchmetrics_forked_amd.functional.classification.precision_fixed_recall import _precision_at_recall
+from torchmetrics_forked_amd.functional.classification.precision_recall_curve import precision_recall_curve_compute
+from torchmetrics_forked_amd.functional.classification.recall_fixed_precision import (
+    _binary_recall_at_fixed_precision_arg_validation,
+    _fixed_compute,
+    _multiclass_recall_at_fixed_precision_arg_validation,
+    _multilabel_recall_at_fixed_precision_arg_validation,
+    _recall_at_precision,
+)
+from torchmetrics_forked_amd.functional.classification.roc import roc_compute
+from torchmetrics_forked_amd.functional.classification.specificity_sensitivity import (
+    _binary_specificity_at_sensitivity_arg_validation,
+    _from_fpr,
+    _multiclass_specificity_at_sensitivity_arg_validation,
+    _multilabel_specificity_at_sensitivity_arg_validation,
+)
+from torchmetrics_forked_amd.metric import Metric
+from torchmetrics_forked_amd.utilities.plot import _AX_TYPE, _PLOT_OUT_TYPE
+
+_Thr = Optional[Union[int, List[float], Tensor]]
+
+
+class _FixedPointMixin:
+    """``compute`` = curve -> per-class operating point.  Subclasses set the reduce/curve functions."""
+
+    is_differentiable: bool = False
+    higher_is_better: Optional[bool] = None
+    full_state_update: bool = False
+    plot_lower_bound: float = 0.0
+    plot_upper_bound: float = 1.0
+    _reduce_fn: Callable
+    _curve_fn: Callable = staticmethod(precision_recall_curve_compute)
+    _min_attr: str
+
+    def compute(self) -> Tuple[Tensor, Tensor]:
+        cls = type(self)
+        return _fixed_compute(
+            self._curve_state(),  # type: ignore[attr-defined]
+            self._task,  # type: ignore[attr-defined]
+            self._num,  # type: ignore[attr-defined]
+            self.thresholds,  # type: ignore[attr-defined]
+            self.ignore_index,  # type: ignore[attr-defined]
+            getattr(self, cls._min_attr),
+            cls._reduce_fn,
+            curve_fn=cls._curve_fn,
+        )
+
+    def plot(self, val: Optional[Any] = None, ax: Optional[_AX_TYPE] = None) -> _PLOT_OUT_TYPE:  # type: ignore[override]
+        val = val if val is not None else self.compute()[0]
+        return self._plot(val, ax)  # type: ignore[attr-defined]
+
+
+def _binary_init(self: Any, min_value: float, attr: str, thresholds: _Thr, ignore_index: Optional[int],
+                 validate_args: bool, validator: Callable, kwargs: dict) -> None:
+    BinaryPrecisionRecallCurve.__init__(self, thresholds, ignore_index, validate_args=False, **kwargs)
+    if validate_args:
+        validator(min_value, thresholds, ignore_index)
+    setattr(self, attr, min_value)
+    self.validate_args = validate_args
+
+
+def _multi_init(self: Any, base: type, num: int, min_value: float, attr: str, thresholds: _Thr,
+                ignore_index: Optional[int], validate_args: bool, validator: Callable, kwargs: dict) -> None:
+    base.__init__(self, num, thresholds=thresholds, ignore_index=ignore_index, validate_args=False, **kwargs)
+    if validate_args:
+        validator(num, min_value, thresholds, ignore_index)
+    setattr(self, attr, min_value)
+    self.validate_args = validate_args
+
+
+# ---------------------------------------------------------------------------------------------- recall @ precision
+class BinaryRecallAtFixedPrecision(_FixedPointMixin, BinaryPrecisionRecallCurve):
+    higher_is_better = True
+    _reduce_fn = staticmethod(_recall_at_precision)
+    _min_attr = "min_precision"
+
+    def __init__(self, min_precision: float, thresholds: _Thr = None, ignore_index: Optional[int] = None,
+                 validate_args: bool = True, **kwargs: Any) -> None:
+        _binary_init(self, min_precision, "min_precision", thresholds, ignore_index, validate_args,
+                     _binary_recall_at_fixed_precision_arg_validation, kwargs)
+
+
+class MulticlassRecallAtFixedPrecision(_FixedPointMixin, MulticlassPrecisionRecallCurve):
+    higher_is_better = True
+    _reduce_fn = staticmethod(_recall_at_precision)
+    _min_attr = "min_precision"
+
+    def __init__(self, num_classes: int, min_precision: float, thresholds: _Thr = None,
+                 ignore_index: Optional[int] = None, validate_args: bool = True, **kwargs: Any) -> None:
+        _multi_init(self, MulticlassPrecisionRecallCurve, num_classes, min_precision, "min_precision", thresholds,
+                    ignore_index, validate_args, _multiclass_recall_at_fixed_precision_arg_validation, kwargs)
+
+
+class MultilabelRecallAtFixedPrecision(_FixedPointMixin, MultilabelPrecisionRecallCurve):
+    higher_is_better = True
+    _reduce_fn = staticmethod(_recall_at_precision)
+    _min_attr = "min_precision"
+
+    def __init__(self, num_labels: int, min_precision: float, thresholds: _Thr = None,
+                 ignore_index: Optional[int] = None, validate_args: bool = True, **kwargs: Any) -> None:
+        _multi_init(self, MultilabelPrecisionRecallCurve, num_labels, min_precision, "min_precision", thresholds,
+                    ignore_index, validate_args, _multilabel_recall_at_fixed_precision_arg_validation, kwargs)
+
+
+# ---------------------------------------------------------------------------------------------- precision @ recall
+class BinaryPrecisionAtFixedRecall(_FixedPointMixin, BinaryPrecisionRecallCurve):
+    higher_is_better = True
+    _reduce_fn = staticmethod(_precision_at_recall)
+    _min_attr = "min_recall"
+
+    def __init__(self, min_recall: float, thresholds: _Thr = None, ignore_index: Optional[int] = None,
+                 validate_args: bool = True, **kwargs: Any) -> None:
+        _binary_init(self, min_recall, "min_recall", thresholds, ignore_index, validate_args,
+                     _binary_recall_at_fixed_precision_arg_validation, kwargs)
+
+
+class MulticlassPrecisionAtFixedRecall(_FixedPointMixin, MulticlassPrecisionRecallCurve):
+    higher_is_better = True
+    _reduce_fn = staticmethod(_precision_at_recall)
+    _min_attr = "min_recall"
+
+    def __init__(self, num_classes: int, min_recall: float, thresholds: _Thr = None,
+                 ignore_index: Optional[int] = None, validate_args: bool = True, **kwargs: Any) -> None:
+        _multi_init(self, MulticlassPrecisionRecallCurve, num_classes, min_recall, "min_recall", thresholds,
+                    ignore_index, validate_args, _multiclass_recall_at_fixed_precision_arg_validation, kwargs)
+
+
+class MultilabelPrecisionAtFixedRecall(_FixedPointMixin, MultilabelPrecisionRecallCurve):
+    higher_is_better = True
+    _reduce_fn = staticmethod(_precision_at_recall)
+    _min_attr = "min_recall"
+
+    def __init__(self, num_labels: int, min_recall: float, thresholds: _Thr = None,
+                 ignore_index: Optional[int] = None, validate_args: bool = True, **kwargs: Any) -> None:
+        _multi_init(self, MultilabelPrecisionRecallCurve, num_labels, min_recall, "min_recall", thresholds,
+                    ignore_index, validate_args, _multilabel_recall_at_fixed_precision_arg_validation, kwargs)
+
+
+# ------------------------------------------------------------------------------------- specificity @ sensitivity
+class BinarySpecificityAtSensitivity(_FixedPointMixin, BinaryPrecisionRecallCurve):
+    higher_is_better = True
+    _reduce_fn = staticmethod(_from_fpr)
+    _curve_fn = staticmethod(roc_compute)
+    _min_attr = "min_sensitivity"
+
+    def __init__(self, min_sensitivity: float, thresholds: _Thr = None, ignore_index: Optional[int] = None,
+                 validate_args: bool = True, **kwargs: Any) -> None:
+        _binary_init(self, min_sensitivity, "min_sensitivity", thresholds, ignore_index, validate_args,
+                     _binary_specificity_at_sensitivity_arg_validation, kwargs)
+
+
+class MulticlassSpecificityAtSensitivity(_FixedPointMixin, MulticlassPrecisionRecallCurve):
+    higher_is_better = True
+    _reduce_fn = staticmethod(_from_fpr)
+    _curve_fn = staticmethod(roc_compute)
+    _min_attr = "min_sensitivity"
+
+    def __init__(self, num_classes: int, min_sensitivity: float, thresholds: _Thr = None,
+                 ignore_index: Optional[int] = None, validate_args: bool = True, **kwargs: Any) -> None:
+        _multi_init(self, MulticlassPrecisionRecallCurve, num_classes, min_sensitivity, "min_sensitivity", thresholds,
+                    ignore_index, validate_args, _multiclass_specificity_at_sensitivity_arg_validation, kwargs)
+
+
+class MultilabelSpecificityAtSensitivity(_FixedPointMixin, MultilabelPrecisionRecallCurve):
+    higher_is_better = True
+    _reduce_fn = staticmethod(_from_fpr)
+    _curve_fn = staticmethod(roc_compute)
+    _min_attr = "min_sensitivity"
+
+    def __init__(self, num_labels: int, min_sensitivity: float, thresholds: _Thr = None,
+                 ignore_index: Optional[int] = None, validate_args: bool = True, **kwargs: Any) -> None:
+        _multi_init(self, MultilabelPrecisionRecallCurve, num_labels, min_sensitivity, "min_sensitivity", thresholds,
+                    ignore_index, validate_args, _multilabel_specificity_at_sensitivity_arg_validation, kwargs)
+
+
+# ------------------------------------------------------------------------------------------------- task wrappers
+def _wrapper(binary: type, multiclass: type, multilabel: type, min_name: str) -> Callable:
+    """``__new__`` of a task wrapper: ``(task, <min_value>, thresholds, num_classes, num_labels, ignore_index,
+    validate_args, **kwargs)`` -- the reference's positional order."""
+    order = (min_name, "thresholds", "num_classes", "num_labels", "ignore_index", "validate_args")
+    defaults = {"thresholds": None, "num_classes": None, "num_labels": None, "ignore_index": None, "validate_args": True}
+
+    def __new__(cls: type, task: Literal["binary", "multiclass", "multilabel"], *args: Any, **kwargs: Any) -> Metric:
+        if len(args) > len(order):
+            raise TypeError(f"{cls.__name__} got too many positional arguments")
+        for name, value in zip(order, args):
+            if name in kwargs:
+                raise TypeError(f"{cls.__name__} got multiple values for argument '{name}'")
+            kwargs[name] = value
+        if min_name not in kwargs:
+            raise TypeError(f"{cls.__name__} missing required argument '{min_name}'")
+        opts = {k: kwargs.pop(k, v) for k, v in defaults.items()}
+        min_value = kwargs.pop(min_name)
+        num_classes, num_labels = opts.pop("num_classes"), opts.pop("num_labels")
+        kwargs.update(opts)
+        return _curve_task_factory(
+            task, binary, multiclass, multilabel, (min_value,), (num_classes, min_value), (num_labels, min_value),
+            num_classes, num_labels, kwargs,
+        )
+
+    return __new__
+
+
+class RecallAtFixedPrecision(_ClassificationTaskWrapper):
+    __new__ = _wrapper(BinaryRecallAtFixedPrecision, MulticlassRecallAtFixedPrecision,  # type: ignore[assignment]
+                       MultilabelRecallAtFixedPrecision, "min_precision")
+
+
+class PrecisionAtFixedRecall(_ClassificationTaskWrapper):
+    __new__ = _wrapper(BinaryPrecisionAtFixedRecall, MulticlassPrecisionAtFixedRecall,  # type: ignore[assignment]
+                       MultilabelPrecisionAtFixedRecall, "min_recall")
+
+
+class SpecificityAtSensitivity(_ClassificationTaskWrapper):
+    __new__ = _wrapper(BinarySpecificityAtSensitivity, MulticlassSpecificityAtSensitivity,  # type: ignore[assignment]
+                       MultilabelSpecificityAtSensitivity, "min_sensitivity")

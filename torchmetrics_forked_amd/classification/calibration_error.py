@@ -1,0 +1,115 @@
+"""Calibration-error modules (API parity: reference ``classification/calibration_error.py:41-395``).
+
+State is the ``[3, n_bins + 1]`` per-bin (count, sum confidence, sum accuracy) table -- O(bins) memory and a
+single all-reduce on sync instead of the reference's O(N) ``cat`` lists (see the functional module docstring)."""
+from typing import Any, Optional, Type
+
+import torch
+from torch import Tensor
+from typing_extensions import Literal
+
+from torchmetrics_forked_amd.classification.base import _ClassificationTaskWrapper
+from torchmetrics_forked_amd.functional.classification._formats import binary_format, multiclass_format
+from torchmetrics_forked_amd.functional.classification.calibration_error import (
+    _binary_calibration_error_arg_validation,
+    _binary_calibration_error_tensor_validation,
+    _ce_bin_update,
+    _ce_from_bins,
+    _multiclass_calibration_error_arg_validation,
+    _multiclass_calibration_error_tensor_validation,
+    _multiclass_calibration_error_update,
+)
+from torchmetrics_forked_amd.metric import Metric
+from torchmetrics_forked_amd.utilities.enums import ClassificationTaskNoMultilabel
+from torchmetrics_forked_amd.utilities.plot import _AX_TYPE, _PLOT_OUT_TYPE
+
+
+class _CalibrationBase(Metric):
+    is_differentiable: bool = False
+    higher_is_better: bool = False
+    full_state_update: bool = False
+    plot_lower_bound: float = 0.0
+    plot_upper_bound: float = 1.0
+    bins: Tensor
+
+    def _create_states(self, n_bins: int) -> None:
+        self.add_state("bins", torch.zeros(3, n_bins + 1, dtype=torch.float64), dist_reduce_fx="sum")
+
+    def compute(self) -> Tensor:
+        return _ce_from_bins(self.bins, self.norm)
+
+    def plot(self, val: Optional[Tensor] = None, ax: Optional[_AX_TYPE] = None) -> _PLOT_OUT_TYPE:
+        return self._plot(val, ax)
+
+
+class BinaryCalibrationError(_CalibrationBase):
+    def __init__(
+        self,
+        n_bins: int = 15,
+        norm: Literal["l1", "l2", "max"] = "l1",
+        ignore_index: Optional[int] = None,
+        validate_args: bool = True,
+        **kwargs: Any,
+    ) -> None:
+        super().__init__(**kwargs)
+        if validate_args:
+            _binary_calibration_error_arg_validation(n_bins, norm, ignore_index)
+        self.validate_args = validate_args
+        self.n_bins = n_bins
+        self.norm = norm
+        self.ignore_index = ignore_index
+        self._create_states(n_bins)
+
+    def update(self, preds: Tensor, target: Tensor) -> None:
+        if self.validate_args:
+            _binary_calibration_error_tensor_validation(preds, target, self.ignore_index)
+        preds, target = binary_format(preds, target, 0.0, self.ignore_index, convert_to_labels=False)
+        _ce_bin_update(preds, target, self.n_bins, self.bins)
+
+
+class MulticlassCalibrationError(_CalibrationBase):
+    def __init__(
+        self,
+        num_classes: int,
+        n_bins: int = 15,
+        norm: Literal["l1", "l2", "max"] = "l1",
+        ignore_index: Optional[int] = None,
+        validate_args: bool = True,
+        **kwargs: Any,
+    ) -> None:
+        super().__init__(**kwargs)
+        if validate_args:
+            _multiclass_calibration_error_arg_validation(num_classes, n_bins, norm, ignore_index)
+        self.validate_args = validate_args
+        self.num_classes = num_classes
+        self.n_bins = n_bins
+        self.norm = norm
+        self.ignore_index = ignore_index
+        self._create_states(n_bins)
+
+    def update(self, preds: Tensor, target: Tensor) -> None:
+        if self.validate_args:
+            _multiclass_calibration_error_tensor_validation(preds, target, self.num_classes, self.ignore_index)
+        preds, target = multiclass_format(preds, target, self.ignore_index, convert_to_labels=False)
+        conf, acc = _multiclass_calibration_error_update(preds, target)
+        _ce_bin_update(conf, acc, self.n_bins, self.bins)
+
+
+class CalibrationError(_ClassificationTaskWrapper):
+    def __new__(  # type: ignore[misc]
+        cls: Type["CalibrationError"],
+        task: Literal["binary", "multiclass"],
+        n_bins: int = 15,
+        norm: Literal["l1", "l2", "max"] = "l1",
+        num_classes: Optional[int] = None,
+        ignore_index: Optional[int] = None,
+        validate_args: bool = True,
+        **kwargs: Any,
+    ) -> Metric:
+        task = ClassificationTaskNoMultilabel.from_str(task)
+        kwargs.update({"n_bins": n_bins, "norm": norm, "ignore_index": ignore_index, "validate_args": validate_args})
+        if task == ClassificationTaskNoMultilabel.BINARY:
+            return BinaryCalibrationError(**kwargs)
+        if not isinstance(num_classes, int):
+            raise ValueError(f"`num_classes` is expected to be `int` but `{type(num_classes)} was passed.`")
+        return MulticlassCalibrationError(num_classes, **kwargs)

@@ -1,0 +1,134 @@
+"""Exact-match modules (API parity: reference ``classification/exact_match.py:44-410``)."""
+from typing import Any, Optional, Type
+
+import torch
+from torch import Tensor
+from typing_extensions import Literal
+
+from torchmetrics_forked_amd.classification.base import _ClassificationTaskWrapper
+from torchmetrics_forked_amd.functional.classification.exact_match import (
+    _exact_match_reduce,
+    _multiclass_exact_match_update,
+    _multilabel_exact_match_update,
+)
+from torchmetrics_forked_amd.functional.classification.stat_scores import (
+    _multiclass_stat_scores_arg_validation,
+    _multiclass_stat_scores_format,
+    _multiclass_stat_scores_tensor_validation,
+    _multilabel_stat_scores_arg_validation,
+    _multilabel_stat_scores_format,
+    _multilabel_stat_scores_tensor_validation,
+)
+from torchmetrics_forked_amd.metric import Metric
+from torchmetrics_forked_amd.utilities.data import dim_zero_cat
+from torchmetrics_forked_amd.utilities.enums import ClassificationTaskNoBinary
+from torchmetrics_forked_amd.utilities.plot import _AX_TYPE, _PLOT_OUT_TYPE
+
+
+class _ExactMatchBase(Metric):
+    is_differentiable: bool = False
+    higher_is_better: bool = True
+    full_state_update: bool = False
+    plot_lower_bound: float = 0.0
+    plot_upper_bound: float = 1.0
+
+    def _create_states(self) -> None:
+        glob = self.multidim_average == "global"
+        self.add_state("correct", torch.zeros(1, dtype=torch.long) if glob else [], dist_reduce_fx="sum" if glob else "cat")
+        self.add_state("total", torch.zeros(1, dtype=torch.long), dist_reduce_fx="sum" if glob else "mean")
+
+    def _accumulate(self, correct: Tensor, total: Tensor) -> None:
+        if self.multidim_average == "samplewise":
+            self.correct.append(correct)
+            self.total = total
+        else:
+            self.correct += correct
+            self.total += total
+
+    def compute(self) -> Tensor:
+        correct = dim_zero_cat(self.correct) if isinstance(self.correct, list) else self.correct
+        return _exact_match_reduce(correct, self.total)
+
+    def plot(self, val: Optional[Tensor] = None, ax: Optional[_AX_TYPE] = None) -> _PLOT_OUT_TYPE:
+        return self._plot(val, ax)
+
+
+class MulticlassExactMatch(_ExactMatchBase):
+    def __init__(
+        self,
+        num_classes: int,
+        multidim_average: Literal["global", "samplewise"] = "global",
+        ignore_index: Optional[int] = None,
+        validate_args: bool = True,
+        **kwargs: Any,
+    ) -> None:
+        super().__init__(**kwargs)
+        if validate_args:
+            _multiclass_stat_scores_arg_validation(num_classes, 1, None, multidim_average, ignore_index)
+        self.num_classes = num_classes
+        self.multidim_average = multidim_average
+        self.ignore_index = ignore_index
+        self.validate_args = validate_args
+        self._create_states()
+
+    def update(self, preds: Tensor, target: Tensor) -> None:
+        if self.validate_args:
+            _multiclass_stat_scores_tensor_validation(
+                preds, target, self.num_classes, self.multidim_average, self.ignore_index, self._validation_sink(target)
+            )
+        preds, target = _multiclass_stat_scores_format(preds, target, 1)
+        self._accumulate(*_multiclass_exact_match_update(preds, target, self.multidim_average, self.ignore_index))
+
+
+class MultilabelExactMatch(_ExactMatchBase):
+    def __init__(
+        self,
+        num_labels: int,
+        threshold: float = 0.5,
+        multidim_average: Literal["global", "samplewise"] = "global",
+        ignore_index: Optional[int] = None,
+        validate_args: bool = True,
+        **kwargs: Any,
+    ) -> None:
+        super().__init__(**kwargs)
+        if validate_args:
+            _multilabel_stat_scores_arg_validation(num_labels, threshold, None, multidim_average, ignore_index)
+        self.num_labels = num_labels
+        self.threshold = threshold
+        self.multidim_average = multidim_average
+        self.ignore_index = ignore_index
+        self.validate_args = validate_args
+        self._create_states()
+
+    def update(self, preds: Tensor, target: Tensor) -> None:
+        if self.validate_args:
+            _multilabel_stat_scores_tensor_validation(
+                preds, target, self.num_labels, self.multidim_average, self.ignore_index, self._validation_sink(target)
+            )
+        preds, target = _multilabel_stat_scores_format(preds, target, self.num_labels, self.threshold, self.ignore_index)
+        self._accumulate(*_multilabel_exact_match_update(preds, target, self.num_labels, self.multidim_average))
+
+
+class ExactMatch(_ClassificationTaskWrapper):
+    def __new__(  # type: ignore[misc]
+        cls: Type["ExactMatch"],
+        task: Literal["multiclass", "multilabel"],
+        threshold: float = 0.5,
+        num_classes: Optional[int] = None,
+        num_labels: Optional[int] = None,
+        multidim_average: Literal["global", "samplewise"] = "global",
+        ignore_index: Optional[int] = None,
+        validate_args: bool = True,
+        **kwargs: Any,
+    ) -> Metric:
+        task = ClassificationTaskNoBinary.from_str(task)
+        kwargs.update({"multidim_average": multidim_average, "ignore_index": ignore_index, "validate_args": validate_args})
+        if task == ClassificationTaskNoBinary.MULTICLASS:
+            if not isinstance(num_classes, int):
+                raise ValueError(f"`num_classes` is expected to be `int` but `{type(num_classes)} was passed.`")
+            return MulticlassExactMatch(num_classes, **kwargs)
+        if task == ClassificationTaskNoBinary.MULTILABEL:
+            if not isinstance(num_labels, int):
+                raise ValueError(f"`num_labels` is expected to be `int` but `{type(num_labels)} was passed.`")
+            return MultilabelExactMatch(num_labels, threshold, **kwargs)
+        raise ValueError(f"Task {task} not supported!")

@@ -1,0 +1,93 @@
+"""Jaccard index modules (API parity: reference ``classification/jaccard.py:32-335``)."""
+from typing import Any, Optional, Type
+
+from torch import Tensor
+from typing_extensions import Literal
+
+from torchmetrics_forked_amd.classification.base import _ClassificationTaskWrapper
+from torchmetrics_forked_amd.classification.confusion_matrix import (
+    BinaryConfusionMatrix,
+    MulticlassConfusionMatrix,
+    MultilabelConfusionMatrix,
+)
+from torchmetrics_forked_amd.classification.stat_scores import _task_factory
+from torchmetrics_forked_amd.functional.classification.jaccard import _check_avg, _jaccard_index_reduce
+from torchmetrics_forked_amd.metric import Metric
+from torchmetrics_forked_amd.utilities.plot import _AX_TYPE, _PLOT_OUT_TYPE
+
+
+class _JaccardMixin:
+    is_differentiable: bool = False
+    higher_is_better: bool = True
+    full_state_update: bool = False
+    plot_lower_bound: float = 0.0
+    plot_upper_bound: float = 1.0
+
+    def plot(self, val: Optional[Tensor] = None, ax: Optional[_AX_TYPE] = None) -> _PLOT_OUT_TYPE:  # type: ignore[override]
+        return self._plot(val, ax)  # type: ignore[attr-defined]
+
+
+class BinaryJaccardIndex(_JaccardMixin, BinaryConfusionMatrix):
+    def __init__(
+        self, threshold: float = 0.5, ignore_index: Optional[int] = None, validate_args: bool = True, **kwargs: Any
+    ) -> None:
+        super().__init__(threshold, ignore_index, normalize=None, validate_args=validate_args, **kwargs)
+
+    def compute(self) -> Tensor:
+        return _jaccard_index_reduce(self.confmat, average="binary")
+
+
+class MulticlassJaccardIndex(_JaccardMixin, MulticlassConfusionMatrix):
+    def __init__(
+        self,
+        num_classes: int,
+        average: Optional[Literal["micro", "macro", "weighted", "none"]] = "macro",
+        ignore_index: Optional[int] = None,
+        validate_args: bool = True,
+        **kwargs: Any,
+    ) -> None:
+        super().__init__(num_classes, ignore_index, normalize=None, validate_args=validate_args, **kwargs)
+        if validate_args:
+            _check_avg(average)
+        self.average = average
+
+    def compute(self) -> Tensor:
+        return _jaccard_index_reduce(self.confmat, average=self.average, ignore_index=self.ignore_index)
+
+
+class MultilabelJaccardIndex(_JaccardMixin, MultilabelConfusionMatrix):
+    def __init__(
+        self,
+        num_labels: int,
+        threshold: float = 0.5,
+        average: Optional[Literal["micro", "macro", "weighted", "none"]] = "macro",
+        ignore_index: Optional[int] = None,
+        validate_args: bool = True,
+        **kwargs: Any,
+    ) -> None:
+        super().__init__(num_labels, threshold, ignore_index, normalize=None, validate_args=validate_args, **kwargs)
+        if validate_args:
+            _check_avg(average)
+        self.average = average
+
+    def compute(self) -> Tensor:
+        return _jaccard_index_reduce(self.confmat, average=self.average, ignore_index=self.ignore_index)
+
+
+class JaccardIndex(_ClassificationTaskWrapper):
+    def __new__(  # type: ignore[misc]
+        cls: Type["JaccardIndex"],
+        task: Literal["binary", "multiclass", "multilabel"],
+        threshold: float = 0.5,
+        num_classes: Optional[int] = None,
+        num_labels: Optional[int] = None,
+        average: Optional[Literal["micro", "macro", "weighted", "none"]] = "macro",
+        ignore_index: Optional[int] = None,
+        validate_args: bool = True,
+        **kwargs: Any,
+    ) -> Metric:
+        kwargs.update({"ignore_index": ignore_index, "validate_args": validate_args})
+        return _task_factory(
+            task, BinaryJaccardIndex, MulticlassJaccardIndex, MultilabelJaccardIndex,
+            (threshold,), (num_classes, average), (num_labels, threshold, average), num_classes, num_labels, None, kwargs,
+        )

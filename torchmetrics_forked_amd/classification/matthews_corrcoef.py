@@ -1,0 +1,74 @@
+"""Matthews correlation modules (API parity: reference ``classification/matthews_corrcoef.py:31-345``)."""
+from typing import Any, Optional, Type
+
+from torch import Tensor
+from typing_extensions import Literal
+
+from torchmetrics_forked_amd.classification.base import _ClassificationTaskWrapper
+from torchmetrics_forked_amd.classification.confusion_matrix import (
+    BinaryConfusionMatrix,
+    MulticlassConfusionMatrix,
+    MultilabelConfusionMatrix,
+)
+from torchmetrics_forked_amd.classification.stat_scores import _task_factory
+from torchmetrics_forked_amd.functional.classification.matthews_corrcoef import _matthews_corrcoef_reduce
+from torchmetrics_forked_amd.metric import Metric
+from torchmetrics_forked_amd.utilities.plot import _AX_TYPE, _PLOT_OUT_TYPE
+
+
+class _MCCMixin:
+    is_differentiable: bool = False
+    higher_is_better: bool = True
+    full_state_update: bool = False
+    plot_lower_bound: float = -1.0
+    plot_upper_bound: float = 1.0
+
+    def compute(self) -> Tensor:
+        return _matthews_corrcoef_reduce(self.confmat)  # type: ignore[attr-defined]
+
+    def plot(self, val: Optional[Tensor] = None, ax: Optional[_AX_TYPE] = None) -> _PLOT_OUT_TYPE:  # type: ignore[override]
+        return self._plot(val, ax)  # type: ignore[attr-defined]
+
+
+class BinaryMatthewsCorrCoef(_MCCMixin, BinaryConfusionMatrix):
+    def __init__(
+        self, threshold: float = 0.5, ignore_index: Optional[int] = None, validate_args: bool = True, **kwargs: Any
+    ) -> None:
+        super().__init__(threshold, ignore_index, normalize=None, validate_args=validate_args, **kwargs)
+
+
+class MulticlassMatthewsCorrCoef(_MCCMixin, MulticlassConfusionMatrix):
+    def __init__(
+        self, num_classes: int, ignore_index: Optional[int] = None, validate_args: bool = True, **kwargs: Any
+    ) -> None:
+        super().__init__(num_classes, ignore_index, normalize=None, validate_args=validate_args, **kwargs)
+
+
+class MultilabelMatthewsCorrCoef(_MCCMixin, MultilabelConfusionMatrix):
+    def __init__(
+        self,
+        num_labels: int,
+        threshold: float = 0.5,
+        ignore_index: Optional[int] = None,
+        validate_args: bool = True,
+        **kwargs: Any,
+    ) -> None:
+        super().__init__(num_labels, threshold, ignore_index, normalize=None, validate_args=validate_args, **kwargs)
+
+
+class MatthewsCorrCoef(_ClassificationTaskWrapper):
+    def __new__(  # type: ignore[misc]
+        cls: Type["MatthewsCorrCoef"],
+        task: Literal["binary", "multiclass", "multilabel"],
+        threshold: float = 0.5,
+        num_classes: Optional[int] = None,
+        num_labels: Optional[int] = None,
+        ignore_index: Optional[int] = None,
+        validate_args: bool = True,
+        **kwargs: Any,
+    ) -> Metric:
+        kwargs.update({"ignore_index": ignore_index, "validate_args": validate_args})
+        return _task_factory(
+            task, BinaryMatthewsCorrCoef, MulticlassMatthewsCorrCoef, MultilabelMatthewsCorrCoef,
+            (threshold,), (num_classes,), (num_labels, threshold), num_classes, num_labels, None, kwargs,
+        )

@@ -1,0 +1,68 @@
+"""Multilabel ranking modules (API parity: reference ``classification/ranking.py:40-395``)."""
+from typing import Any, Callable, Optional
+
+import torch
+from torch import Tensor
+
+from torchmetrics_forked_amd.functional.classification.confusion_matrix import _multilabel_confusion_matrix_arg_validation
+from torchmetrics_forked_amd.functional.classification.ranking import (
+    _multilabel_coverage_error_update,
+    _multilabel_ranking_average_precision_update,
+    _multilabel_ranking_loss_update,
+    _multilabel_ranking_tensor_validation,
+    _ranking_format,
+    _ranking_reduce,
+)
+from torchmetrics_forked_amd.metric import Metric
+from torchmetrics_forked_amd.utilities.plot import _AX_TYPE, _PLOT_OUT_TYPE
+
+
+class _RankingBase(Metric):
+    is_differentiable: bool = False
+    full_state_update: bool = False
+    _update_fn: Callable
+    measure: Tensor
+    total: Tensor
+
+    def __init__(self, num_labels: int, ignore_index: Optional[int] = None, validate_args: bool = True, **kwargs: Any) -> None:
+        super().__init__(**kwargs)
+        if validate_args:
+            _multilabel_confusion_matrix_arg_validation(num_labels, threshold=0.0, ignore_index=ignore_index)
+        self.validate_args = validate_args
+        self.num_labels = num_labels
+        self.ignore_index = ignore_index
+        self.add_state("measure", torch.tensor(0.0), dist_reduce_fx="sum")
+        self.add_state("total", torch.tensor(0.0), dist_reduce_fx="sum")
+
+    def update(self, preds: Tensor, target: Tensor) -> None:
+        if self.validate_args:
+            _multilabel_ranking_tensor_validation(preds, target, self.num_labels, self.ignore_index)
+        preds, target = _ranking_format(preds, target, self.num_labels, self.ignore_index)
+        measure, n = type(self)._update_fn(preds, target)
+        self.measure += measure
+        self.total += n
+
+    def compute(self) -> Tensor:
+        return _ranking_reduce(self.measure, self.total)
+
+    def plot(self, val: Optional[Tensor] = None, ax: Optional[_AX_TYPE] = None) -> _PLOT_OUT_TYPE:
+        return self._plot(val, ax)
+
+
+class MultilabelCoverageError(_RankingBase):
+    higher_is_better: bool = False
+    plot_lower_bound: float = 0.0
+    _update_fn = staticmethod(_multilabel_coverage_error_update)
+
+
+class MultilabelRankingAveragePrecision(_RankingBase):
+    higher_is_better: bool = True
+    plot_lower_bound: float = 0.0
+    plot_upper_bound: float = 1.0
+    _update_fn = staticmethod(_multilabel_ranking_average_precision_update)
+
+
+class MultilabelRankingLoss(_RankingBase):
+    higher_is_better: bool = False
+    plot_lower_bound: float = 0.0
+    _update_fn = staticmethod(_multilabel_ranking_loss_update)

@@ -1,0 +1,172 @@
+"""Top-label calibration error (API parity: reference ``functional/classification/calibration_error.py:26-365``).
+
+MI355X design: instead of keeping every confidence/accuracy pair (reference: two ``cat`` lists, O(N) memory and an
+O(N) all-gather on sync), the state is a fixed ``[3, n_bins + 1]`` table of per-bin (count, sum confidence,
+sum accuracy) -- a ``sum`` state that syncs with one small all-reduce.  ECE / MCE / RMSCE only depend on these
+per-bin sums, so the result is identical up to float summation order.  Bin index = ``bucketize(conf, linspace(0, 1,
+n_bins + 1), right=True) - 1`` exactly as the reference (a confidence of exactly 1.0 lands in the extra last bin).
+"""
+from typing import Optional, Tuple, Union
+
+import torch
+from torch import Tensor
+from typing_extensions import Literal
+
+from torchmetrics_forked_amd.functional.classification._formats import binary_format, multiclass_format
+from torchmetrics_forked_amd.functional.classification.stat_scores import (
+    _binary_stat_scores_tensor_validation,
+    _multiclass_stat_scores_tensor_validation,
+)
+from torchmetrics_forked_amd.ops import classification as cls_ops
+from torchmetrics_forked_amd.utilities.enums import ClassificationTaskNoMultilabel
+
+_NORMS = ("l1", "l2", "max")
+
+
+def _bin_boundaries(n_bins: int, dtype: torch.dtype, device: torch.device) -> Tensor:
+    return torch.linspace(0, 1, n_bins + 1, dtype=dtype, device=device)
+
+
+def _ce_bin_update(confidences: Tensor, accuracies: Tensor, n_bins: int, bins: Optional[Tensor] = None) -> Tensor:
+    """Per-bin ``[3, n_bins + 1]`` (count, sum conf, sum acc) in float64 for one batch."""
+    confidences = confidences.reshape(-1)
+    accuracies = accuracies.reshape(-1).to(confidences.dtype)
+    boundaries = _bin_boundaries(n_bins, confidences.dtype, confidences.device)
+    idx = torch.bucketize(confidences, boundaries, right=True) - 1
+    out = torch.zeros(3, n_bins + 1, dtype=torch.float64, device=confidences.device) if bins is None else bins
+    vals = torch.stack([torch.ones_like(confidences), confidences, accuracies]).to(out.dtype)
+    out.index_add_(1, idx, vals)
+    return out
+
+
+def _ce_from_bins(bins: Tensor, norm: str = "l1", debias: bool = False, dtype: torch.dtype = torch.float32) -> Tensor:
+    if norm not in _NORMS:
+        raise ValueError(f"Argument `norm` is expected to be one of 'l1', 'l2', 'max' but got {norm}")
+    count, conf_sum, acc_sum = bins[0], bins[1], bins[2]
+    conf_bin = torch.nan_to_num(conf_sum / count)
+    acc_bin = torch.nan_to_num(acc_sum / count)
+    total = count.sum()
+    prop_bin = count / total
+    gap = acc_bin - conf_bin
+    if norm == "l1":
+        return torch.sum(gap.abs() * prop_bin).to(dtype)
+    if norm == "max":
+        return gap.abs().max().to(dtype)
+    ce = torch.sum(gap.pow(2) * prop_bin)
+    if debias:
+        debias_bins = (acc_bin * (acc_bin - 1) * prop_bin) / (prop_bin * total - 1)
+        ce = ce + torch.sum(torch.nan_to_num(debias_bins))
+    return torch.sqrt(ce).to(dtype) if ce > 0 else torch.tensor(0)
+
+
+def _ce_compute(
+    confidences: Tensor, accuracies: Tensor, bin_boundaries: Union[Tensor, int], norm: str = "l1", debias: bool = False
+) -> Tensor:
+    """Reference-compatible entry point (``calibration_error.py:62``); integer ``bin_boundaries`` only."""
+    if not isinstance(bin_boundaries, int):
+        bin_boundaries = len(bin_boundaries) - 1
+    if norm not in _NORMS:
+        raise ValueError(f"Argument `norm` is expected to be one of 'l1', 'l2', 'max' but got {norm}")
+    with torch.no_grad():
+        bins = _ce_bin_update(confidences, accuracies, bin_boundaries)
+    return _ce_from_bins(bins, norm, debias, confidences.dtype)
+
+
+def _binary_calibration_error_arg_validation(n_bins: int, norm: str = "l1", ignore_index: Optional[int] = None) -> None:
+    if not isinstance(n_bins, int) or n_bins < 1:
+        raise ValueError(f"Expected argument `n_bins` to be an integer larger than 0, but got {n_bins}")
+    if norm not in _NORMS:
+        raise ValueError(f"Expected argument `norm` to be one of {_NORMS}, but got {norm}.")
+    if ignore_index is not None and not isinstance(ignore_index, int):
+        raise ValueError(f"Expected argument `ignore_index` to either be `None` or an integer, but got {ignore_index}")
+
+
+def _binary_calibration_error_tensor_validation(preds: Tensor, target: Tensor, ignore_index: Optional[int] = None) -> None:
+    _binary_stat_scores_tensor_validation(preds, target, "global", ignore_index)
+    if not preds.is_floating_point():
+        raise ValueError(
+            "Expected argument `preds` to be floating tensor with probabilities/logits"
+            f" but got tensor with dtype {preds.dtype}"
+        )
+
+
+def _binary_calibration_error_update(preds: Tensor, target: Tensor) -> Tuple[Tensor, Tensor]:
+    return preds, target
+
+
+def binary_calibration_error(
+    preds: Tensor,
+    target: Tensor,
+    n_bins: int = 15,
+    norm: Literal["l1", "l2", "max"] = "l1",
+    ignore_index: Optional[int] = None,
+    validate_args: bool = True,
+) -> Tensor:
+    if validate_args:
+        _binary_calibration_error_arg_validation(n_bins, norm, ignore_index)
+        _binary_calibration_error_tensor_validation(preds, target, ignore_index)
+    preds, target = binary_format(preds, target, 0.0, ignore_index, convert_to_labels=False)
+    return _ce_from_bins(_ce_bin_update(preds, target, n_bins), norm, dtype=preds.dtype)
+
+
+def _multiclass_calibration_error_arg_validation(
+    num_classes: int, n_bins: int, norm: str = "l1", ignore_index: Optional[int] = None
+) -> None:
+    if not isinstance(num_classes, int) or num_classes < 2:
+        raise ValueError(f"Expected argument `num_classes` to be an integer larger than 1, but got {num_classes}")
+    _binary_calibration_error_arg_validation(n_bins, norm, ignore_index)
+
+
+def _multiclass_calibration_error_tensor_validation(
+    preds: Tensor, target: Tensor, num_classes: int, ignore_index: Optional[int] = None
+) -> None:
+    _multiclass_stat_scores_tensor_validation(preds, target, num_classes, "global", ignore_index)
+    if not preds.is_floating_point():
+        raise ValueError(
+            "Expected argument `preds` to be floating tensor with probabilities/logits"
+            f" but got tensor with dtype {preds.dtype}"
+        )
+
+
+def _multiclass_calibration_error_update(preds: Tensor, target: Tensor) -> Tuple[Tensor, Tensor]:
+    """Top-1 confidence + correctness; softmax decided on device (no host sync)."""
+    flag = cls_ops.range_flag(preds).bool()
+    preds = torch.where(flag, preds.softmax(1), preds)
+    confidences, predictions = preds.max(dim=1)
+    return confidences.float(), predictions.eq(target).float()
+
+
+def multiclass_calibration_error(
+    preds: Tensor,
+    target: Tensor,
+    num_classes: int,
+    n_bins: int = 15,
+    norm: Literal["l1", "l2", "max"] = "l1",
+    ignore_index: Optional[int] = None,
+    validate_args: bool = True,
+) -> Tensor:
+    if validate_args:
+        _multiclass_calibration_error_arg_validation(num_classes, n_bins, norm, ignore_index)
+        _multiclass_calibration_error_tensor_validation(preds, target, num_classes, ignore_index)
+    preds, target = multiclass_format(preds, target, ignore_index, convert_to_labels=False)
+    conf, acc = _multiclass_calibration_error_update(preds, target)
+    return _ce_from_bins(_ce_bin_update(conf, acc, n_bins), norm, dtype=conf.dtype)
+
+
+def calibration_error(
+    preds: Tensor,
+    target: Tensor,
+    task: Literal["binary", "multiclass"],
+    n_bins: int = 15,
+    norm: Literal["l1", "l2", "max"] = "l1",
+    num_classes: Optional[int] = None,
+    ignore_index: Optional[int] = None,
+    validate_args: bool = True,
+) -> Tensor:
+    task = ClassificationTaskNoMultilabel.from_str(task)
+    assert norm is not None  # noqa: S101
+    if task == ClassificationTaskNoMultilabel.BINARY:
+        return binary_calibration_error(preds, target, n_bins, norm, ignore_index, validate_args)
+    if not isinstance(num_classes, int):
+        raise ValueError(f"`num_classes` is expected to be `int` but `{type(num_classes)} was passed.`")
+    return multiclass_calibration_error(preds, target, num_classes, n_bins, norm, ignore_index, validate_args)

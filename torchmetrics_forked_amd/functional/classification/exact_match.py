@@ -1,0 +1,93 @@
+"""Exact match (API parity: reference ``functional/classification/exact_match.py``)."""
+from typing import Optional, Tuple
+
+import torch
+from torch import Tensor
+from typing_extensions import Literal
+
+from torchmetrics_forked_amd.functional.classification.stat_scores import (
+    _multiclass_stat_scores_arg_validation,
+    _multiclass_stat_scores_format,
+    _multiclass_stat_scores_tensor_validation,
+    _multilabel_stat_scores_arg_validation,
+    _multilabel_stat_scores_format,
+    _multilabel_stat_scores_tensor_validation,
+)
+from torchmetrics_forked_amd.utilities.compute import _safe_divide
+from torchmetrics_forked_amd.utilities.enums import ClassificationTaskNoBinary
+
+
+def _exact_match_reduce(correct: Tensor, total: Tensor) -> Tensor:
+    return _safe_divide(correct, total)
+
+
+def _multiclass_exact_match_update(
+    preds: Tensor, target: Tensor, multidim_average: str = "global", ignore_index: Optional[int] = None
+) -> Tuple[Tensor, Tensor]:
+    if ignore_index is not None:
+        preds = torch.where(target == ignore_index, torch.full_like(preds, ignore_index), preds)
+    correct = (preds == target).sum(1) == preds.shape[1]
+    correct = correct if multidim_average == "samplewise" else correct.sum()
+    total = torch.tensor(preds.shape[0] if multidim_average == "global" else 1, device=correct.device)
+    return correct, total
+
+
+def multiclass_exact_match(
+    preds: Tensor,
+    target: Tensor,
+    num_classes: int,
+    multidim_average: Literal["global", "samplewise"] = "global",
+    ignore_index: Optional[int] = None,
+    validate_args: bool = True,
+) -> Tensor:
+    if validate_args:
+        _multiclass_stat_scores_arg_validation(num_classes, 1, None, multidim_average, ignore_index)
+        _multiclass_stat_scores_tensor_validation(preds, target, num_classes, multidim_average, ignore_index)
+    preds, target = _multiclass_stat_scores_format(preds, target, 1)
+    return _exact_match_reduce(*_multiclass_exact_match_update(preds, target, multidim_average, ignore_index))
+
+
+def _multilabel_exact_match_update(
+    preds: Tensor, target: Tensor, num_labels: int, multidim_average: str = "global"
+) -> Tuple[Tensor, Tensor]:
+    if multidim_average == "global":
+        preds = torch.movedim(preds, 1, -1).reshape(-1, num_labels)
+        target = torch.movedim(target, 1, -1).reshape(-1, num_labels)
+    correct = ((preds == target).sum(1) == num_labels).sum(dim=-1)
+    total = torch.tensor(preds.shape[0 if multidim_average == "global" else 2], device=correct.device)
+    return correct, total
+
+
+def multilabel_exact_match(
+    preds: Tensor,
+    target: Tensor,
+    num_labels: int,
+    threshold: float = 0.5,
+    multidim_average: Literal["global", "samplewise"] = "global",
+    ignore_index: Optional[int] = None,
+    validate_args: bool = True,
+) -> Tensor:
+    if validate_args:
+        _multilabel_stat_scores_arg_validation(num_labels, threshold, None, multidim_average, ignore_index)
+        _multilabel_stat_scores_tensor_validation(preds, target, num_labels, multidim_average, ignore_index)
+    preds, target = _multilabel_stat_scores_format(preds, target, num_labels, threshold, ignore_index)
+    return _exact_match_reduce(*_multilabel_exact_match_update(preds, target, num_labels, multidim_average))
+
+
+def exact_match(
+    preds: Tensor,
+    target: Tensor,
+    task: Literal["multiclass", "multilabel"],
+    num_classes: Optional[int] = None,
+    num_labels: Optional[int] = None,
+    threshold: float = 0.5,
+    multidim_average: Literal["global", "samplewise"] = "global",
+    ignore_index: Optional[int] = None,
+    validate_args: bool = True,
+) -> Tensor:
+    task = ClassificationTaskNoBinary.from_str(task)
+    if task == ClassificationTaskNoBinary.MULTICLASS:
+        assert num_classes is not None  # noqa: S101
+        return multiclass_exact_match(preds, target, num_classes, multidim_average, ignore_index, validate_args)
+    assert num_labels is not None  # noqa: S101
+    return multilabel_exact_match(preds, target, num_labels, threshold, multidim_average, ignore_index, validate_args)
