@@ -1,0 +1,207 @@
+"""Sum-state error metrics (API parity: reference ``regression/{mse,mae,mape,symmetric_mape,wmape,log_mse,log_cosh,
+minkowski,tweedie_deviance}.py``).  Every update is one fused HIP map-reduce pass on the GPU."""
+from typing import Any
+
+import torch
+from torch import Tensor, tensor
+
+from torchmetrics_forked_amd.functional.regression.log_cosh import _log_cosh_error_compute, _log_cosh_error_update
+from torchmetrics_forked_amd.functional.regression.log_mse import (
+    _mean_squared_log_error_compute,
+    _mean_squared_log_error_update,
+)
+from torchmetrics_forked_amd.functional.regression.mae import _mean_absolute_error_compute, _mean_absolute_error_update
+from torchmetrics_forked_amd.functional.regression.mape import (
+    _mean_absolute_percentage_error_compute,
+    _mean_absolute_percentage_error_update,
+)
+from torchmetrics_forked_amd.functional.regression.minkowski import _minkowski_distance_compute, _minkowski_distance_update
+from torchmetrics_forked_amd.functional.regression.mse import _mean_squared_error_compute, _mean_squared_error_update
+from torchmetrics_forked_amd.functional.regression.symmetric_mape import (
+    _symmetric_mean_absolute_percentage_error_compute,
+    _symmetric_mean_absolute_percentage_error_update,
+)
+from torchmetrics_forked_amd.functional.regression.tweedie_deviance import (
+    _tweedie_deviance_score_compute,
+    _tweedie_deviance_score_update,
+)
+from torchmetrics_forked_amd.functional.regression.wmape import (
+    _weighted_mean_absolute_percentage_error_compute,
+    _weighted_mean_absolute_percentage_error_update,
+)
+from torchmetrics_forked_amd.regression._base import _RegressionMetric
+from torchmetrics_forked_amd.utilities.exceptions import TorchMetricsUserError
+
+
+class MeanSquaredError(_RegressionMetric):
+    higher_is_better = False
+    plot_lower_bound: float = 0.0
+
+    def __init__(self, squared: bool = True, num_outputs: int = 1, **kwargs: Any) -> None:
+        super().__init__(**kwargs)
+        if not isinstance(squared, bool):
+            raise ValueError(f"Expected argument `squared` to be a boolean but got {squared}")
+        self.squared = squared
+        if not (isinstance(num_outputs, int) and num_outputs > 0):
+            raise ValueError(f"Expected num_outputs to be a positive integer but got {num_outputs}")
+        self.num_outputs = num_outputs
+        self.add_state("sum_squared_error", default=torch.zeros(num_outputs), dist_reduce_fx="sum")
+        self.add_state("total", default=tensor(0), dist_reduce_fx="sum")
+
+    def update(self, preds: Tensor, target: Tensor) -> None:
+        sse, n = _mean_squared_error_update(preds, target, num_outputs=self.num_outputs)
+        self.sum_squared_error += sse
+        self.total += n
+
+    def compute(self) -> Tensor:
+        return _mean_squared_error_compute(self.sum_squared_error, self.total, squared=self.squared)
+
+
+class MeanAbsoluteError(_RegressionMetric):
+    higher_is_better = False
+    plot_lower_bound: float = 0.0
+
+    def __init__(self, **kwargs: Any) -> None:
+        super().__init__(**kwargs)
+        self.add_state("sum_abs_error", default=tensor(0.0), dist_reduce_fx="sum")
+        self.add_state("total", default=tensor(0), dist_reduce_fx="sum")
+
+    def update(self, preds: Tensor, target: Tensor) -> None:
+        s, n = _mean_absolute_error_update(preds, target)
+        self.sum_abs_error += s
+        self.total += n
+
+    def compute(self) -> Tensor:
+        return _mean_absolute_error_compute(self.sum_abs_error, self.total)
+
+
+class MeanAbsolutePercentageError(_RegressionMetric):
+    higher_is_better = False
+    plot_lower_bound: float = 0.0
+
+    def __init__(self, **kwargs: Any) -> None:
+        super().__init__(**kwargs)
+        self.add_state("sum_abs_per_error", default=tensor(0.0), dist_reduce_fx="sum")
+        self.add_state("total", default=tensor(0.0), dist_reduce_fx="sum")
+
+    def update(self, preds: Tensor, target: Tensor) -> None:
+        s, n = _mean_absolute_percentage_error_update(preds, target)
+        self.sum_abs_per_error += s
+        self.total += n
+
+    def compute(self) -> Tensor:
+        return _mean_absolute_percentage_error_compute(self.sum_abs_per_error, self.total)
+
+
+class SymmetricMeanAbsolutePercentageError(_RegressionMetric):
+    higher_is_better = False
+    plot_lower_bound: float = 0.0
+    plot_upper_bound: float = 2.0
+
+    def __init__(self, **kwargs: Any) -> None:
+        super().__init__(**kwargs)
+        self.add_state("sum_abs_per_error", default=tensor(0.0), dist_reduce_fx="sum")
+        self.add_state("total", default=tensor(0.0), dist_reduce_fx="sum")
+
+    def update(self, preds: Tensor, target: Tensor) -> None:
+        s, n = _symmetric_mean_absolute_percentage_error_update(preds, target)
+        self.sum_abs_per_error += s
+        self.total += n
+
+    def compute(self) -> Tensor:
+        return _symmetric_mean_absolute_percentage_error_compute(self.sum_abs_per_error, self.total)
+
+
+class WeightedMeanAbsolutePercentageError(_RegressionMetric):
+    higher_is_better = False
+    plot_lower_bound: float = 0.0
+
+    def __init__(self, **kwargs: Any) -> None:
+        super().__init__(**kwargs)
+        self.add_state("sum_abs_error", default=torch.tensor(0.0), dist_reduce_fx="sum")
+        self.add_state("sum_scale", default=torch.tensor(0.0), dist_reduce_fx="sum")
+
+    def update(self, preds: Tensor, target: Tensor) -> None:
+        e, s = _weighted_mean_absolute_percentage_error_update(preds, target)
+        self.sum_abs_error += e
+        self.sum_scale += s
+
+    def compute(self) -> Tensor:
+        return _weighted_mean_absolute_percentage_error_compute(self.sum_abs_error, self.sum_scale)
+
+
+class MeanSquaredLogError(_RegressionMetric):
+    higher_is_better = False
+    plot_lower_bound: float = 0.0
+
+    def __init__(self, **kwargs: Any) -> None:
+        super().__init__(**kwargs)
+        self.add_state("sum_squared_log_error", default=tensor(0.0), dist_reduce_fx="sum")
+        self.add_state("total", default=tensor(0), dist_reduce_fx="sum")
+
+    def update(self, preds: Tensor, target: Tensor) -> None:
+        s, n = _mean_squared_log_error_update(preds, target)
+        self.sum_squared_log_error += s
+        self.total += n
+
+    def compute(self) -> Tensor:
+        return _mean_squared_log_error_compute(self.sum_squared_log_error, self.total)
+
+
+class LogCoshError(_RegressionMetric):
+    higher_is_better = False
+    plot_lower_bound: float = 0.0
+
+    def __init__(self, num_outputs: int = 1, **kwargs: Any) -> None:
+        super().__init__(**kwargs)
+        if not isinstance(num_outputs, int) and num_outputs < 1:
+            raise ValueError(f"Expected argument `num_outputs` to be an int larger than 0, but got {num_outputs}")
+        self.num_outputs = num_outputs
+        self.add_state("sum_log_cosh_error", default=torch.zeros(num_outputs), dist_reduce_fx="sum")
+        self.add_state("total", default=torch.tensor(0), dist_reduce_fx="sum")
+
+    def update(self, preds: Tensor, target: Tensor) -> None:
+        s, n = _log_cosh_error_update(preds, target, self.num_outputs)
+        self.sum_log_cosh_error += s
+        self.total += n
+
+    def compute(self) -> Tensor:
+        return _log_cosh_error_compute(self.sum_log_cosh_error, self.total)
+
+
+class MinkowskiDistance(_RegressionMetric):
+    higher_is_better = False
+    plot_lower_bound: float = 0.0
+
+    def __init__(self, p: float, **kwargs: Any) -> None:
+        super().__init__(**kwargs)
+        if not (isinstance(p, (float, int)) and p >= 1):
+            raise TorchMetricsUserError(f"Argument ``p`` must be a float or int greater than 1, but got {p}")
+        self.p = p
+        self.add_state("minkowski_dist_sum", default=tensor(0.0), dist_reduce_fx="sum")
+
+    def update(self, preds: Tensor, targets: Tensor) -> None:
+        self.minkowski_dist_sum += _minkowski_distance_update(preds, targets, self.p)
+
+    def compute(self) -> Tensor:
+        return _minkowski_distance_compute(self.minkowski_dist_sum, self.p)
+
+
+class TweedieDevianceScore(_RegressionMetric):
+    higher_is_better = None
+
+    def __init__(self, power: float = 0.0, **kwargs: Any) -> None:
+        super().__init__(**kwargs)
+        if 0 < power < 1:
+            raise ValueError(f"Deviance Score is not defined for power={power}.")
+        self.power: float = power
+        self.add_state("sum_deviance_score", torch.tensor(0.0), dist_reduce_fx="sum")
+        self.add_state("num_observations", torch.tensor(0), dist_reduce_fx="sum")
+
+    def update(self, preds: Tensor, targets: Tensor) -> None:
+        s, n = _tweedie_deviance_score_update(preds, targets, self.power)
+        self.sum_deviance_score += s
+        self.num_observations += n
+
+    def compute(self) -> Tensor:
+        return _tweedie_deviance_score_compute(self.sum_deviance_score, self.num_observations)

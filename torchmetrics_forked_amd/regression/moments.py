@@ -1,0 +1,161 @@
+"""Moment-based regression metrics (API parity: reference ``regression/{r2,rse,explained_variance,pearson,
+concordance}.py``)."""
+from typing import Any, List, Sequence, Tuple, Union
+
+import torch
+from torch import Tensor, tensor
+from typing_extensions import Literal
+
+from torchmetrics_forked_amd.functional.regression.concordance import _concordance_corrcoef_compute
+from torchmetrics_forked_amd.functional.regression.explained_variance import (
+    ALLOWED_MULTIOUTPUT,
+    _explained_variance_compute,
+    _explained_variance_update,
+)
+from torchmetrics_forked_amd.functional.regression.pearson import _pearson_corrcoef_compute, _pearson_corrcoef_update
+from torchmetrics_forked_amd.functional.regression.r2 import _r2_score_compute, _r2_score_update
+from torchmetrics_forked_amd.functional.regression.rse import _relative_squared_error_compute
+from torchmetrics_forked_amd.regression._base import _RegressionMetric
+
+
+class R2Score(_RegressionMetric):
+    higher_is_better = True
+    plot_upper_bound: float = 1.0
+
+    def __init__(self, num_outputs: int = 1, adjusted: int = 0, multioutput: str = "uniform_average", **kwargs: Any) -> None:
+        super().__init__(**kwargs)
+        self.num_outputs = num_outputs
+        if adjusted < 0 or not isinstance(adjusted, int):
+            raise ValueError("`adjusted` parameter should be an integer larger or equal to 0.")
+        self.adjusted = adjusted
+        allowed = ("raw_values", "uniform_average", "variance_weighted")
+        if multioutput not in allowed:
+            raise ValueError(f"Invalid input to argument `multioutput`. Choose one of the following: {allowed}")
+        self.multioutput = multioutput
+        self.add_state("sum_squared_error", default=torch.zeros(self.num_outputs), dist_reduce_fx="sum")
+        self.add_state("sum_error", default=torch.zeros(self.num_outputs), dist_reduce_fx="sum")
+        self.add_state("residual", default=torch.zeros(self.num_outputs), dist_reduce_fx="sum")
+        self.add_state("total", default=tensor(0), dist_reduce_fx="sum")
+
+    def update(self, preds: Tensor, target: Tensor) -> None:
+        sso, so, rss, n = _r2_score_update(preds, target)
+        self.sum_squared_error += sso
+        self.sum_error += so
+        self.residual += rss
+        self.total += n
+
+    def compute(self) -> Tensor:
+        return _r2_score_compute(self.sum_squared_error, self.sum_error, self.residual, self.total, self.adjusted, self.multioutput)
+
+
+class RelativeSquaredError(_RegressionMetric):
+    higher_is_better = False
+
+    def __init__(self, num_outputs: int = 1, squared: bool = True, **kwargs: Any) -> None:
+        super().__init__(**kwargs)
+        self.num_outputs = num_outputs
+        self.add_state("sum_squared_error", default=torch.zeros(self.num_outputs), dist_reduce_fx="sum")
+        self.add_state("sum_error", default=torch.zeros(self.num_outputs), dist_reduce_fx="sum")
+        self.add_state("residual", default=torch.zeros(self.num_outputs), dist_reduce_fx="sum")
+        self.add_state("total", default=tensor(0), dist_reduce_fx="sum")
+        self.squared = squared
+
+    def update(self, preds: Tensor, target: Tensor) -> None:
+        sso, so, rss, n = _r2_score_update(preds, target)
+        self.sum_squared_error += sso
+        self.sum_error += so
+        self.residual += rss
+        self.total += n
+
+    def compute(self) -> Tensor:
+        return _relative_squared_error_compute(self.sum_squared_error, self.sum_error, self.residual, self.total, squared=self.squared)
+
+
+class ExplainedVariance(_RegressionMetric):
+    higher_is_better = True
+    plot_upper_bound: float = 1.0
+
+    def __init__(
+        self, multioutput: Literal["raw_values", "uniform_average", "variance_weighted"] = "uniform_average", **kwargs: Any
+    ) -> None:
+        super().__init__(**kwargs)
+        if multioutput not in ALLOWED_MULTIOUTPUT:
+            raise ValueError(f"Invalid input to argument `multioutput`. Choose one of the following: {ALLOWED_MULTIOUTPUT}")
+        self.multioutput = multioutput
+        self.add_state("sum_error", default=tensor(0.0), dist_reduce_fx="sum")
+        self.add_state("sum_squared_error", default=tensor(0.0), dist_reduce_fx="sum")
+        self.add_state("sum_target", default=tensor(0.0), dist_reduce_fx="sum")
+        self.add_state("sum_squared_target", default=tensor(0.0), dist_reduce_fx="sum")
+        self.add_state("num_obs", default=tensor(0.0), dist_reduce_fx="sum")
+
+    def update(self, preds: Tensor, target: Tensor) -> None:
+        n, se, sse, st, sst = _explained_variance_update(preds, target)
+        self.num_obs = self.num_obs + n
+        self.sum_error = self.sum_error + se
+        self.sum_squared_error = self.sum_squared_error + sse
+        self.sum_target = self.sum_target + st
+        self.sum_squared_target = self.sum_squared_target + sst
+
+    def compute(self) -> Union[Tensor, Sequence[Tensor]]:
+        return _explained_variance_compute(
+            self.num_obs, self.sum_error, self.sum_squared_error, self.sum_target, self.sum_squared_target, self.multioutput
+        )
+
+
+def _final_aggregation(
+    means_x: Tensor, means_y: Tensor, vars_x: Tensor, vars_y: Tensor, corrs_xy: Tensor, nbs: Tensor
+) -> Tuple[Tensor, Tensor, Tensor, Tensor, Tensor, Tensor]:
+    """Fold per-rank streaming states (stacked on dim 0 by the ``None``-reduced gather) with the parallel merge
+    (reference ``regression/pearson.py:28-70``; same algebra, written as the Chan et al. pairwise update)."""
+    mx, my, vx, vy, cxy, n = means_x[0], means_y[0], vars_x[0], vars_y[0], corrs_xy[0], nbs[0]
+    for i in range(1, len(means_x)):
+        mx2, my2, vx2, vy2, cxy2, n2 = means_x[i], means_y[i], vars_x[i], vars_y[i], corrs_xy[i], nbs[i]
+        nb = n + n2
+        w = n * n2 / nb
+        dx, dy = mx2 - mx, my2 - my
+        vx = vx + vx2 + w * dx * dx
+        vy = vy + vy2 + w * dy * dy
+        cxy = cxy + cxy2 + w * dx * dy
+        mx = (n * mx + n2 * mx2) / nb
+        my = (n * my + n2 * my2) / nb
+        n = nb
+    return mx, my, vx, vy, cxy, n
+
+
+class PearsonCorrCoef(_RegressionMetric):
+    """Streaming Pearson correlation.  States are per-rank Welford moments with ``dist_reduce_fx=None``: the sync
+    engine gathers all six in one packed collective and ``compute`` folds them with ``_final_aggregation``."""
+
+    higher_is_better = None
+    full_state_update: bool = True
+    plot_lower_bound: float = -1.0
+    plot_upper_bound: float = 1.0
+
+    def __init__(self, num_outputs: int = 1, **kwargs: Any) -> None:
+        super().__init__(**kwargs)
+        if not isinstance(num_outputs, int) and num_outputs < 1:
+            raise ValueError("Expected argument `num_outputs` to be an int larger than 0, but got {num_outputs}")
+        self.num_outputs = num_outputs
+        for s in ("mean_x", "mean_y", "var_x", "var_y", "corr_xy", "n_total"):
+            self.add_state(s, default=torch.zeros(self.num_outputs), dist_reduce_fx=None)
+
+    def update(self, preds: Tensor, target: Tensor) -> None:
+        self.mean_x, self.mean_y, self.var_x, self.var_y, self.corr_xy, self.n_total = _pearson_corrcoef_update(
+            preds, target, self.mean_x, self.mean_y, self.var_x, self.var_y, self.corr_xy, self.n_total, self.num_outputs
+        )
+
+    def _aggregated(self) -> Tuple[Tensor, ...]:
+        if (self.num_outputs == 1 and self.mean_x.numel() > 1) or (self.num_outputs > 1 and self.mean_x.ndim > 1):
+            return _final_aggregation(self.mean_x, self.mean_y, self.var_x, self.var_y, self.corr_xy, self.n_total)
+        return self.mean_x, self.mean_y, self.var_x, self.var_y, self.corr_xy, self.n_total
+
+    def compute(self) -> Tensor:
+        _, _, vx, vy, cxy, n = self._aggregated()
+        return _pearson_corrcoef_compute(vx, vy, cxy, n)
+
+
+class ConcordanceCorrCoef(PearsonCorrCoef):
+    higher_is_better = True
+
+    def compute(self) -> Tensor:
+        return _concordance_corrcoef_compute(*self._aggregated())

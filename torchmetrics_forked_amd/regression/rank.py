@@ -1,0 +1,138 @@
+"""Sample-state regression metrics (API parity: reference ``regression/{spearman,kendall,cosine_similarity,
+kl_divergence}.py``)."""
+from typing import Any, List, Optional, Tuple, Union
+
+import torch
+from torch import Tensor
+from typing_extensions import Literal
+
+from torchmetrics_forked_amd.functional.regression.cosine_similarity import (
+    _cosine_similarity_compute,
+    _cosine_similarity_update,
+)
+from torchmetrics_forked_amd.functional.regression.kendall import (
+    _kendall_corrcoef_compute,
+    _kendall_corrcoef_update,
+    _MetricVariant,
+    _TestAlternative,
+)
+from torchmetrics_forked_amd.functional.regression.kl_divergence import _kld_compute, _kld_update
+from torchmetrics_forked_amd.functional.regression.spearman import _spearman_corrcoef_compute, _spearman_corrcoef_update
+from torchmetrics_forked_amd.regression._base import _RegressionMetric
+from torchmetrics_forked_amd.utilities.data import dim_zero_cat
+from torchmetrics_forked_amd.utilities.prints import rank_zero_warn
+
+
+class SpearmanCorrCoef(_RegressionMetric):
+    is_differentiable = False
+    higher_is_better = True
+    plot_lower_bound: float = -1.0
+    plot_upper_bound: float = 1.0
+
+    def __init__(self, num_outputs: int = 1, **kwargs: Any) -> None:
+        super().__init__(**kwargs)
+        rank_zero_warn(
+            "Metric `SpearmanCorrcoef` will save all targets and predictions in the buffer."
+            " For large datasets, this may lead to large memory footprint."
+        )
+        if not isinstance(num_outputs, int) and num_outputs < 1:
+            raise ValueError("Expected argument `num_outputs` to be an int larger than 0, but got {num_outputs}")
+        self.num_outputs = num_outputs
+        self.add_state("preds", default=[], dist_reduce_fx="cat")
+        self.add_state("target", default=[], dist_reduce_fx="cat")
+
+    def update(self, preds: Tensor, target: Tensor) -> None:
+        preds, target = _spearman_corrcoef_update(preds, target, num_outputs=self.num_outputs)
+        self.preds.append(preds)
+        self.target.append(target)
+
+    def compute(self) -> Tensor:
+        return _spearman_corrcoef_compute(dim_zero_cat(self.preds), dim_zero_cat(self.target))
+
+
+class KendallRankCorrCoef(_RegressionMetric):
+    is_differentiable = False
+    higher_is_better = None
+    full_state_update = True
+    plot_lower_bound: float = -1.0
+    plot_upper_bound: float = 1.0
+
+    def __init__(
+        self,
+        variant: Literal["a", "b", "c"] = "b",
+        t_test: bool = False,
+        alternative: Optional[Literal["two-sided", "less", "greater"]] = "two-sided",
+        num_outputs: int = 1,
+        **kwargs: Any,
+    ) -> None:
+        super().__init__(**kwargs)
+        if not isinstance(t_test, bool):
+            raise ValueError(f"Argument `t_test` is expected to be of a type `bool`, but got {type(t_test)}.")
+        if t_test and alternative is None:
+            raise ValueError("Argument `alternative` is required if `t_test=True` but got `None`.")
+        self.variant = _MetricVariant.from_str(str(variant))
+        self.alternative = _TestAlternative.from_str(str(alternative)) if t_test else None
+        self.num_outputs = num_outputs
+        self.add_state("preds", [], dist_reduce_fx="cat")
+        self.add_state("target", [], dist_reduce_fx="cat")
+
+    def update(self, preds: Tensor, target: Tensor) -> None:
+        self.preds, self.target = _kendall_corrcoef_update(preds, target, self.preds, self.target, num_outputs=self.num_outputs)
+
+    def compute(self) -> Union[Tensor, Tuple[Tensor, Tensor]]:
+        tau, p_value = _kendall_corrcoef_compute(dim_zero_cat(self.preds), dim_zero_cat(self.target), self.variant, self.alternative)
+        return (tau, p_value) if p_value is not None else tau
+
+
+class CosineSimilarity(_RegressionMetric):
+    higher_is_better = True
+    plot_lower_bound: float = 0.0
+
+    def __init__(self, reduction: Literal["mean", "sum", "none", None] = "sum", **kwargs: Any) -> None:
+        super().__init__(**kwargs)
+        allowed = ("sum", "mean", "none", None)
+        if reduction not in allowed:
+            raise ValueError(f"Expected argument `reduction` to be one of {allowed} but got {reduction}")
+        self.reduction = reduction
+        self.add_state("preds", [], dist_reduce_fx="cat")
+        self.add_state("target", [], dist_reduce_fx="cat")
+
+    def update(self, preds: Tensor, target: Tensor) -> None:
+        preds, target = _cosine_similarity_update(preds, target)
+        self.preds.append(preds)
+        self.target.append(target)
+
+    def compute(self) -> Tensor:
+        return _cosine_similarity_compute(dim_zero_cat(self.preds), dim_zero_cat(self.target), self.reduction)
+
+
+class KLDivergence(_RegressionMetric):
+    higher_is_better = False
+    plot_lower_bound: float = 0.0
+
+    def __init__(self, log_prob: bool = False, reduction: Literal["mean", "sum", "none", None] = "mean", **kwargs: Any) -> None:
+        super().__init__(**kwargs)
+        if not isinstance(log_prob, bool):
+            raise TypeError(f"Expected argument `log_prob` to be bool but got {log_prob}")
+        self.log_prob = log_prob
+        allowed = ["mean", "sum", "none", None]
+        if reduction not in allowed:
+            raise ValueError(f"Expected argument `reduction` to be one of {allowed} but got {reduction}")
+        self.reduction = reduction
+        if self.reduction in ("mean", "sum"):
+            self.add_state("measures", torch.tensor(0.0), dist_reduce_fx="sum")
+        else:
+            self.add_state("measures", [], dist_reduce_fx="cat")
+        self.add_state("total", torch.tensor(0), dist_reduce_fx="sum")
+
+    def update(self, p: Tensor, q: Tensor) -> None:
+        measures, total = _kld_update(p, q, self.log_prob)
+        if self.reduction is None or self.reduction == "none":
+            self.measures.append(measures)
+        else:
+            self.measures += measures.sum()
+            self.total += total
+
+    def compute(self) -> Tensor:
+        measures = dim_zero_cat(self.measures) if self.reduction in ("none", None) else self.measures
+        return _kld_compute(measures, self.total, self.reduction)
