@@ -6,7 +6,7 @@
 #include <hip/hip_fp16.h>
 #include <ATen/ATen.h>
 #include <c10/hip/HIPStream.h>
-#include <c10/hip/HIPGuard.h>
+#include <c10/core/DeviceGuard.h>
 #include <torch/library.h>
 
 #include <cstdint>

@@ -159,7 +159,7 @@ at::Tensor regression_sums(const at::Tensor& preds_in, const at::Tensor& target_
   TORCH_CHECK(preds_in.dim() == 2, "regression_sums: expected [N, D] inputs");
   TORCH_CHECK(preds_in.scalar_type() == target_in.scalar_type(), "regression_sums: dtype mismatch");
   TORCH_CHECK(op >= 0 && op <= kOpTweedie, "regression_sums: unknown op ", op);
-  const c10::hip::HIPGuard guard(preds_in.device());
+  const at::DeviceGuard guard(preds_in.device());
   auto preds = preds_in.contiguous();
   auto target = target_in.contiguous();
   const int64_t N = preds.size(0);

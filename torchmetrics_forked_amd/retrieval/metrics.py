@@ -1,0 +1,109 @@
+"""Retrieval metrics (API parity: reference ``retrieval/{average_precision,reciprocal_rank,precision,recall,
+fall_out,hit_rate,r_precision,ndcg}.py``)."""
+from typing import Any, Optional
+
+from torch import Tensor
+
+from torchmetrics_forked_amd.functional.retrieval import _grouped as G
+from torchmetrics_forked_amd.retrieval.base import RetrievalMetric
+
+
+def _check_top_k(top_k: Optional[int]) -> None:
+    if top_k is not None and not (isinstance(top_k, int) and top_k > 0):
+        raise ValueError("`top_k` has to be a positive integer or None")
+
+
+class _Bounded(RetrievalMetric):
+    plot_lower_bound: float = 0.0
+    plot_upper_bound: float = 1.0
+
+
+class RetrievalMAP(_Bounded):
+    def __init__(self, empty_target_action: str = "neg", ignore_index: Optional[int] = None, top_k: Optional[int] = None, **kwargs: Any) -> None:
+        super().__init__(empty_target_action=empty_target_action, ignore_index=ignore_index, **kwargs)
+        if top_k is not None and not isinstance(top_k, int) and top_k <= 0:
+            raise ValueError(f"Argument ``top_k`` has to be a positive integer or None, but got {top_k}")
+        self.k = top_k
+
+    def _per_query(self, g: G.Grouped) -> Tensor:
+        return G.per_query_average_precision(g, self.k)
+
+
+class RetrievalMRR(_Bounded):
+    def __init__(self, empty_target_action: str = "neg", ignore_index: Optional[int] = None, top_k: Optional[int] = None, **kwargs: Any) -> None:
+        super().__init__(empty_target_action=empty_target_action, ignore_index=ignore_index, **kwargs)
+        if top_k is not None and not isinstance(top_k, int) and top_k <= 0:
+            raise ValueError(f"Argument ``top_k`` has to be a positive integer or None, but got {top_k}")
+        self.top_k = top_k
+
+    def _per_query(self, g: G.Grouped) -> Tensor:
+        return G.per_query_reciprocal_rank(g, self.top_k)
+
+
+class RetrievalPrecision(_Bounded):
+    def __init__(
+        self,
+        empty_target_action: str = "neg",
+        ignore_index: Optional[int] = None,
+        top_k: Optional[int] = None,
+        adaptive_k: bool = False,
+        **kwargs: Any,
+    ) -> None:
+        super().__init__(empty_target_action=empty_target_action, ignore_index=ignore_index, **kwargs)
+        _check_top_k(top_k)
+        if not isinstance(adaptive_k, bool):
+            raise ValueError("`adaptive_k` has to be a boolean")
+        self.top_k = top_k
+        self.adaptive_k = adaptive_k
+
+    def _per_query(self, g: G.Grouped) -> Tensor:
+        return G.per_query_precision(g, self.top_k, self.adaptive_k)
+
+
+class RetrievalRecall(_Bounded):
+    def __init__(self, empty_target_action: str = "neg", ignore_index: Optional[int] = None, top_k: Optional[int] = None, **kwargs: Any) -> None:
+        super().__init__(empty_target_action=empty_target_action, ignore_index=ignore_index, **kwargs)
+        _check_top_k(top_k)
+        self.top_k = top_k
+
+    def _per_query(self, g: G.Grouped) -> Tensor:
+        return G.per_query_recall(g, self.top_k)
+
+
+class RetrievalFallOut(_Bounded):
+    higher_is_better: bool = False
+    _empty_on_negatives = True
+
+    def __init__(self, empty_target_action: str = "pos", ignore_index: Optional[int] = None, top_k: Optional[int] = None, **kwargs: Any) -> None:
+        super().__init__(empty_target_action=empty_target_action, ignore_index=ignore_index, **kwargs)
+        _check_top_k(top_k)
+        self.top_k = top_k
+
+    def _per_query(self, g: G.Grouped) -> Tensor:
+        return G.per_query_fall_out(g, self.top_k)
+
+
+class RetrievalHitRate(_Bounded):
+    def __init__(self, empty_target_action: str = "neg", ignore_index: Optional[int] = None, top_k: Optional[int] = None, **kwargs: Any) -> None:
+        super().__init__(empty_target_action=empty_target_action, ignore_index=ignore_index, **kwargs)
+        _check_top_k(top_k)
+        self.top_k = top_k
+
+    def _per_query(self, g: G.Grouped) -> Tensor:
+        return G.per_query_hit_rate(g, self.top_k)
+
+
+class RetrievalRPrecision(_Bounded):
+    def _per_query(self, g: G.Grouped) -> Tensor:
+        return G.per_query_r_precision(g)
+
+
+class RetrievalNormalizedDCG(_Bounded):
+    def __init__(self, empty_target_action: str = "neg", ignore_index: Optional[int] = None, top_k: Optional[int] = None, **kwargs: Any) -> None:
+        super().__init__(empty_target_action=empty_target_action, ignore_index=ignore_index, **kwargs)
+        _check_top_k(top_k)
+        self.top_k = top_k
+        self.allow_non_binary_target = True
+
+    def _per_query(self, g: G.Grouped) -> Tensor:
+        return G.per_query_ndcg(g, self.top_k)
