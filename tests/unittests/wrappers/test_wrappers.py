@@ -1,0 +1,156 @@
+"""Wrapper tests (strategy mirrors reference tests/unittests/wrappers/*): bootstrap resampling vs a manual
+oracle, classwise naming, min/max tracking, multioutput column routing with NaN removal, multitask routing,
+tracker best-metric bookkeeping."""
+import pytest
+import torch
+
+import torchmetrics_forked_amd as tm
+from torchmetrics_forked_amd.wrappers import (
+    BootStrapper,
+    ClasswiseWrapper,
+    MetricTracker,
+    MinMaxMetric,
+    MultioutputWrapper,
+    MultitaskWrapper,
+    Running,
+    WrapperMetric,
+)
+from torchmetrics_forked_amd.wrappers.bootstrapping import _bootstrap_sampler
+
+
+@pytest.mark.parametrize("strategy", ["poisson", "multinomial"])
+def test_bootstrap_sampler(strategy):
+    torch.manual_seed(0)
+    idx = _bootstrap_sampler(1000, strategy)
+    assert idx.min() >= 0 and idx.max() < 1000
+    if strategy == "multinomial":
+        assert idx.numel() == 1000
+    else:
+        assert 850 < idx.numel() < 1150
+
+
+@pytest.mark.parametrize("strategy", ["poisson", "multinomial"])
+def test_bootstrapper_matches_manual(strategy):
+    p, t = torch.randn(200), torch.randn(200)
+    torch.manual_seed(42)
+    bs = BootStrapper(tm.MeanSquaredError(), num_bootstraps=5, quantile=torch.tensor([0.05, 0.95]), raw=True,
+                      sampling_strategy=strategy)
+    bs.update(p, t)
+    out = bs.compute()
+    torch.manual_seed(42)
+    vals = []
+    for _ in range(5):
+        idx = _bootstrap_sampler(200, strategy)
+        vals.append(((p[idx] - t[idx]) ** 2).mean())
+    vals = torch.stack(vals)
+    assert torch.allclose(out["raw"], vals, atol=1e-6)
+    assert torch.allclose(out["mean"], vals.mean(), atol=1e-6)
+    assert torch.allclose(out["std"], vals.std(), atol=1e-6)
+    assert torch.allclose(out["quantile"], torch.quantile(vals, torch.tensor([0.05, 0.95])), atol=1e-6)
+
+
+def test_bootstrapper_forward_and_reset():
+    torch.manual_seed(1)
+    bs = BootStrapper(tm.MeanSquaredError(), num_bootstraps=4)
+    batches = [(torch.randn(50), torch.randn(50)) for _ in range(3)]
+    for p, t in batches:
+        res = bs(p, t)
+        assert set(res) == {"mean", "std"}
+    # global state holds each batch exactly once per copy
+    assert all(int(m.total) < 3 * 50 * 2 for m in bs.metrics)
+    bs.reset()
+    assert all(int(m.total) == 0 for m in bs.metrics)
+    with pytest.raises(ValueError, match="sampling_strategy"):
+        BootStrapper(tm.MeanSquaredError(), sampling_strategy="bad")
+    with pytest.raises(ValueError, match="instance"):
+        BootStrapper(lambda x: x)
+
+
+def test_classwise():
+    m = ClasswiseWrapper(tm.MulticlassAccuracy(3, average=None), labels=["a", "b", "c"])
+    p, t = torch.randn(20, 3), torch.randint(0, 3, (20,))
+    out = m(p, t)
+    assert set(out) == {"multiclassaccuracy_a", "multiclassaccuracy_b", "multiclassaccuracy_c"}
+    ref = tm.functional.multiclass_accuracy(p, t, 3, average=None)
+    assert torch.allclose(torch.stack(list(m.compute().values())), ref)
+    m2 = ClasswiseWrapper(tm.MulticlassAccuracy(3, average=None), prefix="acc-", postfix="!")
+    m2.update(p, t)
+    assert set(m2.compute()) == {"acc-0!", "acc-1!", "acc-2!"}
+    with pytest.raises(ValueError, match="labels"):
+        ClasswiseWrapper(tm.MulticlassAccuracy(3, average=None), labels=[1, 2])
+    assert isinstance(m, WrapperMetric)
+
+
+def test_minmax():
+    m = MinMaxMetric(tm.BinaryAccuracy())
+    vals = []
+    g = torch.Generator().manual_seed(3)
+    for _ in range(4):
+        p, t = torch.rand(30, generator=g), torch.randint(0, 2, (30,), generator=g)
+        m.update(p, t)
+        out = m.compute()
+        vals.append(float(out["raw"]))
+        assert float(out["max"]) == max(vals) and float(out["min"]) == min(vals)
+    with pytest.raises(RuntimeError, match="scalar"):
+        bad = MinMaxMetric(tm.MulticlassAccuracy(3, average=None))
+        bad.update(torch.randn(5, 3), torch.randint(0, 3, (5,)))
+        bad.compute()
+
+
+def test_multioutput():
+    p, t = torch.randn(40, 3), torch.randn(40, 3)
+    p[3, 1] = float("nan")
+    m = MultioutputWrapper(tm.MeanSquaredError(), num_outputs=3)
+    m.update(p, t)
+    out = m.compute()
+    ref = []
+    for i in range(3):
+        keep = ~torch.isnan(p[:, i])
+        ref.append(((p[keep, i] - t[keep, i]) ** 2).mean())
+    assert torch.allclose(out, torch.stack(ref))
+    fw = MultioutputWrapper(tm.R2Score(), num_outputs=3)(p.nan_to_num(), t)
+    assert fw.shape == (3,)
+
+
+def test_multitask():
+    mt = MultitaskWrapper({"cls": tm.BinaryAccuracy(), "reg": tm.MeanSquaredError()})
+    preds = {"cls": torch.rand(10), "reg": torch.randn(10)}
+    targets = {"cls": torch.randint(0, 2, (10,)), "reg": torch.randn(10)}
+    fwd = mt(preds, targets)
+    out = mt.compute()
+    assert set(out) == {"cls", "reg"} and set(fwd) == {"cls", "reg"}
+    assert torch.allclose(out["reg"], tm.functional.mean_squared_error(preds["reg"], targets["reg"]))
+    with pytest.raises(ValueError, match="same keys"):
+        mt.update({"cls": preds["cls"]}, targets)
+    with pytest.raises(TypeError):
+        MultitaskWrapper({"a": 1})
+
+
+def test_tracker_single_and_collection():
+    tr = MetricTracker(tm.MeanSquaredError(), maximize=False)
+    with pytest.raises(ValueError, match="increment"):
+        tr.update(torch.randn(3), torch.randn(3))
+    g = torch.Generator().manual_seed(5)
+    for scale in (3.0, 1.0, 2.0):
+        tr.increment()
+        tr.update(torch.randn(20, generator=g) * scale, torch.zeros(20))
+    allv = tr.compute_all()
+    assert allv.shape == (3,)
+    best, step = tr.best_metric(return_step=True)
+    assert step == int(torch.argmin(allv)) and abs(best - float(allv.min())) < 1e-6
+    coll = tm.MetricCollection([tm.MeanSquaredError(), tm.MeanAbsoluteError()])
+    tr2 = MetricTracker(coll, maximize=[False, False])
+    for _ in range(2):
+        tr2.increment()
+        tr2.update(torch.randn(20, generator=g), torch.zeros(20))
+    best = tr2.best_metric()
+    assert set(best) == {"MeanSquaredError", "MeanAbsoluteError"}
+    assert tr2.n_steps == 2
+
+
+def test_running_is_wrapper():
+    r = Running(tm.SumMetric(), window=2)
+    assert isinstance(r, WrapperMetric)
+    for v in (1.0, 2.0, 3.0):
+        r.update(torch.tensor(v))
+    assert float(r.compute()) == 5.0

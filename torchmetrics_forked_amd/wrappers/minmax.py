@@ -1,0 +1,53 @@
+"""Track min / max of a scalar metric across ``compute`` calls (API parity: reference ``wrappers/minmax.py:29-115``)."""
+from typing import Any, Dict, Optional, Sequence, Union
+
+import torch
+from torch import Tensor
+
+from torchmetrics_forked_amd.metric import Metric
+from torchmetrics_forked_amd.utilities.plot import _AX_TYPE, _PLOT_OUT_TYPE
+from torchmetrics_forked_amd.wrappers.abstract import WrapperMetric
+
+
+class MinMaxMetric(WrapperMetric):
+    full_state_update: Optional[bool] = True
+    min_val: Tensor
+    max_val: Tensor
+
+    def __init__(self, base_metric: Metric, **kwargs: Any) -> None:
+        super().__init__(**kwargs)
+        if not isinstance(base_metric, Metric):
+            raise ValueError(f"Expected base metric to be an instance of `torchmetrics.Metric` but received {base_metric}")
+        self._base_metric = base_metric
+        self.min_val = torch.tensor(float("inf"))
+        self.max_val = torch.tensor(float("-inf"))
+
+    def update(self, *args: Any, **kwargs: Any) -> None:
+        self._base_metric.update(*args, **kwargs)
+
+    def compute(self) -> Dict[str, Tensor]:
+        val = self._base_metric.compute()
+        if not self._is_suitable_val(val):
+            raise RuntimeError(f"Returned value from base metric should be a float or scalar tensor, but got {val}.")
+        mx, mn = self.max_val.to(val.device), self.min_val.to(val.device)
+        self.max_val = val if mx < val else mx
+        self.min_val = val if mn > val else mn
+        return {"raw": val, "max": self.max_val, "min": self.min_val}
+
+    def forward(self, *args: Any, **kwargs: Any) -> Any:
+        return Metric.forward(self, *args, **kwargs)
+
+    def reset(self) -> None:
+        super().reset()
+        self._base_metric.reset()
+
+    @staticmethod
+    def _is_suitable_val(val: Union[float, Tensor]) -> bool:
+        if isinstance(val, (int, float)):
+            return True
+        if isinstance(val, Tensor):
+            return val.numel() == 1
+        return False
+
+    def plot(self, val: Optional[Union[Tensor, Sequence[Tensor]]] = None, ax: Optional[_AX_TYPE] = None) -> _PLOT_OUT_TYPE:
+        return self._plot(val, ax)

@@ -10,10 +10,17 @@ from torch import Tensor
 
 from torchmetrics_forked_amd.metric import Metric
 from torchmetrics_forked_amd.utilities.plot import _AX_TYPE, _PLOT_OUT_TYPE
+from torchmetrics_forked_amd.wrappers.abstract import WrapperMetric
 
 
-class Running(Metric):
-    """Compute ``base_metric`` over the last ``window`` calls of ``update``/``forward``."""
+class Running(WrapperMetric):
+    """Compute ``base_metric`` over the last ``window`` calls of ``update``/``forward``.
+
+    Unlike the reference (whose wrapper hooks skip sync), ``compute`` keeps the framework's wrapped compute so the
+    slot states are synchronised across ranks in one coalesced collective."""
+
+    _wrap_update = Metric._wrap_update
+    _wrap_compute = Metric._wrap_compute
 
     def __init__(self, base_metric: Metric, window: int = 5) -> None:
         super().__init__()
