@@ -1,0 +1,54 @@
+"""gfx950 tiled pairwise L1/Lp kernel vs fp64 PyTorch broadcast reference; GPU nominal/clustering vs CPU."""
+import pytest
+import torch
+
+from torchmetrics_forked_amd import ops
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_native(device):
+    ops.require()
+
+
+@pytest.mark.parametrize("shape", [((1, 1), (1, 1)), ((70, 33), (130, 33)), ((257, 100), (64, 100)), ((1000, 3), (999, 3))])
+@pytest.mark.parametrize("p", [1.0, 2.0, 3.0, 1.5])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64, torch.bfloat16])
+def test_pairwise_lp(shape, p, dtype):
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(*shape[0], generator=g).to(dtype)
+    y = torch.randn(*shape[1], generator=g).to(dtype)
+    for fp64 in (False, True):
+        out = torch.ops.tmx.pairwise_lp(x.cuda(), y.cuda(), p, fp64).cpu()
+        xd, yd = x.double(), y.double()
+        ref = (xd.unsqueeze(1) - yd.unsqueeze(0)).abs().pow(p).sum(-1).pow(1 / p)
+        tol = 1e-9 if (fp64 and dtype == torch.float64) else 1e-4
+        assert torch.allclose(out.double(), ref, rtol=tol, atol=tol), (out.double() - ref).abs().max()
+
+
+def test_pairwise_functional_gpu():
+    import torchmetrics_forked_amd.functional.pairwise as FP
+
+    g = torch.Generator().manual_seed(1)
+    x, y = torch.randn(300, 17, generator=g), torch.randn(200, 17, generator=g)
+    for fn, kw in ((FP.pairwise_manhattan_distance, {}), (FP.pairwise_minkowski_distance, {"exponent": 3}),
+                   (FP.pairwise_euclidean_distance, {}), (FP.pairwise_cosine_similarity, {})):
+        a, b = fn(x.cuda(), y.cuda(), **kw).cpu(), fn(x, y, **kw)
+        assert torch.allclose(a, b, atol=1e-4), fn.__name__
+
+
+def test_nominal_clustering_gpu():
+    import torchmetrics_forked_amd.functional.clustering as FC
+    import torchmetrics_forked_amd.functional.nominal as FN
+
+    g = torch.Generator().manual_seed(2)
+    p, t = torch.randint(0, 5, (5000,), generator=g), torch.randint(0, 5, (5000,), generator=g)
+    for fn in (FN.cramers_v, FN.tschuprows_t, FN.theils_u, FN.pearsons_contingency_coefficient,
+               FC.mutual_info_score, FC.adjusted_rand_score, FC.adjusted_mutual_info_score, FC.v_measure_score):
+        a, b = fn(p.cuda(), t.cuda()).cpu(), fn(p, t)
+        assert torch.allclose(a.double(), b.double(), atol=1e-5), fn.__name__
+    data, labels = torch.randn(2000, 4, generator=g), torch.randint(0, 6, (2000,), generator=g)
+    for fn in (FC.calinski_harabasz_score, FC.davies_bouldin_score, FC.dunn_index):
+        a, b = fn(data.cuda(), labels.cuda()).cpu(), fn(data, labels)
+        assert torch.allclose(a, b, rtol=1e-4), fn.__name__

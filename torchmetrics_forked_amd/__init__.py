@@ -20,6 +20,7 @@ from torchmetrics_forked_amd.aggregation import (  # noqa: E402
 from torchmetrics_forked_amd.classification import *  # noqa: E402,F401,F403
 from torchmetrics_forked_amd.collections import MetricCollection  # noqa: E402
 from torchmetrics_forked_amd.metric import CompositionalMetric, Metric  # noqa: E402
+from torchmetrics_forked_amd.nominal import *  # noqa: E402,F401,F403
 from torchmetrics_forked_amd.regression import *  # noqa: E402,F401,F403
 from torchmetrics_forked_amd.wrappers import (  # noqa: E402
     BootStrapper,

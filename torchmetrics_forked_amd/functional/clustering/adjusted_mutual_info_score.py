@@ -1,0 +1,56 @@
+"""Adjusted mutual information (API parity: reference ``functional/clustering/adjusted_mutual_info_score.py``).
+
+The expected mutual information is evaluated as one masked tensor expression over (row, col, n_ij) in fp64,
+chunked over n_ij to bound memory, instead of the reference's triple Python loop."""
+import torch
+from torch import Tensor, tensor
+from typing_extensions import Literal
+
+from torchmetrics_forked_amd.functional.clustering.mutual_info_score import (
+    _mutual_info_score_compute,
+    _mutual_info_score_update,
+)
+from torchmetrics_forked_amd.functional.clustering.utils import (
+    _validate_average_method_arg,
+    calculate_entropy,
+    calculate_generalized_mean,
+)
+
+
+def expected_mutual_info_score(contingency: Tensor, n_samples: int) -> Tensor:
+    a = contingency.sum(dim=1).double()
+    b = contingency.sum(dim=0).double()
+    if a.numel() == 1 or b.numel() == 1:
+        return tensor(0.0, device=a.device)
+    n = float(n_samples)
+    m = int(max(a.max().item(), b.max().item()))
+    ai, bj = a.view(-1, 1, 1), b.view(1, -1, 1)
+    lo = torch.clamp(ai - n + bj, min=1.0)
+    hi = torch.minimum(ai, bj)
+    fixed = (torch.lgamma(ai + 1) + torch.lgamma(bj + 1) + torch.lgamma(n - ai + 1) + torch.lgamma(n - bj + 1)
+             - torch.lgamma(torch.tensor(n + 1, dtype=torch.float64, device=a.device)))
+    emi = torch.zeros((), dtype=torch.float64, device=a.device)
+    chunk = max(1, (1 << 24) // max(1, a.numel() * b.numel()))
+    for s in range(1, m + 1, chunk):
+        nij = torch.arange(s, min(m, s + chunk - 1) + 1, dtype=torch.float64, device=a.device).view(1, 1, -1)
+        valid = (nij >= lo) & (nij <= hi)
+        term1 = nij / n
+        term2 = torch.log(n * nij) - torch.log(ai) - torch.log(bj)
+        gln = (fixed - torch.lgamma(nij + 1) - torch.lgamma(ai - nij + 1) - torch.lgamma(bj - nij + 1)
+               - torch.lgamma(n - ai - bj + nij + 1))
+        emi = emi + torch.where(valid, term1 * term2 * torch.exp(gln), torch.zeros_like(gln)).sum()
+    return emi.float()
+
+
+def adjusted_mutual_info_score(
+    preds: Tensor, target: Tensor, average_method: Literal["min", "geometric", "arithmetic", "max"] = "arithmetic"
+) -> Tensor:
+    _validate_average_method_arg(average_method)
+    contingency = _mutual_info_score_update(preds, target)
+    mutual_info = _mutual_info_score_compute(contingency)
+    emi = expected_mutual_info_score(contingency, target.numel())
+    normalizer = calculate_generalized_mean(torch.stack([calculate_entropy(preds), calculate_entropy(target)]), average_method)
+    denominator = normalizer - emi
+    eps = torch.finfo(denominator.dtype).eps
+    denominator = torch.clamp(denominator, max=-eps) if denominator < 0 else torch.clamp(denominator, min=eps)
+    return (mutual_info - emi) / denominator

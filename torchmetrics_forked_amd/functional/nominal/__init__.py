@@ -1,0 +1,14 @@
+"""Functional nominal-association metrics (API parity: reference ``functional/nominal/__init__.py``)."""
+from torchmetrics_forked_amd.functional.nominal.cramers import cramers_v, cramers_v_matrix
+from torchmetrics_forked_amd.functional.nominal.fleiss_kappa import fleiss_kappa
+from torchmetrics_forked_amd.functional.nominal.pearson import (
+    pearsons_contingency_coefficient,
+    pearsons_contingency_coefficient_matrix,
+)
+from torchmetrics_forked_amd.functional.nominal.theils_u import theils_u, theils_u_matrix
+from torchmetrics_forked_amd.functional.nominal.tschuprows import tschuprows_t, tschuprows_t_matrix
+
+__all__ = [
+    "cramers_v", "cramers_v_matrix", "fleiss_kappa", "pearsons_contingency_coefficient",
+    "pearsons_contingency_coefficient_matrix", "theils_u", "theils_u_matrix", "tschuprows_t", "tschuprows_t_matrix",
+]

@@ -1,0 +1,25 @@
+"""Pairwise cosine similarity (API parity: reference ``functional/pairwise/cosine.py``); GEMM on hipBLASLt."""
+from typing import Optional
+
+import torch
+from torch import Tensor
+from typing_extensions import Literal
+
+from torchmetrics_forked_amd.functional.pairwise.helpers import _check_input, _reduce_distance_matrix
+from torchmetrics_forked_amd.utilities.compute import _safe_matmul
+
+
+def _pairwise_cosine_similarity_update(x: Tensor, y: Optional[Tensor] = None, zero_diagonal: Optional[bool] = None) -> Tensor:
+    x, y, zero_diagonal = _check_input(x, y, zero_diagonal)
+    x = x / torch.norm(x, p=2, dim=1).unsqueeze(1)
+    y = y / torch.norm(y, p=2, dim=1).unsqueeze(1)
+    distance = _safe_matmul(x, y)
+    if zero_diagonal:
+        distance.fill_diagonal_(0)
+    return distance
+
+
+def pairwise_cosine_similarity(
+    x: Tensor, y: Optional[Tensor] = None, reduction: Literal["mean", "sum", "none", None] = None, zero_diagonal: Optional[bool] = None
+) -> Tensor:
+    return _reduce_distance_matrix(_pairwise_cosine_similarity_update(x, y, zero_diagonal), reduction)

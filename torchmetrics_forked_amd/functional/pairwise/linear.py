@@ -1,0 +1,22 @@
+"""Pairwise linear (dot-product) similarity (API parity: reference ``functional/pairwise/linear.py``)."""
+from typing import Optional
+
+from torch import Tensor
+from typing_extensions import Literal
+
+from torchmetrics_forked_amd.functional.pairwise.helpers import _check_input, _reduce_distance_matrix
+from torchmetrics_forked_amd.utilities.compute import _safe_matmul
+
+
+def _pairwise_linear_similarity_update(x: Tensor, y: Optional[Tensor] = None, zero_diagonal: Optional[bool] = None) -> Tensor:
+    x, y, zero_diagonal = _check_input(x, y, zero_diagonal)
+    distance = _safe_matmul(x, y)
+    if zero_diagonal:
+        distance.fill_diagonal_(0)
+    return distance
+
+
+def pairwise_linear_similarity(
+    x: Tensor, y: Optional[Tensor] = None, reduction: Literal["mean", "sum", "none", None] = None, zero_diagonal: Optional[bool] = None
+) -> Tensor:
+    return _reduce_distance_matrix(_pairwise_linear_similarity_update(x, y, zero_diagonal), reduction)

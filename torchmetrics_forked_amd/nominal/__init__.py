@@ -1,0 +1,97 @@
+"""Nominal association metrics (API parity: reference ``nominal/{cramers,tschuprows,pearson,theils_u,
+fleiss_kappa}.py``).  States are the reference's ``confmat`` (float, ``sum``) / ``counts`` (``cat``)."""
+from typing import Any, List, Optional, Sequence, Union
+
+import torch
+from torch import Tensor
+from typing_extensions import Literal
+
+from torchmetrics_forked_amd.functional.nominal.cramers import _cramers_v_compute
+from torchmetrics_forked_amd.functional.nominal.fleiss_kappa import _fleiss_kappa_compute, _fleiss_kappa_update
+from torchmetrics_forked_amd.functional.nominal.pearson import _pearsons_contingency_coefficient_compute
+from torchmetrics_forked_amd.functional.nominal.theils_u import _theils_u_compute
+from torchmetrics_forked_amd.functional.nominal.tschuprows import _tschuprows_t_compute
+from torchmetrics_forked_amd.functional.nominal.utils import _nominal_input_validation, _nominal_update
+from torchmetrics_forked_amd.metric import Metric
+from torchmetrics_forked_amd.utilities.data import dim_zero_cat
+from torchmetrics_forked_amd.utilities.plot import _AX_TYPE, _PLOT_OUT_TYPE
+
+__all__ = ["CramersV", "FleissKappa", "PearsonsContingencyCoefficient", "TheilsU", "TschuprowsT"]
+
+
+class _ContingencyMetric(Metric):
+    full_state_update: bool = False
+    is_differentiable: bool = False
+    higher_is_better: bool = True
+    plot_lower_bound: float = 0.0
+    plot_upper_bound: float = 1.0
+    confmat: Tensor
+
+    def __init__(self, num_classes: int, nan_strategy: Literal["replace", "drop"] = "replace",
+                 nan_replace_value: Optional[float] = 0.0, **kwargs: Any) -> None:
+        super().__init__(**kwargs)
+        self.num_classes = num_classes
+        _nominal_input_validation(nan_strategy, nan_replace_value)
+        self.nan_strategy = nan_strategy
+        self.nan_replace_value = nan_replace_value
+        self.add_state("confmat", torch.zeros(num_classes, num_classes), dist_reduce_fx="sum")
+
+    def update(self, preds: Tensor, target: Tensor) -> None:
+        self.confmat += _nominal_update(preds, target, self.num_classes, self.nan_strategy, self.nan_replace_value)
+
+    def plot(self, val: Optional[Union[Tensor, Sequence[Tensor]]] = None, ax: Optional[_AX_TYPE] = None) -> _PLOT_OUT_TYPE:
+        return self._plot(val, ax)
+
+
+class CramersV(_ContingencyMetric):
+    def __init__(self, num_classes: int, bias_correction: bool = True, nan_strategy: Literal["replace", "drop"] = "replace",
+                 nan_replace_value: Optional[float] = 0.0, **kwargs: Any) -> None:
+        super().__init__(num_classes, nan_strategy, nan_replace_value, **kwargs)
+        self.bias_correction = bias_correction
+
+    def compute(self) -> Tensor:
+        return _cramers_v_compute(self.confmat, self.bias_correction)
+
+
+class TschuprowsT(_ContingencyMetric):
+    def __init__(self, num_classes: int, bias_correction: bool = True, nan_strategy: Literal["replace", "drop"] = "replace",
+                 nan_replace_value: Optional[float] = 0.0, **kwargs: Any) -> None:
+        super().__init__(num_classes, nan_strategy, nan_replace_value, **kwargs)
+        self.bias_correction = bias_correction
+
+    def compute(self) -> Tensor:
+        return _tschuprows_t_compute(self.confmat, self.bias_correction)
+
+
+class PearsonsContingencyCoefficient(_ContingencyMetric):
+    def compute(self) -> Tensor:
+        return _pearsons_contingency_coefficient_compute(self.confmat)
+
+
+class TheilsU(_ContingencyMetric):
+    def compute(self) -> Tensor:
+        return _theils_u_compute(self.confmat)
+
+
+class FleissKappa(Metric):
+    full_state_update: bool = False
+    is_differentiable: bool = False
+    higher_is_better: bool = True
+    plot_upper_bound: float = 1.0
+    counts: List[Tensor]
+
+    def __init__(self, mode: Literal["counts", "probs"] = "counts", **kwargs: Any) -> None:
+        super().__init__(**kwargs)
+        if mode not in ("counts", "probs"):
+            raise ValueError("Argument ``mode`` must be one of 'counts' or 'probs'.")
+        self.mode = mode
+        self.add_state("counts", default=[], dist_reduce_fx="cat")
+
+    def update(self, ratings: Tensor) -> None:
+        self.counts.append(_fleiss_kappa_update(ratings, self.mode))
+
+    def compute(self) -> Tensor:
+        return _fleiss_kappa_compute(dim_zero_cat(self.counts))
+
+    def plot(self, val: Optional[Union[Tensor, Sequence[Tensor]]] = None, ax: Optional[_AX_TYPE] = None) -> _PLOT_OUT_TYPE:
+        return self._plot(val, ax)
