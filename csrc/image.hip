@@ -1,0 +1,196 @@
+// Fused separable-window SSIM for gfx950.
+//
+// The reference reflect-pads both images, stacks (p, t, p², t², p·t) into a 5·B-image batch, runs a grouped
+// conv2d and crops the padded border.  The cropped region is exactly the set of windows that lie fully inside the
+// image, so the per-image SSIM is the mean over all *valid* KS×KS windows and no padding is ever needed.
+//
+// One block = 256 threads = 256 output columns of one (image, channel) plane and a strip of kRowsPerBlock output
+// rows.  Per input row the block stages the row segment (256 + KS − 1 values of p and t) in LDS (double buffered),
+// every thread computes the horizontal window sums of the five moments for its column, and keeps the last KS
+// horizontal results in a register ring.  The ring is addressed with compile-time indices (row loop unrolled by
+// KS), so the vertical pass is pure register FMAs; only the horizontal taps touch LDS.  The SSIM / contrast-
+// sensitivity terms of each valid window are reduced per block (wave shuffles + LDS) into one fp64 partial per
+// (plane, block) — the output image is never materialised.
+#include "common.h"
+
+namespace tmx {
+
+constexpr int kSsimThreads = 256;
+constexpr int kRowsPerBlock = 64;
+
+template <typename T> __device__ __forceinline__ float ld_f(const T* p, int64_t i) { return to_f32<T>(p[i]); }
+
+template <typename T, int KS>
+__global__ __launch_bounds__(kSsimThreads) void ssim_valid_kernel(const T* __restrict__ preds, const T* __restrict__ target,
+                                                                  int H, int W, const float* __restrict__ wx,
+                                                                  const float* __restrict__ wy, const float* __restrict__ consts,
+                                                                  double* __restrict__ partial_sim, double* __restrict__ partial_cs) {
+  constexpr int kSeg = kSsimThreads + KS - 1;
+  __shared__ float sp[2][kSeg];
+  __shared__ float st[2][kSeg];
+  __shared__ float s_w[KS];
+  __shared__ double red[2][kSsimThreads / kWave];
+
+  const int Hv = H - KS + 1, Wv = W - KS + 1;
+  const int64_t plane = blockIdx.z;
+  const int x0 = blockIdx.x * kSsimThreads;
+  const int y0 = blockIdx.y * kRowsPerBlock;
+  const int tid = threadIdx.x;
+  const T* P = preds + plane * static_cast<int64_t>(H) * W;
+  const T* Tt = target + plane * static_cast<int64_t>(H) * W;
+  const float c1 = consts[0], c2 = consts[1];
+  if (tid < KS) s_w[tid] = wx[tid];
+
+  float wyr[KS];
+#pragma unroll
+  for (int k = 0; k < KS; ++k) wyr[k] = wy[k];
+
+  // ring of horizontal window sums: (mu_p, mu_t, E[pp], E[tt], E[pt]) for the last KS input rows
+  float ring[KS][5];
+#pragma unroll
+  for (int k = 0; k < KS; ++k)
+#pragma unroll
+    for (int q = 0; q < 5; ++q) ring[k][q] = 0.f;
+
+  const int out_rows = min(kRowsPerBlock, Hv - y0);
+  const int in_rows = out_rows + KS - 1;  // input rows y0 .. y0 + in_rows - 1
+  const bool col_ok = (x0 + tid) < Wv;
+  double acc_sim = 0.0, acc_cs = 0.0;
+
+  auto stage = [&](int r, int buf) {
+    const int64_t row = static_cast<int64_t>(y0 + r) * W;
+    for (int i = tid; i < kSeg; i += kSsimThreads) {
+      const int x = x0 + i;
+      const bool ok = x < W;
+      sp[buf][i] = ok ? ld_f(P, row + x) : 0.f;
+      st[buf][i] = ok ? ld_f(Tt, row + x) : 0.f;
+    }
+  };
+
+  if (in_rows > 0) stage(0, 0);
+  __syncthreads();
+
+  for (int base = 0; base < in_rows; base += KS) {
+#pragma unroll
+    for (int j = 0; j < KS; ++j) {
+      const int r = base + j;
+      if (r < in_rows) {  // uniform across the block
+        const int buf = r & 1;
+        if (r + 1 < in_rows) stage(r + 1, buf ^ 1);
+        // horizontal pass for this thread's column
+        float hp = 0.f, ht = 0.f, hpp = 0.f, htt = 0.f, hpt = 0.f;
+#pragma unroll
+        for (int k = 0; k < KS; ++k) {
+          const float w = s_w[k];
+          const float p = sp[buf][tid + k];
+          const float t = st[buf][tid + k];
+          const float wp = w * p, wt = w * t;
+          hp += wp;
+          ht += wt;
+          hpp = fmaf(wp, p, hpp);
+          htt = fmaf(wt, t, htt);
+          hpt = fmaf(wp, t, hpt);
+        }
+        ring[j][0] = hp;
+        ring[j][1] = ht;
+        ring[j][2] = hpp;
+        ring[j][3] = htt;
+        ring[j][4] = hpt;
+        if (r >= KS - 1 && col_ok) {
+          // vertical pass: rows r-KS+1 .. r live in ring[(j+1+k) % KS] (oldest first)
+          float m[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int k = 0; k < KS; ++k) {
+            const int slot = (j + 1 + k) % KS;
+#pragma unroll
+            for (int q = 0; q < 5; ++q) m[q] = fmaf(wyr[k], ring[slot][q], m[q]);
+          }
+          const float mu_pp = m[0] * m[0], mu_tt = m[1] * m[1], mu_pt = m[0] * m[1];
+          const float upper = 2.f * (m[4] - mu_pt) + c2;
+          const float lower = (m[2] - mu_pp) + (m[3] - mu_tt) + c2;
+          const float cs = upper / lower;
+          const float sim = (2.f * mu_pt + c1) * upper / ((mu_pp + mu_tt + c1) * lower);
+          acc_sim += static_cast<double>(sim);
+          acc_cs += static_cast<double>(cs);
+        }
+        __syncthreads();  // staged row r+1 visible; buffer r free for r+2
+      }
+    }
+  }
+
+  // block reduction of the two sums
+  acc_sim = wave_sum(acc_sim);
+  acc_cs = wave_sum(acc_cs);
+  const int wave = tid / kWave, lane = tid & (kWave - 1);
+  if (lane == 0) {
+    red[0][wave] = acc_sim;
+    red[1][wave] = acc_cs;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    double s = 0.0, c = 0.0;
+    for (int w = 0; w < kSsimThreads / kWave; ++w) {
+      s += red[0][w];
+      c += red[1][w];
+    }
+    const int64_t idx = (plane * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+    partial_sim[idx] = s;
+    partial_cs[idx] = c;
+  }
+}
+
+template <typename T, int KS>
+void launch_ssim(const at::Tensor& p, const at::Tensor& t, const at::Tensor& wx, const at::Tensor& wy,
+                 const at::Tensor& consts, at::Tensor& ps, at::Tensor& pc, dim3 grid, int H, int W) {
+  hipLaunchKernelGGL((ssim_valid_kernel<T, KS>), grid, kSsimThreads, 0, stream(), reinterpret_cast<const T*>(p.data_ptr()),
+                     reinterpret_cast<const T*>(t.data_ptr()), H, W, wx.data_ptr<float>(), wy.data_ptr<float>(),
+                     consts.data_ptr<float>(), ps.data_ptr<double>(), pc.data_ptr<double>());
+}
+
+// preds/target [P, H, W] planes (P = B*C); wx/wy fp32 [KS] window weights; consts fp32 [2] = (c1, c2) on device.
+// Returns fp64 [2, P]: per-plane sums of SSIM and contrast sensitivity over all valid windows.
+at::Tensor ssim_sums(const at::Tensor& preds_in, const at::Tensor& target_in, const at::Tensor& wx_in,
+                     const at::Tensor& wy_in, const at::Tensor& consts_in) {
+  TORCH_CHECK(preds_in.is_cuda() && target_in.is_cuda(), "ssim_sums: expected GPU tensors");
+  TORCH_CHECK(preds_in.dim() == 3 && preds_in.sizes() == target_in.sizes(), "ssim_sums: expected matching [P, H, W]");
+  TORCH_CHECK(preds_in.scalar_type() == target_in.scalar_type(), "ssim_sums: dtype mismatch");
+  const int64_t KS = wx_in.numel();
+  TORCH_CHECK(wy_in.numel() == KS, "ssim_sums: window size mismatch");
+  const at::DeviceGuard guard(preds_in.device());
+  auto p = preds_in.contiguous();
+  auto t = target_in.contiguous();
+  auto wx = wx_in.to(at::kFloat).contiguous();
+  auto wy = wy_in.to(at::kFloat).contiguous();
+  auto consts = consts_in.to(at::kFloat).contiguous();
+  const int64_t P = p.size(0), H = p.size(1), W = p.size(2);
+  TORCH_CHECK(H >= KS && W >= KS, "ssim_sums: image smaller than the window");
+  TORCH_CHECK(P <= 65535, "ssim_sums: too many planes for one launch");
+  const int64_t Hv = H - KS + 1, Wv = W - KS + 1;
+  dim3 grid(static_cast<unsigned>((Wv + kSsimThreads - 1) / kSsimThreads),
+            static_cast<unsigned>((Hv + kRowsPerBlock - 1) / kRowsPerBlock), static_cast<unsigned>(P));
+  auto opts = p.options().dtype(at::kDouble);
+  auto ps = at::empty({P, static_cast<int64_t>(grid.y) * grid.x}, opts);
+  auto pc = at::empty({P, static_cast<int64_t>(grid.y) * grid.x}, opts);
+  TMX_DISPATCH_FLOAT(p.scalar_type(), "ssim_sums", [&] {
+    switch (KS) {
+      case 3: launch_ssim<scalar_t, 3>(p, t, wx, wy, consts, ps, pc, grid, H, W); break;
+      case 5: launch_ssim<scalar_t, 5>(p, t, wx, wy, consts, ps, pc, grid, H, W); break;
+      case 7: launch_ssim<scalar_t, 7>(p, t, wx, wy, consts, ps, pc, grid, H, W); break;
+      case 9: launch_ssim<scalar_t, 9>(p, t, wx, wy, consts, ps, pc, grid, H, W); break;
+      case 11: launch_ssim<scalar_t, 11>(p, t, wx, wy, consts, ps, pc, grid, H, W); break;
+      case 13: launch_ssim<scalar_t, 13>(p, t, wx, wy, consts, ps, pc, grid, H, W); break;
+      case 15: launch_ssim<scalar_t, 15>(p, t, wx, wy, consts, ps, pc, grid, H, W); break;
+      default: TORCH_CHECK(false, "ssim_sums: unsupported window size ", KS);
+    }
+  });
+  TMX_LAUNCH_CHECK();
+  return at::stack({ps.sum(1), pc.sum(1)});
+}
+
+}  // namespace tmx
+
+TORCH_LIBRARY_FRAGMENT(tmx, m) {
+  m.def("ssim_sums(Tensor preds, Tensor target, Tensor wx, Tensor wy, Tensor consts) -> Tensor");
+}
+
+TORCH_LIBRARY_IMPL(tmx, CUDA, m) { m.impl("ssim_sums", &tmx::ssim_sums); }

@@ -1,0 +1,22 @@
+"""Image metrics (API parity: reference ``image/__init__.py``)."""
+from torchmetrics_forked_amd.image._simple import (
+    ErrorRelativeGlobalDimensionlessSynthesis,
+    MultiScaleStructuralSimilarityIndexMeasure,
+    PeakSignalNoiseRatio,
+    PeakSignalNoiseRatioWithBlockedEffect,
+    RelativeAverageSpectralError,
+    RootMeanSquaredErrorUsingSlidingWindow,
+    SpectralAngleMapper,
+    SpectralDistortionIndex,
+    StructuralSimilarityIndexMeasure,
+    TotalVariation,
+    UniversalImageQualityIndex,
+    VisualInformationFidelity,
+)
+
+__all__ = [
+    "ErrorRelativeGlobalDimensionlessSynthesis", "MultiScaleStructuralSimilarityIndexMeasure", "PeakSignalNoiseRatio",
+    "PeakSignalNoiseRatioWithBlockedEffect", "RelativeAverageSpectralError", "RootMeanSquaredErrorUsingSlidingWindow",
+    "SpectralAngleMapper", "SpectralDistortionIndex", "StructuralSimilarityIndexMeasure", "TotalVariation",
+    "UniversalImageQualityIndex", "VisualInformationFidelity",
+]

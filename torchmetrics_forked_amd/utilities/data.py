@@ -3,7 +3,7 @@
 Differences from the reference (by design):
   * ``_bincount`` never falls back to a per-bin Python loop; under deterministic mode it uses a
     scatter-add of ones (deterministic for integer accumulation) and on ROCm devices it routes to the
-    framework's LDS-privatised histogram kernel (``ops.histogram.bincount``) when the extension is loaded.
+    framework's LDS-privatised histogram kernel (``torch.ops.tmx.bincount``) on GPU tensors.
   * ``_cumsum`` never copies to the host: integer / float cumsum on GPU is done in fp64 on device.
 """
 from typing import Any, Callable, Dict, List, Mapping, Optional, Sequence, Tuple, Union
@@ -102,11 +102,10 @@ def _bincount(x: Tensor, minlength: Optional[int] = None) -> Tensor:
     if minlength is None:
         minlength = int(x.max().item()) + 1 if x.numel() else 0
     x = x.reshape(-1).long()
-    if x.is_cuda:
-        from torchmetrics_forked_amd.ops import histogram as _hist
+    from torchmetrics_forked_amd import ops
 
-        if _hist.available():
-            return _hist.bincount(x, minlength)
+    if ops.use_native(x):
+        return torch.ops.tmx.bincount(x, int(minlength))
     if torch.are_deterministic_algorithms_enabled():
         out = torch.zeros(minlength, dtype=torch.long, device=x.device)
         return out.scatter_add_(0, x, torch.ones_like(x))
