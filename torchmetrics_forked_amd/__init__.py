@@ -8,6 +8,7 @@ _logger.addHandler(__logging.StreamHandler())
 _logger.setLevel(__logging.INFO)
 
 from torchmetrics_forked_amd import functional  # noqa: E402
+from torchmetrics_forked_amd import image, models, retrieval, wrappers  # noqa: E402,F401
 from torchmetrics_forked_amd.aggregation import (  # noqa: E402
     CatMetric,
     MaxMetric,

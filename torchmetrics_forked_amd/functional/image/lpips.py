@@ -1,0 +1,182 @@
+"""Learned perceptual image patch similarity (API parity: reference ``functional/image/lpips.py:44-431``).
+
+Backbones come from :mod:`torchmetrics_forked_amd.models` (torchvision-identical layer layout, randomly initialised
+unless ``backbone_weights`` is given).  The per-layer head — channel L2-normalisation of both feature maps,
+squared difference, 1×1 linear layer and spatial mean — runs as ONE fused gfx950 kernel per layer
+(``tmx::lpips_head``) when no autograd graph is needed; with gradients (or on CPU) the eager formulation is used.
+The linear-head weights load from a LPIPS ``.pth`` via ``model_path`` (``weights_only=True``); without one the head
+is randomly initialised (the reference downloads pretrained weights, which is not possible offline).
+"""
+from typing import List, NamedTuple, Optional, Tuple, Union
+
+import torch
+import torch.nn.functional as F
+from torch import Tensor, nn
+from typing_extensions import Literal
+
+from torchmetrics_forked_amd import ops
+from torchmetrics_forked_amd.models.backbones import alexnet_features, squeezenet1_1_features, vgg16_features
+
+_SLICES = {
+    "alex": [range(0, 2), range(2, 5), range(5, 8), range(8, 10), range(10, 12)],
+    "vgg": [range(0, 4), range(4, 9), range(9, 16), range(16, 23), range(23, 30)],
+    "squeeze": [range(0, 2), range(2, 5), range(5, 8), range(8, 10), range(10, 11), range(11, 12), range(12, 13)],
+}
+_CHANNELS = {"alex": [64, 192, 384, 256, 256], "vgg": [64, 128, 256, 512, 512], "squeeze": [64, 128, 256, 384, 384, 512, 512]}
+_FEATURES = {"alex": alexnet_features, "vgg": vgg16_features, "squeeze": squeezenet1_1_features}
+
+
+class _SlicedBackbone(nn.Module):
+    def __init__(self, net: str, requires_grad: bool = False, weights: Optional[str] = None) -> None:
+        super().__init__()
+        feats = _FEATURES[net]()
+        if weights is not None:
+            state = torch.load(weights, map_location="cpu", weights_only=True)
+            state = {k[len("features."):]: v for k, v in state.items() if k.startswith("features.")} or state
+            feats.load_state_dict(state)
+        self.slices = nn.ModuleList(
+            nn.Sequential(*[feats[i] for i in rng]) for rng in _SLICES[net]
+        )
+        for p in self.parameters():
+            p.requires_grad_(requires_grad)
+
+    def forward(self, x: Tensor) -> List[Tensor]:
+        outs = []
+        for s in self.slices:
+            x = s(x)
+            outs.append(x)
+        return outs
+
+
+def _spatial_average(in_tens: Tensor, keep_dim: bool = True) -> Tensor:
+    return in_tens.mean([2, 3], keepdim=keep_dim)
+
+
+def _upsample(in_tens: Tensor, out_hw: Tuple[int, ...] = (64, 64)) -> Tensor:
+    return F.interpolate(in_tens, size=out_hw, mode="bilinear", align_corners=False)
+
+
+def _normalize_tensor(in_feat: Tensor, eps: float = 1e-8) -> Tensor:
+    return in_feat / torch.sqrt(eps + torch.sum(in_feat**2, dim=1, keepdim=True))
+
+
+def _resize_tensor(x: Tensor, size: int = 64) -> Tensor:
+    if x.shape[-1] > size and x.shape[-2] > size:
+        return F.interpolate(x, (size, size), mode="area")
+    return F.interpolate(x, (size, size), mode="bilinear", align_corners=False)
+
+
+class ScalingLayer(nn.Module):
+    def __init__(self) -> None:
+        super().__init__()
+        self.register_buffer("shift", torch.tensor([-0.030, -0.088, -0.188])[None, :, None, None], persistent=False)
+        self.register_buffer("scale", torch.tensor([0.458, 0.448, 0.450])[None, :, None, None], persistent=False)
+
+    def forward(self, inp: Tensor) -> Tensor:
+        return (inp - self.shift) / self.scale
+
+
+class NetLinLayer(nn.Module):
+    def __init__(self, chn_in: int, chn_out: int = 1, use_dropout: bool = False) -> None:
+        super().__init__()
+        layers: List[nn.Module] = [nn.Dropout()] if use_dropout else []
+        layers += [nn.Conv2d(chn_in, chn_out, 1, stride=1, padding=0, bias=False)]
+        self.model = nn.Sequential(*layers)
+
+    def forward(self, x: Tensor) -> Tensor:
+        return self.model(x)
+
+
+class _LPIPS(nn.Module):
+    def __init__(
+        self,
+        pretrained: bool = True,
+        net: Literal["alex", "vgg", "squeeze"] = "alex",
+        spatial: bool = False,
+        pnet_rand: bool = False,
+        pnet_tune: bool = False,
+        use_dropout: bool = True,
+        model_path: Optional[str] = None,
+        eval_mode: bool = True,
+        resize: Optional[int] = None,
+        backbone_weights: Optional[str] = None,
+    ) -> None:
+        super().__init__()
+        net = "vgg" if net == "vgg16" else net
+        if net not in _CHANNELS:
+            raise ValueError(f"Unknown LPIPS backbone {net}")
+        self.pnet_type = net
+        self.spatial = spatial
+        self.resize = resize
+        self.scaling_layer = ScalingLayer()
+        self.chns = _CHANNELS[net]
+        self.L = len(self.chns)
+        self.net = _SlicedBackbone(net, requires_grad=pnet_tune, weights=backbone_weights)
+        self.lins = nn.ModuleList(NetLinLayer(c, use_dropout=use_dropout) for c in self.chns)
+        for i, lin in enumerate(self.lins):  # reference attribute names lin0..lin6 (state-dict compatible)
+            setattr(self, f"lin{i}", lin)
+        if pretrained and model_path is not None:
+            self.load_state_dict(torch.load(model_path, map_location="cpu", weights_only=True), strict=False)
+        if eval_mode:
+            self.eval()
+
+    def forward(self, in0: Tensor, in1: Tensor, retperlayer: bool = False, normalize: bool = False) -> Union[Tensor, Tuple[Tensor, List[Tensor]]]:
+        if normalize:
+            in0, in1 = 2 * in0 - 1, 2 * in1 - 1
+        x0, x1 = self.scaling_layer(in0), self.scaling_layer(in1)
+        if self.resize is not None:
+            x0, x1 = _resize_tensor(x0, size=self.resize), _resize_tensor(x1, size=self.resize)
+        outs0, outs1 = self.net(x0), self.net(x1)
+        grad = torch.is_grad_enabled() and (in0.requires_grad or in1.requires_grad or any(p.requires_grad for p in self.parameters()))
+        fused = (not self.spatial) and outs0[0].is_cuda and not grad and not self.training and ops.use_native(outs0[0])
+        res = []
+        for kk in range(self.L):
+            if fused:
+                w = self.lins[kk].model[-1].weight.reshape(-1)
+                res.append(torch.ops.tmx.lpips_head(outs0[kk], outs1[kk], w).to(outs0[kk].dtype).reshape(-1, 1, 1, 1))
+                continue
+            diff = (_normalize_tensor(outs0[kk]) - _normalize_tensor(outs1[kk])) ** 2
+            if self.spatial:
+                res.append(_upsample(self.lins[kk](diff), out_hw=tuple(in0.shape[2:])))
+            else:
+                res.append(_spatial_average(self.lins[kk](diff), keep_dim=True))
+        val = sum(res)
+        return (val, res) if retperlayer else val
+
+
+class _NoTrainLpips(_LPIPS):
+    def train(self, mode: bool = True) -> "_NoTrainLpips":
+        return super().train(False)
+
+
+def _valid_img(img: Tensor, normalize: bool) -> bool:
+    value_check = img.max() <= 1.0 and img.min() >= 0.0 if normalize else img.min() >= -1
+    return img.ndim == 4 and img.shape[1] == 3 and bool(value_check)
+
+
+def _lpips_update(img1: Tensor, img2: Tensor, net: nn.Module, normalize: bool) -> Tuple[Tensor, Union[int, Tensor]]:
+    if not (_valid_img(img1, normalize) and _valid_img(img2, normalize)):
+        raise ValueError(
+            "Expected both input arguments to be normalized tensors with shape [N, 3, H, W]."
+            f" Got input with shape {img1.shape} and {img2.shape} and values in range"
+            f" {[img1.min(), img1.max()]} and {[img2.min(), img2.max()]} when all values are"
+            f" expected to be in the {[0, 1] if normalize else [-1, 1]} range."
+        )
+    loss = net(img1, img2, normalize=normalize).squeeze()
+    return loss, img1.shape[0]
+
+
+def _lpips_compute(sum_scores: Tensor, total: Union[Tensor, int], reduction: Literal["sum", "mean"] = "mean") -> Tensor:
+    return sum_scores / total if reduction == "mean" else sum_scores
+
+
+def learned_perceptual_image_patch_similarity(
+    img1: Tensor,
+    img2: Tensor,
+    net_type: Literal["alex", "vgg", "squeeze"] = "alex",
+    reduction: Literal["sum", "mean"] = "mean",
+    normalize: bool = False,
+) -> Tensor:
+    net = _NoTrainLpips(net=net_type).to(img1.device)
+    loss, total = _lpips_update(img1, img2, net, normalize)
+    return _lpips_compute(loss.sum(), total, reduction)

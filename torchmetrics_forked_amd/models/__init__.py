@@ -1,0 +1,8 @@
+"""Feature-extractor networks used by model-based metrics (LPIPS backbones, Inception-v3 for FID/KID/IS/MiFID,
+text encoders).  Defined here from scratch for PyTorch-ROCm (MIOpen convolutions / hipBLASLt GEMMs); weights are
+randomly initialised unless a state dict is supplied (no network access, no torchvision dependency).  Layer
+naming follows the torchvision / torch-fidelity layouts so existing checkpoints load with ``strict=True``."""
+from torchmetrics_forked_amd.models.backbones import alexnet_features, squeezenet1_1_features, vgg16_features
+from torchmetrics_forked_amd.models.inception import FeatureExtractorInceptionV3
+
+__all__ = ["FeatureExtractorInceptionV3", "alexnet_features", "squeezenet1_1_features", "vgg16_features"]
