@@ -1,0 +1,520 @@
+"""Detection metrics: box ops, IoU family, MeanAveragePrecision (native COCO evaluator), masks/RLE.
+
+Oracles: closed-form box formulas; the reference IoU modules and the reference's legacy pure-torch
+``detection/_mean_ap.py`` evaluator (both import ``torchvision.ops`` / ``pycocotools.mask`` lazily, which are not
+installed here — the test supplies stand-in modules whose box/mask primitives are checked separately below);
+and a loop-by-loop Python statement of the COCO algorithm (``_coco_oracle``) for crowd / area / ``maxDets``
+cases.  pycocotools itself is not installed, so direct pycocotools parity is unpinned beyond these oracles."""
+import json
+import math
+import sys
+import types
+
+import numpy as np
+import pytest
+import torch
+
+from torchmetrics_forked_amd.detection import (
+    CompleteIntersectionOverUnion,
+    DistanceIntersectionOverUnion,
+    GeneralizedIntersectionOverUnion,
+    IntersectionOverUnion,
+    MeanAveragePrecision,
+)
+from torchmetrics_forked_amd.detection import _mask_utils as mu
+from torchmetrics_forked_amd.functional.detection import _box_ops as bo
+from torchmetrics_forked_amd.functional.detection import (
+    complete_intersection_over_union,
+    distance_intersection_over_union,
+    generalized_intersection_over_union,
+    intersection_over_union,
+)
+from tests.unittests.detection import _coco_oracle as oracle
+
+
+def _rand_boxes(n, gen, scale=300.0, min_wh=1.0):
+    xy = torch.rand(n, 2, generator=gen) * scale
+    wh = torch.rand(n, 2, generator=gen) * scale / 2 + min_wh
+    return torch.cat([xy, xy + wh], 1)
+
+
+def _closed_form(b1, b2):
+    """Element-by-element IoU/GIoU/DIoU/CIoU with python floats."""
+    out = {k: torch.zeros(len(b1), len(b2), dtype=torch.float64) for k in ("iou", "giou", "diou", "ciou")}
+    for i, a in enumerate(b1.tolist()):
+        for j, b in enumerate(b2.tolist()):
+            iw = max(0.0, min(a[2], b[2]) - max(a[0], b[0]))
+            ih = max(0.0, min(a[3], b[3]) - max(a[1], b[1]))
+            inter = iw * ih
+            aa = (a[2] - a[0]) * (a[3] - a[1])
+            ab = (b[2] - b[0]) * (b[3] - b[1])
+            u = aa + ab - inter
+            iou = inter / u
+            cw = max(a[2], b[2]) - min(a[0], b[0])
+            ch = max(a[3], b[3]) - min(a[1], b[1])
+            giou = iou - (cw * ch - u) / (cw * ch)
+            diag = cw**2 + ch**2 + 1e-7
+            cd = ((a[0] + a[2]) / 2 - (b[0] + b[2]) / 2) ** 2 + ((a[1] + a[3]) / 2 - (b[1] + b[3]) / 2) ** 2
+            diou = iou - cd / diag
+            v = 4 / math.pi**2 * (math.atan((a[2] - a[0]) / (a[3] - a[1])) - math.atan((b[2] - b[0]) / (b[3] - b[1]))) ** 2
+            alpha = v / (1 - iou + v + 1e-7)
+            out["iou"][i, j], out["giou"][i, j], out["diou"][i, j], out["ciou"][i, j] = iou, giou, diou, diou - alpha * v
+    return out
+
+
+def test_box_ops_closed_form():
+    gen = torch.Generator().manual_seed(0)
+    b1, b2 = _rand_boxes(7, gen), _rand_boxes(5, gen)
+    ref = _closed_form(b1, b2)
+    for mode in ("iou", "giou", "diou", "ciou"):
+        torch.testing.assert_close(bo.pairwise_box_overlap(b1.double(), b2.double(), mode), ref[mode], atol=1e-9, rtol=0)
+        torch.testing.assert_close(bo.pairwise_box_overlap(b1, b2, mode).double(), ref[mode], atol=1e-5, rtol=0)
+
+
+def test_box_convert_roundtrip():
+    gen = torch.Generator().manual_seed(1)
+    b = _rand_boxes(10, gen)
+    for fmt in ("xywh", "cxcywh"):
+        torch.testing.assert_close(bo.box_convert(bo.box_convert(b, "xyxy", fmt), fmt, "xyxy"), b)
+    torch.testing.assert_close(bo.box_convert(b, "xyxy", "xywh")[:, 2:], b[:, 2:] - b[:, :2])
+
+
+@pytest.mark.parametrize(
+    ("fn", "mode"),
+    [
+        (intersection_over_union, "iou"),
+        (generalized_intersection_over_union, "giou"),
+        (distance_intersection_over_union, "diou"),
+        (complete_intersection_over_union, "ciou"),
+    ],
+)
+def test_functional_iou(fn, mode):
+    gen = torch.Generator().manual_seed(2)
+    b1, b2 = _rand_boxes(6, gen), _rand_boxes(6, gen)
+    ref = _closed_form(b1, b2)[mode].float()
+    torch.testing.assert_close(fn(b1, b2, aggregate=False), ref, atol=1e-5, rtol=0)
+    torch.testing.assert_close(fn(b1, b2), ref.diag().mean(), atol=1e-5, rtol=0)
+    thr = fn(b1, b2, iou_threshold=0.3, replacement_val=-5, aggregate=False)
+    torch.testing.assert_close(thr, torch.where(ref < 0.3, torch.full_like(ref, -5.0), ref), atol=1e-5, rtol=0)
+    assert fn(b1[:0], b2[:0]) == 0
+
+
+# ----------------------------------------------------------------------------------------------------------
+# stand-ins for the reference's lazily imported torchvision.ops / pycocotools.mask
+# ----------------------------------------------------------------------------------------------------------
+@pytest.fixture()
+def ref_detection(reference, monkeypatch):
+    tv = types.ModuleType("torchvision")
+    tvops = types.ModuleType("torchvision.ops")
+    tvops.box_convert = bo.box_convert
+    tvops.box_area = bo.box_area
+    tvops.box_iou = lambda a, b: bo._eager(a, b, "iou")
+    tvops.generalized_box_iou = lambda a, b: bo._eager(a, b, "giou")
+    tvops.distance_box_iou = lambda a, b: bo._eager(a, b, "diou")
+    tvops.complete_box_iou = lambda a, b: bo._eager(a, b, "ciou")
+    tv.ops = tvops
+    pc = types.ModuleType("pycocotools")
+    pcm = types.ModuleType("pycocotools.mask")
+
+    def encode(m):
+        r = mu.rle_encode(np.asarray(m))
+        return {"size": r["size"], "counts": r["counts"].encode()}
+
+    def area(rles):
+        if isinstance(rles, dict):
+            return mu.rle_area(rles)
+        return np.array([mu.rle_area(r) for r in rles])
+
+    def iou(d, g, crowd):
+        dm = torch.tensor(np.stack([mu.rle_decode(r) for r in d])) if len(d) else torch.zeros(0, 1, 1)
+        gm = torch.tensor(np.stack([mu.rle_decode(r) for r in g])) if len(g) else torch.zeros(0, 1, 1)
+        return mu.mask_iou(dm, gm, torch.tensor(crowd, dtype=torch.bool)).numpy()
+
+    pcm.encode, pcm.area, pcm.iou = encode, area, iou
+    pc.mask = pcm
+    for name, mod in (("torchvision", tv), ("torchvision.ops", tvops), ("pycocotools", pc), ("pycocotools.mask", pcm)):
+        monkeypatch.setitem(sys.modules, name, mod)
+    import importlib
+
+    legacy = importlib.import_module("torchmetrics.detection._mean_ap")
+    ref_iou = importlib.import_module("torchmetrics.detection.iou")
+    monkeypatch.setattr(legacy, "_PYCOCOTOOLS_AVAILABLE", True)
+    monkeypatch.setattr(legacy, "_TORCHVISION_GREATER_EQUAL_0_8", True)
+    monkeypatch.setattr(ref_iou, "_TORCHVISION_GREATER_EQUAL_0_8", True)
+    mods = {"legacy": legacy, "iou": ref_iou}
+    for n in ("giou", "diou", "ciou"):
+        m = importlib.import_module(f"torchmetrics.detection.{n}")
+        for attr in ("_TORCHVISION_GREATER_EQUAL_0_8", "_TORCHVISION_GREATER_EQUAL_0_13"):
+            if hasattr(m, attr):
+                monkeypatch.setattr(m, attr, True)
+        mods[n] = m
+    return mods
+
+
+def _random_detection_batch(
+    gen, n_img, n_cls=4, crowd_p=0.0, with_area=False, max_gt=6, extra_fp=3, tie_scores=False, min_wh=1.0
+):
+    preds, target = [], []
+    for _ in range(n_img):
+        ng = int(torch.randint(0, max_gt + 1, (1,), generator=gen))
+        gtb = _rand_boxes(ng, gen, min_wh=min_wh)
+        gtl = torch.randint(0, n_cls, (ng,), generator=gen)
+        t = {"boxes": gtb, "labels": gtl}
+        if crowd_p:
+            t["iscrowd"] = (torch.rand(ng, generator=gen) < crowd_p).long()
+        if with_area:
+            t["area"] = torch.where(torch.rand(ng, generator=gen) < 0.5, torch.rand(ng, generator=gen) * 20000, torch.zeros(ng))
+        keep = torch.rand(ng, generator=gen) < 0.8
+        jit = gtb[keep] + torch.randn(int(keep.sum()), 4, generator=gen) * 8
+        jit[:, 2:] = torch.maximum(jit[:, 2:], jit[:, :2] + 1)
+        nfp = int(torch.randint(0, extra_fp + 1, (1,), generator=gen))
+        db = torch.cat([jit, _rand_boxes(nfp, gen, min_wh=min_wh)])
+        dl = torch.cat([gtl[keep], torch.randint(0, n_cls, (nfp,), generator=gen)])
+        sc = torch.rand(len(db), generator=gen)
+        if tie_scores:
+            sc = (sc * 4).round() / 4
+        preds.append({"boxes": db, "scores": sc, "labels": dl})
+        target.append(t)
+    return preds, target
+
+
+_KEYS = ("map", "map_50", "map_75", "map_small", "map_medium", "map_large",
+         "mar_1", "mar_10", "mar_100", "mar_small", "mar_medium", "mar_large")
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+@pytest.mark.parametrize("class_metrics", [False, True])
+def test_map_vs_reference_legacy(ref_detection, seed, class_metrics):
+    # large boxes only (no area-range ignores): the legacy evaluator never matches area-ignored ground truth,
+    # which COCO does, so outside this regime the two legitimately differ (exact COCO semantics are pinned by the
+    # oracle tests below)
+    gen = torch.Generator().manual_seed(seed)
+    # recall thresholds that no k/n recall hits exactly: the legacy evaluator computes recall in fp32, COCO in fp64
+    batches = [_random_detection_batch(gen, 5, min_wh=100.0) for _ in range(3)]
+    rec = [(i + 0.37) / 101 for i in range(101)]
+    ours = MeanAveragePrecision(class_metrics=class_metrics, rec_thresholds=rec)
+    ref = ref_detection["legacy"].MeanAveragePrecision(class_metrics=class_metrics, rec_thresholds=rec)
+    for p, t in batches:
+        ours.update(p, t)
+        ref.update(p, t)
+    a, b = ours.compute(), ref.compute()
+    for k in _KEYS:
+        torch.testing.assert_close(a[k].float(), b[k].float(), atol=1e-6, rtol=0, msg=k)
+    if class_metrics:
+        torch.testing.assert_close(a["map_per_class"], b["map_per_class"].float(), atol=1e-6, rtol=0)
+        torch.testing.assert_close(a["mar_100_per_class"], b["mar_100_per_class"].float(), atol=1e-6, rtol=0)
+    assert a["classes"].tolist() == b["classes"].tolist()
+
+
+def _oracle_inputs(batches, box_format="xyxy"):
+    dets, gts, n = [], [], 0
+    for preds, target in batches:
+        for p, t in zip(preds, target):
+            db = bo.box_convert(p["boxes"].double(), box_format, "xywh") if len(p["boxes"]) else p["boxes"].double()
+            gb = bo.box_convert(t["boxes"].double(), box_format, "xywh") if len(t["boxes"]) else t["boxes"].double()
+            for j in range(len(db)):
+                box = db[j].tolist()
+                dets.append(dict(img=n, cat=int(p["labels"][j]), box=box, score=float(p["scores"][j]), area=box[2] * box[3]))
+            crowd = t.get("iscrowd", torch.zeros(len(gb)))
+            area = t.get("area", torch.zeros(len(gb)))
+            for j in range(len(gb)):
+                box = gb[j].tolist()
+                a = float(area[j]) if float(area[j]) > 0 else box[2] * box[3]
+                gts.append(dict(img=n, cat=int(t["labels"][j]), box=box, crowd=int(crowd[j]), area=a))
+            n += 1
+    return dets, gts, n
+
+
+@pytest.mark.parametrize("seed", [3, 4])
+@pytest.mark.parametrize("max_dets", [[1, 10, 100], [1, 2, 3]])
+def test_map_vs_coco_oracle_crowd_area(seed, max_dets):
+    gen = torch.Generator().manual_seed(seed)
+    batches = [_random_detection_batch(gen, 6, crowd_p=0.25, with_area=True, tie_scores=True) for _ in range(2)]
+    metric = MeanAveragePrecision(max_detection_thresholds=max_dets, extended_summary=True, class_metrics=True)
+    for p, t in batches:
+        metric.update(p, t)
+    res = metric.compute()
+    dets, gts, n = _oracle_inputs(batches)
+    cats = sorted({d["cat"] for d in dets} | {g["cat"] for g in gts})
+    prec, rec, ious = oracle.coco_eval(dets, gts, cats, n, metric.iou_thresholds, metric.rec_thresholds, max_dets)
+    np.testing.assert_allclose(res["precision"].numpy(), prec, atol=1e-12)
+    np.testing.assert_allclose(res["recall"].numpy(), rec, atol=1e-12)
+    stats = oracle.summarize(prec, rec, metric.iou_thresholds, max_dets)
+    for k, v in zip(_KEYS, stats):
+        assert abs(float(res[k]) - v) < 1e-6, k
+    for (i, k), mat in ious.items():
+        got = res["ious"][(i, cats[k])]
+        if mat.size == 0:
+            assert isinstance(got, list) and got == []
+        else:
+            np.testing.assert_allclose(got.double().numpy(), mat, atol=1e-6)
+    for k in range(len(cats)):
+        st = oracle.summarize(prec[:, :, k : k + 1], rec[:, k : k + 1], metric.iou_thresholds, max_dets)
+        assert abs(float(res["map_per_class"][k]) - st[0]) < 1e-6
+        assert abs(float(res["mar_100_per_class"][k]) - st[8]) < 1e-6
+
+
+@pytest.mark.parametrize("box_format", ["xywh", "cxcywh"])
+def test_map_box_formats(box_format):
+    gen = torch.Generator().manual_seed(5)
+    preds, target = _random_detection_batch(gen, 6)
+    ours = MeanAveragePrecision()
+    ours.update(preds, target)
+    conv = lambda lst: [dict(d, boxes=bo.box_convert(d["boxes"], "xyxy", box_format)) for d in lst]  # noqa: E731
+    other = MeanAveragePrecision(box_format=box_format)
+    other.update(conv(preds), conv(target))
+    a, b = ours.compute(), other.compute()
+    for k in _KEYS:
+        torch.testing.assert_close(a[k], b[k], atol=1e-5, rtol=0)
+
+
+def test_map_reference_cases():
+    preds = [dict(boxes=torch.tensor([[258.0, 41.0, 606.0, 285.0]]), scores=torch.tensor([0.536]), labels=torch.tensor([0]))]
+    target = [dict(boxes=torch.tensor([[214.0, 41.0, 562.0, 285.0]]), labels=torch.tensor([0]))]
+    assert round(MeanAveragePrecision()(preds, target)["map"].item(), 5) == 0.6
+    # pycocotools evaluates stats[0] at maxDets=100; faster_coco_eval at the largest threshold
+    assert MeanAveragePrecision(max_detection_thresholds=[1, 10, 1000])(preds, target)["map"].item() == -1
+    fast = MeanAveragePrecision(max_detection_thresholds=[1, 10, 1000], backend="faster_coco_eval")
+    assert round(fast(preds, target)["map"].item(), 5) == 0.6
+    for fmt, iou_e, map_e in [("xyxy", 0.25, 1), ("xywh", 0.143, 0.0), ("cxcywh", 0.143, 0.0)]:
+        m = MeanAveragePrecision(box_format=fmt, iou_thresholds=[0.2], extended_summary=True)
+        m.update(
+            [{"boxes": torch.tensor([[0.5, 0.5, 1, 1]]), "scores": torch.tensor([1.0]), "labels": torch.tensor([0])}],
+            [{"boxes": torch.tensor([[0, 0, 1, 1]]), "labels": torch.tensor([0])}],
+        )
+        r = m.compute()
+        assert r["map"].item() == map_e
+        assert round(float(r["ious"][(0, 0)]), 3) == iou_e
+    # missing prediction / missing ground truth keep map below one
+    gts = [{"boxes": torch.tensor([[10.0, 20, 15, 25]]), "labels": torch.tensor([0])}] * 2
+    prs = [{"boxes": torch.tensor([[10.0, 20, 15, 25]]), "scores": torch.tensor([0.9]), "labels": torch.tensor([0])},
+           {"boxes": torch.tensor([]), "scores": torch.tensor([]), "labels": torch.tensor([], dtype=torch.long)}]
+    assert MeanAveragePrecision()(prs, gts)["map"] < 1
+    gts2 = [gts[0], {"boxes": torch.tensor([]), "labels": torch.tensor([], dtype=torch.long)}]
+    prs2 = [prs[0], {"boxes": torch.tensor([[10.0, 20, 15, 25]]), "scores": torch.tensor([0.95]), "labels": torch.tensor([0])}]
+    assert MeanAveragePrecision()(prs2, gts2)["map"] < 1
+    MeanAveragePrecision().compute()  # empty metric
+
+
+def test_map_warning_and_errors():
+    preds = [{"boxes": torch.tensor([[0.5, 0.5, 1, 1]]).repeat(101, 1), "scores": torch.ones(101), "labels": torch.zeros(101, dtype=torch.long)}]
+    target = [{"boxes": torch.tensor([[0.0, 0, 1, 1]]), "labels": torch.tensor([0])}]
+    with pytest.warns(UserWarning, match="Encountered more than 100 detections in a single image"):
+        MeanAveragePrecision().update(preds, target)
+    with pytest.raises(ValueError, match="box_format"):
+        MeanAveragePrecision(box_format="xyz")
+    with pytest.raises(ValueError, match="iou_type"):
+        MeanAveragePrecision(iou_type="foo")
+    with pytest.raises(ValueError, match="average"):
+        MeanAveragePrecision(average="weighted")
+    with pytest.raises(ValueError, match="same length"):
+        MeanAveragePrecision().update(preds, target * 2)
+    with pytest.raises(ValueError, match="contain the `scores` key"):
+        MeanAveragePrecision().update([{"boxes": torch.zeros(1, 4), "labels": torch.zeros(1)}], target)
+
+
+@pytest.mark.parametrize("class_metrics", [False, True])
+def test_map_average_argument(class_metrics):
+    gen = torch.Generator().manual_seed(6)
+    preds, target = _random_detection_batch(gen, 8)
+    if class_metrics:
+        p2, t2 = preds, target
+    else:
+        p2 = [dict(d, labels=torch.ones_like(d["labels"])) for d in preds]
+        t2 = [dict(d, labels=torch.ones_like(d["labels"])) for d in target]
+    macro = MeanAveragePrecision(average="macro", class_metrics=class_metrics)
+    macro.update(p2, t2)
+    micro = MeanAveragePrecision(average="micro", class_metrics=class_metrics)
+    micro.update(preds, target)
+    a, b = macro.compute(), micro.compute()
+    keys = ("map_per_class", "mar_100_per_class") if class_metrics else _KEYS
+    for k in keys:
+        torch.testing.assert_close(a[k], b[k])
+
+
+def test_map_extended_summary_shapes():
+    gen = torch.Generator().manual_seed(7)
+    preds, target = _random_detection_batch(gen, 4, n_cls=6, max_gt=8)
+    m = MeanAveragePrecision(extended_summary=True)
+    m.update(preds, target)
+    r = m.compute()
+    k = len(r["classes"])
+    assert r["precision"].shape == (10, 101, k, 4, 3)
+    assert r["recall"].shape == (10, k, 4, 3)
+    assert len(r["ious"]) == 4 * k
+
+
+# ----------------------------------------------------------------------------------------------------------
+# segmentation
+# ----------------------------------------------------------------------------------------------------------
+def _random_masks(n, gen, h=24, w=20):
+    out = torch.zeros(n, h, w, dtype=torch.bool)
+    for i in range(n):
+        y0, x0 = int(torch.randint(0, h - 4, (1,), generator=gen)), int(torch.randint(0, w - 4, (1,), generator=gen))
+        y1 = y0 + int(torch.randint(3, h - y0 + 1, (1,), generator=gen))
+        x1 = x0 + int(torch.randint(3, w - x0 + 1, (1,), generator=gen))
+        out[i, y0:y1, x0:x1] = True
+        out[i] &= torch.rand(h, w, generator=gen) < 0.9
+    return out
+
+
+def test_rle_roundtrip_and_area():
+    gen = torch.Generator().manual_seed(8)
+    for m in _random_masks(5, gen, 37, 23):
+        rle = mu.rle_encode(m)
+        assert mu.rle_area(rle) == int(m.sum())
+        np.testing.assert_array_equal(mu.rle_decode(rle), m.numpy().astype(np.uint8))
+    assert mu.rle_encode(np.zeros((3, 4), np.uint8))["counts"] == mu._counts_to_string([12])
+    full = mu.rle_encode(np.ones((3, 4), np.uint8))
+    assert mu._string_to_counts(full["counts"]) == [0, 12]
+
+
+def test_polygon_rasterisation():
+    # axis-aligned rectangle polygon: COCO rasterises pixel centres inside the outline
+    mask = mu.poly_to_mask([[2.0, 3.0, 10.0, 3.0, 10.0, 8.0, 2.0, 8.0]], 12, 14)
+    assert mask.shape == (12, 14)
+    assert mask[3:8, 2:10].all() and mask.sum() == 5 * 8
+    tri = mu.poly_to_mask([[0.0, 0.0, 10.0, 0.0, 0.0, 10.0]], 12, 12)
+    assert tri[0, 0] == 1 and tri[9, 9] == 0 and 40 < tri.sum() < 60
+
+
+def test_mask_iou_cpu_vs_loops():
+    gen = torch.Generator().manual_seed(9)
+    d, g = _random_masks(4, gen), _random_masks(3, gen)
+    crowd = torch.tensor([False, True, False])
+    got = mu.mask_iou(d, g, crowd)
+    for i in range(4):
+        for j in range(3):
+            inter = float((d[i] & g[j]).sum())
+            u = float(d[i].sum()) if crowd[j] else float((d[i] | g[j]).sum())
+            assert abs(got[i, j].item() - inter / u) < 1e-12
+    bits = mu.pack_bits(d)
+    assert bits.shape == (4, math.ceil(24 * 20 / 64))
+
+
+def test_map_segm_vs_oracle():
+    gen = torch.Generator().manual_seed(10)
+    preds, target = [], []
+    for _ in range(5):
+        ng, nd = int(torch.randint(0, 4, (1,), generator=gen)), int(torch.randint(0, 5, (1,), generator=gen))
+        target.append({"masks": _random_masks(ng, gen), "labels": torch.randint(0, 2, (ng,), generator=gen),
+                       "iscrowd": (torch.rand(ng, generator=gen) < 0.2).long()})
+        preds.append({"masks": _random_masks(nd, gen), "scores": torch.rand(nd, generator=gen),
+                      "labels": torch.randint(0, 2, (nd,), generator=gen)})
+    m = MeanAveragePrecision(iou_type="segm", extended_summary=True, iou_thresholds=[0.1, 0.3, 0.5])
+    m.update(preds, target)
+    res = m.compute()
+    # oracle: masks IoU; images without ground truth are excluded (reference COCO export skips them in segm mode)
+    dets, gts = [], []
+    for i, (p, t) in enumerate(zip(preds, target)):
+        if len(t["labels"]) == 0:
+            continue
+        for j in range(len(p["labels"])):
+            dets.append(dict(img=i, cat=int(p["labels"][j]), mask=p["masks"][j], score=float(p["scores"][j]),
+                             area=float(p["masks"][j].sum()), box=None))
+        for j in range(len(t["labels"])):
+            gts.append(dict(img=i, cat=int(t["labels"][j]), mask=t["masks"][j], crowd=int(t["iscrowd"][j]),
+                            area=float(t["masks"][j].sum()), box=None))
+
+    def iou_fn(d, g):
+        if not d or not g:
+            return np.zeros((len(d), len(g)))
+        return mu.mask_iou(torch.stack([x["mask"] for x in d]), torch.stack([x["mask"] for x in g]),
+                           torch.tensor([x["crowd"] for x in g], dtype=torch.bool)).numpy()
+
+    cats = sorted(set(torch.cat([p["labels"] for p in preds] + [t["labels"] for t in target]).tolist()))
+    prec, rec, _ = oracle.coco_eval(dets, gts, cats, 5, m.iou_thresholds, m.rec_thresholds, [1, 10, 100], iou_fn)
+    np.testing.assert_allclose(res["precision"].numpy(), prec, atol=1e-12)
+    np.testing.assert_allclose(res["recall"].numpy(), rec, atol=1e-12)
+
+
+def test_map_bbox_and_segm_prefixes():
+    gen = torch.Generator().manual_seed(11)
+    masks = _random_masks(3, gen)
+    boxes = torch.tensor([[0.0, 0, 10, 10], [2, 2, 8, 9], [5, 5, 15, 18]])
+    preds = [{"boxes": boxes, "masks": masks, "scores": torch.tensor([0.9, 0.5, 0.7]), "labels": torch.tensor([0, 1, 0])}]
+    target = [{"boxes": boxes, "masks": masks, "labels": torch.tensor([0, 1, 0])}]
+    r = MeanAveragePrecision(iou_type=("bbox", "segm"))(preds, target)
+    assert r["bbox_map"].item() == pytest.approx(1.0) and r["segm_map"].item() == pytest.approx(1.0)
+    assert "bbox_map_per_class" in r and "segm_mar_100_per_class" in r
+
+
+def test_coco_json_roundtrip(tmp_path):
+    gen = torch.Generator().manual_seed(12)
+    preds, target = _random_detection_batch(gen, 4)
+    for t in target:
+        t["iscrowd"] = torch.zeros_like(t["labels"])
+    m = MeanAveragePrecision(box_format="xyxy")
+    m.update(preds, target)
+    name = str(tmp_path / "tm")
+    m.tm_to_coco(name)
+    with open(f"{name}_target.json") as f:
+        ds = json.load(f)
+    assert {"images", "annotations", "categories"} <= set(ds)
+    p2, t2 = MeanAveragePrecision.coco_to_tm(f"{name}_preds.json", f"{name}_target.json", iou_type="bbox")
+    m2 = MeanAveragePrecision(box_format="xywh")
+    m2.update(p2, t2)
+    # images without annotations are dropped by coco_to_tm (as in the reference): compare on kept images
+    kept = [i for i, t in enumerate(target) if len(t["labels"])]
+    m3 = MeanAveragePrecision(box_format="xyxy")
+    m3.update([preds[i] for i in kept], [target[i] for i in kept])
+    a, b = m2.compute(), m3.compute()
+    for k in _KEYS:
+        torch.testing.assert_close(a[k], b[k], atol=1e-5, rtol=0)
+
+
+# ----------------------------------------------------------------------------------------------------------
+# IoU modules vs reference modules
+# ----------------------------------------------------------------------------------------------------------
+@pytest.mark.parametrize(
+    ("ours_cls", "ref_name", "ref_cls"),
+    [
+        (IntersectionOverUnion, "iou", "IntersectionOverUnion"),
+        (GeneralizedIntersectionOverUnion, "giou", "GeneralizedIntersectionOverUnion"),
+        (DistanceIntersectionOverUnion, "diou", "DistanceIntersectionOverUnion"),
+        (CompleteIntersectionOverUnion, "ciou", "CompleteIntersectionOverUnion"),
+    ],
+)
+@pytest.mark.parametrize("respect_labels", [True, False])
+@pytest.mark.parametrize("iou_threshold", [None, 0.2])
+def test_iou_modules_vs_reference(ref_detection, ours_cls, ref_name, ref_cls, respect_labels, iou_threshold):
+    gen = torch.Generator().manual_seed(13)
+    batches = [_random_detection_batch(gen, 3, max_gt=4, extra_fp=2) for _ in range(2)]
+    kw = dict(class_metrics=True, respect_labels=respect_labels, iou_threshold=iou_threshold)
+    ours = ours_cls(**kw)
+    ref = getattr(ref_detection[ref_name], ref_cls)(**kw)
+    for p, t in batches:
+        p = [{k: v for k, v in d.items() if k != "scores"} for d in p]
+        ours.update(p, t)
+        ref.update(p, t)
+    a, b = ours.compute(), ref.compute()
+    assert set(a) == set(b)
+    for k in a:
+        torch.testing.assert_close(a[k].float(), b[k].float(), atol=1e-5, rtol=0, equal_nan=True, msg=k)
+
+
+# ----------------------------------------------------------------------------------------------------------
+# distributed
+# ----------------------------------------------------------------------------------------------------------
+def _ddp_map_worker(rank, world):
+    gen = torch.Generator().manual_seed(20)
+    batches = [_random_detection_batch(gen, 3, crowd_p=0.2) for _ in range(4)]
+    m = MeanAveragePrecision(class_metrics=True)
+    for b in batches[rank::world]:
+        m.update(*b)
+    return {k: v.tolist() for k, v in m.compute().items()}
+
+
+def test_map_ddp_matches_single_process():
+    from tests.helpers.ddp import run_ddp
+
+    got = run_ddp(_ddp_map_worker)
+    gen = torch.Generator().manual_seed(20)
+    batches = [_random_detection_batch(gen, 3, crowd_p=0.2) for _ in range(4)]
+    m = MeanAveragePrecision(class_metrics=True)
+    for b in batches:
+        m.update(*b)
+    exp = m.compute()
+    for res in got:
+        for k, v in exp.items():
+            np.testing.assert_allclose(np.asarray(res[k], dtype=np.float64), v.double().numpy(), atol=1e-6, err_msg=k)

@@ -1,0 +1,16 @@
+"""Detection metrics (reference ``detection/__init__.py``): mAP/mAR, IoU family, panoptic quality."""
+from torchmetrics_forked_amd.detection.iou import (
+    CompleteIntersectionOverUnion,
+    DistanceIntersectionOverUnion,
+    GeneralizedIntersectionOverUnion,
+    IntersectionOverUnion,
+)
+from torchmetrics_forked_amd.detection.mean_ap import MeanAveragePrecision
+
+__all__ = [
+    "CompleteIntersectionOverUnion",
+    "DistanceIntersectionOverUnion",
+    "GeneralizedIntersectionOverUnion",
+    "IntersectionOverUnion",
+    "MeanAveragePrecision",
+]
