@@ -112,3 +112,20 @@ def test_iou_modules_gpu(cls_name):
     a, c = gpu.compute(), cpu.compute()
     for k in c:
         torch.testing.assert_close(a[k].cpu(), c[k], atol=2e-5, rtol=0, msg=k)
+
+
+@pytest.mark.parametrize("modified", [False, True])
+def test_panoptic_quality_gpu_matches_cpu(modified):
+    from torchmetrics_forked_amd.functional.detection import modified_panoptic_quality, panoptic_quality
+
+    g = torch.Generator().manual_seed(3)
+    cats = torch.tensor([0, 1, 6, 7])
+    def rand():
+        c = cats[torch.randint(0, 4, (4, 32, 32), generator=g)].repeat_interleave(4, 1).repeat_interleave(4, 2)
+        i = torch.randint(0, 3, (4, 32, 32), generator=g).repeat_interleave(4, 1).repeat_interleave(4, 2)
+        return torch.stack([c, i], -1)
+    p, t = rand(), rand()
+    fn = modified_panoptic_quality if modified else panoptic_quality
+    a = fn(p.cuda(), t.cuda(), things={0, 1}, stuffs={6, 7})
+    b = fn(p, t, things={0, 1}, stuffs={6, 7})
+    torch.testing.assert_close(a.cpu(), b, atol=1e-12, rtol=0)

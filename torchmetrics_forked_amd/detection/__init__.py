@@ -6,6 +6,7 @@ from torchmetrics_forked_amd.detection.iou import (
     IntersectionOverUnion,
 )
 from torchmetrics_forked_amd.detection.mean_ap import MeanAveragePrecision
+from torchmetrics_forked_amd.detection.panoptic_qualities import ModifiedPanopticQuality, PanopticQuality
 
 __all__ = [
     "CompleteIntersectionOverUnion",
@@ -13,4 +14,6 @@ __all__ = [
     "GeneralizedIntersectionOverUnion",
     "IntersectionOverUnion",
     "MeanAveragePrecision",
+    "ModifiedPanopticQuality",
+    "PanopticQuality",
 ]
