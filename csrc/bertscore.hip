@@ -1,0 +1,206 @@
+// BERTScore greedy matching on matrix cores.
+//
+// For every sentence pair b:  S_b = P_b · R_bᵀ  (cosine similarities of L2-normalised token embeddings) and the
+// metric needs only   rowmax[b, i] = max_j S_b[i, j]   and   colmax[b, j] = max_i S_b[i, j].
+// The reference materialises the whole [B, Lp, Lr] similarity tensor (and moves embeddings to the CPU).  Here a
+// 256-thread block computes one 64 × 64 tile of S_b with MFMA (4 waves × 2 × 2 tiles of 16 × 16), never writes it,
+// and folds it straight into the row / column maxima with 16-lane shuffles + one order-preserving integer
+// atomicMax per row / column and tile.
+//   * bf16 / fp16 embeddings: v_mfma_f32_16x16x32_{bf16,f16} (K = 32 per instruction, fp32 accumulation);
+//   * fp32 embeddings:        v_mfma_f32_16x16x4_f32 (exact fp32 products, fp32 accumulation).
+// A and B fragments are both "8 (or 1) consecutive k of one row", i.e. 16-byte loads straight from the row-major
+// [tokens, D] embeddings (Rᵀ needs no transpose); tiles are re-read from L2 by neighbouring blocks.
+// Grid: (Lr / 64, Lp / 64, B) — tens of thousands of blocks for the BASELINE shape (B = 1024, L = 512).
+#include "common.h"
+
+namespace tmx {
+
+constexpr int kBsTile = 64;
+constexpr int kBsThreads = 256;
+
+using bs_frag8 = __attribute__((ext_vector_type(8))) short;
+using bs_acc4 = __attribute__((ext_vector_type(4))) float;
+
+__device__ __forceinline__ int ordered_bits(float f) {
+  const int i = __float_as_int(f);
+  return i >= 0 ? i : i ^ 0x7fffffff;
+}
+
+__device__ __forceinline__ float from_ordered(int i) { return __int_as_float(i >= 0 ? i : i ^ 0x7fffffff); }
+
+template <typename T>
+__device__ __forceinline__ bs_frag8 load8(const T* base, int64_t row, int64_t rows, int64_t D, int64_t k) {
+  // 8 consecutive 16-bit values of row `row` starting at k (zero outside the matrix)
+  bs_frag8 v = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (row < rows) {
+    const T* p = base + row * D + k;
+    if ((D & 7) == 0 && k + 8 <= D) {
+      v = *reinterpret_cast<const bs_frag8*>(p);
+    } else {
+      for (int j = 0; j < 8; ++j)
+        if (k + j < D) v[j] = *reinterpret_cast<const short*>(p + j);
+    }
+  }
+  return v;
+}
+
+template <typename T>
+__device__ __forceinline__ bs_acc4 mfma16(bs_frag8 a, bs_frag8 b, bs_acc4 c) {
+  if constexpr (std::is_same<T, __hip_bfloat16>::value) return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+  else return __builtin_amdgcn_mfma_f32_16x16x32_f16(reinterpret_cast<__attribute__((ext_vector_type(8))) _Float16&>(a),
+                                                      reinterpret_cast<__attribute__((ext_vector_type(8))) _Float16&>(b), c, 0, 0, 0);
+}
+
+// Epilogue shared by both paths: acc[mi][ni] is the 16x16 tile at (row0 + 16 mi, col0 + 16 ni) with
+// C mapping col = lane & 15, row = (lane >> 4) * 4 + reg.
+__device__ __forceinline__ void fold_maxima(const bs_acc4 (&acc)[2][2], int64_t row0, int64_t col0, int64_t Lp, int64_t Lr,
+                                            int* __restrict__ rowmax, int* __restrict__ colmax) {
+  const int lane = threadIdx.x % kWave;
+  // row maxima: over the 16 column lanes and both column fragments
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float v = -INFINITY;
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni) {
+        const int64_t col = col0 + 16 * ni + (lane & 15);
+        if (col < Lr) v = fmaxf(v, acc[mi][ni][r]);
+      }
+#pragma unroll
+      for (int off = 8; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, kWave));
+      const int64_t row = row0 + 16 * mi + (lane >> 4) * 4 + r;
+      if ((lane & 15) == 0 && row < Lp && v > -INFINITY) atomicMax(rowmax + row, ordered_bits(v));
+    }
+  }
+  // column maxima: over the 4 registers, the 4 lane groups and both row fragments
+#pragma unroll
+  for (int ni = 0; ni < 2; ++ni) {
+    float v = -INFINITY;
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t row = row0 + 16 * mi + (lane >> 4) * 4 + r;
+        if (row < Lp) v = fmaxf(v, acc[mi][ni][r]);
+      }
+    v = fmaxf(v, __shfl_xor(v, 16, kWave));
+    v = fmaxf(v, __shfl_xor(v, 32, kWave));
+    const int64_t col = col0 + 16 * ni + (lane & 15);
+    if (lane < 16 && col < Lr && v > -INFINITY) atomicMax(colmax + col, ordered_bits(v));
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kBsThreads) void greedy_match_half_kernel(const T* __restrict__ P, const T* __restrict__ R, int64_t Lp, int64_t Lr,
+                                                                       int64_t D, int* __restrict__ rowmax, int* __restrict__ colmax) {
+  const int64_t b = blockIdx.z;
+  const T* Pb = P + b * Lp * D;
+  const T* Rb = R + b * Lr * D;
+  const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
+  const int64_t row0 = static_cast<int64_t>(blockIdx.y) * kBsTile + (wave >> 1) * 32;
+  const int64_t col0 = static_cast<int64_t>(blockIdx.x) * kBsTile + (wave & 1) * 32;
+  bs_acc4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = bs_acc4{0.f, 0.f, 0.f, 0.f};
+  const int kl = 8 * (lane >> 4);
+  for (int64_t k0 = 0; k0 < D; k0 += 32) {
+    bs_frag8 a[2], bb[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      a[i] = load8<T>(Pb, row0 + 16 * i + (lane & 15), Lp, D, k0 + kl);
+      bb[i] = load8<T>(Rb, col0 + 16 * i + (lane & 15), Lr, D, k0 + kl);
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = mfma16<T>(a[i], bb[j], acc[i][j]);
+  }
+  fold_maxima(acc, row0, col0, Lp, Lr, rowmax + b * Lp, colmax + b * Lr);
+}
+
+__global__ __launch_bounds__(kBsThreads) void greedy_match_f32_kernel(const float* __restrict__ P, const float* __restrict__ R, int64_t Lp,
+                                                                      int64_t Lr, int64_t D, int* __restrict__ rowmax, int* __restrict__ colmax) {
+  const int64_t b = blockIdx.z;
+  const float* Pb = P + b * Lp * D;
+  const float* Rb = R + b * Lr * D;
+  const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
+  const int64_t row0 = static_cast<int64_t>(blockIdx.y) * kBsTile + (wave >> 1) * 32;
+  const int64_t col0 = static_cast<int64_t>(blockIdx.x) * kBsTile + (wave & 1) * 32;
+  bs_acc4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = bs_acc4{0.f, 0.f, 0.f, 0.f};
+  const int kl = lane >> 4;  // 16x16x4: lane holds A[row lane&15][k = lane>>4], B[k = lane>>4][col lane&15]
+  for (int64_t k0 = 0; k0 < D; k0 += 4) {
+    const int64_t k = k0 + kl;
+    float a[2], bb[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int64_t pr = row0 + 16 * i + (lane & 15), rr = col0 + 16 * i + (lane & 15);
+      a[i] = (pr < Lp && k < D) ? Pb[pr * D + k] : 0.f;
+      bb[i] = (rr < Lr && k < D) ? Rb[rr * D + k] : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i], bb[j], acc[i][j], 0, 0, 0);
+  }
+  fold_maxima(acc, row0, col0, Lp, Lr, rowmax + b * Lp, colmax + b * Lr);
+}
+
+// P [B, Lp, D], R [B, Lr, D] (same float dtype) -> (rowmax [B, Lp] fp32, colmax [B, Lr] fp32)
+std::tuple<at::Tensor, at::Tensor> bert_greedy_match(const at::Tensor& P_in, const at::Tensor& R_in) {
+  TORCH_CHECK(P_in.is_cuda() && R_in.is_cuda(), "bert_greedy_match: expected GPU tensors");
+  TORCH_CHECK(P_in.dim() == 3 && R_in.dim() == 3 && P_in.size(0) == R_in.size(0) && P_in.size(2) == R_in.size(2),
+              "bert_greedy_match: expected [B, Lp, D] and [B, Lr, D]");
+  TORCH_CHECK(P_in.scalar_type() == R_in.scalar_type(), "bert_greedy_match: dtype mismatch");
+  const at::DeviceGuard guard(P_in.device());
+  auto P = P_in.contiguous(), R = R_in.contiguous();
+  const int64_t B = P.size(0), Lp = P.size(1), Lr = R.size(1), D = P.size(2);
+  TORCH_CHECK(B <= 65535, "bert_greedy_match: at most 65535 pairs per call");
+  auto opts = P.options().dtype(at::kInt);
+  // order-preserving encoding of -inf as the identity of max
+  const int neg_inf_bits = static_cast<int>(0xff800000u ^ 0x7fffffffu);
+  auto rowmax = at::full({B, Lp}, neg_inf_bits, opts);
+  auto colmax = at::full({B, Lr}, neg_inf_bits, opts);
+  if (B == 0 || Lp == 0 || Lr == 0) {
+    return {rowmax.to(at::kFloat).fill_(-INFINITY), colmax.to(at::kFloat).fill_(-INFINITY)};
+  }
+  dim3 grid(static_cast<unsigned>((Lr + kBsTile - 1) / kBsTile), static_cast<unsigned>((Lp + kBsTile - 1) / kBsTile),
+            static_cast<unsigned>(B));
+  switch (P.scalar_type()) {
+    case at::kBFloat16:
+      hipLaunchKernelGGL(greedy_match_half_kernel<__hip_bfloat16>, grid, kBsThreads, 0, stream(),
+                         reinterpret_cast<const __hip_bfloat16*>(P.data_ptr()), reinterpret_cast<const __hip_bfloat16*>(R.data_ptr()),
+                         Lp, Lr, D, rowmax.data_ptr<int>(), colmax.data_ptr<int>());
+      break;
+    case at::kHalf:
+      hipLaunchKernelGGL(greedy_match_half_kernel<__half>, grid, kBsThreads, 0, stream(), reinterpret_cast<const __half*>(P.data_ptr()),
+                         reinterpret_cast<const __half*>(R.data_ptr()), Lp, Lr, D, rowmax.data_ptr<int>(), colmax.data_ptr<int>());
+      break;
+    case at::kFloat:
+      hipLaunchKernelGGL(greedy_match_f32_kernel, grid, kBsThreads, 0, stream(), P.data_ptr<float>(), R.data_ptr<float>(), Lp, Lr, D,
+                         rowmax.data_ptr<int>(), colmax.data_ptr<int>());
+      break;
+    default:
+      TORCH_CHECK(false, "bert_greedy_match: unsupported dtype ", P.scalar_type());
+  }
+  TMX_LAUNCH_CHECK();
+  // decode the ordered integers back to floats (elementwise, on device)
+  auto decode = [](const at::Tensor& bits) {
+    auto neg = bits.lt(0);
+    auto raw = at::where(neg, at::bitwise_xor(bits, 0x7fffffff), bits);
+    return raw.view(at::kFloat);
+  };
+  return {decode(rowmax), decode(colmax)};
+}
+
+}  // namespace tmx
+
+TORCH_LIBRARY_FRAGMENT(tmx, m) { m.def("bert_greedy_match(Tensor preds_emb, Tensor target_emb) -> (Tensor, Tensor)"); }
+
+TORCH_LIBRARY_IMPL(tmx, CUDA, m) { m.impl("bert_greedy_match", &tmx::bert_greedy_match); }

@@ -1,0 +1,21 @@
+"""Character error rate (API parity: reference ``functional/text/cer.py``)."""
+from typing import List, Tuple, Union
+
+from torch import Tensor
+
+from torchmetrics_forked_amd.functional.text._asr import _asr_stats
+
+
+def _cer_update(preds: Union[str, List[str]], target: Union[str, List[str]]) -> Tuple[Tensor, Tensor]:
+    errors, tl, _, _ = _asr_stats(preds, target, chars=True)
+    return errors, tl
+
+
+def _cer_compute(errors: Tensor, total: Tensor) -> Tensor:
+    return errors / total
+
+
+def char_error_rate(preds: Union[str, List[str]], target: Union[str, List[str]]) -> Tensor:
+    """Character-level edit operations divided by the number of reference characters."""
+    errors, total = _cer_update(preds, target)
+    return _cer_compute(errors, total)

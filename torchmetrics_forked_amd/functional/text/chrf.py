@@ -1,0 +1,192 @@
+"""chrF / chrF++ (API parity: reference ``functional/text/chrf.py``; Popović 2015/2017, sacrebleu semantics).
+
+Character and word n-gram overlaps of every (hypothesis, reference) pair come from the native
+``tmx::ngram_overlap`` op; the per-order F-scores, best-reference selection and corpus totals are vectorised fp32
+tensor math with the same operation order as the reference (so sentence scores and tie-breaks are identical)."""
+from typing import Dict, List, Optional, Sequence, Tuple, Union
+
+import torch
+from torch import Tensor, tensor
+
+from torchmetrics_forked_amd import ops
+from torchmetrics_forked_amd.functional.text.helper import _pack, _validate_inputs, _Vocab
+
+_EPS_SMOOTHING = tensor(1e-16)
+_PUNCTUATIONS = set("!\"#$%&'()*+,-./:;<=>?@[\\]^_`{|}~")
+
+
+def _prepare_n_grams_dicts(n_char_order: int, n_word_order: int) -> Tuple[Dict[int, Tensor], ...]:
+    c = lambda: {n + 1: tensor(0.0) for n in range(n_char_order)}  # noqa: E731
+    w = lambda: {n + 1: tensor(0.0) for n in range(n_word_order)}  # noqa: E731
+    return c(), w(), c(), w(), c(), w()
+
+
+def _get_characters(sentence: str, whitespace: bool) -> List[str]:
+    return list(sentence) if whitespace else list(sentence.strip().replace(" ", ""))
+
+
+def _separate_word_and_punctuation(word: str) -> List[str]:
+    if len(word) == 1:
+        return [word]
+    if word[-1] in _PUNCTUATIONS:
+        return [word[:-1], word[-1]]
+    if word[0] in _PUNCTUATIONS:
+        return [word[0], word[1:]]
+    return [word]
+
+
+def _get_words_and_punctuation(sentence: str) -> List[str]:
+    out: List[str] = []
+    for word in sentence.strip().split():
+        out.extend(_separate_word_and_punctuation(word))
+    return out
+
+
+def _order_fscore(match: Tensor, hyp: Tensor, ref: Tensor, beta: float) -> Tensor:
+    """Per-order F-beta in fp32 (columns = orders); mirrors the reference's scalar formula op for op."""
+    zero = torch.zeros((), dtype=torch.float32)
+    p = torch.where(hyp > 0, match / hyp.clamp_min(1e-30), zero)
+    r = torch.where(ref > 0, match / ref.clamp_min(1e-30), zero)
+    den = torch.maximum(beta**2 * p + r, _EPS_SMOOTHING)
+    return (1 + beta**2) * p * r / den
+
+
+def _seq_sum(f: Tensor) -> Tensor:
+    """Left-to-right fp32 sum over the last dim (python ``sum`` order)."""
+    acc = torch.zeros(f.shape[:-1], dtype=torch.float32)
+    for k in range(f.shape[-1]):
+        acc = acc + f[..., k]
+    return acc
+
+
+def _fscore_from_stats(mc: Tensor, hc: Tensor, rc: Tensor, mw: Tensor, hw: Tensor, rw: Tensor, n_order: float, beta: float) -> Tensor:
+    return (_seq_sum(_order_fscore(mc, hc, rc, beta)) + _seq_sum(_order_fscore(mw, hw, rw, beta))) / tensor(n_order)
+
+
+def _overlap(hyps: List[List], refs: List[List[List]], n: int) -> Tuple[Tensor, Tensor, Tensor]:
+    if n == 0:
+        nr = sum(len(r) for r in refs)
+        return torch.zeros(nr, 0), torch.zeros(len(hyps), 0), torch.zeros(nr, 0)
+    vocab = _Vocab()
+    h, h_off = _pack(hyps, vocab)
+    r, r_off = _pack([x for rs in refs for x in rs], vocab)
+    groups = torch.tensor([0] + [len(rs) for rs in refs], dtype=torch.long).cumsum(0)
+    m, ht, rt = torch.ops.tmx.ngram_overlap(h, h_off, r, r_off, groups, n)
+    return m.float(), ht.float(), rt.float()
+
+
+def _chrf_batch(
+    preds: Union[str, Sequence[str]],
+    target: Union[Sequence[str], Sequence[Sequence[str]]],
+    n_char_order: int,
+    n_word_order: int,
+    n_order: float,
+    beta: float,
+    lowercase: bool,
+    whitespace: bool,
+) -> Tuple[Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor]:
+    """Batch totals ``(preds_char [nc], preds_word [nw], target_char, target_word, match_char, match_word)`` (fp32)
+    of the best reference per sentence, plus the sentence scores ``[n]``."""
+    target_corpus, preds = _validate_inputs(target, preds)
+    pairs = list(zip(preds, target_corpus))
+    zc, zw = torch.zeros(n_char_order), torch.zeros(n_word_order)
+    if not pairs:
+        return zc, zw, zc.clone(), zw.clone(), zc.clone(), zw.clone(), torch.zeros(0)
+    ops.require()
+    norm = (lambda s: s.lower()) if lowercase else (lambda s: s)  # noqa: E731
+    hyp_c = [_get_characters(norm(p), whitespace) for p, _ in pairs]
+    hyp_w = [_get_words_and_punctuation(norm(p)) for p, _ in pairs]
+    ref_c = [[_get_characters(norm(t), whitespace) for t in ts] for _, ts in pairs]
+    ref_w = [[_get_words_and_punctuation(norm(t)) for t in ts] for _, ts in pairs]
+    mc, hc, rc = _overlap(hyp_c, ref_c, n_char_order)
+    mw, hw, rw = _overlap(hyp_w, ref_w, n_word_order)
+    owner = torch.repeat_interleave(torch.arange(len(pairs)), torch.tensor([len(ts) for _, ts in pairs]))
+    f = _fscore_from_stats(mc, hc[owner], rc, mw, hw[owner], rw, n_order, beta)  # [R]
+    # best reference per sentence: first strictly-greater score starting from 0 (reference tie / zero rules)
+    best_f = torch.zeros(len(pairs))
+    best_r = torch.full((len(pairs),), -1, dtype=torch.long)
+    for r in range(f.numel()):
+        i = int(owner[r])
+        if f[r] > best_f[i]:
+            best_f[i] = f[r]
+            best_r[i] = r
+    has = best_r >= 0
+    sel = best_r.clamp_min(0)
+    pick = lambda x: torch.where(has[:, None], x[sel], torch.zeros_like(x[sel])).sum(0)  # noqa: E731
+    return hc.sum(0), hw.sum(0), pick(rc), pick(rw), pick(mc), pick(mw), best_f
+
+
+def _chrf_score_update(
+    preds: Union[str, Sequence[str]],
+    target: Union[Sequence[str], Sequence[Sequence[str]]],
+    total_preds_char_n_grams: Dict[int, Tensor],
+    total_preds_word_n_grams: Dict[int, Tensor],
+    total_target_char_n_grams: Dict[int, Tensor],
+    total_target_word_n_grams: Dict[int, Tensor],
+    total_matching_char_n_grams: Dict[int, Tensor],
+    total_matching_word_n_grams: Dict[int, Tensor],
+    n_char_order: int,
+    n_word_order: int,
+    n_order: float,
+    beta: float,
+    lowercase: bool,
+    whitespace: bool,
+    sentence_chrf_score: Optional[List[Tensor]] = None,
+) -> Tuple:
+    """Reference-signature update over per-order dicts (used by the functional API)."""
+    pc, pw, tc, tw, mc, mw, sent = _chrf_batch(preds, target, n_char_order, n_word_order, n_order, beta, lowercase, whitespace)
+    dicts = (total_preds_char_n_grams, total_preds_word_n_grams, total_target_char_n_grams,
+             total_target_word_n_grams, total_matching_char_n_grams, total_matching_word_n_grams)
+    for d, v in zip(dicts, (pc, pw, tc, tw, mc, mw)):
+        for n in range(v.numel()):
+            d[n + 1] = d[n + 1] + v[n]
+    if sentence_chrf_score is not None:
+        sentence_chrf_score.extend(s.reshape(1) for s in sent)
+    return (*dicts, sentence_chrf_score)
+
+
+def _dict_vec(d: Dict[int, Tensor], n: int) -> Tensor:
+    return torch.stack([d[k + 1].float().reshape(()) for k in range(n)]) if n else torch.zeros(0)
+
+
+def _chrf_score_compute(
+    total_preds_char_n_grams: Dict[int, Tensor],
+    total_preds_word_n_grams: Dict[int, Tensor],
+    total_target_char_n_grams: Dict[int, Tensor],
+    total_target_word_n_grams: Dict[int, Tensor],
+    total_matching_char_n_grams: Dict[int, Tensor],
+    total_matching_word_n_grams: Dict[int, Tensor],
+    n_order: float,
+    beta: float,
+) -> Tensor:
+    nc, nw = len(total_preds_char_n_grams), len(total_preds_word_n_grams)
+    return _fscore_from_stats(
+        _dict_vec(total_matching_char_n_grams, nc), _dict_vec(total_preds_char_n_grams, nc), _dict_vec(total_target_char_n_grams, nc),
+        _dict_vec(total_matching_word_n_grams, nw), _dict_vec(total_preds_word_n_grams, nw), _dict_vec(total_target_word_n_grams, nw),
+        n_order, beta,
+    )
+
+
+def chrf_score(
+    preds: Union[str, Sequence[str]],
+    target: Sequence[Union[str, Sequence[str]]],
+    n_char_order: int = 6,
+    n_word_order: int = 2,
+    beta: float = 2.0,
+    lowercase: bool = False,
+    whitespace: bool = False,
+    return_sentence_level_score: bool = False,
+) -> Union[Tensor, Tuple[Tensor, Tensor]]:
+    """Corpus chrF (``n_word_order=0``) or chrF++ (``n_word_order=2``)."""
+    if not isinstance(n_char_order, int) or n_char_order < 1:
+        raise ValueError("Expected argument `n_char_order` to be an integer greater than or equal to 1.")
+    if not isinstance(n_word_order, int) or n_word_order < 0:
+        raise ValueError("Expected argument `n_word_order` to be an integer greater than or equal to 0.")
+    if beta < 0:
+        raise ValueError("Expected argument `beta` to be greater than 0.")
+    n_order = float(n_char_order + n_word_order)
+    pc, pw, tc, tw, mc, mw, sent = _chrf_batch(preds, target, n_char_order, n_word_order, n_order, beta, lowercase, whitespace)
+    score = _fscore_from_stats(mc, pc, tc, mw, pw, tw, n_order, beta)
+    if return_sentence_level_score and sent.numel():
+        return score, sent
+    return score

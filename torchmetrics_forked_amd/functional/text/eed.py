@@ -1,0 +1,113 @@
+"""Extended edit distance (API parity: reference ``functional/text/eed.py``; algorithm of Stanchev et al., 2019).
+
+Sentence preprocessing is host-side string work; every (hypothesis, reference) character DP runs in the native
+``tmx::eed_batch`` kernel, then the best reference per hypothesis is a ``min`` over a ``[n, refs]`` table."""
+import re
+import unicodedata
+from typing import List, Literal, Optional, Sequence, Tuple, Union
+
+import torch
+from torch import Tensor, stack, tensor
+
+from torchmetrics_forked_amd import ops
+from torchmetrics_forked_amd.functional.text.helper import _pack_codepoints, _validate_inputs
+
+_EN_PUNCT = ((".", " ."), ("!", " !"), ("?", " ?"), (",", " ,"))
+_EN_RE = (
+    (re.compile(r"\s+"), r" "),
+    (re.compile(r"(\d) ([.,]) (\d)"), r"\1\2\3"),
+    (re.compile(r"(Dr|Jr|Prof|Rev|Gen|Mr|Mt|Mrs|Ms) ."), r"\1."),
+)
+_EN_ABBREV = (("e . g .", "e.g."), ("i . e .", "i.e."), ("U . S .", "U.S."))
+
+
+def _preprocess_en(sentence: str) -> str:
+    if not isinstance(sentence, str):
+        raise ValueError(f"Only strings allowed during preprocessing step, found {type(sentence)} instead")
+    sentence = sentence.rstrip()
+    for a, b in _EN_PUNCT:
+        sentence = sentence.replace(a, b)
+    for pat, rep in _EN_RE:
+        sentence = pat.sub(rep, sentence)
+    for a, b in _EN_ABBREV:
+        sentence = sentence.replace(a, b)
+    return " " + sentence + " "
+
+
+def _preprocess_ja(sentence: str) -> str:
+    if not isinstance(sentence, str):
+        raise ValueError(f"Only strings allowed during preprocessing step, found {type(sentence)} instead")
+    return unicodedata.normalize("NFKC", sentence.rstrip())
+
+
+def _preprocess_sentences(
+    preds: Union[str, Sequence[str]], target: Sequence[Union[str, Sequence[str]]], language: Literal["en", "ja"]
+) -> Tuple[Sequence[str], Sequence[Sequence[str]]]:
+    target, preds = _validate_inputs(hypothesis_corpus=preds, ref_corpus=target)
+    if language == "en":
+        fn = _preprocess_en
+    elif language == "ja":
+        fn = _preprocess_ja
+    else:
+        raise ValueError(f"Expected argument `language` to either be `en` or `ja` but got {language}")
+    return [fn(p) for p in preds], [[fn(r) for r in refs] for refs in target]
+
+
+def _eed_compute(sentence_level_scores: List[Tensor]) -> Tensor:
+    if len(sentence_level_scores) == 0:
+        return tensor(0.0)
+    return sum(sentence_level_scores) / tensor(len(sentence_level_scores))
+
+
+def _eed_update(
+    preds: Union[str, Sequence[str]],
+    target: Sequence[Union[str, Sequence[str]]],
+    language: Literal["en", "ja"] = "en",
+    alpha: float = 2.0,
+    rho: float = 0.3,
+    deletion: float = 0.2,
+    insertion: float = 1.0,
+    sentence_eed: Optional[List[Tensor]] = None,
+) -> List[Tensor]:
+    preds, target = _preprocess_sentences(preds, target, language)
+    if sentence_eed is None:
+        sentence_eed = []
+    if 0 in (len(preds), len(target[0])):
+        return sentence_eed
+    ops.require()
+    hyps, refs, owner = [], [], []
+    for i, (h, rs) in enumerate(zip(preds, target)):
+        for r in rs:
+            hyps.append(h)
+            refs.append(r)
+            owner.append(i)
+    h, h_off = _pack_codepoints(hyps)
+    r, r_off = _pack_codepoints(refs)
+    scores = torch.ops.tmx.eed_batch(h, h_off, r, r_off, ord(" "), float(alpha), float(rho), float(deletion), float(insertion))
+    n = len(list(zip(preds, target)))
+    best = torch.full((n,), float("inf"), dtype=torch.float64).scatter_reduce(
+        0, torch.tensor(owner, dtype=torch.long), scores, reduce="amin"
+    )
+    sentence_eed.extend(tensor(float(v)) for v in best.tolist())
+    return sentence_eed
+
+
+def extended_edit_distance(
+    preds: Union[str, Sequence[str]],
+    target: Sequence[Union[str, Sequence[str]]],
+    language: Literal["en", "ja"] = "en",
+    return_sentence_level_score: bool = False,
+    alpha: float = 2.0,
+    rho: float = 0.3,
+    deletion: float = 0.2,
+    insertion: float = 1.0,
+) -> Union[Tensor, Tuple[Tensor, Tensor]]:
+    """Corpus EED (mean of per-sentence best-reference scores)."""
+    for name, val in zip(["alpha", "rho", "deletion", "insertion"], [alpha, rho, deletion, insertion]):
+        if not isinstance(val, float) or val < 0:
+            raise ValueError(f"Parameter `{name}` is expected to be a non-negative float.")
+    scores = _eed_update(preds, target, language, alpha, rho, deletion, insertion)
+    average = _eed_compute(scores)
+    if return_sentence_level_score:
+        return average, stack(scores)
+    return average

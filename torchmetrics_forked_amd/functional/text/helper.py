@@ -1,0 +1,68 @@
+"""Text-metric helpers (API parity: reference ``functional/text/helper.py``).
+
+Sentences are tokenised on the host and mapped to int64 ids with a per-call vocabulary, then packed as one flat
+buffer + offsets for the native string kernels in ``csrc/text.cpp`` (``tmx::levenshtein_batch`` and friends).
+"""
+from typing import Dict, Hashable, Iterable, List, Sequence, Tuple, Union
+
+import torch
+from torch import Tensor
+
+from torchmetrics_forked_amd import ops
+
+
+class _Vocab:
+    """Token -> dense int id (shared by both sides of a comparison so equal tokens get equal ids)."""
+
+    def __init__(self) -> None:
+        self._ids: Dict[Hashable, int] = {}
+
+    def encode(self, tokens: Iterable[Hashable]) -> List[int]:
+        ids = self._ids
+        return [ids.setdefault(t, len(ids)) for t in tokens]
+
+
+def _pack(seqs: Sequence[Sequence[Hashable]], vocab: _Vocab) -> Tuple[Tensor, Tensor]:
+    flat: List[int] = []
+    off = [0]
+    for s in seqs:
+        flat.extend(vocab.encode(s))
+        off.append(len(flat))
+    return torch.tensor(flat, dtype=torch.long), torch.tensor(off, dtype=torch.long)
+
+
+def _pack_codepoints(strings: Sequence[str]) -> Tuple[Tensor, Tensor]:
+    flat: List[int] = []
+    off = [0]
+    for s in strings:
+        flat.extend(map(ord, s))
+        off.append(len(flat))
+    return torch.tensor(flat, dtype=torch.long), torch.tensor(off, dtype=torch.long)
+
+
+def _levenshtein_many(preds: Sequence[Sequence[Hashable]], targets: Sequence[Sequence[Hashable]]) -> Tensor:
+    """Exact unit-cost edit distances for token-sequence pairs (int64 ``[n]``)."""
+    ops.require()
+    vocab = _Vocab()
+    a, a_off = _pack(preds, vocab)
+    b, b_off = _pack(targets, vocab)
+    return torch.ops.tmx.levenshtein_batch(a, a_off, b, b_off)
+
+
+def _edit_distance(prediction_tokens: List[str], reference_tokens: List[str]) -> int:
+    """Single-pair exact edit distance (reference signature)."""
+    return int(_levenshtein_many([prediction_tokens], [reference_tokens])[0])
+
+
+def _validate_inputs(
+    ref_corpus: Union[Sequence[str], Sequence[Sequence[str]]],
+    hypothesis_corpus: Union[str, Sequence[str]],
+) -> Tuple[Sequence[Sequence[str]], Sequence[str]]:
+    """Normalise ``(references, hypotheses)`` to ``(list of reference lists, list of hypotheses)``."""
+    if isinstance(hypothesis_corpus, str):
+        hypothesis_corpus = [hypothesis_corpus]
+    if all(isinstance(ref, str) for ref in ref_corpus):
+        ref_corpus = [ref_corpus] if len(hypothesis_corpus) == 1 else [[ref] for ref in ref_corpus]  # type: ignore
+    if hypothesis_corpus and all(ref for ref in ref_corpus) and len(ref_corpus) != len(hypothesis_corpus):
+        raise ValueError(f"Corpus has different size {len(ref_corpus)} != {len(hypothesis_corpus)}")
+    return ref_corpus, hypothesis_corpus

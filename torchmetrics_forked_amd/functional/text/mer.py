@@ -1,0 +1,21 @@
+"""Match error rate (API parity: reference ``functional/text/mer.py``)."""
+from typing import List, Tuple, Union
+
+from torch import Tensor
+
+from torchmetrics_forked_amd.functional.text._asr import _asr_stats
+
+
+def _mer_update(preds: Union[str, List[str]], target: Union[str, List[str]]) -> Tuple[Tensor, Tensor]:
+    errors, _, _, ml = _asr_stats(preds, target)
+    return errors, ml
+
+
+def _mer_compute(errors: Tensor, total: Tensor) -> Tensor:
+    return errors / total
+
+
+def match_error_rate(preds: Union[str, List[str]], target: Union[str, List[str]]) -> Tensor:
+    """Edit operations divided by the per-pair maximum of reference / prediction word counts."""
+    errors, total = _mer_update(preds, target)
+    return _mer_compute(errors, total)

@@ -1,0 +1,21 @@
+"""Word error rate (API parity: reference ``functional/text/wer.py``)."""
+from typing import List, Tuple, Union
+
+from torch import Tensor
+
+from torchmetrics_forked_amd.functional.text._asr import _asr_stats
+
+
+def _wer_update(preds: Union[str, List[str]], target: Union[str, List[str]]) -> Tuple[Tensor, Tensor]:
+    errors, tl, _, _ = _asr_stats(preds, target)
+    return errors, tl
+
+
+def _wer_compute(errors: Tensor, total: Tensor) -> Tensor:
+    return errors / total
+
+
+def word_error_rate(preds: Union[str, List[str]], target: Union[str, List[str]]) -> Tensor:
+    """Word-level edit operations divided by the number of reference words."""
+    errors, total = _wer_update(preds, target)
+    return _wer_compute(errors, total)

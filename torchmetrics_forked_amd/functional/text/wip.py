@@ -1,0 +1,20 @@
+"""Word information preserved (API parity: reference ``functional/text/wip.py``)."""
+from typing import List, Tuple, Union
+
+from torch import Tensor
+
+from torchmetrics_forked_amd.functional.text._asr import _asr_stats
+
+
+def _wip_update(preds: Union[str, List[str]], target: Union[str, List[str]]) -> Tuple[Tensor, Tensor, Tensor]:
+    errors, tl, pl, ml = _asr_stats(preds, target)
+    return errors - ml, tl, pl
+
+
+def _wip_compute(errors: Tensor, target_total: Tensor, preds_total: Tensor) -> Tensor:
+    return (errors / target_total) * (errors / preds_total)
+
+
+def word_information_preserved(preds: Union[str, List[str]], target: Union[str, List[str]]) -> Tensor:
+    """(H / N_target) * (H / N_pred) with H the number of hits."""
+    return _wip_compute(*_wip_update(preds, target))

@@ -1,0 +1,150 @@
+"""EditDistance, ExtendedEditDistance, TranslationEditRate modules (API parity: reference ``text/edit.py``,
+``text/eed.py``, ``text/ter.py``).  All dynamic programmes run in the native text kernels."""
+from typing import Any, List, Literal, Optional, Sequence, Tuple, Union
+
+import torch
+from torch import Tensor, stack, tensor
+
+from torchmetrics_forked_amd.functional.text.edit import _edit_distance_compute, _edit_distance_update
+from torchmetrics_forked_amd.functional.text.eed import _eed_compute, _eed_update
+from torchmetrics_forked_amd.functional.text.ter import _ter_compute, _ter_update, _TercomTokenizer
+from torchmetrics_forked_amd.metric import Metric
+from torchmetrics_forked_amd.utilities.data import dim_zero_cat
+from torchmetrics_forked_amd.utilities.plot import _AX_TYPE, _PLOT_OUT_TYPE
+
+
+class EditDistance(Metric):
+    """Levenshtein distance with configurable substitution cost."""
+
+    higher_is_better: bool = False
+    is_differentiable: bool = False
+    full_state_update: bool = False
+    plot_lower_bound: float = 0.0
+
+    def __init__(self, substitution_cost: int = 1, reduction: Optional[Literal["mean", "sum", "none"]] = "mean", **kwargs: Any) -> None:
+        super().__init__(**kwargs)
+        if not (isinstance(substitution_cost, int) and substitution_cost >= 0):
+            raise ValueError(f"Expected argument `substitution_cost` to be a positive integer, but got {substitution_cost}")
+        self.substitution_cost = substitution_cost
+        allowed = (None, "mean", "sum", "none")
+        if reduction not in allowed:
+            raise ValueError(f"Expected argument `reduction` to be one of {allowed}, but got {reduction}")
+        self.reduction = reduction
+        if self.reduction in ("none", None):
+            self.add_state("edit_scores_list", default=[], dist_reduce_fx="cat")
+        else:
+            self.add_state("edit_scores", default=torch.tensor(0), dist_reduce_fx="sum")
+            self.add_state("num_elements", default=torch.tensor(0), dist_reduce_fx="sum")
+
+    def update(self, preds: Union[str, Sequence[str]], target: Union[str, Sequence[str]]) -> None:
+        distance = _edit_distance_update(preds, target, self.substitution_cost).to(self.device)
+        if self.reduction in ("none", None):
+            self.edit_scores_list.append(distance)
+        else:
+            self.edit_scores += distance.sum()
+            self.num_elements += distance.shape[0]
+
+    def compute(self) -> Tensor:
+        if self.reduction in ("none", None):
+            return _edit_distance_compute(dim_zero_cat(self.edit_scores_list), 1, self.reduction)
+        return _edit_distance_compute(self.edit_scores, self.num_elements, self.reduction)
+
+    def plot(self, val: Optional[Union[Tensor, Sequence[Tensor]]] = None, ax: Optional[_AX_TYPE] = None) -> _PLOT_OUT_TYPE:
+        return self._plot(val, ax)
+
+
+class ExtendedEditDistance(Metric):
+    """Extended edit distance (per-sentence ``cat`` state)."""
+
+    higher_is_better: bool = False
+    is_differentiable: bool = False
+    full_state_update: bool = False
+    plot_lower_bound: float = 0.0
+    plot_upper_bound: float = 1.0
+    sentence_eed: List[Tensor]
+
+    def __init__(
+        self,
+        language: Literal["en", "ja"] = "en",
+        return_sentence_level_score: bool = False,
+        alpha: float = 2.0,
+        rho: float = 0.3,
+        deletion: float = 0.2,
+        insertion: float = 1.0,
+        **kwargs: Any,
+    ) -> None:
+        super().__init__(**kwargs)
+        if language not in ("en", "ja"):
+            raise ValueError(f"Expected argument `language` to either be `en` or `ja` but got {language}")
+        self.language: Literal["en", "ja"] = language
+        self.return_sentence_level_score = return_sentence_level_score
+        for name, val in zip(["alpha", "rho", "deletion", "insertion"], [alpha, rho, deletion, insertion]):
+            if not isinstance(val, float) or val < 0:
+                raise ValueError(f"Parameter `{name}` is expected to be a non-negative float.")
+        self.alpha, self.rho, self.deletion, self.insertion = alpha, rho, deletion, insertion
+        self.add_state("sentence_eed", [], dist_reduce_fx="cat")
+
+    def update(self, preds: Union[str, Sequence[str]], target: Sequence[Union[str, Sequence[str]]]) -> None:
+        scores = _eed_update(preds, target, self.language, self.alpha, self.rho, self.deletion, self.insertion)
+        self.sentence_eed.extend(s.to(self.device) for s in scores)
+
+    def compute(self) -> Union[Tensor, Tuple[Tensor, Tensor]]:
+        scores = self.sentence_eed
+        if isinstance(scores, Tensor):  # after a cat-sync the list state is a single tensor
+            scores = list(scores.reshape(-1))
+        average = _eed_compute(scores)
+        if self.return_sentence_level_score:
+            return average, stack(scores) if scores else torch.zeros(0)
+        return average
+
+    def plot(self, val: Optional[Union[Tensor, Sequence[Tensor]]] = None, ax: Optional[_AX_TYPE] = None) -> _PLOT_OUT_TYPE:
+        return self._plot(val, ax)
+
+
+class TranslationEditRate(Metric):
+    """Corpus TER (Tercom semantics)."""
+
+    is_differentiable: bool = False
+    higher_is_better: bool = False
+    full_state_update: bool = False
+    plot_lower_bound: float = 0.0
+    total_num_edits: Tensor
+    total_tgt_len: Tensor
+    sentence_ter: Optional[List[Tensor]] = None
+
+    def __init__(
+        self,
+        normalize: bool = False,
+        no_punctuation: bool = False,
+        lowercase: bool = True,
+        asian_support: bool = False,
+        return_sentence_level_score: bool = False,
+        **kwargs: Any,
+    ) -> None:
+        super().__init__(**kwargs)
+        for name, val in (("normalize", normalize), ("no_punctuation", no_punctuation), ("lowercase", lowercase), ("asian_support", asian_support)):
+            if not isinstance(val, bool):
+                raise ValueError(f"Expected argument `{name}` to be of type boolean but got {val}.")
+        self.tokenizer = _TercomTokenizer(normalize, no_punctuation, lowercase, asian_support)
+        self.return_sentence_level_score = return_sentence_level_score
+        self.add_state("total_num_edits", tensor(0.0), dist_reduce_fx="sum")
+        self.add_state("total_tgt_len", tensor(0.0), dist_reduce_fx="sum")
+        if self.return_sentence_level_score:
+            self.add_state("sentence_ter", [], dist_reduce_fx="cat")
+
+    def update(self, preds: Union[str, Sequence[str]], target: Sequence[Union[str, Sequence[str]]]) -> None:
+        sent: Optional[List[Tensor]] = [] if self.sentence_ter is not None else None
+        edits, length, sent = _ter_update(preds, target, self.tokenizer, tensor(0.0), tensor(0.0), sent)
+        self.total_num_edits += edits.to(self.total_num_edits)
+        self.total_tgt_len += length.to(self.total_tgt_len)
+        if self.sentence_ter is not None and sent:
+            self.sentence_ter.append(torch.cat(sent).to(self.device))
+
+    def compute(self) -> Union[Tensor, Tuple[Tensor, Tensor]]:
+        ter = _ter_compute(self.total_num_edits, self.total_tgt_len)
+        if self.sentence_ter is not None:
+            return ter, dim_zero_cat(self.sentence_ter)
+        return ter
+
+    def plot(self, val: Optional[Union[Tensor, Sequence[Tensor]]] = None, ax: Optional[_AX_TYPE] = None) -> _PLOT_OUT_TYPE:
+        return self._plot(val, ax)
