@@ -1,0 +1,22 @@
+"""Audio metrics (reference ``audio/__init__.py``)."""
+from torchmetrics_forked_amd.audio.pit import PermutationInvariantTraining
+from torchmetrics_forked_amd.audio.sdr import (
+    ScaleInvariantSignalDistortionRatio,
+    SignalDistortionRatio,
+    SourceAggregatedSignalDistortionRatio,
+)
+from torchmetrics_forked_amd.audio.snr import (
+    ComplexScaleInvariantSignalNoiseRatio,
+    ScaleInvariantSignalNoiseRatio,
+    SignalNoiseRatio,
+)
+
+__all__ = [
+    "PermutationInvariantTraining",
+    "ScaleInvariantSignalDistortionRatio",
+    "SignalDistortionRatio",
+    "SourceAggregatedSignalDistortionRatio",
+    "ScaleInvariantSignalNoiseRatio",
+    "SignalNoiseRatio",
+    "ComplexScaleInvariantSignalNoiseRatio",
+]
