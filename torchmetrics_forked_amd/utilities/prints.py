@@ -56,13 +56,13 @@ _future_warning = partial(warnings.warn, category=FutureWarning)
 
 def _deprecated_root_import_class(name: str, domain: str) -> None:
     _future_warning(
-        f"Importing `{name}` from `torchmetrics` was deprecated and will be removed in 2.0."
-        f" Import `{name}` from `torchmetrics.{domain}` instead."
+        f"Importing `{name}` from `torchmetrics_forked_amd` was deprecated and will be removed in 2.0."
+        f" Import `{name}` from `torchmetrics_forked_amd.{domain}` instead."
     )
 
 
 def _deprecated_root_import_func(name: str, domain: str) -> None:
     _future_warning(
-        f"Importing `{name}` from `torchmetrics.functional` was deprecated and will be removed in 2.0."
-        f" Import `{name}` from `torchmetrics.{domain}` instead."
+        f"Importing `{name}` from `torchmetrics_forked_amd.functional` was deprecated and will be removed in 2.0."
+        f" Import `{name}` from `torchmetrics_forked_amd.{domain}` instead."
     )
