@@ -1,4 +1,5 @@
 """Audio metrics (reference ``audio/__init__.py``)."""
+from torchmetrics_forked_amd.audio.pesq import PerceptualEvaluationSpeechQuality
 from torchmetrics_forked_amd.audio.pit import PermutationInvariantTraining
 from torchmetrics_forked_amd.audio.sdr import (
     ScaleInvariantSignalDistortionRatio,
@@ -10,6 +11,7 @@ from torchmetrics_forked_amd.audio.snr import (
     ScaleInvariantSignalNoiseRatio,
     SignalNoiseRatio,
 )
+from torchmetrics_forked_amd.audio.stoi import ShortTimeObjectiveIntelligibility
 
 __all__ = [
     "PermutationInvariantTraining",
@@ -19,4 +21,6 @@ __all__ = [
     "ScaleInvariantSignalNoiseRatio",
     "SignalNoiseRatio",
     "ComplexScaleInvariantSignalNoiseRatio",
+    "PerceptualEvaluationSpeechQuality",
+    "ShortTimeObjectiveIntelligibility",
 ]
