@@ -99,6 +99,60 @@ at::Tensor toeplitz_solve_cuda(const at::Tensor& r_in, const at::Tensor& b_in) {
   return x.reshape(b_in.sizes());
 }
 
+// ---------------------------------------------------------------------------------------------------------------
+// Per-channel IIR filter (SRMR gammatone and modulation filterbanks): direct form
+//   y[n] = (Σ_k b[k] x[n-k] - Σ_{k≥1} a[k] y[n-k]) / a[0]
+// One thread per channel walks time sequentially; the signal is laid out time-major [T, C] so a wave's 64
+// channels read and write 64 consecutive fp64 values per step (coalesced).  Filter order ≤ 8.
+constexpr int kIirMaxOrder = 8;
+
+__global__ __launch_bounds__(256) void iir_kernel(const double* __restrict__ x, const double* __restrict__ b, const double* __restrict__ a,
+                                                 int64_t C, int64_t T, int K, double* __restrict__ y) {
+  const int64_t c = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double bb[kIirMaxOrder], aa[kIirMaxOrder], xh[kIirMaxOrder], yh[kIirMaxOrder];
+  const double a0 = a[c * K];
+  for (int k = 0; k < K; ++k) {
+    bb[k] = b[c * K + k] / a0;
+    aa[k] = a[c * K + k] / a0;
+    xh[k] = 0.0;
+    yh[k] = 0.0;
+  }
+  for (int64_t n = 0; n < T; ++n) {
+    for (int k = K - 1; k > 0; --k) xh[k] = xh[k - 1];
+    xh[0] = x[n * C + c];
+    double acc = 0.0;
+    for (int k = 0; k < K; ++k) acc += bb[k] * xh[k];
+    for (int k = 1; k < K; ++k) acc -= aa[k] * yh[k - 1];
+    for (int k = K - 1; k > 0; --k) yh[k] = yh[k - 1];
+    yh[0] = acc;
+    y[n * C + c] = acc;
+  }
+}
+
+// x [C, T] fp64, b / a [C, K] -> y [C, T]
+at::Tensor iir_filter_cuda(const at::Tensor& x_in, const at::Tensor& b_in, const at::Tensor& a_in) {
+  TORCH_CHECK(x_in.is_cuda(), "iir_filter: expected GPU tensors");
+  TORCH_CHECK(x_in.dim() == 2 && b_in.dim() == 2 && a_in.sizes() == b_in.sizes() && b_in.size(0) == x_in.size(0),
+              "iir_filter: expected x [C, T], b / a [C, K]");
+  const int K = static_cast<int>(b_in.size(1));
+  TORCH_CHECK(K >= 1 && K <= kIirMaxOrder, "iir_filter: filter length must be in [1, ", kIirMaxOrder, "]");
+  const at::DeviceGuard guard(x_in.device());
+  auto xt = x_in.to(at::kDouble).t().contiguous();  // [T, C]
+  auto b = b_in.to(x_in.device()).to(at::kDouble).contiguous();
+  auto a = a_in.to(x_in.device()).to(at::kDouble).contiguous();
+  const int64_t C = x_in.size(0), T = x_in.size(1);
+  auto yt = at::empty_like(xt);
+  if (C == 0 || T == 0) return yt.t().contiguous();
+  hipLaunchKernelGGL(iir_kernel, dim3(static_cast<unsigned>((C + 255) / 256)), dim3(256), 0, stream(), xt.data_ptr<double>(),
+                     b.data_ptr<double>(), a.data_ptr<double>(), C, T, K, yt.data_ptr<double>());
+  TMX_LAUNCH_CHECK();
+  return yt.t().contiguous();
+}
+
 }  // namespace tmx
 
-TORCH_LIBRARY_IMPL(tmx, CUDA, m) { m.impl("toeplitz_solve", &tmx::toeplitz_solve_cuda); }
+TORCH_LIBRARY_IMPL(tmx, CUDA, m) {
+  m.impl("toeplitz_solve", &tmx::toeplitz_solve_cuda);
+  m.impl("iir_filter", &tmx::iir_filter_cuda);
+}

@@ -135,13 +135,50 @@ at::Tensor linear_assignment(const at::Tensor& metric, bool maximize) {
   return out.to(metric.device());
 }
 
+at::Tensor iir_filter_cpu(const at::Tensor& x_in, const at::Tensor& b_in, const at::Tensor& a_in) {
+  TORCH_CHECK(x_in.dim() == 2 && b_in.dim() == 2 && a_in.sizes() == b_in.sizes() && b_in.size(0) == x_in.size(0),
+              "iir_filter: expected x [C, T], b / a [C, K]");
+  auto x = x_in.to(at::kDouble).contiguous();
+  auto b = b_in.to(at::kDouble).contiguous();
+  auto a = a_in.to(at::kDouble).contiguous();
+  const int64_t C = x.size(0), T = x.size(1), K = b.size(1);
+  auto y = at::empty_like(x);
+  const double* px = x.data_ptr<double>();
+  const double* pb = b.data_ptr<double>();
+  const double* pa = a.data_ptr<double>();
+  double* py = y.data_ptr<double>();
+  at::parallel_for(0, C, 1, [&](int64_t s, int64_t e) {
+    std::vector<double> bb(K), aa(K);
+    for (int64_t c = s; c < e; ++c) {
+      const double a0 = pa[c * K];
+      for (int64_t k = 0; k < K; ++k) {
+        bb[k] = pb[c * K + k] / a0;
+        aa[k] = pa[c * K + k] / a0;
+      }
+      const double* xc = px + c * T;
+      double* yc = py + c * T;
+      for (int64_t n = 0; n < T; ++n) {
+        double acc = 0.0;
+        for (int64_t k = 0; k < K && k <= n; ++k) acc += bb[k] * xc[n - k];
+        for (int64_t k = 1; k < K && k <= n; ++k) acc -= aa[k] * yc[n - k];
+        yc[n] = acc;
+      }
+    }
+  });
+  return y;
+}
+
 }  // namespace tmx
 
 TORCH_LIBRARY_FRAGMENT(tmx, m) {
   m.def("toeplitz_solve(Tensor r, Tensor b) -> Tensor");
   m.def("linear_assignment(Tensor metric, bool maximize) -> Tensor");
+  m.def("iir_filter(Tensor x, Tensor b, Tensor a) -> Tensor");
 }
 
-TORCH_LIBRARY_IMPL(tmx, CPU, m) { m.impl("toeplitz_solve", &tmx::toeplitz_solve_cpu); }
+TORCH_LIBRARY_IMPL(tmx, CPU, m) {
+  m.impl("toeplitz_solve", &tmx::toeplitz_solve_cpu);
+  m.impl("iir_filter", &tmx::iir_filter_cpu);
+}
 
 TORCH_LIBRARY_IMPL(tmx, CompositeExplicitAutograd, m) { m.impl("linear_assignment", &tmx::linear_assignment); }

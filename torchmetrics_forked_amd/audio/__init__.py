@@ -11,6 +11,7 @@ from torchmetrics_forked_amd.audio.snr import (
     ScaleInvariantSignalNoiseRatio,
     SignalNoiseRatio,
 )
+from torchmetrics_forked_amd.audio.srmr import SpeechReverberationModulationEnergyRatio
 from torchmetrics_forked_amd.audio.stoi import ShortTimeObjectiveIntelligibility
 
 __all__ = [
@@ -23,4 +24,5 @@ __all__ = [
     "ComplexScaleInvariantSignalNoiseRatio",
     "PerceptualEvaluationSpeechQuality",
     "ShortTimeObjectiveIntelligibility",
+    "SpeechReverberationModulationEnergyRatio",
 ]
