@@ -30,6 +30,14 @@ if [[ $STEPS == *prof* ]]; then
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 > $OUT/prof.log 2>&1; stop_if_fatal $? prof
   find $OUT/prof -name "*kernel_stats.csv" | head -3
 fi
+if [[ $STEPS == *domain* ]]; then
+  timeout -k 10 900 python tools/domain_bench.py > $OUT/domain_bench.json 2> $OUT/domain_bench.err; stop_if_fatal $? domain; cat $OUT/domain_bench.json
+fi
+if [[ $STEPS == *kkern* ]]; then
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_kern -o kern --output-format csv -- python3 tools/kbench_kernels.py > $OUT/kbench_kernels.log 2>&1; stop_if_fatal $? kkern
+  grep '^{' $OUT/kbench_kernels.log > $OUT/kbench_kernels.json || true
+  cat $OUT/kbench_kernels.json
+fi
 if [[ $STEPS == *ref* ]]; then
   timeout -k 10 900 python tools/ref_bench.py --steps 10 --warmup 2 > $OUT/ref_bench.json 2> $OUT/ref_bench.err; stop_if_fatal $? ref; cat $OUT/ref_bench.json
 fi
