@@ -121,3 +121,46 @@ def _collection_coalesced(rank, world):
 )
 def test_ddp(fn):
     assert all(run_ddp(fn))
+
+
+def _async_sync_worker(rank, world):
+    from torchmetrics_forked_amd.aggregation import CatMetric, MaxMetric, MeanMetric, SumMetric
+    from torchmetrics_forked_amd.classification import MulticlassConfusionMatrix
+
+    ok = True
+    metrics = [SumMetric(), MeanMetric(), MaxMetric(), CatMetric(), MulticlassConfusionMatrix(num_classes=4)]
+    for step in range(3):
+        x = torch.arange(4, dtype=torch.float) + 10 * rank + step
+        for m in metrics[:4]:
+            m.update(x)
+        metrics[4].update(torch.tensor([rank, step % 4, 1, 2]), torch.tensor([step % 4, rank, 1, 3]))
+    expected = []
+    for m in metrics:
+        m.sync()
+        expected.append({k: (v.clone() if isinstance(v, torch.Tensor) else [t.clone() for t in v]) for k, v in m.metric_state.items()})
+        m.unsync()
+    handles = [m.sync(async_op=True) for m in metrics]
+    # unrelated work while the all-reduce buckets are in flight
+    _ = torch.randn(256, 256) @ torch.randn(256, 256)
+    for m, h, exp in zip(metrics, handles, expected):
+        h.wait()
+        for k, v in m.metric_state.items():
+            if isinstance(v, torch.Tensor):
+                ok &= torch.equal(v, exp[k])
+            else:
+                ok &= all(torch.equal(a, b) for a, b in zip(v, exp[k]))
+        m.unsync()
+    return bool(ok)
+
+
+def test_async_sync_matches_blocking_sync():
+    assert all(run_ddp(_async_sync_worker))
+
+
+def test_async_sync_not_distributed_returns_noop_handle():
+    from torchmetrics_forked_amd.aggregation import SumMetric
+
+    m = SumMetric()
+    m.update(torch.tensor(3.0))
+    h = m.sync(async_op=True)
+    assert h.wait() is m and not m._is_synced

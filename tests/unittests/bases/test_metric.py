@@ -195,3 +195,16 @@ def test_device_error_message_rewrite():
 def test_abstract():
     with pytest.raises(TypeError):
         Metric()
+
+
+def test_profiler_ranges_opt_in(monkeypatch):
+    import torchmetrics_forked_amd.metric as M
+    from torchmetrics_forked_amd.aggregation import SumMetric
+
+    monkeypatch.setattr(M, "_PROFILE", True)
+    m = SumMetric()
+    with torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CPU]) as prof:
+        m.update(torch.tensor(1.0))
+        m.compute()
+    names = {e.name for e in prof.events()}
+    assert "tmx/SumMetric.update" in names and "tmx/SumMetric.compute" in names

@@ -10,12 +10,13 @@ MI355X-first choices that differ from the reference while keeping its observable
   A user supplied ``dist_sync_fn`` still gets the per-leaf protocol.
 * ``forward`` on the reduce-state path merges batch state into the global state without re-allocating
   defaults on the host for every step (``_reset_states`` clones device defaults in place).
-* Optional ``sync(async_op=True)`` starts the collectives on the current stream and returns a handle, so the
-  caller can overlap the next step's update kernels with the RCCL traffic (``parallel.streams``).
+* Optional ``sync(async_op=True)`` enqueues the coalesced all-reduce buckets on RCCL (``async_op`` work handles)
+  and returns immediately, so other GPU work overlaps the xGMI transfer; ``handle.wait()`` installs the states.
 """
 import builtins
 import functools
 import inspect
+import os
 from abc import ABC, abstractmethod
 from contextlib import contextmanager
 from copy import deepcopy
@@ -25,7 +26,7 @@ import torch
 from torch import Tensor
 from torch.nn import Module
 
-from torchmetrics_forked_amd.parallel.sync import legacy_sync_states, sync_states
+from torchmetrics_forked_amd.parallel.sync import PendingSync, legacy_sync_states, sync_states, sync_states_async
 from torchmetrics_forked_amd.utilities.data import (
     _flatten,
     _squeeze_if_scalar,
@@ -38,6 +39,27 @@ from torchmetrics_forked_amd.utilities.data import (
 )
 from torchmetrics_forked_amd.utilities.distributed import gather_all_tensors
 from torchmetrics_forked_amd.utilities.exceptions import TorchMetricsUserError
+
+# Opt-in tracing: with TMX_PROFILE=1 every update / compute / sync is wrapped in a profiler range
+# ("tmx/<Metric>.update", ...), visible in torch.profiler traces and rocprofv3 --marker-trace timelines.
+_PROFILE = os.environ.get("TMX_PROFILE", "0") == "1"
+
+
+def _range(name: str) -> Any:
+    if _PROFILE:
+        return torch.profiler.record_function(name)
+    return _NULL_RANGE
+
+
+class _NullRange:
+    def __enter__(self) -> None:
+        return None
+
+    def __exit__(self, *_: Any) -> None:
+        return None
+
+
+_NULL_RANGE = _NullRange()
 from torchmetrics_forked_amd.utilities.plot import _AX_TYPE, _PLOT_OUT_TYPE, plot_single_or_multi_val
 from torchmetrics_forked_amd.utilities.prints import rank_zero_warn
 from torchmetrics_forked_amd.utilities.validation import DeferredChecks, make_sink
@@ -307,7 +329,7 @@ class Metric(Module, ABC):
         def wrapped_func(*args: Any, **kwargs: Any) -> None:
             self._computed = None
             self._update_count += 1
-            with torch.set_grad_enabled(self._enable_grad):
+            with torch.set_grad_enabled(self._enable_grad), _range(f"tmx/{self.__class__.__name__}.update"):
                 try:
                     update(*args, **kwargs)
                 except RuntimeError as err:
@@ -337,18 +359,31 @@ class Metric(Module, ABC):
         process_group: Optional[Any] = None,
         should_sync: bool = True,
         distributed_available: Optional[Callable] = None,
-    ) -> None:
-        """Replace local states by their cross-process reduction (local copies are cached for ``unsync``)."""
+        async_op: bool = False,
+    ) -> Optional["_MetricPendingSync"]:
+        """Replace local states by their cross-process reduction (local copies are cached for ``unsync``).
+
+        With ``async_op=True`` the all-reduce buckets are only enqueued on RCCL and a handle is returned; the
+        caller overlaps other GPU work (e.g. the next step's updates of *other* metrics) and calls
+        ``handle.wait()``, which installs the synced states exactly like the blocking path.  States must not be
+        updated between the two calls."""
         if self._is_synced and should_sync:
             raise TorchMetricsUserError("The Metric has already been synced.")
         if distributed_available is None and self.distributed_available_fn is not None:
             distributed_available = self.distributed_available_fn
         is_distributed = distributed_available() if callable(distributed_available) else None
         if not should_sync or not is_distributed:
-            return
+            return _MetricPendingSync(self, None) if async_op else None
+        if async_op:
+            if dist_sync_fn is not None and dist_sync_fn is not gather_all_tensors:
+                raise TorchMetricsUserError("`async_op=True` uses the coalesced sync engine; a custom `dist_sync_fn` is not supported.")
+            pending = sync_states_async(self.metric_state, self._reductions, group=process_group or self.process_group)
+            return _MetricPendingSync(self, pending)
         self._cache = self.metric_state
-        self._sync_dist(dist_sync_fn, process_group=process_group)
+        with _range(f"tmx/{self.__class__.__name__}.sync"):
+            self._sync_dist(dist_sync_fn, process_group=process_group)
         self._is_synced = True
+        return None
 
     def unsync(self, should_unsync: bool = True) -> None:
         """Restore the local (pre-sync) states."""
@@ -362,6 +397,15 @@ class Metric(Module, ABC):
             setattr(self, name, val)
         self._is_synced = False
         self._cache = None
+
+    def _finish_async_sync(self, pending: PendingSync) -> None:
+        if self._is_synced:
+            raise TorchMetricsUserError("The Metric has already been synced.")
+        local = self.metric_state
+        for name, val in pending.wait().items():
+            setattr(self, name, val)
+        self._cache = local
+        self._is_synced = True
 
     @contextmanager
     def sync_context(
@@ -396,7 +440,7 @@ class Metric(Module, ABC):
                 return self._computed
             if self._deferred is not None:
                 self._deferred.check()
-            with self.sync_context(
+            with _range(f"tmx/{self.__class__.__name__}.compute"), self.sync_context(
                 dist_sync_fn=self.dist_sync_fn, should_sync=self._to_sync, should_unsync=self._should_unsync
             ):
                 value = _squeeze_if_scalar(compute(*args, **kwargs))
@@ -744,3 +788,18 @@ class CompositionalMetric(Metric):
 
     def _wrap_compute(self, compute: Callable) -> Callable:
         return compute
+
+
+class _MetricPendingSync:
+    """Handle returned by ``Metric.sync(async_op=True)``; ``wait()`` installs the synchronised states."""
+
+    def __init__(self, metric: "Metric", pending: Optional[PendingSync]) -> None:
+        self._metric = metric
+        self._pending = pending
+        self._done = pending is None
+
+    def wait(self) -> "Metric":
+        if not self._done:
+            self._metric._finish_async_sync(self._pending)
+            self._done = True
+        return self._metric

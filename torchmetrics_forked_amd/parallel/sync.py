@@ -74,11 +74,18 @@ def _comm_device(sample: Optional[Tensor], group: Optional[Any]) -> torch.device
 # ----------------------------------------------------------------------------------------------------------
 def _all_reduce_coalesced(items: List[Tuple[str, Tensor, str]], group: Optional[Any]) -> Dict[str, Tensor]:
     """All-reduce many tensors with one collective per (op, dtype, device) bucket."""
-    world = _world(group)
+    return _finish_all_reduce(_launch_all_reduce(items, group, async_op=False), group)
+
+
+def _launch_all_reduce(items: List[Tuple[str, Tensor, str]], group: Optional[Any], async_op: bool) -> List[Tuple]:
+    """Pack every (op, dtype, device) bucket into one flat buffer and start its all_reduce.
+
+    With ``async_op`` the collectives are only enqueued (RCCL runs them on its own stream after the packing
+    kernels; the host returns immediately and later kernels on the compute stream overlap the transfer)."""
+    launched = []
     buckets: Dict[Tuple[str, torch.dtype, torch.device], List[Tuple[str, Tensor]]] = {}
     for name, t, op in items:
         buckets.setdefault((op, t.dtype, t.device), []).append((name, t))
-    out: Dict[str, Tensor] = {}
     for (op, dtype, device), members in buckets.items():
         comm_dev = _comm_device(members[0][1], group)
         wire_dtype = dtype
@@ -88,7 +95,17 @@ def _all_reduce_coalesced(items: List[Tuple[str, Tensor, str]], group: Optional[
         if op == "mean" and not flat.is_floating_point():
             flat = flat.double()
         rop = {"sum": dist.ReduceOp.SUM, "mean": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}[op]
-        dist.all_reduce(flat, op=rop, group=group)
+        work = dist.all_reduce(flat, op=rop, group=group, async_op=async_op)
+        launched.append((op, dtype, device, members, flat, work))
+    return launched
+
+
+def _finish_all_reduce(launched: List[Tuple], group: Optional[Any]) -> Dict[str, Tensor]:
+    world = _world(group)
+    out: Dict[str, Tensor] = {}
+    for op, dtype, device, members, flat, work in launched:
+        if work is not None:
+            work.wait()
         if op == "mean":
             flat = flat / world
         offset = 0
@@ -284,6 +301,42 @@ def sync_states(
     states: Dict[str, StateT], reductions: Dict[str, Optional[Callable]], group: Optional[Any] = None
 ) -> Dict[str, StateT]:
     return sync_states_many([states], [reductions], group)[0]
+
+
+class PendingSync:
+    """An in-flight state synchronisation started by :func:`sync_states_async`.
+
+    The all-reduce buckets (sum / mean / min / max states) are already enqueued on RCCL when this object exists;
+    the packed all-gather of list / ``cat`` / ``None`` states (which needs a host-side length exchange) runs in
+    :meth:`wait`.  ``wait`` returns the synchronised state dict."""
+
+    def __init__(self, states: Dict[str, StateT], reductions: Dict[str, Optional[Callable]], group: Optional[Any]) -> None:
+        self._group = group
+        self._reductions = reductions
+        reduce_items, self._rest = [], {}
+        for name, value in states.items():
+            fn = reductions.get(name)
+            if isinstance(value, Tensor) and fn in _REDUCE_OPS:
+                reduce_items.append((name, value, _REDUCE_OPS[fn]))
+            else:
+                self._rest[name] = value
+        self._launched = _launch_all_reduce(reduce_items, group, async_op=True) if reduce_items else []
+        self._result: Optional[Dict[str, StateT]] = None
+
+    def wait(self) -> Dict[str, StateT]:
+        if self._result is None:
+            out = _finish_all_reduce(self._launched, self._group) if self._launched else {}
+            if self._rest:
+                out.update(sync_states(self._rest, {k: self._reductions.get(k) for k in self._rest}, self._group))
+            self._result = out
+        return self._result
+
+
+def sync_states_async(
+    states: Dict[str, StateT], reductions: Dict[str, Optional[Callable]], group: Optional[Any] = None
+) -> PendingSync:
+    """Start synchronising ``states`` and return immediately (see :class:`PendingSync`)."""
+    return PendingSync(states, reductions, group)
 
 
 def legacy_sync_states(
