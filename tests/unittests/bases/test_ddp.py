@@ -164,3 +164,37 @@ def test_async_sync_not_distributed_returns_noop_handle():
     m.update(torch.tensor(3.0))
     h = m.sync(async_op=True)
     assert h.wait() is m and not m._is_synced
+
+
+def _sharded_curve_worker(rank, world):
+    from torchmetrics_forked_amd.classification import (
+        MulticlassAUROC,
+        MulticlassAveragePrecision,
+        MultilabelAUROC,
+        MultilabelAveragePrecision,
+    )
+
+    g = torch.Generator().manual_seed(100 + rank)
+    ok = True
+    for cls, kw, task in [(MulticlassAUROC, {"num_classes": 7}, "mc"), (MulticlassAveragePrecision, {"num_classes": 7}, "mc"),
+                          (MultilabelAUROC, {"num_labels": 5}, "ml"), (MultilabelAveragePrecision, {"num_labels": 5}, "ml")]:
+        for average in ("macro", "weighted", "none"):
+            plain = cls(average=average, **kw)
+            sharded = cls(average=average, sharded_compute=True, **kw)
+            for _ in range(2):
+                if task == "mc":
+                    p = torch.randn(64, 7, generator=g).softmax(-1).bfloat16()
+                    t = torch.randint(0, 7, (64,), generator=g)
+                else:
+                    p = torch.rand(64, 5, generator=g).bfloat16()
+                    t = torch.randint(0, 2, (64, 5), generator=g)
+                plain.update(p, t)
+                sharded.update(p, t)
+            a, b = plain.compute(), sharded.compute()
+            ok &= bool(torch.allclose(a, b, atol=1e-6, equal_nan=True))
+            ok &= sharded._shard_info is None and sharded.score_hist.shape[0] == kw.get("num_classes", kw.get("num_labels"))
+    return ok
+
+
+def test_sharded_compute_matches_replicated():
+    assert all(run_ddp(_sharded_curve_worker))

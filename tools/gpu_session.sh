@@ -8,7 +8,8 @@ mkdir -p $OUT
 export TMPDIR=/tmp
 stop_if_fatal() {  # $1 = exit code, $2 = step name
   local rc=$1
-  if [ $rc -ge 124 ] || [ $rc -eq 134 ] || [ $rc -eq 139 ]; then
+  # any failing GPU step ends the session: a fault, abort, timeout or error leaves nothing else to run
+  if [ $rc -ne 0 ]; then
     echo "FATAL step '$2' rc=$rc - stopping GPU session" | tee -a $OUT/session.log; exit $rc
   fi
   echo "step '$2' rc=$rc" | tee -a $OUT/session.log

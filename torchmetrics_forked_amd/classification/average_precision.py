@@ -15,6 +15,7 @@ from torchmetrics_forked_amd.classification.precision_recall_curve import (
 from torchmetrics_forked_amd.functional.classification.precision_recall_curve import (
     _binary_precision_recall_curve_arg_validation,
 )
+from torchmetrics_forked_amd.functional.classification.auroc import _reduce_auroc
 from torchmetrics_forked_amd.functional.classification.average_precision import (
     _multiclass_average_precision_arg_validation,
     _multilabel_average_precision_arg_validation,
@@ -80,6 +81,9 @@ class MulticlassAveragePrecision(MulticlassPrecisionRecallCurve):
         self.validate_args = validate_args
 
     def compute(self) -> Tensor:
+        if self._shard_info is not None:  # class-sharded compute (``sharded_compute=True`` under DDP)
+            _, ap, pos, _ = self._sharded_scores()
+            return _reduce_auroc(ap.float(), self.average, pos.float())
         return average_precision_compute(self._curve_state(), "multiclass", self.num_classes, self.thresholds, self.average)
 
     def plot(self, val: Optional[Union[Tensor, List[Tensor]]] = None, ax: Optional[_AX_TYPE] = None) -> _PLOT_OUT_TYPE:
@@ -112,6 +116,9 @@ class MultilabelAveragePrecision(MultilabelPrecisionRecallCurve):
         self.validate_args = validate_args
 
     def compute(self) -> Tensor:
+        if self._shard_info is not None:  # label-sharded compute (``sharded_compute=True`` under DDP)
+            _, ap, pos, _ = self._sharded_scores()
+            return _reduce_auroc(ap.float(), self.average, pos.float())
         return average_precision_compute(
             self._curve_state(), "multilabel", self.num_labels, self.thresholds, self.average, self.ignore_index
         )

@@ -32,6 +32,8 @@ from torchmetrics_forked_amd.functional.classification.precision_recall_curve im
     precision_recall_curve_compute,
 )
 from torchmetrics_forked_amd.metric import Metric
+from torchmetrics_forked_amd.parallel.sync import sync_states
+from torchmetrics_forked_amd.utilities.distributed import gather_all_tensors
 from torchmetrics_forked_amd.ops import classification as cls_ops
 from torchmetrics_forked_amd.utilities.data import dim_zero_cat
 from torchmetrics_forked_amd.utilities.enums import ClassificationTask
@@ -134,6 +136,65 @@ class _CurveMetric(Metric):
         super()._reduce_states(incoming_state)
 
     # ---------------------------------------------------------------------------------------------- sync
+    _shard_info: Optional[Tuple[int, int, int, Any]] = None  # (first class, classes owned, shard rows, group)
+
+    def _shardable(self, dist_sync_fn: Any) -> bool:
+        return (
+            self.sharded_compute
+            and self.thresholds is None
+            and self._task != "binary"
+            and getattr(self, "average", None) != "micro"
+            and self.score_hist.numel() > 0
+            and (dist_sync_fn is None or dist_sync_fn is gather_all_tensors)
+        )
+
+    def _sync_sharded(self, group: Optional[Any]) -> None:
+        """State-parallel sync: reduce-scatter the exact histogram by class so each rank owns
+        ``ceil(C / W)`` classes, and sync the remaining states normally."""
+        world = dist.get_world_size(group)
+        rank = dist.get_rank(group)
+        c = self._num
+        per = -(-c // world)
+        full = self.score_hist
+        if per * world != c:
+            full = torch.cat([full, full.new_zeros(per * world - c, *full.shape[1:])])
+        backend = dist.get_backend(group) if group is not None else dist.get_backend()
+        shard = full.new_empty(per, *full.shape[1:])
+        if backend == "nccl":
+            dist.reduce_scatter_tensor(shard, full.contiguous(), op=dist.ReduceOp.SUM, group=group)
+        else:  # gloo has no reduce-scatter: same result through an all-reduce
+            red = full.clone()
+            dist.all_reduce(red, op=dist.ReduceOp.SUM, group=group)
+            shard.copy_(red[rank * per : (rank + 1) * per])
+        others = {k: v for k, v in self.metric_state.items() if k != "score_hist"}
+        for name, val in sync_states(others, self._reductions, group=group).items():
+            setattr(self, name, val)
+        first = rank * per
+        owned = max(0, min(per, c - first))
+        self.score_hist = shard[:owned]
+        self._shard_info = (first, owned, per, group)
+
+    def unsync(self, should_unsync: bool = True) -> None:
+        super().unsync(should_unsync)
+        if should_unsync:
+            self._shard_info = None
+
+    def _sharded_scores(self) -> Tuple[Tensor, Tensor, Tensor, Tensor]:
+        """(auroc, ap, P, N) for all classes from this rank's class shard + one small all-gather."""
+        first, owned, per, group = self._shard_info  # type: ignore[misc]
+        world = dist.get_world_size(group)
+        local = torch.zeros(4, per, dtype=torch.float64, device=self.score_hist.device)
+        if owned > 0:
+            auc, ap, pos, neg = eng.hist_scores(self.score_hist)
+            local[0, :owned], local[1, :owned] = auc.double(), ap.double()
+            local[2, :owned], local[3, :owned] = pos.double(), neg.double()
+        backend = dist.get_backend(group) if group is not None else dist.get_backend()
+        comm = local if backend == "nccl" or not local.is_cuda else local.cpu()
+        parts = [torch.empty_like(comm) for _ in range(world)]
+        dist.all_gather(parts, comm, group=group)
+        allv = torch.cat(parts, dim=1)[:, : self._num].to(local.device)
+        return allv[0], allv[1], allv[2], allv[3]
+
     def _sync_dist(self, dist_sync_fn: Any = None, process_group: Optional[Any] = None) -> None:
         if self.thresholds is None:
             group = process_group or self.process_group
@@ -144,6 +205,9 @@ class _CurveMetric(Metric):
             dist.all_reduce(used, op=dist.ReduceOp.MAX, group=group)
             if int(used.item()) and self.score_hist.numel() == 0:
                 self._ensure_hist(self.device)
+            if self._shardable(dist_sync_fn):
+                self._sync_sharded(group)
+                return
         super()._sync_dist(dist_sync_fn, process_group)
 
     # ------------------------------------------------------------------------------------------- compute

@@ -74,7 +74,7 @@ _STR_REDUCTIONS = {
 _CONST_ATTRS = frozenset(
     ("higher_is_better", "is_differentiable", "full_state_update", "plot_lower_bound", "plot_upper_bound", "plot_legend_name")
 )
-_BOOL_KWARGS = ("compute_on_cpu", "dist_sync_on_step", "sync_on_compute", "compute_with_cache")
+_BOOL_KWARGS = ("compute_on_cpu", "dist_sync_on_step", "sync_on_compute", "compute_with_cache", "sharded_compute")
 
 
 def jit_distributed_available() -> bool:
@@ -95,6 +95,9 @@ class Metric(Module, ABC):
         distributed_available_fn: callable deciding whether we run distributed.
         sync_on_compute: synchronise states when ``compute`` is called (default True).
         compute_with_cache: cache ``compute`` output until the next ``update`` (default True).
+        sharded_compute: framework extension. Metrics that support state-parallel compute
+            reduce-scatter their per-class state across ranks at sync time, compute only their own classes and
+            all-gather the small per-class results; others ignore the flag.  Results are identical.
     """
 
     __jit_ignored_attributes__: ClassVar[List[str]] = ["device"]
@@ -125,10 +128,11 @@ class Metric(Module, ABC):
             "dist_sync_on_step": kwargs.pop("dist_sync_on_step", False),
             "sync_on_compute": kwargs.pop("sync_on_compute", True),
             "compute_with_cache": kwargs.pop("compute_with_cache", True),
+            "sharded_compute": kwargs.pop("sharded_compute", False),
         }
         for key in _BOOL_KWARGS:
             if not isinstance(opts[key], bool):
-                article = "a" if key in ("sync_on_compute", "compute_with_cache") else "an"
+                article = "a" if key in ("sync_on_compute", "compute_with_cache", "sharded_compute") else "an"
                 raise ValueError(f"Expected keyword argument `{key}` to be {article} `bool` but got {opts[key]}")
             setattr(self, key, opts[key])
 
