@@ -2,6 +2,7 @@
 (API parity: reference ``classification/recall_fixed_precision.py``, ``precision_fixed_recall.py``,
 ``specificity_sensitivity.py``).  They subclass the PR-curve modules, so they share the exact 16-bit histogram /
 sample / binned state machinery and its single-collective sync."""
+import inspect
 from typing import Any, Callable, List, Optional, Tuple, Type, Union
 
 from torch import Tensor
@@ -214,6 +215,12 @@ def _wrapper(binary: type, multiclass: type, multilabel: type, min_name: str) ->
             num_classes, num_labels, kwargs,
         )
 
+    P = inspect.Parameter
+    __new__.__signature__ = inspect.Signature(  # type: ignore[attr-defined]
+        [P("cls", P.POSITIONAL_OR_KEYWORD), P("task", P.POSITIONAL_OR_KEYWORD), P(min_name, P.POSITIONAL_OR_KEYWORD)]
+        + [P(k, P.POSITIONAL_OR_KEYWORD, default=v) for k, v in defaults.items()]
+        + [P("kwargs", P.VAR_KEYWORD)]
+    )
     return __new__
 
 

@@ -1,0 +1,5 @@
+"""Module-path alias of reference ``src/torchmetrics/clustering/mutual_info_score.py`` (the implementation lives in ``torchmetrics_forked_amd.clustering``;
+this file keeps ``from torchmetrics.clustering.mutual_info_score import ...`` style imports working)."""
+from torchmetrics_forked_amd.clustering import MutualInfoScore
+
+__all__ = ['MutualInfoScore']

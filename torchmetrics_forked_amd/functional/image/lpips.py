@@ -48,6 +48,43 @@ class _SlicedBackbone(nn.Module):
         return outs
 
 
+class _NamedBackbone(_SlicedBackbone):
+    """Public LPIPS trunks (reference ``functional/image/lpips.py:65-202``): ``forward`` returns a NamedTuple of
+    the per-slice ReLU outputs.  ``pretrained=True`` loads torchvision-layout ``weights`` (a local file: nothing is
+    downloaded); without a file the trunk stays randomly initialised."""
+
+    _net = "alex"
+
+    def __init__(self, requires_grad: bool = False, pretrained: bool = True, weights: Optional[str] = None) -> None:
+        super().__init__(self._net, requires_grad=requires_grad, weights=weights if pretrained else None)
+        self.N_slices = len(self.slices)
+        fields = [(f"relu{i + 1}", Tensor) for i in range(self.N_slices)]
+        if self._net == "vgg":
+            fields = [(n, Tensor) for n in ("relu1_2", "relu2_2", "relu3_3", "relu4_3", "relu5_3")]
+        self._out = NamedTuple(f"_{type(self).__name__}Output", fields)  # type: ignore[misc]
+
+    def forward(self, x: Tensor) -> NamedTuple:  # type: ignore[override]
+        return self._out(*super().forward(x))
+
+
+class SqueezeNet(_NamedBackbone):
+    """SqueezeNet-1.1 trunk, 7 slices."""
+
+    _net = "squeeze"
+
+
+class Alexnet(_NamedBackbone):
+    """AlexNet trunk, 5 slices."""
+
+    _net = "alex"
+
+
+class Vgg16(_NamedBackbone):
+    """VGG16 trunk, 5 slices."""
+
+    _net = "vgg"
+
+
 def _spatial_average(in_tens: Tensor, keep_dim: bool = True) -> Tensor:
     return in_tens.mean([2, 3], keepdim=keep_dim)
 
