@@ -51,6 +51,9 @@ def main() -> None:
     ap.add_argument("--batch", type=int, default=65536)
     ap.add_argument("--pool", type=int, default=4, help="distinct synthetic batches cycled through")
     ap.add_argument("--no-fuse", action="store_true", help="disable the fused collection update plan (A/B)")
+    ap.add_argument("--replicated-compute", action="store_true",
+                    help="all-reduce the full histogram and compute every class on every rank (A/B against the default"
+                         " class-sharded compute: reduce-scatter by class + all-gather of per-class AUROC)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -74,7 +77,7 @@ def main() -> None:
     C, B = args.num_classes, args.batch
     coll = tm.MetricCollection(
         {
-            "auroc": tm.MulticlassAUROC(num_classes=C),
+            "auroc": tm.MulticlassAUROC(num_classes=C, sharded_compute=world > 1 and not args.replicated_compute),
             "confmat": tm.MulticlassConfusionMatrix(num_classes=C),
         }
     ).to(device)
@@ -153,6 +156,7 @@ def main() -> None:
             "compute_incl_sync_ms": round(1000.0 * elapsed - (upd_ms if use_cuda else 0.0), 3),
             "auroc": float(res["auroc"]),
             "fused_update": not args.no_fuse,
+            "sharded_compute": world > 1 and not args.replicated_compute,
             "device": torch.cuda.get_device_name(device) if use_cuda else "cpu",
         }
         print(json.dumps(out), flush=True)

@@ -198,3 +198,34 @@ def _sharded_curve_worker(rank, world):
 
 def test_sharded_compute_matches_replicated():
     assert all(run_ddp(_sharded_curve_worker))
+
+
+def _narrow_hist_worker(rank, world):
+    """The histogram collective narrows to int32 only when the summed per-rank max bin fits; either way the
+    synced histogram is the exact int64 sum and the local state is restored by unsync."""
+    from torchmetrics_forked_amd.classification import MulticlassAUROC
+
+    ok = True
+    for big in (False, True):
+        for sharded in (False, True):
+            m = MulticlassAUROC(num_classes=3, sharded_compute=sharded)
+            m.update(torch.randn(16, 3).softmax(-1).bfloat16(), torch.randint(0, 3, (16,)))
+            if big:
+                m.score_hist[:, 0, 5] += 2**31 - 10  # summed over ranks: beyond int32
+            local = m.score_hist.clone()
+            locals_ = [torch.zeros_like(local) for _ in range(world)]
+            torch.distributed.all_gather(locals_, local)
+            expect = sum(locals_)
+            m.sync()
+            got = m.score_hist
+            if sharded:
+                first, owned, _, _ = m._shard_info
+                expect = expect[first : first + owned]
+            ok &= got.dtype == torch.long and torch.equal(got, expect)
+            m.unsync()
+            ok &= torch.equal(m.score_hist, local)
+    return ok
+
+
+def test_hist_sync_narrowing_exact():
+    assert all(run_ddp(_narrow_hist_worker))

@@ -3,7 +3,7 @@
 
 State layout (``thresholds=None``):
   * ``score_hist`` — exact ``int64 [C, 2, 16384]`` histogram for bf16/fp16 scores, ``"sum"``-reduced (RCCL
-    all-reduce), materialised lazily on the first 16-bit batch so fp32 users pay nothing;
+    all-reduce, sent as int32 whenever that is provably exact), materialised lazily on the first 16-bit batch so fp32 users pay nothing;
   * ``preds`` / ``target`` — ``cat`` lists (reference layout) for fp32/fp64 scores.
 With ``thresholds`` given the state is the reference's ``confmat [T, (C,) 2, 2]``.
 """
@@ -148,14 +148,14 @@ class _CurveMetric(Metric):
             and (dist_sync_fn is None or dist_sync_fn is gather_all_tensors)
         )
 
-    def _sync_sharded(self, group: Optional[Any]) -> None:
+    def _sync_sharded(self, group: Optional[Any], narrow: bool = False) -> None:
         """State-parallel sync: reduce-scatter the exact histogram by class so each rank owns
         ``ceil(C / W)`` classes, and sync the remaining states normally."""
         world = dist.get_world_size(group)
         rank = dist.get_rank(group)
         c = self._num
         per = -(-c // world)
-        full = self.score_hist
+        full = self.score_hist.to(torch.int32) if narrow else self.score_hist
         if per * world != c:
             full = torch.cat([full, full.new_zeros(per * world - c, *full.shape[1:])])
         backend = dist.get_backend(group) if group is not None else dist.get_backend()
@@ -171,7 +171,7 @@ class _CurveMetric(Metric):
             setattr(self, name, val)
         first = rank * per
         owned = max(0, min(per, c - first))
-        self.score_hist = shard[:owned]
+        self.score_hist = shard[:owned].long()
         self._shard_info = (first, owned, per, group)
 
     def unsync(self, should_unsync: bool = True) -> None:
@@ -196,17 +196,31 @@ class _CurveMetric(Metric):
         return allv[0], allv[1], allv[2], allv[3]
 
     def _sync_dist(self, dist_sync_fn: Any = None, process_group: Optional[Any] = None) -> None:
+        """Histogram states travel as int32 whenever the summed per-rank maximum bin proves every global bin fits
+        (halves the dominant collective: 131 MB instead of 262 MB at C=1000); one small all-reduce carries that
+        bound together with the "some rank has a histogram" flag."""
         if self.thresholds is None:
             group = process_group or self.process_group
-            used = torch.tensor([1 if self.score_hist.numel() > 0 else 0], dtype=torch.int32)
             backend = dist.get_backend(group) if group is not None else dist.get_backend()
             dev = self.score_hist.device if backend != "nccl" or self.score_hist.is_cuda else torch.device("cuda")
-            used = used.to(dev if backend == "nccl" else "cpu")
-            dist.all_reduce(used, op=dist.ReduceOp.MAX, group=group)
-            if int(used.item()) and self.score_hist.numel() == 0:
+            has = self.score_hist.numel() > 0
+            local_max = self.score_hist.amax().reshape(1) if has else torch.zeros(1, dtype=torch.long, device=dev)
+            stats = torch.cat([torch.tensor([1 if has else 0], dtype=torch.long, device=local_max.device), local_max.long()])
+            stats = stats.to(dev if backend == "nccl" else "cpu")
+            dist.all_reduce(stats, op=dist.ReduceOp.SUM, group=group)
+            used, bound = (int(v) for v in stats.tolist())
+            if used and self.score_hist.numel() == 0:
                 self._ensure_hist(self.device)
+            narrow = used > 0 and bound < 2**31 - 1
             if self._shardable(dist_sync_fn):
-                self._sync_sharded(group)
+                self._sync_sharded(group, narrow)
+                return
+            if narrow and (dist_sync_fn is None or dist_sync_fn is gather_all_tensors):
+                self.score_hist = self.score_hist.to(torch.int32)
+                try:
+                    super()._sync_dist(dist_sync_fn, process_group)
+                finally:
+                    self.score_hist = self.score_hist.long()
                 return
         super()._sync_dist(dist_sync_fn, process_group)
 
