@@ -32,7 +32,7 @@ if [[ $STEPS == *prof* ]]; then
   find $OUT/prof -name "*kernel_stats.csv" | head -3
 fi
 if [[ $STEPS == *domain* ]]; then
-  timeout -k 10 900 python tools/domain_bench.py > $OUT/domain_bench.json 2> $OUT/domain_bench.err; stop_if_fatal $? domain; cat $OUT/domain_bench.json
+  timeout -k 10 900 python tools/domain_bench.py ${DOMAIN_ARGS:-} > $OUT/domain_bench.json 2> $OUT/domain_bench.err; stop_if_fatal $? domain; cat $OUT/domain_bench.json
 fi
 if [[ $STEPS == *kkern* ]]; then
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_kern -o kern --output-format csv -- python3 tools/kbench_kernels.py > $OUT/kbench_kernels.log 2>&1; stop_if_fatal $? kkern
