@@ -61,39 +61,43 @@ template <> __device__ __forceinline__ int score_code<__half>(uint16_t b) {
 
 // ---------------------------------------------------------------------------------------------------------
 // Two-pass multiclass histogram (C % 8 == 0, C <= 1024):
-//   (A) row pass  — one wave per row pair: 16-B vector loads, fp32 softmax (if flagged) rounded to the input
-//       dtype, argmax (fused confusion matrix), 16-bit code per element with flag bits
-//       (bit 14 = positive label, bit 15 = skip).  Codes of a 64-row tile are transposed to class-major
-//       through an LDS tile [C][32 dwords] (two rows packed per dword), XOR-swizzled by class group so both
-//       the scattered writes and the row read-out are bank-conflict free, then stored as 128-B segments of
-//       a class-major scratch codes[C][n_pad].
-//   (B) class pass — one workgroup per (class, row split): negatives counted in an LDS-privatised u32
-//       histogram (64 KiB, two workgroups per CU), positives (1/C of the data) straight to global; one
-//       int64 atomic per non-empty bin on flush (consecutive codes -> contiguous atomics).
-// Replaces 1 scattered 64-bit global atomic per score (2.8 ms/update at 65536x1000 on MI355X).
+//   (A) row pass (mc_codes_kernel) — one 512-thread block per 32-row tile, two blocks per CU (64-KiB LDS image,
+//       <= 128 VGPRs).  A wave owns 2 row pairs; all four rows are loaded up front (16-B vector loads), then per
+//       row: fp32 softmax (if the mode says so) with expf's exact instruction sequence and a correctly rounded
+//       quotient, rounded to the input dtype; arg-max (fused confusion matrix); 16-bit code per element (bit 14 =
+//       positive label, bit 15 = skip).  The two rows of a pair are packed per dword (v_perm) into an LDS image
+//       [512 NG][16 dwords], pair slot XOR-swizzled by class group (conflict-free writes), then stored as 16-B
+//       pieces of 64-B segments of a class-major scratch codes[C][n_pad] (XCD-aware tile order).
+//   (B) rare rows (mc_slow_rows_kernel) — a row with NaN / +-inf (torch: NaN arg-max semantics, all-NaN softmax)
+//       is appended to a device list by (A) and finished by a separate bounded kernel, keeping (A)'s fast path
+//       free of per-element special cases.
+//   (C) class pass (class_hist_kernel) — one workgroup per (class, row split): negatives counted in an
+//       LDS-privatised u32 histogram (64 KiB), positives straight to global; one int64 RMW per non-empty bin.
+// Measured on MI355X, 65536 x 1000 bf16 logits (tools/kexp/curve_hist_exp.hip): row pass 60 us vs 129 us for the
+// previous one-wave-per-row design (profiles/kexp_rowpass.json).
 // ---------------------------------------------------------------------------------------------------------
-constexpr int kTileRows = 32;   // 16 packed dwords per class -> 64 KiB LDS at C=1024, 2 WGs/CU
-constexpr int kA_Threads = 512;
+constexpr int kRowThreads = 512;
+constexpr int kRowWaves = kRowThreads / kWave;
+constexpr int kTileRows = 32;          // rows per tile: 16 row pairs, 2 per wave
+constexpr int kSlots = kTileRows / 2;  // pair slots = dwords per class per tile (64-B segment of a class row)
 
 template <typename T> __device__ __forceinline__ void unpack8(const uint4& w, float* v);
+// bf16 -> fp32 through the type conversion (not a bit shift): the compiler then knows the values are canonical and
+// emits plain v_max / v_max3 instead of a canonicalising v_max x, x per element.
 template <> __device__ __forceinline__ void unpack8<__hip_bfloat16>(const uint4& w, float* v) {
   const uint32_t p[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    v[2 * k] = __uint_as_float(p[k] << 16);
-    v[2 * k + 1] = __uint_as_float(p[k] & 0xFFFF0000u);
+    v[2 * k] = static_cast<float>(__builtin_bit_cast(__bf16, static_cast<uint16_t>(p[k] & 0xFFFFu)));
+    v[2 * k + 1] = static_cast<float>(__builtin_bit_cast(__bf16, static_cast<uint16_t>(p[k] >> 16)));
   }
 }
 template <> __device__ __forceinline__ void unpack8<__half>(const uint4& w, float* v) {
   const uint32_t p[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    __half lo, hi;
-    uint16_t l16 = p[k] & 0xFFFF, h16 = p[k] >> 16;
-    lo = *reinterpret_cast<__half*>(&l16);
-    hi = *reinterpret_cast<__half*>(&h16);
-    v[2 * k] = __half2float(lo);
-    v[2 * k + 1] = __half2float(hi);
+    v[2 * k] = static_cast<float>(__builtin_bit_cast(_Float16, static_cast<uint16_t>(p[k] & 0xFFFFu)));
+    v[2 * k + 1] = static_cast<float>(__builtin_bit_cast(_Float16, static_cast<uint16_t>(p[k] >> 16)));
   }
 }
 template <typename T> __device__ __forceinline__ uint16_t raw_bits(const uint4& w, int e) {
@@ -101,198 +105,329 @@ template <typename T> __device__ __forceinline__ uint16_t raw_bits(const uint4& 
   return (e & 1) ? (p[e >> 1] >> 16) : (p[e >> 1] & 0xFFFF);
 }
 
-// Ablation switches (standalone harness only; the library instantiates ABL = 0).
-constexpr int kAblNoStore = 1;    // skip the class-major scratch store
-constexpr int kAblNoNorm = 2;     // skip exp/div (raw codes)
-constexpr int kAblNoLds = 4;      // skip the LDS transpose
+// ---- wave reductions: DPP row ops (quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror, row_mirror) leave the 16-lane
+// row's result in every lane of the row; row_bcast:15 (rows 1,3) and row_bcast:31 (rows 2,3) fold the rows into
+// lane 63, read back as a wave-uniform scalar — 6 DPP ops + 1 readlane instead of 6 ds_bpermute round trips.
+template <int CTRL, int ROW_MASK = 0xF>
+__device__ __forceinline__ float dpp_f32(float old, float src) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(old), __float_as_int(src), CTRL, ROW_MASK, 0xF, false));
+}
+template <int CTRL, int ROW_MASK = 0xF>
+__device__ __forceinline__ int dpp_i32(int old, int src) {
+  return __builtin_amdgcn_update_dpp(old, src, CTRL, ROW_MASK, 0xF, false);
+}
+// max / min through order-preserving integer keys (sign-magnitude -> two's complement): integer max has no NaN
+// canonicalisation, so each step folds into one v_max_i32_dpp.  Callers pass NaN-free lane values (fmaxf/fminf
+// partials drop NaN); -0.0 orders below +0.0, which only matters to == comparisons, where the two are equal.
+__device__ __forceinline__ int f32_key(float f) { const int v = __float_as_int(f); return v ^ ((v >> 31) & 0x7FFFFFFF); }
+__device__ __forceinline__ float key_f32(int v) { return __int_as_float(v ^ ((v >> 31) & 0x7FFFFFFF)); }
+__device__ __forceinline__ float wave_max_uniform(float f) {
+  int v = f32_key(f);
+  v = max(v, dpp_i32<0xB1>(v, v));
+  v = max(v, dpp_i32<0x4E>(v, v));
+  v = max(v, dpp_i32<0x141>(v, v));
+  v = max(v, dpp_i32<0x140>(v, v));
+  v = max(v, dpp_i32<0x142, 0xA>(v, v));
+  v = max(v, dpp_i32<0x143, 0xC>(v, v));
+  return key_f32(__builtin_amdgcn_readlane(v, 63));
+}
+__device__ __forceinline__ float wave_min_uniform(float f) {
+  int v = f32_key(f);
+  v = min(v, dpp_i32<0xB1>(v, v));
+  v = min(v, dpp_i32<0x4E>(v, v));
+  v = min(v, dpp_i32<0x141>(v, v));
+  v = min(v, dpp_i32<0x140>(v, v));
+  v = min(v, dpp_i32<0x142, 0xA>(v, v));
+  v = min(v, dpp_i32<0x143, 0xC>(v, v));
+  return key_f32(__builtin_amdgcn_readlane(v, 63));
+}
+__device__ __forceinline__ float wave_sum_uniform(float v) {
+  v += dpp_f32<0xB1>(0.f, v);
+  v += dpp_f32<0x4E>(0.f, v);
+  v += dpp_f32<0x141>(0.f, v);
+  v += dpp_f32<0x140>(0.f, v);
+  v += dpp_f32<0x142, 0xA>(0.f, v);
+  v += dpp_f32<0x143, 0xC>(0.f, v);
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
 
-// Normalisation mode (sigmoid/softmax-if-any-value-outside-[0,1]) is *speculated*: ``mode[0]`` holds the mode
-// used by this launch (the previous batch's verdict, or the range_flag pre-pass result), the kernel records the
-// real verdict for this batch in ``mode[1]`` (plain store of 1 by any block that saw a witness; only
-// non-ignored rows count, as in the reference).  A FIXUP launch of the same kernel exits immediately unless
-// mode[0] != mode[1], in which case it recomputes the codes with the real mode (confusion matrix and error
-// flags are mode independent and are not touched again).  ``class_hist_kernel`` then rolls the prediction
-// forward (mode[0] = mode[1], mode[1] = 0).  Net effect: no separate 131-MB range pass per update.
-// RNE fp32 -> 16-bit pattern without NaN special-casing (NaN / out-of-range patterns are rejected by score_code).
-template <typename T> __device__ __forceinline__ uint32_t rne16(float f);
-template <> __device__ __forceinline__ uint32_t rne16<__hip_bfloat16>(float f) {
+// exp(x) for x <= 0, -inf or NaN: the instruction sequence the compiler emits for expf (2^(x log2e) with a
+// split-precision product, v_exp_f32 on the fractional part, ldexp by the rounded integer part, exact 0 below
+// -103.97) minus the x > 88.72 -> inf test.  Contraction is off: (ph - e) must be a rounded subtraction.
+__device__ __forceinline__ float exp_nonpos(float x) {
+#pragma clang fp contract(off)
+  const float log2e_hi = __uint_as_float(0x3fb8aa3bu), log2e_lo = __uint_as_float(0x32a5705fu);
+  const float ph = x * log2e_hi;
+  float pl = __builtin_fmaf(x, log2e_hi, -ph);
+  const float e = __builtin_rintf(ph);
+  pl = __builtin_fmaf(x, log2e_lo, pl);
+  const float r = __builtin_amdgcn_exp2f((ph - e) + pl);
+  const float y = __builtin_amdgcn_ldexpf(r, static_cast<int>(e));
+  return x < __uint_as_float(0xc2ce8ed0u) ? 0.f : y;
+}
+// correctly rounded e / s from the reciprocal: q = e r, residual e - q s (exact in fma), one correction step — the
+// quotient torch's softmax stores before rounding to 16 bits.
+__device__ __forceinline__ float div_rn(float e, float s, float rinv) {
+  const float q = e * rinv;
+  return __builtin_fmaf(__builtin_fmaf(-q, s, e), rinv, q);
+}
+
+// fp32 word whose high half is the RNE 16-bit rounding (bf16) — packed pairwise with v_perm afterwards.
+template <typename T> __device__ __forceinline__ uint32_t rne_word(float f);
+template <> __device__ __forceinline__ uint32_t rne_word<__hip_bfloat16>(float f) {
   const uint32_t u = __float_as_uint(f);
-  return (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;
+  return u + 0x7FFFu + ((u >> 16) & 1u);
 }
-template <> __device__ __forceinline__ uint32_t rne16<__half>(float f) { return round_bits16<__half>(f); }
+template <> __device__ __forceinline__ uint32_t rne_word<__half>(float f) { return (uint32_t)round_bits16<__half>(f) << 16; }
 
-// softmax output code: RNE16(e * (1/s)).  The reciprocal form differs from an IEEE ``e / s`` by <= 1 fp32 ulp,
-// i.e. it moves a value across a 16-bit rounding boundary with probability ~2^-16 — the same order as the
-// summation-order differences every softmax implementation already has (tests bound the flip rate).
-template <typename T> __device__ __forceinline__ uint32_t quot_code(float e, float rinv) { return rne16<T>(e * rinv); }
-
-// LDS tile [C][kSlots] dwords, 2 rows per dword (u16 halves), slot XOR-swizzled by the class group q so the
-// per-lane scattered writes are (2-way at most) conflict free and the row read-out is conflict free.
-template <int ABL>
-__device__ __forceinline__ void lds_put(uint16_t* s_tile16, int c, int C, int q, int p, int h, uint32_t code) {
-  constexpr int kSlots = kTileRows / 2;
-  if constexpr (!(ABL & kAblNoLds)) {
-    if (c < C) s_tile16[2 * (c * kSlots + (p ^ (q & (kSlots - 1)))) + h] = static_cast<uint16_t>(code);
-  } else {
-    if (code == 0x1234u) s_tile16[threadIdx.x] = 0;  // keep the computation alive
-  }
+// 16-bit code of a raw score pattern: -0.0 -> 0, [0, 1] -> itself, anything else (negative, > 1, inf, NaN) -> skip
+template <typename T> __device__ __forceinline__ uint32_t raw_code(uint32_t b) {
+  return b == 0x8000u ? 0u : (b <= RangeBits<T>::one ? b : 0x8000u);
 }
 
-// One row of up to 1024 classes lives in 2 x 16 B per lane: element j of lane -> class 8 * (lane + 64 * (j>>3)) + (j&7).
-template <typename T, int ABL>
-__device__ __forceinline__ void codes_for_row(const uint4 (&w)[2], int64_t t, bool valid, int C, int nvec, int lane,
-                                              bool do_softmax, bool fixup, int64_t* __restrict__ confmat,
-                                              int* __restrict__ err, bool& saw_bad, bool record_mode, int h, int p,
-                                              uint16_t* __restrict__ s_tile16) {
-  float v[16];
-  bool has_nan = false;
+// Per-row statistics of one wave's share of a row (16 elements per lane for C <= 1024, 8 for C <= 512).
+template <int NG>
+struct RowStat {
+  float v[8 * NG];
+  float mlo, mhi, mx;  // lane maxima of class groups 0 / 1, wave maximum
+  float mn, sum;       // lane minimum and lane sum of the valid elements (probability mode / range witness)
+};
+
+template <typename T, int NG>
+__device__ __forceinline__ void row_stat(const uint4 (&w)[2], bool lo_ok, bool hi_ok, RowStat<NG>& r) {
+  unpack8<T>(w[0], r.v);
+  if constexpr (NG == 1) {  // C <= 512: lanes >= C / 8 hold a clamped duplicate, not classes
 #pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const int q = lane + kWave * k;
-    const bool ok = valid && q < nvec;
-    float tmp[8];
-    unpack8<T>(w[k], tmp);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      v[8 * k + e] = ok ? tmp[e] : -INFINITY;
-      has_nan |= ok && (tmp[e] != tmp[e]);
-      if (!fixup && record_mode && ok) saw_bad |= bad16<T>(raw_bits<T>(w[k], e));
-    }
+    for (int j = 0; j < 8; ++j) r.v[j] = lo_ok ? r.v[j] : -INFINITY;
   }
-  float mx = -INFINITY;
-  if (!fixup || do_softmax) {
-    // lane-local arg-max in increasing class order (strict > keeps the first maximum)
-    float m = v[0];
-    int am = 8 * lane;
-#pragma unroll
-    for (int j = 1; j < 16; ++j) {
-      const int c = 8 * (lane + kWave * (j >> 3)) + (j & 7);
-      if (v[j] > m) { m = v[j]; am = c; }
-    }
-    if (m == -INFINITY) am = C;  // nothing valid in this lane (or all -inf): never wins a tie
-    mx = m;
-    int amx = am;
-    wave_argmax(mx, amx);
-    if (__ballot(has_nan)) {  // rare: torch.argmax returns the first NaN
-      int first = C;
-#pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        const int c = 8 * (lane + kWave * (j >> 3)) + (j & 7);
-        if (v[j] != v[j] && c < first) first = c;
-      }
-#pragma unroll
-      for (int off = 32; off > 0; off >>= 1) first = min(first, __shfl_xor(first, off, kWave));
-      amx = first;
-    }
-    if (!fixup && valid && confmat != nullptr && lane == 0 && t >= 0 && t < C && amx < C) atomic_add_i64(confmat + t * C + amx, 1);
-    if (!fixup && valid && (t < 0 || t >= C) && err != nullptr && lane == 0) atomicOr(err, 1);
+  r.mlo = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaxf(r.v[0], r.v[1]), __builtin_fmaxf(r.v[2], r.v[3])),
+                          __builtin_fmaxf(__builtin_fmaxf(r.v[4], r.v[5]), __builtin_fmaxf(r.v[6], r.v[7])));
+  r.mn = __builtin_fminf(__builtin_fminf(__builtin_fminf(r.v[0], r.v[1]), __builtin_fminf(r.v[2], r.v[3])),
+                         __builtin_fminf(__builtin_fminf(r.v[4], r.v[5]), __builtin_fminf(r.v[6], r.v[7])));
+  r.sum = ((r.v[0] + r.v[1]) + (r.v[2] + r.v[3])) + ((r.v[4] + r.v[5]) + (r.v[6] + r.v[7]));
+  if constexpr (NG == 1) {
+    r.mn = lo_ok ? r.mn : INFINITY;
+    r.sum = lo_ok ? r.sum : 0.f;
   }
-  if (do_softmax && !(ABL & kAblNoNorm)) {
-    float acc = 0.f;
+  r.mhi = -INFINITY;
+  if constexpr (NG == 2) {
+    float u[8];
+    unpack8<T>(w[1], u);
+    const float mh = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaxf(u[0], u[1]), __builtin_fmaxf(u[2], u[3])),
+                                     __builtin_fmaxf(__builtin_fmaxf(u[4], u[5]), __builtin_fmaxf(u[6], u[7])));
+    const float nh = __builtin_fminf(__builtin_fminf(__builtin_fminf(u[0], u[1]), __builtin_fminf(u[2], u[3])),
+                                     __builtin_fminf(__builtin_fminf(u[4], u[5]), __builtin_fminf(u[6], u[7])));
+    const float sh = ((u[0] + u[1]) + (u[2] + u[3])) + ((u[4] + u[5]) + (u[6] + u[7]));
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      v[j] = expf(v[j] - mx);  // -inf (padding) -> 0
-      acc += v[j];
-    }
-    const float s = wave_sum(acc);
-    const float rinv = 1.f / s;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const int c = 8 * (lane + kWave * (j >> 3)) + (j & 7);
-      uint32_t code = 0x8000u;
-      if (valid && c < C) {
-        const int sc = score_code<T>(static_cast<uint16_t>(quot_code<T>(v[j], rinv)));
-        code = sc < 0 ? 0x8000u : (uint32_t)sc | (c == t ? 0x4000u : 0u);
-      }
-      lds_put<ABL>(s_tile16, c, C, lane + kWave * (j >> 3), p, h, code);
-    }
-  } else {
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const int c = 8 * (lane + kWave * (j >> 3)) + (j & 7);
-      uint32_t code = 0x8000u;
-      if (valid && c < C) {
-        const int sc = score_code<T>(raw_bits<T>(w[j >> 3], j & 7));
-        code = sc < 0 ? 0x8000u : (uint32_t)sc | (c == t ? 0x4000u : 0u);
-      }
-      lds_put<ABL>(s_tile16, c, C, lane + kWave * (j >> 3), p, h, code);
-    }
+    for (int j = 0; j < 8; ++j) r.v[8 + j] = hi_ok ? u[j] : -INFINITY;  // padding classes never win / add 0 to exp-sums
+    r.mhi = hi_ok ? mh : -INFINITY;
+    r.mn = hi_ok ? __builtin_fminf(r.mn, nh) : r.mn;
+    r.sum = hi_ok ? r.sum + sh : r.sum;
   }
+  r.mx = wave_max_uniform(__builtin_fmaxf(r.mlo, r.mhi));
 }
 
-// Persistent, software-pipelined row pass.  Each wave walks its row pairs (2 per 32-row tile) and always has the
-// NEXT pair's 2 x 2 x 16 B loads in flight while it computes the current pair.
-template <typename T, bool FIXUP, int ABL = 0>
-__global__ void __launch_bounds__(kA_Threads, 4) mc_codes_kernel(const T* __restrict__ preds, const int64_t* __restrict__ target,
-                                                                  int64_t n, int C, int* __restrict__ mode,
-                                                                  int64_t ignore_index, bool has_ignore,
-                                                                  uint32_t* __restrict__ codes, int64_t n_pad,
-                                                                  int64_t* __restrict__ confmat, int* __restrict__ err,
-                                                                  bool record_mode) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t s_tile[];  // [C][kTileRows / 2]
-  constexpr int kSlots = kTileRows / 2;
-  constexpr int kWavesPerBlock = kA_Threads / kWave;
-  constexpr int kPairsPerWave = kSlots / kWavesPerBlock;
+// arg-max of a row without NaN / inf: first class (ascending) holding the wave maximum.  Classes of group g, lane L,
+// slot k are 512 g + 8 L + k, so the winner is the lowest lane whose group-0 maximum equals mx (else the lowest lane
+// of group 1) and the lowest slot of that lane.
+template <int NG>
+__device__ __forceinline__ int row_argmax(const RowStat<NG>& r) {
+  const uint64_t blo = __ballot(r.mlo == r.mx);
+  const int g = blo != 0 ? 0 : 1;
+  const uint64_t b = blo != 0 ? blo : __ballot(r.mhi == r.mx);
+  const int L = __builtin_ctzll(b | (1ull << 63));
+  int klo = 7, khi = 7;
+#pragma unroll
+  for (int j = 6; j >= 0; --j) {
+    klo = (r.v[j] == r.mx) ? j : klo;
+    if constexpr (NG == 2) khi = (r.v[8 + j] == r.mx) ? j : khi;
+  }
+  return 512 * g + 8 * L + __builtin_amdgcn_readlane(g == 0 ? klo : khi, L);
+}
+
+struct SlowRows {
+  int* rows;   // [2][n]: list 0 = rows of the speculated-mode pass, list 1 = rows of a FIXUP pass
+  int* count;  // [2]
+};
+
+// One 32-row tile of the row pass for a fixed normalisation (SOFTMAX).  Every load is issued up front; stores and
+// global atomics come only after the last wait (a VMEM write pending behind a load makes the compiler drain the
+// whole queue at the next wait).
+
+template <typename T, int NG, bool SOFTMAX, bool FIXUP>
+__device__ __forceinline__ void row_tile(const T* __restrict__ preds, const int64_t* __restrict__ target, int64_t n, int C,
+                                          int64_t ignore_index, bool has_ignore, uint32_t* __restrict__ codes, int64_t n_pad,
+                                          int64_t* __restrict__ confmat, int* __restrict__ err, bool rec, bool& saw_bad,
+                                          SlowRows slow, uint32_t* __restrict__ s_tile, int64_t tile) {
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = threadIdx.x / kWave;
+  const int nvec = C / 8;
+  const bool lo_ok = lane < nvec, hi_ok = lane + kWave < nvec;
+  const int lq = lo_ok ? lane : nvec - 1;  // clamped: every load stays inside its row
+  const int hq = hi_ok ? lane + kWave : nvec - 1;
+  uint4 raw[2][2][2];
+  auto row0_of = [&](int pp) -> int64_t { return tile * kTileRows + 2 * (wave + pp * kRowWaves); };
+  const int64_t tv = target[min(row0_of((lane & 3) >> 1) + (lane & 1), n - 1)];
+#pragma unroll
+  for (int pp = 0; pp < 2; ++pp)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const uint4* row = reinterpret_cast<const uint4*>(preds + min(row0_of(pp) + h, n - 1) * C);
+      raw[pp][h][0] = row[lq];
+      if constexpr (NG == 2) raw[pp][h][1] = row[hq];
+    }
+  auto target_of = [&](int i) -> int64_t {
+    const uint64_t u = static_cast<uint64_t>(tv);
+    const uint32_t lo = __builtin_amdgcn_readlane(static_cast<uint32_t>(u), i);
+    const uint32_t hi = __builtin_amdgcn_readlane(static_cast<uint32_t>(u >> 32), i);
+    return static_cast<int64_t>((static_cast<uint64_t>(hi) << 32) | lo);
+  };
+  int64_t tt[4];
+  int am[4];
+  bool keepv[4], slowv[4], validv[4];
+#pragma unroll
+  for (int pp = 0; pp < 2; ++pp) {
+    const int p = wave + pp * kRowWaves;
+    const int64_t r0 = row0_of(pp);
+    const int64_t ta = target_of(2 * pp), tb = target_of(2 * pp + 1);
+    const bool va = r0 < n && !(has_ignore && ta == ignore_index);
+    const bool vb = r0 + 1 < n && !(has_ignore && tb == ignore_index);
+    RowStat<NG> ra, rb;
+    row_stat<T, NG>(raw[pp][0], lo_ok, hi_ok, ra);
+    row_stat<T, NG>(raw[pp][1], lo_ok, hi_ok, rb);
+    bool fa = __builtin_isfinite(ra.mx), fb = __builtin_isfinite(rb.mx);
+    const int ama = row_argmax<NG>(ra), amb = row_argmax<NG>(rb);
+    float sa = 0.f, sb = 0.f, ia = 0.f, ib = 0.f;
+    if constexpr (SOFTMAX) {
+      float acc_a = 0.f, acc_b = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8 * NG; ++j) {
+        ra.v[j] = exp_nonpos(ra.v[j] - ra.mx);
+        rb.v[j] = exp_nonpos(rb.v[j] - rb.mx);
+        acc_a += ra.v[j];
+        acc_b += rb.v[j];
+      }
+      sa = wave_sum_uniform(acc_a);
+      sb = wave_sum_uniform(acc_b);
+      ia = 1.f / sa;
+      ib = 1.f / sb;
+      fa = fa && sa == sa;
+      fb = fb && sb == sb;
+    } else {
+      fa = fa && __builtin_isfinite(wave_sum_uniform(ra.sum));
+      fb = fb && __builtin_isfinite(wave_sum_uniform(rb.sum));
+    }
+    const bool slow_a = va && !fa, slow_b = vb && !fb;
+    if (rec && !saw_bad) {
+      saw_bad = slow_a || slow_b || (va && ra.mx > 1.f) || (vb && rb.mx > 1.f);
+      if (!saw_bad && (va || vb))
+        saw_bad = wave_min_uniform(__builtin_fminf(va ? ra.mn : INFINITY, vb ? rb.mn : INFINITY)) < 0.f;
+    }
+    const bool ka = va && fa, kb = vb && fb;
+    const uint32_t keep = (ka ? 0x0000FFFFu : 0u) | (kb ? 0xFFFF0000u : 0u);
+    const uint32_t setm = ~keep & 0x80008000u;
+#pragma unroll
+    for (int j = 0; j < 8 * NG; ++j) {
+      uint32_t packed;
+      if constexpr (SOFTMAX) {
+        packed = __builtin_amdgcn_perm(rne_word<T>(div_rn(rb.v[j], sb, ib)), rne_word<T>(div_rn(ra.v[j], sa, ia)), 0x07060302u);
+      } else {
+        const uint32_t ca = raw_code<T>(raw_bits<T>(raw[pp][0][j >> 3], j & 7));
+        const uint32_t cb = raw_code<T>(raw_bits<T>(raw[pp][1][j >> 3], j & 7));
+        packed = ca | (cb << 16);
+      }
+      const int c = 512 * (j >> 3) + 8 * lane + (j & 7);
+      s_tile[c * kSlots + (p ^ (lane & (kSlots - 1)))] = (packed & keep) | setm;
+    }
+    if (lane == 0) {
+      if (ka && ta >= 0 && ta < C) atomicOr(&s_tile[ta * kSlots + (p ^ ((int)(ta >> 3) & (kSlots - 1)))], 0x00004000u);
+      if (kb && tb >= 0 && tb < C) atomicOr(&s_tile[tb * kSlots + (p ^ ((int)(tb >> 3) & (kSlots - 1)))], 0x40000000u);
+    }
+    tt[2 * pp] = ta; tt[2 * pp + 1] = tb;
+    am[2 * pp] = ama; am[2 * pp + 1] = amb;
+    keepv[2 * pp] = ka; keepv[2 * pp + 1] = kb;
+    slowv[2 * pp] = slow_a; slowv[2 * pp + 1] = slow_b;
+    validv[2 * pp] = va; validv[2 * pp + 1] = vb;
+  }
+  // global side effects after every load has been consumed
+  if (lane == 0) {
+    const int list = FIXUP ? 1 : 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int64_t t = tt[i];
+      if constexpr (!FIXUP) {
+        if (confmat != nullptr && keepv[i] && t >= 0 && t < C && am[i] < C) atomic_add_i64(confmat + t * C + am[i], 1);
+        if (err != nullptr && validv[i] && (t < 0 || t >= C)) atomicOr(err, 1);
+      }
+      if (slowv[i]) slow.rows[list * n + atomicAdd(slow.count + list, 1)] = static_cast<int>(row0_of(i >> 1) + (i & 1));
+    }
+  }
+  __syncthreads();
+  {
+    constexpr int kQuads = kSlots / 4;  // 4 x 16 B per class per tile
+    const int64_t seg = tile * kSlots;
+    const int64_t row_dw = n_pad / 2;
+#pragma unroll
+    for (int k = 0; k < 512 * NG * kQuads / kRowThreads; ++k) {
+      const int idx = threadIdx.x + k * kRowThreads;
+      const int c = idx / kQuads, g = idx % kQuads;
+      const int sw = (c >> 3) & (kSlots - 1);
+      const uint4 w = *reinterpret_cast<const uint4*>(&s_tile[c * kSlots + 4 * (g ^ (sw >> 2))]);
+      const int x = sw & 3;
+      const uint32_t e0 = x & 1 ? w.y : w.x, e1 = x & 1 ? w.x : w.y, e2 = x & 1 ? w.w : w.z, e3 = x & 1 ? w.z : w.w;
+      const uint4 o = x & 2 ? make_uint4(e2, e3, e0, e1) : make_uint4(e0, e1, e2, e3);
+      if (c < C) *reinterpret_cast<uint4*>(&codes[c * row_dw + seg + 4 * g]) = o;
+    }
+  }
+}
+
+// Normalisation mode (softmax if any valid score is outside [0, 1], as the reference decides per batch) is
+// *speculated*: ``mode[0]`` is the mode this launch uses (the previous batch's verdict), the kernel records the real
+// verdict for this batch in ``mode[1]`` (a plain store of 1 by any block that saw a witness).  A FIXUP launch exits
+// at once unless mode[0] != mode[1], in which case it redoes the codes with the real mode (confusion matrix and error
+// flags are mode independent and are not touched again).  ``class_hist_kernel`` rolls mode[0] = mode[1].
+// Grid: one block per tile for the main launch (blocks stride over tiles, so a FIXUP launch can use a small grid).
+template <typename T, bool FIXUP, int NG>
+__global__ void __launch_bounds__(kRowThreads, 4) mc_codes_kernel(const T* __restrict__ preds, const int64_t* __restrict__ target,
+                                                                    int64_t n, int C, int* __restrict__ mode,
+                                                                    int64_t ignore_index, bool has_ignore,
+                                                                    uint32_t* __restrict__ codes, int64_t n_pad,
+                                                                    int64_t* __restrict__ confmat, int* __restrict__ err,
+                                                                    bool record_mode, int* __restrict__ slow_rows,
+                                                                    int* __restrict__ slow_count) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_tile[];  // [512 * NG][kSlots]
   int use_mode;
   if constexpr (FIXUP) {
     const int m0 = __hip_atomic_load(mode, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int m1 = __hip_atomic_load(mode + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (m0 == m1) return;  // speculation was right (the common case): nothing to redo
+    if (m0 == m1) return;
     use_mode = m1;
   } else {
     use_mode = mode[0];
   }
-  const bool do_softmax = use_mode != 0;
-  bool saw_bad = false;
-  const int nvec = C / 8;
+  // XCD-aware tile order: dispatch round-robins blocks over the 8 XCDs (block b -> XCD b % 8), so give each XCD a
+  // contiguous run of tiles: tiles 2q and 2q+1 then run on one XCD and the two 64-B halves of every 128-B line of
+  // the class-major scratch meet in that XCD's L2 before write-back.
   const int64_t ntiles = (n + kTileRows - 1) / kTileRows;
-
-  // row sequence of this wave inside a tile: local rows {2w, 2w+1, 2w+16, 2w+17, ...} (pairs w, w+8)
-  auto local_row = [&](int i) { return 2 * (wave + (i >> 1) * kWavesPerBlock) + (i & 1); };
-  constexpr int kRowsPerWave = 2 * kPairsPerWave;
-  auto load_row = [&](int64_t tl, int lr, uint4 (&w)[2], int64_t& tv) {
-    const int64_t r = tl * kTileRows + lr;
-    const bool in = tl < ntiles && r < n;
-    tv = in ? target[r] : INT64_MIN;
-    const uint4* row = reinterpret_cast<const uint4*>(preds + (in ? r : 0) * C);
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int q = lane + kWave * k;
-      w[k] = (in && q < nvec) ? row[q] : make_uint4(0, 0, 0, 0);
-    }
+  const int64_t per_xcd = (ntiles + 7) / 8;
+  const bool rec = !FIXUP && record_mode;
+  bool saw_bad = false;
+  const SlowRows slow{slow_rows, slow_count};
+  auto run_tile = [&](int64_t b) {
+    const int64_t tile = (b % 8) * per_xcd + b / 8;
+    if (tile >= ntiles) return;
+    if (use_mode != 0)
+      row_tile<T, NG, true, FIXUP>(preds, target, n, C, ignore_index, has_ignore, codes, n_pad, confmat, err, rec, saw_bad, slow, s_tile, tile);
+    else
+      row_tile<T, NG, false, FIXUP>(preds, target, n, C, ignore_index, has_ignore, codes, n_pad, confmat, err, rec, saw_bad, slow, s_tile, tile);
   };
-
-  uint4 wcur[2], wnext[2];
-  int64_t tcur, tnext;
-  int64_t tile = blockIdx.x;
-  load_row(tile, local_row(0), wcur, tcur);
-  for (; tile < ntiles; tile += gridDim.x) {
-#pragma unroll 1
-    for (int i = 0; i < kRowsPerWave; ++i) {
-      // keep the next row's loads in flight while this row is computed
-      if (i + 1 < kRowsPerWave) load_row(tile, local_row(i + 1), wnext, tnext);
-      else load_row(tile + gridDim.x, local_row(0), wnext, tnext);
-      const bool valid = tcur != INT64_MIN && !(has_ignore && tcur == ignore_index);
-      codes_for_row<T, ABL>(wcur, tcur, valid, C, nvec, lane, do_softmax, FIXUP, confmat, err, saw_bad, record_mode,
-                            i & 1, wave + (i >> 1) * kWavesPerBlock, reinterpret_cast<uint16_t*>(s_tile));
-      tcur = tnext;
-      wcur[0] = wnext[0];
-      wcur[1] = wnext[1];
+  if constexpr (FIXUP) {  // rare: blocks stride over the tiles (small grid, cheap early exit)
+    for (int64_t b = blockIdx.x; b < per_xcd * 8; b += gridDim.x) {
+      run_tile(b);
+      __syncthreads();  // the LDS image is rewritten by the next tile of this block
     }
-    __syncthreads();
-    if constexpr (!(ABL & kAblNoStore)) {
-      const int64_t seg = tile * (kTileRows / 2);  // dword offset of this tile inside a class row
-      const int64_t row_dw = n_pad / 2;
-      for (int idx = threadIdx.x; idx < C * kSlots; idx += kA_Threads) {
-        const int c = idx / kSlots, d = idx % kSlots;
-        const uint32_t wv = s_tile[idx];
-        const int p = d ^ ((c >> 3) & (kSlots - 1));
-        codes[c * row_dw + seg + p] = wv;
-      }
-    }
-    __syncthreads();
+  } else {  // one tile per block: no loop, so nothing of one tile's register state lives across another's
+    run_tile(blockIdx.x);
   }
   if constexpr (!FIXUP) {
     if (record_mode && __syncthreads_or(saw_bad) && threadIdx.x == 0 &&
@@ -301,13 +436,66 @@ __global__ void __launch_bounds__(kA_Threads, 4) mc_codes_kernel(const T* __rest
   }
 }
 
+// Rows with NaN / +-inf, one wave per listed row (bounded loop over the device-side count).  torch semantics: the
+// softmax of such a row is all NaN (every code skipped); in probability mode each score keeps its own code (NaN /
+// inf skipped); the arg-max is the first NaN, else the first maximum.  List 0 (speculated pass): confusion matrix
+// always, codes unless a FIXUP pass replaced them; list 1 (FIXUP pass): codes with the corrected mode.
+template <typename T>
+__global__ void __launch_bounds__(256) mc_slow_rows_kernel(const T* __restrict__ preds, const int64_t* __restrict__ target,
+                                                           int64_t n, int C, const int* __restrict__ mode, bool speculative,
+                                                           uint16_t* __restrict__ codes, int64_t n_pad,
+                                                           int64_t* __restrict__ confmat, const int* __restrict__ slow_rows,
+                                                           const int* __restrict__ slow_count) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t gw = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / kWave;
+  const int64_t nw = (int64_t)gridDim.x * blockDim.x / kWave;
+  const int m0 = mode[0];
+  const int m1 = speculative ? mode[1] : m0;
+  const bool fixed = speculative && m0 != m1;
+  const int64_t n0 = slow_count[0], n1 = slow_count[1];
+  for (int64_t i = gw; i < n0 + n1; i += nw) {
+    const int lst = i < n0 ? 0 : 1;
+    const int64_t r = slow_rows[lst * n + (lst == 0 ? i : i - n0)];
+    const int64_t t = target[r];
+    const T* row = preds + r * C;
+    const bool write_codes = lst == 1 || !fixed;
+    const bool softmax = (lst == 1 ? m1 : m0) != 0;
+    if (write_codes) {
+      for (int c = lane; c < C; c += kWave) {
+        const uint32_t code = softmax ? 0x8000u : raw_code<T>(bits16<T>(row[c]));
+        codes[(int64_t)c * n_pad + r] = static_cast<uint16_t>(code | (c == t ? 0x4000u : 0u));
+      }
+    }
+    if (lst == 0 && confmat != nullptr && t >= 0 && t < C) {
+      float best = -INFINITY;
+      int bi = C, first_nan = C;
+      for (int c = lane; c < C; c += kWave) {
+        const float v = to_f32<T>(row[c]);
+        if (v != v) first_nan = min(first_nan, c);
+        else if (bi == C || v > best) { best = v; bi = c; }  // ascending classes per lane: strict > keeps the first
+      }
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) first_nan = min(first_nan, __shfl_xor(first_nan, off, kWave));
+      float mb = best;
+      int mi = bi;
+      wave_argmax(mb, mi);
+      const int am = first_nan < C ? first_nan : mi;
+      if (lane == 0 && am < C) atomic_add_i64(confmat + t * C + am, 1);
+    }
+  }
+}
+
 __global__ void __launch_bounds__(512) class_hist_kernel(const uint16_t* __restrict__ codes, int64_t n_pad, int splits,
-                                                         int64_t* __restrict__ hist, int* __restrict__ mode_roll) {
+                                                         int64_t* __restrict__ hist, int* __restrict__ mode_roll,
+                                                         int* __restrict__ slow_count) {
   extern __shared__ __attribute__((aligned(16))) uint32_t s_neg[];  // [kCodes]
   const int c = blockIdx.x / splits, sp = blockIdx.x % splits;
-  if (mode_roll != nullptr && blockIdx.x == 0 && threadIdx.x == 0) {  // previous kernels are complete (stream order)
-    mode_roll[0] = mode_roll[1];
-    mode_roll[1] = 0;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {  // previous kernels are complete (stream order)
+    if (mode_roll != nullptr) {
+      mode_roll[0] = mode_roll[1];
+      mode_roll[1] = 0;
+    }
+    if (slow_count != nullptr) slow_count[0] = slow_count[1] = 0;
   }
   uint4* s4 = reinterpret_cast<uint4*>(s_neg);
   for (int i = threadIdx.x; i < kCodes / 4; i += blockDim.x) s4[i] = make_uint4(0, 0, 0, 0);

@@ -134,3 +134,64 @@ def test_module_auroc_confmat_gpu_matches_cpu():
         out.append({k: v.cpu() for k, v in coll.compute().items()})
     assert torch.equal(out[0]["cm"], out[1]["cm"])
     assert abs(out[0]["auroc"].item() - out[1]["auroc"].item()) < 1e-4
+
+
+def _rare_rows(x, probs):
+    """Sprinkle the rows the row pass hands to its rare-row kernel: NaN, +inf, all -inf, a single -inf, tied maxima."""
+    N, C = x.shape
+    x[5::97, 3] = float("nan")
+    x[11::131, (C // 2)] = float("inf")
+    x[17::211] = float("-inf")
+    x[13::89, 1] = float("-inf")
+    x[23::53, 0] = x[23::53, 2] = 0.75 if probs else 9.0
+    return x
+
+
+@pytest.mark.parametrize("C", [64, 512, 520, 1000])
+@pytest.mark.parametrize("probs", [False, True])
+def test_curve_hist_multiclass_rare_rows(C, probs):
+    """Rows with NaN / inf take mc_slow_rows_kernel: torch semantics (all-NaN softmax, first-NaN arg-max)."""
+    N = 4000
+    x = torch.randn(N, C)
+    x = _rare_rows(x.softmax(1) if probs else x, probs).bfloat16()
+    target = torch.randint(0, C, (N,))
+    target[::19] = -1
+    hist = torch.zeros(C, 2, K.N_CODES, dtype=torch.long)
+    cm = torch.zeros(C, C, dtype=torch.long)
+    g, c, _, _ = _both(K.curve_hist_update, x, target, hist, "multiclass", -1, cm)
+    assert torch.equal(g[5].cpu(), c[5])  # confusion matrix incl. NaN / all -inf rows is exact
+    diff = (g[2].cpu() - c[2]).abs().sum().item()
+    assert diff <= max(8, int(1e-3 * N * C)), diff
+    assert g[2].sum().item() == c[2].sum().item()
+
+
+def test_curve_speculation_flips_across_batches():
+    """The persistent mode word speculates softmax-vs-raw from the previous batch; a wrong guess is redone (FIXUP)."""
+    import torchmetrics_forked_amd as tm
+
+    C, N = 520, 3000
+    gen = torch.Generator().manual_seed(3)
+    batches = []
+    for kind in ("logits", "probs", "probs", "logits", "probs_nan", "logits", "small_logits"):
+        x = torch.randn(N, C, generator=gen)
+        if kind == "probs":
+            x = x.softmax(1)
+        elif kind == "probs_nan":
+            x = x.softmax(1)
+            x[7, 3] = float("nan")  # one NaN makes the reference softmax the whole batch
+        elif kind == "small_logits":
+            x = x.abs().clamp(max=1.0) * torch.where(torch.rand(N, C, generator=gen) < 0.5, -1.0, 1.0)  # max <= 1, some < 0
+        batches.append((x.bfloat16(), torch.randint(0, C, (N,), generator=gen)))
+    res = []
+    for dev in ("cuda", "cpu"):
+        m = tm.MulticlassAUROC(num_classes=C, average="macro").to(dev)
+        cmm = tm.MulticlassConfusionMatrix(num_classes=C).to(dev)
+        vals = []
+        for x, t in batches:
+            m.update(x.to(dev), t.to(dev))
+            cmm.update(x.to(dev), t.to(dev))
+            vals.append(m.compute().item())
+        res.append((vals, cmm.compute().cpu()))
+    assert torch.equal(res[0][1], res[1][1])
+    for a, b in zip(res[0][0], res[1][0]):
+        assert abs(a - b) < 1e-4, (res[0][0], res[1][0])

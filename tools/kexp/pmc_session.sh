@@ -1,17 +1,16 @@
 #!/bin/bash
-# PMC counter passes (kernel-trace only, no sys/runtime trace) over the standalone harness.
+# PMC passes (kernel-trace only) over the standalone harness; one counter group per run.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 OUT=gpurun_out/pmc
 mkdir -p $OUT
 export TMPDIR=/tmp
-rocprofv3 -L > $OUT/counters_list.txt 2>&1 || true
 i=0
 for set in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES" \
-           "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_SALU SQ_INSTS_SMEM" \
-           "FETCH_SIZE" "WRITE_SIZE" "TA_BUSY_avr GRBM_GUI_ACTIVE"; do
+           "SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_SALU SQ_INSTS_SMEM SQ_ACTIVE_INST_VMEM SQ_INST_CYCLES_VMEM" \
+           "FETCH_SIZE" "WRITE_SIZE" "TA_BUSY_avr GRBM_GUI_ACTIVE" "TCC_HIT_sum TCC_MISS_sum"; do
   i=$((i+1))
-  timeout -k 10 180 rocprofv3 --kernel-trace --pmc $set -d $OUT/p$i -o run --output-format csv -- ./build/curve_hist_exp > $OUT/p$i.log 2>&1
-  rc=$?; echo "pass $i rc=$rc"; if [ $rc -ge 124 ]; then exit $rc; fi
+  timeout -s KILL 90 rocprofv3 --kernel-trace --pmc $set -d $OUT/p$i -o run --output-format csv -- ./build/curve_hist_exp > $OUT/p$i.log 2>&1
+  rc=$?; echo "pass $i rc=$rc"; if [ $rc -ne 0 ]; then exit $rc; fi
 done
 echo pmc done
