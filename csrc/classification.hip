@@ -384,7 +384,7 @@ __global__ void __launch_bounds__(256) curve_hist_mc_kernel(const T* __restrict_
 }
 
 template <typename T>
-void launch_two_pass(const T* p, const int64_t* target, int64_t n, int C, int* mode, int* slow_count, bool speculative,
+void launch_two_pass(const T* p, const int64_t* target, int64_t n, int C, int* mode, int* state, bool speculative,
                      int64_t ignore_index, bool has_ignore, int64_t* hist, int64_t* cm, int* err, const at::TensorOptions& opts) {
   TORCH_CHECK(n < (int64_t{1} << 31), "curve_hist_update: more than 2^31 rows in one batch");
   const int64_t n_pad = (n + kTileRows - 1) / kTileRows * kTileRows;
@@ -392,38 +392,35 @@ void launch_two_pass(const T* p, const int64_t* target, int64_t n, int C, int* m
   auto slow_rows = at::empty({2 * n}, opts.dtype(at::kInt));
   const int64_t ntiles = n_pad / kTileRows;
   const int grid = static_cast<int>((ntiles + 7) / 8 * 8);  // one block per tile (XCD-aware order inside)
-  const int NG = C > 512 ? 2 : 1;
-  const size_t shm = (size_t)512 * NG * kSlots * sizeof(uint32_t);  // 32 / 64 KiB -> 2 blocks per CU
+  const int fixup_grid = std::min(grid, 128);                // exits at once unless the speculation was wrong
+  const size_t shm = (size_t)512 * (C > 512 ? 2 : 1) * kSlots * sizeof(uint32_t);  // 32 / 64 KiB -> 2 blocks per CU
   uint32_t* cptr = reinterpret_cast<uint32_t*>(codes.data_ptr());
   int* srows = slow_rows.data_ptr<int>();
-  if (NG == 2) {
+  if (C > 512) {
     hipLaunchKernelGGL((mc_codes_kernel<T, false, 2>), grid, kRowThreads, shm, stream(), p, target, n, C, mode, ignore_index,
-                       has_ignore, cptr, n_pad, cm, err, speculative, srows, slow_count);
+                       has_ignore, cptr, n_pad, cm, err, speculative, srows, state);
     TMX_LAUNCH_CHECK();
-    if (speculative) {  // a no-op unless this batch's verdict differs from the speculated mode: small grid
-      hipLaunchKernelGGL((mc_codes_kernel<T, true, 2>), std::min(grid, 512), kRowThreads, shm, stream(), p, target, n, C, mode,
-                         ignore_index, has_ignore, cptr, n_pad, cm, err, false, srows, slow_count);
+    if (speculative) {
+      hipLaunchKernelGGL((mc_codes_kernel<T, true, 2>), fixup_grid, kRowThreads, shm, stream(), p, target, n, C, mode,
+                         ignore_index, has_ignore, cptr, n_pad, cm, err, false, srows, state);
       TMX_LAUNCH_CHECK();
     }
   } else {
     hipLaunchKernelGGL((mc_codes_kernel<T, false, 1>), grid, kRowThreads, shm, stream(), p, target, n, C, mode, ignore_index,
-                       has_ignore, cptr, n_pad, cm, err, speculative, srows, slow_count);
+                       has_ignore, cptr, n_pad, cm, err, speculative, srows, state);
     TMX_LAUNCH_CHECK();
     if (speculative) {
-      hipLaunchKernelGGL((mc_codes_kernel<T, true, 1>), std::min(grid, 512), kRowThreads, shm, stream(), p, target, n, C, mode,
-                         ignore_index, has_ignore, cptr, n_pad, cm, err, false, srows, slow_count);
+      hipLaunchKernelGGL((mc_codes_kernel<T, true, 1>), fixup_grid, kRowThreads, shm, stream(), p, target, n, C, mode,
+                         ignore_index, has_ignore, cptr, n_pad, cm, err, false, srows, state);
       TMX_LAUNCH_CHECK();
     }
   }
-  hipLaunchKernelGGL(mc_slow_rows_kernel<T>, 64, 256, 0, stream(), p, target, n, C, mode, speculative,
-                     reinterpret_cast<uint16_t*>(cptr), n_pad, cm, srows, slow_count);
-  TMX_LAUNCH_CHECK();
   // row splits only when there are too few classes to fill the chip (exclusive-owner flush when splits == 1)
   int splits = 1;
   while ((int64_t)C * splits < 512 && n_pad / (8 * (splits * 2)) >= 1024) splits *= 2;
-  hipLaunchKernelGGL(class_hist_kernel, C * splits, 512, kCodes * sizeof(uint32_t), stream(),
-                     reinterpret_cast<const uint16_t*>(codes.data_ptr()), n_pad, splits, hist, speculative ? mode : nullptr,
-                     slow_count);
+  hipLaunchKernelGGL(class_hist_kernel<T>, C * splits, kClassThreads, kCodes * sizeof(uint32_t), stream(),
+                     reinterpret_cast<const uint16_t*>(codes.data_ptr()), n_pad, splits, hist, p, target, n, mode, speculative,
+                     srows, state, cm);
   TMX_LAUNCH_CHECK();
 }
 
@@ -463,18 +460,18 @@ void curve_hist_update(const at::Tensor& preds_, const at::Tensor& target_, at::
   const int block = 256;
   const bool two_pass_ok = task == 0 && C % 8 == 0 && C <= 8 * 2 * kWave &&
                            (reinterpret_cast<uintptr_t>(preds.data_ptr()) & 15) == 0;
-  // speculative normalisation mode (persistent int32[4] per metric: mode[2], slow-row counts[2]) replaces the range
-  // pre-pass; the class pass leaves the counts at zero for the next batch
+  // speculative normalisation mode (persistent int32[8] per metric: mode[2], rare-row counts[2], ticket) replaces the
+  // range pre-pass; the class pass leaves the counts at zero for the next batch
   const bool speculative = two_pass_ok && mode_state.has_value() && !norm_flag.has_value();
-  at::Tensor flag, slow_count;
+  at::Tensor flag, state;
   if (speculative) {
-    TORCH_CHECK(mode_state->scalar_type() == at::kInt && mode_state->numel() == 4 && mode_state->is_contiguous(),
-                "mode_state must be int32[4]");
+    TORCH_CHECK(mode_state->scalar_type() == at::kInt && mode_state->numel() == 8 && mode_state->is_contiguous(),
+                "mode_state must be int32[8]");
     flag = *mode_state;
-    slow_count = mode_state->narrow(0, 2, 2);
+    state = mode_state->narrow(0, 2, 6);
   } else {
     flag = norm_flag.has_value() ? norm_flag->to(at::kInt).contiguous() : range_flag(preds);
-    if (two_pass_ok) slow_count = at::zeros({2}, preds.options().dtype(at::kInt));
+    if (two_pass_ok) state = at::zeros({6}, preds.options().dtype(at::kInt));
   }
   int64_t* cm = nullptr;
   if (confmat.has_value()) {
@@ -493,7 +490,7 @@ void curve_hist_update(const at::Tensor& preds_, const at::Tensor& target_, at::
       if (n == 0) return;
       TORCH_CHECK(preds.numel() == n * C, "preds must be [N, C]");
       if (two_pass_ok) {
-        launch_two_pass<scalar_t>(p, target.data_ptr<int64_t>(), n, C, flag.data_ptr<int>(), slow_count.data_ptr<int>(),
+        launch_two_pass<scalar_t>(p, target.data_ptr<int64_t>(), n, C, flag.data_ptr<int>(), state.data_ptr<int>(),
                                   speculative, ignore_index, has_ignore, hist.data_ptr<int64_t>(), cm, err, preds.options());
         return;
       }

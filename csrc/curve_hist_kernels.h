@@ -68,13 +68,12 @@ template <> __device__ __forceinline__ int score_code<__half>(uint16_t b) {
 //       positive label, bit 15 = skip).  The two rows of a pair are packed per dword (v_perm) into an LDS image
 //       [512 NG][16 dwords], pair slot XOR-swizzled by class group (conflict-free writes), then stored as 16-B
 //       pieces of 64-B segments of a class-major scratch codes[C][n_pad] (XCD-aware tile order).
-//   (B) rare rows (mc_slow_rows_kernel) — a row with NaN / +-inf (torch: NaN arg-max semantics, all-NaN softmax)
-//       is appended to a device list by (A) and finished by a separate bounded kernel, keeping (A)'s fast path
-//       free of per-element special cases.
-//   (C) class pass (class_hist_kernel) — one workgroup per (class, row split): negatives counted in an
+//   (B) rare rows — a row with NaN / +-inf (torch: NaN arg-max semantics, all-NaN softmax) is appended to a device
+//       list by (A) and finished inside (C), keeping (A)'s fast path free of per-element special cases.
+//   (C) class pass (class_hist_kernel) — one 1024-thread workgroup per (class, row split): negatives counted in an
 //       LDS-privatised u32 histogram (64 KiB), positives straight to global; one int64 RMW per non-empty bin.
-// Measured on MI355X, 65536 x 1000 bf16 logits (tools/kexp/curve_hist_exp.hip): row pass 60 us vs 129 us for the
-// previous one-wave-per-row design (profiles/kexp_rowpass.json).
+// Measured on MI355X, 65536 x 1000 bf16 logits (tools/kexp/curve_hist_exp.hip, profiles/kexp_rowpass.json): row
+// pass 63 us vs 129 us for the previous one-wave-per-row design; class pass 32 us.
 // ---------------------------------------------------------------------------------------------------------
 constexpr int kRowThreads = 512;
 constexpr int kRowWaves = kRowThreads / kWave;
@@ -436,80 +435,48 @@ __global__ void __launch_bounds__(kRowThreads, 4) mc_codes_kernel(const T* __res
   }
 }
 
-// Rows with NaN / +-inf, one wave per listed row (bounded loop over the device-side count).  torch semantics: the
-// softmax of such a row is all NaN (every code skipped); in probability mode each score keeps its own code (NaN /
-// inf skipped); the arg-max is the first NaN, else the first maximum.  List 0 (speculated pass): confusion matrix
-// always, codes unless a FIXUP pass replaced them; list 1 (FIXUP pass): codes with the corrected mode.
-template <typename T>
-__global__ void __launch_bounds__(256) mc_slow_rows_kernel(const T* __restrict__ preds, const int64_t* __restrict__ target,
-                                                           int64_t n, int C, const int* __restrict__ mode, bool speculative,
-                                                           uint16_t* __restrict__ codes, int64_t n_pad,
-                                                           int64_t* __restrict__ confmat, const int* __restrict__ slow_rows,
-                                                           const int* __restrict__ slow_count) {
-  const int lane = threadIdx.x & (kWave - 1);
-  const int64_t gw = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / kWave;
-  const int64_t nw = (int64_t)gridDim.x * blockDim.x / kWave;
-  const int m0 = mode[0];
-  const int m1 = speculative ? mode[1] : m0;
-  const bool fixed = speculative && m0 != m1;
-  const int64_t n0 = slow_count[0], n1 = slow_count[1];
-  for (int64_t i = gw; i < n0 + n1; i += nw) {
-    const int lst = i < n0 ? 0 : 1;
-    const int64_t r = slow_rows[lst * n + (lst == 0 ? i : i - n0)];
-    const int64_t t = target[r];
-    const T* row = preds + r * C;
-    const bool write_codes = lst == 1 || !fixed;
-    const bool softmax = (lst == 1 ? m1 : m0) != 0;
-    if (write_codes) {
-      for (int c = lane; c < C; c += kWave) {
-        const uint32_t code = softmax ? 0x8000u : raw_code<T>(bits16<T>(row[c]));
-        codes[(int64_t)c * n_pad + r] = static_cast<uint16_t>(code | (c == t ? 0x4000u : 0u));
-      }
-    }
-    if (lst == 0 && confmat != nullptr && t >= 0 && t < C) {
-      float best = -INFINITY;
-      int bi = C, first_nan = C;
-      for (int c = lane; c < C; c += kWave) {
-        const float v = to_f32<T>(row[c]);
-        if (v != v) first_nan = min(first_nan, c);
-        else if (bi == C || v > best) { best = v; bi = c; }  // ascending classes per lane: strict > keeps the first
-      }
-#pragma unroll
-      for (int off = 32; off > 0; off >>= 1) first_nan = min(first_nan, __shfl_xor(first_nan, off, kWave));
-      float mb = best;
-      int mi = bi;
-      wave_argmax(mb, mi);
-      const int am = first_nan < C ? first_nan : mi;
-      if (lane == 0 && am < C) atomic_add_i64(confmat + t * C + am, 1);
-    }
-  }
-}
+// Class pass: one 1024-thread workgroup per (class, row split), two per CU (64-KiB LDS histogram).  Negatives are
+// counted in an LDS-privatised u32 histogram, positives (1/C of the data) go straight to global; one int64 RMW per
+// non-empty bin on flush.  Measured: 1024 threads 32 us vs 39 us at 512 and 47-61 us for a branchless variant with
+// both halves in a 128-KiB LDS histogram (one block per CU): occupancy beats the branch.
+// It also finishes the rare rows of the row pass (NaN / +-inf rows, listed in ``slow_rows``): torch semantics — the
+// softmax of such a row is all NaN (every code skipped), in probability mode each score keeps its own code, the
+// arg-max is the first NaN else the first maximum.  List 0 (speculated pass): codes unless a FIXUP pass replaced
+// them, confusion matrix always; list 1 (FIXUP pass): codes with the corrected mode.
+// ``state`` = {count0, count1, ticket}: the last block to finish (ticket) rolls the speculation word
+// (mode[0] = mode[1], mode[1] = 0) and clears the counts for the next batch — every block has read them by then.
+constexpr int kClassThreads = 1024;
 
-__global__ void __launch_bounds__(512) class_hist_kernel(const uint16_t* __restrict__ codes, int64_t n_pad, int splits,
-                                                         int64_t* __restrict__ hist, int* __restrict__ mode_roll,
-                                                         int* __restrict__ slow_count) {
+template <typename T>
+__global__ void __launch_bounds__(kClassThreads) class_hist_kernel(const uint16_t* __restrict__ codes, int64_t n_pad, int splits,
+                                                                   int64_t* __restrict__ hist, const T* __restrict__ preds,
+                                                                   const int64_t* __restrict__ target, int64_t n,
+                                                                   int* __restrict__ mode, bool speculative,
+                                                                   const int* __restrict__ slow_rows, int* __restrict__ state,
+                                                                   int64_t* __restrict__ confmat) {
   extern __shared__ __attribute__((aligned(16))) uint32_t s_neg[];  // [kCodes]
+  __shared__ int s_info[4];
+  const int C = gridDim.x / splits;
   const int c = blockIdx.x / splits, sp = blockIdx.x % splits;
-  if (blockIdx.x == 0 && threadIdx.x == 0) {  // previous kernels are complete (stream order)
-    if (mode_roll != nullptr) {
-      mode_roll[0] = mode_roll[1];
-      mode_roll[1] = 0;
-    }
-    if (slow_count != nullptr) slow_count[0] = slow_count[1] = 0;
+  if (threadIdx.x == 0) {  // the row-pass kernels are complete (stream order)
+    s_info[0] = mode[0];
+    s_info[1] = speculative ? mode[1] : mode[0];
+    s_info[2] = state[0];
+    s_info[3] = state[1];
   }
   uint4* s4 = reinterpret_cast<uint4*>(s_neg);
-  for (int i = threadIdx.x; i < kCodes / 4; i += blockDim.x) s4[i] = make_uint4(0, 0, 0, 0);
+  for (int i = threadIdx.x; i < kCodes / 4; i += kClassThreads) s4[i] = make_uint4(0, 0, 0, 0);
   __syncthreads();
   const uint4* col = reinterpret_cast<const uint4*>(codes + (int64_t)c * n_pad);
   const int64_t nv = n_pad / 8;
   const int64_t chunk = (nv + splits - 1) / splits;
   const int64_t v0 = sp * chunk, v1 = v0 + chunk < nv ? v0 + chunk : nv;
   int64_t* pos_hist = hist + ((int64_t)c * 2 + 1) * kCodes;
-  const int64_t bstride = blockDim.x;
-  for (int64_t v = v0 + threadIdx.x; v < v1; v += 4 * bstride) {
+  for (int64_t v = v0 + threadIdx.x; v < v1; v += 4 * kClassThreads) {
     uint4 w[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) w[u] = (v + u * bstride < v1) ? col[v + u * bstride] : make_uint4(0x80008000u, 0x80008000u, 0x80008000u, 0x80008000u);
+    for (int u = 0; u < 4; ++u)
+      w[u] = (v + u * kClassThreads < v1) ? col[v + u * kClassThreads] : make_uint4(0x80008000u, 0x80008000u, 0x80008000u, 0x80008000u);
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const uint32_t parts[4] = {w[u].x, w[u].y, w[u].z, w[u].w};
@@ -523,18 +490,63 @@ __global__ void __launch_bounds__(512) class_hist_kernel(const uint16_t* __restr
       }
     }
   }
+  // rare rows (usually none): this class's code of every listed row (split 0 only), and one row's arg-max per block
+  const int m0 = s_info[0], m1 = s_info[1];
+  const bool fixed = speculative && m0 != m1;
+  const int64_t n0 = s_info[2], n1 = s_info[3];
+  if (sp == 0) {
+    for (int64_t i = threadIdx.x; i < n0 + n1; i += kClassThreads) {
+      const int lst = i < n0 ? 0 : 1;
+      if (lst == 0 && fixed) continue;
+      const int64_t r = slow_rows[lst * n + (lst == 0 ? i : i - n0)];
+      if ((lst == 1 ? m1 : m0) != 0) continue;  // softmax of a NaN / inf row: all NaN, every code skipped
+      const uint32_t code = raw_code<T>(bits16<T>(preds[r * C + c]));
+      if (code & 0x8000u) continue;
+      if (target[r] == c) atomic_add_i64(pos_hist + code, 1);
+      else atomicAdd(&s_neg[code], 1u);
+    }
+  }
+  if (confmat != nullptr && threadIdx.x < kWave) {
+    const int lane = threadIdx.x;
+    for (int64_t i = blockIdx.x; i < n0; i += gridDim.x) {
+      const int64_t r = slow_rows[i];
+      const int64_t t = target[r];
+      if (t < 0 || t >= C) continue;
+      const T* row = preds + r * C;
+      float best = -INFINITY;
+      int bi = C, first_nan = C;
+      for (int cc = lane; cc < C; cc += kWave) {
+        const float v = to_f32<T>(row[cc]);
+        if (v != v) first_nan = min(first_nan, cc);
+        else if (bi == C || v > best) { best = v; bi = cc; }  // ascending classes per lane: strict > keeps the first
+      }
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) first_nan = min(first_nan, __shfl_xor(first_nan, off, kWave));
+      wave_argmax(best, bi);
+      const int am = first_nan < C ? first_nan : bi;
+      if (lane == 0 && am < C) atomic_add_i64(confmat + t * C + am, 1);
+    }
+  }
   __syncthreads();
   int64_t* neg_hist = hist + ((int64_t)c * 2) * kCodes;
-  if (splits == 1) {
-    // this workgroup is the only writer of class c's negative bins in this launch: plain read-modify-write
-    for (int i = threadIdx.x; i < kCodes; i += blockDim.x) {
-      const uint32_t cnt = s_neg[i];
-      if (cnt) neg_hist[i] += cnt;
+  for (int i = threadIdx.x; i < kCodes; i += kClassThreads) {
+    const uint32_t cnt = s_neg[i];
+    if (cnt) {
+      if (splits == 1) neg_hist[i] += cnt;  // exclusive owner of class c's negative bins in this launch
+      else atomic_add_i64(neg_hist + i, cnt);
     }
-  } else {
-    for (int i = threadIdx.x; i < kCodes; i += blockDim.x) {
-      const uint32_t cnt = s_neg[i];
-      if (cnt) atomic_add_i64(neg_hist + i, cnt);
+  }
+  if (threadIdx.x == 0) {
+    // No fence: the only ordering needed is "every block's read of mode / counts happened before the reset", and
+    // each block consumed those values (s_info, above) before taking its ticket.  (An agent-scope release here writes
+    // back the XCD's L2 once per block: it doubled the kernel's time.)
+    if (__hip_atomic_fetch_add(state + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1) {
+      if (speculative) {
+        mode[0] = m1;
+        mode[1] = 0;
+      }
+      state[0] = state[1] = 0;
+      state[2] = 0;
     }
   }
 }

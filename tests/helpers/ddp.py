@@ -44,7 +44,11 @@ def _call(fn: Callable, args: tuple) -> Any:
     import torch.distributed as dist
 
     r = dist.get_rank()
-    return r, fn(r, NUM_PROCESSES, *args)
+    out = fn(r, NUM_PROCESSES, *args)
+    # a test body without collectives could finish before the other worker picks up its task, letting one worker
+    # run both; the barrier holds each task until both ranks are in one, so the two tasks land on distinct ranks
+    dist.barrier()
+    return r, out
 
 
 def get_pool():

@@ -71,13 +71,14 @@ class _CurveMetric(Metric):
         return False
 
     def _mode_state(self, preds: Tensor) -> Optional[Tensor]:
-        """Persistent int32[4] device word of the GPU kernels: the speculated softmax decision and the verdict of the
-        last batch ([0:2]), and the rare-row list counts the class pass resets ([2:4]) — see curve_hist_kernels.h."""
+        """Persistent int32[8] device word of the GPU kernels: the speculated softmax decision and the verdict of the
+        last batch ([0:2]), the rare-row list counts and the class pass's completion ticket ([2:5]) — see
+        curve_hist_kernels.h."""
         if not preds.is_cuda:
             return None
         st = getattr(self, "_spec_mode", None)
         if st is None or st.device != preds.device:
-            st = torch.zeros(4, dtype=torch.int32, device=preds.device)
+            st = torch.zeros(8, dtype=torch.int32, device=preds.device)
             self._spec_mode = st
         return st
 

@@ -102,7 +102,7 @@ def curve_hist_update(
         raise TypeError(f"curve_hist_update expects bf16/fp16 scores, got {preds.dtype}")
     tcode = 0 if task == "multiclass" else 1
     if ops.use_native(target):
-        # with a persistent ``mode_state`` (int32[4]) the multiclass kernel speculates the softmax decision and
+        # with a persistent ``mode_state`` (int32[8]) the multiclass kernel speculates the softmax decision and
         # records the real one in-pass (no separate range pass, ignore-aware); otherwise a pre-pass flag is used
         norm = None if (mode_state is not None and task == "multiclass") else _norm_flag(preds, target, task, ignore_index)
         torch.ops.tmx.curve_hist_update(
