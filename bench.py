@@ -134,7 +134,7 @@ def main() -> None:
         value = world * args.steps / elapsed
         base = _baseline()
         out = {
-            "metric": "metric-updates/sec (whole node), MulticlassAUROC 1000-cls bs=65536",
+            "metric": f"metric-updates/sec (whole node), MulticlassAUROC {C}-cls bs={B}",
             "value": round(value, 3),
             "unit": "updates/s",
             "n_gpus": world,
@@ -145,9 +145,9 @@ def main() -> None:
             "scaling": "weak",
             "vs_baseline": round(value / (base * world), 3) if base else None,
             "dtype": "bf16",
-            "data": "synthetic (randn bf16 logits [65536,1000] + uniform int64 labels, pre-generated pool in HBM)",
+            "data": f"synthetic (randn bf16 logits [{B},{C}] + uniform int64 labels, pre-generated pool in HBM)",
             "config": {
-                "model": "MulticlassAUROC(num_classes=1000)+MulticlassConfusionMatrix(num_classes=1000)",
+                "model": f"MulticlassAUROC(num_classes={C})+MulticlassConfusionMatrix(num_classes={C})",
                 "global_batch": B * world,
                 "seq_len": 1,
                 "parallelism": f"dp{world}",

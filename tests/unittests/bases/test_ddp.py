@@ -229,3 +229,37 @@ def _narrow_hist_worker(rank, world):
 
 def test_hist_sync_narrowing_exact():
     assert all(run_ddp(_narrow_hist_worker))
+
+
+def _range_hist_worker(rank, world):
+    """Only the occupied code range travels: ranks with disjoint ranges, and a rank without any update, still give
+    the exact global histogram and the single-process ROC / AUROC."""
+    from torchmetrics_forked_amd.classification import MulticlassAUROC, MulticlassROC
+
+    g = torch.Generator().manual_seed(7)
+    batches = [(torch.rand(40, 4, generator=g) * 0.1, torch.randint(0, 4, (40,), generator=g)),  # rank 0: low codes
+               (0.9 + torch.rand(40, 4, generator=g) * 0.1, torch.randint(0, 4, (40,), generator=g))]  # rank 1: high codes
+    ok = True
+    for sharded in (False, True):
+        for empty_rank in (None, 1):
+            auroc = MulticlassAUROC(num_classes=4, average="macro", sharded_compute=sharded)
+            roc = MulticlassROC(num_classes=4)
+            if rank != empty_rank:
+                p, t = batches[rank]
+                auroc.update(p.bfloat16(), t)
+                roc.update(p.bfloat16(), t)
+            ref_a, ref_r = MulticlassAUROC(num_classes=4, average="macro"), MulticlassROC(num_classes=4)
+            for r in range(world):
+                if r != empty_rank:
+                    ref_a.update(batches[r][0].bfloat16(), batches[r][1])
+                    ref_r.update(batches[r][0].bfloat16(), batches[r][1])
+            ref_a.sync_on_compute = ref_r.sync_on_compute = False
+            ok &= bool(torch.allclose(auroc.compute(), ref_a.compute(), atol=1e-7))
+            got, exp = roc.compute(), ref_r.compute()
+            for x, y in zip(got, exp):
+                ok &= all(torch.equal(a, b) for a, b in zip(x, y))
+    return ok
+
+
+def test_hist_sync_code_range_exact():
+    assert all(run_ddp(_range_hist_worker))

@@ -150,14 +150,16 @@ class _CurveMetric(Metric):
             and (dist_sync_fn is None or dist_sync_fn is gather_all_tensors)
         )
 
-    def _sync_sharded(self, group: Optional[Any], narrow: bool = False) -> None:
+    def _sync_sharded(self, group: Optional[Any], narrow: bool, lo: int, hi: int) -> None:
         """State-parallel sync: reduce-scatter the exact histogram by class so each rank owns
-        ``ceil(C / W)`` classes, and sync the remaining states normally."""
+        ``ceil(C / W)`` classes, and sync the remaining states normally.  Only the occupied code range ``[lo, hi]``
+        (the same on every rank) travels."""
         world = dist.get_world_size(group)
         rank = dist.get_rank(group)
         c = self._num
         per = -(-c // world)
-        full = self.score_hist.to(torch.int32) if narrow else self.score_hist
+        sl = self.score_hist[:, :, lo : hi + 1]
+        full = sl.to(torch.int32) if narrow else sl.contiguous()
         if per * world != c:
             full = torch.cat([full, full.new_zeros(per * world - c, *full.shape[1:])])
         backend = dist.get_backend(group) if group is not None else dist.get_backend()
@@ -173,7 +175,9 @@ class _CurveMetric(Metric):
             setattr(self, name, val)
         first = rank * per
         owned = max(0, min(per, c - first))
-        self.score_hist = shard[:owned].long()
+        hist = torch.zeros(owned, 2, self.score_hist.shape[-1], dtype=torch.long, device=self.score_hist.device)
+        hist[:, :, lo : hi + 1] = shard[:owned]
+        self.score_hist = hist
         self._shard_info = (first, owned, per, group)
 
     def unsync(self, should_unsync: bool = True) -> None:
@@ -198,31 +202,51 @@ class _CurveMetric(Metric):
         return allv[0], allv[1], allv[2], allv[3]
 
     def _sync_dist(self, dist_sync_fn: Any = None, process_group: Optional[Any] = None) -> None:
-        """Histogram states travel as int32 whenever the summed per-rank maximum bin proves every global bin fits
-        (halves the dominant collective: 131 MB instead of 262 MB at C=1000); one small all-reduce carries that
-        bound together with the "some rank has a histogram" flag."""
+        """The exact histogram travels (a) as int32 whenever the summed per-rank maximum bin proves every global
+        bin fits (131 MB instead of 262 MB at C=1000) and (b) only over the code range ``[lo, hi]`` that some rank
+        occupies: softmax scores fill a few bf16 binades, about a fifth of the 16384 codes.  One tiny all-gather of
+        (has-histogram, max bin, lo, hi) per rank decides both; the per-code maxima behind them are one pass."""
         if self.thresholds is None:
             group = process_group or self.process_group
             backend = dist.get_backend(group) if group is not None else dist.get_backend()
             dev = self.score_hist.device if backend != "nccl" or self.score_hist.is_cuda else torch.device("cuda")
             has = self.score_hist.numel() > 0
-            local_max = self.score_hist.amax().reshape(1) if has else torch.zeros(1, dtype=torch.long, device=dev)
-            stats = torch.cat([torch.tensor([1 if has else 0], dtype=torch.long, device=local_max.device), local_max.long()])
+            k = eng.N_CODES
+            if has:
+                per_code = self.score_hist.amax(dim=(0, 1))
+                idx = torch.arange(k, device=per_code.device)
+                occ = per_code > 0
+                stats = torch.stack([
+                    torch.ones((), dtype=torch.long, device=per_code.device), per_code.amax(),
+                    torch.where(occ, idx, k).amin(), torch.where(occ, idx, -1).amax(),
+                ])
+            else:
+                stats = torch.tensor([0, 0, k, -1], dtype=torch.long, device=dev)
             stats = stats.to(dev if backend == "nccl" else "cpu")
-            dist.all_reduce(stats, op=dist.ReduceOp.SUM, group=group)
-            used, bound = (int(v) for v in stats.tolist())
+            parts = [torch.empty_like(stats) for _ in range(dist.get_world_size(group))]
+            dist.all_gather(parts, stats, group=group)
+            allv = torch.stack(parts).tolist()
+            used, bound = sum(v[0] for v in allv), sum(v[1] for v in allv)
+            lo, hi = min(v[2] for v in allv), max(v[3] for v in allv)
             if used and self.score_hist.numel() == 0:
                 self._ensure_hist(self.device)
             narrow = used > 0 and bound < 2**31 - 1
+            if hi < lo:  # no rank counted anything: keep one bin so the collectives stay well-formed
+                lo = hi = 0
             if self._shardable(dist_sync_fn):
-                self._sync_sharded(group, narrow)
+                self._sync_sharded(group, narrow, lo, hi)
                 return
-            if narrow and (dist_sync_fn is None or dist_sync_fn is gather_all_tensors):
-                self.score_hist = self.score_hist.to(torch.int32)
+            if used and (dist_sync_fn is None or dist_sync_fn is gather_all_tensors):
+                shape = self.score_hist.shape
+                sl = self.score_hist[:, :, lo : hi + 1]
+                self.score_hist = sl.to(torch.int32) if narrow else sl.contiguous()
                 try:
                     super()._sync_dist(dist_sync_fn, process_group)
                 finally:
-                    self.score_hist = self.score_hist.long()
+                    synced = self.score_hist
+                    hist = torch.zeros(shape, dtype=torch.long, device=synced.device)
+                    hist[:, :, lo : hi + 1] = synced
+                    self.score_hist = hist
                 return
         super()._sync_dist(dist_sync_fn, process_group)
 
