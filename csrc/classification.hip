@@ -521,62 +521,77 @@ void curve_hist_update(const at::Tensor& preds_, const at::Tensor& target_, at::
   TMX_LAUNCH_CHECK();
 }
 
-// Per-class reduction of the exact histogram (descending code order), one workgroup per class.
+// Per-class reduction of the exact histogram (descending code order), one 1024-thread workgroup per class.
 //   out[c] = {auroc, average_precision, n_pos, n_neg}
 // AUROC = sum_k neg_k * (2*TP_{<k} + pos_k) / (2 * P * N)  (trapezoid over every code; empty codes add 0)
 // AP    = sum_k (pos_k / P) * TP_k / (TP_k + FP_k)
-// Codes are walked in coalesced 256-wide chunks (descending) with a wave shuffle scan + cross-wave carry.
+// Thread t owns 16 consecutive codes (descending positions 16t .. 16t+15) of both halves in registers, so all
+// 256 KiB of a class are in flight at once; one block scan of the per-thread sums gives every thread its
+// TP / FP carry, then each walks its 16 codes.  (The previous form walked 64 dependent 256-code chunks with two
+// barriers each: 107 us at C = 1000.)
+constexpr int kRedThreads = 1024;
+constexpr int kRedPer = kCodes / kRedThreads;  // 16
+
 __device__ __forceinline__ long long shfl_up_i64(long long v, int off) {
   int lo = __shfl_up(static_cast<int>(v & 0xFFFFFFFFll), off, kWave);
   int hi = __shfl_up(static_cast<int>(v >> 32), off, kWave);
   return (static_cast<long long>(hi) << 32) | static_cast<unsigned int>(lo);
 }
 
-__global__ void __launch_bounds__(256) curve_hist_reduce_kernel(const int64_t* __restrict__ hist, int K, double* __restrict__ out) {
+__global__ void __launch_bounds__(kRedThreads) curve_hist_reduce_kernel(const int64_t* __restrict__ hist, double* __restrict__ out) {
+  constexpr int K = kCodes;
+  constexpr int kWaves = kRedThreads / kWave;
   const int c = blockIdx.x;
-  const int64_t* neg = hist + ((int64_t)c * 2 + 0) * K;
-  const int64_t* pos = hist + ((int64_t)c * 2 + 1) * K;
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
-  __shared__ long long s_p[4], s_n[4];
-  long long carry_p = 0, carry_n = 0;
-  double area = 0.0, ap_sum = 0.0;
-  for (int base = 0; base < K; base += 256) {
-    const int q = base + tid;
-    const long long pk = q < K ? pos[K - 1 - q] : 0, nk = q < K ? neg[K - 1 - q] : 0;
-    long long ip = pk, in = nk;
+  const int64_t base = K - kRedPer * (tid + 1);  // lowest code owned by this thread
+  const longlong2* negv = reinterpret_cast<const longlong2*>(hist + ((int64_t)c * 2 + 0) * K + base);
+  const longlong2* posv = reinterpret_cast<const longlong2*>(hist + ((int64_t)c * 2 + 1) * K + base);
+  long long p[kRedPer], n[kRedPer];  // index i = i-th highest owned code
 #pragma unroll
-    for (int off = 1; off < kWave; off <<= 1) {
-      const long long tp = shfl_up_i64(ip, off), tn = shfl_up_i64(in, off);
-      if (lane >= off) { ip += tp; in += tn; }
-    }
-    if (lane == kWave - 1) { s_p[wave] = ip; s_n[wave] = in; }
-    __syncthreads();
-    long long wp = 0, wn = 0, chunk_p = 0, chunk_n = 0;
-#pragma unroll
-    for (int w = 0; w < 4; ++w) {
-      if (w < wave) { wp += s_p[w]; wn += s_n[w]; }
-      chunk_p += s_p[w];
-      chunk_n += s_n[w];
-    }
-    const long long tp_incl = carry_p + wp + ip, fp_incl = carry_n + wn + in;
-    area += (double)nk * (double)(2 * (tp_incl - pk) + pk);
-    if (pk) ap_sum += (double)pk * ((double)tp_incl / (double)(tp_incl + fp_incl));
-    carry_p += chunk_p;
-    carry_n += chunk_n;
-    __syncthreads();
+  for (int v = 0; v < kRedPer / 2; ++v) {
+    const longlong2 a = posv[v], b = negv[v];
+    p[kRedPer - 1 - 2 * v] = a.x; p[kRedPer - 2 - 2 * v] = a.y;
+    n[kRedPer - 1 - 2 * v] = b.x; n[kRedPer - 2 - 2 * v] = b.y;
   }
-  __shared__ double s_a[256], s_b[256];
-  s_a[tid] = area;
-  s_b[tid] = ap_sum;
+  long long sp = 0, sn = 0;
+#pragma unroll
+  for (int i = 0; i < kRedPer; ++i) { sp += p[i]; sn += n[i]; }
+  long long ip = sp, in = sn;  // inclusive wave scan in thread order (= descending code order)
+#pragma unroll
+  for (int off = 1; off < kWave; off <<= 1) {
+    const long long tp = shfl_up_i64(ip, off), tn = shfl_up_i64(in, off);
+    if (lane >= off) { ip += tp; in += tn; }
+  }
+  __shared__ long long s_p[kWaves], s_n[kWaves];
+  __shared__ double s_a[kWaves], s_b[kWaves];
+  if (lane == kWave - 1) { s_p[wave] = ip; s_n[wave] = in; }
   __syncthreads();
-  for (int off = 128; off > 0; off >>= 1) {
-    if (tid < off) { s_a[tid] += s_a[tid + off]; s_b[tid] += s_b[tid + off]; }
-    __syncthreads();
+  long long wp = 0, wn = 0, P = 0, N = 0;
+#pragma unroll
+  for (int w = 0; w < kWaves; ++w) {
+    if (w < wave) { wp += s_p[w]; wn += s_n[w]; }
+    P += s_p[w];
+    N += s_n[w];
   }
+  long long tp = wp + ip - sp, fp = wn + in - sn;  // positives / negatives above this thread's codes
+  double area = 0.0, ap_sum = 0.0;
+#pragma unroll
+  for (int i = 0; i < kRedPer; ++i) {
+    const long long pk = p[i], nk = n[i];
+    tp += pk;
+    fp += nk;
+    area += (double)nk * (double)(2 * (tp - pk) + pk);
+    if (pk) ap_sum += (double)pk * ((double)tp / (double)(tp + fp));
+  }
+  area = wave_sum(area);
+  ap_sum = wave_sum(ap_sum);
+  if (lane == 0) { s_a[wave] = area; s_b[wave] = ap_sum; }
+  __syncthreads();
   if (tid == 0) {
-    const long long P = carry_p, N = carry_n;
-    out[c * 4 + 0] = (P > 0 && N > 0) ? s_a[0] / (2.0 * (double)P * (double)N) : 0.0;
-    out[c * 4 + 1] = P > 0 ? s_b[0] / (double)P : NAN;
+    double a = 0.0, b = 0.0;
+    for (int w = 0; w < kWaves; ++w) { a += s_a[w]; b += s_b[w]; }
+    out[c * 4 + 0] = (P > 0 && N > 0) ? a / (2.0 * (double)P * (double)N) : 0.0;
+    out[c * 4 + 1] = P > 0 ? b / (double)P : NAN;
     out[c * 4 + 2] = (double)P;
     out[c * 4 + 3] = (double)N;
   }
@@ -584,12 +599,12 @@ __global__ void __launch_bounds__(256) curve_hist_reduce_kernel(const int64_t* _
 
 at::Tensor curve_hist_reduce(const at::Tensor& hist_) {
   auto hist = hist_.contiguous();
-  TORCH_CHECK(hist.scalar_type() == at::kLong && hist.dim() == 3 && hist.size(1) == 2);
+  TORCH_CHECK(hist.scalar_type() == at::kLong && hist.dim() == 3 && hist.size(1) == 2 && hist.size(2) == kCodes,
+              "curve_hist_reduce: hist must be int64 [C, 2, 16384]");
   const int C = static_cast<int>(hist.size(0));
   auto out = at::empty({C, 4}, hist.options().dtype(at::kDouble));
   if (C == 0) return out;
-  hipLaunchKernelGGL(curve_hist_reduce_kernel, C, 256, 0, stream(), hist.data_ptr<int64_t>(), (int)hist.size(2),
-                     out.data_ptr<double>());
+  hipLaunchKernelGGL(curve_hist_reduce_kernel, C, kRedThreads, 0, stream(), hist.data_ptr<int64_t>(), out.data_ptr<double>());
   TMX_LAUNCH_CHECK();
   return out;
 }
