@@ -263,3 +263,46 @@ def _range_hist_worker(rank, world):
 
 def test_hist_sync_code_range_exact():
     assert all(run_ddp(_range_hist_worker))
+
+
+def _timeout_worker(rank, world):
+    """A rank that never joins a sync surfaces as SyncTimeoutError on its peers (bounded wait) instead of a hang;
+    once the late rank joins, the pending collective completes and the group stays usable."""
+    import time
+
+    from torchmetrics_forked_amd.aggregation import SumMetric
+    from torchmetrics_forked_amd.parallel import SyncTimeoutError, sync_timeout
+
+    ok = True
+    m = SumMetric(sync_timeout=1.5)
+    m.update(torch.tensor(float(rank + 1)))
+    if rank == 0:
+        t0 = time.time()
+        try:
+            m.compute()
+            ok = False
+        except SyncTimeoutError as err:
+            ok &= "rank 0 of 2" in str(err) and time.time() - t0 < 30
+    else:
+        time.sleep(4.0)  # joins late: completes rank 0's pending all_reduce
+        ok &= float(m.compute()) == 3.0
+    torch.distributed.barrier()
+    # a bound that is met changes nothing
+    m2 = SumMetric()
+    m2.update(torch.tensor(1.0))
+    with sync_timeout(60):
+        ok &= float(m2.compute()) == 2.0
+    return ok
+
+
+def test_sync_timeout_detects_missing_rank():
+    assert all(run_ddp(_timeout_worker))
+
+
+def test_sync_timeout_kwarg_validation():
+    from torchmetrics_forked_amd.aggregation import SumMetric
+
+    for bad in (0, -1, "5", True):
+        with pytest.raises(ValueError, match="sync_timeout"):
+            SumMetric(sync_timeout=bad)
+    assert SumMetric(sync_timeout=2.5).sync_timeout == 2.5

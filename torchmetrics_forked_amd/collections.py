@@ -19,7 +19,7 @@ from torch import Tensor
 from torch.nn import ModuleDict
 
 from torchmetrics_forked_amd.metric import Metric
-from torchmetrics_forked_amd.parallel.sync import sync_states_many
+from torchmetrics_forked_amd.parallel.sync import sync_states_many, sync_timeout
 from torchmetrics_forked_amd.utilities.data import _flatten_dict, allclose
 from torchmetrics_forked_amd.utilities.plot import _AX_TYPE, _PLOT_OUT_TYPE, plot_single_or_multi_val
 from torchmetrics_forked_amd.utilities.prints import rank_zero_warn
@@ -178,7 +178,9 @@ class MetricCollection(ModuleDict):
         if len(groups) != 1:
             return []
         group = next(iter(groups))
-        synced = sync_states_many([m.metric_state for m in eligible], [m._reductions for m in eligible], group=group)
+        bounds = [m.sync_timeout for m in eligible if getattr(m, "sync_timeout", None) is not None]
+        with sync_timeout(min(bounds) if bounds else None):
+            synced = sync_states_many([m.metric_state for m in eligible], [m._reductions for m in eligible], group=group)
         restore: List[Tuple[Metric, bool]] = []
         for m, new_states in zip(eligible, synced):
             m._cache = m.metric_state

@@ -26,7 +26,7 @@ import torch
 from torch import Tensor
 from torch.nn import Module
 
-from torchmetrics_forked_amd.parallel.sync import PendingSync, legacy_sync_states, sync_states, sync_states_async
+from torchmetrics_forked_amd.parallel.sync import PendingSync, legacy_sync_states, sync_states, sync_states_async, sync_timeout
 from torchmetrics_forked_amd.utilities.data import (
     _flatten,
     _squeeze_if_scalar,
@@ -98,6 +98,9 @@ class Metric(Module, ABC):
         sharded_compute: framework extension. Metrics that support state-parallel compute
             reduce-scatter their per-class state across ranks at sync time, compute only their own classes and
             all-gather the small per-class results; others ignore the flag.  Results are identical.
+        sync_timeout: framework extension (SURVEY §5 failure detection). Seconds every sync collective may take
+            before :class:`~torchmetrics_forked_amd.parallel.sync.SyncTimeoutError` is raised (default: the
+            ``TMX_SYNC_TIMEOUT`` environment variable, else unbounded as in the reference).
     """
 
     __jit_ignored_attributes__: ClassVar[List[str]] = ["device"]
@@ -143,6 +146,9 @@ class Metric(Module, ABC):
                 f"Expected keyword argument `dist_sync_fn` to be an callable function but got {self.dist_sync_fn}"
             )
         self.distributed_available_fn = kwargs.pop("distributed_available_fn", None) or jit_distributed_available
+        self.sync_timeout = kwargs.pop("sync_timeout", None)
+        if self.sync_timeout is not None and (isinstance(self.sync_timeout, bool) or not isinstance(self.sync_timeout, (int, float)) or self.sync_timeout <= 0):
+            raise ValueError(f"Expected keyword argument `sync_timeout` to be a positive number of seconds but got {self.sync_timeout}")
         if kwargs:
             raise ValueError(f"Unexpected keyword arguments: {', '.join(f'`{k}`' for k in sorted(kwargs))}")
 
@@ -384,7 +390,7 @@ class Metric(Module, ABC):
             pending = sync_states_async(self.metric_state, self._reductions, group=process_group or self.process_group)
             return _MetricPendingSync(self, pending)
         self._cache = self.metric_state
-        with _range(f"tmx/{self.__class__.__name__}.sync"):
+        with _range(f"tmx/{self.__class__.__name__}.sync"), sync_timeout(getattr(self, "sync_timeout", None)):
             self._sync_dist(dist_sync_fn, process_group=process_group)
         self._is_synced = True
         return None

@@ -19,12 +19,22 @@ Design here:
   rank-interleaved (``_flatten`` of per-element gathers); ``None``-reduced tensors are stacked ``(world, ...)``.
 * ``sync_states_many`` syncs several metrics' states with one plan, so a ``MetricCollection`` pays the collective
   latency once per reduction group rather than once per member.
+* **Failure detection** (the reference has none): with a timeout in force — ``Metric(sync_timeout=...)``,
+  the :func:`sync_timeout` context, or ``TMX_SYNC_TIMEOUT`` seconds in the environment — every collective is issued
+  asynchronously and waited for with that bound; a rank that skipped ``compute()`` / ``sync()`` (or holds a
+  different set of metrics) then surfaces as :class:`SyncTimeoutError` naming the rank instead of a silent hang.
 """
-from typing import Any, Callable, Dict, List, Optional, Sequence, Tuple, Union
+import datetime
+import os
+import threading
+from contextlib import contextmanager
+from typing import Any, Callable, Dict, Iterator, List, Optional, Sequence, Tuple, Union
 
 import torch
 import torch.distributed as dist
 from torch import Tensor
+
+from torchmetrics_forked_amd.utilities.exceptions import TorchMetricsUserError
 
 from torchmetrics_forked_amd.utilities.data import (
     _flatten,
@@ -49,6 +59,64 @@ _REDUCE_OPS = {
     dim_zero_max: "max",
     dim_zero_min: "min",
 }
+
+
+class SyncTimeoutError(TorchMetricsUserError):
+    """A metric-state collective did not complete within the configured timeout."""
+
+
+_TLS = threading.local()
+
+
+def _env_timeout() -> Optional[float]:
+    v = os.environ.get("TMX_SYNC_TIMEOUT")
+    return float(v) if v else None
+
+
+def current_timeout() -> Optional[float]:
+    """Seconds every sync collective may take (innermost :func:`sync_timeout`, else ``TMX_SYNC_TIMEOUT``)."""
+    stack = getattr(_TLS, "stack", None)
+    return stack[-1] if stack else _env_timeout()
+
+
+@contextmanager
+def sync_timeout(seconds: Optional[float]) -> Iterator[None]:
+    """Bound every metric-state collective issued inside the block by ``seconds`` (``None``: no bound)."""
+    stack = getattr(_TLS, "stack", None)
+    if stack is None:
+        stack = _TLS.stack = []
+    stack.append(seconds if seconds is not None else (stack[-1] if stack else _env_timeout()))
+    try:
+        yield
+    finally:
+        stack.pop()
+
+
+def _wait(work: Any, what: str, group: Optional[Any]) -> None:
+    timeout = current_timeout()
+    try:
+        if timeout is None:
+            work.wait()
+            return
+        done = work.wait(timeout=datetime.timedelta(seconds=timeout))
+    except RuntimeError as err:  # gloo / RCCL report an expired wait as a RuntimeError
+        if "timed out" not in str(err).lower() and "timeout" not in str(err).lower():
+            raise
+        done = False
+    if done is False:
+        rank = dist.get_rank(group) if group is not None else dist.get_rank()
+        raise SyncTimeoutError(
+            f"metric sync: {what} did not complete within {timeout:g}s on rank {rank} of {_world(group)}; another rank"
+            " probably skipped compute()/sync() or holds a different set of metrics"
+        )
+
+
+def _collective(fn: Callable, *args: Any, what: str, group: Optional[Any] = None, **kwargs: Any) -> None:
+    """Run one collective; under a timeout it is issued asynchronously and waited for with that bound."""
+    if current_timeout() is None:
+        fn(*args, group=group, **kwargs)
+        return
+    _wait(fn(*args, group=group, async_op=True, **kwargs), what, group)
 
 
 def distributed_available() -> bool:
@@ -95,7 +163,7 @@ def _launch_all_reduce(items: List[Tuple[str, Tensor, str]], group: Optional[Any
         if op == "mean" and not flat.is_floating_point():
             flat = flat.double()
         rop = {"sum": dist.ReduceOp.SUM, "mean": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}[op]
-        work = dist.all_reduce(flat, op=rop, group=group, async_op=async_op)
+        work = dist.all_reduce(flat, op=rop, group=group, async_op=async_op or current_timeout() is not None)
         launched.append((op, dtype, device, members, flat, work))
     return launched
 
@@ -105,7 +173,7 @@ def _finish_all_reduce(launched: List[Tuple], group: Optional[Any]) -> Dict[str,
     out: Dict[str, Tensor] = {}
     for op, dtype, device, members, flat, work in launched:
         if work is not None:
-            work.wait()
+            _wait(work, f"all_reduce({op}, {dtype})", group)
         if op == "mean":
             flat = flat / world
         offset = 0
@@ -163,7 +231,7 @@ def all_gather_packed(
     # 1) header: element count per slot
     counts = torch.tensor([len(lst) for lst in groups], dtype=torch.int64, device=comm_dev)
     all_counts = [torch.empty_like(counts) for _ in range(world)]
-    dist.all_gather(all_counts, counts, group=group)
+    _collective(dist.all_gather, all_counts, counts, what="all_gather(element counts)", group=group)
     all_counts_h = torch.stack(all_counts).cpu()  # (world, slots) - tiny host read
     max_elems = int(all_counts_h.sum(1).max().item()) if n_slots else 0
     if max_elems == 0:
@@ -185,7 +253,7 @@ def all_gather_packed(
         payload_sizes.append(_pad16(nbytes))
     table = table.to(comm_dev)
     all_tables = [torch.empty_like(table) for _ in range(world)]
-    dist.all_gather(all_tables, table, group=group)
+    _collective(dist.all_gather, all_tables, table, what="all_gather(shape table)", group=group)
     tables_h = [tb.cpu() for tb in all_tables]
 
     # 3) payload: one padded byte buffer per rank
@@ -206,7 +274,7 @@ def all_gather_packed(
         pieces.append(torch.zeros(max_bytes - used, dtype=torch.uint8, device=comm_dev))
     buf = torch.cat(pieces)
     gathered = [torch.empty_like(buf) for _ in range(world)]
-    dist.all_gather(gathered, buf, group=group)
+    _collective(dist.all_gather, gathered, buf, what="all_gather(packed states)", group=group)
 
     # 4) unpack
     slot_devices = []
