@@ -418,7 +418,7 @@ void launch_two_pass(const T* p, const int64_t* target, int64_t n, int C, int* m
   // row splits only when there are too few classes to fill the chip (exclusive-owner flush when splits == 1)
   int splits = 1;
   while ((int64_t)C * splits < 512 && n_pad / (8 * (splits * 2)) >= 1024) splits *= 2;
-  hipLaunchKernelGGL(class_hist_kernel<T>, C * splits, kClassThreads, kCodes * sizeof(uint32_t), stream(),
+  hipLaunchKernelGGL((class_hist_kernel<T, false>), C * splits, kClassThreads, kCodes * sizeof(uint32_t), stream(),
                      reinterpret_cast<const uint16_t*>(codes.data_ptr()), n_pad, splits, hist, p, target, n, mode, speculative,
                      srows, state, cm);
   TMX_LAUNCH_CHECK();
@@ -443,6 +443,65 @@ __global__ void curve_hist_ml_kernel(const T* __restrict__ preds, const int64_t*
       b = bits16<T>(preds[i]);
     }
     hist_add(hist, l, t == 1 ? 1 : 0, score_code<T>(b));
+  }
+}
+
+// Binary (single label): one 1024-thread workgroup per CU, a [2][kCodes] u32 histogram privatised in LDS
+// (128 KiB), 8 scores + 8 targets per vector step, non-empty bins flushed with one int64 atomic each.  Replaces one
+// global 64-bit atomic per score, which for BinaryAUROC lands on a few hundred hot bins of ONE class
+// (N = 16.7M bf16: 5.4 ms per update before).  Same sigmoid formula and code rules as curve_hist_ml_kernel.
+constexpr int kBinThreads = 1024;
+
+template <typename T>
+__device__ __forceinline__ void binary_hist_add(uint32_t* s_h, T p, int64_t t, bool do_sigmoid, int64_t ignore_index,
+                                                bool has_ignore) {
+  if (has_ignore && t == ignore_index) return;
+  uint16_t b;
+  if (do_sigmoid) {
+    const float x = to_f32<T>(p);
+    b = round_bits16<T>(1.f / (1.f + expf(-x)));
+  } else {
+    b = bits16<T>(p);
+  }
+  const int code = score_code<T>(b);
+  if (code < 0) return;
+  atomicAdd(&s_h[(t == 1 ? kCodes : 0) + code], 1u);
+}
+
+template <typename T>
+__global__ void __launch_bounds__(kBinThreads) binary_hist_kernel(const T* __restrict__ preds, const int64_t* __restrict__ target,
+                                                                  int64_t total, const int* __restrict__ sigmoid_flag,
+                                                                  int64_t ignore_index, bool has_ignore, int64_t* __restrict__ hist) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_h[];  // [2][kCodes]: negatives, positives
+  uint4* s4 = reinterpret_cast<uint4*>(s_h);
+  for (int i = threadIdx.x; i < 2 * kCodes / 4; i += kBinThreads) s4[i] = make_uint4(0, 0, 0, 0);
+  __syncthreads();
+  const bool do_sigmoid = sigmoid_flag[0] != 0;
+  const int64_t nvec = total / 8;
+  const uint4* pv = reinterpret_cast<const uint4*>(preds);
+  const longlong2* tv = reinterpret_cast<const longlong2*>(target);
+  const int64_t stride = (int64_t)gridDim.x * kBinThreads;
+  for (int64_t v = blockIdx.x * (int64_t)kBinThreads + threadIdx.x; v < nvec; v += stride) {
+    const uint4 w = pv[v];
+    longlong2 tt[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) tt[k] = tv[4 * v + k];
+    const uint32_t parts[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const uint16_t bits = static_cast<uint16_t>((k & 1) ? (parts[k >> 1] >> 16) : (parts[k >> 1] & 0xFFFFu));
+      const int64_t t = (k & 1) ? tt[k >> 1].y : tt[k >> 1].x;
+      binary_hist_add<T>(s_h, *reinterpret_cast<const T*>(&bits), t, do_sigmoid, ignore_index, has_ignore);
+    }
+  }
+  if (blockIdx.x == 0) {  // tail
+    for (int64_t i = nvec * 8 + threadIdx.x; i < total; i += kBinThreads)
+      binary_hist_add<T>(s_h, preds[i], target[i], do_sigmoid, ignore_index, has_ignore);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 2 * kCodes; i += kBinThreads) {
+    const uint32_t cnt = s_h[i];
+    if (cnt) atomic_add_i64(hist + i, cnt);
   }
 }
 
@@ -513,6 +572,43 @@ void curve_hist_update(const at::Tensor& preds_, const at::Tensor& target_, at::
       const int64_t N = target.size(0);
       const int64_t S = total / (N * C);
       TORCH_CHECK(N * C * S == total, "target shape incompatible with num_labels");
+      const bool aligned = (reinterpret_cast<uintptr_t>(preds.data_ptr()) & 15) == 0 &&
+                           (reinterpret_cast<uintptr_t>(target.data_ptr()) & 15) == 0;
+      if (C == 1 && aligned) {
+        static const bool lds_ok = [] {  // > 64 KiB of dynamic LDS needs the attribute (gfx950 has 160 KiB per CU)
+          return hipFuncSetAttribute(reinterpret_cast<const void*>(binary_hist_kernel<scalar_t>),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, 2 * kCodes * sizeof(uint32_t)) == hipSuccess;
+        }();
+        TORCH_CHECK(lds_ok, "binary_hist_kernel: cannot reserve 128 KiB of LDS");
+        const int grid = static_cast<int>(std::min<int64_t>(256, (total + 8 * kBinThreads - 1) / (8 * kBinThreads)));
+        hipLaunchKernelGGL(binary_hist_kernel<scalar_t>, std::max(grid, 1), kBinThreads, 2 * kCodes * sizeof(uint32_t), stream(), p,
+                           target.data_ptr<int64_t>(), total, flag.data_ptr<int>(), ignore_index, has_ignore,
+                           hist.data_ptr<int64_t>());
+        return;
+      }
+      if (S == 1 && C % 8 == 0 && C <= 8 * 2 * kWave && aligned) {
+        // multilabel: the multiclass two-pass layout (labels as classes), per-element targets and sigmoid
+        const int64_t n_pad = (N + kTileRows - 1) / kTileRows * kTileRows;
+        auto codes = at::empty({(int64_t)C * n_pad}, preds.options().dtype(at::kShort));
+        auto state = at::zeros({6}, preds.options().dtype(at::kInt));
+        const int grid = static_cast<int>((n_pad / kTileRows + 7) / 8 * 8);
+        const size_t shm = (size_t)512 * (C > 512 ? 2 : 1) * kSlots * sizeof(uint32_t);
+        uint32_t* cptr = reinterpret_cast<uint32_t*>(codes.data_ptr());
+        if (C > 512)
+          hipLaunchKernelGGL((ml_codes_kernel<scalar_t, 2>), grid, kRowThreads, shm, stream(), p, target.data_ptr<int64_t>(), N, C,
+                             flag.data_ptr<int>(), ignore_index, has_ignore, cptr, n_pad);
+        else
+          hipLaunchKernelGGL((ml_codes_kernel<scalar_t, 1>), grid, kRowThreads, shm, stream(), p, target.data_ptr<int64_t>(), N, C,
+                             flag.data_ptr<int>(), ignore_index, has_ignore, cptr, n_pad);
+        TMX_LAUNCH_CHECK();
+        int splits = 1;
+        while ((int64_t)C * splits < 512 && n_pad / (8 * (splits * 2)) >= 1024) splits *= 2;
+        hipLaunchKernelGGL((class_hist_kernel<scalar_t, true>), C * splits, kClassThreads, kCodes * sizeof(uint32_t), stream(),
+                           reinterpret_cast<const uint16_t*>(cptr), n_pad, splits, hist.data_ptr<int64_t>(), p,
+                           target.data_ptr<int64_t>(), N, flag.data_ptr<int>(), false, static_cast<const int*>(nullptr),
+                           state.data_ptr<int>(), static_cast<int64_t*>(nullptr));
+        return;
+      }
       hipLaunchKernelGGL(curve_hist_ml_kernel<scalar_t>, grid_for(total, block, 4096), block, 0, stream(), p,
                          target.data_ptr<int64_t>(), N, C, S, flag.data_ptr<int>(), ignore_index, has_ignore,
                          hist.data_ptr<int64_t>());

@@ -249,6 +249,28 @@ struct SlowRows {
   int* count;  // [2]
 };
 
+// Store one tile's LDS image as 16-B pieces of the class rows of the class-major scratch (compile-time trip count):
+// thread -> (class c, 16-B group g of the class's 64-B segment).  Segment dword 4g + i lives at LDS slot
+// (4g + i) ^ s (s = class swizzle), i.e. in LDS quad g ^ (s >> 2) at position i ^ (s & 3).
+template <int NG>
+__device__ __forceinline__ void store_tile(const uint32_t* __restrict__ s_tile, uint32_t* __restrict__ codes, int C,
+                                           int64_t n_pad, int64_t tile) {
+  constexpr int kQuads = kSlots / 4;  // 4 x 16 B per class per tile
+  const int64_t seg = tile * kSlots;
+  const int64_t row_dw = n_pad / 2;
+#pragma unroll
+  for (int k = 0; k < 512 * NG * kQuads / kRowThreads; ++k) {
+    const int idx = threadIdx.x + k * kRowThreads;
+    const int c = idx / kQuads, g = idx % kQuads;
+    const int sw = (c >> 3) & (kSlots - 1);
+    const uint4 w = *reinterpret_cast<const uint4*>(&s_tile[c * kSlots + 4 * (g ^ (sw >> 2))]);
+    const int x = sw & 3;
+    const uint32_t e0 = x & 1 ? w.y : w.x, e1 = x & 1 ? w.x : w.y, e2 = x & 1 ? w.w : w.z, e3 = x & 1 ? w.z : w.w;
+    const uint4 o = x & 2 ? make_uint4(e2, e3, e0, e1) : make_uint4(e0, e1, e2, e3);
+    if (c < C) *reinterpret_cast<uint4*>(&codes[c * row_dw + seg + 4 * g]) = o;
+  }
+}
+
 // One 32-row tile of the row pass for a fixed normalisation (SOFTMAX).  Every load is issued up front; stores and
 // global atomics come only after the last wait (a VMEM write pending behind a load makes the compiler drain the
 // whole queue at the next wait).
@@ -362,22 +384,7 @@ __device__ __forceinline__ void row_tile(const T* __restrict__ preds, const int6
     }
   }
   __syncthreads();
-  {
-    constexpr int kQuads = kSlots / 4;  // 4 x 16 B per class per tile
-    const int64_t seg = tile * kSlots;
-    const int64_t row_dw = n_pad / 2;
-#pragma unroll
-    for (int k = 0; k < 512 * NG * kQuads / kRowThreads; ++k) {
-      const int idx = threadIdx.x + k * kRowThreads;
-      const int c = idx / kQuads, g = idx % kQuads;
-      const int sw = (c >> 3) & (kSlots - 1);
-      const uint4 w = *reinterpret_cast<const uint4*>(&s_tile[c * kSlots + 4 * (g ^ (sw >> 2))]);
-      const int x = sw & 3;
-      const uint32_t e0 = x & 1 ? w.y : w.x, e1 = x & 1 ? w.x : w.y, e2 = x & 1 ? w.w : w.z, e3 = x & 1 ? w.z : w.w;
-      const uint4 o = x & 2 ? make_uint4(e2, e3, e0, e1) : make_uint4(e0, e1, e2, e3);
-      if (c < C) *reinterpret_cast<uint4*>(&codes[c * row_dw + seg + 4 * g]) = o;
-    }
-  }
+  store_tile<NG>(s_tile, codes, C, n_pad, tile);
 }
 
 // Normalisation mode (softmax if any valid score is outside [0, 1], as the reference decides per batch) is
@@ -435,10 +442,97 @@ __global__ void __launch_bounds__(kRowThreads, 4) mc_codes_kernel(const T* __res
   }
 }
 
-// Class pass: one 1024-thread workgroup per (class, row split), two per CU (64-KiB LDS histogram).  Negatives are
-// counted in an LDS-privatised u32 histogram, positives (1/C of the data) go straight to global; one int64 RMW per
-// non-empty bin on flush.  Measured: 1024 threads 32 us vs 39 us at 512 and 47-61 us for a branchless variant with
-// both halves in a 128-KiB LDS histogram (one block per CU): occupancy beats the branch.
+// Multilabel row pass: the same tile / LDS image / class-major scratch as the multiclass row pass, but every element
+// is its own binary problem — code = RNE16(sigmoid(x)) (torch's 1 / (1 + exp(-x)) in fp32) or the raw score when the
+// batch is already in [0, 1] (the range pre-pass decides, as in the reference), flags from the element's own target
+// (1 -> positive, ignore_index -> skip, anything else -> negative).  Labels play the role of classes; the class
+// pass is shared.  Targets are int64 [N, L]: the 8 labels a lane owns per group are one 64-B piece of the row.
+template <typename T, int NG>
+__device__ __forceinline__ void row_tile_ml(const T* __restrict__ preds, const int64_t* __restrict__ target, int64_t n, int L,
+                                            bool do_sigmoid, int64_t ignore_index, bool has_ignore,
+                                            uint32_t* __restrict__ codes, int64_t n_pad, uint32_t* __restrict__ s_tile,
+                                            int64_t tile) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wave = threadIdx.x / kWave;
+  const int nvec = L / 8;
+  const bool lo_ok = lane < nvec, hi_ok = lane + kWave < nvec;
+  const int lq = lo_ok ? lane : nvec - 1;
+  const int hq = hi_ok ? lane + kWave : nvec - 1;
+  auto row0_of = [&](int pp) -> int64_t { return tile * kTileRows + 2 * (wave + pp * kRowWaves); };
+  uint4 raw[2][2][2];
+#pragma unroll
+  for (int pp = 0; pp < 2; ++pp)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const uint4* row = reinterpret_cast<const uint4*>(preds + min(row0_of(pp) + h, n - 1) * L);
+      raw[pp][h][0] = row[lq];
+      if constexpr (NG == 2) raw[pp][h][1] = row[hq];
+    }
+#pragma unroll
+  for (int pp = 0; pp < 2; ++pp) {
+    const int p = wave + pp * kRowWaves;
+    const int64_t r0 = row0_of(pp);
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      const bool ok = g == 0 ? lo_ok : hi_ok;
+      const int q = g == 0 ? lq : hq;
+      uint32_t code[2][8];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int64_t r = r0 + h;
+        const bool valid = r < n && ok;
+        const longlong2* trow = reinterpret_cast<const longlong2*>(target + min(r, n - 1) * L + 8 * q);
+        longlong2 tt[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) tt[k] = trow[k];
+        const uint4 w = raw[pp][h][g];
+        float v[8];
+        unpack8<T>(w, v);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int64_t t = (k & 1) ? tt[k >> 1].y : tt[k >> 1].x;
+          const uint32_t b = do_sigmoid ? (uint32_t)round_bits16<T>(1.f / (1.f + expf(-v[k]))) : (uint32_t)raw_bits<T>(w, k);
+          uint32_t c16 = raw_code<T>(b);
+          if (!valid || (has_ignore && t == ignore_index)) c16 = 0x8000u;
+          else if (t == 1 && !(c16 & 0x8000u)) c16 |= 0x4000u;
+          code[h][k] = c16;
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int c = 512 * g + 8 * lane + k;
+        s_tile[c * kSlots + (p ^ (lane & (kSlots - 1)))] = code[0][k] | (code[1][k] << 16);
+      }
+    }
+  }
+  __syncthreads();
+  store_tile<NG>(s_tile, codes, L, n_pad, tile);
+}
+
+template <typename T, int NG>
+__global__ void __launch_bounds__(kRowThreads, 4) ml_codes_kernel(const T* __restrict__ preds, const int64_t* __restrict__ target,
+                                                                   int64_t n, int L, const int* __restrict__ sigmoid_flag,
+                                                                   int64_t ignore_index, bool has_ignore,
+                                                                   uint32_t* __restrict__ codes, int64_t n_pad) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_tile[];  // [512 * NG][kSlots]
+  const int64_t ntiles = (n + kTileRows - 1) / kTileRows;
+  const int64_t per_xcd = (ntiles + 7) / 8;
+  const int64_t b = blockIdx.x;
+  const int64_t tile = (b % 8) * per_xcd + b / 8;  // XCD-aware order, as the multiclass row pass
+  if (tile >= ntiles) return;
+  row_tile_ml<T, NG>(preds, target, n, L, sigmoid_flag[0] != 0, ignore_index, has_ignore, codes, n_pad, s_tile, tile);
+}
+
+// Class pass: one 1024-thread workgroup per (class, row split), two per CU (64-KiB LDS).
+//   PACKED = false (multiclass: positives are 1 / C of the codes): an LDS u32 histogram of the negatives, positives
+//            straight to the int64 bins with global atomics.
+//   PACKED = true (multilabel: ~half the codes are positive; a global atomic per positive took 287 us at
+//            16384 x 1000): both halves in ONE LDS word per code — negatives in the low 16 bits, positives in the high
+//            16 bits — one LDS atomic per code, rows consumed in chunks of at most kClassChunk so a 16-bit half cannot
+//            overflow.
+// Every flush adds the LDS counts to the int64 histogram (plain read-modify-write by the exclusive owner when there
+// is one split, atomics otherwise).  Measured at 65536 x 1000 multiclass: 1024 threads 32 us vs 39 us at 512
+// and 47-61 us for a variant with a 128-KiB two-array histogram (one block per CU): occupancy beats everything else.
 // It also finishes the rare rows of the row pass (NaN / +-inf rows, listed in ``slow_rows``): torch semantics — the
 // softmax of such a row is all NaN (every code skipped), in probability mode each score keeps its own code, the
 // arg-max is the first NaN else the first maximum.  List 0 (speculated pass): codes unless a FIXUP pass replaced
@@ -446,15 +540,35 @@ __global__ void __launch_bounds__(kRowThreads, 4) mc_codes_kernel(const T* __res
 // ``state`` = {count0, count1, ticket}: the last block to finish (ticket) rolls the speculation word
 // (mode[0] = mode[1], mode[1] = 0) and clears the counts for the next batch — every block has read them by then.
 constexpr int kClassThreads = 1024;
+constexpr int64_t kClassChunk = 65528;  // rows per LDS flush: a 16-bit half never overflows (multiple of 8)
 
-template <typename T>
+template <bool PACKED>
+__device__ __forceinline__ void class_flush(uint32_t* __restrict__ s_h, int64_t* __restrict__ neg_hist,
+                                            int64_t* __restrict__ pos_hist, bool exclusive) {
+  for (int i = threadIdx.x; i < kCodes; i += kClassThreads) {
+    const uint32_t w = s_h[i];
+    if (w) {
+      const uint32_t neg = PACKED ? (w & 0xFFFFu) : w, pos = PACKED ? (w >> 16) : 0u;
+      if (exclusive) {
+        if (neg) neg_hist[i] += neg;
+        if (pos) pos_hist[i] += pos;
+      } else {
+        if (neg) atomic_add_i64(neg_hist + i, neg);
+        if (pos) atomic_add_i64(pos_hist + i, pos);
+      }
+      s_h[i] = 0u;
+    }
+  }
+}
+
+template <typename T, bool PACKED>
 __global__ void __launch_bounds__(kClassThreads) class_hist_kernel(const uint16_t* __restrict__ codes, int64_t n_pad, int splits,
                                                                    int64_t* __restrict__ hist, const T* __restrict__ preds,
                                                                    const int64_t* __restrict__ target, int64_t n,
                                                                    int* __restrict__ mode, bool speculative,
                                                                    const int* __restrict__ slow_rows, int* __restrict__ state,
                                                                    int64_t* __restrict__ confmat) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t s_neg[];  // [kCodes]
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_h[];  // [kCodes]: neg, or neg (lo 16) | pos (hi 16)
   __shared__ int s_info[4];
   const int C = gridDim.x / splits;
   const int c = blockIdx.x / splits, sp = blockIdx.x % splits;
@@ -464,30 +578,41 @@ __global__ void __launch_bounds__(kClassThreads) class_hist_kernel(const uint16_
     s_info[2] = state[0];
     s_info[3] = state[1];
   }
-  uint4* s4 = reinterpret_cast<uint4*>(s_neg);
+  uint4* s4 = reinterpret_cast<uint4*>(s_h);
   for (int i = threadIdx.x; i < kCodes / 4; i += kClassThreads) s4[i] = make_uint4(0, 0, 0, 0);
   __syncthreads();
+  int64_t* neg_hist = hist + ((int64_t)c * 2) * kCodes;
+  int64_t* pos_hist = hist + ((int64_t)c * 2 + 1) * kCodes;
+  const bool exclusive = splits == 1;
   const uint4* col = reinterpret_cast<const uint4*>(codes + (int64_t)c * n_pad);
   const int64_t nv = n_pad / 8;
-  const int64_t chunk = (nv + splits - 1) / splits;
-  const int64_t v0 = sp * chunk, v1 = v0 + chunk < nv ? v0 + chunk : nv;
-  int64_t* pos_hist = hist + ((int64_t)c * 2 + 1) * kCodes;
-  for (int64_t v = v0 + threadIdx.x; v < v1; v += 4 * kClassThreads) {
-    uint4 w[4];
+  const int64_t per = (nv + splits - 1) / splits;
+  const int64_t v0 = sp * per, v1 = v0 + per < nv ? v0 + per : nv;
+  constexpr int64_t kChunkV = PACKED ? kClassChunk / 8 : (int64_t{1} << 62);
+  for (int64_t cb = v0; cb < v1; cb += kChunkV) {
+    const int64_t ce = cb + kChunkV < v1 ? cb + kChunkV : v1;
+    for (int64_t v = cb + threadIdx.x; v < ce; v += 4 * kClassThreads) {
+      uint4 w[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
-      w[u] = (v + u * kClassThreads < v1) ? col[v + u * kClassThreads] : make_uint4(0x80008000u, 0x80008000u, 0x80008000u, 0x80008000u);
+      for (int u = 0; u < 4; ++u)
+        w[u] = (v + u * kClassThreads < ce) ? col[v + u * kClassThreads] : make_uint4(0x80008000u, 0x80008000u, 0x80008000u, 0x80008000u);
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const uint32_t parts[4] = {w[u].x, w[u].y, w[u].z, w[u].w};
+      for (int u = 0; u < 4; ++u) {
+        const uint32_t parts[4] = {w[u].x, w[u].y, w[u].z, w[u].w};
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const uint32_t x = (k & 1) ? (parts[k >> 1] >> 16) : (parts[k >> 1] & 0xFFFFu);
-        if (x & 0x8000u) continue;
-        const uint32_t code = x & 0x3FFFu;
-        if (x & 0x4000u) atomic_add_i64(pos_hist + code, 1);
-        else atomicAdd(&s_neg[code], 1u);
+        for (int k = 0; k < 8; ++k) {
+          const uint32_t x = (k & 1) ? (parts[k >> 1] >> 16) : (parts[k >> 1] & 0xFFFFu);
+          if (x & 0x8000u) continue;
+          if constexpr (PACKED) atomicAdd(&s_h[x & 0x3FFFu], (x & 0x4000u) ? 0x10000u : 1u);
+          else if (x & 0x4000u) atomic_add_i64(pos_hist + (x & 0x3FFFu), 1);
+          else atomicAdd(&s_h[x & 0x3FFFu], 1u);
+        }
       }
+    }
+    if (ce < v1) {  // more rows than one chunk: flush before a 16-bit half can overflow
+      __syncthreads();
+      class_flush<PACKED>(s_h, neg_hist, pos_hist, exclusive);
+      __syncthreads();
     }
   }
   // rare rows (usually none): this class's code of every listed row (split 0 only), and one row's arg-max per block
@@ -503,7 +628,7 @@ __global__ void __launch_bounds__(kClassThreads) class_hist_kernel(const uint16_
       const uint32_t code = raw_code<T>(bits16<T>(preds[r * C + c]));
       if (code & 0x8000u) continue;
       if (target[r] == c) atomic_add_i64(pos_hist + code, 1);
-      else atomicAdd(&s_neg[code], 1u);
+      else atomic_add_i64(neg_hist + code, 1);
     }
   }
   if (confmat != nullptr && threadIdx.x < kWave) {
@@ -528,14 +653,8 @@ __global__ void __launch_bounds__(kClassThreads) class_hist_kernel(const uint16_
     }
   }
   __syncthreads();
-  int64_t* neg_hist = hist + ((int64_t)c * 2) * kCodes;
-  for (int i = threadIdx.x; i < kCodes; i += kClassThreads) {
-    const uint32_t cnt = s_neg[i];
-    if (cnt) {
-      if (splits == 1) neg_hist[i] += cnt;  // exclusive owner of class c's negative bins in this launch
-      else atomic_add_i64(neg_hist + i, cnt);
-    }
-  }
+  // rare-row codes went to the int64 bins by atomics: then the last flush must be atomic too
+  class_flush<PACKED>(s_h, neg_hist, pos_hist, exclusive && n0 + n1 == 0);
   if (threadIdx.x == 0) {
     // No fence: the only ordering needed is "every block's read of mode / counts happened before the reset", and
     // each block consumed those values (s_info, above) before taking its ticket.  (An agent-scope release here writes

@@ -195,3 +195,38 @@ def test_curve_speculation_flips_across_batches():
     assert torch.equal(res[0][1], res[1][1])
     for a, b in zip(res[0][0], res[1][0]):
         assert abs(a - b) < 1e-4, (res[0][0], res[1][0])
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("probs", [False, True])
+@pytest.mark.parametrize("offset", [0, 1])
+def test_curve_hist_binary(dtype, probs, offset):
+    """Single-label path (LDS-privatised binary_hist_kernel; offset 1 = misaligned view -> element-wise kernel)."""
+    N = 200_003
+    x = torch.rand(N + offset) if probs else torch.randn(N + offset) * 3
+    x[17::1001] = float("nan")
+    preds = x.to(dtype)[offset:]
+    target = torch.randint(0, 2, (N + offset,))[offset:]
+    target[5::13] = -1
+    hist = torch.zeros(1, 2, K.N_CODES, dtype=torch.long)
+    g, c, _, _ = _both(K.curve_hist_update, preds.reshape(-1, 1, 1), target.reshape(-1, 1, 1), hist, "binary", -1)
+    assert torch.equal(g[2].cpu(), c[2])
+
+
+@pytest.mark.parametrize("L", [8, 64, 520, 1000])
+@pytest.mark.parametrize("probs", [False, True])
+def test_curve_hist_multilabel_two_pass(L, probs):
+    """[N, L] multilabel scores take the two-pass route (ml_codes_kernel + class pass): per-element sigmoid,
+    per-element targets with ignore_index, NaN scores skipped."""
+    N = 3000
+    x = torch.rand(N, L) if probs else torch.randn(N, L) * 2
+    x[7::101, 3] = float("nan")
+    preds = x.bfloat16()
+    target = torch.randint(0, 2, (N, L))
+    target[::11, :5] = -1
+    hist = torch.zeros(L, 2, K.N_CODES, dtype=torch.long)
+    g, c, _, _ = _both(K.curve_hist_update, preds, target, hist, "multilabel", -1)
+    diff = (g[2].cpu() - c[2]).abs().sum().item()
+    assert diff <= max(8, int(1e-4 * N * L)), diff  # CPU vs GPU expf may flip a rare bf16 rounding of the sigmoid
+    assert g[2].sum().item() == c[2].sum().item()
+    assert torch.equal(g[2][:, 1].sum(-1).cpu(), c[2][:, 1].sum(-1))  # positives per label exact
