@@ -383,8 +383,8 @@ __global__ void __launch_bounds__(256) curve_hist_mc_kernel(const T* __restrict_
   }
 }
 
-template <typename T>
-void launch_two_pass(const T* p, const int64_t* target, int64_t n, int C, int* mode, int* state, bool speculative,
+template <typename T, bool PADDED>
+void launch_two_pass(const T* p, const int64_t* target, int64_t n, int C, int ld, int* mode, int* state, bool speculative,
                      int64_t ignore_index, bool has_ignore, int64_t* hist, int64_t* cm, int* err, const at::TensorOptions& opts) {
   TORCH_CHECK(n < (int64_t{1} << 31), "curve_hist_update: more than 2^31 rows in one batch");
   const int64_t n_pad = (n + kTileRows - 1) / kTileRows * kTileRows;
@@ -397,20 +397,20 @@ void launch_two_pass(const T* p, const int64_t* target, int64_t n, int C, int* m
   uint32_t* cptr = reinterpret_cast<uint32_t*>(codes.data_ptr());
   int* srows = slow_rows.data_ptr<int>();
   if (C > 512) {
-    hipLaunchKernelGGL((mc_codes_kernel<T, false, 2>), grid, kRowThreads, shm, stream(), p, target, n, C, mode, ignore_index,
+    hipLaunchKernelGGL((mc_codes_kernel<T, false, 2, PADDED>), grid, kRowThreads, shm, stream(), p, target, n, C, ld, mode, ignore_index,
                        has_ignore, cptr, n_pad, cm, err, speculative, srows, state);
     TMX_LAUNCH_CHECK();
     if (speculative) {
-      hipLaunchKernelGGL((mc_codes_kernel<T, true, 2>), fixup_grid, kRowThreads, shm, stream(), p, target, n, C, mode,
+      hipLaunchKernelGGL((mc_codes_kernel<T, true, 2, PADDED>), fixup_grid, kRowThreads, shm, stream(), p, target, n, C, ld, mode,
                          ignore_index, has_ignore, cptr, n_pad, cm, err, false, srows, state);
       TMX_LAUNCH_CHECK();
     }
   } else {
-    hipLaunchKernelGGL((mc_codes_kernel<T, false, 1>), grid, kRowThreads, shm, stream(), p, target, n, C, mode, ignore_index,
+    hipLaunchKernelGGL((mc_codes_kernel<T, false, 1, PADDED>), grid, kRowThreads, shm, stream(), p, target, n, C, ld, mode, ignore_index,
                        has_ignore, cptr, n_pad, cm, err, speculative, srows, state);
     TMX_LAUNCH_CHECK();
     if (speculative) {
-      hipLaunchKernelGGL((mc_codes_kernel<T, true, 1>), fixup_grid, kRowThreads, shm, stream(), p, target, n, C, mode,
+      hipLaunchKernelGGL((mc_codes_kernel<T, true, 1, PADDED>), fixup_grid, kRowThreads, shm, stream(), p, target, n, C, ld, mode,
                          ignore_index, has_ignore, cptr, n_pad, cm, err, false, srows, state);
       TMX_LAUNCH_CHECK();
     }
@@ -419,7 +419,7 @@ void launch_two_pass(const T* p, const int64_t* target, int64_t n, int C, int* m
   int splits = 1;
   while ((int64_t)C * splits < 512 && n_pad / (8 * (splits * 2)) >= 1024) splits *= 2;
   hipLaunchKernelGGL((class_hist_kernel<T, false>), C * splits, kClassThreads, kCodes * sizeof(uint32_t), stream(),
-                     reinterpret_cast<const uint16_t*>(codes.data_ptr()), n_pad, splits, hist, p, target, n, mode, speculative,
+                     reinterpret_cast<const uint16_t*>(codes.data_ptr()), n_pad, splits, hist, p, ld, target, n, mode, speculative,
                      srows, state, cm);
   TMX_LAUNCH_CHECK();
 }
@@ -517,8 +517,9 @@ void curve_hist_update(const at::Tensor& preds_, const at::Tensor& target_, at::
   auto target = target_.contiguous().to(at::kLong);
   const int C = static_cast<int>(hist.size(0));
   const int block = 256;
-  const bool two_pass_ok = task == 0 && C % 8 == 0 && C <= 8 * 2 * kWave &&
-                           (reinterpret_cast<uintptr_t>(preds.data_ptr()) & 15) == 0;
+  // two-pass multiclass route for C <= 1024; rows are padded to a multiple of 8 classes when C % 8 != 0 (one copy)
+  const bool two_pass_ok = task == 0 && C <= 8 * 2 * kWave &&
+                           (C % 8 != 0 || (reinterpret_cast<uintptr_t>(preds.data_ptr()) & 15) == 0);
   // speculative normalisation mode (persistent int32[8] per metric: mode[2], rare-row counts[2], ticket) replaces the
   // range pre-pass; the class pass leaves the counts at zero for the next batch
   const bool speculative = two_pass_ok && mode_state.has_value() && !norm_flag.has_value();
@@ -549,8 +550,16 @@ void curve_hist_update(const at::Tensor& preds_, const at::Tensor& target_, at::
       if (n == 0) return;
       TORCH_CHECK(preds.numel() == n * C, "preds must be [N, C]");
       if (two_pass_ok) {
-        launch_two_pass<scalar_t>(p, target.data_ptr<int64_t>(), n, C, flag.data_ptr<int>(), state.data_ptr<int>(),
-                                  speculative, ignore_index, has_ignore, hist.data_ptr<int64_t>(), cm, err, preds.options());
+        if (C % 8 != 0) {
+          const int ld = (C + 7) / 8 * 8;
+          const at::Tensor padded = at::constant_pad_nd(preds.view({n, C}), {0, ld - C}, 0).contiguous();
+          launch_two_pass<scalar_t, true>(reinterpret_cast<const scalar_t*>(padded.data_ptr()), target.data_ptr<int64_t>(), n, C,
+                                          ld, flag.data_ptr<int>(), state.data_ptr<int>(), speculative, ignore_index, has_ignore,
+                                          hist.data_ptr<int64_t>(), cm, err, preds.options());
+        } else {
+          launch_two_pass<scalar_t, false>(p, target.data_ptr<int64_t>(), n, C, C, flag.data_ptr<int>(), state.data_ptr<int>(),
+                                           speculative, ignore_index, has_ignore, hist.data_ptr<int64_t>(), cm, err, preds.options());
+        }
         return;
       }
       const int grid = grid_for(n * kWave, block, 4096);
@@ -604,7 +613,7 @@ void curve_hist_update(const at::Tensor& preds_, const at::Tensor& target_, at::
         int splits = 1;
         while ((int64_t)C * splits < 512 && n_pad / (8 * (splits * 2)) >= 1024) splits *= 2;
         hipLaunchKernelGGL((class_hist_kernel<scalar_t, true>), C * splits, kClassThreads, kCodes * sizeof(uint32_t), stream(),
-                           reinterpret_cast<const uint16_t*>(cptr), n_pad, splits, hist.data_ptr<int64_t>(), p,
+                           reinterpret_cast<const uint16_t*>(cptr), n_pad, splits, hist.data_ptr<int64_t>(), p, C,
                            target.data_ptr<int64_t>(), N, flag.data_ptr<int>(), false, static_cast<const int*>(nullptr),
                            state.data_ptr<int>(), static_cast<int64_t*>(nullptr));
         return;

@@ -226,6 +226,30 @@ __device__ __forceinline__ void row_stat(const uint4 (&w)[2], bool lo_ok, bool h
   r.mx = wave_max_uniform(__builtin_fmaxf(r.mlo, r.mhi));
 }
 
+// Row statistics for rows padded to a multiple of 8 classes (host-side pad when C % 8 != 0): element k of group g in
+// lane L is class 512 g + 8 L + k, valid iff below C — nlo / nhi = valid elements of this lane in groups 0 / 1.
+template <typename T, int NG>
+__device__ __forceinline__ void row_stat_padded(const uint4 (&w)[2], int nlo, int nhi, RowStat<NG>& r) {
+  float u[8 * NG];
+  unpack8<T>(w[0], u);
+  if constexpr (NG == 2) unpack8<T>(w[1], u + 8);
+  float mlo = -INFINITY, mhi = -INFINITY, mn = INFINITY, sum = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8 * NG; ++j) {
+    const bool ok = j < 8 ? j < nlo : j - 8 < nhi;
+    r.v[j] = ok ? u[j] : -INFINITY;
+    mn = ok ? __builtin_fminf(mn, u[j]) : mn;
+    sum += ok ? u[j] : 0.f;
+    if (j < 8) mlo = __builtin_fmaxf(mlo, r.v[j]);
+    else mhi = __builtin_fmaxf(mhi, r.v[j]);
+  }
+  r.mlo = mlo;
+  r.mhi = mhi;
+  r.mn = mn;
+  r.sum = sum;
+  r.mx = wave_max_uniform(__builtin_fmaxf(r.mlo, r.mhi));
+}
+
 // arg-max of a row without NaN / inf: first class (ascending) holding the wave maximum.  Classes of group g, lane L,
 // slot k are 512 g + 8 L + k, so the winner is the lowest lane whose group-0 maximum equals mx (else the lowest lane
 // of group 1) and the lowest slot of that lane.
@@ -275,14 +299,15 @@ __device__ __forceinline__ void store_tile(const uint32_t* __restrict__ s_tile, 
 // global atomics come only after the last wait (a VMEM write pending behind a load makes the compiler drain the
 // whole queue at the next wait).
 
-template <typename T, int NG, bool SOFTMAX, bool FIXUP>
-__device__ __forceinline__ void row_tile(const T* __restrict__ preds, const int64_t* __restrict__ target, int64_t n, int C,
+template <typename T, int NG, bool SOFTMAX, bool FIXUP, bool PADDED>
+__device__ __forceinline__ void row_tile(const T* __restrict__ preds, const int64_t* __restrict__ target, int64_t n, int C, int ld,
                                           int64_t ignore_index, bool has_ignore, uint32_t* __restrict__ codes, int64_t n_pad,
                                           int64_t* __restrict__ confmat, int* __restrict__ err, bool rec, bool& saw_bad,
                                           SlowRows slow, uint32_t* __restrict__ s_tile, int64_t tile) {
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = threadIdx.x / kWave;
-  const int nvec = C / 8;
+  const int nvec = ld / 8;
+  const int nlo = min(max(C - 8 * lane, 0), 8), nhi = min(max(C - 8 * (lane + kWave), 0), 8);
   const bool lo_ok = lane < nvec, hi_ok = lane + kWave < nvec;
   const int lq = lo_ok ? lane : nvec - 1;  // clamped: every load stays inside its row
   const int hq = hi_ok ? lane + kWave : nvec - 1;
@@ -293,7 +318,7 @@ __device__ __forceinline__ void row_tile(const T* __restrict__ preds, const int6
   for (int pp = 0; pp < 2; ++pp)
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      const uint4* row = reinterpret_cast<const uint4*>(preds + min(row0_of(pp) + h, n - 1) * C);
+      const uint4* row = reinterpret_cast<const uint4*>(preds + min(row0_of(pp) + h, n - 1) * ld);
       raw[pp][h][0] = row[lq];
       if constexpr (NG == 2) raw[pp][h][1] = row[hq];
     }
@@ -314,8 +339,13 @@ __device__ __forceinline__ void row_tile(const T* __restrict__ preds, const int6
     const bool va = r0 < n && !(has_ignore && ta == ignore_index);
     const bool vb = r0 + 1 < n && !(has_ignore && tb == ignore_index);
     RowStat<NG> ra, rb;
-    row_stat<T, NG>(raw[pp][0], lo_ok, hi_ok, ra);
-    row_stat<T, NG>(raw[pp][1], lo_ok, hi_ok, rb);
+    if constexpr (PADDED) {
+      row_stat_padded<T, NG>(raw[pp][0], nlo, nhi, ra);
+      row_stat_padded<T, NG>(raw[pp][1], nlo, nhi, rb);
+    } else {
+      row_stat<T, NG>(raw[pp][0], lo_ok, hi_ok, ra);
+      row_stat<T, NG>(raw[pp][1], lo_ok, hi_ok, rb);
+    }
     bool fa = __builtin_isfinite(ra.mx), fb = __builtin_isfinite(rb.mx);
     const int ama = row_argmax<NG>(ra), amb = row_argmax<NG>(rb);
     float sa = 0.f, sb = 0.f, ia = 0.f, ib = 0.f;
@@ -393,9 +423,9 @@ __device__ __forceinline__ void row_tile(const T* __restrict__ preds, const int6
 // at once unless mode[0] != mode[1], in which case it redoes the codes with the real mode (confusion matrix and error
 // flags are mode independent and are not touched again).  ``class_hist_kernel`` rolls mode[0] = mode[1].
 // Grid: one block per tile for the main launch (blocks stride over tiles, so a FIXUP launch can use a small grid).
-template <typename T, bool FIXUP, int NG>
+template <typename T, bool FIXUP, int NG, bool PADDED>
 __global__ void __launch_bounds__(kRowThreads, 4) mc_codes_kernel(const T* __restrict__ preds, const int64_t* __restrict__ target,
-                                                                    int64_t n, int C, int* __restrict__ mode,
+                                                                    int64_t n, int C, int ld, int* __restrict__ mode,
                                                                     int64_t ignore_index, bool has_ignore,
                                                                     uint32_t* __restrict__ codes, int64_t n_pad,
                                                                     int64_t* __restrict__ confmat, int* __restrict__ err,
@@ -423,9 +453,9 @@ __global__ void __launch_bounds__(kRowThreads, 4) mc_codes_kernel(const T* __res
     const int64_t tile = (b % 8) * per_xcd + b / 8;
     if (tile >= ntiles) return;
     if (use_mode != 0)
-      row_tile<T, NG, true, FIXUP>(preds, target, n, C, ignore_index, has_ignore, codes, n_pad, confmat, err, rec, saw_bad, slow, s_tile, tile);
+      row_tile<T, NG, true, FIXUP, PADDED>(preds, target, n, C, ld, ignore_index, has_ignore, codes, n_pad, confmat, err, rec, saw_bad, slow, s_tile, tile);
     else
-      row_tile<T, NG, false, FIXUP>(preds, target, n, C, ignore_index, has_ignore, codes, n_pad, confmat, err, rec, saw_bad, slow, s_tile, tile);
+      row_tile<T, NG, false, FIXUP, PADDED>(preds, target, n, C, ld, ignore_index, has_ignore, codes, n_pad, confmat, err, rec, saw_bad, slow, s_tile, tile);
   };
   if constexpr (FIXUP) {  // rare: blocks stride over the tiles (small grid, cheap early exit)
     for (int64_t b = blockIdx.x; b < per_xcd * 8; b += gridDim.x) {
@@ -563,7 +593,7 @@ __device__ __forceinline__ void class_flush(uint32_t* __restrict__ s_h, int64_t*
 
 template <typename T, bool PACKED>
 __global__ void __launch_bounds__(kClassThreads) class_hist_kernel(const uint16_t* __restrict__ codes, int64_t n_pad, int splits,
-                                                                   int64_t* __restrict__ hist, const T* __restrict__ preds,
+                                                                   int64_t* __restrict__ hist, const T* __restrict__ preds, int ld,
                                                                    const int64_t* __restrict__ target, int64_t n,
                                                                    int* __restrict__ mode, bool speculative,
                                                                    const int* __restrict__ slow_rows, int* __restrict__ state,
@@ -625,7 +655,7 @@ __global__ void __launch_bounds__(kClassThreads) class_hist_kernel(const uint16_
       if (lst == 0 && fixed) continue;
       const int64_t r = slow_rows[lst * n + (lst == 0 ? i : i - n0)];
       if ((lst == 1 ? m1 : m0) != 0) continue;  // softmax of a NaN / inf row: all NaN, every code skipped
-      const uint32_t code = raw_code<T>(bits16<T>(preds[r * C + c]));
+      const uint32_t code = raw_code<T>(bits16<T>(preds[r * ld + c]));
       if (code & 0x8000u) continue;
       if (target[r] == c) atomic_add_i64(pos_hist + code, 1);
       else atomic_add_i64(neg_hist + code, 1);
@@ -637,7 +667,7 @@ __global__ void __launch_bounds__(kClassThreads) class_hist_kernel(const uint16_
       const int64_t r = slow_rows[i];
       const int64_t t = target[r];
       if (t < 0 || t >= C) continue;
-      const T* row = preds + r * C;
+      const T* row = preds + r * ld;
       float best = -INFINITY;
       int bi = C, first_nan = C;
       for (int cc = lane; cc < C; cc += kWave) {

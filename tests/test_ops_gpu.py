@@ -147,7 +147,7 @@ def _rare_rows(x, probs):
     return x
 
 
-@pytest.mark.parametrize("C", [64, 512, 520, 1000])
+@pytest.mark.parametrize("C", [10, 64, 100, 512, 520, 1000, 1001])
 @pytest.mark.parametrize("probs", [False, True])
 def test_curve_hist_multiclass_rare_rows(C, probs):
     """Rows with NaN / inf take mc_slow_rows_kernel: torch semantics (all-NaN softmax, first-NaN arg-max)."""

@@ -76,23 +76,23 @@ int main(int argc, char** argv) {
   const size_t shm6 = (size_t)1024 * kSlots * 4;
   auto set_mode = [&](int* m, int m0) { int hm[2] = {m0, 0}; CK(hipMemcpy(m, hm, 8, hipMemcpyHostToDevice)); };
   auto row6 = [&](const __hip_bfloat16* x, const int64_t* t, bool ign, bool rec) {
-    hipLaunchKernelGGL((mc_codes_kernel<__hip_bfloat16, false, 2>), grid6, kRowThreads, shm6, 0, x, t, N, C, mode, -100, ign,
+    hipLaunchKernelGGL((mc_codes_kernel<__hip_bfloat16, false, 2, false>), grid6, kRowThreads, shm6, 0, x, t, N, C, C, mode, -100, ign,
                        codes6, n_pad, cm6, err, rec, slow_rows, state);
   };
   auto fix6 = [&](const __hip_bfloat16* x, const int64_t* t, bool ign) {
-    hipLaunchKernelGGL((mc_codes_kernel<__hip_bfloat16, true, 2>), std::min(grid6, 128), kRowThreads, shm6, 0, x, t, N, C, mode, -100, ign,
+    hipLaunchKernelGGL((mc_codes_kernel<__hip_bfloat16, true, 2, false>), std::min(grid6, 128), kRowThreads, shm6, 0, x, t, N, C, C, mode, -100, ign,
                        codes6, n_pad, cm6, err, false, slow_rows, state);
   };
   auto class6 = [&](const __hip_bfloat16* x, const int64_t* t, bool spec) {
     hipLaunchKernelGGL((class_hist_kernel<__hip_bfloat16, false>), C, kClassThreads, kCodes * 4, 0, (const uint16_t*)codes6, n_pad, 1, hist6,
-                       x, t, N, mode, spec, slow_rows, state, cm6);
+                       x, C, t, N, mode, spec, slow_rows, state, cm6);
   };
   // reference: v2 row pass (mode given), then the same class pass with no rare-row list
   auto ref2 = [&](const __hip_bfloat16* x, const int64_t* t, bool ign) {
     hipLaunchKernelGGL((tmx_ref::mc_codes_kernel<__hip_bfloat16, false, 0>), grid2, tmx_ref::kA_Threads, shm2, 0, x, t, N, C, mode2,
                        -100, ign, codes2, n_pad, cm2, err, false);
     hipLaunchKernelGGL((class_hist_kernel<__hip_bfloat16, false>), C, kClassThreads, kCodes * 4, 0, (const uint16_t*)codes2, n_pad, 1, hist2,
-                       x, t, N, mode2, false, slow_rows, state2, (int64_t*)nullptr);
+                       x, C, t, N, mode2, false, slow_rows, state2, (int64_t*)nullptr);
   };
 
   printf("{\"N\": %lld, \"C\": %d", (long long)N, C);

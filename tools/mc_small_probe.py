@@ -1,0 +1,33 @@
+"""MulticlassAUROC update cost across class counts (two-pass path needs C % 8 == 0; others take the generic kernel)."""
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+import torchmetrics_forked_amd as tm  # noqa: E402
+from torchmetrics_forked_amd import ops  # noqa: E402
+
+ops.require()
+dev = torch.device("cuda", 0)
+
+
+def timed(fn, n=10):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(n):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / n
+
+
+out = {}
+for C, N in ((10, 1 << 20), (16, 1 << 20), (100, 1 << 18), (104, 1 << 18), (1000, 1 << 16), (1001, 1 << 16)):
+    p = torch.randn(N, C, device=dev).bfloat16()
+    t = torch.randint(0, C, (N,), device=dev)
+    m = tm.MulticlassAUROC(num_classes=C).to(dev)
+    out[f"C{C}_N{N}_ms"] = round(1e3 * timed(lambda: m.update(p, t)), 3)
+print(out)
