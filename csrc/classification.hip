@@ -771,6 +771,50 @@ __global__ void binned_hist_kernel(const T* __restrict__ preds, const int64_t* _
   }
 }
 
+// Element-wise (binary / multilabel) binned histogram with the [C][2][T+1] counts privatised in LDS: one copy per wave
+// when they fit (same-address atomics of a wave's lanes then only collide within the wave), else one per block; one
+// global atomic per non-empty bin on flush.  The global-atomic form above put every score of a BinaryAUROC on the
+// same 2 (T + 1) addresses (16M fp32 scores, T = 100: 9.3 ms per update).
+constexpr int kBinnedThreads = 512;
+
+template <typename T>
+__global__ void __launch_bounds__(kBinnedThreads) binned_hist_lds_kernel(const T* __restrict__ preds, const int64_t* __restrict__ target,
+                                                                         int64_t N, int C, int64_t S, const float* __restrict__ thr,
+                                                                         int nT, const int* __restrict__ flag, int64_t ignore_index,
+                                                                         bool has_ignore, int copies, int* __restrict__ hist) {
+  extern __shared__ __attribute__((aligned(16))) int s_mem[];  // [nT] thresholds as float, then [copies][C][2][nT + 1]
+  float* s_thr = reinterpret_cast<float*>(s_mem);
+  const int nT4 = (nT + 3) / 4 * 4;
+  int* s_hist = s_mem + nT4;
+  const int H = C * 2 * (nT + 1);
+  for (int i = threadIdx.x; i < nT; i += kBinnedThreads) s_thr[i] = thr[i];
+  for (int i = threadIdx.x; i < copies * H; i += kBinnedThreads) s_hist[i] = 0;
+  __syncthreads();
+  const bool do_norm = flag[0] != 0;
+  int* my = s_hist + (int)((threadIdx.x / kWave) % copies) * H;
+  const int64_t total = N * C * S;
+  for (int64_t i = blockIdx.x * (int64_t)kBinnedThreads + threadIdx.x; i < total; i += (int64_t)gridDim.x * kBinnedThreads) {
+    const int64_t t = target[i];
+    if (has_ignore && t == ignore_index) continue;
+    if (t != 0 && t != 1) continue;
+    const int l = static_cast<int>((i / S) % C);
+    float v = to_f32<T>(preds[i]);
+    if (do_norm) v = round_trip<T>(1.f / (1.f + expf(-v)));
+    int lo = 0, hi = nT;  // first index with thr > v
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (s_thr[mid] <= v) lo = mid + 1; else hi = mid;
+    }
+    atomicAdd(my + (l * 2 + (int)t) * (nT + 1) + lo, 1);
+  }
+  __syncthreads();
+  for (int b = threadIdx.x; b < H; b += kBinnedThreads) {
+    int cnt = 0;
+    for (int k = 0; k < copies; ++k) cnt += s_hist[k * H + b];
+    if (cnt) atomicAdd(hist + b, cnt);
+  }
+}
+
 // confmat[t, c, y, p]: y = target (0/1), p = (score >= thr[t]).  tp=[1][1] fp=[0][1] fn=[1][0] tn=[0][0]
 __global__ void binned_scan_kernel(const int* __restrict__ hist, int C, int nT, int64_t* __restrict__ confmat) {
   const int c = blockIdx.x;
@@ -817,6 +861,18 @@ void binned_curve_update(const at::Tensor& preds_, const at::Tensor& target_, co
       if (total == 0) return;
       const int64_t N = target.size(0);
       const int64_t S = total / (N * C);
+      const int64_t H = (int64_t)C * 2 * (nT + 1);
+      const int64_t thr_ints = (nT + 3) / 4 * 4;
+      constexpr int64_t kLdsBudget = 64 * 1024 / sizeof(int);
+      if (thr_ints + H <= kLdsBudget) {
+        const int copies = static_cast<int>(std::min<int64_t>(kBinnedThreads / kWave, (kLdsBudget - thr_ints) / H));
+        const size_t shm_lds = (size_t)(thr_ints + copies * H) * sizeof(int);
+        const int grid = static_cast<int>(std::min<int64_t>(1024, (total + kBinnedThreads - 1) / kBinnedThreads));
+        hipLaunchKernelGGL(binned_hist_lds_kernel<scalar_t>, std::max(grid, 1), kBinnedThreads, shm_lds, stream(), p,
+                           target.data_ptr<int64_t>(), N, C, S, thr.data_ptr<float>(), nT, flag.data_ptr<int>(), ignore_index,
+                           has_ignore, copies, hist.data_ptr<int>());
+        return;
+      }
       hipLaunchKernelGGL((binned_hist_kernel<scalar_t, 1>), grid_for(total, block, 4096), block, shm, stream(), p,
                          target.data_ptr<int64_t>(), N, C, S, thr.data_ptr<float>(), nT, flag.data_ptr<int>(), ignore_index,
                          has_ignore, hist.data_ptr<int>());
@@ -824,6 +880,172 @@ void binned_curve_update(const at::Tensor& preds_, const at::Tensor& target_, co
   });
   TMX_LAUNCH_CHECK();
   hipLaunchKernelGGL(binned_scan_kernel, C, 64, 0, stream(), hist.data_ptr<int>(), C, nT, confmat.data_ptr<int64_t>());
+  TMX_LAUNCH_CHECK();
+}
+
+// =========================================================================================================
+// calibration error: bins[3, n_bins + 1] (count, sum confidence, sum accuracy) in float64
+// bin = bucketize(conf, boundaries, right=True) - 1 (boundaries = torch.linspace(0, 1, n_bins + 1) in fp32): the
+// number of boundaries <= conf, minus one; NaN -> the last bin (every comparison false), as torch.bucketize.
+// Per-block LDS accumulation (ds_add_f64), one global f64 atomic per bin and channel per block — the reference's
+// index_add_ puts every sample on the same n_bins + 1 addresses (3.2 ms per update at 65536 x 1000, most of it
+// contended f64 atomics).
+// =========================================================================================================
+constexpr int kCalThreads = 256;
+
+__device__ __forceinline__ int cal_bin(float conf, const float* __restrict__ s_b, int nb1) {
+  int lo = 0, hi = nb1;  // first boundary > conf (NaN: none is <= conf -> lo stays... handled below)
+  if (conf != conf) return nb1 - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (s_b[mid] <= conf) lo = mid + 1; else hi = mid;
+  }
+  return lo - 1 < 0 ? nb1 - 1 : lo - 1;  // conf < 0: bucketize gives 0 -> index -1 -> wraps to the last bin
+}
+
+__device__ __forceinline__ void cal_flush(const double* __restrict__ s_acc, int nb1, double* __restrict__ bins) {
+  for (int i = threadIdx.x; i < 3 * nb1; i += kCalThreads)
+    if (s_acc[i] != 0.0) atomicAdd(bins + i, s_acc[i]);
+}
+
+// element-wise: conf[N] (any float dtype), acc[N] (any numeric dtype, converted to float)
+template <typename T, typename A>
+__global__ void __launch_bounds__(kCalThreads) ce_bins_kernel(const T* __restrict__ conf, const A* __restrict__ acc, int64_t n,
+                                                             const float* __restrict__ boundaries, int nb1, double* __restrict__ bins) {
+  extern __shared__ __attribute__((aligned(16))) double s_acc[];  // [3][nb1], then boundaries
+  float* s_b = reinterpret_cast<float*>(s_acc + 3 * nb1);
+  for (int i = threadIdx.x; i < 3 * nb1; i += kCalThreads) s_acc[i] = 0.0;
+  for (int i = threadIdx.x; i < nb1; i += kCalThreads) s_b[i] = boundaries[i];
+  __syncthreads();
+  for (int64_t i = blockIdx.x * (int64_t)kCalThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kCalThreads) {
+    const float c = static_cast<float>(to_f32<T>(conf[i]));
+    const int b = cal_bin(c, s_b, nb1);
+    atomicAdd(&s_acc[b], 1.0);
+    atomicAdd(&s_acc[nb1 + b], (double)c);
+    atomicAdd(&s_acc[2 * nb1 + b], (double)static_cast<float>(acc[i]));
+  }
+  __syncthreads();
+  cal_flush(s_acc, nb1, bins);
+}
+
+// multiclass, fused: one wave per row of preds[N, C].  Reference semantics (preds.softmax(1) if the batch is not in
+// [0, 1], then .max(1)): conf = the largest softmax value rounded to the input dtype = RNE(1 / sum exp(x - max)),
+// pred = the FIRST class whose rounded softmax equals it (rounding can tie classes the logits order), correct =
+// (pred == target); a row with NaN (or a softmax row with +-inf) gives conf NaN and the first NaN's index.
+template <typename T>
+__global__ void __launch_bounds__(kCalThreads) mc_calibration_kernel(const T* __restrict__ preds, const int64_t* __restrict__ target,
+                                                                    int64_t n, int C, const int* __restrict__ softmax_flag,
+                                                                    const float* __restrict__ boundaries, int nb1,
+                                                                    double* __restrict__ bins) {
+  extern __shared__ __attribute__((aligned(16))) double s_acc[];
+  float* s_b = reinterpret_cast<float*>(s_acc + 3 * nb1);
+  for (int i = threadIdx.x; i < 3 * nb1; i += kCalThreads) s_acc[i] = 0.0;
+  for (int i = threadIdx.x; i < nb1; i += kCalThreads) s_b[i] = boundaries[i];
+  __syncthreads();
+  const bool do_softmax = softmax_flag[0] != 0;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t wave = (blockIdx.x * (int64_t)kCalThreads + threadIdx.x) / kWave;
+  const int64_t nwaves = (int64_t)gridDim.x * kCalThreads / kWave;
+  for (int64_t r = wave; r < n; r += nwaves) {
+    const T* row = preds + r * C;
+    float mx = -INFINITY;
+    int first_nan = C, am = C;
+    for (int c = lane; c < C; c += kWave) {
+      const float v = to_f32<T>(row[c]);
+      if (v != v) first_nan = min(first_nan, c);
+      else if (am == C || v > mx) { mx = v; am = c; }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) first_nan = min(first_nan, __shfl_xor(first_nan, off, kWave));
+    wave_argmax(mx, am);
+    float conf;
+    int pred;
+    if (first_nan < C) {
+      conf = NAN;
+      pred = do_softmax ? 0 : first_nan;  // softmax of a NaN row is all NaN: max returns index 0
+    } else if (!do_softmax) {
+      conf = mx;
+      pred = am;
+    } else if (mx == INFINITY || mx == -INFINITY) {  // inf - inf: the softmax row is NaN everywhere
+      conf = NAN;
+      pred = 0;
+    } else {
+      float s = 0.f;
+      for (int c = lane; c < C; c += kWave) s += expf(to_f32<T>(row[c]) - mx);
+      s = wave_sum(s);
+      conf = round_trip<T>(1.f / s);  // exp(0) / s, rounded as torch stores the softmax
+      int first = C;
+      for (int c = lane; c < C; c += kWave)
+        if (round_trip<T>(expf(to_f32<T>(row[c]) - mx) / s) == conf) { first = c; break; }
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) first = min(first, __shfl_xor(first, off, kWave));
+      pred = first;
+    }
+    if (lane == 0) {
+      const int b = cal_bin(conf, s_b, nb1);
+      atomicAdd(&s_acc[b], 1.0);
+      atomicAdd(&s_acc[nb1 + b], (double)conf);
+      atomicAdd(&s_acc[2 * nb1 + b], pred == target[r] ? 1.0 : 0.0);
+    }
+  }
+  __syncthreads();
+  cal_flush(s_acc, nb1, bins);
+}
+
+void ce_bins_update(const at::Tensor& conf_, const at::Tensor& acc_, const at::Tensor& boundaries_, at::Tensor& bins) {
+  auto conf = conf_.contiguous().reshape(-1);
+  auto acc = acc_.contiguous().reshape(-1);
+  auto bnd = boundaries_.contiguous().to(at::kFloat);
+  const int nb1 = static_cast<int>(bnd.numel());
+  TORCH_CHECK(bins.is_contiguous() && bins.scalar_type() == at::kDouble && bins.numel() == 3 * nb1, "bins must be float64 [3, n_bins + 1]");
+  TORCH_CHECK(conf.numel() == acc.numel(), "confidences / accuracies size mismatch");
+  const int64_t n = conf.numel();
+  if (n == 0) return;
+  if (acc.scalar_type() == at::kBool) acc = acc.to(at::kFloat);
+  const size_t shm = 3 * nb1 * sizeof(double) + nb1 * sizeof(float);
+  TORCH_CHECK(shm <= 64 * 1024, "ce_bins_update: too many bins");
+  const int grid = grid_for(n, kCalThreads, 1024);
+  TMX_DISPATCH_FLOAT(conf.scalar_type(), "ce_bins_update", [&] {
+    using CT = scalar_t;
+    const CT* cp = reinterpret_cast<const CT*>(conf.data_ptr());
+    switch (acc.scalar_type()) {
+      case at::kFloat:
+        hipLaunchKernelGGL((ce_bins_kernel<CT, float>), grid, kCalThreads, shm, stream(), cp, acc.data_ptr<float>(), n,
+                           bnd.data_ptr<float>(), nb1, bins.data_ptr<double>());
+        break;
+      case at::kDouble:
+        hipLaunchKernelGGL((ce_bins_kernel<CT, double>), grid, kCalThreads, shm, stream(), cp, acc.data_ptr<double>(), n,
+                           bnd.data_ptr<float>(), nb1, bins.data_ptr<double>());
+        break;
+      default: {
+        auto a64 = acc.to(at::kLong);
+        hipLaunchKernelGGL((ce_bins_kernel<CT, int64_t>), grid, kCalThreads, shm, stream(), cp, a64.data_ptr<int64_t>(), n,
+                           bnd.data_ptr<float>(), nb1, bins.data_ptr<double>());
+      }
+    }
+  });
+  TMX_LAUNCH_CHECK();
+}
+
+void mc_calibration_update(const at::Tensor& preds_, const at::Tensor& target_, const at::Tensor& boundaries_, at::Tensor& bins) {
+  auto preds = preds_.contiguous();
+  auto target = target_.contiguous().to(at::kLong).reshape(-1);
+  auto bnd = boundaries_.contiguous().to(at::kFloat);
+  const int nb1 = static_cast<int>(bnd.numel());
+  TORCH_CHECK(preds.dim() == 2 && preds.size(0) == target.numel(), "preds must be [N, C] with target [N]");
+  TORCH_CHECK(bins.is_contiguous() && bins.scalar_type() == at::kDouble && bins.numel() == 3 * nb1, "bins must be float64 [3, n_bins + 1]");
+  const int64_t n = preds.size(0);
+  const int C = static_cast<int>(preds.size(1));
+  if (n == 0) return;
+  auto flag = range_flag(preds);
+  const size_t shm = 3 * nb1 * sizeof(double) + nb1 * sizeof(float);
+  TORCH_CHECK(shm <= 64 * 1024, "mc_calibration_update: too many bins");
+  const int grid = grid_for(n * kWave, kCalThreads, 2048);
+  TMX_DISPATCH_FLOAT(preds.scalar_type(), "mc_calibration_update", [&] {
+    hipLaunchKernelGGL(mc_calibration_kernel<scalar_t>, grid, kCalThreads, shm, stream(),
+                       reinterpret_cast<const scalar_t*>(preds.data_ptr()), target.data_ptr<int64_t>(), n, C,
+                       flag.data_ptr<int>(), bnd.data_ptr<float>(), nb1, bins.data_ptr<double>());
+  });
   TMX_LAUNCH_CHECK();
 }
 
@@ -837,6 +1059,8 @@ TORCH_LIBRARY_FRAGMENT(tmx, m) {
   m.def("curve_hist_update(Tensor preds, Tensor target, Tensor(a!) hist, int task, int ignore_index, bool has_ignore, Tensor(b!)? confmat, Tensor? norm_flag, Tensor(c!)? err_flag, Tensor(d!)? mode_state) -> ()");
   m.def("curve_hist_reduce(Tensor hist) -> Tensor");
   m.def("binned_curve_update(Tensor preds, Tensor target, Tensor thresholds, Tensor(a!) confmat, int task, int ignore_index, bool has_ignore, Tensor? norm_flag) -> ()");
+  m.def("ce_bins_update(Tensor conf, Tensor acc, Tensor boundaries, Tensor(a!) bins) -> ()");
+  m.def("mc_calibration_update(Tensor preds, Tensor target, Tensor boundaries, Tensor(a!) bins) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(tmx, CUDA, m) {
@@ -847,4 +1071,6 @@ TORCH_LIBRARY_IMPL(tmx, CUDA, m) {
   m.impl("curve_hist_update", &tmx::curve_hist_update);
   m.impl("curve_hist_reduce", &tmx::curve_hist_reduce);
   m.impl("binned_curve_update", &tmx::binned_curve_update);
+  m.impl("ce_bins_update", &tmx::ce_bins_update);
+  m.impl("mc_calibration_update", &tmx::mc_calibration_update);
 }

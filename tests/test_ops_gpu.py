@@ -230,3 +230,53 @@ def test_curve_hist_multilabel_two_pass(L, probs):
     assert diff <= max(8, int(1e-4 * N * L)), diff  # CPU vs GPU expf may flip a rare bf16 rounding of the sigmoid
     assert g[2].sum().item() == c[2].sum().item()
     assert torch.equal(g[2][:, 1].sum(-1).cpu(), c[2][:, 1].sum(-1))  # positives per label exact
+
+
+@pytest.mark.parametrize("task,C", [("binary", 1), ("multilabel", 5), ("multilabel", 300)])
+def test_binned_curve_lds(task, C):
+    """Element-wise binned histogram with LDS-privatised per-wave / per-block copies vs the CPU path."""
+    N, T = 20_001, 101
+    thr = torch.linspace(0, 1, T)
+    preds = torch.rand(N, C, 1)
+    target = torch.randint(0, 2, (N, C, 1))
+    target[::9] = -1
+    cm = torch.zeros(T, C, 2, 2, dtype=torch.long)
+    g, c, _, _ = _both(K.binned_curve_update, preds, target, thr, cm, task, -1)
+    assert torch.equal(g[3].cpu(), c[3])
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("probs", [False, True])
+def test_multiclass_calibration_fused(dtype, probs):
+    """Fused top-label calibration kernel (rounded softmax max, first arg-max, NaN rows) vs the CPU eager path."""
+    import torchmetrics_forked_amd as tm
+
+    N, C = 5000, 37
+    x = torch.randn(N, C)
+    x = x.softmax(1) if probs else x * 3
+    x[11::97, 5] = float("nan")
+    x[3::101, 1] = x[3::101].max(1).values  # exact ties at the maximum
+    preds = x.to(dtype)
+    target = torch.randint(0, C, (N,))
+    target[::13] = -1
+    out = []
+    for dev in ("cuda", "cpu"):
+        m = tm.MulticlassCalibrationError(num_classes=C, n_bins=15, norm="l1", ignore_index=-1).to(dev)
+        m.update(preds.to(dev), target.to(dev))
+        out.append((m.bins.cpu(), m.compute().cpu()))
+    torch.testing.assert_close(out[0][0], out[1][0], rtol=1e-9, atol=1e-6, equal_nan=True)
+    torch.testing.assert_close(out[0][1], out[1][1], rtol=1e-5, atol=1e-6, equal_nan=True)
+
+
+def test_binary_calibration_bins():
+    import torchmetrics_forked_amd as tm
+
+    N = 100_003
+    preds, target = torch.rand(N), torch.randint(0, 2, (N,))
+    out = []
+    for dev in ("cuda", "cpu"):
+        m = tm.BinaryCalibrationError(n_bins=10, norm="l2").to(dev)
+        m.update(preds.to(dev), target.to(dev))
+        out.append((m.bins.cpu(), m.compute().cpu()))
+    torch.testing.assert_close(out[0][0], out[1][0], rtol=1e-9, atol=1e-6)
+    torch.testing.assert_close(out[0][1], out[1][1], rtol=1e-6, atol=1e-7)
