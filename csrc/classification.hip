@@ -196,6 +196,85 @@ __global__ void mc_confmat_argmax_wave_kernel(const T* __restrict__ preds, const
   if (use_lds) confmat_flush(s_cm, cm, C);
 }
 
+// Vectorised arg-max confusion matrix for aligned rows (C multiple of the 16-B vector width, C <= 64 * VEC * NCH):
+// lane L holds classes [VEC * L, VEC * L + VEC) of each 64 * VEC chunk (ascending per lane), every wave keeps 4
+// rows' 16-B loads in flight, NaN-first arg-max semantics of argmax_better / wave_argmax, one confusion-matrix
+// increment per row.  (One wave per row with scalar 2-B loads: 0.11 ms at 65536 x 1000 bf16.)
+template <typename T> struct VecOf { static constexpr int n = 16 / sizeof(T); };
+
+template <typename T> __device__ __forceinline__ float vec_elem(const uint4& w, int k) {
+  if constexpr (sizeof(T) == 2) {
+    const uint32_t p[4] = {w.x, w.y, w.z, w.w};
+    const uint16_t b = (k & 1) ? (p[k >> 1] >> 16) : (p[k >> 1] & 0xFFFFu);
+    return to_f32<T>(*reinterpret_cast<const T*>(&b));
+  } else if constexpr (sizeof(T) == 4) {
+    const uint32_t p[4] = {w.x, w.y, w.z, w.w};
+    return __uint_as_float(p[k]);
+  } else {
+    const uint64_t q = (k == 0) ? ((uint64_t)w.y << 32 | w.x) : ((uint64_t)w.w << 32 | w.z);
+    return static_cast<float>(__longlong_as_double(static_cast<long long>(q)));
+  }
+}
+
+template <typename T, int NCH>
+__global__ void __launch_bounds__(256) mc_confmat_argmax_vec_kernel(const T* __restrict__ preds, const int64_t* __restrict__ target,
+                                                                    int64_t n, int C, int64_t ignore_index, bool has_ignore,
+                                                                    bool use_lds, int64_t* __restrict__ cm) {
+  constexpr int VEC = VecOf<T>::n;
+  constexpr int kRows = 4;
+  extern __shared__ __attribute__((aligned(16))) int s_cm[];
+  if (use_lds) {
+    for (int b = threadIdx.x; b < C * C; b += blockDim.x) s_cm[b] = 0;
+    __syncthreads();
+  }
+  const int lane = threadIdx.x & (kWave - 1);
+  const int nvec = C / VEC;
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / kWave;
+  const int64_t nwaves = (int64_t)gridDim.x * blockDim.x / kWave;
+  for (int64_t r0 = wave * kRows; r0 < n; r0 += nwaves * kRows) {
+    uint4 w[kRows][NCH];
+#pragma unroll
+    for (int i = 0; i < kRows; ++i) {
+      const uint4* row = reinterpret_cast<const uint4*>(preds + min(r0 + i, n - 1) * C);
+#pragma unroll
+      for (int ch = 0; ch < NCH; ++ch) {
+        const int q = lane + kWave * ch;
+        w[i][ch] = row[q < nvec ? q : nvec - 1];
+      }
+    }
+    int am[kRows];
+#pragma unroll
+    for (int i = 0; i < kRows; ++i) {
+      float best = -INFINITY;
+      int bi = C;
+#pragma unroll
+      for (int ch = 0; ch < NCH; ++ch) {
+        const int q = lane + kWave * ch;
+        if (q >= nvec) continue;
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) {
+          const float v = vec_elem<T>(w[i][ch], k);
+          const int c = VEC * q + k;
+          if (argmax_better(v, c, best, bi)) { best = v; bi = c; }
+        }
+      }
+      wave_argmax(best, bi);
+      am[i] = __builtin_amdgcn_readfirstlane(bi);
+    }
+    if (lane < kRows) {
+      int a = am[0];
+#pragma unroll
+      for (int i = 1; i < kRows; ++i) a = lane == i ? am[i] : a;
+      const int64_t r = r0 + lane;
+      if (r < n) {
+        const int64_t t = target[r];
+        if (!(has_ignore && t == ignore_index)) confmat_add(s_cm, cm, use_lds, C, t, a);
+      }
+    }
+  }
+  if (use_lds) confmat_flush(s_cm, cm, C);
+}
+
 // confmat: int64 [C, C] updated in place.  preds: [N] int64 labels or [N, C] float scores.
 void mc_confmat_update(const at::Tensor& preds_, const at::Tensor& target_, at::Tensor& confmat, int64_t ignore_index,
                        bool has_ignore) {
@@ -217,7 +296,15 @@ void mc_confmat_update(const at::Tensor& preds_, const at::Tensor& target_, at::
     TORCH_CHECK(preds.numel() == n * C, "preds must be [N, C] with C = confmat.size(0)");
     TMX_DISPATCH_FLOAT(preds.scalar_type(), "mc_confmat_update", [&] {
       const scalar_t* p = reinterpret_cast<const scalar_t*>(preds.data_ptr());
-      if (C <= 32) {
+      constexpr int VEC = VecOf<scalar_t>::n;
+      const bool vec_ok = C % VEC == 0 && C > 32 && (reinterpret_cast<uintptr_t>(p) & 15) == 0;
+      if (vec_ok && C <= kWave * VEC) {
+        hipLaunchKernelGGL((mc_confmat_argmax_vec_kernel<scalar_t, 1>), grid_for(n * kWave / 4, block, 4096), block, shm, stream(), p,
+                           target.data_ptr<int64_t>(), n, C, ignore_index, has_ignore, use_lds, confmat.data_ptr<int64_t>());
+      } else if (vec_ok && C <= 2 * kWave * VEC) {
+        hipLaunchKernelGGL((mc_confmat_argmax_vec_kernel<scalar_t, 2>), grid_for(n * kWave / 4, block, 4096), block, shm, stream(), p,
+                           target.data_ptr<int64_t>(), n, C, ignore_index, has_ignore, use_lds, confmat.data_ptr<int64_t>());
+      } else if (C <= 32) {
         hipLaunchKernelGGL(mc_confmat_argmax_thread_kernel<scalar_t>, grid_for(n, block, 2048), block, shm, stream(), p,
                            target.data_ptr<int64_t>(), n, C, ignore_index, has_ignore, use_lds, confmat.data_ptr<int64_t>());
       } else {

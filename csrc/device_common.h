@@ -79,7 +79,9 @@ __device__ __forceinline__ void wave_argmax(float& v, int& idx) {
     float ov = __shfl_xor(v, off, kWave);
     int oi = __shfl_xor(idx, off, kWave);
     bool o_nan = ov != ov, s_nan = v != v;
-    bool take = (o_nan && !s_nan) || (o_nan == s_nan && (ov > v || (ov == v && oi < idx)));
+    // NaN beats numbers; between two NaNs (or equal numbers) the lower index wins, so every lane ends with the
+    // same (value, index) — the first NaN, as torch.argmax returns
+    bool take = (o_nan && !s_nan) || (o_nan == s_nan && (o_nan ? oi < idx : (ov > v || (ov == v && oi < idx))));
     if (take) { v = ov; idx = oi; }
   }
 }

@@ -280,3 +280,19 @@ def test_binary_calibration_bins():
         out.append((m.bins.cpu(), m.compute().cpu()))
     torch.testing.assert_close(out[0][0], out[1][0], rtol=1e-9, atol=1e-6)
     torch.testing.assert_close(out[0][1], out[1][1], rtol=1e-6, atol=1e-7)
+
+
+@pytest.mark.parametrize("C,dtype", [(64, torch.float32), (512, torch.float32), (40, torch.bfloat16), (1000, torch.bfloat16),
+                                     (1024, torch.float16), (96, torch.float64)])
+def test_mc_confmat_vectorised(C, dtype):
+    """Vectorised arg-max confusion matrix (4 rows in flight per wave): ties -> first index, NaN -> first NaN."""
+    N = 9001
+    x = torch.randn(N, C)
+    x[3::17, 2] = x[3::17].max(1).values + 1
+    x[3::17, 7] = x[3::17, 2]  # tie: class 2 must win
+    x[5::29, C // 2] = float("nan")
+    x[5::58, 1] = float("nan")  # two NaNs: the first wins
+    target = torch.randint(0, C, (N,))
+    target[::11] = 3
+    g, c, _, _ = _both(K.mc_confmat_update, x.to(dtype), target, torch.zeros(C, C, dtype=torch.long), 3)
+    assert torch.equal(g[2].cpu(), c[2])
