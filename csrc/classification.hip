@@ -8,6 +8,8 @@
 //                               (stat_scores.py:405-418, confusion_matrix.py:306-337).  One wave per row for
 //                               large C (16-B vector loads), one thread per row for small C; LDS-privatised
 //                               confusion matrix when C*C int32 counters fit in 64 KiB.
+//  * tmx::mc_stat_scores_update — the same pair stream into per-class tp / fp / tn / fn states in place (no
+//                               [C, C] temporary, target/pred range validation folded into device flags).
 //  * tmx::binary_stats_update — one-pass tp/fp/tn/fn per label with the sigmoid-if-needed + threshold rule
 //                               evaluated in the input dtype (stat_scores.py:95-131, 650-681).
 //  * tmx::curve_hist_update   — exact score histogram for 16-bit scores: each (class, label, score-code) is
@@ -110,15 +112,13 @@ at::Tensor bincount(const at::Tensor& x_, int64_t minlength) {
 }
 
 // =========================================================================================================
-// multiclass confusion matrix (labels or argmax of scores)
+// multiclass (target, pred) pair stream: labels or arg-max of scores, accumulated by a policy
+//   ConfmatAcc -> int64 [C, C] confusion matrix
+//   StatAcc    -> per-class (or micro) tp / fp / tn / fn states, updated in place
+// Range validation rides along: a target outside [0, C) that is not the ignore index ORs err_t, an integer
+// prediction outside [0, C) ORs err_p (the deferred-validation flags of utilities/validation.py); such rows are
+// skipped exactly like the confusion matrix skips them.
 // =========================================================================================================
-__device__ __forceinline__ void confmat_add(int* s_cm, int64_t* g_cm, bool use_lds, int C, int64_t t, int64_t p) {
-  if (t < 0 || t >= C || p < 0 || p >= C) return;
-  int64_t idx = t * C + p;
-  if (use_lds) atomicAdd(&s_cm[idx], 1);
-  else atomic_add_i64(g_cm + idx, 1);
-}
-
 __device__ __forceinline__ void confmat_flush(int* s_cm, int64_t* g_cm, int C) {
   __syncthreads();
   for (int b = threadIdx.x; b < C * C; b += blockDim.x) {
@@ -127,34 +127,224 @@ __device__ __forceinline__ void confmat_flush(int* s_cm, int64_t* g_cm, int C) {
   }
 }
 
-__global__ void mc_confmat_labels_kernel(const int64_t* __restrict__ preds, const int64_t* __restrict__ target, int64_t n,
-                                         int C, int64_t ignore_index, bool has_ignore, bool use_lds, int64_t* __restrict__ cm) {
-  extern __shared__ __attribute__((aligned(16))) int s_cm[];
-  if (use_lds) {
-    for (int b = threadIdx.x; b < C * C; b += blockDim.x) s_cm[b] = 0;
+// Grid-wide sums of K int64 values with last-workgroup detection, without same-address pile-ups: workgroup b adds
+// its values into the 128-B line of group b % 8 (one group per XCD under the round-robin dispatch) and takes that
+// line's ticket; the group's last workgroup moves the group sums into the top line and takes the top ticket; the
+// last of those sees the grid totals.  Sums are read and reset with atomic exchanges (performed at the coherence
+// point, after the adds: every adder waits for its adds (vmcnt 0) before taking a ticket), tickets reset the
+// same way, so the table is back to zero when the kernel ends.  Called by ONE thread per workgroup; true in
+// exactly one workgroup of the grid.  slots: kGridSlotsWords zeroed int64 words.
+constexpr int kGridSlotLine = 16;                    // int64 words per 128-B line
+constexpr int kGridSlotsWords = 9 * kGridSlotLine;   // 8 group lines + top line
+template <int K>
+__device__ bool grid_sum_last(unsigned long long* slots, const long long (&v)[K], long long (&tot)[K]) {
+  const unsigned G = gridDim.x, x = blockIdx.x & 7u;
+  const unsigned groups = G < 8u ? G : 8u;
+  const unsigned gsize = (G - x + 7u) / 8u;
+  unsigned long long* line = slots + x * kGridSlotLine;
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+    if (v[k]) atomicAdd(line + 1 + k, (unsigned long long)v[k]);
+  __builtin_amdgcn_s_waitcnt(0);
+  if (atomicAdd(line, 1ull) != gsize - 1u) return false;
+  long long gs[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) gs[k] = (long long)atomicExch(line + 1 + k, 0ull);
+  atomicExch(line, 0ull);
+  unsigned long long* top = slots + 8 * kGridSlotLine;
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+    if (gs[k]) atomicAdd(top + 1 + k, (unsigned long long)gs[k]);
+  __builtin_amdgcn_s_waitcnt(0);
+  if (atomicAdd(top, 1ull) != groups - 1u) return false;
+#pragma unroll
+  for (int k = 0; k < K; ++k) tot[k] = (long long)atomicExch(top + 1 + k, 0ull);
+  atomicExch(top, 0ull);
+  return true;
+}
+
+struct ConfmatAcc {
+  int64_t* cm;
+  int C;
+  bool use_lds;
+  // LDS copy only for tiny C: zeroing + flushing C*C words per workgroup costs more than the contention it saves
+  static ConfmatAcc make(int64_t* cm, int C) { return {cm, C, C <= 32}; }
+  int64_t lds_words() const { return use_lds ? (int64_t)C * C : 0; }
+  __host__ size_t lds_bytes() const { return use_lds ? (size_t)C * C * sizeof(int) : 0; }
+  __device__ void init(int* s) {
+    if (!use_lds) return;
+    for (int b = threadIdx.x; b < C * C; b += blockDim.x) s[b] = 0;
     __syncthreads();
   }
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    int64_t t = target[i];
-    if (has_ignore && t == ignore_index) continue;
-    confmat_add(s_cm, cm, use_lds, C, t, preds[i]);
+  __device__ void add(int* s, int t, int p) {
+    const int idx = t * C + p;
+    if (use_lds) atomicAdd(&s[idx], 1);
+    else atomic_add_i64(cm + idx, 1);
   }
-  if (use_lds) confmat_flush(s_cm, cm, C);
+  __device__ void flush(int* s) {
+    if (use_lds) confmat_flush(s, cm, C);
+  }
+};
+
+// tp[t] / fp[p] / fn[t] per valid row, privatised in LDS ([3][C] ints) when they fit.  tn[c] = V - tp - fp - fn
+// with V the batch's valid-row count: each block subtracts its (tp + fp + fn)[c] sparsely and contributes its V
+// to grid_sum_last; the last block adds the total V to every class, so a batch costs one launch and no
+// temporary.  micro: four scalar states, tn += C * V - tp - 2 * fp (every wrong row is one fp and one fn), the
+// per-block sums also go through grid_sum_last (4096 blocks x 4 atomics on one line cost ~35 us).
+enum StatMode { kStatLds = 0, kStatGlobal = 1, kStatMicro = 2 };
+
+template <int MODE>
+struct StatAcc {
+  static constexpr bool use_lds = MODE == kStatLds;
+  static constexpr bool micro = MODE == kStatMicro;
+  int64_t *tp, *fp, *tn, *fn;
+  unsigned long long* ticket;
+  int C;
+  int n_valid, n_tp, n_fp;  // per-thread counters
+
+  static bool lds_fits(int C) { return 3 * (int64_t)C * 4 <= 60 * 1024; }
+  __host__ __device__ int base() const { return use_lds ? 3 * C : 0; }
+  __host__ size_t lds_bytes() const { return (size_t)(base() + 4) * sizeof(int); }
+  int64_t lds_words() const { return base(); }
+  __device__ void init(int* s) {
+    const int nb = base() + 4;
+    for (int b = threadIdx.x; b < nb; b += blockDim.x) s[b] = 0;
+    __syncthreads();
+  }
+  __device__ void add(int* s, int t, int p) {
+    ++n_valid;
+    if constexpr (micro) {
+      if (p == t) ++n_tp;
+      else ++n_fp;
+    } else if constexpr (use_lds) {
+      if (p == t) {
+        atomicAdd(&s[t], 1);
+      } else {
+        atomicAdd(&s[C + p], 1);
+        atomicAdd(&s[2 * C + t], 1);
+      }
+    } else if (p == t) {
+      atomic_add_i64(tp + t, 1);
+      atomic_add_i64(tn + t, -1);
+    } else {
+      atomic_add_i64(fp + p, 1);
+      atomic_add_i64(fn + t, 1);
+      atomic_add_i64(tn + p, -1);
+      atomic_add_i64(tn + t, -1);
+    }
+  }
+  __device__ void flush(int* s) {
+    const int b0 = base();
+    const int lane = threadIdx.x & (kWave - 1);
+    const long long v = wave_sum((long long)n_valid);
+    const long long wt = micro ? wave_sum((long long)n_tp) : 0;
+    const long long wf = micro ? wave_sum((long long)n_fp) : 0;
+    if constexpr (use_lds) {
+      __shared__ long long s_total;
+      __syncthreads();  // every LDS increment of the block is done
+      if (lane == 0 && v) atomicAdd(&s[b0], (int)v);
+      for (int c = threadIdx.x; c < C; c += blockDim.x) {
+        const int a = s[c], b = s[C + c], d = s[2 * C + c];
+        if (a) atomic_add_i64(tp + c, a);
+        if (b) atomic_add_i64(fp + c, b);
+        if (d) atomic_add_i64(fn + c, d);
+        if (a | b | d) atomic_add_i64(tn + c, -(long long)(a + b + d));
+      }
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        const long long mine[1] = {s[b0]};
+        long long tot[1];
+        s_total = grid_sum_last<1>(ticket, mine, tot) ? tot[0] : -1;
+      }
+      __syncthreads();
+      const long long total = s_total;
+      if (total > 0)
+        for (int c = threadIdx.x; c < C; c += blockDim.x) atomic_add_i64(tn + c, total);
+      return;
+    }
+    // No per-class LDS: no end-of-kernel barrier either (finished waves leave instead of holding their slots at
+    // __syncthreads).  Each wave adds its sums to LDS and counts itself done; the block's last wave contributes.
+    int done = 0;
+    if (lane == 0) {
+      if (v) atomicAdd(&s[b0], (int)v);
+      if (wt) atomicAdd(&s[b0 + 1], (int)wt);
+      if (wf) atomicAdd(&s[b0 + 2], (int)wf);
+      done = __hip_atomic_fetch_add(&s[b0 + 3], 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    done = __builtin_amdgcn_readfirstlane(done);
+    if (done != (int)(blockDim.x / kWave) - 1) return;
+    int last = 0;
+    long long tot[3] = {0, 0, 0};
+    if (lane == 0) {
+      if constexpr (micro) {
+        const long long mine[3] = {s[b0], s[b0 + 1], s[b0 + 2]};
+        last = grid_sum_last<3>(ticket, mine, tot);
+      } else {
+        const long long mine[1] = {s[b0]};
+        long long t1[1];
+        last = grid_sum_last<1>(ticket, mine, t1);
+        tot[0] = t1[0];
+      }
+    }
+    if (!__builtin_amdgcn_readfirstlane(last)) return;
+    if constexpr (micro) {
+      if (lane == 0) {
+        const long long V = tot[0], T = tot[1], F = tot[2];
+        atomic_add_i64(tp, T);
+        atomic_add_i64(fp, F);
+        atomic_add_i64(fn, F);
+        atomic_add_i64(tn, (long long)C * V - T - 2 * F);
+      }
+    } else {
+      const long long total = __shfl(tot[0], 0);
+      if (total > 0)
+        for (int c = lane; c < C; c += kWave) atomic_add_i64(tn + c, total);
+    }
+  }
+};
+
+struct PairChecks {
+  bool bad_t = false, bad_p = false;
+  // true when the (target, pred) pair should be accumulated
+  __device__ __forceinline__ bool keep(int64_t t, int64_t p, int C, int64_t ignore_index, bool has_ignore) {
+    if (p < 0 || p >= C) bad_p = true;
+    if (has_ignore && t == ignore_index) return false;
+    if (t < 0 || t >= C) {
+      bad_t = true;
+      return false;
+    }
+    return p >= 0 && p < C;
+  }
+  __device__ __forceinline__ void report(int* err_t, int* err_p) const {
+    if (bad_t && err_t) atomicOr(err_t, 1);
+    if (bad_p && err_p) atomicOr(err_p, 1);
+  }
+};
+
+template <class Acc>
+__global__ void mc_pairs_labels_kernel(const int64_t* __restrict__ preds, const int64_t* __restrict__ target, int64_t n,
+                                       int C, int64_t ignore_index, bool has_ignore, Acc acc, int* err_t, int* err_p) {
+  extern __shared__ __attribute__((aligned(16))) int s_pairs[];
+  acc.init(s_pairs);
+  PairChecks chk;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t t = target[i], p = preds[i];
+    if (chk.keep(t, p, C, ignore_index, has_ignore)) acc.add(s_pairs, (int)t, (int)p);
+  }
+  chk.report(err_t, err_p);
+  acc.flush(s_pairs);
 }
 
 // one thread per row (small C)
-template <typename T>
-__global__ void mc_confmat_argmax_thread_kernel(const T* __restrict__ preds, const int64_t* __restrict__ target, int64_t n,
-                                                int C, int64_t ignore_index, bool has_ignore, bool use_lds,
-                                                int64_t* __restrict__ cm) {
-  extern __shared__ __attribute__((aligned(16))) int s_cm[];
-  if (use_lds) {
-    for (int b = threadIdx.x; b < C * C; b += blockDim.x) s_cm[b] = 0;
-    __syncthreads();
-  }
+template <typename T, class Acc>
+__global__ void mc_pairs_argmax_thread_kernel(const T* __restrict__ preds, const int64_t* __restrict__ target, int64_t n,
+                                              int C, int64_t ignore_index, bool has_ignore, Acc acc, int* err_t) {
+  extern __shared__ __attribute__((aligned(16))) int s_pairs[];
+  acc.init(s_pairs);
+  PairChecks chk;
   for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
-    int64_t t = target[r];
-    if (has_ignore && t == ignore_index) continue;
+    const int64_t t = target[r];
+    if (!chk.keep(t, 0, C, ignore_index, has_ignore)) continue;
     const T* row = preds + r * C;
     float best = to_f32<T>(row[0]);
     int bi = 0;
@@ -162,27 +352,25 @@ __global__ void mc_confmat_argmax_thread_kernel(const T* __restrict__ preds, con
       float v = to_f32<T>(row[c]);
       if (argmax_better(v, c, best, bi)) { best = v; bi = c; }
     }
-    confmat_add(s_cm, cm, use_lds, C, t, bi);
+    acc.add(s_pairs, (int)t, bi);
   }
-  if (use_lds) confmat_flush(s_cm, cm, C);
+  chk.report(err_t, nullptr);
+  acc.flush(s_pairs);
 }
 
-// one wave per row (large C)
-template <typename T>
-__global__ void mc_confmat_argmax_wave_kernel(const T* __restrict__ preds, const int64_t* __restrict__ target, int64_t n,
-                                              int C, int64_t ignore_index, bool has_ignore, bool use_lds,
-                                              int64_t* __restrict__ cm) {
-  extern __shared__ __attribute__((aligned(16))) int s_cm[];
-  if (use_lds) {
-    for (int b = threadIdx.x; b < C * C; b += blockDim.x) s_cm[b] = 0;
-    __syncthreads();
-  }
+// one wave per row (large or unaligned C)
+template <typename T, class Acc>
+__global__ void mc_pairs_argmax_wave_kernel(const T* __restrict__ preds, const int64_t* __restrict__ target, int64_t n,
+                                            int C, int64_t ignore_index, bool has_ignore, Acc acc, int* err_t) {
+  extern __shared__ __attribute__((aligned(16))) int s_pairs[];
+  acc.init(s_pairs);
+  PairChecks chk;
   const int lane = threadIdx.x & (kWave - 1);
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / kWave;
   const int64_t nwaves = (int64_t)gridDim.x * blockDim.x / kWave;
   for (int64_t r = wave; r < n; r += nwaves) {
-    int64_t t = target[r];
-    if (has_ignore && t == ignore_index) continue;
+    const int64_t t = target[r];
+    if (!chk.keep(t, 0, C, ignore_index, has_ignore)) continue;
     const T* row = preds + r * C;
     float best = -INFINITY;
     int bi = C;  // sentinel larger than any index
@@ -191,15 +379,16 @@ __global__ void mc_confmat_argmax_wave_kernel(const T* __restrict__ preds, const
       if (argmax_better(v, c, best, bi)) { best = v; bi = c; }
     }
     wave_argmax(best, bi);
-    if (lane == 0) confmat_add(s_cm, cm, use_lds, C, t, bi);
+    if (lane == 0) acc.add(s_pairs, (int)t, bi);
   }
-  if (use_lds) confmat_flush(s_cm, cm, C);
+  chk.report(err_t, nullptr);
+  acc.flush(s_pairs);
 }
 
-// Vectorised arg-max confusion matrix for aligned rows (C multiple of the 16-B vector width, C <= 64 * VEC * NCH):
-// lane L holds classes [VEC * L, VEC * L + VEC) of each 64 * VEC chunk (ascending per lane), every wave keeps 4
-// rows' 16-B loads in flight, NaN-first arg-max semantics of argmax_better / wave_argmax, one confusion-matrix
-// increment per row.  (One wave per row with scalar 2-B loads: 0.11 ms at 65536 x 1000 bf16.)
+// Vectorised arg-max for aligned rows (C multiple of the 16-B vector width, C <= 64 * VEC * NCH): lane L holds
+// classes [VEC * L, VEC * L + VEC) of each 64 * VEC chunk (ascending per lane), every wave keeps 4 rows' 16-B
+// loads in flight, NaN-first arg-max semantics of argmax_better / wave_argmax, one pair per row.  (One wave per
+// row with scalar 2-B loads: 0.11 ms at 65536 x 1000 bf16.)
 template <typename T> struct VecOf { static constexpr int n = 16 / sizeof(T); };
 
 template <typename T> __device__ __forceinline__ float vec_elem(const uint4& w, int k) {
@@ -216,17 +405,15 @@ template <typename T> __device__ __forceinline__ float vec_elem(const uint4& w, 
   }
 }
 
-template <typename T, int NCH>
-__global__ void __launch_bounds__(256) mc_confmat_argmax_vec_kernel(const T* __restrict__ preds, const int64_t* __restrict__ target,
-                                                                    int64_t n, int C, int64_t ignore_index, bool has_ignore,
-                                                                    bool use_lds, int64_t* __restrict__ cm) {
+template <typename T, int NCH, class Acc>
+__global__ void __launch_bounds__(512) mc_pairs_argmax_vec_kernel(const T* __restrict__ preds, const int64_t* __restrict__ target,
+                                                                  int64_t n, int C, int64_t ignore_index, bool has_ignore,
+                                                                  Acc acc, int* err_t) {
   constexpr int VEC = VecOf<T>::n;
   constexpr int kRows = 4;
-  extern __shared__ __attribute__((aligned(16))) int s_cm[];
-  if (use_lds) {
-    for (int b = threadIdx.x; b < C * C; b += blockDim.x) s_cm[b] = 0;
-    __syncthreads();
-  }
+  extern __shared__ __attribute__((aligned(16))) int s_pairs[];
+  acc.init(s_pairs);
+  PairChecks chk;
   const int lane = threadIdx.x & (kWave - 1);
   const int nvec = C / VEC;
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / kWave;
@@ -245,21 +432,61 @@ __global__ void __launch_bounds__(256) mc_confmat_argmax_vec_kernel(const T* __r
     int am[kRows];
 #pragma unroll
     for (int i = 0; i < kRows; ++i) {
-      float best = -INFINITY;
-      int bi = C;
+      // per-chunk max and first position of it; any NaN in the row -> the exact NaN-first shuffle reduction
+      float m[NCH];
+      int kk[NCH];
+      bool nan = false;
 #pragma unroll
       for (int ch = 0; ch < NCH; ++ch) {
-        const int q = lane + kWave * ch;
-        if (q >= nvec) continue;
+        const bool active = lane + kWave * ch < nvec;
+        float mm = -INFINITY;
 #pragma unroll
         for (int k = 0; k < VEC; ++k) {
           const float v = vec_elem<T>(w[i][ch], k);
-          const int c = VEC * q + k;
-          if (argmax_better(v, c, best, bi)) { best = v; bi = c; }
+          nan |= active && v != v;
+          mm = __builtin_fmaxf(mm, v);
         }
+        int kf = VEC - 1;
+#pragma unroll
+        for (int k = VEC - 2; k >= 0; --k) kf = vec_elem<T>(w[i][ch], k) == mm ? k : kf;
+        m[ch] = active ? mm : -INFINITY;
+        kk[ch] = kf;
       }
-      wave_argmax(best, bi);
-      am[i] = __builtin_amdgcn_readfirstlane(bi);
+      if (__ballot(nan)) {
+        float best = -INFINITY;
+        int bi = C;
+#pragma unroll
+        for (int ch = 0; ch < NCH; ++ch) {
+          const int q = lane + kWave * ch;
+          if (q >= nvec) continue;
+#pragma unroll
+          for (int k = 0; k < VEC; ++k) {
+            const float v = vec_elem<T>(w[i][ch], k);
+            const int c = VEC * q + k;
+            if (argmax_better(v, c, best, bi)) { best = v; bi = c; }
+          }
+        }
+        wave_argmax(best, bi);
+        am[i] = __builtin_amdgcn_readfirstlane(bi);
+      } else {
+        float mx = m[0];
+#pragma unroll
+        for (int ch = 1; ch < NCH; ++ch) mx = __builtin_fmaxf(mx, m[ch]);
+        mx = wave_max_uniform(mx);
+        // lanes own ascending class runs per chunk, so the lowest lane of the first chunk holding the max has the
+        // first arg-max (an all -inf row: lane 0, position 0)
+        uint64_t b = __ballot(m[0] == mx);
+        int ch = 0;
+        if constexpr (NCH == 2) {
+          if (b == 0) {
+            b = __ballot(m[1] == mx);
+            ch = 1;
+          }
+        }
+        const int L = __builtin_ctzll(b);
+        const int kl = __builtin_amdgcn_readlane(NCH == 2 && ch ? kk[NCH - 1] : kk[0], L);
+        am[i] = VEC * (L + kWave * ch) + kl;
+      }
     }
     if (lane < kRows) {
       int a = am[0];
@@ -268,51 +495,99 @@ __global__ void __launch_bounds__(256) mc_confmat_argmax_vec_kernel(const T* __r
       const int64_t r = r0 + lane;
       if (r < n) {
         const int64_t t = target[r];
-        if (!(has_ignore && t == ignore_index)) confmat_add(s_cm, cm, use_lds, C, t, a);
+        if (chk.keep(t, 0, C, ignore_index, has_ignore)) acc.add(s_pairs, (int)t, a);
       }
     }
   }
-  if (use_lds) confmat_flush(s_cm, cm, C);
+  chk.report(err_t, nullptr);
+  acc.flush(s_pairs);
 }
 
-// confmat: int64 [C, C] updated in place.  preds: [N] int64 labels or [N, C] float scores.
-void mc_confmat_update(const at::Tensor& preds_, const at::Tensor& target_, at::Tensor& confmat, int64_t ignore_index,
-                       bool has_ignore) {
+// Dispatch one pair stream.  preds: [N] int64 labels or [N, C] float scores (contiguous).
+template <class Acc>
+void launch_pairs(const at::Tensor& preds_, const at::Tensor& target, int64_t n, int C, int64_t ignore_index, bool has_ignore,
+                  Acc acc, int* err_t, int* err_p) {
+  const size_t shm = acc.lds_bytes();
+  const int block = 256;
+  if (!preds_.is_floating_point()) {
+    auto preds = preds_.contiguous().to(at::kLong);
+    TORCH_CHECK(preds.numel() == n, "preds/target size mismatch");
+    hipLaunchKernelGGL(mc_pairs_labels_kernel<Acc>, grid_for(n, block * 4, 1024), block, shm, stream(), preds.data_ptr<int64_t>(),
+                       target.data_ptr<int64_t>(), n, C, ignore_index, has_ignore, acc, err_t, err_p);
+    return;
+  }
+  auto preds = preds_.contiguous();
+  TORCH_CHECK(preds.numel() == n * C, "preds must be [N, C] with C classes");
+  TMX_DISPATCH_FLOAT(preds.scalar_type(), "mc_pairs", [&] {
+    const scalar_t* p = reinterpret_cast<const scalar_t*>(preds.data_ptr());
+    const int64_t* t = target.data_ptr<int64_t>();
+    constexpr int VEC = VecOf<scalar_t>::n;
+    const bool vec_ok = C % VEC == 0 && C > 32 && (reinterpret_cast<uintptr_t>(p) & 15) == 0;
+    if (vec_ok && C <= kWave * VEC) {
+      hipLaunchKernelGGL((mc_pairs_argmax_vec_kernel<scalar_t, 1, Acc>), grid_for(n * kWave / 4, 512, 2048), 512, shm,
+                         stream(), p, t, n, C, ignore_index, has_ignore, acc, err_t);
+    } else if (vec_ok && C <= 2 * kWave * VEC) {
+      hipLaunchKernelGGL((mc_pairs_argmax_vec_kernel<scalar_t, 2, Acc>), grid_for(n * kWave / 4, 512, 2048), 512, shm,
+                         stream(), p, t, n, C, ignore_index, has_ignore, acc, err_t);
+    } else if (C <= 32) {
+      hipLaunchKernelGGL((mc_pairs_argmax_thread_kernel<scalar_t, Acc>), grid_for(n, block, 2048), block, shm, stream(), p, t, n,
+                         C, ignore_index, has_ignore, acc, err_t);
+    } else {
+      hipLaunchKernelGGL((mc_pairs_argmax_wave_kernel<scalar_t, Acc>), grid_for(n * kWave, block, 2048), block, shm, stream(), p,
+                         t, n, C, ignore_index, has_ignore, acc, err_t);
+    }
+  });
+}
+
+int* flag_ptr(const c10::optional<at::Tensor>& f) {
+  if (!f.has_value()) return nullptr;
+  TORCH_CHECK(f->scalar_type() == at::kInt && f->numel() >= 1 && f->is_contiguous(), "validation flags must be int32");
+  return f->data_ptr<int>();
+}
+
+// confmat: int64 [C, C] updated in place.
+void mc_confmat_update(const at::Tensor& preds, const at::Tensor& target_, at::Tensor& confmat, int64_t ignore_index,
+                       bool has_ignore, const c10::optional<at::Tensor>& err_t, const c10::optional<at::Tensor>& err_p) {
   TORCH_CHECK(confmat.is_contiguous() && confmat.scalar_type() == at::kLong, "confmat must be contiguous int64");
   const int C = static_cast<int>(confmat.size(0));
   auto target = target_.contiguous().to(at::kLong);
   const int64_t n = target.numel();
   if (n == 0) return;
-  const bool use_lds = (int64_t)C * C * 4 <= 64 * 1024;
-  const size_t shm = use_lds ? (size_t)C * C * sizeof(int) : 0;
-  const int block = 256;
-  if (!preds_.is_floating_point()) {
-    auto preds = preds_.contiguous().to(at::kLong);
-    TORCH_CHECK(preds.numel() == n, "preds/target size mismatch");
-    hipLaunchKernelGGL(mc_confmat_labels_kernel, grid_for(n, block * 4, 1024), block, shm, stream(), preds.data_ptr<int64_t>(),
-                       target.data_ptr<int64_t>(), n, C, ignore_index, has_ignore, use_lds, confmat.data_ptr<int64_t>());
-  } else {
-    auto preds = preds_.contiguous();
-    TORCH_CHECK(preds.numel() == n * C, "preds must be [N, C] with C = confmat.size(0)");
-    TMX_DISPATCH_FLOAT(preds.scalar_type(), "mc_confmat_update", [&] {
-      const scalar_t* p = reinterpret_cast<const scalar_t*>(preds.data_ptr());
-      constexpr int VEC = VecOf<scalar_t>::n;
-      const bool vec_ok = C % VEC == 0 && C > 32 && (reinterpret_cast<uintptr_t>(p) & 15) == 0;
-      if (vec_ok && C <= kWave * VEC) {
-        hipLaunchKernelGGL((mc_confmat_argmax_vec_kernel<scalar_t, 1>), grid_for(n * kWave / 4, block, 4096), block, shm, stream(), p,
-                           target.data_ptr<int64_t>(), n, C, ignore_index, has_ignore, use_lds, confmat.data_ptr<int64_t>());
-      } else if (vec_ok && C <= 2 * kWave * VEC) {
-        hipLaunchKernelGGL((mc_confmat_argmax_vec_kernel<scalar_t, 2>), grid_for(n * kWave / 4, block, 4096), block, shm, stream(), p,
-                           target.data_ptr<int64_t>(), n, C, ignore_index, has_ignore, use_lds, confmat.data_ptr<int64_t>());
-      } else if (C <= 32) {
-        hipLaunchKernelGGL(mc_confmat_argmax_thread_kernel<scalar_t>, grid_for(n, block, 2048), block, shm, stream(), p,
-                           target.data_ptr<int64_t>(), n, C, ignore_index, has_ignore, use_lds, confmat.data_ptr<int64_t>());
-      } else {
-        hipLaunchKernelGGL(mc_confmat_argmax_wave_kernel<scalar_t>, grid_for(n * kWave, block, 2048), block, shm, stream(), p,
-                           target.data_ptr<int64_t>(), n, C, ignore_index, has_ignore, use_lds, confmat.data_ptr<int64_t>());
-      }
-    });
-  }
+  launch_pairs(preds, target, n, C, ignore_index, has_ignore, ConfmatAcc::make(confmat.data_ptr<int64_t>(), C), flag_ptr(err_t),
+               flag_ptr(err_p));
+  TMX_LAUNCH_CHECK();
+}
+
+// Multiclass stat scores accumulated into the metric states in place: tp / fp / tn / fn int64 [C] (or [1] with
+// micro), ticket int64 [1] zero-initialised scratch owned by the caller (returned to zero by every launch).
+void mc_stat_scores_update(const at::Tensor& preds, const at::Tensor& target_, int64_t num_classes, at::Tensor& tp,
+                           at::Tensor& fp, at::Tensor& tn, at::Tensor& fn, at::Tensor& ticket, int64_t ignore_index,
+                           bool has_ignore, bool micro, const c10::optional<at::Tensor>& err_t,
+                           const c10::optional<at::Tensor>& err_p) {
+  const int64_t want = micro ? 1 : num_classes;
+  for (const at::Tensor* s : {&tp, &fp, &tn, &fn})
+    TORCH_CHECK(s->is_contiguous() && s->scalar_type() == at::kLong && s->numel() == want, "stat states must be int64 [",
+                want, "]");
+  TORCH_CHECK(ticket.is_contiguous() && ticket.scalar_type() == at::kLong && ticket.numel() >= kGridSlotsWords,
+              "ticket must be a zeroed int64 [", kGridSlotsWords, "] scratch");
+  const int C = static_cast<int>(num_classes);
+  auto target = target_.contiguous().to(at::kLong);
+  const int64_t n = target.numel();
+  if (n == 0) return;
+  TORCH_CHECK(n < (1ll << 40), "too many rows for one update");
+  int64_t* p_tp = tp.data_ptr<int64_t>();
+  int64_t* p_fp = fp.data_ptr<int64_t>();
+  int64_t* p_tn = tn.data_ptr<int64_t>();
+  int64_t* p_fn = fn.data_ptr<int64_t>();
+  auto* tk = reinterpret_cast<unsigned long long*>(ticket.data_ptr<int64_t>());
+  int* et = flag_ptr(err_t);
+  int* ep = flag_ptr(err_p);
+  if (micro)
+    launch_pairs(preds, target, n, C, ignore_index, has_ignore, StatAcc<kStatMicro>{p_tp, p_fp, p_tn, p_fn, tk, C, 0, 0, 0}, et, ep);
+  else if (StatAcc<kStatLds>::lds_fits(C))
+    launch_pairs(preds, target, n, C, ignore_index, has_ignore, StatAcc<kStatLds>{p_tp, p_fp, p_tn, p_fn, tk, C, 0, 0, 0}, et, ep);
+  else
+    launch_pairs(preds, target, n, C, ignore_index, has_ignore, StatAcc<kStatGlobal>{p_tp, p_fp, p_tn, p_fn, tk, C, 0, 0, 0}, et, ep);
   TMX_LAUNCH_CHECK();
 }
 
@@ -402,6 +677,271 @@ void binary_stats_update(const at::Tensor& preds_, const at::Tensor& target_, at
     auto preds = preds_.contiguous().to(at::kLong);
     hipLaunchKernelGGL((binary_stats_int_kernel<false>), grid, block, shm, stream(), preds.data_ptr<int64_t>(),
                        target.data_ptr<int64_t>(), N, L, S, ignore_index, has_ignore, counts.data_ptr<int64_t>());
+  }
+  TMX_LAUNCH_CHECK();
+}
+
+// =========================================================================================================
+// binary / multilabel stat scores in ONE launch, straight into the metric states
+// (BinaryStatScores / Accuracy / F1 / ..., Multilabel*; reference stat_scores.py:95-131, 650-681)
+//
+// The reference decides "sigmoid or not" from the whole batch (any pred outside [0, 1]) before thresholding,
+// which used to cost a range-flag pre-pass.  Here every element is thresholded both ways and the workgroups count
+// (valid, pos, p_raw, tp_raw, p_sig, tp_sig) per label into a scratch table (L == 1: straight through
+// grid_sum_last); the last workgroup reads the table with atomic exchanges (reset in the same op), picks the raw
+// or sigmoid counts from the batch-wide out-of-range count, and adds tp / fp / tn / fn into the states.
+// Layout: the input is [R, W] with W = L * S columns (label of column j = j / S).  A thread owns one vector of
+// VEC consecutive columns for its whole life (grid = nvec * rp threads), so its labels are fixed and its counts
+// live in registers; 16-B loads for the scores and for the int64 targets.  L == 1 is a flat stream.
+// The value checks of the reference (targets in {0, 1} or ignore_index; label preds in {0, 1}) ride along as
+// device flags (deferred validation, utilities/validation.py).
+// =========================================================================================================
+template <typename T, int N> struct alignas(16) Pack16 { T v[N]; };
+
+struct BinCnt {
+  int valid = 0, pos = 0, rp = 0, rtp = 0, sp = 0, stp = 0;
+};
+
+template <typename T> struct BinTraits {
+  static constexpr bool kLabel = false;
+  using A = float;
+  __device__ static A val(T v) { return to_f32<T>(v); }
+  __device__ static A sig(A v) { return round_trip<T>(1.f / (1.f + expf(-v))); }
+  __device__ static A thr(double t) { return round_trip<T>((float)t); }
+};
+template <> struct BinTraits<double> {
+  static constexpr bool kLabel = false;
+  using A = double;
+  __device__ static A val(double v) { return v; }
+  __device__ static A sig(A v) { return 1.0 / (1.0 + exp(-v)); }
+  __device__ static A thr(double t) { return t; }
+};
+template <> struct BinTraits<int64_t> {
+  static constexpr bool kLabel = true;
+  using A = int64_t;
+  __device__ static A val(int64_t v) { return v; }
+  __device__ static A sig(A v) { return v; }
+  __device__ static A thr(double) { return 0; }
+};
+
+template <typename T>
+__device__ __forceinline__ void bin_count(BinCnt& c, T x, int64_t t, typename BinTraits<T>::A thr, int64_t ignore_index,
+                                          bool has_ignore, bool& oor, bool& bad_t, bool& bad_p) {
+  using Tr = BinTraits<T>;
+  const auto v = Tr::val(x);
+  const bool ign = has_ignore && t == ignore_index;
+  const bool tv = t == 0 || t == 1;
+  bad_t |= !ign && !tv;
+  const int valid = (!ign && tv) ? 1 : 0;
+  const int pos = valid & (t == 1 ? 1 : 0);
+  int p_raw, p_sig;
+  if constexpr (Tr::kLabel) {
+    bad_p |= v != 0 && v != 1;
+    p_raw = p_sig = v != 0;
+  } else {
+    oor |= !(v >= 0 && v <= 1);
+    p_raw = v > thr;
+    p_sig = Tr::sig(v) > thr;
+  }
+  c.valid += valid;
+  c.pos += pos;
+  c.rp += valid & p_raw;
+  c.rtp += pos & p_raw;
+  c.sp += valid & p_sig;
+  c.stp += pos & p_sig;
+}
+
+template <typename T, int VEC, bool UNIFORM>
+__global__ void __launch_bounds__(256) binary_stats_fused_kernel(
+    const T* __restrict__ preds, const int64_t* __restrict__ target, int64_t rows, int nvec, int64_t rp, int64_t tail_start,
+    int64_t total, int L, int64_t S, double threshold, int64_t ignore_index, bool has_ignore, int64_t* __restrict__ tp,
+    int64_t* __restrict__ fp, int64_t* __restrict__ tn, int64_t* __restrict__ fn, unsigned long long* __restrict__ scratch,
+    bool use_lds, int* err_t, int* err_p) {
+  extern __shared__ __attribute__((aligned(16))) int s_bin[];  // [L][6] when use_lds
+  __shared__ int s_oor;
+  using Tr = BinTraits<T>;
+  const auto thr = Tr::thr(threshold);
+  if (use_lds)
+    for (int b = threadIdx.x; b < 6 * L; b += blockDim.x) s_bin[b] = 0;
+  if (threadIdx.x == 0) s_oor = 0;
+  __syncthreads();
+
+  constexpr int NC = UNIFORM ? 1 : VEC;
+  BinCnt cnt[NC];
+  bool oor = false, bad_t = false, bad_p = false;
+  const int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int cv = (int)(g % nvec);
+  if (g < (int64_t)nvec * rp) {
+    using PP = Pack16<T, VEC>;
+    using TP = Pack16<int64_t, VEC>;
+    auto process = [&](const PP& p, const TP& t) {
+#pragma unroll
+      for (int k = 0; k < VEC; ++k)
+        bin_count<T>(cnt[UNIFORM ? 0 : k], p.v[k], t.v[k], thr, ignore_index, has_ignore, oor, bad_t, bad_p);
+    };
+    int64_t r = g / nvec;
+    for (; r + rp < rows; r += 2 * rp) {
+      const int64_t e0 = (r * nvec + cv) * VEC, e1 = ((r + rp) * nvec + cv) * VEC;
+      const PP p0 = *reinterpret_cast<const PP*>(preds + e0);
+      const PP p1 = *reinterpret_cast<const PP*>(preds + e1);
+      const TP t0 = *reinterpret_cast<const TP*>(target + e0);
+      const TP t1 = *reinterpret_cast<const TP*>(target + e1);
+      process(p0, t0);
+      process(p1, t1);
+    }
+    if (r < rows) {
+      const int64_t e0 = (r * nvec + cv) * VEC;
+      process(*reinterpret_cast<const PP*>(preds + e0), *reinterpret_cast<const TP*>(target + e0));
+    }
+  }
+  // flat-stream tail (L == 1, total not a multiple of VEC)
+  if (blockIdx.x == 0 && tail_start + threadIdx.x < total) {
+    const int64_t e = tail_start + threadIdx.x;
+    bin_count<T>(cnt[0], preds[e], target[e], thr, ignore_index, has_ignore, oor, bad_t, bad_p);
+  }
+  if (bad_t && err_t) atomicOr(err_t, 1);
+  if (bad_p && err_p) atomicOr(err_p, 1);
+  if (__ballot(oor) && (threadIdx.x & (kWave - 1)) == 0) s_oor = 1;
+
+  // workgroup reduction.  L == 1: six wave sums -> LDS -> grid_sum_last (no table).  L > 1: per-label table
+  // scratch[L][6] (LDS-privatised when it fits), grid_sum_last only carries the out-of-range count.
+  __shared__ int s_one[6];
+  __shared__ long long s_last[7];
+  auto put = [&](int lab, const BinCnt& c) {
+    const int v[6] = {c.valid, c.pos, c.rp, c.rtp, c.sp, c.stp};
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      if (!v[j]) continue;
+      if (use_lds) atomicAdd(&s_bin[lab * 6 + j], v[j]);
+      else atomicAdd(&scratch[lab * 6 + j], (unsigned long long)v[j]);
+    }
+  };
+  const bool single = UNIFORM && L == 1;
+  if (threadIdx.x < 6) s_one[threadIdx.x] = 0;
+  __syncthreads();
+  if (single) {
+    const int w[6] = {(int)wave_sum((long long)cnt[0].valid), (int)wave_sum((long long)cnt[0].pos),
+                      (int)wave_sum((long long)cnt[0].rp),    (int)wave_sum((long long)cnt[0].rtp),
+                      (int)wave_sum((long long)cnt[0].sp),    (int)wave_sum((long long)cnt[0].stp)};
+    if ((threadIdx.x & (kWave - 1)) == 0)
+#pragma unroll
+      for (int j = 0; j < 6; ++j)
+        if (w[j]) atomicAdd(&s_one[j], w[j]);
+  } else if (g < (int64_t)nvec * rp) {
+#pragma unroll
+    for (int k = 0; k < NC; ++k) {
+      const int64_t col = (int64_t)cv * VEC + k;
+      put((int)(col / S), cnt[k]);
+    }
+  }
+  __syncthreads();
+  if (!single && use_lds)
+    for (int b = threadIdx.x; b < 6 * L; b += blockDim.x)
+      if (s_bin[b]) atomicAdd(&scratch[b], (unsigned long long)s_bin[b]);
+  __builtin_amdgcn_s_waitcnt(0);  // every thread's table atomics are performed before the workgroup's ticket
+  __syncthreads();
+  unsigned long long* slots = scratch + (single ? 0 : 6 * (int64_t)L);
+  if (threadIdx.x == 0) {
+    s_last[6] = -1;
+    if (single) {
+      const long long mine[7] = {s_one[0], s_one[1], s_one[2], s_one[3], s_one[4], s_one[5], s_oor};
+      long long tot[7];
+      if (grid_sum_last<7>(slots, mine, tot)) {
+#pragma unroll
+        for (int j = 0; j < 7; ++j) s_last[j] = tot[j];
+      }
+    } else {
+      // this workgroup's table atomics are performed before its ticket (grid_sum_last waits vmcnt(0) first)
+      const long long mine[1] = {s_oor};
+      long long tot[1];
+      if (grid_sum_last<1>(slots, mine, tot)) s_last[6] = tot[0];
+    }
+  }
+  __syncthreads();
+  if (s_last[6] < 0) return;
+  const bool sig = s_last[6] > 0;
+  for (int l = threadIdx.x; l < L; l += blockDim.x) {
+    long long v[6];
+#pragma unroll
+    for (int j = 0; j < 6; ++j) v[j] = single ? s_last[j] : (long long)atomicExch(&scratch[l * 6 + j], 0ull);
+    const long long ptp = sig ? v[5] : v[3], pp1 = sig ? v[4] : v[2];
+    const long long d_fp = pp1 - ptp, d_fn = v[1] - ptp, d_tn = v[0] - v[1] - d_fp;
+    if (ptp) atomic_add_i64(tp + l, ptp);
+    if (d_fp) atomic_add_i64(fp + l, d_fp);
+    if (d_tn) atomic_add_i64(tn + l, d_tn);
+    if (d_fn) atomic_add_i64(fn + l, d_fn);
+  }
+}
+
+template <typename T>
+void launch_binary_fused(const T* p, const int64_t* t, int64_t total, int64_t N, int L, int64_t S, double threshold,
+                         int64_t ignore_index, bool has_ignore, int64_t* tp, int64_t* fp, int64_t* tn, int64_t* fn,
+                         unsigned long long* scratch, int* err_t, int* err_p) {
+  constexpr int VEC = 16 / sizeof(T);
+  const bool aligned = ((reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(t)) & 15) == 0;
+  const int64_t W = (int64_t)L * S;
+  const int block = 256;
+  const bool use_lds = 6 * (int64_t)L * 4 <= 48 * 1024;
+  const size_t shm = use_lds ? 6 * (size_t)L * sizeof(int) : 0;
+  const int64_t want = 256 * 1024;  // resident threads to aim for (256 CUs x 1024)
+  auto go = [&](auto vec_c, auto uni_c, int64_t rows, int64_t nvec, int64_t tail_start) {
+    constexpr int V = decltype(vec_c)::value;
+    constexpr bool U = decltype(uni_c)::value;
+    TORCH_CHECK(nvec <= INT32_MAX, "too many columns");
+    int64_t rp = std::max<int64_t>(1, std::min<int64_t>(rows, want / nvec));
+    const int64_t threads = std::max<int64_t>(nvec * rp, 1);
+    const int grid = (int)std::max<int64_t>(1, (threads + block - 1) / block);
+    hipLaunchKernelGGL((binary_stats_fused_kernel<T, V, U>), grid, block, shm, stream(), p, t, rows, (int)nvec, rp, tail_start,
+                       total, L, S, threshold, ignore_index, has_ignore, tp, fp, tn, fn, scratch, use_lds, err_t, err_p);
+  };
+  using I1 = std::integral_constant<int, 1>;
+  using IV = std::integral_constant<int, VEC>;
+  using BT = std::true_type;
+  using BF = std::false_type;
+  if (L == 1) {
+    if (aligned) go(IV{}, BT{}, total / VEC, 1, (total / VEC) * VEC);
+    else go(I1{}, BT{}, total, 1, total);
+  } else if (aligned && W % VEC == 0) {
+    if (S % VEC == 0) go(IV{}, BT{}, N, W / VEC, total);
+    else go(IV{}, BF{}, N, W / VEC, total);
+  } else {
+    go(I1{}, BF{}, N, W, total);
+  }
+}
+
+// tp / fp / tn / fn: int64 [L] states updated in place; scratch: int64 [6 L + kGridSlotsWords] zeros owned by the
+// caller (left at zero by every launch).  preds [N, L, ...] float scores/probabilities or integer labels, target same shape.
+void binary_stats_fused(const at::Tensor& preds_, const at::Tensor& target_, at::Tensor& tp, at::Tensor& fp, at::Tensor& tn,
+                        at::Tensor& fn, at::Tensor& scratch, int64_t num_labels, double threshold, int64_t ignore_index,
+                        bool has_ignore, const c10::optional<at::Tensor>& err_t, const c10::optional<at::Tensor>& err_p) {
+  const int L = static_cast<int>(num_labels);
+  for (const at::Tensor* s : {&tp, &fp, &tn, &fn})
+    TORCH_CHECK(s->is_contiguous() && s->scalar_type() == at::kLong && s->numel() == L, "stat states must be int64 [", L, "]");
+  TORCH_CHECK(scratch.is_contiguous() && scratch.scalar_type() == at::kLong &&
+                  scratch.numel() >= 6 * (int64_t)L + kGridSlotsWords,
+              "scratch must be a zeroed int64 [6 L + ", kGridSlotsWords, "]");
+  auto target = target_.contiguous().to(at::kLong);
+  const int64_t total = target.numel();
+  if (total == 0) return;
+  TORCH_CHECK(preds_.numel() == total, "preds/target size mismatch");
+  const int64_t N = target.size(0);
+  const int64_t S = total / (N * L);
+  TORCH_CHECK(N * L * S == total, "target shape incompatible with num_labels");
+  auto* sc = reinterpret_cast<unsigned long long*>(scratch.data_ptr<int64_t>());
+  int* et = flag_ptr(err_t);
+  int* ep = flag_ptr(err_p);
+  if (preds_.is_floating_point()) {
+    auto preds = preds_.contiguous();
+    TMX_DISPATCH_FLOAT(preds.scalar_type(), "binary_stats_fused", [&] {
+      launch_binary_fused<scalar_t>(reinterpret_cast<const scalar_t*>(preds.data_ptr()), target.data_ptr<int64_t>(), total, N, L,
+                                    S, threshold, ignore_index, has_ignore, tp.data_ptr<int64_t>(), fp.data_ptr<int64_t>(),
+                                    tn.data_ptr<int64_t>(), fn.data_ptr<int64_t>(), sc, et, ep);
+    });
+  } else {
+    auto preds = preds_.contiguous().to(at::kLong);
+    launch_binary_fused<int64_t>(preds.data_ptr<int64_t>(), target.data_ptr<int64_t>(), total, N, L, S, threshold,
+                                 ignore_index, has_ignore, tp.data_ptr<int64_t>(), fp.data_ptr<int64_t>(), tn.data_ptr<int64_t>(),
+                                 fn.data_ptr<int64_t>(), sc, et, ep);
   }
   TMX_LAUNCH_CHECK();
 }
@@ -1141,7 +1681,9 @@ void mc_calibration_update(const at::Tensor& preds_, const at::Tensor& target_, 
 TORCH_LIBRARY_FRAGMENT(tmx, m) {
   m.def("range_flag(Tensor x) -> Tensor");
   m.def("bincount(Tensor x, int minlength) -> Tensor");
-  m.def("mc_confmat_update(Tensor preds, Tensor target, Tensor(a!) confmat, int ignore_index, bool has_ignore) -> ()");
+  m.def("mc_confmat_update(Tensor preds, Tensor target, Tensor(a!) confmat, int ignore_index, bool has_ignore, Tensor(b!)? err_t=None, Tensor(c!)? err_p=None) -> ()");
+  m.def("mc_stat_scores_update(Tensor preds, Tensor target, int num_classes, Tensor(a!) tp, Tensor(b!) fp, Tensor(c!) tn, Tensor(d!) fn, Tensor(e!) ticket, int ignore_index, bool has_ignore, bool micro, Tensor(f!)? err_t=None, Tensor(g!)? err_p=None) -> ()");
+  m.def("binary_stats_fused(Tensor preds, Tensor target, Tensor(a!) tp, Tensor(b!) fp, Tensor(c!) tn, Tensor(d!) fn, Tensor(e!) scratch, int num_labels, float threshold, int ignore_index, bool has_ignore, Tensor(f!)? err_t=None, Tensor(g!)? err_p=None) -> ()");
   m.def("binary_stats_update(Tensor preds, Tensor target, Tensor(a!) counts, int num_labels, float threshold, int ignore_index, bool has_ignore) -> ()");
   m.def("curve_hist_update(Tensor preds, Tensor target, Tensor(a!) hist, int task, int ignore_index, bool has_ignore, Tensor(b!)? confmat, Tensor? norm_flag, Tensor(c!)? err_flag, Tensor(d!)? mode_state) -> ()");
   m.def("curve_hist_reduce(Tensor hist) -> Tensor");
@@ -1154,7 +1696,9 @@ TORCH_LIBRARY_IMPL(tmx, CUDA, m) {
   m.impl("range_flag", &tmx::range_flag);
   m.impl("bincount", &tmx::bincount);
   m.impl("mc_confmat_update", &tmx::mc_confmat_update);
+  m.impl("mc_stat_scores_update", &tmx::mc_stat_scores_update);
   m.impl("binary_stats_update", &tmx::binary_stats_update);
+  m.impl("binary_stats_fused", &tmx::binary_stats_fused);
   m.impl("curve_hist_update", &tmx::curve_hist_update);
   m.impl("curve_hist_reduce", &tmx::curve_hist_reduce);
   m.impl("binned_curve_update", &tmx::binned_curve_update);

@@ -296,3 +296,177 @@ def test_mc_confmat_vectorised(C, dtype):
     target[::11] = 3
     g, c, _, _ = _both(K.mc_confmat_update, x.to(dtype), target, torch.zeros(C, C, dtype=torch.long), 3)
     assert torch.equal(g[2].cpu(), c[2])
+
+
+def _stat_oracle(preds, target, C, ignore_index, micro):
+    cm = torch.zeros(C, C, dtype=torch.long)
+    K.mc_confmat_update(preds.cpu(), target.cpu(), cm, ignore_index)
+    tp = cm.diag()
+    fp, fn = cm.sum(0) - tp, cm.sum(1) - tp
+    tn = cm.sum() - (tp + fp + fn)
+    out = [tp, fp, tn, fn]
+    return [o.sum().reshape(1) for o in out] if micro else out
+
+
+@pytest.mark.parametrize(
+    ("C", "dtype"),
+    [(3, torch.float32), (10, torch.bfloat16), (40, torch.bfloat16), (64, torch.float16), (100, torch.float32),
+     (1000, torch.bfloat16), (1001, torch.bfloat16), (1024, torch.float64), (6000, torch.float32)],
+)
+@pytest.mark.parametrize("micro", [False, True])
+@pytest.mark.parametrize("ignore_index", [None, 1, -100])
+def test_mc_stat_scores_fused(C, dtype, micro, ignore_index):
+    """Fused arg-max -> tp/fp/tn/fn into the states (LDS-privatised, global-atomic and micro tiers; ticket word
+    returns to zero so consecutive updates accumulate)."""
+    torch.manual_seed(C)
+    size = 1 if micro else C
+    states = [torch.zeros(size, dtype=torch.long, device="cuda") for _ in range(4)]
+    ticket = torch.zeros(K.GRID_SLOTS, dtype=torch.long, device="cuda")
+    expect = [torch.zeros(size, dtype=torch.long) for _ in range(4)]
+    for N in (1, 777, 20000):
+        x = torch.randn(N, C).to(dtype)
+        t = torch.randint(0, C, (N,))
+        if ignore_index is not None:
+            t[::7] = ignore_index
+        K.mc_stat_scores_update(x.cuda(), t.cuda(), C, *states, ticket, ignore_index, micro)
+        for e, o in zip(expect, _stat_oracle(x, t, C, ignore_index, micro)):
+            e += o
+        torch.cuda.synchronize()
+        assert int(ticket.abs().sum().item()) == 0
+        for s, e in zip(states, expect):
+            assert torch.equal(s.cpu(), e)
+
+
+@pytest.mark.parametrize("C", [5, 300])
+def test_mc_stat_scores_labels_and_flags(C):
+    """Integer predictions, and the deferred range flags (bad target / bad pred) raised at compute."""
+    N = 5000
+    p = torch.randint(0, C, (N,))
+    t = torch.randint(0, C, (N,))
+    states = [torch.zeros(C, dtype=torch.long, device="cuda") for _ in range(4)]
+    ticket = torch.zeros(K.GRID_SLOTS, dtype=torch.long, device="cuda")
+    et = torch.zeros(1, dtype=torch.int32, device="cuda")
+    ep = torch.zeros(1, dtype=torch.int32, device="cuda")
+    K.mc_stat_scores_update(p.cuda(), t.cuda(), C, *states, ticket, None, False, et, ep)
+    for s, e in zip(states, _stat_oracle(p, t, C, None, False)):
+        assert torch.equal(s.cpu(), e)
+    assert int(et.item()) == 0 and int(ep.item()) == 0
+    t[17] = C
+    p[33] = -1
+    K.mc_stat_scores_update(p.cuda(), t.cuda(), C, *states, ticket, None, False, et, ep)
+    assert int(et.item()) == 1 and int(ep.item()) == 1
+
+
+def test_multiclass_modules_fused_path():
+    """Accuracy / F1 / ConfusionMatrix modules on the fused path agree with the CPU path over several updates, and
+    an out-of-range target raises at compute (deferred validation)."""
+    from torchmetrics_forked_amd.classification import MulticlassAccuracy, MulticlassConfusionMatrix, MulticlassF1Score
+
+    C = 37
+    for cls, kw in ((MulticlassAccuracy, {"average": "macro"}), (MulticlassAccuracy, {"average": "micro"}),
+                    (MulticlassF1Score, {"average": "weighted", "ignore_index": 2}), (MulticlassConfusionMatrix, {})):
+        mg, mc = cls(num_classes=C, **kw).cuda(), cls(num_classes=C, **kw)
+        for _ in range(3):
+            x = torch.randn(4000, C)
+            t = torch.randint(0, C, (4000,))
+            mg.update(x.cuda(), t.cuda())
+            mc.update(x, t)
+        torch.testing.assert_close(mg.compute().cpu(), mc.compute())
+        bad = cls(num_classes=C, **kw).cuda()
+        t = torch.randint(0, C, (100,))
+        t[5] = C + 3
+        bad.update(torch.randn(100, C).cuda(), t.cuda())
+        with pytest.raises(RuntimeError, match="unique values in `target`"):
+            bad.compute()
+
+
+def _bin_case(shape, dtype, logits, ignore_index, seed):
+    g = torch.Generator().manual_seed(seed)
+    if dtype == torch.int64:
+        p = torch.randint(0, 2, shape, generator=g)
+    else:
+        p = (torch.randn(shape, generator=g) * 3 if logits else torch.rand(shape, generator=g)).to(dtype)
+    t = torch.randint(0, 2, shape, generator=g)
+    if ignore_index is not None:
+        t.view(-1)[::5] = ignore_index
+    return p, t
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16, torch.float64, torch.int64])
+@pytest.mark.parametrize(
+    ("shape", "L"),
+    [((1,), 1), ((7,), 1), ((1001,), 1), ((1 << 20) + 3, 1),
+     ((333, 3), 3), ((4096, 8), 8), ((2048, 1000), 1000), ((100, 5, 4), 5), ((64, 6, 16), 6), ((50, 3000), 3000)],
+)
+@pytest.mark.parametrize("logits", [False, True])
+@pytest.mark.parametrize("ignore_index", [None, -1])
+def test_binary_stats_fused(dtype, shape, L, logits, ignore_index):
+    """One-launch binary / multilabel stats (raw and sigmoid counts, last workgroup picks) vs the eager path, over
+    three updates so the scratch / ticket reset is exercised."""
+    if isinstance(shape, int):
+        shape = (shape,)
+    states = tuple(torch.zeros(L, dtype=torch.long, device="cuda") for _ in range(4))
+    scratch = torch.zeros(6 * L + K.GRID_SLOTS, dtype=torch.long, device="cuda")
+    expect = torch.zeros(L, 4, dtype=torch.long)
+    for seed in range(3):
+        p, t = _bin_case(shape, dtype, logits and seed != 1, ignore_index, seed)
+        K.binary_stats_fused(p.cuda(), t.cuda(), states, scratch, L, 0.3, ignore_index)
+        K.binary_stats_update(p, t, expect, L, 0.3, ignore_index)
+        torch.cuda.synchronize()
+        assert int(scratch.abs().sum().item()) == 0
+        got = torch.stack([s.cpu() for s in states], dim=1)
+        assert torch.equal(got, expect), (got - expect).abs().max()
+
+
+def test_binary_stats_fused_misaligned_and_flags():
+    L = 8
+    p = torch.rand(4097, L)
+    t = torch.randint(0, 2, (4097, L))
+    pg, tg = p.cuda()[1:], t.cuda()[1:]  # 32-B offset rows: still 16-B aligned; then a 4-B offset view
+    states = tuple(torch.zeros(L, dtype=torch.long, device="cuda") for _ in range(4))
+    scratch = torch.zeros(6 * L + K.GRID_SLOTS, dtype=torch.long, device="cuda")
+    K.binary_stats_fused(pg, tg, states, scratch, L, 0.5, None)
+    expect = torch.zeros(L, 4, dtype=torch.long)
+    K.binary_stats_update(p[1:], t[1:], expect, L, 0.5, None)
+    flat_p, flat_t = p.reshape(-1)[1:4097 * L - 7], t.reshape(-1)[1:4097 * L - 7]
+    s1 = tuple(torch.zeros(1, dtype=torch.long, device="cuda") for _ in range(4))
+    sc1 = torch.zeros(6 + K.GRID_SLOTS, dtype=torch.long, device="cuda")
+    K.binary_stats_fused(flat_p.cuda(), flat_t.cuda(), s1, sc1, 1, 0.5, None)
+    e1 = torch.zeros(1, 4, dtype=torch.long)
+    K.binary_stats_update(flat_p, flat_t, e1, 1, 0.5, None)
+    torch.cuda.synchronize()
+    assert torch.equal(torch.stack([s.cpu() for s in states], 1), expect)
+    assert torch.equal(torch.stack([s.cpu() for s in s1], 1), e1)
+    et = torch.zeros(1, dtype=torch.int32, device="cuda")
+    ep = torch.zeros(1, dtype=torch.int32, device="cuda")
+    lp = torch.randint(0, 2, (1000,))
+    lt = torch.randint(0, 2, (1000,))
+    K.binary_stats_fused(lp.cuda(), lt.cuda(), s1, sc1, 1, 0.5, -1, et, ep)
+    assert int(et.item()) == 0 and int(ep.item()) == 0
+    lt[10] = -1  # ignored: fine
+    K.binary_stats_fused(lp.cuda(), lt.cuda(), s1, sc1, 1, 0.5, -1, et, ep)
+    assert int(et.item()) == 0
+    lt[11] = 2
+    lp[12] = 3
+    K.binary_stats_fused(lp.cuda(), lt.cuda(), s1, sc1, 1, 0.5, -1, et, ep)
+    assert int(et.item()) == 1 and int(ep.item()) == 1
+
+
+def test_binary_multilabel_modules_fused_path():
+    from torchmetrics_forked_amd.classification import BinaryAccuracy, BinaryF1Score, MultilabelF1Score, MultilabelPrecision
+
+    for mk, shape in ((lambda: BinaryAccuracy(), (5000,)), (lambda: BinaryF1Score(ignore_index=-1), (5000,)),
+                      (lambda: MultilabelF1Score(num_labels=12), (3000, 12)),
+                      (lambda: MultilabelPrecision(num_labels=12, average="micro"), (3000, 12))):
+        mg, mc = mk().cuda(), mk()
+        for seed in range(3):
+            p, t = _bin_case(shape, torch.float32, seed == 2, None, seed)
+            mg.update(p.cuda(), t.cuda())
+            mc.update(p, t)
+        torch.testing.assert_close(mg.compute().cpu(), mc.compute())
+        bad = mk().cuda()
+        p, t = _bin_case(shape, torch.float32, False, None, 0)
+        t.view(-1)[3] = 7
+        bad.update(p.cuda(), t.cuda())
+        with pytest.raises(RuntimeError, match="`target`"):
+            bad.compute()

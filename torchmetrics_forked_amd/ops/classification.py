@@ -4,7 +4,7 @@ Each function dispatches to ``torch.ops.tmx.*`` for GPU tensors (native library 
 eager PyTorch implementation for CPU tensors.  The eager implementations follow the reference semantics
 operation-by-operation and double as the numerics oracle in ``tests/test_ops_gpu.py``.
 """
-from typing import Optional
+from typing import Optional, Tuple
 
 import torch
 from torch import Tensor
@@ -12,6 +12,7 @@ from torch import Tensor
 from torchmetrics_forked_amd import ops
 
 N_CODES = 1 << 14
+GRID_SLOTS = 9 * 16  # zeroed int64 scratch words of the fused kernels' grid reduction (csrc kGridSlotsWords)
 
 
 def range_flag(x: Tensor) -> Tensor:
@@ -21,11 +22,23 @@ def range_flag(x: Tensor) -> Tensor:
     return (~((x >= 0) & (x <= 1))).any().reshape(1).int()
 
 
-def mc_confmat_update(preds: Tensor, target: Tensor, confmat: Tensor, ignore_index: Optional[int]) -> None:
-    """``confmat[t, p] += 1`` for every (target, argmax/label pred) pair; rows with ``t == ignore_index`` skipped."""
+def mc_confmat_update(
+    preds: Tensor,
+    target: Tensor,
+    confmat: Tensor,
+    ignore_index: Optional[int],
+    err_t: Optional[Tensor] = None,
+    err_p: Optional[Tensor] = None,
+) -> None:
+    """``confmat[t, p] += 1`` for every (target, argmax/label pred) pair; rows with ``t == ignore_index`` skipped.
+
+    ``err_t`` / ``err_p`` (int32[1] device flags, GPU only) are OR-ed with 1 when a target outside ``[0, C)`` that
+    is not the ignore index, or an integer prediction outside ``[0, C)``, is seen (deferred validation)."""
     C = confmat.shape[0]
     if ops.use_native(target):
-        torch.ops.tmx.mc_confmat_update(preds, target, confmat, -1 if ignore_index is None else ignore_index, ignore_index is not None)
+        torch.ops.tmx.mc_confmat_update(
+            preds, target, confmat, -1 if ignore_index is None else ignore_index, ignore_index is not None, err_t, err_p
+        )
         return
     p = preds.argmax(dim=1) if preds.is_floating_point() else preds
     p, t = p.reshape(-1).long(), target.reshape(-1).long()
@@ -34,6 +47,67 @@ def mc_confmat_update(preds: Tensor, target: Tensor, confmat: Tensor, ignore_ind
         keep &= t != ignore_index
     idx = (t * C + p)[keep]
     confmat += torch.bincount(idx, minlength=C * C).reshape(C, C)
+
+
+def mc_stat_scores_update(
+    preds: Tensor,
+    target: Tensor,
+    num_classes: int,
+    tp: Tensor,
+    fp: Tensor,
+    tn: Tensor,
+    fn: Tensor,
+    ticket: Tensor,
+    ignore_index: Optional[int],
+    micro: bool,
+    err_t: Optional[Tensor] = None,
+    err_p: Optional[Tensor] = None,
+) -> None:
+    """Accumulate multiclass tp / fp / tn / fn (int64 ``[C]``, or ``[1]``/0-dim with ``micro``) in place.
+
+    Same pair semantics as :func:`mc_confmat_update` (a row counts once: tp of its class, or fp of the predicted
+    class + fn of the true one; tn = valid rows - tp - fp - fn per class).  ``ticket`` is an int64 ``[GRID_SLOTS]`` zero
+    scratch the GPU kernel uses for its grid reduction; it is left at zero."""
+    if ops.use_native(target):
+        torch.ops.tmx.mc_stat_scores_update(
+            preds, target, num_classes, tp, fp, tn, fn, ticket,
+            -1 if ignore_index is None else ignore_index, ignore_index is not None, micro, err_t, err_p,
+        )
+        return
+    confmat = torch.zeros(num_classes, num_classes, dtype=torch.long, device=target.device)
+    mc_confmat_update(preds, target, confmat, ignore_index)
+    d_tp = confmat.diag()
+    d_fp = confmat.sum(0) - d_tp
+    d_fn = confmat.sum(1) - d_tp
+    d_tn = confmat.sum() - (d_tp + d_fp + d_fn)
+    for state, delta in ((tp, d_tp), (fp, d_fp), (tn, d_tn), (fn, d_fn)):
+        state += delta.sum().reshape(state.shape) if micro else delta
+
+
+def binary_stats_fused(
+    preds: Tensor,
+    target: Tensor,
+    states: Tuple[Tensor, Tensor, Tensor, Tensor],
+    scratch: Tensor,
+    num_labels: int,
+    threshold: float,
+    ignore_index: Optional[int],
+    err_t: Optional[Tensor] = None,
+    err_p: Optional[Tensor] = None,
+) -> None:
+    """Accumulate per-label (tp, fp, tn, fn) into ``states`` (int64 ``[L]`` each) in place, sigmoid-if-needed rule
+    included.  ``scratch`` is an int64 ``[6 L + GRID_SLOTS]`` zero buffer (left at zero); ``err_t`` / ``err_p`` are the
+    deferred-validation flags for targets outside {0, 1, ignore_index} and label preds outside {0, 1}."""
+    if ops.use_native(target):
+        torch.ops.tmx.binary_stats_fused(
+            preds, target, *states, scratch, num_labels, float(threshold),
+            -1 if ignore_index is None else ignore_index, ignore_index is not None, err_t, err_p,
+        )
+        return
+    counts = torch.zeros(num_labels, 4, dtype=torch.long, device=target.device)
+    binary_stats_update(preds, target, counts, num_labels, threshold, ignore_index)
+    for k, state in enumerate(states):
+        state += counts[:, k].reshape(state.shape)
 
 
 def binary_stats_update(
