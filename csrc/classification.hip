@@ -503,6 +503,80 @@ __global__ void __launch_bounds__(512) mc_pairs_argmax_vec_kernel(const T* __res
   acc.flush(s_pairs);
 }
 
+// Small C (<= 128, any alignment of C): a workgroup streams a contiguous tile of 256 / G rows (tile * C * size
+// bytes, a multiple of 16) into LDS with coalesced 16-B loads, then a group of G lanes (C / G <= 16 elements each)
+// reduces one row's arg-max from LDS.  Replaces one-thread-per-row scalar loads (20-B stride at C = 10: every load
+// instruction touched ten cache lines) and the vector kernel's idle lanes at C = 64 (8 of 64 lanes per row).
+template <typename T>
+__device__ __forceinline__ void group_argmax(float& v, int& idx, int G) {
+  for (int off = 1; off < G; off <<= 1) {
+    const float ov = __shfl_xor(v, off, kWave);
+    const int oi = __shfl_xor(idx, off, kWave);
+    const bool o_nan = ov != ov, s_nan = v != v;
+    const bool take = (o_nan && !s_nan) || (o_nan == s_nan && (o_nan ? oi < idx : (ov > v || (ov == v && oi < idx))));
+    if (take) { v = ov; idx = oi; }
+  }
+}
+
+template <typename T, class Acc>
+__global__ void __launch_bounds__(1024) mc_pairs_argmax_staged_kernel(const T* __restrict__ preds, const int64_t* __restrict__ target,
+                                                                     int64_t n, int C, int glog, int acc_words, int64_t ignore_index,
+                                                                     bool has_ignore, Acc acc, int* err_t) {
+  extern __shared__ __attribute__((aligned(16))) int s_pairs[];
+  acc.init(s_pairs);
+  T* s_tile = reinterpret_cast<T*>(s_pairs + acc_words);
+  PairChecks chk;
+  const int G = 1 << glog;
+  const int tile_rows = blockDim.x >> glog;
+  const int grp = threadIdx.x >> glog, gl = threadIdx.x & (G - 1);
+  const int64_t total_bytes = n * C * (int64_t)sizeof(T);
+  const int nchunks = tile_rows * C * (int)sizeof(T) / 16;
+  const char* base = reinterpret_cast<const char*>(preds);
+  const int64_t ntiles = (n + tile_rows - 1) / tile_rows;
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int64_t r0 = tile * tile_rows;
+    const int64_t r = r0 + grp;
+    const int64_t t = (gl == 0 && r < n) ? target[r] : 0;
+    const int64_t off0 = r0 * C * (int64_t)sizeof(T);
+    for (int q = threadIdx.x; q < nchunks; q += blockDim.x) {
+      const int64_t off = off0 + 16 * (int64_t)q;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (off + 16 <= total_bytes) {
+        v = *reinterpret_cast<const uint4*>(base + off);
+      } else if (off < total_bytes) {
+        // last partial chunk: 16-bit pieces (element sizes are >= 2 B), constant indices so v stays in registers
+        const int rem = (int)(total_bytes - off);
+        uint32_t d[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          uint32_t x = 0;
+#pragma unroll
+          for (int h = 0; h < 2; ++h)
+            if (4 * j + 2 * h < rem) x |= (uint32_t)*reinterpret_cast<const uint16_t*>(base + off + 4 * j + 2 * h) << (16 * h);
+          d[j] = x;
+        }
+        v = make_uint4(d[0], d[1], d[2], d[3]);
+      }
+      reinterpret_cast<uint4*>(s_tile)[q] = v;
+    }
+    __syncthreads();
+    float best = -INFINITY;
+    int bi = C;
+    if (r < n) {
+      const T* row = s_tile + grp * C;
+      for (int c = gl; c < C; c += G) {
+        const float v = to_f32<T>(row[c]);
+        if (argmax_better(v, c, best, bi)) { best = v; bi = c; }
+      }
+    }
+    group_argmax<T>(best, bi, G);
+    if (gl == 0 && r < n && chk.keep(t, 0, C, ignore_index, has_ignore)) acc.add(s_pairs, (int)t, bi);
+    __syncthreads();
+  }
+  chk.report(err_t, nullptr);
+  acc.flush(s_pairs);
+}
+
 // Dispatch one pair stream.  preds: [N] int64 labels or [N, C] float scores (contiguous).
 template <class Acc>
 void launch_pairs(const at::Tensor& preds_, const at::Tensor& target, int64_t n, int C, int64_t ignore_index, bool has_ignore,
@@ -522,8 +596,19 @@ void launch_pairs(const at::Tensor& preds_, const at::Tensor& target, int64_t n,
     const scalar_t* p = reinterpret_cast<const scalar_t*>(preds.data_ptr());
     const int64_t* t = target.data_ptr<int64_t>();
     constexpr int VEC = VecOf<scalar_t>::n;
-    const bool vec_ok = C % VEC == 0 && C > 32 && (reinterpret_cast<uintptr_t>(p) & 15) == 0;
-    if (vec_ok && C <= kWave * VEC) {
+    const bool aligned = (reinterpret_cast<uintptr_t>(p) & 15) == 0;
+    const bool vec_ok = C % VEC == 0 && C > 32 && aligned;
+    if (aligned && C <= 128) {
+      int glog = 0;
+      while ((C + (1 << glog) - 1) >> glog > 16) ++glog;
+      const int acc_words = (int)((shm + 15) / 16 * 4);
+      // big workgroups (tile <= 16 B x 2048 = 32 KB): 4x fewer per-workgroup flushes than 256 threads
+      const int threads = std::min(1024, 2048 / (int)sizeof(scalar_t));
+      const int tile_rows = threads >> glog;
+      const size_t shm_t = (size_t)acc_words * 4 + (size_t)tile_rows * C * sizeof(scalar_t);
+      hipLaunchKernelGGL((mc_pairs_argmax_staged_kernel<scalar_t, Acc>), grid_for(n, tile_rows, 2048), threads, shm_t, stream(), p,
+                         t, n, C, glog, acc_words, ignore_index, has_ignore, acc, err_t);
+    } else if (vec_ok && C <= kWave * VEC) {
       hipLaunchKernelGGL((mc_pairs_argmax_vec_kernel<scalar_t, 1, Acc>), grid_for(n * kWave / 4, 512, 2048), 512, shm,
                          stream(), p, t, n, C, ignore_index, has_ignore, acc, err_t);
     } else if (vec_ok && C <= 2 * kWave * VEC) {
@@ -700,6 +785,21 @@ template <typename T, int N> struct alignas(16) Pack16 { T v[N]; };
 
 struct BinCnt {
   int valid = 0, pos = 0, rp = 0, rtp = 0, sp = 0, stp = 0;
+  __device__ void add(int v, int p, int r, int rt, int sg, int st) {
+    valid += v; pos += p; rp += r; rtp += rt; sp += sg; stp += st;
+  }
+  __device__ void get(int (&o)[6]) const { o[0] = valid; o[1] = pos; o[2] = rp; o[3] = rtp; o[4] = sp; o[5] = stp; }
+};
+// Two 16-bit counts per register (a thread sees < 65536 rows, enforced on the host): the per-column counters of
+// the multilabel path are 3 VGPRs per column instead of 6.
+struct BinCnt16 {
+  uint32_t a = 0, b = 0, c = 0;
+  __device__ void add(int v, int p, int r, int rt, int sg, int st) {
+    a += (uint32_t)v | ((uint32_t)p << 16); b += (uint32_t)r | ((uint32_t)rt << 16); c += (uint32_t)sg | ((uint32_t)st << 16);
+  }
+  __device__ void get(int (&o)[6]) const {
+    o[0] = a & 0xFFFF; o[1] = a >> 16; o[2] = b & 0xFFFF; o[3] = b >> 16; o[4] = c & 0xFFFF; o[5] = c >> 16;
+  }
 };
 
 template <typename T> struct BinTraits {
@@ -724,8 +824,8 @@ template <> struct BinTraits<int64_t> {
   __device__ static A thr(double) { return 0; }
 };
 
-template <typename T>
-__device__ __forceinline__ void bin_count(BinCnt& c, T x, int64_t t, typename BinTraits<T>::A thr, int64_t ignore_index,
+template <typename T, class Cnt>
+__device__ __forceinline__ void bin_count(Cnt& c, T x, int64_t t, typename BinTraits<T>::A thr, int64_t ignore_index,
                                           bool has_ignore, bool& oor, bool& bad_t, bool& bad_p) {
   using Tr = BinTraits<T>;
   const auto v = Tr::val(x);
@@ -743,35 +843,42 @@ __device__ __forceinline__ void bin_count(BinCnt& c, T x, int64_t t, typename Bi
     p_raw = v > thr;
     p_sig = Tr::sig(v) > thr;
   }
-  c.valid += valid;
-  c.pos += pos;
-  c.rp += valid & p_raw;
-  c.rtp += pos & p_raw;
-  c.sp += valid & p_sig;
-  c.stp += pos & p_sig;
+  c.add(valid, pos, valid & p_raw, pos & p_raw, valid & p_sig, pos & p_sig);
 }
 
+// Thread mapping: workgroup b = (column group cg = b % cgroups, row group rg = b / cgroups); thread t owns column
+// vector cg * CVB + t % CVB and walks rows rg * RL + t / CVB, stepping rgroups * RL (RL = 256 / CVB).  Consecutive
+// threads read consecutive 16-B column vectors of a row.  The workgroup's labels are the contiguous range covering
+// its columns, so its LDS table and its flush are [nl][6] with nl <= CVB * VEC / S + 1, and a label's scratch row
+// receives one flush per row group.  L == 1 is the same mapping with one column vector (a flat stream).
 template <typename T, int VEC, bool UNIFORM>
 __global__ void __launch_bounds__(256) binary_stats_fused_kernel(
-    const T* __restrict__ preds, const int64_t* __restrict__ target, int64_t rows, int nvec, int64_t rp, int64_t tail_start,
-    int64_t total, int L, int64_t S, double threshold, int64_t ignore_index, bool has_ignore, int64_t* __restrict__ tp,
-    int64_t* __restrict__ fp, int64_t* __restrict__ tn, int64_t* __restrict__ fn, unsigned long long* __restrict__ scratch,
-    bool use_lds, int* err_t, int* err_p) {
-  extern __shared__ __attribute__((aligned(16))) int s_bin[];  // [L][6] when use_lds
+    const T* __restrict__ preds, const int64_t* __restrict__ target, int64_t rows, int nvec, int cvb, int cgroups,
+    int64_t rgroups, int64_t tail_start, int64_t total, int L, int64_t S, double threshold, int64_t ignore_index,
+    bool has_ignore, int64_t* __restrict__ tp, int64_t* __restrict__ fp, int64_t* __restrict__ tn, int64_t* __restrict__ fn,
+    unsigned long long* __restrict__ scratch, int* err_t, int* err_p) {
+  extern __shared__ __attribute__((aligned(16))) int s_bin[];  // [nl][6]
   __shared__ int s_oor;
   using Tr = BinTraits<T>;
   const auto thr = Tr::thr(threshold);
-  if (use_lds)
-    for (int b = threadIdx.x; b < 6 * L; b += blockDim.x) s_bin[b] = 0;
+  const int cg = (int)(blockIdx.x % cgroups);
+  const int64_t rg = blockIdx.x / cgroups;
+  const int RL = blockDim.x / cvb;
+  const int64_t col_lo = (int64_t)cg * cvb * VEC;
+  const int lab_lo = L == 1 ? 0 : (int)(col_lo / S);
+  const int lab_hi = L == 1 ? 0 : (int)min<int64_t>(L - 1, (std::min<int64_t>(col_lo + (int64_t)cvb * VEC, (int64_t)nvec * VEC) - 1) / S);
+  const int nl = lab_hi - lab_lo + 1;
+  for (int b = threadIdx.x; b < 6 * nl; b += blockDim.x) s_bin[b] = 0;
   if (threadIdx.x == 0) s_oor = 0;
   __syncthreads();
 
   constexpr int NC = UNIFORM ? 1 : VEC;
-  BinCnt cnt[NC];
+  using Cnt = std::conditional_t<UNIFORM, BinCnt, BinCnt16>;
+  Cnt cnt[NC];
   bool oor = false, bad_t = false, bad_p = false;
-  const int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  const int cv = (int)(g % nvec);
-  if (g < (int64_t)nvec * rp) {
+  const int cv = cg * cvb + (int)(threadIdx.x % cvb);
+  const bool col_ok = cv < nvec && (int)(threadIdx.x / cvb) < RL;
+  if (col_ok) {
     using PP = Pack16<T, VEC>;
     using TP = Pack16<int64_t, VEC>;
     auto process = [&](const PP& p, const TP& t) {
@@ -779,9 +886,10 @@ __global__ void __launch_bounds__(256) binary_stats_fused_kernel(
       for (int k = 0; k < VEC; ++k)
         bin_count<T>(cnt[UNIFORM ? 0 : k], p.v[k], t.v[k], thr, ignore_index, has_ignore, oor, bad_t, bad_p);
     };
-    int64_t r = g / nvec;
-    for (; r + rp < rows; r += 2 * rp) {
-      const int64_t e0 = (r * nvec + cv) * VEC, e1 = ((r + rp) * nvec + cv) * VEC;
+    const int64_t step = rgroups * RL;
+    int64_t r = rg * RL + threadIdx.x / cvb;
+    for (; r + step < rows; r += 2 * step) {
+      const int64_t e0 = (r * nvec + cv) * VEC, e1 = ((r + step) * nvec + cv) * VEC;
       const PP p0 = *reinterpret_cast<const PP*>(preds + e0);
       const PP p1 = *reinterpret_cast<const PP*>(preds + e1);
       const TP t0 = *reinterpret_cast<const TP*>(target + e0);
@@ -803,55 +911,48 @@ __global__ void __launch_bounds__(256) binary_stats_fused_kernel(
   if (bad_p && err_p) atomicOr(err_p, 1);
   if (__ballot(oor) && (threadIdx.x & (kWave - 1)) == 0) s_oor = 1;
 
-  // workgroup reduction.  L == 1: six wave sums -> LDS -> grid_sum_last (no table).  L > 1: per-label table
-  // scratch[L][6] (LDS-privatised when it fits), grid_sum_last only carries the out-of-range count.
-  __shared__ int s_one[6];
+  // workgroup reduction.  L == 1: six wave sums -> LDS -> grid_sum_last (no table).  L > 1: the workgroup's
+  // [nl][6] LDS table -> scratch[L][6]; grid_sum_last only carries the out-of-range count.
   __shared__ long long s_last[7];
-  auto put = [&](int lab, const BinCnt& c) {
-    const int v[6] = {c.valid, c.pos, c.rp, c.rtp, c.sp, c.stp};
-#pragma unroll
-    for (int j = 0; j < 6; ++j) {
-      if (!v[j]) continue;
-      if (use_lds) atomicAdd(&s_bin[lab * 6 + j], v[j]);
-      else atomicAdd(&scratch[lab * 6 + j], (unsigned long long)v[j]);
-    }
-  };
-  const bool single = UNIFORM && L == 1;
-  if (threadIdx.x < 6) s_one[threadIdx.x] = 0;
-  __syncthreads();
+  const bool single = L == 1;
   if (single) {
-    const int w[6] = {(int)wave_sum((long long)cnt[0].valid), (int)wave_sum((long long)cnt[0].pos),
-                      (int)wave_sum((long long)cnt[0].rp),    (int)wave_sum((long long)cnt[0].rtp),
-                      (int)wave_sum((long long)cnt[0].sp),    (int)wave_sum((long long)cnt[0].stp)};
+    int c6[6];
+    cnt[0].get(c6);
+    int w[6];
+#pragma unroll
+    for (int j = 0; j < 6; ++j) w[j] = (int)wave_sum((long long)c6[j]);
     if ((threadIdx.x & (kWave - 1)) == 0)
 #pragma unroll
       for (int j = 0; j < 6; ++j)
-        if (w[j]) atomicAdd(&s_one[j], w[j]);
-  } else if (g < (int64_t)nvec * rp) {
+        if (w[j]) atomicAdd(&s_bin[j], w[j]);
+  } else if (col_ok) {
 #pragma unroll
     for (int k = 0; k < NC; ++k) {
-      const int64_t col = (int64_t)cv * VEC + k;
-      put((int)(col / S), cnt[k]);
+      const int lab = (int)(((int64_t)cv * VEC + k) / S) - lab_lo;
+      int c6[6];
+      cnt[k].get(c6);
+#pragma unroll
+      for (int j = 0; j < 6; ++j)
+        if (c6[j]) atomicAdd(&s_bin[lab * 6 + j], c6[j]);
     }
   }
   __syncthreads();
-  if (!single && use_lds)
-    for (int b = threadIdx.x; b < 6 * L; b += blockDim.x)
-      if (s_bin[b]) atomicAdd(&scratch[b], (unsigned long long)s_bin[b]);
+  if (!single)
+    for (int b = threadIdx.x; b < 6 * nl; b += blockDim.x)
+      if (s_bin[b]) atomicAdd(&scratch[lab_lo * 6 + b], (unsigned long long)s_bin[b]);
   __builtin_amdgcn_s_waitcnt(0);  // every thread's table atomics are performed before the workgroup's ticket
   __syncthreads();
   unsigned long long* slots = scratch + (single ? 0 : 6 * (int64_t)L);
   if (threadIdx.x == 0) {
     s_last[6] = -1;
     if (single) {
-      const long long mine[7] = {s_one[0], s_one[1], s_one[2], s_one[3], s_one[4], s_one[5], s_oor};
+      const long long mine[7] = {s_bin[0], s_bin[1], s_bin[2], s_bin[3], s_bin[4], s_bin[5], s_oor};
       long long tot[7];
       if (grid_sum_last<7>(slots, mine, tot)) {
 #pragma unroll
         for (int j = 0; j < 7; ++j) s_last[j] = tot[j];
       }
     } else {
-      // this workgroup's table atomics are performed before its ticket (grid_sum_last waits vmcnt(0) first)
       const long long mine[1] = {s_oor};
       long long tot[1];
       if (grid_sum_last<1>(slots, mine, tot)) s_last[6] = tot[0];
@@ -881,18 +982,27 @@ void launch_binary_fused(const T* p, const int64_t* t, int64_t total, int64_t N,
   const bool aligned = ((reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(t)) & 15) == 0;
   const int64_t W = (int64_t)L * S;
   const int block = 256;
-  const bool use_lds = 6 * (int64_t)L * 4 <= 48 * 1024;
-  const size_t shm = use_lds ? 6 * (size_t)L * sizeof(int) : 0;
-  const int64_t want = 256 * 1024;  // resident threads to aim for (256 CUs x 1024)
   auto go = [&](auto vec_c, auto uni_c, int64_t rows, int64_t nvec, int64_t tail_start) {
     constexpr int V = decltype(vec_c)::value;
     constexpr bool U = decltype(uni_c)::value;
     TORCH_CHECK(nvec <= INT32_MAX, "too many columns");
-    int64_t rp = std::max<int64_t>(1, std::min<int64_t>(rows, want / nvec));
-    const int64_t threads = std::max<int64_t>(nvec * rp, 1);
-    const int grid = (int)std::max<int64_t>(1, (threads + block - 1) / block);
-    hipLaunchKernelGGL((binary_stats_fused_kernel<T, V, U>), grid, block, shm, stream(), p, t, rows, (int)nvec, rp, tail_start,
-                       total, L, S, threshold, ignore_index, has_ignore, tp, fp, tn, fn, scratch, use_lds, err_t, err_p);
+    const int cvb = (int)std::min<int64_t>(nvec, 16);
+    const int RL = block / cvb;
+    const int64_t cgroups = (nvec + cvb - 1) / cvb;
+    TORCH_CHECK(cgroups <= INT32_MAX, "too many column groups");
+    // ~1024 workgroups, >= 8 rows per thread when there are that many (fewer table flushes), and fewer than 65536
+    // rows per thread for the 16-bit packed counters
+    int64_t rgroups = std::max<int64_t>(1, std::min<int64_t>(std::max<int64_t>(1, 1024 / cgroups), rows / ((int64_t)RL * 8)));
+    if (L == 1) rgroups = std::max<int64_t>(1, std::min<int64_t>(1024, (rows + RL - 1) / RL));
+    rgroups = std::max<int64_t>(rgroups, (rows + (int64_t)RL * 32768 - 1) / ((int64_t)RL * 32768));
+    const int64_t grid = cgroups * rgroups;
+    TORCH_CHECK(grid <= INT32_MAX, "grid too large");
+    const int max_nl = L == 1 ? 1 : (int)std::min<int64_t>(L, (int64_t)cvb * V / S + 2);
+    const size_t shm = 6 * (size_t)max_nl * sizeof(int);
+    TORCH_CHECK(shm <= 64 * 1024, "label table too large");
+    hipLaunchKernelGGL((binary_stats_fused_kernel<T, V, U>), (int)grid, block, shm, stream(), p, t, rows, (int)nvec, cvb,
+                       (int)cgroups, rgroups, tail_start, total, L, S, threshold, ignore_index, has_ignore, tp, fp, tn, fn,
+                       scratch, err_t, err_p);
   };
   using I1 = std::integral_constant<int, 1>;
   using IV = std::integral_constant<int, VEC>;

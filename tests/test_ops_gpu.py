@@ -283,13 +283,15 @@ def test_binary_calibration_bins():
 
 
 @pytest.mark.parametrize("C,dtype", [(64, torch.float32), (512, torch.float32), (40, torch.bfloat16), (1000, torch.bfloat16),
-                                     (1024, torch.float16), (96, torch.float64)])
+                                     (1024, torch.float16), (96, torch.float64), (10, torch.bfloat16), (17, torch.float32),
+                                     (100, torch.bfloat16), (128, torch.float64), (33, torch.float16), (3, torch.float32)])
 def test_mc_confmat_vectorised(C, dtype):
     """Vectorised arg-max confusion matrix (4 rows in flight per wave): ties -> first index, NaN -> first NaN."""
     N = 9001
     x = torch.randn(N, C)
-    x[3::17, 2] = x[3::17].max(1).values + 1
-    x[3::17, 7] = x[3::17, 2]  # tie: class 2 must win
+    a, b = (2, 7) if C > 7 else (0, C - 1)
+    x[3::17, a] = x[3::17].max(1).values + 1
+    x[3::17, b] = x[3::17, a]  # tie: class a must win
     x[5::29, C // 2] = float("nan")
     x[5::58, 1] = float("nan")  # two NaNs: the first wins
     target = torch.randint(0, C, (N,))
