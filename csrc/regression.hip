@@ -186,10 +186,90 @@ at::Tensor regression_sums(const at::Tensor& preds_in, const at::Tensor& target_
   return gx == 1 ? partial[0] : partial.sum(0);
 }
 
+// Streaming Pearson / concordance moments (reference regression/pearson.py update): the batch's per-block partial
+// sums are reduced in a fixed order (bitwise reproducible, like partial.sum(0)) and merged into the states in place
+// with the pairwise (Chan et al.) update in fp64 -- one small kernel instead of ~25 ATen ops per update.
+template <typename S>
+__global__ __launch_bounds__(256) void pearson_merge_kernel(const double* __restrict__ partial, int64_t G, int D, double nb,
+                                                            S* __restrict__ mean_x, S* __restrict__ mean_y, S* __restrict__ var_x,
+                                                            S* __restrict__ var_y, S* __restrict__ corr_xy, S* __restrict__ n_total) {
+  const int d = blockIdx.x;
+  __shared__ double red[5][256];
+  double a[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+  for (int64_t g = threadIdx.x; g < G; g += blockDim.x)
+#pragma unroll
+    for (int ch = 0; ch < 5; ++ch) a[ch] += partial[(g * kRegCh + ch) * D + d];
+#pragma unroll
+  for (int ch = 0; ch < 5; ++ch) red[ch][threadIdx.x] = a[ch];
+  __syncthreads();
+  for (int w = blockDim.x / 2; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w)
+#pragma unroll
+      for (int ch = 0; ch < 5; ++ch) red[ch][threadIdx.x] += red[ch][threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x != 0) return;
+  const double s0 = red[0][0], s1 = red[1][0], s2 = red[2][0], s3 = red[3][0], s4 = red[4][0];
+  const double mxb = s0 / nb, myb = s1 / nb;
+  const double m2x = s2 - s0 * mxb, m2y = s3 - s1 * myb, cxy = s4 - s0 * myb;
+  const double n0 = (double)n_total[d];
+  const double n = n0 + nb;
+  const double mx0 = (double)mean_x[d], my0 = (double)mean_y[d];
+  const double dx = mxb - mx0, dy = myb - my0;
+  const double w = n0 * nb / n;
+  mean_x[d] = (S)(mx0 + dx * (nb / n));
+  mean_y[d] = (S)(my0 + dy * (nb / n));
+  var_x[d] = (S)((double)var_x[d] + m2x + w * dx * dx);
+  var_y[d] = (S)((double)var_y[d] + m2y + w * dy * dy);
+  corr_xy[d] = (S)((double)corr_xy[d] + cxy + w * dx * dy);
+  n_total[d] = n_total[d] + (S)nb;  // state-dtype add, as `num_prior + num_obs` on the state tensor
+}
+
+void pearson_update(const at::Tensor& preds_in, const at::Tensor& target_in, at::Tensor& mean_x, at::Tensor& mean_y,
+                    at::Tensor& var_x, at::Tensor& var_y, at::Tensor& corr_xy, at::Tensor& n_total) {
+  TORCH_CHECK(preds_in.sizes() == target_in.sizes() && preds_in.dim() == 2, "pearson_update: expected matching [N, D] inputs");
+  TORCH_CHECK(preds_in.scalar_type() == target_in.scalar_type(), "pearson_update: dtype mismatch");
+  const int64_t N = preds_in.size(0), D64 = preds_in.size(1);
+  for (const at::Tensor* st : {&mean_x, &mean_y, &var_x, &var_y, &corr_xy, &n_total}) {
+    TORCH_CHECK(st->is_contiguous() && st->numel() == D64 && st->scalar_type() == mean_x.scalar_type() &&
+                    (st->scalar_type() == at::kFloat || st->scalar_type() == at::kDouble),
+                "pearson_update: states must be contiguous float32/float64 [D] of one dtype");
+  }
+  if (N == 0) return;
+  const at::DeviceGuard guard(preds_in.device());
+  auto preds = preds_in.contiguous();
+  auto target = target_in.contiguous();
+  TORCH_CHECK(D64 >= 1 && D64 <= (1 << 20), "pearson_update: unsupported column count ", D64);
+  const int D = static_cast<int>(D64);
+  const int tiles = (D + kWave - 1) / kWave;
+  const int W0 = std::min(kWave, D);
+  const int rows_per_block = 4 * (kWave / W0);
+  const int64_t gx = std::min<int64_t>((N + rows_per_block - 1) / rows_per_block, std::max<int64_t>(1, 2048 / tiles));
+  auto partial = at::empty({gx, kRegCh, D64}, preds.options().dtype(at::kDouble));
+  dim3 grid(static_cast<unsigned>(gx), static_cast<unsigned>(tiles));
+  TMX_DISPATCH_FLOAT(preds.scalar_type(), "pearson_update", [&] {
+    launch_regression_sums<scalar_t>(preds, target, N, D, kOpNone, 0.0, partial, grid);
+  });
+  if (mean_x.scalar_type() == at::kFloat) {
+    hipLaunchKernelGGL(pearson_merge_kernel<float>, D, 256, 0, stream(), partial.data_ptr<double>(), gx, D, (double)N,
+                       mean_x.data_ptr<float>(), mean_y.data_ptr<float>(), var_x.data_ptr<float>(), var_y.data_ptr<float>(),
+                       corr_xy.data_ptr<float>(), n_total.data_ptr<float>());
+  } else {
+    hipLaunchKernelGGL(pearson_merge_kernel<double>, D, 256, 0, stream(), partial.data_ptr<double>(), gx, D, (double)N,
+                       mean_x.data_ptr<double>(), mean_y.data_ptr<double>(), var_x.data_ptr<double>(), var_y.data_ptr<double>(),
+                       corr_xy.data_ptr<double>(), n_total.data_ptr<double>());
+  }
+  TMX_LAUNCH_CHECK();
+}
+
 }  // namespace tmx
 
 TORCH_LIBRARY_FRAGMENT(tmx, m) {
   m.def("regression_sums(Tensor preds, Tensor target, int op, float param) -> Tensor");
+  m.def("pearson_update(Tensor preds, Tensor target, Tensor(a!) mean_x, Tensor(b!) mean_y, Tensor(c!) var_x, Tensor(d!) var_y, Tensor(e!) corr_xy, Tensor(f!) n_total) -> ()");
 }
 
-TORCH_LIBRARY_IMPL(tmx, CUDA, m) { m.impl("regression_sums", &tmx::regression_sums); }
+TORCH_LIBRARY_IMPL(tmx, CUDA, m) {
+  m.impl("regression_sums", &tmx::regression_sums);
+  m.impl("pearson_update", &tmx::pearson_update);
+}

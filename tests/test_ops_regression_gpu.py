@@ -69,3 +69,22 @@ def test_regression_modules_gpu():
             mc.update(p, t)
         a, b = mg.compute().cpu(), mc.compute()
         assert torch.allclose(a.double(), b.double(), rtol=1e-4, atol=1e-6), (cls.__name__, a, b)
+
+
+def test_pearson_inplace_update_gpu():
+    """In-place native update (sums + merge kernel) vs the CPU module: 1-D and fp64 inputs, forward(), states."""
+    import torchmetrics_forked_amd.regression as RG
+
+    g = torch.Generator().manual_seed(7)
+    for dtype in (torch.float32, torch.float64):
+        mg, mc = RG.PearsonCorrCoef().cuda(), RG.PearsonCorrCoef()
+        for i in range(4):
+            p = (torch.randn(50000, generator=g) * 3 + 1).to(dtype)
+            t = (0.5 * p + torch.randn(50000, generator=g, dtype=dtype)).to(dtype)
+            bg = mg(p.cuda(), t.cuda())
+            bc = mc(p, t)
+            assert torch.allclose(bg.cpu().double(), bc.double(), rtol=1e-5, atol=1e-6)
+        for name in ("mean_x", "mean_y", "var_x", "var_y", "corr_xy", "n_total"):
+            a, b = getattr(mg, name).cpu().double(), getattr(mc, name).double()
+            assert torch.allclose(a, b, rtol=1e-5, atol=1e-5), (name, a, b)
+        assert torch.allclose(mg.compute().cpu().double(), mc.compute().double(), rtol=1e-5)
