@@ -1165,12 +1165,14 @@ void launch_two_pass(const T* p, const int64_t* target, int64_t n, int C, int ld
 template <typename T>
 __global__ void curve_hist_ml_kernel(const T* __restrict__ preds, const int64_t* __restrict__ target, int64_t N, int L,
                                      int64_t S, const int* __restrict__ sigmoid_flag, int64_t ignore_index, bool has_ignore,
-                                     int64_t* __restrict__ hist) {
+                                     int64_t* __restrict__ hist, int* __restrict__ err) {
   const bool do_sigmoid = sigmoid_flag[0] != 0;
   const int64_t total = N * L * S;
+  bool bad = false;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
     int64_t t = target[i];
     if (has_ignore && t == ignore_index) continue;
+    bad |= t != 0 && t != 1;
     const int l = static_cast<int>((i / S) % L);
     uint16_t b;
     if (do_sigmoid) {
@@ -1181,6 +1183,7 @@ __global__ void curve_hist_ml_kernel(const T* __restrict__ preds, const int64_t*
     }
     hist_add(hist, l, t == 1 ? 1 : 0, score_code<T>(b));
   }
+  if (bad && err) atomicOr(err, 1);
 }
 
 // Binary (single label): one 1024-thread workgroup per CU, a [2][kCodes] u32 histogram privatised in LDS
@@ -1191,8 +1194,9 @@ constexpr int kBinThreads = 1024;
 
 template <typename T>
 __device__ __forceinline__ void binary_hist_add(uint32_t* s_h, T p, int64_t t, bool do_sigmoid, int64_t ignore_index,
-                                                bool has_ignore) {
+                                                bool has_ignore, bool& bad) {
   if (has_ignore && t == ignore_index) return;
+  bad |= t != 0 && t != 1;
   uint16_t b;
   if (do_sigmoid) {
     const float x = to_f32<T>(p);
@@ -1208,8 +1212,10 @@ __device__ __forceinline__ void binary_hist_add(uint32_t* s_h, T p, int64_t t, b
 template <typename T>
 __global__ void __launch_bounds__(kBinThreads) binary_hist_kernel(const T* __restrict__ preds, const int64_t* __restrict__ target,
                                                                   int64_t total, const int* __restrict__ sigmoid_flag,
-                                                                  int64_t ignore_index, bool has_ignore, int64_t* __restrict__ hist) {
+                                                                  int64_t ignore_index, bool has_ignore, int64_t* __restrict__ hist,
+                                                                  int* __restrict__ err) {
   extern __shared__ __attribute__((aligned(16))) uint32_t s_h[];  // [2][kCodes]: negatives, positives
+  bool bad = false;
   uint4* s4 = reinterpret_cast<uint4*>(s_h);
   for (int i = threadIdx.x; i < 2 * kCodes / 4; i += kBinThreads) s4[i] = make_uint4(0, 0, 0, 0);
   __syncthreads();
@@ -1228,13 +1234,14 @@ __global__ void __launch_bounds__(kBinThreads) binary_hist_kernel(const T* __res
     for (int k = 0; k < 8; ++k) {
       const uint16_t bits = static_cast<uint16_t>((k & 1) ? (parts[k >> 1] >> 16) : (parts[k >> 1] & 0xFFFFu));
       const int64_t t = (k & 1) ? tt[k >> 1].y : tt[k >> 1].x;
-      binary_hist_add<T>(s_h, *reinterpret_cast<const T*>(&bits), t, do_sigmoid, ignore_index, has_ignore);
+      binary_hist_add<T>(s_h, *reinterpret_cast<const T*>(&bits), t, do_sigmoid, ignore_index, has_ignore, bad);
     }
   }
   if (blockIdx.x == 0) {  // tail
     for (int64_t i = nvec * 8 + threadIdx.x; i < total; i += kBinThreads)
-      binary_hist_add<T>(s_h, preds[i], target[i], do_sigmoid, ignore_index, has_ignore);
+      binary_hist_add<T>(s_h, preds[i], target[i], do_sigmoid, ignore_index, has_ignore, bad);
   }
+  if (bad && err) atomicOr(err, 1);
   __syncthreads();
   for (int i = threadIdx.x; i < 2 * kCodes; i += kBinThreads) {
     const uint32_t cnt = s_h[i];
@@ -1329,7 +1336,7 @@ void curve_hist_update(const at::Tensor& preds_, const at::Tensor& target_, at::
         const int grid = static_cast<int>(std::min<int64_t>(256, (total + 8 * kBinThreads - 1) / (8 * kBinThreads)));
         hipLaunchKernelGGL(binary_hist_kernel<scalar_t>, std::max(grid, 1), kBinThreads, 2 * kCodes * sizeof(uint32_t), stream(), p,
                            target.data_ptr<int64_t>(), total, flag.data_ptr<int>(), ignore_index, has_ignore,
-                           hist.data_ptr<int64_t>());
+                           hist.data_ptr<int64_t>(), err);
         return;
       }
       if (S == 1 && C % 8 == 0 && C <= 8 * 2 * kWave && aligned) {
@@ -1342,10 +1349,10 @@ void curve_hist_update(const at::Tensor& preds_, const at::Tensor& target_, at::
         uint32_t* cptr = reinterpret_cast<uint32_t*>(codes.data_ptr());
         if (C > 512)
           hipLaunchKernelGGL((ml_codes_kernel<scalar_t, 2>), grid, kRowThreads, shm, stream(), p, target.data_ptr<int64_t>(), N, C,
-                             flag.data_ptr<int>(), ignore_index, has_ignore, cptr, n_pad);
+                             flag.data_ptr<int>(), ignore_index, has_ignore, cptr, n_pad, err);
         else
           hipLaunchKernelGGL((ml_codes_kernel<scalar_t, 1>), grid, kRowThreads, shm, stream(), p, target.data_ptr<int64_t>(), N, C,
-                             flag.data_ptr<int>(), ignore_index, has_ignore, cptr, n_pad);
+                             flag.data_ptr<int>(), ignore_index, has_ignore, cptr, n_pad, err);
         TMX_LAUNCH_CHECK();
         int splits = 1;
         while ((int64_t)C * splits < 512 && n_pad / (8 * (splits * 2)) >= 1024) splits *= 2;
@@ -1357,7 +1364,7 @@ void curve_hist_update(const at::Tensor& preds_, const at::Tensor& target_, at::
       }
       hipLaunchKernelGGL(curve_hist_ml_kernel<scalar_t>, grid_for(total, block, 4096), block, 0, stream(), p,
                          target.data_ptr<int64_t>(), N, C, S, flag.data_ptr<int>(), ignore_index, has_ignore,
-                         hist.data_ptr<int64_t>());
+                         hist.data_ptr<int64_t>(), err);
     }
   });
   TMX_LAUNCH_CHECK();
@@ -1458,8 +1465,9 @@ at::Tensor curve_hist_reduce(const at::Tensor& hist_) {
 template <typename T, int MODE>  // MODE 0: multiclass rows (softmax), 1: elementwise (sigmoid)
 __global__ void binned_hist_kernel(const T* __restrict__ preds, const int64_t* __restrict__ target, int64_t N, int C,
                                    int64_t S, const float* __restrict__ thr, int nT, const int* __restrict__ flag,
-                                   int64_t ignore_index, bool has_ignore, int* __restrict__ hist) {
+                                   int64_t ignore_index, bool has_ignore, int* __restrict__ hist, int* __restrict__ err) {
   extern __shared__ __attribute__((aligned(16))) float s_thr[];
+  bool bad = false;
   for (int i = threadIdx.x; i < nT; i += blockDim.x) s_thr[i] = thr[i];
   __syncthreads();
   const bool do_norm = flag[0] != 0;
@@ -1478,6 +1486,7 @@ __global__ void binned_hist_kernel(const T* __restrict__ preds, const int64_t* _
     for (int64_t r = wave; r < N; r += nwaves) {
       const int64_t t = target[r];
       if (has_ignore && t == ignore_index) continue;
+      bad |= t < 0 || t >= C;
       const T* row = preds + r * C;
       float mx = -INFINITY, s = 0.f;
       if (do_norm) {
@@ -1498,7 +1507,10 @@ __global__ void binned_hist_kernel(const T* __restrict__ preds, const int64_t* _
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
       const int64_t t = target[i];
       if (has_ignore && t == ignore_index) continue;
-      if (t != 0 && t != 1) continue;
+      if (t != 0 && t != 1) {
+        bad = true;
+        continue;
+      }
       const int l = static_cast<int>((i / S) % C);
       float v = to_f32<T>(preds[i]);
       if (do_norm) v = round_trip<T>(1.f / (1.f + expf(-v)));
@@ -1506,6 +1518,7 @@ __global__ void binned_hist_kernel(const T* __restrict__ preds, const int64_t* _
       atomicAdd(hist + ((int64_t)l * 2 + (int)t) * (nT + 1) + b, 1);
     }
   }
+  if (bad && err) atomicOr(err, 1);
 }
 
 // Element-wise (binary / multilabel) binned histogram with the [C][2][T+1] counts privatised in LDS: one copy per wave
@@ -1518,7 +1531,9 @@ template <typename T>
 __global__ void __launch_bounds__(kBinnedThreads) binned_hist_lds_kernel(const T* __restrict__ preds, const int64_t* __restrict__ target,
                                                                          int64_t N, int C, int64_t S, const float* __restrict__ thr,
                                                                          int nT, const int* __restrict__ flag, int64_t ignore_index,
-                                                                         bool has_ignore, int copies, int* __restrict__ hist) {
+                                                                         bool has_ignore, int copies, int* __restrict__ hist,
+                                                                         int* __restrict__ err) {
+  bool bad = false;
   extern __shared__ __attribute__((aligned(16))) int s_mem[];  // [nT] thresholds as float, then [copies][C][2][nT + 1]
   float* s_thr = reinterpret_cast<float*>(s_mem);
   const int nT4 = (nT + 3) / 4 * 4;
@@ -1533,7 +1548,10 @@ __global__ void __launch_bounds__(kBinnedThreads) binned_hist_lds_kernel(const T
   for (int64_t i = blockIdx.x * (int64_t)kBinnedThreads + threadIdx.x; i < total; i += (int64_t)gridDim.x * kBinnedThreads) {
     const int64_t t = target[i];
     if (has_ignore && t == ignore_index) continue;
-    if (t != 0 && t != 1) continue;
+    if (t != 0 && t != 1) {
+      bad = true;
+      continue;
+    }
     const int l = static_cast<int>((i / S) % C);
     float v = to_f32<T>(preds[i]);
     if (do_norm) v = round_trip<T>(1.f / (1.f + expf(-v)));
@@ -1544,6 +1562,7 @@ __global__ void __launch_bounds__(kBinnedThreads) binned_hist_lds_kernel(const T
     }
     atomicAdd(my + (l * 2 + (int)t) * (nT + 1) + lo, 1);
   }
+  if (bad && err) atomicOr(err, 1);
   __syncthreads();
   for (int b = threadIdx.x; b < H; b += kBinnedThreads) {
     int cnt = 0;
@@ -1553,27 +1572,46 @@ __global__ void __launch_bounds__(kBinnedThreads) binned_hist_lds_kernel(const T
 }
 
 // confmat[t, c, y, p]: y = target (0/1), p = (score >= thr[t]).  tp=[1][1] fp=[0][1] fn=[1][0] tn=[0][0]
-__global__ void binned_scan_kernel(const int* __restrict__ hist, int C, int nT, int64_t* __restrict__ confmat) {
+// One workgroup per class: the (nT + 1)-bucket histogram is suffix-summed in LDS (Hillis-Steele over 2 * (nT + 1)
+// words), then thread t writes threshold t's four cells.  (A single thread walking the buckets took 41 us.)
+__global__ void __launch_bounds__(1024) binned_scan_kernel(const int* __restrict__ hist, int C, int nT, int64_t* __restrict__ confmat) {
+  extern __shared__ __attribute__((aligned(16))) long long s_suf[];  // [2][nT + 1] suffix sums, then [2][nT + 1] scratch
   const int c = blockIdx.x;
-  for (int y = 0; y < 2; ++y) {
-    const int* h = hist + ((int64_t)c * 2 + y) * (nT + 1);
-    if (threadIdx.x == 0) {
-      long long total = 0;
-      for (int b = 0; b <= nT; ++b) total += h[b];
-      long long above = 0;  // # with bucket > t  (score >= thr[t])
-      for (int t = nT - 1; t >= 0; --t) {
-        above += h[t + 1];
-        int64_t* cell = confmat + ((int64_t)t * C + c) * 4 + y * 2;
-        cell[1] += above;          // predicted positive
-        cell[0] += total - above;  // predicted negative
-      }
+  const int M = nT + 1;
+  long long* a = s_suf;
+  long long* b = s_suf + 2 * M;
+  for (int i = threadIdx.x; i < 2 * M; i += blockDim.x) a[i] = hist[(int64_t)c * 2 * M + i];
+  __syncthreads();
+  for (int off = 1; off < M; off <<= 1) {  // suffix sums within each of the two rows
+    for (int i = threadIdx.x; i < 2 * M; i += blockDim.x) {
+      const int j = i % M;
+      b[i] = a[i] + (j + off < M ? a[i + off] : 0);
+    }
+    __syncthreads();
+    long long* tmp = a;
+    a = b;
+    b = tmp;
+  }
+  for (int t = threadIdx.x; t < nT; t += blockDim.x) {
+#pragma unroll
+    for (int y = 0; y < 2; ++y) {
+      const long long total = a[y * M];
+      const long long above = a[y * M + t + 1];  // # with bucket > t  (score >= thr[t])
+      int64_t* cell = confmat + ((int64_t)t * C + c) * 4 + y * 2;
+      cell[1] += above;          // predicted positive
+      cell[0] += total - above;  // predicted negative
     }
   }
 }
 
 void binned_curve_update(const at::Tensor& preds_, const at::Tensor& target_, const at::Tensor& thresholds_,
                          at::Tensor& confmat, int64_t task, int64_t ignore_index, bool has_ignore,
-                         c10::optional<at::Tensor> norm_flag) {
+                         c10::optional<at::Tensor> norm_flag, c10::optional<at::Tensor> err_flag) {
+  int* err = nullptr;
+  if (err_flag.has_value()) {
+    TORCH_CHECK(err_flag->scalar_type() == at::kInt && err_flag->is_contiguous(), "err_flag must be int32");
+    err = err_flag->data_ptr<int>();
+  }
   auto preds = preds_.contiguous();
   auto target = target_.contiguous().to(at::kLong);
   auto thr = thresholds_.contiguous().to(at::kFloat);
@@ -1592,7 +1630,7 @@ void binned_curve_update(const at::Tensor& preds_, const at::Tensor& target_, co
       if (n == 0) return;
       hipLaunchKernelGGL((binned_hist_kernel<scalar_t, 0>), grid_for(n * kWave, block, 4096), block, shm, stream(), p,
                          target.data_ptr<int64_t>(), n, C, (int64_t)1, thr.data_ptr<float>(), nT, flag.data_ptr<int>(),
-                         ignore_index, has_ignore, hist.data_ptr<int>());
+                         ignore_index, has_ignore, hist.data_ptr<int>(), err);
     } else {
       const int64_t total = target.numel();
       if (total == 0) return;
@@ -1607,16 +1645,18 @@ void binned_curve_update(const at::Tensor& preds_, const at::Tensor& target_, co
         const int grid = static_cast<int>(std::min<int64_t>(1024, (total + kBinnedThreads - 1) / kBinnedThreads));
         hipLaunchKernelGGL(binned_hist_lds_kernel<scalar_t>, std::max(grid, 1), kBinnedThreads, shm_lds, stream(), p,
                            target.data_ptr<int64_t>(), N, C, S, thr.data_ptr<float>(), nT, flag.data_ptr<int>(), ignore_index,
-                           has_ignore, copies, hist.data_ptr<int>());
+                           has_ignore, copies, hist.data_ptr<int>(), err);
         return;
       }
       hipLaunchKernelGGL((binned_hist_kernel<scalar_t, 1>), grid_for(total, block, 4096), block, shm, stream(), p,
                          target.data_ptr<int64_t>(), N, C, S, thr.data_ptr<float>(), nT, flag.data_ptr<int>(), ignore_index,
-                         has_ignore, hist.data_ptr<int>());
+                         has_ignore, hist.data_ptr<int>(), err);
     }
   });
   TMX_LAUNCH_CHECK();
-  hipLaunchKernelGGL(binned_scan_kernel, C, 64, 0, stream(), hist.data_ptr<int>(), C, nT, confmat.data_ptr<int64_t>());
+  const size_t scan_shm = 4 * (size_t)(nT + 1) * sizeof(long long);
+  TORCH_CHECK(scan_shm <= 64 * 1024, "binned_curve_update: too many thresholds for the LDS scan");
+  hipLaunchKernelGGL(binned_scan_kernel, C, 256, scan_shm, stream(), hist.data_ptr<int>(), C, nT, confmat.data_ptr<int64_t>());
   TMX_LAUNCH_CHECK();
 }
 
@@ -1797,7 +1837,7 @@ TORCH_LIBRARY_FRAGMENT(tmx, m) {
   m.def("binary_stats_update(Tensor preds, Tensor target, Tensor(a!) counts, int num_labels, float threshold, int ignore_index, bool has_ignore) -> ()");
   m.def("curve_hist_update(Tensor preds, Tensor target, Tensor(a!) hist, int task, int ignore_index, bool has_ignore, Tensor(b!)? confmat, Tensor? norm_flag, Tensor(c!)? err_flag, Tensor(d!)? mode_state) -> ()");
   m.def("curve_hist_reduce(Tensor hist) -> Tensor");
-  m.def("binned_curve_update(Tensor preds, Tensor target, Tensor thresholds, Tensor(a!) confmat, int task, int ignore_index, bool has_ignore, Tensor? norm_flag) -> ()");
+  m.def("binned_curve_update(Tensor preds, Tensor target, Tensor thresholds, Tensor(a!) confmat, int task, int ignore_index, bool has_ignore, Tensor? norm_flag, Tensor(b!)? err_flag=None) -> ()");
   m.def("ce_bins_update(Tensor conf, Tensor acc, Tensor boundaries, Tensor(a!) bins) -> ()");
   m.def("mc_calibration_update(Tensor preds, Tensor target, Tensor boundaries, Tensor(a!) bins) -> ()");
 }

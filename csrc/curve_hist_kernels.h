@@ -481,10 +481,11 @@ template <typename T, int NG>
 __device__ __forceinline__ void row_tile_ml(const T* __restrict__ preds, const int64_t* __restrict__ target, int64_t n, int L,
                                             bool do_sigmoid, int64_t ignore_index, bool has_ignore,
                                             uint32_t* __restrict__ codes, int64_t n_pad, uint32_t* __restrict__ s_tile,
-                                            int64_t tile) {
+                                            int64_t tile, int* __restrict__ err) {
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = threadIdx.x / kWave;
   const int nvec = L / 8;
+  bool bad = false;
   const bool lo_ok = lane < nvec, hi_ok = lane + kWave < nvec;
   const int lq = lo_ok ? lane : nvec - 1;
   const int hq = hi_ok ? lane + kWave : nvec - 1;
@@ -523,6 +524,7 @@ __device__ __forceinline__ void row_tile_ml(const T* __restrict__ preds, const i
           const int64_t t = (k & 1) ? tt[k >> 1].y : tt[k >> 1].x;
           const uint32_t b = do_sigmoid ? (uint32_t)round_bits16<T>(1.f / (1.f + expf(-v[k]))) : (uint32_t)raw_bits<T>(w, k);
           uint32_t c16 = raw_code<T>(b);
+          bad |= valid && !(has_ignore && t == ignore_index) && t != 0 && t != 1;
           if (!valid || (has_ignore && t == ignore_index)) c16 = 0x8000u;
           else if (t == 1 && !(c16 & 0x8000u)) c16 |= 0x4000u;
           code[h][k] = c16;
@@ -535,6 +537,7 @@ __device__ __forceinline__ void row_tile_ml(const T* __restrict__ preds, const i
       }
     }
   }
+  if (bad && err) atomicOr(err, 1);
   __syncthreads();
   store_tile<NG>(s_tile, codes, L, n_pad, tile);
 }
@@ -543,14 +546,14 @@ template <typename T, int NG>
 __global__ void __launch_bounds__(kRowThreads, 4) ml_codes_kernel(const T* __restrict__ preds, const int64_t* __restrict__ target,
                                                                    int64_t n, int L, const int* __restrict__ sigmoid_flag,
                                                                    int64_t ignore_index, bool has_ignore,
-                                                                   uint32_t* __restrict__ codes, int64_t n_pad) {
+                                                                   uint32_t* __restrict__ codes, int64_t n_pad, int* __restrict__ err) {
   extern __shared__ __attribute__((aligned(16))) uint32_t s_tile[];  // [512 * NG][kSlots]
   const int64_t ntiles = (n + kTileRows - 1) / kTileRows;
   const int64_t per_xcd = (ntiles + 7) / 8;
   const int64_t b = blockIdx.x;
   const int64_t tile = (b % 8) * per_xcd + b / 8;  // XCD-aware order, as the multiclass row pass
   if (tile >= ntiles) return;
-  row_tile_ml<T, NG>(preds, target, n, L, sigmoid_flag[0] != 0, ignore_index, has_ignore, codes, n_pad, s_tile, tile);
+  row_tile_ml<T, NG>(preds, target, n, L, sigmoid_flag[0] != 0, ignore_index, has_ignore, codes, n_pad, s_tile, tile, err);
 }
 
 // Class pass: one 1024-thread workgroup per (class, row split), two per CU (64-KiB LDS).

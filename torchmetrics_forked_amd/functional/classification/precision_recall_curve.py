@@ -63,9 +63,18 @@ def _check_target_int(target: Tensor, msg_tail: str = " with ground truth labels
         )
 
 
+BINARY_TARGET_MSG = "Detected values in `target` outside {0, 1, ignore_index}."
+
+
 def _binary_precision_recall_curve_tensor_validation(
-    preds: Tensor, target: Tensor, ignore_index: Optional[int] = None, sink: Optional[DeferredChecks] = None
+    preds: Tensor,
+    target: Tensor,
+    ignore_index: Optional[int] = None,
+    sink: Optional[DeferredChecks] = None,
+    check_values: bool = True,
 ) -> None:
+    """``check_values=False``: the target value check is left to a native kernel that ORs the sink's
+    ``BINARY_TARGET_MSG`` flag while it streams the batch."""
     _check_same_shape(preds, target)
     _check_target_int(target)
     if not preds.is_floating_point():
@@ -73,6 +82,8 @@ def _binary_precision_recall_curve_tensor_validation(
             "Expected argument `preds` to be an floating tensor with probability/logit scores,"
             f" but got tensor with dtype {preds.dtype}"
         )
+    if not check_values:
+        return
     bad = (target != 0) & (target != 1)
     if ignore_index is not None:
         bad &= target != ignore_index
@@ -84,7 +95,7 @@ def _binary_precision_recall_curve_tensor_validation(
             f" the following values {[0, 1] if ignore_index is None else [ignore_index]}."
         ),
         sink,
-        "Detected values in `target` outside {0, 1, ignore_index}.",
+        BINARY_TARGET_MSG,
     )
 
 
@@ -153,9 +164,14 @@ def _multilabel_precision_recall_curve_arg_validation(
 
 
 def _multilabel_precision_recall_curve_tensor_validation(
-    preds: Tensor, target: Tensor, num_labels: int, ignore_index: Optional[int] = None, sink: Optional[DeferredChecks] = None
+    preds: Tensor,
+    target: Tensor,
+    num_labels: int,
+    ignore_index: Optional[int] = None,
+    sink: Optional[DeferredChecks] = None,
+    check_values: bool = True,
 ) -> None:
-    _binary_precision_recall_curve_tensor_validation(preds, target, ignore_index, sink)
+    _binary_precision_recall_curve_tensor_validation(preds, target, ignore_index, sink, check_values)
     if preds.shape[1] != num_labels:
         raise ValueError(
             "Expected both `target.shape[1]` and `preds.shape[1]` to be equal to the number of labels"

@@ -237,14 +237,23 @@ def curve_hist_reduce(hist: Tensor) -> Tensor:
 
 
 def binned_curve_update(
-    preds: Tensor, target: Tensor, thresholds: Tensor, confmat: Tensor, task: str, ignore_index: Optional[int]
+    preds: Tensor,
+    target: Tensor,
+    thresholds: Tensor,
+    confmat: Tensor,
+    task: str,
+    ignore_index: Optional[int],
+    err_flag: Optional[Tensor] = None,
 ) -> None:
-    """``confmat[T, C, 2, 2] += `` multi-threshold confusion counts (score >= thr[t]) per class/label."""
+    """``confmat[T, C, 2, 2] += `` multi-threshold confusion counts (score >= thr[t]) per class/label.
+
+    ``err_flag`` (int32[1], GPU only) is OR-ed with 1 when a non-ignored target is outside {0, 1} (binary /
+    multilabel) or ``[0, C)`` (multiclass) -- the deferred value check, folded into the histogram pass."""
     tcode = 0 if task == "multiclass" else 1
     if ops.use_native(target):
         torch.ops.tmx.binned_curve_update(
             preds, target, thresholds, confmat, tcode, -1 if ignore_index is None else ignore_index, ignore_index is not None,
-            _norm_flag(preds, target, task, ignore_index),
+            _norm_flag(preds, target, task, ignore_index), err_flag,
         )
         return
     T, C = confmat.shape[0], confmat.shape[1]
