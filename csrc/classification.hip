@@ -1804,6 +1804,225 @@ void ce_bins_update(const at::Tensor& conf_, const at::Tensor& acc_, const at::T
   TMX_LAUNCH_CHECK();
 }
 
+// One-pass top-label calibration update straight from the raw [N, C] scores (aligned rows, C a multiple of the
+// 16-B vector width, C <= 128 * VEC): 4 rows per wave in flight, DPP max / sum and ballot arg-max as the pair-stream
+// kernel.  The reference decides "softmax or not" on the whole (ignore-filtered) batch; here every row is binned
+// both ways -- raw (max, first arg-max) and softmax (rounded 1 / sum exp, first index whose rounded softmax equals
+// it) -- into a [2][3][nb1] table, and the last workgroup (grid_sum_last carrying the out-of-range row count) adds
+// the right half to the bins.  Ignored rows are skipped in-kernel (no boolean-index copy); a target outside
+// [0, C) ORs err (deferred validation).
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+  v += dpp_f32<0xB1>(0.f, v);
+  v += dpp_f32<0x4E>(0.f, v);
+  v += dpp_f32<0x141>(0.f, v);
+  v += dpp_f32<0x140>(0.f, v);
+  v += dpp_f32<0x142, 0xA>(0.f, v);
+  v += dpp_f32<0x143, 0xC>(0.f, v);
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+
+template <typename T, int NCH>
+__global__ void __launch_bounds__(256) mc_calibration_vec_kernel(const T* __restrict__ preds, const int64_t* __restrict__ target,
+                                                                 int64_t n, int C, int64_t ignore_index, bool has_ignore,
+                                                                 const float* __restrict__ boundaries, int nb1,
+                                                                 double* __restrict__ bins, unsigned long long* __restrict__ scratch,
+                                                                 int* __restrict__ err) {
+  constexpr int VEC = VecOf<T>::n;
+  constexpr int kRows = 4;
+  extern __shared__ __attribute__((aligned(16))) double s_cal[];  // [2 modes][3][nb1], then boundaries (float)
+  float* s_b = reinterpret_cast<float*>(s_cal + 6 * nb1);
+  __shared__ int s_oor;
+  __shared__ long long s_last;
+  for (int i = threadIdx.x; i < 6 * nb1; i += blockDim.x) s_cal[i] = 0.0;
+  for (int i = threadIdx.x; i < nb1; i += blockDim.x) s_b[i] = boundaries[i];
+  if (threadIdx.x == 0) s_oor = 0;
+  __syncthreads();
+  const int lane = threadIdx.x & (kWave - 1);
+  const int nvec = C / VEC;
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / kWave;
+  const int64_t nwaves = (int64_t)gridDim.x * blockDim.x / kWave;
+  int oor_rows = 0;
+  bool bad_t = false;
+  for (int64_t r0 = wave * kRows; r0 < n; r0 += nwaves * kRows) {
+    uint4 w[kRows][NCH];
+#pragma unroll
+    for (int i = 0; i < kRows; ++i) {
+      const uint4* row = reinterpret_cast<const uint4*>(preds + min(r0 + i, n - 1) * C);
+#pragma unroll
+      for (int ch = 0; ch < NCH; ++ch) {
+        const int q = lane + kWave * ch;
+        w[i][ch] = row[q < nvec ? q : nvec - 1];
+      }
+    }
+    int64_t tt[kRows];
+#pragma unroll
+    for (int i = 0; i < kRows; ++i) tt[i] = target[min(r0 + i, n - 1)];
+#pragma unroll
+    for (int i = 0; i < kRows; ++i) {
+      const int64_t t = tt[i];
+      if (r0 + i >= n || (has_ignore && t == ignore_index)) continue;  // wave-uniform
+      bad_t |= t < 0 || t >= C;
+      float m[NCH];
+      int kk[NCH];
+      bool nan = false, out = false;
+#pragma unroll
+      for (int ch = 0; ch < NCH; ++ch) {
+        const bool active = lane + kWave * ch < nvec;
+        float mm = -INFINITY;
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) {
+          const float v = vec_elem<T>(w[i][ch], k);
+          nan |= active && v != v;
+          out |= active && !(v >= 0.f && v <= 1.f);
+          mm = __builtin_fmaxf(mm, v);
+        }
+        int kf = VEC - 1;
+#pragma unroll
+        for (int k = VEC - 2; k >= 0; --k) kf = vec_elem<T>(w[i][ch], k) == mm ? k : kf;
+        m[ch] = active ? mm : -INFINITY;
+        kk[ch] = kf;
+      }
+      const bool row_nan = __ballot(nan) != 0;
+      const bool row_oor = __ballot(out) != 0;
+      oor_rows += row_oor ? 1 : 0;
+      float mx = m[0];
+#pragma unroll
+      for (int ch = 1; ch < NCH; ++ch) mx = __builtin_fmaxf(mx, m[ch]);
+      mx = wave_max_uniform(mx);
+      // raw mode (only chosen when no row of the batch is out of [0, 1], so never for NaN rows)
+      uint64_t b = __ballot(m[0] == mx);
+      int ch0 = 0;
+      if constexpr (NCH == 2) {
+        if (b == 0) {
+          b = __ballot(m[1] == mx);
+          ch0 = 1;
+        }
+      }
+      const int L0 = b ? __builtin_ctzll(b) : 0;
+      const int pred_raw = VEC * (L0 + kWave * ch0) + __builtin_amdgcn_readlane(NCH == 2 && ch0 ? kk[NCH - 1] : kk[0], L0);
+      const float conf_raw = row_nan ? NAN : mx;
+      // softmax mode
+      float conf_sm = NAN;
+      int pred_sm = 0;
+      if (!row_nan && mx != INFINITY && mx != -INFINITY) {
+        float sum = 0.f;
+#pragma unroll
+        for (int ch = 0; ch < NCH; ++ch) {
+          const bool active = lane + kWave * ch < nvec;
+#pragma unroll
+          for (int k = 0; k < VEC; ++k)  // hardware exp2 (~1 ulp, like the summation-order difference to ATen)
+            sum += active ? __builtin_amdgcn_exp2f((vec_elem<T>(w[i][ch], k) - mx) * 1.4426950408889634f) : 0.f;
+        }
+        sum = wave_sum_dpp(sum);
+        conf_sm = round_trip<T>(1.f / sum);
+        // An element can round to the max's softmax value only if exp(v - max) > 1 - 2^-7 (bf16; tighter for fp16 /
+        // fp32), i.e. v > max - 0.0079.  Without such a runner-up the answer is the raw first arg-max.
+        bool near = false;
+#pragma unroll
+        for (int ch = 0; ch < NCH; ++ch) {
+          const bool active = lane + kWave * ch < nvec;
+#pragma unroll
+          for (int k = 0; k < VEC; ++k) {
+            const float v = vec_elem<T>(w[i][ch], k);
+            near |= active && v < mx && v > mx - 0.01f;
+          }
+        }
+        pred_sm = pred_raw;
+        if (__ballot(near)) {
+          int first[NCH];
+#pragma unroll
+          for (int ch = 0; ch < NCH; ++ch) {
+            const bool active = lane + kWave * ch < nvec;
+            int f = VEC;
+#pragma unroll
+            for (int k = VEC - 1; k >= 0; --k) {
+              const float v = vec_elem<T>(w[i][ch], k);
+              if (active && v > mx - 0.01f && round_trip<T>(expf(v - mx) / sum) == conf_sm) f = k;
+            }
+            first[ch] = f;
+          }
+          uint64_t bs = __ballot(first[0] < VEC);
+          int chs = 0;
+          if constexpr (NCH == 2) {
+            if (bs == 0) {
+              bs = __ballot(first[1] < VEC);
+              chs = 1;
+            }
+          }
+          const int Ls = bs ? __builtin_ctzll(bs) : 0;
+          pred_sm = VEC * (Ls + kWave * chs) + __builtin_amdgcn_readlane(NCH == 2 && chs ? first[NCH - 1] : first[0], Ls);
+        }
+      }
+      if (lane == 0) {
+        const int br = cal_bin(conf_raw, s_b, nb1), bsm = cal_bin(conf_sm, s_b, nb1);
+        atomicAdd(&s_cal[br], 1.0);
+        atomicAdd(&s_cal[nb1 + br], (double)conf_raw);
+        atomicAdd(&s_cal[2 * nb1 + br], pred_raw == t ? 1.0 : 0.0);
+        atomicAdd(&s_cal[3 * nb1 + bsm], 1.0);
+        atomicAdd(&s_cal[4 * nb1 + bsm], (double)conf_sm);
+        atomicAdd(&s_cal[5 * nb1 + bsm], pred_sm == t ? 1.0 : 0.0);
+      }
+    }
+  }
+  if (bad_t && lane == 0 && err) atomicOr(err, 1);
+  if (lane == 0 && oor_rows) atomicAdd(&s_oor, oor_rows);
+  __syncthreads();
+  for (int i = threadIdx.x; i < 6 * nb1; i += blockDim.x)
+    if (s_cal[i] != 0.0) atomicAdd(reinterpret_cast<double*>(scratch) + i, s_cal[i]);
+  __builtin_amdgcn_s_waitcnt(0);  // table atomics performed before this workgroup's ticket
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const long long mine[1] = {s_oor};
+    long long tot[1];
+    s_last = grid_sum_last<1>(scratch + 6 * nb1, mine, tot) ? tot[0] : -1;
+  }
+  __syncthreads();
+  if (s_last < 0) return;
+  const int mode = s_last > 0 ? 1 : 0;
+  for (int i = threadIdx.x; i < 3 * nb1; i += blockDim.x) {
+    const double keep = __longlong_as_double((long long)atomicExch(&scratch[mode * 3 * nb1 + i], 0ull));
+    atomicExch(&scratch[(1 - mode) * 3 * nb1 + i], 0ull);
+    if (keep != 0.0 || keep != keep) atomicAdd(bins + i, keep);
+  }
+}
+
+// Returns false when the shape / alignment does not qualify (caller falls back to the filtered path).
+bool mc_calibration_fused(const at::Tensor& preds, const at::Tensor& target_, const at::Tensor& boundaries_, at::Tensor& bins,
+                          at::Tensor& scratch, int64_t ignore_index, bool has_ignore, const c10::optional<at::Tensor>& err_flag) {
+  TORCH_CHECK(preds.dim() == 2, "preds must be [N, C]");
+  auto target = target_.contiguous().to(at::kLong).reshape(-1);
+  auto bnd = boundaries_.contiguous().to(at::kFloat);
+  const int nb1 = static_cast<int>(bnd.numel());
+  TORCH_CHECK(bins.is_contiguous() && bins.scalar_type() == at::kDouble && bins.numel() == 3 * nb1, "bins must be float64 [3, n_bins + 1]");
+  TORCH_CHECK(scratch.is_contiguous() && scratch.scalar_type() == at::kDouble && scratch.numel() >= 6 * nb1 + kGridSlotsWords,
+              "scratch must be a zeroed float64 [6 (n_bins + 1) + ", kGridSlotsWords, "]");
+  const int64_t n = preds.size(0);
+  const int C = static_cast<int>(preds.size(1));
+  TORCH_CHECK(target.numel() == n, "preds must be [N, C] with target [N]");
+  if (!preds.is_contiguous() || !preds.is_floating_point()) return false;
+  const size_t shm = 6 * nb1 * sizeof(double) + nb1 * sizeof(float);
+  if (shm > 48 * 1024) return false;
+  if (n == 0) return true;
+  int* err = flag_ptr(err_flag);
+  bool done = false;
+  TMX_DISPATCH_FLOAT(preds.scalar_type(), "mc_calibration_fused", [&] {
+    constexpr int VEC = VecOf<scalar_t>::n;
+    const scalar_t* p = reinterpret_cast<const scalar_t*>(preds.data_ptr());
+    if (C % VEC != 0 || C < 2 || C > 2 * kWave * VEC || (reinterpret_cast<uintptr_t>(p) & 15) != 0) return;
+    auto* sc = reinterpret_cast<unsigned long long*>(scratch.data_ptr<double>());
+    const int grid = grid_for(n * kWave / 4, 256, 2048);
+    if (C <= kWave * VEC)
+      hipLaunchKernelGGL((mc_calibration_vec_kernel<scalar_t, 1>), grid, 256, shm, stream(), p, target.data_ptr<int64_t>(), n, C,
+                         ignore_index, has_ignore, bnd.data_ptr<float>(), nb1, bins.data_ptr<double>(), sc, err);
+    else
+      hipLaunchKernelGGL((mc_calibration_vec_kernel<scalar_t, 2>), grid, 256, shm, stream(), p, target.data_ptr<int64_t>(), n, C,
+                         ignore_index, has_ignore, bnd.data_ptr<float>(), nb1, bins.data_ptr<double>(), sc, err);
+    done = true;
+  });
+  TMX_LAUNCH_CHECK();
+  return done;
+}
+
 void mc_calibration_update(const at::Tensor& preds_, const at::Tensor& target_, const at::Tensor& boundaries_, at::Tensor& bins) {
   auto preds = preds_.contiguous();
   auto target = target_.contiguous().to(at::kLong).reshape(-1);
@@ -1840,6 +2059,7 @@ TORCH_LIBRARY_FRAGMENT(tmx, m) {
   m.def("binned_curve_update(Tensor preds, Tensor target, Tensor thresholds, Tensor(a!) confmat, int task, int ignore_index, bool has_ignore, Tensor? norm_flag, Tensor(b!)? err_flag=None) -> ()");
   m.def("ce_bins_update(Tensor conf, Tensor acc, Tensor boundaries, Tensor(a!) bins) -> ()");
   m.def("mc_calibration_update(Tensor preds, Tensor target, Tensor boundaries, Tensor(a!) bins) -> ()");
+  m.def("mc_calibration_fused(Tensor preds, Tensor target, Tensor boundaries, Tensor(a!) bins, Tensor(b!) scratch, int ignore_index, bool has_ignore, Tensor(c!)? err_flag=None) -> bool");
 }
 
 TORCH_LIBRARY_IMPL(tmx, CUDA, m) {
@@ -1854,4 +2074,5 @@ TORCH_LIBRARY_IMPL(tmx, CUDA, m) {
   m.impl("binned_curve_update", &tmx::binned_curve_update);
   m.impl("ce_bins_update", &tmx::ce_bins_update);
   m.impl("mc_calibration_update", &tmx::mc_calibration_update);
+  m.impl("mc_calibration_fused", &tmx::mc_calibration_fused);
 }
