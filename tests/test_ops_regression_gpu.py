@@ -88,3 +88,26 @@ def test_pearson_inplace_update_gpu():
             a, b = getattr(mg, name).cpu().double(), getattr(mc, name).double()
             assert torch.allclose(a, b, rtol=1e-5, atol=1e-5), (name, a, b)
         assert torch.allclose(mg.compute().cpu().double(), mc.compute().double(), rtol=1e-5)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16, torch.float64])
+@pytest.mark.parametrize("op", range(8))
+def test_regression_sums_single_column(dtype, op):
+    """D == 1 sums (aligned and offset views, odd N) vs an fp64 CPU reference; repeated calls are bitwise equal."""
+    g = torch.Generator().manual_seed(op)
+    N = 1_000_003
+    p = (torch.rand(N + 1, generator=g) * 2 + 0.1).to(dtype)
+    t = (torch.rand(N + 1, generator=g) * 2 + 0.1).to(dtype)
+    param = 1.5 if op in (5, 7) else 0.0
+    pg, tg = p.cuda(), t.cuda()
+    flat = torch.ops.tmx.regression_sums(pg[:N].unsqueeze(1), tg[:N].unsqueeze(1), op, param)
+    again = torch.ops.tmx.regression_sums(pg[:N].unsqueeze(1), tg[:N].unsqueeze(1), op, param)
+    tiled = torch.ops.tmx.regression_sums(pg[1:].unsqueeze(1), tg[1:].unsqueeze(1), op, param)  # 2-B/4-B offset: tiled
+    ref_tiled = torch.ops.tmx.regression_sums(pg[1 : N + 1].unsqueeze(1), tg[1 : N + 1].unsqueeze(1), op, param)
+    assert torch.equal(flat, again)
+    assert flat.shape == (8, 1)
+    pc, tc = p[:N].double(), t[:N].double()
+    d = pc - tc
+    ref = torch.stack([pc.sum(), tc.sum(), (pc * pc).sum(), (tc * tc).sum(), (pc * tc).sum(), (d * d).sum(), d.abs().sum()])
+    torch.testing.assert_close(flat[:7, 0].cpu(), ref, rtol=1e-4 if dtype != torch.float64 else 1e-10, atol=1e-6)
+    assert tiled.shape == ref_tiled.shape == (8, 1)

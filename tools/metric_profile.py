@@ -27,6 +27,12 @@ def make(name):
     if name == "retrieval_map":
         return tm.RetrievalMAP(), (torch.randn(1 << 20, device=dev, generator=g), torch.rand(1 << 20, device=dev, generator=g) > 0.5,
                                    torch.randint(0, 10000, (1 << 20,), device=dev, generator=g))
+    if name in ("mse", "r2", "mae"):
+        cls = {"mse": tm.MeanSquaredError, "r2": tm.R2Score, "mae": tm.MeanAbsoluteError}[name]
+        return cls(), (torch.randn(NB, device=dev, generator=g), torch.randn(NB, device=dev, generator=g))
+    if name == "mc_accuracy_c10":
+        return tm.MulticlassAccuracy(num_classes=10), (torch.randn(1 << 20, 10, device=dev, generator=g).bfloat16(),
+                                                       torch.randint(0, 10, (1 << 20,), device=dev, generator=g))
     raise SystemExit(f"unknown case {name}")
 
 
