@@ -434,8 +434,9 @@ __global__ void __launch_bounds__(kRowThreads, 4) mc_codes_kernel(const T* __res
   extern __shared__ __attribute__((aligned(16))) uint32_t s_tile[];  // [512 * NG][kSlots]
   int use_mode;
   if constexpr (FIXUP) {
-    const int m0 = __hip_atomic_load(mode, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int m1 = __hip_atomic_load(mode + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // the row pass that wrote mode[1] has completed (stream order, kernel-boundary release/acquire): plain loads
+    const int m0 = mode[0];
+    const int m1 = mode[1];
     if (m0 == m1) return;
     use_mode = m1;
   } else {
