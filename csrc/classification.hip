@@ -533,33 +533,53 @@ __global__ void __launch_bounds__(1024) mc_pairs_argmax_staged_kernel(const T* _
   const int nchunks = tile_rows * C * (int)sizeof(T) / 16;
   const char* base = reinterpret_cast<const char*>(preds);
   const int64_t ntiles = (n + tile_rows - 1) / tile_rows;
-  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const int64_t r0 = tile * tile_rows;
-    const int64_t r = r0 + grp;
-    const int64_t t = (gl == 0 && r < n) ? target[r] : 0;
-    const int64_t off0 = r0 * C * (int64_t)sizeof(T);
-    for (int q = threadIdx.x; q < nchunks; q += blockDim.x) {
-      const int64_t off = off0 + 16 * (int64_t)q;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (off + 16 <= total_bytes) {
-        v = *reinterpret_cast<const uint4*>(base + off);
-      } else if (off < total_bytes) {
-        // last partial chunk: 16-bit pieces (element sizes are >= 2 B), constant indices so v stays in registers
-        const int rem = (int)(total_bytes - off);
-        uint32_t d[4];
+  // each thread moves at most sizeof(T) 16-B chunks per tile (tile <= 16 B x 2048 threads' worth / blockDim); the
+  // next tile's chunks and target are loaded into registers while the current tile is reduced from LDS
+  constexpr int CH = sizeof(T);
+  auto load_chunk = [&](int64_t off) -> uint4 {
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (off + 16 <= total_bytes) {
+      v = *reinterpret_cast<const uint4*>(base + off);
+    } else if (off < total_bytes) {
+      // last partial chunk: 16-bit pieces (element sizes are >= 2 B), constant indices so v stays in registers
+      const int rem = (int)(total_bytes - off);
+      uint32_t d[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          uint32_t x = 0;
+      for (int j = 0; j < 4; ++j) {
+        uint32_t x = 0;
 #pragma unroll
-          for (int h = 0; h < 2; ++h)
-            if (4 * j + 2 * h < rem) x |= (uint32_t)*reinterpret_cast<const uint16_t*>(base + off + 4 * j + 2 * h) << (16 * h);
-          d[j] = x;
-        }
-        v = make_uint4(d[0], d[1], d[2], d[3]);
+        for (int h = 0; h < 2; ++h)
+          if (4 * j + 2 * h < rem) x |= (uint32_t)*reinterpret_cast<const uint16_t*>(base + off + 4 * j + 2 * h) << (16 * h);
+        d[j] = x;
       }
-      reinterpret_cast<uint4*>(s_tile)[q] = v;
+      v = make_uint4(d[0], d[1], d[2], d[3]);
+    }
+    return v;
+  };
+  uint4 nxt[CH];
+  int64_t t_nxt = 0;
+  auto prefetch = [&](int64_t tile) {
+    const int64_t off0 = tile * tile_rows * C * (int64_t)sizeof(T);
+#pragma unroll
+    for (int j = 0; j < CH; ++j) {
+      const int q = threadIdx.x + j * blockDim.x;
+      nxt[j] = (q < nchunks && tile < ntiles) ? load_chunk(off0 + 16 * (int64_t)q) : make_uint4(0, 0, 0, 0);
+    }
+    const int64_t r = tile * tile_rows + grp;
+    t_nxt = (gl == 0 && tile < ntiles && r < n) ? target[r] : 0;
+  };
+  int64_t tile = blockIdx.x;
+  if (tile < ntiles) prefetch(tile);
+  for (; tile < ntiles; tile += gridDim.x) {
+    const int64_t r = tile * tile_rows + grp;
+    const int64_t t = t_nxt;
+#pragma unroll
+    for (int j = 0; j < CH; ++j) {
+      const int q = threadIdx.x + j * blockDim.x;
+      if (q < nchunks) reinterpret_cast<uint4*>(s_tile)[q] = nxt[j];
     }
     __syncthreads();
+    prefetch(tile + gridDim.x);
     float best = -INFINITY;
     int bi = C;
     if (r < n) {
@@ -606,7 +626,9 @@ void launch_pairs(const at::Tensor& preds_, const at::Tensor& target, int64_t n,
       const int threads = std::min(1024, 2048 / (int)sizeof(scalar_t));
       const int tile_rows = threads >> glog;
       const size_t shm_t = (size_t)acc_words * 4 + (size_t)tile_rows * C * sizeof(scalar_t);
-      hipLaunchKernelGGL((mc_pairs_argmax_staged_kernel<scalar_t, Acc>), grid_for(n, tile_rows, 2048), threads, shm_t, stream(), p,
+      const int64_t ntiles = (n + tile_rows - 1) / tile_rows;
+      const int sgrid = (int)std::max<int64_t>(1, std::min<int64_t>(ntiles, std::max<int64_t>(512, ntiles / 2)));
+      hipLaunchKernelGGL((mc_pairs_argmax_staged_kernel<scalar_t, Acc>), std::min(sgrid, 2048), threads, shm_t, stream(), p,
                          t, n, C, glog, acc_words, ignore_index, has_ignore, acc, err_t);
     } else if (vec_ok && C <= kWave * VEC) {
       hipLaunchKernelGGL((mc_pairs_argmax_vec_kernel<scalar_t, 1, Acc>), grid_for(n * kWave / 4, 512, 2048), 512, shm,
