@@ -44,7 +44,12 @@ class RetrievalMetric(Metric, ABC):
         if indexes is None:
             raise ValueError("Argument `indexes` cannot be None")
         indexes, preds, target = _check_retrieval_inputs(
-            indexes, preds, target, allow_non_binary_target=self.allow_non_binary_target, ignore_index=self.ignore_index
+            indexes,
+            preds,
+            target,
+            allow_non_binary_target=self.allow_non_binary_target,
+            ignore_index=self.ignore_index,
+            sink=self._validation_sink(target),
         )
         self.indexes.append(indexes)
         self.preds.append(preds)

@@ -27,14 +27,20 @@ def _check_same_shape(preds: Tensor, target: Tensor) -> None:
 
 
 def _check_retrieval_target_and_prediction_types(
-    preds: Tensor, target: Tensor, allow_non_binary_target: bool = False
+    preds: Tensor, target: Tensor, allow_non_binary_target: bool = False, sink: Optional[Any] = None
 ) -> Tuple[Tensor, Tensor]:
+    """``sink`` (a ``DeferredChecks``): the binary-target check becomes a device flag raised at ``compute`` instead
+    of two host synchronisations per update; bool targets are binary by construction and skip it."""
     if target.dtype not in (torch.bool, torch.long, torch.int) and not torch.is_floating_point(target):
         raise ValueError("`target` must be a tensor of booleans, integers or floats")
     if not preds.is_floating_point():
         raise ValueError("`preds` must be a tensor of floats")
-    if not allow_non_binary_target and (target.max() > 1 or target.min() < 0):
-        raise ValueError("`target` must contain `binary` values")
+    if not allow_non_binary_target and target.dtype != torch.bool:
+        if sink is None:
+            if target.max() > 1 or target.min() < 0:
+                raise ValueError("`target` must contain `binary` values")
+        else:
+            sink.add((target > 1) | (target < 0), ValueError, "`target` must contain `binary` values")
     target = target.float() if target.is_floating_point() else target.long()
     return preds.float().flatten(), target.flatten()
 
@@ -55,6 +61,7 @@ def _check_retrieval_inputs(
     target: Tensor,
     allow_non_binary_target: bool = False,
     ignore_index: Optional[int] = None,
+    sink: Optional[Any] = None,
 ) -> Tuple[Tensor, Tensor, Tensor]:
     if indexes.shape != preds.shape or preds.shape != target.shape:
         raise ValueError("`indexes`, `preds` and `target` must be of the same shape")
@@ -65,7 +72,7 @@ def _check_retrieval_inputs(
         indexes, preds, target = indexes[keep], preds[keep], target[keep]
     if not indexes.numel() or not indexes.size():
         raise ValueError("`indexes`, `preds` and `target` must be non-empty and non-scalar tensors")
-    preds, target = _check_retrieval_target_and_prediction_types(preds, target, allow_non_binary_target)
+    preds, target = _check_retrieval_target_and_prediction_types(preds, target, allow_non_binary_target, sink)
     return indexes.long().flatten(), preds, target
 
 
