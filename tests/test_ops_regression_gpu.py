@@ -111,3 +111,39 @@ def test_regression_sums_single_column(dtype, op):
     ref = torch.stack([pc.sum(), tc.sum(), (pc * pc).sum(), (tc * tc).sum(), (pc * tc).sum(), (d * d).sum(), d.abs().sum()])
     torch.testing.assert_close(flat[:7, 0].cpu(), ref, rtol=1e-4 if dtype != torch.float64 else 1e-10, atol=1e-6)
     assert tiled.shape == ref_tiled.shape == (8, 1)
+
+
+@pytest.mark.parametrize("cls", ["MeanMetric", "SumMetric", "MaxMetric", "MinMetric"])
+@pytest.mark.parametrize("strategy", ["warn", "ignore", "error", 0.5])
+def test_aggregation_nan_policy_without_host_sync(cls, strategy):
+    """GPU aggregation: NaN policy applied on device (neutralised entries, deferred warn / error at compute); the
+    values match the CPU module, Python-scalar values and weights included."""
+    import warnings
+
+    import torchmetrics_forked_amd as tm
+
+    mk = getattr(tm.aggregation, cls)
+    mg, mc = mk(nan_strategy=strategy).cuda(), mk(nan_strategy=strategy)
+    g = torch.Generator().manual_seed(2)
+    batches = [torch.randn(100, generator=g), torch.randn(50, generator=g)]
+    batches[1][[3, 17]] = float("nan")
+    if strategy == "error":
+        mg.update(batches[1].cuda())
+        with pytest.raises(RuntimeError, match="nan"):
+            mg.compute()
+        return
+    with warnings.catch_warnings(record=True) as wg:
+        warnings.simplefilter("always")
+        for b in batches:
+            if cls == "MeanMetric":
+                mg.update(b.cuda(), 2.0)
+                mc.update(b, 2.0)
+            else:
+                mg.update(b.cuda())
+                mc.update(b)
+        mg.update(1.5)
+        mc.update(1.5)
+        out_g = mg.compute().cpu()
+    torch.testing.assert_close(out_g, mc.compute(), rtol=1e-6, atol=1e-6)
+    warned = any("nan" in str(w.message) for w in wg)
+    assert warned == (strategy == "warn")

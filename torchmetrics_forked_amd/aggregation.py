@@ -42,19 +42,40 @@ class BaseAggregator(Metric):
         self.add_state(state_name, default=default_value, dist_reduce_fx=fn)
         self.state_name = state_name
 
+    # value that neutralises a NaN entry in this aggregation (sum/mean: 0 with weight 0, max: -inf, min: +inf);
+    # None = the entry must be removed (cat), which needs the host to know the new length
+    _nan_neutral: Optional[float] = None
+
     def _as_float_tensor(self, x: Union[float, Tensor]) -> Tensor:
-        return x if isinstance(x, Tensor) else torch.as_tensor(x, dtype=torch.float32, device=self.device)
+        if isinstance(x, Tensor):
+            return x
+        # a fill kernel, not a pageable host-to-device copy (which blocks the host on the GPU)
+        return torch.full((), float(x), dtype=torch.float32, device=self.device)
 
     def _cast_and_nan_check_input(
         self, x: Union[float, Tensor], weight: Optional[Union[float, Tensor]] = None
     ) -> Tuple[Tensor, Tensor]:
-        """Convert to float tensors and apply the NaN policy (filters NaNs for error-free strategies)."""
+        """Convert to float tensors and apply the NaN policy (filters NaNs for error-free strategies).
+
+        On the GPU with deferred validation (the default there) the policy runs without a host sync: "error" /
+        "warn" become device flags raised / warned at ``compute``, and NaN entries are neutralised in place (sum /
+        mean: value and weight 0; max / min: -inf / +inf) instead of being removed by boolean indexing."""
         x = self._as_float_tensor(x)
         weight = torch.ones_like(x) if weight is None else self._as_float_tensor(weight)
         bad = torch.isnan(x) | torch.isnan(weight)
         if isinstance(self.nan_strategy, float):
             x = torch.where(bad, torch.full_like(x, self.nan_strategy), x)
             weight = torch.where(bad, torch.full_like(weight, self.nan_strategy), weight)
+            return x.float(), weight.float()
+        sink = self._validation_sink(x) if self._nan_neutral is not None else None
+        if sink is not None:
+            if self.nan_strategy == "error":
+                sink.add(bad, RuntimeError, "Encountered `nan` values in tensor")
+            elif self.nan_strategy == "warn":
+                sink.add(bad, UserWarning, "Encountered `nan` values in tensor. Will be removed.")
+            if self.nan_strategy in ("warn", "ignore"):
+                x = torch.where(bad, torch.full_like(x, self._nan_neutral), x)
+                weight = torch.where(bad, torch.zeros_like(weight), weight)
             return x.float(), weight.float()
         if self.nan_strategy in ("error", "warn") and bool(bad.any()):
             if self.nan_strategy == "error":
@@ -77,6 +98,7 @@ class MaxMetric(BaseAggregator):
 
     full_state_update: bool = True
     max_value: Tensor
+    _nan_neutral = float("-inf")
 
     def __init__(self, nan_strategy: Union[str, float] = "warn", **kwargs: Any) -> None:
         super().__init__("max", -torch.tensor(float("inf")), nan_strategy, state_name="max_value", **kwargs)
@@ -95,6 +117,7 @@ class MinMetric(BaseAggregator):
 
     full_state_update: bool = True
     min_value: Tensor
+    _nan_neutral = float("inf")
 
     def __init__(self, nan_strategy: Union[str, float] = "warn", **kwargs: Any) -> None:
         super().__init__("min", torch.tensor(float("inf")), nan_strategy, state_name="min_value", **kwargs)
@@ -112,6 +135,7 @@ class SumMetric(BaseAggregator):
     """Running sum of all values seen."""
 
     sum_value: Tensor
+    _nan_neutral = 0.0
 
     def __init__(self, nan_strategy: Union[str, float] = "warn", **kwargs: Any) -> None:
         super().__init__("sum", torch.tensor(0.0), nan_strategy, state_name="sum_value", **kwargs)
@@ -147,6 +171,7 @@ class MeanMetric(BaseAggregator):
 
     mean_value: Tensor
     weight: Tensor
+    _nan_neutral = 0.0
 
     def __init__(self, nan_strategy: Union[str, float] = "warn", **kwargs: Any) -> None:
         super().__init__("sum", torch.tensor(0.0), nan_strategy, state_name="mean_value", **kwargs)

@@ -67,7 +67,7 @@ class BinaryCalibrationError(_CalibrationBase):
 
     def update(self, preds: Tensor, target: Tensor) -> None:
         if self.validate_args:
-            _binary_calibration_error_tensor_validation(preds, target, self.ignore_index)
+            _binary_calibration_error_tensor_validation(preds, target, self.ignore_index, self._validation_sink(target))
         preds, target = binary_format(preds, target, 0.0, self.ignore_index, convert_to_labels=False)
         _ce_bin_update(preds, target, self.n_bins, self.bins)
 
@@ -108,7 +108,9 @@ class MulticlassCalibrationError(_CalibrationBase):
             _mc_calibration_fused(preds, target, self.n_bins, self.bins, scratch, self.ignore_index, err)
             return
         if self.validate_args:
-            _multiclass_calibration_error_tensor_validation(preds, target, self.num_classes, self.ignore_index)
+            _multiclass_calibration_error_tensor_validation(
+                preds, target, self.num_classes, self.ignore_index, self._validation_sink(target)
+            )
         preds, target = multiclass_format(preds, target, self.ignore_index, convert_to_labels=False)
         if _multiclass_calibration_bins(preds, target, self.n_bins, self.bins):
             return

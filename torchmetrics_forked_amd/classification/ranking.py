@@ -36,7 +36,7 @@ class _RankingBase(Metric):
 
     def update(self, preds: Tensor, target: Tensor) -> None:
         if self.validate_args:
-            _multilabel_ranking_tensor_validation(preds, target, self.num_labels, self.ignore_index)
+            _multilabel_ranking_tensor_validation(preds, target, self.num_labels, self.ignore_index, self._validation_sink(target))
         preds, target = _ranking_format(preds, target, self.num_labels, self.ignore_index)
         measure, n = type(self)._update_fn(preds, target)
         self.measure += measure

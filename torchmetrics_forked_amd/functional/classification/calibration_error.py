@@ -87,8 +87,10 @@ def _binary_calibration_error_arg_validation(n_bins: int, norm: str = "l1", igno
         raise ValueError(f"Expected argument `ignore_index` to either be `None` or an integer, but got {ignore_index}")
 
 
-def _binary_calibration_error_tensor_validation(preds: Tensor, target: Tensor, ignore_index: Optional[int] = None) -> None:
-    _binary_stat_scores_tensor_validation(preds, target, "global", ignore_index)
+def _binary_calibration_error_tensor_validation(
+    preds: Tensor, target: Tensor, ignore_index: Optional[int] = None, sink: Optional[DeferredChecks] = None
+) -> None:
+    _binary_stat_scores_tensor_validation(preds, target, "global", ignore_index, sink)
     if not preds.is_floating_point():
         raise ValueError(
             "Expected argument `preds` to be floating tensor with probabilities/logits"

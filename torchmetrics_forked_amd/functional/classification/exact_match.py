@@ -28,7 +28,7 @@ def _multiclass_exact_match_update(
         preds = torch.where(target == ignore_index, torch.full_like(preds, ignore_index), preds)
     correct = (preds == target).sum(1) == preds.shape[1]
     correct = correct if multidim_average == "samplewise" else correct.sum()
-    total = torch.tensor(preds.shape[0] if multidim_average == "global" else 1, device=correct.device)
+    total = torch.full((), preds.shape[0] if multidim_average == "global" else 1, dtype=torch.long, device=correct.device)
     return correct, total
 
 

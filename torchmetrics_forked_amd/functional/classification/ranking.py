@@ -5,7 +5,7 @@ per row).  Here every row is ranked at once: ``rank_j = #{k : p_k >= p_j}`` (the
 via one batched ``sort`` + ``searchsorted``; the within-relevant rank uses the same search on a copy whose
 non-relevant entries are pushed to ``+inf``.
 """
-from typing import Optional, Tuple
+from typing import Any, Optional, Tuple
 
 import torch
 from torch import Tensor
@@ -25,8 +25,10 @@ def _ranking_reduce(score: Tensor, num_elements: int) -> Tensor:
     return score / num_elements
 
 
-def _multilabel_ranking_tensor_validation(preds: Tensor, target: Tensor, num_labels: int, ignore_index: Optional[int] = None) -> None:
-    _multilabel_stat_scores_tensor_validation(preds, target, num_labels, "global", ignore_index)
+def _multilabel_ranking_tensor_validation(
+    preds: Tensor, target: Tensor, num_labels: int, ignore_index: Optional[int] = None, sink: Optional[Any] = None
+) -> None:
+    _multilabel_stat_scores_tensor_validation(preds, target, num_labels, "global", ignore_index, sink)
     if not preds.is_floating_point():
         raise ValueError(f"Expected preds tensor to be floating point, but received input with dtype {preds.dtype}")
 

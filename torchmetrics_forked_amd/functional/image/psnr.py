@@ -27,7 +27,7 @@ def _psnr_update(preds: Tensor, target: Tensor, dim: Optional[Union[int, Tuple[i
     if dim is None:
         sums = fused_sums(preds, target, flatten=True)
         sse = sums[5, 0].to(preds.dtype) if sums is not None else torch.sum(torch.pow(preds - target, 2))
-        return sse, tensor(target.numel(), device=target.device)
+        return sse, torch.full((), target.numel(), dtype=torch.long, device=target.device)  # fill, not an H2D copy
     diff = preds - target
     sse = torch.sum(diff * diff, dim=dim)
     dims = [dim] if isinstance(dim, int) else list(dim)

@@ -111,8 +111,9 @@ def _ssim_update(
             w1 = _gaussian(gks[0], sigma[0], torch.float32, device).reshape(-1)
         else:
             w1 = torch.full((window[0],), 1.0 / window[0], dtype=torch.float32, device=device)
-        consts = torch.stack([torch.as_tensor(c1, device=device, dtype=torch.float32),
-                              torch.as_tensor(c2, device=device, dtype=torch.float32)])
+        # fill kernels for Python-float constants (a pageable host-to-device copy would block the host)
+        consts = torch.stack([c.to(device, torch.float32) if isinstance(c, torch.Tensor) else torch.full((), float(c), device=device)
+                              for c in (c1, c2)])
         b, c, h, w = preds.shape
         sums = torch.ops.tmx.ssim_sums(preds.reshape(b * c, h, w), target.reshape(b * c, h, w), w1, w1, consts)
         n_valid = c * (h - window[0] + 1) * (w - window[1] + 1)

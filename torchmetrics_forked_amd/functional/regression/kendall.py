@@ -101,7 +101,7 @@ def _column_stats(x: Tensor, y: Tensor) -> Tuple[Tensor, ...]:
 def _get_metric_metadata(preds: Tensor, target: Tensor, variant: _MetricVariant) -> Tuple:
     cols = [_column_stats(preds[:, i], target[:, i]) for i in range(preds.shape[1])]
     stack = [torch.stack([torch.as_tensor(c[k], device=preds.device) for c in cols]) for k in range(10)]
-    return tuple(stack) + (torch.tensor(preds.shape[0], device=preds.device),)
+    return tuple(stack) + (torch.full((), preds.shape[0], dtype=torch.long, device=preds.device),)
 
 
 def _calculate_tau(con: Tensor, dis: Tensor, n_total: Tensor, ties_x: Tensor, ties_y: Tensor, ux: Tensor, uy: Tensor,

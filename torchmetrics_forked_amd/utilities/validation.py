@@ -11,6 +11,7 @@ SURVEY §0 fact 6).  On MI355X that stalls the HIP stream once or twice per step
   raising the same exception type and message.
 """
 import os
+import warnings
 from typing import Callable, Dict, List, Optional, Tuple, Type
 
 import torch
@@ -60,9 +61,15 @@ class DeferredChecks:
         flags = torch.cat([self._flags[k].reshape(1).to(torch.int32).cpu() for k in keys])  # one host sync
         for k in keys:
             self._flags[k].zero_()
+        errors = []
         for k, f in zip(keys, flags.tolist()):
             if f:
-                raise k[0](k[1])
+                if issubclass(k[0], Warning):  # deferred warnings (e.g. aggregation nan_strategy="warn")
+                    warnings.warn(k[1], k[0], stacklevel=3)
+                else:
+                    errors.append(k)
+        if errors:
+            raise errors[0][0](errors[0][1])
 
     def clear(self) -> None:
         for f in self._flags.values():
