@@ -67,20 +67,21 @@ def _multilabel_ranking_average_precision_update(preds: Tensor, target: Tensor) 
     return per_row.sum(), num_preds
 
 
-def _multilabel_ranking_loss_update(preds: Tensor, target: Tensor) -> Tuple[Tensor, int]:
+def _multilabel_ranking_loss_update(preds: Tensor, target: Tensor) -> Tuple[Tensor, Tensor]:
+    """Reference semantics (rows with no or only relevant labels are dropped; an all-degenerate batch counts as
+    loss 0 over 1 sample) computed with masks instead of boolean indexing, so the GPU update never waits on the
+    host for the number of kept rows."""
     num_preds, num_labels = preds.shape
     relevant = target == 1
     num_relevant = relevant.sum(dim=1)
     mask = (num_relevant > 0) & (num_relevant < num_labels)
-    preds, relevant, num_relevant = preds[mask], relevant[mask], num_relevant[mask]
-    if len(preds) == 0:
-        return torch.tensor(0.0, device=preds.device), 1
     inverse = preds.argsort(dim=1, stable=True).argsort(dim=1, stable=True)
     per_label_loss = ((num_labels - inverse) * relevant).to(torch.float32)
     correction = 0.5 * num_relevant * (num_relevant + 1)
-    denom = num_relevant * (num_labels - num_relevant)
-    loss = (per_label_loss.sum(dim=1) - correction) / denom
-    return loss.sum(), num_preds
+    denom = (num_relevant * (num_labels - num_relevant)).clamp(min=1)
+    loss = torch.where(mask, (per_label_loss.sum(dim=1) - correction) / denom, torch.zeros((), device=preds.device))
+    n = torch.where(mask.any(), torch.full((), num_preds, device=preds.device), torch.ones((), dtype=torch.long, device=preds.device))
+    return loss.sum(), n
 
 
 def _validate(preds: Tensor, target: Tensor, num_labels: int, ignore_index: Optional[int]) -> None:
