@@ -1484,6 +1484,27 @@ at::Tensor curve_hist_reduce(const at::Tensor& hist_) {
 // binned (multi-threshold) curve:  confmat[T, C, 2, 2] += counts
 // bucket b(p) = #thresholds <= p  (p >= thr[i]  <=>  i < b(p));  hist[C][2][T+1] then suffix-sum.
 // =========================================================================================================
+// bucket b(p) = #thresholds <= p.  Thresholds are almost always linspace: guess from the spacing, verify with the
+// one or two neighbouring thresholds, and fall back to the binary search for any other spacing (exact either way).
+__device__ __forceinline__ int thr_bucket(float p, const float* __restrict__ s_thr, int nT, float t0, float inv_step) {
+  if (p != p) return 0;  // NaN: no threshold is <= NaN
+  float gf = (p - t0) * inv_step + 1.f;
+  gf = fminf(fmaxf(gf, 0.f), (float)nT);
+  const int g = (int)gf;
+#pragma unroll
+  for (int d = 0; d < 3; ++d) {
+    const int c = d == 0 ? g : (d == 1 ? g + 1 : g - 1);
+    if (c < 0 || c > nT) continue;
+    if ((c == 0 || s_thr[c - 1] <= p) && (c == nT || s_thr[c] > p)) return c;
+  }
+  int lo = 0, hi = nT;  // first index with thr > p
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (s_thr[mid] <= p) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
 template <typename T, int MODE>  // MODE 0: multiclass rows (softmax), 1: elementwise (sigmoid)
 __global__ void binned_hist_kernel(const T* __restrict__ preds, const int64_t* __restrict__ target, int64_t N, int C,
                                    int64_t S, const float* __restrict__ thr, int nT, const int* __restrict__ flag,
@@ -1493,14 +1514,9 @@ __global__ void binned_hist_kernel(const T* __restrict__ preds, const int64_t* _
   for (int i = threadIdx.x; i < nT; i += blockDim.x) s_thr[i] = thr[i];
   __syncthreads();
   const bool do_norm = flag[0] != 0;
-  auto bucket = [&](float p) {
-    int lo = 0, hi = nT;  // first index with thr > p
-    while (lo < hi) {
-      int mid = (lo + hi) >> 1;
-      if (s_thr[mid] <= p) lo = mid + 1; else hi = mid;
-    }
-    return lo;
-  };
+  const float t0 = s_thr[0];
+  const float inv_step = nT > 1 && s_thr[nT - 1] > t0 ? (float)(nT - 1) / (s_thr[nT - 1] - t0) : 0.f;
+  auto bucket = [&](float p) { return thr_bucket(p, s_thr, nT, t0, inv_step); };
   if constexpr (MODE == 0) {
     const int lane = threadIdx.x & (kWave - 1);
     const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / kWave;
@@ -1554,7 +1570,7 @@ __global__ void __launch_bounds__(kBinnedThreads) binned_hist_lds_kernel(const T
                                                                          int64_t N, int C, int64_t S, const float* __restrict__ thr,
                                                                          int nT, const int* __restrict__ flag, int64_t ignore_index,
                                                                          bool has_ignore, int copies, int* __restrict__ hist,
-                                                                         int* __restrict__ err) {
+                                                                         int* __restrict__ err, bool vec_ok) {
   bool bad = false;
   extern __shared__ __attribute__((aligned(16))) int s_mem[];  // [nT] thresholds as float, then [copies][C][2][nT + 1]
   float* s_thr = reinterpret_cast<float*>(s_mem);
@@ -1565,9 +1581,36 @@ __global__ void __launch_bounds__(kBinnedThreads) binned_hist_lds_kernel(const T
   for (int i = threadIdx.x; i < copies * H; i += kBinnedThreads) s_hist[i] = 0;
   __syncthreads();
   const bool do_norm = flag[0] != 0;
+  const float t0 = s_thr[0];
+  const float inv_step = nT > 1 && s_thr[nT - 1] > t0 ? (float)(nT - 1) / (s_thr[nT - 1] - t0) : 0.f;
   int* my = s_hist + (int)((threadIdx.x / kWave) % copies) * H;
   const int64_t total = N * C * S;
-  for (int64_t i = blockIdx.x * (int64_t)kBinnedThreads + threadIdx.x; i < total; i += (int64_t)gridDim.x * kBinnedThreads) {
+  int64_t start = 0;
+  if (C == 1 && vec_ok) {
+    // binary: 16-B loads of scores and targets (one label, so no per-element label arithmetic)
+    constexpr int VEC = 16 / sizeof(T);
+    using PP = Pack16<T, VEC>;
+    using TP = Pack16<int64_t, VEC>;
+    const int64_t nv = total / VEC;
+    for (int64_t v = blockIdx.x * (int64_t)kBinnedThreads + threadIdx.x; v < nv; v += (int64_t)gridDim.x * kBinnedThreads) {
+      const PP pv = reinterpret_cast<const PP*>(preds)[v];
+      const TP tv = reinterpret_cast<const TP*>(target)[v];
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) {
+        const int64_t t = tv.v[k];
+        if (has_ignore && t == ignore_index) continue;
+        if (t != 0 && t != 1) {
+          bad = true;
+          continue;
+        }
+        float x = to_f32<T>(pv.v[k]);
+        if (do_norm) x = round_trip<T>(1.f / (1.f + expf(-x)));
+        atomicAdd(my + (int)t * (nT + 1) + thr_bucket(x, s_thr, nT, t0, inv_step), 1);
+      }
+    }
+    start = nv * VEC;  // tail below, by every thread of the grid-stride loop
+  }
+  for (int64_t i = start + blockIdx.x * (int64_t)kBinnedThreads + threadIdx.x; i < total; i += (int64_t)gridDim.x * kBinnedThreads) {
     const int64_t t = target[i];
     if (has_ignore && t == ignore_index) continue;
     if (t != 0 && t != 1) {
@@ -1577,12 +1620,7 @@ __global__ void __launch_bounds__(kBinnedThreads) binned_hist_lds_kernel(const T
     const int l = static_cast<int>((i / S) % C);
     float v = to_f32<T>(preds[i]);
     if (do_norm) v = round_trip<T>(1.f / (1.f + expf(-v)));
-    int lo = 0, hi = nT;  // first index with thr > v
-    while (lo < hi) {
-      const int mid = (lo + hi) >> 1;
-      if (s_thr[mid] <= v) lo = mid + 1; else hi = mid;
-    }
-    atomicAdd(my + (l * 2 + (int)t) * (nT + 1) + lo, 1);
+    atomicAdd(my + (l * 2 + (int)t) * (nT + 1) + thr_bucket(v, s_thr, nT, t0, inv_step), 1);
   }
   if (bad && err) atomicOr(err, 1);
   __syncthreads();
@@ -1667,7 +1705,8 @@ void binned_curve_update(const at::Tensor& preds_, const at::Tensor& target_, co
         const int grid = static_cast<int>(std::min<int64_t>(1024, (total + kBinnedThreads - 1) / kBinnedThreads));
         hipLaunchKernelGGL(binned_hist_lds_kernel<scalar_t>, std::max(grid, 1), kBinnedThreads, shm_lds, stream(), p,
                            target.data_ptr<int64_t>(), N, C, S, thr.data_ptr<float>(), nT, flag.data_ptr<int>(), ignore_index,
-                           has_ignore, copies, hist.data_ptr<int>(), err);
+                           has_ignore, copies, hist.data_ptr<int>(), err,
+                           ((reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(target.data_ptr())) & 15) == 0);
         return;
       }
       hipLaunchKernelGGL((binned_hist_kernel<scalar_t, 1>), grid_for(total, block, 4096), block, shm, stream(), p,

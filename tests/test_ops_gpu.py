@@ -562,3 +562,26 @@ def test_multiclass_calibration_one_pass(C, dtype, probs):
     bad.update(torch.randn(64, C).to(dtype).cuda(), t.cuda())
     with pytest.raises(RuntimeError):
         bad.compute()
+
+
+@pytest.mark.parametrize("kind", ["linspace", "irregular", "single"])
+def test_binned_bucket_guess_exact(kind):
+    """Bucket lookup (arithmetic guess + neighbour check + binary-search fallback) matches the eager path, with
+    scores exactly on thresholds, outside [0, 1] neighbours, and NaN."""
+    T = {"linspace": 101, "irregular": 37, "single": 1}[kind]
+    if kind == "irregular":
+        thr = torch.sort(torch.rand(T, generator=torch.Generator().manual_seed(1)) ** 3).values
+    else:
+        thr = torch.linspace(0, 1, T)
+    p = torch.rand(20000, generator=torch.Generator().manual_seed(2))
+    p[:T] = thr  # exactly on each threshold
+    p[T : T + 3] = torch.tensor([0.0, 1.0, 0.5])
+    t = torch.randint(0, 2, (20000,), generator=torch.Generator().manual_seed(3))
+    for tensor_in in (p, p.reshape(4000, 5)):
+        C = 1 if tensor_in.ndim == 1 else 5
+        tt = t.reshape(tensor_in.shape)
+        cm = torch.zeros(T, C, 2, 2, dtype=torch.long)
+        pin = tensor_in.reshape(-1, 1, 1) if C == 1 else tensor_in
+        tin = tt.reshape(-1, 1, 1) if C == 1 else tt
+        g, c, _, _ = _both(K.binned_curve_update, pin, tin, thr, cm, "binary" if C == 1 else "multilabel", None)
+        assert torch.equal(g[3].cpu(), c[3])
