@@ -8,25 +8,52 @@ The timed window is exactly K steps followed by ONE ``compute()`` (cross-rank RC
 classes + confusion matrix), bracketed by barrier + device synchronize on both sides; the max over ranks is
 reported.  ``value`` = world_size * K / max_rank_seconds (whole-job aggregate, weak scaling: per-GPU batch fixed).
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W]   (N>1 under torch.distributed.run)
+Usage::
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config auroc|map|image|bert]
+
+* ``--gpus 1`` (default): one process.
+* ``--gpus N`` without ``WORLD_SIZE`` in the environment: this process launches ``torch.distributed.run`` with N
+  ranks on 127.0.0.1 as a child and exits with its code.  The launcher never touches the GPU itself.
+* under ``torch.distributed.run`` (``WORLD_SIZE``/``RANK``/``LOCAL_RANK`` set): one rank per GPU, RCCL
+  (``nccl`` backend) when a GPU is visible, gloo on CPU-only hosts.
+
+Secondary BASELINE configs (``--config map|image|bert``) are implemented in ``tools/config_bench.py`` and print one
+JSON line in the same format.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
-import torch
-import torch.distributed as dist
 
-BASELINE_UPDATES_PER_SEC = None  # filled from BASELINE.json "published" (none published) / measured ref
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _launch_ranks(n: int, argv: list) -> int:
+    """Run this script under ``torch.distributed.run`` with ``n`` local ranks (child process; no exec, no GPU)."""
+    cmd = [
+        sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+        "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__), *argv,
+    ]
+    env = dict(os.environ)
+    env.setdefault("OMP_NUM_THREADS", "4")
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
 
 
 def _baseline() -> "float | None":
-    """BASELINE.json publishes no number; BASELINE.md's config-2 row holds the reference measured on MI355X with
-    this same harness (per-GPU updates/s, ``profiles/reference_baseline_mi355x.json``).  Weak scaling: the
-    whole-node baseline for N GPUs is N x the 1-GPU reference rate (the reference cannot do better: its compute
-    gathers every rank's scores and sorts per class on every rank)."""
+    """BASELINE.json publishes no number.  BASELINE.md's config-2 row holds a builder-measured rate of the
+    unmodified reference on one MI355X under this same harness (``profiles/reference_baseline_mi355x.json``, per-GPU
+    updates/s).  Weak scaling: the whole-node baseline for N GPUs is N x that rate."""
     here = os.path.dirname(os.path.abspath(__file__))
     try:
         with open(os.path.join(here, "BASELINE.json")) as f:
@@ -42,11 +69,12 @@ def _baseline() -> "float | None":
         return None
 
 
-def main() -> None:
+def _parse(argv: list) -> argparse.Namespace:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="auroc", choices=["auroc", "map", "image", "bert"])
     ap.add_argument("--num-classes", type=int, default=1000)
     ap.add_argument("--batch", type=int, default=65536)
     ap.add_argument("--pool", type=int, default=4, help="distinct synthetic batches cycled through")
@@ -54,11 +82,19 @@ def main() -> None:
     ap.add_argument("--replicated-compute", action="store_true",
                     help="all-reduce the full histogram and compute every class on every rank (A/B against the default"
                          " class-sharded compute: reduce-scatter by class + all-gather of per-class AUROC)")
-    args = ap.parse_args()
+    ap.add_argument("--small", action="store_true", help="(secondary configs) reduced shapes for CPU smoke runs")
+    return ap.parse_args(argv)
+
+
+def _worker(args: argparse.Namespace) -> None:
+    import torch
+    import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print(f"[bench] --gpus {args.gpus} but WORLD_SIZE={world}: reporting the launched world size", file=sys.stderr)
     use_cuda = torch.cuda.is_available()
     if use_cuda:
         torch.cuda.set_device(local_rank)
@@ -67,6 +103,17 @@ def main() -> None:
         device = torch.device("cpu")
     if world > 1:
         dist.init_process_group("nccl" if use_cuda else "gloo", device_id=device if use_cuda else None)
+
+    if args.config != "auroc":
+        sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "tools"))
+        from config_bench import run_config
+
+        out = run_config(args, device, world, rank)
+        if rank == 0 and out is not None:
+            print(json.dumps(out), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
 
     import torchmetrics_forked_amd as tm
     from torchmetrics_forked_amd import ops
@@ -153,15 +200,25 @@ def main() -> None:
                 "parallelism": f"dp{world}",
             },
             "update_only_ms_per_step": round(upd_ms / args.steps, 4) if use_cuda else None,
-            "compute_incl_sync_ms": round(1000.0 * elapsed - (upd_ms if use_cuda else 0.0), 3),
+            "compute_incl_sync_ms": round(1000.0 * elapsed - (upd_ms if use_cuda else 0.0), 3) if use_cuda else None,
             "auroc": float(res["auroc"]),
             "fused_update": not args.no_fuse,
             "sharded_compute": world > 1 and not args.replicated_compute,
+            "backend": (dist.get_backend() if world > 1 else None),
             "device": torch.cuda.get_device_name(device) if use_cuda else "cpu",
         }
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def main() -> None:
+    argv = sys.argv[1:]
+    args = _parse(argv)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # launcher: N ranks as a child process group; this process never initialises the GPU
+        sys.exit(_launch_ranks(args.gpus, argv))
+    _worker(args)
 
 
 if __name__ == "__main__":

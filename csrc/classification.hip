@@ -1144,7 +1144,8 @@ __global__ void __launch_bounds__(256) curve_hist_mc_kernel(const T* __restrict_
 
 template <typename T, bool PADDED>
 void launch_two_pass(const T* p, const int64_t* target, int64_t n, int C, int ld, int* mode, int* state, bool speculative,
-                     int64_t ignore_index, bool has_ignore, int64_t* hist, int64_t* cm, int* err, const at::TensorOptions& opts) {
+                     int64_t ignore_index, bool has_ignore, int64_t* hist, int64_t* cm, int* err, const at::TensorOptions& opts,
+                     int* code_range) {
   TORCH_CHECK(n < (int64_t{1} << 31), "curve_hist_update: more than 2^31 rows in one batch");
   const int64_t n_pad = (n + kTileRows - 1) / kTileRows * kTileRows;
   auto codes = at::empty({(int64_t)C * n_pad}, opts.dtype(at::kShort));
@@ -1179,7 +1180,7 @@ void launch_two_pass(const T* p, const int64_t* target, int64_t n, int C, int ld
   while ((int64_t)C * splits < 512 && n_pad / (8 * (splits * 2)) >= 1024) splits *= 2;
   hipLaunchKernelGGL((class_hist_kernel<T, false>), C * splits, kClassThreads, kCodes * sizeof(uint32_t), stream(),
                      reinterpret_cast<const uint16_t*>(codes.data_ptr()), n_pad, splits, hist, p, ld, target, n, mode, speculative,
-                     srows, state, cm);
+                     srows, state, cm, code_range);
   TMX_LAUNCH_CHECK();
 }
 
@@ -1276,9 +1277,22 @@ __global__ void __launch_bounds__(kBinThreads) binary_hist_kernel(const T* __res
 void curve_hist_update(const at::Tensor& preds_, const at::Tensor& target_, at::Tensor& hist, int64_t task,
                        int64_t ignore_index, bool has_ignore, c10::optional<at::Tensor> confmat,
                        c10::optional<at::Tensor> norm_flag, c10::optional<at::Tensor> err_flag,
-                       c10::optional<at::Tensor> mode_state) {
+                       c10::optional<at::Tensor> mode_state, c10::optional<at::Tensor> code_range) {
   TORCH_CHECK(hist.is_contiguous() && hist.scalar_type() == at::kLong && hist.dim() == 3 && hist.size(1) == 2 &&
               hist.size(2) == kCodes, "hist must be int64 [C, 2, 16384]");
+  // code_range (int32[2], optional): the occupied code range [lo, hi] of ``hist``.  The two-pass routes widen it
+  // in the class pass; every other route (rare shapes) marks it as the full range, so it is always conservative.
+  int* crange = nullptr;
+  bool range_tracked = false;
+  if (code_range.has_value()) {
+    TORCH_CHECK(code_range->scalar_type() == at::kInt && code_range->numel() == 2 && code_range->is_contiguous() &&
+                code_range->device() == hist.device(), "code_range must be int32[2] on the histogram's device");
+    crange = code_range->data_ptr<int>();
+  }
+  struct RangeGuard {  // on exit, routes that did not track the range widen it to everything
+    c10::optional<at::Tensor>& r; bool& tracked;
+    ~RangeGuard() { if (r.has_value() && !tracked) { r->narrow(0, 0, 1).fill_(0); r->narrow(0, 1, 1).fill_(kCodes - 1); } }
+  } range_guard{code_range, range_tracked};
   auto preds = preds_.contiguous();
   auto target = target_.contiguous().to(at::kLong);
   const int C = static_cast<int>(hist.size(0));
@@ -1313,7 +1327,7 @@ void curve_hist_update(const at::Tensor& preds_, const at::Tensor& target_, at::
     const scalar_t* p = reinterpret_cast<const scalar_t*>(preds.data_ptr());
     if (task == 0) {
       const int64_t n = target.numel();
-      if (n == 0) return;
+      if (n == 0) { range_tracked = true; return; }
       TORCH_CHECK(preds.numel() == n * C, "preds must be [N, C]");
       if (two_pass_ok) {
         if (C % 8 != 0) {
@@ -1321,11 +1335,13 @@ void curve_hist_update(const at::Tensor& preds_, const at::Tensor& target_, at::
           const at::Tensor padded = at::constant_pad_nd(preds.view({n, C}), {0, ld - C}, 0).contiguous();
           launch_two_pass<scalar_t, true>(reinterpret_cast<const scalar_t*>(padded.data_ptr()), target.data_ptr<int64_t>(), n, C,
                                           ld, flag.data_ptr<int>(), state.data_ptr<int>(), speculative, ignore_index, has_ignore,
-                                          hist.data_ptr<int64_t>(), cm, err, preds.options());
+                                          hist.data_ptr<int64_t>(), cm, err, preds.options(), crange);
         } else {
           launch_two_pass<scalar_t, false>(p, target.data_ptr<int64_t>(), n, C, C, flag.data_ptr<int>(), state.data_ptr<int>(),
-                                           speculative, ignore_index, has_ignore, hist.data_ptr<int64_t>(), cm, err, preds.options());
+                                           speculative, ignore_index, has_ignore, hist.data_ptr<int64_t>(), cm, err, preds.options(),
+                                           crange);
         }
+        range_tracked = true;
         return;
       }
       const int grid = grid_for(n * kWave, block, 4096);
@@ -1342,7 +1358,7 @@ void curve_hist_update(const at::Tensor& preds_, const at::Tensor& target_, at::
       }
     } else {
       const int64_t total = target.numel();
-      if (total == 0) return;
+      if (total == 0) { range_tracked = true; return; }
       TORCH_CHECK(preds.numel() == total, "preds/target size mismatch");
       const int64_t N = target.size(0);
       const int64_t S = total / (N * C);
@@ -1381,7 +1397,8 @@ void curve_hist_update(const at::Tensor& preds_, const at::Tensor& target_, at::
         hipLaunchKernelGGL((class_hist_kernel<scalar_t, true>), C * splits, kClassThreads, kCodes * sizeof(uint32_t), stream(),
                            reinterpret_cast<const uint16_t*>(cptr), n_pad, splits, hist.data_ptr<int64_t>(), p, C,
                            target.data_ptr<int64_t>(), N, flag.data_ptr<int>(), false, static_cast<const int*>(nullptr),
-                           state.data_ptr<int>(), static_cast<int64_t*>(nullptr));
+                           state.data_ptr<int>(), static_cast<int64_t*>(nullptr), crange);
+        range_tracked = true;
         return;
       }
       hipLaunchKernelGGL(curve_hist_ml_kernel<scalar_t>, grid_for(total, block, 4096), block, 0, stream(), p,
@@ -1409,20 +1426,44 @@ __device__ __forceinline__ long long shfl_up_i64(long long v, int off) {
   return (static_cast<long long>(hi) << 32) | static_cast<unsigned int>(lo);
 }
 
-__global__ void __launch_bounds__(kRedThreads) curve_hist_reduce_kernel(const int64_t* __restrict__ hist, double* __restrict__ out) {
+__global__ void __launch_bounds__(kRedThreads) curve_hist_reduce_kernel(const int64_t* __restrict__ hist,
+                                                                         const int* __restrict__ code_range,
+                                                                         double* __restrict__ out) {
   constexpr int K = kCodes;
   constexpr int kWaves = kRedThreads / kWave;
   const int c = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
-  const int64_t base = K - kRedPer * (tid + 1);  // lowest code owned by this thread
-  const longlong2* negv = reinterpret_cast<const longlong2*>(hist + ((int64_t)c * 2 + 0) * K + base);
-  const longlong2* posv = reinterpret_cast<const longlong2*>(hist + ((int64_t)c * 2 + 1) * K + base);
+  // only the occupied code range [lo, hi] is read (softmax scores fill about a fifth of the codes); thread t owns
+  // the q consecutive codes hi - q t, ..., hi - q t - q + 1 (descending order = thread order)
+  int lo = 0, hi = K - 1;
+  if (code_range != nullptr) {
+    lo = max(code_range[0], 0);
+    hi = min(code_range[1], K - 1);
+  }
+  const int R = hi >= lo ? hi - lo + 1 : 0;
+  const int q = (R + kRedThreads - 1) / kRedThreads;  // <= kRedPer
+  const int64_t* negh = hist + ((int64_t)c * 2 + 0) * K;
+  const int64_t* posh = hist + ((int64_t)c * 2 + 1) * K;
   long long p[kRedPer], n[kRedPer];  // index i = i-th highest owned code
+  const int top = hi - q * tid;
+  if (q == kRedPer) {  // full range: 16-B loads, as before
+    const int64_t base = top - (kRedPer - 1);
+    const longlong2* negv = reinterpret_cast<const longlong2*>(negh + base);
+    const longlong2* posv = reinterpret_cast<const longlong2*>(posh + base);
 #pragma unroll
-  for (int v = 0; v < kRedPer / 2; ++v) {
-    const longlong2 a = posv[v], b = negv[v];
-    p[kRedPer - 1 - 2 * v] = a.x; p[kRedPer - 2 - 2 * v] = a.y;
-    n[kRedPer - 1 - 2 * v] = b.x; n[kRedPer - 2 - 2 * v] = b.y;
+    for (int v = 0; v < kRedPer / 2; ++v) {
+      const longlong2 a = posv[v], b = negv[v];
+      p[kRedPer - 1 - 2 * v] = a.x; p[kRedPer - 2 - 2 * v] = a.y;
+      n[kRedPer - 1 - 2 * v] = b.x; n[kRedPer - 2 - 2 * v] = b.y;
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < kRedPer; ++i) {
+      const int code = top - i;
+      const bool ok = i < q && code >= lo;
+      p[i] = ok ? posh[code] : 0;
+      n[i] = ok ? negh[code] : 0;
+    }
   }
   long long sp = 0, sn = 0;
 #pragma unroll
@@ -1468,14 +1509,20 @@ __global__ void __launch_bounds__(kRedThreads) curve_hist_reduce_kernel(const in
   }
 }
 
-at::Tensor curve_hist_reduce(const at::Tensor& hist_) {
+at::Tensor curve_hist_reduce(const at::Tensor& hist_, c10::optional<at::Tensor> code_range) {
   auto hist = hist_.contiguous();
   TORCH_CHECK(hist.scalar_type() == at::kLong && hist.dim() == 3 && hist.size(1) == 2 && hist.size(2) == kCodes,
               "curve_hist_reduce: hist must be int64 [C, 2, 16384]");
+  const int* cr = nullptr;
+  if (code_range.has_value()) {
+    TORCH_CHECK(code_range->scalar_type() == at::kInt && code_range->numel() == 2 && code_range->is_contiguous() &&
+                code_range->device() == hist.device(), "code_range must be int32[2] on the histogram's device");
+    cr = code_range->data_ptr<int>();
+  }
   const int C = static_cast<int>(hist.size(0));
   auto out = at::empty({C, 4}, hist.options().dtype(at::kDouble));
   if (C == 0) return out;
-  hipLaunchKernelGGL(curve_hist_reduce_kernel, C, kRedThreads, 0, stream(), hist.data_ptr<int64_t>(), out.data_ptr<double>());
+  hipLaunchKernelGGL(curve_hist_reduce_kernel, C, kRedThreads, 0, stream(), hist.data_ptr<int64_t>(), cr, out.data_ptr<double>());
   TMX_LAUNCH_CHECK();
   return out;
 }
@@ -2115,8 +2162,8 @@ TORCH_LIBRARY_FRAGMENT(tmx, m) {
   m.def("mc_stat_scores_update(Tensor preds, Tensor target, int num_classes, Tensor(a!) tp, Tensor(b!) fp, Tensor(c!) tn, Tensor(d!) fn, Tensor(e!) ticket, int ignore_index, bool has_ignore, bool micro, Tensor(f!)? err_t=None, Tensor(g!)? err_p=None) -> ()");
   m.def("binary_stats_fused(Tensor preds, Tensor target, Tensor(a!) tp, Tensor(b!) fp, Tensor(c!) tn, Tensor(d!) fn, Tensor(e!) scratch, int num_labels, float threshold, int ignore_index, bool has_ignore, Tensor(f!)? err_t=None, Tensor(g!)? err_p=None) -> ()");
   m.def("binary_stats_update(Tensor preds, Tensor target, Tensor(a!) counts, int num_labels, float threshold, int ignore_index, bool has_ignore) -> ()");
-  m.def("curve_hist_update(Tensor preds, Tensor target, Tensor(a!) hist, int task, int ignore_index, bool has_ignore, Tensor(b!)? confmat, Tensor? norm_flag, Tensor(c!)? err_flag, Tensor(d!)? mode_state) -> ()");
-  m.def("curve_hist_reduce(Tensor hist) -> Tensor");
+  m.def("curve_hist_update(Tensor preds, Tensor target, Tensor(a!) hist, int task, int ignore_index, bool has_ignore, Tensor(b!)? confmat, Tensor? norm_flag, Tensor(c!)? err_flag, Tensor(d!)? mode_state, Tensor(e!)? code_range=None) -> ()");
+  m.def("curve_hist_reduce(Tensor hist, Tensor? code_range=None) -> Tensor");
   m.def("binned_curve_update(Tensor preds, Tensor target, Tensor thresholds, Tensor(a!) confmat, int task, int ignore_index, bool has_ignore, Tensor? norm_flag, Tensor(b!)? err_flag=None) -> ()");
   m.def("ce_bins_update(Tensor conf, Tensor acc, Tensor boundaries, Tensor(a!) bins) -> ()");
   m.def("mc_calibration_update(Tensor preds, Tensor target, Tensor boundaries, Tensor(a!) bins) -> ()");

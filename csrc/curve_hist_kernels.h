@@ -578,10 +578,12 @@ constexpr int64_t kClassChunk = 65528;  // rows per LDS flush: a 16-bit half nev
 
 template <bool PACKED>
 __device__ __forceinline__ void class_flush(uint32_t* __restrict__ s_h, int64_t* __restrict__ neg_hist,
-                                            int64_t* __restrict__ pos_hist, bool exclusive) {
+                                            int64_t* __restrict__ pos_hist, bool exclusive, int& lo, int& hi) {
   for (int i = threadIdx.x; i < kCodes; i += kClassThreads) {
     const uint32_t w = s_h[i];
     if (w) {
+      lo = min(lo, i);
+      hi = max(hi, i);
       const uint32_t neg = PACKED ? (w & 0xFFFFu) : w, pos = PACKED ? (w >> 16) : 0u;
       if (exclusive) {
         if (neg) neg_hist[i] += neg;
@@ -601,9 +603,11 @@ __global__ void __launch_bounds__(kClassThreads) class_hist_kernel(const uint16_
                                                                    const int64_t* __restrict__ target, int64_t n,
                                                                    int* __restrict__ mode, bool speculative,
                                                                    const int* __restrict__ slow_rows, int* __restrict__ state,
-                                                                   int64_t* __restrict__ confmat) {
+                                                                   int64_t* __restrict__ confmat, int* __restrict__ code_range) {
   extern __shared__ __attribute__((aligned(16))) uint32_t s_h[];  // [kCodes]: neg, or neg (lo 16) | pos (hi 16)
   __shared__ int s_info[4];
+  __shared__ int s_range[2];
+  int lo = kCodes, hi = -1;  // occupied code range this thread touched (compute() then scans only that range)
   const int C = gridDim.x / splits;
   const int c = blockIdx.x / splits, sp = blockIdx.x % splits;
   if (threadIdx.x == 0) {  // the row-pass kernels are complete (stream order)
@@ -611,6 +615,8 @@ __global__ void __launch_bounds__(kClassThreads) class_hist_kernel(const uint16_
     s_info[1] = speculative ? mode[1] : mode[0];
     s_info[2] = state[0];
     s_info[3] = state[1];
+    s_range[0] = kCodes;
+    s_range[1] = -1;
   }
   uint4* s4 = reinterpret_cast<uint4*>(s_h);
   for (int i = threadIdx.x; i < kCodes / 4; i += kClassThreads) s4[i] = make_uint4(0, 0, 0, 0);
@@ -638,14 +644,17 @@ __global__ void __launch_bounds__(kClassThreads) class_hist_kernel(const uint16_
           const uint32_t x = (k & 1) ? (parts[k >> 1] >> 16) : (parts[k >> 1] & 0xFFFFu);
           if (x & 0x8000u) continue;
           if constexpr (PACKED) atomicAdd(&s_h[x & 0x3FFFu], (x & 0x4000u) ? 0x10000u : 1u);
-          else if (x & 0x4000u) atomic_add_i64(pos_hist + (x & 0x3FFFu), 1);
-          else atomicAdd(&s_h[x & 0x3FFFu], 1u);
+          else if (x & 0x4000u) {
+            atomic_add_i64(pos_hist + (x & 0x3FFFu), 1);
+            lo = min(lo, (int)(x & 0x3FFFu));
+            hi = max(hi, (int)(x & 0x3FFFu));
+          } else atomicAdd(&s_h[x & 0x3FFFu], 1u);
         }
       }
     }
     if (ce < v1) {  // more rows than one chunk: flush before a 16-bit half can overflow
       __syncthreads();
-      class_flush<PACKED>(s_h, neg_hist, pos_hist, exclusive);
+      class_flush<PACKED>(s_h, neg_hist, pos_hist, exclusive, lo, hi);
       __syncthreads();
     }
   }
@@ -661,6 +670,8 @@ __global__ void __launch_bounds__(kClassThreads) class_hist_kernel(const uint16_
       if ((lst == 1 ? m1 : m0) != 0) continue;  // softmax of a NaN / inf row: all NaN, every code skipped
       const uint32_t code = raw_code<T>(bits16<T>(preds[r * ld + c]));
       if (code & 0x8000u) continue;
+      lo = min(lo, (int)code);
+      hi = max(hi, (int)code);
       if (target[r] == c) atomic_add_i64(pos_hist + code, 1);
       else atomic_add_i64(neg_hist + code, 1);
     }
@@ -688,7 +699,20 @@ __global__ void __launch_bounds__(kClassThreads) class_hist_kernel(const uint16_
   }
   __syncthreads();
   // rare-row codes went to the int64 bins by atomics: then the last flush must be atomic too
-  class_flush<PACKED>(s_h, neg_hist, pos_hist, exclusive && n0 + n1 == 0);
+  class_flush<PACKED>(s_h, neg_hist, pos_hist, exclusive && n0 + n1 == 0, lo, hi);
+  if (code_range != nullptr) {
+    lo = wave_min_i32(lo);
+    hi = wave_max_i32(hi);
+    if ((threadIdx.x & (kWave - 1)) == 0 && hi >= 0) {
+      atomicMin(&s_range[0], lo);
+      atomicMax(&s_range[1], hi);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0 && s_range[1] >= 0) {
+      atomicMin(code_range, s_range[0]);
+      atomicMax(code_range + 1, s_range[1]);
+    }
+  }
   if (threadIdx.x == 0) {
     // No fence: the only ordering needed is "every block's read of mode / counts happened before the reset", and
     // each block consumed those values (s_info, above) before taking its ticket.  (An agent-scope release here writes

@@ -72,6 +72,17 @@ __device__ __forceinline__ long long wave_sum(long long v) {
   return v;
 }
 
+__device__ __forceinline__ int wave_min_i32(int v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = min(v, __shfl_xor(v, off, kWave));
+  return v;
+}
+__device__ __forceinline__ int wave_max_i32(int v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = max(v, __shfl_xor(v, off, kWave));
+  return v;
+}
+
 // (value, index) arg-max reduction across a wave; ties -> lowest index, NaN counts as +inf-beyond-inf.
 __device__ __forceinline__ void wave_argmax(float& v, int& idx) {
 #pragma unroll

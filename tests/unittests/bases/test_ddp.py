@@ -212,6 +212,7 @@ def _narrow_hist_worker(rank, world):
             m.update(torch.randn(16, 3).softmax(-1).bfloat16(), torch.randint(0, 3, (16,)))
             if big:
                 m.score_hist[:, 0, 5] += 2**31 - 10  # summed over ranks: beyond int32
+                m._invalidate_range()  # in-place edit of the internal histogram
             local = m.score_hist.clone()
             locals_ = [torch.zeros_like(local) for _ in range(world)]
             torch.distributed.all_gather(locals_, local)

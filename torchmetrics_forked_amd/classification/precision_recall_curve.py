@@ -93,7 +93,42 @@ class _CurveMetric(Metric):
     def _ensure_hist(self, device: torch.device) -> Tensor:
         if self.score_hist.numel() == 0:
             self.score_hist = torch.zeros(self._num, 2, eng.N_CODES, dtype=torch.long, device=device)
+            self._set_range(self.score_hist, torch.tensor([eng.N_CODES, -1], dtype=torch.int32, device=device))
         return self.score_hist
+
+    # ---- occupied code range of ``score_hist`` ------------------------------------------------------------
+    # ``_code_range`` (int32[2] = [lo, hi], on the histogram's device) is widened by the class-pass kernel of every
+    # update; ``compute`` and the histogram collectives then touch only [lo, hi] (softmax scores fill a few binades,
+    # about a fifth of the 16384 codes).  It belongs to the tensor object in ``_range_hist``: when ``score_hist`` is
+    # replaced by anything that does not maintain it (load_state_dict, forward's merge, .to(...)), the range is
+    # recomputed on device from the histogram at its next use — one pass, no host sync.  ``score_hist`` is internal
+    # state; code that edits it in place must call ``_invalidate_range()``.
+    _range_hist: Optional[Tensor] = None
+    _code_range: Optional[Tensor] = None
+    _rows_bound: Optional[int] = None  # rows counted into the tracked histogram: bounds every bin (host int)
+
+    def _set_range(self, hist: Tensor, rng: Tensor, rows: Optional[int] = 0) -> None:
+        self._range_hist = hist
+        self._code_range = rng
+        self._rows_bound = rows
+
+    def _invalidate_range(self) -> None:
+        self._range_hist = None
+        self._code_range = None
+        self._rows_bound = None
+
+    def _tracked_range(self) -> Optional[Tensor]:
+        """The occupied-code range of the current histogram (a device tensor; recomputed when stale)."""
+        hist = self.score_hist
+        if not isinstance(hist, Tensor) or hist.numel() == 0:
+            return None
+        if self._range_hist is hist and self._code_range is not None and self._code_range.device == hist.device:
+            return self._code_range
+        occ = hist.amax(dim=(0, 1)) > 0
+        idx = torch.arange(hist.shape[-1], device=hist.device)
+        rng = torch.stack([torch.where(occ, idx, hist.shape[-1]).amin(), torch.where(occ, idx, -1).amax()]).to(torch.int32)
+        self._set_range(hist, rng, None)
+        return rng
 
     def _curve_update(
         self, preds: Tensor, target: Tensor, confmat_out: Optional[Tensor] = None, err_flag: Optional[Tensor] = None
@@ -122,13 +157,22 @@ class _CurveMetric(Metric):
         if self._hist_ok(preds):
             hist = self._ensure_hist(preds.device)
             self._hist_dtype = preds.dtype
+            rng = self._tracked_range() if hist.is_cuda else None
             if self._task == "binary":
-                cls_ops.curve_hist_update(preds.reshape(-1, 1, 1), target.reshape(-1, 1, 1), hist, "binary", ii, err_flag=err_flag)
+                cls_ops.curve_hist_update(
+                    preds.reshape(-1, 1, 1), target.reshape(-1, 1, 1), hist, "binary", ii, err_flag=err_flag, code_range=rng
+                )
             elif self._task == "multiclass":
                 p = torch.movedim(preds, 1, -1).reshape(-1, self._num)
-                cls_ops.curve_hist_update(p, target.reshape(-1), hist, "multiclass", ii, confmat_out, err_flag, self._mode_state(p))
+                cls_ops.curve_hist_update(
+                    p, target.reshape(-1), hist, "multiclass", ii, confmat_out, err_flag, self._mode_state(p), code_range=rng
+                )
             else:
-                cls_ops.curve_hist_update(preds, target, hist, "multilabel", ii, err_flag=err_flag)
+                cls_ops.curve_hist_update(preds, target, hist, "multilabel", ii, err_flag=err_flag, code_range=rng)
+            if rng is None:
+                self._invalidate_range()
+            elif self._rows_bound is not None:
+                self._rows_bound += preds.numel() // self._num
             return
         if self.score_hist.numel() > 0:
             raise NotImplementedError(
@@ -180,14 +224,8 @@ class _CurveMetric(Metric):
         full = sl.to(torch.int32) if narrow else sl.contiguous()
         if per * world != c:
             full = torch.cat([full, full.new_zeros(per * world - c, *full.shape[1:])])
-        backend = dist.get_backend(group) if group is not None else dist.get_backend()
         shard = full.new_empty(per, *full.shape[1:])
-        if backend == "nccl":
-            _collective(dist.reduce_scatter_tensor, shard, full.contiguous(), op=dist.ReduceOp.SUM, what="reduce_scatter(score_hist)", group=group)
-        else:  # gloo has no reduce-scatter: same result through an all-reduce
-            red = full.clone()
-            _collective(dist.all_reduce, red, op=dist.ReduceOp.SUM, what="all_reduce(score_hist)", group=group)
-            shard.copy_(red[rank * per : (rank + 1) * per])
+        _collective(dist.reduce_scatter_tensor, shard, full.contiguous(), op=dist.ReduceOp.SUM, what="reduce_scatter(score_hist)", group=group)
         others = {k: v for k, v in self.metric_state.items() if k != "score_hist"}
         for name, val in sync_states(others, self._reductions, group=group).items():
             setattr(self, name, val)
@@ -196,12 +234,17 @@ class _CurveMetric(Metric):
         hist = torch.zeros(owned, 2, self.score_hist.shape[-1], dtype=torch.long, device=self.score_hist.device)
         hist[:, :, lo : hi + 1] = shard[:owned]
         self.score_hist = hist
+        self._set_range(hist, torch.tensor([lo, hi], dtype=torch.int32, device=hist.device), None)
         self._shard_info = (first, owned, per, group)
 
     def unsync(self, should_unsync: bool = True) -> None:
         super().unsync(should_unsync)
         if should_unsync:
             self._shard_info = None
+            saved = getattr(self, "_range_saved", None)
+            if saved is not None:
+                self._range_hist, self._code_range, self._rows_bound = saved
+                self._range_saved = None
 
     def _sharded_scores(self) -> Tuple[Tensor, Tensor, Tensor, Tensor]:
         """(auroc, ap, P, N) for all classes from this rank's class shard + one small all-gather."""
@@ -209,48 +252,70 @@ class _CurveMetric(Metric):
         world = dist.get_world_size(group)
         local = torch.zeros(4, per, dtype=torch.float64, device=self.score_hist.device)
         if owned > 0:
-            auc, ap, pos, neg = eng.hist_scores(self.score_hist)
+            auc, ap, pos, neg = eng.hist_scores(self.score_hist, self._tracked_range())
             local[0, :owned], local[1, :owned] = auc.double(), ap.double()
             local[2, :owned], local[3, :owned] = pos.double(), neg.double()
         backend = dist.get_backend(group) if group is not None else dist.get_backend()
         comm = local if backend == "nccl" or not local.is_cuda else local.cpu()
-        parts = [torch.empty_like(comm) for _ in range(world)]
-        _collective(dist.all_gather, parts, comm, what="all_gather(per-class scores)", group=group)
-        allv = torch.cat(parts, dim=1)[:, : self._num].to(local.device)
+        allv = comm.new_empty(world, 4, per)
+        _collective(dist.all_gather_into_tensor, allv.view(-1), comm.reshape(-1), what="all_gather(per-class scores)", group=group)
+        allv = allv.permute(1, 0, 2).reshape(4, world * per)[:, : self._num].to(local.device)
         return allv[0], allv[1], allv[2], allv[3]
 
+    _DTYPE_CODES = {None: 0, torch.bfloat16: 1, torch.float16: 2}
+
     def _sync_dist(self, dist_sync_fn: Any = None, process_group: Optional[Any] = None) -> None:
-        """The exact histogram travels (a) as int32 whenever the summed per-rank maximum bin proves every global
-        bin fits (131 MB instead of 262 MB at C=1000) and (b) only over the code range ``[lo, hi]`` that some rank
-        occupies: softmax scores fill a few bf16 binades, about a fifth of the 16384 codes.  One tiny all-gather of
-        (has-histogram, max bin, lo, hi) per rank decides both; the per-code maxima behind them are one pass."""
+        """The exact histogram travels (a) as int32 whenever the summed per-rank bin bounds prove every global
+        bin fits (half the bytes) and (b) only over the code range ``[lo, hi]`` some rank occupies: softmax scores
+        fill a few bf16 binades, about a fifth of the 16384 codes.  One tiny all-gather of per-rank (has-histogram,
+        bin bound, lo, hi, score dtype, has-samples) decides both and checks that the ranks agree on the state kind.
+        The bin bound is the number of rows counted (host-tracked); only a histogram of unknown origin (loaded,
+        merged) pays a device max over its bins.  Ranks without a histogram adopt the score dtype of the others."""
         if self.thresholds is None:
             group = process_group or self.process_group
             backend = dist.get_backend(group) if group is not None else dist.get_backend()
             dev = self.score_hist.device if backend != "nccl" or self.score_hist.is_cuda else torch.device("cuda")
             has = self.score_hist.numel() > 0
             k = eng.N_CODES
+            dcode = self._DTYPE_CODES.get(self._hist_dtype if has else None, 0)
+            has_samples = int(isinstance(self.preds, list) and len(self.preds) > 0)
             if has:
-                per_code = self.score_hist.amax(dim=(0, 1))
-                idx = torch.arange(k, device=per_code.device)
-                occ = per_code > 0
-                stats = torch.stack([
-                    torch.ones((), dtype=torch.long, device=per_code.device), per_code.amax(),
-                    torch.where(occ, idx, k).amin(), torch.where(occ, idx, -1).amax(),
+                rng = self._tracked_range()
+                if self._rows_bound is not None:
+                    bound = torch.tensor([self._rows_bound], dtype=torch.long, device=rng.device)
+                else:
+                    bound = self.score_hist.amax().reshape(1)
+                stats = torch.cat([
+                    torch.ones(1, dtype=torch.long, device=rng.device), bound.long(), rng.long(),
+                    torch.tensor([dcode, has_samples], dtype=torch.long, device=rng.device),
                 ])
             else:
-                stats = torch.tensor([0, 0, k, -1], dtype=torch.long, device=dev)
+                stats = torch.tensor([0, 0, k, -1, 0, has_samples], dtype=torch.long, device=dev)
             stats = stats.to(dev if backend == "nccl" else "cpu")
-            parts = [torch.empty_like(stats) for _ in range(dist.get_world_size(group))]
-            _collective(dist.all_gather, parts, stats, what="all_gather(histogram stats)", group=group)
-            allv = torch.stack(parts).tolist()
+            allv = torch.empty(dist.get_world_size(group), stats.numel(), dtype=stats.dtype, device=stats.device)
+            _collective(dist.all_gather_into_tensor, allv.view(-1), stats, what="all_gather(histogram stats)", group=group)
+            allv = allv.tolist()
             used, bound = sum(v[0] for v in allv), sum(v[1] for v in allv)
             lo, hi = min(v[2] for v in allv), max(v[3] for v in allv)
-            if used and self.score_hist.numel() == 0:
-                self._ensure_hist(self.device)
+            dcodes = {v[4] for v in allv if v[0]}
+            if len(dcodes) > 1:
+                raise RuntimeError(
+                    "Ranks accumulated curve scores in different 16-bit dtypes (bf16 on some, fp16 on others); their"
+                    " exact histograms cannot be combined. Cast the inputs to one dtype on every rank."
+                )
+            if used and any(v[5] for v in allv):
+                raise RuntimeError(
+                    "Some ranks hold 16-bit score histograms and others fp32/fp64 score lists for the same curve metric;"
+                    " cast the inputs to one dtype on every rank."
+                )
+            if used and not has:
+                self._hist_dtype = {v: kk for kk, v in self._DTYPE_CODES.items()}[dcodes.pop()]
             narrow = used > 0 and bound < 2**31 - 1
             if hi < lo:  # no rank counted anything: keep one bin so the collectives stay well-formed
                 lo = hi = 0
+            if used and self.score_hist.numel() == 0:
+                self._ensure_hist(self.device)
+            self._range_saved = (self._range_hist, self._code_range, self._rows_bound)
             if self._shardable(dist_sync_fn):
                 self._sync_sharded(group, narrow, lo, hi)
                 return
@@ -265,6 +330,7 @@ class _CurveMetric(Metric):
                     hist = torch.zeros(shape, dtype=torch.long, device=synced.device)
                     hist[:, :, lo : hi + 1] = synced
                     self.score_hist = hist
+                    self._set_range(hist, torch.tensor([lo, hi], dtype=torch.int32, device=hist.device), bound)
                 return
         super()._sync_dist(dist_sync_fn, process_group)
 
@@ -274,7 +340,7 @@ class _CurveMetric(Metric):
             cm = self.confmat.unsqueeze(1) if self._task == "binary" else self.confmat
             return ("binned", cm)
         if isinstance(self.score_hist, Tensor) and self.score_hist.numel() > 0:
-            return ("hist", self.score_hist, self._hist_dtype or torch.bfloat16)
+            return ("hist", self.score_hist, self._hist_dtype or torch.bfloat16, self._tracked_range())
         return ("samples", dim_zero_cat(self.preds), dim_zero_cat(self.target))
 
     def plot(

@@ -35,9 +35,10 @@ def codes_to_values(dtype: torch.dtype, device: torch.device) -> Tensor:
 # ---------------------------------------------------------------------------------------------------------
 # reductions (AUROC / AP for all classes at once)
 # ---------------------------------------------------------------------------------------------------------
-def hist_scores(hist: Tensor) -> Tuple[Tensor, Tensor, Tensor, Tensor]:
-    """(auroc, ap, n_pos, n_neg) per class from an exact histogram ``[C, 2, K]`` (float64)."""
-    out = cls_ops.curve_hist_reduce(hist)
+def hist_scores(hist: Tensor, code_range: Optional[Tensor] = None) -> Tuple[Tensor, Tensor, Tensor, Tensor]:
+    """(auroc, ap, n_pos, n_neg) per class from an exact histogram ``[C, 2, K]`` (float64); bins outside
+    ``code_range`` ([lo, hi], when given) are known to be empty and are not read."""
+    out = cls_ops.curve_hist_reduce(hist, code_range)
     return out[:, 0], out[:, 1], out[:, 2], out[:, 3]
 
 

@@ -62,7 +62,7 @@ class _NullRange:
 _NULL_RANGE = _NullRange()
 from torchmetrics_forked_amd.utilities.plot import _AX_TYPE, _PLOT_OUT_TYPE, plot_single_or_multi_val
 from torchmetrics_forked_amd.utilities.prints import rank_zero_warn
-from torchmetrics_forked_amd.utilities.validation import DeferredChecks, make_sink
+from torchmetrics_forked_amd.utilities.validation import DeferredChecks, host_checks, make_sink
 
 _STR_REDUCTIONS = {
     "sum": dim_zero_sum,
@@ -241,10 +241,18 @@ class Metric(Module, ABC):
             raise TorchMetricsUserError(
                 "The Metric shouldn't be synced when performing ``forward``. HINT: Did you forget to call ``unsync`` ?."
             )
-        if self.full_state_update or self.full_state_update is None or self.dist_sync_on_step:
-            self._forward_cache = self._forward_full_state_update(*args, **kwargs)
-        else:
-            self._forward_cache = self._forward_reduce_state_update(*args, **kwargs)
+        full = self.full_state_update or self.full_state_update is None or self.dist_sync_on_step
+        if self._deferred is None:
+            self._forward_cache = (self._forward_full_state_update if full else self._forward_reduce_state_update)(*args, **kwargs)
+            return self._forward_cache
+        # the batch value's compute checks (and clears) only the batch's deferred flags; the ones accumulated by
+        # earlier update() calls are kept for the user's compute()
+        snap = self._deferred.snapshot()
+        self._deferred.clear()
+        try:
+            self._forward_cache = (self._forward_full_state_update if full else self._forward_reduce_state_update)(*args, **kwargs)
+        finally:
+            self._deferred.restore(snap)
         return self._forward_cache
 
     def _enter_batch_mode(self) -> bool:
@@ -387,7 +395,10 @@ class Metric(Module, ABC):
         if async_op:
             if dist_sync_fn is not None and dist_sync_fn is not gather_all_tensors:
                 raise TorchMetricsUserError("`async_op=True` uses the coalesced sync engine; a custom `dist_sync_fn` is not supported.")
-            pending = sync_states_async(self.metric_state, self._reductions, group=process_group or self.process_group)
+            pending = sync_states_async(
+                self.metric_state, self._reductions, group=process_group or self.process_group,
+                timeout=getattr(self, "sync_timeout", None),
+            )
             return _MetricPendingSync(self, pending)
         self._cache = self.metric_state
         with _range(f"tmx/{self.__class__.__name__}.sync"), sync_timeout(getattr(self, "sync_timeout", None)):
@@ -448,17 +459,24 @@ class Metric(Module, ABC):
                 )
             if self._computed is not None:
                 return self._computed
-            if self._deferred is not None:
-                self._deferred.check()
-            with _range(f"tmx/{self.__class__.__name__}.compute"), self.sync_context(
-                dist_sync_fn=self.dist_sync_fn, should_sync=self._to_sync, should_unsync=self._should_unsync
-            ):
-                value = _squeeze_if_scalar(compute(*args, **kwargs))
-            if self.compute_with_cache:
-                self._computed = value
+            # every host-side consequence of device flags (deferred input checks, degenerate-class warnings, ...)
+            # is read once, when the outermost compute (or MetricCollection.compute) ends
+            with host_checks() as batch:
+                if self._deferred is not None:
+                    self._deferred.check()
+                with _range(f"tmx/{self.__class__.__name__}.compute"), self.sync_context(
+                    dist_sync_fn=self.dist_sync_fn, should_sync=self._to_sync, should_unsync=self._should_unsync
+                ):
+                    value = _squeeze_if_scalar(compute(*args, **kwargs))
+                if self.compute_with_cache:
+                    self._computed = value
+                    batch.on_error(self._drop_computed)
             return value
 
         return wrapped_func
+
+    def _drop_computed(self) -> None:
+        self._computed = None
 
     @abstractmethod
     def update(self, *_: Any, **__: Any) -> None:

@@ -165,8 +165,12 @@ def curve_hist_update(
     confmat: Optional[Tensor] = None,
     err_flag: Optional[Tensor] = None,
     mode_state: Optional[Tensor] = None,
+    code_range: Optional[Tensor] = None,
 ) -> None:
     """Accumulate the exact 16-bit score histogram ``hist[C, 2, 16384]`` (see csrc/classification.hip).
+
+    ``code_range`` (int32[2] on the GPU, optional) is widened to cover every code this batch touched, so
+    :func:`curve_hist_reduce` and the histogram collectives can skip the never-occupied codes.
 
     ``task="multiclass"``: preds ``[N, C]`` scores (softmax applied if any value outside [0,1]), target ``[N]``;
     optionally also accumulates the argmax confusion matrix (fused plan).  ``task="multilabel"``/``"binary"``:
@@ -181,7 +185,7 @@ def curve_hist_update(
         norm = None if (mode_state is not None and task == "multiclass") else _norm_flag(preds, target, task, ignore_index)
         torch.ops.tmx.curve_hist_update(
             preds, target, hist, tcode, -1 if ignore_index is None else ignore_index, ignore_index is not None, confmat,
-            norm, err_flag, mode_state,
+            norm, err_flag, mode_state, code_range,
         )
         return
     C = hist.shape[0]
@@ -219,10 +223,12 @@ def curve_hist_update(
     hist += torch.bincount(flat.reshape(-1), minlength=hist.numel()).reshape(hist.shape)
 
 
-def curve_hist_reduce(hist: Tensor) -> Tensor:
-    """float64 ``[C, 4]`` = (auroc, average_precision, n_pos, n_neg) per class, from ``hist[C, 2, K]``."""
+def curve_hist_reduce(hist: Tensor, code_range: Optional[Tensor] = None) -> Tensor:
+    """float64 ``[C, 4]`` = (auroc, average_precision, n_pos, n_neg) per class, from ``hist[C, 2, K]``.
+
+    ``code_range`` (int32[2] ``[lo, hi]``, GPU): every bin outside it is known to be zero and is not read."""
     if ops.use_native(hist):
-        return torch.ops.tmx.curve_hist_reduce(hist)
+        return torch.ops.tmx.curve_hist_reduce(hist, code_range)
     neg = hist[:, 0].flip(-1).double()
     pos = hist[:, 1].flip(-1).double()
     tp = pos.cumsum(-1)

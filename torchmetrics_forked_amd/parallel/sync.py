@@ -199,8 +199,8 @@ def _to_bytes(t: Tensor) -> Tensor:
 
 
 def _from_bytes(buf: Tensor, dtype: torch.dtype, shape: Sequence[int]) -> Tensor:
-    if dtype == torch.bool:
-        return buf.view(torch.uint8).reshape(shape).to(torch.bool)
+    if buf.numel() == 0:
+        return torch.empty(shape, dtype=dtype, device=buf.device)
     return buf.view(dtype).reshape(shape)
 
 
@@ -208,10 +208,22 @@ def _pad16(n: int) -> int:
     return (n + _ALIGN - 1) // _ALIGN * _ALIGN
 
 
+def _gather_flat(buf: Tensor, world: int, what: str, group: Optional[Any]) -> Tensor:
+    """All-gather equal-sized 1-D buffers into one ``(world, n)`` tensor (one RCCL / gloo collective)."""
+    out = buf.new_empty(world, buf.numel())
+    _collective(dist.all_gather_into_tensor, out.view(-1), buf, what=what, group=group)
+    return out
+
+
 def all_gather_packed(
     groups: List[List[Tensor]], group: Optional[Any], device_hint: Optional[Tensor] = None
 ) -> List[List[List[Tensor]]]:
     """Gather several lists of tensors (of arbitrary, per-rank-varying shapes/lengths) from every rank.
+
+    Two collectives in total, whatever the number of tensors: a fixed-size header (element count per slot and
+    payload bytes) and one padded buffer holding this rank's shape table followed by every tensor's bytes at
+    16-byte aligned offsets.  The only host reads are the header and the shape tables (one small copy each); the
+    returned tensors are views into the gathered buffer (no per-element copies or ``.item()`` calls).
 
     Args:
         groups: ``groups[s]`` is this rank's list of tensors for slot ``s`` (same number of slots on every rank).
@@ -228,71 +240,63 @@ def all_gather_packed(
                 break
     comm_dev = _comm_device(sample, group)
 
-    # 1) header: element count per slot
-    counts = torch.tensor([len(lst) for lst in groups], dtype=torch.int64, device=comm_dev)
-    all_counts = [torch.empty_like(counts) for _ in range(world)]
-    _collective(dist.all_gather, all_counts, counts, what="all_gather(element counts)", group=group)
-    all_counts_h = torch.stack(all_counts).cpu()  # (world, slots) - tiny host read
-    max_elems = int(all_counts_h.sum(1).max().item()) if n_slots else 0
-    if max_elems == 0:
-        return [[[] for _ in range(world)] for _ in range(n_slots)]
-
-    # 2) shape table: per element [dtype, ndim, nbytes, dims...]
-    rec = 3 + _MAX_DIMS
-    table = torch.zeros(max_elems, rec, dtype=torch.int64)
     flat_elems: List[Tensor] = [t for lst in groups for t in lst]
-    payload_sizes = []
-    for i, t in enumerate(flat_elems):
+    rec = 3 + _MAX_DIMS
+    rows: List[List[int]] = []
+    payload = 0
+    for t in flat_elems:
         if t.ndim > _MAX_DIMS:
             raise ValueError(f"metric state with ndim={t.ndim} > {_MAX_DIMS} cannot be synced")
         nbytes = t.numel() * t.element_size()
-        table[i, 0] = _DTYPE_CODE[t.dtype]
-        table[i, 1] = t.ndim
-        table[i, 2] = nbytes
-        table[i, 3 : 3 + t.ndim] = torch.tensor(list(t.shape), dtype=torch.int64)
-        payload_sizes.append(_pad16(nbytes))
-    table = table.to(comm_dev)
-    all_tables = [torch.empty_like(table) for _ in range(world)]
-    _collective(dist.all_gather, all_tables, table, what="all_gather(shape table)", group=group)
-    tables_h = [tb.cpu() for tb in all_tables]
+        rows.append([_DTYPE_CODE[t.dtype], t.ndim, nbytes, *t.shape] + [0] * (_MAX_DIMS - t.ndim))
+        payload += _pad16(nbytes)
 
-    # 3) payload: one padded byte buffer per rank
-    rank_bytes = []
-    for r in range(world):
-        n = int(all_counts_h[r].sum().item())
-        rank_bytes.append(sum(_pad16(int(tables_h[r][i, 2].item())) for i in range(n)))
-    max_bytes = max(max(rank_bytes), _ALIGN)
-    pieces: List[Tensor] = []
-    used = 0
-    for t, sz in zip(flat_elems, payload_sizes):
+    # 1) header: element count per slot + payload bytes of this rank
+    header = torch.tensor([len(lst) for lst in groups] + [payload], dtype=torch.int64, device=comm_dev)
+    hdr = _gather_flat(header, world, "all_gather(element counts)", group).tolist()
+    counts = [row[:n_slots] for row in hdr]
+    max_elems = max(sum(c) for c in counts) if n_slots else 0
+    if max_elems == 0:
+        return [[[] for _ in range(world)] for _ in range(n_slots)]
+    table_bytes = _pad16(max_elems * rec * 8)
+    span = table_bytes + max(max(row[n_slots] for row in hdr), _ALIGN)
+
+    # 2) one buffer per rank: [shape table | payload], padded to the largest rank
+    table = torch.zeros(table_bytes // 8, dtype=torch.int64)
+    if rows:
+        table[: len(rows) * rec] = torch.tensor(rows, dtype=torch.int64).reshape(-1)
+    pieces: List[Tensor] = [table.view(torch.uint8).to(comm_dev)]
+    used = table_bytes
+    for t in flat_elems:
         b = _to_bytes(t).to(comm_dev)
         pieces.append(b)
-        if sz > b.numel():
-            pieces.append(torch.zeros(sz - b.numel(), dtype=torch.uint8, device=comm_dev))
-        used += sz
-    if max_bytes > used:
-        pieces.append(torch.zeros(max_bytes - used, dtype=torch.uint8, device=comm_dev))
-    buf = torch.cat(pieces)
-    gathered = [torch.empty_like(buf) for _ in range(world)]
-    _collective(dist.all_gather, gathered, buf, what="all_gather(packed states)", group=group)
+        pad = _pad16(b.numel()) - b.numel()
+        if pad:
+            pieces.append(torch.zeros(pad, dtype=torch.uint8, device=comm_dev))
+        used += b.numel() + pad
+    if span > used:
+        pieces.append(torch.zeros(span - used, dtype=torch.uint8, device=comm_dev))
+    gathered = _gather_flat(torch.cat(pieces), world, "all_gather(packed states)", group)
+    tables = gathered[:, :table_bytes].cpu().view(torch.int64)[:, : max_elems * rec].reshape(world, max_elems, rec).tolist()
 
-    # 4) unpack
-    slot_devices = []
-    for lst in groups:
-        slot_devices.append(lst[0].device if lst else (sample.device if sample is not None else torch.device("cpu")))
+    # 3) unpack as views of the gathered buffer (moved once per slot device when it differs)
+    by_dev: Dict[torch.device, Tensor] = {torch.device(comm_dev): gathered}
     result: List[List[List[Tensor]]] = [[[] for _ in range(world)] for _ in range(n_slots)]
+    for s, lst in enumerate(groups):
+        dev = lst[0].device if lst else (sample.device if sample is not None else torch.device("cpu"))
+        if dev not in by_dev:
+            by_dev[dev] = gathered.to(dev)
     for r in range(world):
-        tb = tables_h[r]
-        off = 0
+        tb = tables[r]
+        off = table_bytes
         e = 0
-        for s in range(n_slots):
-            for _ in range(int(all_counts_h[r, s].item())):
-                dtype = _DTYPES[int(tb[e, 0])]
-                ndim = int(tb[e, 1])
-                nbytes = int(tb[e, 2])
-                shape = [int(v) for v in tb[e, 3 : 3 + ndim]]
-                piece = gathered[r][off : off + nbytes].clone() if nbytes else torch.empty(0, dtype=torch.uint8, device=comm_dev)
-                result[s][r].append(_from_bytes(piece, dtype, shape).to(slot_devices[s]))
+        for s, lst in enumerate(groups):
+            dev = lst[0].device if lst else (sample.device if sample is not None else torch.device("cpu"))
+            src = by_dev[dev][r]
+            out = result[s][r]
+            for _ in range(counts[r][s]):
+                code, ndim, nbytes = tb[e][0], tb[e][1], tb[e][2]
+                out.append(_from_bytes(src[off : off + nbytes], _DTYPES[code], tb[e][3 : 3 + ndim]))
                 off += _pad16(nbytes)
                 e += 1
     return result
@@ -378,9 +382,17 @@ class PendingSync:
     the packed all-gather of list / ``cat`` / ``None`` states (which needs a host-side length exchange) runs in
     :meth:`wait`.  ``wait`` returns the synchronised state dict."""
 
-    def __init__(self, states: Dict[str, StateT], reductions: Dict[str, Optional[Callable]], group: Optional[Any]) -> None:
+    def __init__(
+        self,
+        states: Dict[str, StateT],
+        reductions: Dict[str, Optional[Callable]],
+        group: Optional[Any],
+        timeout: Optional[float] = None,
+    ) -> None:
         self._group = group
         self._reductions = reductions
+        # the bound in force at launch (metric ``sync_timeout``, context or env) also bounds ``wait()``
+        self._timeout = timeout if timeout is not None else current_timeout()
         reduce_items, self._rest = [], {}
         for name, value in states.items():
             fn = reductions.get(name)
@@ -393,18 +405,24 @@ class PendingSync:
 
     def wait(self) -> Dict[str, StateT]:
         if self._result is None:
-            out = _finish_all_reduce(self._launched, self._group) if self._launched else {}
-            if self._rest:
-                out.update(sync_states(self._rest, {k: self._reductions.get(k) for k in self._rest}, self._group))
+            with sync_timeout(self._timeout):
+                out = _finish_all_reduce(self._launched, self._group) if self._launched else {}
+                if self._rest:
+                    out.update(sync_states(self._rest, {k: self._reductions.get(k) for k in self._rest}, self._group))
             self._result = out
         return self._result
 
 
 def sync_states_async(
-    states: Dict[str, StateT], reductions: Dict[str, Optional[Callable]], group: Optional[Any] = None
+    states: Dict[str, StateT],
+    reductions: Dict[str, Optional[Callable]],
+    group: Optional[Any] = None,
+    timeout: Optional[float] = None,
 ) -> PendingSync:
-    """Start synchronising ``states`` and return immediately (see :class:`PendingSync`)."""
-    return PendingSync(states, reductions, group)
+    """Start synchronising ``states`` and return immediately (see :class:`PendingSync`); ``timeout`` (else the
+    bound in force) limits both the launch and ``wait()``."""
+    with sync_timeout(timeout):
+        return PendingSync(states, reductions, group, timeout)
 
 
 def legacy_sync_states(

@@ -11,8 +11,10 @@ SURVEY §0 fact 6).  On MI355X that stalls the HIP stream once or twice per step
   raising the same exception type and message.
 """
 import os
+import threading
 import warnings
-from typing import Callable, Dict, List, Optional, Tuple, Type
+from contextlib import contextmanager
+from typing import Any, Callable, Dict, Iterator, List, Optional, Tuple, Type
 
 import torch
 from torch import Tensor
@@ -20,6 +22,99 @@ from torch import Tensor
 
 def validation_mode() -> str:
     return os.environ.get("TMX_VALIDATION", "auto")
+
+
+# ---------------------------------------------------------------------------------------------------------
+# one host read per compute()
+# ---------------------------------------------------------------------------------------------------------
+class HostCheckBatch:
+    """Device-side flags whose host-side consequences (raise / warn) wait for ONE device->host read.
+
+    ``compute()`` used to stall the stream once per check: the deferred input flags, the degenerate-class warnings,
+    the NaN-class warning of macro averages ...  Inside :func:`host_checks` each of them only registers its flags
+    here (no sync); when the outermost block ends, every flag travels in one small copy and the callbacks run:
+    error callbacks first (the first to raise wins, as the eager order would have it), then warning callbacks.
+    A ``MetricCollection.compute`` opens the outer block, so a whole collection pays one read."""
+
+    def __init__(self) -> None:
+        self._items: List[Tuple[Tensor, Callable[[List[int]], None], bool]] = []
+        self._on_error: List[Callable[[], None]] = []
+
+    def add(self, flags: Tensor, callback: Callable[[List[int]], None], error: bool = False) -> None:
+        self._items.append((flags.reshape(-1).to(torch.int32), callback, error))
+
+    def on_error(self, fn: Callable[[], None]) -> None:
+        """Run ``fn`` if an error callback raises (e.g. drop a cached compute value)."""
+        self._on_error.append(fn)
+
+    def resolve(self) -> None:
+        items, self._items = self._items, []
+        on_error, self._on_error = self._on_error, []
+        if not items:
+            return
+        devs = {t.device for t, _, _ in items}
+        if len(devs) == 1:
+            vals = torch.cat([t for t, _, _ in items]).tolist()  # the one host read
+        else:
+            vals = torch.cat([t.cpu() for t, _, _ in items]).tolist()
+        chunks, off = [], 0
+        for t, _, _ in items:
+            chunks.append(vals[off : off + t.numel()])
+            off += t.numel()
+        try:
+            for (_, cb, err), v in zip(items, chunks):
+                if err:
+                    cb(v)
+        except Exception:
+            for fn in on_error:
+                fn()
+            raise
+        for (_, cb, err), v in zip(items, chunks):
+            if not err:
+                cb(v)
+
+
+_HOST = threading.local()
+
+
+def _batch_stack() -> List[HostCheckBatch]:
+    st = getattr(_HOST, "stack", None)
+    if st is None:
+        st = _HOST.stack = []
+    return st
+
+
+def current_host_checks() -> Optional[HostCheckBatch]:
+    st = _batch_stack()
+    return st[0] if st else None
+
+
+@contextmanager
+def host_checks() -> Iterator[HostCheckBatch]:
+    """Collect host checks until the OUTERMOST block ends, then resolve them with a single device->host read."""
+    st = _batch_stack()
+    if st:
+        yield st[0]
+        return
+    batch = HostCheckBatch()
+    st.append(batch)
+    ok = False
+    try:
+        yield batch
+        ok = True
+    finally:
+        st.pop()
+        if ok:
+            batch.resolve()
+
+
+def defer_host_check(flags: Tensor, callback: Callable[[List[int]], None], error: bool = False) -> None:
+    """Register ``flags`` with the active :func:`host_checks` block, or read them now when there is none."""
+    batch = current_host_checks()
+    if batch is None:
+        callback(flags.reshape(-1).to(torch.int32).tolist())
+    else:
+        batch.add(flags, callback, error)
 
 
 class DeferredChecks:
@@ -55,25 +150,57 @@ class DeferredChecks:
         self._flags[(exc, message)] = flag
 
     def check(self) -> None:
+        """Raise / warn for every set flag and clear them.  Inside :func:`host_checks` the flags are snapshotted
+        on device and inspected together with the block's other checks (one host read for the whole compute)."""
         if not self._flags:
             return
         keys = list(self._flags.keys())
-        flags = torch.cat([self._flags[k].reshape(1).to(torch.int32).cpu() for k in keys])  # one host sync
+        devs = {self._flags[k].device for k in keys}
+        if len(devs) == 1:
+            snap = torch.cat([self._flags[k].reshape(1).to(torch.int32) for k in keys])
+        else:
+            snap = torch.cat([self._flags[k].reshape(1).to(torch.int32).cpu() for k in keys])
         for k in keys:
             self._flags[k].zero_()
-        errors = []
-        for k, f in zip(keys, flags.tolist()):
-            if f:
-                if issubclass(k[0], Warning):  # deferred warnings (e.g. aggregation nan_strategy="warn")
+        warn_keys = [k for k in keys if issubclass(k[0], Warning)]
+
+        def _raise(vals: List[int]) -> None:
+            for k, f in zip(keys, vals):
+                if f and not issubclass(k[0], Warning):
+                    raise k[0](k[1])
+
+        def _warn(vals: List[int]) -> None:
+            for k, f in zip(keys, vals):
+                if f and issubclass(k[0], Warning):  # deferred warnings (e.g. aggregation nan_strategy="warn")
                     warnings.warn(k[1], k[0], stacklevel=3)
-                else:
-                    errors.append(k)
-        if errors:
-            raise errors[0][0](errors[0][1])
+
+        batch = current_host_checks()
+        if batch is None:
+            vals = snap.tolist()  # one host sync
+            _warn(vals)
+            _raise(vals)
+            return
+        batch.add(snap, _raise, error=True)
+        if warn_keys:
+            batch.add(snap, _warn, error=False)
 
     def clear(self) -> None:
         for f in self._flags.values():
             f.zero_()
+
+    def snapshot(self) -> Dict[Tuple[Type[Exception], str], Tensor]:
+        """Device copies of the current flags (no host sync) — ``forward`` keeps the accumulated ones across its
+        internal reset/compute of the batch."""
+        return {k: f.clone() for k, f in self._flags.items()}
+
+    def restore(self, snap: Dict[Tuple[Type[Exception], str], Tensor]) -> None:
+        """OR previously snapshotted flags back in."""
+        for k, f in snap.items():
+            cur = self._flags.get(k)
+            if cur is None or cur.device != f.device:
+                self._flags[k] = f
+            else:
+                cur.bitwise_or_(f)
 
 
 def make_sink(t: Tensor) -> Optional[DeferredChecks]:
