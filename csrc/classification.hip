@@ -22,6 +22,12 @@
 //  * tmx::binned_curve_update — bucketize (binary search over T thresholds in LDS) + per-(class, label,
 //                               bucket) histogram, then a suffix scan into the reference's [T, C, 2, 2]
 //                               multi-threshold confusion matrix (K5) — O(N*C*log T) instead of O(N*C*T).
+#include <mutex>
+#include <unordered_map>
+
+#include <c10/hip/HIPCachingAllocator.h>
+#include <c10/hip/HIPGuard.h>
+
 #include "common.h"
 #include "curve_hist_kernels.h"
 
@@ -1142,20 +1148,17 @@ __global__ void __launch_bounds__(256) curve_hist_mc_kernel(const T* __restrict_
   }
 }
 
+// Row pass of the multiclass two-pass route (+ FIXUP and the speculation roll when speculative), into caller-owned
+// scratch: ``codes`` int16 [C * n_pad] (class-major), ``slow_rows`` int32 [2 n], ``state`` int32[6] (counts zero).
 template <typename T, bool PADDED>
-void launch_two_pass(const T* p, const int64_t* target, int64_t n, int C, int ld, int* mode, int* state, bool speculative,
-                     int64_t ignore_index, bool has_ignore, int64_t* hist, int64_t* cm, int* err, const at::TensorOptions& opts,
-                     int* code_range) {
+void launch_row_pass(const T* p, const int64_t* target, int64_t n, int C, int ld, int* mode, int* state, bool speculative,
+                     int64_t ignore_index, bool has_ignore, int64_t* cm, int* err, uint32_t* cptr, int* srows) {
   TORCH_CHECK(n < (int64_t{1} << 31), "curve_hist_update: more than 2^31 rows in one batch");
   const int64_t n_pad = (n + kTileRows - 1) / kTileRows * kTileRows;
-  auto codes = at::empty({(int64_t)C * n_pad}, opts.dtype(at::kShort));
-  auto slow_rows = at::empty({2 * n}, opts.dtype(at::kInt));
   const int64_t ntiles = n_pad / kTileRows;
   const int grid = static_cast<int>((ntiles + 7) / 8 * 8);  // one block per tile (XCD-aware order inside)
   const int fixup_grid = std::min(grid, 128);                // exits at once unless the speculation was wrong
   const size_t shm = (size_t)512 * (C > 512 ? 2 : 1) * kSlots * sizeof(uint32_t);  // 32 / 64 KiB -> 2 blocks per CU
-  uint32_t* cptr = reinterpret_cast<uint32_t*>(codes.data_ptr());
-  int* srows = slow_rows.data_ptr<int>();
   if (C > 512) {
     hipLaunchKernelGGL((mc_codes_kernel<T, false, 2, PADDED>), grid, kRowThreads, shm, stream(), p, target, n, C, ld, mode, ignore_index,
                        has_ignore, cptr, n_pad, cm, err, speculative, srows, state);
@@ -1175,13 +1178,192 @@ void launch_two_pass(const T* p, const int64_t* target, int64_t n, int C, int ld
       TMX_LAUNCH_CHECK();
     }
   }
+  if (speculative) {
+    hipLaunchKernelGGL(mode_roll_kernel, 1, 1, 0, stream(), mode, state + 3);
+    TMX_LAUNCH_CHECK();
+  }
+}
+
+// Class pass of the multiclass two-pass route.  ``bmode`` = the batch's (used, real) mode pair (state + 3 after a
+// speculative row pass, else the pre-pass flag with speculative = false).
+template <typename T>
+void launch_class_pass(const uint32_t* cptr, int64_t n, int C, int ld, const T* p, const int64_t* target, const int* bmode,
+                       bool speculative, const int* srows, int* state, int64_t* hist, int64_t* cm, int* code_range) {
+  const int64_t n_pad = (n + kTileRows - 1) / kTileRows * kTileRows;
   // row splits only when there are too few classes to fill the chip (exclusive-owner flush when splits == 1)
   int splits = 1;
   while ((int64_t)C * splits < 512 && n_pad / (8 * (splits * 2)) >= 1024) splits *= 2;
   hipLaunchKernelGGL((class_hist_kernel<T, false>), C * splits, kClassThreads, kCodes * sizeof(uint32_t), stream(),
-                     reinterpret_cast<const uint16_t*>(codes.data_ptr()), n_pad, splits, hist, p, ld, target, n, mode, speculative,
+                     reinterpret_cast<const uint16_t*>(cptr), n_pad, splits, hist, p, ld, target, n, bmode, speculative,
                      srows, state, cm, code_range);
   TMX_LAUNCH_CHECK();
+}
+
+template <typename T, bool PADDED>
+void launch_two_pass(const T* p, const int64_t* target, int64_t n, int C, int ld, int* mode, int* state, bool speculative,
+                     int64_t ignore_index, bool has_ignore, int64_t* hist, int64_t* cm, int* err, const at::TensorOptions& opts,
+                     int* code_range) {
+  const int64_t n_pad = (n + kTileRows - 1) / kTileRows * kTileRows;
+  auto codes = at::empty({(int64_t)C * n_pad}, opts.dtype(at::kShort));
+  auto slow_rows = at::empty({2 * n}, opts.dtype(at::kInt));
+  uint32_t* cptr = reinterpret_cast<uint32_t*>(codes.data_ptr());
+  int* srows = slow_rows.data_ptr<int>();
+  launch_row_pass<T, PADDED>(p, target, n, C, ld, mode, state, speculative, ignore_index, has_ignore, cm, err, cptr, srows);
+  launch_class_pass<T>(cptr, n, C, ld, p, target, speculative ? state + 3 : mode, speculative, srows, state, hist, cm, code_range);
+}
+
+// ---- one-call overlapped update: row pass on the current stream, class pass on a per-device side stream ----------
+// Events live in a registry keyed by the (per-metric) double-buffered codes scratch: ``done[b]`` marks the class pass
+// that last read buffer b (the row pass that reuses b waits for it), ``ready`` hands the row pass over to the side
+// stream.  All metrics of a device share one side stream; its FIFO order keeps their class passes (and hence every
+// histogram flush) ordered.  Host cost: 2 event records + 2 stream waits, no Python objects.
+struct SideEvents {
+  hipEvent_t ready = nullptr;
+  hipEvent_t done[2] = {nullptr, nullptr};
+};
+
+static SideEvents& side_events(const void* key) {
+  static std::mutex mu;
+  static std::unordered_map<const void*, SideEvents> registry;
+  std::lock_guard<std::mutex> lock(mu);
+  auto it = registry.find(key);
+  if (it != registry.end()) return it->second;
+  SideEvents ev;
+  TMX_CHECK_HIP(hipEventCreateWithFlags(&ev.ready, hipEventDisableTiming));
+  TMX_CHECK_HIP(hipEventCreateWithFlags(&ev.done[0], hipEventDisableTiming));
+  TMX_CHECK_HIP(hipEventCreateWithFlags(&ev.done[1], hipEventDisableTiming));
+  return registry.emplace(key, ev).first->second;
+}
+
+static c10::hip::HIPStream side_stream(c10::DeviceIndex dev) {
+  static std::mutex mu;
+  static std::unordered_map<int, c10::hip::HIPStream> streams;
+  std::lock_guard<std::mutex> lock(mu);
+  auto it = streams.find(dev);
+  if (it == streams.end()) it = streams.emplace(dev, c10::hip::getStreamFromPool(false, dev)).first;
+  return it->second;
+}
+
+void curve_mc_update_overlapped(const at::Tensor& preds, const at::Tensor& target, at::Tensor& mode, at::Tensor& states,
+                                at::Tensor& codes, at::Tensor& slow_rows, int64_t buf, at::Tensor& hist, int64_t ignore_index,
+                                bool has_ignore, c10::optional<at::Tensor> confmat, c10::optional<at::Tensor> err_flag,
+                                c10::optional<at::Tensor> code_range) {
+  TORCH_CHECK(preds.dim() == 2 && preds.is_contiguous() && target.is_contiguous() && target.scalar_type() == at::kLong &&
+              target.numel() == preds.size(0), "curve_mc_update_overlapped: preds [N, C] and int64 target [N], contiguous");
+  const int64_t n = preds.size(0);
+  const int C = static_cast<int>(preds.size(1));
+  TORCH_CHECK(buf == 0 || buf == 1, "buf must be 0 or 1");
+  TORCH_CHECK(C % 8 == 0 && C <= 8 * 2 * kWave && (reinterpret_cast<uintptr_t>(preds.data_ptr()) & 15) == 0,
+              "curve_mc_update_overlapped: C must be a multiple of 8, <= 1024, preds 16-B aligned");
+  const int64_t n_pad = (n + kTileRows - 1) / kTileRows * kTileRows;
+  TORCH_CHECK(codes.dim() == 2 && codes.size(0) == 2 && codes.size(1) >= (int64_t)C * n_pad && codes.scalar_type() == at::kShort &&
+              codes.is_contiguous(), "codes scratch must be int16 [2, >= C * n_pad]");
+  TORCH_CHECK(slow_rows.dim() == 2 && slow_rows.size(0) == 2 && slow_rows.size(1) >= 2 * n && slow_rows.scalar_type() == at::kInt &&
+              slow_rows.is_contiguous(), "slow_rows scratch must be int32 [2, >= 2 N]");
+  TORCH_CHECK(states.scalar_type() == at::kInt && states.numel() == 12 && states.is_contiguous(), "states must be int32 [2, 6]");
+  TORCH_CHECK(mode.scalar_type() == at::kInt && mode.numel() >= 2, "mode must be int32[>= 2]");
+  TORCH_CHECK(hist.is_contiguous() && hist.scalar_type() == at::kLong && hist.numel() == (int64_t)C * 2 * kCodes,
+              "hist must be int64 [C, 2, 16384]");
+  int64_t* cm = nullptr;
+  if (confmat.has_value()) {
+    TORCH_CHECK(confmat->is_contiguous() && confmat->scalar_type() == at::kLong && confmat->numel() == (int64_t)C * C);
+    cm = confmat->data_ptr<int64_t>();
+  }
+  int* err = err_flag.has_value() ? err_flag->data_ptr<int>() : nullptr;
+  int* cr = nullptr;
+  if (code_range.has_value()) {
+    TORCH_CHECK(code_range->scalar_type() == at::kInt && code_range->numel() == 2 * C && code_range->is_contiguous(),
+                "code_range must be int32[C, 2]");
+    cr = code_range->data_ptr<int>();
+  }
+  if (n == 0) return;
+  const c10::DeviceIndex dev = preds.device().index();
+  SideEvents& ev = side_events(codes.data_ptr());
+  const c10::hip::HIPStream main = c10::hip::getCurrentHIPStream(dev);
+  const c10::hip::HIPStream side = side_stream(dev);
+  uint32_t* cptr = reinterpret_cast<uint32_t*>(codes[buf].data_ptr());
+  int* srows = slow_rows[buf].data_ptr<int>();
+  int* state = states.data_ptr<int>() + 6 * buf;
+  TMX_CHECK_HIP(hipStreamWaitEvent(main.stream(), ev.done[buf], 0));  // buffer b free again
+  TMX_DISPATCH_HALF(preds.scalar_type(), "curve_mc_update_overlapped", [&] {
+    const scalar_t* p = reinterpret_cast<const scalar_t*>(preds.data_ptr());
+    launch_row_pass<scalar_t, false>(p, target.data_ptr<int64_t>(), n, C, C, mode.data_ptr<int>(), state, true, ignore_index,
+                                     has_ignore, cm, err, cptr, srows);
+    TMX_CHECK_HIP(hipEventRecord(ev.ready, main.stream()));
+    TMX_CHECK_HIP(hipStreamWaitEvent(side.stream(), ev.ready, 0));
+    {
+      c10::hip::HIPStreamGuard guard(side);
+      launch_class_pass<scalar_t>(cptr, n, C, C, p, target.data_ptr<int64_t>(), state + 3, true, srows, state,
+                                  hist.data_ptr<int64_t>(), cm, cr);
+    }
+    TMX_CHECK_HIP(hipEventRecord(ev.done[buf], side.stream()));
+  });
+  // the side stream reads these after this call returns: keep their blocks from being reused before it is done
+  for (const at::Tensor* t : std::initializer_list<const at::Tensor*>{&preds, &target, &codes, &slow_rows, &states, &hist})
+    c10::hip::HIPCachingAllocator::recordStream(t->storage().data_ptr(), side);
+  if (confmat.has_value()) c10::hip::HIPCachingAllocator::recordStream(confmat->storage().data_ptr(), side);
+  if (code_range.has_value()) c10::hip::HIPCachingAllocator::recordStream(code_range->storage().data_ptr(), side);
+}
+
+// Make the current stream wait for every class pass issued on the scratch ``codes`` (no-op for unknown buffers).
+void curve_side_join(const at::Tensor& codes) {
+  SideEvents& ev = side_events(codes.data_ptr());
+  const hipStream_t main = c10::hip::getCurrentHIPStream(codes.device().index()).stream();
+  TMX_CHECK_HIP(hipStreamWaitEvent(main, ev.done[0], 0));
+  TMX_CHECK_HIP(hipStreamWaitEvent(main, ev.done[1], 0));
+}
+
+// Split form of the speculative multiclass route for a side-stream class pass (module updates): the caller owns the
+// double-buffered scratch and orders the two launches with events (the class pass of batch k overlaps the row pass of
+// batch k + 1).  Both run on the current stream of their call.
+void curve_mc_rowpass(const at::Tensor& preds, const at::Tensor& target, at::Tensor& mode, at::Tensor& state, at::Tensor& codes,
+                      at::Tensor& slow_rows, int64_t ignore_index, bool has_ignore, c10::optional<at::Tensor> confmat,
+                      c10::optional<at::Tensor> err_flag) {
+  TORCH_CHECK(preds.dim() == 2 && preds.is_contiguous() && target.is_contiguous() && target.scalar_type() == at::kLong &&
+              target.numel() == preds.size(0), "curve_mc_rowpass: preds [N, C] and int64 target [N], contiguous");
+  const int64_t n = preds.size(0);
+  const int C = static_cast<int>(preds.size(1));
+  TORCH_CHECK(C % 8 == 0 && C <= 8 * 2 * kWave && (reinterpret_cast<uintptr_t>(preds.data_ptr()) & 15) == 0,
+              "curve_mc_rowpass: C must be a multiple of 8, <= 1024, preds 16-B aligned");
+  const int64_t n_pad = (n + kTileRows - 1) / kTileRows * kTileRows;
+  TORCH_CHECK(mode.scalar_type() == at::kInt && mode.numel() == 2 && state.scalar_type() == at::kInt && state.numel() == 6 &&
+              codes.scalar_type() == at::kShort && codes.numel() >= (int64_t)C * n_pad && slow_rows.scalar_type() == at::kInt &&
+              slow_rows.numel() >= 2 * n, "curve_mc_rowpass: scratch shapes");
+  int64_t* cm = nullptr;
+  if (confmat.has_value()) {
+    TORCH_CHECK(confmat->is_contiguous() && confmat->scalar_type() == at::kLong && confmat->numel() == (int64_t)C * C);
+    cm = confmat->data_ptr<int64_t>();
+  }
+  int* err = err_flag.has_value() ? err_flag->data_ptr<int>() : nullptr;
+  if (n == 0) return;
+  TMX_DISPATCH_HALF(preds.scalar_type(), "curve_mc_rowpass", [&] {
+    launch_row_pass<scalar_t, false>(reinterpret_cast<const scalar_t*>(preds.data_ptr()), target.data_ptr<int64_t>(), n, C, C,
+                                     mode.data_ptr<int>(), state.data_ptr<int>(), true, ignore_index, has_ignore, cm, err,
+                                     reinterpret_cast<uint32_t*>(codes.data_ptr()), slow_rows.data_ptr<int>());
+  });
+}
+
+void curve_mc_classpass(const at::Tensor& codes, const at::Tensor& slow_rows, at::Tensor& state, at::Tensor& hist,
+                        const at::Tensor& preds, const at::Tensor& target, c10::optional<at::Tensor> confmat,
+                        c10::optional<at::Tensor> code_range) {
+  const int64_t n = preds.size(0);
+  const int C = static_cast<int>(preds.size(1));
+  TORCH_CHECK(hist.is_contiguous() && hist.scalar_type() == at::kLong && hist.numel() == (int64_t)C * 2 * kCodes,
+              "curve_mc_classpass: hist must be int64 [C, 2, 16384]");
+  int64_t* cm = confmat.has_value() ? confmat->data_ptr<int64_t>() : nullptr;
+  int* cr = nullptr;
+  if (code_range.has_value()) {
+    TORCH_CHECK(code_range->scalar_type() == at::kInt && code_range->numel() == 2 * C && code_range->is_contiguous(),
+                "code_range must be int32[C, 2]");
+    cr = code_range->data_ptr<int>();
+  }
+  if (n == 0) return;
+  TMX_DISPATCH_HALF(preds.scalar_type(), "curve_mc_classpass", [&] {
+    launch_class_pass<scalar_t>(reinterpret_cast<const uint32_t*>(codes.data_ptr()), n, C, C,
+                                reinterpret_cast<const scalar_t*>(preds.data_ptr()), target.data_ptr<int64_t>(),
+                                state.data_ptr<int>() + 3, true, slow_rows.data_ptr<int>(), state.data_ptr<int>(),
+                                hist.data_ptr<int64_t>(), cm, cr);
+  });
 }
 
 // Binary / multilabel: element-wise (sigmoid if flagged). preds/target viewed as [N, L, S].
@@ -1280,18 +1462,24 @@ void curve_hist_update(const at::Tensor& preds_, const at::Tensor& target_, at::
                        c10::optional<at::Tensor> mode_state, c10::optional<at::Tensor> code_range) {
   TORCH_CHECK(hist.is_contiguous() && hist.scalar_type() == at::kLong && hist.dim() == 3 && hist.size(1) == 2 &&
               hist.size(2) == kCodes, "hist must be int64 [C, 2, 16384]");
-  // code_range (int32[2], optional): the occupied code range [lo, hi] of ``hist``.  The two-pass routes widen it
+  // code_range (int32[C, 2], optional): the occupied code range [lo, hi] of each class of ``hist``.  The two-pass routes widen it
   // in the class pass; every other route (rare shapes) marks it as the full range, so it is always conservative.
   int* crange = nullptr;
   bool range_tracked = false;
   if (code_range.has_value()) {
-    TORCH_CHECK(code_range->scalar_type() == at::kInt && code_range->numel() == 2 && code_range->is_contiguous() &&
-                code_range->device() == hist.device(), "code_range must be int32[2] on the histogram's device");
+    TORCH_CHECK(code_range->scalar_type() == at::kInt && code_range->numel() == 2 * hist.size(0) && code_range->is_contiguous() &&
+                code_range->device() == hist.device(), "code_range must be int32[C, 2] on the histogram's device");
     crange = code_range->data_ptr<int>();
   }
   struct RangeGuard {  // on exit, routes that did not track the range widen it to everything
     c10::optional<at::Tensor>& r; bool& tracked;
-    ~RangeGuard() { if (r.has_value() && !tracked) { r->narrow(0, 0, 1).fill_(0); r->narrow(0, 1, 1).fill_(kCodes - 1); } }
+    ~RangeGuard() {
+      if (r.has_value() && !tracked) {
+        auto v = r->view({-1, 2});
+        v.select(1, 0).fill_(0);
+        v.select(1, 1).fill_(kCodes - 1);
+      }
+    }
   } range_guard{code_range, range_tracked};
   auto preds = preds_.contiguous();
   auto target = target_.contiguous().to(at::kLong);
@@ -1409,16 +1597,18 @@ void curve_hist_update(const at::Tensor& preds_, const at::Tensor& target_, at::
   TMX_LAUNCH_CHECK();
 }
 
-// Per-class reduction of the exact histogram (descending code order), one 1024-thread workgroup per class.
+// Per-class reduction of the exact histogram (descending code order), one 256-thread workgroup per class.
 //   out[c] = {auroc, average_precision, n_pos, n_neg}
 // AUROC = sum_k neg_k * (2*TP_{<k} + pos_k) / (2 * P * N)  (trapezoid over every code; empty codes add 0)
 // AP    = sum_k (pos_k / P) * TP_k / (TP_k + FP_k)
-// Thread t owns 16 consecutive codes (descending positions 16t .. 16t+15) of both halves in registers, so all
-// 256 KiB of a class are in flight at once; one block scan of the per-thread sums gives every thread its
-// TP / FP carry, then each walks its 16 codes.  (The previous form walked 64 dependent 256-code chunks with two
-// barriers each: 107 us at C = 1000.)
-constexpr int kRedThreads = 1024;
-constexpr int kRedPer = kCodes / kRedThreads;  // 16
+// Only the class's occupied code range [lo, hi] (``code_range[c]``, tracked by the class pass) is read, in chunks of 4096 codes
+// from the top: thread t owns the 16 consecutive codes of its 128-B aligned segment (two 16-B loads per 32 B of each
+// half), one block scan of the per-thread sums gives every thread its TP / FP carry, then each walks its codes.
+// Softmax scores of 1000 classes occupy ~3000 codes: one chunk, 53 MB read instead of 262 MB, and 4 small
+// workgroups per CU keep every class resident at once (the previous 1024-thread, full-range form took 105 us).
+constexpr int kRedThreads = 256;
+constexpr int kRedPer = 16;
+constexpr int kRedChunk = kRedThreads * kRedPer;
 
 __device__ __forceinline__ long long shfl_up_i64(long long v, int off) {
   int lo = __shfl_up(static_cast<int>(v & 0xFFFFFFFFll), off, kWave);
@@ -1433,67 +1623,66 @@ __global__ void __launch_bounds__(kRedThreads) curve_hist_reduce_kernel(const in
   constexpr int kWaves = kRedThreads / kWave;
   const int c = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
-  // only the occupied code range [lo, hi] is read (softmax scores fill about a fifth of the codes); thread t owns
-  // the q consecutive codes hi - q t, ..., hi - q t - q + 1 (descending order = thread order)
   int lo = 0, hi = K - 1;
   if (code_range != nullptr) {
-    lo = max(code_range[0], 0);
-    hi = min(code_range[1], K - 1);
+    lo = max(code_range[2 * c], 0);
+    hi = min(code_range[2 * c + 1], K - 1);
   }
-  const int R = hi >= lo ? hi - lo + 1 : 0;
-  const int q = (R + kRedThreads - 1) / kRedThreads;  // <= kRedPer
   const int64_t* negh = hist + ((int64_t)c * 2 + 0) * K;
   const int64_t* posh = hist + ((int64_t)c * 2 + 1) * K;
-  long long p[kRedPer], n[kRedPer];  // index i = i-th highest owned code
-  const int top = hi - q * tid;
-  if (q == kRedPer) {  // full range: 16-B loads, as before
-    const int64_t base = top - (kRedPer - 1);
-    const longlong2* negv = reinterpret_cast<const longlong2*>(negh + base);
-    const longlong2* posv = reinterpret_cast<const longlong2*>(posh + base);
-#pragma unroll
-    for (int v = 0; v < kRedPer / 2; ++v) {
-      const longlong2 a = posv[v], b = negv[v];
-      p[kRedPer - 1 - 2 * v] = a.x; p[kRedPer - 2 - 2 * v] = a.y;
-      n[kRedPer - 1 - 2 * v] = b.x; n[kRedPer - 2 - 2 * v] = b.y;
-    }
-  } else {
-#pragma unroll
-    for (int i = 0; i < kRedPer; ++i) {
-      const int code = top - i;
-      const bool ok = i < q && code >= lo;
-      p[i] = ok ? posh[code] : 0;
-      n[i] = ok ? negh[code] : 0;
-    }
-  }
-  long long sp = 0, sn = 0;
-#pragma unroll
-  for (int i = 0; i < kRedPer; ++i) { sp += p[i]; sn += n[i]; }
-  long long ip = sp, in = sn;  // inclusive wave scan in thread order (= descending code order)
-#pragma unroll
-  for (int off = 1; off < kWave; off <<= 1) {
-    const long long tp = shfl_up_i64(ip, off), tn = shfl_up_i64(in, off);
-    if (lane >= off) { ip += tp; in += tn; }
-  }
   __shared__ long long s_p[kWaves], s_n[kWaves];
   __shared__ double s_a[kWaves], s_b[kWaves];
-  if (lane == kWave - 1) { s_p[wave] = ip; s_n[wave] = in; }
-  __syncthreads();
-  long long wp = 0, wn = 0, P = 0, N = 0;
-#pragma unroll
-  for (int w = 0; w < kWaves; ++w) {
-    if (w < wave) { wp += s_p[w]; wn += s_n[w]; }
-    P += s_p[w];
-    N += s_n[w];
-  }
-  long long tp = wp + ip - sp, fp = wn + in - sn;  // positives / negatives above this thread's codes
+  long long carry_p = 0, carry_n = 0;
   double area = 0.0, ap_sum = 0.0;
+  if (hi >= lo) {
+    const int top = hi | (kRedPer - 1), bottom = lo & ~(kRedPer - 1);  // segment-aligned, still inside [0, K)
+    for (int chunk_top = top; chunk_top >= bottom; chunk_top -= kRedChunk) {
+      const int seg_hi = chunk_top - kRedPer * tid;
+      long long p[kRedPer], n[kRedPer];  // index i = i-th highest owned code
+      if (seg_hi >= bottom) {
+        const longlong2* negv = reinterpret_cast<const longlong2*>(negh + (seg_hi - (kRedPer - 1)));
+        const longlong2* posv = reinterpret_cast<const longlong2*>(posh + (seg_hi - (kRedPer - 1)));
 #pragma unroll
-  for (int i = 0; i < kRedPer; ++i) {
-    const long long pk = p[i], nk = n[i];
-    tp += pk;
-    fp += nk;
-    area += (double)nk * (double)(2 * (tp - pk) + pk);
-    if (pk) ap_sum += (double)pk * ((double)tp / (double)(tp + fp));
+        for (int v = 0; v < kRedPer / 2; ++v) {
+          const longlong2 a = posv[v], b = negv[v];
+          p[kRedPer - 1 - 2 * v] = a.x; p[kRedPer - 2 - 2 * v] = a.y;
+          n[kRedPer - 1 - 2 * v] = b.x; n[kRedPer - 2 - 2 * v] = b.y;
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < kRedPer; ++i) p[i] = n[i] = 0;
+      }
+      long long sp = 0, sn = 0;
+#pragma unroll
+      for (int i = 0; i < kRedPer; ++i) { sp += p[i]; sn += n[i]; }
+      long long ip = sp, in = sn;  // inclusive wave scan in thread order (= descending code order)
+#pragma unroll
+      for (int off = 1; off < kWave; off <<= 1) {
+        const long long tp = shfl_up_i64(ip, off), tn = shfl_up_i64(in, off);
+        if (lane >= off) { ip += tp; in += tn; }
+      }
+      if (lane == kWave - 1) { s_p[wave] = ip; s_n[wave] = in; }
+      __syncthreads();
+      long long wp = 0, wn = 0, bp = 0, bn = 0;
+#pragma unroll
+      for (int w = 0; w < kWaves; ++w) {
+        if (w < wave) { wp += s_p[w]; wn += s_n[w]; }
+        bp += s_p[w];
+        bn += s_n[w];
+      }
+      long long tp = carry_p + wp + ip - sp, fp = carry_n + wn + in - sn;  // positives / negatives above this thread
+#pragma unroll
+      for (int i = 0; i < kRedPer; ++i) {
+        const long long pk = p[i], nk = n[i];
+        tp += pk;
+        fp += nk;
+        area += (double)nk * (double)(2 * (tp - pk) + pk);
+        if (pk) ap_sum += (double)pk * ((double)tp / (double)(tp + fp));
+      }
+      carry_p += bp;
+      carry_n += bn;
+      __syncthreads();  // s_p / s_n are rewritten by the next chunk
+    }
   }
   area = wave_sum(area);
   ap_sum = wave_sum(ap_sum);
@@ -1502,10 +1691,62 @@ __global__ void __launch_bounds__(kRedThreads) curve_hist_reduce_kernel(const in
   if (tid == 0) {
     double a = 0.0, b = 0.0;
     for (int w = 0; w < kWaves; ++w) { a += s_a[w]; b += s_b[w]; }
+    const long long P = carry_p, N = carry_n;
     out[c * 4 + 0] = (P > 0 && N > 0) ? a / (2.0 * (double)P * (double)N) : 0.0;
     out[c * 4 + 1] = P > 0 ? b / (double)P : NAN;
     out[c * 4 + 2] = (double)P;
     out[c * 4 + 3] = (double)N;
+  }
+}
+
+// Class averages and warning flags of curve_hist_reduce's [C, 4] output in one workgroup (replaces ~20 small ATen
+// launches and their tiny tensors in compute()):
+//   summary = {any N <= 0, any P <= 0, any auroc NaN, any AP NaN,
+//              macro AUROC, weighted AUROC, macro AP, weighted AP}   (NaN classes ignored, weights = P)
+constexpr int kSumThreads = 256;
+__global__ void __launch_bounds__(kSumThreads) curve_summary_kernel(const double* __restrict__ sc, int C, double* __restrict__ summary) {
+  constexpr int kWaves = kSumThreads / kWave;
+  double v[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};  // flags x4 | sum_a, cnt_a, wsum_a, sum_ap, cnt_ap, wsum_ap
+  double wa = 0.0, wap = 0.0;                     // weight totals over the non-NaN classes
+  for (int c = threadIdx.x; c < C; c += kSumThreads) {
+    const double a = sc[c * 4 + 0], ap = sc[c * 4 + 1], P = sc[c * 4 + 2], N = sc[c * 4 + 3];
+    v[0] += N <= 0.0;
+    v[1] += P <= 0.0;
+    const bool na = a != a, nap = ap != ap;
+    v[2] += na;
+    v[3] += nap;
+    if (!na) { v[4] += a; v[5] += 1.0; v[6] += a * P; wa += P; }
+    if (!nap) { v[7] += ap; v[8] += 1.0; v[9] += ap * P; wap += P; }
+  }
+  __shared__ double s[kWaves][12];
+#pragma unroll
+  for (int i = 0; i < 10; ++i) v[i] = wave_sum(v[i]);
+  wa = wave_sum(wa);
+  wap = wave_sum(wap);
+  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+  if (lane == 0) {
+#pragma unroll
+    for (int i = 0; i < 10; ++i) s[wave][i] = v[i];
+    s[wave][10] = wa;
+    s[wave][11] = wap;
+  }
+  __syncthreads();
+  if (wave == 0) {  // lane i < 12 folds quantity i over the waves in parallel, lane 0 gathers the 12 totals
+    double acc = 0.0;
+    if (lane < 12)
+      for (int w = 0; w < kWaves; ++w) acc += s[w][lane];
+    double t[12];
+#pragma unroll
+    for (int i = 0; i < 12; ++i) t[i] = __shfl(acc, i, kWave);
+    if (lane != 0) return;
+    summary[0] = t[0] > 0;
+    summary[1] = t[1] > 0;
+    summary[2] = t[2] > 0;
+    summary[3] = t[3] > 0;
+    summary[4] = t[5] > 0 ? t[4] / t[5] : NAN;
+    summary[5] = t[10] > 0 ? t[6] / t[10] : NAN;
+    summary[6] = t[8] > 0 ? t[7] / t[8] : NAN;
+    summary[7] = t[11] > 0 ? t[9] / t[11] : NAN;
   }
 }
 
@@ -1515,8 +1756,8 @@ at::Tensor curve_hist_reduce(const at::Tensor& hist_, c10::optional<at::Tensor> 
               "curve_hist_reduce: hist must be int64 [C, 2, 16384]");
   const int* cr = nullptr;
   if (code_range.has_value()) {
-    TORCH_CHECK(code_range->scalar_type() == at::kInt && code_range->numel() == 2 && code_range->is_contiguous() &&
-                code_range->device() == hist.device(), "code_range must be int32[2] on the histogram's device");
+    TORCH_CHECK(code_range->scalar_type() == at::kInt && code_range->numel() == 2 * hist.size(0) && code_range->is_contiguous() &&
+                code_range->device() == hist.device(), "code_range must be int32[C, 2] on the histogram's device");
     cr = code_range->data_ptr<int>();
   }
   const int C = static_cast<int>(hist.size(0));
@@ -1525,6 +1766,16 @@ at::Tensor curve_hist_reduce(const at::Tensor& hist_, c10::optional<at::Tensor> 
   hipLaunchKernelGGL(curve_hist_reduce_kernel, C, kRedThreads, 0, stream(), hist.data_ptr<int64_t>(), cr, out.data_ptr<double>());
   TMX_LAUNCH_CHECK();
   return out;
+}
+
+at::Tensor curve_summary(const at::Tensor& scores_) {
+  auto scores = scores_.contiguous();
+  TORCH_CHECK(scores.scalar_type() == at::kDouble && scores.dim() == 2 && scores.size(1) == 4, "curve_summary: scores must be float64 [C, 4]");
+  auto summary = at::empty({8}, scores.options());
+  hipLaunchKernelGGL(curve_summary_kernel, 1, kSumThreads, 0, stream(), scores.data_ptr<double>(),
+                     static_cast<int>(scores.size(0)), summary.data_ptr<double>());
+  TMX_LAUNCH_CHECK();
+  return summary;
 }
 
 // =========================================================================================================
@@ -2164,6 +2415,11 @@ TORCH_LIBRARY_FRAGMENT(tmx, m) {
   m.def("binary_stats_update(Tensor preds, Tensor target, Tensor(a!) counts, int num_labels, float threshold, int ignore_index, bool has_ignore) -> ()");
   m.def("curve_hist_update(Tensor preds, Tensor target, Tensor(a!) hist, int task, int ignore_index, bool has_ignore, Tensor(b!)? confmat, Tensor? norm_flag, Tensor(c!)? err_flag, Tensor(d!)? mode_state, Tensor(e!)? code_range=None) -> ()");
   m.def("curve_hist_reduce(Tensor hist, Tensor? code_range=None) -> Tensor");
+  m.def("curve_summary(Tensor scores) -> Tensor");
+  m.def("curve_mc_update_overlapped(Tensor preds, Tensor target, Tensor(a!) mode, Tensor(b!) states, Tensor(c!) codes, Tensor(d!) slow_rows, int buf, Tensor(e!) hist, int ignore_index, bool has_ignore, Tensor(f!)? confmat, Tensor(g!)? err_flag, Tensor(h!)? code_range) -> ()");
+  m.def("curve_side_join(Tensor codes) -> ()");
+  m.def("curve_mc_rowpass(Tensor preds, Tensor target, Tensor(a!) mode, Tensor(b!) state, Tensor(c!) codes, Tensor(d!) slow_rows, int ignore_index, bool has_ignore, Tensor(e!)? confmat, Tensor(f!)? err_flag) -> ()");
+  m.def("curve_mc_classpass(Tensor codes, Tensor slow_rows, Tensor(a!) state, Tensor(b!) hist, Tensor preds, Tensor target, Tensor(c!)? confmat, Tensor(d!)? code_range) -> ()");
   m.def("binned_curve_update(Tensor preds, Tensor target, Tensor thresholds, Tensor(a!) confmat, int task, int ignore_index, bool has_ignore, Tensor? norm_flag, Tensor(b!)? err_flag=None) -> ()");
   m.def("ce_bins_update(Tensor conf, Tensor acc, Tensor boundaries, Tensor(a!) bins) -> ()");
   m.def("mc_calibration_update(Tensor preds, Tensor target, Tensor boundaries, Tensor(a!) bins) -> ()");
@@ -2179,6 +2435,11 @@ TORCH_LIBRARY_IMPL(tmx, CUDA, m) {
   m.impl("binary_stats_fused", &tmx::binary_stats_fused);
   m.impl("curve_hist_update", &tmx::curve_hist_update);
   m.impl("curve_hist_reduce", &tmx::curve_hist_reduce);
+  m.impl("curve_summary", &tmx::curve_summary);
+  m.impl("curve_mc_rowpass", &tmx::curve_mc_rowpass);
+  m.impl("curve_mc_update_overlapped", &tmx::curve_mc_update_overlapped);
+  m.impl("curve_side_join", &tmx::curve_side_join);
+  m.impl("curve_mc_classpass", &tmx::curve_mc_classpass);
   m.impl("binned_curve_update", &tmx::binned_curve_update);
   m.impl("ce_bins_update", &tmx::ce_bins_update);
   m.impl("mc_calibration_update", &tmx::mc_calibration_update);

@@ -571,8 +571,9 @@ __global__ void __launch_bounds__(kRowThreads, 4) ml_codes_kernel(const T* __res
 // softmax of such a row is all NaN (every code skipped), in probability mode each score keeps its own code, the
 // arg-max is the first NaN else the first maximum.  List 0 (speculated pass): codes unless a FIXUP pass replaced
 // them, confusion matrix always; list 1 (FIXUP pass): codes with the corrected mode.
-// ``state`` = {count0, count1, ticket}: the last block to finish (ticket) rolls the speculation word
-// (mode[0] = mode[1], mode[1] = 0) and clears the counts for the next batch — every block has read them by then.
+// ``state`` = {count0, count1, ticket, bmode0, bmode1}: the batch's mode pair comes from bmode (written by
+// mode_roll_kernel); the last block to finish (ticket) clears the counts for the next batch that uses this state —
+// every block has read them by then.
 constexpr int kClassThreads = 1024;
 constexpr int64_t kClassChunk = 65528;  // rows per LDS flush: a 16-bit half never overflows (multiple of 8)
 
@@ -601,22 +602,19 @@ template <typename T, bool PACKED>
 __global__ void __launch_bounds__(kClassThreads) class_hist_kernel(const uint16_t* __restrict__ codes, int64_t n_pad, int splits,
                                                                    int64_t* __restrict__ hist, const T* __restrict__ preds, int ld,
                                                                    const int64_t* __restrict__ target, int64_t n,
-                                                                   int* __restrict__ mode, bool speculative,
+                                                                   const int* __restrict__ bmode, bool speculative,
                                                                    const int* __restrict__ slow_rows, int* __restrict__ state,
                                                                    int64_t* __restrict__ confmat, int* __restrict__ code_range) {
   extern __shared__ __attribute__((aligned(16))) uint32_t s_h[];  // [kCodes]: neg, or neg (lo 16) | pos (hi 16)
   __shared__ int s_info[4];
-  __shared__ int s_range[2];
   int lo = kCodes, hi = -1;  // occupied code range this thread touched (compute() then scans only that range)
   const int C = gridDim.x / splits;
   const int c = blockIdx.x / splits, sp = blockIdx.x % splits;
-  if (threadIdx.x == 0) {  // the row-pass kernels are complete (stream order)
-    s_info[0] = mode[0];
-    s_info[1] = speculative ? mode[1] : mode[0];
+  if (threadIdx.x == 0) {  // the row-pass kernels of this batch are complete (stream order / event wait)
+    s_info[0] = bmode[0];
+    s_info[1] = speculative ? bmode[1] : bmode[0];
     s_info[2] = state[0];
     s_info[3] = state[1];
-    s_range[0] = kCodes;
-    s_range[1] = -1;
   }
   uint4* s4 = reinterpret_cast<uint4*>(s_h);
   for (int i = threadIdx.x; i < kCodes / 4; i += kClassThreads) s4[i] = make_uint4(0, 0, 0, 0);
@@ -700,17 +698,12 @@ __global__ void __launch_bounds__(kClassThreads) class_hist_kernel(const uint16_
   __syncthreads();
   // rare-row codes went to the int64 bins by atomics: then the last flush must be atomic too
   class_flush<PACKED>(s_h, neg_hist, pos_hist, exclusive && n0 + n1 == 0, lo, hi);
-  if (code_range != nullptr) {
+  if (code_range != nullptr) {  // per-class running range [C][2]: one min / max per wave, no block barrier
     lo = wave_min_i32(lo);
     hi = wave_max_i32(hi);
     if ((threadIdx.x & (kWave - 1)) == 0 && hi >= 0) {
-      atomicMin(&s_range[0], lo);
-      atomicMax(&s_range[1], hi);
-    }
-    __syncthreads();
-    if (threadIdx.x == 0 && s_range[1] >= 0) {
-      atomicMin(code_range, s_range[0]);
-      atomicMax(code_range + 1, s_range[1]);
+      atomicMin(code_range + 2 * c, lo);
+      atomicMax(code_range + 2 * c + 1, hi);
     }
   }
   if (threadIdx.x == 0) {
@@ -718,14 +711,22 @@ __global__ void __launch_bounds__(kClassThreads) class_hist_kernel(const uint16_
     // each block consumed those values (s_info, above) before taking its ticket.  (An agent-scope release here writes
     // back the XCD's L2 once per block: it doubled the kernel's time.)
     if (__hip_atomic_fetch_add(state + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1) {
-      if (speculative) {
-        mode[0] = m1;
-        mode[1] = 0;
-      }
       state[0] = state[1] = 0;
       state[2] = 0;
     }
   }
+}
+
+// Speculation roll, one thread, in row-pass stream order right after the FIXUP launch: the batch's (used, real) mode
+// pair is snapshotted into its own state (``bmode`` = state[3:5], read by that batch's class pass) and the next batch
+// speculates the real one.  Keeping the roll out of the class pass lets the class pass of batch k run on a side
+// stream while the row pass of batch k + 1 reads the rolled word.
+__global__ void mode_roll_kernel(int* __restrict__ mode, int* __restrict__ bmode) {
+  const int m0 = mode[0], m1 = mode[1];
+  bmode[0] = m0;
+  bmode[1] = m1;
+  mode[0] = m1;
+  mode[1] = 0;
 }
 
 

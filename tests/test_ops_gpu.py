@@ -585,3 +585,147 @@ def test_binned_bucket_guess_exact(kind):
         tin = tt.reshape(-1, 1, 1) if C == 1 else tt
         g, c, _, _ = _both(K.binned_curve_update, pin, tin, thr, cm, "binary" if C == 1 else "multilabel", None)
         assert torch.equal(g[3].cpu(), c[3])
+
+
+@pytest.mark.parametrize("C", [3, 1000])
+@pytest.mark.parametrize("span", ["narrow", "wide", "full", "empty"])
+def test_curve_hist_reduce_tracked_range(C, span):
+    """The range-limited reduction (chunks of 4096 codes from the top of the tracked range) equals the full-range
+    reduction of the same histogram, for ranges inside one chunk, across chunks, the full range and an empty one."""
+    g = torch.Generator().manual_seed(C)
+    hist = torch.zeros(C, 2, K.N_CODES, dtype=torch.long)
+    lo, hi = {"narrow": (16001, 16200), "wide": (3, 12345), "full": (0, K.N_CODES - 1), "empty": (K.N_CODES, -1)}[span]
+    if hi >= lo:
+        hist[:, :, lo : hi + 1] = torch.randint(0, 4, (C, 2, hi - lo + 1), generator=g) * (torch.rand(C, 2, hi - lo + 1, generator=g) < 0.3)
+        hist[0, 1] = 0  # a class without positives (AP NaN, degenerate flag)
+    rng = torch.tensor([lo, hi], dtype=torch.int32, device="cuda").repeat(C, 1)
+    got = K.curve_hist_reduce(hist.cuda(), rng).cpu()
+    full = K.curve_hist_reduce(hist.cuda()).cpu()
+    ref = K.curve_hist_reduce(hist)
+    torch.testing.assert_close(got, ref, rtol=1e-12, atol=1e-12, equal_nan=True)
+    torch.testing.assert_close(full, ref, rtol=1e-12, atol=1e-12, equal_nan=True)
+    summ = K.curve_summary(got.cuda()).cpu()
+    torch.testing.assert_close(summ, K.curve_summary(ref), rtol=1e-12, atol=1e-12, equal_nan=True)
+
+
+def test_tracked_code_range_module():
+    """The class pass widens the module's tracked code range to exactly the occupied codes; the range-limited compute
+    equals the compute over a histogram of unknown range (recomputed) and the CPU path."""
+    import torchmetrics_forked_amd as tm
+
+    C = 100
+    m = tm.MulticlassAUROC(num_classes=C, average=None).cuda()
+    x = torch.randn(4096, C).bfloat16()
+    t = torch.randint(0, C, (4096,))
+    m.update(x.cuda(), t.cuda())
+    rng = m._tracked_range().cpu()
+    for c in (0, 17, C - 1):
+        occ = (m.score_hist[c].amax(0) > 0).nonzero().flatten().cpu()
+        assert rng[c].tolist() == [int(occ.min()), int(occ.max())]
+    a = m.compute().cpu()
+    m._invalidate_range()
+    m._computed = None
+    b = m.compute().cpu()
+    cpu = tm.MulticlassAUROC(num_classes=C, average=None)
+    cpu.update(x, t)
+    torch.testing.assert_close(a, b, rtol=0, atol=0)
+    torch.testing.assert_close(a, cpu.compute(), rtol=0, atol=2e-4)
+
+
+def _hist_from_scores(scores, target, C):
+    """Exact (class, label, 16-bit code) histogram of 16-bit scores in [0, 1] (-0.0 -> code 0)."""
+    codes = scores.view(torch.int16).long() & 0x7FFF
+    codes = torch.where(codes > 0x3FFF, torch.zeros_like(codes), codes)
+    lab = (torch.arange(C, device=scores.device)[None, :] == target[:, None]).long()
+    flat = (torch.arange(C, device=scores.device)[None, :] * 2 + lab) * K.N_CODES + codes
+    h = torch.zeros(C, 2, K.N_CODES, dtype=torch.long, device=scores.device)
+    h.view(-1).index_add_(0, flat.reshape(-1), torch.ones_like(flat.reshape(-1)))
+    return h
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_curve_hist_codes_vs_aten_softmax_same_device(dtype):
+    """Pinned bound of the fused softmax codes against ATen's GPU softmax of the same logits (what the reference
+    computes).  The row pass sums exp(x - max) in a different fp32 order than ATen's warp softmax (64 lanes x 16
+    sequential, xor butterfly 32..1; ``tools/probes/softmax_order_probe.py``), so a quotient within an ulp of a 16-bit
+    rounding boundary can round to the neighbouring code.  Checked per element (the row pass's class-major codes):
+    every difference is exactly one code, at most 2e-5 (bf16) / 1.5e-4 (fp16) of the elements differ (measured
+    ~5e-6 / ~8e-5), and AUROC / AP over all classes equal the sort-based computation on ATen's scores to 1e-7."""
+    from torchmetrics_forked_amd.functional.classification import _curve_engine as eng
+
+    N, C = 65536, 1000
+    g = torch.Generator(device="cuda").manual_seed(11)
+    x = torch.randn(N, C, device="cuda", generator=g).to(dtype)
+    t = torch.randint(0, C, (N,), device="cuda", generator=g)
+    mode = torch.ones(2, dtype=torch.int32, device="cuda")  # speculate softmax (logits batch): no FIXUP pass
+    state = torch.zeros(6, dtype=torch.int32, device="cuda")
+    n_pad = (N + 31) // 32 * 32
+    codes = torch.empty(C * n_pad, dtype=torch.int16, device="cuda")
+    rows = torch.empty(2 * N, dtype=torch.int32, device="cuda")
+    torch.ops.tmx.curve_mc_rowpass(x, t, mode, state, codes, rows, -1, False, None, None)
+    kc = (codes.view(C, n_pad)[:, :N].t().int() & 0x3FFF)
+    ref = torch.softmax(x, dim=1)
+    rc = ref.view(torch.int16).int() & 0x7FFF
+    diff = (kc - rc).abs()
+    assert int(diff.max()) <= 1, int(diff.max())
+    moved = int((diff != 0).sum())
+    assert moved <= (2e-5 if dtype == torch.bfloat16 else 1.5e-4) * N * C, moved
+    # the histogram built from these codes by the class pass, reduced, vs sorting ATen's scores
+    hist = torch.zeros(C, 2, K.N_CODES, dtype=torch.long, device="cuda")
+    K.curve_hist_update(x, t, hist, "multiclass", None)
+    assert torch.equal(hist, _hist_from_scores(kc.to(torch.int16).view(dtype), t, C))
+    red = K.curve_hist_reduce(hist)
+    labels = torch.nn.functional.one_hot(t, C).bool()
+    auc_s, ap_s, _, _ = eng.samples_scores(ref, labels)
+    assert abs(red[:, 0].mean().item() - auc_s.mean().item()) <= 1e-7
+    assert abs(red[:, 1].mean().item() - ap_s.mean().item()) <= 1e-7
+    # classes without a moved score: the histogram reduction IS the sort-based result
+    same = (diff.sum(0) == 0)
+    torch.testing.assert_close(red[same, 0], auc_s[same], rtol=0, atol=1e-12)
+    torch.testing.assert_close(red[same, 1], ap_s[same], rtol=0, atol=1e-12)
+
+
+def _flip_batches(C, N, seed=5):
+    gen = torch.Generator().manual_seed(seed)
+    out = []
+    for kind in ("logits", "probs", "probs", "logits", "nan_rows", "logits", "probs_nan", "logits"):
+        x = torch.randn(N, C, generator=gen)
+        if kind.startswith("probs"):
+            x = x.softmax(1)
+        if kind.endswith("nan") or kind == "nan_rows":
+            x = _rare_rows(x, kind.startswith("probs"))
+        out.append((x.bfloat16(), torch.randint(0, C, (N,), generator=gen)))
+    return out
+
+
+@pytest.mark.parametrize("C", [520, 1000])
+def test_side_stream_class_pass_matches_single_stream(C, monkeypatch):
+    """Back-to-back updates with the class pass on a side stream (overlapping the next row pass, double-buffered
+    scratch, rolled speculation word) give exactly the single-stream histogram, confusion matrix and code range —
+    across speculation flips, rare rows, a reset in the middle and state_dict / compute consumers."""
+    import torchmetrics_forked_amd as tm
+
+    N = 4096 + 32 * 7 + 5
+    batches = [(x.cuda(), t.cuda()) for x, t in _flip_batches(C, N)]
+
+    def run(side: bool):
+        monkeypatch.setenv("TMX_CURVE_SIDE_STREAM", "1" if side else "0")
+        coll = tm.MetricCollection({"auroc": tm.MulticlassAUROC(num_classes=C, average=None),
+                                    "cm": tm.MulticlassConfusionMatrix(num_classes=C)}).cuda()
+        snaps = []
+        for k, (x, t) in enumerate(batches):
+            coll.update(x, t)
+            if k == 3:
+                snaps.append({n: v.clone() for n, v in coll["auroc"].metric_state.items() if isinstance(v, torch.Tensor)})
+                coll.reset()
+        out = coll.compute()
+        st = coll["auroc"]
+        return out, st.score_hist.clone(), st._tracked_range().clone(), snaps
+
+    a, ha, ra, sa = run(True)
+    b, hb, rb, sb = run(False)
+    assert torch.equal(ha, hb)
+    assert torch.equal(ra, rb)
+    assert torch.equal(a["cm"], b["cm"])
+    torch.testing.assert_close(a["auroc"], b["auroc"], rtol=0, atol=0)
+    assert torch.equal(sa[0]["score_hist"], sb[0]["score_hist"])

@@ -14,9 +14,9 @@ stop_if_fatal() {  # $1 = exit code, $2 = step name
   fi
   echo "step '$2' rc=$rc" | tee -a $OUT/session.log
 }
-STEPS="${STEPS:-pytest,kbench,bench,prof,ref}"
+STEPS="${STEPS:-pytest,bench,prof}"
 if [[ $STEPS == *pytest* ]]; then
-  timeout -k 10 600 python -m pytest tests -m gpu -x -q > $OUT/pytest_gpu.log 2>&1; stop_if_fatal $? pytest; tail -5 $OUT/pytest_gpu.log
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1; stop_if_fatal $? pytest; tail -5 $OUT/pytest_gpu.log
 fi
 if [[ $STEPS == *kexp* ]]; then
   timeout -k 10 120 ./build/curve_hist_exp > $OUT/kexp.json 2> $OUT/kexp.err; stop_if_fatal $? kexp; cat $OUT/kexp.json

@@ -87,9 +87,10 @@ class MulticlassAUROC(MulticlassPrecisionRecallCurve):
 
     def compute(self) -> Tensor:
         if self._shard_info is not None:  # class-sharded compute (``sharded_compute=True`` under DDP)
-            auc, _, pos, neg = self._sharded_scores()
-            _warn_degenerate(pos, neg)
-            return _reduce_auroc(auc.float(), self.average, pos.float())
+            sc = self._sharded_scores()
+            auc, _, pos, neg = sc
+            _warn_degenerate(pos, neg, sc.summary)
+            return _reduce_auroc(auc.float(), self.average, pos.float(), summary=sc.summary, col=0)
         return auroc_compute(self._curve_state(), "multiclass", self.num_classes, self.thresholds, self.average)
 
     def plot(self, val: Optional[Union[Tensor, List[Tensor]]] = None, ax: Optional[_AX_TYPE] = None) -> _PLOT_OUT_TYPE:
@@ -123,9 +124,10 @@ class MultilabelAUROC(MultilabelPrecisionRecallCurve):
 
     def compute(self) -> Tensor:
         if self._shard_info is not None:  # label-sharded compute (``sharded_compute=True`` under DDP)
-            auc, _, pos, neg = self._sharded_scores()
-            _warn_degenerate(pos, neg)
-            return _reduce_auroc(auc.float(), self.average, pos.float())
+            sc = self._sharded_scores()
+            auc, _, pos, neg = sc
+            _warn_degenerate(pos, neg, sc.summary)
+            return _reduce_auroc(auc.float(), self.average, pos.float(), summary=sc.summary, col=0)
         return auroc_compute(
             self._curve_state(), "multilabel", self.num_labels, self.thresholds, self.average, ignore_index=self.ignore_index
         )

@@ -82,8 +82,9 @@ class MulticlassAveragePrecision(MulticlassPrecisionRecallCurve):
 
     def compute(self) -> Tensor:
         if self._shard_info is not None:  # class-sharded compute (``sharded_compute=True`` under DDP)
-            _, ap, pos, _ = self._sharded_scores()
-            return _reduce_auroc(ap.float(), self.average, pos.float())
+            sc = self._sharded_scores()
+            _, ap, pos, _ = sc
+            return _reduce_auroc(ap.float(), self.average, pos.float(), summary=sc.summary, col=1)
         return average_precision_compute(self._curve_state(), "multiclass", self.num_classes, self.thresholds, self.average)
 
     def plot(self, val: Optional[Union[Tensor, List[Tensor]]] = None, ax: Optional[_AX_TYPE] = None) -> _PLOT_OUT_TYPE:
@@ -117,8 +118,9 @@ class MultilabelAveragePrecision(MultilabelPrecisionRecallCurve):
 
     def compute(self) -> Tensor:
         if self._shard_info is not None:  # label-sharded compute (``sharded_compute=True`` under DDP)
-            _, ap, pos, _ = self._sharded_scores()
-            return _reduce_auroc(ap.float(), self.average, pos.float())
+            sc = self._sharded_scores()
+            _, ap, pos, _ = sc
+            return _reduce_auroc(ap.float(), self.average, pos.float(), summary=sc.summary, col=1)
         return average_precision_compute(
             self._curve_state(), "multilabel", self.num_labels, self.thresholds, self.average, self.ignore_index
         )

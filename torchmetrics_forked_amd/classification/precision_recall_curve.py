@@ -7,6 +7,7 @@ State layout (``thresholds=None``):
   * ``preds`` / ``target`` — ``cat`` lists (reference layout) for fp32/fp64 scores.
 With ``thresholds`` given the state is the reference's ``confmat [T, (C,) 2, 2]``.
 """
+import os
 from typing import Any, List, Optional, Sequence, Tuple, Type, Union
 
 import torch
@@ -41,6 +42,41 @@ from torchmetrics_forked_amd.ops import classification as cls_ops
 from torchmetrics_forked_amd.utilities.data import dim_zero_cat
 from torchmetrics_forked_amd.utilities.enums import ClassificationTask
 from torchmetrics_forked_amd.utilities.plot import _AX_TYPE, _PLOT_OUT_TYPE, plot_curve
+
+
+def _side_stream_ok(p: Tensor, rng: Optional[Tensor]) -> bool:
+    """The split (side-stream) route takes aligned ``[N, C]`` 16-bit rows with C % 8 == 0, C <= 1024 on the GPU.
+
+    Opt-in (``TMX_CURVE_SIDE_STREAM=1``): measured on MI355X at 65536 x 1000 bf16, back-to-back updates take
+    117.7 us each with the class pass overlapping the next row pass vs 110.5 us on one stream
+    (``profiles/side_stream_overlap.json``).  The row pass holds 128 KiB of LDS per CU (two 64-KiB blocks), so a
+    64-KiB class-pass block cannot co-reside; the two passes only time-slice the CUs and compete for HBM."""
+    if rng is None or not p.is_cuda or os.environ.get("TMX_CURVE_SIDE_STREAM", "0") != "1":
+        return False
+    n, c = p.shape
+    return p.is_contiguous() and c % 8 == 0 and c <= 1024 and p.data_ptr() % 16 == 0 and n > 0
+
+
+def _side_buffers(metric: Any, p: Tensor) -> dict:
+    """Per-metric double-buffered scratch (class-major codes, rare-row lists, pass states) for the overlapped update,
+    in ``__dict__["_side_bufs"]`` (left out of pickling / deepcopy by ``Metric.__getstate__``); the side stream and
+    its events live in the native library, keyed by the codes buffer."""
+    n, c = p.shape
+    n_pad = (n + 31) // 32 * 32
+    bufs = metric.__dict__.get("_side_bufs")
+    if bufs is None or bufs["codes"].device != p.device or bufs["codes"].shape[1] < c * n_pad or bufs["rows"].shape[1] < 2 * n:
+        if bufs is not None:  # buffers about to be dropped: the current stream waits for their last readers
+            bufs["join"]()
+        codes = torch.empty(2, c * n_pad, dtype=torch.int16, device=p.device)
+        bufs = {
+            "codes": codes,
+            "rows": torch.empty(2, 2 * n, dtype=torch.int32, device=p.device),
+            "states": torch.zeros(2, 6, dtype=torch.int32, device=p.device),
+            "next": 0,
+            "join": lambda: torch.ops.tmx.curve_side_join(codes),
+        }
+        metric.__dict__["_side_bufs"] = bufs
+    return bufs
 
 
 class _CurveMetric(Metric):
@@ -93,13 +129,14 @@ class _CurveMetric(Metric):
     def _ensure_hist(self, device: torch.device) -> Tensor:
         if self.score_hist.numel() == 0:
             self.score_hist = torch.zeros(self._num, 2, eng.N_CODES, dtype=torch.long, device=device)
-            self._set_range(self.score_hist, torch.tensor([eng.N_CODES, -1], dtype=torch.int32, device=device))
+            empty = torch.tensor([eng.N_CODES, -1], dtype=torch.int32, device=device).repeat(self._num, 1)
+            self._set_range(self.score_hist, empty)
         return self.score_hist
 
     # ---- occupied code range of ``score_hist`` ------------------------------------------------------------
-    # ``_code_range`` (int32[2] = [lo, hi], on the histogram's device) is widened by the class-pass kernel of every
-    # update; ``compute`` and the histogram collectives then touch only [lo, hi] (softmax scores fill a few binades,
-    # about a fifth of the 16384 codes).  It belongs to the tensor object in ``_range_hist``: when ``score_hist`` is
+    # ``_code_range`` (int32[C, 2] = per-class [lo, hi], on the histogram's device) is widened by the class-pass kernel
+    # of every update; ``compute`` reads only each class's [lo, hi] and the histogram collectives only the union
+    # (softmax scores fill a few binades, about a fifth of the 16384 codes).  It belongs to the tensor object in ``_range_hist``: when ``score_hist`` is
     # replaced by anything that does not maintain it (load_state_dict, forward's merge, .to(...)), the range is
     # recomputed on device from the histogram at its next use — one pass, no host sync.  ``score_hist`` is internal
     # state; code that edits it in place must call ``_invalidate_range()``.
@@ -124,9 +161,10 @@ class _CurveMetric(Metric):
             return None
         if self._range_hist is hist and self._code_range is not None and self._code_range.device == hist.device:
             return self._code_range
-        occ = hist.amax(dim=(0, 1)) > 0
+        occ = hist.amax(dim=1) > 0  # [C, K]
         idx = torch.arange(hist.shape[-1], device=hist.device)
-        rng = torch.stack([torch.where(occ, idx, hist.shape[-1]).amin(), torch.where(occ, idx, -1).amax()]).to(torch.int32)
+        rng = torch.stack([torch.where(occ, idx, hist.shape[-1]).amin(-1), torch.where(occ, idx, -1).amax(-1)], 1)
+        rng = rng.to(torch.int32).contiguous()
         self._set_range(hist, rng, None)
         return rng
 
@@ -164,9 +202,12 @@ class _CurveMetric(Metric):
                 )
             elif self._task == "multiclass":
                 p = torch.movedim(preds, 1, -1).reshape(-1, self._num)
-                cls_ops.curve_hist_update(
-                    p, target.reshape(-1), hist, "multiclass", ii, confmat_out, err_flag, self._mode_state(p), code_range=rng
-                )
+                if _side_stream_ok(p, rng):
+                    self._mc_update_side_stream(p, target.reshape(-1), hist, ii, confmat_out, err_flag, rng)
+                else:
+                    cls_ops.curve_hist_update(
+                        p, target.reshape(-1), hist, "multiclass", ii, confmat_out, err_flag, self._mode_state(p), code_range=rng
+                    )
             else:
                 cls_ops.curve_hist_update(preds, target, hist, "multilabel", ii, err_flag=err_flag, code_range=rng)
             if rng is None:
@@ -187,6 +228,27 @@ class _CurveMetric(Metric):
             st = multilabel_curve_update(preds, target, self._num, None, ii, force_samples=True)
         self.preds.append(st[1])
         self.target.append(st[2])
+
+    def _mc_update_side_stream(
+        self, p: Tensor, target: Tensor, hist: Tensor, ii: Optional[int], confmat_out: Optional[Tensor],
+        err_flag: Optional[Tensor], rng: Tensor,
+    ) -> None:
+        """Multiclass exact-histogram update with the class pass on a side stream.
+
+        The row pass (softmax codes, arg-max + confusion matrix, HBM-bound) runs on the current stream and writes
+        class-major codes into one of two scratch buffers; the class pass (LDS histograms, flush into
+        ``score_hist``) of this batch then runs on a side stream and overlaps the NEXT batch's row pass, which uses
+        the other buffer.  Reusing a buffer waits for the class pass that last read it; every state consumer joins
+        the side stream first (``Metric._join_side_work``)."""
+        bufs = _side_buffers(self, p)
+        i = bufs["next"]
+        bufs["next"] = i ^ 1
+        t = target if target.dtype == torch.long and target.is_contiguous() else target.long().contiguous()
+        torch.ops.tmx.curve_mc_update_overlapped(
+            p, t, self._mode_state(p), bufs["states"], bufs["codes"], bufs["rows"], i, hist, -1 if ii is None else ii,
+            ii is not None, confmat_out, err_flag, rng,
+        )
+        self.__dict__["_side_event"] = bufs["join"]
 
     def _reduce_states(self, incoming_state: dict) -> None:
         """``forward`` merge: the lazily materialised histogram may be empty on either side."""
@@ -234,7 +296,7 @@ class _CurveMetric(Metric):
         hist = torch.zeros(owned, 2, self.score_hist.shape[-1], dtype=torch.long, device=self.score_hist.device)
         hist[:, :, lo : hi + 1] = shard[:owned]
         self.score_hist = hist
-        self._set_range(hist, torch.tensor([lo, hi], dtype=torch.int32, device=hist.device), None)
+        self._set_range(hist, torch.tensor([lo, hi], dtype=torch.int32, device=hist.device).repeat(owned, 1), None)
         self._shard_info = (first, owned, per, group)
 
     def unsync(self, should_unsync: bool = True) -> None:
@@ -260,7 +322,10 @@ class _CurveMetric(Metric):
         allv = comm.new_empty(world, 4, per)
         _collective(dist.all_gather_into_tensor, allv.view(-1), comm.reshape(-1), what="all_gather(per-class scores)", group=group)
         allv = allv.permute(1, 0, 2).reshape(4, world * per)[:, : self._num].to(local.device)
-        return allv[0], allv[1], allv[2], allv[3]
+        from torchmetrics_forked_amd.functional.classification.auroc import ExactScores
+
+        summ = cls_ops.curve_summary(allv.t().contiguous()) if allv.is_cuda else None
+        return ExactScores.of(allv[0], allv[1], allv[2], allv[3], summ)
 
     _DTYPE_CODES = {None: 0, torch.bfloat16: 1, torch.float16: 2}
 
@@ -286,7 +351,8 @@ class _CurveMetric(Metric):
                 else:
                     bound = self.score_hist.amax().reshape(1)
                 stats = torch.cat([
-                    torch.ones(1, dtype=torch.long, device=rng.device), bound.long(), rng.long(),
+                    torch.ones(1, dtype=torch.long, device=rng.device), bound.long(),
+                    rng[:, 0].amin().reshape(1).long(), rng[:, 1].amax().reshape(1).long(),
                     torch.tensor([dcode, has_samples], dtype=torch.long, device=rng.device),
                 ])
             else:
@@ -330,7 +396,7 @@ class _CurveMetric(Metric):
                     hist = torch.zeros(shape, dtype=torch.long, device=synced.device)
                     hist[:, :, lo : hi + 1] = synced
                     self.score_hist = hist
-                    self._set_range(hist, torch.tensor([lo, hi], dtype=torch.int32, device=hist.device), bound)
+                    self._set_range(hist, torch.tensor([lo, hi], dtype=torch.int32, device=hist.device).repeat(shape[0], 1), bound)
                 return
         super()._sync_dist(dist_sync_fn, process_group)
 

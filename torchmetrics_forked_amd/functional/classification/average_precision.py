@@ -40,11 +40,12 @@ def average_precision_compute(
         if task == "binary":
             return res[0]
         return _reduce_auroc(res, average, state[1][0, :, 1, :].sum(-1))
-    _, ap, P, _ = _exact_scores(state, task, num, ignore_index)
+    sc = _exact_scores(state, task, num, ignore_index)
+    _, ap, P, _ = sc
     res = ap.to(torch.float32)
     if task == "binary":
         return res[0]
-    return _reduce_auroc(res, average, P.to(torch.float32))
+    return _reduce_auroc(res, average, P.to(torch.float32), summary=sc.summary, col=1)
 
 
 def binary_average_precision(

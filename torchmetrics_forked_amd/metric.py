@@ -197,7 +197,24 @@ class Metric(Module, ABC):
 
     @property
     def metric_state(self) -> Dict[str, Union[List[Tensor], Tensor]]:
+        self._join_side_work()
         return {name: getattr(self, name) for name in self._defaults}
+
+    # ---- side-stream work ------------------------------------------------------------------------------------
+    # An update may leave kernels that write this metric's states running on a side HIP stream (the curve metrics'
+    # class pass overlaps the next batch's row pass).  ``_side_event`` marks the last of them; every consumer of
+    # the states (compute, sync, reset, state_dict, pickling, device moves, forward) makes the current stream wait
+    # for it first.
+    _side_event: Optional[Any] = None
+
+    def _join_side_work(self) -> None:
+        ev = self.__dict__.get("_side_event")
+        if ev is not None:
+            self.__dict__["_side_event"] = None
+            if callable(ev):  # native join (the current stream waits for the side-stream passes)
+                ev()
+            else:
+                torch.cuda.current_stream().wait_event(ev)
 
     @property
     def device(self) -> "torch.device":
@@ -459,6 +476,7 @@ class Metric(Module, ABC):
                 )
             if self._computed is not None:
                 return self._computed
+            self._join_side_work()
             # every host-side consequence of device flags (deferred input checks, degenerate-class warnings, ...)
             # is read once, when the outermost compute (or MetricCollection.compute) ends
             with host_checks() as batch:
@@ -504,6 +522,7 @@ class Metric(Module, ABC):
 
     def reset(self) -> None:
         """Restore every state to its default (on the state's current device)."""
+        self._join_side_work()
         self._update_count = 0
         self._forward_cache = None
         self._computed = None
@@ -523,7 +542,8 @@ class Metric(Module, ABC):
         return deepcopy(self)
 
     def __getstate__(self) -> Dict[str, Any]:
-        return {k: v for k, v in self.__dict__.items() if k not in ("update", "compute", "_update_signature")}
+        self._join_side_work()
+        return {k: v for k, v in self.__dict__.items() if k not in ("update", "compute", "_update_signature", "_side_bufs")}
 
     def __setstate__(self, state: Dict[str, Any]) -> None:
         self.__dict__.update(state)
@@ -557,6 +577,7 @@ class Metric(Module, ABC):
         return out
 
     def _apply(self, fn: Callable, exclude_state: Sequence[str] = "") -> Module:
+        self._join_side_work()
         this = super()._apply(fn)
         fs = str(fn)
         is_cast = any(f in fs for f in ("Module.type", "Module.half", "Module.float", "Module.double", "Module.bfloat16"))
@@ -592,6 +613,7 @@ class Metric(Module, ABC):
     def state_dict(  # type: ignore[override]
         self, destination: Optional[Dict[str, Any]] = None, prefix: str = "", keep_vars: bool = False
     ) -> Dict[str, Any]:
+        self._join_side_work()
         destination = super().state_dict(destination=destination, prefix=prefix, keep_vars=keep_vars)  # type: ignore
         for key in self._defaults:
             if not self._persistent[key]:

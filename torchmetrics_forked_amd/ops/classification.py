@@ -169,7 +169,7 @@ def curve_hist_update(
 ) -> None:
     """Accumulate the exact 16-bit score histogram ``hist[C, 2, 16384]`` (see csrc/classification.hip).
 
-    ``code_range`` (int32[2] on the GPU, optional) is widened to cover every code this batch touched, so
+    ``code_range`` (int32[C, 2] on the GPU, optional) is widened per class to cover every code this batch touched, so
     :func:`curve_hist_reduce` and the histogram collectives can skip the never-occupied codes.
 
     ``task="multiclass"``: preds ``[N, C]`` scores (softmax applied if any value outside [0,1]), target ``[N]``;
@@ -226,7 +226,7 @@ def curve_hist_update(
 def curve_hist_reduce(hist: Tensor, code_range: Optional[Tensor] = None) -> Tensor:
     """float64 ``[C, 4]`` = (auroc, average_precision, n_pos, n_neg) per class, from ``hist[C, 2, K]``.
 
-    ``code_range`` (int32[2] ``[lo, hi]``, GPU): every bin outside it is known to be zero and is not read."""
+    ``code_range`` (int32[C, 2], per-class ``[lo, hi]``, GPU): every bin outside it is known to be zero and is not read."""
     if ops.use_native(hist):
         return torch.ops.tmx.curve_hist_reduce(hist, code_range)
     neg = hist[:, 0].flip(-1).double()
@@ -240,6 +240,23 @@ def curve_hist_reduce(hist: Tensor, code_range: Optional[Tensor] = None) -> Tens
     prec = torch.where(tp + fp > 0, tp / (tp + fp).clamp_min(1), torch.zeros_like(tp))
     ap = torch.where(P > 0, (pos * prec).sum(-1) / P.clamp_min(1), torch.full_like(P, float("nan")))
     return torch.stack([auroc, ap, P, N], dim=1)
+
+
+def curve_summary(scores: Tensor) -> Tensor:
+    """float64[8] from ``curve_hist_reduce``'s ``[C, 4]``: (any N<=0, any P<=0, any AUROC NaN, any AP NaN, macro AUROC,
+    weighted AUROC, macro AP, weighted AP) with NaN classes ignored and weights = P (one native launch on the GPU)."""
+    if ops.use_native(scores):
+        return torch.ops.tmx.curve_summary(scores.contiguous())
+    a, ap, P, N = scores.double().unbind(1)
+    out = []
+    for v in (a, ap):
+        ok = ~torch.isnan(v)
+        macro = v[ok].mean() if ok.any() else torch.tensor(float("nan"), dtype=torch.float64)
+        w = P[ok]
+        weighted = (v[ok] * w).sum() / w.sum() if w.sum() > 0 else torch.tensor(float("nan"), dtype=torch.float64)
+        out += [macro, weighted]
+    flags = [(N <= 0).any(), (P <= 0).any(), torch.isnan(a).any(), torch.isnan(ap).any()]
+    return torch.stack([f.double() for f in flags] + [o.double() for o in out]).to(scores.device)
 
 
 def binned_curve_update(

@@ -53,6 +53,12 @@ class _MulticlassScoresPlan:
             m._computed = None
             m._update_count += 1
         curve._curve_update(preds, target, confmat_out=delta, err_flag=err)
+        side = curve.__dict__.get("_side_event")
+        if side is not None:  # the side-stream class pass also adds rare rows into the confusion matrix
+            if len(confmats) > 1:
+                curve._join_side_work()
+            else:
+                confmats[0].__dict__["_side_event"] = side
         if len(confmats) > 1:
             for cm in confmats:
                 cm.confmat += delta
