@@ -264,3 +264,41 @@ def test_dice_errors():
         m.dice(torch.rand(4), torch.randint(0, 2, (4,)), average="bad")
     with pytest.raises(ValueError, match="number of classes"):
         m.dice(torch.rand(4), torch.randint(0, 2, (4,)), average="macro")
+
+
+@pytest.mark.parametrize("thresholds", [[0.9, 0.1, 0.5], [0.5, 0.5, 0.2, 0.8], torch.tensor([1.0, 0.0, 0.3])])
+def test_binned_curves_unsorted_thresholds(reference, thresholds):
+    """Thresholds in any order (reference: every threshold compared on its own, rows in the given order)."""
+    import torchmetrics_forked_amd.functional.classification as F
+    import torchmetrics_forked_amd.classification as M
+
+    R = reference.functional.classification
+    g = torch.Generator().manual_seed(3)
+    n, c = 200, 4
+    cases = [
+        ("binary_precision_recall_curve", (torch.rand(n, generator=g), torch.randint(0, 2, (n,), generator=g)), {}),
+        ("binary_roc", (torch.rand(n, generator=g), torch.randint(0, 2, (n,), generator=g)), {}),
+        ("multiclass_precision_recall_curve", (torch.randn(n, c, generator=g).softmax(-1), torch.randint(0, c, (n,), generator=g)), {"num_classes": c}),
+        ("multilabel_roc", (torch.rand(n, c, generator=g), torch.randint(0, 2, (n, c), generator=g)), {"num_labels": c}),
+        ("multiclass_average_precision", (torch.randn(n, c, generator=g).softmax(-1), torch.randint(0, c, (n,), generator=g)), {"num_classes": c}),
+    ]
+    for name, args, kw in cases:
+        thr = thresholds.clone() if isinstance(thresholds, torch.Tensor) else list(thresholds)
+        got = getattr(F, name)(*args, thresholds=thr, **kw)
+        exp = getattr(R, name)(*args, thresholds=thresholds.clone() if isinstance(thresholds, torch.Tensor) else list(thresholds), **kw)
+        _cmp_tree(got, exp)
+    m = M.BinaryPrecisionRecallCurve(thresholds=list(thresholds) if not isinstance(thresholds, torch.Tensor) else thresholds.clone())
+    p, t = torch.rand(n, generator=g), torch.randint(0, 2, (n,), generator=g)
+    m.update(p[:100], t[:100])
+    m.update(p[100:], t[100:])
+    _cmp_tree(m.compute(), R.binary_precision_recall_curve(p, t, thresholds=list(thresholds) if not isinstance(thresholds, torch.Tensor) else thresholds.clone()))
+
+
+def _cmp_tree(a, b):
+    if isinstance(a, (list, tuple)):
+        assert len(a) == len(b)
+        for x, y in zip(a, b):
+            _cmp_tree(x, y)
+        return
+    assert a.shape == b.shape, (a.shape, b.shape)
+    assert torch.allclose(a.double(), b.double(), atol=1e-6, equal_nan=True), (a, b)

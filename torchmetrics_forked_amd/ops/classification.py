@@ -259,6 +259,22 @@ def curve_summary(scores: Tensor) -> Tensor:
     return torch.stack([f.double() for f in flags] + [o.double() for o in out]).to(scores.device)
 
 
+def _threshold_order(thresholds: Tensor) -> Optional[Tensor]:
+    """``argsort(thresholds)`` when they are not ascending, else ``None``.  Cached on the tensor (keyed by its version
+    counter), so the one host read happens once per threshold tensor, not per update."""
+    cached = getattr(thresholds, "_tmx_order", None)
+    if cached is not None and cached[0] == thresholds._version:
+        return cached[1]
+    order = None
+    if thresholds.numel() > 1 and not bool((thresholds[1:] >= thresholds[:-1]).all()):
+        order = torch.argsort(thresholds, stable=True)
+    try:
+        thresholds._tmx_order = (thresholds._version, order)
+    except (AttributeError, RuntimeError):  # pragma: no cover - tensors that refuse attributes
+        pass
+    return order
+
+
 def binned_curve_update(
     preds: Tensor,
     target: Tensor,
@@ -272,6 +288,14 @@ def binned_curve_update(
 
     ``err_flag`` (int32[1], GPU only) is OR-ed with 1 when a non-ignored target is outside {0, 1} (binary /
     multilabel) or ``[0, C)`` (multiclass) -- the deferred value check, folded into the histogram pass."""
+    order = _threshold_order(thresholds)
+    if order is not None:
+        # the bucket search below counts "#thresholds <= p", which needs ascending thresholds; the reference compares
+        # every threshold on its own (any order), so bin against the sorted copy and add the rows back in place
+        part = torch.zeros_like(confmat)
+        binned_curve_update(preds, target, thresholds[order], part, task, ignore_index, err_flag)
+        confmat.index_add_(0, order, part)
+        return
     tcode = 0 if task == "multiclass" else 1
     if ops.use_native(target):
         torch.ops.tmx.binned_curve_update(

@@ -1,15 +1,19 @@
-"""Legacy ("auto-detected case") classification input handling used by ``Dice``.
+"""Auto-detected ("legacy") classification inputs, used only by ``Dice``.
 
-Behavioural parity with reference ``utilities/checks.py:33-456`` (``_input_format_classification`` and its case
-checks) and ``functional/classification/stat_scores.py:820-1070`` (``_stat_scores_update`` /
-``_reduce_stat_scores``).  The task-specific (binary / multiclass / multilabel) metrics do not use this path.
+Behavioural parity with the reference's ``utilities/checks.py:33-456`` (``_input_format_classification``) and
+``functional/classification/stat_scores.py:820-1070`` (``_stat_scores_update`` / ``_reduce_stat_scores``); the
+task-specific metrics never come here.  The error messages are part of the contract and are kept verbatim.
 
-Inputs fall into one of four cases deduced from shape and dtype:
-  binary (N,) float preds; multi-class (N,) int preds or (N, C) float preds; multi-label (N, ...) float preds with
-  same-shape binary target; multi-dim multi-class (N, C, ...) float or (N, ...) int preds.
-They are converted to int one-hot style ``(N, C)`` or ``(N, C, X)`` tensors.
+Structure:
+
+* :func:`_detect_case` derives the input case from shapes / dtypes — binary ``(N,)`` float preds, multi-class
+  ``(N,)`` int or ``(N, C)`` float preds, multi-label ``(N, ...)`` float preds with a same-shape binary target,
+  multi-dim multi-class ``(N, C, ...)`` float or ``(N, ...)`` int preds — and the number of classes it implies;
+* the checks are ordered rule tables ``(violated?, message)`` evaluated lazily, first violation raises;
+* :func:`_input_format_classification` converts every case to int one-hot layouts ``(N, C)`` / ``(N, C, X)``;
+* :func:`_stat_scores` counts tp / fp / tn / fn with one stacked reduction.
 """
-from typing import List, Optional, Tuple, Union
+from typing import Callable, List, Optional, Sequence, Tuple, Union
 
 import torch
 from torch import Tensor
@@ -17,134 +21,117 @@ from torch import Tensor
 from torchmetrics_forked_amd.utilities.data import select_topk, to_onehot
 from torchmetrics_forked_amd.utilities.enums import AverageMethod, DataType, MDMCAverageMethod
 
+_Rule = Tuple[Callable[[], bool], str]
+
+
+def _raise_first(rules: Sequence[_Rule]) -> None:
+    """Evaluate the rules in order (lazily: later conditions may assume earlier ones held) and raise on the first hit."""
+    for violated, message in rules:
+        if violated():
+            raise ValueError(message)
+
 
 def _empty(preds: Tensor, target: Tensor) -> bool:
     return preds.numel() == target.numel() == 0
 
 
-def _basic_input_validation(
-    preds: Tensor, target: Tensor, threshold: float, multiclass: Optional[bool], ignore_index: Optional[int]
-) -> None:
-    if _empty(preds, target):
-        return
-    if target.is_floating_point():
-        raise ValueError("The `target` has to be an integer tensor.")
-    # negative targets are only legal when they are the (negative) ignore index; ignore_index=0 is exempt too
-    negatives_forbidden = ignore_index is None or ignore_index > 0
-    if negatives_forbidden and target.min() < 0:
-        raise ValueError("The `target` has to be a non-negative tensor.")
-    p_float = preds.is_floating_point()
-    if not p_float and preds.min() < 0:
-        raise ValueError("If `preds` are integers, they have to be non-negative.")
-    if preds.shape[0] != target.shape[0]:
-        raise ValueError("The `preds` and `target` should have the same first dimension.")
-    if multiclass is False and target.max() > 1:
-        raise ValueError("If you set `multiclass=False`, then `target` should not exceed 1.")
-    if multiclass is False and not p_float and preds.max() > 1:
-        raise ValueError("If you set `multiclass=False` and `preds` are integers, then `preds` should not exceed 1.")
-
-
-def _check_shape_and_type_consistency(preds: Tensor, target: Tensor) -> Tuple[DataType, int]:
-    p_float = preds.is_floating_point()
+def _detect_case(preds: Tensor, target: Tensor) -> Tuple[DataType, int]:
+    """(case, implied number of classes) from the shapes and dtypes; raises on inconsistent inputs."""
+    floating = preds.is_floating_point()
     if preds.ndim == target.ndim:
-        if preds.shape != target.shape:
-            raise ValueError(
-                "The `preds` and `target` should have the same shape,",
-                f" got `preds` with shape={preds.shape} and `target` with shape={target.shape}.",
-            )
-        if p_float and target.numel() > 0 and target.max() > 1:
-            raise ValueError(
-                "If `preds` and `target` are of shape (N, ...) and `preds` are floats, `target` should be binary."
-            )
-        if preds.ndim == 1:
-            case = DataType.BINARY if p_float else DataType.MULTICLASS
-        else:
-            case = DataType.MULTILABEL if p_float else DataType.MULTIDIM_MULTICLASS
-        implied = preds[0].numel() if preds.numel() > 0 else 0
-        return case, implied
+        _raise_first([
+            (lambda: preds.shape != target.shape,
+             "The `preds` and `target` should have the same shape,"
+             f" got `preds` with shape={preds.shape} and `target` with shape={target.shape}."),
+            (lambda: floating and target.numel() > 0 and bool(target.max() > 1),
+             "If `preds` and `target` are of shape (N, ...) and `preds` are floats, `target` should be binary."),
+        ])
+        flat = preds.ndim == 1
+        case = (DataType.BINARY if flat else DataType.MULTILABEL) if floating else (
+            DataType.MULTICLASS if flat else DataType.MULTIDIM_MULTICLASS)
+        return case, (preds[0].numel() if preds.numel() > 0 else 0)
     if preds.ndim == target.ndim + 1:
-        if not p_float:
-            raise ValueError("If `preds` have one dimension more than `target`, `preds` should be a float tensor.")
-        if preds.shape[2:] != target.shape[1:]:
-            raise ValueError(
-                "If `preds` have one dimension more than `target`, the shape of `preds` should be"
-                " (N, C, ...), and the shape of `target` should be (N, ...)."
-            )
-        implied = preds.shape[1] if preds.numel() > 0 else 0
-        return (DataType.MULTICLASS if preds.ndim == 2 else DataType.MULTIDIM_MULTICLASS), implied
+        _raise_first([
+            (lambda: not floating, "If `preds` have one dimension more than `target`, `preds` should be a float tensor."),
+            (lambda: preds.shape[2:] != target.shape[1:],
+             "If `preds` have one dimension more than `target`, the shape of `preds` should be"
+             " (N, C, ...), and the shape of `target` should be (N, ...)."),
+        ])
+        case = DataType.MULTICLASS if preds.ndim == 2 else DataType.MULTIDIM_MULTICLASS
+        return case, (preds.shape[1] if preds.numel() > 0 else 0)
     raise ValueError(
         "Either `preds` and `target` both should have the (same) shape (N, ...), or `target` should be (N, ...)"
         " and `preds` should be (N, C, ...)."
     )
 
 
-def _check_num_classes_binary(num_classes: int, multiclass: Optional[bool]) -> None:
-    if num_classes > 2:
-        raise ValueError("Your data is binary, but `num_classes` is larger than 2.")
-    if num_classes == 2 and not multiclass:
-        raise ValueError(
-            "Your data is binary and `num_classes=2`, but `multiclass` is not True."
-            " Set it to True if you want to transform binary data to multi-class format."
-        )
-    if num_classes == 1 and multiclass:
-        raise ValueError(
-            "You have binary data and have set `multiclass=True`, but `num_classes` is 1."
-            " Either set `multiclass=None`(default) or set `num_classes=2`"
-            " to transform binary data to multi-class format."
-        )
+def _basic_rules(preds: Tensor, target: Tensor, multiclass: Optional[bool], ignore_index: Optional[int]) -> List[_Rule]:
+    floating = preds.is_floating_point()
+    # negative targets are legal only as a negative ignore_index (ignore_index=0 exempts them as well)
+    negatives_forbidden = ignore_index is None or ignore_index > 0
+    return [
+        (lambda: target.is_floating_point(), "The `target` has to be an integer tensor."),
+        (lambda: negatives_forbidden and bool(target.min() < 0), "The `target` has to be a non-negative tensor."),
+        (lambda: not floating and bool(preds.min() < 0), "If `preds` are integers, they have to be non-negative."),
+        (lambda: preds.shape[0] != target.shape[0], "The `preds` and `target` should have the same first dimension."),
+        (lambda: multiclass is False and bool(target.max() > 1), "If you set `multiclass=False`, then `target` should not exceed 1."),
+        (lambda: multiclass is False and not floating and bool(preds.max() > 1),
+         "If you set `multiclass=False` and `preds` are integers, then `preds` should not exceed 1."),
+    ]
 
 
-def _check_num_classes_mc(
-    preds: Tensor, target: Tensor, num_classes: int, multiclass: Optional[bool], implied_classes: int
-) -> None:
-    if num_classes == 1 and multiclass is not False:
-        raise ValueError(
-            "You have set `num_classes=1`, but predictions are integers."
-            " If you want to convert (multi-dimensional) multi-class data with 2 classes"
-            " to binary/multi-label, set `multiclass=False`."
-        )
-    if num_classes > 1:
-        if multiclass is False and implied_classes != num_classes:
-            raise ValueError(
-                "You have set `multiclass=False`, but the implied number of classes "
-                " (from shape of inputs) does not match `num_classes`. If you are trying to"
-                " transform multi-dim multi-class data with 2 classes to multi-label, `num_classes`"
-                " should be either None or the product of the size of extra dimensions (...)."
-                " See Input Types in Metrics documentation."
-            )
-        if target.numel() > 0 and num_classes <= target.max():
-            raise ValueError("The highest label in `target` should be smaller than `num_classes`.")
-        if preds.shape != target.shape and num_classes != implied_classes:
-            raise ValueError("The size of C dimension of `preds` does not match `num_classes`.")
-
-
-def _check_num_classes_ml(num_classes: int, multiclass: Optional[bool], implied_classes: int) -> None:
-    if multiclass and num_classes != 2:
-        raise ValueError(
-            "Your have set `multiclass=True`, but `num_classes` is not equal to 2."
-            " If you are trying to transform multi-label data to 2 class multi-dimensional"
-            " multi-class, you should set `num_classes` to either 2 or None."
-        )
-    if not multiclass and num_classes != implied_classes:
-        raise ValueError("The implied number of classes (from shape of inputs) does not match num_classes.")
-
-
-def _check_top_k(top_k: int, case: str, implied_classes: int, multiclass: Optional[bool], preds_float: bool) -> None:
+def _num_classes_rules(
+    case: DataType, preds: Tensor, target: Tensor, num_classes: int, multiclass: Optional[bool], implied: int
+) -> List[_Rule]:
     if case == DataType.BINARY:
-        raise ValueError("You can not use `top_k` parameter with binary data.")
-    if not isinstance(top_k, int) or top_k <= 0:
-        raise ValueError("The `top_k` has to be an integer larger than 0.")
-    if not preds_float:
-        raise ValueError("You have set `top_k`, but you do not have probability predictions.")
-    if multiclass is False:
-        raise ValueError("If you set `multiclass=False`, you can not set `top_k`.")
-    if case == DataType.MULTILABEL and multiclass:
-        raise ValueError(
-            "If you want to transform multi-label data to 2 class multi-dimensional"
-            "multi-class data using `multiclass=True`, you can not use `top_k`."
-        )
-    if top_k >= implied_classes:
-        raise ValueError("The `top_k` has to be strictly smaller than the `C` dimension of `preds`.")
+        return [
+            (lambda: num_classes > 2, "Your data is binary, but `num_classes` is larger than 2."),
+            (lambda: num_classes == 2 and not multiclass,
+             "Your data is binary and `num_classes=2`, but `multiclass` is not True."
+             " Set it to True if you want to transform binary data to multi-class format."),
+            (lambda: num_classes == 1 and bool(multiclass),
+             "You have binary data and have set `multiclass=True`, but `num_classes` is 1."
+             " Either set `multiclass=None`(default) or set `num_classes=2`"
+             " to transform binary data to multi-class format."),
+        ]
+    if case in (DataType.MULTICLASS, DataType.MULTIDIM_MULTICLASS):
+        return [
+            (lambda: num_classes == 1 and multiclass is not False,
+             "You have set `num_classes=1`, but predictions are integers."
+             " If you want to convert (multi-dimensional) multi-class data with 2 classes"
+             " to binary/multi-label, set `multiclass=False`."),
+            (lambda: num_classes > 1 and multiclass is False and implied != num_classes,
+             "You have set `multiclass=False`, but the implied number of classes "
+             " (from shape of inputs) does not match `num_classes`. If you are trying to"
+             " transform multi-dim multi-class data with 2 classes to multi-label, `num_classes`"
+             " should be either None or the product of the size of extra dimensions (...)."
+             " See Input Types in Metrics documentation."),
+            (lambda: num_classes > 1 and target.numel() > 0 and bool(num_classes <= target.max()),
+             "The highest label in `target` should be smaller than `num_classes`."),
+            (lambda: num_classes > 1 and preds.shape != target.shape and num_classes != implied,
+             "The size of C dimension of `preds` does not match `num_classes`."),
+        ]
+    return [
+        (lambda: bool(multiclass) and num_classes != 2,
+         "Your have set `multiclass=True`, but `num_classes` is not equal to 2."
+         " If you are trying to transform multi-label data to 2 class multi-dimensional"
+         " multi-class, you should set `num_classes` to either 2 or None."),
+        (lambda: not multiclass and num_classes != implied,
+         "The implied number of classes (from shape of inputs) does not match num_classes."),
+    ]
+
+
+def _top_k_rules(top_k: int, case: DataType, implied: int, multiclass: Optional[bool], floating: bool) -> List[_Rule]:
+    return [
+        (lambda: case == DataType.BINARY, "You can not use `top_k` parameter with binary data."),
+        (lambda: not isinstance(top_k, int) or top_k <= 0, "The `top_k` has to be an integer larger than 0."),
+        (lambda: not floating, "You have set `top_k`, but you do not have probability predictions."),
+        (lambda: multiclass is False, "If you set `multiclass=False`, you can not set `top_k`."),
+        (lambda: case == DataType.MULTILABEL and bool(multiclass),
+         "If you want to transform multi-label data to 2 class multi-dimensional"
+         "multi-class data using `multiclass=True`, you can not use `top_k`."),
+        (lambda: top_k >= implied, "The `top_k` has to be strictly smaller than the `C` dimension of `preds`."),
+    ]
 
 
 def _check_classification_inputs(
@@ -156,27 +143,21 @@ def _check_classification_inputs(
     top_k: Optional[int],
     ignore_index: Optional[int] = None,
 ) -> DataType:
-    _basic_input_validation(preds, target, threshold, multiclass, ignore_index)
-    case, implied = _check_shape_and_type_consistency(preds, target)
+    if not _empty(preds, target):
+        _raise_first(_basic_rules(preds, target, multiclass, ignore_index))
+    case, implied = _detect_case(preds, target)
     if preds.shape != target.shape:
-        if multiclass is False and implied != 2:
-            raise ValueError(
-                "You have set `multiclass=False`, but have more than 2 classes in your data,"
-                " based on the C dimension of `preds`."
-            )
-        if target.max() >= implied:
-            raise ValueError(
-                "The highest label in `target` should be smaller than the size of the `C` dimension of `preds`."
-            )
+        _raise_first([
+            (lambda: multiclass is False and implied != 2,
+             "You have set `multiclass=False`, but have more than 2 classes in your data,"
+             " based on the C dimension of `preds`."),
+            (lambda: bool(target.max() >= implied),
+             "The highest label in `target` should be smaller than the size of the `C` dimension of `preds`."),
+        ])
     if num_classes:
-        if case == DataType.BINARY:
-            _check_num_classes_binary(num_classes, multiclass)
-        elif case in (DataType.MULTICLASS, DataType.MULTIDIM_MULTICLASS):
-            _check_num_classes_mc(preds, target, num_classes, multiclass, implied)
-        else:
-            _check_num_classes_ml(num_classes, multiclass, implied)
+        _raise_first(_num_classes_rules(case, preds, target, num_classes, multiclass, implied))
     if top_k is not None:
-        _check_top_k(top_k, case, implied, multiclass, preds.is_floating_point())
+        _raise_first(_top_k_rules(top_k, case, implied, multiclass, preds.is_floating_point()))
     return case
 
 
@@ -196,17 +177,22 @@ def _input_format_classification(
     multiclass: Optional[bool] = None,
     ignore_index: Optional[int] = None,
 ) -> Tuple[Tensor, Tensor, DataType]:
+    """Validated int one-hot layouts: ``(N, C)`` for binary / multi-label / multi-class, ``(N, C, X)`` for
+    multi-dim multi-class (``multiclass=False`` keeps the positive class only, ``True`` expands binary data)."""
     preds, target = _input_squeeze(preds, target)
     if preds.dtype == torch.float16:
         preds = preds.float()
     case = _check_classification_inputs(preds, target, threshold, num_classes, multiclass, top_k, ignore_index)
+    label_like = case in (DataType.BINARY, DataType.MULTILABEL)
+    class_like = case in (DataType.MULTICLASS, DataType.MULTIDIM_MULTICLASS)
 
-    if case in (DataType.BINARY, DataType.MULTILABEL) and not top_k:
-        preds = (preds >= threshold).int()
-        num_classes = num_classes if not multiclass else 2
-    if case == DataType.MULTILABEL and top_k:
-        preds = select_topk(preds, top_k)
-    if case in (DataType.MULTICLASS, DataType.MULTIDIM_MULTICLASS) or multiclass:
+    if label_like:
+        if top_k:
+            preds = select_topk(preds, top_k) if case == DataType.MULTILABEL else preds
+        else:
+            preds = (preds >= threshold).int()
+            num_classes = 2 if multiclass else num_classes
+    if class_like or multiclass:
         if preds.is_floating_point():
             num_classes = preds.shape[1]
             preds = select_topk(preds, top_k or 1)
@@ -218,25 +204,24 @@ def _input_format_classification(
             preds, target = preds[:, 1, ...], target[:, 1, ...]
 
     if not _empty(preds, target):
-        if (case in (DataType.MULTICLASS, DataType.MULTIDIM_MULTICLASS) and multiclass is not False) or multiclass:
-            target = target.reshape(target.shape[0], target.shape[1], -1)
-            preds = preds.reshape(preds.shape[0], preds.shape[1], -1)
-        else:
-            target = target.reshape(target.shape[0], -1)
-            preds = preds.reshape(preds.shape[0], -1)
+        keep_class_dim = (class_like and multiclass is not False) or bool(multiclass)
+        lead = (preds.shape[0], preds.shape[1], -1) if keep_class_dim else (preds.shape[0], -1)
+        preds, target = preds.reshape(lead), target.reshape(lead)
     if preds.ndim > 2:
         preds, target = preds.squeeze(-1), target.squeeze(-1)
     return preds.int(), target.int(), case
 
 
-def _del_column(data: Tensor, idx: int) -> Tensor:
-    return torch.cat([data[:, :idx], data[:, idx + 1 :]], 1)
+def _without_column(data: Tensor, idx: int) -> Tensor:
+    keep = torch.arange(data.shape[1], device=data.device) != idx
+    return data[:, keep]
 
 
 def _drop_negative_ignored_indices(preds: Tensor, target: Tensor, ignore_index: int, mode: DataType) -> Tuple[Tensor, Tensor]:
+    """Remove the samples whose target is a negative ``ignore_index`` (multi-dim inputs flattened first)."""
     if mode == DataType.MULTIDIM_MULTICLASS and preds.dtype == torch.float:
-        c = preds.shape[1]
-        preds = preds.transpose(1, preds.ndim - 1).reshape(-1, c)
+        n_cls = preds.shape[1]
+        preds = preds.movedim(1, -1).reshape(-1, n_cls)
         target = target.reshape(-1)
     if mode in (DataType.MULTICLASS, DataType.MULTIDIM_MULTICLASS):
         keep = target != ignore_index
@@ -245,19 +230,13 @@ def _drop_negative_ignored_indices(preds: Tensor, target: Tensor, ignore_index: 
 
 
 def _stat_scores(preds: Tensor, target: Tensor, reduce: Optional[str] = "micro") -> Tuple[Tensor, Tensor, Tensor, Tensor]:
-    if reduce == "micro":
-        dim: Union[int, List[int]] = [0, 1] if preds.ndim == 2 else [1, 2]
-    elif reduce == "macro":
-        dim = 0 if preds.ndim == 2 else 2
-    else:
-        dim = 1
-    eq, pos = target == preds, preds == 1
-    neg = preds == 0
-    tp = (eq & pos).sum(dim=dim)
-    fp = (~eq & pos).sum(dim=dim)
-    tn = (eq & neg).sum(dim=dim)
-    fn = (~eq & neg).sum(dim=dim)
-    return tp.long(), fp.long(), tn.long(), fn.long()
+    """tp, fp, tn, fn of one-hot int layouts, summed over the axes ``reduce`` removes (one stacked reduction)."""
+    flat = preds.ndim == 2
+    axes: Union[int, List[int]] = {"micro": [0, 1] if flat else [1, 2], "macro": 0 if flat else 2}.get(reduce or "", 1)
+    hit, said_one = target == preds, preds == 1
+    masks = torch.stack([hit & said_one, ~hit & said_one, hit & ~said_one, ~hit & ~said_one])
+    counts = masks.sum(dim=[a + 1 for a in axes] if isinstance(axes, list) else axes + 1).long()
+    return counts[0], counts[1], counts[2], counts[3]
 
 
 def _stat_scores_update(
@@ -272,10 +251,9 @@ def _stat_scores_update(
     ignore_index: Optional[int] = None,
     mode: Optional[DataType] = None,
 ) -> Tuple[Tensor, Tensor, Tensor, Tensor]:
-    dropped = False
-    if ignore_index is not None and ignore_index < 0 and mode is not None:
-        preds, target = _drop_negative_ignored_indices(preds, target, ignore_index, mode)
-        dropped = True
+    dropped = ignore_index is not None and ignore_index < 0 and mode is not None
+    if dropped:
+        preds, target = _drop_negative_ignored_indices(preds, target, ignore_index, mode)  # type: ignore[arg-type]
     preds, target, _ = _input_format_classification(
         preds, target, threshold=threshold, num_classes=num_classes, multiclass=multiclass, top_k=top_k,
         ignore_index=ignore_index,
@@ -290,12 +268,13 @@ def _stat_scores_update(
                 "When your inputs are multi-dimensional multi-class, you have to set the `mdmc_reduce` parameter"
             )
         if mdmc_reduce == "global":
-            preds = preds.transpose(1, 2).reshape(-1, preds.shape[1])
-            target = target.transpose(1, 2).reshape(-1, target.shape[1])
-    if ignore_index is not None and reduce != "macro" and not dropped:
-        preds, target = _del_column(preds, ignore_index), _del_column(target, ignore_index)
+            preds = preds.movedim(1, 2).reshape(-1, preds.shape[1])
+            target = target.movedim(1, 2).reshape(-1, target.shape[1])
+    masked_macro = ignore_index is not None and not dropped
+    if masked_macro and reduce != "macro":
+        preds, target = _without_column(preds, ignore_index), _without_column(target, ignore_index)  # type: ignore[arg-type]
     tp, fp, tn, fn = _stat_scores(preds, target, reduce=reduce)
-    if ignore_index is not None and reduce == "macro" and not dropped:
+    if masked_macro and reduce == "macro":
         for t in (tp, fp, tn, fn):
             t[..., ignore_index] = -1
     return tp, fp, tn, fn
@@ -309,22 +288,19 @@ def _reduce_stat_scores(
     mdmc_average: Optional[str],
     zero_division: int = 0,
 ) -> Tensor:
-    """``weights * numerator / denominator`` with zero-division fill and negative-denominator (ignored) masking."""
-    numerator, denominator = numerator.float(), denominator.float()
-    zero_mask = denominator == 0
-    ignore_mask = denominator < 0
-    weights = torch.ones_like(denominator) if weights is None else weights.float()
-    zd = torch.tensor(zero_division, dtype=numerator.dtype, device=numerator.device)
-    numerator = torch.where(zero_mask, zd, numerator)
-    denominator = torch.where(zero_mask | ignore_mask, torch.ones_like(denominator), denominator)
-    weights = torch.where(ignore_mask, torch.zeros_like(weights), weights)
+    """``weights * numerator / denominator`` with zero-division fill; a negative denominator marks an ignored
+    class (weight 0, NaN in the per-class output)."""
+    num, den = numerator.float(), denominator.float()
+    zero, ignored = den == 0, den < 0
+    fill = torch.tensor(float(zero_division), device=num.device)
+    w = torch.ones_like(den) if weights is None else weights.float()
+    w = w.masked_fill(ignored, 0.0)
     if average not in (AverageMethod.MICRO, AverageMethod.NONE, None):
-        weights = weights / weights.sum(dim=-1, keepdim=True)
-    scores = weights * (numerator / denominator)
-    scores = torch.where(torch.isnan(scores), zd.to(scores.dtype), scores)
+        w = w / w.sum(dim=-1, keepdim=True)
+    ratio = torch.where(zero, fill, num) / torch.where(zero | ignored, torch.ones_like(den), den)
+    scores = torch.nan_to_num(w * ratio, nan=float(zero_division), posinf=float("inf"), neginf=float("-inf"))
     if mdmc_average == MDMCAverageMethod.SAMPLEWISE:
-        scores = scores.mean(dim=0)
-        ignore_mask = ignore_mask.sum(dim=0).bool()
+        scores, ignored = scores.mean(dim=0), ignored.any(dim=0)
     if average in (AverageMethod.NONE, None):
-        return torch.where(ignore_mask, torch.tensor(float("nan"), device=scores.device), scores)
+        return scores.masked_fill(ignored, float("nan"))
     return scores.sum()

@@ -1,4 +1,12 @@
-"""Track a metric over steps / epochs (API parity: reference ``wrappers/tracker.py:31-311``)."""
+"""MetricTracker: one copy of a metric (or collection) per step / epoch, with history and best-value queries.
+
+API parity: reference ``wrappers/tracker.py:31-311`` (``increment``, ``update``/``forward``/``compute`` on the
+current step, ``compute_all``, ``best_metric``, ``reset``/``reset_all``, ``n_steps``, ``plot``).
+
+Layout: the ``ModuleList`` holds the untouched base metric at index 0 and one deep copy per ``increment()`` after it,
+so step ``k`` is ``self[k + 1]``.  ``compute_all`` stacks the per-step results; ``best_metric`` reduces that history
+with one ``max``/``min`` per tracked quantity and reads the winners back to the host once.
+"""
 from copy import deepcopy
 from typing import Any, Dict, List, Optional, Sequence, Tuple, Union
 
@@ -11,8 +19,68 @@ from torchmetrics_forked_amd.metric import Metric
 from torchmetrics_forked_amd.utilities.plot import _AX_TYPE, _PLOT_OUT_TYPE, plot_single_or_multi_val
 from torchmetrics_forked_amd.utilities.prints import rank_zero_warn
 
+_BestT = Union[None, float, Tuple[float, int], Tuple[None, None], Dict[str, Optional[float]],
+               Tuple[Dict[str, Optional[float]], Dict[str, Optional[int]]]]
+
+
+def _check_maximize(metric: Union[Metric, MetricCollection], maximize: Union[bool, List[bool]]) -> None:
+    if not isinstance(maximize, (bool, list)):
+        raise ValueError("Argument `maximize` should either be a single bool or list of bool")
+    if isinstance(metric, Metric) and not isinstance(maximize, bool):
+        raise ValueError("Argument `maximize` should be a single bool when `metric` is a single Metric")
+    if isinstance(metric, MetricCollection) and isinstance(maximize, list) and len(maximize) != len(metric):
+        raise ValueError("The len of argument `maximize` should match the length of the metric collection")
+
+
+def _stack_history(history: List[Any]) -> Any:
+    """Per-step results -> one tensor (or dict of tensors) with the step as leading dim; ragged results stay a list."""
+    first = history[0]
+    try:
+        if isinstance(first, dict):
+            return {key: torch.stack([step[key] for step in history]) for key in first}
+        if isinstance(first, list):
+            return torch.stack([torch.stack(step) for step in history])
+        return torch.stack(history)
+    except TypeError:
+        return history
+
+
+def _arg_best(values: Tensor, maximize: bool, what: str) -> Tuple[Optional[float], Optional[int]]:
+    """(best value, its step) of a 1-D history; ``(None, None)`` with a warning when "best" is undefined for it."""
+    try:
+        best, step = (torch.max if maximize else torch.min)(values, 0)
+        pair = torch.stack([best.double(), step.double()]).tolist()  # one host read for both
+        return pair[0], int(pair[1])
+    except (ValueError, RuntimeError) as err:
+        rank_zero_warn(
+            f"Encountered the following error when trying to get the best metric{what}: {err}"
+            " this is probably due to the 'best' not being defined for this metric. Returning `None` instead.",
+            UserWarning,
+        )
+        return None, None
+
 
 class MetricTracker(ModuleList):
+    """Keep one copy of ``metric`` per step (epoch) and query the history.
+
+    Args:
+        metric: a ``Metric`` or ``MetricCollection`` to track.
+        maximize: whether higher is better (one bool, or one per collection member).
+
+    Example:
+        >>> import torch
+        >>> from torchmetrics_forked_amd.wrappers import MetricTracker
+        >>> from torchmetrics_forked_amd.classification import MulticlassAccuracy
+        >>> tracker = MetricTracker(MulticlassAccuracy(num_classes=3, average="micro"))
+        >>> for epoch, hits in enumerate([2, 4, 3]):
+        ...     tracker.increment()
+        ...     tracker.update(torch.tensor([0, 1, 2, 0]), torch.tensor([0, 1, 2, 0][:hits] + [1] * (4 - hits)))
+        >>> tracker.compute_all()
+        tensor([0.5000, 1.0000, 0.7500])
+        >>> tracker.best_metric(return_step=True)
+        (1.0, 1)
+    """
+
     def __init__(self, metric: Union[Metric, MetricCollection], maximize: Union[bool, List[bool]] = True) -> None:
         super().__init__()
         if not isinstance(metric, (Metric, MetricCollection)):
@@ -20,61 +88,53 @@ class MetricTracker(ModuleList):
                 "Metric arg need to be an instance of a torchmetrics"
                 f" `Metric` or `MetricCollection` but got {metric}"
             )
+        _check_maximize(metric, maximize)
         self._base_metric = metric
-        if not isinstance(maximize, (bool, list)):
-            raise ValueError("Argument `maximize` should either be a single bool or list of bool")
-        if isinstance(maximize, list) and isinstance(metric, MetricCollection) and len(maximize) != len(metric):
-            raise ValueError("The len of argument `maximize` should match the length of the metric collection")
-        if isinstance(metric, Metric) and not isinstance(maximize, bool):
-            raise ValueError("Argument `maximize` should be a single bool when `metric` is a single Metric")
         self.maximize = maximize
         self._increment_called = False
 
+    # ---------------------------------------------------------------------------------------------- steps
     @property
     def n_steps(self) -> int:
+        """Number of ``increment()`` calls so far."""
         return len(self) - 1
 
     def increment(self) -> None:
+        """Start a new step with a fresh copy of the base metric."""
         self._increment_called = True
         self.append(deepcopy(self._base_metric))
 
-    def forward(self, *args: Any, **kwargs: Any) -> None:
-        self._check_for_increment("forward")
-        return self[-1](*args, **kwargs)
+    def _current(self, method: str) -> Union[Metric, MetricCollection]:
+        if not self._increment_called:
+            raise ValueError(f"`{method}` cannot be called before `.increment()` has been called.")
+        return self[-1]
+
+    def forward(self, *args: Any, **kwargs: Any) -> Any:
+        return self._current("forward")(*args, **kwargs)
 
     def update(self, *args: Any, **kwargs: Any) -> None:
-        self._check_for_increment("update")
-        self[-1].update(*args, **kwargs)
+        self._current("update").update(*args, **kwargs)
 
     def compute(self) -> Any:
-        self._check_for_increment("compute")
-        return self[-1].compute()
-
-    def compute_all(self) -> Any:
-        self._check_for_increment("compute_all")
-        res = [metric.compute() for i, metric in enumerate(self) if i != 0]
-        try:
-            if isinstance(res[0], dict):
-                return {k: torch.stack([r[k] for r in res], dim=0) for k in res[0]}
-            if isinstance(res[0], list):
-                return torch.stack([torch.stack(r, dim=0) for r in res], 0)
-            return torch.stack(res, dim=0)
-        except TypeError:
-            return res
+        return self._current("compute").compute()
 
     def reset(self) -> None:
         self[-1].reset()
 
     def reset_all(self) -> None:
-        for metric in self:
-            metric.reset()
+        for m in self:
+            m.reset()
 
-    def best_metric(
-        self, return_step: bool = False
-    ) -> Union[None, float, Tuple[float, int], Tuple[None, None], Dict[str, Union[float, None]],
-               Tuple[Dict[str, Union[float, None]], Dict[str, Union[int, None]]]]:
-        res = self.compute_all()
-        if isinstance(res, list):
+    # ---------------------------------------------------------------------------------------------- history
+    def compute_all(self) -> Any:
+        """Results of every step, stacked along a leading step dimension (list when they do not stack)."""
+        self._current("compute_all")
+        return _stack_history([m.compute() for m in list(self)[1:]])
+
+    def best_metric(self, return_step: bool = False) -> _BestT:
+        """Best value over the steps (and the step it was reached at), per member for a collection."""
+        history = self.compute_all()
+        if isinstance(history, list):
             rank_zero_warn(
                 "Encountered nested structure. You are probably using a metric collection inside a metric collection,"
                 " or a metric wrapper inside a metric collection, which is not supported by `.best_metric()` method."
@@ -82,39 +142,17 @@ class MetricTracker(ModuleList):
             )
             return (None, None) if return_step else None
         if isinstance(self._base_metric, Metric):
-            fn = torch.max if self.maximize else torch.min
-            try:
-                value, idx = fn(res, 0)
-                return (value.item(), idx.item()) if return_step else value.item()
-            except (ValueError, RuntimeError) as error:
-                rank_zero_warn(
-                    f"Encountered the following error when trying to get the best metric: {error}"
-                    "this is probably due to the 'best' not being defined for this metric."
-                    "Returning `None` instead.",
-                    UserWarning,
-                )
+            value, step = _arg_best(history, bool(self.maximize), "")
+            if value is None:
                 return (None, None) if return_step else None
-        maximize = self.maximize if isinstance(self.maximize, list) else len(res) * [self.maximize]
-        value, idx = {}, {}
-        for i, (k, v) in enumerate(res.items()):
-            try:
-                fn = torch.max if maximize[i] else torch.min
-                out = fn(v, 0)
-                value[k], idx[k] = out[0].item(), out[1].item()
-            except (ValueError, RuntimeError) as error:
-                rank_zero_warn(
-                    f"Encountered the following error when trying to get the best metric for metric {k}:"
-                    f"{error} this is probably due to the 'best' not being defined for this metric."
-                    "Returning `None` instead.",
-                    UserWarning,
-                )
-                value[k], idx[k] = None, None
-        return (value, idx) if return_step else value
-
-    def _check_for_increment(self, method: str) -> None:
-        if not self._increment_called:
-            raise ValueError(f"`{method}` cannot be called before `.increment()` has been called.")
+            return (value, step) if return_step else value
+        flags = self.maximize if isinstance(self.maximize, list) else [self.maximize] * len(history)
+        values: Dict[str, Optional[float]] = {}
+        steps: Dict[str, Optional[int]] = {}
+        for (key, hist), maximize in zip(history.items(), flags):
+            values[key], steps[key] = _arg_best(hist, maximize, f" for metric {key}")
+        return (values, steps) if return_step else values
 
     def plot(self, val: Optional[Union[Tensor, Sequence[Tensor]]] = None, ax: Optional[_AX_TYPE] = None) -> _PLOT_OUT_TYPE:
-        val = val if val is not None else self.compute_all()
-        return plot_single_or_multi_val(val, ax=ax, name=self.__class__.__name__)
+        """Plot the history (``compute_all()`` unless ``val`` is given)."""
+        return plot_single_or_multi_val(val if val is not None else self.compute_all(), ax=ax, name=self.__class__.__name__)
