@@ -4,9 +4,12 @@ Backbones come from :mod:`torchmetrics_forked_amd.models` (torchvision-identical
 unless ``backbone_weights`` is given).  The per-layer head — channel L2-normalisation of both feature maps,
 squared difference, 1×1 linear layer and spatial mean — runs as ONE fused gfx950 kernel per layer
 (``tmx::lpips_head``) when no autograd graph is needed; with gradients (or on CPU) the eager formulation is used.
-The linear-head weights load from a LPIPS ``.pth`` via ``model_path`` (``weights_only=True``); without one the head
-is randomly initialised (the reference downloads pretrained weights, which is not possible offline).
+With ``pretrained=True`` the linear heads are the published LPIPS v0.1 weights shipped with the package
+(``models/lpips_heads.safetensors``, the same values as the reference's ``lpips_models/{net}.pth``), or a LPIPS
+``.pth`` given as ``model_path`` (loaded ``weights_only=True``).  The backbone trunks are random unless
+``backbone_weights`` points at torchvision-layout weights (the reference downloads ImageNet weights; offline here).
 """
+import os
 from typing import List, NamedTuple, Optional, Tuple, Union
 
 import torch
@@ -24,6 +27,9 @@ _SLICES = {
 }
 _CHANNELS = {"alex": [64, 192, 384, 256, 256], "vgg": [64, 128, 256, 512, 512], "squeeze": [64, 128, 256, 384, 384, 512, 512]}
 _FEATURES = {"alex": alexnet_features, "vgg": vgg16_features, "squeeze": squeezenet1_1_features}
+# LPIPS v0.1 linear heads (``tools/convert_lpips_heads.py`` from the reference's lpips_models/*.pth): the default for
+# ``pretrained=True``, as in the reference (``functional/image/lpips.py:318-325``)
+_HEADS_FILE = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))), "models", "lpips_heads.safetensors")
 
 
 class _SlicedBackbone(nn.Module):
@@ -152,10 +158,22 @@ class _LPIPS(nn.Module):
         self.lins = nn.ModuleList(NetLinLayer(c, use_dropout=use_dropout) for c in self.chns)
         for i, lin in enumerate(self.lins):  # reference attribute names lin0..lin6 (state-dict compatible)
             setattr(self, f"lin{i}", lin)
-        if pretrained and model_path is not None:
-            self.load_state_dict(torch.load(model_path, map_location="cpu", weights_only=True), strict=False)
+        if pretrained:
+            if model_path is not None:
+                self.load_state_dict(torch.load(model_path, map_location="cpu", weights_only=True), strict=False)
+            else:  # the published LPIPS v0.1 heads shipped with the package (reference lpips_models/{net}.pth)
+                self._load_packaged_heads(net)
         if eval_mode:
             self.eval()
+
+    def _load_packaged_heads(self, net: str) -> None:
+        from safetensors.torch import load_file
+
+        heads = load_file(_HEADS_FILE)
+        with torch.no_grad():
+            for i, lin in enumerate(self.lins):
+                conv = lin.model[-1]
+                conv.weight.copy_(heads[f"{net}.lin{i}"].reshape(conv.weight.shape))
 
     def forward(self, in0: Tensor, in1: Tensor, retperlayer: bool = False, normalize: bool = False) -> Union[Tensor, Tuple[Tensor, List[Tensor]]]:
         if normalize:

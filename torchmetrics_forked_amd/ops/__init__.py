@@ -16,7 +16,9 @@ from typing import Optional
 
 import torch
 
-_LIB = Path(__file__).resolve().parent / "_tmx_native.so"
+# ``TMX_NATIVE_LIB`` points at an alternative build of the same ops (e.g. the ASan/UBSan host-only library of
+# ``tools/sanitize_host.py``); default: the in-tree gfx950 library
+_LIB = Path(os.environ.get("TMX_NATIVE_LIB") or Path(__file__).resolve().parent / "_tmx_native.so")
 _lock = threading.Lock()
 _loaded: Optional[bool] = None
 _error: Optional[str] = None
