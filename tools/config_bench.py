@@ -1,0 +1,180 @@
+"""Secondary BASELINE configs for ``bench.py --config map|image|bert`` (BASELINE.json configs 3-5).
+
+Same contract as the headline: ``args.warmup`` untimed steps, then exactly ``args.steps`` steps followed by one
+``compute()`` (including the cross-rank sync), bracketed by barrier + device synchronize on both sides; the max over
+ranks is reported, ``value`` = world * steps / seconds (whole-job updates/s, weak scaling: per-GPU batch fixed).
+
+* ``map``   MeanAveragePrecision, COCO-80 synthetic: 512 images / step, 100 detections + 20 ground truths / image
+* ``image`` SSIM + PSNR + LPIPS(VGG16 trunk random-init, published linear heads) on 3x1024x1024 fp32, 256 images / step
+* ``bert``  BERTScore with a random-init bert-base (bf16), 512-token pairs, 1024 pairs / step
+
+``--small`` shrinks every shape for CPU smoke runs (not a benchmark).  There is no reference number for these configs
+(BASELINE.json publishes none), so ``vs_baseline`` is null.
+"""
+import argparse
+import time
+from typing import Any, Callable, Dict, Optional
+
+import torch
+import torch.distributed as dist
+
+
+def _sync(device: torch.device) -> None:
+    if device.type == "cuda":
+        torch.cuda.synchronize(device)
+
+
+def _timed_window(step: Callable[[int], None], compute: Callable[[], Any], steps: int, warmup: int, reset: Callable[[], None],
+                  device: torch.device, world: int) -> Dict[str, Any]:
+    for i in range(warmup):
+        step(i)
+    if warmup:
+        compute()
+    reset()
+    _sync(device)
+    if world > 1:
+        dist.barrier()
+    _sync(device)
+    t0 = time.perf_counter()
+    for i in range(steps):
+        step(i)
+    _sync(device)
+    t_upd = time.perf_counter() - t0
+    res = compute()
+    _sync(device)
+    if world > 1:
+        dist.barrier()
+    _sync(device)
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed, t_upd], dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return {"elapsed": float(t[0]), "update_s": float(t[1]), "result": res}
+
+
+def _line(metric: str, value: float, unit: str, world: int, args: argparse.Namespace, elapsed: float, dtype: str, data: str,
+          model: str, global_batch: int, seq_len: int, extra: Dict[str, Any]) -> Dict[str, Any]:
+    out = {
+        "metric": metric, "value": round(value, 3), "unit": unit, "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(1000.0 * elapsed / args.steps, 3), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": dtype, "data": data,
+        "config": {"model": model, "global_batch": global_batch, "seq_len": seq_len, "parallelism": f"dp{world}"},
+    }
+    out.update(extra)
+    return out
+
+
+# --------------------------------------------------------------------------------------------------------------
+def _map(args: argparse.Namespace, device: torch.device, world: int, rank: int) -> Dict[str, Any]:
+    from torchmetrics_forked_amd.detection import MeanAveragePrecision
+
+    n_img, n_det, n_gt, n_cls = (512, 100, 20, 80) if not args.small else (16, 10, 4, 5)
+    g = torch.Generator(device=device).manual_seed(7 + rank)
+
+    def batch():
+        xy = torch.rand(n_img, n_gt, 2, device=device, generator=g) * 500
+        gt = torch.cat([xy, xy + torch.rand(n_img, n_gt, 2, device=device, generator=g) * 150 + 4], -1)
+        jitter = gt + torch.randn(n_img, n_gt, 4, device=device, generator=g) * 6
+        extra_idx = torch.randint(0, n_gt, (n_img, n_det - n_gt), device=device, generator=g)
+        extra = torch.gather(torch.cat([xy, xy + 50], -1), 1, extra_idx[..., None].expand(-1, -1, 4)) + 30
+        det = torch.cat([jitter, extra], 1)
+        det[..., 2:] = torch.maximum(det[..., 2:], det[..., :2] + 1)
+        gl = torch.randint(0, n_cls, (n_img, n_gt), device=device, generator=g)
+        dl = torch.cat([gl, torch.randint(0, n_cls, (n_img, n_det - n_gt), device=device, generator=g)], 1)
+        sc = torch.rand(n_img, n_det, device=device, generator=g)
+        preds = [{"boxes": det[i], "scores": sc[i], "labels": dl[i]} for i in range(n_img)]
+        target = [{"boxes": gt[i], "labels": gl[i]} for i in range(n_img)]
+        return preds, target
+
+    pool = [batch() for _ in range(2)]
+    m = MeanAveragePrecision().to(device)
+    r = _timed_window(lambda i: m.update(*pool[i % 2]), m.compute, args.steps, args.warmup, m.reset, device, world)
+    return _line(
+        f"metric-updates/sec (whole node), MeanAveragePrecision COCO-80 {n_img} img/step x {n_det} det",
+        world * args.steps / r["elapsed"], "updates/s", world, args, r["elapsed"], "fp32",
+        f"synthetic boxes ({n_img} images/step/rank, {n_det} detections + {n_gt} ground truths per image, 80 classes)",
+        "MeanAveragePrecision(iou_type='bbox')", n_img * world, 1,
+        {"images_per_sec": round(world * args.steps * n_img / r["elapsed"], 1),
+         "update_ms_per_step": round(1000.0 * r["update_s"] / args.steps, 3),
+         "compute_incl_sync_ms": round(1000.0 * (r["elapsed"] - r["update_s"]), 3),
+         "map": round(float(r["result"]["map"]), 5)},
+    )
+
+
+def _image(args: argparse.Namespace, device: torch.device, world: int, rank: int) -> Dict[str, Any]:
+    import torchmetrics_forked_amd as tm
+    from torchmetrics_forked_amd.image import LearnedPerceptualImagePatchSimilarity, PeakSignalNoiseRatio, StructuralSimilarityIndexMeasure
+
+    b, hw = (256, 1024) if not args.small else (4, 64)
+    g = torch.Generator(device=device).manual_seed(11 + rank)
+    target = torch.rand(b, 3, hw, hw, device=device, generator=g)
+    preds = (target + 0.05 * torch.randn(b, 3, hw, hw, device=device, generator=g)).clamp(0, 1)
+    coll = tm.MetricCollection({
+        "ssim": StructuralSimilarityIndexMeasure(data_range=1.0),
+        "psnr": PeakSignalNoiseRatio(data_range=1.0),
+        "lpips": LearnedPerceptualImagePatchSimilarity(net_type="vgg", normalize=True),
+    }).to(device)
+    with torch.no_grad():
+        r = _timed_window(lambda i: coll.update(preds, target), coll.compute, args.steps, args.warmup, coll.reset, device, world)
+    res = r["result"]
+    return _line(
+        f"metric-updates/sec (whole node), SSIM+PSNR+LPIPS(vgg) 3x{hw}x{hw} bs={b}",
+        world * args.steps / r["elapsed"], "updates/s", world, args, r["elapsed"], "fp32",
+        f"synthetic images (uniform target + gaussian noise, {b} pairs/step/rank); VGG16 trunk random-init, LPIPS v0.1 heads",
+        "SSIM(gaussian 11x11)+PSNR+LPIPS(net_type='vgg')", b * world, hw * hw,
+        {"images_per_sec": round(world * args.steps * b / r["elapsed"], 2),
+         "update_ms_per_step": round(1000.0 * r["update_s"] / args.steps, 3),
+         "compute_incl_sync_ms": round(1000.0 * (r["elapsed"] - r["update_s"]), 3),
+         "ssim": round(float(res["ssim"]), 6), "psnr": round(float(res["psnr"]), 4), "lpips": round(float(res["lpips"]), 6)},
+    )
+
+
+def _bert(args: argparse.Namespace, device: torch.device, world: int, rank: int) -> Dict[str, Any]:
+    import transformers
+
+    from torchmetrics_forked_amd.aggregation import MeanMetric
+    from torchmetrics_forked_amd.functional.text import bert_score
+
+    n, L = (1024, 512) if not args.small else (8, 32)
+    cfg = transformers.BertConfig() if not args.small else transformers.BertConfig(
+        hidden_size=64, num_hidden_layers=2, num_attention_heads=2, intermediate_size=128)
+    torch.manual_seed(0)  # identical random-init weights on every rank
+    dtype = torch.bfloat16 if device.type == "cuda" else torch.float32
+    model = transformers.BertModel(cfg).eval().to(device).to(dtype)
+    g = torch.Generator().manual_seed(13 + rank)
+    ids_p = torch.randint(1000, cfg.vocab_size, (n, L), generator=g)
+    ids_t = torch.randint(1000, cfg.vocab_size, (n, L), generator=g)
+    mask = torch.ones(n, L, dtype=torch.long)
+    preds = {"input_ids": ids_p, "attention_mask": mask}
+    target = {"input_ids": ids_t, "attention_mask": mask}
+    agg = MeanMetric().to(device)
+    bs = 128 if not args.small else 4
+
+    def step(i: int) -> None:
+        # one step = BERTScore of this rank's 1024 pairs (embedding forward + fused greedy matching), folded into a
+        # synced running mean (the reference's module only tokenises in update() and runs all of this in compute())
+        out = bert_score(preds, target, model=model, batch_size=bs, device=device, num_layers=cfg.num_hidden_layers)
+        agg.update(out["f1"].to(device))
+
+    with torch.no_grad():
+        r = _timed_window(step, agg.compute, args.steps, args.warmup, agg.reset, device, world)
+    f1 = r["result"]
+    return _line(
+        f"metric-updates/sec (whole node), BERTScore bert-base {L}-token pairs bs={n}",
+        world * args.steps / r["elapsed"], "updates/s", world, args, r["elapsed"], "bf16" if dtype == torch.bfloat16 else "fp32",
+        f"synthetic token ids ({n} pairs/step/rank, {L} tokens, full attention mask); random-init bert-base weights",
+        "BERTScore(bert-base geometry, random init, last layer)", n * world, L,
+        {"pairs_per_sec": round(world * args.steps * n / r["elapsed"], 1),
+         "update_ms_per_step": round(1000.0 * r["update_s"] / args.steps, 3),
+         "compute_incl_sync_ms": round(1000.0 * (r["elapsed"] - r["update_s"]), 3),
+         "f1_mean": round(float(f1.float().mean()), 6)},
+    )
+
+
+def run_config(args: argparse.Namespace, device: torch.device, world: int, rank: int) -> Optional[Dict[str, Any]]:
+    from torchmetrics_forked_amd import ops
+
+    if device.type == "cuda":
+        ops.require()
+    fn = {"map": _map, "image": _image, "bert": _bert}[args.config]
+    return fn(args, device, world, rank)

@@ -217,8 +217,27 @@ def _lpips_update(img1: Tensor, img2: Tensor, net: nn.Module, normalize: bool) -
             f" {[img1.min(), img1.max()]} and {[img2.min(), img2.max()]} when all values are"
             f" expected to be in the {[0, 1] if normalize else [-1, 1]} range."
         )
-    loss = net(img1, img2, normalize=normalize).squeeze()
-    return loss, img1.shape[0]
+    n = img1.shape[0]
+    chunk = _lpips_chunk(img1, net)
+    if chunk >= n or torch.is_grad_enabled() and (img1.requires_grad or img2.requires_grad):
+        loss = net(img1, img2, normalize=normalize).squeeze()
+    else:  # bounded activation memory: the trunk's feature maps of a chunk, not of the whole batch
+        loss = torch.cat([
+            net(img1[i : i + chunk], img2[i : i + chunk], normalize=normalize).reshape(-1) for i in range(0, n, chunk)
+        ]).squeeze()
+    return loss, n
+
+
+# feature-map channels kept alive per input pixel by each trunk (sum over the tapped stages of C / stride^2) — sizes
+# the chunks of a large LPIPS batch (3x1024x1024 x 256 images through VGG16 would hold ~260 GB of activations)
+_ACT_CHANNELS_PER_PIXEL = {"vgg": 128.0, "alex": 10.0, "squeeze": 12.0}
+_LPIPS_ACT_BUDGET = float(os.environ.get("TMX_LPIPS_ACT_BUDGET_GB", "24")) * 2**30
+
+
+def _lpips_chunk(img: Tensor, net: nn.Module) -> int:
+    kind = getattr(net, "pnet_type", "vgg")
+    per_image = 2 * 4 * img.shape[-1] * img.shape[-2] * _ACT_CHANNELS_PER_PIXEL.get(kind, 128.0) * 2  # both inputs, fp32, 2x slack
+    return max(1, int(_LPIPS_ACT_BUDGET // per_image))
 
 
 def _lpips_compute(sum_scores: Tensor, total: Union[Tensor, int], reduction: Literal["sum", "mean"] = "mean") -> Tensor:
