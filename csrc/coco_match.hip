@@ -1,0 +1,414 @@
+// COCO evaluation on the GPU: pycocotools' evaluateImg + accumulate semantics for
+// MeanAveragePrecision, without leaving the device.  Replaces the reference's COCO JSON round trip through
+// pycocotools / faster-coco-eval (reference detection/mean_ap.py:501-575, legacy matcher _mean_ap.py:521-649,
+// accumulate _mean_ap.py:696-857).  The host C++ evaluator (coco_eval.cpp) stays as the CPU path and as the
+// oracle the GPU tests compare against.
+//
+// Pipeline (all on the metric's device; ATen is only used for the stable orderings):
+//   1. detections ordered by (image, class, score desc, input row) with two stable sorts; rank within the
+//      (image, class) pair; rows past maxDets[-1] dropped.  Ground truth ordered by (image, class, input row).
+//   2. coco_match_kernel: one wave per (image, class) pair.  Lane l owns one (IoU threshold t, area range a)
+//      combination (l = t * A + a, so T * A <= 64) and runs the sequential greedy match of that combination:
+//      non-ignored ground truth first, crowd boxes re-matchable, ties resolved to the later ground truth exactly
+//      as pycocotools does.  Detections are visited in lock-step, so each detection's per-combination results
+//      are two wave ballots: a 64-bit "matched" mask and a 64-bit "ignored" mask.  Per-lane "gt already matched"
+//      bitsets live in LDS.  Non-ignored ground-truth counts per (class, area) are integer atomics.
+//   3. detections re-ordered by (class, score desc, image, rank) - the order pycocotools' stable mergesort of the
+//      per-image concatenation produces - with stable sorts.
+//   4. coco_accumulate_kernel: one wave per (class, area, maxDet, IoU threshold).  A forward ballot pass counts
+//      TP / FP / kept detections; a backward pass rebuilds each prefix count from the totals, forms the
+//      precision, keeps the running precision envelope (suffix max) in a wave scan, and answers every recall
+//      threshold at the detection where the prefix TP first reaches ceil(thr * npig) - the same element
+//      np.searchsorted(rc, thr, side="left") finds, computed with the same double arithmetic.
+//
+// Limits of the GPU path (the caller falls back to the C++ evaluator beyond them): T * A <= 64,
+// <= 1024 ground-truth boxes per (image, class) pair, <= 256 recall thresholds.
+#include "common.h"
+
+#include <limits>
+
+namespace tmx {
+
+constexpr int kCocoMaxGt = 1024;               // per (image, class) pair
+constexpr int kCocoGtWords = kCocoMaxGt / 32;  // matched bitset words per lane
+constexpr int kCocoMaxRec = 256;
+constexpr int kCocoMatchWaves = 2;             // waves per block in the match kernel
+
+__device__ __forceinline__ double coco_box_iou(const double* d, const double* g, bool crowd) {
+  const double ow = fmin(d[0] + d[2], g[0] + g[2]) - fmax(d[0], g[0]);
+  if (ow <= 0) return 0.0;
+  const double oh = fmin(d[1] + d[3], g[1] + g[3]) - fmax(d[1], g[1]);
+  if (oh <= 0) return 0.0;
+  const double inter = ow * oh;
+  const double u = crowd ? d[2] * d[3] : d[2] * d[3] + g[2] * g[3] - inter;
+  return u > 0 ? inter / u : 0.0;
+}
+
+struct CocoPairs {
+  const int64_t* det_start;  // [P] first row of the pair in the sorted detection arrays
+  const int64_t* det_count;  // [P] (<= maxDets[-1])
+  const int64_t* gt_start;   // [P]
+  const int64_t* gt_count;   // [P]
+  const int64_t* cls;        // [P] class index
+  const int64_t* img;        // [P] image index
+  const int64_t* iou_off;    // [P] offset of the pair's [nd, ng] block in the exported IoU buffer
+};
+
+// custom (segmentation) IoU: per-image [n_det_img, n_gt_img] matrices
+struct CocoCustomIoU {
+  const double* mats;       // concatenated matrices
+  const int64_t* img_off;   // [I] offset of the image's matrix
+  const int64_t* img_ng;    // [I] ground-truth count of the image (matrix width)
+  const int64_t* det_local; // [sorted dets] row of the detection within its image
+  const int64_t* gt_local;  // [sorted gts] row of the ground truth within its image
+};
+
+__global__ __launch_bounds__(kCocoMatchWaves * kWave) void coco_match_kernel(
+    CocoPairs pairs, int64_t P, const double* __restrict__ dbox, const double* __restrict__ darea,
+    const double* __restrict__ gbox, const int64_t* __restrict__ gcrowd, const double* __restrict__ garea,
+    const double* __restrict__ iou_thr, int T, const double* __restrict__ area_rng, int A, bool custom,
+    CocoCustomIoU cust, bool export_iou, double* __restrict__ iou_out, uint64_t* __restrict__ matched_out,
+    uint64_t* __restrict__ ignored_out, int64_t* __restrict__ npig) {
+  __shared__ uint32_t gtm_all[kCocoMatchWaves][kCocoGtWords][kWave];  // [word][lane]: conflict-free per word
+  const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
+  const int64_t p = static_cast<int64_t>(blockIdx.x) * kCocoMatchWaves + wave;
+  if (p >= P) return;  // whole wave leaves together (p is wave-uniform); no block barriers below
+  uint32_t(*gtm)[kWave] = gtm_all[wave];
+  const int64_t d0 = pairs.det_start[p], nd = pairs.det_count[p];
+  const int64_t g0 = pairs.gt_start[p], ng = pairs.gt_count[p];
+  const int64_t k = pairs.cls[p];
+
+  auto iou_of = [&](int64_t d, int64_t g) -> double {
+    if (custom) {
+      const int64_t im = pairs.img[p];
+      return cust.mats[cust.img_off[im] + cust.det_local[d0 + d] * cust.img_ng[im] + cust.gt_local[g0 + g]];
+    }
+    return coco_box_iou(dbox + 4 * (d0 + d), gbox + 4 * (g0 + g), gcrowd[g0 + g] != 0);
+  };
+
+  if (export_iou && nd > 0 && ng > 0) {
+    const int64_t off = pairs.iou_off[p];
+    for (int64_t idx = lane; idx < nd * ng; idx += kWave) iou_out[off + idx] = iou_of(idx / ng, idx % ng);
+  }
+
+  const bool active = lane < T * A;
+  const int t = active ? lane / A : 0, a = active ? lane % A : 0;
+  const double lo = area_rng[2 * a], hi = area_rng[2 * a + 1];
+  const double thr = fmin(iou_thr[t], 1.0 - 1e-10);
+  const int words = static_cast<int>((ng + 31) / 32);
+  for (int w = 0; w < words; ++w) gtm[w][lane] = 0u;
+
+  auto gt_ignored = [&](int64_t g) -> bool {
+    const double ar = garea[g0 + g];
+    return gcrowd[g0 + g] != 0 || ar < lo || ar > hi;
+  };
+
+  if (active && t == 0) {
+    int64_t c = 0;
+    for (int64_t g = 0; g < ng; ++g) c += gt_ignored(g) ? 0 : 1;
+    if (c) atomic_add_i64(npig + k * A + a, c);
+  }
+
+  for (int64_t d = 0; d < nd; ++d) {  // wave-uniform trip count
+    int64_t m = -1;
+    bool m_ig = false;
+    if (active && ng > 0) {
+      double best = thr;
+      // pass 0: non-ignored ground truth in input order; pass 1: ignored ones (only if nothing matched yet,
+      // the reference's "break once a non-ignored match exists and the ignored block starts")
+      for (int pass = 0; pass < 2 && !(pass == 1 && m >= 0); ++pass) {
+        for (int64_t g = 0; g < ng; ++g) {
+          const bool ig = gt_ignored(g);
+          if (ig != (pass == 1)) continue;
+          const bool crowd = gcrowd[g0 + g] != 0;
+          if (!crowd && ((gtm[g >> 5][lane] >> (g & 31)) & 1u)) continue;
+          const double v = iou_of(d, g);
+          if (v < best) continue;
+          best = v;
+          m = g;
+          m_ig = ig;
+        }
+      }
+      if (m >= 0) gtm[m >> 5][lane] |= 1u << (m & 31);
+    }
+    bool ign = m >= 0 ? m_ig : false;
+    if (active && m < 0) {
+      const double ar = darea[d0 + d];
+      ign = ar < lo || ar > hi;
+    }
+    const uint64_t mb = __ballot(active && m >= 0);
+    const uint64_t ib = __ballot(active && ign);
+    if (lane == 0) {
+      matched_out[d0 + d] = mb;
+      ignored_out[d0 + d] = ib;
+    }
+  }
+}
+
+// One wave per (class k, area a, maxDet m, IoU threshold t).  Arrays are in accumulate order: class segments,
+// score descending, ties by (image, rank).  Outputs were pre-filled with -1 by the host.
+__global__ __launch_bounds__(kWave) void coco_accumulate_kernel(
+    const int64_t* __restrict__ seg, int K, int A, int M, int T, int R, const int64_t* __restrict__ max_dets,
+    const double* __restrict__ rec_thr, const int32_t* __restrict__ rank, const uint64_t* __restrict__ matched,
+    const uint64_t* __restrict__ ignored, const double* __restrict__ score, const int64_t* __restrict__ npig_all,
+    double* __restrict__ prec_out, double* __restrict__ rec_out, double* __restrict__ score_out) {
+  __shared__ int64_t ctab[kCocoMaxRec];
+  __shared__ double p_res[kCocoMaxRec];
+  __shared__ double s_res[kCocoMaxRec];
+  const int lane = threadIdx.x;
+  int64_t q = blockIdx.x;
+  const int t = static_cast<int>(q % T); q /= T;
+  const int m = static_cast<int>(q % M); q /= M;
+  const int a = static_cast<int>(q % A); q /= A;
+  const int k = static_cast<int>(q);
+  const int64_t npig = npig_all[k * A + a];
+  if (npig == 0) return;  // stays -1 (no ground truth for this class / area)
+  const int64_t s = seg[k], e = seg[k + 1];
+  const int bit = t * A + a;
+  const int64_t maxd = max_dets[m];
+  const double eps = 2.220446049250313e-16;  // np.spacing(1)
+
+  // smallest TP count whose recall reaches each threshold (same double arithmetic as rc = tp / npig)
+  for (int r = lane; r < R; r += kWave) {
+    const double thr = rec_thr[r];
+    int64_t c = 0;
+    if (thr > 0) {
+      double cf = ceil(thr * static_cast<double>(npig));
+      c = cf < 0 ? 0 : static_cast<int64_t>(cf);
+      while (c > 0 && static_cast<double>(c - 1) / static_cast<double>(npig) >= thr) --c;
+      while (static_cast<double>(c) / static_cast<double>(npig) < thr) ++c;
+      if (c == 0) c = 1;  // thr > 0 needs at least one true positive
+    }
+    ctab[r] = c;
+    p_res[r] = 0.0;
+    s_res[r] = 0.0;
+  }
+  __syncthreads();
+
+  // pass 1: totals and the first kept element
+  int64_t nd = 0, tp_tot = 0, fp_tot = 0, first = -1;
+  for (int64_t base = s; base < e; base += kWave) {
+    const int64_t j = base + lane;
+    bool valid = false, tp = false, fp = false;
+    if (j < e && rank[j] < maxd) {
+      valid = true;
+      const bool mt = (matched[j] >> bit) & 1ull, ig = (ignored[j] >> bit) & 1ull;
+      tp = mt && !ig;
+      fp = !mt && !ig;
+    }
+    const uint64_t vb = __ballot(valid), tb = __ballot(tp), fb = __ballot(fp);
+    if (first < 0 && vb) first = base + __builtin_ctzll(vb);
+    nd += __builtin_popcountll(vb);
+    tp_tot += __builtin_popcountll(tb);
+    fp_tot += __builtin_popcountll(fb);
+  }
+  const int64_t rec_idx = ((static_cast<int64_t>(t) * K + k) * A + a) * M + m;
+  if (lane == 0) rec_out[rec_idx] = nd ? static_cast<double>(tp_tot) / static_cast<double>(npig) : 0.0;
+
+  // pass 2: backward, suffix-max precision envelope, answer thresholds at their TP element
+  double carry = -1.0;  // precisions are >= 0
+  int64_t tp_after = 0, fp_after = 0;
+  const uint64_t above = lane == 63 ? 0ull : (~0ull << (lane + 1));
+  for (int64_t hi = e; hi > s; hi -= kWave) {
+    const int64_t lo_j = hi - kWave > s ? hi - kWave : s;
+    const int64_t j = lo_j + lane;
+    bool valid = false, tp = false, fp = false;
+    if (j < hi && rank[j] < maxd) {
+      valid = true;
+      const bool mt = (matched[j] >> bit) & 1ull, ig = (ignored[j] >> bit) & 1ull;
+      tp = mt && !ig;
+      fp = !mt && !ig;
+    }
+    const uint64_t tb = __ballot(tp), fb = __ballot(fp);
+    const int64_t tp_sum = tp_tot - (tp_after + __builtin_popcountll(tb & above));
+    const int64_t fp_sum = fp_tot - (fp_after + __builtin_popcountll(fb & above));
+    double env = valid ? static_cast<double>(tp_sum) / (static_cast<double>(fp_sum) + static_cast<double>(tp_sum) + eps) : -1.0;
+#pragma unroll
+    for (int off = 1; off < kWave; off <<= 1) {
+      const double o = __shfl_down(env, off, kWave);
+      if (lane + off < kWave) env = fmax(env, o);
+    }
+    env = fmax(env, carry);
+    carry = __shfl(env, 0, kWave);
+    if (valid && (tp || j == first)) {
+      // thresholds answered here: TP elements serve ctab == tp_sum, the first kept element serves ctab == 0
+      for (int pass = 0; pass < 2; ++pass) {
+        int64_t want;
+        if (pass == 0) {
+          if (!tp) continue;
+          want = tp_sum;
+        } else {
+          if (j != first) continue;
+          want = 0;
+        }
+        int lo_r = 0, hi_r = R;  // lower_bound(ctab, want)
+        while (lo_r < hi_r) {
+          const int mid = (lo_r + hi_r) >> 1;
+          if (ctab[mid] < want) lo_r = mid + 1; else hi_r = mid;
+        }
+        for (int r = lo_r; r < R && ctab[r] == want; ++r) {
+          p_res[r] = env;
+          s_res[r] = score[j];
+        }
+      }
+    }
+    tp_after += __builtin_popcountll(tb);
+    fp_after += __builtin_popcountll(fb);
+  }
+  __syncthreads();
+  for (int r = lane; r < R; r += kWave) {
+    const int64_t idx = (((static_cast<int64_t>(t) * R + r) * K + k) * A + a) * M + m;
+    prec_out[idx] = p_res[r];
+    score_out[idx] = s_res[r];
+  }
+}
+
+// ------------------------------------------------------------------------------------------------ host side
+namespace {
+
+at::Tensor stable_order(const at::Tensor& key, bool descending) {
+  return std::get<1>(at::sort(key, /*stable=*/true, /*dim=*/0, descending));
+}
+
+}  // namespace
+
+// Same contract as the host op tmx::coco_evaluate (coco_eval.cpp), except that class labels come in already
+// mapped to class indices (det_cls / gt_cls in [0, K)), every tensor lives on the GPU, and iou_index lists only
+// the (image, class) pairs that hold a detection or a ground truth.
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor> coco_evaluate_gpu(
+    const at::Tensor& det_boxes_, const at::Tensor& det_scores_, const at::Tensor& det_cls_, const at::Tensor& det_img_,
+    const at::Tensor& det_area_, const at::Tensor& gt_boxes_, const at::Tensor& gt_cls_, const at::Tensor& gt_img_,
+    const at::Tensor& gt_crowd_, const at::Tensor& gt_area_, int64_t K, int64_t num_images, const at::Tensor& iou_thrs_,
+    const at::Tensor& rec_thrs_, const at::Tensor& max_dets_, const at::Tensor& area_rng_,
+    const c10::optional<at::Tensor>& img_iou_, const c10::optional<at::Tensor>& img_iou_offsets_,
+    const c10::optional<at::Tensor>& det_local_, const c10::optional<at::Tensor>& gt_local_,
+    const c10::optional<at::Tensor>& img_ng_, bool export_iou) {
+  TORCH_CHECK(det_scores_.is_cuda(), "coco_evaluate_gpu: expected GPU tensors");
+  const c10::DeviceGuard guard(det_scores_.device());
+  const auto dev = det_scores_.device();
+  auto f64 = [&](const at::Tensor& t) { return t.to(dev, at::kDouble).contiguous(); };
+  auto i64 = [&](const at::Tensor& t) { return t.to(dev, at::kLong).contiguous(); };
+  const auto det_boxes = f64(det_boxes_).reshape({-1, 4}), det_scores = f64(det_scores_), det_area = f64(det_area_);
+  const auto gt_boxes = f64(gt_boxes_).reshape({-1, 4}), gt_area = f64(gt_area_);
+  const auto det_cls = i64(det_cls_), det_img = i64(det_img_), gt_cls = i64(gt_cls_), gt_img = i64(gt_img_);
+  const auto gt_crowd = i64(gt_crowd_);
+  const auto iou_thrs = f64(iou_thrs_), rec_thrs = f64(rec_thrs_), area_rng = f64(area_rng_).reshape({-1, 2});
+  const auto max_dets_cpu = max_dets_.to(at::kCPU, at::kLong).contiguous();
+  const auto max_dets = max_dets_cpu.to(dev);
+  const int64_t T = iou_thrs.numel(), R = rec_thrs.numel(), M = max_dets.numel(), A = area_rng.size(0);
+  TORCH_CHECK(T > 0 && R > 0 && M > 0 && A > 0, "coco_evaluate_gpu: empty parameter list");
+  TORCH_CHECK(T * A <= 64, "coco_evaluate_gpu: at most 64 (IoU threshold, area range) combinations");
+  TORCH_CHECK(R <= kCocoMaxRec, "coco_evaluate_gpu: at most ", kCocoMaxRec, " recall thresholds");
+  const int64_t max_det_last = max_dets_cpu.data_ptr<int64_t>()[M - 1];
+  const bool custom = img_iou_.has_value() && img_iou_->defined();
+
+  auto precision = at::full({T, R, K, A, M}, -1.0, det_scores.options());
+  auto recall = at::full({T, K, A, M}, -1.0, det_scores.options());
+  auto scores_out = at::full({T, R, K, A, M}, -1.0, det_scores.options());
+  auto lopt = det_cls.options();
+  if (K == 0) return {precision, recall, scores_out, at::zeros({0}, det_scores.options()), at::zeros({0, 5}, lopt)};
+
+  // ---- 1. orderings ------------------------------------------------------------------------------------
+  const auto det_pair = det_img * K + det_cls;
+  at::Tensor order = stable_order(det_scores, /*descending=*/true);
+  order = order.index_select(0, stable_order(det_pair.index_select(0, order), false));
+  const auto det_pair_sorted = det_pair.index_select(0, order);
+  const auto first_of_pair = at::searchsorted(det_pair_sorted, det_pair_sorted, /*out_int32=*/false, /*right=*/false);
+  const auto rank_all = at::arange(det_pair_sorted.numel(), lopt) - first_of_pair;
+  const auto keep = at::nonzero(rank_all < max_det_last).reshape({-1});
+  const auto dsel = order.index_select(0, keep);  // kept detections in (image, class, rank) order
+  const auto d_pair = det_pair_sorted.index_select(0, keep);
+  const auto d_rank = rank_all.index_select(0, keep).to(at::kInt);
+  const auto gorder = stable_order(gt_img * K + gt_cls, false);
+  const auto g_pair = (gt_img * K + gt_cls).index_select(0, gorder);
+
+  const auto pair_keys = std::get<0>(at::_unique(at::cat({d_pair, g_pair}), /*sorted=*/true));
+  const int64_t P = pair_keys.numel();
+  const auto det_start = at::searchsorted(d_pair, pair_keys, false, false);
+  const auto det_count = at::searchsorted(d_pair, pair_keys, false, true) - det_start;
+  const auto gt_start = at::searchsorted(g_pair, pair_keys, false, false);
+  const auto gt_count = at::searchsorted(g_pair, pair_keys, false, true) - gt_start;
+  const auto pair_cls = pair_keys.remainder(K);
+  const auto pair_img = pair_keys.div(K, "floor");
+  const auto pair_cells = det_count * gt_count;
+  const auto iou_off = pair_cells.cumsum(0) - pair_cells;
+  // one host read for both the export size and the per-pair ground-truth limit
+  const auto host = at::stack({P ? pair_cells.sum() : at::zeros({}, lopt), P ? gt_count.max() : at::zeros({}, lopt)}).cpu();
+  const int64_t total_cells = host.data_ptr<int64_t>()[0];
+  TORCH_CHECK(host.data_ptr<int64_t>()[1] <= kCocoMaxGt, "coco_evaluate_gpu: more than ", kCocoMaxGt,
+              " ground-truth boxes of one class in one image");
+
+  const auto sd_box = det_boxes.index_select(0, dsel).contiguous();
+  const auto sd_area = det_area.index_select(0, dsel).contiguous();
+  const auto sd_score = det_scores.index_select(0, dsel).contiguous();
+  const auto sg_box = gt_boxes.index_select(0, gorder).contiguous();
+  const auto sg_crowd = gt_crowd.index_select(0, gorder).contiguous();
+  const auto sg_area = gt_area.index_select(0, gorder).contiguous();
+  at::Tensor mats, img_off, img_ng, det_local, gt_local;
+  CocoCustomIoU cust{nullptr, nullptr, nullptr, nullptr, nullptr};
+  if (custom) {
+    mats = f64(*img_iou_);
+    img_off = i64(*img_iou_offsets_);
+    img_ng = i64(*img_ng_);
+    det_local = i64(*det_local_).index_select(0, dsel).contiguous();
+    gt_local = i64(*gt_local_).index_select(0, gorder).contiguous();
+    cust = {mats.data_ptr<double>(), img_off.data_ptr<int64_t>(), img_ng.data_ptr<int64_t>(), det_local.data_ptr<int64_t>(),
+            gt_local.data_ptr<int64_t>()};
+  }
+
+  // ---- 2. matching -------------------------------------------------------------------------------------
+  const int64_t Nk = dsel.numel();
+  auto matched = at::zeros({Nk}, lopt);
+  auto ignored = at::zeros({Nk}, lopt);
+  auto npig = at::zeros({K * A}, lopt);
+  auto iou_values = at::empty({export_iou ? total_cells : 0}, det_scores.options());
+  if (P > 0) {
+    CocoPairs pairs{det_start.data_ptr<int64_t>(), det_count.data_ptr<int64_t>(), gt_start.data_ptr<int64_t>(),
+                    gt_count.data_ptr<int64_t>(), pair_cls.data_ptr<int64_t>(), pair_img.data_ptr<int64_t>(),
+                    iou_off.data_ptr<int64_t>()};
+    const int blocks = static_cast<int>((P + kCocoMatchWaves - 1) / kCocoMatchWaves);
+    coco_match_kernel<<<blocks, kCocoMatchWaves * kWave, 0, stream()>>>(
+        pairs, P, sd_box.data_ptr<double>(), sd_area.data_ptr<double>(), sg_box.data_ptr<double>(),
+        sg_crowd.data_ptr<int64_t>(), sg_area.data_ptr<double>(), iou_thrs.data_ptr<double>(), static_cast<int>(T),
+        area_rng.data_ptr<double>(), static_cast<int>(A), custom, cust, export_iou,
+        export_iou ? iou_values.data_ptr<double>() : nullptr, reinterpret_cast<uint64_t*>(matched.data_ptr<int64_t>()),
+        reinterpret_cast<uint64_t*>(ignored.data_ptr<int64_t>()), npig.data_ptr<int64_t>());
+    TMX_LAUNCH_CHECK();
+  }
+
+  // ---- 3. accumulate order: (class, score desc, image, rank) ------------------------------------------
+  const auto d_cls = d_pair.remainder(K);
+  at::Tensor acc = stable_order(sd_score, true);
+  acc = acc.index_select(0, stable_order(d_cls.index_select(0, acc), false));
+  const auto a_rank = d_rank.index_select(0, acc).contiguous();
+  const auto a_matched = matched.index_select(0, acc).contiguous();
+  const auto a_ignored = ignored.index_select(0, acc).contiguous();
+  const auto a_score = sd_score.index_select(0, acc).contiguous();
+  const auto seg = at::searchsorted(d_cls.index_select(0, acc).contiguous(), at::arange(K + 1, lopt), false, false);
+
+  // ---- 4. accumulate -----------------------------------------------------------------------------------
+  const int64_t combos = K * A * M * T;
+  coco_accumulate_kernel<<<static_cast<unsigned>(combos), kWave, 0, stream()>>>(
+      seg.data_ptr<int64_t>(), static_cast<int>(K), static_cast<int>(A), static_cast<int>(M), static_cast<int>(T),
+      static_cast<int>(R), max_dets.data_ptr<int64_t>(), rec_thrs.data_ptr<double>(), a_rank.data_ptr<int32_t>(),
+      reinterpret_cast<const uint64_t*>(a_matched.data_ptr<int64_t>()),
+      reinterpret_cast<const uint64_t*>(a_ignored.data_ptr<int64_t>()), a_score.data_ptr<double>(),
+      npig.data_ptr<int64_t>(), precision.data_ptr<double>(), recall.data_ptr<double>(), scores_out.data_ptr<double>());
+  TMX_LAUNCH_CHECK();
+
+  auto iou_index = at::stack({pair_img, pair_cls, det_count, gt_count, iou_off}, 1);
+  return {precision, recall, scores_out, iou_values, iou_index};
+}
+
+}  // namespace tmx
+
+TORCH_LIBRARY_FRAGMENT(tmx, m) {
+  m.def(
+      "coco_evaluate_gpu(Tensor det_boxes, Tensor det_scores, Tensor det_cls, Tensor det_img, Tensor det_area, "
+      "Tensor gt_boxes, Tensor gt_cls, Tensor gt_img, Tensor gt_crowd, Tensor gt_area, int num_classes, "
+      "int num_images, Tensor iou_thrs, Tensor rec_thrs, Tensor max_dets, Tensor area_rng, Tensor? img_iou, "
+      "Tensor? img_iou_offsets, Tensor? det_local, Tensor? gt_local, Tensor? img_ng, bool export_iou) "
+      "-> (Tensor, Tensor, Tensor, Tensor, Tensor)");
+}
+
+TORCH_LIBRARY_IMPL(tmx, CUDA, m) { m.impl("coco_evaluate_gpu", &tmx::coco_evaluate_gpu); }

@@ -97,6 +97,109 @@ def test_map_segm_gpu_matches_cpu():
         torch.testing.assert_close(a[k].cpu(), c[k], atol=1e-6, rtol=0, msg=k)
 
 
+def _coco_inputs(seed, n_img, n_cls, max_det_img, max_gt_img, tie_scores):
+    """Flat COCO evaluator inputs with crowds, zero/huge areas, score ties and >100 detections in some pairs."""
+    g = torch.Generator().manual_seed(seed)
+    d_img, g_img, d_box, g_box = [], [], [], []
+    for i in range(n_img):
+        ng = int(torch.randint(0, max_gt_img + 1, (1,), generator=g))
+        nd = int(torch.randint(0, max_det_img + 1, (1,), generator=g))
+        gb = _boxes(ng, g) if ng else torch.zeros(0, 4)
+        src = gb[torch.randint(0, max(ng, 1), (nd,), generator=g)] if ng else _boxes(nd, g)
+        db = src + torch.randn(nd, 4, generator=g) * 8
+        db[:, 2:] = torch.maximum(db[:, 2:], db[:, :2] + 1)
+        g_box.append(gb); d_box.append(db)
+        g_img += [i] * ng; d_img += [i] * nd
+    xyxy2xywh = lambda b: torch.cat([b[:, :2], b[:, 2:] - b[:, :2]], 1).double()
+    det_boxes, gt_boxes = xyxy2xywh(torch.cat(d_box)), xyxy2xywh(torch.cat(g_box))
+    nd, ng = det_boxes.shape[0], gt_boxes.shape[0]
+    scores = torch.rand(nd, generator=g).double()
+    if tie_scores:
+        scores = (scores * 8).floor() / 8
+    det_labels = torch.randint(0, n_cls, (nd,), generator=g) * 3 + 1  # sparse category ids
+    gt_labels = torch.randint(0, n_cls, (ng,), generator=g) * 3 + 1
+    gt_crowd = (torch.rand(ng, generator=g) < 0.1).long()
+    gt_area = torch.where(torch.rand(ng, generator=g) < 0.3, torch.zeros(ng).double(), gt_boxes[:, 2] * gt_boxes[:, 3] * 1.3)
+    gt_area = torch.where(gt_area > 0, gt_area, gt_boxes[:, 2] * gt_boxes[:, 3])
+    det_area = det_boxes[:, 2] * det_boxes[:, 3]
+    return dict(det_boxes=det_boxes, det_scores=scores, det_labels=det_labels, det_img=torch.tensor(d_img, dtype=torch.long),
+                det_area=det_area, gt_boxes=gt_boxes, gt_labels=gt_labels, gt_img=torch.tensor(g_img, dtype=torch.long),
+                gt_crowd=gt_crowd, gt_area=gt_area)
+
+
+@pytest.mark.parametrize("cfg", [
+    dict(seed=0, n_img=40, n_cls=6, max_det_img=30, max_gt_img=12, tie_scores=False, max_dets=[1, 10, 100]),
+    dict(seed=1, n_img=25, n_cls=3, max_det_img=260, max_gt_img=70, tie_scores=True, max_dets=[1, 10, 100]),
+    dict(seed=2, n_img=60, n_cls=10, max_det_img=15, max_gt_img=6, tie_scores=True, max_dets=[2, 5, 300]),
+    dict(seed=3, n_img=7, n_cls=2, max_det_img=0, max_gt_img=5, tie_scores=False, max_dets=[1, 10, 100]),
+    dict(seed=4, n_img=9, n_cls=2, max_det_img=12, max_gt_img=0, tie_scores=False, max_dets=[1, 10, 100]),
+])
+def test_coco_evaluate_gpu_matches_host(cfg):
+    """Device matcher + accumulator (csrc/coco_match.hip) against the host evaluator (coco_eval.cpp): precision,
+    recall, score tables and exported IoUs are bit-identical (same double arithmetic)."""
+    from torchmetrics_forked_amd.detection.mean_ap import _AREA_RANGES
+
+    x = _coco_inputs(cfg["seed"], cfg["n_img"], cfg["n_cls"], cfg["max_det_img"], cfg["max_gt_img"], cfg["tie_scores"])
+    cats = torch.cat([x["det_labels"], x["gt_labels"]]).unique()
+    iou_thr = torch.linspace(0.5, 0.95, 10, dtype=torch.float64)
+    rec_thr = torch.linspace(0.0, 1.0, 101, dtype=torch.float64)
+    max_dets = torch.tensor(cfg["max_dets"], dtype=torch.long)
+    area = torch.tensor(_AREA_RANGES, dtype=torch.float64)
+    host = torch.ops.tmx.coco_evaluate(
+        x["det_boxes"], x["det_scores"], x["det_labels"], x["det_img"], x["det_area"], x["gt_boxes"], x["gt_labels"],
+        x["gt_img"], x["gt_crowd"], x["gt_area"], cats, cfg["n_img"], iou_thr, rec_thr, max_dets, area, None, None)
+    c = lambda t: t.cuda()
+    dev = torch.ops.tmx.coco_evaluate_gpu(
+        c(x["det_boxes"]), c(x["det_scores"]), c(torch.searchsorted(cats, x["det_labels"])), c(x["det_img"]),
+        c(x["det_area"]), c(x["gt_boxes"]), c(torch.searchsorted(cats, x["gt_labels"])), c(x["gt_img"]),
+        c(x["gt_crowd"]), c(x["gt_area"]), cats.numel(), cfg["n_img"], c(iou_thr), c(rec_thr), max_dets, c(area),
+        None, None, None, None, None, True)
+    for name, h, d in zip(("precision", "recall", "scores"), host[:3], dev[:3]):
+        assert torch.equal(h, d.cpu()), (name, (h - d.cpu()).abs().max())
+    # exported IoU blocks: device lists non-empty pairs only
+    hv, hi = host[3], host[4]
+    dv, di = dev[3].cpu(), dev[4].cpu()
+    hmap = {(int(r[0]), int(r[1])): hv[r[4]: r[4] + r[2] * r[3]] for r in hi if r[2] and r[3]}
+    dmap = {(int(r[0]), int(r[1])): dv[r[4]: r[4] + r[2] * r[3]] for r in di if r[2] and r[3]}
+    assert hmap.keys() == dmap.keys()
+    for key in hmap:
+        assert torch.equal(hmap[key], dmap[key]), key
+
+
+def test_map_module_gpu_many_dets_crowds_matches_cpu():
+    """Module level: crowd ground truth, supplied areas, > max_det detections, extended summary and micro average."""
+    from torchmetrics_forked_amd.detection import MeanAveragePrecision
+
+    g = torch.Generator().manual_seed(5)
+    preds, target = [], []
+    for _ in range(12):
+        ng = int(torch.randint(1, 30, (1,), generator=g))
+        gt = _boxes(ng, g)
+        lab = torch.randint(0, 4, (ng,), generator=g)
+        nd = int(torch.randint(50, 160, (1,), generator=g))
+        det = gt[torch.randint(0, ng, (nd,), generator=g)] + torch.randn(nd, 4, generator=g) * 12
+        det[:, 2:] = torch.maximum(det[:, 2:], det[:, :2] + 1)
+        preds.append({"boxes": det, "scores": (torch.rand(nd, generator=g) * 16).floor() / 16,
+                      "labels": torch.randint(0, 4, (nd,), generator=g)})
+        target.append({"boxes": gt, "labels": lab, "iscrowd": (torch.rand(ng, generator=g) < 0.15).long(),
+                       "area": torch.rand(ng, generator=g) * 20000})
+    for avg in ("macro", "micro"):
+        kw = dict(class_metrics=True, extended_summary=True, average=avg)
+        gpu, cpu = MeanAveragePrecision(**kw).cuda(), MeanAveragePrecision(**kw)
+        gpu.warn_on_many_detections = cpu.warn_on_many_detections = False
+        gpu.update(*_to((preds, target), "cuda"))
+        cpu.update(preds, target)
+        a, c = gpu.compute(), cpu.compute()
+        for k in c:
+            if k == "ious":
+                assert a[k].keys() == c[k].keys()
+                for key in c[k]:
+                    va, vc = a[k][key], c[k][key]
+                    assert (isinstance(va, list) and isinstance(vc, list)) or torch.equal(va.cpu(), vc), key
+            else:
+                torch.testing.assert_close(a[k].cpu(), c[k], atol=0, rtol=0, msg=k)
+
+
 @pytest.mark.parametrize("cls_name", ["IntersectionOverUnion", "GeneralizedIntersectionOverUnion",
                                       "DistanceIntersectionOverUnion", "CompleteIntersectionOverUnion"])
 def test_iou_modules_gpu(cls_name):

@@ -38,11 +38,12 @@ _STAT_NAMES = (
 
 
 class _EvalResult:
-    __slots__ = ("precision", "recall", "iou_values", "iou_index", "cat_ids")
+    __slots__ = ("precision", "recall", "iou_values", "iou_index", "cat_ids", "num_images")
 
-    def __init__(self, precision: Tensor, recall: Tensor, iou_values: Tensor, iou_index: Tensor, cat_ids: List[int]):
-        self.precision, self.recall, self.iou_values, self.iou_index, self.cat_ids = (
-            precision, recall, iou_values, iou_index, cat_ids,
+    def __init__(self, precision: Tensor, recall: Tensor, iou_values: Tensor, iou_index: Tensor, cat_ids: List[int],
+                 num_images: int):
+        self.precision, self.recall, self.iou_values, self.iou_index, self.cat_ids, self.num_images = (
+            precision, recall, iou_values, iou_index, cat_ids, num_images,
         )
 
 
@@ -127,41 +128,70 @@ class MeanAveragePrecision(Metric):
     # ------------------------------------------------------------------------------------------------------
     # update
     # ------------------------------------------------------------------------------------------------------
-    def _get_safe_item_values(self, item: Dict[str, Any], warn: bool = False) -> Tuple[Optional[Tensor], Optional[Tensor]]:
-        boxes = masks = None
-        if "bbox" in self.iou_type:
-            boxes = _fix_empty_tensors(item["boxes"])
-            if boxes.numel() > 0:
-                boxes = box_convert(boxes, in_fmt=self.box_format, out_fmt="xywh")
-            else:
-                boxes = boxes.reshape(0, 4)
-        if "segm" in self.iou_type:
-            masks = item["masks"]
-            masks = masks.reshape(0, 0, 0) if masks.numel() == 0 else masks.to(torch.bool)
-        limit = self.max_detection_thresholds[-1]
-        if warn and ((boxes is not None and len(boxes) > limit) or (masks is not None and len(masks) > limit)):
-            _warning_on_too_many_detections(limit)
-        return boxes, masks
-
     def update(self, preds: List[Dict[str, Tensor]], target: List[Dict[str, Tensor]]) -> None:
+        """Append one batch of images.  Box conversion runs once over the whole batch (one ``cat`` + one convert,
+        then per-image views), and missing ``iscrowd`` / ``area`` entries share one zero buffer, so the per-image
+        cost is list bookkeeping only (the reference converts and allocates per image, ``mean_ap.py:501-540``)."""
         _input_validator(preds, target, iou_type=self.iou_type)
-        for item in preds:
-            boxes, masks = self._get_safe_item_values(item, warn=self.warn_on_many_detections)
-            if boxes is not None:
-                self.detection_box.append(boxes)
-            if masks is not None:
-                self.detection_mask.append(masks)
-            self.detection_labels.append(item["labels"])
-            self.detection_scores.append(item["scores"])
-        for item in target:
-            boxes, masks = self._get_safe_item_values(item)
-            if boxes is not None:
-                self.groundtruth_box.append(boxes)
-            if masks is not None:
-                self.groundtruth_mask.append(masks)
-            self.groundtruth_labels.append(item["labels"])
-            self.groundtruth_crowds.append(item.get("iscrowd", torch.zeros_like(item["labels"])))
-            self.groundtruth_area.append(item.get("area", torch.zeros_like(item["labels"])))
+        limit = self.max_detection_thresholds[-1]
+        if "bbox" in self.iou_type:
+            det_boxes = self._convert_boxes([item["boxes"] for item in preds])
+            if self.warn_on_many_detections and any(len(b) > limit for b in det_boxes):
+                _warning_on_too_many_detections(limit)
+            self.detection_box.extend(det_boxes)
+            self.groundtruth_box.extend(self._convert_boxes([item["boxes"] for item in target]))
+        if "segm" in self.iou_type:
+            det_masks = [self._as_mask(item["masks"]) for item in preds]
+            if self.warn_on_many_detections and "bbox" not in self.iou_type and any(len(m) > limit for m in det_masks):
+                _warning_on_too_many_detections(limit)
+            self.detection_mask.extend(det_masks)
+            self.groundtruth_mask.extend(self._as_mask(item["masks"]) for item in target)
+        self.detection_labels.extend(item["labels"] for item in preds)
+        self.detection_scores.extend(item["scores"] for item in preds)
+        labels = [item["labels"] for item in target]
+        self.groundtruth_labels.extend(labels)
+        self.groundtruth_crowds.extend(self._optional_column(target, "iscrowd", labels))
+        self.groundtruth_area.extend(self._optional_column(target, "area", labels))
+
+    @staticmethod
+    def _as_mask(masks: Tensor) -> Tensor:
+        return masks.reshape(0, 0, 0) if masks.numel() == 0 else masks.to(torch.bool)
+
+    def _convert_boxes(self, boxes: List[Tensor]) -> List[Tensor]:
+        """Per-image ``xywh`` boxes; one conversion kernel for the whole batch when the images share device/dtype."""
+        boxes = [_fix_empty_tensors(b) for b in boxes]
+        uniform = (
+            len(boxes) > 1
+            and all(b.ndim == 2 and b.shape[-1] == 4 for b in boxes)
+            and len({(b.device, b.dtype) for b in boxes}) == 1
+        )
+        if not uniform:
+            out = []
+            for b in boxes:
+                out.append(box_convert(b, in_fmt=self.box_format, out_fmt="xywh") if b.numel() > 0 else b.reshape(0, 4))
+            return out
+        sizes = [b.shape[0] for b in boxes]
+        flat = torch.cat(boxes)
+        if flat.numel() > 0:
+            flat = box_convert(flat, in_fmt=self.box_format, out_fmt="xywh")
+        return list(torch.split(flat, sizes))
+
+    @staticmethod
+    def _optional_column(items: List[Dict[str, Tensor]], key: str, labels: List[Tensor]) -> List[Tensor]:
+        """``item[key]`` where present, else zeros shaped like the labels (one shared buffer for the batch)."""
+        missing = [i for i, item in enumerate(items) if key not in item]
+        out: List[Optional[Tensor]] = [item.get(key) for item in items]
+        if missing:
+            ref = labels[missing[0]]
+            if all(labels[i].device == ref.device and labels[i].dtype == ref.dtype for i in missing):
+                sizes = [labels[i].numel() for i in missing]
+                zeros = torch.zeros(sum(sizes), dtype=ref.dtype, device=ref.device)
+                for i, z in zip(missing, torch.split(zeros, sizes)):
+                    out[i] = z.view_as(labels[i])
+            else:
+                for i in missing:
+                    out[i] = torch.zeros_like(labels[i])
+        return out  # type: ignore[return-value]
 
     # ------------------------------------------------------------------------------------------------------
     # evaluation
@@ -178,7 +208,116 @@ class MeanAveragePrecision(Metric):
         rows = [t.detach().reshape(-1, width) if width else t.detach().reshape(-1) for t in lst]
         return torch.cat([r.cpu() for r in rows])
 
+    def _gpu_eligible(self) -> bool:
+        """The device evaluator covers T * A <= 64 (IoU thresholds x 4 area ranges) and up to 256 ascending recall
+        thresholds; anything else (and CPU states) takes the host evaluator ``tmx::coco_evaluate``."""
+        if not self.groundtruth_labels and not self.detection_labels:
+            return False
+        sample = (self.detection_labels or self.groundtruth_labels)[0]
+        if not (sample.is_cuda and ops.use_native(sample)):
+            return False
+        rt = self.rec_thresholds
+        return (
+            len(self.iou_thresholds) * len(_AREA_RANGES) <= 64
+            and len(rt) <= 256
+            and all(rt[i] <= rt[i + 1] for i in range(len(rt) - 1))
+        )
+
     def _evaluate(self, i_type: str, average: str, classes: List[int]) -> _EvalResult:
+        if self._gpu_eligible():
+            try:
+                return self._evaluate_gpu(i_type, average, classes)
+            except RuntimeError as err:  # > 1024 ground truths of one class in one image: host evaluator
+                if "ground-truth boxes of one class" not in str(err):
+                    raise
+        return self._evaluate_host(i_type, average, classes)
+
+    def _evaluate_gpu(self, i_type: str, average: str, classes: List[int]) -> _EvalResult:
+        """Flatten the per-image states on the device and run ``tmx::coco_evaluate_gpu`` (csrc/coco_match.hip):
+        matching and accumulation never leave the GPU; one small host read sizes the IoU export."""
+        dev = (self.detection_labels or self.groundtruth_labels)[0].device
+        num_images = len(self.groundtruth_labels)
+        det_sizes = [t.numel() for t in self.detection_labels]
+        gt_sizes = [t.numel() for t in self.groundtruth_labels]
+        n_det, n_gt = sum(det_sizes), sum(gt_sizes)
+
+        def flat(lst: List[Tensor], n: int, dtype: torch.dtype, width: int = 0) -> Tensor:
+            shape = (n, width) if width else (n,)
+            if not lst:
+                return torch.zeros(shape, dtype=dtype, device=dev)
+            return torch.cat([t.reshape(-1, width) if width else t.reshape(-1) for t in lst]).to(dev, dtype)
+
+        det_img = torch.repeat_interleave(
+            torch.arange(len(det_sizes), device=dev), torch.tensor(det_sizes, device=dev), output_size=n_det
+        )
+        gt_img = torch.repeat_interleave(
+            torch.arange(num_images, device=dev), torch.tensor(gt_sizes, device=dev), output_size=n_gt
+        )
+        det_labels = flat(self.detection_labels, n_det, torch.long)
+        gt_labels = flat(self.groundtruth_labels, n_gt, torch.long)
+        det_scores = flat(self.detection_scores, n_det, torch.float64)
+        gt_crowd = flat(self.groundtruth_crowds, n_gt, torch.long)
+        gt_area = flat(self.groundtruth_area, n_gt, torch.float64)
+        if average == "micro":
+            cat_ids = [0] if classes else []
+            det_cls, gt_cls = torch.zeros_like(det_labels), torch.zeros_like(gt_labels)
+        else:
+            cat_ids = list(classes)
+            cats = torch.tensor(cat_ids, dtype=torch.long, device=dev)
+            det_cls = torch.searchsorted(cats, det_labels)
+            gt_cls = torch.searchsorted(cats, gt_labels)
+
+        segm_in = "segm" in self.iou_type
+        if segm_in:
+            det_mask_area = flat([m.flatten(1).sum(1) if m.dim() > 1 else m.new_zeros(0) for m in self.detection_mask],
+                                 n_det, torch.float64)
+            gt_mask_area = flat([m.flatten(1).sum(1) if m.dim() > 1 else m.new_zeros(0) for m in self.groundtruth_mask],
+                                n_gt, torch.float64)
+        if "bbox" in self.iou_type:
+            det_boxes = flat(self.detection_box, n_det, torch.float64, 4)
+            gt_boxes = flat(self.groundtruth_box, n_gt, torch.float64, 4)
+        else:
+            det_boxes = torch.zeros(n_det, 4, dtype=torch.float64, device=dev)
+            gt_boxes = torch.zeros(n_gt, 4, dtype=torch.float64, device=dev)
+        det_area = det_mask_area if i_type == "segm" else det_boxes[:, 2] * det_boxes[:, 3]
+        gt_fallback = gt_mask_area if segm_in else gt_boxes[:, 2] * gt_boxes[:, 3]
+        gt_area = torch.where(gt_area > 0, gt_area, gt_fallback)
+
+        img_iou = img_off = det_local = gt_local = img_ng = None
+        if i_type == "segm":
+            mats, offs, off = [], [], 0
+            for i in range(num_images):
+                d, g = self.detection_mask[i], self.groundtruth_mask[i]
+                m = mask_iou(d, g.to(d.device), self.groundtruth_crowds[i].reshape(-1)).reshape(-1) \
+                    if d.numel() and g.numel() else torch.zeros(0, dtype=torch.float64, device=dev)
+                offs.append(off)
+                mats.append(m.to(dev))
+                off += m.numel()
+            img_iou = torch.cat(mats) if mats else torch.zeros(0, dtype=torch.float64, device=dev)
+            img_off = torch.tensor(offs, dtype=torch.long, device=dev)
+            img_ng = torch.tensor(gt_sizes, dtype=torch.long, device=dev)
+            det_first = torch.tensor(det_sizes, device=dev).cumsum(0) - torch.tensor(det_sizes, device=dev)
+            gt_first = img_ng.cumsum(0) - img_ng
+            det_local = torch.arange(n_det, device=dev) - det_first[det_img]
+            gt_local = torch.arange(n_gt, device=dev) - gt_first[gt_img]
+            if len(self.iou_type) == 1:
+                # the reference's COCO export drops images without ground-truth masks from the evaluated image set
+                keep = (img_ng > 0)[det_img]
+                det_boxes, det_scores, det_cls, det_area = det_boxes[keep], det_scores[keep], det_cls[keep], det_area[keep]
+                det_img, det_local = det_img[keep], det_local[keep]
+
+        prec, rec, _scores, iou_values, iou_index = torch.ops.tmx.coco_evaluate_gpu(
+            det_boxes, det_scores, det_cls, det_img, det_area, gt_boxes, gt_cls, gt_img, gt_crowd, gt_area,
+            len(cat_ids), num_images,
+            torch.tensor(self.iou_thresholds, dtype=torch.float64, device=dev),
+            torch.tensor(self.rec_thresholds, dtype=torch.float64, device=dev),
+            torch.tensor(self.max_detection_thresholds, dtype=torch.long),
+            torch.tensor(_AREA_RANGES, dtype=torch.float64, device=dev),
+            img_iou, img_off, det_local, gt_local, img_ng, self.extended_summary,
+        )
+        return _EvalResult(prec.cpu(), rec.cpu(), iou_values.cpu(), iou_index.cpu(), cat_ids, num_images)
+
+    def _evaluate_host(self, i_type: str, average: str, classes: List[int]) -> _EvalResult:
         num_images = len(self.groundtruth_labels)
         det_counts = torch.tensor([t.numel() for t in self.detection_labels], dtype=torch.long)
         gt_counts = torch.tensor([t.numel() for t in self.groundtruth_labels], dtype=torch.long)
@@ -249,7 +388,7 @@ class MeanAveragePrecision(Metric):
             torch.tensor(_AREA_RANGES, dtype=torch.float64),
             img_iou, img_off,
         )
-        return _EvalResult(prec, rec, iou_values, iou_index, cat_ids)
+        return _EvalResult(prec, rec, iou_values, iou_index, cat_ids, num_images)
 
     def _summarize(self, precision: Tensor, recall: Tensor) -> List[float]:
         """COCO ``summarize()`` statistics from accumulated ``precision [T,R,K,A,M]`` / ``recall [T,K,A,M]``."""
@@ -286,11 +425,13 @@ class MeanAveragePrecision(Metric):
         return {f"{prefix}{n}": torch.tensor([v], dtype=torch.float32) for n, v in zip(_STAT_NAMES, stats)}
 
     def _ious_dict(self, ev: _EvalResult) -> Dict[Tuple[int, int], Any]:
-        out: Dict[Tuple[int, int], Any] = {}
+        """Every (image, category) pair in pycocotools' order; pairs without both detections and ground truth
+        map to ``[]``."""
+        out: Dict[Tuple[int, int], Any] = {(i, c): [] for i in range(ev.num_images) for c in ev.cat_ids}
         vals = ev.iou_values
         for img, k, nd, ng, off in ev.iou_index.tolist():
-            key = (img, ev.cat_ids[k])
-            out[key] = vals[off : off + nd * ng].reshape(nd, ng).float() if nd and ng else []
+            if nd and ng:
+                out[(img, ev.cat_ids[k])] = vals[off : off + nd * ng].reshape(nd, ng).float()
         return out
 
     def compute(self) -> dict:
