@@ -47,6 +47,28 @@ __global__ void range_flag_kernel(const T* __restrict__ x, int64_t n, int* __res
   if (m && (threadIdx.x & (kWave - 1)) == 0) atomicOr(flag, 1);
 }
 
+// fp32: 16-B loads, four in flight per thread, and an early exit once any wave has found an out-of-range value
+// (logits trip the flag in the first few elements, so the remaining blocks read nothing)
+__global__ __launch_bounds__(256) void range_flag_f32_kernel(const float4* __restrict__ x, int64_t nvec, const float* __restrict__ tail,
+                                                             int ntail, int* __restrict__ flag) {
+  auto out = [](float v) { return !(v >= 0.f && v <= 1.f); };
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  bool bad = i < ntail && out(tail[i]);
+  for (; i < nvec; i += 4 * stride) {
+    if (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+    float4 q[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) q[u] = i + u * stride < nvec ? x[i + u * stride] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) bad |= out(q[u].x) | out(q[u].y) | out(q[u].z) | out(q[u].w);
+    if (__ballot(bad)) break;
+  }
+  // one store per wave that found something, and only while the flag is still clear (no same-address storm)
+  if (__ballot(bad) && (threadIdx.x & (kWave - 1)) == 0 && !__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+    atomicOr(flag, 1);
+}
+
 at::Tensor range_flag(const at::Tensor& x_) {
   auto x = x_.contiguous();
   auto flag = at::zeros({1}, x.options().dtype(at::kInt));
@@ -64,6 +86,19 @@ at::Tensor range_flag(const at::Tensor& x_) {
       hipLaunchKernelGGL(range_flag16_kernel<__hip_bfloat16>, grid, block, 0, stream(), xv, nvec, tail, ntail, flag.data_ptr<int>());
     else
       hipLaunchKernelGGL(range_flag16_kernel<__half>, grid, block, 0, stream(), xv, nvec, tail, ntail, flag.data_ptr<int>());
+  } else if (x.scalar_type() == at::kFloat && aligned) {
+    const int64_t nvec = n / 4;
+    const int ntail = static_cast<int>(n - nvec * 4);
+    const float* tail = x.data_ptr<float>() + nvec * 4;
+    // a one-block probe over the head first: for logits it sets the flag and every wave of the main pass leaves
+    // after one flag read; probabilities (all in range) are read once in full, without any atomics
+    const float4* xv = reinterpret_cast<const float4*>(x.data_ptr<float>());
+    const int64_t head = std::min<int64_t>(nvec, 16384);
+    hipLaunchKernelGGL(range_flag_f32_kernel, 1, block, 0, stream(), xv, head, tail, ntail, flag.data_ptr<int>());
+    if (nvec > head) {
+      const int grid = grid_for(std::max<int64_t>((nvec - head + 3) / 4, 1), block, 2048);
+      hipLaunchKernelGGL(range_flag_f32_kernel, grid, block, 0, stream(), xv + head, nvec - head, tail, 0, flag.data_ptr<int>());
+    }
   } else {
     TMX_DISPATCH_FLOAT(x.scalar_type(), "range_flag", [&] {
       hipLaunchKernelGGL(range_flag_kernel<scalar_t>, grid_for(n, block), block, 0, stream(),

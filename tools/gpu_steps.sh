@@ -15,7 +15,7 @@ for s in ${STEPS}; do
     t) run "pytest $arg" 600 python -u -m pytest "$arg" -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/pytest_$tag.log 2>&1; tail -3 $OUT/pytest_$tag.log ;;
     b) run "bench $arg" 600 python bench.py --config $arg ${BENCH_ARGS:-} > $OUT/bench_$tag.json 2> $OUT/bench_$tag.err; cat $OUT/bench_$tag.json ;;
     p) run "prof $arg" 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_$tag -o run --output-format csv -- python3 bench.py --config $arg ${BENCH_ARGS:-} > $OUT/prof_$tag.log 2>&1 ;;
-    k) run "script $arg" 600 python $arg > $OUT/script_$tag.log 2>&1; tail -20 $OUT/script_$tag.log ;;
+    k) run "script $arg" 600 env PYTHONPATH=$PWD python $arg > $OUT/script_$tag.log 2>&1; tail -20 $OUT/script_$tag.log ;;
   esac
 done
 echo "session done"

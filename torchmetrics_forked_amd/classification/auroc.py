@@ -91,7 +91,7 @@ class MulticlassAUROC(MulticlassPrecisionRecallCurve):
             auc, _, pos, neg = sc
             _warn_degenerate(pos, neg, sc.summary)
             return _reduce_auroc(auc.float(), self.average, pos.float(), summary=sc.summary, col=0)
-        return auroc_compute(self._curve_state(), "multiclass", self.num_classes, self.thresholds, self.average)
+        return auroc_compute(self._curve_state(lazy=True), "multiclass", self.num_classes, self.thresholds, self.average)
 
     def plot(self, val: Optional[Union[Tensor, List[Tensor]]] = None, ax: Optional[_AX_TYPE] = None) -> _PLOT_OUT_TYPE:
         return self._plot(val, ax)

@@ -85,7 +85,7 @@ class MulticlassAveragePrecision(MulticlassPrecisionRecallCurve):
             sc = self._sharded_scores()
             _, ap, pos, _ = sc
             return _reduce_auroc(ap.float(), self.average, pos.float(), summary=sc.summary, col=1)
-        return average_precision_compute(self._curve_state(), "multiclass", self.num_classes, self.thresholds, self.average)
+        return average_precision_compute(self._curve_state(lazy=True), "multiclass", self.num_classes, self.thresholds, self.average)
 
     def plot(self, val: Optional[Union[Tensor, List[Tensor]]] = None, ax: Optional[_AX_TYPE] = None) -> _PLOT_OUT_TYPE:
         return self._plot(val, ax)

@@ -105,7 +105,11 @@ class _CurveMetric(Metric):
     def _kernel_validates(self, preds: Tensor, target: Tensor) -> bool:
         """True when this batch takes a native pass that checks the target values itself (binned or exact
         histogram on the GPU): validation then skips its value-check kernels and hands over a device flag."""
-        return ops.use_native(target) and (self.thresholds is not None or self._hist_ok(preds))
+        return ops.use_native(target) and (
+            self.thresholds is not None
+            or self._hist_ok(preds)
+            or (self._task == "multiclass" and self._colmajor_ok(preds) and not (isinstance(self.score_hist, Tensor) and self.score_hist.numel() > 0))
+        )
 
     def _hist_ok(self, preds: Tensor) -> bool:
         if preds.dtype not in eng.HIST_DTYPES:
@@ -220,6 +224,16 @@ class _CurveMetric(Metric):
                 "Mixing 16-bit (exact-histogram) and 32/64-bit score batches in one curve metric is not supported;"
                 f" got {preds.dtype} after {self._hist_dtype}. Cast the inputs to one dtype."
             )
+        if self._task == "multiclass" and self._colmajor_ok(preds):
+            # GPU fp32: softmax decision + transpose in one pass; the state keeps the class-major buffer behind a
+            # transposed [N, C] view (same shape / values / checkpoint format as the reference's rows)
+            p, t = _rows_mc(preds, target, self._num)
+            if ii is not None:
+                keep = t != ii
+                p, t = p[keep], t[keep]
+            self.preds.append(cls_ops.softmax_colmajor(p.contiguous(), t, err_flag).t())
+            self.target.append(t)
+            return
         if self._task == "binary":
             st = binary_curve_update(preds, target, None, ii, force_samples=True)
         elif self._task == "multiclass":
@@ -401,12 +415,21 @@ class _CurveMetric(Metric):
         super()._sync_dist(dist_sync_fn, process_group)
 
     # ------------------------------------------------------------------------------------------- compute
-    def _curve_state(self) -> CurveState:
+    def _colmajor_ok(self, preds: Tensor) -> bool:
+        return preds.is_cuda and preds.dtype == torch.float32 and self._num <= 1024 and self._num % 4 == 0 and ops.use_native(preds)
+
+    def _curve_state(self, lazy: bool = False) -> CurveState:
+        """``lazy=True`` (class-averaged AUROC / AP only): fp32 samples written class-major by the GPU update are
+        handed over as ``ColumnChunks`` and streamed in place instead of being concatenated."""
         if self.thresholds is not None:
             cm = self.confmat.unsqueeze(1) if self._task == "binary" else self.confmat
             return ("binned", cm)
         if isinstance(self.score_hist, Tensor) and self.score_hist.numel() > 0:
             return ("hist", self.score_hist, self._hist_dtype or torch.bfloat16, self._tracked_range())
+        if lazy and isinstance(self.preds, list) and self.preds:
+            cols = [p.t() for p in self.preds]
+            if all(c.is_cuda and c.dtype == torch.float32 and c.is_contiguous() for c in cols):
+                return ("samples", eng.ColumnChunks(cols), dim_zero_cat(self.target))
         return ("samples", dim_zero_cat(self.preds), dim_zero_cat(self.target))
 
     def plot(

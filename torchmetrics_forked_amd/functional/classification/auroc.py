@@ -108,6 +108,11 @@ def _exact_scores(state: CurveState, task: str, num: int, ignore_index: Optional
         summ = cls_ops.curve_summary(sc) if sc.is_cuda else None
         return ExactScores.of(sc[:, 0], sc[:, 1], sc[:, 2], sc[:, 3], summ)
     preds, target = state[1], state[2]
+    anchored = eng.anchored_scores(preds, target, task, num, ignore_index)
+    if anchored is not None:
+        return ExactScores.of(anchored[:, 0], anchored[:, 1], anchored[:, 2], anchored[:, 3], cls_ops.curve_summary(anchored))
+    if isinstance(preds, eng.ColumnChunks):
+        preds = preds.materialize()
     if task == "binary":
         return ExactScores.of(*eng.samples_scores(preds, target == 1))
     if task == "multiclass":

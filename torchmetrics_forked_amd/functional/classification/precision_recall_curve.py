@@ -314,6 +314,8 @@ def _micro_state(state: CurveState, task: str, num: int, ignore_index: Optional[
     if kind == "hist":
         return ("hist", state[1].sum(0, keepdim=True), state[2])
     preds, target = state[1], state[2]
+    if isinstance(preds, eng.ColumnChunks):
+        preds = preds.materialize()
     if task == "multiclass":
         return ("samples", preds.flatten(), torch.nn.functional.one_hot(target, num).flatten())
     p, t = preds.flatten(), target.flatten()

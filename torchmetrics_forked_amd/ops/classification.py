@@ -4,7 +4,7 @@ Each function dispatches to ``torch.ops.tmx.*`` for GPU tensors (native library 
 eager PyTorch implementation for CPU tensors.  The eager implementations follow the reference semantics
 operation-by-operation and double as the numerics oracle in ``tests/test_ops_gpu.py``.
 """
-from typing import Optional, Tuple
+from typing import List, Optional, Tuple
 
 import torch
 from torch import Tensor
@@ -337,3 +337,21 @@ def binned_curve_update(
     below = total - above
     upd = torch.stack([below, above], dim=-1)  # [C, 2(y), T, 2(p)]
     confmat += upd.permute(2, 0, 1, 3)
+
+
+ANCHOR_MAX_POS = 8192  # csrc/curve_anchor.hip kAnchorMaxPos
+
+
+def anchored_scores(cols: List[Tensor], pos_off: Tensor, pos_rows: Tensor, max_pos: int) -> Tensor:
+    """float64 ``[C, 4]`` = (auroc, ap, n_pos, n_neg) from class-major fp32 score chunks ``cols[k] [C, n_k]`` whose
+    positives (global rows over the chunks) are ``pos_rows[pos_off[c]:pos_off[c+1]]`` (GPU, at most
+    ``ANCHOR_MAX_POS`` per class): one streaming pass, no sort and no concatenation of the samples
+    (csrc/curve_anchor.hip)."""
+    return torch.ops.tmx.anchored_curve_scores(cols, pos_off, pos_rows, int(max_pos))
+
+
+def softmax_colmajor(rows: Tensor, target: Optional[Tensor] = None, err_flag: Optional[Tensor] = None) -> Tensor:
+    """Class-major ``[C, N]`` fp32 probabilities of GPU fp32 rows ``[N, C]`` (C % 4 == 0, C <= 1024): softmax iff any value of the
+    batch is outside [0, 1] (the reference's rule), in one pass that also transposes (csrc/curve_anchor.hip).
+    With ``target`` and ``err_flag`` the pass also ORs "a target outside [0, C)" into the flag."""
+    return torch.ops.tmx.softmax_colmajor(rows, target, err_flag)
