@@ -24,10 +24,13 @@ constexpr int kAnchorMaxPos = 8192;  // per class; larger anchor sets take the s
 constexpr int kAnchorThreads = 1024;
 constexpr int kAnchorTable = 8192;   // bucket-table entries of the stream kernel (32 KiB)
 
-// monotone uint32 image of a float (-0 == +0; NaN lands outside every finite bucket)
+typedef float AnchorF4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) AnchorF4 GlobalF4;
+
+// monotone uint32 image of a float (-0 == +0 via x + 0; NaN lands outside every finite bucket)
 __device__ __forceinline__ uint32_t anchor_order_key(float x) {
-  uint32_t u = __float_as_uint(x == 0.f ? 0.f : x);
-  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+  const int i = __float_as_int(x + 0.0f);
+  return static_cast<uint32_t>(i ^ ((i >> 31) | static_cast<int>(0x80000000u)));
 }
 
 // ------------------------------------------------------------------------------------------- 1. prepare
@@ -164,6 +167,7 @@ __global__ __launch_bounds__(kAnchorThreads) void anchor_stream_kernel(
   // counted in registers and added once per wave, not with per-element LDS atomics
   uint32_t n_above = 0, n_below = 0;
   const int last = nt - 1;
+  const int dmax = D > 0 ? D - 1 : 0;
 
   constexpr int kE = 8;  // elements per thread per round: every phase is issued for all of them before one wait
   auto drop_batch = [&](const float (&x)[kE], int valid) {
@@ -175,33 +179,39 @@ __global__ __launch_bounds__(kAnchorThreads) void anchor_stream_kernel(
     }
     float k0[kE];
 #pragma unroll
-    for (int e = 0; e < kE; ++e) k0[e] = keys[min(static_cast<int>(ent[e] & 0xFFFFu), D - 1 < 0 ? 0 : D - 1)];
+    for (int e = 0; e < kE; ++e) k0[e] = keys[min(static_cast<int>(ent[e] & 0xFFFFu), dmax)];
+    int slot[kE];
+    bool any_deep = false;
 #pragma unroll
     for (int e = 0; e < kE; ++e) {
-      if (e >= valid) break;
-      int first = static_cast<int>(ent[e] & 0xFFFFu);
-      const int cnt = static_cast<int>(ent[e] >> 16);
-      int slot;
-      if (cnt == 0 || x[e] > k0[e]) {
-        slot = 2 * first;
-      } else if (x[e] == k0[e]) {
-        slot = 2 * first + 1;
-      } else {  // below the bucket's first key: search the rest of the bucket (rare: >= 2 keys in one bucket)
-        int lo = first + 1, hi = first + cnt;
-        const int end = hi;
-        while (lo < hi) {
-          const int mid = (lo + hi) >> 1;
-          if (keys[mid] > x[e]) lo = mid + 1; else hi = mid;
+      // common case without branches: the bucket holds 0 or 1 keys, or x is not below its first key
+      const int first = static_cast<int>(ent[e] & 0xFFFFu);
+      const bool gt = ent[e] < 0x10000u || x[e] > k0[e];
+      slot[e] = 2 * first + (gt ? 0 : (x[e] == k0[e] ? 1 : 2));
+      any_deep |= !gt && x[e] < k0[e] && ent[e] >= 0x20000u;
+    }
+    if (__ballot(any_deep)) {  // below the first of several keys in one bucket: search the bucket (rare)
+#pragma unroll
+      for (int e = 0; e < kE; ++e) {
+        const int first = static_cast<int>(ent[e] & 0xFFFFu), cnt = static_cast<int>(ent[e] >> 16);
+        if (cnt > 1 && x[e] < k0[e]) {
+          int lo = first + 1, hi = first + cnt;
+          const int end = hi;
+          while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (keys[mid] > x[e]) lo = mid + 1; else hi = mid;
+          }
+          slot[e] = (lo < end && keys[lo] == x[e]) ? 2 * lo + 1 : 2 * lo;
         }
-        slot = (lo < end && keys[lo] == x[e]) ? 2 * lo + 1 : 2 * lo;
       }
-      if (slot == 0) {
-        ++n_above;
-      } else if (slot == 2 * D) {
-        ++n_below;
-      } else {
-        atomicAdd(bins + slot, 1u);
-      }
+    }
+#pragma unroll
+    for (int e = 0; e < kE; ++e) {
+      const bool live = e < valid;
+      const bool above = slot[e] == 0, below = slot[e] == 2 * D;
+      n_above += (live && above) ? 1u : 0u;
+      n_below += (live && below) ? 1u : 0u;
+      if (live && !above && !below) atomicAdd(bins + slot[e], 1u);
     }
   };
 
@@ -210,19 +220,28 @@ __global__ __launch_bounds__(kAnchorThreads) void anchor_stream_kernel(
     const int64_t n_k = tl[1], r0 = tl[2], r1 = tl[3];
     const float* col = reinterpret_cast<const float*>(tl[0]) + static_cast<int64_t>(c) * n_k;
     if (VEC) {  // every chunk has n_k % 4 == 0 and segment bounds on multiples of 4; two 16-B loads in flight
-      const float4* c4 = reinterpret_cast<const float4*>(col);
-      const int64_t e4 = r1 / 4;
+      // global (not flat) loads: flat loads count on lgkmcnt too, so every LDS wait would also wait for them
+      const GlobalF4* c4 = (const GlobalF4*)(col);  // address-space cast
+      const int e4 = static_cast<int>(r1 / 4 - r0 / 4);  // float4s of this segment (< 2^31)
+      c4 += r0 / 4;
       const int stride = blockDim.x;
-      for (int64_t i = r0 / 4 + threadIdx.x; i < e4; i += 2 * stride) {
-        float x[kE];
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          const float4 q = i + u * stride < e4 ? c4[i + u * stride] : make_float4(0.f, 0.f, 0.f, 0.f);
-          x[4 * u] = q.x; x[4 * u + 1] = q.y; x[4 * u + 2] = q.z; x[4 * u + 3] = q.w;
+      // software pipeline: the next round's two loads are issued before this round's LDS work
+      int i = threadIdx.x;
+      AnchorF4 n0, n1;
+      if (i < e4) {
+        n0 = c4[i];
+        n1 = c4[i + stride < e4 ? i + stride : i];  // unconditional load, ignored when out of range
+      }
+      for (; i < e4; i += 2 * stride) {
+        const bool second = i + stride < e4;
+        const AnchorF4 q0 = n0, q1 = n1;
+        const int nx = i + 2 * stride;
+        if (nx < e4) {
+          n0 = c4[nx];
+          n1 = c4[nx + stride < e4 ? nx + stride : nx];
         }
-        const int64_t left = e4 - i;  // float4s of this thread still in range: u < left / stride (rounded up)
-        const int valid = static_cast<int>(min<int64_t>(2, (left + stride - 1) / stride)) * 4;
-        drop_batch(x, valid);
+        const float x[kE] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+        drop_batch(x, second ? 8 : 4);
       }
     } else {
       for (int64_t i = r0 + threadIdx.x * kE; i < r1; i += static_cast<int64_t>(blockDim.x) * kE) {
