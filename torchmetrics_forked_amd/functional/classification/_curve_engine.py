@@ -169,3 +169,24 @@ def samples_curve_points(preds: Tensor, labels: Tensor) -> Tuple[Tensor, Tensor,
         tps = torch.cumsum(sl * 1.0, dim=0)[thr_idx]
         fps = 1 + thr_idx - tps
         return fps, tps, sp[thr_idx]
+
+
+def samples_curve_points_columns(preds: Tensor, labels: Tensor) -> List[Tuple[Tensor, Tensor, Tensor]]:
+    """(fps, tps, thresholds) for every column of ``preds [N, C]`` against binary ``labels [N, C]``, from ONE batched
+    sort of the class-major scores (the reference runs one argsort per class in a Python loop,
+    ``precision_recall_curve.py:558-563``).  Ties are merged into one point, so the sort order among equal scores
+    does not matter; one host read sizes the per-class outputs."""
+    with torch.no_grad():
+        cols = preds.t().contiguous()
+        sv, order = torch.sort(cols, dim=1, descending=True)
+        sl = torch.gather(labels.t().to(torch.float32), 1, order)
+        tps = torch.cumsum(sl, dim=1)
+        n = cols.shape[1]
+        idx = torch.arange(n, device=cols.device, dtype=torch.float32).expand_as(tps)
+        fps = idx + 1 - tps
+        last = torch.ones_like(sv, dtype=torch.bool)
+        last[:, :-1] = sv[:, 1:] != sv[:, :-1]
+        counts = last.sum(1).tolist()
+        f_sel, t_sel, v_sel = fps[last], tps[last], sv[last]
+        return list(zip(torch.split(f_sel, counts), torch.split(t_sel, counts), torch.split(v_sel, counts)))
+

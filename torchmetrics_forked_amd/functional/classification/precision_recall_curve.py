@@ -272,8 +272,15 @@ def _points(state: CurveState, task: str, num: int, ignore_index: Optional[int])
     if kind == "hist":
         return eng.hist_curve_points(state[1], state[2])
     preds, target = state[1], state[2]
+    if isinstance(preds, eng.ColumnChunks):
+        preds = preds.materialize()
     if task == "binary":
         return [eng.samples_curve_points(preds, target == 1)]
+    if task == "multiclass" and preds.shape[0] > 0:
+        labels = target.reshape(-1, 1) == torch.arange(num, device=target.device).reshape(1, -1)
+        return eng.samples_curve_points_columns(preds, labels)
+    if task == "multilabel" and ignore_index is None and preds.shape[0] > 0:
+        return eng.samples_curve_points_columns(preds, target == 1)
     out = []
     for i in range(num):
         if task == "multiclass":
