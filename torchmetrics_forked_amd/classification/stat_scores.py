@@ -200,6 +200,21 @@ class MulticlassStatScores(_AbstractStatScores):
         if not self._fused_update(preds, target):
             self._update_state(*self._batch_stats(preds, target))
 
+    def _fusion_key(self) -> Optional[Tuple]:
+        """Collection fusion (ops/fused.py): global top-1 stats derive from the shared argmax pair counts."""
+        if self.multidim_average != "global" or self.top_k != 1:
+            return None
+        return ("multiclass_scores", self.num_classes, self.ignore_index)
+
+    def _fold_states(self) -> Optional[Tuple[Tensor, Tensor, Tensor, Tensor, bool]]:
+        """(tp, fp, tn, fn, micro) states the fused plan's ``confmat_fold`` adds into, or None when not fusable."""
+        if self.multidim_average != "global" or self.top_k != 1:
+            return None
+        states = (self.tp, self.fp, self.tn, self.fn)
+        if not all(isinstance(s, Tensor) and s.dtype == torch.long and s.is_contiguous() for s in states):
+            return None
+        return (*states, self.average == "micro")
+
     def compute(self) -> Tensor:
         tp, fp, tn, fn = self._final_state()
         return _multiclass_stat_scores_compute(tp, fp, tn, fn, self.average, self.multidim_average)

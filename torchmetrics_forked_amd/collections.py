@@ -95,8 +95,7 @@ class MetricCollection(ModuleDict):
             members = [n for n in plan.names if n in names]
             if len(members) < 2:
                 continue
-            if plan.run({n: self._modules[n] for n in members}, args, kwargs):
-                done.update(members)
+            done.update(plan.run({n: self._modules[n] for n in members}, args, kwargs))
         return done
 
     def _merge_compute_groups(self) -> None:
@@ -212,11 +211,37 @@ class MetricCollection(ModuleDict):
         if self._groups_checked:
             self._compute_groups_create_state_ref()
 
+    def _forward_fused(self, args: Tuple, kwargs: Dict[str, Any]) -> Dict[str, Any]:
+        """``forward`` of plan members through the fused update: every eligible member (reduce-state forward) parks
+        its global state, the plan updates all of them from one pass over the inputs, and each member computes
+        its batch value and merges the global state back (``Metric._fused_forward_begin/_end``)."""
+        from torchmetrics_forked_amd.ops.fused import build_fused_plans
+
+        if self._fused_plans is None:
+            self._fused_plans = build_fused_plans(self._modules)
+        out: Dict[str, Any] = {}
+        for plan in self._fused_plans:
+            mods = {n: self._modules[n] for n in plan.names if n in self._modules and n not in out}
+            mods = {n: m for n, m in mods.items() if m._fused_forward_ok()}
+            if len(mods) < 2:
+                continue
+            ctx = {n: m._fused_forward_begin() for n, m in mods.items()}
+            done = set(plan.run(mods, args, kwargs))
+            for n, m in mods.items():
+                if n not in done:
+                    m.update(*args, **m._filter_kwargs(**kwargs))
+            for n, m in mods.items():
+                out[n] = m._fused_forward_end(ctx[n])
+        return out
+
     def _compute_and_reduce(self, method_name: str, *args: Any, **kwargs: Any) -> Dict[str, Any]:
         result = {}
+        fused = self._forward_fused(args, kwargs) if method_name == "forward" else {}
         for k, m in self.items(keep_base=True, copy_state=False):
             if method_name == "compute":
                 res = m.compute()
+            elif method_name == "forward" and k in fused:
+                res = fused[k]
             elif method_name == "forward":
                 res = m(*args, **m._filter_kwargs(**kwargs))
             else:

@@ -319,6 +319,39 @@ class Metric(Module, ABC):
         self._leave_batch_mode(saved)
         return batch_val
 
+    # ---- split reduce-state forward, used by MetricCollection to run one fused update for several members ----
+    def _fused_forward_ok(self) -> bool:
+        full = self.full_state_update or self.full_state_update is None or self.dist_sync_on_step
+        return not full and not self._is_synced
+
+    def _fused_forward_begin(self) -> Tuple[Any, ...]:
+        """First half of ``_forward_reduce_state_update``: park the global state (and deferred flags), start a
+        fresh batch state; the caller then updates this metric (possibly through a fused collection kernel)."""
+        snap_def = None
+        if self._deferred is not None:
+            snap_def = self._deferred.snapshot()
+            self._deferred.clear()
+        snapshot = self.metric_state
+        count = self._update_count
+        self.reset()
+        saved = self._enter_batch_mode()
+        return snapshot, count, saved, snap_def
+
+    def _fused_forward_end(self, ctx: Tuple[Any, ...]) -> Any:
+        """Second half: batch value from the batch state, then merge the parked global state back in."""
+        snapshot, count, saved, snap_def = ctx
+        try:
+            batch_val = self.compute()
+            self._update_count = count + 1
+            with torch.no_grad():
+                self._reduce_states(snapshot)
+            self._leave_batch_mode(saved)
+        finally:
+            if snap_def is not None:
+                self._deferred.restore(snap_def)
+        self._forward_cache = batch_val
+        return batch_val
+
     def _reduce_states(self, incoming_state: Dict[str, Any]) -> None:
         """Merge ``incoming_state`` (global) with the current (batch) state according to each reduction."""
         for name in self._defaults:

@@ -1,68 +1,140 @@
 """Fused update plans for ``MetricCollection`` ("metrics reading the same inputs share one
-fused kernel").
+fused kernel"; the reference's compute groups, ``collections.py:200-307``, only share the states of metrics that
+would compute identical states).
 
-A plan groups collection members whose ``_fusion_key()`` matches and for which a fused kernel exists.  The
-plan is attempted on every update; if the inputs do not qualify (e.g. fp32 scores, thresholds set) it returns
-``False`` and the collection falls back to per-metric updates, so results never depend on fusion.
+A plan groups collection members whose ``_fusion_key()`` matches.  It is attempted on every update (and on
+``forward``); if the inputs do not qualify it returns ``False`` and the collection falls back to per-metric updates,
+so results never depend on fusion.
 
-Implemented plan:
-  * ``multiclass_scores``: one curve metric on the exact-histogram path (``MulticlassAUROC`` /
-    ``MulticlassAveragePrecision`` / ``MulticlassROC`` / ``MulticlassPrecisionRecallCurve``) + any number of
-    ``MulticlassConfusionMatrix`` members -> one pass over the ``[N, C]`` scores computes the softmax code
-    histogram *and* the argmax confusion matrix (``tmx::curve_hist_update`` with ``confmat``).
+``multiclass_scores`` plan (key ``("multiclass_scores", C, ignore_index)``) over
+  * at most one curve metric on the exact-histogram path (``MulticlassAUROC`` / ``AveragePrecision`` / ``ROC`` /
+    ``PrecisionRecallCurve``, bf16 / fp16 scores),
+  * any number of confusion-matrix members (``MulticlassConfusionMatrix``),
+  * any number of StatScores-family members (``MulticlassAccuracy`` / ``Precision`` / ``Recall`` / ``F1Score`` /
+    ``FBetaScore`` / ``Specificity`` / ``HammingDistance`` / ``StatScores``; global, top-1).
+One pass over the ``[N, C]`` scores -- the curve's row pass (softmax code histogram + argmax pairs) or, without a
+curve member, the argmax pair stream -- counts the batch's (target, argmax) pairs into a scratch ``[C, C]`` matrix;
+``tmx::confmat_fold`` (csrc/fused.hip) then adds it to every confusion-matrix state and turns its diagonal / row /
+column sums into every stat member's tp / fp / tn / fn.  With a single confusion-matrix member and no stat member
+the pass accumulates straight into that member's state.
 """
-from typing import Any, Dict, List, Tuple
+from typing import Any, Dict, List, Optional, Tuple
 
 import torch
 from torch import Tensor
 
+from torchmetrics_forked_amd import ops
 from torchmetrics_forked_amd.functional.classification import _curve_engine as eng
 
 
+def _stat_fusable(m: Any) -> bool:
+    return hasattr(m, "_fold_states") and m._fold_states() is not None
+
+
 class _MulticlassScoresPlan:
-    def __init__(self, names: List[str], curve_name: str, confmat_names: List[str]) -> None:
-        self.names = names
+    def __init__(self, curve_name: Optional[str], confmat_names: List[str], stat_names: List[str]) -> None:
         self.curve_name = curve_name
         self.confmat_names = confmat_names
+        self.stat_names = stat_names
+        self.names = ([curve_name] if curve_name else []) + confmat_names + stat_names
+        self._scratch: Dict[torch.device, Tuple[Tensor, Tensor]] = {}
 
-    def run(self, members: Dict[str, Any], args: Tuple, kwargs: Dict[str, Any]) -> bool:
-        if self.curve_name not in members or len(members) < 2:
-            return False
+    def _buffers(self, C: int, device: torch.device) -> Tuple[Tensor, Tensor]:
+        buf = self._scratch.get(device)
+        if buf is None or buf[0].shape[0] != C:
+            # zeroed once; confmat_fold leaves both zero again after every batch
+            buf = (torch.zeros(C, C, dtype=torch.long, device=device), torch.zeros(3 * C, dtype=torch.long, device=device))
+            self._scratch[device] = buf
+        return buf
+
+    def run(self, members: Dict[str, Any], args: Tuple, kwargs: Dict[str, Any]) -> List[str]:
+        """Update the qualifying members with one pass; returns their names (empty: nothing was done)."""
+        if len(members) < 2:
+            return []
         preds = kwargs.get("preds", args[0] if len(args) > 0 else None)
         target = kwargs.get("target", args[1] if len(args) > 1 else None)
-        if not isinstance(preds, Tensor) or not isinstance(target, Tensor):
-            return False
-        curve = members[self.curve_name]
-        if preds.dtype not in eng.HIST_DTYPES or preds.ndim != 2 or not curve._hist_ok(preds):
-            return False
+        if not isinstance(preds, Tensor) or not isinstance(target, Tensor) or not preds.is_floating_point():
+            return []
+        if preds.ndim != 2 or target.ndim != 1 or not ops.use_native(preds):
+            return []
+        curve = members.get(self.curve_name) if self.curve_name else None
+        if curve is not None and (preds.dtype not in eng.HIST_DTYPES or not curve._hist_ok(preds)):
+            curve = None
         confmats = [members[n] for n in self.confmat_names if n in members]
-        # validation: host-side shape checks per member; the target range check runs inside the fused kernel
-        # (device flag shared by every member's deferred sink, raised at compute) or eagerly on CPU.
-        from torchmetrics_forked_amd.functional.classification.precision_recall_curve import TARGET_RANGE_MSG
+        stats = [members[n] for n in self.stat_names if n in members and _stat_fusable(members[n])]
+        if len(confmats) + len(stats) + (curve is not None) < 2 or len(confmats) > 8 or len(stats) > 8:
+            return []
+        C = preds.shape[1]
+        if any(m.num_classes != C for m in confmats + stats):
+            return []
 
-        err = curve._validate_fused(preds, target)
+        from torchmetrics_forked_amd.functional.classification.precision_recall_curve import TARGET_RANGE_MSG
+        from torchmetrics_forked_amd.functional.classification.stat_scores import (
+            _TARGET_RANGE_MSG,
+            _multiclass_range_flags,
+            _multiclass_stat_scores_tensor_validation,
+        )
+
+        # validation: host-side shape checks per member; the target range check runs inside the fused pass (one
+        # device flag shared by every member's deferred sink, raised at compute) or eagerly on CPU
+        if curve is not None:
+            err = curve._validate_fused(preds, target)
+        else:
+            lead = (confmats + stats)[0]
+            err = _multiclass_range_flags(lead._validation_sink(target), preds)[0] if lead.validate_args else None
         for cm in confmats:
             cm._validate(preds, target, check_values=err is None)
-            if err is not None and cm.validate_args:
-                cm._validation_sink(target).attach(RuntimeError, TARGET_RANGE_MSG, err)
-        if len(confmats) == 1:
-            delta = confmats[0].confmat  # accumulate straight into the state
+        for st in stats:
+            if st.validate_args:
+                _multiclass_stat_scores_tensor_validation(
+                    preds, target, st.num_classes, "global", st.ignore_index, st._validation_sink(target), check_values=err is None
+                )
+        pending: List[Tuple[Tensor, Tensor]] = []
+        if err is not None:
+            for m, msg in [(cm, TARGET_RANGE_MSG) for cm in confmats] + [(st, _TARGET_RANGE_MSG) for st in stats]:
+                if not m.validate_args:
+                    continue
+                sink = m._validation_sink(target)
+                prev = sink._flags.get((RuntimeError, msg))
+                if prev is None:
+                    sink.attach(RuntimeError, msg, err)
+                elif prev is not err:
+                    pending.append((prev, err))
+
+        direct = len(confmats) == 1 and not stats
+        if direct:
+            delta, sums = confmats[0].confmat, None
         else:
-            delta = torch.zeros_like(confmats[0].confmat)
-        for m in [curve, *confmats]:
+            delta, sums = self._buffers(C, preds.device)
+        for m in ([curve] if curve is not None else []) + confmats + stats:
             m._computed = None
             m._update_count += 1
-        curve._curve_update(preds, target, confmat_out=delta, err_flag=err)
-        side = curve.__dict__.get("_side_event")
-        if side is not None:  # the side-stream class pass also adds rare rows into the confusion matrix
-            if len(confmats) > 1:
-                curve._join_side_work()
-            else:
-                confmats[0].__dict__["_side_event"] = side
-        if len(confmats) > 1:
-            for cm in confmats:
-                cm.confmat += delta
-        return True
+        if curve is not None:
+            curve._curve_update(preds, target, confmat_out=delta, err_flag=err)
+            side = curve.__dict__.get("_side_event")
+            if side is not None:  # the side-stream class pass also adds rare rows into the confusion matrix
+                if not direct:
+                    curve._join_side_work()
+                else:
+                    confmats[0].__dict__["_side_event"] = side
+        else:
+            from torchmetrics_forked_amd.ops import classification as cls_ops
+
+            ii = (confmats + stats)[0].ignore_index
+            cls_ops.mc_confmat_update(preds, target, delta, ii, err, None)
+        if not direct:
+            states: List[Tensor] = []
+            micro: List[int] = []
+            for st in stats:
+                tp, fp, tn, fn, is_micro = st._fold_states()
+                states += [tp, fp, tn, fn]
+                micro.append(int(is_micro))
+            torch.ops.tmx.confmat_fold(delta, [cm.confmat for cm in confmats], states, micro, sums)
+        # a member whose sink already held a range flag of its own gets the shared flag OR-ed in after the pass
+        for prev, e in pending:
+            prev.bitwise_or_(e)
+        updated = ([curve] if curve is not None else []) + confmats + stats
+        return [n for n, m in members.items() if any(m is u for u in updated)]
 
 
 def build_fused_plans(modules: Dict[str, Any]) -> List[Any]:
@@ -79,7 +151,8 @@ def build_fused_plans(modules: Dict[str, Any]) -> List[Any]:
         if key[0] != "multiclass_scores" or len(names) < 2:
             continue
         curves = [n for n in names if hasattr(modules[n], "_curve_update")]
-        confmats = [n for n in names if n not in curves and hasattr(modules[n], "confmat")]
-        if len(curves) >= 1 and confmats:
-            plans.append(_MulticlassScoresPlan([curves[0], *confmats], curves[0], confmats))
+        stats = [n for n in names if n not in curves and hasattr(modules[n], "_fold_states")]
+        confmats = [n for n in names if n not in curves and n not in stats and hasattr(modules[n], "confmat")]
+        if len(curves[:1]) + len(confmats) + len(stats) >= 2 and (confmats or stats):
+            plans.append(_MulticlassScoresPlan(curves[0] if curves else None, confmats, stats))
     return plans
