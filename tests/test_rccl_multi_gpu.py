@@ -201,6 +201,55 @@ def check_dtype_mismatch(rank, world, device):
     e.unsync()
 
 
+def check_sharded_retrieval(rank, world, device):
+    """Query-sharded retrieval (all_to_all of rows to the owning rank) equals the replicated computation and the
+    single-process computation over every rank's rows in rank order; the last rank holds no rows at all."""
+    import torchmetrics_forked_amd as tm
+
+    def rows(r):
+        g = torch.Generator().manual_seed(77 + r)
+        n = 0 if (r == world - 1 and world > 2) else 40 + 9 * r
+        idx = torch.randint(0, 11, (n,), generator=g)
+        preds = (torch.rand(n, generator=g) * 8).floor() / 8  # ties inside queries
+        target = (torch.rand(n, generator=g) < 0.3).long()
+        target[idx == 3] = 0  # query 3 has no positive document
+        return idx, preds, target
+
+    makers = [
+        lambda **kw: tm.RetrievalMAP(empty_target_action="skip", **kw),
+        lambda **kw: tm.RetrievalMRR(empty_target_action="pos", **kw),
+        lambda **kw: tm.RetrievalNormalizedDCG(top_k=3, **kw),
+        lambda **kw: tm.RetrievalPrecision(top_k=2, adaptive_k=True, **kw),
+        lambda **kw: tm.RetrievalPrecisionRecallCurve(**kw),
+        lambda **kw: tm.RetrievalFallOut(**kw),
+    ]
+    idx, preds, target = rows(rank)
+    all_rows = [rows(r) for r in range(world)]
+    for make in makers:
+        sharded, replicated, single = make(sharded_compute=True).to(device), make().to(device), make(sync_on_compute=False)
+        if idx.numel():
+            sharded.update(preds.to(device), target.to(device), indexes=idx.to(device))
+            replicated.update(preds.to(device), target.to(device), indexes=idx.to(device))
+        for i, p, t in all_rows:
+            if i.numel():
+                single.update(p, t, indexes=i)
+        a, b = sharded.compute(), replicated.compute()
+        c = single.compute()
+        a, b = (a if isinstance(a, tuple) else (a,)), (b if isinstance(b, tuple) else (b,))
+        c = c if isinstance(c, tuple) else (c,)
+        for x, y, z in zip(a, b, c):
+            torch.testing.assert_close(x.cpu().double(), y.cpu().double(), atol=1e-6, rtol=0)
+            torch.testing.assert_close(x.cpu().double(), z.double(), atol=1e-6, rtol=0)
+        # the local state is restored after compute (unsync)
+        assert sum(t.numel() for t in sharded.indexes) == idx.numel()
+    # "error" policy raises on every rank when any rank owns an empty query
+    err = tm.RetrievalMAP(empty_target_action="error", sharded_compute=True).to(device)
+    if idx.numel():
+        err.update(preds.to(device), target.to(device), indexes=idx.to(device))
+    with pytest.raises(ValueError, match="no positive target"):
+        err.compute()
+
+
 def check_timeout(rank, world, device):
     import time
 
@@ -231,7 +280,7 @@ def check_timeout(rank, world, device):
 
 
 CHECKS = [check_reductions, check_lists, check_sharded_auroc, check_narrowing, check_collection, check_async,
-          check_dtype_mismatch]
+          check_dtype_mismatch, check_sharded_retrieval]
 
 
 def _run_all(rank, world, device):
