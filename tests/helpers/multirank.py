@@ -33,6 +33,9 @@ def _entry(rank: int, fn: Callable, world: int, backend: str, port: int, outdir:
             torch.cuda.set_device(rank)
             device = torch.device("cuda", rank)
             dist.init_process_group("nccl", rank=rank, world_size=world, device_id=device)
+        elif backend == "gloo_cuda":  # gloo collectives (host), metric states on the one visible GPU
+            device = torch.device("cuda", 0)
+            dist.init_process_group("gloo", rank=rank, world_size=world)
         else:
             device = torch.device("cpu")
             dist.init_process_group("gloo", rank=rank, world_size=world)
