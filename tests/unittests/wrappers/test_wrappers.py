@@ -154,3 +154,39 @@ def test_running_is_wrapper():
     for v in (1.0, 2.0, 3.0):
         r.update(torch.tensor(v))
     assert float(r.compute()) == 5.0
+
+
+@pytest.mark.parametrize("strategy", ["poisson", "multinomial"])
+@pytest.mark.parametrize("make", [
+    lambda: tm.MeanSquaredError(),
+    lambda: tm.MeanSquaredError(num_outputs=3),
+    lambda: tm.MeanAbsoluteError(),
+    lambda: tm.MulticlassAccuracy(num_classes=5),
+    lambda: tm.MulticlassAccuracy(num_classes=5, average="micro"),
+    lambda: tm.MulticlassF1Score(num_classes=5, average="weighted", ignore_index=2),
+    lambda: tm.MulticlassPrecision(num_classes=5, average="none"),
+])
+def test_bootstrapper_weighted_path_matches_per_copy(strategy, make):
+    """The weighted fast path (one reduction over the [B, N] resample counts) equals resampling every copy."""
+    from torchmetrics_forked_amd.wrappers import bootstrapping as bsm
+
+    m0 = make()
+    if isinstance(m0, tm.MeanSquaredError) and m0.num_outputs == 3:
+        data = [(torch.randn(64, 3), torch.randn(64, 3)) for _ in range(3)]
+    elif isinstance(m0, (tm.MeanSquaredError, tm.MeanAbsoluteError)):
+        data = [(torch.randn(64, 2), torch.randn(64, 2)) for _ in range(3)]
+    else:
+        data = [(torch.randn(64, 5), torch.randint(0, 5, (64,))) for _ in range(3)]
+    torch.manual_seed(3)
+    fast = BootStrapper(make(), num_bootstraps=6, raw=True, sampling_strategy=strategy)
+    for p, t in data:
+        fast.update(p, t)
+    torch.manual_seed(3)
+    slow = BootStrapper(make(), num_bootstraps=6, raw=True, sampling_strategy=strategy)
+    for m in slow.metrics:  # force the per-copy path
+        m._bootstrap_deltas = None
+    for p, t in data:
+        slow.update(p, t)
+    torch.testing.assert_close(fast.compute()["raw"], slow.compute()["raw"], atol=1e-5, rtol=1e-5)
+    assert [int(m._update_count) for m in fast.metrics] == [int(m._update_count) for m in slow.metrics]
+    assert bsm is not None

@@ -3,7 +3,7 @@
 Global states are ``int64`` tensors reduced with ``"sum"`` (one coalesced RCCL all-reduce for all four);
 ``samplewise`` states are ``cat`` lists.  Updates run one fused HIP pass per batch (see functional module).
 """
-from typing import Any, Callable, List, Optional, Sequence, Tuple, Type, Union
+from typing import Any, Callable, Dict, List, Optional, Sequence, Tuple, Type, Union
 
 import torch
 from torch import Tensor
@@ -199,6 +199,34 @@ class MulticlassStatScores(_AbstractStatScores):
     def update(self, preds: Tensor, target: Tensor) -> None:
         if not self._fused_update(preds, target):
             self._update_state(*self._batch_stats(preds, target))
+
+    def _bootstrap_deltas(self, weights: Tensor, preds: Tensor, target: Tensor) -> Optional[Dict[str, Tensor]]:
+        """BootStrapper's weighted path: tp / fp / tn / fn increments of all B resamples at once from the
+        resample counts ``weights [B, N]`` -- three weighted scatters over the (target, argmax) pairs instead of B
+        resampled updates.  Global top-1 with ``[N, C]`` scores or ``[N]`` labels only (else None: per-copy path)."""
+        if self.multidim_average != "global" or self.top_k != 1 or target.ndim != 1 or preds.ndim not in (1, 2):
+            return None
+        C = self.num_classes
+        if self.validate_args:
+            _multiclass_stat_scores_tensor_validation(preds, target, C, "global", self.ignore_index)
+        p = preds.argmax(1) if preds.ndim == 2 else preds.long()
+        t = target.long()
+        w = weights.to(t.device, torch.float64)
+        keep = (t >= 0) & (t < C) & (p >= 0) & (p < C)
+        if self.ignore_index is not None:
+            keep &= t != self.ignore_index
+        w = w * keep.to(w.dtype)
+        tc, pc = t.clamp(0, C - 1), p.clamp(0, C - 1)
+        B = w.shape[0]
+        cnt_t = torch.zeros(B, C, dtype=w.dtype, device=w.device).index_add_(1, tc, w)
+        cnt_p = torch.zeros(B, C, dtype=w.dtype, device=w.device).index_add_(1, pc, w)
+        cnt_tp = torch.zeros(B, C, dtype=w.dtype, device=w.device).index_add_(1, tc, w * (tc == pc).to(w.dtype))
+        n = w.sum(1, keepdim=True)
+        tp, fp, fn = cnt_tp, cnt_p - cnt_tp, cnt_t - cnt_tp
+        tn = n - tp - fp - fn
+        if self.average == "micro":
+            tp, fp, fn, tn = tp.sum(1), fp.sum(1), fn.sum(1), tn.sum(1)
+        return {k: v.round().long() for k, v in (("tp", tp), ("fp", fp), ("tn", tn), ("fn", fn))}
 
     def _fusion_key(self) -> Optional[Tuple]:
         """Collection fusion (ops/fused.py): global top-1 stats derive from the shared argmax pair counts."""

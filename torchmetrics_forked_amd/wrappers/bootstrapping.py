@@ -1,9 +1,10 @@
 """Bootstrap confidence estimates (API parity: reference ``wrappers/bootstrapping.py:30-212``).
 
-Resampling indices for all bootstraps are drawn with the reference's sampler (same RNG stream, so seeded runs
-agree), moved to the metric's device once per update and applied with ``index_select`` on device."""
+Resamples are drawn with the reference's sampler calls (same RNG stream, so seeded runs agree) as one ``[B, N]``
+count matrix.  Sum-state base metrics take the weighted path (``Metric._bootstrap_deltas``: one weighted reduction
+for all B copies); the rest get one batched ``index_select`` and a per-copy update."""
 from copy import deepcopy
-from typing import Any, Dict, Optional, Sequence, Union
+from typing import Any, Dict, List, Optional, Sequence, Tuple, Union
 
 import torch
 from torch import Tensor
@@ -53,27 +54,78 @@ class BootStrapper(WrapperMetric):
             raise ValueError(f"Expected argument ``sampling_strategy`` to be one of {allowed} but received {sampling_strategy}")
         self.sampling_strategy = sampling_strategy
 
-    def _resampled(self, args: Any, kwargs: Any) -> Any:
-        """Yield ``(bootstrap index, resampled args, resampled kwargs)`` for every non-empty resample."""
+    def _batch_size(self, args: Any, kwargs: Any) -> int:
         args_sizes = apply_to_collection(args, Tensor, len)
         kwargs_sizes = list(apply_to_collection(kwargs, Tensor, len))
         if len(args_sizes) > 0:
-            size = args_sizes[0]
-        elif len(kwargs_sizes) > 0:
-            size = kwargs_sizes[0]
+            return args_sizes[0]
+        if len(kwargs_sizes) > 0:
+            return kwargs_sizes[0]
+        raise ValueError("None of the input contained tensors, so could not determine the sampling size")
+
+    def _resample_counts(self, size: int) -> Tuple[Tensor, Optional[List[Tensor]]]:
+        """``[B, N]`` int64 multiplicity of every sample in every bootstrap resample, drawn with exactly the
+        reference's per-bootstrap sampler calls (same RNG stream as ``num_bootstraps`` ``_bootstrap_sampler`` calls).
+        Multinomial resamples also keep their drawn index order (order-sensitive base metrics see the reference's
+        sequence); Poisson resamples are in sample order, as the reference's ``repeat_interleave`` produces them."""
+        rows, orders = [], []
+        for _ in range(self.num_bootstraps):
+            if self.sampling_strategy == "poisson":
+                rows.append(torch.distributions.Poisson(1).sample((size,)).long())
+            else:
+                idx = _bootstrap_sampler(size, "multinomial")
+                orders.append(idx)
+                rows.append(torch.bincount(idx, minlength=size))
+        counts = torch.stack(rows) if rows else torch.zeros(0, size, dtype=torch.long)
+        return counts, (orders if self.sampling_strategy == "multinomial" else None)
+
+    def _resampled(self, drawn: Tuple[Tensor, Optional[List[Tensor]]], args: Any, kwargs: Any) -> Any:
+        """Yield ``(bootstrap index, resampled args, resampled kwargs)`` for every non-empty resample.  All index
+        vectors go to the device in one copy, the inputs are gathered with one ``index_select`` each and split into
+        per-bootstrap views."""
+        counts, orders = drawn
+        size = counts.shape[1]
+        if orders is not None:
+            lengths = [o.numel() for o in orders]
+            idx = torch.cat(orders).to(self.device) if orders else torch.zeros(0, dtype=torch.long, device=self.device)
         else:
-            raise ValueError("None of the input contained tensors, so could not determine the sampling size")
-        for idx in range(self.num_bootstraps):
-            sample_idx = _bootstrap_sampler(size, sampling_strategy=self.sampling_strategy).to(self.device)
-            if sample_idx.numel() == 0:
+            cnt = counts.to(self.device)
+            lengths = cnt.sum(1).tolist()
+            idx = torch.arange(size, device=self.device).repeat(self.num_bootstraps).repeat_interleave(cnt.reshape(-1))
+        flat_args = apply_to_collection(args, Tensor, torch.index_select, dim=0, index=idx)
+        flat_kwargs = apply_to_collection(kwargs, Tensor, torch.index_select, dim=0, index=idx)
+        offsets = [0]
+        for n in lengths:
+            offsets.append(offsets[-1] + n)
+        for b in range(self.num_bootstraps):
+            if lengths[b] == 0:
                 continue
-            new_args = apply_to_collection(args, Tensor, torch.index_select, dim=0, index=sample_idx)
-            new_kwargs = apply_to_collection(kwargs, Tensor, torch.index_select, dim=0, index=sample_idx)
-            yield idx, new_args, new_kwargs
+            lo, hi = offsets[b], offsets[b + 1]
+            yield (b, apply_to_collection(flat_args, Tensor, lambda t: t[lo:hi]),
+                   apply_to_collection(flat_kwargs, Tensor, lambda t: t[lo:hi]))
 
     def update(self, *args: Any, **kwargs: Any) -> None:
-        for idx, new_args, new_kwargs in self._resampled(args, kwargs):
-            self.metrics[idx].update(*new_args, **new_kwargs)
+        """Weighted fast path: for sum-state base metrics that expose ``_bootstrap_deltas`` (MSE, MAE,
+        the multiclass stat-score family) every bootstrap's state increment is ``W @ per-sample contribution`` for
+        the ``[B, N]`` resample-count matrix ``W`` -- one GEMM / one weighted scatter for all copies, no resampled
+        copies of the inputs.  Other metrics are updated copy by copy on their resample (the reference algorithm)."""
+        drawn = self._resample_counts(self._batch_size(args, kwargs))
+        counts = drawn[0]
+        fast = getattr(self.metrics[0], "_bootstrap_deltas", None) if len(self.metrics) else None
+        deltas = fast(counts.to(self.device), *args, **kwargs) if fast is not None else None
+        if deltas is None:
+            for idx, new_args, new_kwargs in self._resampled(drawn, args, kwargs):
+                self.metrics[idx].update(*new_args, **new_kwargs)
+            return
+        nonempty = (counts.sum(1) > 0).tolist()
+        for b, m in enumerate(self.metrics):
+            if not nonempty[b]:
+                continue
+            for name, d in deltas.items():
+                cur = getattr(m, name)
+                setattr(m, name, cur + d[b].reshape(cur.shape).to(cur.dtype))
+            m._update_count += 1
+            m._computed = None
 
     def _summarize(self, vals: Tensor) -> Dict[str, Tensor]:
         out: Dict[str, Tensor] = {}
@@ -95,7 +147,8 @@ class BootStrapper(WrapperMetric):
 
         Each copy runs its own ``forward`` on its resample (one update per copy; the reference's generic
         full-state forward updates every copy twice and so double-counts the batch in the global state)."""
-        vals = [self.metrics[idx](*a, **k) for idx, a, k in self._resampled(args, kwargs)]
+        drawn = self._resample_counts(self._batch_size(args, kwargs))
+        vals = [self.metrics[idx](*a, **k) for idx, a, k in self._resampled(drawn, args, kwargs)]
         self._computed = None
         return self._summarize(torch.stack(vals, dim=0)) if vals else {}
 
