@@ -71,3 +71,33 @@ def test_bert_score_gpu_matches_cpu():
     gpu = bert_score(preds, target, model=model.cuda(), idf=True, device="cuda")
     for k in ("precision", "recall", "f1"):
         torch.testing.assert_close(gpu[k].cpu(), cpu[k], atol=1e-4, rtol=0)
+
+
+@pytest.mark.parametrize("max_len,vocab,n", [(20, 6, 500), (64, 3, 300), (65, 4, 200), (300, 5, 64), (1024, 8, 16), (200, 1000, 50)])
+def test_levenshtein_gpu_matches_host(max_len, vocab, n):
+    """One wave per pair, multi-word bit-parallel DP (csrc/text_gpu.hip) vs the host kernel (Myers / two-row DP)."""
+    from torchmetrics_forked_amd.functional.text.helper import _levenshtein_many
+
+    g = torch.Generator().manual_seed(max_len * 7 + vocab)
+    preds = [torch.randint(0, vocab, (int(torch.randint(0, max_len + 1, (1,), generator=g)),), generator=g).tolist() for _ in range(n)]
+    target = [torch.randint(0, vocab, (int(torch.randint(0, max_len + 1, (1,), generator=g)),), generator=g).tolist() for _ in range(n)]
+    target[0], preds[1] = [], []  # empty sides
+    host = _levenshtein_many(preds, target)
+    dev = _levenshtein_many(preds, target, torch.device("cuda"), force_gpu=True)
+    assert dev.is_cuda
+    assert torch.equal(dev.cpu(), host)
+
+
+def test_wer_family_gpu_states_large_batch_matches_cpu():
+    import torchmetrics_forked_amd.text as T
+
+    g = torch.Generator().manual_seed(0)
+    words = ["w%d" % i for i in range(30)]
+    mk = lambda k: " ".join(words[int(i)] for i in torch.randint(0, 30, (k,), generator=g))  # noqa: E731
+    preds = [mk(int(torch.randint(1, 90, (1,), generator=g))) for _ in range(3000)]
+    target = [mk(int(torch.randint(1, 90, (1,), generator=g))) for _ in range(3000)]
+    for cls in (T.WordErrorRate, T.CharErrorRate, T.MatchErrorRate, T.WordInfoLost, T.WordInfoPreserved):
+        gpu, cpu = cls().cuda(), cls()
+        gpu.update(preds, target)
+        cpu.update(preds, target)
+        torch.testing.assert_close(gpu.compute().cpu(), cpu.compute(), atol=1e-6, rtol=1e-6)

@@ -3,7 +3,7 @@
 Sentences are tokenised on the host and mapped to int64 ids with a per-call vocabulary, then packed as one flat
 buffer + offsets for the native string kernels in ``csrc/text.cpp`` (``tmx::levenshtein_batch`` and friends).
 """
-from typing import Dict, Hashable, Iterable, List, Sequence, Tuple, Union
+from typing import Dict, Hashable, Iterable, List, Optional, Sequence, Tuple, Union
 
 import torch
 from torch import Tensor
@@ -40,12 +40,31 @@ def _pack_codepoints(strings: Sequence[str]) -> Tuple[Tensor, Tensor]:
     return torch.tensor(flat, dtype=torch.long), torch.tensor(off, dtype=torch.long)
 
 
-def _levenshtein_many(preds: Sequence[Sequence[Hashable]], targets: Sequence[Sequence[Hashable]]) -> Tensor:
-    """Exact unit-cost edit distances for token-sequence pairs (int64 ``[n]``)."""
+# DP cells (prediction tokens x 64-token reference words) above which a GPU-resident metric scores the batch on the
+# device (csrc/text_gpu.hip); smaller batches are cheaper on the host than one H2D copy + launch
+GPU_LEVENSHTEIN_MIN_WORK = 1 << 16
+GPU_LEVENSHTEIN_MAX_REF = 1024
+
+
+def _levenshtein_many(
+    preds: Sequence[Sequence[Hashable]], targets: Sequence[Sequence[Hashable]], device: Optional[torch.device] = None,
+    force_gpu: Optional[bool] = None,
+) -> Tensor:
+    """Exact unit-cost edit distances for token-sequence pairs (int64 ``[n]``).
+
+    With a GPU ``device`` and enough work (or ``force_gpu``) the packed ids go to the device once and one wave per
+    pair runs the multi-word bit-parallel DP there (``tmx::levenshtein_gpu``), returning a device tensor; otherwise
+    the host kernel (``tmx::levenshtein_batch``, parallel over pairs) runs."""
     ops.require()
     vocab = _Vocab()
     a, a_off = _pack(preds, vocab)
     b, b_off = _pack(targets, vocab)
+    if device is not None and device.type == "cuda" and force_gpu is not False and len(targets):
+        max_ref = max(len(t) for t in targets)
+        work = sum(len(p) * ((len(t) + 63) // 64) for p, t in zip(preds, targets))
+        if max_ref <= GPU_LEVENSHTEIN_MAX_REF and (force_gpu or work >= GPU_LEVENSHTEIN_MIN_WORK):
+            d = [x.to(device, non_blocking=True) for x in (a, a_off, b, b_off)]
+            return torch.ops.tmx.levenshtein_gpu(*d, max_ref)
     return torch.ops.tmx.levenshtein_batch(a, a_off, b, b_off)
 
 

@@ -31,7 +31,7 @@ class _ErrorsOverTotal(Metric):
         self.add_state("total", tensor(0, dtype=torch.float), dist_reduce_fx="sum")
 
     def update(self, preds: Union[str, List[str]], target: Union[str, List[str]]) -> None:
-        errors, total = self._update_fn(preds, target)
+        errors, total = self._update_fn(preds, target, device=self.device)
         self.errors += errors.to(self.errors)
         self.total += total.to(self.total)
 
@@ -78,7 +78,7 @@ class _WordInfo(Metric):
         self.add_state("preds_total", tensor(0.0), dist_reduce_fx="sum")
 
     def update(self, preds: Union[str, List[str]], target: Union[str, List[str]]) -> None:
-        errors, target_total, preds_total = self._update_fn(preds, target)
+        errors, target_total, preds_total = self._update_fn(preds, target, device=self.device)
         self.errors += errors.to(self.errors)
         self.target_total += target_total.to(self.target_total)
         self.preds_total += preds_total.to(self.preds_total)
