@@ -162,3 +162,79 @@ class RefFn:
 
         mod = importlib.import_module(f"torchmetrics.functional.{self.domain}" if self.domain else "torchmetrics.functional")
         return getattr(mod, self.name)(p, t, **self.kwargs)
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# further MetricTester checks (reference ``tests/unittests/helpers/testers.py:285-317, 454-520``)
+# ---------------------------------------------------------------------------------------------------------------
+def run_precision_test(
+    preds: Tensor, target: Tensor, metric_class: Callable, metric_functional: Optional[Callable] = None,
+    metric_args: Optional[Dict[str, Any]] = None, dtype: torch.dtype = torch.half, device: str = "cpu", atol: float = 5e-2,
+) -> None:
+    """Reduced-precision inputs: module (``update`` over the batches + ``compute``) and functional run, give finite
+    results and agree with the fp32 run within ``atol``; the module's floating states may be ``set_dtype``-cast."""
+    metric_args = metric_args or {}
+
+    def cast(x: Tensor) -> Tensor:
+        return x.to(dtype) if x.is_floating_point() else x
+
+    ref_m = metric_class(**metric_args).to(device)
+    low_m = metric_class(**metric_args).to(device)
+    for i in range(len(preds)):
+        ref_m.update(preds[i].to(device), target[i].to(device))
+        low_m.update(cast(preds[i]).to(device), cast(target[i]).to(device))
+    ref, low = _to_cpu(ref_m.compute()), _to_cpu(low_m.compute())
+    assert_allclose(low, ref, atol)
+    if metric_functional is not None:
+        out = metric_functional(cast(preds[0]).to(device), cast(target[0]).to(device), **metric_args)
+        ref_f = metric_functional(preds[0].to(device), target[0].to(device), **metric_args)
+        assert_allclose(out, ref_f, atol)
+    # set_dtype casts every floating state (and default, so reset keeps it); updates then follow the reference's
+    # own promotion rules (e.g. Pearson's first batch mean takes the input dtype, as in the reference)
+    cast_m = metric_class(**metric_args).to(device).set_dtype(torch.float64)
+    for _ in range(2):
+        for name, v in cast_m.metric_state.items():
+            if isinstance(v, Tensor) and v.is_floating_point():
+                assert v.dtype == torch.float64, (name, v.dtype)
+        cast_m.update(preds[0].to(device), target[0].to(device))
+        cast_m.reset()
+
+
+def run_differentiability_test(
+    preds: Tensor, target: Tensor, metric_class: Callable, metric_functional: Optional[Callable] = None,
+    metric_args: Optional[Dict[str, Any]] = None,
+) -> None:
+    """``is_differentiable`` metrics propagate gradients to ``preds`` through ``forward`` and the functional; the
+    others return results that do not require grad (reference ``run_differentiability_test``)."""
+    metric_args = metric_args or {}
+    metric = metric_class(**metric_args)
+    p = preds[0].clone().to(torch.float64 if preds.is_floating_point() else preds.dtype)
+    if not p.is_floating_point():
+        return
+    p.requires_grad_(True)
+    out = metric(p, target[0])
+    outs = [o for o in (out.values() if isinstance(out, dict) else (out if isinstance(out, (list, tuple)) else [out]))
+            if isinstance(o, Tensor)]
+    if metric.is_differentiable:
+        assert any(o.requires_grad for o in outs), "is_differentiable metric returned no grad-carrying output"
+        total = sum(o.double().sum() for o in outs if o.requires_grad)
+        total.backward()
+        assert p.grad is not None and torch.isfinite(p.grad).all()
+        if metric_functional is not None:
+            q = p.detach().clone().requires_grad_(True)
+            metric_functional(q, target[0], **metric_args).double().sum().backward()
+            assert q.grad is not None
+    else:
+        assert not any(o.requires_grad for o in outs), "non-differentiable metric returned a grad-carrying output"
+
+
+def run_scriptable_test(metric_class: Callable, preds: Tensor, target: Tensor, metric_args: Optional[Dict[str, Any]] = None) -> None:
+    """``torch.jit.script`` succeeds on a fresh and on an updated module (the reference's ``check_scriptable``), and
+    scripting leaves the eager module's value unchanged."""
+    metric_args = metric_args or {}
+    torch.jit.script(metric_class(**metric_args))
+    eager = metric_class(**metric_args)
+    eager.update(preds[0], target[0])
+    before = _to_cpu(eager.compute())
+    torch.jit.script(eager)
+    assert_allclose(eager.compute(), before, 0.0)

@@ -69,7 +69,8 @@ class BinaryCalibrationError(_CalibrationBase):
         if self.validate_args:
             _binary_calibration_error_tensor_validation(preds, target, self.ignore_index, self._validation_sink(target))
         preds, target = binary_format(preds, target, 0.0, self.ignore_index, convert_to_labels=False)
-        _ce_bin_update(preds, target, self.n_bins, self.bins)
+        with torch.no_grad():
+            _ce_bin_update(preds, target, self.n_bins, self.bins)
 
 
 class MulticlassCalibrationError(_CalibrationBase):
@@ -112,10 +113,11 @@ class MulticlassCalibrationError(_CalibrationBase):
                 preds, target, self.num_classes, self.ignore_index, self._validation_sink(target)
             )
         preds, target = multiclass_format(preds, target, self.ignore_index, convert_to_labels=False)
-        if _multiclass_calibration_bins(preds, target, self.n_bins, self.bins):
-            return
-        conf, acc = _multiclass_calibration_error_update(preds, target)
-        _ce_bin_update(conf, acc, self.n_bins, self.bins)
+        with torch.no_grad():  # the reference bins under no_grad: the metric is not differentiable
+            if _multiclass_calibration_bins(preds, target, self.n_bins, self.bins):
+                return
+            conf, acc = _multiclass_calibration_error_update(preds, target)
+            _ce_bin_update(conf, acc, self.n_bins, self.bins)
 
 
 class CalibrationError(_ClassificationTaskWrapper):
