@@ -112,7 +112,7 @@ class MulticlassConfusionMatrix(_ConfmatPlot, Metric):
             )
 
     def update(self, preds: Tensor, target: Tensor) -> None:
-        if ops.use_native(target):
+        if ops.use_native(target) and self.confmat.dtype == torch.long:
             # straight into the state with the value checks as device flags: no [C, C] temporary, one kernel
             sink = self._validation_sink(target) if self.validate_args else None
             self._validate(preds, target, check_values=sink is None)

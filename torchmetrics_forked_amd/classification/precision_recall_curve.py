@@ -106,8 +106,8 @@ class _CurveMetric(Metric):
         """True when this batch takes a native pass that checks the target values itself (binned or exact
         histogram on the GPU): validation then skips its value-check kernels and hands over a device flag."""
         return ops.use_native(target) and (
-            self.thresholds is not None
-            or self._hist_ok(preds)
+            (self.thresholds is not None and self.confmat.dtype == torch.long)
+            or (self.thresholds is None and self._hist_ok(preds))
             or (self._task == "multiclass" and self._colmajor_ok(preds) and not (isinstance(self.score_hist, Tensor) and self.score_hist.numel() > 0))
         )
 
@@ -177,7 +177,7 @@ class _CurveMetric(Metric):
     ) -> None:
         thr = self.thresholds
         ii = self.ignore_index
-        if thr is not None and ops.use_native(target):
+        if thr is not None and ops.use_native(target) and self.confmat.dtype == torch.long:
             # straight into the [T, (C,) 2, 2] state, value check folded into the histogram pass
             if self._task == "binary":
                 p, t, cm = preds.reshape(-1, 1, 1), target.reshape(-1, 1, 1), self.confmat.view(len(thr), 1, 2, 2)

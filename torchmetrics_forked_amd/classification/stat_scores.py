@@ -52,6 +52,11 @@ class _AbstractStatScores(Metric):
             else:
                 self.add_state(name, torch.zeros(size, dtype=torch.long), dist_reduce_fx="sum")
 
+    def _int64_states(self) -> bool:
+        """The native kernels count into int64 states; after ``set_dtype`` (which, as in the reference, casts every
+        state) the generic update path takes over."""
+        return all(isinstance(getattr(self, n), Tensor) and getattr(self, n).dtype == torch.long for n in ("tp", "fp", "tn", "fn"))
+
     def _scratch(self, numel: int, device: torch.device) -> Tensor:
         """Zero int64 scratch of the fused GPU kernels (left at zero by every launch; not a metric state)."""
         buf = getattr(self, "_ticket", None)
@@ -62,7 +67,7 @@ class _AbstractStatScores(Metric):
     def _binary_fused_update(self, preds: Tensor, target: Tensor, num_labels: int, validate: Callable) -> bool:
         """GPU fast path for global binary / multilabel stats: one kernel, counts straight into the states, value
         checks as device flags (csrc/classification.hip ``binary_stats_fused``)."""
-        if self.multidim_average != "global" or not ops.use_native(target):
+        if self.multidim_average != "global" or not ops.use_native(target) or not self._int64_states():
             return False
         sink = self._validation_sink(target) if self.validate_args else None
         if self.validate_args:
@@ -181,7 +186,7 @@ class MulticlassStatScores(_AbstractStatScores):
         """GPU fast path for global top-1 stats: validation shape checks on the host, value checks as device flags
         and the counts straight into the states -- one kernel per update instead of a [C, C] temporary plus ~25
         small kernels (csrc/classification.hip ``mc_stat_scores_update``)."""
-        if self.multidim_average != "global" or self.top_k != 1 or not ops.use_native(target):
+        if self.multidim_average != "global" or self.top_k != 1 or not ops.use_native(target) or not self._int64_states():
             return False
         sink = self._validation_sink(target) if self.validate_args else None
         if self.validate_args:
