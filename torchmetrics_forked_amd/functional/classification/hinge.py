@@ -76,6 +76,10 @@ def _multiclass_hinge_loss_tensor_validation(preds: Tensor, target: Tensor, num_
 def _multiclass_hinge_loss_update(
     preds: Tensor, target: Tensor, squared: bool, multiclass_mode: str = "crammer-singer"
 ) -> Tuple[Tensor, Tensor]:
+    if preds.ndim == 2 and cls_ops.row_kernel_ok(preds, preds.shape[1]):
+        # csrc/rowwise.hip: one wave per row (device softmax decision, margins, clamp, square, fixed-order sums)
+        measures = cls_ops.mc_hinge(preds, target, squared, multiclass_mode != "crammer-singer").to(preds.dtype)
+        return measures, torch.tensor(preds.shape[0], device=preds.device)
     flag = cls_ops.range_flag(preds).bool()
     preds = torch.where(flag, preds.softmax(1), preds)
     onehot = to_onehot(target, max(2, preds.shape[1])).bool()

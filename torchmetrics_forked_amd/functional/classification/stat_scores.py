@@ -321,8 +321,17 @@ def _multiclass_onehot_stats(
     multidim_average: str,
     ignore_index: Optional[int],
 ) -> Tuple[Tensor, Tensor, Tensor, Tensor]:
-    """Samplewise / top-k path: one-hot compare (reference stat_scores.py:363-393 semantics)."""
-    ignore_in = ignore_index is not None and 0 <= ignore_index <= num_classes - 1
+    """Samplewise / top-k path: one-hot compare (reference stat_scores.py:363-393 semantics).
+
+    GPU rows take ``csrc/rowwise.hip`` (k wave arg-max rounds per row, counts straight into the states): scores
+    ``[N, C, X]`` are read as ``N * X`` rows of ``C``; label predictions ``[N, X]`` as ``N * X`` single picks."""
+    if top_k > 1 and preds.ndim == 3 and cls_ops.row_kernel_ok(preds, num_classes):
+        n, c, x = preds.shape
+        rows = preds.movedim(1, -1).reshape(n * x, c) if x > 1 else preds.reshape(n, c)
+        return cls_ops.topk_stats(rows, None, target, num_classes, top_k, ignore_index, n, multidim_average == "samplewise")
+    if top_k == 1 and not preds.is_floating_point() and preds.shape == target.shape and ops.use_native(target):
+        return cls_ops.topk_stats(None, preds, target, num_classes, 1, ignore_index, preds.shape[0], multidim_average == "samplewise")
+    ignore_in =ignore_index is not None and 0 <= ignore_index <= num_classes - 1
     ignore_out = ignore_index is not None and not ignore_in
     if ignore_out:
         mask = target == ignore_index

@@ -8,6 +8,7 @@ from typing import Tuple
 import torch
 from torch import Tensor
 
+from torchmetrics_forked_amd import ops
 from torchmetrics_forked_amd.functional.regression._common import _check_data_shape_to_num_outputs
 from torchmetrics_forked_amd.utilities.checks import _check_same_shape
 
@@ -28,6 +29,9 @@ def _rank_data(data: Tensor) -> Tensor:
     if n == 0:
         return data.clone()
     srt, idx = data.sort()
+    if data.is_cuda and data.dtype in (torch.float32, torch.float64) and ops.use_native(data):
+        # csrc/rank.hip: each sorted position finds its tie run by binary search and writes the run's average rank
+        return torch.ops.tmx.rank_average(srt.reshape(1, -1), idx.reshape(1, -1)).reshape(data.shape)
     new = torch.ones(n, dtype=torch.bool, device=data.device)
     new[1:] = srt[1:] != srt[:-1]
     gid = torch.cumsum(new, 0) - 1
@@ -37,6 +41,12 @@ def _rank_data(data: Tensor) -> Tensor:
     rank = torch.empty_like(data)
     rank[idx] = avg[gid]
     return rank
+
+
+def _rank_columns(data: Tensor) -> Tensor:
+    """Average ranks of every column of a GPU ``[n, D]`` tensor: one batched sort + one rank kernel launch."""
+    srt, idx = data.t().contiguous().sort(dim=1)
+    return torch.ops.tmx.rank_average(srt, idx.contiguous()).t()
 
 
 def _spearman_corrcoef_update(preds: Tensor, target: Tensor, num_outputs: int) -> Tuple[Tensor, Tensor]:
@@ -53,6 +63,8 @@ def _spearman_corrcoef_update(preds: Tensor, target: Tensor, num_outputs: int) -
 def _spearman_corrcoef_compute(preds: Tensor, target: Tensor, eps: float = 1e-6) -> Tensor:
     if preds.ndim == 1:
         preds, target = _rank_data(preds), _rank_data(target)
+    elif preds.is_cuda and preds.dtype in (torch.float32, torch.float64) and ops.use_native(preds):
+        preds, target = _rank_columns(preds), _rank_columns(target)
     else:
         preds = torch.stack([_rank_data(p) for p in preds.T]).T
         target = torch.stack([_rank_data(t) for t in target.T]).T

@@ -355,3 +355,62 @@ def softmax_colmajor(rows: Tensor, target: Optional[Tensor] = None, err_flag: Op
     batch is outside [0, 1] (the reference's rule), in one pass that also transposes (csrc/curve_anchor.hip).
     With ``target`` and ``err_flag`` the pass also ORs "a target outside [0, C)" into the flag."""
     return torch.ops.tmx.softmax_colmajor(rows, target, err_flag)
+
+
+# ---------------------------------------------------------------------------------------------- csrc/rowwise.hip
+ROW_MAX_CLASSES = 2048  # one wave per row, the row held in registers (64 lanes x 32 values)
+_ROW_DTYPES = (torch.float32, torch.bfloat16, torch.float16)  # fp64 would be narrowed to fp32 compares: eager path
+
+
+def row_kernel_ok(x: Tensor, width: int) -> bool:
+    """True when a GPU tensor of rows of ``width`` scores can take the register-resident row kernels."""
+    return ops.use_native(x) and x.dtype in _ROW_DTYPES and 1 <= width <= ROW_MAX_CLASSES
+
+
+def topk_stats(
+    scores: Optional[Tensor],
+    labels: Optional[Tensor],
+    target: Tensor,
+    num_classes: int,
+    top_k: int,
+    ignore_index: Optional[int],
+    samples: int,
+    samplewise: bool,
+) -> Tuple[Tensor, Tensor, Tensor, Tensor]:
+    """Multiclass ``(tp, fp, tn, fn)`` of top-k picks (or label predictions) for GPU rows, one wave per row.
+
+    ``scores`` [M, C] (or ``labels`` [M] with ``top_k == 1``), ``target`` [M]; rows ``s * X .. (s + 1) * X - 1``
+    belong to sample ``s`` (``M = samples * X``).  Results are ``[C]`` (global) or ``[samples, C]`` (samplewise)."""
+    t = target.reshape(-1).long().contiguous()
+    m = t.numel()
+    x = max(1, m // max(1, samples)) if samplewise else 1
+    tp, fp, fn, nvalid = torch.ops.tmx.topk_stats(
+        scores.contiguous() if scores is not None else t,
+        labels.reshape(-1).long().contiguous() if labels is not None else None,
+        t,
+        int(num_classes),
+        int(top_k),
+        int(ignore_index) if ignore_index is not None else 0,
+        ignore_index is not None,
+        int(x),
+        bool(samplewise),
+    )
+    tn = (nvalid.unsqueeze(-1) if samplewise else nvalid) - tp - fp - fn
+    return tp, fp, tn, fn
+
+
+def mc_hinge(preds: Tensor, target: Tensor, squared: bool, one_vs_all: bool) -> Tensor:
+    """Sum over rows of the multiclass hinge measures (fp32; ``[]`` crammer-singer, ``[C]`` one-vs-all), with the
+    reference's per-batch softmax rule decided on the device."""
+    flag = torch.ops.tmx.range_flag(preds)
+    return torch.ops.tmx.mc_hinge(preds.contiguous(), target.long().contiguous(), flag, bool(squared), bool(one_vs_all))
+
+
+def ml_ranking(preds: Tensor, target: Tensor, kind: int) -> Tuple[Tensor, Optional[Tensor]]:
+    """Per-row fp32 values of a multilabel ranking metric (kind 0 coverage, 1 LRAP, 2 ranking loss) and, for the loss,
+    an int32 flag "some row was not degenerate"."""
+    p = preds.contiguous()
+    shift = (p.min().abs() + 10).float().reshape(1) if kind == 0 else None
+    flag = torch.zeros(1, dtype=torch.int32, device=p.device) if kind == 2 else None
+    out = torch.ops.tmx.ml_ranking(p, target.long().contiguous(), int(kind), shift, flag)
+    return out, flag
