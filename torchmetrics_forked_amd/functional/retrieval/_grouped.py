@@ -16,6 +16,8 @@ from typing import Optional, Tuple
 import torch
 from torch import Tensor
 
+from torchmetrics_forked_amd import ops
+
 
 class Grouped:
     """Queries laid out contiguously, documents sorted by descending score within each query."""
@@ -63,12 +65,43 @@ class Grouped:
     def in_top(self, k: Tensor) -> Tensor:
         return self.pos < k[self.gid]
 
+    # ---------------------------------------------------------------------------------------- native path
+    def stats(self, top_k: Optional[int], adaptive: bool = False, ideal: Optional[Tensor] = None) -> Optional[Tensor]:
+        """fp64 ``[Q, 10]`` per-query statistics from ``csrc/retrieval.hip`` (one wave per query): (rel_total,
+        neg_total, rel_in_k, neg_in_k, ap_sum, first_rel, rel_in_R, dcg, idcg, k); ``None`` off the GPU."""
+        p, t = self.preds, self.target
+        if not (p.is_cuda and p.dtype in (torch.float32, torch.float64) and ops.use_native(p)):
+            return None
+        if t.dtype not in (torch.float32, torch.float64, torch.int64, torch.int32):
+            t = t.float() if t.is_floating_point() else t.long()
+        ideal = t if ideal is None else ideal.to(t.dtype).contiguous()
+        key = (p.device, self.n)
+        dtab = _DTAB.get(key)
+        if dtab is None:
+            disc = 1.0 / torch.log2(torch.arange(self.n, dtype=torch.float64, device=p.device) + 2.0)
+            dtab = torch.cat([torch.zeros(1, dtype=torch.float64, device=p.device), torch.cumsum(disc, 0)])
+            _DTAB.clear()
+            _DTAB[key] = dtab
+        return torch.ops.tmx.retrieval_segments(
+            p.contiguous(), t.contiguous(), ideal, self.start, self.sizes, -1 if top_k is None else int(top_k), bool(adaptive), dtab
+        )
+
+
+_DTAB: dict = {}  # discount prefix table of the last (device, length)
+
+
+def _safe_div(num: Tensor, den: Tensor) -> Tensor:
+    return torch.where(den > 0, num / den.clamp(min=1e-300), torch.zeros_like(num)).float()
+
 
 def _binary(target: Tensor) -> Tensor:
     return (target > 0).to(torch.float32)
 
 
 def per_query_average_precision(g: Grouped, top_k: Optional[int]) -> Tensor:
+    st = g.stats(top_k)
+    if st is not None:
+        return _safe_div(st[:, 4], st[:, 2])
     rel = _binary(g.target) * g.in_top(g.k_per_query(top_k)).float()
     cum = g.seg_cumsum(rel)
     contrib = torch.where(rel > 0, cum / (g.pos + 1).float(), torch.zeros_like(cum))
@@ -77,6 +110,9 @@ def per_query_average_precision(g: Grouped, top_k: Optional[int]) -> Tensor:
 
 
 def per_query_reciprocal_rank(g: Grouped, top_k: Optional[int]) -> Tensor:
+    st = g.stats(top_k)
+    if st is not None:
+        return torch.where(st[:, 5] >= 0, 1.0 / (st[:, 5] + 1.0), torch.zeros_like(st[:, 5])).float()
     rel = (g.target > 0) & g.in_top(g.k_per_query(top_k))
     big = torch.full_like(g.pos, g.n + 1)
     first = torch.full((g.Q,), g.n + 1, dtype=torch.long, device=g.pos.device)
@@ -90,6 +126,9 @@ def per_query_relevant_in_top(g: Grouped, k: Tensor, negatives: bool = False) ->
 
 
 def per_query_precision(g: Grouped, top_k: Optional[int], adaptive_k: bool) -> Tensor:
+    st = g.stats(top_k, adaptive=adaptive_k)
+    if st is not None:
+        return torch.where(st[:, 0] > 0, st[:, 2] / st[:, 9].clamp(min=1), torch.zeros_like(st[:, 2])).float()
     k = g.k_per_query(top_k, adaptive=adaptive_k)
     rel = per_query_relevant_in_top(g, k)
     total = g.seg_sum(_binary(g.target))
@@ -97,22 +136,34 @@ def per_query_precision(g: Grouped, top_k: Optional[int], adaptive_k: bool) -> T
 
 
 def per_query_recall(g: Grouped, top_k: Optional[int]) -> Tensor:
+    st = g.stats(top_k)
+    if st is not None:
+        return _safe_div(st[:, 2], st[:, 0])
     rel = per_query_relevant_in_top(g, g.k_per_query(top_k))
     total = g.seg_sum(_binary(g.target))
     return torch.where(total > 0, rel / total.clamp(min=1), torch.zeros_like(rel))
 
 
 def per_query_fall_out(g: Grouped, top_k: Optional[int]) -> Tensor:
+    st = g.stats(top_k)
+    if st is not None:
+        return _safe_div(st[:, 3], st[:, 1])
     neg = per_query_relevant_in_top(g, g.k_per_query(top_k), negatives=True)
     total = g.seg_sum((g.target <= 0).float())
     return torch.where(total > 0, neg / total.clamp(min=1), torch.zeros_like(neg))
 
 
 def per_query_hit_rate(g: Grouped, top_k: Optional[int]) -> Tensor:
+    st = g.stats(top_k)
+    if st is not None:
+        return (st[:, 2] > 0).float()
     return (per_query_relevant_in_top(g, g.k_per_query(top_k)) > 0).float()
 
 
 def per_query_r_precision(g: Grouped) -> Tensor:
+    st = g.stats(None)
+    if st is not None:
+        return _safe_div(st[:, 6], st[:, 0])
     total = g.seg_sum(_binary(g.target))
     rel = per_query_relevant_in_top(g, total.long())
     return torch.where(total > 0, rel / total.clamp(min=1), torch.zeros_like(rel))
@@ -124,8 +175,12 @@ def _discount(pos: Tensor, k: Tensor) -> Tensor:
 
 
 def per_query_ndcg(g: Grouped, top_k: Optional[int]) -> Tensor:
-    k = g.k_per_query(top_k)[g.gid]
     target = g.target.float()
+    if g.preds.is_cuda and g.preds.dtype in (torch.float32, torch.float64) and ops.use_native(g.preds):
+        ideal_t = Grouped(target, target, g.gid if g.Q > 1 else None, sort_key=target).target
+        st = g.stats(top_k, ideal=ideal_t)
+        return torch.where(st[:, 8] == 0, torch.zeros_like(st[:, 7]), st[:, 7] / torch.where(st[:, 8] == 0, torch.ones_like(st[:, 8]), st[:, 8])).float()
+    k = g.k_per_query(top_k)[g.gid]
     # tie-averaged DCG: documents with equal score inside a query share the mean gain over their positions
     new = torch.ones(g.n, dtype=torch.bool, device=target.device)
     new[1:] = (g.gid[1:] != g.gid[:-1]) | (g.preds[1:] != g.preds[:-1])
