@@ -13,6 +13,8 @@
 // Grid: (Lr / 64, Lp / 64, B) — tens of thousands of blocks for the BASELINE shape (B = 1024, L = 512).
 #include "common.h"
 
+#include <cstdlib>
+
 namespace tmx {
 
 constexpr int kBsTile = 64;
@@ -287,6 +289,135 @@ __global__ __launch_bounds__(kTThreads) void greedy_match_tiled_kernel(const T* 
   }
 }
 
+// ------------------------------------------------------------------------------------ 256 x 256 MFMA path
+// Same pipeline as the 128 x 128 tile, twice the edge: 8 waves as 4 (M) x 2 (N), each owning a 64 x 128 block
+// (4 x 8 MFMA 16x16x32 tiles, 128 accumulator registers), so a 32-deep K step issues 32 MFMAs per 12 ds_read_b128
+// (2.7 MFMA per LDS read vs 2.0) and every block streams half the L2 bytes per FLOP.  Double-buffered 64-wide K
+// slices with padded rows: 2 x (256 + 256) x 72 x 2 B = 144 KiB of the 160 KiB LDS, one block per CU.
+constexpr int kW = 256;
+constexpr int kWThreads = 512;
+
+template <typename T>
+__global__ __launch_bounds__(kWThreads) void greedy_match_w256_kernel(const T* __restrict__ P, const T* __restrict__ R, int64_t B, int64_t Lp,
+                                                                      int64_t Lr, int64_t D, int tiles_m, int tiles_n,
+                                                                      int* __restrict__ rowmax, int* __restrict__ colmax) {
+  __shared__ __attribute__((aligned(16))) short lds[2][2][kW * kTLd];  // [buffer][A|B][row * kTLd + k]
+  const int64_t nwg = static_cast<int64_t>(gridDim.x);
+  const int64_t orig = blockIdx.x, xcd = orig % 8, q = nwg / 8, rr = nwg % 8;
+  const int64_t id = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
+  const int64_t per_pair = static_cast<int64_t>(tiles_m) * tiles_n;
+  const int64_t b = id / per_pair;
+  const int tm = static_cast<int>((id % per_pair) / tiles_n), tn = static_cast<int>(id % tiles_n);
+  if (b >= B) return;
+  const T* Pb = P + b * Lp * D;
+  const T* Rb = R + b * Lr * D;
+  const int64_t row0 = static_cast<int64_t>(tm) * kW, col0 = static_cast<int64_t>(tn) * kW;
+  const int tid = threadIdx.x, wave = tid / kWave, lane = tid % kWave;
+  const int wr = wave >> 1, wc = wave & 1;
+
+  // global -> register staging: chunk c = tid + 512 i (i < 4) of a 256 x 64 slice: row c / 8, 16-B column c % 8
+  bs_frag8 ra[4], rb[4];
+  auto load_slice = [&](int64_t k0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = tid + kWThreads * i;
+      const int r = c >> 3, kk = (c & 7) * 8;
+      const int64_t k = k0 + kk;
+      ra[i] = (row0 + r < Lp && k < D) ? *reinterpret_cast<const bs_frag8*>(Pb + (row0 + r) * D + k) : bs_frag8{0, 0, 0, 0, 0, 0, 0, 0};
+      rb[i] = (col0 + r < Lr && k < D) ? *reinterpret_cast<const bs_frag8*>(Rb + (col0 + r) * D + k) : bs_frag8{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+  };
+  auto store_slice = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = tid + kWThreads * i;
+      const int r = c >> 3, kk = (c & 7) * 8;
+      *reinterpret_cast<bs_frag8*>(&lds[buf][0][r * kTLd + kk]) = ra[i];
+      *reinterpret_cast<bs_frag8*>(&lds[buf][1][r * kTLd + kk]) = rb[i];
+    }
+  };
+
+  bs_acc4 acc[4][8];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = bs_acc4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = static_cast<int>((D + kTK - 1) / kTK);
+  load_slice(0);
+  store_slice(0);
+  __syncthreads();
+  const int fr = lane & 15, fk = 8 * (lane >> 4);
+  for (int s = 0; s < nk; ++s) {
+    const int buf = s & 1;
+    if (s + 1 < nk) load_slice(static_cast<int64_t>(s + 1) * kTK);  // in flight during this slice's MFMAs
+    const short* A = lds[buf][0];
+    const short* Bt = lds[buf][1];
+#pragma unroll
+    for (int kh = 0; kh < kTK; kh += 32) {
+      bs_frag8 af[4], bf[8];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const bs_frag8*>(A + (wr * 64 + 16 * i + fr) * kTLd + kh + fk);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) bf[j] = *reinterpret_cast<const bs_frag8*>(Bt + (wc * 128 + 16 * j + fr) * kTLd + kh + fk);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i][j] = mfma16<T>(af[i], bf[j], acc[i][j]);
+    }
+    if (s + 1 < nk) store_slice(buf ^ 1);  // the other buffer was last read one slice ago, before the previous barrier
+    __syncthreads();
+  }
+
+  int* rmax = rowmax + b * Lp;
+  int* cmax = colmax + b * Lr;
+  const int64_t wrow0 = row0 + wr * 64, wcol0 = col0 + wc * 128;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float v = -INFINITY;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int64_t col = wcol0 + 16 * j + fr;
+        if (col < Lr) v = fmaxf(v, acc[i][j][r]);
+      }
+#pragma unroll
+      for (int off = 8; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, kWave));
+      const int64_t row = wrow0 + 16 * i + (lane >> 4) * 4 + r;
+      if (fr == 0 && row < Lp && v > -INFINITY) atomicMax(rmax + row, ordered_bits(v));
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    float v = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t row = wrow0 + 16 * i + (lane >> 4) * 4 + r;
+        if (row < Lp) v = fmaxf(v, acc[i][j][r]);
+      }
+    v = fmaxf(v, __shfl_xor(v, 16, kWave));
+    v = fmaxf(v, __shfl_xor(v, 32, kWave));
+    const int64_t col = wcol0 + 16 * j + fr;
+    if (lane < 16 && col < Lr && v > -INFINITY) atomicMax(cmax + col, ordered_bits(v));
+  }
+}
+
+// one launch fills both maxima with the ordered encoding of -inf; one launch decodes both in place to fp32 bits
+__global__ void bs_fill_kernel(int* __restrict__ a, int64_t na, int* __restrict__ b, int64_t nb, int v) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < na + nb; i += (int64_t)gridDim.x * blockDim.x)
+    (i < na ? a[i] : b[i - na]) = v;
+}
+__global__ void bs_decode_kernel(int* __restrict__ a, int64_t na, int* __restrict__ b, int64_t nb) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < na + nb; i += (int64_t)gridDim.x * blockDim.x) {
+    int* p = i < na ? a + i : b + (i - na);
+    const int x = *p;
+    *p = x >= 0 ? x : x ^ 0x7fffffff;
+  }
+}
+
 // P [B, Lp, D], R [B, Lr, D] (same float dtype) -> (rowmax [B, Lp] fp32, colmax [B, Lr] fp32)
 std::tuple<at::Tensor, at::Tensor> bert_greedy_match(const at::Tensor& P_in, const at::Tensor& R_in) {
   TORCH_CHECK(P_in.is_cuda() && R_in.is_cuda(), "bert_greedy_match: expected GPU tensors");
@@ -300,16 +431,37 @@ std::tuple<at::Tensor, at::Tensor> bert_greedy_match(const at::Tensor& P_in, con
   auto opts = P.options().dtype(at::kInt);
   // order-preserving encoding of -inf as the identity of max
   const int neg_inf_bits = static_cast<int>(0xff800000u ^ 0x7fffffffu);
-  auto rowmax = at::full({B, Lp}, neg_inf_bits, opts);
-  auto colmax = at::full({B, Lr}, neg_inf_bits, opts);
+  auto rowmax = at::empty({B, Lp}, opts);
+  auto colmax = at::empty({B, Lr}, opts);
   if (B == 0 || Lp == 0 || Lr == 0) {
     return {rowmax.to(at::kFloat).fill_(-INFINITY), colmax.to(at::kFloat).fill_(-INFINITY)};
   }
+  const int64_t n_fill = B * (Lp + Lr);
+  hipLaunchKernelGGL(bs_fill_kernel, grid_for(n_fill, 256), 256, 0, stream(), rowmax.data_ptr<int>(), B * Lp, colmax.data_ptr<int>(),
+                     B * Lr, neg_inf_bits);
+  TMX_LAUNCH_CHECK();
   dim3 grid(static_cast<unsigned>((Lr + kBsTile - 1) / kBsTile), static_cast<unsigned>((Lp + kBsTile - 1) / kBsTile),
             static_cast<unsigned>(B));
   const bool tiled = (P.scalar_type() == at::kBFloat16 || P.scalar_type() == at::kHalf) && D % 8 == 0 &&
                      (reinterpret_cast<uintptr_t>(P.data_ptr()) & 15) == 0 && (reinterpret_cast<uintptr_t>(R.data_ptr()) & 15) == 0;
-  if (tiled) {
+  // 256-wide tiles when they waste little of the pair (<= 25 % padding); else the 128-wide tile
+  const int64_t wm = (Lp + kW - 1) / kW, wn = (Lr + kW - 1) / kW;
+  const bool wide = tiled && Lp >= kW && Lr >= kW && 4 * wm * wn * kW * kW <= 5 * Lp * Lr &&
+                    std::getenv("TMX_BERT_TILE128") == nullptr;
+  if (wide) {
+    const int64_t nblocks = B * wm * wn;
+    TORCH_CHECK(nblocks < (1ll << 31), "bert_greedy_match: too many tiles");
+    if (P.scalar_type() == at::kBFloat16) {
+      greedy_match_w256_kernel<__hip_bfloat16><<<static_cast<unsigned>(nblocks), kWThreads, 0, stream()>>>(
+          reinterpret_cast<const __hip_bfloat16*>(P.data_ptr()), reinterpret_cast<const __hip_bfloat16*>(R.data_ptr()), B, Lp, Lr, D,
+          static_cast<int>(wm), static_cast<int>(wn), rowmax.data_ptr<int>(), colmax.data_ptr<int>());
+    } else {
+      greedy_match_w256_kernel<__half><<<static_cast<unsigned>(nblocks), kWThreads, 0, stream()>>>(
+          reinterpret_cast<const __half*>(P.data_ptr()), reinterpret_cast<const __half*>(R.data_ptr()), B, Lp, Lr, D, static_cast<int>(wm),
+          static_cast<int>(wn), rowmax.data_ptr<int>(), colmax.data_ptr<int>());
+    }
+    TMX_LAUNCH_CHECK();
+  } else if (tiled) {
     const int tiles_m = static_cast<int>((Lp + kT - 1) / kT), tiles_n = static_cast<int>((Lr + kT - 1) / kT);
     const int64_t nblocks = B * tiles_m * tiles_n;
     TORCH_CHECK(nblocks < (1ll << 31), "bert_greedy_match: too many tiles");
@@ -341,13 +493,10 @@ std::tuple<at::Tensor, at::Tensor> bert_greedy_match(const at::Tensor& P_in, con
       TORCH_CHECK(false, "bert_greedy_match: unsupported dtype ", P.scalar_type());
   }
   TMX_LAUNCH_CHECK();
-  // decode the ordered integers back to floats (elementwise, on device)
-  auto decode = [](const at::Tensor& bits) {
-    auto neg = bits.lt(0);
-    auto raw = at::where(neg, at::bitwise_xor(bits, 0x7fffffff), bits);
-    return raw.view(at::kFloat);
-  };
-  return {decode(rowmax), decode(colmax)};
+  // decode the ordered integers back to fp32 bits in place (one launch for both)
+  hipLaunchKernelGGL(bs_decode_kernel, grid_for(n_fill, 256), 256, 0, stream(), rowmax.data_ptr<int>(), B * Lp, colmax.data_ptr<int>(), B * Lr);
+  TMX_LAUNCH_CHECK();
+  return {rowmax.view(at::kFloat), colmax.view(at::kFloat)};
 }
 
 }  // namespace tmx

@@ -38,7 +38,7 @@ def test_perplexity_gpu_matches_cpu():
                                atol=1e-4, rtol=1e-5)
 
 
-@pytest.mark.parametrize("shape", [(3, 40, 50, 32), (2, 128, 64, 768), (5, 17, 33, 24), (64, 512, 512, 768), (2, 300, 129, 72), (2, 130, 257, 20)])
+@pytest.mark.parametrize("shape", [(3, 40, 50, 32), (2, 1000, 1024, 40), (1, 256, 768, 776), (3, 512, 512, 64), (2, 128, 64, 768), (5, 17, 33, 24), (64, 512, 512, 768), (2, 300, 129, 72), (2, 130, 257, 20)])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
 def test_bert_greedy_match_kernel(shape, dtype):
     b, lp, lr, d = shape
