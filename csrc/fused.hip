@@ -9,14 +9,15 @@
 //   * StatScores-family members (Accuracy, Precision, Recall, F-beta, Specificity, Hamming, StatScores; global top-1):
 //       tp_c += delta[c, c],  fp_c += colsum_c - tp_c,  fn_c += rowsum_c - tp_c,  tn_c += N_valid - tp_c - fp_c - fn_c
 //     (micro: the class sums and tn = C * N_valid - tp - fp - fn, the reference's multiclass micro convention)
-// Two launches: fold_rows (a block owns a 32-row x 256-column tile: adds it into the confusion-matrix states, the
-// diagonal, row and column partial sums, and zeroes the delta for the next batch) and fold_stats (one block: per-class deltas into every stat member, then zeroes the sums).
+// One launch: fold_rows (a block owns a 16-row x 256-column tile: adds it into the confusion-matrix states, the
+// diagonal, row and column partial sums, and zeroes the delta for the next batch); the last block to finish folds the
+// per-class deltas into every stat member and zeroes the sums.
 #include "common.h"
 
 namespace tmx {
 
 constexpr int kFoldMax = 8;  // members per kind handled by one launch
-constexpr int kFoldRows = 32;
+constexpr int kFoldRows = 16;  // 16-row chunks: 4 x 63 blocks at C = 1000
 constexpr int kFoldThreads = 256;
 
 struct FoldCms {
@@ -37,7 +38,9 @@ struct FoldStats {
 // Block (row chunk of 32, column tile of 256): every thread owns one column of the tile; its 32 loads are issued
 // before any use; row partial sums are reduced in the block and added with one atomic per row and tile, column
 // partial sums with one atomic per column and row chunk.
-__global__ __launch_bounds__(kFoldThreads) void fold_rows_kernel(int64_t* __restrict__ delta, int C, FoldCms cms,
+__device__ void fold_stats_body(int C, const FoldStats& st, int64_t* __restrict__ sums);
+
+__global__ __launch_bounds__(kFoldThreads) void fold_rows_kernel(int64_t* __restrict__ delta, int C, FoldCms cms, FoldStats st,
                                                                  int64_t* __restrict__ sums) {
   __shared__ long long s_row[kFoldThreads / kWave][kFoldRows];
   const int r0 = blockIdx.y * kFoldRows;
@@ -51,10 +54,11 @@ __global__ __launch_bounds__(kFoldThreads) void fold_rows_kernel(int64_t* __rest
   for (int i = 0; i < kFoldRows; ++i) {
     if (v[i]) {
       const int64_t idx = static_cast<int64_t>(r0 + i) * C + c;
-      for (int m = 0; m < cms.n; ++m) cms.p[m][idx] += v[i];
+      // no-return atomics: fire-and-forget adds, so a thread never waits on the latency of a read-modify-write
+      for (int m = 0; m < cms.n; ++m) atomic_add_i64(cms.p[m] + idx, v[i]);
       delta[idx] = 0;
       col += v[i];
-      if (c == r0 + i) sums[C + c] = v[i];
+      if (c == r0 + i) atomic_add_i64(sums + C + c, v[i]);  // atomic: read by another XCD's last workgroup
     }
   }
   if (col) atomic_add_i64(sums + 2 * C + c, col);
@@ -69,17 +73,34 @@ __global__ __launch_bounds__(kFoldThreads) void fold_rows_kernel(int64_t* __rest
     for (int w = 0; w < kFoldThreads / kWave; ++w) t += s_row[w][threadIdx.x];
     if (t) atomic_add_i64(sums + r0 + threadIdx.x, t);
   }
+  if (st.n == 0) return;
+  // last workgroup to finish folds the class sums into the stat members (one launch for the whole fold): every
+  // thread's sum atomics are performed (vmcnt 0) before the workgroup takes its ticket
+  __shared__ int s_last;
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    auto* ticket = reinterpret_cast<unsigned long long*>(sums + 3 * C);
+    const unsigned long long nblk = (unsigned long long)gridDim.x * gridDim.y;
+    s_last = atomicAdd(ticket, 1ull) == nblk - 1;
+    if (s_last) atomicExch(ticket, 0ull);
+  }
+  __syncthreads();
+  if (s_last) fold_stats_body(C, st, sums);
 }
 
-__global__ __launch_bounds__(1024) void fold_stats_kernel(int C, FoldStats st, int64_t* __restrict__ sums) {
-  __shared__ long long s_red[1024 / kWave][2];
+// Runs in the last workgroup of fold_rows: every other workgroup's sums are in place (ticket order); they are read
+// with atomicExch (coherent read that also re-zeroes the scratch for the next batch).
+__device__ void fold_stats_body(int C, const FoldStats& st, int64_t* __restrict__ sums) {
+  __shared__ long long s_red[kFoldThreads / kWave][2];
   __shared__ long long s_tot[2];
+  auto* u = reinterpret_cast<unsigned long long*>(sums);
   const int lane = threadIdx.x % kWave, wave = threadIdx.x / kWave;
   // N_valid = sum of row sums (every valid row lands in exactly one row of the delta); micro tp = sum of diagonal
   long long nv = 0, dg = 0;
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    nv += sums[c];
-    dg += sums[C + c];
+    nv += (long long)__hip_atomic_load(u + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    dg += (long long)__hip_atomic_load(u + C + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   nv = wave_sum(nv);
   dg = wave_sum(dg);
@@ -100,40 +121,39 @@ __global__ __launch_bounds__(1024) void fold_stats_kernel(int C, FoldStats st, i
   __syncthreads();
   const long long N = s_tot[0], TP = s_tot[1];
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    const long long rs = sums[c], tp = sums[C + c], cs = sums[2 * C + c];
+    const long long rs = (long long)atomicExch(u + c, 0ull), tp = (long long)atomicExch(u + C + c, 0ull),
+                    cs = (long long)atomicExch(u + 2 * C + c, 0ull);
     const long long fp = cs - tp, fn = rs - tp, tn = N - tp - fp - fn;
     for (int m = 0; m < st.n; ++m) {
       if (st.micro[m]) continue;
-      st.tp[m][c] += tp;
-      st.fp[m][c] += fp;
-      st.fn[m][c] += fn;
-      st.tn[m][c] += tn;
+      // exclusive owner per (member, class): no-return atomics, no wait on a read-modify-write
+      atomic_add_i64(st.tp[m] + c, tp);
+      atomic_add_i64(st.fp[m] + c, fp);
+      atomic_add_i64(st.fn[m] + c, fn);
+      atomic_add_i64(st.tn[m] + c, tn);
     }
-    sums[c] = 0;
-    sums[C + c] = 0;
-    sums[2 * C + c] = 0;
   }
   if (threadIdx.x == 0) {
     const long long fp = N - TP;  // = fn
     for (int m = 0; m < st.n; ++m) {
       if (!st.micro[m]) continue;
-      st.tp[m][0] += TP;
-      st.fp[m][0] += fp;
-      st.fn[m][0] += fp;
-      st.tn[m][0] += static_cast<long long>(C) * N - TP - 2 * fp;
+      atomic_add_i64(st.tp[m], TP);
+      atomic_add_i64(st.fp[m], fp);
+      atomic_add_i64(st.fn[m], fp);
+      atomic_add_i64(st.tn[m], static_cast<long long>(C) * N - TP - 2 * fp);
     }
   }
 }
 
 // delta: int64 [C, C] batch confusion matrix (zeroed on return); cms: confusion-matrix states (+= delta);
 // stats: flattened (tp, fp, tn, fn) int64 states per member, micro[m] = 1 for a one-element (micro) state;
-// sums: int64 [3 C] zeroed scratch (zeroed again on return).
+// sums: int64 [3 C + 1] zeroed scratch (class sums + ticket; zeroed again on return).
 void confmat_fold(at::Tensor& delta, at::TensorList cms, at::TensorList stats, at::IntArrayRef micro, at::Tensor& sums) {
   TORCH_CHECK(delta.is_cuda() && delta.dim() == 2 && delta.size(0) == delta.size(1) && delta.scalar_type() == at::kLong &&
                   delta.is_contiguous(), "confmat_fold: delta must be a contiguous int64 [C, C] GPU tensor");
   const int C = static_cast<int>(delta.size(0));
-  TORCH_CHECK(sums.is_contiguous() && sums.scalar_type() == at::kLong && sums.numel() == 3 * static_cast<int64_t>(C),
-              "confmat_fold: sums must be int64 [3 C]");
+  TORCH_CHECK(sums.is_contiguous() && sums.scalar_type() == at::kLong && sums.numel() == 3 * static_cast<int64_t>(C) + 1,
+              "confmat_fold: sums must be int64 [3 C + 1] (class sums + the workgroup ticket)");
   TORCH_CHECK(static_cast<int64_t>(cms.size()) <= kFoldMax && stats.size() == 4 * micro.size() &&
                   static_cast<int64_t>(micro.size()) <= kFoldMax, "confmat_fold: too many members");
   const c10::DeviceGuard guard(delta.device());
@@ -159,14 +179,9 @@ void confmat_fold(at::Tensor& delta, at::TensorList cms, at::TensorList stats, a
   }
   if (C == 0) return;
   const dim3 grid((C + kFoldThreads - 1) / kFoldThreads, (C + kFoldRows - 1) / kFoldRows);
-  fold_rows_kernel<<<grid, kFoldThreads, 0, stream()>>>(delta.data_ptr<int64_t>(), C, fc, sums.data_ptr<int64_t>());
+  fold_rows_kernel<<<grid, kFoldThreads, 0, stream()>>>(delta.data_ptr<int64_t>(), C, fc, fs, sums.data_ptr<int64_t>());
   TMX_LAUNCH_CHECK();
-  if (fs.n > 0) {
-    fold_stats_kernel<<<1, 1024, 0, stream()>>>(C, fs, sums.data_ptr<int64_t>());
-    TMX_LAUNCH_CHECK();
-  } else {
-    sums.zero_();
-  }
+  if (fs.n == 0) sums.zero_();
 }
 
 }  // namespace tmx

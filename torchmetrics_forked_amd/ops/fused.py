@@ -43,7 +43,7 @@ class _MulticlassScoresPlan:
         buf = self._scratch.get(device)
         if buf is None or buf[0].shape[0] != C:
             # zeroed once; confmat_fold leaves both zero again after every batch
-            buf = (torch.zeros(C, C, dtype=torch.long, device=device), torch.zeros(3 * C, dtype=torch.long, device=device))
+            buf = (torch.zeros(C, C, dtype=torch.long, device=device), torch.zeros(3 * C + 1, dtype=torch.long, device=device))  # class sums + workgroup ticket
             self._scratch[device] = buf
         return buf
 
