@@ -1187,7 +1187,8 @@ __global__ void __launch_bounds__(256) curve_hist_mc_kernel(const T* __restrict_
 // scratch: ``codes`` int16 [C * n_pad] (class-major), ``slow_rows`` int32 [2 n], ``state`` int32[6] (counts zero).
 template <typename T, bool PADDED>
 void launch_row_pass(const T* p, const int64_t* target, int64_t n, int C, int ld, int* mode, int* state, bool speculative,
-                     int64_t ignore_index, bool has_ignore, int64_t* cm, int* err, uint32_t* cptr, int* srows) {
+                     int64_t ignore_index, bool has_ignore, int64_t* cm, int* err, uint32_t* cptr, int* srows,
+                     bool roll_in_class_pass = false) {
   TORCH_CHECK(n < (int64_t{1} << 31), "curve_hist_update: more than 2^31 rows in one batch");
   const int64_t n_pad = (n + kTileRows - 1) / kTileRows * kTileRows;
   const int64_t ntiles = n_pad / kTileRows;
@@ -1213,7 +1214,7 @@ void launch_row_pass(const T* p, const int64_t* target, int64_t n, int C, int ld
       TMX_LAUNCH_CHECK();
     }
   }
-  if (speculative) {
+  if (speculative && !roll_in_class_pass) {
     hipLaunchKernelGGL(mode_roll_kernel, 1, 1, 0, stream(), mode, state + 3);
     TMX_LAUNCH_CHECK();
   }
@@ -1223,14 +1224,15 @@ void launch_row_pass(const T* p, const int64_t* target, int64_t n, int C, int ld
 // speculative row pass, else the pre-pass flag with speculative = false).
 template <typename T>
 void launch_class_pass(const uint32_t* cptr, int64_t n, int C, int ld, const T* p, const int64_t* target, const int* bmode,
-                       bool speculative, const int* srows, int* state, int64_t* hist, int64_t* cm, int* code_range) {
+                       bool speculative, const int* srows, int* state, int64_t* hist, int64_t* cm, int* code_range,
+                       int* roll_mode = nullptr) {
   const int64_t n_pad = (n + kTileRows - 1) / kTileRows * kTileRows;
   // row splits only when there are too few classes to fill the chip (exclusive-owner flush when splits == 1)
   int splits = 1;
   while ((int64_t)C * splits < 512 && n_pad / (8 * (splits * 2)) >= 1024) splits *= 2;
   hipLaunchKernelGGL((class_hist_kernel<T, false>), C * splits, kClassThreads, kCodes * sizeof(uint32_t), stream(),
                      reinterpret_cast<const uint16_t*>(cptr), n_pad, splits, hist, p, ld, target, n, bmode, speculative,
-                     srows, state, cm, code_range);
+                     srows, state, cm, code_range, roll_mode);
   TMX_LAUNCH_CHECK();
 }
 
@@ -1243,8 +1245,9 @@ void launch_two_pass(const T* p, const int64_t* target, int64_t n, int C, int ld
   auto slow_rows = at::empty({2 * n}, opts.dtype(at::kInt));
   uint32_t* cptr = reinterpret_cast<uint32_t*>(codes.data_ptr());
   int* srows = slow_rows.data_ptr<int>();
-  launch_row_pass<T, PADDED>(p, target, n, C, ld, mode, state, speculative, ignore_index, has_ignore, cm, err, cptr, srows);
-  launch_class_pass<T>(cptr, n, C, ld, p, target, speculative ? state + 3 : mode, speculative, srows, state, hist, cm, code_range);
+  // single stream: the class pass reads the (used, real) pair straight from ``mode`` and its last workgroup rolls it
+  launch_row_pass<T, PADDED>(p, target, n, C, ld, mode, state, speculative, ignore_index, has_ignore, cm, err, cptr, srows, true);
+  launch_class_pass<T>(cptr, n, C, ld, p, target, mode, speculative, srows, state, hist, cm, code_range, speculative ? mode : nullptr);
 }
 
 // ---- one-call overlapped update: row pass on the current stream, class pass on a per-device side stream ----------
@@ -1620,7 +1623,7 @@ void curve_hist_update(const at::Tensor& preds_, const at::Tensor& target_, at::
         hipLaunchKernelGGL((class_hist_kernel<scalar_t, true>), C * splits, kClassThreads, kCodes * sizeof(uint32_t), stream(),
                            reinterpret_cast<const uint16_t*>(cptr), n_pad, splits, hist.data_ptr<int64_t>(), p, C,
                            target.data_ptr<int64_t>(), N, flag.data_ptr<int>(), false, static_cast<const int*>(nullptr),
-                           state.data_ptr<int>(), static_cast<int64_t*>(nullptr), crange);
+                           state.data_ptr<int>(), static_cast<int64_t*>(nullptr), crange, static_cast<int*>(nullptr));
         range_tracked = true;
         return;
       }

@@ -604,7 +604,8 @@ __global__ void __launch_bounds__(kClassThreads) class_hist_kernel(const uint16_
                                                                    const int64_t* __restrict__ target, int64_t n,
                                                                    const int* __restrict__ bmode, bool speculative,
                                                                    const int* __restrict__ slow_rows, int* __restrict__ state,
-                                                                   int64_t* __restrict__ confmat, int* __restrict__ code_range) {
+                                                                   int64_t* __restrict__ confmat, int* __restrict__ code_range,
+                                                                   int* __restrict__ roll_mode) {
   extern __shared__ __attribute__((aligned(16))) uint32_t s_h[];  // [kCodes]: neg, or neg (lo 16) | pos (hi 16)
   __shared__ int s_info[4];
   int lo = kCodes, hi = -1;  // occupied code range this thread touched (compute() then scans only that range)
@@ -713,11 +714,17 @@ __global__ void __launch_bounds__(kClassThreads) class_hist_kernel(const uint16_
     if (__hip_atomic_fetch_add(state + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1) {
       state[0] = state[1] = 0;
       state[2] = 0;
+      if (roll_mode != nullptr) {  // speculation roll (every block read the mode pair before its ticket)
+        const int m1 = roll_mode[1];
+        roll_mode[0] = m1;
+        roll_mode[1] = 0;
+      }
     }
   }
 }
 
-// Speculation roll, one thread, in row-pass stream order right after the FIXUP launch: the batch's (used, real) mode
+// Speculation roll, one thread, in row-pass stream order right after the FIXUP launch (side-stream route; the
+// single-stream route rolls in the class pass's last workgroup instead, one launch fewer): the batch's (used, real) mode
 // pair is snapshotted into its own state (``bmode`` = state[3:5], read by that batch's class pass) and the next batch
 // speculates the real one.  Keeping the roll out of the class pass lets the class pass of batch k run on a side
 // stream while the row pass of batch k + 1 reads the rolled word.
