@@ -1343,6 +1343,104 @@ void curve_mc_update_overlapped(const at::Tensor& preds, const at::Tensor& targe
   if (code_range.has_value()) c10::hip::HIPCachingAllocator::recordStream(code_range->storage().data_ptr(), side);
 }
 
+// Single-stream overlapped route: ONE dual-role launch runs the row pass of this batch (scratch buffer ``buf``) and the
+// deferred class pass of the previous batch (buffer buf ^ 1: ``prev_preds`` / ``prev_target`` / ``prev_confmat``),
+// then the FIXUP and the speculation roll of this batch (snapshot in states[buf][3:5]).  This batch's class pass is
+// left to the next call or to ``curve_mc_classpass`` (the metric's flush at any state consumer).
+void curve_mc_update_dual(const at::Tensor& preds, const at::Tensor& target, at::Tensor& mode, at::Tensor& states, at::Tensor& codes,
+                          at::Tensor& slow_rows, int64_t buf, at::Tensor& hist, int64_t ignore_index, bool has_ignore,
+                          c10::optional<at::Tensor> confmat, c10::optional<at::Tensor> err_flag, c10::optional<at::Tensor> code_range,
+                          c10::optional<at::Tensor> prev_preds, c10::optional<at::Tensor> prev_target,
+                          c10::optional<at::Tensor> prev_confmat) {
+  TORCH_CHECK(preds.dim() == 2 && preds.is_contiguous() && target.is_contiguous() && target.scalar_type() == at::kLong &&
+              target.numel() == preds.size(0), "curve_mc_update_dual: preds [N, C] and int64 target [N], contiguous");
+  const int64_t n = preds.size(0);
+  const int C = static_cast<int>(preds.size(1));
+  TORCH_CHECK(buf == 0 || buf == 1, "buf must be 0 or 1");
+  TORCH_CHECK(C % 8 == 0 && C <= 8 * 2 * kWave && (reinterpret_cast<uintptr_t>(preds.data_ptr()) & 15) == 0,
+              "curve_mc_update_dual: C must be a multiple of 8, <= 1024, preds 16-B aligned");
+  const int64_t n_pad = (n + kTileRows - 1) / kTileRows * kTileRows;
+  TORCH_CHECK(codes.dim() == 2 && codes.size(0) == 2 && codes.size(1) >= (int64_t)C * n_pad && codes.scalar_type() == at::kShort &&
+              codes.is_contiguous(), "codes scratch must be int16 [2, >= C * n_pad]");
+  TORCH_CHECK(slow_rows.dim() == 2 && slow_rows.size(0) == 2 && slow_rows.size(1) >= 2 * n && slow_rows.scalar_type() == at::kInt &&
+              slow_rows.is_contiguous(), "slow_rows scratch must be int32 [2, >= 2 N]");
+  TORCH_CHECK(states.scalar_type() == at::kInt && states.numel() == 12 && states.is_contiguous(), "states must be int32 [2, 6]");
+  TORCH_CHECK(mode.scalar_type() == at::kInt && mode.numel() >= 2, "mode must be int32[>= 2]");
+  TORCH_CHECK(hist.is_contiguous() && hist.scalar_type() == at::kLong && hist.numel() == (int64_t)C * 2 * kCodes,
+              "hist must be int64 [C, 2, 16384]");
+  auto cm_ptr = [&](const c10::optional<at::Tensor>& t) -> int64_t* {
+    if (!t.has_value()) return nullptr;
+    TORCH_CHECK(t->is_contiguous() && t->scalar_type() == at::kLong && t->numel() == (int64_t)C * C, "confusion matrix int64 [C, C]");
+    return t->data_ptr<int64_t>();
+  };
+  int64_t* cm = cm_ptr(confmat);
+  int64_t* pcm = cm_ptr(prev_confmat);
+  int* err = err_flag.has_value() ? err_flag->data_ptr<int>() : nullptr;
+  int* cr = nullptr;
+  if (code_range.has_value()) {
+    TORCH_CHECK(code_range->scalar_type() == at::kInt && code_range->numel() == 2 * C && code_range->is_contiguous(),
+                "code_range must be int32[C, 2]");
+    cr = code_range->data_ptr<int>();
+  }
+  const bool has_prev = prev_preds.has_value() && prev_target.has_value() && prev_target->numel() > 0;
+  int64_t pn = 0, pn_pad = 0;
+  if (has_prev) {
+    TORCH_CHECK(prev_preds->dim() == 2 && prev_preds->size(1) == C && prev_preds->scalar_type() == preds.scalar_type() &&
+                prev_preds->is_contiguous() && prev_target->scalar_type() == at::kLong && prev_target->is_contiguous() &&
+                prev_target->numel() == prev_preds->size(0), "curve_mc_update_dual: previous batch shapes");
+    pn = prev_preds->size(0);
+    pn_pad = (pn + kTileRows - 1) / kTileRows * kTileRows;
+    TORCH_CHECK(codes.size(1) >= (int64_t)C * pn_pad && slow_rows.size(1) >= 2 * pn, "curve_mc_update_dual: scratch too small for the previous batch");
+  }
+  const int pb = static_cast<int>(buf ^ 1);
+  uint32_t* cptr = reinterpret_cast<uint32_t*>(codes[buf].data_ptr());
+  int* srows = slow_rows[buf].data_ptr<int>();
+  int* state = states.data_ptr<int>() + 6 * buf;
+  int* pstate = states.data_ptr<int>() + 6 * pb;
+  TMX_DISPATCH_HALF(preds.scalar_type(), "curve_mc_update_dual", [&] {
+    const scalar_t* p = reinterpret_cast<const scalar_t*>(preds.data_ptr());
+    const int64_t ntiles = n_pad / kTileRows;
+    const int64_t row_blocks = n > 0 ? (ntiles + 7) / 8 * 8 : 0;
+    const int fixup_grid = static_cast<int>(std::min<int64_t>(std::max<int64_t>(row_blocks, 8), 128));
+    const size_t row_shm = (size_t)512 * (C > 512 ? 2 : 1) * kSlots * sizeof(uint32_t);
+    int splits = 1;
+    while (has_prev && (int64_t)C * splits < 512 && pn_pad / (8 * (splits * 2)) >= 1024) splits *= 2;
+    const int64_t class_blocks = has_prev ? (int64_t)C * splits : 0;
+    const int64_t groups = row_blocks / 8 + (class_blocks + 7) / 8;
+    if (groups > 0) {
+      const size_t shm = std::max(row_shm, has_prev ? (size_t)kCodes * sizeof(uint32_t) : (size_t)0);
+      const scalar_t* pp = has_prev ? reinterpret_cast<const scalar_t*>(prev_preds->data_ptr()) : p;
+      const int64_t* pt = has_prev ? prev_target->data_ptr<int64_t>() : target.data_ptr<int64_t>();
+      const uint16_t* pc = reinterpret_cast<const uint16_t*>(codes[pb].data_ptr());
+      const int* ps = slow_rows[pb].data_ptr<int>();
+      if (C > 512)
+        hipLaunchKernelGGL((mc_dual_kernel<scalar_t, 2>), static_cast<int>(groups * 8), kRowThreads, shm, stream(), p,
+                           target.data_ptr<int64_t>(), n, C, mode.data_ptr<int>(), ignore_index, has_ignore, cptr, n_pad, cm, err, srows,
+                           state, row_blocks, pc, pn_pad, splits, hist.data_ptr<int64_t>(), pp, pt, pn, pstate + 3, ps, pstate, pcm, cr,
+                           class_blocks, groups, (class_blocks + 7) / 8);
+      else
+        hipLaunchKernelGGL((mc_dual_kernel<scalar_t, 1>), static_cast<int>(groups * 8), kRowThreads, shm, stream(), p,
+                           target.data_ptr<int64_t>(), n, C, mode.data_ptr<int>(), ignore_index, has_ignore, cptr, n_pad, cm, err, srows,
+                           state, row_blocks, pc, pn_pad, splits, hist.data_ptr<int64_t>(), pp, pt, pn, pstate + 3, ps, pstate, pcm, cr,
+                           class_blocks, groups, (class_blocks + 7) / 8);
+      TMX_LAUNCH_CHECK();
+    }
+    if (n > 0) {
+      if (C > 512)
+        hipLaunchKernelGGL((mc_codes_kernel<scalar_t, true, 2, false>), fixup_grid, kRowThreads, row_shm, stream(), p,
+                           target.data_ptr<int64_t>(), n, C, C, mode.data_ptr<int>(), ignore_index, has_ignore, cptr, n_pad, cm, err, false,
+                           srows, state);
+      else
+        hipLaunchKernelGGL((mc_codes_kernel<scalar_t, true, 1, false>), fixup_grid, kRowThreads, row_shm, stream(), p,
+                           target.data_ptr<int64_t>(), n, C, C, mode.data_ptr<int>(), ignore_index, has_ignore, cptr, n_pad, cm, err, false,
+                           srows, state);
+      TMX_LAUNCH_CHECK();
+      hipLaunchKernelGGL(mode_roll_kernel, 1, 1, 0, stream(), mode.data_ptr<int>(), state + 3);
+      TMX_LAUNCH_CHECK();
+    }
+  });
+}
+
 // Make the current stream wait for every class pass issued on the scratch ``codes`` (no-op for unknown buffers).
 void curve_side_join(const at::Tensor& codes) {
   SideEvents& ev = side_events(codes.data_ptr());
@@ -2456,6 +2554,7 @@ TORCH_LIBRARY_FRAGMENT(tmx, m) {
   m.def("curve_summary(Tensor scores) -> Tensor");
   m.def("curve_mc_update_overlapped(Tensor preds, Tensor target, Tensor(a!) mode, Tensor(b!) states, Tensor(c!) codes, Tensor(d!) slow_rows, int buf, Tensor(e!) hist, int ignore_index, bool has_ignore, Tensor(f!)? confmat, Tensor(g!)? err_flag, Tensor(h!)? code_range) -> ()");
   m.def("curve_side_join(Tensor codes) -> ()");
+  m.def("curve_mc_update_dual(Tensor preds, Tensor target, Tensor(a!) mode, Tensor(b!) states, Tensor(c!) codes, Tensor(d!) slow_rows, int buf, Tensor(e!) hist, int ignore_index, bool has_ignore, Tensor(f!)? confmat, Tensor(g!)? err_flag, Tensor(h!)? code_range, Tensor? prev_preds, Tensor? prev_target, Tensor(i!)? prev_confmat) -> ()");
   m.def("curve_mc_rowpass(Tensor preds, Tensor target, Tensor(a!) mode, Tensor(b!) state, Tensor(c!) codes, Tensor(d!) slow_rows, int ignore_index, bool has_ignore, Tensor(e!)? confmat, Tensor(f!)? err_flag) -> ()");
   m.def("curve_mc_classpass(Tensor codes, Tensor slow_rows, Tensor(a!) state, Tensor(b!) hist, Tensor preds, Tensor target, Tensor(c!)? confmat, Tensor(d!)? code_range) -> ()");
   m.def("binned_curve_update(Tensor preds, Tensor target, Tensor thresholds, Tensor(a!) confmat, int task, int ignore_index, bool has_ignore, Tensor? norm_flag, Tensor(b!)? err_flag=None) -> ()");
@@ -2477,6 +2576,7 @@ TORCH_LIBRARY_IMPL(tmx, CUDA, m) {
   m.impl("curve_mc_rowpass", &tmx::curve_mc_rowpass);
   m.impl("curve_mc_update_overlapped", &tmx::curve_mc_update_overlapped);
   m.impl("curve_side_join", &tmx::curve_side_join);
+  m.impl("curve_mc_update_dual", &tmx::curve_mc_update_dual);
   m.impl("curve_mc_classpass", &tmx::curve_mc_classpass);
   m.impl("binned_curve_update", &tmx::binned_curve_update);
   m.impl("ce_bins_update", &tmx::ce_bins_update);

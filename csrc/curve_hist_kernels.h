@@ -424,13 +424,11 @@ __device__ __forceinline__ void row_tile(const T* __restrict__ preds, const int6
 // flags are mode independent and are not touched again).  ``class_hist_kernel`` rolls mode[0] = mode[1].
 // Grid: one block per tile for the main launch (blocks stride over tiles, so a FIXUP launch can use a small grid).
 template <typename T, bool FIXUP, int NG, bool PADDED>
-__global__ void __launch_bounds__(kRowThreads, 4) mc_codes_kernel(const T* __restrict__ preds, const int64_t* __restrict__ target,
-                                                                    int64_t n, int C, int ld, int* __restrict__ mode,
-                                                                    int64_t ignore_index, bool has_ignore,
-                                                                    uint32_t* __restrict__ codes, int64_t n_pad,
-                                                                    int64_t* __restrict__ confmat, int* __restrict__ err,
-                                                                    bool record_mode, int* __restrict__ slow_rows,
-                                                                    int* __restrict__ slow_count) {
+__device__ __forceinline__ void mc_codes_block(int64_t vb, int64_t vgrid, const T* __restrict__ preds, const int64_t* __restrict__ target,
+                                               int64_t n, int C, int ld, int* __restrict__ mode, int64_t ignore_index, bool has_ignore,
+                                               uint32_t* __restrict__ codes, int64_t n_pad, int64_t* __restrict__ confmat,
+                                               int* __restrict__ err, bool record_mode, int* __restrict__ slow_rows,
+                                               int* __restrict__ slow_count) {
   extern __shared__ __attribute__((aligned(16))) uint32_t s_tile[];  // [512 * NG][kSlots]
   int use_mode;
   if constexpr (FIXUP) {
@@ -459,18 +457,30 @@ __global__ void __launch_bounds__(kRowThreads, 4) mc_codes_kernel(const T* __res
       row_tile<T, NG, false, FIXUP, PADDED>(preds, target, n, C, ld, ignore_index, has_ignore, codes, n_pad, confmat, err, rec, saw_bad, slow, s_tile, tile);
   };
   if constexpr (FIXUP) {  // rare: blocks stride over the tiles (small grid, cheap early exit)
-    for (int64_t b = blockIdx.x; b < per_xcd * 8; b += gridDim.x) {
+    for (int64_t b = vb; b < per_xcd * 8; b += vgrid) {
       run_tile(b);
       __syncthreads();  // the LDS image is rewritten by the next tile of this block
     }
   } else {  // one tile per block: no loop, so nothing of one tile's register state lives across another's
-    run_tile(blockIdx.x);
+    run_tile(vb);
   }
   if constexpr (!FIXUP) {
     if (record_mode && __syncthreads_or(saw_bad) && threadIdx.x == 0 &&
         __hip_atomic_load(mode + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
       __hip_atomic_store(mode + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+}
+
+template <typename T, bool FIXUP, int NG, bool PADDED>
+__global__ void __launch_bounds__(kRowThreads, 4) mc_codes_kernel(const T* __restrict__ preds, const int64_t* __restrict__ target,
+                                                                    int64_t n, int C, int ld, int* __restrict__ mode,
+                                                                    int64_t ignore_index, bool has_ignore,
+                                                                    uint32_t* __restrict__ codes, int64_t n_pad,
+                                                                    int64_t* __restrict__ confmat, int* __restrict__ err,
+                                                                    bool record_mode, int* __restrict__ slow_rows,
+                                                                    int* __restrict__ slow_count) {
+  mc_codes_block<T, FIXUP, NG, PADDED>(blockIdx.x, gridDim.x, preds, target, n, C, ld, mode, ignore_index, has_ignore, codes, n_pad,
+                                       confmat, err, record_mode, slow_rows, slow_count);
 }
 
 // Multilabel row pass: the same tile / LDS image / class-major scratch as the multiclass row pass, but every element
@@ -577,10 +587,10 @@ __global__ void __launch_bounds__(kRowThreads, 4) ml_codes_kernel(const T* __res
 constexpr int kClassThreads = 1024;
 constexpr int64_t kClassChunk = 65528;  // rows per LDS flush: a 16-bit half never overflows (multiple of 8)
 
-template <bool PACKED>
+template <bool PACKED, int NT = kClassThreads>
 __device__ __forceinline__ void class_flush(uint32_t* __restrict__ s_h, int64_t* __restrict__ neg_hist,
                                             int64_t* __restrict__ pos_hist, bool exclusive, int& lo, int& hi) {
-  for (int i = threadIdx.x; i < kCodes; i += kClassThreads) {
+  for (int i = threadIdx.x; i < kCodes; i += NT) {
     const uint32_t w = s_h[i];
     if (w) {
       lo = min(lo, i);
@@ -598,19 +608,17 @@ __device__ __forceinline__ void class_flush(uint32_t* __restrict__ s_h, int64_t*
   }
 }
 
-template <typename T, bool PACKED>
-__global__ void __launch_bounds__(kClassThreads) class_hist_kernel(const uint16_t* __restrict__ codes, int64_t n_pad, int splits,
-                                                                   int64_t* __restrict__ hist, const T* __restrict__ preds, int ld,
-                                                                   const int64_t* __restrict__ target, int64_t n,
-                                                                   const int* __restrict__ bmode, bool speculative,
-                                                                   const int* __restrict__ slow_rows, int* __restrict__ state,
-                                                                   int64_t* __restrict__ confmat, int* __restrict__ code_range,
-                                                                   int* __restrict__ roll_mode) {
+template <typename T, bool PACKED, int NT>
+__device__ __forceinline__ void class_hist_block(int64_t vb, int64_t vgrid, const uint16_t* __restrict__ codes, int64_t n_pad, int splits,
+                                                 int64_t* __restrict__ hist, const T* __restrict__ preds, int ld,
+                                                 const int64_t* __restrict__ target, int64_t n, const int* __restrict__ bmode,
+                                                 bool speculative, const int* __restrict__ slow_rows, int* __restrict__ state,
+                                                 int64_t* __restrict__ confmat, int* __restrict__ code_range, int* __restrict__ roll_mode) {
   extern __shared__ __attribute__((aligned(16))) uint32_t s_h[];  // [kCodes]: neg, or neg (lo 16) | pos (hi 16)
   __shared__ int s_info[4];
   int lo = kCodes, hi = -1;  // occupied code range this thread touched (compute() then scans only that range)
-  const int C = gridDim.x / splits;
-  const int c = blockIdx.x / splits, sp = blockIdx.x % splits;
+  const int C = static_cast<int>(vgrid / splits);
+  const int c = static_cast<int>(vb / splits), sp = static_cast<int>(vb % splits);
   if (threadIdx.x == 0) {  // the row-pass kernels of this batch are complete (stream order / event wait)
     s_info[0] = bmode[0];
     s_info[1] = speculative ? bmode[1] : bmode[0];
@@ -618,7 +626,7 @@ __global__ void __launch_bounds__(kClassThreads) class_hist_kernel(const uint16_
     s_info[3] = state[1];
   }
   uint4* s4 = reinterpret_cast<uint4*>(s_h);
-  for (int i = threadIdx.x; i < kCodes / 4; i += kClassThreads) s4[i] = make_uint4(0, 0, 0, 0);
+  for (int i = threadIdx.x; i < kCodes / 4; i += NT) s4[i] = make_uint4(0, 0, 0, 0);
   __syncthreads();
   int64_t* neg_hist = hist + ((int64_t)c * 2) * kCodes;
   int64_t* pos_hist = hist + ((int64_t)c * 2 + 1) * kCodes;
@@ -630,11 +638,11 @@ __global__ void __launch_bounds__(kClassThreads) class_hist_kernel(const uint16_
   constexpr int64_t kChunkV = PACKED ? kClassChunk / 8 : (int64_t{1} << 62);
   for (int64_t cb = v0; cb < v1; cb += kChunkV) {
     const int64_t ce = cb + kChunkV < v1 ? cb + kChunkV : v1;
-    for (int64_t v = cb + threadIdx.x; v < ce; v += 4 * kClassThreads) {
+    for (int64_t v = cb + threadIdx.x; v < ce; v += 4 * NT) {
       uint4 w[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u)
-        w[u] = (v + u * kClassThreads < ce) ? col[v + u * kClassThreads] : make_uint4(0x80008000u, 0x80008000u, 0x80008000u, 0x80008000u);
+        w[u] = (v + u * NT < ce) ? col[v + u * NT] : make_uint4(0x80008000u, 0x80008000u, 0x80008000u, 0x80008000u);
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const uint32_t parts[4] = {w[u].x, w[u].y, w[u].z, w[u].w};
@@ -653,7 +661,7 @@ __global__ void __launch_bounds__(kClassThreads) class_hist_kernel(const uint16_
     }
     if (ce < v1) {  // more rows than one chunk: flush before a 16-bit half can overflow
       __syncthreads();
-      class_flush<PACKED>(s_h, neg_hist, pos_hist, exclusive, lo, hi);
+      class_flush<PACKED, NT>(s_h, neg_hist, pos_hist, exclusive, lo, hi);
       __syncthreads();
     }
   }
@@ -662,7 +670,7 @@ __global__ void __launch_bounds__(kClassThreads) class_hist_kernel(const uint16_
   const bool fixed = speculative && m0 != m1;
   const int64_t n0 = s_info[2], n1 = s_info[3];
   if (sp == 0) {
-    for (int64_t i = threadIdx.x; i < n0 + n1; i += kClassThreads) {
+    for (int64_t i = threadIdx.x; i < n0 + n1; i += NT) {
       const int lst = i < n0 ? 0 : 1;
       if (lst == 0 && fixed) continue;
       const int64_t r = slow_rows[lst * n + (lst == 0 ? i : i - n0)];
@@ -677,7 +685,7 @@ __global__ void __launch_bounds__(kClassThreads) class_hist_kernel(const uint16_
   }
   if (confmat != nullptr && threadIdx.x < kWave) {
     const int lane = threadIdx.x;
-    for (int64_t i = blockIdx.x; i < n0; i += gridDim.x) {
+    for (int64_t i = vb; i < n0; i += vgrid) {
       const int64_t r = slow_rows[i];
       const int64_t t = target[r];
       if (t < 0 || t >= C) continue;
@@ -698,7 +706,7 @@ __global__ void __launch_bounds__(kClassThreads) class_hist_kernel(const uint16_
   }
   __syncthreads();
   // rare-row codes went to the int64 bins by atomics: then the last flush must be atomic too
-  class_flush<PACKED>(s_h, neg_hist, pos_hist, exclusive && n0 + n1 == 0, lo, hi);
+  class_flush<PACKED, NT>(s_h, neg_hist, pos_hist, exclusive && n0 + n1 == 0, lo, hi);
   if (code_range != nullptr) {  // per-class running range [C][2]: one min / max per wave, no block barrier
     lo = wave_min_i32(lo);
     hi = wave_max_i32(hi);
@@ -711,7 +719,7 @@ __global__ void __launch_bounds__(kClassThreads) class_hist_kernel(const uint16_
     // No fence: the only ordering needed is "every block's read of mode / counts happened before the reset", and
     // each block consumed those values (s_info, above) before taking its ticket.  (An agent-scope release here writes
     // back the XCD's L2 once per block: it doubled the kernel's time.)
-    if (__hip_atomic_fetch_add(state + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1) {
+    if (__hip_atomic_fetch_add(state + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)vgrid - 1) {
       state[0] = state[1] = 0;
       state[2] = 0;
       if (roll_mode != nullptr) {  // speculation roll (every block read the mode pair before its ticket)
@@ -720,6 +728,49 @@ __global__ void __launch_bounds__(kClassThreads) class_hist_kernel(const uint16_
         roll_mode[1] = 0;
       }
     }
+  }
+}
+
+template <typename T, bool PACKED>
+__global__ void __launch_bounds__(kClassThreads) class_hist_kernel(const uint16_t* __restrict__ codes, int64_t n_pad, int splits,
+                                                                   int64_t* __restrict__ hist, const T* __restrict__ preds, int ld,
+                                                                   const int64_t* __restrict__ target, int64_t n,
+                                                                   const int* __restrict__ bmode, bool speculative,
+                                                                   const int* __restrict__ slow_rows, int* __restrict__ state,
+                                                                   int64_t* __restrict__ confmat, int* __restrict__ code_range,
+                                                                   int* __restrict__ roll_mode) {
+  class_hist_block<T, PACKED, kClassThreads>(blockIdx.x, gridDim.x, codes, n_pad, splits, hist, preds, ld, target, n, bmode, speculative,
+                                             slow_rows, state, confmat, code_range, roll_mode);
+}
+
+// Dual-role launch: the row pass of batch k and the class pass of batch k - 1 (the other scratch buffer) in ONE grid,
+// so the long HBM-bound class blocks run beside the row tiles on every CU instead of after them (two 64-KiB blocks
+// per CU whatever their roles; the side-stream variant could not co-reside, profiles/side_stream_overlap.json).
+// Physical blocks come in groups of 8 (one per XCD); group g is a class group when the even spread of the
+// ``class_groups`` over all ``groups`` says so, and virtual ids keep ``vb % 8`` = the physical XCD, so the row role
+// keeps its XCD-aware tile order.  Class blocks run with the row pass's 512 threads.
+template <typename T, int NG>
+__global__ void __launch_bounds__(kRowThreads, 4) mc_dual_kernel(
+    const T* __restrict__ preds, const int64_t* __restrict__ target, int64_t n, int C, int* __restrict__ mode, int64_t ignore_index,
+    bool has_ignore, uint32_t* __restrict__ codes, int64_t n_pad, int64_t* __restrict__ confmat, int* __restrict__ err,
+    int* __restrict__ slow_rows, int* __restrict__ slow_count, int64_t row_blocks,
+    const uint16_t* __restrict__ pcodes, int64_t pn_pad, int splits, int64_t* __restrict__ hist, const T* __restrict__ ppreds,
+    const int64_t* __restrict__ ptarget, int64_t pn, const int* __restrict__ pbmode, const int* __restrict__ pslow_rows,
+    int* __restrict__ pstate, int64_t* __restrict__ pconfmat, int* __restrict__ code_range, int64_t class_blocks, int64_t groups,
+    int64_t class_groups) {
+  const int64_t g = blockIdx.x / 8, x = blockIdx.x % 8;
+  const int64_t cg_before = g * class_groups / groups;
+  const bool is_class = (g + 1) * class_groups / groups > cg_before;
+  if (is_class) {
+    const int64_t vb = cg_before * 8 + x;
+    if (vb >= class_blocks) return;
+    class_hist_block<T, false, kRowThreads>(vb, class_blocks, pcodes, pn_pad, splits, hist, ppreds, C, ptarget, pn, pbmode, true,
+                                            pslow_rows, pstate, pconfmat, code_range, nullptr);
+  } else {
+    const int64_t vb = (g - cg_before) * 8 + x;
+    if (vb >= row_blocks) return;
+    mc_codes_block<T, false, NG, false>(vb, row_blocks, preds, target, n, C, C, mode, ignore_index, has_ignore, codes, n_pad, confmat,
+                                        err, true, slow_rows, slow_count);
   }
 }
 
