@@ -94,7 +94,17 @@ class BaseAggregator(Metric):
 
 
 class MaxMetric(BaseAggregator):
-    """Running maximum of all values seen."""
+    """Running maximum of all values seen.
+
+    Example:
+        >>> import torch
+        >>> from torchmetrics_forked_amd.aggregation import MaxMetric
+        >>> metric = MaxMetric()
+        >>> metric.update(1)
+        >>> metric.update(torch.tensor([2, 3]))
+        >>> metric.compute()
+        tensor(3.)
+    """
 
     full_state_update: bool = True
     max_value: Tensor
@@ -132,7 +142,17 @@ class MinMetric(BaseAggregator):
 
 
 class SumMetric(BaseAggregator):
-    """Running sum of all values seen."""
+    """Running sum of all values seen.
+
+    Example:
+        >>> import torch
+        >>> from torchmetrics_forked_amd.aggregation import SumMetric
+        >>> metric = SumMetric()
+        >>> metric.update(1)
+        >>> metric.update(torch.tensor([2, 3]))
+        >>> metric.compute()
+        tensor(6.)
+    """
 
     sum_value: Tensor
     _nan_neutral = 0.0
@@ -150,7 +170,17 @@ class SumMetric(BaseAggregator):
 
 
 class CatMetric(BaseAggregator):
-    """Concatenation of all values seen (flattened)."""
+    """Concatenation of all values seen (flattened).
+
+    Example:
+        >>> import torch
+        >>> from torchmetrics_forked_amd.aggregation import CatMetric
+        >>> metric = CatMetric()
+        >>> metric.update(1)
+        >>> metric.update(torch.tensor([2, 3]))
+        >>> metric.compute()
+        tensor([1., 2., 3.])
+    """
 
     def __init__(self, nan_strategy: Union[str, float] = "warn", **kwargs: Any) -> None:
         super().__init__("cat", [], nan_strategy, **kwargs)
@@ -167,7 +197,17 @@ class CatMetric(BaseAggregator):
 
 
 class MeanMetric(BaseAggregator):
-    """(Weighted) running mean: ``sum(value * weight) / sum(weight)``."""
+    """(Weighted) running mean: ``sum(value * weight) / sum(weight)``.
+
+    Example:
+        >>> import torch
+        >>> from torchmetrics_forked_amd.aggregation import MeanMetric
+        >>> metric = MeanMetric()
+        >>> metric.update(1)
+        >>> metric.update(torch.tensor([2, 3]))
+        >>> metric.compute()
+        tensor(2.)
+    """
 
     mean_value: Tensor
     weight: Tensor

@@ -12,7 +12,14 @@ from torchmetrics_forked_amd.functional.audio.snr import (
 
 
 class SignalNoiseRatio(_MeanSignalMetric):
-    """Mean SNR over signals."""
+    """Mean SNR over signals.
+
+    Example:
+        >>> import torch
+        >>> from torchmetrics_forked_amd.audio import SignalNoiseRatio
+        >>> SignalNoiseRatio()(torch.tensor([2.5, 0.0, 2.0, 8.0]), torch.tensor([3.0, -0.5, 2.0, 7.0]))
+        tensor(16.1805)
+    """
 
     _sum_name = "sum_snr"
 

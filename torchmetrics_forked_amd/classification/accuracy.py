@@ -20,7 +20,15 @@ from torchmetrics_forked_amd.utilities.plot import _AX_TYPE, _PLOT_OUT_TYPE
 
 
 class BinaryAccuracy(BinaryStatScores):
-    """Accuracy for binary tasks."""
+    """Accuracy for binary tasks.
+
+    Example:
+        >>> import torch
+        >>> from torchmetrics_forked_amd.classification import BinaryAccuracy
+        >>> metric = BinaryAccuracy()
+        >>> metric(torch.tensor([0.1, 0.8, 0.6, 0.3]), torch.tensor([0, 1, 0, 0]))
+        tensor(0.7500)
+    """
 
     is_differentiable: bool = False
     higher_is_better: Optional[bool] = True
@@ -34,7 +42,18 @@ class BinaryAccuracy(BinaryStatScores):
 
 
 class MulticlassAccuracy(MulticlassStatScores):
-    """Accuracy for multiclass tasks."""
+    """Accuracy for multiclass tasks.
+
+    Example:
+        >>> import torch
+        >>> from torchmetrics_forked_amd.classification import MulticlassAccuracy
+        >>> target = torch.tensor([2, 1, 0, 0])
+        >>> preds = torch.tensor([2, 1, 0, 1])
+        >>> MulticlassAccuracy(num_classes=3)(preds, target)
+        tensor(0.8333)
+        >>> MulticlassAccuracy(num_classes=3, average=None)(preds, target)
+        tensor([0.5000, 1.0000, 1.0000])
+    """
 
     is_differentiable: bool = False
     higher_is_better: Optional[bool] = True
@@ -49,7 +68,16 @@ class MulticlassAccuracy(MulticlassStatScores):
 
 
 class MultilabelAccuracy(MultilabelStatScores):
-    """Accuracy for multilabel tasks."""
+    """Accuracy for multilabel tasks.
+
+    Example:
+        >>> import torch
+        >>> from torchmetrics_forked_amd.classification import MultilabelAccuracy
+        >>> target = torch.tensor([[0, 1, 0], [1, 0, 1]])
+        >>> preds = torch.tensor([[0.2, 0.9, 0.1], [0.7, 0.4, 0.3]])
+        >>> MultilabelAccuracy(num_labels=3)(preds, target)
+        tensor(0.8333)
+    """
 
     is_differentiable: bool = False
     higher_is_better: Optional[bool] = True

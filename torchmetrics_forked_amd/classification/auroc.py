@@ -29,7 +29,15 @@ from torchmetrics_forked_amd.utilities.plot import _AX_TYPE, _PLOT_OUT_TYPE
 
 
 class BinaryAUROC(BinaryPrecisionRecallCurve):
-    """Area under the ROC curve for binary tasks."""
+    """Area under the ROC curve for binary tasks.
+
+    Example:
+        >>> import torch
+        >>> from torchmetrics_forked_amd.classification import BinaryAUROC
+        >>> metric = BinaryAUROC()
+        >>> metric(torch.tensor([0.1, 0.4, 0.35, 0.8]), torch.tensor([0, 0, 1, 1]))
+        tensor(0.7500)
+    """
 
     is_differentiable: bool = False
     higher_is_better: Optional[bool] = True
@@ -59,7 +67,18 @@ class BinaryAUROC(BinaryPrecisionRecallCurve):
 
 
 class MulticlassAUROC(MulticlassPrecisionRecallCurve):
-    """One-vs-rest AUROC for multiclass tasks."""
+    """One-vs-rest AUROC for multiclass tasks.
+
+    Example:
+        >>> import torch
+        >>> from torchmetrics_forked_amd.classification import MulticlassAUROC
+        >>> preds = torch.tensor([[0.75, 0.05, 0.20], [0.05, 0.75, 0.20], [0.05, 0.05, 0.90], [0.20, 0.10, 0.70]])
+        >>> target = torch.tensor([0, 1, 2, 2])
+        >>> MulticlassAUROC(num_classes=3)(preds, target)
+        tensor(1.)
+        >>> MulticlassAUROC(num_classes=3, average=None)(preds, target)
+        tensor([1., 1., 1.])
+    """
 
     is_differentiable: bool = False
     higher_is_better: Optional[bool] = True

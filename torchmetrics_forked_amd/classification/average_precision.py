@@ -54,7 +54,15 @@ class BinaryAveragePrecision(BinaryPrecisionRecallCurve):
 
 
 class MulticlassAveragePrecision(MulticlassPrecisionRecallCurve):
-    """One-vs-rest AveragePrecision for multiclass tasks."""
+    """One-vs-rest AveragePrecision for multiclass tasks.
+
+    Example:
+        >>> import torch
+        >>> from torchmetrics_forked_amd.classification import MulticlassAveragePrecision
+        >>> preds = torch.tensor([[0.75, 0.05, 0.20], [0.05, 0.75, 0.20], [0.05, 0.05, 0.90], [0.20, 0.10, 0.70]])
+        >>> MulticlassAveragePrecision(num_classes=3)(preds, torch.tensor([0, 1, 2, 2]))
+        tensor(1.)
+    """
 
     is_differentiable: bool = False
     higher_is_better: Optional[bool] = True

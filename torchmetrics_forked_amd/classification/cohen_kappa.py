@@ -47,6 +47,14 @@ class BinaryCohenKappa(BinaryConfusionMatrix):
 
 
 class MulticlassCohenKappa(MulticlassConfusionMatrix):
+    """Cohen's kappa for multiclass tasks.
+
+    Example:
+        >>> import torch
+        >>> from torchmetrics_forked_amd.classification import MulticlassCohenKappa
+        >>> MulticlassCohenKappa(num_classes=3)(torch.tensor([2, 1, 0, 1]), torch.tensor([2, 1, 0, 0]))
+        tensor(0.6364)
+    """
     is_differentiable: bool = False
     higher_is_better: bool = True
     full_state_update: bool = False

@@ -78,7 +78,17 @@ class BinaryConfusionMatrix(_ConfmatPlot, Metric):
 
 
 class MulticlassConfusionMatrix(_ConfmatPlot, Metric):
-    """``[C, C]`` confusion matrix for multiclass tasks (fused argmax + LDS histogram on device)."""
+    """``[C, C]`` confusion matrix for multiclass tasks (fused argmax + LDS histogram on device).
+
+    Example:
+        >>> import torch
+        >>> from torchmetrics_forked_amd.classification import MulticlassConfusionMatrix
+        >>> metric = MulticlassConfusionMatrix(num_classes=3)
+        >>> metric(torch.tensor([2, 1, 0, 1]), torch.tensor([2, 1, 0, 0]))
+        tensor([[1, 1, 0],
+                [0, 1, 0],
+                [0, 0, 1]])
+    """
 
     is_differentiable: bool = False
     higher_is_better: Optional[bool] = None

@@ -54,6 +54,16 @@ class _ExactMatchBase(Metric):
 
 
 class MulticlassExactMatch(_ExactMatchBase):
+    """Exact match (all positions correct) for multiclass tasks.
+
+    Example:
+        >>> import torch
+        >>> from torchmetrics_forked_amd.classification import MulticlassExactMatch
+        >>> target = torch.tensor([[[0, 1], [2, 1], [0, 2]], [[1, 1], [2, 0], [1, 2]]])
+        >>> preds = torch.tensor([[[0, 1], [2, 1], [0, 2]], [[2, 2], [2, 1], [1, 0]]])
+        >>> MulticlassExactMatch(num_classes=3, multidim_average='global')(preds, target)
+        tensor(0.5000)
+    """
     def __init__(
         self,
         num_classes: int,

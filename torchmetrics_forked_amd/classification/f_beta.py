@@ -123,7 +123,15 @@ class BinaryF1Score(BinaryFBetaScore):
 
 
 class MulticlassF1Score(MulticlassFBetaScore):
-    """F1 score for multiclass tasks."""
+    """F1 score for multiclass tasks.
+
+    Example:
+        >>> import torch
+        >>> from torchmetrics_forked_amd.classification import MulticlassF1Score
+        >>> metric = MulticlassF1Score(num_classes=3)
+        >>> metric(torch.tensor([2, 1, 0, 1]), torch.tensor([2, 1, 0, 0]))
+        tensor(0.7778)
+    """
 
     def __init__(
         self,

@@ -59,6 +59,17 @@ class BinaryHingeLoss(_HingeBase):
 
 
 class MulticlassHingeLoss(_HingeBase):
+    """Multiclass hinge loss (crammer-singer or one-vs-all).
+
+    Example:
+        >>> import torch
+        >>> from torchmetrics_forked_amd.classification import MulticlassHingeLoss
+        >>> preds = torch.tensor([[0.25, 0.20, 0.55], [0.55, 0.05, 0.40], [0.10, 0.30, 0.60], [0.90, 0.05, 0.05]])
+        >>> MulticlassHingeLoss(num_classes=3)(preds, torch.tensor([0, 1, 2, 0]))
+        tensor(0.9125)
+        >>> MulticlassHingeLoss(num_classes=3, multiclass_mode='one-vs-all')(preds, torch.tensor([0, 1, 2, 0]))
+        tensor([0.8750, 1.1250, 1.1000])
+    """
     def __init__(
         self,
         num_classes: int,

@@ -38,6 +38,14 @@ class BinaryJaccardIndex(_JaccardMixin, BinaryConfusionMatrix):
 
 
 class MulticlassJaccardIndex(_JaccardMixin, MulticlassConfusionMatrix):
+    """Jaccard index (IoU) for multiclass tasks.
+
+    Example:
+        >>> import torch
+        >>> from torchmetrics_forked_amd.classification import MulticlassJaccardIndex
+        >>> MulticlassJaccardIndex(num_classes=3)(torch.tensor([2, 1, 0, 1]), torch.tensor([2, 1, 0, 0]))
+        tensor(0.6667)
+    """
     def __init__(
         self,
         num_classes: int,

@@ -38,6 +38,14 @@ class BinaryMatthewsCorrCoef(_MCCMixin, BinaryConfusionMatrix):
 
 
 class MulticlassMatthewsCorrCoef(_MCCMixin, MulticlassConfusionMatrix):
+    """Matthews correlation coefficient for multiclass tasks.
+
+    Example:
+        >>> import torch
+        >>> from torchmetrics_forked_amd.classification import MulticlassMatthewsCorrCoef
+        >>> MulticlassMatthewsCorrCoef(num_classes=3)(torch.tensor([2, 1, 0, 1]), torch.tensor([2, 1, 0, 0]))
+        tensor(0.7000)
+    """
     def __init__(
         self, num_classes: int, ignore_index: Optional[int] = None, validate_args: bool = True, **kwargs: Any
     ) -> None:

@@ -35,7 +35,15 @@ class BinaryPrecision(BinaryStatScores):
 
 
 class MulticlassPrecision(MulticlassStatScores):
-    """Precision for multiclass tasks."""
+    """Precision for multiclass tasks.
+
+    Example:
+        >>> import torch
+        >>> from torchmetrics_forked_amd.classification import MulticlassPrecision
+        >>> metric = MulticlassPrecision(num_classes=3, average='micro')
+        >>> metric(torch.tensor([2, 1, 0, 1]), torch.tensor([2, 1, 0, 0]))
+        tensor(0.7500)
+    """
 
     is_differentiable: bool = False
     higher_is_better: Optional[bool] = True
@@ -103,7 +111,15 @@ class BinaryRecall(BinaryStatScores):
 
 
 class MulticlassRecall(MulticlassStatScores):
-    """Recall for multiclass tasks."""
+    """Recall for multiclass tasks.
+
+    Example:
+        >>> import torch
+        >>> from torchmetrics_forked_amd.classification import MulticlassRecall
+        >>> metric = MulticlassRecall(num_classes=3, average=None)
+        >>> metric(torch.tensor([2, 1, 0, 1]), torch.tensor([2, 1, 0, 0]))
+        tensor([0.5000, 1.0000, 1.0000])
+    """
 
     is_differentiable: bool = False
     higher_is_better: Optional[bool] = True

@@ -526,7 +526,17 @@ class _CurveMetric(Metric):
 
 
 class BinaryPrecisionRecallCurve(_CurveMetric):
-    """Precision-recall curve for binary tasks."""
+    """Precision-recall curve for binary tasks.
+
+    Example:
+        >>> import torch
+        >>> from torchmetrics_forked_amd.classification import BinaryPrecisionRecallCurve
+        >>> precision, recall, thresholds = BinaryPrecisionRecallCurve()(torch.tensor([0.0, 0.5, 0.7, 0.8]), torch.tensor([0, 1, 1, 0]))
+        >>> precision
+        tensor([0.5000, 0.6667, 0.5000, 0.0000, 1.0000])
+        >>> recall
+        tensor([1.0000, 1.0000, 0.5000, 0.0000, 0.0000])
+    """
 
     _task = "binary"
 

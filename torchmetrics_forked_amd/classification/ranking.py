@@ -63,6 +63,15 @@ class MultilabelRankingAveragePrecision(_RankingBase):
 
 
 class MultilabelRankingLoss(_RankingBase):
+    """Label ranking loss for multilabel tasks.
+
+    Example:
+        >>> import torch
+        >>> from torchmetrics_forked_amd.classification import MultilabelRankingLoss
+        >>> preds = torch.tensor([[0.9, 0.2, 0.6], [0.1, 0.8, 0.4], [0.5, 0.3, 0.7]])
+        >>> MultilabelRankingLoss(num_labels=3)(preds, torch.tensor([[1, 0, 0], [0, 0, 1], [1, 1, 0]]))
+        tensor(0.5000)
+    """
     higher_is_better: bool = False
     plot_lower_bound: float = 0.0
     _update_fn = staticmethod(_multilabel_ranking_loss_update)

@@ -34,7 +34,14 @@ class BinarySpecificity(BinaryStatScores):
 
 
 class MulticlassSpecificity(MulticlassStatScores):
-    """Specificity for multiclass tasks."""
+    """Specificity for multiclass tasks.
+
+    Example:
+        >>> import torch
+        >>> from torchmetrics_forked_amd.classification import MulticlassSpecificity
+        >>> MulticlassSpecificity(num_classes=3)(torch.tensor([2, 1, 0, 1]), torch.tensor([2, 1, 0, 0]))
+        tensor(0.8889)
+    """
 
     is_differentiable: bool = False
     higher_is_better: Optional[bool] = True

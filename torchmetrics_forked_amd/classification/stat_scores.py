@@ -146,7 +146,17 @@ class BinaryStatScores(_AbstractStatScores):
 
 
 class MulticlassStatScores(_AbstractStatScores):
-    """tp / fp / tn / fn / support for multiclass tasks."""
+    """tp / fp / tn / fn / support for multiclass tasks.
+
+    Example:
+        >>> import torch
+        >>> from torchmetrics_forked_amd.classification import MulticlassStatScores
+        >>> metric = MulticlassStatScores(num_classes=3, average=None)
+        >>> metric(torch.tensor([2, 1, 0, 1]), torch.tensor([2, 1, 0, 0]))
+        tensor([[1, 0, 2, 1, 2],
+                [1, 1, 2, 0, 1],
+                [1, 0, 3, 0, 1]])
+    """
 
     is_differentiable: bool = False
     higher_is_better: Optional[bool] = None

@@ -172,6 +172,14 @@ class MultiScaleStructuralSimilarityIndexMeasure(_ImageMetric):
 
 
 class PeakSignalNoiseRatio(_ImageMetric):
+    """Peak signal-to-noise ratio.
+
+    Example:
+        >>> import torch
+        >>> from torchmetrics_forked_amd.image import PeakSignalNoiseRatio
+        >>> PeakSignalNoiseRatio()(torch.tensor([[0.0, 1.0], [2.0, 3.0]]), torch.tensor([[3.0, 2.0], [1.0, 0.0]]))
+        tensor(2.5527)
+    """
     higher_is_better: bool = True
     plot_lower_bound: float = 0.0
 

@@ -44,6 +44,14 @@ class _ContingencyMetric(Metric):
 
 
 class CramersV(_ContingencyMetric):
+    """Cramer's V association between two categorical series.
+
+    Example:
+        >>> import torch
+        >>> from torchmetrics_forked_amd.nominal import CramersV
+        >>> CramersV(num_classes=3)(torch.tensor([0, 1, 2, 2, 1, 0, 1, 2]), torch.tensor([0, 1, 2, 1, 1, 0, 0, 2]))
+        tensor(0.5477)
+    """
     def __init__(self, num_classes: int, bias_correction: bool = True, nan_strategy: Literal["replace", "drop"] = "replace",
                  nan_replace_value: Optional[float] = 0.0, **kwargs: Any) -> None:
         super().__init__(num_classes, nan_strategy, nan_replace_value, **kwargs)

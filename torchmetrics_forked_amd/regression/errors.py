@@ -35,6 +35,14 @@ from torchmetrics_forked_amd.utilities.exceptions import TorchMetricsUserError
 
 
 class MeanSquaredError(_RegressionMetric):
+    """Mean squared error.
+
+    Example:
+        >>> import torch
+        >>> from torchmetrics_forked_amd.regression import MeanSquaredError
+        >>> MeanSquaredError()(torch.tensor([2.5, 5.0, 4.0, 8.0]), torch.tensor([3.0, 5.0, 2.5, 7.0]))
+        tensor(0.8750)
+    """
     higher_is_better = False
     plot_lower_bound: float = 0.0
 
@@ -71,6 +79,14 @@ class MeanSquaredError(_RegressionMetric):
 
 
 class MeanAbsoluteError(_RegressionMetric):
+    """Mean absolute error.
+
+    Example:
+        >>> import torch
+        >>> from torchmetrics_forked_amd.regression import MeanAbsoluteError
+        >>> MeanAbsoluteError()(torch.tensor([2.5, 0.0, 2.0, 8.0]), torch.tensor([3.0, -0.5, 2.0, 7.0]))
+        tensor(0.5000)
+    """
     higher_is_better = False
     plot_lower_bound: float = 0.0
 

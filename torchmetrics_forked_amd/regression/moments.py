@@ -23,6 +23,14 @@ from torchmetrics_forked_amd.regression._base import _RegressionMetric
 
 
 class R2Score(_RegressionMetric):
+    """Coefficient of determination.
+
+    Example:
+        >>> import torch
+        >>> from torchmetrics_forked_amd.regression import R2Score
+        >>> R2Score()(torch.tensor([2.5, 0.0, 2.0, 8.0]), torch.tensor([3.0, -0.5, 2.0, 7.0]))
+        tensor(0.9486)
+    """
     higher_is_better = True
     plot_upper_bound: float = 1.0
 
@@ -76,6 +84,14 @@ class RelativeSquaredError(_RegressionMetric):
 
 
 class ExplainedVariance(_RegressionMetric):
+    """Explained variance.
+
+    Example:
+        >>> import torch
+        >>> from torchmetrics_forked_amd.regression import ExplainedVariance
+        >>> ExplainedVariance()(torch.tensor([2.5, 0.0, 2.0, 8.0]), torch.tensor([3.0, -0.5, 2.0, 7.0]))
+        tensor(0.9572)
+    """
     higher_is_better = True
     plot_upper_bound: float = 1.0
 
@@ -128,7 +144,14 @@ def _final_aggregation(
 
 class PearsonCorrCoef(_RegressionMetric):
     """Streaming Pearson correlation.  States are per-rank Welford moments with ``dist_reduce_fx=None``: the sync
-    engine gathers all six in one packed collective and ``compute`` folds them with ``_final_aggregation``."""
+    engine gathers all six in one packed collective and ``compute`` folds them with ``_final_aggregation``.
+
+    Example:
+        >>> import torch
+        >>> from torchmetrics_forked_amd.regression import PearsonCorrCoef
+        >>> PearsonCorrCoef()(torch.tensor([2.5, 0.0, 2.0, 8.0]), torch.tensor([3.0, -0.5, 2.0, 7.0]))
+        tensor(0.9849)
+    """
 
     higher_is_better = None
     full_state_update: bool = True

@@ -24,6 +24,14 @@ from torchmetrics_forked_amd.utilities.prints import rank_zero_warn
 
 
 class SpearmanCorrCoef(_RegressionMetric):
+    """Spearman rank correlation coefficient.
+
+    Example:
+        >>> import torch
+        >>> from torchmetrics_forked_amd.regression import SpearmanCorrCoef
+        >>> SpearmanCorrCoef()(torch.tensor([2.5, 0.0, 2.0, 8.0]), torch.tensor([3.0, -0.5, 2.0, 7.0]))
+        tensor(1.0000)
+    """
     is_differentiable = False
     higher_is_better = True
     plot_lower_bound: float = -1.0
@@ -51,6 +59,14 @@ class SpearmanCorrCoef(_RegressionMetric):
 
 
 class KendallRankCorrCoef(_RegressionMetric):
+    """Kendall rank correlation coefficient (tau-a / b / c).
+
+    Example:
+        >>> import torch
+        >>> from torchmetrics_forked_amd.regression import KendallRankCorrCoef
+        >>> KendallRankCorrCoef()(torch.tensor([2.5, 0.0, 2.0, 8.0]), torch.tensor([3.0, -0.5, 2.0, 7.0]))
+        tensor(1.)
+    """
     is_differentiable = False
     higher_is_better = None
     full_state_update = True

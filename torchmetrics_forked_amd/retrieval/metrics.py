@@ -19,6 +19,17 @@ class _Bounded(RetrievalMetric):
 
 
 class RetrievalMAP(_Bounded):
+    """Mean average precision over queries.
+
+    Example:
+        >>> import torch
+        >>> from torchmetrics_forked_amd.retrieval import RetrievalMAP
+        >>> indexes = torch.tensor([0, 0, 0, 1, 1, 1, 1])
+        >>> preds = torch.tensor([0.2, 0.3, 0.5, 0.1, 0.3, 0.5, 0.2])
+        >>> target = torch.tensor([False, False, True, False, True, False, True])
+        >>> RetrievalMAP()(preds, target, indexes=indexes)
+        tensor(0.7917)
+    """
     def __init__(self, empty_target_action: str = "neg", ignore_index: Optional[int] = None, top_k: Optional[int] = None, **kwargs: Any) -> None:
         super().__init__(empty_target_action=empty_target_action, ignore_index=ignore_index, **kwargs)
         if top_k is not None and not isinstance(top_k, int) and top_k <= 0:
@@ -30,6 +41,17 @@ class RetrievalMAP(_Bounded):
 
 
 class RetrievalMRR(_Bounded):
+    """Mean reciprocal rank over queries.
+
+    Example:
+        >>> import torch
+        >>> from torchmetrics_forked_amd.retrieval import RetrievalMRR
+        >>> indexes = torch.tensor([0, 0, 0, 1, 1, 1, 1])
+        >>> preds = torch.tensor([0.2, 0.3, 0.5, 0.1, 0.3, 0.5, 0.2])
+        >>> target = torch.tensor([False, False, True, False, True, False, True])
+        >>> RetrievalMRR()(preds, target, indexes=indexes)
+        tensor(0.7500)
+    """
     def __init__(self, empty_target_action: str = "neg", ignore_index: Optional[int] = None, top_k: Optional[int] = None, **kwargs: Any) -> None:
         super().__init__(empty_target_action=empty_target_action, ignore_index=ignore_index, **kwargs)
         if top_k is not None and not isinstance(top_k, int) and top_k <= 0:
@@ -99,6 +121,17 @@ class RetrievalRPrecision(_Bounded):
 
 
 class RetrievalNormalizedDCG(_Bounded):
+    """Normalized discounted cumulative gain over queries.
+
+    Example:
+        >>> import torch
+        >>> from torchmetrics_forked_amd.retrieval import RetrievalNormalizedDCG
+        >>> indexes = torch.tensor([0, 0, 0, 1, 1, 1, 1])
+        >>> preds = torch.tensor([0.2, 0.3, 0.5, 0.1, 0.3, 0.5, 0.2])
+        >>> target = torch.tensor([0, 0, 2, 0, 1, 0, 3])
+        >>> RetrievalNormalizedDCG()(preds, target, indexes=indexes)
+        tensor(0.7934)
+    """
     def __init__(self, empty_target_action: str = "neg", ignore_index: Optional[int] = None, top_k: Optional[int] = None, **kwargs: Any) -> None:
         super().__init__(empty_target_action=empty_target_action, ignore_index=ignore_index, **kwargs)
         _check_top_k(top_k)

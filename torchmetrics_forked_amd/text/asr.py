@@ -43,11 +43,23 @@ class _ErrorsOverTotal(Metric):
 
 
 class WordErrorRate(_ErrorsOverTotal):
-    """Word error rate."""
+    """Word error rate.
+
+    Example:
+        >>> from torchmetrics_forked_amd.text import WordErrorRate
+        >>> WordErrorRate()(['this is the prediction', 'there is an other sample'], ['this is the reference', 'there is another one'])
+        tensor(0.5000)
+    """
 
 
 class CharErrorRate(_ErrorsOverTotal):
-    """Character error rate."""
+    """Character error rate.
+
+    Example:
+        >>> from torchmetrics_forked_amd.text import CharErrorRate
+        >>> CharErrorRate()(['this is the prediction', 'there is an other sample'], ['this is the reference', 'there is another one'])
+        tensor(0.3415)
+    """
 
     _update_fn = staticmethod(_cer_update)
     _compute_fn = staticmethod(_cer_compute)

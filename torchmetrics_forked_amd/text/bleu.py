@@ -11,7 +11,13 @@ from torchmetrics_forked_amd.utilities.plot import _AX_TYPE, _PLOT_OUT_TYPE
 
 
 class BLEUScore(Metric):
-    """Corpus BLEU (``sum`` states: lengths and clipped / total n-gram counts)."""
+    """Corpus BLEU (``sum`` states: lengths and clipped / total n-gram counts).
+
+    Example:
+        >>> from torchmetrics_forked_amd.text import BLEUScore
+        >>> BLEUScore()(['the squirrel is eating the nut'], [['a squirrel is eating a nut', 'the squirrel is eating a tasty nut']])
+        tensor(0.5373)
+    """
 
     is_differentiable: bool = False
     higher_is_better: bool = True

@@ -14,7 +14,13 @@ from torchmetrics_forked_amd.utilities.plot import _AX_TYPE, _PLOT_OUT_TYPE
 
 
 class EditDistance(Metric):
-    """Levenshtein distance with configurable substitution cost."""
+    """Levenshtein distance with configurable substitution cost.
+
+    Example:
+        >>> from torchmetrics_forked_amd.text import EditDistance
+        >>> EditDistance()(['rain'], ['shine'])
+        tensor(3.)
+    """
 
     higher_is_better: bool = False
     is_differentiable: bool = False
