@@ -175,6 +175,114 @@ SPECS: List[Tuple[str, str, str, List[str]]] = [
         "CramersV(num_classes=3)(torch.tensor([0, 1, 2, 2, 1, 0, 1, 2]), torch.tensor([0, 1, 2, 1, 1, 0, 0, 2]))"]),
 ]
 
+BP = "preds = torch.tensor([0.1, 0.8, 0.6, 0.3, 0.9, 0.2])"
+BT = "target = torch.tensor([0, 1, 0, 0, 1, 1])"
+MP = "preds = torch.tensor([2, 1, 0, 1, 2, 0])"
+MT = "target = torch.tensor([2, 1, 0, 0, 1, 0])"
+LP = "preds = torch.tensor([[0.2, 0.9, 0.1], [0.7, 0.4, 0.3], [0.6, 0.8, 0.9]])"
+LT = "target = torch.tensor([[0, 1, 0], [1, 0, 1], [1, 1, 0]])"
+RP = "preds = torch.tensor([2.5, 0.0, 2.0, 8.0, 4.2])"
+RT = "target = torch.tensor([3.0, 0.5, 2.0, 7.0, 4.0])"
+
+
+def _bin(cls, call="metric(preds, target)", kw=""):
+    return ("classification", cls, f"{cls} (binary task).", [T, f"from torchmetrics_forked_amd.classification import {cls}", BP, BT,
+                                                               f"metric = {cls}({kw})", call])
+
+
+def _mc(cls, kw="num_classes=3", call="metric(preds, target)"):
+    return ("classification", cls, f"{cls} (multiclass task).", [T, f"from torchmetrics_forked_amd.classification import {cls}", MP, MT,
+                                                                   f"metric = {cls}({kw})", call])
+
+
+def _ml(cls, kw="num_labels=3", call="metric(preds, target)"):
+    return ("classification", cls, f"{cls} (multilabel task).", [T, f"from torchmetrics_forked_amd.classification import {cls}", LP, LT,
+                                                                   f"metric = {cls}({kw})", call])
+
+
+def _reg(cls, call="metric(preds, target)", kw="", pre=()):
+    return ("regression", cls, f"{cls}.", [T, f"from torchmetrics_forked_amd.regression import {cls}", *pre, RP, RT, f"metric = {cls}({kw})", call])
+
+
+def _clu(cls, kw=""):
+    return ("clustering", cls, f"{cls}.", [T, f"from torchmetrics_forked_amd.clustering import {cls}",
+                                           "preds = torch.tensor([2, 1, 0, 1, 0, 2])", "target = torch.tensor([0, 2, 1, 1, 0, 2])",
+                                           f"{cls}({kw})(preds, target)"])
+
+
+def _ret(cls, kw=""):
+    return ("retrieval", cls, f"{cls} over queries.", [T, f"from torchmetrics_forked_amd.retrieval import {cls}",
+                                                       "indexes = torch.tensor([0, 0, 0, 1, 1, 1, 1])",
+                                                       "preds = torch.tensor([0.2, 0.3, 0.5, 0.1, 0.3, 0.5, 0.2])",
+                                                       "target = torch.tensor([False, False, True, False, True, False, True])",
+                                                       f"{cls}({kw})(preds, target, indexes=indexes)"])
+
+
+SPECS += [
+    _bin("BinaryF1Score"), _bin("BinaryPrecision"), _bin("BinaryRecall"), _bin("BinarySpecificity"), _bin("BinaryConfusionMatrix"),
+    _bin("BinaryAveragePrecision"), _bin("BinaryCalibrationError", kw="n_bins=2"), _bin("BinaryHingeLoss"), _bin("BinaryCohenKappa"),
+    _bin("BinaryMatthewsCorrCoef"), _bin("BinaryJaccardIndex"), _bin("BinaryStatScores"), _bin("BinaryHammingDistance"),
+    _bin("BinaryFBetaScore", kw="beta=2.0"), _bin("BinaryPrecisionAtFixedRecall", kw="min_recall=0.5"),
+    _bin("BinaryRecallAtFixedPrecision", kw="min_precision=0.5"), _bin("BinarySpecificityAtSensitivity", kw="min_sensitivity=0.5"),
+    _mc("MulticlassHammingDistance"), _mc("MulticlassFBetaScore", kw="num_classes=3, beta=0.5"), _mc("MulticlassExactMatch", call="metric(preds.reshape(2, 3), target.reshape(2, 3))"),
+    _ml("MultilabelF1Score"), _ml("MultilabelPrecision"), _ml("MultilabelRecall"), _ml("MultilabelAUROC", kw="num_labels=3, average=None"),
+    _ml("MultilabelConfusionMatrix"), _ml("MultilabelCoverageError"), _ml("MultilabelRankingAveragePrecision"), _ml("MultilabelHammingDistance"),
+    _ml("MultilabelAveragePrecision", kw="num_labels=3, average=None"), _ml("MultilabelExactMatch"), _ml("MultilabelStatScores", kw="num_labels=3, average=None"),
+    _reg("MeanSquaredLogError"), _reg("MeanAbsolutePercentageError"), _reg("SymmetricMeanAbsolutePercentageError"),
+    _reg("WeightedMeanAbsolutePercentageError"), _reg("LogCoshError"), _reg("MinkowskiDistance", kw="p=3"),
+    _reg("TweedieDevianceScore", kw="power=0.0"), _reg("ConcordanceCorrCoef"), _reg("RelativeSquaredError"), _reg("CosineSimilarity", kw="reduction='mean'", call="metric(preds.reshape(1, -1), target.reshape(1, -1))"),
+    ("regression", "KLDivergence", "KL divergence between distributions.", [T, "from torchmetrics_forked_amd.regression import KLDivergence",
+        "p = torch.tensor([[0.36, 0.48, 0.16]])", "q = torch.tensor([[1 / 3, 1 / 3, 1 / 3]])", "KLDivergence()(p, q)"]),
+    _clu("RandScore"), _clu("NormalizedMutualInfoScore"), _clu("AdjustedMutualInfoScore"), _clu("FowlkesMallowsIndex"),
+    _clu("HomogeneityScore"), _clu("CompletenessScore"), _clu("VMeasureScore"),
+    ("clustering", "CalinskiHarabaszScore", "Calinski-Harabasz score of a clustering.", [T, "from torchmetrics_forked_amd.clustering import CalinskiHarabaszScore",
+        "data = torch.tensor([[0.0, 0.1], [0.2, 0.0], [5.0, 5.1], [5.2, 4.9], [9.9, 0.1], [10.1, 0.0]])", "labels = torch.tensor([0, 0, 1, 1, 2, 2])",
+        "CalinskiHarabaszScore()(data, labels)"]),
+    ("clustering", "DaviesBouldinScore", "Davies-Bouldin score of a clustering.", [T, "from torchmetrics_forked_amd.clustering import DaviesBouldinScore",
+        "data = torch.tensor([[0.0, 0.1], [0.2, 0.0], [5.0, 5.1], [5.2, 4.9], [9.9, 0.1], [10.1, 0.0]])", "labels = torch.tensor([0, 0, 1, 1, 2, 2])",
+        "DaviesBouldinScore()(data, labels)"]),
+    _ret("RetrievalPrecision", kw="top_k=2"), _ret("RetrievalRecall", kw="top_k=2"), _ret("RetrievalFallOut", kw="top_k=2"),
+    _ret("RetrievalHitRate", kw="top_k=2"), _ret("RetrievalRPrecision"),
+    ("nominal", "TschuprowsT", "Tschuprow's T association.", [T, "from torchmetrics_forked_amd.nominal import TschuprowsT",
+        "TschuprowsT(num_classes=3)(torch.tensor([0, 1, 2, 2, 1, 0, 1, 2]), torch.tensor([0, 1, 2, 1, 1, 0, 0, 2]))"]),
+    ("nominal", "PearsonsContingencyCoefficient", "Pearson's contingency coefficient.", [T, "from torchmetrics_forked_amd.nominal import PearsonsContingencyCoefficient",
+        "PearsonsContingencyCoefficient(num_classes=3)(torch.tensor([0, 1, 2, 2, 1, 0, 1, 2]), torch.tensor([0, 1, 2, 1, 1, 0, 0, 2]))"]),
+    ("nominal", "TheilsU", "Theil's U (uncertainty coefficient).", [T, "from torchmetrics_forked_amd.nominal import TheilsU",
+        "TheilsU(num_classes=3)(torch.tensor([0, 1, 2, 2, 1, 0, 1, 2]), torch.tensor([0, 1, 2, 1, 1, 0, 0, 2]))"]),
+    ("text", "MatchErrorRate", "Match error rate.", ["from torchmetrics_forked_amd.text import MatchErrorRate",
+        "MatchErrorRate()(['this is the prediction', 'there is an other sample'], ['this is the reference', 'there is another one'])"]),
+    ("text", "WordInfoLost", "Word information lost.", ["from torchmetrics_forked_amd.text import WordInfoLost",
+        "WordInfoLost()(['this is the prediction', 'there is an other sample'], ['this is the reference', 'there is another one'])"]),
+    ("text", "CHRFScore", "chrF score of a corpus.", ["from torchmetrics_forked_amd.text import CHRFScore",
+        "CHRFScore()(['the cat is on the mat'], [['there is a cat on the mat', 'a cat is on the mat']])"]),
+    ("text", "TranslationEditRate", "Translation edit rate.", ["from torchmetrics_forked_amd.text import TranslationEditRate",
+        "TranslationEditRate()(['the cat is on the mat'], [['there is a cat on the mat', 'a cat is on the mat']])"]),
+    ("text", "SacreBLEUScore", "SacreBLEU score of a corpus.", ["from torchmetrics_forked_amd.text import SacreBLEUScore",
+        "SacreBLEUScore()(['the squirrel is eating the nut'], [['a squirrel is eating a nut', 'the squirrel is eating a tasty nut']])"]),
+    ("image", "StructuralSimilarityIndexMeasure", "Structural similarity index.", [T, "from torchmetrics_forked_amd.image import StructuralSimilarityIndexMeasure",
+        "preds = torch.linspace(0, 1, 2 * 3 * 16 * 16).reshape(2, 3, 16, 16)", "target = preds.flip(-1) * 0.75",
+        "StructuralSimilarityIndexMeasure(data_range=1.0)(preds, target)"]),
+    ("image", "UniversalImageQualityIndex", "Universal image quality index.", [T, "from torchmetrics_forked_amd.image import UniversalImageQualityIndex",
+        "preds = torch.linspace(0, 1, 2 * 3 * 16 * 16).reshape(2, 3, 16, 16)", "target = preds.flip(-1) * 0.75",
+        "UniversalImageQualityIndex()(preds, target)"]),
+    ("image", "TotalVariation", "Total variation of images.", [T, "from torchmetrics_forked_amd.image import TotalVariation",
+        "img = torch.linspace(0, 1, 2 * 3 * 8 * 8).reshape(2, 3, 8, 8)", "TotalVariation()(img)"]),
+    ("detection", "IntersectionOverUnion", "Box IoU for object detection.", [T, "from torchmetrics_forked_amd.detection import IntersectionOverUnion",
+        "preds = [{'boxes': torch.tensor([[296.55, 93.96, 314.97, 152.79], [298.55, 98.96, 314.97, 151.79]]), 'labels': torch.tensor([4, 5])}]",
+        "target = [{'boxes': torch.tensor([[300.00, 100.00, 315.00, 150.00]]), 'labels': torch.tensor([5])}]",
+        "IntersectionOverUnion()(preds, target)"]),
+    ("audio", "ScaleInvariantSignalNoiseRatio", "Scale-invariant signal-to-noise ratio.", [T, "from torchmetrics_forked_amd.audio import ScaleInvariantSignalNoiseRatio",
+        RP, RT, "ScaleInvariantSignalNoiseRatio()(preds, target)"]),
+    ("wrappers", "MinMaxMetric", "Tracks the min and max of a base metric's value.", [T, "from torchmetrics_forked_amd.wrappers import MinMaxMetric",
+        "from torchmetrics_forked_amd.classification import BinaryAccuracy", "metric = MinMaxMetric(BinaryAccuracy())",
+        "metric.update(torch.tensor([0.9, 0.2]), torch.tensor([1, 0]))", "metric.compute()",
+        "metric.update(torch.tensor([0.9, 0.8]), torch.tensor([0, 0]))", "metric.compute()"]),
+    ("wrappers", "ClasswiseWrapper", "Splits a per-class metric output into a dict.", [T, "from torchmetrics_forked_amd.wrappers import ClasswiseWrapper",
+        "from torchmetrics_forked_amd.classification import MulticlassAccuracy",
+        "metric = ClasswiseWrapper(MulticlassAccuracy(num_classes=3, average=None), labels=['cat', 'dog', 'fish'])",
+        "metric(torch.tensor([2, 1, 0, 1]), torch.tensor([2, 1, 0, 0]))"]),
+]
+
 
 def _run(lines: List[str]) -> List[str]:
     """Execute the example lines; returns the doctest text (``>>>`` lines + expected outputs)."""
@@ -193,9 +301,9 @@ def _run(lines: List[str]) -> List[str]:
             res = eval(code, ns) if is_expr else exec(code, ns)  # noqa: S307 - our own example lines
         printed = buf.getvalue().rstrip("\n")
         if printed:
-            out.extend(printed.splitlines())
+            out.extend(r if r.strip() else "<BLANKLINE>" for r in printed.splitlines())
         if is_expr and res is not None:
-            out.extend(repr(res).splitlines())
+            out.extend(r if r.strip() else "<BLANKLINE>" for r in repr(res).splitlines())
     return out
 
 

@@ -32,7 +32,16 @@ class SignalNoiseRatio(_MeanSignalMetric):
 
 
 class ScaleInvariantSignalNoiseRatio(_MeanSignalMetric):
-    """Mean SI-SNR over signals."""
+    """Mean SI-SNR over signals.
+
+    Example:
+        >>> import torch
+        >>> from torchmetrics_forked_amd.audio import ScaleInvariantSignalNoiseRatio
+        >>> preds = torch.tensor([2.5, 0.0, 2.0, 8.0, 4.2])
+        >>> target = torch.tensor([3.0, 0.5, 2.0, 7.0, 4.0])
+        >>> ScaleInvariantSignalNoiseRatio()(preds, target)
+        tensor(20.6068)
+    """
 
     _sum_name = "sum_si_snr"
 

@@ -117,7 +117,17 @@ class MulticlassAUROC(MulticlassPrecisionRecallCurve):
 
 
 class MultilabelAUROC(MultilabelPrecisionRecallCurve):
-    """Per-label AUROC (optionally averaged)."""
+    """Per-label AUROC (optionally averaged).
+
+    Example:
+        >>> import torch
+        >>> from torchmetrics_forked_amd.classification import MultilabelAUROC
+        >>> preds = torch.tensor([[0.2, 0.9, 0.1], [0.7, 0.4, 0.3], [0.6, 0.8, 0.9]])
+        >>> target = torch.tensor([[0, 1, 0], [1, 0, 1], [1, 1, 0]])
+        >>> metric = MultilabelAUROC(num_labels=3, average=None)
+        >>> metric(preds, target)
+        tensor([1.0000, 1.0000, 0.5000])
+    """
 
     is_differentiable: bool = False
     higher_is_better: Optional[bool] = True

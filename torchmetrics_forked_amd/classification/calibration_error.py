@@ -48,6 +48,17 @@ class _CalibrationBase(Metric):
 
 
 class BinaryCalibrationError(_CalibrationBase):
+    """BinaryCalibrationError (binary task).
+
+    Example:
+        >>> import torch
+        >>> from torchmetrics_forked_amd.classification import BinaryCalibrationError
+        >>> preds = torch.tensor([0.1, 0.8, 0.6, 0.3, 0.9, 0.2])
+        >>> target = torch.tensor([0, 1, 0, 0, 1, 1])
+        >>> metric = BinaryCalibrationError(n_bins=2)
+        >>> metric(preds, target)
+        tensor(0.1167)
+    """
     def __init__(
         self,
         n_bins: int = 15,

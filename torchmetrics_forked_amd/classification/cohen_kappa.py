@@ -19,6 +19,17 @@ from torchmetrics_forked_amd.utilities.plot import _AX_TYPE, _PLOT_OUT_TYPE
 
 
 class BinaryCohenKappa(BinaryConfusionMatrix):
+    """BinaryCohenKappa (binary task).
+
+    Example:
+        >>> import torch
+        >>> from torchmetrics_forked_amd.classification import BinaryCohenKappa
+        >>> preds = torch.tensor([0.1, 0.8, 0.6, 0.3, 0.9, 0.2])
+        >>> target = torch.tensor([0, 1, 0, 0, 1, 1])
+        >>> metric = BinaryCohenKappa()
+        >>> metric(preds, target)
+        tensor(0.3333)
+    """
     is_differentiable: bool = False
     higher_is_better: bool = True
     full_state_update: bool = False

@@ -91,6 +91,17 @@ class MulticlassExactMatch(_ExactMatchBase):
 
 
 class MultilabelExactMatch(_ExactMatchBase):
+    """MultilabelExactMatch (multilabel task).
+
+    Example:
+        >>> import torch
+        >>> from torchmetrics_forked_amd.classification import MultilabelExactMatch
+        >>> preds = torch.tensor([[0.2, 0.9, 0.1], [0.7, 0.4, 0.3], [0.6, 0.8, 0.9]])
+        >>> target = torch.tensor([[0, 1, 0], [1, 0, 1], [1, 1, 0]])
+        >>> metric = MultilabelExactMatch(num_labels=3)
+        >>> metric(preds, target)
+        tensor(0.3333)
+    """
     def __init__(
         self,
         num_labels: int,

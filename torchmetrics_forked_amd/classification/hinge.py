@@ -37,6 +37,17 @@ class _HingeBase(Metric):
 
 
 class BinaryHingeLoss(_HingeBase):
+    """BinaryHingeLoss (binary task).
+
+    Example:
+        >>> import torch
+        >>> from torchmetrics_forked_amd.classification import BinaryHingeLoss
+        >>> preds = torch.tensor([0.1, 0.8, 0.6, 0.3, 0.9, 0.2])
+        >>> target = torch.tensor([0, 1, 0, 0, 1, 1])
+        >>> metric = BinaryHingeLoss()
+        >>> metric(preds, target)
+        tensor(0.8500)
+    """
     def __init__(
         self, squared: bool = False, ignore_index: Optional[int] = None, validate_args: bool = True, **kwargs: Any
     ) -> None:

@@ -28,6 +28,17 @@ class _JaccardMixin:
 
 
 class BinaryJaccardIndex(_JaccardMixin, BinaryConfusionMatrix):
+    """BinaryJaccardIndex (binary task).
+
+    Example:
+        >>> import torch
+        >>> from torchmetrics_forked_amd.classification import BinaryJaccardIndex
+        >>> preds = torch.tensor([0.1, 0.8, 0.6, 0.3, 0.9, 0.2])
+        >>> target = torch.tensor([0, 1, 0, 0, 1, 1])
+        >>> metric = BinaryJaccardIndex()
+        >>> metric(preds, target)
+        tensor(0.5000)
+    """
     def __init__(
         self, threshold: float = 0.5, ignore_index: Optional[int] = None, validate_args: bool = True, **kwargs: Any
     ) -> None:

@@ -20,7 +20,17 @@ from torchmetrics_forked_amd.utilities.plot import _AX_TYPE, _PLOT_OUT_TYPE
 
 
 class BinarySpecificity(BinaryStatScores):
-    """Specificity for binary tasks."""
+    """Specificity for binary tasks.
+
+    Example:
+        >>> import torch
+        >>> from torchmetrics_forked_amd.classification import BinarySpecificity
+        >>> preds = torch.tensor([0.1, 0.8, 0.6, 0.3, 0.9, 0.2])
+        >>> target = torch.tensor([0, 1, 0, 0, 1, 1])
+        >>> metric = BinarySpecificity()
+        >>> metric(preds, target)
+        tensor(0.6667)
+    """
 
     is_differentiable: bool = False
     higher_is_better: Optional[bool] = True

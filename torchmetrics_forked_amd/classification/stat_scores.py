@@ -100,7 +100,17 @@ class _AbstractStatScores(Metric):
 
 
 class BinaryStatScores(_AbstractStatScores):
-    """tp / fp / tn / fn / support for binary tasks."""
+    """tp / fp / tn / fn / support for binary tasks.
+
+    Example:
+        >>> import torch
+        >>> from torchmetrics_forked_amd.classification import BinaryStatScores
+        >>> preds = torch.tensor([0.1, 0.8, 0.6, 0.3, 0.9, 0.2])
+        >>> target = torch.tensor([0, 1, 0, 0, 1, 1])
+        >>> metric = BinaryStatScores()
+        >>> metric(preds, target)
+        tensor([2, 1, 2, 1, 3])
+    """
 
     is_differentiable: bool = False
     higher_is_better: Optional[bool] = None
@@ -264,7 +274,19 @@ class MulticlassStatScores(_AbstractStatScores):
 
 
 class MultilabelStatScores(_AbstractStatScores):
-    """tp / fp / tn / fn / support for multilabel tasks."""
+    """tp / fp / tn / fn / support for multilabel tasks.
+
+    Example:
+        >>> import torch
+        >>> from torchmetrics_forked_amd.classification import MultilabelStatScores
+        >>> preds = torch.tensor([[0.2, 0.9, 0.1], [0.7, 0.4, 0.3], [0.6, 0.8, 0.9]])
+        >>> target = torch.tensor([[0, 1, 0], [1, 0, 1], [1, 1, 0]])
+        >>> metric = MultilabelStatScores(num_labels=3, average=None)
+        >>> metric(preds, target)
+        tensor([[2, 0, 1, 0, 2],
+                [2, 0, 1, 0, 2],
+                [0, 1, 1, 1, 1]])
+    """
 
     is_differentiable: bool = False
     higher_is_better: Optional[bool] = None

@@ -58,6 +58,16 @@ class MutualInfoScore(_ExtrinsicClustering):
 
 
 class NormalizedMutualInfoScore(MutualInfoScore):
+    """NormalizedMutualInfoScore.
+
+    Example:
+        >>> import torch
+        >>> from torchmetrics_forked_amd.clustering import NormalizedMutualInfoScore
+        >>> preds = torch.tensor([2, 1, 0, 1, 0, 2])
+        >>> target = torch.tensor([0, 2, 1, 1, 0, 2])
+        >>> NormalizedMutualInfoScore()(preds, target)
+        tensor(0.3691)
+    """
     higher_is_better = None
     plot_upper_bound: float = 0.0
     _fn = staticmethod(F.normalized_mutual_info_score)
@@ -72,11 +82,31 @@ class NormalizedMutualInfoScore(MutualInfoScore):
 
 
 class AdjustedMutualInfoScore(NormalizedMutualInfoScore):
+    """AdjustedMutualInfoScore.
+
+    Example:
+        >>> import torch
+        >>> from torchmetrics_forked_amd.clustering import AdjustedMutualInfoScore
+        >>> preds = torch.tensor([2, 1, 0, 1, 0, 2])
+        >>> target = torch.tensor([0, 2, 1, 1, 0, 2])
+        >>> AdjustedMutualInfoScore()(preds, target)
+        tensor(-0.2500)
+    """
     plot_upper_bound: float = 1.0
     _fn = staticmethod(F.adjusted_mutual_info_score)
 
 
 class RandScore(_ExtrinsicClustering):
+    """RandScore.
+
+    Example:
+        >>> import torch
+        >>> from torchmetrics_forked_amd.clustering import RandScore
+        >>> preds = torch.tensor([2, 1, 0, 1, 0, 2])
+        >>> target = torch.tensor([0, 2, 1, 1, 0, 2])
+        >>> RandScore()(preds, target)
+        tensor(0.6000)
+    """
     higher_is_better = None
     full_state_update: bool = True
     _fn = staticmethod(F.rand_score)
@@ -99,21 +129,61 @@ class AdjustedRandScore(_ExtrinsicClustering):
 
 
 class FowlkesMallowsIndex(_ExtrinsicClustering):
+    """FowlkesMallowsIndex.
+
+    Example:
+        >>> import torch
+        >>> from torchmetrics_forked_amd.clustering import FowlkesMallowsIndex
+        >>> preds = torch.tensor([2, 1, 0, 1, 0, 2])
+        >>> target = torch.tensor([0, 2, 1, 1, 0, 2])
+        >>> FowlkesMallowsIndex()(preds, target)
+        tensor(0.)
+    """
     plot_upper_bound: float = 1.0
     _fn = staticmethod(F.fowlkes_mallows_index)
 
 
 class HomogeneityScore(_ExtrinsicClustering):
+    """HomogeneityScore.
+
+    Example:
+        >>> import torch
+        >>> from torchmetrics_forked_amd.clustering import HomogeneityScore
+        >>> preds = torch.tensor([2, 1, 0, 1, 0, 2])
+        >>> target = torch.tensor([0, 2, 1, 1, 0, 2])
+        >>> HomogeneityScore()(preds, target)
+        tensor(0.3691)
+    """
     plot_upper_bound: float = 1.0
     _fn = staticmethod(F.homogeneity_score)
 
 
 class CompletenessScore(_ExtrinsicClustering):
+    """CompletenessScore.
+
+    Example:
+        >>> import torch
+        >>> from torchmetrics_forked_amd.clustering import CompletenessScore
+        >>> preds = torch.tensor([2, 1, 0, 1, 0, 2])
+        >>> target = torch.tensor([0, 2, 1, 1, 0, 2])
+        >>> CompletenessScore()(preds, target)
+        tensor(0.3691)
+    """
     plot_upper_bound: float = 1.0
     _fn = staticmethod(F.completeness_score)
 
 
 class VMeasureScore(_ExtrinsicClustering):
+    """VMeasureScore.
+
+    Example:
+        >>> import torch
+        >>> from torchmetrics_forked_amd.clustering import VMeasureScore
+        >>> preds = torch.tensor([2, 1, 0, 1, 0, 2])
+        >>> target = torch.tensor([0, 2, 1, 1, 0, 2])
+        >>> VMeasureScore()(preds, target)
+        tensor(0.3691)
+    """
     plot_upper_bound: float = 1.0
     _fn = staticmethod(F.v_measure_score)
 
@@ -154,10 +224,30 @@ class _IntrinsicClustering(Metric):
 
 
 class CalinskiHarabaszScore(_IntrinsicClustering):
+    """Calinski-Harabasz score of a clustering.
+
+    Example:
+        >>> import torch
+        >>> from torchmetrics_forked_amd.clustering import CalinskiHarabaszScore
+        >>> data = torch.tensor([[0.0, 0.1], [0.2, 0.0], [5.0, 5.1], [5.2, 4.9], [9.9, 0.1], [10.1, 0.0]])
+        >>> labels = torch.tensor([0, 0, 1, 1, 2, 2])
+        >>> CalinskiHarabaszScore()(data, labels)
+        tensor(2178.0535)
+    """
     _fn = staticmethod(F.calinski_harabasz_score)
 
 
 class DaviesBouldinScore(_IntrinsicClustering):
+    """Davies-Bouldin score of a clustering.
+
+    Example:
+        >>> import torch
+        >>> from torchmetrics_forked_amd.clustering import DaviesBouldinScore
+        >>> data = torch.tensor([[0.0, 0.1], [0.2, 0.0], [5.0, 5.1], [5.2, 4.9], [9.9, 0.1], [10.1, 0.0]])
+        >>> labels = torch.tensor([0, 0, 1, 1, 2, 2])
+        >>> DaviesBouldinScore()(data, labels)
+        tensor(0.0362)
+    """
     _fn = staticmethod(F.davies_bouldin_score)
 
 

@@ -23,7 +23,16 @@ from torchmetrics_forked_amd.utilities.plot import _AX_TYPE, _PLOT_OUT_TYPE
 
 
 class IntersectionOverUnion(Metric):
-    """Mean IoU between predicted and ground-truth boxes (optionally per ground-truth class)."""
+    """Mean IoU between predicted and ground-truth boxes (optionally per ground-truth class).
+
+    Example:
+        >>> import torch
+        >>> from torchmetrics_forked_amd.detection import IntersectionOverUnion
+        >>> preds = [{'boxes': torch.tensor([[296.55, 93.96, 314.97, 152.79], [298.55, 98.96, 314.97, 151.79]]), 'labels': torch.tensor([4, 5])}]
+        >>> target = [{'boxes': torch.tensor([[300.00, 100.00, 315.00, 150.00]]), 'labels': torch.tensor([5])}]
+        >>> IntersectionOverUnion()(preds, target)
+        {'iou': tensor(0.8614)}
+    """
 
     is_differentiable: bool = False
     higher_is_better: Optional[bool] = True

@@ -62,6 +62,14 @@ class CramersV(_ContingencyMetric):
 
 
 class TschuprowsT(_ContingencyMetric):
+    """Tschuprow's T association.
+
+    Example:
+        >>> import torch
+        >>> from torchmetrics_forked_amd.nominal import TschuprowsT
+        >>> TschuprowsT(num_classes=3)(torch.tensor([0, 1, 2, 2, 1, 0, 1, 2]), torch.tensor([0, 1, 2, 1, 1, 0, 0, 2]))
+        tensor(0.5477)
+    """
     def __init__(self, num_classes: int, bias_correction: bool = True, nan_strategy: Literal["replace", "drop"] = "replace",
                  nan_replace_value: Optional[float] = 0.0, **kwargs: Any) -> None:
         super().__init__(num_classes, nan_strategy, nan_replace_value, **kwargs)
@@ -72,11 +80,27 @@ class TschuprowsT(_ContingencyMetric):
 
 
 class PearsonsContingencyCoefficient(_ContingencyMetric):
+    """Pearson's contingency coefficient.
+
+    Example:
+        >>> import torch
+        >>> from torchmetrics_forked_amd.nominal import PearsonsContingencyCoefficient
+        >>> PearsonsContingencyCoefficient(num_classes=3)(torch.tensor([0, 1, 2, 2, 1, 0, 1, 2]), torch.tensor([0, 1, 2, 1, 1, 0, 0, 2]))
+        tensor(0.7071)
+    """
     def compute(self) -> Tensor:
         return _pearsons_contingency_coefficient_compute(self.confmat)
 
 
 class TheilsU(_ContingencyMetric):
+    """Theil's U (uncertainty coefficient).
+
+    Example:
+        >>> import torch
+        >>> from torchmetrics_forked_amd.nominal import TheilsU
+        >>> TheilsU(num_classes=3)(torch.tensor([0, 1, 2, 2, 1, 0, 1, 2]), torch.tensor([0, 1, 2, 1, 1, 0, 0, 2]))
+        tensor(0.5589)
+    """
     def compute(self) -> Tensor:
         return _theils_u_compute(self.confmat)
 

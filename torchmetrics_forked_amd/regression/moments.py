@@ -61,6 +61,17 @@ class R2Score(_RegressionMetric):
 
 
 class RelativeSquaredError(_RegressionMetric):
+    """RelativeSquaredError.
+
+    Example:
+        >>> import torch
+        >>> from torchmetrics_forked_amd.regression import RelativeSquaredError
+        >>> preds = torch.tensor([2.5, 0.0, 2.0, 8.0, 4.2])
+        >>> target = torch.tensor([3.0, 0.5, 2.0, 7.0, 4.0])
+        >>> metric = RelativeSquaredError()
+        >>> metric(preds, target)
+        tensor(0.0647)
+    """
     higher_is_better = False
 
     def __init__(self, num_outputs: int = 1, squared: bool = True, **kwargs: Any) -> None:
@@ -185,6 +196,17 @@ class PearsonCorrCoef(_RegressionMetric):
 
 
 class ConcordanceCorrCoef(PearsonCorrCoef):
+    """ConcordanceCorrCoef.
+
+    Example:
+        >>> import torch
+        >>> from torchmetrics_forked_amd.regression import ConcordanceCorrCoef
+        >>> preds = torch.tensor([2.5, 0.0, 2.0, 8.0, 4.2])
+        >>> target = torch.tensor([3.0, 0.5, 2.0, 7.0, 4.0])
+        >>> metric = ConcordanceCorrCoef()
+        >>> metric(preds, target)
+        tensor(0.9743)
+    """
     higher_is_better = True
 
     def compute(self) -> Tensor:

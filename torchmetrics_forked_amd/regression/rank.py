@@ -101,6 +101,17 @@ class KendallRankCorrCoef(_RegressionMetric):
 
 
 class CosineSimilarity(_RegressionMetric):
+    """CosineSimilarity.
+
+    Example:
+        >>> import torch
+        >>> from torchmetrics_forked_amd.regression import CosineSimilarity
+        >>> preds = torch.tensor([2.5, 0.0, 2.0, 8.0, 4.2])
+        >>> target = torch.tensor([3.0, 0.5, 2.0, 7.0, 4.0])
+        >>> metric = CosineSimilarity(reduction='mean')
+        >>> metric(preds.reshape(1, -1), target.reshape(1, -1))
+        tensor(0.9941)
+    """
     higher_is_better = True
     plot_lower_bound: float = 0.0
 
@@ -123,6 +134,16 @@ class CosineSimilarity(_RegressionMetric):
 
 
 class KLDivergence(_RegressionMetric):
+    """KL divergence between distributions.
+
+    Example:
+        >>> import torch
+        >>> from torchmetrics_forked_amd.regression import KLDivergence
+        >>> p = torch.tensor([[0.36, 0.48, 0.16]])
+        >>> q = torch.tensor([[1 / 3, 1 / 3, 1 / 3]])
+        >>> KLDivergence()(p, q)
+        tensor(0.0853)
+    """
     higher_is_better = False
     plot_lower_bound: float = 0.0
 

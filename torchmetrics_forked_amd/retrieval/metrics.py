@@ -63,6 +63,17 @@ class RetrievalMRR(_Bounded):
 
 
 class RetrievalPrecision(_Bounded):
+    """RetrievalPrecision over queries.
+
+    Example:
+        >>> import torch
+        >>> from torchmetrics_forked_amd.retrieval import RetrievalPrecision
+        >>> indexes = torch.tensor([0, 0, 0, 1, 1, 1, 1])
+        >>> preds = torch.tensor([0.2, 0.3, 0.5, 0.1, 0.3, 0.5, 0.2])
+        >>> target = torch.tensor([False, False, True, False, True, False, True])
+        >>> RetrievalPrecision(top_k=2)(preds, target, indexes=indexes)
+        tensor(0.5000)
+    """
     def __init__(
         self,
         empty_target_action: str = "neg",
@@ -83,6 +94,17 @@ class RetrievalPrecision(_Bounded):
 
 
 class RetrievalRecall(_Bounded):
+    """RetrievalRecall over queries.
+
+    Example:
+        >>> import torch
+        >>> from torchmetrics_forked_amd.retrieval import RetrievalRecall
+        >>> indexes = torch.tensor([0, 0, 0, 1, 1, 1, 1])
+        >>> preds = torch.tensor([0.2, 0.3, 0.5, 0.1, 0.3, 0.5, 0.2])
+        >>> target = torch.tensor([False, False, True, False, True, False, True])
+        >>> RetrievalRecall(top_k=2)(preds, target, indexes=indexes)
+        tensor(0.7500)
+    """
     def __init__(self, empty_target_action: str = "neg", ignore_index: Optional[int] = None, top_k: Optional[int] = None, **kwargs: Any) -> None:
         super().__init__(empty_target_action=empty_target_action, ignore_index=ignore_index, **kwargs)
         _check_top_k(top_k)
@@ -93,6 +115,17 @@ class RetrievalRecall(_Bounded):
 
 
 class RetrievalFallOut(_Bounded):
+    """RetrievalFallOut over queries.
+
+    Example:
+        >>> import torch
+        >>> from torchmetrics_forked_amd.retrieval import RetrievalFallOut
+        >>> indexes = torch.tensor([0, 0, 0, 1, 1, 1, 1])
+        >>> preds = torch.tensor([0.2, 0.3, 0.5, 0.1, 0.3, 0.5, 0.2])
+        >>> target = torch.tensor([False, False, True, False, True, False, True])
+        >>> RetrievalFallOut(top_k=2)(preds, target, indexes=indexes)
+        tensor(0.5000)
+    """
     higher_is_better: bool = False
     _empty_on_negatives = True
 
@@ -106,6 +139,17 @@ class RetrievalFallOut(_Bounded):
 
 
 class RetrievalHitRate(_Bounded):
+    """RetrievalHitRate over queries.
+
+    Example:
+        >>> import torch
+        >>> from torchmetrics_forked_amd.retrieval import RetrievalHitRate
+        >>> indexes = torch.tensor([0, 0, 0, 1, 1, 1, 1])
+        >>> preds = torch.tensor([0.2, 0.3, 0.5, 0.1, 0.3, 0.5, 0.2])
+        >>> target = torch.tensor([False, False, True, False, True, False, True])
+        >>> RetrievalHitRate(top_k=2)(preds, target, indexes=indexes)
+        tensor(1.)
+    """
     def __init__(self, empty_target_action: str = "neg", ignore_index: Optional[int] = None, top_k: Optional[int] = None, **kwargs: Any) -> None:
         super().__init__(empty_target_action=empty_target_action, ignore_index=ignore_index, **kwargs)
         _check_top_k(top_k)
@@ -116,6 +160,17 @@ class RetrievalHitRate(_Bounded):
 
 
 class RetrievalRPrecision(_Bounded):
+    """RetrievalRPrecision over queries.
+
+    Example:
+        >>> import torch
+        >>> from torchmetrics_forked_amd.retrieval import RetrievalRPrecision
+        >>> indexes = torch.tensor([0, 0, 0, 1, 1, 1, 1])
+        >>> preds = torch.tensor([0.2, 0.3, 0.5, 0.1, 0.3, 0.5, 0.2])
+        >>> target = torch.tensor([False, False, True, False, True, False, True])
+        >>> RetrievalRPrecision()(preds, target, indexes=indexes)
+        tensor(0.7500)
+    """
     def _per_query(self, g: G.Grouped) -> Tensor:
         return G.per_query_r_precision(g)
 

@@ -66,7 +66,13 @@ class CharErrorRate(_ErrorsOverTotal):
 
 
 class MatchErrorRate(_ErrorsOverTotal):
-    """Match error rate."""
+    """Match error rate.
+
+    Example:
+        >>> from torchmetrics_forked_amd.text import MatchErrorRate
+        >>> MatchErrorRate()(['this is the prediction', 'there is an other sample'], ['this is the reference', 'there is another one'])
+        tensor(0.4444)
+    """
 
     _update_fn = staticmethod(_mer_update)
     _compute_fn = staticmethod(_mer_compute)
@@ -103,7 +109,13 @@ class _WordInfo(Metric):
 
 
 class WordInfoLost(_WordInfo):
-    """Word information lost."""
+    """Word information lost.
+
+    Example:
+        >>> from torchmetrics_forked_amd.text import WordInfoLost
+        >>> WordInfoLost()(['this is the prediction', 'there is an other sample'], ['this is the reference', 'there is another one'])
+        tensor(0.6528)
+    """
 
     higher_is_better: bool = False
 

@@ -57,7 +57,13 @@ class BLEUScore(Metric):
 
 
 class SacreBLEUScore(BLEUScore):
-    """BLEU with sacrebleu tokenisation."""
+    """BLEU with sacrebleu tokenisation.
+
+    Example:
+        >>> from torchmetrics_forked_amd.text import SacreBLEUScore
+        >>> SacreBLEUScore()(['the squirrel is eating the nut'], [['a squirrel is eating a nut', 'the squirrel is eating a tasty nut']])
+        tensor(0.5373)
+    """
 
     def __init__(
         self,

@@ -16,7 +16,13 @@ _TEXT_LEVELS = ("preds", "target", "matching")
 
 
 class CHRFScore(Metric):
-    """chrF (``n_word_order=0``) / chrF++ (``n_word_order=2``)."""
+    """chrF (``n_word_order=0``) / chrF++ (``n_word_order=2``).
+
+    Example:
+        >>> from torchmetrics_forked_amd.text import CHRFScore
+        >>> CHRFScore()(['the cat is on the mat'], [['there is a cat on the mat', 'a cat is on the mat']])
+        tensor(0.8640)
+    """
 
     is_differentiable: bool = False
     higher_is_better: bool = True

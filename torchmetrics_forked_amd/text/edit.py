@@ -108,7 +108,13 @@ class ExtendedEditDistance(Metric):
 
 
 class TranslationEditRate(Metric):
-    """Corpus TER (Tercom semantics)."""
+    """Corpus TER (Tercom semantics).
+
+    Example:
+        >>> from torchmetrics_forked_amd.text import TranslationEditRate
+        >>> TranslationEditRate()(['the cat is on the mat'], [['there is a cat on the mat', 'a cat is on the mat']])
+        tensor(0.1538)
+    """
 
     is_differentiable: bool = False
     higher_is_better: bool = False

@@ -9,6 +9,16 @@ from torchmetrics_forked_amd.wrappers.abstract import WrapperMetric
 
 
 class ClasswiseWrapper(WrapperMetric):
+    """Splits a per-class metric output into a dict.
+
+    Example:
+        >>> import torch
+        >>> from torchmetrics_forked_amd.wrappers import ClasswiseWrapper
+        >>> from torchmetrics_forked_amd.classification import MulticlassAccuracy
+        >>> metric = ClasswiseWrapper(MulticlassAccuracy(num_classes=3, average=None), labels=['cat', 'dog', 'fish'])
+        >>> metric(torch.tensor([2, 1, 0, 1]), torch.tensor([2, 1, 0, 0]))
+        {'multiclassaccuracy_cat': tensor(0.5000), 'multiclassaccuracy_dog': tensor(1.), 'multiclassaccuracy_fish': tensor(1.)}
+    """
     def __init__(
         self, metric: Metric, labels: Optional[List[str]] = None, prefix: Optional[str] = None, postfix: Optional[str] = None
     ) -> None:

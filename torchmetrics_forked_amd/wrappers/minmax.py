@@ -10,6 +10,20 @@ from torchmetrics_forked_amd.wrappers.abstract import WrapperMetric
 
 
 class MinMaxMetric(WrapperMetric):
+    """Tracks the min and max of a base metric's value.
+
+    Example:
+        >>> import torch
+        >>> from torchmetrics_forked_amd.wrappers import MinMaxMetric
+        >>> from torchmetrics_forked_amd.classification import BinaryAccuracy
+        >>> metric = MinMaxMetric(BinaryAccuracy())
+        >>> metric.update(torch.tensor([0.9, 0.2]), torch.tensor([1, 0]))
+        >>> metric.compute()
+        {'raw': tensor(1.), 'max': tensor(1.), 'min': tensor(1.)}
+        >>> metric.update(torch.tensor([0.9, 0.8]), torch.tensor([0, 0]))
+        >>> metric.compute()
+        {'raw': tensor(0.5000), 'max': tensor(1.), 'min': tensor(0.5000)}
+    """
     full_state_update: Optional[bool] = True
     min_val: Tensor
     max_val: Tensor
