@@ -779,3 +779,29 @@ def test_dual_role_update_matches_sequential(C, members, monkeypatch):
         torch.testing.assert_close(a[k], b[k], rtol=0, atol=0, msg=k)
     assert torch.equal(sa[0], sb[0]) and torch.equal(sa[1], sb[1])
     assert sa[2].keys() == sb[2].keys() and all(torch.equal(sa[2][k], sb[2][k]) for k in sa[2])
+
+
+@pytest.mark.parametrize("strategy", ["warn", "ignore", "error"])
+def test_cat_metric_gpu_defers_nan_drop(strategy):
+    """CatMetric on the GPU: no host sync per update (NaN policy as a device flag, NaN entries dropped once by the
+    first state consumer), same result as the CPU metric, including across forward() and state_dict()."""
+    import warnings
+
+    import torchmetrics_forked_amd as tm
+
+    xs = [torch.tensor([1.0, float("nan"), 3.0]), torch.tensor([4.0]), torch.tensor([float("nan"), 6.0])]
+    mg, mc = tm.aggregation.CatMetric(nan_strategy=strategy).cuda(), tm.aggregation.CatMetric(nan_strategy=strategy)
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        if strategy == "error":
+            mg.update(xs[0].cuda())
+            with pytest.raises(RuntimeError, match="nan"):
+                mg.compute()
+            return
+        mg.update(xs[0].cuda())
+        out_fwd = mg(xs[1].cuda())
+        mg.update(xs[2].cuda())
+        for x in xs:
+            mc.update(x)
+        assert torch.equal(out_fwd.cpu(), torch.tensor([4.0]))
+        assert torch.equal(mg.compute().cpu(), mc.compute())

@@ -186,9 +186,32 @@ class CatMetric(BaseAggregator):
         super().__init__("cat", [], nan_strategy, **kwargs)
 
     def update(self, value: Union[float, Tensor]) -> None:
-        value, _ = self._cast_and_nan_check_input(value)
-        if value.numel():
-            self.value.append(value)
+        x = self._as_float_tensor(value)
+        sink = self._validation_sink(x) if isinstance(self.nan_strategy, str) and x.is_cuda else None
+        if sink is None:
+            value, _ = self._cast_and_nan_check_input(value)
+            if value.numel():
+                self.value.append(value)
+            return
+        # GPU, deferred validation: no host sync per update.  The NaN policy becomes a device flag (raised / warned
+        # at compute) and NaN entries are dropped once, by the first consumer of the state (``_join_side_work``),
+        # instead of by a boolean index (two host syncs) per update.
+        if not x.numel():
+            return
+        bad = torch.isnan(x)
+        if self.nan_strategy == "error":
+            sink.add(bad, RuntimeError, "Encountered `nan` values in tensor")
+        elif self.nan_strategy == "warn":
+            sink.add(bad, UserWarning, "Encountered `nan` values in tensor. Will be removed.")
+        self.value.append(x.float())
+        if self.nan_strategy in ("warn", "ignore"):
+            self.__dict__["_side_event"] = self._drop_pending_nans
+
+    def _drop_pending_nans(self) -> None:
+        """Remove the NaN entries appended by deferred updates (one boolean index over the concatenated state)."""
+        if isinstance(self.value, list) and self.value:
+            cat = dim_zero_cat(self.value)
+            self.value = [cat[~torch.isnan(cat)]]
 
     def compute(self) -> Tensor:
         if isinstance(self.value, list) and self.value:

@@ -258,6 +258,7 @@ class Metric(Module, ABC):
             raise TorchMetricsUserError(
                 "The Metric shouldn't be synced when performing ``forward``. HINT: Did you forget to call ``unsync`` ?."
             )
+        self._join_side_work()  # pending state work (side-stream passes, deferred NaN drops) before states are cached
         full = self.full_state_update or self.full_state_update is None or self.dist_sync_on_step
         if self._deferred is None:
             self._forward_cache = (self._forward_full_state_update if full else self._forward_reduce_state_update)(*args, **kwargs)
