@@ -165,3 +165,19 @@ def test_expected_mutual_info_kernel_vs_fp64_oracle():
     ref = expected_mutual_info_score(cont, n).double()  # CPU: masked fp64 tensor expression
     got = expected_mutual_info(cont.sum(1).double().cuda(), cont.sum(0).double().cuda(), n).cpu()
     assert abs(float(got) - float(ref)) <= 1e-6 * max(1.0, abs(float(ref)))
+
+
+@pytest.mark.parametrize("C", [3, 17, 200])
+@pytest.mark.parametrize("kind", ["roc", "pr"])
+def test_macro_curve_interp_gpu_vs_cpu(C, kind):
+    """Macro-averaged ROC / PR curves: one csrc/interp.hip launch over all classes vs the per-class interp loop."""
+    g = torch.Generator().manual_seed(C)
+    x = torch.randn(3000, C, generator=g).softmax(1)
+    x = (x * 50).round() / 50  # ties: repeated curve points and zero-width segments
+    t = torch.randint(0, C, (3000,), generator=g)
+    fn = F.multiclass_roc if kind == "roc" else F.multiclass_precision_recall_curve
+    for thresholds in (None, 50):
+        cpu = fn(x, t, num_classes=C, average="macro", thresholds=thresholds)
+        gpu = fn(x.cuda(), t.cuda(), num_classes=C, average="macro", thresholds=thresholds)
+        for a, b in zip(gpu, cpu):
+            torch.testing.assert_close(a.cpu(), b, rtol=1e-6, atol=1e-6)

@@ -99,3 +99,24 @@ def interp(x: Tensor, xp: Tensor, fp: Tensor) -> Tensor:
     idx = torch.searchsorted(torch.sort(xp).values.contiguous(), x.contiguous(), right=True) - 1
     idx = idx.clamp(0, slope.numel() - 1)
     return slope[idx] * x + intercept[idx]
+
+
+def macro_interp_sum(x: Tensor, xps: "list", fps: "list") -> "Optional[Tensor]":
+    """Sum over the curves ``(xps[c], fps[c])`` of ``interp(x, xps[c], fps[c])`` in one GPU launch
+    (csrc/interp.hip); ``None`` when the inputs do not qualify (CPU, non-fp32), so the caller keeps its loop."""
+    from torchmetrics_forked_amd import ops
+
+    if not (x.is_cuda and x.dtype == torch.float32 and ops.use_native(x)):
+        return None
+    if any(t.dtype != torch.float32 or not t.is_cuda for t in list(xps) + list(fps)):
+        return None
+    lens = torch.tensor([0] + [t.numel() for t in xps], dtype=torch.long)
+    off = torch.cumsum(lens, 0).to(x.device)
+    xp = torch.cat([t.reshape(-1) for t in xps])
+    fp = torch.cat([t.reshape(-1) for t in fps])
+    cls = torch.repeat_interleave(torch.arange(len(xps), device=x.device), lens[1:].to(x.device))
+    # every class's values sorted inside its segment: stable sort by value, then stable by class
+    o1 = torch.sort(xp, stable=True).indices
+    o2 = torch.sort(cls[o1], stable=True).indices
+    xs = xp[o1[o2]]
+    return torch.ops.tmx.macro_interp(x, xp, fp, xs, off)
