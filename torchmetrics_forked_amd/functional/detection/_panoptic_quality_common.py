@@ -15,6 +15,8 @@ from typing import Collection, Dict, Optional, Set, Tuple
 import torch
 from torch import Tensor
 
+from torchmetrics_forked_amd import ops
+
 from torchmetrics_forked_amd.utilities.prints import rank_zero_warn
 
 
@@ -100,6 +102,23 @@ def _segments(flat: Tensor, cat_idx: Tensor) -> Tuple[Tensor, Tensor, Tensor]:
     return inv, uniq[:, 1], area
 
 
+def _segments_native(fp: Tensor, ft: Tensor, id_t: Tensor, cont_t: Tensor, k: int) -> Optional[Tuple[Tuple[Tensor, ...], ...]]:
+    """GPU: one csrc/panoptic.hip pass packs (image, category index, instance) of every pixel into an ordered int64
+    key; segments come from a 1-D unique of the keys (same order as the row unique).  ``None`` -> row path."""
+    if not (fp.is_cuda and fp.dtype == torch.long and ft.dtype == torch.long and ops.use_native(fp)):
+        return None
+    if fp.shape[0] >= 32768 or k >= 65535 or id_t.numel() > 4096:
+        return None
+    pkey, tkey, overflow = torch.ops.tmx.panoptic_segment_keys(fp, ft, id_t, cont_t)
+    if int(overflow.item()):
+        return None
+    out = []
+    for key in (pkey, tkey):
+        uniq, inv, area = torch.unique(key, sorted=True, return_inverse=True, return_counts=True)
+        out.append((inv, (uniq >> 32) & 0xFFFF, area))
+    return tuple(out)
+
+
 def _panoptic_quality_update(
     flatten_preds: Tensor,
     flatten_target: Tensor,
@@ -133,8 +152,12 @@ def _panoptic_quality_update(
         hit = id_t[pos] == cat
         return torch.where(hit, cont_t[pos], torch.full_like(cat, k))
 
-    p_inv, p_cat, p_area = _segments(flatten_preds, to_idx(flatten_preds[..., 0]))
-    t_inv, t_cat, t_area = _segments(flatten_target, to_idx(flatten_target[..., 0]))
+    segs = _segments_native(flatten_preds, flatten_target, id_t, cont_t, k)
+    if segs is not None:
+        (p_inv, p_cat, p_area), (t_inv, t_cat, t_area) = segs
+    else:
+        p_inv, p_cat, p_area = _segments(flatten_preds, to_idx(flatten_preds[..., 0]))
+        t_inv, t_cat, t_area = _segments(flatten_target, to_idx(flatten_target[..., 0]))
     n_p, n_t = p_cat.numel(), t_cat.numel()
     pair, inter_all = torch.unique(p_inv * n_t + t_inv, return_counts=True)
     ps, ts = pair // n_t, pair % n_t
