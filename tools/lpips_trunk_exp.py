@@ -39,6 +39,7 @@ def main():
     with torch.no_grad():
         ref = net(torch.cat([a[:2], b[:2]]))
         out["nchw_ms"] = round(timed(lambda: (net(a), net(b))), 2)
+        print(json.dumps(out), flush=True)
         out["nchw_cat_ms"] = round(timed(lambda: net(torch.cat([a, b]))), 2)
         net_cl = vgg16_features().eval().to(dev)
         net_cl.load_state_dict(net.state_dict())
@@ -47,6 +48,10 @@ def main():
         out["nhwc_cat_ms"] = round(timed(lambda: net_cl(ab_cl)), 2)
         got = net_cl(torch.cat([a[:2], b[:2]]).contiguous(memory_format=torch.channels_last))
         out["nhwc_max_rel_diff"] = float(((got - ref).abs().max() / ref.abs().max()))
+        print(json.dumps(out), flush=True)
+        if os.environ.get("LPIPS_BENCHMARK_MODE", "0") != "1":  # MIOpen exhaustive find at 1024^2 ran > 3 min silent
+            print(json.dumps(out), flush=True)
+            return
         torch.backends.cudnn.benchmark = True
         t0 = time.perf_counter()
         net(torch.cat([a, b]))

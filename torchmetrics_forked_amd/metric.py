@@ -37,6 +37,7 @@ from torchmetrics_forked_amd.utilities.data import (
     dim_zero_min,
     dim_zero_sum,
 )
+from torchmetrics_forked_amd.utilities.arena import StateArena
 from torchmetrics_forked_amd.utilities.distributed import gather_all_tensors
 from torchmetrics_forked_amd.utilities.exceptions import TorchMetricsUserError
 
@@ -245,7 +246,7 @@ class Metric(Module, ABC):
             raise ValueError("`dist_reduce_fx` must be callable or one of ['mean', 'sum', 'cat', 'min', 'max', None]")
         if isinstance(default, Tensor):
             default = default.contiguous()
-        setattr(self, name, default)
+        setattr(self, name, default if isinstance(default, Tensor) else StateArena())
         self._defaults[name] = deepcopy(default)
         self._persistent[name] = persistent
         self._reductions[name] = fx
@@ -371,7 +372,11 @@ class Metric(Module, ABC):
                 if isinstance(glob, Tensor) and isinstance(local, Tensor):
                     merged = torch.cat([glob, local])
                 else:
-                    merged = list(glob) + list(local) if isinstance(glob, list) else glob + local
+                    merged = (StateArena(glob) if not isinstance(glob, StateArena) else glob) if isinstance(glob, list) else glob
+                    if isinstance(merged, list):
+                        merged.extend(local)
+                    else:
+                        merged = merged + local
             elif fx is None and isinstance(glob, Tensor):
                 merged = torch.stack([glob, local])
             elif fx is None and isinstance(glob, list):
@@ -566,7 +571,7 @@ class Metric(Module, ABC):
                 dev = current.device if isinstance(current, Tensor) else default.device
                 setattr(self, name, default.detach().clone().to(dev))
             else:
-                setattr(self, name, [])
+                setattr(self, name, StateArena())
         self._cache = None
         self._is_synced = False
         if self._deferred is not None:
@@ -628,7 +633,7 @@ class Metric(Module, ABC):
             if isinstance(current, Tensor):
                 setattr(this, key, fn(current))
             elif isinstance(current, Sequence):
-                setattr(this, key, [fn(v) for v in current])
+                setattr(this, key, StateArena(fn(v) for v in current) if isinstance(current, StateArena) else [fn(v) for v in current])
             else:
                 raise TypeError(
                     f"Expected metric state to be either a Tensor or a list of Tensor, but encountered {current}"
@@ -656,6 +661,9 @@ class Metric(Module, ABC):
             if not keep_vars:
                 if isinstance(val, Tensor):
                     val = val.detach()
+                elif isinstance(val, StateArena):  # one storage per item, as the reference's lists
+                    destination[prefix + key] = val.compact_items()
+                    continue
                 elif isinstance(val, list):
                     val = [v.detach() if isinstance(v, Tensor) else v for v in val]
             destination[prefix + key] = deepcopy(val)

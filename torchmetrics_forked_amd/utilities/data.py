@@ -11,6 +11,8 @@ from typing import Any, Callable, Dict, List, Mapping, Optional, Sequence, Tuple
 import torch
 from torch import Tensor
 
+from torchmetrics_forked_amd.utilities.arena import StateArena
+
 METRIC_EPS = 1e-6
 
 
@@ -18,6 +20,8 @@ def dim_zero_cat(x: Union[Tensor, List[Tensor]]) -> Tensor:
     """Concatenate a list (or a tensor) along dim 0; 0-d entries are promoted to 1-d."""
     if isinstance(x, Tensor):
         return x
+    if isinstance(x, StateArena):  # compacted list state: a view of its buffer (utilities/arena.py)
+        return x.cat()
     parts = [y.unsqueeze(0) if y.numel() == 1 and y.ndim == 0 else y for y in x]
     if not parts:
         raise ValueError("No samples to concatenate")
