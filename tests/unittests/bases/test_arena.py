@@ -147,14 +147,26 @@ def test_arena_on_device_per_step_compute():
     if not torch.cuda.is_available():
         pytest.skip("needs a GPU")
     dev = torch.device("cuda", 0)
-    m = CatMetric().to(dev)
+    m = CatMetric(nan_strategy="ignore").to(dev)
     seen = []
     for step in range(40):
         x = torch.randn(1000 + step, device=dev)
-        seen.append(x)
+        if step % 5 == 1:
+            x[::7] = float("nan")  # dropped once, by the next consumer, over the new items only
+        seen.append(x[~torch.isnan(x)])
         m.update(x)
         if step % 3 == 0:
             out = m.compute()
             assert out.device.type == "cuda" and torch.equal(out, torch.cat(seen))
     assert torch.equal(m.compute(), torch.cat(seen))
     assert isinstance(m.value, StateArena) and m.value.capacity >= sum(t.numel() for t in seen)
+
+
+def test_truncate_keeps_the_buffer():
+    a = StateArena([torch.arange(3.0), torch.arange(3.0, 5.0), torch.arange(5.0, 9.0)])
+    a.cat()
+    ptr = a._buf.data_ptr()
+    a.truncate(1)
+    assert len(a) == 1 and a._rows == 3 and a._covered == 1
+    a.append(torch.tensor([42.0, 43.0]))  # copied into the freed tail
+    assert a._buf.data_ptr() == ptr and torch.equal(a.cat(), torch.tensor([0.0, 1, 2, 42, 43]))

@@ -1,0 +1,58 @@
+"""Eager vs HIP-graph-replayed metric updates on small batches (utilities/graphs.py), one MI355X.
+Host-bound shapes: BASELINE config 1 (MulticlassAccuracy, C=5, batch 10) and a few more. Prints one JSON line."""
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torchmetrics_forked_amd as tm  # noqa: E402
+from torchmetrics_forked_amd.utilities.graphs import GraphedUpdate  # noqa: E402
+
+
+def per_update_us(fn, data, reps=2000):
+    for i in range(50):
+        fn(*data[i % len(data)])
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(reps):
+        fn(*data[i % len(data)])
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / reps * 1e6
+
+
+def main():
+    cases = {
+        "MulticlassAccuracy C=5 bs=10 (config 1)": (lambda: tm.MulticlassAccuracy(num_classes=5), (10, 5), 5, torch.float32),
+        "MulticlassF1Score C=5 bs=10": (lambda: tm.MulticlassF1Score(num_classes=5), (10, 5), 5, torch.float32),
+        "MulticlassConfusionMatrix C=100 bs=512": (lambda: tm.MulticlassConfusionMatrix(num_classes=100), (512, 100), 100, torch.bfloat16),
+        "MulticlassAUROC C=1000 bs=256 bf16": (lambda: tm.MulticlassAUROC(num_classes=1000), (256, 1000), 1000, torch.bfloat16),
+        "{Accuracy, Precision, Recall, F1} C=10 bs=32": (
+            lambda: tm.MetricCollection([tm.MulticlassAccuracy(num_classes=10), tm.MulticlassPrecision(num_classes=10),
+                                         tm.MulticlassRecall(num_classes=10), tm.MulticlassF1Score(num_classes=10)]),
+            (32, 10), 10, torch.float32),
+        "8 distinct metrics on one [256, 10] batch (no shared states)": (
+            lambda: tm.MetricCollection({
+                "acc": tm.MulticlassAccuracy(num_classes=10), "acc_top3": tm.MulticlassAccuracy(num_classes=10, top_k=3),
+                "cm": tm.MulticlassConfusionMatrix(num_classes=10), "ece": tm.MulticlassCalibrationError(num_classes=10),
+                "auroc_binned": tm.MulticlassAUROC(num_classes=10, thresholds=64), "hinge": tm.MulticlassHingeLoss(num_classes=10),
+                "kappa": tm.MulticlassCohenKappa(num_classes=10), "mcc": tm.MulticlassMatthewsCorrCoef(num_classes=10),
+            }, compute_groups=False),
+            (256, 10), 10, torch.float32),
+    }
+    out = {}
+    for name, (make, shape, C, dtype) in cases.items():
+        data = [(torch.randn(*shape, device="cuda").to(dtype), torch.randint(0, C, shape[:1], device="cuda")) for _ in range(8)]
+        eager = make().cuda()
+        t_e = per_update_us(eager.update, data)
+        g = make().cuda()
+        step = GraphedUpdate(g, *data[0])
+        t_g = per_update_us(step, data)
+        out[name] = {"eager_us": round(t_e, 1), "graph_us": round(t_g, 1), "speedup": round(t_e / t_g, 2)}
+        print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

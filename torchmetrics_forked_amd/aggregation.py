@@ -10,6 +10,7 @@ import torch
 from torch import Tensor
 
 from torchmetrics_forked_amd.metric import Metric
+from torchmetrics_forked_amd.utilities.arena import StateArena
 from torchmetrics_forked_amd.utilities.data import dim_zero_cat
 from torchmetrics_forked_amd.utilities.plot import _AX_TYPE, _PLOT_OUT_TYPE
 from torchmetrics_forked_amd.utilities.prints import rank_zero_warn
@@ -208,10 +209,22 @@ class CatMetric(BaseAggregator):
             self.__dict__["_side_event"] = self._drop_pending_nans
 
     def _drop_pending_nans(self) -> None:
-        """Remove the NaN entries appended by deferred updates (one boolean index over the concatenated state)."""
-        if isinstance(self.value, list) and self.value:
-            cat = dim_zero_cat(self.value)
-            self.value = [cat[~torch.isnan(cat)]]
+        """Remove the NaN entries appended by deferred updates since the last drop (one boolean index over the new
+        items only; earlier items are already clean and stay in the state's arena buffer)."""
+        v = self.value
+        if not (isinstance(v, list) and v):
+            return
+        mark = self.__dict__.get("_nan_clean")
+        k = mark[1] if mark is not None and mark[0] == id(v) and mark[1] <= len(v) else 0
+        if k == len(v):
+            return
+        tail = dim_zero_cat(list(v[k:]))
+        kept = tail[~torch.isnan(tail)]
+        if not isinstance(v, StateArena):
+            v = self.value = StateArena(v)
+        v.truncate(k)
+        v.append(kept)
+        self.__dict__["_nan_clean"] = (id(v), len(v))
 
     def compute(self) -> Tensor:
         if isinstance(self.value, list) and self.value:

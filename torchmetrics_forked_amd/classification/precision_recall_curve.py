@@ -201,6 +201,11 @@ class _CurveMetric(Metric):
         self._code_range = rng
         self._rows_bound = rows
 
+    def _after_graph_capture(self) -> None:
+        """``utilities.graphs.GraphedUpdate``: replays do not advance the host row count, so the sync bounds the
+        histogram bins with a device max instead (the device-side code range stays exact: kernels widen it)."""
+        self._rows_bound = None
+
     def _invalidate_range(self) -> None:
         self._range_hist = None
         self._code_range = None

@@ -105,6 +105,16 @@ class StateArena(list):
     reverse = _mutating("reverse")
     del _mutating
 
+    def truncate(self, k: int) -> None:
+        """Drop the items from ``k`` on, keeping the buffer (and its free tail) when it covers the first ``k``."""
+        k = max(0, min(k, len(self)))
+        if self._buf is not None and self._covered >= k:
+            self._rows = sum(self._rows_of(t)[0] for t in self[:k])
+            self._covered = k
+        else:
+            self._drop()
+        list.__delitem__(self, slice(k, None))
+
     # ------------------------------------------------------------------------------------------------ reads
     def cat(self) -> Tensor:
         """The concatenation along dim 0 (0-d items promoted to 1-d), as a view of the compacted buffer."""
