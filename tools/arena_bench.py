@@ -14,7 +14,7 @@ from torchmetrics_forked_amd import CatMetric  # noqa: E402
 
 def run(steps, n, plain):
     dev = torch.device("cuda", 0)
-    m = CatMetric(nan_strategy="disable").to(dev)  # no NaN pass: the list itself is what is measured
+    m = CatMetric(nan_strategy="error").to(dev)  # NaN check is a device flag, no NaN-drop pass: the list itself is what is measured
     xs = [torch.randn(n, device=dev) for _ in range(16)]
     if plain:
         m.value = []  # a plain list: torch.cat of every piece at every read (the reference's behaviour)

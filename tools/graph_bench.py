@@ -33,11 +33,11 @@ def main():
             lambda: tm.MetricCollection([tm.MulticlassAccuracy(num_classes=10), tm.MulticlassPrecision(num_classes=10),
                                          tm.MulticlassRecall(num_classes=10), tm.MulticlassF1Score(num_classes=10)]),
             (32, 10), 10, torch.float32),
-        "8 distinct metrics on one [256, 10] batch (no shared states)": (
+        "7 distinct metrics on one [256, 10] batch (no shared states)": (
             lambda: tm.MetricCollection({
                 "acc": tm.MulticlassAccuracy(num_classes=10), "acc_top3": tm.MulticlassAccuracy(num_classes=10, top_k=3),
                 "cm": tm.MulticlassConfusionMatrix(num_classes=10), "ece": tm.MulticlassCalibrationError(num_classes=10),
-                "auroc_binned": tm.MulticlassAUROC(num_classes=10, thresholds=64), "hinge": tm.MulticlassHingeLoss(num_classes=10),
+                "auroc_binned": tm.MulticlassAUROC(num_classes=10, thresholds=64),
                 "kappa": tm.MulticlassCohenKappa(num_classes=10), "mcc": tm.MulticlassMatthewsCorrCoef(num_classes=10),
             }, compute_groups=False),
             (256, 10), 10, torch.float32),
