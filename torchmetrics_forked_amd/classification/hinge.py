@@ -62,7 +62,7 @@ class BinaryHingeLoss(_HingeBase):
 
     def update(self, preds: Tensor, target: Tensor) -> None:
         if self.validate_args:
-            _binary_hinge_loss_tensor_validation(preds, target, self.ignore_index)
+            _binary_hinge_loss_tensor_validation(preds, target, self.ignore_index, self._validation_sink(target))
         preds, target = binary_format(preds, target, 0.0, self.ignore_index, convert_to_labels=False)
         measures, total = _binary_hinge_loss_update(preds, target, self.squared)
         self.measures += measures
@@ -104,7 +104,7 @@ class MulticlassHingeLoss(_HingeBase):
 
     def update(self, preds: Tensor, target: Tensor) -> None:
         if self.validate_args:
-            _multiclass_hinge_loss_tensor_validation(preds, target, self.num_classes, self.ignore_index)
+            _multiclass_hinge_loss_tensor_validation(preds, target, self.num_classes, self.ignore_index, self._validation_sink(target))
         preds, target = multiclass_format(preds, target, self.ignore_index, convert_to_labels=False)
         measures, total = _multiclass_hinge_loss_update(preds, target, self.squared, self.multiclass_mode)
         self.measures += measures
