@@ -276,6 +276,11 @@ struct SlowRows {
 // Store one tile's LDS image as 16-B pieces of the class rows of the class-major scratch (compile-time trip count):
 // thread -> (class c, 16-B group g of the class's 64-B segment).  Segment dword 4g + i lives at LDS slot
 // (4g + i) ^ s (s = class swizzle), i.e. in LDS quad g ^ (s >> 2) at position i ^ (s & 3).
+// Code stores of the row pass.  TMX_ROWPASS_NT_STORE=1 builds them as non-temporal (streaming) stores, so the
+// class-major codes need not sit dirty in the XCD L2s until the kernel-boundary write-back.
+#ifndef TMX_ROWPASS_NT_STORE
+#define TMX_ROWPASS_NT_STORE 0
+#endif
 template <int NG>
 __device__ __forceinline__ void store_tile(const uint32_t* __restrict__ s_tile, uint32_t* __restrict__ codes, int C,
                                            int64_t n_pad, int64_t tile) {
@@ -291,7 +296,15 @@ __device__ __forceinline__ void store_tile(const uint32_t* __restrict__ s_tile, 
     const int x = sw & 3;
     const uint32_t e0 = x & 1 ? w.y : w.x, e1 = x & 1 ? w.x : w.y, e2 = x & 1 ? w.w : w.z, e3 = x & 1 ? w.z : w.w;
     const uint4 o = x & 2 ? make_uint4(e2, e3, e0, e1) : make_uint4(e0, e1, e2, e3);
-    if (c < C) *reinterpret_cast<uint4*>(&codes[c * row_dw + seg + 4 * g]) = o;
+    if (c < C) {
+#if TMX_ROWPASS_NT_STORE
+      using v4u = __attribute__((ext_vector_type(4))) unsigned int;
+      v4u v = {o.x, o.y, o.z, o.w};
+      __builtin_nontemporal_store(v, reinterpret_cast<v4u*>(&codes[c * row_dw + seg + 4 * g]));
+#else
+      *reinterpret_cast<uint4*>(&codes[c * row_dw + seg + 4 * g]) = o;
+#endif
+    }
   }
 }
 

@@ -85,14 +85,14 @@ int main(int argc, char** argv) {
   };
   auto class6 = [&](const __hip_bfloat16* x, const int64_t* t, bool spec) {
     hipLaunchKernelGGL((class_hist_kernel<__hip_bfloat16, false>), C, kClassThreads, kCodes * 4, 0, (const uint16_t*)codes6, n_pad, 1, hist6,
-                       x, C, t, N, mode, spec, slow_rows, state, cm6);
+                       x, C, t, N, mode, spec, slow_rows, state, cm6, (int*)nullptr, spec ? mode : (int*)nullptr);
   };
   // reference: v2 row pass (mode given), then the same class pass with no rare-row list
   auto ref2 = [&](const __hip_bfloat16* x, const int64_t* t, bool ign) {
     hipLaunchKernelGGL((tmx_ref::mc_codes_kernel<__hip_bfloat16, false, 0>), grid2, tmx_ref::kA_Threads, shm2, 0, x, t, N, C, mode2,
                        -100, ign, codes2, n_pad, cm2, err, false);
     hipLaunchKernelGGL((class_hist_kernel<__hip_bfloat16, false>), C, kClassThreads, kCodes * 4, 0, (const uint16_t*)codes2, n_pad, 1, hist2,
-                       x, C, t, N, mode2, false, slow_rows, state2, (int64_t*)nullptr);
+                       x, C, t, N, mode2, false, slow_rows, state2, (int64_t*)nullptr, (int*)nullptr, (int*)nullptr);
   };
 
   printf("{\"N\": %lld, \"C\": %d", (long long)N, C);
