@@ -340,7 +340,7 @@ NgramCount count_ngrams(const int64_t* t, int64_t len, int64_t n_gram) {
 }
 
 // ---- longest common subsequence (ROUGE-L) -------------------------------------------------------------------
-int64_t lcs_dp(const int64_t* a, int64_t n, const int64_t* b, int64_t m) {
+[[maybe_unused]] int64_t lcs_dp(const int64_t* a, int64_t n, const int64_t* b, int64_t m) {  // O(n m) oracle
   std::vector<int64_t> prev(m + 1, 0), cur(m + 1, 0);
   for (int64_t i = 1; i <= n; ++i) {
     for (int64_t j = 1; j <= m; ++j) cur[j] = (a[i - 1] == b[j - 1]) ? prev[j - 1] + 1 : std::max(prev[j], cur[j - 1]);
@@ -364,6 +364,44 @@ int64_t lcs_bits(const int64_t* a, int64_t n, const int64_t* b, int64_t m) {
     v = ((v + u) | (v - u)) & mask;
   }
   return m - __builtin_popcountll(v);
+}
+
+// Multi-word form (any m): V' = (V + (V & Peq)) | (V & ~Peq) with the addition's carry rippling from word to word
+// (V - (V & Peq) = V & ~Peq has no borrows).  O(n * ceil(m / 64)) word operations instead of the O(n * m) DP.
+int64_t lcs_bits_multi(const int64_t* a, int64_t n, const int64_t* b, int64_t m) {
+  if (m == 0 || n == 0) return 0;
+  const int64_t words = (m + 63) / 64;
+  std::unordered_map<int64_t, int64_t> row;  // token -> row of the match-mask table
+  row.reserve(static_cast<size_t>(m) * 2);
+  std::vector<uint64_t> peq;
+  for (int64_t j = 0; j < m; ++j) {
+    auto it = row.find(b[j]);
+    if (it == row.end()) {
+      it = row.emplace(b[j], static_cast<int64_t>(peq.size() / words)).first;
+      peq.resize(peq.size() + words, 0ull);
+    }
+    peq[it->second * words + j / 64] |= 1ull << (j % 64);
+  }
+  std::vector<uint64_t> v(words, ~0ull);
+  const uint64_t last = (m % 64) ? ((1ull << (m % 64)) - 1) : ~0ull;
+  v[words - 1] = last;
+  for (int64_t i = 0; i < n; ++i) {
+    auto it = row.find(a[i]);
+    if (it == row.end()) continue;
+    const uint64_t* pm = peq.data() + it->second * words;
+    uint64_t carry = 0;
+    for (int64_t k = 0; k < words; ++k) {
+      const uint64_t u = v[k] & pm[k];
+      const uint64_t s1 = v[k] + u;
+      const uint64_t s2 = s1 + carry;
+      carry = (s1 < v[k]) | (s2 < s1);
+      v[k] = s2 | (v[k] & ~pm[k]);
+    }
+    v[words - 1] &= last;
+  }
+  int64_t ones = 0;
+  for (int64_t k = 0; k < words; ++k) ones += __builtin_popcountll(v[k]);
+  return m - ones;
 }
 
 }  // namespace
@@ -517,7 +555,7 @@ at::Tensor lcs_batch(const at::Tensor& a, const at::Tensor& a_off, const at::Ten
   at::parallel_for(0, fa.n, 16, [&](int64_t s, int64_t e) {
     for (int64_t i = s; i < e; ++i) {
       const int64_t n = fa.len(i), m = fb.len(i);
-      o[i] = (m <= 64) ? lcs_bits(fa.ptr(i), n, fb.ptr(i), m) : lcs_dp(fa.ptr(i), n, fb.ptr(i), m);
+      o[i] = (m <= 64) ? lcs_bits(fa.ptr(i), n, fb.ptr(i), m) : lcs_bits_multi(fa.ptr(i), n, fb.ptr(i), m);
     }
   });
   return out;

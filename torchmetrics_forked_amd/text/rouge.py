@@ -67,7 +67,7 @@ class ROUGEScore(Metric):
             target = [[target]]
         out = _rouge_score_update(
             preds, target, self.rouge_keys_values, stemmer=self.stemmer, normalizer=self.normalizer,
-            tokenizer=self.tokenizer, accumulate=self.accumulate,
+            tokenizer=self.tokenizer, accumulate=self.accumulate, device=self.device,
         )
         for key, metrics in out.items():
             for m in metrics:
