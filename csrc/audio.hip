@@ -150,9 +150,116 @@ at::Tensor iir_filter_cuda(const at::Tensor& x_in, const at::Tensor& b_in, const
   return yt.t().contiguous();
 }
 
+// ---- batched Hungarian assignment for PIT ------------------------------------------------
+// One 64-lane workgroup per [S, S] problem (S <= 64): the shortest-augmenting-path Hungarian of the host solver
+// (audio_host.cpp ``hungarian``) with the column loop spread over the lanes — lane l owns column l + 1 (its potential
+// v, slack minv and used flag in registers), the row potentials u, the matching p and the path ``way`` live in LDS,
+// and the per-step arg-min over the free columns is a wave reduction of (slack, column) pairs, lowest column on ties
+// (the host loop's strict ``<``).  Same fp64 operations in the same order, so the same assignment as the host solver.
+constexpr int kHunLanes = 64;
+
+__global__ __launch_bounds__(kHunLanes) void hungarian_kernel(const double* __restrict__ metric, int S, bool maximize,
+                                                              int64_t* __restrict__ col_of_row) {
+  __shared__ double u[kHunLanes + 1];
+  __shared__ int p[kHunLanes + 1];
+  __shared__ int way[kHunLanes + 1];
+  const int lane = threadIdx.x;
+  const int j = lane + 1;  // column owned by this lane (1-based, column 0 is the virtual root)
+  const bool valid = j <= S;
+  const double* cost = metric + static_cast<int64_t>(blockIdx.x) * S * S;
+  const double inf = __builtin_huge_val();
+  for (int k = lane; k <= S; k += kHunLanes) {
+    u[k] = 0.0;
+    p[k] = 0;
+    way[k] = 0;
+  }
+  double v = 0.0;
+  __syncthreads();
+  for (int i = 1; i <= S; ++i) {
+    if (lane == 0) p[0] = i;
+    double minv = inf;
+    bool used = false;
+    int j0 = 0;
+    __syncthreads();
+    while (true) {
+      if (j == j0) used = true;
+      const int i0 = p[j0];
+      const double ui0 = u[i0];
+      const bool open = valid && !used;
+      if (open) {
+        const double c = cost[(i0 - 1) * S + lane];
+        const double cur = (maximize ? -c : c) - ui0 - v;
+        if (cur < minv) {
+          minv = cur;
+          way[j] = j0;
+        }
+      }
+      // arg-min of the free columns' slack, lowest column on ties
+      double best = open ? minv : inf;
+      int bj = open ? j : kHunLanes + 1;
+#pragma unroll
+      for (int off = kHunLanes / 2; off > 0; off >>= 1) {
+        const double ob = __shfl_xor(best, off, kHunLanes);
+        const int oj = __shfl_xor(bj, off, kHunLanes);
+        if (ob < best || (ob == best && oj < bj)) {
+          best = ob;
+          bj = oj;
+        }
+      }
+      if (bj > S) break;  // unreachable for finite costs (the wrapper sanitises them): never index past the arrays
+      const double delta = best;
+      const int j1 = bj;
+      __syncthreads();  // every lane has read u[i0] / p[j0] before the potentials move
+      if (valid) {
+        if (used) {
+          u[p[j]] += delta;
+          v -= delta;
+        } else {
+          minv -= delta;
+        }
+      }
+      if (lane == 0) u[p[0]] += delta;  // the root column is always in the tree
+      __syncthreads();
+      j0 = j1;
+      if (p[j0] == 0) break;
+    }
+    if (lane == 0) {  // augment along the alternating path
+      do {
+        const int j1 = way[j0];
+        p[j0] = p[j1];
+        j0 = j1;
+      } while (j0);
+    }
+    __syncthreads();
+  }
+  if (valid && p[j] >= 1) col_of_row[static_cast<int64_t>(blockIdx.x) * S + (p[j] - 1)] = j - 1;
+}
+
+// metric [B, S, S] on the GPU (rows = target speaker, cols = predicted speaker) -> perm [B, S] int64, maximising
+// (or minimising) the summed metric; no host round trip.
+at::Tensor linear_assignment_gpu(const at::Tensor& metric, bool maximize) {
+  TORCH_CHECK(metric.is_cuda() && metric.dim() == 3 && metric.size(1) == metric.size(2), "linear_assignment_gpu: expected GPU [B, S, S]");
+  const int64_t B = metric.size(0), S = metric.size(1);
+  TORCH_CHECK(S >= 1 && S <= kHunLanes, "linear_assignment_gpu: 1 <= S <= ", kHunLanes);
+  const at::DeviceGuard guard(metric.device());
+  // finite costs keep every augmenting step well defined: NaN is the worst score, +-inf a large finite one (as the host)
+  constexpr double kBig = 1e150;
+  auto m = at::nan_to_num(metric.detach().to(at::kDouble), maximize ? -kBig : kBig, kBig, -kBig).contiguous();
+  auto out = at::zeros({B, S}, metric.options().dtype(at::kLong));
+  if (B == 0) return out;
+  TORCH_CHECK(B < (int64_t{1} << 31), "linear_assignment_gpu: too many problems");
+  hipLaunchKernelGGL(hungarian_kernel, dim3(static_cast<unsigned>(B)), dim3(kHunLanes), 0, stream(), m.data_ptr<double>(),
+                     static_cast<int>(S), maximize, out.data_ptr<int64_t>());
+  TMX_LAUNCH_CHECK();
+  return out;
+}
+
 }  // namespace tmx
+
+TORCH_LIBRARY_FRAGMENT(tmx, m) { m.def("linear_assignment_gpu(Tensor metric, bool maximize) -> Tensor"); }
 
 TORCH_LIBRARY_IMPL(tmx, CUDA, m) {
   m.impl("toeplitz_solve", &tmx::toeplitz_solve_cuda);
   m.impl("iir_filter", &tmx::iir_filter_cuda);
+  m.impl("linear_assignment_gpu", &tmx::linear_assignment_gpu);
 }

@@ -119,7 +119,9 @@ at::Tensor toeplitz_solve_cpu(const at::Tensor& r_in, const at::Tensor& b_in) {
 // maximising (or minimising) the summed metric.
 at::Tensor linear_assignment(const at::Tensor& metric, bool maximize) {
   TORCH_CHECK(metric.dim() == 3 && metric.size(1) == metric.size(2), "linear_assignment: expected [B, S, S]");
-  auto m = metric.detach().to(at::kCPU).to(at::kDouble).contiguous();
+  // NaN = worst score, +-inf = large finite (an all-infinite row would otherwise leave no finite slack to augment on)
+  constexpr double kBig = 1e150;
+  auto m = at::nan_to_num(metric.detach().to(at::kCPU).to(at::kDouble), maximize ? -kBig : kBig, kBig, -kBig).contiguous();
   const int64_t B = m.size(0), S = m.size(1);
   auto out = at::empty({B, S}, at::kLong);
   const double* pm = m.data_ptr<double>();

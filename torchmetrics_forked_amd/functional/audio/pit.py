@@ -3,7 +3,8 @@
 Speaker-wise mode builds the [B, S, S] metric matrix (one batched call for the framework's own audio metrics,
 which are independent per batch element; the reference's S² loop for arbitrary user functions), then picks the
 best permutation by exhaustive search over all S! permutations (S ≤ 3, as the reference) or by the native batched
-Hungarian solver ``tmx::linear_assignment`` (C++; replaces scipy's ``linear_sum_assignment``)."""
+Hungarian solver ``tmx::linear_assignment`` (C++; replaces scipy's ``linear_sum_assignment``), or its batched GPU form
+``tmx::linear_assignment_gpu`` (one wave per problem) when the metric matrix is on the GPU."""
 from itertools import permutations
 from typing import Any, Callable, Dict, Literal, Tuple
 
@@ -24,7 +25,10 @@ def _gen_permutations(spk_num: int, device: torch.device) -> Tensor:
 
 def _find_best_perm_by_linear_sum_assignment(metric_mtx: Tensor, eval_func: Callable) -> Tuple[Tensor, Tensor]:
     ops.require()
-    best_perm = torch.ops.tmx.linear_assignment(metric_mtx, eval_func == torch.max).to(metric_mtx.device)
+    if metric_mtx.is_cuda and metric_mtx.shape[-1] <= 64:  # batched GPU Hungarian: no host round trip (csrc/audio.hip)
+        best_perm = torch.ops.tmx.linear_assignment_gpu(metric_mtx, eval_func == torch.max)
+    else:
+        best_perm = torch.ops.tmx.linear_assignment(metric_mtx, eval_func == torch.max).to(metric_mtx.device)
     best_metric = torch.gather(metric_mtx, 2, best_perm[:, :, None]).mean([-1, -2])
     return best_metric, best_perm
 
