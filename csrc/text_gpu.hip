@@ -120,6 +120,124 @@ __global__ __launch_bounds__(kLevWaves * kWave) void lcs_wave_kernel(const int64
   if (lane == 0) out[pair] = m - ones;
 }
 
+// BLEU sufficient statistics, one wave per hypothesis: the same outputs as the host op
+// ``bleu_stats`` (text.cpp).  An n-gram (n <= 4) of token ids < 65535 packs exactly into 64 bits ((id + 1) per 16-bit
+// field), so n-grams compare as integers.  Lane l owns hypothesis positions l + 64 k (k < kBleuSlots); for every
+// order n the wave (1) counts each of its n-grams inside the hypothesis and marks first occurrences (the keys are
+// broadcast position by position with lane shuffles), (2) streams every reference of the group position by position
+// (wave-uniform loads) and keeps, per hypothesis n-gram, the maximum count over the references, and (3) sums
+// min(count, max reference count) over first occurrences — the clipped matches — with one wave reduction.
+constexpr int kBleuSlots = 4;  // hypotheses up to 256 tokens on this path
+
+__device__ __forceinline__ uint64_t gram_key(const int64_t* __restrict__ t, int64_t pos, int n) {
+  uint64_t k = 0;
+  for (int j = 0; j < n; ++j) k = (k << 16) | static_cast<uint64_t>(t[pos + j] + 1);
+  return k;
+}
+
+__global__ __launch_bounds__(kLevWaves * kWave) void bleu_stats_wave_kernel(
+    const int64_t* __restrict__ hyp, const int64_t* __restrict__ hyp_off, const int64_t* __restrict__ ref,
+    const int64_t* __restrict__ ref_off, const int64_t* __restrict__ group_off, int64_t nhyp, int n_gram,
+    double* __restrict__ num, double* __restrict__ den, double* __restrict__ lens) {
+  const int lane = threadIdx.x % kWave;
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * kLevWaves + threadIdx.x / kWave;
+  if (i >= nhyp) return;  // wave-uniform
+  const int64_t h0 = hyp_off[i], hl = hyp_off[i + 1] - h0;
+  const int64_t g0 = group_off[i], g1 = group_off[i + 1];
+  if (lane == 0) {  // lengths: hypothesis and closest reference (first minimum), as the host op
+    int64_t best_diff = -1, best_len = 0;
+    for (int64_t r = g0; r < g1; ++r) {
+      const int64_t rl = ref_off[r + 1] - ref_off[r];
+      const int64_t d = hl > rl ? hl - rl : rl - hl;
+      if (best_diff < 0 || d < best_diff) {
+        best_diff = d;
+        best_len = rl;
+      }
+    }
+    lens[2 * i] = static_cast<double>(hl);
+    lens[2 * i + 1] = static_cast<double>(best_len);
+  }
+  for (int n = 1; n <= n_gram; ++n) {
+    const int64_t ng = hl - n + 1;  // n-grams in the hypothesis
+    uint64_t key[kBleuSlots];
+    int cnt[kBleuSlots], mx[kBleuSlots], cur[kBleuSlots];
+    bool first[kBleuSlots];
+#pragma unroll
+    for (int k = 0; k < kBleuSlots; ++k) {
+      const int64_t p = lane + 64 * k;
+      key[k] = p < ng ? gram_key(hyp + h0, p, n) : 0ull;
+      cnt[k] = 0;
+      mx[k] = 0;
+      first[k] = true;
+    }
+    // (1) counts inside the hypothesis + first occurrences
+#pragma unroll
+    for (int kq = 0; kq < kBleuSlots; ++kq) {
+      if (64 * kq >= ng) break;
+      for (int ql = 0; ql < kWave && 64 * kq + ql < ng; ++ql) {
+        const uint64_t kqv = __shfl(key[kq], ql, kWave);
+        const int64_t q = 64 * kq + ql;
+#pragma unroll
+        for (int k = 0; k < kBleuSlots; ++k) {
+          const int64_t p = lane + 64 * k;
+          if (p < ng && key[k] == kqv) {
+            ++cnt[k];
+            if (q < p) first[k] = false;
+          }
+        }
+      }
+    }
+    // (2) maximum count over the references
+    for (int64_t r = g0; r < g1; ++r) {
+      const int64_t r0 = ref_off[r], rng = ref_off[r + 1] - r0 - n + 1;
+#pragma unroll
+      for (int k = 0; k < kBleuSlots; ++k) cur[k] = 0;
+      for (int64_t q = 0; q < rng; ++q) {
+        const uint64_t kr = gram_key(ref + r0, q, n);  // wave-uniform loads
+#pragma unroll
+        for (int k = 0; k < kBleuSlots; ++k) cur[k] += (key[k] == kr) ? 1 : 0;
+      }
+#pragma unroll
+      for (int k = 0; k < kBleuSlots; ++k) mx[k] = max(mx[k], cur[k]);
+    }
+    // (3) clipped matches over first occurrences, hypothesis n-gram total
+    int clipped = 0;
+#pragma unroll
+    for (int k = 0; k < kBleuSlots; ++k) {
+      const int64_t p = lane + 64 * k;
+      if (p < ng && first[k]) clipped += min(cnt[k], mx[k]);
+    }
+#pragma unroll
+    for (int off = kWave / 2; off > 0; off >>= 1) clipped += __shfl_xor(clipped, off, kWave);
+    if (lane == 0) {
+      num[i * n_gram + (n - 1)] = static_cast<double>(clipped);
+      den[i * n_gram + (n - 1)] = static_cast<double>(ng > 0 ? ng : 0);
+    }
+  }
+}
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor> bleu_stats_gpu(const at::Tensor& hyp, const at::Tensor& hyp_off, const at::Tensor& ref,
+                                                              const at::Tensor& ref_off, const at::Tensor& group_off, int64_t n_gram,
+                                                              int64_t max_hyp_len) {
+  for (const at::Tensor* t : {&hyp, &hyp_off, &ref, &ref_off, &group_off})
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kLong, "bleu_stats_gpu: expected int64 GPU tensors");
+  TORCH_CHECK(n_gram >= 1 && n_gram <= 4, "bleu_stats_gpu: n_gram must be in [1, 4] (exact 64-bit n-gram keys)");
+  TORCH_CHECK(max_hyp_len <= 64 * kBleuSlots, "bleu_stats_gpu: hypothesis longer than ", 64 * kBleuSlots, " tokens");
+  TORCH_CHECK(group_off.numel() == hyp_off.numel(), "bleu_stats_gpu: group offsets must have n + 1 entries");
+  const c10::DeviceGuard guard(hyp.device());
+  const int64_t n = hyp_off.numel() - 1;
+  auto opts = hyp.options().dtype(at::kDouble);
+  auto num = at::zeros({n, n_gram}, opts), den = at::zeros({n, n_gram}, opts), lens = at::zeros({n, 2}, opts);
+  if (n <= 0) return {num, den, lens};
+  const auto h = hyp.contiguous(), ho = hyp_off.contiguous(), r = ref.contiguous(), ro = ref_off.contiguous(), go = group_off.contiguous();
+  const unsigned grid = static_cast<unsigned>((n + kLevWaves - 1) / kLevWaves);
+  bleu_stats_wave_kernel<<<grid, kLevWaves * kWave, 0, stream()>>>(h.data_ptr<int64_t>(), ho.data_ptr<int64_t>(), r.data_ptr<int64_t>(),
+                                                                   ro.data_ptr<int64_t>(), go.data_ptr<int64_t>(), n, static_cast<int>(n_gram),
+                                                                   num.data_ptr<double>(), den.data_ptr<double>(), lens.data_ptr<double>());
+  TMX_LAUNCH_CHECK();
+  return {num, den, lens};
+}
+
 // a / b: flat int64 token ids (GPU), a_off / b_off: int64 [n + 1] offsets (GPU).  Returns int64 [n] distances.
 at::Tensor levenshtein_gpu(const at::Tensor& a, const at::Tensor& a_off, const at::Tensor& b, const at::Tensor& b_off,
                            int64_t max_ref_len) {
@@ -165,9 +283,11 @@ at::Tensor lcs_gpu(const at::Tensor& a, const at::Tensor& a_off, const at::Tenso
 TORCH_LIBRARY_FRAGMENT(tmx, m) {
   m.def("levenshtein_gpu(Tensor a, Tensor a_off, Tensor b, Tensor b_off, int max_ref_len) -> Tensor");
   m.def("lcs_gpu(Tensor a, Tensor a_off, Tensor b, Tensor b_off, int max_ref_len) -> Tensor");
+  m.def("bleu_stats_gpu(Tensor hyp, Tensor hyp_off, Tensor ref, Tensor ref_off, Tensor ref_group_off, int n_gram, int max_hyp_len) -> (Tensor, Tensor, Tensor)");
 }
 
 TORCH_LIBRARY_IMPL(tmx, CUDA, m) {
   m.impl("levenshtein_gpu", &tmx::levenshtein_gpu);
   m.impl("lcs_gpu", &tmx::lcs_gpu);
+  m.impl("bleu_stats_gpu", &tmx::bleu_stats_gpu);
 }

@@ -1,7 +1,9 @@
 """BLEU (API parity: reference ``functional/text/bleu.py``).
 
 Tokens are mapped to ids on the host; clipped n-gram matches / totals / lengths for the whole batch come from the
-native ``tmx::bleu_stats`` op (hashed n-gram maps, parallel over sentences) instead of per-sentence ``Counter``s."""
+native ``tmx::bleu_stats`` op (hashed n-gram maps, parallel over sentences) instead of per-sentence ``Counter``s, or
+from ``tmx::bleu_stats_gpu`` (one wave per hypothesis, exact packed n-gram keys) when the metric's states are on the
+GPU."""
 from typing import Callable, Optional, Sequence, Tuple, Union
 
 import torch
@@ -36,7 +38,14 @@ def _bleu_score_update(
     h, h_off = _pack(hyps, vocab)
     r, r_off = _pack([x for rs in refs for x in rs], vocab)
     groups = torch.tensor([0] + [len(rs) for rs in refs], dtype=torch.long).cumsum(0)
-    num, den, lens = torch.ops.tmx.bleu_stats(h, h_off, r, r_off, groups, n_gram)
+    max_hyp = max((len(x) for x in hyps), default=0)
+    if numerator.is_cuda and n_gram <= 4 and len(vocab._ids) < 65535 and max_hyp <= 256:
+        # GPU-resident states: exact 64-bit n-gram keys, one wave per hypothesis (csrc/text_gpu.hip); the statistics
+        # never leave the device
+        d = [x.to(numerator.device, non_blocking=True) for x in (h, h_off, r, r_off, groups)]
+        num, den, lens = torch.ops.tmx.bleu_stats_gpu(*d, n_gram, max_hyp)
+    else:
+        num, den, lens = torch.ops.tmx.bleu_stats(h, h_off, r, r_off, groups, n_gram)
     numerator += num.sum(0).to(numerator)
     denominator += den.sum(0).to(denominator)
     tot = lens.sum(0)
