@@ -339,6 +339,17 @@ NgramCount count_ngrams(const int64_t* t, int64_t len, int64_t n_gram) {
   return c;
 }
 
+// Packed n-grams (n <= 4, ids < 65535): (id + 1) per 16-bit field, so an n-gram is one exact 64-bit key and its order
+// is the number of occupied fields — no per-n-gram allocation (the generic map above allocates a vector per key).
+inline int64_t packed_order(uint64_t k) { return (64 - __builtin_clzll(k) + 15) / 16; }
+
+bool packable(const at::Tensor& a, const at::Tensor& b, int64_t n_gram) {
+  if (n_gram > 4) return false;
+  for (const at::Tensor* t : {&a, &b})
+    if (t->numel() && (t->min().item<int64_t>() < 0 || t->max().item<int64_t>() >= 65535)) return false;
+  return true;
+}
+
 // ---- longest common subsequence (ROUGE-L) -------------------------------------------------------------------
 [[maybe_unused]] int64_t lcs_dp(const int64_t* a, int64_t n, const int64_t* b, int64_t m) {  // O(n m) oracle
   std::vector<int64_t> prev(m + 1, 0), cur(m + 1, 0);
@@ -486,6 +497,59 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> bleu_stats(const at::Tensor& hyp,
   double* pn = num.data_ptr<double>();
   double* pd = den.data_ptr<double>();
   double* pl = lens.data_ptr<double>();
+  if (packable(hyp, ref, n_gram)) {  // sorted packed keys + run-length: no hash-map nodes per n-gram
+    at::parallel_for(0, fh.n, 8, [&](int64_t s, int64_t e) {
+      std::vector<uint64_t> keys;
+      std::vector<std::pair<uint64_t, int64_t>> tgt, runs;
+      auto sorted_runs = [&](const int64_t* t, int64_t len, std::vector<std::pair<uint64_t, int64_t>>& out) {
+        keys.clear();
+        for (int64_t j = 0; j < len; ++j) {
+          uint64_t k = 0;
+          for (int64_t n = 1; n <= n_gram && j + n <= len; ++n) {
+            k = (k << 16) | static_cast<uint64_t>(t[j + n - 1] + 1);
+            keys.push_back(k);
+          }
+        }
+        std::sort(keys.begin(), keys.end());
+        for (size_t a = 0; a < keys.size();) {
+          size_t b = a + 1;
+          while (b < keys.size() && keys[b] == keys[a]) ++b;
+          out.emplace_back(keys[a], static_cast<int64_t>(b - a));
+          a = b;
+        }
+      };
+      for (int64_t i = s; i < e; ++i) {
+        const int64_t hl = fh.len(i);
+        pl[2 * i] = static_cast<double>(hl);
+        int64_t best_diff = -1, best_len = 0;
+        tgt.clear();
+        for (int64_t r = go[i]; r < go[i + 1]; ++r) {
+          const int64_t rl = fr.len(r);
+          const int64_t d = std::llabs(hl - rl);
+          if (best_diff < 0 || d < best_diff) {
+            best_diff = d;
+            best_len = rl;
+          }
+          sorted_runs(fr.ptr(r), rl, tgt);  // appended per reference; max per key below
+        }
+        pl[2 * i + 1] = static_cast<double>(best_len);
+        std::sort(tgt.begin(), tgt.end());  // by key, then count: the last of each key run is its maximum
+        runs.clear();
+        sorted_runs(fh.ptr(i), hl, runs);
+        size_t q = 0;
+        for (const auto& kv : runs) {
+          const int64_t n = packed_order(kv.first) - 1;
+          pd[i * n_gram + n] += static_cast<double>(kv.second);
+          while (q < tgt.size() && tgt[q].first < kv.first) ++q;
+          size_t last = q;
+          while (last < tgt.size() && tgt[last].first == kv.first) ++last;
+          if (last > q) pn[i * n_gram + n] += static_cast<double>(std::min(kv.second, tgt[last - 1].second));
+          q = last;
+        }
+      }
+    });
+    return {num, den, lens};
+  }
   at::parallel_for(0, fh.n, 8, [&](int64_t s, int64_t e) {
     for (int64_t i = s; i < e; ++i) {
       const int64_t hl = fh.len(i);
