@@ -343,6 +343,26 @@ NgramCount count_ngrams(const int64_t* t, int64_t len, int64_t n_gram) {
 // is the number of occupied fields — no per-n-gram allocation (the generic map above allocates a vector per key).
 inline int64_t packed_order(uint64_t k) { return (64 - __builtin_clzll(k) + 15) / 16; }
 
+// Sorted (key, count) runs of every packed n-gram (orders 1..n_gram) of t, appended to ``out``.
+void packed_runs(const int64_t* t, int64_t len, int64_t n_gram, std::vector<uint64_t>& keys,
+                 std::vector<std::pair<uint64_t, int64_t>>& out) {
+  keys.clear();
+  for (int64_t j = 0; j < len; ++j) {
+    uint64_t k = 0;
+    for (int64_t n = 1; n <= n_gram && j + n <= len; ++n) {
+      k = (k << 16) | static_cast<uint64_t>(t[j + n - 1] + 1);
+      keys.push_back(k);
+    }
+  }
+  std::sort(keys.begin(), keys.end());
+  for (size_t a = 0; a < keys.size();) {
+    size_t b = a + 1;
+    while (b < keys.size() && keys[b] == keys[a]) ++b;
+    out.emplace_back(keys[a], static_cast<int64_t>(b - a));
+    a = b;
+  }
+}
+
 bool packable(const at::Tensor& a, const at::Tensor& b, int64_t n_gram) {
   if (n_gram > 4) return false;
   for (const at::Tensor* t : {&a, &b})
@@ -502,21 +522,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> bleu_stats(const at::Tensor& hyp,
       std::vector<uint64_t> keys;
       std::vector<std::pair<uint64_t, int64_t>> tgt, runs;
       auto sorted_runs = [&](const int64_t* t, int64_t len, std::vector<std::pair<uint64_t, int64_t>>& out) {
-        keys.clear();
-        for (int64_t j = 0; j < len; ++j) {
-          uint64_t k = 0;
-          for (int64_t n = 1; n <= n_gram && j + n <= len; ++n) {
-            k = (k << 16) | static_cast<uint64_t>(t[j + n - 1] + 1);
-            keys.push_back(k);
-          }
-        }
-        std::sort(keys.begin(), keys.end());
-        for (size_t a = 0; a < keys.size();) {
-          size_t b = a + 1;
-          while (b < keys.size() && keys[b] == keys[a]) ++b;
-          out.emplace_back(keys[a], static_cast<int64_t>(b - a));
-          a = b;
-        }
+        packed_runs(t, len, n_gram, keys, out);
       };
       for (int64_t i = s; i < e; ++i) {
         const int64_t hl = fh.len(i);
@@ -593,6 +599,35 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> ngram_overlap(const at::Tensor& h
   int64_t* pm = match.data_ptr<int64_t>();
   int64_t* ph = htot.data_ptr<int64_t>();
   int64_t* pr = rtot.data_ptr<int64_t>();
+  if (packable(hyp, ref, n_order)) {  // sorted packed runs of both sides, merged per reference
+    at::parallel_for(0, fh.n, 4, [&](int64_t s, int64_t e) {
+      std::vector<uint64_t> keys;
+      std::vector<std::pair<uint64_t, int64_t>> hr, rr;
+      for (int64_t i = s; i < e; ++i) {
+        const int64_t hl = fh.len(i);
+        for (int64_t n = 1; n <= n_order; ++n) ph[i * n_order + n - 1] = std::max<int64_t>(hl - n + 1, 0);
+        hr.clear();
+        packed_runs(fh.ptr(i), hl, n_order, keys, hr);
+        for (int64_t r = go[i]; r < go[i + 1]; ++r) {
+          const int64_t rl = fr.len(r);
+          for (int64_t n = 1; n <= n_order; ++n) pr[r * n_order + n - 1] = std::max<int64_t>(rl - n + 1, 0);
+          rr.clear();
+          packed_runs(fr.ptr(r), rl, n_order, keys, rr);
+          size_t a = 0, b = 0;
+          while (a < hr.size() && b < rr.size()) {
+            if (hr[a].first < rr[b].first) ++a;
+            else if (rr[b].first < hr[a].first) ++b;
+            else {
+              pm[r * n_order + packed_order(hr[a].first) - 1] += std::min(hr[a].second, rr[b].second);
+              ++a;
+              ++b;
+            }
+          }
+        }
+      }
+    });
+    return {match, htot, rtot};
+  }
   at::parallel_for(0, fh.n, 4, [&](int64_t s, int64_t e) {
     for (int64_t i = s; i < e; ++i) {
       const int64_t hl = fh.len(i);
