@@ -39,6 +39,8 @@ cases = {
     "MulticlassCalibrationError": (tm.classification.MulticlassCalibrationError(num_classes=C), (mc_p, mc_t)),
     "MulticlassCohenKappa": (tm.classification.MulticlassCohenKappa(num_classes=C), (mc_p, mc_t)),
     "MulticlassMatthewsCorrCoef": (tm.classification.MulticlassMatthewsCorrCoef(num_classes=C), (mc_p, mc_t)),
+    "MulticlassHingeLoss": (tm.classification.MulticlassHingeLoss(num_classes=C), (mc_p, mc_t)),
+    "BinaryHingeLoss": (tm.classification.BinaryHingeLoss(), (b_p, mc_t % 2)),
     "MulticlassJaccardIndex": (tm.classification.MulticlassJaccardIndex(num_classes=C), (mc_p, mc_t)),
     "MulticlassExactMatch": (tm.classification.MulticlassExactMatch(num_classes=C), (mc_p.argmax(1).reshape(64, 64), mc_t.reshape(64, 64))),
     "MultilabelAccuracy": (tm.classification.MultilabelAccuracy(num_labels=5), (ml_p, ml_t)),
