@@ -49,6 +49,16 @@ class GraphedUpdate:
         example_args / example_kwargs: a batch with the shapes and dtypes of every later batch (its values are not
             accumulated). Non-tensor arguments are frozen at capture time.
         warmup: side-stream warm-up updates before capture (rolled back).
+
+    Example (needs a GPU)::
+
+        coll = tm.MetricCollection({"acc": tm.MulticlassAccuracy(num_classes=10),
+                                    "ece": tm.MulticlassCalibrationError(num_classes=10),
+                                    "cm": tm.MulticlassConfusionMatrix(num_classes=10)}, compute_groups=False).cuda()
+        step = GraphedUpdate(coll, logits, labels)   # example batch: shapes / dtypes only
+        for logits, labels in loader:                # same shapes every step
+            step(logits, labels)                     # one graph replay instead of the eager update
+        coll.compute()
     """
 
     def __init__(self, metric: Union[Metric, MetricCollection], *example_args: Any, warmup: int = 2, **example_kwargs: Any) -> None:
