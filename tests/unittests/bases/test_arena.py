@@ -170,3 +170,13 @@ def test_truncate_keeps_the_buffer():
     assert len(a) == 1 and a._rows == 3 and a._covered == 1
     a.append(torch.tensor([42.0, 43.0]))  # copied into the freed tail
     assert a._buf.data_ptr() == ptr and torch.equal(a.cat(), torch.tensor([0.0, 1, 2, 42, 43]))
+
+
+def test_adopt_takes_the_buffer_without_touching_the_source():
+    a = StateArena([torch.arange(4.0)])
+    a.cat()
+    a._buf = torch.cat([a._buf, torch.zeros(4)])  # free tail of 4 rows
+    b = StateArena.adopt(a)
+    b.append(torch.tensor([9.0]))
+    assert len(a) == 1 and torch.equal(a.cat(), torch.arange(4.0))  # the source never sees b's appends
+    assert torch.equal(b.cat(), torch.tensor([0.0, 1, 2, 3, 9]))

@@ -372,7 +372,7 @@ class Metric(Module, ABC):
                 if isinstance(glob, Tensor) and isinstance(local, Tensor):
                     merged = torch.cat([glob, local])
                 else:
-                    merged = (StateArena(glob) if not isinstance(glob, StateArena) else glob) if isinstance(glob, list) else glob
+                    merged = (StateArena.adopt(glob) if isinstance(glob, StateArena) else StateArena(glob)) if isinstance(glob, list) else glob
                     if isinstance(merged, list):
                         merged.extend(local)
                     else:

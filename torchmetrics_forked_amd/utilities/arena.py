@@ -105,6 +105,17 @@ class StateArena(list):
     reverse = _mutating("reverse")
     del _mutating
 
+    @classmethod
+    def adopt(cls, other: "StateArena") -> "StateArena":
+        """A new arena with ``other``'s items that takes over its buffer (and free tail); ``other`` keeps its items
+        (views of the untouched prefix) but no longer appends into that buffer, so a list that is still shared
+        elsewhere is never extended behind its holders' backs."""
+        out = cls(other)
+        if other._buf is not None and other._covered == len(other):
+            out._buf, out._rows, out._covered = other._buf, other._rows, other._covered
+        other._drop()
+        return out
+
     def truncate(self, k: int) -> None:
         """Drop the items from ``k`` on, keeping the buffer (and its free tail) when it covers the first ``k``."""
         k = max(0, min(k, len(self)))
