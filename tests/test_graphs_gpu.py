@@ -97,3 +97,48 @@ def test_graphed_deferred_checks_still_raise():
     step(p, bad)
     with pytest.raises(RuntimeError):
         m.compute()
+
+
+@gpu
+@needs_gpu
+@pytest.mark.parametrize(
+    "make, C, shape_p, dtype",
+    [
+        (lambda: tm.MulticlassConfusionMatrix(num_classes=20), 20, (256, 20), torch.float32),
+        (lambda: tm.MulticlassAUROC(num_classes=1000), 1000, (256, 1000), torch.bfloat16),
+        (lambda: tm.MetricCollection({"acc": tm.MulticlassAccuracy(num_classes=20),
+                                      "cm": tm.MulticlassConfusionMatrix(num_classes=20)}), 20, (256, 20), torch.float32),
+    ],
+)
+def test_graphed_survives_reset_forward_and_compute(make, C, shape_p, dtype):
+    """reset() / forward() rebind states; the graphed step must keep accumulating into the live
+    states (re-capture), not into orphaned buffers."""
+    data = _batches(9, shape_p, (shape_p[0],), C, dtype=dtype)
+    graphed, eager = make().cuda(), make().cuda()
+    step = GraphedUpdate(graphed, *data[0])
+    for p, t in data[:3]:
+        step(p, t)
+        eager.update(p, t)
+    _close(graphed.compute(), eager.compute())
+    graphed.reset()
+    eager.reset()
+    for p, t in data[3:6]:
+        step(p, t)
+        eager.update(p, t)
+    _close(graphed.compute(), eager.compute())
+    assert step.captures >= 2
+    graphed(*data[6])  # forward rebinds the reduce-state accumulators
+    eager(*data[6])
+    for p, t in data[7:]:
+        step(p, t)
+        eager.update(p, t)
+    _close(graphed.compute(), eager.compute())
+
+
+def _close(a, b):
+    if isinstance(a, dict):
+        assert a.keys() == b.keys()
+        for k in a:
+            _close(a[k], b[k])
+        return
+    torch.testing.assert_close(a.float(), b.float(), atol=1e-6, rtol=1e-6)

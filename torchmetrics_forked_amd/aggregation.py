@@ -214,8 +214,7 @@ class CatMetric(BaseAggregator):
         v = self.value
         if not (isinstance(v, list) and v):
             return
-        mark = self.__dict__.get("_nan_clean")
-        k = mark[1] if mark is not None and mark[0] == id(v) and mark[1] <= len(v) else 0
+        k = min(v.clean, len(v)) if isinstance(v, StateArena) else 0
         if k == len(v):
             return
         tail = dim_zero_cat(list(v[k:]))
@@ -224,7 +223,7 @@ class CatMetric(BaseAggregator):
             v = self.value = StateArena(v)
         v.truncate(k)
         v.append(kept)
-        self.__dict__["_nan_clean"] = (id(v), len(v))
+        v.clean = len(v)
 
     def compute(self) -> Tensor:
         if isinstance(self.value, list) and self.value:

@@ -524,7 +524,7 @@ class Metric(Module, ABC):
                 with _range(f"tmx/{self.__class__.__name__}.compute"), self.sync_context(
                     dist_sync_fn=self.dist_sync_fn, should_sync=self._to_sync, should_unsync=self._should_unsync
                 ):
-                    value = _squeeze_if_scalar(compute(*args, **kwargs))
+                    value = self._unalias(_squeeze_if_scalar(compute(*args, **kwargs)))
                 if self.compute_with_cache:
                     self._computed = value
                     batch.on_error(self._drop_computed)
@@ -534,6 +534,24 @@ class Metric(Module, ABC):
 
     def _drop_computed(self) -> None:
         self._computed = None
+
+    def _unalias(self, value: Any) -> Any:
+        """Copy result tensors that are views of a ``cat`` state's arena buffer (``utilities/arena.py``): the reference's
+        ``dim_zero_cat`` returns a fresh tensor, so in-place edits of a result must not reach the accumulated state."""
+        arenas = [v for v in (getattr(self, n, None) for n in self._defaults) if isinstance(v, StateArena) and v._buf is not None]
+        if not arenas:
+            return value
+
+        def fix(x: Any) -> Any:
+            if isinstance(x, Tensor):
+                return x.clone() if any(a.owns(x) for a in arenas) else x
+            if isinstance(x, dict):
+                return {k: fix(v) for k, v in x.items()}
+            if isinstance(x, (list, tuple)):
+                return type(x)(fix(v) for v in x) if not hasattr(x, "_fields") else type(x)(*(fix(v) for v in x))
+            return x
+
+        return fix(value)
 
     @abstractmethod
     def update(self, *_: Any, **__: Any) -> None:

@@ -16,7 +16,9 @@ previous capacity.  Over any sequence of appends and reads every sample is copie
 * The first compaction allocates exactly the filled size (a single read never costs more HBM than ``torch.cat``).
 * Pieces that differ in dtype / device / trailing shape, or that require grad, keep the plain-list behaviour.
 * Any list mutation other than ``append`` / ``extend`` drops the buffer (the next read compacts again).
-* ``cat()`` returns a view of the state; consumers treat it as read-only, as they treat a tensor state.
+* ``cat()`` returns a view of the state; internal consumers treat it as read-only, as they treat a tensor state.
+  ``Metric.compute`` copies any result that aliases an arena buffer before handing it to the user (the reference's
+  ``dim_zero_cat`` always returns a fresh ``torch.cat``).
 """
 from copy import deepcopy
 from typing import Any, Iterable, List, Optional, Tuple
@@ -28,13 +30,16 @@ from torch import Tensor
 class StateArena(list):
     """A list of tensors with a lazily compacted, growable backing buffer (see module docstring)."""
 
-    __slots__ = ("_buf", "_rows", "_covered")
+    __slots__ = ("_buf", "_rows", "_covered", "clean")
 
     def __init__(self, items: Iterable[Any] = ()) -> None:
         super().__init__(items)
         self._buf: Optional[Tensor] = None  # [capacity, *tail]
         self._rows = 0  # rows of _buf in use
         self._covered = 0  # list items [0, _covered) are views of _buf, in order
+        # leading items a consumer has already filtered (CatMetric's deferred NaN drop); owned by this object, so it
+        # cannot leak to a later arena the way an id()-keyed mark could
+        self.clean = 0
 
     # ---------------------------------------------------------------------------------------------- helpers
     @staticmethod
@@ -90,6 +95,7 @@ class StateArena(list):
 
         def method(self: "StateArena", *args: Any, **kwargs: Any) -> Any:
             self._drop()
+            self.clean = 0
             return base(self, *args, **kwargs)
 
         method.__name__ = name
@@ -111,6 +117,7 @@ class StateArena(list):
         (views of the untouched prefix) but no longer appends into that buffer, so a list that is still shared
         elsewhere is never extended behind its holders' backs."""
         out = cls(other)
+        out.clean = other.clean
         if other._buf is not None and other._covered == len(other):
             out._buf, out._rows, out._covered = other._buf, other._rows, other._covered
         other._drop()
@@ -119,6 +126,7 @@ class StateArena(list):
     def truncate(self, k: int) -> None:
         """Drop the items from ``k`` on, keeping the buffer (and its free tail) when it covers the first ``k``."""
         k = max(0, min(k, len(self)))
+        self.clean = min(self.clean, k)
         if self._buf is not None and self._covered >= k:
             self._rows = sum(self._rows_of(t)[0] for t in self[:k])
             self._covered = k
@@ -150,6 +158,10 @@ class StateArena(list):
         self._buf, self._rows, self._covered = buf, total, len(self)
         return buf[:total]
 
+    def owns(self, t: Tensor) -> bool:
+        """True if ``t`` is a view of this arena's buffer."""
+        return self._buf is not None and t.untyped_storage().data_ptr() == self._buf.untyped_storage().data_ptr()
+
     @property
     def capacity(self) -> int:
         """Rows of the backing buffer (0 before the first compaction)."""
@@ -175,5 +187,6 @@ class StateArena(list):
             out._buf, out._rows, out._covered = buf, self._rows, len(self)
         else:
             list.extend(out, (deepcopy(t, memo) for t in self))
+        out.clean = self.clean
         memo[id(self)] = out
         return out

@@ -17,6 +17,11 @@ Requirements (checked, with a clear error instead of wrong numbers):
 
 Warm-up updates run on a side stream before capture (as for any graph capture) and are rolled back: states and
 deferred-check flags are restored, so the graphed metric holds exactly the replayed batches.
+
+The graph writes into the storage the states had at capture time.  ``reset()``, ``forward()``, ``.to()`` and
+``load_state_dict`` rebind states to new tensors, so every replay first compares the members' current state and flag
+storages with the captured ones and re-captures (same warm-up and roll-back) when any of them moved: the usual
+``compute(); reset()`` epoch loop keeps accumulating into the live states instead of into orphaned buffers.
 """
 from typing import Any, Dict, List, Tuple, Union
 
@@ -65,14 +70,20 @@ class GraphedUpdate:
         if not torch.cuda.is_available():
             raise RuntimeError("GraphedUpdate needs a GPU")
         self.metric = metric
-        self._members = _members(metric)
+        self._warmup = warmup
         inputs = _flatten_inputs(example_args, example_kwargs)
         self._static_args = tuple(a.clone() if isinstance(a, Tensor) else a for a in example_args)
         self._static_kwargs = {k: (v.clone() if isinstance(v, Tensor) else v) for k, v in example_kwargs.items()}
         self._static_inputs = _flatten_inputs(self._static_args, self._static_kwargs)
         self._shapes = [(t.shape, t.dtype) for t in inputs]
-        device = inputs[0].device if inputs else torch.device("cuda", torch.cuda.current_device())
+        self._device = inputs[0].device if inputs else torch.device("cuda", torch.cuda.current_device())
+        self.captures = 0
+        self._capture()
 
+    def _capture(self) -> None:
+        """Warm up on a side stream, roll back, capture one update; records the storages the graph writes."""
+        metric, warmup, device = self.metric, self._warmup, self._device
+        self._members = _members(metric)
         counts = [m._update_count for m in self._members]
         lists = self._list_lengths()
         states = self._tensor_states()
@@ -115,6 +126,8 @@ class GraphedUpdate:
                 hook()
         self._graph = graph
         self._reset_counts(counts)
+        self._ptrs = self._storage_ptrs()
+        self.captures += 1
         torch.cuda.synchronize(device)
 
     # -------------------------------------------------------------------------------------------- helpers
@@ -129,6 +142,20 @@ class GraphedUpdate:
                     raise ValueError(f"GraphedUpdate: state `{name}` of {type(m).__name__} is not on the GPU")
                 out[(i, name)] = val
         return out
+
+    def _storage_ptrs(self) -> List[int]:
+        """Data pointers of every tensor state and deferred-check flag the graph writes (plus the member identities)."""
+        members = _members(self.metric)
+        ptrs: List[int] = [id(m) for m in members]
+        for m in members:
+            for name in m._defaults:
+                val = getattr(m, name)
+                if isinstance(val, Tensor):
+                    ptrs.append(val.data_ptr())
+            d = m._deferred
+            if d is not None:
+                ptrs.extend(f.data_ptr() for f in d._flags.values())
+        return ptrs
 
     def _list_lengths(self) -> List[int]:
         return [len(getattr(m, n)) for m in self._members for n in m._defaults if isinstance(getattr(m, n), list)]
@@ -182,6 +209,11 @@ class GraphedUpdate:
                 f"GraphedUpdate: batch shapes {[(tuple(t.shape), t.dtype) for t in inputs]} differ from the captured"
                 f" {[(tuple(s), d) for s, d in self._shapes]}"
             )
+        if self._storage_ptrs() != self._ptrs:
+            # reset() / forward() / .to() / load_state_dict rebound a state or flag: the captured graph would add into
+            # the old storage, so capture again against the live one
+            self._graph = None
+            self._capture()
         for dst, src in zip(self._static_inputs, inputs):
             dst.copy_(src, non_blocking=True)
         self._graph.replay()

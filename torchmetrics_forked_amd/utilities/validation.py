@@ -39,6 +39,7 @@ class HostCheckBatch:
     def __init__(self) -> None:
         self._items: List[Tuple[Tensor, Callable[[List[int]], None], bool]] = []
         self._on_error: List[Callable[[], None]] = []
+        self._on_abandon: List[Callable[[], None]] = []
 
     def add(self, flags: Tensor, callback: Callable[[List[int]], None], error: bool = False) -> None:
         self._items.append((flags.reshape(-1).to(torch.int32), callback, error))
@@ -47,7 +48,19 @@ class HostCheckBatch:
         """Run ``fn`` if an error callback raises (e.g. drop a cached compute value)."""
         self._on_error.append(fn)
 
+    def on_abandon(self, fn: Callable[[], None]) -> None:
+        """Run ``fn`` if the block ends by an exception before resolving (e.g. put consumed device flags back, so the
+        next compute still raises for the invalid inputs)."""
+        self._on_abandon.append(fn)
+
+    def abandon(self) -> None:
+        fns, self._on_abandon = self._on_abandon, []
+        self._items, self._on_error = [], []
+        for fn in fns:
+            fn()
+
     def resolve(self) -> None:
+        self._on_abandon = []
         items, self._items = self._items, []
         on_error, self._on_error = self._on_error, []
         if not items:
@@ -106,6 +119,8 @@ def host_checks() -> Iterator[HostCheckBatch]:
         st.pop()
         if ok:
             batch.resolve()
+        else:
+            batch.abandon()
 
 
 def defer_host_check(flags: Tensor, callback: Callable[[List[int]], None], error: bool = False) -> None:
@@ -183,6 +198,13 @@ class DeferredChecks:
         batch.add(snap, _raise, error=True)
         if warn_keys:
             batch.add(snap, _warn, error=False)
+        flags = [self._flags[k] for k in keys]
+
+        def _put_back() -> None:  # the block raised before reading: the flags still owe their exception
+            for i, f in enumerate(flags):
+                f.bitwise_or_(snap[i].to(f.device, f.dtype).reshape(f.shape))
+
+        batch.on_abandon(_put_back)
 
     def clear(self) -> None:
         for f in self._flags.values():

@@ -112,6 +112,9 @@ class BootStrapper(WrapperMetric):
         drawn = self._resample_counts(self._batch_size(args, kwargs))
         counts = drawn[0]
         fast = getattr(self.metrics[0], "_bootstrap_deltas", None) if len(self.metrics) else None
+        if fast is not None and getattr(self.metrics[0], "compute_on_cpu", False):
+            fast = None  # the copies' wrapped update moves states to the host; keep that path
+        # the deltas validate the un-resampled batch eagerly (same checks and messages as the base update)
         deltas = fast(counts.to(self.device), *args, **kwargs) if fast is not None else None
         if deltas is None:
             for idx, new_args, new_kwargs in self._resampled(drawn, args, kwargs):
@@ -123,7 +126,7 @@ class BootStrapper(WrapperMetric):
                 continue
             for name, d in deltas.items():
                 cur = getattr(m, name)
-                setattr(m, name, cur + d[b].reshape(cur.shape).to(cur.dtype))
+                cur.add_(d[b].reshape(cur.shape).to(cur.dtype))  # in place: the state keeps its storage
             m._update_count += 1
             m._computed = None
 
