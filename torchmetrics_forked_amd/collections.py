@@ -1,9 +1,13 @@
 """``MetricCollection`` (API parity: reference ``collections.py:34-660``) with two MI355X-first additions.
 
-1. **Collection-level coalesced sync.**  ``compute()`` synchronises the states of *all* members (compute-group
-   leaders only, members share state by reference) with one :func:`parallel.sync.sync_states_many` plan: one
-   RCCL ``all_reduce`` per (op, dtype) bucket and one packed all-gather for list states, instead of each member
-   syncing on its own (reference SURVEY §3.4: members re-gather shared tensors).
+1. **Collection-level coalesced, overlapped sync.**  ``compute()`` synchronises the states of *all* members
+   (compute-group leaders only, members share state by reference) with coalesced plans
+   (:class:`parallel.sync.PendingSyncMany`): one RCCL ``all_reduce`` per (op, dtype) bucket and one packed
+   all-gather for list states per member group, instead of each member syncing on its own (reference SURVEY §3.4:
+   members re-gather shared tensors).  Members are grouped in compute order up to ~1 MiB of reducible state; every
+   group's all-reduces are enqueued up front and a group is waited for only when its first member computes, so
+   member ``i``'s compute kernels overlap the transfers of the members after it (reference: blocking per-member
+   sync inside each ``compute``, ``collections.py:309-358`` / ``metric.py:423-453``).
 2. **Fused update plans.**  Members that consume the same ``(preds, target)`` and advertise a compatible
    ``_fusion_key()`` (e.g. ``MulticlassAUROC`` exact-histogram + ``MulticlassConfusionMatrix`` on the same
    logits) are updated by one fused kernel pass over ``preds`` (:mod:`..ops.fused`), instead of one pass per
@@ -19,7 +23,7 @@ from torch import Tensor
 from torch.nn import ModuleDict
 
 from torchmetrics_forked_amd.metric import Metric
-from torchmetrics_forked_amd.parallel.sync import sync_states_many, sync_timeout
+from torchmetrics_forked_amd.parallel.sync import PendingSyncMany, sync_states_many, sync_timeout
 from torchmetrics_forked_amd.utilities.data import _flatten_dict, allclose
 from torchmetrics_forked_amd.utilities.plot import _AX_TYPE, _PLOT_OUT_TYPE, plot_single_or_multi_val
 from torchmetrics_forked_amd.utilities.prints import rank_zero_warn
@@ -157,8 +161,18 @@ class MetricCollection(ModuleDict):
             finally:
                 self._collection_unsync(synced)
 
+    # reducible bytes per async sync group: members are grouped in compute order until a group carries this much
+    # (one coalesced all-reduce per group and dtype); small states stay in one collective, large ones (confusion
+    # matrices, FID moments, histograms) get their own so the next member's transfer overlaps this one's compute
+    _OVERLAP_GROUP_BYTES = 1 << 20
+
     def _collection_sync(self) -> List[Tuple[Metric, bool]]:
-        """Sync every eligible leader in one coalesced plan; returns (metric, previous _to_sync) to restore."""
+        """Start syncing every eligible leader (async, grouped); returns (metric, previous _to_sync) to restore.
+
+        The all-reduce buckets of every group are enqueued at once, in member order (the same on every rank); each
+        group's states are installed only when its first member computes (``_install_pending``), so the compute
+        kernels of earlier members run while later groups' collectives are still in flight on RCCL's stream."""
+        self._pending_sync: Dict[int, Any] = {}
         members = list(self._modules.values())
         if not members:
             return []
@@ -174,34 +188,70 @@ class MetricCollection(ModuleDict):
             and type(m)._sync_dist is Metric._sync_dist
             and m.distributed_available_fn()
         ]
-        if len(eligible) < 2:
+        if not eligible:
             return []
         groups = {m.process_group for m in eligible}
         if len(groups) != 1:
             return []
         group = next(iter(groups))
         bounds = [m.sync_timeout for m in eligible if getattr(m, "sync_timeout", None) is not None]
-        with sync_timeout(min(bounds) if bounds else None):
-            synced = sync_states_many([m.metric_state for m in eligible], [m._reductions for m in eligible], group=group)
-        restore: List[Tuple[Metric, bool]] = []
-        for m, new_states in zip(eligible, synced):
-            m._cache = m.metric_state
-            for k, v in new_states.items():
-                setattr(m, k, v)
-            m._is_synced = True
-        if self._groups_checked:
-            self._compute_groups_create_state_ref()
+        timeout = min(bounds) if bounds else None
+        batches: List[List[Metric]] = [[]]
+        size = 0
+        for m in eligible:
+            batches[-1].append(m)
+            size += sum(v.numel() * v.element_size() for v in m.metric_state.values() if isinstance(v, Tensor))
+            if size >= self._OVERLAP_GROUP_BYTES:
+                batches.append([])
+                size = 0
+        for batch in batches:
+            if not batch:
+                continue
+            pending = PendingSyncMany([m.metric_state for m in batch], [m._reductions for m in batch], group, timeout)
+            for i, m in enumerate(batch):
+                self._pending_sync[id(m)] = (pending, batch, i)
         eligible_ids = {id(m) for m in eligible}
         if self._groups_checked:
             affected = [getattr(self, n) for cg in self._groups.values() if id(getattr(self, cg[0])) in eligible_ids for n in cg]
         else:
             affected = eligible
+        restore: List[Tuple[Metric, bool]] = []
         for m in affected:
             restore.append((m, m._to_sync))
             m._to_sync = False
         return restore
 
+    def _install_pending(self, m: Metric) -> None:
+        """Wait for the async sync group holding ``m`` (or its compute-group leader) and install the synced states."""
+        pend = getattr(self, "_pending_sync", None)
+        if not pend:
+            return
+        key = id(m)
+        if key not in pend and self._groups_checked:
+            for cg in self._groups.values():
+                names = [n for n in cg if getattr(self, n) is m]
+                if names:
+                    key = id(getattr(self, cg[0]))
+                    break
+        entry = pend.get(key)
+        if entry is None:
+            return
+        pending, batch, _ = entry
+        synced = pending.wait()
+        for bm, new_states in zip(batch, synced):
+            pend.pop(id(bm), None)
+            bm._cache = bm.metric_state
+            for k, v in new_states.items():
+                setattr(bm, k, v)
+            bm._is_synced = True
+        if self._groups_checked:
+            self._compute_groups_create_state_ref()
+
     def _collection_unsync(self, restore: List[Tuple[Metric, bool]]) -> None:
+        pend = getattr(self, "_pending_sync", None)
+        if pend:  # a member raised before computing: still complete its collectives (every rank issued them)
+            for m in [getattr(self, n) for n in self._leaders()]:
+                self._install_pending(m)
         if not restore:
             return
         for m, to_sync in restore:
@@ -239,6 +289,7 @@ class MetricCollection(ModuleDict):
         fused = self._forward_fused(args, kwargs) if method_name == "forward" else {}
         for k, m in self.items(keep_base=True, copy_state=False):
             if method_name == "compute":
+                self._install_pending(m)
                 res = m.compute()
             elif method_name == "forward" and k in fused:
                 res = fused[k]

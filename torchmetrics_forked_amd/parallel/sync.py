@@ -215,15 +215,49 @@ def _gather_flat(buf: Tensor, world: int, what: str, group: Optional[Any]) -> Te
     return out
 
 
+_KIND_ELEMS, _KIND_RAGGED, _KIND_SCALARS = 0, 1, 2
+
+
+def _ragged_layout(lst: List[Any]) -> Optional[Tuple[int, Tuple[int, ...], List[int], Tensor]]:
+    """(kind, trailing shape, rows per item, one contiguous buffer) when every item of ``lst`` is a tensor of one
+    dtype / device and either all are 0-d (``_KIND_SCALARS``) or all share the trailing shape (``_KIND_RAGGED``: item
+    ``i`` is ``[rows_i, *tail]``); ``None`` otherwise.  The buffer is the arena's compacted view when the list is a
+    ``StateArena`` (no copy), else one ``torch.cat`` -- one kernel per state instead of one piece per item."""
+    if len(lst) < 2:
+        return None
+    first = lst[0]
+    if not isinstance(first, Tensor) or first.requires_grad:
+        return None
+    dtype, device = first.dtype, first.device
+    if first.ndim == 0:
+        for t in lst:
+            if not isinstance(t, Tensor) or t.ndim != 0 or t.dtype != dtype or t.device != device:
+                return None
+        return _KIND_SCALARS, (), [1] * len(lst), dim_zero_cat(lst)
+    tail = tuple(first.shape[1:])
+    rows: List[int] = []
+    for t in lst:
+        if not isinstance(t, Tensor) or t.ndim == 0 or t.dtype != dtype or t.device != device or tuple(t.shape[1:]) != tail:
+            return None
+        rows.append(t.shape[0])
+    return _KIND_RAGGED, tail, rows, dim_zero_cat(lst)
+
+
 def all_gather_packed(
     groups: List[List[Tensor]], group: Optional[Any], device_hint: Optional[Tensor] = None
 ) -> List[List[List[Tensor]]]:
     """Gather several lists of tensors (of arbitrary, per-rank-varying shapes/lengths) from every rank.
 
-    Two collectives in total, whatever the number of tensors: a fixed-size header (element count per slot and
-    payload bytes) and one padded buffer holding this rank's shape table followed by every tensor's bytes at
-    16-byte aligned offsets.  The only host reads are the header and the shape tables (one small copy each); the
-    returned tensors are views into the gathered buffer (no per-element copies or ``.item()`` calls).
+    Two collectives in total, whatever the number of tensors: a fixed-size header (element count per slot, table
+    words and payload bytes) and one padded buffer holding this rank's layout table followed by the payload at
+    16-byte aligned offsets.
+
+    Host work is O(slots), not O(tensors), for the common list states (mAP's per-image boxes / labels / scores,
+    retrieval's per-batch rows, KID feature lists): a slot whose items share dtype, device and trailing shape is
+    moved as ONE buffer plus a row-count vector (``_ragged_layout``; a ``StateArena`` hands over its compacted buffer
+    without a copy) and split back with one ``torch.split`` per rank.  Only lists mixing dtypes / trailing shapes
+    fall back to one table record and one payload piece per tensor.  The only host reads are the header and the
+    layout tables (one copy each).
 
     Args:
         groups: ``groups[s]`` is this rank's list of tensors for slot ``s`` (same number of slots on every rank).
@@ -240,65 +274,94 @@ def all_gather_packed(
                 break
     comm_dev = _comm_device(sample, group)
 
-    flat_elems: List[Tensor] = [t for lst in groups for t in lst]
-    rec = 3 + _MAX_DIMS
-    rows: List[List[int]] = []
+    # 1) layout table (int64 words) and payload pieces of this rank
+    table: List[int] = []
+    pieces: List[Tensor] = []
     payload = 0
-    for t in flat_elems:
-        if t.ndim > _MAX_DIMS:
-            raise ValueError(f"metric state with ndim={t.ndim} > {_MAX_DIMS} cannot be synced")
-        nbytes = t.numel() * t.element_size()
-        rows.append([_DTYPE_CODE[t.dtype], t.ndim, nbytes, *t.shape] + [0] * (_MAX_DIMS - t.ndim))
-        payload += _pad16(nbytes)
+    for lst in groups:
+        lay = _ragged_layout(lst)
+        if lay is not None:
+            kind, tail, rows, buf = lay
+            if len(tail) > _MAX_DIMS:
+                raise ValueError(f"metric state with ndim={len(tail) + 1} > {_MAX_DIMS} cannot be synced")
+            b = _to_bytes(buf)
+            table += [kind, _DTYPE_CODE[buf.dtype], len(tail), *tail, *([0] * (_MAX_DIMS - len(tail))), b.numel(), len(rows)]
+            if kind == _KIND_RAGGED:
+                table += rows
+            pieces.append(b)
+            payload += _pad16(b.numel())
+            continue
+        table += [_KIND_ELEMS, len(lst)]
+        for t in lst:
+            if t.ndim > _MAX_DIMS:
+                raise ValueError(f"metric state with ndim={t.ndim} > {_MAX_DIMS} cannot be synced")
+            b = _to_bytes(t)
+            table += [_DTYPE_CODE[t.dtype], t.ndim, b.numel(), *t.shape, *([0] * (_MAX_DIMS - t.ndim))]
+            pieces.append(b)
+            payload += _pad16(b.numel())
 
-    # 1) header: element count per slot + payload bytes of this rank
-    header = torch.tensor([len(lst) for lst in groups] + [payload], dtype=torch.int64, device=comm_dev)
+    # 2) header: element count per slot + table words + payload bytes of this rank
+    header = torch.tensor([len(lst) for lst in groups] + [len(table), payload], dtype=torch.int64, device=comm_dev)
     hdr = _gather_flat(header, world, "all_gather(element counts)", group).tolist()
     counts = [row[:n_slots] for row in hdr]
-    max_elems = max(sum(c) for c in counts) if n_slots else 0
-    if max_elems == 0:
+    if not n_slots or max(sum(c) for c in counts) == 0:
         return [[[] for _ in range(world)] for _ in range(n_slots)]
-    table_bytes = _pad16(max_elems * rec * 8)
-    span = table_bytes + max(max(row[n_slots] for row in hdr), _ALIGN)
+    table_bytes = _pad16(max(row[n_slots] for row in hdr) * 8)
+    span = table_bytes + max(max(row[n_slots + 1] for row in hdr), _ALIGN)
 
-    # 2) one buffer per rank: [shape table | payload], padded to the largest rank
-    table = torch.zeros(table_bytes // 8, dtype=torch.int64)
-    if rows:
-        table[: len(rows) * rec] = torch.tensor(rows, dtype=torch.int64).reshape(-1)
-    pieces: List[Tensor] = [table.view(torch.uint8).to(comm_dev)]
-    used = table_bytes
-    for t in flat_elems:
-        b = _to_bytes(t).to(comm_dev)
-        pieces.append(b)
+    # 3) one buffer per rank [table | payload], padded to the largest rank: a single concatenation
+    send = torch.zeros(span, dtype=torch.uint8, device=comm_dev)
+    if table:
+        send[: len(table) * 8] = torch.tensor(table, dtype=torch.int64).view(torch.uint8).to(comm_dev)
+    off = table_bytes
+    cat_parts: List[Tensor] = []
+    for b in pieces:
         pad = _pad16(b.numel()) - b.numel()
+        cat_parts.append(b.to(comm_dev))
         if pad:
-            pieces.append(torch.zeros(pad, dtype=torch.uint8, device=comm_dev))
-        used += b.numel() + pad
-    if span > used:
-        pieces.append(torch.zeros(span - used, dtype=torch.uint8, device=comm_dev))
-    gathered = _gather_flat(torch.cat(pieces), world, "all_gather(packed states)", group)
-    tables = gathered[:, :table_bytes].cpu().view(torch.int64)[:, : max_elems * rec].reshape(world, max_elems, rec).tolist()
+            cat_parts.append(send.new_zeros(pad))
+        off += b.numel() + pad
+    if cat_parts:
+        torch.cat(cat_parts, out=send[table_bytes:off])
+    gathered = _gather_flat(send, world, "all_gather(packed states)", group)
+    tables = gathered[:, :table_bytes].cpu().view(torch.int64).tolist()
 
-    # 3) unpack as views of the gathered buffer (moved once per slot device when it differs)
+    # 4) unpack as views of the gathered buffer (moved once per slot device when it differs)
+    devs = [lst[0].device if lst else (sample.device if sample is not None else torch.device("cpu")) for lst in groups]
     by_dev: Dict[torch.device, Tensor] = {torch.device(comm_dev): gathered}
-    result: List[List[List[Tensor]]] = [[[] for _ in range(world)] for _ in range(n_slots)]
-    for s, lst in enumerate(groups):
-        dev = lst[0].device if lst else (sample.device if sample is not None else torch.device("cpu"))
+    for dev in devs:
         if dev not in by_dev:
             by_dev[dev] = gathered.to(dev)
+    result: List[List[List[Tensor]]] = [[[] for _ in range(world)] for _ in range(n_slots)]
     for r in range(world):
         tb = tables[r]
-        off = table_bytes
-        e = 0
-        for s, lst in enumerate(groups):
-            dev = lst[0].device if lst else (sample.device if sample is not None else torch.device("cpu"))
-            src = by_dev[dev][r]
-            out = result[s][r]
-            for _ in range(counts[r][s]):
-                code, ndim, nbytes = tb[e][0], tb[e][1], tb[e][2]
-                out.append(_from_bytes(src[off : off + nbytes], _DTYPES[code], tb[e][3 : 3 + ndim]))
-                off += _pad16(nbytes)
-                e += 1
+        pos, off = 0, table_bytes
+        for s in range(n_slots):
+            src = by_dev[devs[s]][r]
+            kind = tb[pos]
+            if kind == _KIND_ELEMS:
+                n = tb[pos + 1]
+                pos += 2
+                out = result[s][r]
+                for _ in range(n):
+                    code, ndim, nbytes = tb[pos], tb[pos + 1], tb[pos + 2]
+                    out.append(_from_bytes(src[off : off + nbytes], _DTYPES[code], tb[pos + 3 : pos + 3 + ndim]))
+                    off += _pad16(nbytes)
+                    pos += 3 + _MAX_DIMS
+                continue
+            code, ndim = tb[pos + 1], tb[pos + 2]
+            tail = tb[pos + 3 : pos + 3 + ndim]
+            nbytes, n = tb[pos + 3 + _MAX_DIMS], tb[pos + 4 + _MAX_DIMS]
+            pos += 5 + _MAX_DIMS
+            if kind == _KIND_SCALARS:
+                flat = _from_bytes(src[off : off + nbytes], _DTYPES[code], [n])
+                result[s][r] = list(flat.unbind(0))
+            else:
+                rows = tb[pos : pos + n]
+                pos += n
+                flat = _from_bytes(src[off : off + nbytes], _DTYPES[code], [sum(rows), *tail])
+                result[s][r] = list(torch.split(flat, rows))
+            off += _pad16(nbytes)
     return result
 
 
@@ -314,6 +377,32 @@ def sync_states_many(
     group: Optional[Any] = None,
 ) -> List[Dict[str, StateT]]:
     """Synchronise the states of several metrics with one coalesced plan (see module docstring)."""
+    return _sync_many(state_dicts, reduction_dicts, group, None)
+
+
+def _split_reducible(
+    state_dicts: List[Dict[str, StateT]], reduction_dicts: List[Dict[str, Optional[Callable]]]
+) -> Tuple[List[Tuple[str, Tensor, str]], List[Dict[str, StateT]]]:
+    reduce_items: List[Tuple[str, Tensor, str]] = []
+    rest: List[Dict[str, StateT]] = [dict() for _ in state_dicts]
+    for mi, (states, reds) in enumerate(zip(state_dicts, reduction_dicts)):
+        for name, value in states.items():
+            fn = reds.get(name)
+            if isinstance(value, Tensor) and fn in _REDUCE_OPS:
+                reduce_items.append((f"{mi}:{name}", value, _REDUCE_OPS[fn]))
+            else:
+                rest[mi][name] = value
+    return reduce_items, rest
+
+
+def _sync_many(
+    state_dicts: List[Dict[str, StateT]],
+    reduction_dicts: List[Dict[str, Optional[Callable]]],
+    group: Optional[Any],
+    launched: Optional[List[Tuple]],
+) -> List[Dict[str, StateT]]:
+    """``sync_states_many`` body; ``launched`` = all-reduce buckets already started for the reducible states (then
+    ``state_dicts`` hold only the other states)."""
     reduce_items: List[Tuple[str, Tensor, str]] = []
     gather_slots: List[List[Tensor]] = []
     gather_meta: List[Tuple[int, str, str]] = []  # (metric idx, state name, kind)
@@ -343,8 +432,8 @@ def sync_states_many(
                 gather_slots.append(list(value))
                 gather_meta.append((mi, name, "list"))
 
-    if reduce_items:
-        reduced = _all_reduce_coalesced(reduce_items, group)
+    if reduce_items or launched:
+        reduced = _finish_all_reduce(launched, group) if launched is not None else _all_reduce_coalesced(reduce_items, group)
         for key, t in reduced.items():
             mi, name = key.split(":", 1)
             outputs[int(mi)][name] = t
@@ -410,6 +499,35 @@ class PendingSync:
                 if self._rest:
                     out.update(sync_states(self._rest, {k: self._reductions.get(k) for k in self._rest}, self._group))
             self._result = out
+        return self._result
+
+
+class PendingSyncMany:
+    """``sync_states_many`` split in two: the constructor enqueues the coalesced all-reduce buckets of every metric's
+    reducible states (RCCL runs them while the caller keeps the compute stream busy); :meth:`wait` finishes them, runs
+    the packed all-gather of the remaining (list / ``cat`` / ``None``) states and returns one synced dict per metric.
+    ``MetricCollection.compute`` starts one of these per member group up front and waits for each group just before
+    its members compute, so member ``i``'s compute kernels overlap member ``i + 1``'s transfers."""
+
+    def __init__(
+        self,
+        state_dicts: List[Dict[str, StateT]],
+        reduction_dicts: List[Dict[str, Optional[Callable]]],
+        group: Optional[Any],
+        timeout: Optional[float] = None,
+    ) -> None:
+        self._group = group
+        self._reductions = reduction_dicts
+        self._timeout = timeout if timeout is not None else current_timeout()
+        reduce_items, self._rest = _split_reducible(state_dicts, reduction_dicts)
+        with sync_timeout(self._timeout):
+            self._launched = _launch_all_reduce(reduce_items, group, async_op=True)
+        self._result: Optional[List[Dict[str, StateT]]] = None
+
+    def wait(self) -> List[Dict[str, StateT]]:
+        if self._result is None:
+            with sync_timeout(self._timeout):
+                self._result = _sync_many(self._rest, self._reductions, self._group, self._launched)
         return self._result
 
 
