@@ -1629,8 +1629,8 @@ void curve_hist_update(const at::Tensor& preds_, const at::Tensor& target_, at::
   const bool speculative = two_pass_ok && mode_state.has_value() && !norm_flag.has_value();
   at::Tensor flag, state;
   if (speculative) {
-    TORCH_CHECK(mode_state->scalar_type() == at::kInt && mode_state->numel() == 8 && mode_state->is_contiguous(),
-                "mode_state must be int32[8]");
+    TORCH_CHECK(mode_state->scalar_type() == at::kInt && mode_state->numel() >= 8 && mode_state->is_contiguous(),
+                "mode_state must be int32[>= 8]");
     flag = *mode_state;
     state = mode_state->narrow(0, 2, 6);
   } else {

@@ -1,5 +1,9 @@
-// Single-launch exact-histogram multiclass update (device code + launch helper, no torch headers; shared by
-// csrc/classification.hip and the harness tools/kexp/persist_exp.hip).
+// EXPERIMENT (not on the library's hot path): persistent producer / consumer exact-histogram multiclass update, with
+// its harness tools/kexp/persist_exp.hip.  Bit-identical to the two-pass route on every harness case (logits, NaN /
+// inf / tied rows, ignore_index, probabilities, both mis-speculations, u16 wrap at N = 131072) but measured 2.2x
+// SLOWER at 65536 x 1000 bf16 (profiles/persist_curve_experiment.json): the consumer's 127 KiB of class histograms
+// leave the producer half a CU (8 waves), and a 32-row tile then takes ~15 us per CU (two-pass row pass: two
+// 64-KiB blocks per CU, ~8 us per tile per CU).  Kept for the record and for future hardware with more LDS.
 //
 // Why: the two-pass route (curve_hist_kernels.h) writes the whole batch as class-major 16-bit codes to HBM and reads
 // it back in a second launch: 131 MB logits + 131 MB codes written + 131 MB codes read per 65536 x 1000 bf16 update,
@@ -35,18 +39,27 @@
 
 namespace tmx {
 
-constexpr int kPThreads = 512;
+#ifndef TMX_PERSIST_TILE_PROF
+#define TMX_PERSIST_TILE_PROF 0  // harness-only: per-tile producer stamps instead of per-chunk phase stamps
+#endif
+constexpr int kPThreads = 512;  // producer workgroup
+constexpr int kCThreads = 256;  // consumer workgroup: one wave per SIMD beside the producer's two
 constexpr int kPWaves = kPThreads / kWave;  // 8: two row pairs of the 32-row tile per wave (pairs w and w + 8)
 constexpr int kPHistWords = 8132;          // u16 pairs: codes 0 .. 16263 >= 16256 (bf16 1.0) and 15360 (fp16 1.0)
 constexpr int kPMaxClasses = 4;            // classes per workgroup
 constexpr int kPImageWords = 512 * kSlots; // one 512-class half of a 32-row tile (32 KiB)
-constexpr int kPWrapSlots = 32;
-constexpr int kPMaxChunks = 48;
+constexpr int kPWrapSlots = 16;
+constexpr int kPMaxChunks = 46;
 // control words (int32) after the 8 words of mode_state: ready[2][kPMaxChunks] (round 1 / round 2), then
-constexpr int kPCtrlTicket = 2 * kPMaxChunks;
-constexpr int kPCtrlTimeout = kPCtrlTicket + 1;
+constexpr int kPCtrlTicket = 2 * kPMaxChunks;      // 2 G arrivals (producers and consumers)
+constexpr int kPCtrlTimeout = kPCtrlTicket + 1;    // sticky error word (read as a deferred check at compute)
+constexpr int kPCtrlProdDone = kPCtrlTicket + 2;   // producers done with round 0 (verdict barrier among producers)
 constexpr int kPCtrlWords = kPCtrlTicket + 4;
-constexpr size_t kPLdsBytes = (size_t)kPMaxClasses * kPHistWords * 4 + (size_t)kPImageWords * 4 + (size_t)kPWrapSlots * 8 + 64;
+// Two kernels share every CU: the consumer workgroup (4 class histograms) and the producer workgroup (one 512-class
+// LDS image of a tile).  130,368 + 32,784 B <= 163,840 B with 512-B allocation granules (130,560 + 33,280).
+constexpr size_t kPConsumerLds = (size_t)kPMaxClasses * kPHistWords * 4 + (size_t)kPWrapSlots * 8 + 128;
+constexpr size_t kPProducerLds = (size_t)kPImageWords * 4 + 16;
+constexpr size_t kPLdsBytes = kPConsumerLds;
 constexpr long long kPSpinLimit = 1 << 22;  // ~4M polls with s_sleep(2): far beyond any healthy wait
 
 // buffer resource over a byte range (< 2^31 B): raw loads / stores with an explicit cache policy
@@ -54,6 +67,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t p_rsrc(const void* base, uint3
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, bytes, 0x00020000);
 }
 using p_v4u = __attribute__((ext_vector_type(4))) unsigned int;
+#ifndef TMX_PERSIST_STORE_POLICY
+#define TMX_PERSIST_STORE_POLICY 16  // harness A/B only: 0 = plain stores (NOT a valid hand-off across XCDs)
+#endif
 constexpr int kSc1 = 16;  // CPol SC1 (agent-coherent: write-through / L1 bypass)
 
 // Workgroup barrier for LDS hand-offs only.  __syncthreads() on gfx950 also waits for every outstanding global load
@@ -96,9 +112,13 @@ __device__ __forceinline__ int p_spin_until(int* ctr, int target, int* timeout_f
 
 // Codes of one row pair (rows r0, r0 + 1 of this wave) for a fixed mode; the same arithmetic as row_tile.
 // code[8 g + j] = class 512 g + 8 lane + j, row r0 in the low half, r0 + 1 in the high half.
-template <typename T, int NG, bool SOFTMAX, bool ROUND2>
+// SOFTMAX and ROUND2 are wave-uniform RUNTIME flags (scalar branches), not template parameters: one copy of this
+// body in the kernel (four inlined instances made a 280 KB code object).
+// ``pos_t[h]`` = the target class of row r0 + h when the row is kept and its target is a class (its positive code is
+// extracted from the LDS image in p_store_tile), else -1.
+template <typename T, int NG>
 __device__ __forceinline__ void p_pair_codes(const uint4 (&raw)[2][2], int64_t tv, int tlane, int64_t r0, const PersistArgs& a, int nvec,
-                                             uint32_t (&code)[8 * NG], bool& saw_bad) {
+                                             uint32_t (&code)[8 * NG], int (&pos_t)[2], bool& saw_bad, const bool SOFTMAX, const bool ROUND2) {
   const int lane = threadIdx.x & (kWave - 1);
   const bool lo_ok = lane < nvec, hi_ok = lane + kWave < nvec;
   const int64_t n = a.n;
@@ -117,12 +137,12 @@ __device__ __forceinline__ void p_pair_codes(const uint4 (&raw)[2][2], int64_t t
   row_stat<T, NG>(raw[1], lo_ok, hi_ok, rb);
   bool fa = __builtin_isfinite(ra.mx), fb = __builtin_isfinite(rb.mx);
   int ama = 0, amb = 0;
-  if constexpr (!ROUND2) {
+  if (!ROUND2) {
     ama = row_argmax<NG>(ra);
     amb = row_argmax<NG>(rb);
   }
   float sa = 0.f, sb = 0.f, ia = 0.f, ib = 0.f;
-  if constexpr (SOFTMAX) {
+  if (SOFTMAX) {
     float acc_a = 0.f, acc_b = 0.f;
 #pragma unroll
     for (int j = 0; j < 8 * NG; ++j) {
@@ -149,33 +169,20 @@ __device__ __forceinline__ void p_pair_codes(const uint4 (&raw)[2][2], int64_t t
   const bool ka = va && fa, kb = vb && fb;
   const uint32_t keep = (ka ? 0x0000FFFFu : 0u) | (kb ? 0xFFFF0000u : 0u);
   const uint32_t setm = ~keep & 0x80008000u;
-  // the target class of each row sits in lane (t & 511) >> 3, element 8 (t >> 9) + (t & 7) (wave-uniform)
-  const bool pa = ka && ta >= 0 && ta < C, pb = kb && tb >= 0 && tb < C;
-  const int La = pa ? static_cast<int>((ta & 511) >> 3) : 0, Ea = pa ? static_cast<int>(8 * (ta >> 9) + (ta & 7)) : -1;
-  const int Lb = pb ? static_cast<int>((tb & 511) >> 3) : 0, Eb = pb ? static_cast<int>(8 * (tb >> 9) + (tb & 7)) : -1;
-  uint32_t sel_a = 0x8000u, sel_b = 0x80000000u;
 #pragma unroll
   for (int j = 0; j < 8 * NG; ++j) {
     uint32_t packed;
-    if constexpr (SOFTMAX) {
+    if (SOFTMAX) {
       packed = __builtin_amdgcn_perm(rne_word<T>(div_rn(rb.v[j], sb, ib)), rne_word<T>(div_rn(ra.v[j], sa, ia)), 0x07060302u);
     } else {
       const uint32_t ca = raw_code<T>(raw_bits<T>(raw[0][j >> 3], j & 7));
       const uint32_t cb = raw_code<T>(raw_bits<T>(raw[1][j >> 3], j & 7));
       packed = ca | (cb << 16);
     }
-    const uint32_t w = (packed & keep) | setm;
-    sel_a = j == Ea ? w : sel_a;
-    sel_b = j == Eb ? w : sel_b;
-    // the positive element leaves the hand-off (skip bit); its code travels through pos_code instead
-    code[j] = w | ((lane == La && j == Ea) ? 0x00008000u : 0u) | ((lane == Lb && j == Eb) ? 0x80000000u : 0u);
+    code[j] = (packed & keep) | setm;
   }
-  const uint32_t pos_a = pa ? (__builtin_amdgcn_readlane(sel_a, La) & 0xFFFFu) : 0x8000u;
-  const uint32_t pos_b = pb ? (__builtin_amdgcn_readlane(sel_b, Lb) >> 16) : 0x8000u;
-  if (lane == 0) {
-    if (r0 < n) a.pos_code[r0] = static_cast<uint16_t>(pos_a);
-    if (r0 + 1 < n) a.pos_code[r0 + 1] = static_cast<uint16_t>(pos_b);
-  }
+  pos_t[0] = (ka && ta >= 0 && ta < C) ? static_cast<int>(ta) : -1;
+  pos_t[1] = (kb && tb >= 0 && tb < C) ? static_cast<int>(tb) : -1;
   if (lane == 0) {
     const int64_t tt[2] = {ta, tb};
     const int am[2] = {ama, amb};
@@ -183,7 +190,7 @@ __device__ __forceinline__ void p_pair_codes(const uint4 (&raw)[2][2], int64_t t
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int64_t t = tt[i];
-      if constexpr (!ROUND2) {
+      if (!ROUND2) {
         if (a.confmat != nullptr && keepv[i] && t >= 0 && t < C && am[i] < C) atomic_add_i64(a.confmat + t * C + am[i], 1);
         if (a.err != nullptr && validv[i] && (t < 0 || t >= C)) atomicOr(a.err, 1);
       }
@@ -196,20 +203,12 @@ __device__ __forceinline__ void p_pair_codes(const uint4 (&raw)[2][2], int64_t t
   }
 }
 
-// The corrected round (mis-speculation only).  Inlined like everything else here: an out-of-line call taking the
-// register arrays by reference puts them (and the kernel arguments) in scratch memory for the whole kernel.
-template <typename T, int NG>
-__device__ __forceinline__ void p_pair_codes_round2(bool softmax, const uint4 (&raw)[2][2], int64_t tv, int tlane, int64_t r0,
-                                                 const PersistArgs& a, int nvec, uint32_t (&code)[8 * NG]) {
-  bool unused = true;
-  if (softmax) p_pair_codes<T, NG, true, true>(raw, tv, tlane, r0, a, nvec, code, unused);
-  else p_pair_codes<T, NG, false, true>(raw, tv, tlane, r0, a, nvec, code, unused);
-}
-
 // LDS transposition of one tile (all 16 waves hold one pair each) and write-through stores of its class segments.
+// The positive element of each row leaves the hand-off here: lane 0 of each wave reads its rows' target-class words
+// from the image, keeps the row's code in pos_code and sets the element's skip bit before the stores.
 template <int NG>
-__device__ __forceinline__ void p_store_tile(const uint32_t (&code)[2][8 * NG], uint32_t* __restrict__ s_img, const PersistArgs& a,
-                                             __amdgpu_buffer_rsrc_t codes_rs, int64_t tile) {
+__device__ __forceinline__ void p_store_tile(const uint32_t (&code)[2][8 * NG], const int (&pos_t)[2][2], uint32_t* __restrict__ s_img,
+                                             const PersistArgs& a, __amdgpu_buffer_rsrc_t codes_rs, int64_t tile) {
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = threadIdx.x / kWave;
 #pragma unroll
@@ -219,6 +218,21 @@ __device__ __forceinline__ void p_store_tile(const uint32_t (&code)[2][8 * NG], 
       const int p = wave + pp * kPWaves;  // pair slot
 #pragma unroll
       for (int j = 0; j < 8; ++j) s_img[(8 * lane + j) * kSlots + (p ^ (lane & (kSlots - 1)))] = code[pp][8 * g + j];
+    }
+    lds_barrier();
+    if (lane < 4) {  // lanes 0..3: (pair pp, row h) of this wave
+      const int pp = lane >> 1, h = lane & 1;
+      const int t = lane == 0 ? pos_t[0][0] : lane == 1 ? pos_t[0][1] : lane == 2 ? pos_t[1][0] : pos_t[1][1];  // no dynamic index
+      const int64_t r = tile * kTileRows + 2 * (wave + pp * kPWaves) + h;
+      if (t >= 0 && (t >> 9) == g) {
+        const int cl = t & 511;
+        const int idx = cl * kSlots + ((wave + pp * kPWaves) ^ ((cl >> 3) & (kSlots - 1)));
+        const uint32_t wd = s_img[idx];
+        a.pos_code[r] = static_cast<uint16_t>(h ? (wd >> 16) : (wd & 0xFFFFu));
+        atomicOr(&s_img[idx], h ? 0x80000000u : 0x00008000u);  // both rows of a pair may share the word
+      } else if (t < 0 && g == 0 && r < a.n) {
+        a.pos_code[r] = 0x8000u;
+      }
     }
     lds_barrier();
     constexpr int kQuads = kSlots / 4;
@@ -234,7 +248,7 @@ __device__ __forceinline__ void p_store_tile(const uint32_t (&code)[2][8 * NG], 
       const p_v4u o = x & 2 ? p_v4u{e2, e3, e0, e1} : p_v4u{e0, e1, e2, e3};
       if (c < a.C) {
         const uint32_t off = static_cast<uint32_t>((int64_t)c * a.n_pad * 2 + tile * (kTileRows * 2) + q * 16);
-        __builtin_amdgcn_raw_buffer_store_b128(o, codes_rs, off, 0, kSc1);
+        __builtin_amdgcn_raw_buffer_store_b128(o, codes_rs, off, 0, TMX_PERSIST_STORE_POLICY);
       }
     }
     lds_barrier();
@@ -270,31 +284,34 @@ struct PConsumer {
   int* s_misc;     // [0] wrap slots used, [1] overflow-to-atomic flag
 };
 
-__device__ __forceinline__ void p_note_wrap(const PConsumer& pc, int cls, int bin, int64_t* neg_hist_of_cls) {
+// Rare path (a 16-bit count wrapped): out of line, scalar arguments only, so it costs one call site per use instead
+// of an unrolled 32-slot probe inlined at every LDS atomic.
+__device__ __noinline__ void p_note_wrap(uint32_t* s_wk, uint32_t* s_wc, int* s_misc, int cls, int bin, int64_t* neg_hist_of_cls) {
   const uint32_t key = (static_cast<uint32_t>(cls) << 16) | static_cast<uint32_t>(bin);
-  for (int i = 0; i < kPWrapSlots; ++i) {  // rare: linear probe of a tiny table
-    const uint32_t prev = atomicCAS(&pc.s_wk[i], 0xFFFFFFFFu, key);
+#pragma unroll 1
+  for (int i = 0; i < kPWrapSlots; ++i) {  // linear probe of a tiny table
+    const uint32_t prev = atomicCAS(&s_wk[i], 0xFFFFFFFFu, key);
     if (prev == 0xFFFFFFFFu || prev == key) {
-      atomicAdd(&pc.s_wc[i], 1u);
+      atomicAdd(&s_wc[i], 1u);
+      atomicMax(&s_misc[0], i + 1);
       return;
     }
   }
   atomic_add_i64(neg_hist_of_cls + bin, 65536);  // table full: straight to the bins; flush then adds atomically
-  atomicOr(&pc.s_misc[1], 1);
+  atomicOr(&s_misc[1], 1);
 }
 
 // Consume rows [rb, re) (multiple of 8) of this workgroup's classes from the hand-off buffer.
-template <bool RTN>
 __device__ __forceinline__ void p_consume(const PersistArgs& a, const PConsumer& pc, __amdgpu_buffer_rsrc_t codes_rs, int c0, int kc,
-                                          int64_t rb, int64_t re) {
+                                          int64_t rb, int64_t re, const bool RTN) {
   const int64_t nv = (re - rb) / 8;  // uint4 per class
   const int64_t total = nv * kc;
-  for (int64_t base = 0; base < total; base += 4 * kPThreads) {
+  for (int64_t base = 0; base < total; base += 4 * kCThreads) {
     p_v4u w[4];
     int cls[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const int64_t i = base + threadIdx.x + u * kPThreads;
+      const int64_t i = base + threadIdx.x + u * kCThreads;
       cls[u] = -1;
       w[u] = p_v4u{0x80008000u, 0x80008000u, 0x80008000u, 0x80008000u};
       if (i < total) {
@@ -315,12 +332,12 @@ __device__ __forceinline__ void p_consume(const PersistArgs& a, const PConsumer&
         if (x & 0x8000u) continue;  // skipped, or the row's positive (pos_code)
         const uint32_t code = x & 0x3FFFu;
         const uint32_t inc = (code & 1u) ? 0x10000u : 1u;
-        if constexpr (RTN) {
+        if (RTN) {
           const uint32_t old = atomicAdd(&h[code >> 1], inc);
           const uint32_t half = (code & 1u) ? (old >> 16) : (old & 0xFFFFu);
           if (half == 0xFFFFu) {  // this add wrapped the 16-bit count: undo the carry into the neighbour, note +65536
             if (!(code & 1u)) atomicAdd(&h[code >> 1], 0xFFFF0000u);
-            p_note_wrap(pc, cls[u], static_cast<int>(code), a.hist + ((int64_t)(c0 + cls[u]) * 2) * kCodes);
+            p_note_wrap(pc.s_wk, pc.s_wc, pc.s_misc, cls[u], static_cast<int>(code), a.hist + ((int64_t)(c0 + cls[u]) * 2) * kCodes);
           }
         } else {
           atomicAdd(&h[code >> 1], inc);
@@ -328,11 +345,6 @@ __device__ __forceinline__ void p_consume(const PersistArgs& a, const PConsumer&
       }
     }
   }
-}
-
-__device__ __forceinline__ void p_consume_rtn(const PersistArgs& a, const PConsumer& pc, __amdgpu_buffer_rsrc_t codes_rs, int c0, int kc,
-                                           int64_t rb, int64_t re) {
-  p_consume<true>(a, pc, codes_rs, c0, kc, rb, re);
 }
 
 // Add the LDS counts of this workgroup's classes to the int64 histogram (exclusive owner) and widen the code range.
@@ -344,11 +356,11 @@ __device__ __forceinline__ void p_flush(const PersistArgs& a, const PConsumer& p
     uint32_t* h = pc.s_h + cl * kPHistWords;
     int64_t* neg = a.hist + ((int64_t)(c0 + cl) * 2) * kCodes;
     int lo = kCodes, hi = -1;
-    for (int base = threadIdx.x; base < kPHistWords; base += kB * kPThreads) {
+    for (int base = threadIdx.x; base < kPHistWords; base += kB * kCThreads) {
       int64_t cnt[2 * kB], old[2 * kB];
 #pragma unroll
       for (int u = 0; u < kB; ++u) {
-        const int i = base + u * kPThreads;
+        const int i = base + u * kCThreads;
         const uint32_t w = i < kPHistWords ? h[i] : 0u;
         cnt[2 * u] = static_cast<int64_t>(w & 0xFFFFu);
         cnt[2 * u + 1] = static_cast<int64_t>(w >> 16);
@@ -360,12 +372,12 @@ __device__ __forceinline__ void p_flush(const PersistArgs& a, const PConsumer& p
       }
       if (!atomic_mode) {
 #pragma unroll
-        for (int q = 0; q < 2 * kB; ++q) old[q] = cnt[q] ? neg[2 * (base + (q >> 1) * kPThreads) + (q & 1)] : 0;
+        for (int q = 0; q < 2 * kB; ++q) old[q] = cnt[q] ? neg[2 * (base + (q >> 1) * kCThreads) + (q & 1)] : 0;
       }
 #pragma unroll
       for (int q = 0; q < 2 * kB; ++q) {
         if (cnt[q] == 0) continue;
-        const int bin = 2 * (base + (q >> 1) * kPThreads) + (q & 1);
+        const int bin = 2 * (base + (q >> 1) * kCThreads) + (q & 1);
         lo = min(lo, bin);
         hi = max(hi, bin);
         if (atomic_mode) atomic_add_i64(neg + bin, cnt[q]);
@@ -373,7 +385,7 @@ __device__ __forceinline__ void p_flush(const PersistArgs& a, const PConsumer& p
       }
 #pragma unroll
       for (int u = 0; u < kB; ++u)
-        if (base + u * kPThreads < kPHistWords) h[base + u * kPThreads] = 0u;
+        if (base + u * kCThreads < kPHistWords) h[base + u * kCThreads] = 0u;
     }
     lo = wave_min_i32(lo);
     hi = wave_max_i32(hi);
@@ -384,173 +396,194 @@ __device__ __forceinline__ void p_flush(const PersistArgs& a, const PConsumer& p
   }
 }
 
+// Tile bookkeeping shared by both roles (tiles of chunk s: s * tpw * G + j * G + w, j < tpw).
+struct PTiles {
+  int64_t ntiles, chunk_tiles;
+  int G, tpw, w;
+  __device__ __forceinline__ int64_t tile(int s, int j) const {
+    const int64_t t = (int64_t)s * chunk_tiles + (int64_t)j * G + w;
+    return t < min<int64_t>((int64_t)(s + 1) * chunk_tiles, ntiles) ? t : ntiles;
+  }
+  __device__ __forceinline__ int in_chunk(int s) const {
+    return static_cast<int>(min<int64_t>((int64_t)(s + 1) * chunk_tiles, ntiles) - (int64_t)s * chunk_tiles);
+  }
+};
+
+// The last of the 2 G workgroups (producers and consumers) resets the hand-off counters, the rare-row counts and
+// rolls the speculation; every workgroup read all of them before taking its ticket.
+__device__ __forceinline__ void p_ticket(const PersistArgs& a, int verdict) {
+  if (__hip_atomic_fetch_add(a.ctrl + kPCtrlTicket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 2 * a.G - 1) {
+    for (int i = 0; i < 2 * kPMaxChunks; ++i) a.ctrl[i] = 0;
+    a.ctrl[kPCtrlTicket] = 0;
+    a.ctrl[kPCtrlProdDone] = 0;
+    a.state[0] = a.state[1] = 0;
+    a.mode[0] = verdict;
+    a.mode[1] = 0;
+  }
+}
+
+// Producer role: one 512-thread workgroup per CU turns its tiles of each chunk into class-major codes (write-through
+// stores) and signals the chunk.  Round 1 (mis-speculated batches only) recomputes the codes with the real mode once
+// every producer has finished round 0 (the verdict is then final).  Finally it adds its rows' positive codes.
 template <typename T, int NG>
-__global__ void __launch_bounds__(kPThreads, 2) mc_persist_kernel(PersistArgs a) {
+__global__ void __launch_bounds__(kPThreads, 2) mc_persist_producer(PersistArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t p_lds[];
-  PConsumer pc;
-  pc.s_h = p_lds;
-  uint32_t* s_img = p_lds + kPMaxClasses * kPHistWords;
-  pc.s_wk = s_img + kPImageWords;
-  pc.s_wc = pc.s_wk + kPWrapSlots;
-  pc.s_misc = reinterpret_cast<int*>(pc.s_wc + kPWrapSlots);  // [0] wrap slots used, [1] atomic flush, [2] verdict, [3] bad
-  int* s_range = pc.s_misc + 4;                                // [kPMaxClasses][2]
+  uint32_t* s_img = p_lds;
+  int* s_p = reinterpret_cast<int*>(p_lds + kPImageWords);  // [0] saw a probability-mode witness, [1] verdict
   const int w = blockIdx.x;
   const int C = a.C;
   const int nvec = C / 8;
-  const int c0 = min(w * a.k, C), kc = min(a.k, C - c0);
-  const int64_t ntiles = a.n_pad / kTileRows;
-  const int64_t chunk_tiles = (int64_t)a.tpw * a.G;
+  const PTiles tl{a.n_pad / kTileRows, (int64_t)a.tpw * a.G, a.G, a.tpw, w};
   const __amdgpu_buffer_rsrc_t codes_rs = p_rsrc(a.codes, static_cast<uint32_t>((int64_t)C * a.n_pad * 2));
   int* timeout = a.ctrl + kPCtrlTimeout;
-
-  {  // zero the LDS histograms and tables
-    uint4* s4 = reinterpret_cast<uint4*>(pc.s_h);
-    for (int i = threadIdx.x; i < kPMaxClasses * kPHistWords / 4; i += kPThreads) s4[i] = make_uint4(0, 0, 0, 0);
-    if (threadIdx.x < kPWrapSlots) { pc.s_wk[threadIdx.x] = 0xFFFFFFFFu; pc.s_wc[threadIdx.x] = 0u; }
-    if (threadIdx.x < 4) pc.s_misc[threadIdx.x] = 0;
-    if (threadIdx.x < 2 * kPMaxClasses) s_range[threadIdx.x] = (threadIdx.x & 1) ? -1 : kCodes;
-  }
-  const int used_mode = a.mode[0];  // previous batch's verdict (kernel-boundary ordered: plain load)
-  __syncthreads();
-
-  auto tile_of = [&](int s, int j) -> int64_t {  // j-th tile of this workgroup in chunk s (ntiles if none)
-    const int64_t t = (int64_t)s * chunk_tiles + (int64_t)j * a.G + w;
-    return t < min<int64_t>((int64_t)(s + 1) * chunk_tiles, ntiles) ? t : ntiles;
-  };
-  auto chunk_rows = [&](int s, int64_t& rb, int64_t& re) {
-    rb = (int64_t)s * chunk_tiles * kTileRows;
-    re = min<int64_t>((int64_t)(s + 1) * chunk_tiles, ntiles) * kTileRows;
-  };
-  auto tiles_in = [&](int s) -> int {
-    return static_cast<int>(min<int64_t>((int64_t)(s + 1) * chunk_tiles, ntiles) - (int64_t)s * chunk_tiles);
-  };
-
+  if (threadIdx.x < 2) s_p[threadIdx.x] = 0;
+  const int used_mode = a.mode[0];  // previous batch's verdict (kernel-boundary ordered)
+  lds_barrier();
+  int verdict = used_mode;
   for (int round = 0; round < 2; ++round) {
-    int mode_now = used_mode;
-    if (round == 1) {
-      // every workgroup reached the same verdict (all producers signalled after writing it)
-      mode_now = pc.s_misc[2];
-      if (mode_now == used_mode) break;
-    }
+    if (round == 1 && verdict == used_mode) break;
+    const int mode_now = round == 0 ? used_mode : verdict;
     int* ready = a.ctrl + round * kPMaxChunks;
-    int64_t since_flush = 0;
     bool saw_bad = false;
     uint4 raw[2][2][2];
     int64_t tv = 0;
-    {
-      const int64_t t0 = tile_of(0, 0);
-      if (t0 < ntiles) p_load_tile<T, NG>(a, t0, nvec, raw, tv);
-    }
-    for (int s = 0; s <= a.nchunks; ++s) {
+    if (tl.tile(0, 0) < tl.ntiles) p_load_tile<T, NG>(a, tl.tile(0, 0), nvec, raw, tv);
+    for (int s = 0; s < a.nchunks; ++s) {
       long long* pf = (a.prof != nullptr && round == 0 && threadIdx.x == 0) ? a.prof + (int64_t)w * (4 * kPMaxChunks + 4) : nullptr;
-      if (pf && s < a.nchunks) pf[4 * s] = wall_clock64();
-      if (s < a.nchunks) {
-        // ---- producer: this workgroup's tiles of chunk s
-        int produced = 0;
-        for (int j = 0; j < a.tpw; ++j) {
-          const int64_t tile = tile_of(s, j);
-          if (tile >= ntiles) break;
-          uint32_t code[2][8 * NG];
+      if (pf) pf[4 * s] = wall_clock64();
+      int produced = 0;
+      for (int j = 0; j < a.tpw; ++j) {
+        const int64_t tile = tl.tile(s, j);
+        if (tile >= tl.ntiles) break;
+        uint32_t code[2][8 * NG];
+        int pos_t[2][2];
 #pragma unroll
-          for (int pp = 0; pp < 2; ++pp) {
-            const int64_t r0 = tile * kTileRows + 2 * (threadIdx.x / kWave + pp * kPWaves);
-            if (round == 0) {
-              if (mode_now != 0) p_pair_codes<T, NG, true, false>(raw[pp], tv, 2 * pp, r0, a, nvec, code[pp], saw_bad);
-              else p_pair_codes<T, NG, false, false>(raw[pp], tv, 2 * pp, r0, a, nvec, code[pp], saw_bad);
-            } else {
-              p_pair_codes_round2<T, NG>(mode_now != 0, raw[pp], tv, 2 * pp, r0, a, nvec, code[pp]);
-            }
-          }
-          // the next tile of this chunk (if any) is loaded now; the next chunk's first after the hand-off below
-          if (j + 1 < a.tpw && tile_of(s, j + 1) < ntiles) p_load_tile<T, NG>(a, tile_of(s, j + 1), nvec, raw, tv);
-          p_store_tile<NG>(code, s_img, a, codes_rs, tile);
-          ++produced;
+        for (int pp = 0; pp < 2; ++pp) {
+          const int64_t r0 = tile * kTileRows + 2 * (threadIdx.x / kWave + pp * kPWaves);
+          p_pair_codes<T, NG>(raw[pp], tv, 2 * pp, r0, a, nvec, code[pp], pos_t[pp], saw_bad, mode_now != 0, round != 0);
         }
-        if (round == 0 && saw_bad) pc.s_misc[3] = 1;  // benign race: any witness
-        // hand-off: every wave's stores (and slow-row words) complete, then one agent-scope add
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (threadIdx.x == 0 && produced > 0) {
-          if (round == 0 && pc.s_misc[3] && __hip_atomic_load(a.mode + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
-            __hip_atomic_store(a.mode + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // the verdict precedes the signal
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          }
-          __hip_atomic_fetch_add(ready + s, produced, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        if (pf) pf[4 * s + 1] = wall_clock64();
-        // prefetch this workgroup's first tile of the next chunk: in flight while chunk s - 1 is consumed
-        if (s + 1 < a.nchunks && tile_of(s + 1, 0) < ntiles) p_load_tile<T, NG>(a, tile_of(s + 1, 0), nvec, raw, tv);
+        // prefetch this chunk's next tile now; the next chunk's first is loaded after the hand-off below (whose
+        // vmcnt(0) would otherwise wait for it)
+        if (j + 1 < a.tpw && tl.tile(s, j + 1) < tl.ntiles) p_load_tile<T, NG>(a, tl.tile(s, j + 1), nvec, raw, tv);
+        p_store_tile<NG>(code, pos_t, s_img, a, codes_rs, tile);
+        ++produced;
       }
-      if (s >= 1 && kc > 0) {
-        // ---- consumer: chunk s - 1 of this workgroup's classes
-        const int cs = s - 1;
-        int64_t rb, re;
-        chunk_rows(cs, rb, re);
-        if (threadIdx.x == 0) p_spin_until(ready + cs, tiles_in(cs), timeout);
-        if (pf) pf[4 * cs + 2] = wall_clock64();
-        lds_barrier();  // the poll's outcome; the payload loads below are sc1 (no acquire needed, table row 1)
-        const int64_t rows = re - rb;
-        if (since_flush + rows > 65535) p_consume_rtn(a, pc, codes_rs, c0, kc, rb, re);
-        else p_consume<false>(a, pc, codes_rs, c0, kc, rb, re);
-        since_flush += rows;
-        if (pf) { __syncthreads(); pf[4 * cs + 3] = wall_clock64(); }
-      } else if (s >= 1 && threadIdx.x == 0) {
-        // no classes: still wait, so the verdict read below follows every producer
-        p_spin_until(ready + (s - 1), tiles_in(s - 1), timeout);
-      }
-    }
-    __syncthreads();
-    if (round == 0 && threadIdx.x == 0) pc.s_misc[2] = __hip_atomic_load(a.mode + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-    if (round == 0 && pc.s_misc[2] != used_mode) {
-      // mis-speculated: consumers only touched LDS in this round (positives wait in pos_code), so dropping the LDS
-      // counts undoes the round; the wrap table's "full" fallback is the one global side effect (never reached below
-      // ~2M identical codes per class and round): flag it instead of returning wrong counts silently
-      if (threadIdx.x == 0 && pc.s_misc[1]) __hip_atomic_store(timeout, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      uint4* s4 = reinterpret_cast<uint4*>(pc.s_h);
-      for (int i = threadIdx.x; i < kPMaxClasses * kPHistWords / 4; i += kPThreads) s4[i] = make_uint4(0, 0, 0, 0);
-      if (threadIdx.x < kPWrapSlots) { pc.s_wk[threadIdx.x] = 0xFFFFFFFFu; pc.s_wc[threadIdx.x] = 0u; }
-      if (threadIdx.x < 2) pc.s_misc[threadIdx.x] = 0;
+      if (round == 0 && saw_bad) s_p[0] = 1;  // benign race: any witness
+      // hand-off (MI355X_MICROARCH.md table row 1): every wave's sc1 stores and slow-row words complete, one
+      // workgroup barrier, then one agent-scope add by one lane (the verdict word first when this chunk saw a witness)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
-    }
-  }
-
-  // ---------------------------------------------------------------------------------------------- end phase
-  if (a.prof != nullptr && threadIdx.x == 0) a.prof[(int64_t)w * (4 * kPMaxChunks + 4) + 4 * kPMaxChunks] = wall_clock64();
-  const int verdict = pc.s_misc[2];
-  const bool fixed = verdict != used_mode;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's pos_code stores, before other waves read them
-  __syncthreads();
-  // (1) positives of this workgroup's rows (its tiles of every chunk), final mode known
-  {
-    const T* preds = static_cast<const T*>(a.preds);
-    (void)preds;
-    const int tiles_mine = a.nchunks * a.tpw;
-    for (int base = 0; base < tiles_mine * kTileRows; base += kPThreads) {
-      const int idx = base + threadIdx.x;
-      if (idx >= tiles_mine * kTileRows) break;
-      const int slot = idx / kTileRows;
-      const int64_t tile = tile_of(slot / a.tpw, slot % a.tpw);
-      if (tile >= ntiles) continue;
-      const int64_t r = tile * kTileRows + idx % kTileRows;
-      if (r >= a.n) continue;
-      const uint32_t x = a.pos_code[r];
-      if (x & 0x8000u) continue;
-      const int64_t t = a.target[r];
-      atomic_add_i64(a.hist + (t * 2 + 1) * kCodes + (x & 0x3FFFu), 1);
-      if (a.code_range != nullptr) {
-        atomicMin(a.code_range + 2 * t, static_cast<int>(x & 0x3FFFu));
-        atomicMax(a.code_range + 2 * t + 1, static_cast<int>(x & 0x3FFFu));
+      if (threadIdx.x == 0 && produced > 0) {
+        if (round == 0 && s_p[0] && __hip_atomic_load(a.mode + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+          __hip_atomic_store(a.mode + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __hip_atomic_fetch_add(ready + s, produced, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
+      if (pf) pf[4 * s + 1] = wall_clock64();
+      if (s + 1 < a.nchunks && tl.tile(s + 1, 0) < tl.ntiles) p_load_tile<T, NG>(a, tl.tile(s + 1, 0), nvec, raw, tv);
+    }
+    if (round == 0) {
+      // the verdict is final once every producer finished round 0 (each wrote it before its last signal)
+      if (threadIdx.x == 0) {
+        __hip_atomic_fetch_add(a.ctrl + kPCtrlProdDone, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        p_spin_until(a.ctrl + kPCtrlProdDone, a.G, timeout);
+        s_p[1] = __hip_atomic_load(a.mode + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      lds_barrier();
+      verdict = s_p[1];
     }
   }
-  // (2) rare rows (NaN / inf rows, listed by the producers) of this workgroup's classes; list 0 = the speculated
-  //     round, list 1 = the corrected round (fixed): the class pass's rules (curve_hist_kernels.h class_hist_block)
+  // positives of this workgroup's rows, with the final codes (pos_code was written by this workgroup's own lanes)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const int tiles_mine = a.nchunks * a.tpw;
+  for (int base = 0; base < tiles_mine * kTileRows; base += kPThreads) {
+    const int idx = base + threadIdx.x;
+    if (idx >= tiles_mine * kTileRows) break;
+    const int slot = idx / kTileRows;
+    const int64_t tile = tl.tile(slot / a.tpw, slot % a.tpw);
+    if (tile >= tl.ntiles) continue;
+    const int64_t r = tile * kTileRows + idx % kTileRows;
+    if (r >= a.n) continue;
+    const uint32_t x = a.pos_code[r];
+    if (x & 0x8000u) continue;
+    const int64_t t = a.target[r];
+    atomic_add_i64(a.hist + (t * 2 + 1) * kCodes + (x & 0x3FFFu), 1);
+    if (a.code_range != nullptr) {
+      atomicMin(a.code_range + 2 * t, static_cast<int>(x & 0x3FFFu));
+      atomicMax(a.code_range + 2 * t + 1, static_cast<int>(x & 0x3FFFu));
+    }
+  }
+  if (threadIdx.x == 0) p_ticket(a, verdict);
+}
+
+// Consumer role: one workgroup per CU owns k = ceil(C / G) <= 4 classes: LDS histograms of their negative codes for
+// the whole batch, chunk by chunk as producers signal them; then the rare rows of its classes, its share of the
+// rare rows' confusion-matrix entries, the flush into the int64 histogram and the occupied code range.
+template <typename T>
+__global__ void __launch_bounds__(kCThreads, 1) mc_persist_consumer(PersistArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t p_lds[];
+  PConsumer pc;
+  pc.s_h = p_lds;
+  pc.s_wk = p_lds + kPMaxClasses * kPHistWords;
+  pc.s_wc = pc.s_wk + kPWrapSlots;
+  pc.s_misc = reinterpret_cast<int*>(pc.s_wc + kPWrapSlots);  // [0] wrap slots used, [1] atomic flush, [2] verdict
+  int* s_range = pc.s_misc + 4;                                // [kPMaxClasses][2]
+  const int w = blockIdx.x;
+  const int C = a.C;
+  const int c0 = min(w * a.k, C), kc = min(a.k, C - c0);
+  const PTiles tl{a.n_pad / kTileRows, (int64_t)a.tpw * a.G, a.G, a.tpw, w};
+  const __amdgpu_buffer_rsrc_t codes_rs = p_rsrc(a.codes, static_cast<uint32_t>((int64_t)C * a.n_pad * 2));
+  int* timeout = a.ctrl + kPCtrlTimeout;
+  auto clear = [&]() {
+    uint4* s4 = reinterpret_cast<uint4*>(pc.s_h);
+    for (int i = threadIdx.x; i < kPMaxClasses * kPHistWords / 4; i += kCThreads) s4[i] = make_uint4(0, 0, 0, 0);
+    if (threadIdx.x < kPWrapSlots) { pc.s_wk[threadIdx.x] = 0xFFFFFFFFu; pc.s_wc[threadIdx.x] = 0u; }
+    if (threadIdx.x < 2) pc.s_misc[threadIdx.x] = 0;
+  };
+  clear();
+  if (threadIdx.x < 2 * kPMaxClasses) s_range[threadIdx.x] = (threadIdx.x & 1) ? -1 : kCodes;
+  const int used_mode = a.mode[0];
+  lds_barrier();
+  int verdict = used_mode;
+  for (int round = 0; round < 2; ++round) {
+    if (round == 1) {
+      if (verdict == used_mode) break;
+      clear();  // mis-speculated: round 0 only touched LDS (positives wait in pos_code)
+      lds_barrier();
+    }
+    int* ready = a.ctrl + round * kPMaxChunks;
+    int64_t since_flush = 0;
+    for (int s = 0; s < a.nchunks; ++s) {
+      const int64_t rb = (int64_t)s * tl.chunk_tiles * kTileRows;
+      const int64_t re = min<int64_t>((int64_t)(s + 1) * tl.chunk_tiles, tl.ntiles) * kTileRows;
+      if (threadIdx.x == 0) p_spin_until(ready + s, tl.in_chunk(s), timeout);
+      long long* pf = (a.prof != nullptr && round == 0 && threadIdx.x == 0) ? a.prof + (int64_t)w * (4 * kPMaxChunks + 4) : nullptr;
+      if (pf) pf[4 * s + 2] = wall_clock64();
+      lds_barrier();  // the poll's outcome; the payload loads are sc1 (table row 1: no acquire needed)
+      if (kc > 0) p_consume(a, pc, codes_rs, c0, kc, rb, re, since_flush + (re - rb) > 65535);
+      since_flush += re - rb;
+      if (pf) pf[4 * s + 3] = wall_clock64();
+    }
+    if (round == 0) {
+      if (threadIdx.x == 0) {
+        pc.s_misc[2] = __hip_atomic_load(a.mode + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (pc.s_misc[2] != used_mode && pc.s_misc[1]) __hip_atomic_store(timeout, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      lds_barrier();
+      verdict = pc.s_misc[2];
+    }
+  }
+  if (a.prof != nullptr && threadIdx.x == 0) a.prof[(int64_t)w * (4 * kPMaxChunks + 4) + 4 * kPMaxChunks] = wall_clock64();
+  const bool fixed = verdict != used_mode;
+  // rare rows (NaN / inf rows listed by producers) of this workgroup's classes: list 0 = speculated round, list 1 =
+  // corrected round (fixed) — the class pass's rules (curve_hist_kernels.h class_hist_block)
   const int n0 = __hip_atomic_load(a.state + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int n1 = fixed ? __hip_atomic_load(a.state + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+  const T* preds = static_cast<const T*>(a.preds);
   if (kc > 0 && n0 + n1 > 0) {
-    const T* preds = static_cast<const T*>(a.preds);
-    for (int64_t i = threadIdx.x; i < (int64_t)(n0 + n1) * kc; i += kPThreads) {
+    for (int64_t i = threadIdx.x; i < (int64_t)(n0 + n1) * kc; i += kCThreads) {
       const int64_t li = i / kc;
       const int cl = static_cast<int>(i % kc);
       const int lst = li < n0 ? 0 : 1;
@@ -569,15 +602,14 @@ __global__ void __launch_bounds__(kPThreads, 2) mc_persist_kernel(PersistArgs a)
         const uint32_t half = (code & 1u) ? (old >> 16) : (old & 0xFFFFu);
         if (half == 0xFFFFu) {
           if (!(code & 1u)) atomicAdd(&pc.s_h[cl * kPHistWords + (code >> 1)], 0xFFFF0000u);
-          p_note_wrap(pc, cl, static_cast<int>(code), a.hist + ((int64_t)c * 2) * kCodes);
+          p_note_wrap(pc.s_wk, pc.s_wc, pc.s_misc, cl, static_cast<int>(code), a.hist + ((int64_t)c * 2) * kCodes);
         }
       }
     }
   }
-  // (3) confusion matrix of the listed rows of the speculated round (their arg-max: NaN first, else first maximum)
+  // confusion matrix of the listed rows of the speculated round (their arg-max: NaN first, else first maximum)
   if (a.confmat != nullptr && threadIdx.x < kWave) {
     const int lane = threadIdx.x;
-    const T* preds = static_cast<const T*>(a.preds);
     for (int64_t i = w; i < n0; i += a.G) {
       const int64_t r = __hip_atomic_load(a.slow_rows + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const int64_t t = a.target[r];
@@ -597,28 +629,17 @@ __global__ void __launch_bounds__(kPThreads, 2) mc_persist_kernel(PersistArgs a)
       if (lane == 0 && am < C) atomic_add_i64(a.confmat + t * C + am, 1);
     }
   }
-  __syncthreads();
-  // (4) LDS counts -> int64 bins, occupied code range
+  lds_barrier();
   if (kc > 0) {
     p_flush(a, pc, c0, kc, s_range);
-    __syncthreads();
+    lds_barrier();
     if (a.code_range != nullptr && threadIdx.x < kc && s_range[2 * threadIdx.x + 1] >= 0) {
       atomicMin(a.code_range + 2 * (c0 + threadIdx.x), s_range[2 * threadIdx.x]);
       atomicMax(a.code_range + 2 * (c0 + threadIdx.x) + 1, s_range[2 * threadIdx.x + 1]);
     }
   }
   if (a.prof != nullptr && threadIdx.x == 0) a.prof[(int64_t)w * (4 * kPMaxChunks + 4) + 4 * kPMaxChunks + 1] = wall_clock64();
-  // (5) the last workgroup resets the hand-off counters, the rare-row counts and rolls the speculation (every
-  //     workgroup read all of them before taking its ticket)
-  if (threadIdx.x == 0) {
-    if (__hip_atomic_fetch_add(a.ctrl + kPCtrlTicket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.G - 1) {
-      for (int i = 0; i < 2 * kPMaxChunks; ++i) a.ctrl[i] = 0;
-      a.ctrl[kPCtrlTicket] = 0;
-      a.state[0] = a.state[1] = 0;
-      a.mode[0] = verdict;
-      a.mode[1] = 0;
-    }
-  }
+  if (threadIdx.x == 0) p_ticket(a, verdict);
 }
 
 // Host side: the launch geometry (grid = one workgroup per CU; None when the route does not apply).

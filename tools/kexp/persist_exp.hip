@@ -4,7 +4,7 @@
 // the rolled mode words must be IDENTICAL on every case (logits, NaN / inf / tied rows, ignore_index, probabilities
 // with and without NaN, both mis-speculations); then both are timed on a pool of 4 distinct batches (cold inputs, as
 // bench.py cycles them).
-// Build: hipcc -O3 --offload-arch=gfx950 -I csrc tools/kexp/persist_exp.hip -o build/persist_exp
+// Build: hipcc -O3 --offload-arch=gfx950 -I csrc -I tools/kexp tools/kexp/persist_exp.hip -o build/persist_exp
 // Run:   build/persist_exp [N] [C]
 #include <cmath>
 #include <cstdio>
@@ -31,11 +31,17 @@ int main(int argc, char** argv) {
   const int tpw_min = argc > 3 ? atoi(argv[3]) : 1;
   const PersistPlan pl = persist_plan(N, C, cus, tpw_min);
   if (!pl.ok) { printf("{\"error\": \"no persistent plan\"}\n"); return 1; }
-  auto kern = mc_persist_kernel<__hip_bfloat16, 2>;
-  CK(hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPLdsBytes));
+  auto kprod = mc_persist_producer<__hip_bfloat16, 2>;
+  auto kcons = mc_persist_consumer<__hip_bfloat16>;
+  CK(hipFuncSetAttribute(reinterpret_cast<const void*>(kcons), hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPConsumerLds));
   int nb = 0;
-  CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, kPThreads, kPLdsBytes));
-  if (nb < 1) { printf("{\"error\": \"persistent kernel does not fit a CU\"}\n"); return 1; }
+  CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kcons, kCThreads, kPConsumerLds));
+  if (nb < 1) { printf("{\"error\": \"consumer kernel does not fit a CU\"}\n"); return 1; }
+  hipStream_t side;
+  hipEvent_t evA, evB;
+  CK(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
+  CK(hipEventCreateWithFlags(&evA, hipEventDisableTiming));
+  CK(hipEventCreateWithFlags(&evB, hipEventDisableTiming));
 
   const int64_t n_pad = (N + kTileRows - 1) / kTileRows * kTileRows;
   std::vector<uint16_t> h(N * C), hp(N * C);
@@ -94,7 +100,13 @@ int main(int argc, char** argv) {
     a.preds = x; a.target = t; a.n = N; a.n_pad = n_pad; a.C = C; a.k = pl.k; a.G = pl.G; a.nchunks = pl.nchunks; a.tpw = pl.tpw;
     a.mode = msB; a.state = msB + 2; a.ctrl = msB + 8; a.ignore_index = -100; a.has_ignore = ign; a.codes = codesB; a.hist = histB;
     a.confmat = cmB; a.err = err; a.slow_rows = rowsB; a.code_range = crB; a.pos_code = pos; a.prof = prof;
-    hipLaunchKernelGGL(kern, pl.G, kPThreads, kPLdsBytes, 0, a);
+    // consumer on the main (null) stream, producer on a side stream: they share every CU
+    CK(hipEventRecord(evA, 0));
+    CK(hipStreamWaitEvent(side, evA, 0));
+    hipLaunchKernelGGL(kcons, pl.G, kCThreads, kPConsumerLds, 0, a);
+    hipLaunchKernelGGL(kprod, pl.G, kPThreads, kPProducerLds, side, a);
+    CK(hipEventRecord(evB, side));
+    CK(hipStreamWaitEvent(0, evB, 0));
   };
   auto set_mode = [&](int* m, int m0) { int hm[2] = {m0, 0}; CK(hipMemcpy(m, hm, 8, hipMemcpyHostToDevice)); };
   auto reset_range = [&](int* cr) {
@@ -103,8 +115,8 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(cr, v.data(), C * 8, hipMemcpyHostToDevice));
   };
 
-  printf("{\"N\": %lld, \"C\": %d, \"G\": %d, \"k\": %d, \"nchunks\": %d, \"tpw\": %d, \"lds\": %zu", (long long)N, C, pl.G, pl.k,
-         pl.nchunks, pl.tpw, kPLdsBytes);
+  printf("{\"N\": %lld, \"C\": %d, \"G\": %d, \"k\": %d, \"nchunks\": %d, \"tpw\": %d, \"lds\": [%zu, %zu]", (long long)N, C, pl.G,
+         pl.k, pl.nchunks, pl.tpw, kPConsumerLds, kPProducerLds);
   struct Case { const char* name; const __hip_bfloat16* x; const int64_t* t; bool ign; int spec_mode; };
   Case cases[] = {{"logits", d, dt, false, 1}, {"logits_nan_inf_ties", dn, dt, false, 1}, {"logits_ignore", dn, dti, true, 1},
                   {"probs", dp, dt, false, 0}, {"probs_nan", dpn, dt, false, 0}, {"logits_misspeculated", dn, dti, true, 0},
@@ -184,7 +196,20 @@ int main(int argc, char** argv) {
   }
   double e0 = 0, e1 = 0;
   for (int g = 0; g < pl.G; ++g) { e0 += (hpf[(size_t)g * PW + 4 * kPMaxChunks] - t0) / 100.0; e1 = std::max(e1, (hpf[(size_t)g * PW + 4 * kPMaxChunks + 1] - t0) / 100.0); }
-  printf("], \"end_start_avg\": %.1f, \"end_done_max\": %.1f", e0 / pl.G, e1);
+  printf("]");
+#if TMX_PERSIST_TILE_PROF
+  printf(", \"tiles_us\": [");
+  for (int j = 0; j < pl.tpw && j < kPMaxChunks; ++j) {
+    double w0 = 0, c1 = 0, s2 = 0;
+    for (int g = 0; g < pl.G; ++g) {
+      const long long* q = &hpf[(size_t)g * PW + 4 * j];
+      w0 += (q[0] - t0) / 100.0; c1 += (q[1] - q[0]) / 100.0; s2 += (q[2] - q[1]) / 100.0;
+    }
+    printf("%s{\"loads_done\": %.2f, \"codes\": %.2f, \"store_tile\": %.2f}", j ? ", " : "", w0 / pl.G, c1 / pl.G, s2 / pl.G);
+  }
+  printf("]");
+#endif
+  printf(", \"end_start_avg\": %.1f, \"end_done_max\": %.1f", e0 / pl.G, e1);
   int wB[8 + kPCtrlWords];
   CK(hipMemcpy(wB, msB, (8 + kPCtrlWords) * 4, hipMemcpyDeviceToHost));
   printf(", \"two_pass_us\": %.1f, \"persist_us\": %.1f, \"persist_same_batch_us\": %.1f, \"timeout_after_timing\": %d, \"all_ok\": %s}\n",
