@@ -22,6 +22,7 @@
 //  * tmx::binned_curve_update — bucketize (binary search over T thresholds in LDS) + per-(class, label,
 //                               bucket) histogram, then a suffix scan into the reference's [T, C, 2, 2]
 //                               multi-threshold confusion matrix (K5) — O(N*C*log T) instead of O(N*C*T).
+#include <cstdlib>
 #include <mutex>
 #include <unordered_map>
 
@@ -1183,6 +1184,190 @@ __global__ void __launch_bounds__(256) curve_hist_mc_kernel(const T* __restrict_
   }
 }
 
+// ---------------------------------------------------------------------------------------------------------
+// Small-class row pass (C <= 256): the tile row pass spreads ONE row over a wave (8 classes per lane), so at C = 10
+// two lanes of 64 work and a 1M-row update took 0.6 ms.  Here a row gets T = ceil(C / 16) lanes (T in 1..16, at most
+// 16 classes per lane) and a block 64 rows (64 T threads):
+//   1. the block's rows (64 C contiguous 16-bit scores) are staged into LDS with 16-B loads — no host-side padding
+//      copy for C % 8 != 0;
+//   2. each lane takes its classes of its row, row statistics by T-lane shuffles: the same rules as row_tile (fp32
+//      softmax with expf's instruction sequence and a correctly rounded quotient, RNE to the input dtype; arg-max +
+//      confusion matrix; rows with NaN / inf listed for the class pass; probability-mode witness);
+//   3. codes go through an LDS image [C][64] to the class-major scratch as 128-B class segments.
+// The FIXUP instance redoes the codes of a mis-speculated batch (mode[0] != mode[1]); the class pass is shared.
+// ---------------------------------------------------------------------------------------------------------
+constexpr int kSmallRows = 64;
+constexpr int kSmallVpt = 16;
+
+template <typename T, int TL, bool FIXUP>
+__global__ void __launch_bounds__(kSmallRows * TL) mc_codes_small_kernel(
+    const T* __restrict__ preds, const int64_t* __restrict__ target, int64_t n, int C, int* __restrict__ mode, int64_t ignore_index,
+    bool has_ignore, uint16_t* __restrict__ codes, int64_t n_pad, int64_t* __restrict__ confmat, int* __restrict__ err,
+    bool record_mode, int* __restrict__ slow_rows, int* __restrict__ slow_count) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t s_small[];  // staging [64][C], then image [C][64]
+  int use_mode;
+  if constexpr (FIXUP) {
+    const int m0 = mode[0], m1 = mode[1];
+    if (m0 == m1) return;
+    use_mode = m1;
+  } else {
+    use_mode = mode[0];
+  }
+  const int64_t r0 = (int64_t)blockIdx.x * kSmallRows;
+  const int rows = static_cast<int>(min<int64_t>(kSmallRows, n - r0));
+  // 1. stage the block's scores (byte range [r0 C, (r0 + rows) C) x 2; r0 C x 2 is a multiple of 128 B)
+  {
+    const int64_t nelem = (int64_t)rows * C;
+    const uint16_t* src = reinterpret_cast<const uint16_t*>(preds) + r0 * C;
+    const int nvec = static_cast<int>(nelem / 8);
+    for (int i = threadIdx.x; i < nvec; i += kSmallRows * TL)
+      reinterpret_cast<uint4*>(s_small)[i] = reinterpret_cast<const uint4*>(src)[i];
+    for (int i = nvec * 8 + threadIdx.x; i < nelem; i += kSmallRows * TL) s_small[i] = src[i];
+  }
+  __syncthreads();
+  const int q = threadIdx.x % TL, lr = threadIdx.x / TL;  // lane within the row, row within the block
+  const int64_t r = r0 + lr;
+  const int cb = q * kSmallVpt;
+  const bool in_rows = lr < rows;
+  float v[kSmallVpt];
+  uint16_t raw[kSmallVpt];
+#pragma unroll
+  for (int j = 0; j < kSmallVpt; ++j) {
+    const int c = cb + j;
+    const bool ok = in_rows && c < C;
+    raw[j] = ok ? s_small[lr * C + c] : (uint16_t)0;
+    v[j] = ok ? to_f32<T>(*reinterpret_cast<const T*>(&raw[j])) : -INFINITY;
+  }
+  const int64_t t = in_rows ? target[r] : -1;
+  const bool valid = in_rows && !(has_ignore && t == ignore_index);
+  // row statistics over the TL lanes of the row (xor shuffles stay inside aligned groups of TL lanes)
+  float mx = -INFINITY, mn = INFINITY, sum = 0.f;
+#pragma unroll
+  for (int j = 0; j < kSmallVpt; ++j) {
+    if (cb + j < C) {
+      mx = __builtin_fmaxf(mx, v[j]);
+      mn = __builtin_fminf(mn, v[j]);
+      sum += v[j];
+    }
+  }
+#pragma unroll
+  for (int off = 1; off < TL; off <<= 1) {
+    mx = __builtin_fmaxf(mx, __shfl_xor(mx, off, kWave));
+    mn = __builtin_fminf(mn, __shfl_xor(mn, off, kWave));
+    sum += __shfl_xor(sum, off, kWave);
+  }
+  bool fin = __builtin_isfinite(mx);
+  // arg-max of a finite row: the first class holding the maximum
+  int am = C;
+#pragma unroll
+  for (int j = kSmallVpt - 1; j >= 0; --j)
+    if (cb + j < C && v[j] == mx) am = cb + j;
+#pragma unroll
+  for (int off = 1; off < TL; off <<= 1) am = min(am, __shfl_xor(am, off, kWave));
+  float s = 0.f, inv = 0.f;
+  if (use_mode != 0) {
+    float acc = 0.f;
+#pragma unroll
+    for (int j = 0; j < kSmallVpt; ++j) {
+      v[j] = cb + j < C ? exp_nonpos(v[j] - mx) : 0.f;
+      acc += v[j];
+    }
+#pragma unroll
+    for (int off = 1; off < TL; off <<= 1) acc += __shfl_xor(acc, off, kWave);
+    s = acc;
+    inv = 1.f / s;
+    fin = fin && s == s;
+  } else {
+    fin = fin && __builtin_isfinite(sum);
+  }
+  const bool slow = valid && !fin;
+  const bool keep = valid && fin;
+  // 3. codes into the image [C][64] (the staging area is free once every lane holds its values)
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kSmallVpt; ++j) {
+    const int c = cb + j;
+    if (!in_rows || c >= C) continue;
+    uint32_t code = 0x8000u;
+    if (keep) {
+      const uint32_t b = use_mode != 0 ? (rne_word<T>(div_rn(v[j], s, inv)) >> 16) : (uint32_t)raw[j];
+      code = raw_code<T>(b);
+      if (c == t && !(code & 0x8000u)) code |= 0x4000u;
+    }
+    s_small[c * kSmallRows + lr] = static_cast<uint16_t>(code);
+  }
+  if (lr >= rows && q == 0) {  // padding rows of the last block: skipped codes
+    for (int c = 0; c < C; ++c) s_small[c * kSmallRows + lr] = 0x8000u;
+  }
+  if (q == 0 && in_rows) {
+    if constexpr (!FIXUP) {
+      if (confmat != nullptr && keep && t >= 0 && t < C && am < C) atomic_add_i64(confmat + t * C + am, 1);
+      if (err != nullptr && valid && (t < 0 || t >= C)) atomicOr(err, 1);
+    }
+    if (slow) {
+      const int list = FIXUP ? 1 : 0;
+      slow_rows[list * n + atomicAdd(slow_count + list, 1)] = static_cast<int>(r);
+    }
+  }
+  bool bad = false;
+  if (!FIXUP && record_mode && q == 0) bad = slow || (valid && (mx > 1.f || mn < 0.f));
+  __syncthreads();
+  // class segments: C rows of 64 codes = 8 x 16 B each
+  for (int i = threadIdx.x; i < C * 8; i += kSmallRows * TL) {
+    const int c = i >> 3, k = i & 7;
+    reinterpret_cast<uint4*>(codes + (int64_t)c * n_pad + r0)[k] = reinterpret_cast<const uint4*>(s_small + c * kSmallRows)[k];
+  }
+  if constexpr (!FIXUP) {
+    if (record_mode && __syncthreads_or(bad) && threadIdx.x == 0 &&
+        __hip_atomic_load(mode + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
+      __hip_atomic_store(mode + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+template <typename T, bool FIXUP>
+void launch_small_rows(int TL, int grid, const T* p, const int64_t* target, int64_t n, int C, int* mode, int64_t ignore_index, bool has_ignore,
+                       uint16_t* codes, int64_t n_pad, int64_t* cm, int* err, bool rec, int* srows, int* scount) {
+  const size_t shm = (size_t)kSmallRows * C * sizeof(uint16_t);
+#define TMX_SMALL_CASE(TLV)                                                                                                      \
+  case TLV:                                                                                                                      \
+    hipLaunchKernelGGL((mc_codes_small_kernel<T, TLV, FIXUP>), grid, kSmallRows * TLV, shm, stream(), p, target, n, C, mode,   \
+                       ignore_index, has_ignore, codes, n_pad, cm, err, rec, srows, scount);                                      \
+    break;
+  switch (TL) {
+    TMX_SMALL_CASE(1) TMX_SMALL_CASE(2) TMX_SMALL_CASE(4) TMX_SMALL_CASE(8) TMX_SMALL_CASE(16)
+    default: TORCH_CHECK(false, "mc_codes_small: unsupported lanes per row");
+  }
+#undef TMX_SMALL_CASE
+  TMX_LAUNCH_CHECK();
+}
+
+// Small-class two-pass route: small row pass (+ FIXUP), then the shared class pass (which finishes rare rows and
+// rolls the speculation).  Codes are class-major [C][n_pad], n_pad = 64-row blocks.
+template <typename T>
+void launch_small_two_pass(const T* p, const int64_t* target, int64_t n, int C, int* mode, int* state, bool speculative,
+                           int64_t ignore_index, bool has_ignore, int64_t* hist, int64_t* cm, int* err, const at::TensorOptions& opts,
+                           int* code_range) {
+  TORCH_CHECK(n < (int64_t{1} << 31), "curve_hist_update: more than 2^31 rows in one batch");
+  const int64_t n_pad = (n + kSmallRows - 1) / kSmallRows * kSmallRows;
+  const int grid = static_cast<int>(n_pad / kSmallRows);
+  int TL = 1;
+  while (TL * kSmallVpt < C) TL *= 2;
+  auto codes = at::empty({(int64_t)C * n_pad}, opts.dtype(at::kShort));
+  auto slow_rows = at::empty({2 * n}, opts.dtype(at::kInt));
+  uint16_t* cptr = reinterpret_cast<uint16_t*>(codes.data_ptr());
+  int* srows = slow_rows.data_ptr<int>();
+  launch_small_rows<T, false>(TL, grid, p, target, n, C, mode, ignore_index, has_ignore, cptr, n_pad, cm, err, speculative, srows, state);
+  if (speculative)
+    launch_small_rows<T, true>(TL, std::min(grid, 1024), p, target, n, C, mode, ignore_index, has_ignore, cptr, n_pad, cm, err, false,
+                               srows, state);
+  // the class pass reads n_pad as a multiple of 8 rows (uint4) and ld = C (unpadded rows)
+  int splits = 1;
+  while ((int64_t)C * splits < 512 && n_pad / (8 * (splits * 2)) >= 1024) splits *= 2;
+  hipLaunchKernelGGL((class_hist_kernel<T, false>), C * splits, kClassThreads, kCodes * sizeof(uint32_t), stream(), cptr, n_pad, splits,
+                     hist, p, C, target, n, mode, speculative, srows, state, cm, code_range, speculative ? mode : nullptr);
+  TMX_LAUNCH_CHECK();
+}
+
 // Row pass of the multiclass two-pass route (+ FIXUP and the speculation roll when speculative), into caller-owned
 // scratch: ``codes`` int16 [C * n_pad] (class-major), ``slow_rows`` int32 [2 n], ``state`` int32[6] (counts zero).
 template <typename T, bool PADDED>
@@ -1653,6 +1838,14 @@ void curve_hist_update(const at::Tensor& preds_, const at::Tensor& target_, at::
       const int64_t n = target.numel();
       if (n == 0) { range_tracked = true; return; }
       TORCH_CHECK(preds.numel() == n * C, "preds must be [N, C]");
+      static const bool small_off = std::getenv("TMX_CURVE_SMALL_OFF") != nullptr;  // A/B against the tile row pass
+      const bool small_ok = !small_off && C <= kSmallVpt * 16 && (reinterpret_cast<uintptr_t>(preds.data_ptr()) & 15) == 0;
+      if (small_ok) {
+        launch_small_two_pass<scalar_t>(p, target.data_ptr<int64_t>(), n, C, flag.data_ptr<int>(), state.data_ptr<int>(), speculative,
+                                        ignore_index, has_ignore, hist.data_ptr<int64_t>(), cm, err, preds.options(), crange);
+        range_tracked = true;
+        return;
+      }
       if (two_pass_ok) {
         if (C % 8 != 0) {
           const int ld = (C + 7) / 8 * 8;

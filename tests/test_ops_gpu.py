@@ -806,3 +806,52 @@ def test_cat_metric_gpu_defers_nan_drop(strategy):
         mc.update(xs[2])
         assert torch.equal(out_fwd.cpu(), ref_fwd)
         assert torch.equal(mg.compute().cpu(), mc.compute())
+
+
+@pytest.mark.parametrize("C", [2, 3, 10, 16, 17, 64, 100, 200, 256])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_curve_hist_small_classes_vs_aten_softmax(C, dtype):
+    """Small-class row pass (C <= 256, T lanes per row, csrc/classification.hip mc_codes_small_kernel): the histogram
+    equals the one built from ATen's softmax codes up to one-code moves of rounding-boundary quotients (same bound as
+    the wide row pass), totals and the fused confusion matrix are exact."""
+    N = 200_003  # not a multiple of the 64-row block
+    g = torch.Generator(device="cuda").manual_seed(C)
+    x = (torch.randn(N, C, device="cuda", generator=g) * 3).to(dtype)
+    t = torch.randint(0, C, (N,), device="cuda", generator=g)
+    t[::29] = -1
+    hist = torch.zeros(C, 2, K.N_CODES, dtype=torch.long, device="cuda")
+    cm = torch.zeros(C, C, dtype=torch.long, device="cuda")
+    K.curve_hist_update(x, t, hist, "multiclass", -1, cm)
+    keep = t != -1
+    ref = torch.softmax(x[keep].float(), dim=1).to(dtype)
+    href = _hist_from_scores(ref, t[keep], C)
+    moved = int((hist - href).abs().sum()) // 2
+    assert moved <= max(4, int((2e-5 if dtype == torch.bfloat16 else 1.5e-4) * N * C)), moved
+    assert int(hist.sum()) == int(href.sum())
+    cm_ref = torch.zeros(C, C, dtype=torch.long, device="cuda")
+    cm_ref.view(-1).index_add_(0, t[keep] * C + x[keep].float().argmax(1), torch.ones_like(t[keep]))
+    assert torch.equal(cm, cm_ref)
+
+
+@pytest.mark.parametrize("C", [2, 10, 64, 200])
+def test_curve_small_classes_speculation_and_rare_rows(C):
+    """Module path through the small-class route: mode speculation flips (logits <-> probabilities, NaN batches),
+    rare NaN / inf rows and ignore_index agree with the CPU implementation."""
+    import torchmetrics_forked_amd as tm
+
+    batches = _flip_batches(C, 5000, seed=C)
+    res = []
+    for dev in ("cuda", "cpu"):
+        m = tm.MulticlassAUROC(num_classes=C, average="macro", ignore_index=-1).to(dev)
+        cmm = tm.MulticlassConfusionMatrix(num_classes=C, ignore_index=-1).to(dev)
+        vals = []
+        for x, t in batches:
+            t = t.clone()
+            t[::31] = -1
+            m.update(x.to(dev), t.to(dev))
+            cmm.update(x.to(dev), t.to(dev))
+            vals.append(m.compute().item())
+        res.append((vals, cmm.compute().cpu()))
+    assert torch.equal(res[0][1], res[1][1])
+    for a, b in zip(res[0][0], res[1][0]):
+        assert abs(a - b) < 1e-4 or (a != a and b != b), (res[0][0], res[1][0])

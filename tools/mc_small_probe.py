@@ -1,4 +1,5 @@
 """MulticlassAUROC update cost across class counts (two-pass path needs C % 8 == 0; others take the generic kernel)."""
+import json
 import os
 import sys
 import time
@@ -25,9 +26,11 @@ def timed(fn, n=10):
 
 
 out = {}
-for C, N in ((10, 1 << 20), (16, 1 << 20), (100, 1 << 18), (104, 1 << 18), (1000, 1 << 16), (1001, 1 << 16)):
+for C, N in ((2, 1 << 20), (10, 1 << 20), (16, 1 << 20), (64, 1 << 20), (100, 1 << 18), (104, 1 << 18), (256, 1 << 18),
+             (1000, 1 << 16), (1001, 1 << 16)):
     p = torch.randn(N, C, device=dev).bfloat16()
     t = torch.randint(0, C, (N,), device=dev)
     m = tm.MulticlassAUROC(num_classes=C).to(dev)
-    out[f"C{C}_N{N}_ms"] = round(1e3 * timed(lambda: m.update(p, t)), 3)
-print(out)
+    ms = 1e3 * timed(lambda: m.update(p, t))
+    out[f"C{C}_N{N}"] = {"ms": round(ms, 4), "input_TBps": round(p.numel() * 2 / (ms * 1e-3) / 1e12, 3)}
+print(json.dumps(out))
