@@ -1,0 +1,578 @@
+// K6 for fp32 / fp64 scores at any size: a hand-written stable segmented LSD radix sort of class-major scores with a
+// fused tie-group scan (reference `_binary_clf_curve`, TF/classification/precision_recall_curve.py:
+// 28-80, one argsort per class in a Python loop at :558-563, and roc.py:182-187).
+//
+//   * prep     — every (segment = class / label, sample) score becomes an order key whose ascending order is the
+//                DESCENDING score order (NaN first, -0.0 == +0.0), with a one-byte payload: bit 0 = positive label,
+//                bit 1 = ignored sample.  Multiclass labels come from target == class (no one-hot tensor).
+//   * sort     — LSD radix, 8-bit digits (4 passes for fp32 keys, 8 for fp64), each pass = tile histograms ->
+//                segmented exclusive scan -> scatter.  A tile is 4096 keys of ONE segment (256 threads x 16);
+//                the scatter ranks stably per wave: 64 consecutive keys per round, digit groups by 8 ballots, a
+//                running count per (wave, digit) in LDS, then a prefix over the 4 waves — deterministic.
+//   * reduce   — per tile: cumulative positive / negative weights (tile sums scanned per segment), tie-group ends
+//                where the next key differs, the previous group end's cumulative counts by a block scan (and a
+//                binary search when a tie group spans tiles); AUROC trapezoid and AP step terms summed in fp64,
+//                per-tile partials combined in a fixed order (deterministic); optional curve points (fps, tps,
+//                threshold) at every group end, compacted by a scanned count.
+// Replaces ATen's torch.sort + gather + cumsum + cummax chain in functional/classification/_curve_engine.py.
+#include <c10/hip/HIPGuard.h>
+
+#include "common.h"
+
+namespace tmx {
+
+constexpr int kRsThreads = 256;
+constexpr int kRsItems = 16;
+constexpr int kRsTile = kRsThreads * kRsItems;  // 4096 keys of one segment
+constexpr int kRsBins = 256;
+constexpr int kScanChunk = 2048;                // values per block of the segmented scan (256 threads x 8)
+
+template <typename K> struct KeyOf;
+template <> struct KeyOf<float> {
+  using type = uint32_t;
+  __device__ static uint32_t desc(float f) {
+    if (f != f) return 0u;                      // NaN: largest score -> first
+    uint32_t b = __float_as_uint(f == 0.f ? 0.f : f);  // -0.0 == +0.0
+    const uint32_t u = (b & 0x80000000u) ? ~b : (b | 0x80000000u);  // ascending float order
+    return ~u;                                   // ascending key = descending score
+  }
+  __device__ static float value(uint32_t k) {
+    const uint32_t u = ~k;
+    const uint32_t b = (u & 0x80000000u) ? (u & 0x7FFFFFFFu) : ~u;
+    return k == 0u ? __uint_as_float(0x7FC00000u) : __uint_as_float(b);
+  }
+};
+template <> struct KeyOf<double> {
+  using type = uint64_t;
+  __device__ static uint64_t desc(double f) {
+    if (f != f) return 0ull;
+    uint64_t b = static_cast<uint64_t>(__double_as_longlong(f == 0.0 ? 0.0 : f));
+    const uint64_t u = (b >> 63) ? ~b : (b | (1ull << 63));
+    return ~u;
+  }
+  __device__ static double value(uint64_t k) {
+    const uint64_t u = ~k;
+    const uint64_t b = (u >> 63) ? (u & 0x7FFFFFFFFFFFFFFFull) : ~u;
+    return k == 0ull ? __longlong_as_double(0x7FF8000000000000ll) : __longlong_as_double(static_cast<long long>(b));
+  }
+};
+
+// ---------------------------------------------------------------------------------------------------------- prep
+// Scores of one chunk: element (s, r) at p[s * ss + r * rs], r < n_k, written to keys[s][off + r].
+// task 0 (multiclass): label = target[off + r] == s, ignored when == ignore_index;  task 1 (per element): target is
+// row-major [n, S]: label = t == 1, ignored when t == ignore_index.
+template <typename T>
+__global__ void rs_prep_kernel(const T* __restrict__ p, int64_t ss, int64_t rs, int64_t n_k, int64_t off, int S, int64_t n,
+                               const int64_t* __restrict__ target, int task, int64_t ignore_index, bool has_ignore,
+                               typename KeyOf<T>::type* __restrict__ keys, uint8_t* __restrict__ pay) {
+  const int64_t total = (int64_t)S * n_k;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int s = static_cast<int>(i / n_k);
+    const int64_t r = i % n_k;
+    const int64_t row = off + r;
+    const int64_t t = task == 0 ? target[row] : target[row * S + s];
+    const bool ign = has_ignore && t == ignore_index;
+    const bool pos = task == 0 ? (t == s) : (t == 1);
+    keys[(int64_t)s * n + row] = KeyOf<T>::desc(p[s * ss + r * rs]);
+    pay[(int64_t)s * n + row] = static_cast<uint8_t>((pos && !ign ? 1 : 0) | (ign ? 2 : 0));
+  }
+}
+
+// ----------------------------------------------------------------------------------------------- sort: histograms
+// hist layout [S][256][T] (digit-major per segment): the scan of a segment is then one contiguous run.
+template <typename KT>
+__global__ void __launch_bounds__(kRsThreads) rs_hist_kernel(const KT* __restrict__ keys, int64_t n, int T, int shift, uint32_t* __restrict__ hist) {
+  __shared__ uint32_t h[4][kRsBins];
+  const int s = blockIdx.x / T, t = blockIdx.x % T;
+  const int wave = threadIdx.x / kWave;
+  for (int i = threadIdx.x; i < 4 * kRsBins; i += kRsThreads) (&h[0][0])[i] = 0u;
+  __syncthreads();
+  const int64_t base = (int64_t)s * n + (int64_t)t * kRsTile;
+  const int64_t len = min<int64_t>(kRsTile, n - (int64_t)t * kRsTile);
+  for (int i = threadIdx.x; i < len; i += kRsThreads) atomicAdd(&h[wave][(keys[base + i] >> shift) & 0xFF], 1u);
+  __syncthreads();
+  const uint32_t c = h[0][threadIdx.x] + h[1][threadIdx.x] + h[2][threadIdx.x] + h[3][threadIdx.x];
+  hist[((int64_t)s * kRsBins + threadIdx.x) * T + t] = c;
+}
+
+// ------------------------------------------------------------------------------- segmented exclusive scan (u32)
+// a [S][L] array; chunks of 2048 never straddle segments (cps = chunks per segment).  Level 1 scans each chunk in
+// place and writes its total; level 2 scans each segment's chunk totals in place (cps <= 4096).
+__global__ void __launch_bounds__(256) seg_scan_local_kernel(uint32_t* __restrict__ a, int64_t L, int cps, uint32_t* __restrict__ csum) {
+  __shared__ uint32_t part[256];
+  const int s = blockIdx.x / cps, c = blockIdx.x % cps;
+  uint32_t* seg = a + (int64_t)s * L;
+  const int64_t c0 = (int64_t)c * kScanChunk;
+  uint32_t v[8];
+  uint32_t tot = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int64_t i = c0 + threadIdx.x * 8 + k;
+    v[k] = i < L ? seg[i] : 0u;
+    tot += v[k];
+  }
+  part[threadIdx.x] = tot;
+  __syncthreads();
+  for (int off = 1; off < 256; off <<= 1) {  // inclusive Hillis-Steele over 256 thread totals
+    const uint32_t x = threadIdx.x >= off ? part[threadIdx.x - off] : 0u;
+    __syncthreads();
+    part[threadIdx.x] += x;
+    __syncthreads();
+  }
+  uint32_t run = threadIdx.x ? part[threadIdx.x - 1] : 0u;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int64_t i = c0 + threadIdx.x * 8 + k;
+    if (i < L) seg[i] = run;
+    run += v[k];
+  }
+  if (threadIdx.x == 255) csum[(int64_t)s * cps + c] = part[255];
+}
+
+__global__ void __launch_bounds__(256) seg_scan_csum_kernel(uint32_t* __restrict__ csum, int cps) {
+  __shared__ uint32_t part[256];
+  uint32_t* seg = csum + (int64_t)blockIdx.x * cps;
+  const int per = (cps + 255) / 256;  // <= 16
+  uint32_t v[16];
+  uint32_t tot = 0;
+  for (int k = 0; k < per; ++k) {
+    const int i = threadIdx.x * per + k;
+    v[k] = i < cps ? seg[i] : 0u;
+    tot += v[k];
+  }
+  part[threadIdx.x] = tot;
+  __syncthreads();
+  for (int off = 1; off < 256; off <<= 1) {
+    const uint32_t x = threadIdx.x >= off ? part[threadIdx.x - off] : 0u;
+    __syncthreads();
+    part[threadIdx.x] += x;
+    __syncthreads();
+  }
+  uint32_t run = threadIdx.x ? part[threadIdx.x - 1] : 0u;
+  for (int k = 0; k < per; ++k) {
+    const int i = threadIdx.x * per + k;
+    if (i < cps) seg[i] = run;
+    run += v[k];
+  }
+}
+
+// value i of segment s after both levels: a[s][i] + csum[s][i / 2048]
+__device__ __forceinline__ uint32_t seg_scanned(const uint32_t* a, const uint32_t* csum, int64_t L, int cps, int s, int64_t i) {
+  return a[(int64_t)s * L + i] + csum[(int64_t)s * cps + i / kScanChunk];
+}
+
+inline void seg_exclusive_scan(uint32_t* a, int S, int64_t L, uint32_t* csum, int cps) {
+  hipLaunchKernelGGL(seg_scan_local_kernel, S * cps, 256, 0, stream(), a, L, cps, csum);
+  TMX_LAUNCH_CHECK();
+  hipLaunchKernelGGL(seg_scan_csum_kernel, S, 256, 0, stream(), csum, cps);
+  TMX_LAUNCH_CHECK();
+}
+
+// ----------------------------------------------------------------------------------------------- sort: scatter
+// Wave w ranks tile keys [w * 1024, w * 1024 + 1024) in 16 rounds of 64 consecutive keys; equal-digit lanes of a
+// round are found with 8 ballots; cnt[w][d] is the wave's running count of digit d.  The tile is then reordered by
+// digit in LDS (stable) and written out in digit runs: consecutive threads store consecutive addresses of a run
+// (a direct scatter would touch up to 64 cache lines per store instruction).
+template <typename KT>
+__global__ void __launch_bounds__(kRsThreads) rs_scatter_kernel(const KT* __restrict__ kin, const uint8_t* __restrict__ pin,
+                                                                 KT* __restrict__ kout, uint8_t* __restrict__ pout, int64_t n, int T,
+                                                                 int shift, const uint32_t* __restrict__ hist, const uint32_t* __restrict__ csum,
+                                                                 int64_t L, int cps) {
+  __shared__ uint32_t cnt[4][kRsBins];
+  __shared__ uint32_t gbase[kRsBins];   // destination of the tile's first key of digit d (segment-relative)
+  __shared__ uint32_t lstart[kRsBins];  // first tile position of digit d after the local reorder
+  __shared__ KT s_key[kRsTile];
+  __shared__ uint8_t s_pay[kRsTile];
+  const int s = blockIdx.x / T, t = blockIdx.x % T;
+  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+  for (int i = threadIdx.x; i < 4 * kRsBins; i += kRsThreads) (&cnt[0][0])[i] = 0u;
+  gbase[threadIdx.x] = seg_scanned(hist, csum, L, cps, s, (int64_t)threadIdx.x * T + t);
+  __syncthreads();
+  const int64_t seg0 = (int64_t)s * n;
+  const int64_t tb = (int64_t)t * kRsTile;
+  const int64_t len = min<int64_t>(kRsTile, n - tb);
+  KT key[kRsItems];
+  uint8_t pay[kRsItems];
+  uint32_t rank[kRsItems];
+#pragma unroll
+  for (int k = 0; k < kRsItems; ++k) {
+    const int64_t i = (int64_t)wave * (kRsTile / 4) + k * kWave + lane;
+    const bool ok = i < len;
+    key[k] = ok ? kin[seg0 + tb + i] : KT(0);
+    pay[k] = ok ? pin[seg0 + tb + i] : uint8_t(0);
+  }
+#pragma unroll
+  for (int k = 0; k < kRsItems; ++k) {
+    const int64_t i = (int64_t)wave * (kRsTile / 4) + k * kWave + lane;
+    const bool ok = i < len;
+    const uint32_t d = static_cast<uint32_t>((key[k] >> shift) & 0xFF);
+    uint64_t match = __ballot(ok);
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      const uint64_t bal = __ballot((d >> b) & 1u);
+      match &= ((d >> b) & 1u) ? bal : ~bal;
+    }
+    const uint64_t lower = match & ((1ull << lane) - 1ull);
+    const uint32_t before = cnt[wave][d];  // running count of this digit in this wave (earlier rounds)
+    rank[k] = ok ? before + static_cast<uint32_t>(__popcll(lower)) : 0xFFFFFFFFu;
+    // the lowest lane of each digit group advances the running count (one writer per digit per round)
+    if (ok && lower == 0ull) cnt[wave][d] = before + static_cast<uint32_t>(__popcll(match));
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the next round reads what this one wrote
+  }
+  __syncthreads();
+  {
+    // per digit: prefix over the waves (wave 0's keys precede wave 1's in the tile), and the tile's digit totals
+    const uint32_t c0 = cnt[0][threadIdx.x], c1 = cnt[1][threadIdx.x], c2 = cnt[2][threadIdx.x], c3 = cnt[3][threadIdx.x];
+    __syncthreads();
+    cnt[0][threadIdx.x] = 0u;
+    cnt[1][threadIdx.x] = c0;
+    cnt[2][threadIdx.x] = c0 + c1;
+    cnt[3][threadIdx.x] = c0 + c1 + c2;
+    lstart[threadIdx.x] = c0 + c1 + c2 + c3;  // tile total of digit d, scanned below
+  }
+  __syncthreads();
+  for (int off = 1; off < kRsBins; off <<= 1) {  // inclusive scan of the digit totals (256 entries, one per thread)
+    const uint32_t x = threadIdx.x >= off ? lstart[threadIdx.x - off] : 0u;
+    __syncthreads();
+    lstart[threadIdx.x] += x;
+    __syncthreads();
+  }
+  const uint32_t my_excl = threadIdx.x ? lstart[threadIdx.x - 1] : 0u;
+  __syncthreads();
+  lstart[threadIdx.x] = my_excl;
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < kRsItems; ++k) {
+    if (rank[k] == 0xFFFFFFFFu) continue;
+    const uint32_t d = static_cast<uint32_t>((key[k] >> shift) & 0xFF);
+    const uint32_t lp = lstart[d] + cnt[wave][d] + rank[k];
+    s_key[lp] = key[k];
+    s_pay[lp] = pay[k];
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < len; j += kRsThreads) {
+    const KT k = s_key[j];
+    const uint32_t d = static_cast<uint32_t>((k >> shift) & 0xFF);
+    const int64_t dst = seg0 + gbase[d] + (j - lstart[d]);
+    kout[dst] = k;
+    pout[dst] = s_pay[j];
+  }
+}
+
+// ------------------------------------------------------------------------------------------------ reduce (fused)
+// Tile sums: positive weight, negative weight, group ends (key differs from the next key, or last of segment).
+template <typename KT>
+__global__ void __launch_bounds__(kRsThreads) rs_tile_sums_kernel(const KT* __restrict__ keys, const uint8_t* __restrict__ pay, int64_t n, int T,
+                                                                   uint32_t* __restrict__ pos_t, uint32_t* __restrict__ neg_t,
+                                                                   uint32_t* __restrict__ end_t) {
+  const int s = blockIdx.x / T, t = blockIdx.x % T;
+  const int64_t seg0 = (int64_t)s * n, tb = (int64_t)t * kRsTile;
+  const int64_t len = min<int64_t>(kRsTile, n - tb);
+  uint32_t p = 0, q = 0, e = 0;
+  for (int64_t i = threadIdx.x; i < len; i += kRsThreads) {
+    const uint8_t w = pay[seg0 + tb + i];
+    p += (w & 1u) ? 1u : 0u;
+    q += (w & 3u) == 0u ? 1u : 0u;
+    const int64_t g = tb + i;
+    e += (g + 1 == n || keys[seg0 + g] != keys[seg0 + g + 1]) ? 1u : 0u;
+  }
+  __shared__ uint32_t r[3][kRsThreads / kWave];
+  p = static_cast<uint32_t>(wave_sum((long long)p));
+  q = static_cast<uint32_t>(wave_sum((long long)q));
+  e = static_cast<uint32_t>(wave_sum((long long)e));
+  if ((threadIdx.x & (kWave - 1)) == 0) { r[0][threadIdx.x / kWave] = p; r[1][threadIdx.x / kWave] = q; r[2][threadIdx.x / kWave] = e; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    pos_t[(int64_t)s * T + t] = r[0][0] + r[0][1] + r[0][2] + r[0][3];
+    neg_t[(int64_t)s * T + t] = r[1][0] + r[1][1] + r[1][2] + r[1][3];
+    end_t[(int64_t)s * T + t] = r[2][0] + r[2][1] + r[2][2] + r[2][3];
+  }
+}
+
+struct RsScan {  // a segment-scanned [S][T] array
+  const uint32_t* a;
+  const uint32_t* csum;
+  int cps;
+};
+
+// Per tile (blocked: thread j owns keys [16 j, 16 j + 16) of the tile): cumulative weights, group ends, AUROC / AP
+// terms at every group end against the previous group end, curve points.  part[s][t] = {area, ap} (fp64).
+template <typename T, typename KT>
+__global__ void __launch_bounds__(kRsThreads) rs_reduce_kernel(const KT* __restrict__ keys, const uint8_t* __restrict__ pay, int64_t n, int Tt,
+                                                                RsScan ps, RsScan qs, RsScan es, double* __restrict__ part,
+                                                                float* __restrict__ pt_fps, float* __restrict__ pt_tps, T* __restrict__ pt_thr,
+                                                                const int64_t* __restrict__ pt_base) {
+  const int s = blockIdx.x / Tt, t = blockIdx.x % Tt;
+  const int64_t seg0 = (int64_t)s * n, tb = (int64_t)t * kRsTile;
+  const int64_t len = min<int64_t>(kRsTile, n - tb);
+  __shared__ uint32_t sp[kRsThreads], sq[kRsThreads], se[kRsThreads];
+  __shared__ int32_t slast[kRsThreads];   // thread's last group end (tile index) or -1
+  __shared__ uint32_t slp[kRsThreads], slq[kRsThreads];
+  __shared__ double red[2][kRsThreads / kWave];
+  __shared__ uint32_t s_prev[2];
+  const int j0 = threadIdx.x * kRsItems;
+  uint32_t cp = 0, cq = 0, ce = 0;
+  int32_t last = -1;
+  uint32_t lp = 0, lq = 0;
+  for (int k = 0; k < kRsItems; ++k) {
+    const int64_t i = j0 + k;
+    if (i >= len) break;
+    const uint8_t w = pay[seg0 + tb + i];
+    cp += (w & 1u) ? 1u : 0u;
+    cq += (w & 3u) == 0u ? 1u : 0u;
+    const int64_t g = tb + i;
+    if (g + 1 == n || keys[seg0 + g] != keys[seg0 + g + 1]) { ++ce; last = static_cast<int32_t>(i); lp = cp; lq = cq; }
+  }
+  sp[threadIdx.x] = cp; sq[threadIdx.x] = cq; se[threadIdx.x] = ce;
+  slast[threadIdx.x] = last; slp[threadIdx.x] = lp; slq[threadIdx.x] = lq;
+  __syncthreads();
+  // inclusive scans over the 256 threads (log steps): counts, and "cumulative at the latest group end" (a thread with
+  // no group end inherits its predecessor's); slp / slq become tile-relative cumulative counts at that end
+  for (int off = 1; off < kRsThreads; off <<= 1) {
+    const bool has = threadIdx.x >= off;
+    const uint32_t ap_ = has ? sp[threadIdx.x - off] : 0u, aq_ = has ? sq[threadIdx.x - off] : 0u, ae_ = has ? se[threadIdx.x - off] : 0u;
+    const int32_t al = has ? slast[threadIdx.x - off] : -1;
+    const uint32_t alp = has ? slp[threadIdx.x - off] : 0u, alq = has ? slq[threadIdx.x - off] : 0u;
+    __syncthreads();
+    if (has) {
+      // combine (earlier = a*, later = mine): a later end wins; its cumulative gains the earlier block's counts
+      if (slast[threadIdx.x] >= 0) { slp[threadIdx.x] += ap_; slq[threadIdx.x] += aq_; }
+      else if (al >= 0) { slast[threadIdx.x] = al; slp[threadIdx.x] = alp; slq[threadIdx.x] = alq; }
+      sp[threadIdx.x] += ap_; sq[threadIdx.x] += aq_; se[threadIdx.x] += ae_;
+    }
+    __syncthreads();
+  }
+  // exclusive values for this thread = inclusive values of the previous thread
+  const bool first = threadIdx.x == 0;
+  const uint32_t xp = first ? 0u : sp[threadIdx.x - 1], xq = first ? 0u : sq[threadIdx.x - 1], xe = first ? 0u : se[threadIdx.x - 1];
+  const int32_t plast = first ? -1 : slast[threadIdx.x - 1];
+  const uint32_t pl_p = first ? 0u : slp[threadIdx.x - 1], pl_q = first ? 0u : slq[threadIdx.x - 1];
+  const uint32_t P0 = seg_scanned(ps.a, ps.csum, Tt, ps.cps, s, t), Q0 = seg_scanned(qs.a, qs.csum, Tt, qs.cps, s, t);
+  const uint32_t E0 = seg_scanned(es.a, es.csum, Tt, es.cps, s, t);
+  // cumulative at the last group end before the tile: P0 / Q0 when the tile starts a group, else the counts before
+  // the start of the group that runs into the tile (binary search for its first key; rare: ties across tiles)
+  if (threadIdx.x == 0) {
+    uint32_t bp = P0, bq = Q0;
+    if (t > 0 && keys[seg0 + tb - 1] == keys[seg0 + tb]) {
+      const KT k0 = keys[seg0 + tb];
+      int64_t lo = 0, hi = tb - 1;  // first index with key == k0 (keys ascending)
+      while (lo < hi) {
+        const int64_t mid = (lo + hi) / 2;
+        if (keys[seg0 + mid] < k0) lo = mid + 1; else hi = mid;
+      }
+      const int64_t g0 = lo;
+      const int tg = static_cast<int>(g0 / kRsTile);
+      bp = seg_scanned(ps.a, ps.csum, Tt, ps.cps, s, tg);
+      bq = seg_scanned(qs.a, qs.csum, Tt, qs.cps, s, tg);
+      for (int64_t i = (int64_t)tg * kRsTile; i < g0; ++i) {  // partial tile before the group start
+        const uint8_t w = pay[seg0 + i];
+        bp += (w & 1u) ? 1u : 0u;
+        bq += (w & 3u) == 0u ? 1u : 0u;
+      }
+    }
+    s_prev[0] = bp;
+    s_prev[1] = bq;
+  }
+  __syncthreads();
+  // previous group end's cumulative for this thread's first group end
+  double tp_prev = plast >= 0 ? (double)(P0 + pl_p) : (double)s_prev[0];
+  double fp_prev = plast >= 0 ? (double)(Q0 + pl_q) : (double)s_prev[1];
+  uint32_t rp = P0 + xp, rq = Q0 + xq;
+  int64_t ob = pt_base != nullptr ? pt_base[s] + E0 + xe : 0;
+  double area = 0.0, ap = 0.0;
+  for (int k = 0; k < kRsItems; ++k) {
+    const int64_t i = j0 + k;
+    if (i >= len) break;
+    const uint8_t w = pay[seg0 + tb + i];
+    rp += (w & 1u) ? 1u : 0u;
+    rq += (w & 3u) == 0u ? 1u : 0u;
+    const int64_t g = tb + i;
+    const KT kk = keys[seg0 + g];
+    if (g + 1 == n || kk != keys[seg0 + g + 1]) {
+      const double tp = rp, fp = rq;
+      area += (fp - fp_prev) * (tp + tp_prev);
+      if (tp + fp > 0.0) ap += (tp - tp_prev) * (tp / (tp + fp));
+      if (pt_base != nullptr) {
+        pt_fps[ob] = static_cast<float>(fp);
+        pt_tps[ob] = static_cast<float>(tp);
+        pt_thr[ob] = static_cast<T>(KeyOf<T>::value(kk));
+        ++ob;
+      }
+      tp_prev = tp;
+      fp_prev = fp;
+    }
+  }
+  area = wave_sum(area);
+  ap = wave_sum(ap);
+  if ((threadIdx.x & (kWave - 1)) == 0) { red[0][threadIdx.x / kWave] = area; red[1][threadIdx.x / kWave] = ap; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    part[((int64_t)s * Tt + t) * 2] = ((red[0][0] + red[0][1]) + red[0][2]) + red[0][3];
+    part[((int64_t)s * Tt + t) * 2 + 1] = ((red[1][0] + red[1][1]) + red[1][2]) + red[1][3];
+  }
+}
+
+// out[s] = {auroc, ap, P, N}: per-tile partials summed by one 256-thread block per segment in a fixed order (strided
+// per-thread sums, then a fixed pairwise tree): deterministic run to run.
+__global__ void __launch_bounds__(256) rs_final_kernel(const double* __restrict__ part, int Tt, RsScan ps, RsScan qs,
+                                                        const uint32_t* __restrict__ pos_last, const uint32_t* __restrict__ neg_last,
+                                                        double* __restrict__ out) {
+  __shared__ double red[2][256];
+  const int s = blockIdx.x;
+  double area = 0.0, ap = 0.0;
+  for (int t = threadIdx.x; t < Tt; t += 256) {
+    area += part[((int64_t)s * Tt + t) * 2];
+    ap += part[((int64_t)s * Tt + t) * 2 + 1];
+  }
+  red[0][threadIdx.x] = area;
+  red[1][threadIdx.x] = ap;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w) {
+      red[0][threadIdx.x] += red[0][threadIdx.x + w];
+      red[1][threadIdx.x] += red[1][threadIdx.x + w];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x != 0) return;
+  area = red[0][0];
+  ap = red[1][0];
+  const double P = (double)seg_scanned(ps.a, ps.csum, Tt, ps.cps, s, Tt - 1) + pos_last[s];
+  const double N = (double)seg_scanned(qs.a, qs.csum, Tt, qs.cps, s, Tt - 1) + neg_last[s];
+  out[4 * s + 0] = (P > 0 && N > 0) ? area / (2.0 * P * N) : 0.0;
+  out[4 * s + 1] = P > 0 ? ap / P : __longlong_as_double(0x7FF8000000000000ll);
+  out[4 * s + 2] = P;
+  out[4 * s + 3] = N;
+}
+
+__global__ void rs_copy_last_kernel(const uint32_t* __restrict__ a, int Tt, uint32_t* __restrict__ last, int S) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s < S) last[s] = a[(int64_t)s * Tt + Tt - 1];
+}
+
+// --------------------------------------------------------------------------------------------------- host op
+// chunks: score tensors whose element (s, r) is at data + s * stride(0) + r * stride(1) (class-major [S, n_k] views of
+// the curve state's chunks, or row-major [n, S] via .t()); target int64 ([n] multiclass, [n, S] per-element).
+// Returns scores [S, 4] fp64 {auroc, ap, P, N} and, with want_points, (counts [S] int64, fps, tps, thr) of the curve
+// points at every distinct score (descending; ignored-only groups included, dropped by the caller).
+std::vector<at::Tensor> curve_sorted(const std::vector<at::Tensor>& chunks, const at::Tensor& target, int64_t task, int64_t ignore_index,
+                                     bool has_ignore, bool want_points) {
+  TORCH_CHECK(!chunks.empty(), "curve_sorted: no score chunks");
+  const at::ScalarType dt = chunks[0].scalar_type();
+  TORCH_CHECK(dt == at::kFloat || dt == at::kDouble, "curve_sorted: fp32 / fp64 scores");
+  const int S = static_cast<int>(chunks[0].size(0));
+  int64_t n = 0;
+  for (const auto& c : chunks) {
+    TORCH_CHECK(c.dim() == 2 && c.size(0) == S && c.scalar_type() == dt && c.is_cuda(), "curve_sorted: chunks [S, n_k] on the GPU");
+    n += c.size(1);
+  }
+  TORCH_CHECK(target.scalar_type() == at::kLong && target.is_contiguous() && target.numel() == (task == 0 ? n : n * S),
+              "curve_sorted: int64 target [n] (multiclass) or [n, S]");
+  const c10::DeviceGuard guard(chunks[0].device());
+  auto opts = chunks[0].options();
+  auto out = at::zeros({S, 4}, opts.dtype(at::kDouble));
+  if (n == 0 || S == 0) {
+    return {out};
+  }
+  const int Tt = static_cast<int>((n + kRsTile - 1) / kRsTile);
+  TORCH_CHECK((int64_t)Tt <= (int64_t)kScanChunk * 4096 / kRsBins, "curve_sorted: more than 2^25 samples per class");
+  const int64_t L = (int64_t)kRsBins * Tt;
+  const int cps_h = static_cast<int>((L + kScanChunk - 1) / kScanChunk);
+  const int cps_t = (Tt + kScanChunk - 1) / kScanChunk;
+  std::vector<at::Tensor> res;
+  AT_DISPATCH_FLOATING_TYPES(dt, "curve_sorted", [&] {
+    using T = scalar_t;
+    using KT = typename KeyOf<T>::type;
+    const auto kdt = sizeof(KT) == 4 ? at::kInt : at::kLong;
+    auto k0 = at::empty({(int64_t)S * n}, opts.dtype(kdt)), k1 = at::empty({(int64_t)S * n}, opts.dtype(kdt));
+    auto p0 = at::empty({(int64_t)S * n}, opts.dtype(at::kByte)), p1 = at::empty({(int64_t)S * n}, opts.dtype(at::kByte));
+    KT* ka = reinterpret_cast<KT*>(k0.data_ptr());
+    KT* kb = reinterpret_cast<KT*>(k1.data_ptr());
+    uint8_t* pa = p0.data_ptr<uint8_t>();
+    uint8_t* pb = p1.data_ptr<uint8_t>();
+    int64_t off = 0;
+    for (const auto& c : chunks) {
+      const int64_t nk = c.size(1);
+      if (nk > 0) {
+        hipLaunchKernelGGL(rs_prep_kernel<T>, grid_for((int64_t)S * nk, 256, 4096), 256, 0, stream(), c.data_ptr<T>(), c.stride(0),
+                           c.stride(1), nk, off, S, n, target.data_ptr<int64_t>(), static_cast<int>(task), ignore_index, has_ignore, ka, pa);
+        TMX_LAUNCH_CHECK();
+      }
+      off += nk;
+    }
+    auto hist = at::empty({L * S}, opts.dtype(at::kInt));
+    auto csum = at::empty({(int64_t)S * cps_h}, opts.dtype(at::kInt));
+    uint32_t* h = reinterpret_cast<uint32_t*>(hist.data_ptr());
+    uint32_t* cs = reinterpret_cast<uint32_t*>(csum.data_ptr());
+    const int passes = static_cast<int>(sizeof(KT));
+    for (int pss = 0; pss < passes; ++pss) {
+      hipLaunchKernelGGL(rs_hist_kernel<KT>, S * Tt, kRsThreads, 0, stream(), ka, n, Tt, 8 * pss, h);
+      TMX_LAUNCH_CHECK();
+      seg_exclusive_scan(h, S, L, cs, cps_h);
+      hipLaunchKernelGGL(rs_scatter_kernel<KT>, S * Tt, kRsThreads, 0, stream(), ka, pa, kb, pb, n, Tt, 8 * pss, h, cs, L, cps_h);
+      TMX_LAUNCH_CHECK();
+      std::swap(ka, kb);
+      std::swap(pa, pb);
+    }
+    // tile sums -> scans -> fused reduce
+    auto sums = at::empty({3 * (int64_t)S * Tt}, opts.dtype(at::kInt));
+    auto scs = at::empty({3 * (int64_t)S * cps_t}, opts.dtype(at::kInt));
+    auto last = at::empty({2 * (int64_t)S}, opts.dtype(at::kInt));
+    uint32_t* su = reinterpret_cast<uint32_t*>(sums.data_ptr());
+    uint32_t* sc = reinterpret_cast<uint32_t*>(scs.data_ptr());
+    uint32_t* la = reinterpret_cast<uint32_t*>(last.data_ptr());
+    uint32_t *pos_t = su, *neg_t = su + (int64_t)S * Tt, *end_t = su + 2 * (int64_t)S * Tt;
+    hipLaunchKernelGGL(rs_tile_sums_kernel<KT>, S * Tt, kRsThreads, 0, stream(), ka, pa, n, Tt, pos_t, neg_t, end_t);
+    TMX_LAUNCH_CHECK();
+    // the totals need the last tile's own sums (the scan is exclusive)
+    hipLaunchKernelGGL(rs_copy_last_kernel, (S + 255) / 256, 256, 0, stream(), pos_t, Tt, la, S);
+    hipLaunchKernelGGL(rs_copy_last_kernel, (S + 255) / 256, 256, 0, stream(), neg_t, Tt, la + S, S);
+    TMX_LAUNCH_CHECK();
+    at::Tensor ends_total;
+    if (want_points)  // per-segment point counts = sum of the end tile sums (taken before the in-place scan)
+      ends_total = sums.narrow(0, 2 * (int64_t)S * Tt, (int64_t)S * Tt).view({S, Tt}).to(at::kLong).sum(1);
+    seg_exclusive_scan(pos_t, S, Tt, sc, cps_t);
+    seg_exclusive_scan(neg_t, S, Tt, sc + (int64_t)S * cps_t, cps_t);
+    seg_exclusive_scan(end_t, S, Tt, sc + 2 * (int64_t)S * cps_t, cps_t);
+    const RsScan ps{pos_t, sc, cps_t}, qs{neg_t, sc + (int64_t)S * cps_t, cps_t}, es{end_t, sc + 2 * (int64_t)S * cps_t, cps_t};
+    auto part = at::empty({(int64_t)S * Tt * 2}, opts.dtype(at::kDouble));
+    at::Tensor fps, tps, thr, base, counts;
+    float *fp = nullptr, *tp = nullptr;
+    T* th = nullptr;
+    const int64_t* bp = nullptr;
+    if (want_points) {
+      counts = ends_total;
+      base = at::zeros({S}, counts.options());
+      if (S > 1) base.narrow(0, 1, S - 1).copy_(counts.cumsum(0).narrow(0, 0, S - 1));
+      const int64_t total = counts.sum().item<int64_t>();  // one host read sizes the outputs
+      fps = at::empty({total}, opts.dtype(at::kFloat));
+      tps = at::empty({total}, opts.dtype(at::kFloat));
+      thr = at::empty({total}, opts.dtype(dt));
+      fp = fps.data_ptr<float>();
+      tp = tps.data_ptr<float>();
+      th = thr.data_ptr<T>();
+      bp = base.data_ptr<int64_t>();
+    }
+    hipLaunchKernelGGL((rs_reduce_kernel<T, KT>), S * Tt, kRsThreads, 0, stream(), ka, pa, n, Tt, ps, qs, es, part.data_ptr<double>(),
+                       fp, tp, th, bp);
+    TMX_LAUNCH_CHECK();
+    hipLaunchKernelGGL(rs_final_kernel, S, 256, 0, stream(), part.data_ptr<double>(), Tt, ps, qs, la, la + S, out.data_ptr<double>());
+    TMX_LAUNCH_CHECK();
+    res = {out};
+    if (want_points) {
+      res.push_back(counts);
+      res.push_back(fps);
+      res.push_back(tps);
+      res.push_back(thr);
+    }
+  });
+  return res;
+}
+
+}  // namespace tmx
+
+TORCH_LIBRARY_FRAGMENT(tmx, m) {
+  m.def("curve_sorted(Tensor[] chunks, Tensor target, int task, int ignore_index, bool has_ignore, bool want_points) -> Tensor[]");
+}
+
+TORCH_LIBRARY_IMPL(tmx, CUDA, m) { m.impl("curve_sorted", &tmx::curve_sorted); }

@@ -833,7 +833,7 @@ def test_curve_hist_small_classes_vs_aten_softmax(C, dtype):
     assert torch.equal(cm, cm_ref)
 
 
-@pytest.mark.parametrize("C", [2, 10, 64, 200])
+@pytest.mark.parametrize("C", [4, 10, 64, 200])
 def test_curve_small_classes_speculation_and_rare_rows(C):
     """Module path through the small-class route: mode speculation flips (logits <-> probabilities, NaN batches),
     rare NaN / inf rows and ignore_index agree with the CPU implementation."""

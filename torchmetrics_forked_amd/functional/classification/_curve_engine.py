@@ -8,8 +8,10 @@ SURVEY §3.5).  Three state kinds are used here instead:
             (``csrc/classification.hip: curve_hist_update``).  Fixed size -> all-reduced by RCCL instead of
             all-gathered; AUROC / AP for *all* classes come out of one kernel (``curve_hist_reduce``) with no
             per-class loop.  Exact: code order == value order and every distinct score keeps its own bin.
-``samples`` ``(preds [N, C], labels [N, C], valid [N, C])`` for fp32/fp64 scores: all classes are sorted at once
-            (one segmented sort), tie groups are found with one vectorised pass; no per-class loop for AUROC/AP.
+``samples`` ``(preds [N, C], labels [N, C], valid [N, C])`` for fp32/fp64 scores.  On the GPU every class is sorted
+            by the hand-written segmented radix sort with a fused tie-group scan (``csrc/radix.hip``, ``sorted_scores``
+            / ``sorted_curve_points``: AUROC, AP and curve points at any size, no ATen sort); on the CPU all classes
+            are sorted at once with one vectorised tie pass; no per-class loop for AUROC/AP either way.
 ``binned``  the reference's multi-threshold confusion matrix ``[T, C, 2, 2]`` (``binned_curve_update``).
 
 Curve *points* (distinct thresholds with cumulative tps/fps) are produced per class only when a caller asks
@@ -89,6 +91,88 @@ def samples_scores(preds: Tensor, labels: Tensor, valid: Optional[Tensor] = None
     return auroc, ap, P, N
 
 
+# ---------------------------------------------------------------------------------------------------------
+# GPU fp32 / fp64: segmented radix sort + fused scan (csrc/radix.hip)
+# ---------------------------------------------------------------------------------------------------------
+_SORT_MAX_ELEMS = 1 << 31  # keys per launch (classes are processed in groups above this)
+
+
+def _sorted_inputs(preds: Union[Tensor, "ColumnChunks"], target: Tensor, task: str) -> Optional[Tuple[List[Tensor], Tensor, int]]:
+    """(chunks [S, n_k], int64 target, task code) for the radix route, or None (CPU / 16-bit / no native library)."""
+    if isinstance(preds, ColumnChunks):
+        chunks = list(preds.cols)
+    else:
+        if preds.dtype not in (torch.float32, torch.float64):
+            return None
+        p2 = preds.reshape(-1, 1) if task == "binary" else preds
+        chunks = [p2.t()]
+    sample = chunks[0]
+    if not (sample.is_cuda and sample.dtype in (torch.float32, torch.float64) and ops.use_native(sample)):
+        return None
+    t = target.long()
+    if task == "multiclass":
+        return chunks, t.reshape(-1).contiguous(), 0
+    return chunks, t.reshape(chunks[0].shape[1] if task == "binary" else t.shape[0], -1).contiguous(), 1
+
+
+def _class_groups(chunks: List[Tensor]) -> List[Tuple[int, int]]:
+    S = chunks[0].shape[0]
+    n = sum(c.shape[1] for c in chunks)
+    per = max(1, min(S, _SORT_MAX_ELEMS // max(n, 1)))
+    return [(s0, min(S, s0 + per)) for s0 in range(0, S, per)]
+
+
+def _group_target(t: Tensor, code: int, s0: int, s1: int) -> Tensor:
+    """Target of the class group [s0, s1): multiclass ids shifted so class s0 is segment 0; label columns sliced."""
+    if code == 0:
+        return t if s0 == 0 else (t - s0).contiguous()
+    return t if (s0 == 0 and s1 == t.shape[1]) else t[:, s0:s1].contiguous()
+
+
+def sorted_scores(
+    preds: Union[Tensor, "ColumnChunks"], target: Tensor, task: str, ignore_index: Optional[int]
+) -> Optional[Tensor]:
+    """(auroc, ap, P, N) ``[S, 4]`` float64 per class / label from GPU fp32 / fp64 samples, or None off the GPU."""
+    prep = _sorted_inputs(preds, target, task)
+    if prep is None:
+        return None
+    chunks, t, code = prep
+    if chunks[0].shape[1] == 0 and len(chunks) == 1:
+        return None
+    ii = ignore_index if task == "multilabel" else None
+    outs = []
+    for s0, s1 in _class_groups(chunks):
+        outs.append(cls_ops.curve_sorted([c[s0:s1] for c in chunks], _group_target(t, code, s0, s1), code, ii, False)[0])
+    return torch.cat(outs) if len(outs) > 1 else outs[0]
+
+
+def sorted_curve_points(
+    preds: Union[Tensor, "ColumnChunks"], target: Tensor, task: str, ignore_index: Optional[int]
+) -> Optional[List[Tuple[Tensor, Tensor, Tensor]]]:
+    """Per class / label: (fps, tps, thresholds) at every distinct score (descending) from GPU fp32 / fp64 samples."""
+    prep = _sorted_inputs(preds, target, task)
+    if prep is None:
+        return None
+    chunks, t, code = prep
+    ii = ignore_index if task == "multilabel" else None
+    out: List[Tuple[Tensor, Tensor, Tensor]] = []
+    for s0, s1 in _class_groups(chunks):
+        _, counts, fps, tps, thr = cls_ops.curve_sorted([c[s0:s1] for c in chunks], _group_target(t, code, s0, s1), code, ii, True)
+        if ii is not None and fps.numel():
+            # groups made only of ignored samples (kept by the kernel) are not thresholds of the reference
+            seg = torch.repeat_interleave(torch.arange(counts.numel(), device=fps.device), counts, output_size=fps.numel())
+            first = torch.ones_like(seg, dtype=torch.bool)
+            first[1:] = seg[1:] != seg[:-1]
+            prev_f = torch.where(first, torch.zeros_like(fps), fps.roll(1))
+            prev_t = torch.where(first, torch.zeros_like(tps), tps.roll(1))
+            keep = (fps != prev_f) | (tps != prev_t)
+            counts = torch.bincount(seg[keep], minlength=counts.numel())
+            fps, tps, thr = fps[keep], tps[keep], thr[keep]
+        sizes = counts.tolist()
+        out.extend(zip(torch.split(fps, sizes), torch.split(tps, sizes), torch.split(thr, sizes)))
+    return out
+
+
 class ColumnChunks:
     """Samples of a multiclass fp32 curve state kept as the class-major ``[C, n_k]`` buffers the GPU update wrote
     (one per ``update``): ``anchored_scores`` streams them in place; everything else calls ``materialize()``."""
@@ -120,17 +204,19 @@ def anchored_scores(
         C = num
         t = target.reshape(-1).long()
         counts = torch.bincount(t, minlength=C)[:C]
-        pos_rows = torch.sort(t, stable=True)[1]
+        pos_rows = None  # sorted below, only when the anchored route is taken
     else:
         p2 = preds.reshape(-1, 1) if task == "binary" else preds
         lab = (target.reshape(p2.shape) == 1).t()
         C = p2.shape[1]
-        cls_idx, pos_rows = lab.nonzero(as_tuple=True)
-        counts = torch.bincount(cls_idx, minlength=C)
+        counts = lab.sum(1)  # the positions of the positives only when the anchored route is taken (below)
+        pos_rows = None
         preds = p2
     max_pos = int(counts.max()) if counts.numel() else 0
     if max_pos > cls_ops.ANCHOR_MAX_POS:
         return None
+    if pos_rows is None:
+        pos_rows = torch.sort(t, stable=True)[1] if task == "multiclass" else lab.nonzero(as_tuple=True)[1]
     pos_off = torch.zeros(C + 1, dtype=torch.long, device=sample.device)
     pos_off[1:] = counts.cumsum(0)
     if cols is None:

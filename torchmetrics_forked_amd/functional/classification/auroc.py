@@ -111,6 +111,9 @@ def _exact_scores(state: CurveState, task: str, num: int, ignore_index: Optional
     anchored = eng.anchored_scores(preds, target, task, num, ignore_index)
     if anchored is not None:
         return ExactScores.of(anchored[:, 0], anchored[:, 1], anchored[:, 2], anchored[:, 3], cls_ops.curve_summary(anchored))
+    radix = eng.sorted_scores(preds, target, task, ignore_index)  # GPU fp32 / fp64: csrc/radix.hip, no ATen sort
+    if radix is not None:
+        return ExactScores.of(radix[:, 0], radix[:, 1], radix[:, 2], radix[:, 3], cls_ops.curve_summary(radix))
     if isinstance(preds, eng.ColumnChunks):
         preds = preds.materialize()
     if task == "binary":

@@ -272,6 +272,9 @@ def _points(state: CurveState, task: str, num: int, ignore_index: Optional[int])
     if kind == "hist":
         return eng.hist_curve_points(state[1], state[2])
     preds, target = state[1], state[2]
+    radix = eng.sorted_curve_points(preds, target, task, ignore_index)  # GPU fp32 / fp64: csrc/radix.hip
+    if radix is not None:
+        return radix
     if isinstance(preds, eng.ColumnChunks):
         preds = preds.materialize()
     if task == "binary":

@@ -350,6 +350,17 @@ def anchored_scores(cols: List[Tensor], pos_off: Tensor, pos_rows: Tensor, max_p
     return torch.ops.tmx.anchored_curve_scores(cols, pos_off, pos_rows, int(max_pos))
 
 
+def curve_sorted(chunks: List[Tensor], target: Tensor, task: int, ignore_index: Optional[int], want_points: bool) -> List[Tensor]:
+    """fp32 / fp64 curve scores by the hand-written segmented radix sort + fused tie-group scan (csrc/radix.hip).
+
+    ``chunks[k]`` are ``[S, n_k]`` score views (element (s, r) = class / label s of sample r; any strides), ``target``
+    int64: ``[n]`` class ids for ``task`` 0 (multiclass: positive iff target == s) or row-major ``[n, S]`` labels for
+    ``task`` 1 (positive iff == 1).  Returns ``[scores [S, 4] float64 (auroc, ap, P, N)]`` and, with ``want_points``,
+    ``counts [S]``, ``fps``, ``tps`` (float32) and ``thresholds`` (input dtype) of every distinct score, descending."""
+    return list(torch.ops.tmx.curve_sorted(chunks, target, int(task), -1 if ignore_index is None else int(ignore_index),
+                                           ignore_index is not None, bool(want_points)))
+
+
 def softmax_colmajor(rows: Tensor, target: Optional[Tensor] = None, err_flag: Optional[Tensor] = None) -> Tensor:
     """Class-major ``[C, N]`` fp32 probabilities of GPU fp32 rows ``[N, C]`` (C % 4 == 0, C <= 1024): softmax iff any value of the
     batch is outside [0, 1] (the reference's rule), in one pass that also transposes (csrc/curve_anchor.hip).
