@@ -1366,6 +1366,8 @@ void launch_small_two_pass(const T* p, const int64_t* target, int64_t n, int C, 
   // few thousand bins (measured: 238 us at C = 10, 1M rows, for 20 MB of codes).
   int splits = 1;
   while ((int64_t)C * splits < 512 && n_pad / (8 * (splits * 2)) >= 1024) splits *= 2;
+  static const int forced_splits = [] { const char* v = std::getenv("TMX_SMALL_SPLITS"); return v ? std::atoi(v) : 0; }();
+  if (forced_splits > 0) splits = forced_splits;  // experiment knob (tools/mc_small_probe.py sweeps)
   hipLaunchKernelGGL((class_hist_kernel<T, true>), C * splits, kClassThreads, kCodes * sizeof(uint32_t), stream(), cptr, n_pad, splits,
                      hist, p, C, target, n, mode, speculative, srows, state, cm, code_range, speculative ? mode : nullptr);
   TMX_LAUNCH_CHECK();

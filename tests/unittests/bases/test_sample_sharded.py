@@ -1,0 +1,104 @@
+"""Sample-sharded compute (``sharded_compute=True`` under DDP) for Spearman, Kendall and the extrinsic clustering
+metrics (``parallel/sample_sort.py``): gloo world 2 and 3 (one rank without samples) must equal the replicated
+result on the concatenated samples of all ranks, ties across ranks included."""
+import pytest
+import torch
+
+from tests.helpers.multirank import run_multirank
+
+
+def _data(rank, world, n=None, dims=None, kind="float"):
+    sizes = [37, 0, 23] if world == 3 else [41, 29]
+    g = torch.Generator().manual_seed(1234)
+    shape = lambda m: (m,) if dims is None else (m, dims)  # noqa: E731
+    if kind == "float":  # coarse grid -> many ties, spread over ranks
+        parts = [(torch.randint(0, 9, shape(m), generator=g) / 2.0).double() for m in sizes]
+        parts2 = [(torch.randint(0, 7, shape(m), generator=g) / 3.0 + 0.1 * torch.randint(0, 2, shape(m), generator=g)).double() for m in sizes]
+    else:
+        parts = [torch.randint(0, 6, shape(m), generator=g) * 3 for m in sizes]
+        parts2 = [torch.randint(2, 7, shape(m), generator=g) for m in sizes]
+    return parts[rank], parts2[rank], torch.cat(parts), torch.cat(parts2)
+
+
+def _close(a, b, atol=1e-6):
+    torch.testing.assert_close(torch.as_tensor(a).double().cpu(), torch.as_tensor(b).double().cpu(), atol=atol, rtol=0)
+
+
+def check_rank_metrics(rank, world, device):
+    from torchmetrics_forked_amd.functional.regression import kendall_rank_corrcoef, spearman_corrcoef
+    from torchmetrics_forked_amd.parallel.sample_sort import global_average_ranks
+    from torchmetrics_forked_amd.functional.regression.spearman import _rank_data
+    from torchmetrics_forked_amd.regression import KendallRankCorrCoef, SpearmanCorrCoef
+
+    p, t, allp, allt = _data(rank, world)
+    # global ranks of the local values equal the ranks of the full vector at this rank's rows
+    sizes = [37, 0, 23] if world == 3 else [41, 29]
+    lo = sum(sizes[:rank])
+    _close(global_average_ranks(p.to(device)), _rank_data(allp)[lo:lo + p.numel()], atol=0)
+    for dims in (None, 3):
+        p, t, allp, allt = _data(rank, world, dims=dims)
+        nout = 1 if dims is None else dims
+        m = SpearmanCorrCoef(num_outputs=nout, sharded_compute=True).to(device)
+        if p.numel():
+            m.update(p[: p.shape[0] // 2].to(device), t[: p.shape[0] // 2].to(device))
+            m.update(p[p.shape[0] // 2:].to(device), t[p.shape[0] // 2:].to(device))
+        _close(m.compute(), spearman_corrcoef(allp, allt))
+        for variant in ("a", "b", "c"):
+            k = KendallRankCorrCoef(variant=variant, t_test=True, num_outputs=nout, sharded_compute=True).to(device)
+            if p.numel():
+                k.update(p.to(device), t.to(device))
+            tau, pval = k.compute()
+            ref_tau, ref_p = kendall_rank_corrcoef(allp, allt, variant=variant, t_test=True)
+            _close(tau, ref_tau)
+            _close(pval, ref_p)
+            assert not k._is_synced and k._sample_shard is None
+
+
+def check_clustering_metrics(rank, world, device):
+    from torchmetrics_forked_amd import clustering as C
+    from torchmetrics_forked_amd.functional import clustering as F
+
+    p, t, allp, allt = _data(rank, world, kind="int")
+    cases = [
+        (C.MutualInfoScore, F.mutual_info_score, {}),
+        (C.NormalizedMutualInfoScore, F.normalized_mutual_info_score, {"average_method": "geometric"}),
+        (C.AdjustedMutualInfoScore, F.adjusted_mutual_info_score, {"average_method": "max"}),
+        (C.RandScore, F.rand_score, {}),
+        (C.AdjustedRandScore, F.adjusted_rand_score, {}),
+        (C.FowlkesMallowsIndex, F.fowlkes_mallows_index, {}),
+        (C.HomogeneityScore, F.homogeneity_score, {}),
+        (C.CompletenessScore, F.completeness_score, {}),
+        (C.VMeasureScore, F.v_measure_score, {"beta": 2.0}),
+    ]
+    for cls, fn, kw in cases:
+        m = cls(sharded_compute=True, **kw).to(device)
+        if p.numel():
+            m.update(p.to(device), t.to(device))
+        # the sharded path never materialises the gathered samples
+        out = m.compute()
+        _close(out, fn(allp, allt, **kw))
+        assert len(m.preds) <= 1 and (not m.preds or m.preds[0].numel() == p.numel())
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sample_sharded_rank_metrics(world):
+    run_multirank(check_rank_metrics, world, "gloo")
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sample_sharded_clustering(world):
+    run_multirank(check_clustering_metrics, world, "gloo")
+
+
+def test_kendall_cross_range_counting_single_process():
+    """The three-way split of discordant pairs is exact for any assignment of x / y ranges (no process group)."""
+    from torchmetrics_forked_amd.functional.regression.kendall import _count_inversions
+    from torchmetrics_forked_amd.parallel.sample_sort import _greater_in_lower_ranges
+
+    g = torch.Generator().manual_seed(0)
+    y = torch.randint(0, 10, (200,), generator=g).double()
+    xr = torch.randint(0, 4, (200,), generator=g)
+    # brute force: pairs with y_a > y_b and xr_a < xr_b
+    brute = int(((y[:, None] > y[None, :]) & (xr[:, None] < xr[None, :])).sum())
+    assert _greater_in_lower_ranges(y, xr, 4) == brute
+    assert int(_count_inversions(torch.tensor([3.0, 1.0, 2.0]))) == 2

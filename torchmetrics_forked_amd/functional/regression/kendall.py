@@ -103,8 +103,7 @@ def _column_stats(x: Tensor, y: Tensor) -> Tuple[Tensor, ...]:
 
 def _get_metric_metadata(preds: Tensor, target: Tensor, variant: _MetricVariant) -> Tuple:
     cols = [_column_stats(preds[:, i], target[:, i]) for i in range(preds.shape[1])]
-    stack = [torch.stack([torch.as_tensor(c[k], device=preds.device) for c in cols]) for k in range(10)]
-    return tuple(stack) + (torch.full((), preds.shape[0], dtype=torch.long, device=preds.device),)
+    return _stack_column_stats(cols, preds.shape[0], preds.device)
 
 
 def _calculate_tau(con: Tensor, dis: Tensor, n_total: Tensor, ties_x: Tensor, ties_y: Tensor, ux: Tensor, uy: Tensor,
@@ -175,7 +174,18 @@ def _kendall_corrcoef_compute(
 ) -> Tuple[Tensor, Optional[Tensor]]:
     if preds.ndim == 1:
         preds, target = preds.unsqueeze(1), target.unsqueeze(1)
-    con, dis, tx, p1x, p2x, ty, p1y, p2y, ux, uy, n_total = _get_metric_metadata(preds, target, variant)
+    return _kendall_from_metadata(_get_metric_metadata(preds, target, variant), variant, alternative)
+
+
+def _stack_column_stats(cols: List[Tuple], n_total: int, device: torch.device) -> Tuple:
+    stack = [torch.stack([torch.as_tensor(c[k], device=device) for c in cols]) for k in range(10)]
+    return tuple(stack) + (torch.full((), n_total, dtype=torch.long, device=device),)
+
+
+def _kendall_from_metadata(
+    meta: Tuple, variant: _MetricVariant, alternative: Optional[_TestAlternative]
+) -> Tuple[Tensor, Optional[Tensor]]:
+    con, dis, tx, p1x, p2x, ty, p1y, p2y, ux, uy, n_total = meta
     tau = _calculate_tau(con, dis, n_total, tx, ty, ux, uy, variant)
     p_value = (
         _calculate_p_value(con - dis, n_total, tx, p1x, p2x, ty, p1y, p2y, variant, alternative) if alternative else None
