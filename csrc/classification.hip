@@ -1198,13 +1198,14 @@ __global__ void __launch_bounds__(256) curve_hist_mc_kernel(const T* __restrict_
 // ---------------------------------------------------------------------------------------------------------
 constexpr int kSmallRows = 64;
 constexpr int kSmallVpt = 16;
+constexpr int kSmallCmMax = 64;  // LDS-privatised confusion matrix up to 64 x 64 (16 KiB)
 
 template <typename T, int TL, bool FIXUP>
 __global__ void __launch_bounds__(kSmallRows * TL) mc_codes_small_kernel(
     const T* __restrict__ preds, const int64_t* __restrict__ target, int64_t n, int C, int* __restrict__ mode, int64_t ignore_index,
     bool has_ignore, uint16_t* __restrict__ codes, int64_t n_pad, int64_t* __restrict__ confmat, int* __restrict__ err,
     bool record_mode, int* __restrict__ slow_rows, int* __restrict__ slow_count) {
-  extern __shared__ __attribute__((aligned(16))) uint16_t s_small[];  // staging [64][C], then image [C][64]
+  extern __shared__ __attribute__((aligned(16))) uint16_t s_small[];  // staging [64][C], then image [C][64]; cm [C][C]
   int use_mode;
   if constexpr (FIXUP) {
     const int m0 = mode[0], m1 = mode[1];
@@ -1213,7 +1214,16 @@ __global__ void __launch_bounds__(kSmallRows * TL) mc_codes_small_kernel(
   } else {
     use_mode = mode[0];
   }
-  const int64_t r0 = (int64_t)blockIdx.x * kSmallRows;
+  // C <= 64: the confusion matrix is privatised in LDS (at C = 2 every row's atomic hit one of 4 global words)
+  uint32_t* s_cm = reinterpret_cast<uint32_t*>(s_small + kSmallRows * C);
+  const bool lds_cm = !FIXUP && confmat != nullptr && C <= kSmallCmMax;
+  if (lds_cm)
+    for (int i = threadIdx.x; i < C * C; i += kSmallRows * TL) s_cm[i] = 0u;
+  const int64_t ntiles = n_pad / kSmallRows;
+  bool bad = false;
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+  __syncthreads();  // previous tile's class segments were read from the image
+  const int64_t r0 = tile * kSmallRows;
   const int rows = static_cast<int>(min<int64_t>(kSmallRows, n - r0));
   // 1. stage the block's scores (byte range [r0 C, (r0 + rows) C) x 2; r0 C x 2 is a multiple of 128 B)
   {
@@ -1301,7 +1311,10 @@ __global__ void __launch_bounds__(kSmallRows * TL) mc_codes_small_kernel(
   }
   if (q == 0 && in_rows) {
     if constexpr (!FIXUP) {
-      if (confmat != nullptr && keep && t >= 0 && t < C && am < C) atomic_add_i64(confmat + t * C + am, 1);
+      if (confmat != nullptr && keep && t >= 0 && t < C && am < C) {
+        if (lds_cm) atomicAdd(s_cm + t * C + am, 1u);
+        else atomic_add_i64(confmat + t * C + am, 1);
+      }
       if (err != nullptr && valid && (t < 0 || t >= C)) atomicOr(err, 1);
     }
     if (slow) {
@@ -1309,13 +1322,18 @@ __global__ void __launch_bounds__(kSmallRows * TL) mc_codes_small_kernel(
       slow_rows[list * n + atomicAdd(slow_count + list, 1)] = static_cast<int>(r);
     }
   }
-  bool bad = false;
-  if (!FIXUP && record_mode && q == 0) bad = slow || (valid && (mx > 1.f || mn < 0.f));
+  if (!FIXUP && record_mode && q == 0) bad = bad || slow || (valid && (mx > 1.f || mn < 0.f));
   __syncthreads();
   // class segments: C rows of 64 codes = 8 x 16 B each
   for (int i = threadIdx.x; i < C * 8; i += kSmallRows * TL) {
     const int c = i >> 3, k = i & 7;
     reinterpret_cast<uint4*>(codes + (int64_t)c * n_pad + r0)[k] = reinterpret_cast<const uint4*>(s_small + c * kSmallRows)[k];
+  }
+  }  // tiles
+  if (lds_cm) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < C * C; i += kSmallRows * TL)
+      if (s_cm[i]) atomic_add_i64(confmat + i, s_cm[i]);
   }
   if constexpr (!FIXUP) {
     if (record_mode && __syncthreads_or(bad) && threadIdx.x == 0 &&
@@ -1327,8 +1345,8 @@ __global__ void __launch_bounds__(kSmallRows * TL) mc_codes_small_kernel(
 template <typename T, bool FIXUP>
 void launch_small_rows(int TL, int grid, const T* p, const int64_t* target, int64_t n, int C, int* mode, int64_t ignore_index, bool has_ignore,
                        uint16_t* codes, int64_t n_pad, int64_t* cm, int* err, bool rec, int* srows, int* scount) {
-  const size_t shm = (size_t)kSmallRows * C * sizeof(uint16_t);
-#define TMX_SMALL_CASE(TLV)                                                                                                      \
+  const size_t shm = (size_t)kSmallRows * C * sizeof(uint16_t) + (C <= kSmallCmMax ? (size_t)C * C * sizeof(uint32_t) : 0);
+#define TMX_SMALL_CASE(TLV)                                                                                                     \
   case TLV:                                                                                                                      \
     hipLaunchKernelGGL((mc_codes_small_kernel<T, TLV, FIXUP>), grid, kSmallRows * TLV, shm, stream(), p, target, n, C, mode,   \
                        ignore_index, has_ignore, codes, n_pad, cm, err, rec, srows, scount);                                      \
@@ -1349,9 +1367,11 @@ void launch_small_two_pass(const T* p, const int64_t* target, int64_t n, int C, 
                            int* code_range) {
   TORCH_CHECK(n < (int64_t{1} << 31), "curve_hist_update: more than 2^31 rows in one batch");
   const int64_t n_pad = (n + kSmallRows - 1) / kSmallRows * kSmallRows;
-  const int grid = static_cast<int>(n_pad / kSmallRows);
+  const int64_t ntiles = n_pad / kSmallRows;
   int TL = 1;
   while (TL * kSmallVpt < C) TL *= 2;
+  // a block loops over 64-row tiles: ~16 waves per CU in flight, and one LDS confusion-matrix flush per block
+  const int grid = static_cast<int>(std::min<int64_t>(ntiles, std::max(256, 8192 / TL)));
   auto codes = at::empty({(int64_t)C * n_pad}, opts.dtype(at::kShort));
   auto slow_rows = at::empty({2 * n}, opts.dtype(at::kInt));
   uint16_t* cptr = reinterpret_cast<uint16_t*>(codes.data_ptr());
@@ -1360,16 +1380,24 @@ void launch_small_two_pass(const T* p, const int64_t* target, int64_t n, int C, 
   if (speculative)
     launch_small_rows<T, true>(TL, std::min(grid, 1024), p, target, n, C, mode, ignore_index, has_ignore, cptr, n_pad, cm, err, false,
                                srows, state);
-  // the class pass reads n_pad as a multiple of 8 rows (uint4) and ld = C (unpadded rows).  With few classes a large
-  // share of the codes are positives (1 / C): the packed LDS layout (negatives low / positives high half of one
-  // word) keeps them out of global int64 atomics, which every row split of a class would otherwise hit on the same
-  // few thousand bins (measured: 238 us at C = 10, 1M rows, for 20 MB of codes).
-  int splits = 1;
-  while ((int64_t)C * splits < 512 && n_pad / (8 * (splits * 2)) >= 1024) splits *= 2;
+  // Class pass: packed LDS histogram per (class, row split) — with few classes 1 / C of the codes are positives —
+  // and a partial flush (plain stores of the occupied range, then one reduce launch) instead of global int64 atomics:
+  // every split of a class hits the same few thousand bins.  Splits: enough (class, split) blocks to fill the chip,
+  // at least ~8k rows per block (the flush writes up to the occupied range, ~4k words for softmax scores), and at most
+  // kClassChunk rows per block so the 16-bit halves never need a mid-stream flush.
+  const int64_t nv = n_pad / 8;
+  int splits = static_cast<int>(std::max<int64_t>(1, (nv + kClassChunk / 8 - 1) / (kClassChunk / 8)));
+  while ((int64_t)C * splits < 1024 && nv / (splits * 2) >= 1024) splits *= 2;
   static const int forced_splits = [] { const char* v = std::getenv("TMX_SMALL_SPLITS"); return v ? std::atoi(v) : 0; }();
   if (forced_splits > 0) splits = forced_splits;  // experiment knob (tools/mc_small_probe.py sweeps)
-  hipLaunchKernelGGL((class_hist_kernel<T, true>), C * splits, kClassThreads, kCodes * sizeof(uint32_t), stream(), cptr, n_pad, splits,
-                     hist, p, C, target, n, mode, speculative, srows, state, cm, code_range, speculative ? mode : nullptr);
+  auto partial = at::empty({(int64_t)C * splits * kCodes}, opts.dtype(at::kInt));
+  auto prange = at::empty({(int64_t)C * splits * 2}, opts.dtype(at::kInt));
+  uint32_t* pp = reinterpret_cast<uint32_t*>(partial.data_ptr<int>());
+  hipLaunchKernelGGL((class_hist_partial_kernel<T>), C * splits, kClassThreads, kCodes * sizeof(uint32_t), stream(), cptr, n_pad, splits,
+                     hist, p, C, target, n, mode, speculative, srows, state, cm, code_range, speculative ? mode : nullptr, pp,
+                     prange.data_ptr<int>());
+  TMX_LAUNCH_CHECK();
+  hipLaunchKernelGGL(class_partial_reduce_kernel, dim3(kCodes / 256, C), 256, 0, stream(), pp, prange.data_ptr<int>(), splits, hist);
   TMX_LAUNCH_CHECK();
 }
 

@@ -636,12 +636,49 @@ __device__ __forceinline__ void class_flush(uint32_t* __restrict__ s_h, int64_t*
   }
 }
 
+// Partial flush (small-class route): the block's occupied LDS range [blo, bhi] goes to its own slice of a scratch
+// [C][splits][kCodes] with plain coalesced stores and the range to ``prange``; class_partial_reduce_kernel then sums
+// the splits per bin.  With few classes every split of a class hits the same few thousand bins, and a global int64
+// atomic per (split, bin) was the class pass's cost (C = 10, 1M rows: 640 blocks x ~4k bins).
+template <int NT>
+__device__ __forceinline__ void class_store_partial(const uint32_t* __restrict__ s_h, uint32_t* __restrict__ out,
+                                                    int* __restrict__ range, int& lo, int& hi) {
+  __shared__ int s_rng[2];
+  if (threadIdx.x == 0) {
+    s_rng[0] = kCodes;
+    s_rng[1] = -1;
+  }
+  __syncthreads();
+  int tlo = kCodes, thi = -1;
+  for (int i = threadIdx.x; i < kCodes; i += NT)
+    if (s_h[i]) {
+      tlo = min(tlo, i);
+      thi = max(thi, i);
+    }
+  tlo = wave_min_i32(tlo);
+  thi = wave_max_i32(thi);
+  if ((threadIdx.x & (kWave - 1)) == 0 && thi >= 0) {
+    atomicMin(&s_rng[0], tlo);
+    atomicMax(&s_rng[1], thi);
+  }
+  __syncthreads();
+  const int blo = s_rng[0], bhi = s_rng[1];
+  for (int i = blo + static_cast<int>(threadIdx.x); i <= bhi; i += NT) out[i] = s_h[i];
+  if (threadIdx.x == 0) {
+    range[0] = blo;
+    range[1] = bhi;
+  }
+  lo = min(lo, blo);
+  hi = max(hi, bhi);
+}
+
 template <typename T, bool PACKED, int NT>
 __device__ __forceinline__ void class_hist_block(int64_t vb, int64_t vgrid, const uint16_t* __restrict__ codes, int64_t n_pad, int splits,
                                                  int64_t* __restrict__ hist, const T* __restrict__ preds, int ld,
                                                  const int64_t* __restrict__ target, int64_t n, const int* __restrict__ bmode,
                                                  bool speculative, const int* __restrict__ slow_rows, int* __restrict__ state,
-                                                 int64_t* __restrict__ confmat, int* __restrict__ code_range, int* __restrict__ roll_mode) {
+                                                 int64_t* __restrict__ confmat, int* __restrict__ code_range, int* __restrict__ roll_mode,
+                                                 uint32_t* __restrict__ partial = nullptr, int* __restrict__ prange = nullptr) {
   extern __shared__ __attribute__((aligned(16))) uint32_t s_h[];  // [kCodes]: neg, or neg (lo 16) | pos (hi 16)
   __shared__ int s_info[4];
   int lo = kCodes, hi = -1;  // occupied code range this thread touched (compute() then scans only that range)
@@ -734,7 +771,8 @@ __device__ __forceinline__ void class_hist_block(int64_t vb, int64_t vgrid, cons
   }
   __syncthreads();
   // rare-row codes went to the int64 bins by atomics: then the last flush must be atomic too
-  class_flush<PACKED, NT>(s_h, neg_hist, pos_hist, exclusive && n0 + n1 == 0, lo, hi);
+  if (partial != nullptr) class_store_partial<NT>(s_h, partial + vb * kCodes, prange + 2 * vb, lo, hi);
+  else class_flush<PACKED, NT>(s_h, neg_hist, pos_hist, exclusive && n0 + n1 == 0, lo, hi);
   if (code_range != nullptr) {  // per-class running range [C][2]: one min / max per wave, no block barrier
     lo = wave_min_i32(lo);
     hi = wave_max_i32(hi);
@@ -769,6 +807,37 @@ __global__ void __launch_bounds__(kClassThreads) class_hist_kernel(const uint16_
                                                                    int* __restrict__ roll_mode) {
   class_hist_block<T, PACKED, kClassThreads>(blockIdx.x, gridDim.x, codes, n_pad, splits, hist, preds, ld, target, n, bmode, speculative,
                                              slow_rows, state, confmat, code_range, roll_mode);
+}
+
+// Small-class class pass: packed LDS histogram per (class, split), partial flush (class_store_partial).
+template <typename T>
+__global__ void __launch_bounds__(kClassThreads) class_hist_partial_kernel(
+    const uint16_t* __restrict__ codes, int64_t n_pad, int splits, int64_t* __restrict__ hist, const T* __restrict__ preds, int ld,
+    const int64_t* __restrict__ target, int64_t n, const int* __restrict__ bmode, bool speculative, const int* __restrict__ slow_rows,
+    int* __restrict__ state, int64_t* __restrict__ confmat, int* __restrict__ code_range, int* __restrict__ roll_mode,
+    uint32_t* __restrict__ partial, int* __restrict__ prange) {
+  class_hist_block<T, true, kClassThreads>(blockIdx.x, gridDim.x, codes, n_pad, splits, hist, preds, ld, target, n, bmode, speculative,
+                                           slow_rows, state, confmat, code_range, roll_mode, partial, prange);
+}
+
+// Sum of the splits' partial packed words per (class, bin) into the int64 histogram: one owner thread per bin, so a
+// plain read-modify-write; splits whose range misses the bin are not read.
+__global__ void __launch_bounds__(256) class_partial_reduce_kernel(const uint32_t* __restrict__ partial, const int* __restrict__ prange,
+                                                                   int splits, int64_t* __restrict__ hist) {
+  const int c = blockIdx.y;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  uint64_t neg = 0, pos = 0;
+  for (int s = 0; s < splits; ++s) {
+    const int64_t b = (int64_t)c * splits + s;
+    const int lo = prange[2 * b], hi = prange[2 * b + 1];
+    if (i >= lo && i <= hi) {
+      const uint32_t w = partial[b * kCodes + i];
+      neg += w & 0xFFFFu;
+      pos += w >> 16;
+    }
+  }
+  if (neg) hist[(int64_t)c * 2 * kCodes + i] += static_cast<int64_t>(neg);
+  if (pos) hist[((int64_t)c * 2 + 1) * kCodes + i] += static_cast<int64_t>(pos);
 }
 
 // Dual-role launch: the row pass of batch k and the class pass of batch k - 1 (the other scratch buffer) in ONE grid,

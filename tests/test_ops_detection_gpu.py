@@ -97,6 +97,80 @@ def test_map_segm_gpu_matches_cpu():
         torch.testing.assert_close(a[k].cpu(), c[k], atol=1e-6, rtol=0, msg=k)
 
 
+def _box_masks(k, h, w, g):
+    """Rectangle masks (realistic run counts) plus the corner cases of the encoder: all / none / first pixel."""
+    x0 = torch.randint(0, w, (k, 1, 1), generator=g)
+    y0 = torch.randint(0, h, (k, 1, 1), generator=g)
+    x1 = x0 + torch.randint(1, w, (k, 1, 1), generator=g)
+    y1 = y0 + torch.randint(1, h, (k, 1, 1), generator=g)
+    yy = torch.arange(h).view(1, h, 1)
+    xx = torch.arange(w).view(1, 1, w)
+    m = (yy >= y0) & (yy < y1) & (xx >= x0) & (xx < x1)
+    if k > 3:
+        m[0] = True
+        m[1] = False
+        m[2] = torch.rand(h, w, generator=g) > 0.5
+        m[3, 0, 0] = True
+    return m
+
+
+@pytest.mark.parametrize("h,w", [(1, 1), (37, 23), (64, 64), (100, 190), (257, 129)])
+def test_rle_encode_decode_gpu_matches_cpu(h, w):
+    """csrc/rle.hip encode (change words, positions, COCO strings) and decode bits are byte-identical to the CPU ops."""
+    g = torch.Generator().manual_seed(h * 7 + w)
+    m = _box_masks(9, h, w, g)
+    cg, og = torch.ops.tmx.rle_encode(m.cuda())
+    cc, oc = torch.ops.tmx.rle_encode(m)
+    assert torch.equal(og, oc) and torch.equal(cg, cc)
+    bg, ag = torch.ops.tmx.rle_decode_bits(cc.cuda(), oc.cuda(), h, w)
+    bc, ac = torch.ops.tmx.rle_decode_bits(cc, oc, h, w)
+    assert torch.equal(bg.cpu(), bc) and torch.equal(ag.cpu(), ac)
+
+
+def test_mask_iou_tiles_gpu_matches_cpu_and_dense():
+    from torchmetrics_forked_amd.detection._mask_utils import encode_mask_batch, mask_iou, rle_segm_ious
+
+    g = torch.Generator().manual_seed(3)
+    imgs = [(_box_masks(int(torch.randint(0, 40, (1,), generator=g)), 96, 80, g),
+             _box_masks(int(torch.randint(0, 30, (1,), generator=g)), 96, 80, g)) for _ in range(12)]
+    crowd = [torch.randint(0, 2, (gm.shape[0],), generator=g) for _, gm in imgs]
+    det = encode_mask_batch([d.cuda() for d, _ in imgs])
+    gt = encode_mask_batch([gm.cuda() for _, gm in imgs])
+    assert det == encode_mask_batch([d for d, _ in imgs])
+    on_gpu = rle_segm_ious(det, gt, crowd, torch.device("cuda"))
+    on_cpu = rle_segm_ious(det, gt, crowd, torch.device("cpu"))
+    for a, b in zip(on_gpu, on_cpu):
+        assert torch.equal(a.cpu(), b)
+    pos = 0
+    for i, (d, gm) in enumerate(imgs):
+        if d.shape[0] and gm.shape[0]:
+            ref = mask_iou(d, gm, crowd[i]).reshape(-1)
+            assert torch.equal(on_cpu[0][pos:pos + ref.numel()], ref)
+            pos += ref.numel()
+
+
+def test_map_segm_rle_device_path_equals_host_evaluator():
+    """Segm mAP with RLE states on the device (one decode + one IoU launch per mask size) equals the host evaluator."""
+    from torchmetrics_forked_amd.detection import MeanAveragePrecision
+
+    g = torch.Generator().manual_seed(11)
+    preds, target = [], []
+    for _ in range(24):
+        ng = int(torch.randint(1, 8, (1,), generator=g))
+        gm = _box_masks(ng, 128, 96, g)
+        dm = torch.cat([gm, _box_masks(3, 128, 96, g)]) ^ (torch.rand(ng + 3, 128, 96, generator=g) > 0.97)
+        target.append({"masks": gm, "labels": torch.randint(0, 3, (ng,), generator=g), "iscrowd": torch.randint(0, 2, (ng,), generator=g) * (torch.rand(ng, generator=g) > 0.8)})
+        preds.append({"masks": dm, "scores": torch.rand(ng + 3, generator=g), "labels": torch.randint(0, 3, (ng + 3,), generator=g)})
+    gpu = MeanAveragePrecision(iou_type="segm", class_metrics=True).cuda()
+    gpu.update(*_to((preds, target), "cuda"))
+    cpu = MeanAveragePrecision(iou_type="segm", class_metrics=True)
+    cpu.update(preds, target)
+    assert gpu.detection_mask == cpu.detection_mask
+    a, c = gpu.compute(), cpu.compute()
+    for k in c:
+        assert torch.equal(a[k].cpu(), c[k]), k
+
+
 def _coco_inputs(seed, n_img, n_cls, max_det_img, max_gt_img, tie_scores):
     """Flat COCO evaluator inputs with crowds, zero/huge areas, score ties and >100 detections in some pairs."""
     g = torch.Generator().manual_seed(seed)

@@ -7,7 +7,7 @@
 * ``mask_iou``: pairwise mask IoU.  On GPU masks are bit-packed 64 pixels per word and intersected with the
   ``tmx::mask_iou`` popcount kernel; on CPU a float matmul of the flattened masks (exact integer counts).
 """
-from typing import Any, Dict, List, Sequence, Union
+from typing import Any, Dict, List, Sequence, Tuple, Union
 
 import math
 
@@ -98,6 +98,133 @@ def rle_decode(rle: Dict[str, Any]) -> np.ndarray:
 
 def rle_area(rle: Dict[str, Any]) -> int:
     return int(sum(_rle_counts(rle)[1::2]))
+
+
+RleState = Tuple[Tuple[int, int], bytes]  # the reference's per-mask state entry: ((H, W), compressed counts)
+
+
+def encode_mask_batch(masks: Sequence[Tensor]) -> List[Tuple[RleState, ...]]:
+    """Per image ``[K_i, H, W]`` masks -> per image tuple of ``((H, W), counts)`` (the reference's segm state,
+    ``mean_ap.py:811-816``).  Images sharing (device, H, W) are encoded by ONE ``tmx::rle_encode`` call (the GPU
+    kernels when the masks live there; only the strings come back to the host)."""
+    out: List[Tuple[RleState, ...]] = [()] * len(masks)
+    groups: Dict[Tuple[Any, int, int], List[int]] = {}
+    for i, m in enumerate(masks):
+        if m.numel() == 0 or m.shape[0] == 0:
+            continue
+        groups.setdefault((m.device, int(m.shape[-2]), int(m.shape[-1])), []).append(i)
+    native = ops.load()
+    for (dev, h, w), idx in groups.items():
+        if native and (dev.type == "cpu" or ops.use_native(masks[idx[0]])):
+            stack = torch.cat([masks[i].reshape(-1, h, w) for i in idx]) if len(idx) > 1 else masks[idx[0]].reshape(-1, h, w)
+            chars, off = torch.ops.tmx.rle_encode(stack)
+            buf, o = chars.numpy().tobytes(), off.tolist()
+            k = 0
+            for i in idx:
+                n = int(masks[i].shape[0])
+                out[i] = tuple(((h, w), buf[o[k + j]:o[k + j + 1]]) for j in range(n))
+                k += n
+        else:
+            for i in idx:
+                out[i] = tuple(((h, w), rle_encode(m)["counts"].encode("ascii")) for m in masks[i])
+    return out
+
+
+def rle_state_area(entry: RleState) -> int:
+    return rle_area({"size": list(entry[0]), "counts": entry[1]})
+
+
+def _tiles(d_sizes: Sequence[int], g_sizes: Sequence[int], tile: int = 16) -> np.ndarray:
+    """[T, 3] int32 (image, d0, g0) covering every image's [D_i, G_i] IoU block with tile x tile tiles."""
+    d = np.asarray(d_sizes, dtype=np.int64)
+    g = np.asarray(g_sizes, dtype=np.int64)
+    nd, ng = (d + tile - 1) // tile, (g + tile - 1) // tile
+    per = nd * ng
+    img = np.repeat(np.arange(len(d)), per)
+    if img.size == 0:
+        return np.zeros((0, 3), dtype=np.int32)
+    first = np.repeat(np.cumsum(per) - per, per)
+    local = np.arange(img.size) - first
+    ngi = ng[img]
+    return np.stack([img, (local // ngi) * tile, (local % ngi) * tile], axis=1).astype(np.int32)
+
+
+def rle_segm_ious(
+    det: Sequence[Tuple[RleState, ...]], gt: Sequence[Tuple[RleState, ...]], gt_crowd: Sequence[Tensor], device: torch.device,
+    max_bits_bytes: int = 1 << 31,
+) -> Tuple[Tensor, Tensor, Tensor, Tensor]:
+    """Mask IoU blocks of every image from the RLE states (the reference's COCOeval ``computeIoU`` for segm).
+
+    Returns ``(ious, offsets, det_area, gt_area)``: image i's ``[D_i, G_i]`` IoU block (fp64, crowd ground truth
+    divides by the detection area) starts at ``offsets[i]`` of the flat ``ious`` (empty when D_i or G_i is 0), and
+    the mask areas of every detection / ground truth in image-major order.  Strings are decoded to bit-packed masks
+    on ``device`` (``tmx::rle_decode_bits``) for image chunks of at most ``max_bits_bytes``, and every chunk's IoU
+    tiles run in ONE ``tmx::mask_iou_tiles`` launch."""
+    n_img = len(gt)
+    d_sizes = [len(det[i]) if i < len(det) else 0 for i in range(n_img)]
+    g_sizes = [len(t) for t in gt]
+    blk = [d * g for d, g in zip(d_sizes, g_sizes)]
+    offsets = np.concatenate([[0], np.cumsum(blk)[:-1]]).astype(np.int64) if n_img else np.zeros(0, dtype=np.int64)
+    total = int(sum(blk))
+    ious = torch.zeros(total, dtype=torch.float64, device=device)
+    det_first = np.concatenate([[0], np.cumsum(d_sizes)]).astype(np.int64)
+    gt_first = np.concatenate([[0], np.cumsum(g_sizes)]).astype(np.int64)
+    det_area = torch.zeros(int(det_first[-1]), dtype=torch.float64, device=device)
+    gt_area = torch.zeros(int(gt_first[-1]), dtype=torch.float64, device=device)
+    crowd_all = [c.reshape(-1).to(torch.bool).cpu() for c in gt_crowd]
+    # images grouped by mask size (all of an image's masks share it), then chunked by decoded-bits bytes
+    by_size: Dict[Tuple[int, int], List[int]] = {}
+    for i in range(n_img):
+        e = (det[i][0] if d_sizes[i] else gt[i][0] if g_sizes[i] else None)
+        if e is not None:
+            by_size.setdefault((int(e[0][0]), int(e[0][1])), []).append(i)
+    for (h, w), imgs in by_size.items():
+        words = (h * w + 63) // 64
+        chunk: List[int] = []
+        masks_in_chunk = 0
+        for pos, i in enumerate(imgs + [None]):  # type: ignore[list-item]
+            if i is not None and (not chunk or (masks_in_chunk + d_sizes[i] + g_sizes[i]) * words * 8 <= max_bits_bytes):
+                chunk.append(i)
+                masks_in_chunk += d_sizes[i] + g_sizes[i]
+                continue
+            _iou_chunk(chunk, det, gt, d_sizes, g_sizes, crowd_all, offsets, det_first, gt_first, h, w, device, ious, det_area, gt_area)
+            chunk, masks_in_chunk = ([i], d_sizes[i] + g_sizes[i]) if i is not None else ([], 0)
+    return ious, torch.as_tensor(offsets, device=device), det_area, gt_area
+
+
+def _decode(entries: List[RleState], h: int, w: int, device: torch.device) -> Tuple[Tensor, Tensor]:
+    lens = np.fromiter((len(e[1]) for e in entries), dtype=np.int64, count=len(entries))
+    off = torch.from_numpy(np.concatenate([[0], np.cumsum(lens)]).astype(np.int64))
+    raw = b"".join(e[1] for e in entries)
+    chars = torch.frombuffer(bytearray(raw), dtype=torch.uint8) if raw else torch.zeros(0, dtype=torch.uint8)
+    return torch.ops.tmx.rle_decode_bits(chars.to(device), off.to(device), h, w)
+
+
+def _iou_chunk(chunk, det, gt, d_sizes, g_sizes, crowd_all, offsets, det_first, gt_first, h, w, device, ious, det_area, gt_area):
+    if not chunk:
+        return
+    d_entries = [e for i in chunk for e in det[i]]
+    g_entries = [e for i in chunk for e in gt[i]]
+    dbits, darea = _decode(d_entries, h, w, device)
+    gbits, garea = _decode(g_entries, h, w, device)
+    dsz = [d_sizes[i] for i in chunk]
+    gsz = [g_sizes[i] for i in chunk]
+    d_rows = torch.as_tensor(np.concatenate([np.arange(det_first[i], det_first[i] + d_sizes[i]) for i in chunk]), device=device)
+    g_rows = torch.as_tensor(np.concatenate([np.arange(gt_first[i], gt_first[i] + g_sizes[i]) for i in chunk]), device=device)
+    det_area[d_rows] = darea
+    gt_area[g_rows] = garea
+    tiles = _tiles(dsz, gsz)
+    if tiles.shape[0] == 0:
+        return
+    crowd = torch.cat([crowd_all[i] for i in chunk]) if chunk else torch.zeros(0, dtype=torch.bool)
+    det_off = torch.as_tensor(np.concatenate([[0], np.cumsum(dsz)]), dtype=torch.long)
+    gt_off = torch.as_tensor(np.concatenate([[0], np.cumsum(gsz)]), dtype=torch.long)
+    out_off = torch.as_tensor(offsets[chunk], dtype=torch.long)
+    part = torch.ops.tmx.mask_iou_tiles(
+        dbits, gbits, darea, garea, crowd.to(device), det_off.to(device), gt_off.to(device), out_off.to(device),
+        torch.from_numpy(tiles).to(device), ious.numel(),
+    )
+    ious.add_(part)
 
 
 # ------------------------------------------------------------------------------------------------------------

@@ -4,8 +4,10 @@ Same constructor, states (nine ``None``-reduced per-image lists), output keys an
 reference, but no COCO JSON round trip and no pycocotools: ``compute`` flattens the per-image lists into one
 row per box and hands them to the native evaluator ``tmx::coco_evaluate`` (C++ evaluateImg + accumulate,
 parallel over categories; csrc/coco_eval.cpp).  Segmentation IoUs are computed on the metric's device with the
-bit-packed popcount kernel (``tmx::mask_iou``) and passed in as per-image matrices.  Masks are kept as binary
-tensors (not RLE tuples), so they sync through the same packed all-gather as every other state.
+IoU kernel and passed in as per-image matrices.  Masks are stored as the reference stores them — per image a tuple
+of ``((H, W), counts)`` COCO RLE entries (``mean_ap.py:811-816``) — but encoded by the GPU kernels of
+``csrc/rle.hip`` (one launch group per update batch; only the strings reach the host), and segm IoUs of all images
+come from one decode + one tiled popcount launch per mask size (``_mask_utils.rle_segm_ious``).
 
 ``backend`` only selects the summary convention: ``"pycocotools"`` evaluates ``map`` (stats[0]) at
 ``maxDets == 100`` (``-1`` when 100 is not among ``max_detection_thresholds``, as the official tool does),
@@ -23,7 +25,12 @@ import torch
 from torch import Tensor
 
 from torchmetrics_forked_amd import ops
-from torchmetrics_forked_amd.detection._mask_utils import mask_iou, rle_area, rle_encode, segmentation_to_mask
+from torchmetrics_forked_amd.detection._mask_utils import (
+    encode_mask_batch,
+    rle_segm_ious,
+    rle_state_area,
+    segmentation_to_mask,
+)
 from torchmetrics_forked_amd.detection.helpers import _fix_empty_tensors, _input_validator, _validate_iou_type_arg
 from torchmetrics_forked_amd.functional.detection._box_ops import box_convert
 from torchmetrics_forked_amd.metric import Metric
@@ -57,11 +64,11 @@ class MeanAveragePrecision(Metric):
     plot_upper_bound: float = 1.0
 
     detection_box: List[Tensor]
-    detection_mask: List[Tensor]
+    detection_mask: List[Tuple[Tuple[Tuple[int, int], bytes], ...]]
     detection_scores: List[Tensor]
     detection_labels: List[Tensor]
     groundtruth_box: List[Tensor]
-    groundtruth_mask: List[Tensor]
+    groundtruth_mask: List[Tuple[Tuple[Tuple[int, int], bytes], ...]]
     groundtruth_labels: List[Tensor]
     groundtruth_crowds: List[Tensor]
     groundtruth_area: List[Tensor]
@@ -141,21 +148,17 @@ class MeanAveragePrecision(Metric):
             self.detection_box.extend(det_boxes)
             self.groundtruth_box.extend(self._convert_boxes([item["boxes"] for item in target]))
         if "segm" in self.iou_type:
-            det_masks = [self._as_mask(item["masks"]) for item in preds]
+            det_masks = encode_mask_batch([item["masks"] for item in preds])
             if self.warn_on_many_detections and "bbox" not in self.iou_type and any(len(m) > limit for m in det_masks):
                 _warning_on_too_many_detections(limit)
             self.detection_mask.extend(det_masks)
-            self.groundtruth_mask.extend(self._as_mask(item["masks"]) for item in target)
+            self.groundtruth_mask.extend(encode_mask_batch([item["masks"] for item in target]))
         self.detection_labels.extend(item["labels"] for item in preds)
         self.detection_scores.extend(item["scores"] for item in preds)
         labels = [item["labels"] for item in target]
         self.groundtruth_labels.extend(labels)
         self.groundtruth_crowds.extend(self._optional_column(target, "iscrowd", labels))
         self.groundtruth_area.extend(self._optional_column(target, "area", labels))
-
-    @staticmethod
-    def _as_mask(masks: Tensor) -> Tensor:
-        return masks.reshape(0, 0, 0) if masks.numel() == 0 else masks.to(torch.bool)
 
     def _convert_boxes(self, boxes: List[Tensor]) -> List[Tensor]:
         """Per-image ``xywh`` boxes; one conversion kernel for the whole batch when the images share device/dtype."""
@@ -235,6 +238,16 @@ class MeanAveragePrecision(Metric):
                     raise
         return self._evaluate_host(i_type, average, classes)
 
+    _segm_cache: Optional[Tuple[str, Tuple[Tensor, ...]]] = None
+
+    def _segm(self, dev: torch.device) -> Tuple[Tensor, ...]:
+        """(flat IoU blocks, per-image offsets, detection mask areas, ground-truth mask areas) from the RLE states,
+        computed once per ``compute`` (bbox + segm and class_metrics evaluations reuse it)."""
+        key = str(dev)
+        if self._segm_cache is None or self._segm_cache[0] != key:
+            self._segm_cache = (key, rle_segm_ious(self.detection_mask, self.groundtruth_mask, self.groundtruth_crowds, dev))
+        return self._segm_cache[1]
+
     def _evaluate_gpu(self, i_type: str, average: str, classes: List[int]) -> _EvalResult:
         """Flatten the per-image states on the device and run ``tmx::coco_evaluate_gpu`` (csrc/coco_match.hip):
         matching and accumulation never leave the GPU; one small host read sizes the IoU export."""
@@ -269,10 +282,7 @@ class MeanAveragePrecision(Metric):
 
         segm_in = "segm" in self.iou_type
         if segm_in:
-            det_mask_area = flat([m.flatten(1).sum(1) if m.dim() > 1 else m.new_zeros(0) for m in self.detection_mask],
-                                 n_det, torch.float64)
-            gt_mask_area = flat([m.flatten(1).sum(1) if m.dim() > 1 else m.new_zeros(0) for m in self.groundtruth_mask],
-                                n_gt, torch.float64)
+            seg_iou, seg_off, det_mask_area, gt_mask_area = self._segm(dev)
         if "bbox" in self.iou_type:
             det_boxes = flat(self.detection_box, n_det, torch.float64, 4)
             gt_boxes = flat(self.groundtruth_box, n_gt, torch.float64, 4)
@@ -285,16 +295,7 @@ class MeanAveragePrecision(Metric):
 
         img_iou = img_off = det_local = gt_local = img_ng = None
         if i_type == "segm":
-            mats, offs, off = [], [], 0
-            for i in range(num_images):
-                d, g = self.detection_mask[i], self.groundtruth_mask[i]
-                m = mask_iou(d, g.to(d.device), self.groundtruth_crowds[i].reshape(-1)).reshape(-1) \
-                    if d.numel() and g.numel() else torch.zeros(0, dtype=torch.float64, device=dev)
-                offs.append(off)
-                mats.append(m.to(dev))
-                off += m.numel()
-            img_iou = torch.cat(mats) if mats else torch.zeros(0, dtype=torch.float64, device=dev)
-            img_off = torch.tensor(offs, dtype=torch.long, device=dev)
+            img_iou, img_off = seg_iou, seg_off
             img_ng = torch.tensor(gt_sizes, dtype=torch.long, device=dev)
             det_first = torch.tensor(det_sizes, device=dev).cumsum(0) - torch.tensor(det_sizes, device=dev)
             gt_first = img_ng.cumsum(0) - img_ng
@@ -336,10 +337,7 @@ class MeanAveragePrecision(Metric):
 
         segm_in = "segm" in self.iou_type
         if segm_in:
-            det_mask_area = torch.cat([m.flatten(1).sum(1).cpu() if m.dim() > 1 else m.new_zeros(0).cpu() for m in self.detection_mask]).double() \
-                if self.detection_mask else torch.zeros(0, dtype=torch.float64)
-            gt_mask_area = torch.cat([m.flatten(1).sum(1).cpu() if m.dim() > 1 else m.new_zeros(0).cpu() for m in self.groundtruth_mask]).double() \
-                if self.groundtruth_mask else torch.zeros(0, dtype=torch.float64)
+            seg_iou, seg_off, det_mask_area, gt_mask_area = (t.cpu() for t in self._segm(torch.device("cpu")))
         if "bbox" in self.iou_type:
             det_boxes = self._flat(self.detection_box, 4).double()
             gt_boxes = self._flat(self.groundtruth_box, 4).double()
@@ -355,19 +353,7 @@ class MeanAveragePrecision(Metric):
 
         img_iou = img_off = None
         if i_type == "segm":
-            mats, offs, off = [], [], 0
-            for i in range(num_images):
-                d, g = self.detection_mask[i], self.groundtruth_mask[i]
-                crowd = self.groundtruth_crowds[i].reshape(-1)
-                if d.numel() and g.numel():
-                    m = mask_iou(d, g.to(d.device), crowd).cpu().reshape(-1)
-                else:
-                    m = torch.zeros(0, dtype=torch.float64)
-                offs.append(off)
-                mats.append(m)
-                off += m.numel()
-            img_iou = torch.cat(mats) if mats else torch.zeros(0, dtype=torch.float64)
-            img_off = torch.tensor(offs, dtype=torch.long)
+            img_iou, img_off = seg_iou, seg_off
             if len(self.iou_type) == 1:
                 # the reference's COCO export drops images without ground-truth masks from the evaluated image set
                 keep_img = gt_counts > 0
@@ -432,7 +418,15 @@ class MeanAveragePrecision(Metric):
 
     def _sync_dist(self, dist_sync_fn: Any = None, process_group: Optional[Any] = None) -> None:
         if not self._shardable(dist_sync_fn):
+            if "segm" in self.iou_type:
+                # RLE tuples ride the packed all-gather as one uint8 tensor per image (same element-major,
+                # rank-interleaved order as every other list state; the reference uses all_gather_object)
+                self.detection_mask = _pack_rle_states(self.detection_mask, self.device)
+                self.groundtruth_mask = _pack_rle_states(self.groundtruth_mask, self.device)
             super()._sync_dist(dist_sync_fn, process_group)
+            if "segm" in self.iou_type:
+                self.detection_mask = _unpack_rle_states(self.detection_mask)
+                self.groundtruth_mask = _unpack_rle_states(self.groundtruth_mask)
             return
         import torch.distributed as dist
 
@@ -474,6 +468,17 @@ class MeanAveragePrecision(Metric):
         super().unsync(should_unsync)
         if should_unsync:
             self._shard_flat = None
+
+    def sync(self, dist_sync_fn: Any = None, process_group: Optional[Any] = None, should_sync: bool = True,
+             distributed_available: Optional[Any] = None, async_op: bool = False) -> Any:
+        """RLE mask states are packed around the blocking sync (``_sync_dist``); ``async_op`` therefore completes the
+        sync before returning an already-finished handle when masks are tracked."""
+        if async_op and "segm" in self.iou_type:
+            from torchmetrics_forked_amd.metric import _MetricPendingSync
+
+            super().sync(dist_sync_fn, process_group, should_sync, distributed_available, async_op=False)
+            return _MetricPendingSync(self, None)
+        return super().sync(dist_sync_fn, process_group, should_sync, distributed_available, async_op=async_op)
 
     def _evaluate_sharded(self, classes: List[int]) -> _EvalResult:
         """This rank's classes from the exchanged rows, then MAX all-reduce of the tables (-1 = not evaluated here)."""
@@ -553,6 +558,13 @@ class MeanAveragePrecision(Metric):
 
     def compute(self) -> dict:
         ops.require()
+        self._segm_cache = None
+        try:
+            return self._compute()
+        finally:
+            self._segm_cache = None
+
+    def _compute(self) -> dict:
         sharded = self._shard_flat is not None
         classes = self._shard_flat["classes"] if sharded else self._get_classes()
         result: Dict[str, Any] = {}
@@ -667,11 +679,11 @@ class MeanAveragePrecision(Metric):
             lab_l = lab.cpu().tolist()
             box_l = boxes[img_id].cpu().tolist() if "bbox" in self.iou_type else None
             msk = masks[img_id] if "segm" in self.iou_type else None
-            if msk is not None and msk.numel():
-                images[-1]["height"], images[-1]["width"] = int(msk.shape[-2]), int(msk.shape[-1])
+            if msk:
+                images[-1]["height"], images[-1]["width"] = int(msk[0][0][0]), int(msk[0][0][1])
             for k, label in enumerate(lab_l):
                 ann: Dict[str, Any] = {"id": ann_id, "image_id": img_id, "category_id": int(label)}
-                rle = rle_encode(msk[k]) if msk is not None else None
+                rle = {"size": list(msk[k][0]), "counts": msk[k][1].decode("ascii")} if msk else None
                 if detections:
                     ann["score"] = float(self.detection_scores[img_id][k])
                     ann["iscrowd"] = 0
@@ -680,7 +692,7 @@ class MeanAveragePrecision(Metric):
                     ann["iscrowd"] = int(self.groundtruth_crowds[img_id][k])
                     area = float(self.groundtruth_area[img_id][k])
                 if area is None or area <= 0:
-                    area = float(rle_area(rle)) if rle is not None else float(box_l[k][2] * box_l[k][3])
+                    area = float(rle_state_area(msk[k])) if rle is not None else float(box_l[k][2] * box_l[k][3])
                 ann["area"] = area
                 if box_l is not None:
                     ann["bbox"] = box_l[k]
@@ -719,6 +731,45 @@ def _flat_rows(lst: List[Tensor], n: int, dtype: torch.dtype, dev: torch.device,
     except RuntimeError:
         out = torch.cat([t.reshape(-1, width) if width else t.reshape(-1) for t in lst])
     return out.to(dev, dtype)
+
+
+def _pack_rle_states(states: List[Tuple[Tuple[Tuple[int, int], bytes], ...]], device: torch.device) -> List[Tensor]:
+    """Per image: one uint8 tensor ``[n, (h, w, len) x n]`` (int64 little endian) + the concatenated counts, built
+    as ONE host buffer moved to ``device`` once and split into per-image views."""
+    parts: List[bytes] = []
+    sizes: List[int] = []
+    for entry in states:
+        head = np.empty(1 + 3 * len(entry), dtype="<i8")
+        head[0] = len(entry)
+        for j, ((h, w), counts) in enumerate(entry):
+            head[1 + 3 * j: 4 + 3 * j] = (h, w, len(counts))
+        blob = head.tobytes() + b"".join(c for _, c in entry)
+        parts.append(blob)
+        sizes.append(len(blob))
+    if not parts:
+        return []
+    flat = torch.frombuffer(bytearray(b"".join(parts)), dtype=torch.uint8).to(device)
+    return list(torch.split(flat, sizes))
+
+
+def _unpack_rle_states(packed: List[Tensor]) -> List[Tuple[Tuple[Tuple[int, int], bytes], ...]]:
+    if not packed:
+        return []
+    sizes = [int(t.numel()) for t in packed]
+    buf = torch.cat([t.reshape(-1) for t in packed]).cpu().numpy().tobytes()
+    out: List[Tuple[Tuple[Tuple[int, int], bytes], ...]] = []
+    pos = 0
+    for size in sizes:
+        n = int(np.frombuffer(buf, dtype="<i8", count=1, offset=pos)[0])
+        head = np.frombuffer(buf, dtype="<i8", count=3 * n, offset=pos + 8).reshape(n, 3)
+        p = pos + 8 * (1 + 3 * n)
+        entry = []
+        for h, w, ln in head.tolist():
+            entry.append(((int(h), int(w)), buf[p:p + ln]))
+            p += ln
+        out.append(tuple(entry))
+        pos += size
+    return out
 
 
 def _warning_on_too_many_detections(limit: int) -> None:

@@ -425,7 +425,7 @@ class Metric(Module, ABC):
         for name in self._defaults:
             val = getattr(self, name)
             if isinstance(val, Sequence):
-                setattr(self, name, [v.to("cpu") for v in val])
+                setattr(self, name, [v.to("cpu") if isinstance(v, Tensor) else v for v in val])
 
     def sync(
         self,
@@ -646,12 +646,13 @@ class Metric(Module, ABC):
             if isinstance(value, Tensor):
                 this._defaults[key] = fn(value)
             elif isinstance(value, Sequence):
-                this._defaults[key] = [fn(v) for v in value]
+                this._defaults[key] = [fn(v) if isinstance(v, Tensor) else v for v in value]
             current = getattr(this, key)
             if isinstance(current, Tensor):
                 setattr(this, key, fn(current))
-            elif isinstance(current, Sequence):
-                setattr(this, key, StateArena(fn(v) for v in current) if isinstance(current, StateArena) else [fn(v) for v in current])
+            elif isinstance(current, Sequence):  # non-tensor items (segm RLE tuples) are device independent
+                items = (fn(v) if isinstance(v, Tensor) else v for v in current)
+                setattr(this, key, StateArena(items) if isinstance(current, StateArena) else list(items))
             else:
                 raise TypeError(
                     f"Expected metric state to be either a Tensor or a list of Tensor, but encountered {current}"
