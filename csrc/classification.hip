@@ -1204,7 +1204,7 @@ template <typename T, int TL, bool FIXUP>
 __global__ void __launch_bounds__(kSmallRows * TL) mc_codes_small_kernel(
     const T* __restrict__ preds, const int64_t* __restrict__ target, int64_t n, int C, int* __restrict__ mode, int64_t ignore_index,
     bool has_ignore, uint16_t* __restrict__ codes, int64_t n_pad, int64_t* __restrict__ confmat, int* __restrict__ err,
-    bool record_mode, int* __restrict__ slow_rows, int* __restrict__ slow_count) {
+    bool record_mode, int* __restrict__ slow_rows, int* __restrict__ slow_count, uint32_t* __restrict__ pcm) {
   extern __shared__ __attribute__((aligned(16))) uint16_t s_small[];  // staging [64][C], then image [C][64]; cm [C][C]
   int use_mode;
   if constexpr (FIXUP) {
@@ -1330,10 +1330,13 @@ __global__ void __launch_bounds__(kSmallRows * TL) mc_codes_small_kernel(
     reinterpret_cast<uint4*>(codes + (int64_t)c * n_pad + r0)[k] = reinterpret_cast<const uint4*>(s_small + c * kSmallRows)[k];
   }
   }  // tiles
-  if (lds_cm) {
+  if (lds_cm) {  // per-block partial (summed by class_partial_reduce_kernel), else atomics on the few cells
     __syncthreads();
-    for (int i = threadIdx.x; i < C * C; i += kSmallRows * TL)
-      if (s_cm[i]) atomic_add_i64(confmat + i, s_cm[i]);
+    if (pcm != nullptr)
+      for (int i = threadIdx.x; i < C * C; i += kSmallRows * TL) pcm[(int64_t)blockIdx.x * C * C + i] = s_cm[i];
+    else
+      for (int i = threadIdx.x; i < C * C; i += kSmallRows * TL)
+        if (s_cm[i]) atomic_add_i64(confmat + i, s_cm[i]);
   }
   if constexpr (!FIXUP) {
     if (record_mode && __syncthreads_or(bad) && threadIdx.x == 0 &&
@@ -1344,12 +1347,12 @@ __global__ void __launch_bounds__(kSmallRows * TL) mc_codes_small_kernel(
 
 template <typename T, bool FIXUP>
 void launch_small_rows(int TL, int grid, const T* p, const int64_t* target, int64_t n, int C, int* mode, int64_t ignore_index, bool has_ignore,
-                       uint16_t* codes, int64_t n_pad, int64_t* cm, int* err, bool rec, int* srows, int* scount) {
+                       uint16_t* codes, int64_t n_pad, int64_t* cm, int* err, bool rec, int* srows, int* scount, uint32_t* pcm) {
   const size_t shm = (size_t)kSmallRows * C * sizeof(uint16_t) + (C <= kSmallCmMax ? (size_t)C * C * sizeof(uint32_t) : 0);
 #define TMX_SMALL_CASE(TLV)                                                                                                     \
   case TLV:                                                                                                                      \
     hipLaunchKernelGGL((mc_codes_small_kernel<T, TLV, FIXUP>), grid, kSmallRows * TLV, shm, stream(), p, target, n, C, mode,   \
-                       ignore_index, has_ignore, codes, n_pad, cm, err, rec, srows, scount);                                      \
+                       ignore_index, has_ignore, codes, n_pad, cm, err, rec, srows, scount, pcm);                                 \
     break;
   switch (TL) {
     TMX_SMALL_CASE(1) TMX_SMALL_CASE(2) TMX_SMALL_CASE(4) TMX_SMALL_CASE(8) TMX_SMALL_CASE(16)
@@ -1370,16 +1373,21 @@ void launch_small_two_pass(const T* p, const int64_t* target, int64_t n, int C, 
   const int64_t ntiles = n_pad / kSmallRows;
   int TL = 1;
   while (TL * kSmallVpt < C) TL *= 2;
-  // a block loops over 64-row tiles: ~16 waves per CU in flight, and one LDS confusion-matrix flush per block
-  const int grid = static_cast<int>(std::min<int64_t>(ntiles, std::max(256, 8192 / TL)));
+  // a block loops over 64-row tiles: ~8-16 waves per CU in flight, and one LDS confusion-matrix flush per block
+  const int grid = static_cast<int>(std::min<int64_t>(ntiles, std::max(256, 2048 / TL)));
+  // confusion-matrix partials per block (C <= 32: at most 4 MiB), summed by the reduce launch: no same-cell atomics
+  const bool use_pcm = cm != nullptr && C <= 32;
+  auto pcm_t = use_pcm ? at::empty({(int64_t)grid * C * C}, opts.dtype(at::kInt)) : at::Tensor();
+  uint32_t* pcm = use_pcm ? reinterpret_cast<uint32_t*>(pcm_t.data_ptr<int>()) : nullptr;
   auto codes = at::empty({(int64_t)C * n_pad}, opts.dtype(at::kShort));
   auto slow_rows = at::empty({2 * n}, opts.dtype(at::kInt));
   uint16_t* cptr = reinterpret_cast<uint16_t*>(codes.data_ptr());
   int* srows = slow_rows.data_ptr<int>();
-  launch_small_rows<T, false>(TL, grid, p, target, n, C, mode, ignore_index, has_ignore, cptr, n_pad, cm, err, speculative, srows, state);
+  launch_small_rows<T, false>(TL, grid, p, target, n, C, mode, ignore_index, has_ignore, cptr, n_pad, cm, err, speculative, srows, state,
+                              pcm);
   if (speculative)
     launch_small_rows<T, true>(TL, std::min(grid, 1024), p, target, n, C, mode, ignore_index, has_ignore, cptr, n_pad, cm, err, false,
-                               srows, state);
+                               srows, state, nullptr);
   // Class pass: packed LDS histogram per (class, row split) — with few classes 1 / C of the codes are positives —
   // and a partial flush (plain stores of the occupied range, then one reduce launch) instead of global int64 atomics:
   // every split of a class hits the same few thousand bins.  Splits: enough (class, split) blocks to fill the chip,
@@ -1397,7 +1405,8 @@ void launch_small_two_pass(const T* p, const int64_t* target, int64_t n, int C, 
                      hist, p, C, target, n, mode, speculative, srows, state, cm, code_range, speculative ? mode : nullptr, pp,
                      prange.data_ptr<int>());
   TMX_LAUNCH_CHECK();
-  hipLaunchKernelGGL(class_partial_reduce_kernel, dim3(kCodes / 256, C), 256, 0, stream(), pp, prange.data_ptr<int>(), splits, hist);
+  hipLaunchKernelGGL(class_partial_reduce_kernel, dim3(kCodes / 256 + 1, C), 256, 0, stream(), pp, prange.data_ptr<int>(), splits, hist,
+                     code_range, state, speculative ? mode : nullptr, pcm, grid, cm, C);
   TMX_LAUNCH_CHECK();
 }
 

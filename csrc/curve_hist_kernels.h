@@ -773,6 +773,10 @@ __device__ __forceinline__ void class_hist_block(int64_t vb, int64_t vgrid, cons
   // rare-row codes went to the int64 bins by atomics: then the last flush must be atomic too
   if (partial != nullptr) class_store_partial<NT>(s_h, partial + vb * kCodes, prange + 2 * vb, lo, hi);
   else class_flush<PACKED, NT>(s_h, neg_hist, pos_hist, exclusive && n0 + n1 == 0, lo, hi);
+  // partial mode: class_partial_reduce_kernel derives the class ranges from prange and resets / rolls the state
+  // (no per-block global atomics on the same few words — with few classes hundreds of blocks share each class);
+  // only rare-row codes (tracked in lo / hi here, not in the partial histogram) still go through atomics
+  if (partial != nullptr && n0 + n1 == 0) return;
   if (code_range != nullptr) {  // per-class running range [C][2]: one min / max per wave, no block barrier
     lo = wave_min_i32(lo);
     hi = wave_max_i32(hi);
@@ -781,6 +785,7 @@ __device__ __forceinline__ void class_hist_block(int64_t vb, int64_t vgrid, cons
       atomicMax(code_range + 2 * c + 1, hi);
     }
   }
+  if (partial != nullptr) return;
   if (threadIdx.x == 0) {
     // No fence: the only ordering needed is "every block's read of mode / counts happened before the reset", and
     // each block consumed those values (s_info, above) before taking its ticket.  (An agent-scope release here writes
@@ -821,10 +826,45 @@ __global__ void __launch_bounds__(kClassThreads) class_hist_partial_kernel(
 }
 
 // Sum of the splits' partial packed words per (class, bin) into the int64 histogram: one owner thread per bin, so a
-// plain read-modify-write; splits whose range misses the bin are not read.
+// plain read-modify-write; splits whose range misses the bin are not read.  The extra block column x = kCodes / 256
+// does the per-class work the class pass left out: the class's occupied range (min / max over its splits) into
+// code_range, the row pass's per-block confusion-matrix partials of row c (pcm [blocks][C][C], C <= 64), and —
+// block (x, 0) — the batch's state reset and speculation roll (the class pass has completed: stream order).
 __global__ void __launch_bounds__(256) class_partial_reduce_kernel(const uint32_t* __restrict__ partial, const int* __restrict__ prange,
-                                                                   int splits, int64_t* __restrict__ hist) {
+                                                                   int splits, int64_t* __restrict__ hist, int* __restrict__ code_range,
+                                                                   int* __restrict__ state, int* __restrict__ roll_mode,
+                                                                   const uint32_t* __restrict__ pcm, int pcm_blocks,
+                                                                   int64_t* __restrict__ confmat, int C) {
   const int c = blockIdx.y;
+  if (blockIdx.x == kCodes / 256) {
+    if (threadIdx.x == 0 && code_range != nullptr) {
+      int lo = kCodes, hi = -1;
+      for (int s = 0; s < splits; ++s) {
+        const int64_t b = (int64_t)c * splits + s;
+        lo = min(lo, prange[2 * b]);
+        hi = max(hi, prange[2 * b + 1]);
+      }
+      if (hi >= 0) {
+        atomicMin(code_range + 2 * c, lo);
+        atomicMax(code_range + 2 * c + 1, hi);
+      }
+    }
+    if (pcm != nullptr && threadIdx.x < C) {
+      uint64_t acc = 0;
+      for (int b = 0; b < pcm_blocks; ++b) acc += pcm[((int64_t)b * C + c) * C + threadIdx.x];
+      if (acc) confmat[(int64_t)c * C + threadIdx.x] += static_cast<int64_t>(acc);
+    }
+    if (c == 0 && threadIdx.x == 0) {
+      state[0] = state[1] = 0;
+      state[2] = 0;
+      if (roll_mode != nullptr) {
+        const int m1 = roll_mode[1];
+        roll_mode[0] = m1;
+        roll_mode[1] = 0;
+      }
+    }
+    return;
+  }
   const int i = blockIdx.x * 256 + threadIdx.x;
   uint64_t neg = 0, pos = 0;
   for (int s = 0; s < splits; ++s) {

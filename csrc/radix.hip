@@ -366,28 +366,48 @@ __global__ void __launch_bounds__(kRsThreads) rs_reduce_kernel(const KT* __restr
   const uint32_t P0 = seg_scanned(ps.a, ps.csum, Tt, ps.cps, s, t), Q0 = seg_scanned(qs.a, qs.csum, Tt, qs.cps, s, t);
   const uint32_t E0 = seg_scanned(es.a, es.csum, Tt, es.cps, s, t);
   // cumulative at the last group end before the tile: P0 / Q0 when the tile starts a group, else the counts before
-  // the start of the group that runs into the tile (binary search for its first key; rare: ties across tiles)
+  // the start g0 of the group that runs into the tile: thread 0 binary-searches g0, then the whole block counts the
+  // partial tile [tile(g0) start, g0) (a serial count here cost ~500 us at 16.7M rand() scores, where every other
+  // tile boundary falls inside a tie group)
+  __shared__ long long s_g0;
+  __shared__ uint32_t s_cnt[2][kRsThreads / kWave];
   if (threadIdx.x == 0) {
-    uint32_t bp = P0, bq = Q0;
-    if (t > 0 && keys[seg0 + tb - 1] == keys[seg0 + tb]) {
-      const KT k0 = keys[seg0 + tb];
+    long long g0 = -1;
+    if (t > 0 && key_at(0) == keys[seg0 + tb - 1]) {
+      const KT k0 = key_at(0);
       int64_t lo = 0, hi = tb - 1;  // first index with key == k0 (keys ascending)
       while (lo < hi) {
         const int64_t mid = (lo + hi) / 2;
         if (keys[seg0 + mid] < k0) lo = mid + 1; else hi = mid;
       }
-      const int64_t g0 = lo;
-      const int tg = static_cast<int>(g0 / kRsTile);
-      bp = seg_scanned(ps.a, ps.csum, Tt, ps.cps, s, tg);
-      bq = seg_scanned(qs.a, qs.csum, Tt, qs.cps, s, tg);
-      for (int64_t i = (int64_t)tg * kRsTile; i < g0; ++i) {  // partial tile before the group start
-        const uint8_t w = pay[seg0 + i];
-        bp += (w & 1u) ? 1u : 0u;
-        bq += (w & 3u) == 0u ? 1u : 0u;
-      }
+      g0 = lo;
     }
-    s_prev[0] = bp;
-    s_prev[1] = bq;
+    s_g0 = g0;
+  }
+  __syncthreads();
+  const long long g0 = s_g0;
+  if (g0 >= 0) {  // block-uniform
+    const int tg = static_cast<int>(g0 / kRsTile);
+    uint32_t bp = 0, bq = 0;
+    for (int64_t i = (int64_t)tg * kRsTile + threadIdx.x; i < g0; i += kRsThreads) {
+      const uint8_t w = pay[seg0 + i];
+      bp += (w & 1u) ? 1u : 0u;
+      bq += (w & 3u) == 0u ? 1u : 0u;
+    }
+    bp = static_cast<uint32_t>(wave_sum((long long)bp));
+    bq = static_cast<uint32_t>(wave_sum((long long)bq));
+    if ((threadIdx.x & (kWave - 1)) == 0) {
+      s_cnt[0][threadIdx.x / kWave] = bp;
+      s_cnt[1][threadIdx.x / kWave] = bq;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      s_prev[0] = seg_scanned(ps.a, ps.csum, Tt, ps.cps, s, tg) + s_cnt[0][0] + s_cnt[0][1] + s_cnt[0][2] + s_cnt[0][3];
+      s_prev[1] = seg_scanned(qs.a, qs.csum, Tt, qs.cps, s, tg) + s_cnt[1][0] + s_cnt[1][1] + s_cnt[1][2] + s_cnt[1][3];
+    }
+  } else if (threadIdx.x == 0) {
+    s_prev[0] = P0;
+    s_prev[1] = Q0;
   }
   __syncthreads();
   // previous group end's cumulative for this thread's first group end

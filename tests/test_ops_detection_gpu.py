@@ -101,8 +101,8 @@ def _box_masks(k, h, w, g):
     """Rectangle masks (realistic run counts) plus the corner cases of the encoder: all / none / first pixel."""
     x0 = torch.randint(0, w, (k, 1, 1), generator=g)
     y0 = torch.randint(0, h, (k, 1, 1), generator=g)
-    x1 = x0 + torch.randint(1, w, (k, 1, 1), generator=g)
-    y1 = y0 + torch.randint(1, h, (k, 1, 1), generator=g)
+    x1 = x0 + torch.randint(1, max(w, 2), (k, 1, 1), generator=g)
+    y1 = y0 + torch.randint(1, max(h, 2), (k, 1, 1), generator=g)
     yy = torch.arange(h).view(1, h, 1)
     xx = torch.arange(w).view(1, 1, w)
     m = (yy >= y0) & (yy < y1) & (xx >= x0) & (xx < x1)

@@ -71,8 +71,12 @@ def _ssim_update(
     k2: float = 0.03,
     return_full_image: bool = False,
     return_contrast_sensitivity: bool = False,
+    sse_out: Optional[List[Tensor]] = None,
 ) -> Union[Tensor, Tuple[Tensor, Tensor]]:
-    """Per-image SSIM ``[B]`` (optionally with per-image contrast sensitivity or the full SSIM map)."""
+    """Per-image SSIM ``[B]`` (optionally with per-image contrast sensitivity or the full SSIM map).
+
+    ``sse_out``: when the native kernel runs, the total squared error of the batch (fp64) is appended to it — the
+    kernel accumulates it while staging the pixels (fused PSNR of a ``MetricCollection``, ``ops/fused.py``)."""
     is_3d = preds.ndim == 5
     if not isinstance(kernel_size, Sequence):
         kernel_size = 3 * [kernel_size] if is_3d else 2 * [kernel_size]
@@ -115,7 +119,9 @@ def _ssim_update(
         consts = torch.stack([c.to(device, torch.float32) if isinstance(c, torch.Tensor) else torch.full((), float(c), device=device)
                               for c in (c1, c2)])
         b, c, h, w = preds.shape
-        sums = torch.ops.tmx.ssim_sums(preds.reshape(b * c, h, w), target.reshape(b * c, h, w), w1, w1, consts)
+        sums = torch.ops.tmx.ssim_sums(preds.reshape(b * c, h, w), target.reshape(b * c, h, w), w1, w1, consts, sse_out is not None)
+        if sse_out is not None:
+            sse_out.append(sums[2].sum())
         n_valid = c * (h - window[0] + 1) * (w - window[1] + 1)
         sim = (sums[0].reshape(b, c).sum(1) / n_valid).to(dtype)
         if return_contrast_sensitivity:

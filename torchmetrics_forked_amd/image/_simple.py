@@ -98,6 +98,19 @@ class StructuralSimilarityIndexMeasure(_ImageMetric):
         else:
             self.similarity.append(similarity)
 
+    # fused {SSIM, PSNR} collection pass (ops/fused.py): the SSIM kernel also returns the batch's squared error
+    def _fusion_key(self) -> Optional[Tuple[str]]:
+        plain = self.reduction in ("elementwise_mean", "sum") and not self.return_full_image and not self.return_contrast_sensitivity
+        fixed_range = isinstance(self.data_range, (int, float)) and not isinstance(self.data_range, bool)
+        return ("image_pair",) if plain and fixed_range else None
+
+    def _fused_update(self, preds: Tensor, target: Tensor, sse_out: List[Tensor]) -> None:
+        preds, target = _ssim_check_inputs(preds, target)
+        similarity = _ssim_update(preds, target, self.gaussian_kernel, self.sigma, self.kernel_size, self.data_range, self.k1,
+                                  self.k2, False, False, sse_out=sse_out)
+        self.similarity += similarity.sum()
+        self.total += preds.shape[0]
+
     def compute(self) -> Union[Tensor, Tuple[Tensor, Tensor]]:
         if self.reduction == "elementwise_mean":
             similarity = self.similarity / self.total
@@ -240,6 +253,14 @@ class PeakSignalNoiseRatio(_ImageMetric):
         else:
             self.sum_squared_error.append(sse)
             self.total.append(n)
+
+    def _fusion_key(self) -> Optional[Tuple[str]]:
+        fixed = self.dim is None and self.clamping_fn is None and self.data_range is not None
+        return ("image_pair",) if fixed else None
+
+    def _fused_add(self, sse: Tensor, n: int) -> None:
+        self.sum_squared_error += sse.to(self.sum_squared_error.dtype)
+        self.total += n
 
     def compute(self) -> Tensor:
         data_range = self.data_range if self.data_range is not None else self.max_target - self.min_target

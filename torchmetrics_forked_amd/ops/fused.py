@@ -17,6 +17,11 @@ curve member, the argmax pair stream -- counts the batch's (target, argmax) pair
 ``tmx::confmat_fold`` (csrc/fused.hip) then adds it to every confusion-matrix state and turns its diagonal / row /
 column sums into every stat member's tp / fp / tn / fn.  With a single confusion-matrix member and no stat member
 the pass accumulates straight into that member's state.
+
+``image_pair`` plan (key ``("image_pair",)``) over one ``StructuralSimilarityIndexMeasure`` (fixed ``data_range``,
+scalar reduction) and any number of ``PeakSignalNoiseRatio`` members (fixed ``data_range``, ``dim=None``): the SSIM
+kernel (csrc/image.hip ``ssim_v2_kernel<KS, true>``) adds every input pixel's squared error while it stages the two
+images, so PSNR costs no second pass over them (256 x 3 x 1024^2 fp32: 6.4 GB not re-read).
 """
 from typing import Any, Dict, List, Optional, Tuple
 
@@ -137,6 +142,39 @@ class _MulticlassScoresPlan:
         return [n for n, m in members.items() if any(m is u for u in updated)]
 
 
+class _ImagePairPlan:
+    def __init__(self, ssim_name: str, psnr_names: List[str]) -> None:
+        self.ssim_name = ssim_name
+        self.psnr_names = psnr_names
+        self.names = [ssim_name] + psnr_names
+
+    def run(self, members: Dict[str, Any], args: Tuple, kwargs: Dict[str, Any]) -> List[str]:
+        ssim = members.get(self.ssim_name)
+        psnrs = [members[n] for n in self.psnr_names if n in members]
+        if ssim is None or not psnrs:
+            return []
+        preds = kwargs.get("preds", args[0] if len(args) > 0 else None)
+        target = kwargs.get("target", args[1] if len(args) > 1 else None)
+        if not isinstance(preds, Tensor) or not isinstance(target, Tensor) or preds.ndim != 4 or preds.dtype != torch.float32:
+            return []
+        if preds.shape != target.shape or not ops.use_native(preds) or torch.is_grad_enabled() and preds.requires_grad:
+            return []
+        if any(p.sum_squared_error.device != preds.device for p in psnrs):
+            return []
+        sse: List[Tensor] = []
+        for m in [ssim] + psnrs:
+            m._computed = None
+            m._update_count += 1
+        ssim._fused_update(preds, target, sse)
+        for p in psnrs:
+            if sse:
+                p._fused_add(sse[0], preds.numel())
+            else:  # the kernel could not take the inputs (window / shape): PSNR's own pass
+                p._update_count -= 1
+                p.update(preds, target)
+        return [n for n, m in members.items() if m is ssim or any(m is p for p in psnrs)]
+
+
 def build_fused_plans(modules: Dict[str, Any]) -> List[Any]:
     groups: Dict[Tuple, List[str]] = {}
     for name, m in modules.items():
@@ -148,6 +186,12 @@ def build_fused_plans(modules: Dict[str, Any]) -> List[Any]:
             groups.setdefault(key, []).append(name)
     plans: List[Any] = []
     for key, names in groups.items():
+        if key[0] == "image_pair":
+            ssims = [n for n in names if hasattr(modules[n], "_fused_update")]
+            psnrs = [n for n in names if hasattr(modules[n], "_fused_add")]
+            if ssims and psnrs:
+                plans.append(_ImagePairPlan(ssims[0], psnrs))
+            continue
         if key[0] != "multiclass_scores" or len(names) < 2:
             continue
         curves = [n for n in names if hasattr(modules[n], "_curve_update")]
