@@ -12,6 +12,8 @@ ranks is reported, ``value`` = world * steps / seconds (whole-job updates/s, wea
 (BASELINE.json publishes none), so ``vs_baseline`` is null.
 """
 import argparse
+import sys
+import threading
 import time
 from typing import Any, Callable, Dict, Optional
 
@@ -24,8 +26,31 @@ def _sync(device: torch.device) -> None:
         torch.cuda.synchronize(device)
 
 
+def _heartbeat(label: str, every: float = 30.0) -> threading.Event:
+    """Print a progress line to stderr every ``every`` s until the returned event is set (long configs: the first
+    MIOpen calls at 1024^2 compile kernels for minutes without output)."""
+    stop = threading.Event()
+    t0 = time.perf_counter()
+
+    def beat() -> None:
+        while not stop.wait(every):
+            print(f"[config_bench] {label}: {time.perf_counter() - t0:.0f} s", file=sys.stderr, flush=True)
+
+    threading.Thread(target=beat, daemon=True).start()
+    return stop
+
+
 def _timed_window(step: Callable[[int], None], compute: Callable[[], Any], steps: int, warmup: int, reset: Callable[[], None],
                   device: torch.device, world: int) -> Dict[str, Any]:
+    stop = _heartbeat("running")
+    try:
+        return _timed_window_inner(step, compute, steps, warmup, reset, device, world)
+    finally:
+        stop.set()
+
+
+def _timed_window_inner(step: Callable[[int], None], compute: Callable[[], Any], steps: int, warmup: int,
+                        reset: Callable[[], None], device: torch.device, world: int) -> Dict[str, Any]:
     for i in range(warmup):
         step(i)
     if warmup:

@@ -1,0 +1,84 @@
+"""GPU text kernels of csrc/text_dp.hip vs their host ops (one MI355X + the box's CPU cores):
+  * EED pair DPs: ``tmx::eed_gpu`` (one thread per pair, bit-identical) vs ``tmx::eed_batch`` (parallel host);
+  * chrF character n-gram overlap (order 6) and ROUGE-2 word overlap: ``tmx::ngram_overlap_gpu`` vs ``tmx::ngram_overlap``.
+GPU times include the host-to-device copies of the packed ids and the copy back.  Prints one JSON line."""
+import json
+import os
+import random
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from torchmetrics_forked_amd import ops  # noqa: E402
+from torchmetrics_forked_amd.functional.text.helper import _pack, _pack_codepoints, _Vocab  # noqa: E402
+
+WORDS = "the a cat sat on mat dog ran far away home blue sky today , . ! ? and of to in it is was model data".split()
+
+
+def sent(rnd, lo, hi):
+    return " ".join(rnd.choice(WORDS) for _ in range(rnd.randint(lo, hi)))
+
+
+def best_of(fn, reps=3):
+    fn()
+    torch.cuda.synchronize()
+    best = float("inf")
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        fn()
+        torch.cuda.synchronize()
+        best = min(best, time.perf_counter() - t0)
+    return 1e3 * best
+
+
+def main() -> None:
+    ops.require()
+    dev = torch.device("cuda", 0)
+    rnd = random.Random(0)
+    out = {"host_threads": torch.get_num_threads()}
+    # EED
+    n = 4096
+    hyps = [" " + sent(rnd, 15, 40) + " " for _ in range(n)]
+    refs = [" " + sent(rnd, 15, 40) + " " for _ in range(n)]
+    h, ho = _pack_codepoints(hyps)
+    r, ro = _pack_codepoints(refs)
+    args = (ord(" "), 2.0, 0.3, 0.2, 1.0)
+    mx = max(len(x) for x in hyps)
+    out["eed_pairs"] = n
+    out["eed_mean_chars"] = round(h.numel() / n, 1)
+    out["eed_host_ms"] = round(best_of(lambda: torch.ops.tmx.eed_batch(h, ho, r, ro, *args)), 2)
+    out["eed_gpu_ms"] = round(best_of(lambda: torch.ops.tmx.eed_gpu(h.to(dev), ho.to(dev), r.to(dev), ro.to(dev), *args, mx).cpu()), 2)
+    a = torch.ops.tmx.eed_batch(h, ho, r, ro, *args)
+    b = torch.ops.tmx.eed_gpu(h.to(dev), ho.to(dev), r.to(dev), ro.to(dev), *args, mx).cpu()
+    out["eed_identical"] = bool(torch.equal(a, b))
+    # n-gram overlap
+    for name, tok, order, nh in (("chrf_char6", list, 6, 20000), ("rouge2_word", str.split, 2, 50000)):
+        hs, rs, groups = [], [], [0]
+        for _ in range(nh):
+            hs.append(tok(sent(rnd, 10, 30)))
+            for _ in range(2):
+                rs.append(tok(sent(rnd, 10, 30)))
+            groups.append(groups[-1] + 2)
+        vocab = _Vocab()
+        hh, hho = _pack(hs, vocab)
+        rr, rro = _pack(rs, vocab)
+        g = torch.tensor(groups)
+        bits = max(1, len(vocab._ids).bit_length())
+        mh = max(len(x) for x in hs)
+        out[f"{name}_hyps"] = nh
+        out[f"{name}_host_ms"] = round(best_of(lambda: torch.ops.tmx.ngram_overlap(hh, hho, rr, rro, g, order)), 2)
+
+        def gpu():
+            d = [x.to(dev) for x in (hh, hho, rr, rro, g)]
+            return [t.cpu() for t in torch.ops.tmx.ngram_overlap_gpu(*d, order, bits, mh)]
+
+        out[f"{name}_gpu_ms"] = round(best_of(gpu), 2)
+        host = torch.ops.tmx.ngram_overlap(hh, hho, rr, rro, g, order)
+        out[f"{name}_identical"] = all(torch.equal(x, y) for x, y in zip(gpu(), host))
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -40,6 +40,25 @@ def _pack_codepoints(strings: Sequence[str]) -> Tuple[Tensor, Tensor]:
     return torch.tensor(flat, dtype=torch.long), torch.tensor(off, dtype=torch.long)
 
 
+# tokens (hypothesis side) above which a GPU-resident metric counts n-gram overlaps on the device
+GPU_NGRAM_MIN_TOKENS = 4096
+
+
+def ngram_overlap(h: Tensor, h_off: Tensor, r: Tensor, r_off: Tensor, groups: Tensor, n: int, vocab_size: int,
+                  device: Optional[torch.device] = None) -> Tuple[Tensor, Tensor, Tensor]:
+    """Clipped n-gram overlap (``tmx::ngram_overlap`` semantics) on the GPU (``tmx::ngram_overlap_gpu``, one wave per
+    hypothesis, exact 128-bit keys of the dense ids) when the metric lives there, the batch is large enough and the
+    keys fit; else the host op.  Results are always returned on the CPU (the callers' score algebra runs there)."""
+    if device is not None and device.type == "cuda" and h.numel() >= GPU_NGRAM_MIN_TOKENS and ops.use_native(torch.empty(0, device=device)):
+        bits = max(1, int(vocab_size).bit_length())
+        lens = h_off[1:] - h_off[:-1]
+        max_hyp = int(lens.max()) if lens.numel() else 0
+        if n * bits <= 128 and max_hyp <= 512:
+            d = [x.to(device, non_blocking=True) for x in (h, h_off, r, r_off, groups)]
+            return tuple(t.cpu() for t in torch.ops.tmx.ngram_overlap_gpu(*d, n, bits, max_hyp))  # type: ignore[return-value]
+    return torch.ops.tmx.ngram_overlap(h, h_off, r, r_off, groups, n)
+
+
 # DP cells (prediction tokens x 64-token reference words) above which a GPU-resident metric scores the batch on the
 # device (csrc/text_gpu.hip); smaller batches are cheaper on the host than one H2D copy + launch
 GPU_LEVENSHTEIN_MIN_WORK = 1 << 16

@@ -75,7 +75,8 @@ class CHRFScore(Metric):
 
     def update(self, preds: Sequence[str], target: Sequence[Sequence[str]]) -> None:
         pc, pw, tc, tw, mc, mw, sent = _chrf_batch(
-            preds, target, self.n_char_order, self.n_word_order, self.n_order, self.beta, self.lowercase, self.whitespace
+            preds, target, self.n_char_order, self.n_word_order, self.n_order, self.beta, self.lowercase, self.whitespace,
+            self.device,
         )
         vals = {("preds", "char"): pc, ("preds", "word"): pw, ("target", "char"): tc, ("target", "word"): tw,
                 ("matching", "char"): mc, ("matching", "word"): mw}

@@ -91,7 +91,7 @@ class ExtendedEditDistance(Metric):
         self.add_state("sentence_eed", [], dist_reduce_fx="cat")
 
     def update(self, preds: Union[str, Sequence[str]], target: Sequence[Union[str, Sequence[str]]]) -> None:
-        scores = _eed_update(preds, target, self.language, self.alpha, self.rho, self.deletion, self.insertion)
+        scores = _eed_update(preds, target, self.language, self.alpha, self.rho, self.deletion, self.insertion, device=self.device)
         self.sentence_eed.extend(s.to(self.device) for s in scores)
 
     def compute(self) -> Union[Tensor, Tuple[Tensor, Tensor]]:
