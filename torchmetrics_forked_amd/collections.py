@@ -284,9 +284,24 @@ class MetricCollection(ModuleDict):
                 out[n] = m._fused_forward_end(ctx[n])
         return out
 
+    def _forward_step_synced(self, args: Tuple, kwargs: Dict[str, Any], skip: Dict[str, Any]) -> Dict[str, Any]:
+        """``dist_sync_on_step`` members under DDP: launch every member's batch-state collectives, then compute the
+        batch values in order (``Metric._step_sync_begin/_end``) — member i computes while member j's RCCL work runs."""
+        from torchmetrics_forked_amd.parallel.sync import distributed_available
+
+        if not distributed_available():
+            return {}
+        mods = {k: m for k, m in self.items(keep_base=True, copy_state=False) if k not in skip and m._step_sync_ok()}
+        if not mods:
+            return {}
+        ctx = {k: m._step_sync_begin(args, m._filter_kwargs(**kwargs)) for k, m in mods.items()}
+        return {k: m._step_sync_end(ctx[k]) for k, m in mods.items()}
+
     def _compute_and_reduce(self, method_name: str, *args: Any, **kwargs: Any) -> Dict[str, Any]:
         result = {}
         fused = self._forward_fused(args, kwargs) if method_name == "forward" else {}
+        if method_name == "forward":
+            fused.update(self._forward_step_synced(args, kwargs, fused))
         for k, m in self.items(keep_base=True, copy_state=False):
             if method_name == "compute":
                 self._install_pending(m)
