@@ -7,7 +7,10 @@ import os
 import socket
 from typing import Any, Callable, List
 
+from multiprocessing import TimeoutError as mp_TimeoutError
+
 NUM_PROCESSES = 2
+DDP_TIMEOUT_S = float(os.environ.get("TMX_TEST_DDP_TIMEOUT", "90"))
 _POOL = None
 
 
@@ -65,8 +68,16 @@ def get_pool():
 
 def run_ddp(fn: Callable, *args: Any) -> List[Any]:
     """Run ``fn(rank, world, *args)`` on both workers concurrently; returns results ordered by rank."""
+    global _POOL
     pool = get_pool()
-    res = pool.starmap(_call, [(fn, args)] * NUM_PROCESSES, chunksize=1)
+    try:
+        # bounded: a rank that raised while its peer waits in a collective would otherwise hang the whole session
+        res = pool.starmap_async(_call, [(fn, args)] * NUM_PROCESSES, chunksize=1).get(timeout=DDP_TIMEOUT_S)
+    except mp_TimeoutError:
+        pool.terminate()
+        pool.join()
+        _POOL = None
+        raise AssertionError(f"ddp test body did not finish within {DDP_TIMEOUT_S} s (a rank hung in a collective)") from None
     assert sorted(r for r, _ in res) == list(range(NUM_PROCESSES)), "pool tasks did not land on distinct ranks"
     return [v for _, v in sorted(res, key=lambda x: x[0])]
 

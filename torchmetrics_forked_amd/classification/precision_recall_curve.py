@@ -178,12 +178,37 @@ class _CurveMetric(Metric):
             self._spec_mode = st
         return st
 
+    def _fresh_hist(self, device: torch.device) -> Tuple[Tensor, Tensor]:
+        """A zeroed ``[C, 2, 16384]`` histogram and its empty per-class code range ([16384, -1] rows), built with fill
+        kernels only (no host-to-device copy, so no stream synchronisation)."""
+        hist = torch.zeros(self._num, 2, eng.N_CODES, dtype=torch.long, device=device)
+        rng = torch.full((self._num, 2), -1, dtype=torch.int32, device=device)
+        rng[:, 0].fill_(eng.N_CODES)
+        return hist, rng
+
     def _ensure_hist(self, device: torch.device) -> Tensor:
         if self.score_hist.numel() == 0:
-            self.score_hist = torch.zeros(self._num, 2, eng.N_CODES, dtype=torch.long, device=device)
-            empty = torch.tensor([eng.N_CODES, -1], dtype=torch.int32, device=device).repeat(self._num, 1)
-            self._set_range(self.score_hist, empty)
+            spare = self.__dict__.pop("_hist_spare", None)
+            hist, rng = spare if spare is not None and spare[0].device == device else self._fresh_hist(device)
+            self.score_hist = hist
+            self._set_range(hist, rng)
         return self.score_hist
+
+    def reset(self) -> None:
+        """Reference semantics (every state back to its default; ``score_hist`` empty again).  A histogram that was
+        in use on the GPU is re-armed as a private spare: its storage goes back to the caching allocator and a zeroed
+        one of the same shape is prepared now, so the next epoch's first update binds it instead of allocating and
+        zero-filling ``2 C 16384`` int64 (262 MB at C = 1000) inside its own window.  The spare is not state: it is
+        dropped from pickles / checkpoints, and a batch on another device ignores it."""
+        prev = self.score_hist if self.thresholds is None else None
+        rearm = isinstance(prev, Tensor) and prev.numel() > 0 and prev.is_cuda
+        dev = prev.device if rearm else None
+        prev = None
+        super().reset()
+        self._invalidate_range()
+        self.__dict__.pop("_hist_spare", None)
+        if rearm:
+            self._hist_spare = self._fresh_hist(dev)
 
     # ---- occupied code range of ``score_hist`` ------------------------------------------------------------
     # ``_code_range`` (int32[C, 2] = per-class [lo, hi], on the histogram's device) is widened by the class-pass kernel

@@ -649,7 +649,7 @@ class Metric(Module, ABC):
 
     def __getstate__(self) -> Dict[str, Any]:
         self._join_side_work()
-        return {k: v for k, v in self.__dict__.items() if k not in ("update", "compute", "_update_signature", "_side_bufs", "_dual_bufs")}
+        return {k: v for k, v in self.__dict__.items() if k not in ("update", "compute", "_update_signature", "_side_bufs", "_dual_bufs", "_hist_spare")}
 
     def __setstate__(self, state: Dict[str, Any]) -> None:
         self.__dict__.update(state)
