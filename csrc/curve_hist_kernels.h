@@ -171,6 +171,35 @@ __device__ __forceinline__ float div_rn(float e, float s, float rinv) {
   return __builtin_fmaf(__builtin_fmaf(-q, s, e), rinv, q);
 }
 
+// ---- packed (two-row) forms of the above: the row pass handles the rows of a pair together, element j of row a in
+// .x and of row b in .y, so every IEEE mul / add / fma of the chain issues as one v_pk_*_f32 (CDNA3/4 packed fp32:
+// two results per lane per instruction).  Each component performs exactly the scalar sequence -> bit-identical.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// exp_nonpos for two values.  The x < -103.97 -> 0 select is replaced by clamping the scaled exponent at -151:
+// for every x >= -104.66 nothing changes (ph > -151), and below it, or in the window where the scalar form forces
+// 0, ldexp(r, e) with e <= -150 and r < 2^(ph - e) lands below half the smallest denormal and rounds to 0 too (the
+// reference expf's result).  -inf gives pl = -inf -> exp2 -> 0; NaN still propagates through pl (v_max drops it
+// from ph only), so a NaN row keeps its NaN exp-sum.  One v_max replaces a compare + select per element.
+__device__ __forceinline__ f32x2 exp_nonpos2(f32x2 x) {
+#pragma clang fp contract(off)
+  const float hi_s = __uint_as_float(0x3fb8aa3bu), lo_s = __uint_as_float(0x32a5705fu);
+  const f32x2 log2e_hi = {hi_s, hi_s}, log2e_lo = {lo_s, lo_s};
+  f32x2 ph = x * log2e_hi;
+  ph.x = __builtin_fmaxf(ph.x, -151.f);
+  ph.y = __builtin_fmaxf(ph.y, -151.f);
+  f32x2 pl = __builtin_elementwise_fma(x, log2e_hi, -ph);
+  const f32x2 e = {__builtin_rintf(ph.x), __builtin_rintf(ph.y)};
+  pl = __builtin_elementwise_fma(x, log2e_lo, pl);
+  const f32x2 t = (ph - e) + pl;
+  return f32x2{__builtin_amdgcn_ldexpf(__builtin_amdgcn_exp2f(t.x), static_cast<int>(e.x)),
+               __builtin_amdgcn_ldexpf(__builtin_amdgcn_exp2f(t.y), static_cast<int>(e.y))};
+}
+__device__ __forceinline__ f32x2 div_rn2(f32x2 e, f32x2 s, f32x2 rinv) {
+  const f32x2 q = e * rinv;
+  return __builtin_elementwise_fma(__builtin_elementwise_fma(-q, s, e), rinv, q);
+}
+
 // fp32 word whose high half is the RNE 16-bit rounding (bf16) — packed pairwise with v_perm afterwards.
 template <typename T> __device__ __forceinline__ uint32_t rne_word(float f);
 template <> __device__ __forceinline__ uint32_t rne_word<__hip_bfloat16>(float f) {
@@ -178,6 +207,17 @@ template <> __device__ __forceinline__ uint32_t rne_word<__hip_bfloat16>(float f
   return u + 0x7FFFu + ((u >> 16) & 1u);
 }
 template <> __device__ __forceinline__ uint32_t rne_word<__half>(float f) { return (uint32_t)round_bits16<__half>(f) << 16; }
+
+// two RNE 16-bit roundings packed into one dword (a low, b high): gfx950's v_cvt_pk_bf16_f32 for bf16 (one
+// instruction for what rne_word + v_perm did in five), the rne_word pair for fp16
+template <typename T> __device__ __forceinline__ uint32_t pack_rne2(f32x2 q);
+template <> __device__ __forceinline__ uint32_t pack_rne2<__hip_bfloat16>(f32x2 q) {
+  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(q, bf16x2));
+}
+template <> __device__ __forceinline__ uint32_t pack_rne2<__half>(f32x2 q) {
+  return __builtin_amdgcn_perm(rne_word<__half>(q.y), rne_word<__half>(q.x), 0x07060302u);
+}
 
 // 16-bit code of a raw score pattern: -0.0 -> 0, [0, 1] -> itself, anything else (negative, > 1, inf, NaN) -> skip
 template <typename T> __device__ __forceinline__ uint32_t raw_code(uint32_t b) {
@@ -253,19 +293,25 @@ __device__ __forceinline__ void row_stat_padded(const uint4 (&w)[2], int nlo, in
 // arg-max of a row without NaN / inf: first class (ascending) holding the wave maximum.  Classes of group g, lane L,
 // slot k are 512 g + 8 L + k, so the winner is the lowest lane whose group-0 maximum equals mx (else the lowest lane
 // of group 1) and the lowest slot of that lane.
+// The slot is found with one ballot per slot of the winning (wave-uniform) group and a scalar bit test of lane L —
+// one v_cmp per slot instead of a compare + select per element of both groups.
 template <int NG>
 __device__ __forceinline__ int row_argmax(const RowStat<NG>& r) {
   const uint64_t blo = __ballot(r.mlo == r.mx);
   const int g = blo != 0 ? 0 : 1;
   const uint64_t b = blo != 0 ? blo : __ballot(r.mhi == r.mx);
   const int L = __builtin_ctzll(b | (1ull << 63));
-  int klo = 7, khi = 7;
+  int k = 7;
+  if (NG == 1 || g == 0) {
 #pragma unroll
-  for (int j = 6; j >= 0; --j) {
-    klo = (r.v[j] == r.mx) ? j : klo;
-    if constexpr (NG == 2) khi = (r.v[8 + j] == r.mx) ? j : khi;
+    for (int j = 6; j >= 0; --j)
+      if ((__ballot(r.v[j] == r.mx) >> L) & 1ull) k = j;
+  } else {
+#pragma unroll
+    for (int j = 6; j >= 0; --j)
+      if ((__ballot(r.v[8 * (NG - 1) + j] == r.mx) >> L) & 1ull) k = j;
   }
-  return 512 * g + 8 * L + __builtin_amdgcn_readlane(g == 0 ? klo : khi, L);
+  return 512 * g + 8 * L + k;
 }
 
 struct SlowRows {
@@ -378,16 +424,17 @@ __device__ __forceinline__ void row_tile(const T* __restrict__ preds, const int6
     const int ama = row_argmax<NG>(ra), amb = row_argmax<NG>(rb);
     float sa = 0.f, sb = 0.f, ia = 0.f, ib = 0.f;
     if constexpr (SOFTMAX) {
-      float acc_a = 0.f, acc_b = 0.f;
+      f32x2 acc = {0.f, 0.f};
+      const f32x2 mx2 = {ra.mx, rb.mx};
 #pragma unroll
       for (int j = 0; j < 8 * NG; ++j) {
-        ra.v[j] = exp_nonpos(ra.v[j] - ra.mx);
-        rb.v[j] = exp_nonpos(rb.v[j] - rb.mx);
-        acc_a += ra.v[j];
-        acc_b += rb.v[j];
+        const f32x2 e = exp_nonpos2(f32x2{ra.v[j], rb.v[j]} - mx2);
+        ra.v[j] = e.x;
+        rb.v[j] = e.y;
+        acc = acc + e;  // per row: the same sequential fp32 order as before
       }
-      sa = wave_sum_uniform(acc_a);
-      sb = wave_sum_uniform(acc_b);
+      sa = wave_sum_uniform(acc.x);
+      sb = wave_sum_uniform(acc.y);
       ia = 1.f / sa;
       ib = 1.f / sb;
       fa = fa && sa == sa;
@@ -409,7 +456,7 @@ __device__ __forceinline__ void row_tile(const T* __restrict__ preds, const int6
     for (int j = 0; j < 8 * NG; ++j) {
       uint32_t packed;
       if constexpr (SOFTMAX) {
-        packed = __builtin_amdgcn_perm(rne_word<T>(div_rn(rb.v[j], sb, ib)), rne_word<T>(div_rn(ra.v[j], sa, ia)), 0x07060302u);
+        packed = pack_rne2<T>(div_rn2(f32x2{ra.v[j], rb.v[j]}, f32x2{sa, sb}, f32x2{ia, ib}));
       } else {
         const uint32_t ca = raw_code<T>(raw_bits<T>(raw[pp][0][j >> 3], j & 7));
         const uint32_t cb = raw_code<T>(raw_bits<T>(raw[pp][1][j >> 3], j & 7));
