@@ -660,13 +660,14 @@ __global__ void __launch_bounds__(kRowThreads, 4) ml_codes_kernel(const T* __res
 // mode_roll_kernel); the last block to finish (ticket) clears the counts for the next batch that uses this state —
 // every block has read them by then.
 constexpr int kClassThreads = 1024;
+constexpr int kTrashBin = kCodes - 1;  // no valid 16-bit score in [0, 1] maps here (bf16 <= 0x3F80, fp16 <= 0x3C00)
 constexpr int64_t kClassChunk = 65528;  // rows per LDS flush: a 16-bit half never overflows (multiple of 8)
 
 template <bool PACKED, int NT = kClassThreads>
 __device__ __forceinline__ void class_flush(uint32_t* __restrict__ s_h, int64_t* __restrict__ neg_hist,
                                             int64_t* __restrict__ pos_hist, bool exclusive, int& lo, int& hi) {
   for (int i = threadIdx.x; i < kCodes; i += NT) {
-    const uint32_t w = s_h[i];
+    const uint32_t w = i == kTrashBin ? 0u : s_h[i];  // the trash bin holds skipped codes (non-PACKED pass)
     if (w) {
       lo = min(lo, i);
       hi = max(hi, i);
@@ -758,16 +759,36 @@ __device__ __forceinline__ void class_hist_block(int64_t vb, int64_t vgrid, cons
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const uint32_t parts[4] = {w[u].x, w[u].y, w[u].z, w[u].w};
+        if constexpr (PACKED) {
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const uint32_t x = (k & 1) ? (parts[k >> 1] >> 16) : (parts[k >> 1] & 0xFFFFu);
-          if (x & 0x8000u) continue;
-          if constexpr (PACKED) atomicAdd(&s_h[x & 0x3FFFu], (x & 0x4000u) ? 0x10000u : 1u);
-          else if (x & 0x4000u) {
-            atomic_add_i64(pos_hist + (x & 0x3FFFu), 1);
-            lo = min(lo, (int)(x & 0x3FFFu));
-            hi = max(hi, (int)(x & 0x3FFFu));
-          } else atomicAdd(&s_h[x & 0x3FFFu], 1u);
+          for (int k = 0; k < 8; ++k) {
+            const uint32_t x = (k & 1) ? (parts[k >> 1] >> 16) : (parts[k >> 1] & 0xFFFFu);
+            if (x & 0x8000u) continue;
+            atomicAdd(&s_h[x & 0x3FFFu], (x & 0x4000u) ? 0x10000u : 1u);
+          }
+        } else {
+          // Branch-free common case: every code is counted into the LDS bin of its value (a skip code into the
+          // never-used trash bin), positives included; the rare positive (1 / C of the codes) is then moved from the
+          // LDS bin to the int64 positive histogram under a wave-uniform test of the whole 16-B word.  Before, every
+          // code took a two-level divergent branch (exec-mask save / restore per code).
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const uint32_t x = (k & 1) ? (parts[k >> 1] >> 16) : (parts[k >> 1] & 0xFFFFu);
+            atomicAdd(&s_h[(x & 0x8000u) ? kTrashBin : (x & 0x3FFFu)], 1u);
+          }
+          const uint32_t anypos = (parts[0] | parts[1] | parts[2] | parts[3]) & 0x40004000u;
+          if (__builtin_expect(__ballot(anypos != 0) != 0, 0) && anypos != 0) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+              const uint32_t x = (k & 1) ? (parts[k >> 1] >> 16) : (parts[k >> 1] & 0xFFFFu);
+              if ((x & 0xC000u) == 0x4000u) {
+                atomicSub(&s_h[x & 0x3FFFu], 1u);
+                atomic_add_i64(pos_hist + (x & 0x3FFFu), 1);
+                lo = min(lo, (int)(x & 0x3FFFu));
+                hi = max(hi, (int)(x & 0x3FFFu));
+              }
+            }
+          }
         }
       }
     }
