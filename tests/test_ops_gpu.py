@@ -85,9 +85,12 @@ def test_curve_hist_multiclass(C, dtype, probs):
     hist = torch.zeros(C, 2, K.N_CODES, dtype=torch.long)
     cm = torch.zeros(C, C, dtype=torch.long)
     g, c, _, _ = _both(K.curve_hist_update, preds, target, hist, "multiclass", -1, cm)
-    # softmax rounding of the fused fp32 kernel may flip a handful of bf16 roundings vs ATen's softmax
+    # probabilities are coded from their raw bits: exact.  Logits: the fused softmax sums exp(x - max) in another fp32
+    # order than ATen's, so a few elements land one 16-bit code away (pinned per element at <= 2e-5 / 1.5e-4 of the
+    # elements by test_curve_hist_codes_vs_aten_softmax_same_device); each moved element changes two bins
     diff = (g[2].cpu() - c[2]).abs().sum().item()
-    assert diff <= max(8, int(1e-3 * N * C)), diff
+    rate = 2e-5 if dtype == torch.bfloat16 else 1.5e-4
+    assert diff == 0 if probs else diff <= max(8, int(2 * rate * N * C)), diff
     assert g[2].sum().item() == c[2].sum().item()
     assert torch.equal(g[5].cpu(), c[5])  # fused argmax confusion matrix is exact
     red_g = K.curve_hist_reduce(g[2]).cpu()
@@ -133,7 +136,9 @@ def test_module_auroc_confmat_gpu_matches_cpu():
             coll.update(logits[i::4].to(dev), target[i::4].to(dev))
         out.append({k: v.cpu() for k, v in coll.compute().items()})
     assert torch.equal(out[0]["cm"], out[1]["cm"])
-    assert abs(out[0]["auroc"].item() - out[1]["auroc"].item()) < 1e-4
+    # ~4 of the 819200 bf16 softmax scores may sit one code away from ATen's (see above); each moves a class AUROC by
+    # at most (crossed pairs) / (P N) ~ 1.5e-6, the macro mean by ~1e-8
+    assert abs(out[0]["auroc"].item() - out[1]["auroc"].item()) < 1e-6
 
 
 def _rare_rows(x, probs):
@@ -161,7 +166,8 @@ def test_curve_hist_multiclass_rare_rows(C, probs):
     g, c, _, _ = _both(K.curve_hist_update, x, target, hist, "multiclass", -1, cm)
     assert torch.equal(g[5].cpu(), c[5])  # confusion matrix incl. NaN / all -inf rows is exact
     diff = (g[2].cpu() - c[2]).abs().sum().item()
-    assert diff <= max(8, int(1e-3 * N * C)), diff
+    # the sprinkled NaN / inf make even the probability batches softmax batches (reference rule): the logits bound
+    assert diff <= max(8, int(2 * 2e-5 * N * C)), diff  # see test_curve_hist_multiclass
     assert g[2].sum().item() == c[2].sum().item()
 
 
@@ -194,7 +200,7 @@ def test_curve_speculation_flips_across_batches():
         res.append((vals, cmm.compute().cpu()))
     assert torch.equal(res[0][1], res[1][1])
     for a, b in zip(res[0][0], res[1][0]):
-        assert abs(a - b) < 1e-4, (res[0][0], res[1][0])
+        assert abs(a - b) < 2e-5, (res[0][0], res[1][0])
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
@@ -855,4 +861,4 @@ def test_curve_small_classes_speculation_and_rare_rows(C, n):
         res.append((vals, cmm.compute().cpu()))
     assert torch.equal(res[0][1], res[1][1])
     for a, b in zip(res[0][0], res[1][0]):
-        assert abs(a - b) < 1e-4 or (a != a and b != b), (res[0][0], res[1][0])
+        assert abs(a - b) < 2e-5 or (a != a and b != b), (res[0][0], res[1][0])
