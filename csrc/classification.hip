@@ -1374,7 +1374,10 @@ void launch_small_two_pass(const T* p, const int64_t* target, int64_t n, int C, 
   int TL = 1;
   while (TL * kSmallVpt < C) TL *= 2;
   // a block loops over 64-row tiles: ~8-16 waves per CU in flight, and one LDS confusion-matrix flush per block
-  const int grid = static_cast<int>(std::min<int64_t>(ntiles, std::max(256, 2048 / TL)));
+  // (8192 / TL blocks: up to 32 waves per CU — at 2048 / TL the one-wave blocks of C <= 16 left the CUs at 8 waves and
+  // the row pass latency-bound, 40 us for 1M x 10 bf16)
+  static const int grid_cap = [] { const char* v = std::getenv("TMX_SMALL_GRID"); return v ? std::atoi(v) : 8192; }();
+  const int grid = static_cast<int>(std::min<int64_t>(ntiles, std::max(256, grid_cap / TL)));
   // confusion-matrix partials per block (C <= 32: at most 4 MiB), summed by the reduce launch: no same-cell atomics
   const bool use_pcm = cm != nullptr && C <= 32;
   auto pcm_t = use_pcm ? at::empty({(int64_t)grid * C * C}, opts.dtype(at::kInt)) : at::Tensor();
@@ -1405,8 +1408,9 @@ void launch_small_two_pass(const T* p, const int64_t* target, int64_t n, int C, 
                      hist, p, C, target, n, mode, speculative, srows, state, cm, code_range, speculative ? mode : nullptr, pp,
                      prange.data_ptr<int>());
   TMX_LAUNCH_CHECK();
-  hipLaunchKernelGGL(class_partial_reduce_kernel, dim3(kCodes / 256 + 1, C), 256, 0, stream(), pp, prange.data_ptr<int>(), splits, hist,
-                     code_range, state, speculative ? mode : nullptr, pcm, grid, cm, C);
+  const int pcm_slices = use_pcm ? std::max(1, std::min(64, grid / 256)) : 0;
+  hipLaunchKernelGGL(class_partial_reduce_kernel, dim3(kCodes / 256 + 1 + pcm_slices, C), 256, 0, stream(), pp, prange.data_ptr<int>(),
+                     splits, hist, code_range, state, speculative ? mode : nullptr, pcm, grid, cm, C, pcm_slices);
   TMX_LAUNCH_CHECK();
 }
 

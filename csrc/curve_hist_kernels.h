@@ -902,8 +902,29 @@ __global__ void __launch_bounds__(256) class_partial_reduce_kernel(const uint32_
                                                                    int splits, int64_t* __restrict__ hist, int* __restrict__ code_range,
                                                                    int* __restrict__ state, int* __restrict__ roll_mode,
                                                                    const uint32_t* __restrict__ pcm, int pcm_blocks,
-                                                                   int64_t* __restrict__ confmat, int C) {
+                                                                   int64_t* __restrict__ confmat, int C, int pcm_slices) {
   const int c = blockIdx.y;
+  if (blockIdx.x > kCodes / 256) {
+    // confusion-matrix row c: slice p of the row pass's per-block partials, 256 / C thread groups stride over the
+    // slice's blocks, an LDS fold per cell, one int64 atomic per (slice, cell) — a serial loop over thousands of
+    // partials per cell was the reduce launch's cost
+    __shared__ uint64_t s_acc[256];
+    const int p = blockIdx.x - (kCodes / 256 + 1);
+    const int G = 256 / C, cell = threadIdx.x % C, g = threadIdx.x / C;
+    const int per = (pcm_blocks + pcm_slices - 1) / pcm_slices;
+    const int b0 = p * per, b1 = min(pcm_blocks, b0 + per);
+    uint64_t acc = 0;
+    if (g < G)
+      for (int b = b0 + g; b < b1; b += G) acc += pcm[((int64_t)b * C + c) * C + cell];
+    s_acc[threadIdx.x] = acc;
+    __syncthreads();
+    if (threadIdx.x < C) {
+      uint64_t tot = 0;
+      for (int q = 0; q < G; ++q) tot += s_acc[q * C + threadIdx.x];
+      if (tot) atomic_add_i64(confmat + (int64_t)c * C + threadIdx.x, static_cast<int64_t>(tot));
+    }
+    return;
+  }
   if (blockIdx.x == kCodes / 256) {
     if (threadIdx.x == 0 && code_range != nullptr) {
       int lo = kCodes, hi = -1;
@@ -916,11 +937,6 @@ __global__ void __launch_bounds__(256) class_partial_reduce_kernel(const uint32_
         atomicMin(code_range + 2 * c, lo);
         atomicMax(code_range + 2 * c + 1, hi);
       }
-    }
-    if (pcm != nullptr && threadIdx.x < C) {
-      uint64_t acc = 0;
-      for (int b = 0; b < pcm_blocks; ++b) acc += pcm[((int64_t)b * C + c) * C + threadIdx.x];
-      if (acc) confmat[(int64_t)c * C + threadIdx.x] += static_cast<int64_t>(acc);
     }
     if (c == 0 && threadIdx.x == 0) {
       state[0] = state[1] = 0;
