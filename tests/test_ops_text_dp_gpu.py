@@ -87,3 +87,39 @@ def test_text_modules_gpu_equal_cpu():
                 assert torch.allclose(a[k].float(), b[k].float().cpu(), atol=1e-6), k
         else:
             assert torch.allclose(a.float(), b.float().cpu(), atol=1e-6)
+
+
+@pytest.mark.parametrize("sub", [1, 2, 5])
+@pytest.mark.parametrize("n_pairs", [1, 37, 600])
+def test_levenshtein_beam_gpu_identical_to_host(sub, n_pairs):
+    """EditDistance's Tercom beam DP on the GPU (one thread per pair) vs the host op: identical integers, including
+    empty strings, pairs far off the diagonal (|n - m| > beam) and a long reference (beam widened by m / 2n)."""
+    rnd = random.Random(sub * 1000 + n_pairs)
+    preds = [_sent(rnd, 1, 40) for _ in range(n_pairs)]
+    refs = [_sent(rnd, 1, 40) for _ in range(n_pairs)]
+    preds[0] = ""
+    if n_pairs > 2:
+        refs[1] = ""
+        preds[2] = "ab"
+        refs[2] = _sent(rnd, 60, 80)  # ratio m / n >> 50: wide beam
+    p, po = _pack(preds)
+    r, ro = _pack(refs)
+    host = torch.ops.tmx.levenshtein_beam_batch(p, po, r, ro, 1, 1, sub)
+    dev = torch.ops.tmx.levenshtein_beam_gpu(p.cuda(), po.cuda(), r.cuda(), ro.cuda(), 1, 1, sub, max(len(x) for x in refs))
+    assert torch.equal(dev.cpu(), host)
+
+
+def test_edit_distance_module_gpu_states_equal_cpu():
+    import torchmetrics_forked_amd as tm
+    from torchmetrics_forked_amd.functional.text import edit as edit_fn
+
+    rnd = random.Random(3)
+    batches = [([_sent(rnd) for _ in range(120)], [_sent(rnd) for _ in range(120)]) for _ in range(3)]
+    assert sum(len(x) for x in batches[0][1]) >= edit_fn.GPU_EDIT_MIN_CHARS  # the device path is taken
+    for red in ("mean", "none"):
+        g = tm.text.EditDistance(substitution_cost=2, reduction=red).cuda()
+        c = tm.text.EditDistance(substitution_cost=2, reduction=red)
+        for p, t in batches:
+            g.update(p, t)
+            c.update(p, t)
+        torch.testing.assert_close(g.compute().cpu(), c.compute(), rtol=0, atol=0)

@@ -612,3 +612,46 @@ def test_differentiability(name):
         if leaked:  # a grad-carrying output of a non-differentiable metric must at least not reach the inputs
             sum(o.double().sum() for o in leaked).backward()
             assert p.grad is None, "non-differentiable metric propagated a gradient to preds"
+
+
+def _to_dev(x: Any, dev: str) -> Any:
+    if isinstance(x, Tensor):
+        return x.to(dev)
+    if isinstance(x, dict):
+        return {k: _to_dev(v, dev) for k, v in x.items()}
+    if isinstance(x, (list, tuple)):
+        return type(x)(_to_dev(v, dev) for v in x)
+    return x
+
+
+def _run_on(spec: Spec, batches: List[tuple], dev: str) -> Any:
+    torch.manual_seed(7)
+    m = spec.make(tm).to(dev)
+    vals = []
+    for b in batches:
+        b = _to_dev(b, dev)
+        if spec.batch:
+            vals.append(m(*b))
+        else:
+            m.update(*b)
+    if spec.seeded:
+        torch.manual_seed(11)
+    return vals, m.compute()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", sorted(SPECS))
+def test_gpu_vs_cpu(name):
+    """Every spec with its states on the MI355X (the native update / compute paths) against the same module on the
+    CPU: per-batch forward values and the final value."""
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    spec = SPECS[name]
+    batches = _data(spec.data)
+    g_vals, g_res = _run_on(spec, batches, "cuda")
+    c_vals, c_res = _run_on(spec, batches, "cpu")
+    # GPU reductions run in other orders (atomics, tree sums): fp32 agreement, not bit equality
+    atol = max(spec.atol, 1e-4)
+    for a, b in zip(g_vals, c_vals):
+        _values_equal(a, b, atol)
+    _values_equal(g_res, c_res, atol)

@@ -11,11 +11,19 @@ from torchmetrics_forked_amd import ops
 from torchmetrics_forked_amd.functional.text.helper import _pack_codepoints
 
 
+# characters (reference side) above which a GPU-resident metric runs the pair DPs on the device
+GPU_EDIT_MIN_CHARS = 2048
+
+
 def _edit_distance_update(
     preds: Union[str, Sequence[str]],
     target: Union[str, Sequence[str]],
     substitution_cost: int = 1,
+    device: Optional[torch.device] = None,
 ) -> Tensor:
+    """Per-pair distances.  With ``device`` on the GPU (a GPU-resident ``EditDistance``) and enough text, the beam DPs
+    run there (``tmx::levenshtein_beam_gpu``, one thread per pair, identical integers) and the scores stay on the
+    device; otherwise the host op."""
     if isinstance(preds, str):
         preds = [preds]
     if isinstance(target, str):
@@ -31,6 +39,10 @@ def _edit_distance_update(
     ops.require()
     p, p_off = _pack_codepoints(preds)
     t, t_off = _pack_codepoints(target)
+    if device is not None and device.type == "cuda" and t.numel() >= GPU_EDIT_MIN_CHARS and ops.use_native(torch.empty(0, device=device)):
+        d = [x.to(device, non_blocking=True) for x in (p, p_off, t, t_off)]
+        max_ref = max((len(x) for x in target), default=0)
+        return torch.ops.tmx.levenshtein_beam_gpu(*d, 1, 1, int(substitution_cost), max_ref).int()
     return torch.ops.tmx.levenshtein_beam_batch(p, p_off, t, t_off, 1, 1, int(substitution_cost)).int()
 
 

@@ -43,7 +43,7 @@ class EditDistance(Metric):
             self.add_state("num_elements", default=torch.tensor(0), dist_reduce_fx="sum")
 
     def update(self, preds: Union[str, Sequence[str]], target: Union[str, Sequence[str]]) -> None:
-        distance = _edit_distance_update(preds, target, self.substitution_cost).to(self.device)
+        distance = _edit_distance_update(preds, target, self.substitution_cost, device=self.device).to(self.device)
         if self.reduction in ("none", None):
             self.edit_scores_list.append(distance)
         else:
