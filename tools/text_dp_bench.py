@@ -1,5 +1,6 @@
 """GPU text kernels of csrc/text_dp.hip vs their host ops (one MI355X + the box's CPU cores):
   * EED pair DPs: ``tmx::eed_gpu`` (one thread per pair, bit-identical) vs ``tmx::eed_batch`` (parallel host);
+  * EditDistance beam DPs: ``tmx::levenshtein_beam_gpu`` vs ``tmx::levenshtein_beam_batch``;
   * chrF character n-gram overlap (order 6) and ROUGE-2 word overlap: ``tmx::ngram_overlap_gpu`` vs ``tmx::ngram_overlap``.
 GPU times include the host-to-device copies of the packed ids and the copy back.  Prints one JSON line."""
 import json
@@ -53,6 +54,17 @@ def main() -> None:
     a = torch.ops.tmx.eed_batch(h, ho, r, ro, *args)
     b = torch.ops.tmx.eed_gpu(h.to(dev), ho.to(dev), r.to(dev), ro.to(dev), *args, mx).cpu()
     out["eed_identical"] = bool(torch.equal(a, b))
+    # EditDistance beam DP (substitution cost 2)
+    preds = [sent(rnd, 15, 40) for _ in range(n)]
+    tgts = [sent(rnd, 15, 40) for _ in range(n)]
+    p, po = _pack_codepoints(preds)
+    t, to = _pack_codepoints(tgts)
+    mr = max(len(x) for x in tgts)
+    out["edit_pairs"] = n
+    out["edit_host_ms"] = round(best_of(lambda: torch.ops.tmx.levenshtein_beam_batch(p, po, t, to, 1, 1, 2)), 2)
+    out["edit_gpu_ms"] = round(best_of(lambda: torch.ops.tmx.levenshtein_beam_gpu(p.to(dev), po.to(dev), t.to(dev), to.to(dev), 1, 1, 2, mr).cpu()), 2)
+    out["edit_identical"] = bool(torch.equal(torch.ops.tmx.levenshtein_beam_batch(p, po, t, to, 1, 1, 2),
+                                             torch.ops.tmx.levenshtein_beam_gpu(p.to(dev), po.to(dev), t.to(dev), to.to(dev), 1, 1, 2, mr).cpu()))
     # n-gram overlap
     for name, tok, order, nh in (("chrf_char6", list, 6, 20000), ("rouge2_word", str.split, 2, 50000)):
         hs, rs, groups = [], [], [0]
