@@ -123,3 +123,69 @@ def test_edit_distance_module_gpu_states_equal_cpu():
             g.update(p, t)
             c.update(p, t)
         torch.testing.assert_close(g.compute().cpu(), c.compute(), rtol=0, atol=0)
+
+
+def _ter_pairs(rnd, n_pairs, lo=2, hi=25):
+    refs, hyps = [], []
+    for k in range(n_pairs):
+        r = _sent(rnd, lo, hi).split()
+        h = list(r)
+        # block moves, substitutions, drops: the shift search has work to do
+        if len(h) > 4:
+            s = rnd.randrange(len(h) - 2)
+            ln = rnd.randint(1, min(4, len(h) - s))
+            blk = h[s:s + ln]
+            del h[s:s + ln]
+            t = rnd.randrange(len(h) + 1)
+            h[t:t] = blk
+        for _ in range(rnd.randint(0, 3)):
+            if h:
+                h[rnd.randrange(len(h))] = rnd.choice(_WORDS)
+        if k % 7 == 3 and h:
+            h.pop()
+        refs.append(r)
+        hyps.append(h)
+    return refs, hyps
+
+
+@pytest.mark.parametrize("n_pairs,hi", [(1, 12), (64, 25), (700, 30), (40, 120)])
+def test_ter_gpu_identical_to_host(n_pairs, hi):
+    """Tercom shift search on the GPU (one wave per pair, candidate DPs across lanes) vs the host op: identical edit
+    counts, incl. empty hypotheses / references and long repetitive sentences that hit the 1000-candidate limit."""
+    from torchmetrics_forked_amd.functional.text.helper import _pack as pack_ids
+    from torchmetrics_forked_amd.functional.text.helper import _Vocab
+
+    rnd = random.Random(n_pairs + hi)
+    refs, hyps = _ter_pairs(rnd, n_pairs, 2, hi)
+    if n_pairs > 3:
+        hyps[1] = []
+        refs[2] = []
+        refs[3] = ["the"] * 60
+        hyps[3] = ["the", "a"] * 30
+    vocab = _Vocab()
+    a, ao = pack_ids(refs, vocab)
+    b, bo = pack_ids(hyps, vocab)
+    groups = torch.arange(n_pairs + 1)
+    host, _ = torch.ops.tmx.ter_batch(b, bo, a, ao, groups)
+    dev = torch.ops.tmx.ter_gpu(a.int().cuda(), ao.cuda(), b.int().cuda(), bo.cuda(), max(map(len, refs)), max(map(len, hyps)))
+    assert torch.equal(dev.cpu(), host), (dev.cpu() - host).abs().max()
+
+
+def test_ter_module_gpu_states_equal_cpu():
+    import torchmetrics_forked_amd as tm
+    from torchmetrics_forked_amd.functional.text import ter as ter_fn
+
+    rnd = random.Random(5)
+    batches = []
+    for _ in range(2):
+        refs, hyps = _ter_pairs(rnd, 150)
+        batches.append(([" ".join(h) for h in hyps], [[" ".join(r), _sent(rnd)] for r in refs]))
+    assert 2 * 150 >= ter_fn.GPU_TER_MIN_PAIRS  # the device path is taken
+    g = tm.text.TranslationEditRate(return_sentence_level_score=True).cuda()
+    c = tm.text.TranslationEditRate(return_sentence_level_score=True)
+    for p, t in batches:
+        g.update(p, t)
+        c.update(p, t)
+    (gs, gsent), (cs, csent) = g.compute(), c.compute()
+    torch.testing.assert_close(gs.cpu(), cs, rtol=0, atol=0)
+    torch.testing.assert_close(gsent.cpu(), csent, rtol=0, atol=0)

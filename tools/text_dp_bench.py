@@ -65,6 +65,30 @@ def main() -> None:
     out["edit_gpu_ms"] = round(best_of(lambda: torch.ops.tmx.levenshtein_beam_gpu(p.to(dev), po.to(dev), t.to(dev), to.to(dev), 1, 1, 2, mr).cpu()), 2)
     out["edit_identical"] = bool(torch.equal(torch.ops.tmx.levenshtein_beam_batch(p, po, t, to, 1, 1, 2),
                                              torch.ops.tmx.levenshtein_beam_gpu(p.to(dev), po.to(dev), t.to(dev), to.to(dev), 1, 1, 2, mr).cpu()))
+    # TER shift search (one reference per hypothesis, block moves + substitutions)
+    nt = 4096
+    refs_w, hyps_w = [], []
+    for _ in range(nt):
+        r = sent(rnd, 10, 30).split()
+        h = list(r)
+        s0 = rnd.randrange(len(h) - 2)
+        blk = h[s0:s0 + 3]
+        del h[s0:s0 + 3]
+        t0 = rnd.randrange(len(h) + 1)
+        h[t0:t0] = blk
+        h[rnd.randrange(len(h))] = rnd.choice(WORDS)
+        refs_w.append(r)
+        hyps_w.append(h)
+    vocab_t = _Vocab()
+    ta, tao = _pack(refs_w, vocab_t)
+    tb, tbo = _pack(hyps_w, vocab_t)
+    tg = torch.arange(nt + 1)
+    ma, mb = max(map(len, refs_w)), max(map(len, hyps_w))
+    out["ter_pairs"] = nt
+    out["ter_host_ms"] = round(best_of(lambda: torch.ops.tmx.ter_batch(tb, tbo, ta, tao, tg)), 2)
+    out["ter_gpu_ms"] = round(best_of(lambda: torch.ops.tmx.ter_gpu(ta.int().to(dev), tao.to(dev), tb.int().to(dev), tbo.to(dev), ma, mb).cpu()), 2)
+    out["ter_identical"] = bool(torch.equal(torch.ops.tmx.ter_batch(tb, tbo, ta, tao, tg)[0],
+                                            torch.ops.tmx.ter_gpu(ta.int().to(dev), tao.to(dev), tb.int().to(dev), tbo.to(dev), ma, mb).cpu()))
     # n-gram overlap
     for name, tok, order, nh in (("chrf_char6", list, 6, 20000), ("rouge2_word", str.split, 2, 50000)):
         hs, rs, groups = [], [], [0]

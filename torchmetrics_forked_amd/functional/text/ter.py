@@ -87,12 +87,35 @@ def _compute_ter_score_from_statistics(num_edits: Tensor, tgt_length: Tensor) ->
     return tensor(0.0)
 
 
-def _ter_sentence_stats(pred_words: List[List[str]], target_words: List[List[List[str]]]) -> Tuple[Tensor, Tensor]:
-    """Best edit count and mean reference length per hypothesis (fp64 ``[n]`` each)."""
+# (reference, hypothesis) pairs above which a GPU-resident metric runs the shift searches on the device
+GPU_TER_MIN_PAIRS = 256
+
+
+def _ter_sentence_stats(
+    pred_words: List[List[str]], target_words: List[List[List[str]]], device: Optional[torch.device] = None
+) -> Tuple[Tensor, Tensor]:
+    """Best edit count and mean reference length per hypothesis (fp64 ``[n]`` each).  Host op ``tmx::ter_batch``;
+    with ``device`` on the GPU and enough pairs, ``tmx::ter_gpu`` (one wave per (reference, hypothesis) pair, the
+    same shift search, identical counts) and the best-of-references fold on the device."""
     ops.require()
     vocab = _Vocab()
-    hyp, hyp_off = _pack(pred_words, vocab)
     flat_refs = [r for refs in target_words for r in refs]
+    if device is not None and device.type == "cuda" and len(flat_refs) >= GPU_TER_MIN_PAIRS and ops.use_native(torch.empty(0, device=device)):
+        owner = [i for i, refs in enumerate(target_words) for _ in refs]
+        a, a_off = _pack(flat_refs, vocab)
+        b, b_off = _pack([pred_words[i] for i in owner], vocab)
+        d = [a.int().to(device, non_blocking=True), a_off.to(device, non_blocking=True), b.int().to(device, non_blocking=True),
+             b_off.to(device, non_blocking=True)]
+        max_a = max((len(r) for r in flat_refs), default=0)
+        max_b = max((len(h) for h in pred_words), default=0)
+        edits = torch.ops.tmx.ter_gpu(*d, max_a, max_b)
+        n = len(target_words)
+        best = torch.full((n,), 2e16, dtype=torch.float64, device=device).scatter_reduce(
+            0, torch.tensor(owner, dtype=torch.long).to(device, non_blocking=True), edits, reduce="amin"
+        )
+        lens = [sum(len(r) for r in refs) / len(refs) if refs else 0.0 for refs in target_words]
+        return best, torch.tensor(lens, dtype=torch.float64).to(device, non_blocking=True)
+    hyp, hyp_off = _pack(pred_words, vocab)
     ref, ref_off = _pack(flat_refs, vocab)
     groups = torch.tensor([0] + [len(r) for r in target_words], dtype=torch.long).cumsum(0)
     return torch.ops.tmx.ter_batch(hyp, hyp_off, ref, ref_off, groups)
@@ -105,6 +128,7 @@ def _ter_update(
     total_num_edits: Tensor,
     total_tgt_length: Tensor,
     sentence_ter: Optional[List[Tensor]] = None,
+    device: Optional[torch.device] = None,
 ) -> Tuple[Tensor, Tensor, Optional[List[Tensor]]]:
     target, preds = _validate_inputs(target, preds)
     pairs = list(zip(preds, target))
@@ -112,13 +136,18 @@ def _ter_update(
         return total_num_edits, total_tgt_length, sentence_ter
     pw = [_preprocess_sentence(p, tokenizer).split() for p, _ in pairs]
     tw = [[_preprocess_sentence(t, tokenizer).split() for t in tgt] for _, tgt in pairs]
-    edits, lengths = _ter_sentence_stats(pw, tw)
+    edits, lengths = _ter_sentence_stats(pw, tw, device)
     edits_f, lengths_f = edits.float(), lengths.float()
     total_num_edits = total_num_edits + edits_f.sum().to(total_num_edits.dtype)
     total_tgt_length = total_tgt_length + lengths_f.sum().to(total_tgt_length.dtype)
     if sentence_ter is not None:
-        for e, ln in zip(edits_f, lengths_f):
-            sentence_ter.append(_compute_ter_score_from_statistics(e, ln).unsqueeze(0))
+        # _compute_ter_score_from_statistics per sentence, vectorised (no host read per sentence on the GPU)
+        score = torch.where(
+            (lengths_f > 0) & (edits_f > 0),
+            edits_f / lengths_f.clamp_min(1e-30),
+            torch.where((lengths_f == 0) & (edits_f > 0), torch.ones_like(edits_f), torch.zeros_like(edits_f)),
+        )
+        sentence_ter.extend(score.unsqueeze(1).unbind(0))
     return total_num_edits, total_tgt_length, sentence_ter
 
 

@@ -146,7 +146,7 @@ class TranslationEditRate(Metric):
 
     def update(self, preds: Union[str, Sequence[str]], target: Sequence[Union[str, Sequence[str]]]) -> None:
         sent: Optional[List[Tensor]] = [] if self.sentence_ter is not None else None
-        edits, length, sent = _ter_update(preds, target, self.tokenizer, tensor(0.0), tensor(0.0), sent)
+        edits, length, sent = _ter_update(preds, target, self.tokenizer, tensor(0.0), tensor(0.0), sent, device=self.device)
         self.total_num_edits += edits.to(self.total_num_edits)
         self.total_tgt_len += length.to(self.total_tgt_len)
         if self.sentence_ter is not None and sent:
