@@ -75,9 +75,14 @@ template <> __device__ __forceinline__ int score_code<__half>(uint16_t b) {
 // Measured on MI355X, 65536 x 1000 bf16 logits (tools/kexp/curve_hist_exp.hip, profiles/kexp_rowpass.json): row
 // pass 63 us vs 129 us for the previous one-wave-per-row design; class pass 32 us.
 // ---------------------------------------------------------------------------------------------------------
-constexpr int kRowThreads = 512;
+// Rows per tile (two row pairs per wave): 32 rows -> 512-thread blocks with a 64-KiB LDS image (2 blocks per CU);
+// 16 rows -> 256 threads and 32 KiB (4 per CU) was slower.  Compile-time switch for A/B runs.
+#ifndef TMX_ROW_TILE_ROWS
+#define TMX_ROW_TILE_ROWS 32  // measured: 16-row tiles 70.7 us vs 64.0 us at 65536 x 1000 bf16 (profiles/row_tile_ab_r3.json)
+#endif
+constexpr int kTileRows = TMX_ROW_TILE_ROWS;
+constexpr int kRowThreads = kTileRows * 16;
 constexpr int kRowWaves = kRowThreads / kWave;
-constexpr int kTileRows = 32;          // rows per tile: 16 row pairs, 2 per wave
 constexpr int kSlots = kTileRows / 2;  // pair slots = dwords per class per tile (64-B segment of a class row)
 
 template <typename T> __device__ __forceinline__ void unpack8(const uint4& w, float* v);
