@@ -665,6 +665,11 @@ __global__ void __launch_bounds__(kRowThreads, 4) ml_codes_kernel(const T* __res
 // mode_roll_kernel); the last block to finish (ticket) clears the counts for the next batch that uses this state —
 // every block has read them by then.
 constexpr int kClassThreads = 1024;
+// 16-B code vectors in flight per thread per iteration (a 65536-row class is 8 vectors per thread of 1024)
+#ifndef TMX_CLASS_UNROLL
+#define TMX_CLASS_UNROLL 8
+#endif
+constexpr int kClassUnroll = TMX_CLASS_UNROLL;
 constexpr int kTrashBin = kCodes - 1;  // no valid 16-bit score in [0, 1] maps here (bf16 <= 0x3F80, fp16 <= 0x3C00)
 constexpr int64_t kClassChunk = 65528;  // rows per LDS flush: a 16-bit half never overflows (multiple of 8)
 
@@ -756,13 +761,13 @@ __device__ __forceinline__ void class_hist_block(int64_t vb, int64_t vgrid, cons
   constexpr int64_t kChunkV = PACKED ? kClassChunk / 8 : (int64_t{1} << 62);
   for (int64_t cb = v0; cb < v1; cb += kChunkV) {
     const int64_t ce = cb + kChunkV < v1 ? cb + kChunkV : v1;
-    for (int64_t v = cb + threadIdx.x; v < ce; v += 4 * NT) {
-      uint4 w[4];
+    for (int64_t v = cb + threadIdx.x; v < ce; v += kClassUnroll * NT) {
+      uint4 w[kClassUnroll];
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
+      for (int u = 0; u < kClassUnroll; ++u)
         w[u] = (v + u * NT < ce) ? col[v + u * NT] : make_uint4(0x80008000u, 0x80008000u, 0x80008000u, 0x80008000u);
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < kClassUnroll; ++u) {
         const uint32_t parts[4] = {w[u].x, w[u].y, w[u].z, w[u].w};
         if constexpr (PACKED) {
 #pragma unroll
