@@ -30,6 +30,9 @@
 #include <c10/hip/HIPGuard.h>
 
 #include "common.h"
+
+#include <map>
+#include <mutex>
 #include "curve_hist_kernels.h"
 
 namespace tmx {
@@ -1467,12 +1470,28 @@ void launch_class_pass(const uint32_t* cptr, int64_t n, int C, int ld, const T* 
   TMX_LAUNCH_CHECK();
 }
 
+// Class-major code scratch of the two-pass route, cached per (device, stream) and grown on demand (never freed).  Taken
+// from the caching allocator per update it was re-allocated (hipMalloc, ~200 us of host time) on the first update after
+// a compute(), whose temporaries had split the cached block (tools/alloc_probe.py).  Work on one stream is ordered, so
+// one buffer per stream is race-free.  Under HIP-graph capture the allocator is used (the graph's private pool).
+at::Tensor codes_scratch(const at::TensorOptions& opts, int64_t elems) {
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  TMX_CHECK_HIP(hipStreamIsCapturing(stream(), &cap));
+  if (cap != hipStreamCaptureStatusNone) return at::empty({elems}, opts.dtype(at::kShort));
+  static std::mutex mu;
+  static auto* cache = new std::map<std::pair<int, hipStream_t>, at::Tensor>();  // leaked: no teardown-order issue
+  std::lock_guard<std::mutex> lock(mu);
+  at::Tensor& t = (*cache)[{static_cast<int>(opts.device().index()), stream()}];
+  if (!t.defined() || t.numel() < elems) t = at::empty({elems}, opts.dtype(at::kShort));
+  return t.narrow(0, 0, elems);
+}
+
 template <typename T, bool PADDED>
 void launch_two_pass(const T* p, const int64_t* target, int64_t n, int C, int ld, int* mode, int* state, bool speculative,
                      int64_t ignore_index, bool has_ignore, int64_t* hist, int64_t* cm, int* err, const at::TensorOptions& opts,
                      int* code_range) {
   const int64_t n_pad = (n + kTileRows - 1) / kTileRows * kTileRows;
-  auto codes = at::empty({(int64_t)C * n_pad}, opts.dtype(at::kShort));
+  auto codes = codes_scratch(opts, (int64_t)C * n_pad);
   auto slow_rows = at::empty({2 * n}, opts.dtype(at::kInt));
   uint32_t* cptr = reinterpret_cast<uint32_t*>(codes.data_ptr());
   int* srows = slow_rows.data_ptr<int>();

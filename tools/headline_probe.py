@@ -61,10 +61,17 @@ if os.environ.get("TMX_PROBE_PROFILE"):
     torch.cuda.synchronize()
     from torch.profiler import ProfilerActivity, profile
 
-    with profile(activities=[ProfilerActivity.CPU], with_stack=False) as prof:
+    with profile(activities=[ProfilerActivity.CPU], with_stack=True) as prof:
         coll2.update(*pool[0])
     print("=== first update after reset ===")
     print(prof.key_averages().table(sort_by="cpu_time_total", row_limit=25))
+    print("=== first update after reset: stacks of copies / aranges / fills ===")
+    for ev in prof.key_averages(group_by_stack_n=12):
+        if ev.key in ("aten::copy_", "aten::arange", "aten::cat", "aten::fill_", "aten::zero_", "aten::empty", "aten::add"):
+            print(ev.key, round(ev.cpu_time_total, 1), "us")
+            for fr in ev.stack:
+                if "torchmetrics_forked_amd" in fr:
+                    print("    ", fr)
     with profile(activities=[ProfilerActivity.CPU]) as prof:
         coll2.update(*pool[1])
     print("=== steady update ===")
