@@ -87,3 +87,28 @@ if os.environ.get("TMX_PROBE_PROFILE"):
     coll2.update(*pool[0])
     pr.disable()
     pstats.Stats(pr).sort_stats("cumulative").print_stats(30)
+
+if os.environ.get("TMX_PROBE_COMPUTE"):
+    # host-side op breakdown of the collection compute() that closes the timed window
+    coll3 = tm.MetricCollection({"auroc": tm.MulticlassAUROC(num_classes=C), "confmat": tm.MulticlassConfusionMatrix(num_classes=C)}).to(dev)
+    for i in range(6):
+        coll3.update(*pool[i % 4])
+    coll3.compute()
+    coll3.reset()
+    for i in range(6):
+        coll3.update(*pool[i % 4])
+    torch.cuda.synchronize()
+    from torch.profiler import ProfilerActivity, profile
+
+    with profile(activities=[ProfilerActivity.CPU], with_stack=True) as prof:
+        coll3.compute()
+        torch.cuda.synchronize()
+    print("=== compute ===")
+    print(prof.key_averages().table(sort_by="cpu_time_total", row_limit=30))
+    for ev in prof.key_averages(group_by_stack_n=10):
+        if ev.key in ("aten::copy_", "aten::to", "aten::cat", "aten::fill_", "aten::zero_", "aten::item", "aten::_local_scalar_dense",
+                      "aten::stack", "aten::clone", "aten::div", "aten::mean"):
+            print(ev.key, round(ev.cpu_time_total, 1), "us", ev.count)
+            for fr in ev.stack[:6]:
+                if "torchmetrics_forked_amd" in fr:
+                    print("    ", fr)
