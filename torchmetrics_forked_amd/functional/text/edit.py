@@ -39,9 +39,11 @@ def _edit_distance_update(
     ops.require()
     p, p_off = _pack_codepoints(preds)
     t, t_off = _pack_codepoints(target)
-    if device is not None and device.type == "cuda" and t.numel() >= GPU_EDIT_MIN_CHARS and ops.use_native(torch.empty(0, device=device)):
+    max_ref = max((len(x) for x in target), default=0)
+    if (device is not None and device.type == "cuda" and t.numel() >= GPU_EDIT_MIN_CHARS
+            and (max_ref + 1) * len(target) * 8 <= (1 << 30)  # one int64 DP row per pair in the scratch
+            and ops.use_native(torch.empty(0, device=device))):
         d = [x.to(device, non_blocking=True) for x in (p, p_off, t, t_off)]
-        max_ref = max((len(x) for x in target), default=0)
         return torch.ops.tmx.levenshtein_beam_gpu(*d, 1, 1, int(substitution_cost), max_ref).int()
     return torch.ops.tmx.levenshtein_beam_batch(p, p_off, t, t_off, 1, 1, int(substitution_cost)).int()
 

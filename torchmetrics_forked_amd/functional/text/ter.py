@@ -100,14 +100,15 @@ def _ter_sentence_stats(
     ops.require()
     vocab = _Vocab()
     flat_refs = [r for refs in target_words for r in refs]
-    if device is not None and device.type == "cuda" and len(flat_refs) >= GPU_TER_MIN_PAIRS and ops.use_native(torch.empty(0, device=device)):
+    max_a = max((len(r) for r in flat_refs), default=0)
+    max_b = max((len(h) for h in pred_words), default=0)
+    if (device is not None and device.type == "cuda" and len(flat_refs) >= GPU_TER_MIN_PAIRS and max(max_a, max_b) < 1024
+            and ops.use_native(torch.empty(0, device=device))):  # longer sentences: the host op (scratch per wave ~ len^2)
         owner = [i for i, refs in enumerate(target_words) for _ in refs]
         a, a_off = _pack(flat_refs, vocab)
         b, b_off = _pack([pred_words[i] for i in owner], vocab)
         d = [a.int().to(device, non_blocking=True), a_off.to(device, non_blocking=True), b.int().to(device, non_blocking=True),
              b_off.to(device, non_blocking=True)]
-        max_a = max((len(r) for r in flat_refs), default=0)
-        max_b = max((len(h) for h in pred_words), default=0)
         edits = torch.ops.tmx.ter_gpu(*d, max_a, max_b)
         n = len(target_words)
         best = torch.full((n,), 2e16, dtype=torch.float64, device=device).scatter_reduce(
