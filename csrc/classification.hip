@@ -1480,12 +1480,28 @@ at::Tensor codes_scratch(const at::TensorOptions& opts, int64_t elems) {
   hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
   TMX_CHECK_HIP(hipStreamIsCapturing(stream(), &cap));
   if (cap != hipStreamCaptureStatusNone) return at::empty({elems}, opts.dtype(at::kShort));
+  // At most kMaxScratch (device, stream) entries, least recently used evicted: a buffer goes back to the caching
+  // allocator, which only hands it out again on the stream it was allocated on (stream-ordered, so safe).
+  constexpr size_t kMaxScratch = 4;
+  struct Entry {
+    at::Tensor t;
+    uint64_t used;
+  };
   static std::mutex mu;
-  static auto* cache = new std::map<std::pair<int, hipStream_t>, at::Tensor>();  // leaked: no teardown-order issue
+  static uint64_t tick = 0;
+  static auto* cache = new std::map<std::pair<int, hipStream_t>, Entry>();  // leaked: no teardown-order issue
   std::lock_guard<std::mutex> lock(mu);
-  at::Tensor& t = (*cache)[{static_cast<int>(opts.device().index()), stream()}];
-  if (!t.defined() || t.numel() < elems) t = at::empty({elems}, opts.dtype(at::kShort));
-  return t.narrow(0, 0, elems);
+  const std::pair<int, hipStream_t> key{static_cast<int>(opts.device().index()), stream()};
+  if (cache->find(key) == cache->end() && cache->size() >= kMaxScratch) {
+    auto lru = cache->begin();
+    for (auto it = cache->begin(); it != cache->end(); ++it)
+      if (it->second.used < lru->second.used) lru = it;
+    cache->erase(lru);
+  }
+  Entry& e = (*cache)[key];
+  e.used = ++tick;
+  if (!e.t.defined() || e.t.numel() < elems) e.t = at::empty({elems}, opts.dtype(at::kShort));
+  return e.t.narrow(0, 0, elems);
 }
 
 template <typename T, bool PADDED>

@@ -862,3 +862,32 @@ def test_curve_small_classes_speculation_and_rare_rows(C, n):
     assert torch.equal(res[0][1], res[1][1])
     for a, b in zip(res[0][0], res[1][0]):
         assert abs(a - b) < 2e-5 or (a != a and b != b), (res[0][0], res[1][0])
+
+
+def test_curve_scratch_cache_across_streams():
+    """The two-pass route caches its class-major code scratch per (device, stream), at most 4 entries (LRU): metrics
+    updated on six different streams (forcing evictions) give the same histograms as one update sequence on the
+    default stream."""
+    import torchmetrics_forked_amd as tm
+
+    C, N = 1000, 4096
+    g = torch.Generator().manual_seed(11)
+    batches = [(torch.randn(N, C, generator=g).bfloat16().cuda(), torch.randint(0, C, (N,), generator=g).cuda()) for _ in range(6)]
+    ref = tm.MulticlassAUROC(num_classes=C).cuda()
+    for x, t in batches:
+        ref.update(x, t)
+    streams = [torch.cuda.Stream() for _ in range(6)]
+    ms = [tm.MulticlassAUROC(num_classes=C).cuda() for _ in range(6)]
+    torch.cuda.synchronize()
+    for rnd in range(2):  # every metric sees every batch once, each round on another stream
+        for k, (m, s) in enumerate(zip(ms, streams)):
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                for x, t in batches[rnd * 3:(rnd + 1) * 3]:
+                    m.update(x, t)
+            torch.cuda.current_stream().wait_stream(s)
+        streams = streams[1:] + streams[:1]
+    torch.cuda.synchronize()
+    want = ref.score_hist.cpu()
+    for m in ms:
+        assert torch.equal(m.score_hist.cpu(), want)
