@@ -891,3 +891,52 @@ def test_curve_scratch_cache_across_streams():
     want = ref.score_hist.cpu()
     for m in ms:
         assert torch.equal(m.score_hist.cpu(), want)
+
+
+def test_calibration_error_deterministic_mode_reproducible():
+    """Under torch.use_deterministic_algorithms(True) calibration error avoids its fp64-atomic kernels: two runs are
+    bit-identical and equal the fast path to fp64 rounding."""
+    import torchmetrics_forked_amd as tm
+
+    g = torch.Generator().manual_seed(4)
+    x = torch.randn(20000, 10, generator=g).softmax(1).cuda()
+    t = torch.randint(0, 10, (20000,), generator=g).cuda()
+    fast = tm.MulticlassCalibrationError(num_classes=10, n_bins=15).cuda()(x, t)
+    # a host-resident metric takes the GPU batch (the reference keeps list states here): binned on the GPU, folded in
+    host = tm.MulticlassCalibrationError(num_classes=10, n_bins=15)
+    host.update(x, t)
+    torch.testing.assert_close(host.compute(), fast.cpu(), rtol=1e-6, atol=1e-7)
+    hb = tm.BinaryCalibrationError(n_bins=15)
+    hb.update(x[:, 0], (t == 0).long())
+    gb = tm.BinaryCalibrationError(n_bins=15).cuda()
+    gb.update(x[:, 0], (t == 0).long())
+    torch.testing.assert_close(hb.compute(), gb.compute().cpu(), rtol=1e-6, atol=1e-7)
+    prev = torch.are_deterministic_algorithms_enabled()
+    torch.use_deterministic_algorithms(True, warn_only=True)
+    try:
+        a = tm.MulticlassCalibrationError(num_classes=10, n_bins=15).cuda()(x, t)
+        b = tm.MulticlassCalibrationError(num_classes=10, n_bins=15).cuda()(x, t)
+    finally:
+        torch.use_deterministic_algorithms(prev)
+    assert torch.equal(a, b)
+    torch.testing.assert_close(a, fast, rtol=1e-6, atol=1e-7)
+
+
+@pytest.mark.parametrize("make", ["confmat", "auroc_binned", "collection"])
+def test_host_state_metric_with_gpu_batch_raises_not_faults(make):
+    """A metric whose tensor states stay on the host, fed GPU tensors: the device error of the reference (raised before
+    any native kernel sees a host pointer), and the GPU keeps working."""
+    import torchmetrics_forked_amd as tm
+
+    x = torch.randn(256, 8).cuda()
+    t = torch.randint(0, 8, (256,)).cuda()
+    if make == "confmat":
+        m = tm.MulticlassConfusionMatrix(num_classes=8)
+    elif make == "auroc_binned":
+        m = tm.MulticlassAUROC(num_classes=8, thresholds=5)
+    else:
+        m = tm.MetricCollection({"cm": tm.MulticlassConfusionMatrix(num_classes=8), "acc": tm.MulticlassAccuracy(num_classes=8)})
+    with pytest.raises(RuntimeError, match="different devices|same device"):
+        m.update(x, t)
+    torch.cuda.synchronize()
+    assert int(torch.ones(4, device="cuda").sum()) == 4

@@ -40,6 +40,11 @@ class _CalibrationBase(Metric):
     def _create_states(self, n_bins: int) -> None:
         self.add_state("bins", torch.zeros(3, n_bins + 1, dtype=torch.float64), dist_reduce_fx="sum")
 
+    def _state_device_adapts(self, name: str) -> bool:
+        # the reference keeps list states here, so a host metric takes GPU batches: the batch is binned on its own
+        # device and folded into ``bins`` (MulticlassCalibrationError.update, _ce_bin_update)
+        return name == "bins"
+
     def compute(self) -> Tensor:
         return _ce_from_bins(self.bins, self.norm)
 
@@ -114,6 +119,17 @@ class MulticlassCalibrationError(_CalibrationBase):
         self._create_states(n_bins)
 
     def update(self, preds: Tensor, target: Tensor) -> None:
+        if self.bins.device != preds.device:
+            # host-resident metric, GPU batch (or the reverse): bin on the batch's device, fold into the state
+            # (the reference's list states accept any device)
+            state, self.bins = self.bins, torch.zeros_like(self.bins, device=preds.device)
+            try:
+                self.update(preds, target)
+                self._update_count -= 1  # the nested call went through the wrapper too
+            finally:
+                batch, self.bins = self.bins, state
+            self.bins += batch.to(state.device)
+            return
         if _mc_calibration_fused_ok(preds, target):
             # one launch from the raw rows: ignore filtering, softmax decision and the target range check in-kernel
             sink = self._validation_sink(target) if self.validate_args else None

@@ -34,7 +34,18 @@ def _ce_bin_update(confidences: Tensor, accuracies: Tensor, n_bins: int, bins: O
     confidences = confidences.reshape(-1)
     accuracies = accuracies.reshape(-1).to(confidences.dtype)
     boundaries = _bin_boundaries(n_bins, confidences.dtype, confidences.device)
+    if bins is not None and bins.device != confidences.device:  # state elsewhere: bin on the batch's device, fold in
+        bins += _ce_bin_update(confidences, accuracies, n_bins).to(bins.device)
+        return bins
     out = torch.zeros(3, n_bins + 1, dtype=torch.float64, device=confidences.device) if bins is None else bins
+    if confidences.is_cuda and torch.are_deterministic_algorithms_enabled():
+        # deterministic mode (reference utilities/data.py:194-198 loops its bincount the same way): the native kernel
+        # and index_add_ accumulate fp64 with atomics in run-dependent order; per-bin masked sums are reproducible
+        idx = torch.bucketize(confidences, boundaries, right=True) - 1
+        vals = torch.stack([torch.ones_like(confidences), confidences, accuracies]).to(out.dtype)
+        for b in range(n_bins + 1):
+            out[:, b] += (vals * (idx == b)).sum(dim=1)
+        return out
     if ops.use_native(confidences) and confidences.dtype == torch.float32:
         # per-block LDS accumulation instead of n_bins + 1 contended f64 atomics (csrc/classification.hip)
         torch.ops.tmx.ce_bins_update(confidences, accuracies, boundaries, out)
@@ -158,6 +169,8 @@ def _mc_calibration_fused_ok(preds: Tensor, target: Tensor) -> bool:
     """Shapes the one-pass kernel takes (csrc ``mc_calibration_fused``): raw [N, C] GPU scores, contiguous,
     16-B aligned, C a multiple of the 16-B vector width and <= 128 vectors."""
     if not ops.use_native(target) or preds.ndim != 2 or target.ndim != 1 or not preds.is_floating_point():
+        return False
+    if torch.are_deterministic_algorithms_enabled():  # fp64 atomics in the fused kernel: run-dependent summation order
         return False
     vec = 16 // preds.element_size()
     C = preds.shape[1]

@@ -454,6 +454,7 @@ class Metric(Module, ABC):
             self._update_count += 1
             with torch.set_grad_enabled(self._enable_grad), _range(f"tmx/{self.__class__.__name__}.update"):
                 try:
+                    self._check_state_devices(args, kwargs)
                     update(*args, **kwargs)
                 except RuntimeError as err:
                     if "Expected all tensors to be on" in str(err):
@@ -469,6 +470,31 @@ class Metric(Module, ABC):
                 self._move_list_states_to_cpu()
 
         return wrapped_func
+
+    def _check_state_devices(self, args: Tuple, kwargs: Dict[str, Any]) -> None:
+        """GPU inputs with a tensor state on another device: raise torch's device error (re-worded by the caller, as in
+        the reference) *before* any native kernel runs — a HIP kernel handed a host or other-device state pointer would
+        fault the GPU instead of raising.  List states and empty placeholders are created on the input device."""
+        dev = None
+        for a in args:
+            if isinstance(a, Tensor) and a.is_cuda:
+                dev = a.device
+                break
+        if dev is None:
+            for a in kwargs.values():
+                if isinstance(a, Tensor) and a.is_cuda:
+                    dev = a.device
+                    break
+        if dev is None:
+            return
+        for name in self._defaults:
+            v = getattr(self, name, None)
+            if isinstance(v, Tensor) and v.numel() > 0 and v.device != dev and not self._state_device_adapts(name):
+                raise RuntimeError(f"Expected all tensors to be on the same device, but found at least two devices, {dev} and {v.device}!")
+
+    def _state_device_adapts(self, name: str) -> bool:
+        """States a metric's update moves to the input device itself (override per metric)."""
+        return False
 
     def _move_list_states_to_cpu(self) -> None:
         for name in self._defaults:
