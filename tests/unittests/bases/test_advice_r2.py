@@ -71,3 +71,17 @@ def test_bootstrapper_weighted_path_updates_in_place():
     bs.update(torch.rand(16), torch.rand(16))
     assert [m.sum_squared_error.data_ptr() for m in bs.metrics] == ptrs
     assert all(int(m.total) == 16 for m in bs.metrics)
+
+
+def test_use_native_rejects_mixed_devices_before_launch():
+    """ops.use_native(t, *others): a host tensor mixed with a GPU tensor raises torch's device error (checked on the
+    host, before any native launch could receive a host pointer); all-host calls stay on the CPU path."""
+    import pytest
+    import torch
+
+    from torchmetrics_forked_amd import ops
+
+    a = torch.zeros(3)
+    assert ops.use_native(a, torch.zeros(2), None, torch.tensor(1.0)) is False  # host-only: the CPU path
+    err = ops._device_error(torch.device("cuda", 0), torch.device("cpu"))
+    assert "same device" in str(err)  # the message the Metric wrapper re-words (GPU cases: tests/test_ops_gpu.py)

@@ -57,13 +57,27 @@ def require(tensor: Optional[torch.Tensor] = None) -> None:
         raise RuntimeError(f"torchmetrics_forked_amd native HIP library required{where}: {_error}")
 
 
-def use_native(t: torch.Tensor) -> bool:
-    """True when ``t`` lives on the GPU; then the native library is mandatory (raises if missing)."""
+def _device_error(a: torch.device, b: torch.device) -> RuntimeError:
+    return RuntimeError(f"Expected all tensors to be on the same device, but found at least two devices, {a} and {b}!")
+
+
+def use_native(t: torch.Tensor, *others: Optional[torch.Tensor]) -> bool:
+    """True when ``t`` lives on the GPU; then the native library is mandatory (raises if missing).
+
+    ``others``: every further tensor the native call would read or write.  They must sit on ``t``'s device (0-dim
+    host scalars excepted): a HIP kernel handed a host pointer faults the GPU instead of raising, so the device error
+    torch itself would give is raised here, before any launch."""
     if t.is_cuda:
+        for o in others:
+            if isinstance(o, torch.Tensor) and o.device != t.device and not (o.device.type == "cpu" and o.dim() == 0):
+                raise _device_error(t.device, o.device)
         if os.environ.get("TMX_DISABLE_NATIVE", "0") == "1":
             return False
         require(t)
         return True
+    for o in others:
+        if isinstance(o, torch.Tensor) and o.is_cuda:
+            raise _device_error(o.device, t.device)
     return False
 
 

@@ -35,7 +35,7 @@ def mc_confmat_update(
     ``err_t`` / ``err_p`` (int32[1] device flags, GPU only) are OR-ed with 1 when a target outside ``[0, C)`` that
     is not the ignore index, or an integer prediction outside ``[0, C)``, is seen (deferred validation)."""
     C = confmat.shape[0]
-    if ops.use_native(target):
+    if ops.use_native(target, preds, confmat, err_t, err_p):
         torch.ops.tmx.mc_confmat_update(
             preds, target, confmat, -1 if ignore_index is None else ignore_index, ignore_index is not None, err_t, err_p
         )
@@ -68,7 +68,7 @@ def mc_stat_scores_update(
     Same pair semantics as :func:`mc_confmat_update` (a row counts once: tp of its class, or fp of the predicted
     class + fn of the true one; tn = valid rows - tp - fp - fn per class).  ``ticket`` is an int64 ``[GRID_SLOTS]`` zero
     scratch the GPU kernel uses for its grid reduction; it is left at zero."""
-    if ops.use_native(target):
+    if ops.use_native(target, preds, tp, fp, tn, fn, ticket, err_t, err_p):
         torch.ops.tmx.mc_stat_scores_update(
             preds, target, num_classes, tp, fp, tn, fn, ticket,
             -1 if ignore_index is None else ignore_index, ignore_index is not None, micro, err_t, err_p,
@@ -98,7 +98,7 @@ def binary_stats_fused(
     """Accumulate per-label (tp, fp, tn, fn) into ``states`` (int64 ``[L]`` each) in place, sigmoid-if-needed rule
     included.  ``scratch`` is an int64 ``[6 L + GRID_SLOTS]`` zero buffer (left at zero); ``err_t`` / ``err_p`` are the
     deferred-validation flags for targets outside {0, 1, ignore_index} and label preds outside {0, 1}."""
-    if ops.use_native(target):
+    if ops.use_native(target, preds, *states, scratch, err_t, err_p):
         torch.ops.tmx.binary_stats_fused(
             preds, target, *states, scratch, num_labels, float(threshold),
             -1 if ignore_index is None else ignore_index, ignore_index is not None, err_t, err_p,
@@ -114,7 +114,7 @@ def binary_stats_update(
     preds: Tensor, target: Tensor, counts: Tensor, num_labels: int, threshold: float, ignore_index: Optional[int]
 ) -> None:
     """``counts[L, 4] += (tp, fp, tn, fn)`` per label; preds/target are ``[N, L, ...]`` (``L=1`` for binary)."""
-    if ops.use_native(target):
+    if ops.use_native(target, preds, counts):
         torch.ops.tmx.binary_stats_update(
             preds, target, counts, num_labels, float(threshold), -1 if ignore_index is None else ignore_index, ignore_index is not None
         )
@@ -179,7 +179,7 @@ def curve_hist_update(
     if preds.dtype not in (torch.bfloat16, torch.float16):
         raise TypeError(f"curve_hist_update expects bf16/fp16 scores, got {preds.dtype}")
     tcode = 0 if task == "multiclass" else 1
-    if ops.use_native(target):
+    if ops.use_native(target, preds, hist, confmat, err_flag, mode_state, code_range):
         # with a persistent ``mode_state`` (int32[8]) the multiclass kernel speculates the softmax decision and
         # records the real one in-pass (no separate range pass, ignore-aware); otherwise a pre-pass flag is used
         norm = None if (mode_state is not None and task == "multiclass") else _norm_flag(preds, target, task, ignore_index)
@@ -227,7 +227,7 @@ def curve_hist_reduce(hist: Tensor, code_range: Optional[Tensor] = None) -> Tens
     """float64 ``[C, 4]`` = (auroc, average_precision, n_pos, n_neg) per class, from ``hist[C, 2, K]``.
 
     ``code_range`` (int32[C, 2], per-class ``[lo, hi]``, GPU): every bin outside it is known to be zero and is not read."""
-    if ops.use_native(hist):
+    if ops.use_native(hist, code_range):
         return torch.ops.tmx.curve_hist_reduce(hist, code_range)
     neg = hist[:, 0].flip(-1).double()
     pos = hist[:, 1].flip(-1).double()
@@ -297,7 +297,7 @@ def binned_curve_update(
         confmat.index_add_(0, order, part)
         return
     tcode = 0 if task == "multiclass" else 1
-    if ops.use_native(target):
+    if ops.use_native(target, preds, thresholds, confmat, err_flag):
         torch.ops.tmx.binned_curve_update(
             preds, target, thresholds, confmat, tcode, -1 if ignore_index is None else ignore_index, ignore_index is not None,
             _norm_flag(preds, target, task, ignore_index), err_flag,

@@ -60,7 +60,7 @@ class _MulticlassScoresPlan:
         target = kwargs.get("target", args[1] if len(args) > 1 else None)
         if not isinstance(preds, Tensor) or not isinstance(target, Tensor) or not preds.is_floating_point():
             return []
-        if preds.ndim != 2 or target.ndim != 1 or not ops.use_native(preds):
+        if preds.ndim != 2 or target.ndim != 1 or target.device != preds.device or not ops.use_native(preds):
             return []
         curve = members.get(self.curve_name) if self.curve_name else None
         if curve is not None and (preds.dtype not in eng.HIST_DTYPES or not curve._hist_ok(preds)):
