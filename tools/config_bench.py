@@ -12,6 +12,7 @@ ranks is reported, ``value`` = world * steps / seconds (whole-job updates/s, wea
 (BASELINE.json publishes none), so ``vs_baseline`` is null.
 """
 import argparse
+import os
 import sys
 import threading
 import time
@@ -127,6 +128,8 @@ def _map(args: argparse.Namespace, device: torch.device, world: int, rank: int) 
 
 
 def _image(args: argparse.Namespace, device: torch.device, world: int, rank: int) -> Dict[str, Any]:
+    if os.environ.get("TMX_CONV_BENCHMARK", "0") == "1":
+        torch.backends.cudnn.benchmark = True  # MIOpen Find per conv shape (the warm-up step pays the search)
     import torchmetrics_forked_amd as tm
     from torchmetrics_forked_amd.image import LearnedPerceptualImagePatchSimilarity, PeakSignalNoiseRatio, StructuralSimilarityIndexMeasure
 
