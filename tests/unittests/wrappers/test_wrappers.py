@@ -66,6 +66,20 @@ def test_bootstrapper_forward_and_reset():
         BootStrapper(lambda x: x)
 
 
+def test_bootstrapper_weighted_path_validates_inputs():
+    """The weighted fast path never calls the copies' update: the base metric's input checks must still fire on the
+    un-resampled batch, and a valid batch must leave every copy's state storage in place."""
+    bs = BootStrapper(tm.MulticlassAccuracy(num_classes=3), num_bootstraps=3)
+    with pytest.raises(RuntimeError, match="target"):
+        bs.update(torch.randn(8, 3), torch.tensor([0, 1, 2, 3, 0, 1, 2, 0]))
+    bs_mse = BootStrapper(tm.MeanSquaredError(), num_bootstraps=3)
+    with pytest.raises(RuntimeError, match="shape"):
+        bs_mse.update(torch.randn(8), torch.randn(7))
+    ptrs = [m.total.data_ptr() for m in bs_mse.metrics]
+    bs_mse.update(torch.randn(8), torch.randn(8))
+    assert [m.total.data_ptr() for m in bs_mse.metrics] == ptrs
+
+
 def test_classwise():
     m = ClasswiseWrapper(tm.MulticlassAccuracy(3, average=None), labels=["a", "b", "c"])
     p, t = torch.randn(20, 3), torch.randint(0, 3, (20,))
