@@ -1,0 +1,207 @@
+"""Parity against scikit-learn / scipy on random inputs -- the reference's own oracle strategy (its unittests
+compare every classification, regression, clustering and pairwise metric to ``sklearn.metrics`` / ``scipy``, e.g.
+``/root/reference/tests/unittests/classification/test_accuracy.py`` ``_reference_sklearn_accuracy_*``).  CPU only."""
+import numpy as np
+import pytest
+import torch
+
+sklearn_metrics = pytest.importorskip("sklearn.metrics")
+scipy_stats = pytest.importorskip("scipy.stats")
+
+import torchmetrics_forked_amd.functional as F  # noqa: E402
+import torchmetrics_forked_amd.functional.clustering as FC  # noqa: E402
+
+SEEDS = [0, 1, 2]
+N, C, L = 300, 5, 4
+
+
+def _gen(seed):
+    return torch.Generator().manual_seed(seed)
+
+
+def _close(ours, ref, atol=1e-5, rtol=1e-4):
+    ours = ours.detach().double().numpy() if isinstance(ours, torch.Tensor) else np.asarray(ours, dtype=np.float64)
+    np.testing.assert_allclose(ours, np.asarray(ref, dtype=np.float64), atol=atol, rtol=rtol)
+
+
+# --------------------------------------------------------------------------------------------- classification
+@pytest.mark.parametrize("seed", SEEDS)
+def test_binary_family(seed):
+    g = _gen(seed)
+    p, t = torch.rand(N, generator=g), torch.randint(0, 2, (N,), generator=g)
+    hard = (p > 0.5).long().numpy()
+    tn = t.numpy()
+    _close(F.binary_accuracy(p, t), sklearn_metrics.accuracy_score(tn, hard))
+    _close(F.binary_precision(p, t), sklearn_metrics.precision_score(tn, hard))
+    _close(F.binary_recall(p, t), sklearn_metrics.recall_score(tn, hard))
+    _close(F.binary_f1_score(p, t), sklearn_metrics.f1_score(tn, hard))
+    _close(F.binary_fbeta_score(p, t, beta=2.0), sklearn_metrics.fbeta_score(tn, hard, beta=2.0))
+    _close(F.binary_matthews_corrcoef(p, t), sklearn_metrics.matthews_corrcoef(tn, hard))
+    _close(F.binary_cohen_kappa(p, t), sklearn_metrics.cohen_kappa_score(tn, hard))
+    _close(F.binary_jaccard_index(p, t), sklearn_metrics.jaccard_score(tn, hard))
+    _close(F.binary_hamming_distance(p, t), sklearn_metrics.hamming_loss(tn, hard))
+    _close(F.binary_confusion_matrix(p, t), sklearn_metrics.confusion_matrix(tn, hard))
+    _close(F.binary_auroc(p, t), sklearn_metrics.roc_auc_score(tn, p.numpy()))
+    _close(F.binary_average_precision(p, t), sklearn_metrics.average_precision_score(tn, p.numpy()))
+
+
+@pytest.mark.parametrize("seed", SEEDS)
+def test_binary_curves(seed):
+    g = _gen(seed)
+    p, t = torch.rand(N, generator=g), torch.randint(0, 2, (N,), generator=g)
+    fpr, tpr, thr = F.binary_roc(p, t)
+    rfpr, rtpr, _ = sklearn_metrics.roc_curve(t.numpy(), p.numpy(), drop_intermediate=False)
+    _close(fpr, rfpr)
+    _close(tpr, rtpr)
+    prec, rec, _ = F.binary_precision_recall_curve(p, t)
+    rprec, rrec, _ = sklearn_metrics.precision_recall_curve(t.numpy(), p.numpy())
+    # sklearn drops the points past full recall; both end at (precision 1, recall 0)
+    _close(prec[-len(rprec):], rprec)
+    _close(rec[-len(rrec):], rrec)
+
+
+@pytest.mark.parametrize("seed", SEEDS)
+@pytest.mark.parametrize("average", ["micro", "macro", "weighted"])
+def test_multiclass_family(seed, average):
+    g = _gen(seed)
+    logits, t = torch.randn(N, C, generator=g), torch.randint(0, C, (N,), generator=g)
+    hard, tn = logits.argmax(1).numpy(), t.numpy()
+    kw = {"num_classes": C, "average": average}
+    _close(F.multiclass_accuracy(logits, t, **kw), sklearn_metrics.recall_score(tn, hard, average=average)
+           if average != "micro" else sklearn_metrics.accuracy_score(tn, hard))
+    _close(F.multiclass_precision(logits, t, **kw), sklearn_metrics.precision_score(tn, hard, average=average))
+    _close(F.multiclass_recall(logits, t, **kw), sklearn_metrics.recall_score(tn, hard, average=average))
+    _close(F.multiclass_f1_score(logits, t, **kw), sklearn_metrics.f1_score(tn, hard, average=average))
+    _close(F.multiclass_jaccard_index(logits, t, **kw), sklearn_metrics.jaccard_score(tn, hard, average=average))
+    if average != "micro":
+        probs = logits.softmax(1).numpy()
+        _close(F.multiclass_auroc(logits.softmax(1), t, num_classes=C, average=average),
+               sklearn_metrics.roc_auc_score(tn, probs, multi_class="ovr", average=average))
+
+
+@pytest.mark.parametrize("seed", SEEDS)
+def test_multiclass_matrix_stats(seed):
+    g = _gen(seed)
+    logits, t = torch.randn(N, C, generator=g), torch.randint(0, C, (N,), generator=g)
+    hard, tn = logits.argmax(1).numpy(), t.numpy()
+    _close(F.multiclass_confusion_matrix(logits, t, C), sklearn_metrics.confusion_matrix(tn, hard, labels=range(C)))
+    _close(F.multiclass_matthews_corrcoef(logits, t, C), sklearn_metrics.matthews_corrcoef(tn, hard))
+    _close(F.multiclass_cohen_kappa(logits, t, C), sklearn_metrics.cohen_kappa_score(tn, hard))
+    _close(F.multiclass_cohen_kappa(logits, t, C, weights="quadratic"),
+           sklearn_metrics.cohen_kappa_score(tn, hard, weights="quadratic"))
+    _close(F.multiclass_hamming_distance(logits, t, C, average="micro"), sklearn_metrics.hamming_loss(tn, hard))
+
+
+@pytest.mark.parametrize("seed", SEEDS)
+def test_multilabel_family(seed):
+    g = _gen(seed)
+    p, t = torch.rand(N, L, generator=g), torch.randint(0, 2, (N, L), generator=g)
+    hard, tn, pn = (p > 0.5).long().numpy(), t.numpy(), p.numpy()
+    for average in ["micro", "macro", "weighted"]:
+        kw = {"num_labels": L, "average": average}
+        _close(F.multilabel_precision(p, t, **kw), sklearn_metrics.precision_score(tn, hard, average=average))
+        _close(F.multilabel_recall(p, t, **kw), sklearn_metrics.recall_score(tn, hard, average=average))
+        _close(F.multilabel_f1_score(p, t, **kw), sklearn_metrics.f1_score(tn, hard, average=average))
+        _close(F.multilabel_auroc(p, t, **kw), sklearn_metrics.roc_auc_score(tn, pn, average=average))
+        _close(F.multilabel_average_precision(p, t, **kw),
+               sklearn_metrics.average_precision_score(tn, pn, average=average))
+    _close(F.multilabel_hamming_distance(p, t, L, average="micro"), sklearn_metrics.hamming_loss(tn, hard))
+    _close(F.multilabel_exact_match(p, t, L), sklearn_metrics.accuracy_score(tn, hard))
+    _close(F.multilabel_confusion_matrix(p, t, L), sklearn_metrics.multilabel_confusion_matrix(tn, hard))
+    _close(F.multilabel_coverage_error(p, t, L), sklearn_metrics.coverage_error(tn, pn))
+    _close(F.multilabel_ranking_average_precision(p, t, L), sklearn_metrics.label_ranking_average_precision_score(tn, pn))
+    _close(F.multilabel_ranking_loss(p, t, L), sklearn_metrics.label_ranking_loss(tn, pn))
+
+
+@pytest.mark.parametrize("seed", SEEDS)
+def test_hinge(seed):
+    g = _gen(seed)
+    p, t = torch.rand(N, generator=g), torch.randint(0, 2, (N,), generator=g)
+    _close(F.binary_hinge_loss(p, t), sklearn_metrics.hinge_loss(t.numpy() * 2 - 1, p.numpy()))
+    logits, tc = torch.randn(N, C, generator=g), torch.randint(0, C, (N,), generator=g)
+    _close(F.multiclass_hinge_loss(logits, tc, C, multiclass_mode="crammer-singer"),
+           sklearn_metrics.hinge_loss(tc.numpy(), logits.softmax(1).numpy(), labels=list(range(C))))  # logits -> softmax
+
+
+# ----------------------------------------------------------------------------------------------------- regression
+@pytest.mark.parametrize("seed", SEEDS)
+def test_regression_family(seed):
+    g = _gen(seed)
+    p, t = torch.randn(N, generator=g), torch.randn(N, generator=g)
+    pn, tn = p.numpy(), t.numpy()
+    _close(F.mean_squared_error(p, t), sklearn_metrics.mean_squared_error(tn, pn))
+    _close(F.mean_squared_error(p, t, squared=False), np.sqrt(sklearn_metrics.mean_squared_error(tn, pn)))
+    _close(F.mean_absolute_error(p, t), sklearn_metrics.mean_absolute_error(tn, pn))
+    _close(F.r2_score(p, t), sklearn_metrics.r2_score(tn, pn))
+    _close(F.explained_variance(p, t), sklearn_metrics.explained_variance_score(tn, pn))
+    _close(F.mean_absolute_percentage_error(p, t), sklearn_metrics.mean_absolute_percentage_error(tn, pn), rtol=1e-3)
+    pp, tp = p.abs(), t.abs()
+    _close(F.mean_squared_log_error(pp, tp), sklearn_metrics.mean_squared_log_error(tp.numpy(), pp.numpy()))
+    _close(F.tweedie_deviance_score(pp + 0.1, tp + 0.1, power=1.5),
+           sklearn_metrics.mean_tweedie_deviance((tp + 0.1).numpy(), (pp + 0.1).numpy(), power=1.5))
+    _close(F.pearson_corrcoef(p, t), scipy_stats.pearsonr(pn, tn)[0])
+    _close(F.spearman_corrcoef(p, t), scipy_stats.spearmanr(pn, tn)[0])
+    _close(F.kendall_rank_corrcoef(p, t), scipy_stats.kendalltau(pn, tn)[0])
+
+
+@pytest.mark.parametrize("seed", SEEDS)
+def test_multioutput_regression(seed):
+    g = _gen(seed)
+    p, t = torch.randn(N, 3, generator=g), torch.randn(N, 3, generator=g)
+    pn, tn = p.numpy(), t.numpy()
+    _close(F.r2_score(p, t, multioutput="raw_values"), sklearn_metrics.r2_score(tn, pn, multioutput="raw_values"))
+    _close(F.r2_score(p, t, multioutput="variance_weighted"),
+           sklearn_metrics.r2_score(tn, pn, multioutput="variance_weighted"))
+    _close(F.explained_variance(p, t, multioutput="raw_values"),
+           sklearn_metrics.explained_variance_score(tn, pn, multioutput="raw_values"))
+
+
+# ------------------------------------------------------------------------------------------------------ clustering
+@pytest.mark.parametrize("seed", SEEDS)
+def test_extrinsic_clustering(seed):
+    g = _gen(seed)
+    a, b = torch.randint(0, 6, (N,), generator=g), torch.randint(0, 4, (N,), generator=g)
+    an, bn = a.numpy(), b.numpy()
+    _close(FC.mutual_info_score(a, b), sklearn_metrics.mutual_info_score(bn, an))
+    _close(FC.adjusted_rand_score(a, b), sklearn_metrics.adjusted_rand_score(bn, an))
+    _close(FC.rand_score(a, b), sklearn_metrics.rand_score(bn, an))
+    _close(FC.fowlkes_mallows_index(a, b), sklearn_metrics.fowlkes_mallows_score(bn, an))
+    _close(FC.homogeneity_score(a, b), sklearn_metrics.homogeneity_score(bn, an))
+    _close(FC.completeness_score(a, b), sklearn_metrics.completeness_score(bn, an))
+    _close(FC.v_measure_score(a, b), sklearn_metrics.v_measure_score(bn, an))
+    for method in ["arithmetic", "geometric", "min", "max"]:
+        _close(FC.normalized_mutual_info_score(a, b, average_method=method),
+               sklearn_metrics.normalized_mutual_info_score(bn, an, average_method=method))
+    _close(FC.adjusted_mutual_info_score(a, b), sklearn_metrics.adjusted_mutual_info_score(bn, an), atol=1e-4)
+
+
+@pytest.mark.parametrize("seed", SEEDS)
+def test_intrinsic_clustering(seed):
+    g = _gen(seed)
+    x, lab = torch.randn(N, 3, generator=g), torch.randint(0, 4, (N,), generator=g)
+    _close(FC.calinski_harabasz_score(x, lab), sklearn_metrics.calinski_harabasz_score(x.numpy(), lab.numpy()),
+           rtol=1e-4)
+    _close(FC.davies_bouldin_score(x, lab), sklearn_metrics.davies_bouldin_score(x.numpy(), lab.numpy()), rtol=1e-4)
+
+
+# ------------------------------------------------------------------------------------------------ pairwise / retrieval
+@pytest.mark.parametrize("seed", SEEDS)
+def test_pairwise(seed):
+    g = _gen(seed)
+    x, y = torch.randn(20, 6, generator=g), torch.randn(15, 6, generator=g)
+    xn, yn = x.numpy(), y.numpy()
+    _close(F.pairwise_cosine_similarity(x, y), sklearn_metrics.pairwise.cosine_similarity(xn, yn))
+    _close(F.pairwise_euclidean_distance(x, y), sklearn_metrics.pairwise.euclidean_distances(xn, yn), atol=1e-4)
+    _close(F.pairwise_manhattan_distance(x, y), sklearn_metrics.pairwise.manhattan_distances(xn, yn), atol=1e-4)
+    _close(F.pairwise_linear_similarity(x, y), sklearn_metrics.pairwise.linear_kernel(xn, yn), atol=1e-4)
+
+
+@pytest.mark.parametrize("seed", SEEDS)
+def test_retrieval_ndcg(seed):
+    g = _gen(seed)
+    p, t = torch.rand(40, generator=g), torch.randint(0, 4, (40,), generator=g)
+    _close(F.retrieval_normalized_dcg(p, t), sklearn_metrics.ndcg_score(t[None].numpy(), p[None].numpy()))
+    _close(F.retrieval_normalized_dcg(p, t, top_k=10),
+           sklearn_metrics.ndcg_score(t[None].numpy(), p[None].numpy(), k=10))
+    tb = (t > 1).long()
+    _close(F.retrieval_average_precision(p, tb), sklearn_metrics.average_precision_score(tb.numpy(), p.numpy()))
