@@ -205,3 +205,59 @@ def test_retrieval_ndcg(seed):
            sklearn_metrics.ndcg_score(t[None].numpy(), p[None].numpy(), k=10))
     tb = (t > 1).long()
     _close(F.retrieval_average_precision(p, tb), sklearn_metrics.average_precision_score(tb.numpy(), p.numpy()))
+
+
+# ------------------------------------------------------------------------------- modules: batched accumulation
+import torchmetrics_forked_amd as tm  # noqa: E402
+
+_MODULE_CASES = [
+    ("binary_prob", lambda: tm.BinaryAUROC(), lambda p, t: sklearn_metrics.roc_auc_score(t, p)),
+    ("binary_prob", lambda: tm.BinaryAveragePrecision(), lambda p, t: sklearn_metrics.average_precision_score(t, p)),
+    ("binary_prob", lambda: tm.BinaryF1Score(), lambda p, t: sklearn_metrics.f1_score(t, p > 0.5)),
+    ("binary_prob", lambda: tm.BinarySpecificity(), lambda p, t: sklearn_metrics.recall_score(1 - t, p <= 0.5)),
+    ("multiclass", lambda: tm.MulticlassAccuracy(num_classes=C, average="micro"),
+     lambda p, t: sklearn_metrics.accuracy_score(t, p.argmax(1))),
+    ("multiclass", lambda: tm.MulticlassF1Score(num_classes=C, average="macro"),
+     lambda p, t: sklearn_metrics.f1_score(t, p.argmax(1), average="macro")),
+    ("multiclass", lambda: tm.MulticlassAUROC(num_classes=C),
+     lambda p, t: sklearn_metrics.roc_auc_score(t, p, multi_class="ovr", average="macro")),
+    ("multiclass", lambda: tm.MulticlassCohenKappa(num_classes=C),
+     lambda p, t: sklearn_metrics.cohen_kappa_score(t, p.argmax(1))),
+    ("multiclass", lambda: tm.MulticlassMatthewsCorrCoef(num_classes=C),
+     lambda p, t: sklearn_metrics.matthews_corrcoef(t, p.argmax(1))),
+    ("regression", lambda: tm.MeanSquaredError(), lambda p, t: sklearn_metrics.mean_squared_error(t, p)),
+    ("regression", lambda: tm.R2Score(), lambda p, t: sklearn_metrics.r2_score(t, p)),
+    ("regression", lambda: tm.ExplainedVariance(), lambda p, t: sklearn_metrics.explained_variance_score(t, p)),
+    ("regression", lambda: tm.PearsonCorrCoef(), lambda p, t: scipy_stats.pearsonr(p, t)[0]),
+    ("regression", lambda: tm.SpearmanCorrCoef(), lambda p, t: scipy_stats.spearmanr(p, t)[0]),
+    ("regression", lambda: tm.KendallRankCorrCoef(), lambda p, t: scipy_stats.kendalltau(p, t)[0]),
+]
+
+
+def _batches(kind, seed, nb=4, bs=64):
+    g = _gen(seed)
+    if kind == "binary_prob":
+        return [(torch.rand(bs, generator=g), torch.randint(0, 2, (bs,), generator=g)) for _ in range(nb)]
+    if kind == "multiclass":
+        return [(torch.randn(bs, C, generator=g).softmax(1), torch.randint(0, C, (bs,), generator=g))
+                for _ in range(nb)]
+    return [(torch.randn(bs, generator=g), torch.randn(bs, generator=g)) for _ in range(nb)]
+
+
+@pytest.mark.parametrize("seed", SEEDS[:2])
+@pytest.mark.parametrize(("kind", "make", "oracle"), _MODULE_CASES, ids=[f"{k}-{i}" for i, (k, _, _) in enumerate(_MODULE_CASES)])
+def test_module_accumulation_matches_oracle(kind, make, oracle, seed):
+    """Reference ``run_class_metric_test`` pattern: update over several batches (forward on each, so the per-batch
+    value is checked too) and compare the accumulated compute() with the oracle on the concatenated data."""
+    m = make()
+    batches = _batches(kind, seed)
+    for p, t in batches:
+        batch_val = m(p, t)
+        _close(batch_val, oracle(p.numpy(), t.numpy()), atol=1e-4)
+    P = torch.cat([b[0] for b in batches]).numpy()
+    T = torch.cat([b[1] for b in batches]).numpy()
+    _close(m.compute(), oracle(P, T), atol=1e-5)
+    m.reset()
+    p, t = batches[0]
+    m.update(p, t)
+    _close(m.compute(), oracle(p.numpy(), t.numpy()), atol=1e-5)
