@@ -261,3 +261,25 @@ def test_module_accumulation_matches_oracle(kind, make, oracle, seed):
     p, t = batches[0]
     m.update(p, t)
     _close(m.compute(), oracle(p.numpy(), t.numpy()), atol=1e-5)
+
+
+@pytest.mark.parametrize("seed", SEEDS)
+@pytest.mark.parametrize("variant", ["b", "c"])
+def test_kendall_variants_with_ties(seed, variant):
+    g = _gen(seed)
+    p, t = torch.randint(0, 8, (N,), generator=g).float(), torch.randint(0, 6, (N,), generator=g).float()
+    ref = scipy_stats.kendalltau(p.numpy(), t.numpy(), variant=variant)
+    _close(F.kendall_rank_corrcoef(p, t, variant=variant), ref[0])
+    tau, pval = F.kendall_rank_corrcoef(p, t, variant=variant, t_test=True, alternative="two-sided")
+    _close(tau, ref[0])
+    if variant == "b":  # scipy's p-value for tau-c uses the tau-b variance as well; pin b only
+        _close(pval, ref[1], atol=1e-4, rtol=1e-3)
+
+
+@pytest.mark.parametrize("seed", SEEDS)
+def test_spearman_ties_and_multioutput(seed):
+    g = _gen(seed)
+    p, t = torch.randint(0, 10, (N, 2), generator=g).float(), torch.randn(N, 2, generator=g)
+    ours = F.spearman_corrcoef(p, t)
+    ref = [scipy_stats.spearmanr(p[:, j].numpy(), t[:, j].numpy())[0] for j in range(2)]
+    _close(ours, ref, atol=1e-4)
