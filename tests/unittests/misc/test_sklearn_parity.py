@@ -283,3 +283,39 @@ def test_spearman_ties_and_multioutput(seed):
     ours = F.spearman_corrcoef(p, t)
     ref = [scipy_stats.spearmanr(p[:, j].numpy(), t[:, j].numpy())[0] for j in range(2)]
     _close(ours, ref, atol=1e-4)
+
+
+@pytest.mark.parametrize("seed", SEEDS)
+def test_ignore_index_matches_masked_oracle(seed):
+    """``ignore_index`` drops those targets (reference ``_reference_sklearn_*`` helpers mask them before sklearn)."""
+    g = _gen(seed)
+    logits, t = torch.randn(N, C, generator=g), torch.randint(0, C, (N,), generator=g)
+    t[torch.rand(N, generator=g) < 0.2] = -100
+    keep = (t != -100).numpy()
+    hard, tn = logits.argmax(1).numpy()[keep], t.numpy()[keep]
+    for average in ["micro", "macro"]:
+        kw = {"num_classes": C, "average": average, "ignore_index": -100}
+        _close(F.multiclass_f1_score(logits, t, **kw), sklearn_metrics.f1_score(tn, hard, average=average))
+        _close(F.multiclass_precision(logits, t, **kw), sklearn_metrics.precision_score(tn, hard, average=average))
+    _close(F.multiclass_confusion_matrix(logits, t, C, ignore_index=-100),
+           sklearn_metrics.confusion_matrix(tn, hard, labels=range(C)))
+    _close(F.multiclass_auroc(logits.softmax(1), t, C, ignore_index=-100),
+           sklearn_metrics.roc_auc_score(tn, logits.softmax(1).numpy()[keep], multi_class="ovr"))
+    p, tb = torch.rand(N, generator=g), torch.randint(0, 2, (N,), generator=g)
+    tb[torch.rand(N, generator=g) < 0.2] = -1
+    kb = (tb != -1).numpy()
+    _close(F.binary_auroc(p, tb, ignore_index=-1), sklearn_metrics.roc_auc_score(tb.numpy()[kb], p.numpy()[kb]))
+    _close(F.binary_accuracy(p, tb, ignore_index=-1),
+           sklearn_metrics.accuracy_score(tb.numpy()[kb], (p.numpy()[kb] > 0.5)))
+
+
+@pytest.mark.parametrize("seed", SEEDS)
+def test_multidim_multiclass_global(seed):
+    """Extra dims ``[N, C, X]`` flatten into samples for ``multidim_average='global'``."""
+    g = _gen(seed)
+    logits, t = torch.randn(40, C, 7, generator=g), torch.randint(0, C, (40, 7), generator=g)
+    hard = logits.argmax(1).flatten().numpy()
+    tn = t.flatten().numpy()
+    _close(F.multiclass_accuracy(logits, t, C, average="micro"), sklearn_metrics.accuracy_score(tn, hard))
+    _close(F.multiclass_f1_score(logits, t, C, average="macro"), sklearn_metrics.f1_score(tn, hard, average="macro"))
+    _close(F.multiclass_confusion_matrix(logits, t, C), sklearn_metrics.confusion_matrix(tn, hard, labels=range(C)))
