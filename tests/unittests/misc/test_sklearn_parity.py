@@ -319,3 +319,19 @@ def test_multidim_multiclass_global(seed):
     _close(F.multiclass_accuracy(logits, t, C, average="micro"), sklearn_metrics.accuracy_score(tn, hard))
     _close(F.multiclass_f1_score(logits, t, C, average="macro"), sklearn_metrics.f1_score(tn, hard, average="macro"))
     _close(F.multiclass_confusion_matrix(logits, t, C), sklearn_metrics.confusion_matrix(tn, hard, labels=range(C)))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize(("kind", "make", "oracle"), _MODULE_CASES, ids=[f"{k}-{i}" for i, (k, _, _) in enumerate(_MODULE_CASES)])
+def test_module_accumulation_matches_oracle_gpu(kind, make, oracle):
+    """Same oracle on ``cuda:0``: states and kernels on the device (native path), results compared on the host."""
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    dev = torch.device("cuda", 0)
+    m = make().to(dev)
+    batches = _batches(kind, 0, bs=4096)
+    for p, t in batches:
+        m.update(p.to(dev), t.to(dev))
+    P = torch.cat([b[0] for b in batches]).numpy()
+    T = torch.cat([b[1] for b in batches]).numpy()
+    _close(m.compute().cpu(), oracle(P, T), atol=2e-5, rtol=2e-4)
