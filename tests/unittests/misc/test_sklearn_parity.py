@@ -335,3 +335,27 @@ def test_module_accumulation_matches_oracle_gpu(kind, make, oracle):
     P = torch.cat([b[0] for b in batches]).numpy()
     T = torch.cat([b[1] for b in batches]).numpy()
     _close(m.compute().cpu(), oracle(P, T), atol=2e-5, rtol=2e-4)
+
+
+@pytest.mark.parametrize("seed", SEEDS)
+def test_regression_formula_oracles(seed):
+    """Metrics without a scikit-learn counterpart, against their numpy / scipy definitions."""
+    g = _gen(seed)
+    p, t = torch.randn(N, generator=g), torch.randn(N, generator=g)
+    pn, tn = p.double().numpy(), t.double().numpy()
+    _close(F.log_cosh_error(p, t), np.mean(np.log(np.cosh(pn - tn))))
+    _close(F.relative_squared_error(p, t), np.sum((tn - pn) ** 2) / np.sum((tn - tn.mean()) ** 2))
+    _close(F.symmetric_mean_absolute_percentage_error(p, t),
+           np.mean(2 * np.abs(pn - tn) / np.maximum(np.abs(pn) + np.abs(tn), 1.17e-06)), rtol=1e-4)
+    _close(F.weighted_mean_absolute_percentage_error(p, t), np.sum(np.abs(pn - tn)) / np.sum(np.abs(tn)))
+    _close(F.minkowski_distance(p, t, p=3), scipy_spatial.distance.minkowski(pn, tn, p=3), rtol=1e-4)
+    x, y = torch.randn(20, 6, generator=g), torch.randn(20, 6, generator=g)
+    _close(F.cosine_similarity(x, y, reduction="none"),
+           1 - np.array([scipy_spatial.distance.cosine(a, b) for a, b in zip(x.numpy(), y.numpy())]), atol=1e-5)
+    pp, tp = p.abs() + 0.1, t.abs() + 0.1
+    for power in [0.0, 1.0, 2.0, 3.0]:
+        _close(F.tweedie_deviance_score(pp, tp, power=power),
+               sklearn_metrics.mean_tweedie_deviance(tp.numpy(), pp.numpy(), power=power), rtol=1e-4)
+
+
+scipy_spatial = pytest.importorskip("scipy.spatial")
