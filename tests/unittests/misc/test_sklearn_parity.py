@@ -359,3 +359,43 @@ def test_regression_formula_oracles(seed):
 
 
 scipy_spatial = pytest.importorskip("scipy.spatial")
+
+
+_CLUSTER_MODULES = [
+    (lambda: tm.clustering.MutualInfoScore(), sklearn_metrics.mutual_info_score),
+    (lambda: tm.clustering.AdjustedRandScore(), sklearn_metrics.adjusted_rand_score),
+    (lambda: tm.clustering.RandScore(), sklearn_metrics.rand_score),
+    (lambda: tm.clustering.FowlkesMallowsIndex(), sklearn_metrics.fowlkes_mallows_score),
+    (lambda: tm.clustering.HomogeneityScore(), sklearn_metrics.homogeneity_score),
+    (lambda: tm.clustering.CompletenessScore(), sklearn_metrics.completeness_score),
+    (lambda: tm.clustering.VMeasureScore(), sklearn_metrics.v_measure_score),
+    (lambda: tm.clustering.NormalizedMutualInfoScore(), sklearn_metrics.normalized_mutual_info_score),
+    (lambda: tm.clustering.AdjustedMutualInfoScore(), sklearn_metrics.adjusted_mutual_info_score),
+]
+
+
+@pytest.mark.parametrize("seed", SEEDS[:2])
+@pytest.mark.parametrize(("make", "oracle"), _CLUSTER_MODULES, ids=[o.__name__ for _, o in _CLUSTER_MODULES])
+def test_clustering_modules_accumulate(make, oracle, seed):
+    g = _gen(seed)
+    batches = [(torch.randint(0, 5, (80,), generator=g), torch.randint(0, 4, (80,), generator=g)) for _ in range(3)]
+    m = make()
+    for p, t in batches:
+        m.update(p, t)
+    P = torch.cat([b[0] for b in batches]).numpy()
+    T = torch.cat([b[1] for b in batches]).numpy()
+    _close(m.compute(), oracle(T, P), atol=1e-4)
+
+
+@pytest.mark.parametrize("seed", SEEDS[:2])
+def test_intrinsic_clustering_modules_accumulate(seed):
+    g = _gen(seed)
+    batches = [(torch.randn(60, 3, generator=g), torch.randint(0, 4, (60,), generator=g)) for _ in range(3)]
+    X = torch.cat([b[0] for b in batches]).numpy()
+    lab = torch.cat([b[1] for b in batches]).numpy()
+    for make, oracle in [(tm.clustering.CalinskiHarabaszScore, sklearn_metrics.calinski_harabasz_score),
+                         (tm.clustering.DaviesBouldinScore, sklearn_metrics.davies_bouldin_score)]:
+        m = make()
+        for x, lb in batches:
+            m.update(x, lb)
+        _close(m.compute(), oracle(X, lab), rtol=1e-4)
