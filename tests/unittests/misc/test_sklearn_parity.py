@@ -399,3 +399,35 @@ def test_intrinsic_clustering_modules_accumulate(seed):
         for x, lb in batches:
             m.update(x, lb)
         _close(m.compute(), oracle(X, lab), rtol=1e-4)
+
+
+@pytest.mark.parametrize("seed", SEEDS)
+def test_nominal_vs_scipy_association(seed):
+    """Cramer's V / Tschuprow's T / Pearson's contingency coefficient without bias correction equal
+    ``scipy.stats.contingency.association`` on the contingency table of the two label vectors."""
+    from scipy.stats.contingency import association, crosstab
+
+    g = _gen(seed)
+    a, b = torch.randint(0, 5, (N,), generator=g), torch.randint(0, 4, (N,), generator=g)
+    table = crosstab(a.numpy(), b.numpy()).count
+    _close(F.cramers_v(a, b, bias_correction=False), association(table, method="cramer"), atol=1e-5)
+    _close(F.tschuprows_t(a, b, bias_correction=False), association(table, method="tschuprow"), atol=1e-5)
+    _close(F.pearsons_contingency_coefficient(a, b), association(table, method="pearson"), atol=1e-5)
+
+
+@pytest.mark.parametrize("seed", SEEDS)
+@pytest.mark.parametrize("norm", ["l1", "max"])
+def test_binary_calibration_error_vs_numpy(seed, norm):
+    g = _gen(seed)
+    p, t = torch.rand(N, generator=g), torch.randint(0, 2, (N,), generator=g)
+    pn, tn, n_bins = p.double().numpy(), t.numpy(), 10
+    # uniform bins over [0, 1], right-closed as torch.bucketize(right=True) - 1 on the boundaries
+    bins = np.clip(np.searchsorted(np.linspace(0, 1, n_bins + 1), pn, side="right") - 1, 0, n_bins - 1)
+    gaps, weights = [], []
+    for k in range(n_bins):
+        m = bins == k
+        if m.any():
+            gaps.append(abs(pn[m].mean() - tn[m].mean()))
+            weights.append(m.mean())
+    ref = np.sum(np.array(gaps) * np.array(weights)) if norm == "l1" else np.max(gaps)
+    _close(F.binary_calibration_error(p, t, n_bins=n_bins, norm=norm), ref, atol=1e-5)
