@@ -431,3 +431,32 @@ def test_binary_calibration_error_vs_numpy(seed, norm):
             weights.append(m.mean())
     ref = np.sum(np.array(gaps) * np.array(weights)) if norm == "l1" else np.max(gaps)
     _close(F.binary_calibration_error(p, t, n_bins=n_bins, norm=norm), ref, atol=1e-5)
+
+
+@pytest.mark.parametrize("seed", SEEDS)
+def test_logit_inputs_are_sigmoided(seed):
+    """Binary / multilabel preds outside [0, 1] are logits: sigmoid, then threshold (reference
+    ``_binary_stat_scores_format``); the oracle gets the sigmoid probabilities."""
+    g = _gen(seed)
+    x, t = torch.randn(N, generator=g) * 3, torch.randint(0, 2, (N,), generator=g)
+    prob = torch.sigmoid(x).numpy()
+    _close(F.binary_f1_score(x, t), sklearn_metrics.f1_score(t.numpy(), prob > 0.5))
+    _close(F.binary_auroc(x, t), sklearn_metrics.roc_auc_score(t.numpy(), prob))
+    _close(F.binary_precision(x, t, threshold=0.3), sklearn_metrics.precision_score(t.numpy(), prob > 0.3))
+    xm, tm_ = torch.randn(N, L, generator=g) * 3, torch.randint(0, 2, (N, L), generator=g)
+    pm = torch.sigmoid(xm).numpy()
+    _close(F.multilabel_f1_score(xm, tm_, L, average="macro"),
+           sklearn_metrics.f1_score(tm_.numpy(), pm > 0.5, average="macro"))
+
+
+@pytest.mark.parametrize("seed", SEEDS)
+def test_multiclass_calibration_error_vs_numpy(seed):
+    g = _gen(seed)
+    probs, t = torch.randn(N, C, generator=g).softmax(1), torch.randint(0, C, (N,), generator=g)
+    conf, pred = probs.max(1)
+    conf, acc = conf.double().numpy(), (pred == t).double().numpy()
+    n_bins = 15
+    bins = np.clip(np.searchsorted(np.linspace(0, 1, n_bins + 1), conf, side="right") - 1, 0, n_bins - 1)
+    ref = sum(abs(conf[bins == k].mean() - acc[bins == k].mean()) * (bins == k).mean()
+              for k in range(n_bins) if (bins == k).any())
+    _close(F.multiclass_calibration_error(probs, t, C, n_bins=n_bins), ref, atol=1e-5)
