@@ -460,3 +460,31 @@ def test_multiclass_calibration_error_vs_numpy(seed):
     ref = sum(abs(conf[bins == k].mean() - acc[bins == k].mean()) * (bins == k).mean()
               for k in range(n_bins) if (bins == k).any())
     _close(F.multiclass_calibration_error(probs, t, C, n_bins=n_bins), ref, atol=1e-5)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_half_precision_curve_histogram_matches_sklearn_gpu(dtype):
+    """The exact-histogram curve path (one bin per 16-bit score code) is exact: AUROC / AP of half-precision
+    probabilities equal scikit-learn on the same values widened to fp64, ties included."""
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    dev = torch.device("cuda", 0)
+    g = _gen(7)
+    n = 200_000
+    p = torch.rand(n, generator=g).to(dtype)
+    t = (torch.rand(n, generator=g) < p.float()).long()
+    pn, tn = p.double().numpy(), t.numpy()
+    for make, oracle in [(tm.BinaryAUROC, sklearn_metrics.roc_auc_score),
+                         (tm.BinaryAveragePrecision, sklearn_metrics.average_precision_score)]:
+        m = make().to(dev)
+        for chunk in range(4):
+            sl = slice(chunk * n // 4, (chunk + 1) * n // 4)
+            m.update(p[sl].to(dev), t[sl].to(dev))
+        _close(m.compute().cpu(), oracle(tn, pn), atol=1e-6, rtol=1e-6)
+    probs = torch.randn(n // 4, C, generator=g).softmax(1).to(dtype)
+    tc = torch.randint(0, C, (n // 4,), generator=g)
+    m = tm.MulticlassAUROC(num_classes=C).to(dev)
+    m.update(probs.to(dev), tc.to(dev))
+    ref = np.mean([sklearn_metrics.roc_auc_score(tc.numpy() == k, probs[:, k].double().numpy()) for k in range(C)])
+    _close(m.compute().cpu(), ref, atol=1e-6, rtol=1e-6)
