@@ -488,3 +488,18 @@ def test_half_precision_curve_histogram_matches_sklearn_gpu(dtype):
     m.update(probs.to(dev), tc.to(dev))
     ref = np.mean([sklearn_metrics.roc_auc_score(tc.numpy() == k, probs[:, k].double().numpy()) for k in range(C)])
     _close(m.compute().cpu(), ref, atol=1e-6, rtol=1e-6)
+
+
+@pytest.mark.parametrize("seed", SEEDS)
+def test_multilabel_ignore_index_per_label_mask(seed):
+    """Multilabel ``ignore_index`` masks entries per label: each label's score uses only its own kept samples."""
+    g = _gen(seed)
+    p, t = torch.rand(N, L, generator=g), torch.randint(0, 2, (N, L), generator=g)
+    t[torch.rand(N, L, generator=g) < 0.15] = -1
+    ref_auc, ref_ap = [], []
+    for j in range(L):
+        keep = (t[:, j] != -1).numpy()
+        ref_auc.append(sklearn_metrics.roc_auc_score(t[:, j].numpy()[keep], p[:, j].numpy()[keep]))
+        ref_ap.append(sklearn_metrics.average_precision_score(t[:, j].numpy()[keep], p[:, j].numpy()[keep]))
+    _close(F.multilabel_auroc(p, t, L, average=None, ignore_index=-1), ref_auc)
+    _close(F.multilabel_average_precision(p, t, L, average=None, ignore_index=-1), ref_ap)
