@@ -503,3 +503,12 @@ def test_multilabel_ignore_index_per_label_mask(seed):
         ref_ap.append(sklearn_metrics.average_precision_score(t[:, j].numpy()[keep], p[:, j].numpy()[keep]))
     _close(F.multilabel_auroc(p, t, L, average=None, ignore_index=-1), ref_auc)
     _close(F.multilabel_average_precision(p, t, L, average=None, ignore_index=-1), ref_ap)
+
+
+@pytest.mark.parametrize("seed", SEEDS)
+@pytest.mark.parametrize("k", [2, 3])
+def test_top_k_accuracy(seed, k):
+    g = _gen(seed)
+    probs, t = torch.randn(N, C, generator=g).softmax(1), torch.randint(0, C, (N,), generator=g)
+    _close(F.multiclass_accuracy(probs, t, C, average="micro", top_k=k),
+           sklearn_metrics.top_k_accuracy_score(t.numpy(), probs.numpy(), k=k, labels=list(range(C))))
