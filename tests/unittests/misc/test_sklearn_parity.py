@@ -512,3 +512,21 @@ def test_top_k_accuracy(seed, k):
     probs, t = torch.randn(N, C, generator=g).softmax(1), torch.randint(0, C, (N,), generator=g)
     _close(F.multiclass_accuracy(probs, t, C, average="micro", top_k=k),
            sklearn_metrics.top_k_accuracy_score(t.numpy(), probs.numpy(), k=k, labels=list(range(C))))
+
+
+@pytest.mark.parametrize("seed", SEEDS)
+def test_per_class_scores(seed):
+    """``average=None`` returns one score per class, in label order (sklearn ``average=None``)."""
+    g = _gen(seed)
+    logits, t = torch.randn(N, C, generator=g), torch.randint(0, C, (N,), generator=g)
+    hard, tn = logits.argmax(1).numpy(), t.numpy()
+    kw = {"num_classes": C, "average": None}
+    _close(F.multiclass_precision(logits, t, **kw), sklearn_metrics.precision_score(tn, hard, average=None))
+    _close(F.multiclass_recall(logits, t, **kw), sklearn_metrics.recall_score(tn, hard, average=None))
+    _close(F.multiclass_f1_score(logits, t, **kw), sklearn_metrics.f1_score(tn, hard, average=None))
+    _close(F.multiclass_fbeta_score(logits, t, beta=0.5, **kw),
+           sklearn_metrics.fbeta_score(tn, hard, beta=0.5, average=None))
+    _close(F.multiclass_jaccard_index(logits, t, **kw), sklearn_metrics.jaccard_score(tn, hard, average=None))
+    probs = logits.softmax(1)
+    _close(F.multiclass_average_precision(probs, t, **kw),
+           [sklearn_metrics.average_precision_score(tn == k, probs[:, k].numpy()) for k in range(C)])
