@@ -1518,208 +1518,8 @@ void launch_two_pass(const T* p, const int64_t* target, int64_t n, int C, int ld
   launch_class_pass<T>(cptr, n, C, ld, p, target, mode, speculative, srows, state, hist, cm, code_range, speculative ? mode : nullptr);
 }
 
-// ---- one-call overlapped update: row pass on the current stream, class pass on a per-device side stream ----------
-// Events live in a registry keyed by the (per-metric) double-buffered codes scratch: ``done[b]`` marks the class pass
-// that last read buffer b (the row pass that reuses b waits for it), ``ready`` hands the row pass over to the side
-// stream.  All metrics of a device share one side stream; its FIFO order keeps their class passes (and hence every
-// histogram flush) ordered.  Host cost: 2 event records + 2 stream waits, no Python objects.
-struct SideEvents {
-  hipEvent_t ready = nullptr;
-  hipEvent_t done[2] = {nullptr, nullptr};
-};
-
-static SideEvents& side_events(const void* key) {
-  static std::mutex mu;
-  static std::unordered_map<const void*, SideEvents> registry;
-  std::lock_guard<std::mutex> lock(mu);
-  auto it = registry.find(key);
-  if (it != registry.end()) return it->second;
-  SideEvents ev;
-  TMX_CHECK_HIP(hipEventCreateWithFlags(&ev.ready, hipEventDisableTiming));
-  TMX_CHECK_HIP(hipEventCreateWithFlags(&ev.done[0], hipEventDisableTiming));
-  TMX_CHECK_HIP(hipEventCreateWithFlags(&ev.done[1], hipEventDisableTiming));
-  return registry.emplace(key, ev).first->second;
-}
-
-static c10::hip::HIPStream side_stream(c10::DeviceIndex dev) {
-  static std::mutex mu;
-  static std::unordered_map<int, c10::hip::HIPStream> streams;
-  std::lock_guard<std::mutex> lock(mu);
-  auto it = streams.find(dev);
-  if (it == streams.end()) it = streams.emplace(dev, c10::hip::getStreamFromPool(false, dev)).first;
-  return it->second;
-}
-
-void curve_mc_update_overlapped(const at::Tensor& preds, const at::Tensor& target, at::Tensor& mode, at::Tensor& states,
-                                at::Tensor& codes, at::Tensor& slow_rows, int64_t buf, at::Tensor& hist, int64_t ignore_index,
-                                bool has_ignore, c10::optional<at::Tensor> confmat, c10::optional<at::Tensor> err_flag,
-                                c10::optional<at::Tensor> code_range) {
-  TORCH_CHECK(preds.dim() == 2 && preds.is_contiguous() && target.is_contiguous() && target.scalar_type() == at::kLong &&
-              target.numel() == preds.size(0), "curve_mc_update_overlapped: preds [N, C] and int64 target [N], contiguous");
-  const int64_t n = preds.size(0);
-  const int C = static_cast<int>(preds.size(1));
-  TORCH_CHECK(buf == 0 || buf == 1, "buf must be 0 or 1");
-  TORCH_CHECK(C % 8 == 0 && C <= 8 * 2 * kWave && (reinterpret_cast<uintptr_t>(preds.data_ptr()) & 15) == 0,
-              "curve_mc_update_overlapped: C must be a multiple of 8, <= 1024, preds 16-B aligned");
-  const int64_t n_pad = (n + kTileRows - 1) / kTileRows * kTileRows;
-  TORCH_CHECK(codes.dim() == 2 && codes.size(0) == 2 && codes.size(1) >= (int64_t)C * n_pad && codes.scalar_type() == at::kShort &&
-              codes.is_contiguous(), "codes scratch must be int16 [2, >= C * n_pad]");
-  TORCH_CHECK(slow_rows.dim() == 2 && slow_rows.size(0) == 2 && slow_rows.size(1) >= 2 * n && slow_rows.scalar_type() == at::kInt &&
-              slow_rows.is_contiguous(), "slow_rows scratch must be int32 [2, >= 2 N]");
-  TORCH_CHECK(states.scalar_type() == at::kInt && states.numel() == 12 && states.is_contiguous(), "states must be int32 [2, 6]");
-  TORCH_CHECK(mode.scalar_type() == at::kInt && mode.numel() >= 2, "mode must be int32[>= 2]");
-  TORCH_CHECK(hist.is_contiguous() && hist.scalar_type() == at::kLong && hist.numel() == (int64_t)C * 2 * kCodes,
-              "hist must be int64 [C, 2, 16384]");
-  int64_t* cm = nullptr;
-  if (confmat.has_value()) {
-    TORCH_CHECK(confmat->is_contiguous() && confmat->scalar_type() == at::kLong && confmat->numel() == (int64_t)C * C);
-    cm = confmat->data_ptr<int64_t>();
-  }
-  int* err = err_flag.has_value() ? err_flag->data_ptr<int>() : nullptr;
-  int* cr = nullptr;
-  if (code_range.has_value()) {
-    TORCH_CHECK(code_range->scalar_type() == at::kInt && code_range->numel() == 2 * C && code_range->is_contiguous(),
-                "code_range must be int32[C, 2]");
-    cr = code_range->data_ptr<int>();
-  }
-  if (n == 0) return;
-  const c10::DeviceIndex dev = preds.device().index();
-  SideEvents& ev = side_events(codes.data_ptr());
-  const c10::hip::HIPStream main = c10::hip::getCurrentHIPStream(dev);
-  const c10::hip::HIPStream side = side_stream(dev);
-  uint32_t* cptr = reinterpret_cast<uint32_t*>(codes[buf].data_ptr());
-  int* srows = slow_rows[buf].data_ptr<int>();
-  int* state = states.data_ptr<int>() + 6 * buf;
-  TMX_CHECK_HIP(hipStreamWaitEvent(main.stream(), ev.done[buf], 0));  // buffer b free again
-  TMX_DISPATCH_HALF(preds.scalar_type(), "curve_mc_update_overlapped", [&] {
-    const scalar_t* p = reinterpret_cast<const scalar_t*>(preds.data_ptr());
-    launch_row_pass<scalar_t, false>(p, target.data_ptr<int64_t>(), n, C, C, mode.data_ptr<int>(), state, true, ignore_index,
-                                     has_ignore, cm, err, cptr, srows);
-    TMX_CHECK_HIP(hipEventRecord(ev.ready, main.stream()));
-    TMX_CHECK_HIP(hipStreamWaitEvent(side.stream(), ev.ready, 0));
-    {
-      c10::hip::HIPStreamGuard guard(side);
-      launch_class_pass<scalar_t>(cptr, n, C, C, p, target.data_ptr<int64_t>(), state + 3, true, srows, state,
-                                  hist.data_ptr<int64_t>(), cm, cr);
-    }
-    TMX_CHECK_HIP(hipEventRecord(ev.done[buf], side.stream()));
-  });
-  // the side stream reads these after this call returns: keep their blocks from being reused before it is done
-  for (const at::Tensor* t : std::initializer_list<const at::Tensor*>{&preds, &target, &codes, &slow_rows, &states, &hist})
-    c10::hip::HIPCachingAllocator::recordStream(t->storage().data_ptr(), side);
-  if (confmat.has_value()) c10::hip::HIPCachingAllocator::recordStream(confmat->storage().data_ptr(), side);
-  if (code_range.has_value()) c10::hip::HIPCachingAllocator::recordStream(code_range->storage().data_ptr(), side);
-}
-
-// Single-stream overlapped route: ONE dual-role launch runs the row pass of this batch (scratch buffer ``buf``) and the
-// deferred class pass of the previous batch (buffer buf ^ 1: ``prev_preds`` / ``prev_target`` / ``prev_confmat``),
-// then the FIXUP and the speculation roll of this batch (snapshot in states[buf][3:5]).  This batch's class pass is
-// left to the next call or to ``curve_mc_classpass`` (the metric's flush at any state consumer).
-void curve_mc_update_dual(const at::Tensor& preds, const at::Tensor& target, at::Tensor& mode, at::Tensor& states, at::Tensor& codes,
-                          at::Tensor& slow_rows, int64_t buf, at::Tensor& hist, int64_t ignore_index, bool has_ignore,
-                          c10::optional<at::Tensor> confmat, c10::optional<at::Tensor> err_flag, c10::optional<at::Tensor> code_range,
-                          c10::optional<at::Tensor> prev_preds, c10::optional<at::Tensor> prev_target,
-                          c10::optional<at::Tensor> prev_confmat) {
-  TORCH_CHECK(preds.dim() == 2 && preds.is_contiguous() && target.is_contiguous() && target.scalar_type() == at::kLong &&
-              target.numel() == preds.size(0), "curve_mc_update_dual: preds [N, C] and int64 target [N], contiguous");
-  const int64_t n = preds.size(0);
-  const int C = static_cast<int>(preds.size(1));
-  TORCH_CHECK(buf == 0 || buf == 1, "buf must be 0 or 1");
-  TORCH_CHECK(C % 8 == 0 && C <= 8 * 2 * kWave && (reinterpret_cast<uintptr_t>(preds.data_ptr()) & 15) == 0,
-              "curve_mc_update_dual: C must be a multiple of 8, <= 1024, preds 16-B aligned");
-  const int64_t n_pad = (n + kTileRows - 1) / kTileRows * kTileRows;
-  TORCH_CHECK(codes.dim() == 2 && codes.size(0) == 2 && codes.size(1) >= (int64_t)C * n_pad && codes.scalar_type() == at::kShort &&
-              codes.is_contiguous(), "codes scratch must be int16 [2, >= C * n_pad]");
-  TORCH_CHECK(slow_rows.dim() == 2 && slow_rows.size(0) == 2 && slow_rows.size(1) >= 2 * n && slow_rows.scalar_type() == at::kInt &&
-              slow_rows.is_contiguous(), "slow_rows scratch must be int32 [2, >= 2 N]");
-  TORCH_CHECK(states.scalar_type() == at::kInt && states.numel() == 12 && states.is_contiguous(), "states must be int32 [2, 6]");
-  TORCH_CHECK(mode.scalar_type() == at::kInt && mode.numel() >= 2, "mode must be int32[>= 2]");
-  TORCH_CHECK(hist.is_contiguous() && hist.scalar_type() == at::kLong && hist.numel() == (int64_t)C * 2 * kCodes,
-              "hist must be int64 [C, 2, 16384]");
-  auto cm_ptr = [&](const c10::optional<at::Tensor>& t) -> int64_t* {
-    if (!t.has_value()) return nullptr;
-    TORCH_CHECK(t->is_contiguous() && t->scalar_type() == at::kLong && t->numel() == (int64_t)C * C, "confusion matrix int64 [C, C]");
-    return t->data_ptr<int64_t>();
-  };
-  int64_t* cm = cm_ptr(confmat);
-  int64_t* pcm = cm_ptr(prev_confmat);
-  int* err = err_flag.has_value() ? err_flag->data_ptr<int>() : nullptr;
-  int* cr = nullptr;
-  if (code_range.has_value()) {
-    TORCH_CHECK(code_range->scalar_type() == at::kInt && code_range->numel() == 2 * C && code_range->is_contiguous(),
-                "code_range must be int32[C, 2]");
-    cr = code_range->data_ptr<int>();
-  }
-  const bool has_prev = prev_preds.has_value() && prev_target.has_value() && prev_target->numel() > 0;
-  int64_t pn = 0, pn_pad = 0;
-  if (has_prev) {
-    TORCH_CHECK(prev_preds->dim() == 2 && prev_preds->size(1) == C && prev_preds->scalar_type() == preds.scalar_type() &&
-                prev_preds->is_contiguous() && prev_target->scalar_type() == at::kLong && prev_target->is_contiguous() &&
-                prev_target->numel() == prev_preds->size(0), "curve_mc_update_dual: previous batch shapes");
-    pn = prev_preds->size(0);
-    pn_pad = (pn + kTileRows - 1) / kTileRows * kTileRows;
-    TORCH_CHECK(codes.size(1) >= (int64_t)C * pn_pad && slow_rows.size(1) >= 2 * pn, "curve_mc_update_dual: scratch too small for the previous batch");
-  }
-  const int pb = static_cast<int>(buf ^ 1);
-  uint32_t* cptr = reinterpret_cast<uint32_t*>(codes[buf].data_ptr());
-  int* srows = slow_rows[buf].data_ptr<int>();
-  int* state = states.data_ptr<int>() + 6 * buf;
-  int* pstate = states.data_ptr<int>() + 6 * pb;
-  TMX_DISPATCH_HALF(preds.scalar_type(), "curve_mc_update_dual", [&] {
-    const scalar_t* p = reinterpret_cast<const scalar_t*>(preds.data_ptr());
-    const int64_t ntiles = n_pad / kTileRows;
-    const int64_t row_blocks = n > 0 ? (ntiles + 7) / 8 * 8 : 0;
-    const int fixup_grid = static_cast<int>(std::min<int64_t>(std::max<int64_t>(row_blocks, 8), 128));
-    const size_t row_shm = (size_t)512 * (C > 512 ? 2 : 1) * kSlots * sizeof(uint32_t);
-    int splits = 1;
-    while (has_prev && (int64_t)C * splits < 512 && pn_pad / (8 * (splits * 2)) >= 1024) splits *= 2;
-    const int64_t class_blocks = has_prev ? (int64_t)C * splits : 0;
-    const int64_t groups = row_blocks / 8 + (class_blocks + 7) / 8;
-    if (groups > 0) {
-      const size_t shm = std::max(row_shm, has_prev ? (size_t)kCodes * sizeof(uint32_t) : (size_t)0);
-      const scalar_t* pp = has_prev ? reinterpret_cast<const scalar_t*>(prev_preds->data_ptr()) : p;
-      const int64_t* pt = has_prev ? prev_target->data_ptr<int64_t>() : target.data_ptr<int64_t>();
-      const uint16_t* pc = reinterpret_cast<const uint16_t*>(codes[pb].data_ptr());
-      const int* ps = slow_rows[pb].data_ptr<int>();
-      if (C > 512)
-        hipLaunchKernelGGL((mc_dual_kernel<scalar_t, 2>), static_cast<int>(groups * 8), kRowThreads, shm, stream(), p,
-                           target.data_ptr<int64_t>(), n, C, mode.data_ptr<int>(), ignore_index, has_ignore, cptr, n_pad, cm, err, srows,
-                           state, row_blocks, pc, pn_pad, splits, hist.data_ptr<int64_t>(), pp, pt, pn, pstate + 3, ps, pstate, pcm, cr,
-                           class_blocks, groups, (class_blocks + 7) / 8);
-      else
-        hipLaunchKernelGGL((mc_dual_kernel<scalar_t, 1>), static_cast<int>(groups * 8), kRowThreads, shm, stream(), p,
-                           target.data_ptr<int64_t>(), n, C, mode.data_ptr<int>(), ignore_index, has_ignore, cptr, n_pad, cm, err, srows,
-                           state, row_blocks, pc, pn_pad, splits, hist.data_ptr<int64_t>(), pp, pt, pn, pstate + 3, ps, pstate, pcm, cr,
-                           class_blocks, groups, (class_blocks + 7) / 8);
-      TMX_LAUNCH_CHECK();
-    }
-    if (n > 0) {
-      if (C > 512)
-        hipLaunchKernelGGL((mc_codes_kernel<scalar_t, true, 2, false>), fixup_grid, kRowThreads, row_shm, stream(), p,
-                           target.data_ptr<int64_t>(), n, C, C, mode.data_ptr<int>(), ignore_index, has_ignore, cptr, n_pad, cm, err, false,
-                           srows, state);
-      else
-        hipLaunchKernelGGL((mc_codes_kernel<scalar_t, true, 1, false>), fixup_grid, kRowThreads, row_shm, stream(), p,
-                           target.data_ptr<int64_t>(), n, C, C, mode.data_ptr<int>(), ignore_index, has_ignore, cptr, n_pad, cm, err, false,
-                           srows, state);
-      TMX_LAUNCH_CHECK();
-      hipLaunchKernelGGL(mode_roll_kernel, 1, 1, 0, stream(), mode.data_ptr<int>(), state + 3);
-      TMX_LAUNCH_CHECK();
-    }
-  });
-}
-
-// Make the current stream wait for every class pass issued on the scratch ``codes`` (no-op for unknown buffers).
-void curve_side_join(const at::Tensor& codes) {
-  SideEvents& ev = side_events(codes.data_ptr());
-  const hipStream_t main = c10::hip::getCurrentHIPStream(codes.device().index()).stream();
-  TMX_CHECK_HIP(hipStreamWaitEvent(main, ev.done[0], 0));
-  TMX_CHECK_HIP(hipStreamWaitEvent(main, ev.done[1], 0));
-}
-
-// Split form of the speculative multiclass route for a side-stream class pass (module updates): the caller owns the
-// double-buffered scratch and orders the two launches with events (the class pass of batch k overlaps the row pass of
-// batch k + 1).  Both run on the current stream of their call.
+// The row pass alone into caller-owned scratch (class-major codes + rare-row list): the per-element code pin of
+// tests/test_ops_gpu.py::test_curve_hist_codes_vs_aten_softmax_same_device reads the codes it writes.
 void curve_mc_rowpass(const at::Tensor& preds, const at::Tensor& target, at::Tensor& mode, at::Tensor& state, at::Tensor& codes,
                       at::Tensor& slow_rows, int64_t ignore_index, bool has_ignore, c10::optional<at::Tensor> confmat,
                       c10::optional<at::Tensor> err_flag) {
@@ -1744,29 +1544,6 @@ void curve_mc_rowpass(const at::Tensor& preds, const at::Tensor& target, at::Ten
     launch_row_pass<scalar_t, false>(reinterpret_cast<const scalar_t*>(preds.data_ptr()), target.data_ptr<int64_t>(), n, C, C,
                                      mode.data_ptr<int>(), state.data_ptr<int>(), true, ignore_index, has_ignore, cm, err,
                                      reinterpret_cast<uint32_t*>(codes.data_ptr()), slow_rows.data_ptr<int>());
-  });
-}
-
-void curve_mc_classpass(const at::Tensor& codes, const at::Tensor& slow_rows, at::Tensor& state, at::Tensor& hist,
-                        const at::Tensor& preds, const at::Tensor& target, c10::optional<at::Tensor> confmat,
-                        c10::optional<at::Tensor> code_range) {
-  const int64_t n = preds.size(0);
-  const int C = static_cast<int>(preds.size(1));
-  TORCH_CHECK(hist.is_contiguous() && hist.scalar_type() == at::kLong && hist.numel() == (int64_t)C * 2 * kCodes,
-              "curve_mc_classpass: hist must be int64 [C, 2, 16384]");
-  int64_t* cm = confmat.has_value() ? confmat->data_ptr<int64_t>() : nullptr;
-  int* cr = nullptr;
-  if (code_range.has_value()) {
-    TORCH_CHECK(code_range->scalar_type() == at::kInt && code_range->numel() == 2 * C && code_range->is_contiguous(),
-                "code_range must be int32[C, 2]");
-    cr = code_range->data_ptr<int>();
-  }
-  if (n == 0) return;
-  TMX_DISPATCH_HALF(preds.scalar_type(), "curve_mc_classpass", [&] {
-    launch_class_pass<scalar_t>(reinterpret_cast<const uint32_t*>(codes.data_ptr()), n, C, C,
-                                reinterpret_cast<const scalar_t*>(preds.data_ptr()), target.data_ptr<int64_t>(),
-                                state.data_ptr<int>() + 3, true, slow_rows.data_ptr<int>(), state.data_ptr<int>(),
-                                hist.data_ptr<int64_t>(), cm, cr);
   });
 }
 
@@ -2828,11 +2605,7 @@ TORCH_LIBRARY_FRAGMENT(tmx, m) {
   m.def("curve_hist_update(Tensor preds, Tensor target, Tensor(a!) hist, int task, int ignore_index, bool has_ignore, Tensor(b!)? confmat, Tensor? norm_flag, Tensor(c!)? err_flag, Tensor(d!)? mode_state, Tensor(e!)? code_range=None) -> ()");
   m.def("curve_hist_reduce(Tensor hist, Tensor? code_range=None) -> Tensor");
   m.def("curve_summary(Tensor scores) -> Tensor");
-  m.def("curve_mc_update_overlapped(Tensor preds, Tensor target, Tensor(a!) mode, Tensor(b!) states, Tensor(c!) codes, Tensor(d!) slow_rows, int buf, Tensor(e!) hist, int ignore_index, bool has_ignore, Tensor(f!)? confmat, Tensor(g!)? err_flag, Tensor(h!)? code_range) -> ()");
-  m.def("curve_side_join(Tensor codes) -> ()");
-  m.def("curve_mc_update_dual(Tensor preds, Tensor target, Tensor(a!) mode, Tensor(b!) states, Tensor(c!) codes, Tensor(d!) slow_rows, int buf, Tensor(e!) hist, int ignore_index, bool has_ignore, Tensor(f!)? confmat, Tensor(g!)? err_flag, Tensor(h!)? code_range, Tensor? prev_preds, Tensor? prev_target, Tensor(i!)? prev_confmat) -> ()");
   m.def("curve_mc_rowpass(Tensor preds, Tensor target, Tensor(a!) mode, Tensor(b!) state, Tensor(c!) codes, Tensor(d!) slow_rows, int ignore_index, bool has_ignore, Tensor(e!)? confmat, Tensor(f!)? err_flag) -> ()");
-  m.def("curve_mc_classpass(Tensor codes, Tensor slow_rows, Tensor(a!) state, Tensor(b!) hist, Tensor preds, Tensor target, Tensor(c!)? confmat, Tensor(d!)? code_range) -> ()");
   m.def("binned_curve_update(Tensor preds, Tensor target, Tensor thresholds, Tensor(a!) confmat, int task, int ignore_index, bool has_ignore, Tensor? norm_flag, Tensor(b!)? err_flag=None) -> ()");
   m.def("ce_bins_update(Tensor conf, Tensor acc, Tensor boundaries, Tensor(a!) bins) -> ()");
   m.def("mc_calibration_update(Tensor preds, Tensor target, Tensor boundaries, Tensor(a!) bins) -> ()");
@@ -2850,10 +2623,6 @@ TORCH_LIBRARY_IMPL(tmx, CUDA, m) {
   m.impl("curve_hist_reduce", &tmx::curve_hist_reduce);
   m.impl("curve_summary", &tmx::curve_summary);
   m.impl("curve_mc_rowpass", &tmx::curve_mc_rowpass);
-  m.impl("curve_mc_update_overlapped", &tmx::curve_mc_update_overlapped);
-  m.impl("curve_side_join", &tmx::curve_side_join);
-  m.impl("curve_mc_update_dual", &tmx::curve_mc_update_dual);
-  m.impl("curve_mc_classpass", &tmx::curve_mc_classpass);
   m.impl("binned_curve_update", &tmx::binned_curve_update);
   m.impl("ce_bins_update", &tmx::ce_bins_update);
   m.impl("mc_calibration_update", &tmx::mc_calibration_update);

@@ -974,42 +974,9 @@ __global__ void __launch_bounds__(256) class_partial_reduce_kernel(const uint32_
   if (pos) hist[((int64_t)c * 2 + 1) * kCodes + i] += static_cast<int64_t>(pos);
 }
 
-// Dual-role launch: the row pass of batch k and the class pass of batch k - 1 (the other scratch buffer) in ONE grid,
-// so the long HBM-bound class blocks run beside the row tiles on every CU instead of after them (two 64-KiB blocks
-// per CU whatever their roles; the side-stream variant could not co-reside, profiles/side_stream_overlap.json).
-// Physical blocks come in groups of 8 (one per XCD); group g is a class group when the even spread of the
-// ``class_groups`` over all ``groups`` says so, and virtual ids keep ``vb % 8`` = the physical XCD, so the row role
-// keeps its XCD-aware tile order.  Class blocks run with the row pass's 512 threads.
-template <typename T, int NG>
-__global__ void __launch_bounds__(kRowThreads, 4) mc_dual_kernel(
-    const T* __restrict__ preds, const int64_t* __restrict__ target, int64_t n, int C, int* __restrict__ mode, int64_t ignore_index,
-    bool has_ignore, uint32_t* __restrict__ codes, int64_t n_pad, int64_t* __restrict__ confmat, int* __restrict__ err,
-    int* __restrict__ slow_rows, int* __restrict__ slow_count, int64_t row_blocks,
-    const uint16_t* __restrict__ pcodes, int64_t pn_pad, int splits, int64_t* __restrict__ hist, const T* __restrict__ ppreds,
-    const int64_t* __restrict__ ptarget, int64_t pn, const int* __restrict__ pbmode, const int* __restrict__ pslow_rows,
-    int* __restrict__ pstate, int64_t* __restrict__ pconfmat, int* __restrict__ code_range, int64_t class_blocks, int64_t groups,
-    int64_t class_groups) {
-  const int64_t g = blockIdx.x / 8, x = blockIdx.x % 8;
-  const int64_t cg_before = g * class_groups / groups;
-  const bool is_class = (g + 1) * class_groups / groups > cg_before;
-  if (is_class) {
-    const int64_t vb = cg_before * 8 + x;
-    if (vb >= class_blocks) return;
-    class_hist_block<T, false, kRowThreads>(vb, class_blocks, pcodes, pn_pad, splits, hist, ppreds, C, ptarget, pn, pbmode, true,
-                                            pslow_rows, pstate, pconfmat, code_range, nullptr);
-  } else {
-    const int64_t vb = (g - cg_before) * 8 + x;
-    if (vb >= row_blocks) return;
-    mc_codes_block<T, false, NG, false>(vb, row_blocks, preds, target, n, C, C, mode, ignore_index, has_ignore, codes, n_pad, confmat,
-                                        err, true, slow_rows, slow_count);
-  }
-}
-
-// Speculation roll, one thread, in row-pass stream order right after the FIXUP launch (side-stream route; the
-// single-stream route rolls in the class pass's last workgroup instead, one launch fewer): the batch's (used, real) mode
-// pair is snapshotted into its own state (``bmode`` = state[3:5], read by that batch's class pass) and the next batch
-// speculates the real one.  Keeping the roll out of the class pass lets the class pass of batch k run on a side
-// stream while the row pass of batch k + 1 reads the rolled word.
+// Speculation roll, one thread, in row-pass stream order right after the FIXUP launch (standalone row pass only; the
+// update route rolls in the class pass's last workgroup instead, one launch fewer): the batch's (used, real) mode pair
+// is snapshotted into ``bmode`` = state[3:5] and the next batch speculates the real one.
 __global__ void mode_roll_kernel(int* __restrict__ mode, int* __restrict__ bmode) {
   const int m0 = mode[0], m1 = mode[1];
   bmode[0] = m0;

@@ -704,89 +704,6 @@ def _flip_batches(C, N, seed=5):
     return out
 
 
-@pytest.mark.parametrize("C", [520, 1000])
-def test_side_stream_class_pass_matches_single_stream(C, monkeypatch):
-    """Back-to-back updates with the class pass on a side stream (overlapping the next row pass, double-buffered
-    scratch, rolled speculation word) give exactly the single-stream histogram, confusion matrix and code range —
-    across speculation flips, rare rows, a reset in the middle and state_dict / compute consumers."""
-    import torchmetrics_forked_amd as tm
-
-    N = 4096 + 32 * 7 + 5
-    batches = [(x.cuda(), t.cuda()) for x, t in _flip_batches(C, N)]
-
-    def run(side: bool):
-        monkeypatch.setenv("TMX_CURVE_SIDE_STREAM", "1" if side else "0")
-        coll = tm.MetricCollection({"auroc": tm.MulticlassAUROC(num_classes=C, average=None),
-                                    "cm": tm.MulticlassConfusionMatrix(num_classes=C)}).cuda()
-        snaps = []
-        for k, (x, t) in enumerate(batches):
-            coll.update(x, t)
-            if k == 3:
-                snaps.append({n: v.clone() for n, v in coll["auroc"].metric_state.items() if isinstance(v, torch.Tensor)})
-                coll.reset()
-        out = coll.compute()
-        st = coll["auroc"]
-        return out, st.score_hist.clone(), st._tracked_range().clone(), snaps
-
-    a, ha, ra, sa = run(True)
-    b, hb, rb, sb = run(False)
-    assert torch.equal(ha, hb)
-    assert torch.equal(ra, rb)
-    assert torch.equal(a["cm"], b["cm"])
-    torch.testing.assert_close(a["auroc"], b["auroc"], rtol=0, atol=0)
-    assert torch.equal(sa[0]["score_hist"], sb[0]["score_hist"])
-
-
-@pytest.mark.parametrize("C", [520, 1000])
-@pytest.mark.parametrize("members", ["auroc+cm", "auroc", "auroc+cm+acc"])
-def test_dual_role_update_matches_sequential(C, members, monkeypatch):
-    """One dual-role launch per update (this batch's row pass + the previous batch's class pass in one grid, the last
-    class pass flushed by the first state consumer) gives exactly the sequential route's histogram, code range,
-    confusion matrix and stat states -- across speculation flips, rare rows, growing / shrinking batch sizes (scratch
-    re-allocation with a pending class pass), a reset, a clone and a state_dict in the middle."""
-    import copy
-
-    import torchmetrics_forked_amd as tm
-
-    sizes = [4096 + 32 * 7 + 5, 1000, 6000, 4096 + 3, 777, 5000, 4096, 2049]
-    gen = torch.Generator().manual_seed(9)
-    batches = []
-    for k, (x, t) in enumerate(_flip_batches(C, max(sizes))):
-        batches.append((x[: sizes[k]].cuda(), t[: sizes[k]].cuda()))
-
-    def run(dual: bool):
-        monkeypatch.setenv("TMX_CURVE_SIDE_STREAM", "0")
-        monkeypatch.setenv("TMX_CURVE_DUAL", "1" if dual else "0")  # opt-in route vs the default
-        ms = {"auroc": tm.MulticlassAUROC(num_classes=C, average=None)}
-        if "cm" in members:
-            ms["cm"] = tm.MulticlassConfusionMatrix(num_classes=C)
-        if "acc" in members:
-            ms["acc"] = tm.MulticlassAccuracy(num_classes=C, average=None)
-        coll = tm.MetricCollection(ms).cuda()
-        snaps = []
-        for k, (x, t) in enumerate(batches):
-            coll.update(x, t)
-            if k == 2:
-                snaps.append(copy.deepcopy(coll["auroc"]).score_hist.clone())
-            if k == 3:
-                snaps.append(coll["auroc"].metric_state["score_hist"].clone())
-                coll.reset()
-            if k == 5:
-                snaps.append({n: v.clone() for n, v in coll["auroc"].state_dict().items()})
-        out = coll.compute()
-        st = coll["auroc"]
-        return out, st.score_hist.clone(), st._tracked_range().clone(), snaps
-
-    a, ha, ra, sa = run(True)
-    b, hb, rb, sb = run(False)
-    assert torch.equal(ha, hb)
-    assert torch.equal(ra, rb)
-    for k in a:
-        torch.testing.assert_close(a[k], b[k], rtol=0, atol=0, msg=k)
-    assert torch.equal(sa[0], sb[0]) and torch.equal(sa[1], sb[1])
-    assert sa[2].keys() == sb[2].keys() and all(torch.equal(sa[2][k], sb[2][k]) for k in sa[2])
-
-
 @pytest.mark.parametrize("strategy", ["warn", "ignore", "error"])
 def test_cat_metric_gpu_defers_nan_drop(strategy):
     """CatMetric on the GPU: no host sync per update (NaN policy as a device flag, NaN entries dropped once by the

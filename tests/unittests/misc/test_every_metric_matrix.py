@@ -655,3 +655,41 @@ def test_gpu_vs_cpu(name):
     for a, b in zip(g_vals, c_vals):
         _values_equal(a, b, atol)
     _values_equal(g_res, c_res, atol)
+
+
+# ---- TorchScript: every spec (the reference's testers script every metric class by default, testers.py:131-133) --------
+# The wrappers below take ``*args`` / ``**kwargs`` in update / forward, which TorchScript cannot compile; the reference's
+# classes fail identically (checked by test_scriptable_exemptions_fail_in_reference too).
+SCRIPT_EXEMPT = {
+    "BootStrapper": "update(*args, **kwargs)", "ClasswiseWrapper": "update(*args, **kwargs)",
+    "MinMaxMetric": "update(*args, **kwargs)", "Running": "update(*args, **kwargs)",
+    "RunningMean": "Running(MeanMetric): update(*args, **kwargs)", "RunningSum": "Running(SumMetric): update(*args, **kwargs)",
+    "MultitaskWrapper": "update(task_preds: Dict, task_targets: Dict) over nested metrics (JIT internal assert, as the reference)",
+}
+
+
+@pytest.mark.parametrize("name", sorted(n for n in SPECS if n not in SCRIPT_EXEMPT))
+def test_scriptable(name):
+    """``torch.jit.script`` on a fresh and on an updated module; scripting leaves the eager value unchanged."""
+    spec = SPECS[name]
+    torch.jit.script(spec.make(tm))
+    metric = spec.make(tm)
+    for b in _data(spec.data):
+        metric.update(*b)
+    if spec.seeded:
+        torch.manual_seed(11)
+    before = metric.compute()
+    torch.jit.script(metric)
+    metric._computed = None
+    if spec.seeded:
+        torch.manual_seed(11)
+    _values_equal(metric.compute(), before, 0.0)
+
+
+@pytest.mark.parametrize("name", sorted(SCRIPT_EXEMPT))
+def test_scriptable_exemptions_fail_in_reference(reference, name):
+    spec = SPECS[name]
+    with pytest.raises(Exception):
+        torch.jit.script(spec.make(tm))
+    with pytest.raises(Exception):
+        torch.jit.script(spec.make(reference))

@@ -44,89 +44,6 @@ from torchmetrics_forked_amd.utilities.enums import ClassificationTask
 from torchmetrics_forked_amd.utilities.plot import _AX_TYPE, _PLOT_OUT_TYPE, plot_curve
 
 
-def _side_stream_ok(p: Tensor, rng: Optional[Tensor]) -> bool:
-    """The split (side-stream) route takes aligned ``[N, C]`` 16-bit rows with C % 8 == 0, C <= 1024 on the GPU.
-
-    Opt-in (``TMX_CURVE_SIDE_STREAM=1``): measured on MI355X at 65536 x 1000 bf16, back-to-back updates take
-    117.7 us each with the class pass overlapping the next row pass vs 110.5 us on one stream
-    (``profiles/side_stream_overlap.json``).  The row pass holds 128 KiB of LDS per CU (two 64-KiB blocks), so a
-    64-KiB class-pass block cannot co-reside; the two passes only time-slice the CUs and compete for HBM."""
-    if rng is None or not p.is_cuda or os.environ.get("TMX_CURVE_SIDE_STREAM", "0") != "1":
-        return False
-    n, c = p.shape
-    return p.is_contiguous() and c % 8 == 0 and c <= 1024 and p.data_ptr() % 16 == 0 and n > 0
-
-
-def metric_dual_buffers(metric: Any, p: Tensor) -> dict:
-    """Double-buffered scratch of the dual-role route in ``__dict__["_dual_bufs"]`` (left out of pickling): class-major
-    codes, rare-row lists, pass states, and the pending (previous) batch whose class pass has not run yet.  ``flush``
-    runs that class pass on the current stream (idempotent)."""
-    n, c = p.shape
-    n_pad = (n + 31) // 32 * 32
-    bufs = metric.__dict__.get("_dual_bufs")
-    if bufs is not None and (bufs["codes"].device != p.device or bufs["codes"].shape[1] < c * n_pad or bufs["rows"].shape[1] < 2 * n):
-        bufs["flush"]()  # the pending class pass reads the old scratch: run it before the scratch is replaced
-        bufs = None
-    if bufs is None:
-        bufs = {
-            "codes": torch.empty(2, c * n_pad, dtype=torch.int16, device=p.device),
-            "rows": torch.empty(2, 2 * n, dtype=torch.int32, device=p.device),
-            "states": torch.zeros(2, 6, dtype=torch.int32, device=p.device),
-            "next": 0,
-            "pending": None,
-        }
-
-        def flush(b: dict = bufs) -> None:
-            pend = b["pending"]
-            if pend is None:
-                return
-            b["pending"] = None
-            j = pend["buf"]
-            torch.ops.tmx.curve_mc_classpass(
-                b["codes"][j], b["rows"][j], b["states"][j], pend["hist"], pend["p"], pend["t"], pend["cm"], pend["rng"]
-            )
-
-        bufs["flush"] = flush
-        metric.__dict__["_dual_bufs"] = bufs
-    return bufs
-
-
-def _dual_ok(p: Tensor, rng: Optional[Tensor]) -> bool:
-    """Opt-in (``TMX_CURVE_DUAL=1``) multiclass exact-histogram route: aligned ``[N, C]`` 16-bit rows with C % 8 == 0,
-    C <= 1024.  Each update is one dual-role launch -- this batch's row pass and the previous batch's class pass in
-    one grid (csrc/curve_hist_kernels.h ``mc_dual_kernel``) -- and the last class pass is flushed by the first
-    consumer of the states (``Metric._join_side_work``).  Measured on MI355X at 65536 x 1000 bf16 (bench.py, 50
-    steps): 0.133 ms per update vs 0.124 ms sequential (``profiles/dual_role_update.json``): the sequential class
-    pass reads the codes the row pass just wrote partly from the Infinity Cache (FETCH_SIZE ~76 of 131 MB), the
-    deferred one reads them after the next batch's logits and codes have streamed through it."""
-    if rng is None or not p.is_cuda or os.environ.get("TMX_CURVE_DUAL", "0") != "1":
-        return False
-    n, c = p.shape
-    return p.is_contiguous() and c % 8 == 0 and c <= 1024 and p.data_ptr() % 16 == 0 and n > 0
-
-
-def _side_buffers(metric: Any, p: Tensor) -> dict:
-    """Per-metric double-buffered scratch (class-major codes, rare-row lists, pass states) for the overlapped update,
-    in ``__dict__["_side_bufs"]`` (left out of pickling / deepcopy by ``Metric.__getstate__``); the side stream and
-    its events live in the native library, keyed by the codes buffer."""
-    n, c = p.shape
-    n_pad = (n + 31) // 32 * 32
-    bufs = metric.__dict__.get("_side_bufs")
-    if bufs is None or bufs["codes"].device != p.device or bufs["codes"].shape[1] < c * n_pad or bufs["rows"].shape[1] < 2 * n:
-        if bufs is not None:  # buffers about to be dropped: the current stream waits for their last readers
-            bufs["join"]()
-        codes = torch.empty(2, c * n_pad, dtype=torch.int16, device=p.device)
-        bufs = {
-            "codes": codes,
-            "rows": torch.empty(2, 2 * n, dtype=torch.int32, device=p.device),
-            "states": torch.zeros(2, 6, dtype=torch.int32, device=p.device),
-            "next": 0,
-            "join": lambda: torch.ops.tmx.curve_side_join(codes),
-        }
-        metric.__dict__["_side_bufs"] = bufs
-    return bufs
-
-
 class _CurveMetric(Metric):
     """Owns the curve states; subclasses choose the task and implement ``compute`` from ``_curve_state()``."""
 
@@ -284,14 +201,9 @@ class _CurveMetric(Metric):
                 )
             elif self._task == "multiclass":
                 p = torch.movedim(preds, 1, -1).reshape(-1, self._num)
-                if _side_stream_ok(p, rng):
-                    self._mc_update_side_stream(p, target.reshape(-1), hist, ii, confmat_out, err_flag, rng)
-                elif _dual_ok(p, rng):
-                    self._mc_update_dual(p, target.reshape(-1), hist, ii, confmat_out, err_flag, rng)
-                else:
-                    cls_ops.curve_hist_update(
-                        p, target.reshape(-1), hist, "multiclass", ii, confmat_out, err_flag, self._mode_state(p), code_range=rng
-                    )
+                cls_ops.curve_hist_update(
+                    p, target.reshape(-1), hist, "multiclass", ii, confmat_out, err_flag, self._mode_state(p), code_range=rng
+                )
             else:
                 cls_ops.curve_hist_update(preds, target, hist, "multilabel", ii, err_flag=err_flag, code_range=rng)
             if rng is None:
@@ -322,50 +234,6 @@ class _CurveMetric(Metric):
             st = multilabel_curve_update(preds, target, self._num, None, ii, force_samples=True)
         self.preds.append(st[1])
         self.target.append(st[2])
-
-    def _mc_update_side_stream(
-        self, p: Tensor, target: Tensor, hist: Tensor, ii: Optional[int], confmat_out: Optional[Tensor],
-        err_flag: Optional[Tensor], rng: Tensor,
-    ) -> None:
-        """Multiclass exact-histogram update with the class pass on a side stream.
-
-        The row pass (softmax codes, arg-max + confusion matrix, HBM-bound) runs on the current stream and writes
-        class-major codes into one of two scratch buffers; the class pass (LDS histograms, flush into
-        ``score_hist``) of this batch then runs on a side stream and overlaps the NEXT batch's row pass, which uses
-        the other buffer.  Reusing a buffer waits for the class pass that last read it; every state consumer joins
-        the side stream first (``Metric._join_side_work``)."""
-        bufs = _side_buffers(self, p)
-        i = bufs["next"]
-        bufs["next"] = i ^ 1
-        t = target if target.dtype == torch.long and target.is_contiguous() else target.long().contiguous()
-        torch.ops.tmx.curve_mc_update_overlapped(
-            p, t, self._mode_state(p), bufs["states"], bufs["codes"], bufs["rows"], i, hist, -1 if ii is None else ii,
-            ii is not None, confmat_out, err_flag, rng,
-        )
-        self.__dict__["_side_event"] = bufs["join"]
-
-    def _mc_update_dual(
-        self, p: Tensor, target: Tensor, hist: Tensor, ii: Optional[int], confmat_out: Optional[Tensor],
-        err_flag: Optional[Tensor], rng: Tensor,
-    ) -> None:
-        """Multiclass exact-histogram update as one dual-role launch (this batch's row pass + the previous batch's
-        class pass, double-buffered scratch); this batch's class pass stays pending until the next update or the
-        first state consumer (``_side_event`` = the flush)."""
-        bufs = metric_dual_buffers(self, p)
-        pend = bufs["pending"]
-        if pend is not None and (pend["hist"] is not hist or pend["rng"] is not rng):
-            bufs["flush"]()  # the states were replaced since: finish the old batch on its own first
-            pend = None
-        i = bufs["next"]
-        bufs["next"] = i ^ 1
-        t = target if target.dtype == torch.long and target.is_contiguous() else target.long().contiguous()
-        torch.ops.tmx.curve_mc_update_dual(
-            p, t, self._mode_state(p), bufs["states"], bufs["codes"], bufs["rows"], i, hist, -1 if ii is None else ii,
-            ii is not None, confmat_out, err_flag, rng,
-            pend["p"] if pend else None, pend["t"] if pend else None, pend["cm"] if pend else None,
-        )
-        bufs["pending"] = {"p": p, "t": t, "buf": i, "cm": confmat_out, "hist": hist, "rng": rng}
-        self.__dict__["_side_event"] = bufs["flush"]
 
     def _reduce_states(self, incoming_state: dict) -> None:
         """``forward`` merge: the lazily materialised histogram may be empty on either side."""
@@ -415,6 +283,10 @@ class _CurveMetric(Metric):
         self.score_hist = hist
         self._set_range(hist, torch.tensor([lo, hi], dtype=torch.int32, device=hist.device).repeat(owned, 1), None)
         self._shard_info = (first, owned, per, group)
+
+    def _leave_batch_mode(self, saved_compute_on_cpu: bool) -> None:
+        super()._leave_batch_mode(saved_compute_on_cpu)
+        self._shard_info = None  # a batch compute's sharded sync is never unsynced: forget it with the synced flag
 
     def unsync(self, should_unsync: bool = True) -> None:
         super().unsync(should_unsync)

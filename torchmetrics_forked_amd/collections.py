@@ -23,6 +23,7 @@ from torch import Tensor
 from torch.nn import ModuleDict
 
 from torchmetrics_forked_amd.metric import Metric
+from torchmetrics_forked_amd.parallel.sync import _REDUCE_OPS as _ALLREDUCED
 from torchmetrics_forked_amd.parallel.sync import PendingSyncMany, sync_states_many, sync_timeout
 from torchmetrics_forked_amd.utilities.data import _flatten_dict, allclose
 from torchmetrics_forked_amd.utilities.plot import _AX_TYPE, _PLOT_OUT_TYPE, plot_single_or_multi_val
@@ -200,7 +201,13 @@ class MetricCollection(ModuleDict):
         size = 0
         for m in eligible:
             batches[-1].append(m)
-            size += sum(v.numel() * v.element_size() for v in m.metric_state.values() if isinstance(v, Tensor))
+            # only all-reduced states count: their shapes agree on every rank, so every rank cuts the groups at the
+            # same members ('cat' / None / custom states may differ in size per rank)
+            size += sum(
+                v.numel() * v.element_size()
+                for k, v in m.metric_state.items()
+                if isinstance(v, Tensor) and m._reductions.get(k) in _ALLREDUCED
+            )
             if size >= self._OVERLAP_GROUP_BYTES:
                 batches.append([])
                 size = 0
@@ -294,8 +301,30 @@ class MetricCollection(ModuleDict):
         mods = {k: m for k, m in self.items(keep_base=True, copy_state=False) if k not in skip and m._step_sync_ok()}
         if not mods:
             return {}
-        ctx = {k: m._step_sync_begin(args, m._filter_kwargs(**kwargs)) for k, m in mods.items()}
-        return {k: m._step_sync_end(ctx[k]) for k, m in mods.items()}
+        # exception-safe: a member whose begin or end raises must not strand the others in batch mode with their
+        # global state parked in a ctx (and their launched collectives unwaited) -- every started member is finished
+        ctx: Dict[str, Any] = {}
+        out: Dict[str, Any] = {}
+        try:
+            for k, m in mods.items():
+                ctx[k] = m._step_sync_begin(args, m._filter_kwargs(**kwargs))
+        except BaseException:
+            for k in list(ctx):
+                try:
+                    mods[k]._step_sync_end(ctx.pop(k))
+                except Exception:  # noqa: S110 - the first error is the one to report
+                    pass
+            raise
+        err: Optional[BaseException] = None
+        for k in list(ctx):
+            try:
+                out[k] = mods[k]._step_sync_end(ctx.pop(k))
+            except BaseException as e:  # finish (restore) the remaining members, then re-raise the first error
+                if err is None:
+                    err = e
+        if err is not None:
+            raise err
+        return out
 
     def _compute_and_reduce(self, method_name: str, *args: Any, **kwargs: Any) -> Dict[str, Any]:
         result = {}

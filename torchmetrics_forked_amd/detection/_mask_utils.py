@@ -177,6 +177,12 @@ def rle_segm_ious(
     for i in range(n_img):
         e = (det[i][0] if d_sizes[i] else gt[i][0] if g_sizes[i] else None)
         if e is not None:
+            sizes = {(int(x[0][0]), int(x[0][1])) for x in (list(det[i]) if d_sizes[i] else []) + list(gt[i])}
+            if len(sizes) > 1:
+                # one decode size per image: a mismatch would be clamped by the decoder into wrong IoUs / areas
+                raise ValueError(
+                    f"Image {i}: predicted and ground-truth masks must have the same spatial size, got {sorted(sizes)}"
+                )
             by_size.setdefault((int(e[0][0]), int(e[0][1])), []).append(i)
     for (h, w), imgs in by_size.items():
         words = (h * w + 63) // 64

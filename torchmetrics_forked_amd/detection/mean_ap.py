@@ -18,7 +18,7 @@ category ids in the COCO dataset while relabelling every annotation to 0, which 
 is not one of the labels).
 """
 import json
-from typing import Any, Dict, List, Literal, Optional, Sequence, Tuple, Union
+from typing import ClassVar, Any, Dict, List, Literal, Optional, Sequence, Tuple, Union
 
 import numpy as np
 import torch
@@ -63,17 +63,23 @@ class MeanAveragePrecision(Metric):
     plot_lower_bound: float = 0.0
     plot_upper_bound: float = 1.0
 
+    # TorchScript-facing declarations (as the reference's ``mean_ap.py:325-350``): the mask states actually hold one
+    # tuple of ``((H, W), rle bytes)`` per image, which the JIT type system cannot express; ``update`` / ``compute`` are
+    # ``torch.jit.unused`` in script, so only the attribute types must be inferable
     detection_box: List[Tensor]
-    detection_mask: List[Tuple[Tuple[Tuple[int, int], bytes], ...]]
+    detection_mask: List[Tensor]
     detection_scores: List[Tensor]
     detection_labels: List[Tensor]
     groundtruth_box: List[Tensor]
-    groundtruth_mask: List[Tuple[Tuple[Tuple[int, int], bytes], ...]]
+    groundtruth_mask: List[Tensor]
     groundtruth_labels: List[Tensor]
     groundtruth_crowds: List[Tensor]
     groundtruth_area: List[Tensor]
 
     warn_on_many_detections: bool = True
+
+    # host-side evaluation caches (segm IoU blocks, class-sharded flat states): not module state, invisible to script
+    __jit_ignored_attributes__: ClassVar[List[str]] = ["device", "_segm_cache", "_shard_flat"]
 
     def __init__(
         self,

@@ -62,6 +62,15 @@ def _eed_compute(sentence_level_scores: List[Tensor]) -> Tensor:
     return sum(sentence_level_scores) / tensor(len(sentence_level_scores))
 
 
+# device scratch of ``tmx::eed_gpu``: two fp64 DP rows and one int32 row of (max_hyp + 1) entries per pair; beyond
+# this bound (as EditDistance's 1 GiB cap) the host op runs instead of risking a device OOM
+GPU_EED_MAX_SCRATCH = 1 << 30
+
+
+def _eed_gpu_scratch_bytes(max_hyp: int, pairs: int) -> int:
+    return (max_hyp + 1) * pairs * (2 * 8 + 4)
+
+
 def _eed_update(
     preds: Union[str, Sequence[str]],
     target: Sequence[Union[str, Sequence[str]]],
@@ -90,9 +99,13 @@ def _eed_update(
     h, h_off = _pack_codepoints(hyps)
     r, r_off = _pack_codepoints(refs)
     n = len(list(zip(preds, target)))
-    if device is not None and device.type == "cuda" and h.numel() >= GPU_EED_MIN_CHARS and ops.use_native(torch.empty(0, device=device)):
+    max_hyp = max((len(x) for x in hyps), default=0)
+    if (
+        device is not None and device.type == "cuda" and h.numel() >= GPU_EED_MIN_CHARS
+        and _eed_gpu_scratch_bytes(max_hyp, len(hyps)) <= GPU_EED_MAX_SCRATCH
+        and ops.use_native(torch.empty(0, device=device))
+    ):
         d = [x.to(device, non_blocking=True) for x in (h, h_off, r, r_off)]
-        max_hyp = max((len(x) for x in hyps), default=0)
         scores = torch.ops.tmx.eed_gpu(*d, ord(" "), float(alpha), float(rho), float(deletion), float(insertion), max_hyp)
         best = torch.full((n,), float("inf"), dtype=torch.float64, device=device).scatter_reduce(
             0, torch.tensor(owner, dtype=torch.long).to(device, non_blocking=True), scores, reduce="amin"

@@ -201,21 +201,17 @@ class Metric(Module, ABC):
         self._join_side_work()
         return {name: getattr(self, name) for name in self._defaults}
 
-    # ---- side-stream work ------------------------------------------------------------------------------------
-    # An update may leave kernels that write this metric's states running on a side HIP stream (the curve metrics'
-    # class pass overlaps the next batch's row pass).  ``_side_event`` marks the last of them; every consumer of
-    # the states (compute, sync, reset, state_dict, pickling, device moves, forward) makes the current stream wait
-    # for it first.
+    # ---- deferred state work ---------------------------------------------------------------------------------
+    # An update may leave a pending fix-up of this metric's states (CatMetric drops NaN entries once, at the first
+    # consumer, instead of synchronising the host per update).  ``_side_event`` holds it; every consumer of the states
+    # (compute, sync, reset, state_dict, pickling, device moves, forward) runs it first.
     _side_event: Optional[Any] = None
 
     def _join_side_work(self) -> None:
         ev = self.__dict__.get("_side_event")
         if ev is not None:
             self.__dict__["_side_event"] = None
-            if callable(ev):  # native join (the current stream waits for the side-stream passes)
-                ev()
-            else:
-                torch.cuda.current_stream().wait_event(ev)
+            ev()
 
     @property
     def device(self) -> "torch.device":
@@ -259,7 +255,11 @@ class Metric(Module, ABC):
             raise TorchMetricsUserError(
                 "The Metric shouldn't be synced when performing ``forward``. HINT: Did you forget to call ``unsync`` ?."
             )
-        self._join_side_work()  # pending state work (side-stream passes, deferred NaN drops) before states are cached
+        self._join_side_work()  # pending state work (deferred NaN drops) before states are cached
+        if self.dist_sync_on_step and self._step_sync_ok() and self.distributed_available_fn():
+            # batch-state collectives launched first, the global update runs beside them (``_step_sync_begin``)
+            self._forward_cache = self._step_sync_end(self._step_sync_begin(args, kwargs))
+            return self._forward_cache
         full = self.full_state_update or self.full_state_update is None or self.dist_sync_on_step
         if self._deferred is None:
             self._forward_cache = (self._forward_full_state_update if full else self._forward_reduce_state_update)(*args, **kwargs)
@@ -284,6 +284,7 @@ class Metric(Module, ABC):
 
     def _leave_batch_mode(self, saved_compute_on_cpu: bool) -> None:
         self._is_synced = False
+        self._cache = None  # the batch compute's pre-sync states (a batch sync is never unsynced): do not pin them
         self._should_unsync = True
         self._to_sync = self.sync_on_compute
         self._computed = None
@@ -321,11 +322,12 @@ class Metric(Module, ABC):
         self._leave_batch_mode(saved)
         return batch_val
 
-    # ---- overlapped dist_sync_on_step (MetricCollection.forward) ---------------------------------------------------
-    # The reference syncs and computes each member's batch value in turn (``metric.py:273-305``): member j's
-    # collectives only start after member i's batch value is computed.  Split in two, the collection launches every
-    # member's batch-state collectives first (``sync(async_op=True)``: coalesced buckets enqueued on RCCL's stream) and
-    # then computes the batch values in order, so member i computes while the later members' collectives are in flight.
+    # ---- overlapped dist_sync_on_step (Metric.forward and MetricCollection.forward) ------------------------------
+    # The reference syncs and computes each batch value in turn (``metric.py:273-305``): global update, batch update,
+    # then a blocking gather inside compute.  Here the batch update runs first and its collectives are launched at once
+    # (``sync(async_op=True)``: coalesced buckets enqueued on RCCL's stream); the global-state update then runs while
+    # they are in flight (it touches other tensors), and only the batch compute waits for them.  A collection launches
+    # every member's collectives before computing any batch value, so member i computes while member j's sync runs.
     def _step_sync_ok(self) -> bool:
         from torchmetrics_forked_amd.utilities.distributed import gather_all_tensors
 
@@ -335,38 +337,61 @@ class Metric(Module, ABC):
         )
 
     def _step_sync_begin(self, args: Tuple, kwargs: Dict[str, Any]) -> Tuple[Any, ...]:
-        """First half of the (full-state) ``forward`` with ``dist_sync_on_step``: global update, fresh batch state,
-        batch update, batch-state collectives launched."""
+        """First half of ``forward`` with ``dist_sync_on_step``: fresh batch state, batch update, batch-state
+        collectives launched, then the global update beside them.  On an exception the global state is restored
+        (and launched collectives completed, since every rank issued them) before it propagates."""
         self._join_side_work()
         snap_def = None
         if self._deferred is not None:
             snap_def = self._deferred.snapshot()
             self._deferred.clear()
-        self.update(*args, **kwargs)
         count = self._update_count
+        glob = self.metric_state
         saved = self._enter_batch_mode()
-        snapshot = self.metric_state
-        self.reset()
-        self.update(*args, **kwargs)
-        handle = self.sync(dist_sync_fn=self.dist_sync_fn, async_op=True)
-        return snap_def, count, saved, snapshot, handle
+        handle = None
+        try:
+            self.reset()
+            self.update(*args, **kwargs)
+            handle = self.sync(dist_sync_fn=self.dist_sync_fn, async_op=True)
+            batch = self.metric_state
+            for name, val in glob.items():
+                setattr(self, name, val)
+            self._update_count = count
+            self._enable_grad, self.compute_on_cpu = False, saved  # the global update as a plain update() call
+            try:
+                self.update(*args, **kwargs)
+            finally:
+                self._enable_grad, self.compute_on_cpu = True, False
+            glob, count = self.metric_state, self._update_count
+            for name, val in batch.items():
+                setattr(self, name, val)
+            self._update_count = 1
+        except BaseException:
+            if handle is not None:
+                handle.wait()
+            self._step_sync_restore(snap_def, count, saved, glob)
+            raise
+        return snap_def, count, saved, glob, handle
+
+    def _step_sync_restore(self, snap_def: Any, count: int, saved: bool, glob: Dict[str, Any]) -> None:
+        for name, val in glob.items():
+            setattr(self, name, val)
+        self._update_count = count
+        self._cache = None
+        self._leave_batch_mode(saved)
+        if snap_def is not None:
+            self._deferred.restore(snap_def)
 
     def _step_sync_end(self, ctx: Tuple[Any, ...]) -> Any:
-        """Second half: wait for this member's collectives, compute the synced batch value, restore the global state."""
-        snap_def, count, saved, snapshot, handle = ctx
+        """Second half: wait for this metric's collectives, compute the synced batch value, restore the global state."""
+        snap_def, count, saved, glob, handle = ctx
         try:
             if handle is not None:
                 handle.wait()
             self._to_sync = False  # already synced (or not distributed)
             batch_val = self.compute()
         finally:
-            for name, val in snapshot.items():
-                setattr(self, name, val)
-            self._update_count = count
-            self._cache = None
-            self._leave_batch_mode(saved)
-            if snap_def is not None:
-                self._deferred.restore(snap_def)
+            self._step_sync_restore(snap_def, count, saved, glob)
         self._forward_cache = batch_val
         return batch_val
 
@@ -675,7 +700,7 @@ class Metric(Module, ABC):
 
     def __getstate__(self) -> Dict[str, Any]:
         self._join_side_work()
-        return {k: v for k, v in self.__dict__.items() if k not in ("update", "compute", "_update_signature", "_side_bufs", "_dual_bufs", "_hist_spare")}
+        return {k: v for k, v in self.__dict__.items() if k not in ("update", "compute", "_update_signature", "_hist_spare")}
 
     def __setstate__(self, state: Dict[str, Any]) -> None:
         self.__dict__.update(state)

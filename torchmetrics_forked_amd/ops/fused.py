@@ -120,12 +120,6 @@ class _MulticlassScoresPlan:
             m._update_count += 1
         if curve is not None:
             curve._curve_update(preds, target, confmat_out=delta, err_flag=err)
-            side = curve.__dict__.get("_side_event")
-            if side is not None:  # the side-stream class pass also adds rare rows into the confusion matrix
-                if not direct:
-                    curve._join_side_work()
-                else:
-                    confmats[0].__dict__["_side_event"] = side
         else:
             from torchmetrics_forked_amd.ops import classification as cls_ops
 

@@ -237,6 +237,12 @@ class SampleShardedMixin:
         if should_unsync:
             self._sample_shard = None
 
+    def _leave_batch_mode(self, saved_compute_on_cpu: bool) -> None:
+        # forward's batch compute (dist_sync_on_step) syncs without unsync: forget the group with the synced flag, so a
+        # later compute that skips the sync takes the local path instead of issuing collectives
+        super()._leave_batch_mode(saved_compute_on_cpu)  # type: ignore[misc]
+        self._sample_shard = None
+
     def _local_samples(self, *names: str, empty_dtype: torch.dtype = torch.float32) -> List[Tensor]:
         """This rank's concatenated sample states (empty rank: a length-0 tensor of ``empty_dtype``)."""
         from torchmetrics_forked_amd.utilities.data import dim_zero_cat
