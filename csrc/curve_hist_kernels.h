@@ -378,29 +378,49 @@ __device__ __forceinline__ uint4 stream_load16(const uint4* p) {
 #endif
 }
 
-template <typename T, int NG, bool SOFTMAX, bool FIXUP, bool PADDED>
-__device__ __forceinline__ void row_tile(const T* __restrict__ preds, const int64_t* __restrict__ target, int64_t n, int C, int ld,
-                                          int64_t ignore_index, bool has_ignore, uint32_t* __restrict__ codes, int64_t n_pad,
-                                          int64_t* __restrict__ confmat, int* __restrict__ err, bool rec, bool& saw_bad,
-                                          SlowRows slow, uint32_t* __restrict__ s_tile, int64_t tile) {
+// One tile's loads, issued as one batch (the persistent row pass issues the NEXT tile's batch before computing the
+// current one): a wave's two row pairs as 16-B vectors per lane and the int64 targets of its four rows (lanes 0-3).
+template <int NG>
+struct RowLoads {
+  uint4 raw[2][2][2];
+  int64_t tv;
+};
+
+template <typename T, int NG>
+__device__ __forceinline__ void row_tile_load(const T* __restrict__ preds, const int64_t* __restrict__ target, int64_t n, int ld,
+                                              int64_t tile, RowLoads<NG>& L) {
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = threadIdx.x / kWave;
   const int nvec = ld / 8;
-  const int nlo = min(max(C - 8 * lane, 0), 8), nhi = min(max(C - 8 * (lane + kWave), 0), 8);
   const bool lo_ok = lane < nvec, hi_ok = lane + kWave < nvec;
   const int lq = lo_ok ? lane : nvec - 1;  // clamped: every load stays inside its row
   const int hq = hi_ok ? lane + kWave : nvec - 1;
-  uint4 raw[2][2][2];
   auto row0_of = [&](int pp) -> int64_t { return tile * kTileRows + 2 * (wave + pp * kRowWaves); };
-  const int64_t tv = target[min(row0_of((lane & 3) >> 1) + (lane & 1), n - 1)];
+  L.tv = target[min(row0_of((lane & 3) >> 1) + (lane & 1), n - 1)];
 #pragma unroll
   for (int pp = 0; pp < 2; ++pp)
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const uint4* row = reinterpret_cast<const uint4*>(preds + min(row0_of(pp) + h, n - 1) * ld);
-      raw[pp][h][0] = stream_load16(row + lq);
-      if constexpr (NG == 2) raw[pp][h][1] = stream_load16(row + hq);
+      L.raw[pp][h][0] = stream_load16(row + lq);
+      if constexpr (NG == 2) L.raw[pp][h][1] = stream_load16(row + hq);
     }
+}
+
+// Compute half of a tile: codes into the LDS image, confusion matrix / error / rare-row side effects.  The caller
+// stores the image (after a barrier).
+template <typename T, int NG, bool SOFTMAX, bool FIXUP, bool PADDED>
+__device__ __forceinline__ void row_tile_compute(const RowLoads<NG>& L, int64_t n, int C, int ld, int64_t ignore_index, bool has_ignore,
+                                                 int64_t* __restrict__ confmat, int* __restrict__ err, bool rec, bool& saw_bad,
+                                                 SlowRows slow, uint32_t* __restrict__ s_tile, int64_t tile) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wave = threadIdx.x / kWave;
+  const int nvec = ld / 8;
+  const int nlo = min(max(C - 8 * lane, 0), 8), nhi = min(max(C - 8 * (lane + kWave), 0), 8);
+  const bool lo_ok = lane < nvec, hi_ok = lane + kWave < nvec;
+  auto row0_of = [&](int pp) -> int64_t { return tile * kTileRows + 2 * (wave + pp * kRowWaves); };
+  const int64_t tv = L.tv;
+  const auto& raw = L.raw;
   auto target_of = [&](int i) -> int64_t {
     const uint64_t u = static_cast<uint64_t>(tv);
     const uint32_t lo = __builtin_amdgcn_readlane(static_cast<uint32_t>(u), i);
@@ -493,6 +513,16 @@ __device__ __forceinline__ void row_tile(const T* __restrict__ preds, const int6
       if (slowv[i]) slow.rows[list * n + atomicAdd(slow.count + list, 1)] = static_cast<int>(row0_of(i >> 1) + (i & 1));
     }
   }
+}
+
+template <typename T, int NG, bool SOFTMAX, bool FIXUP, bool PADDED>
+__device__ __forceinline__ void row_tile(const T* __restrict__ preds, const int64_t* __restrict__ target, int64_t n, int C, int ld,
+                                          int64_t ignore_index, bool has_ignore, uint32_t* __restrict__ codes, int64_t n_pad,
+                                          int64_t* __restrict__ confmat, int* __restrict__ err, bool rec, bool& saw_bad,
+                                          SlowRows slow, uint32_t* __restrict__ s_tile, int64_t tile) {
+  RowLoads<NG> L;
+  row_tile_load<T, NG>(preds, target, n, ld, tile, L);
+  row_tile_compute<T, NG, SOFTMAX, FIXUP, PADDED>(L, n, C, ld, ignore_index, has_ignore, confmat, err, rec, saw_bad, slow, s_tile, tile);
   __syncthreads();
   store_tile<NG>(s_tile, codes, C, n_pad, tile);
 }
@@ -561,6 +591,57 @@ __global__ void __launch_bounds__(kRowThreads, 4) mc_codes_kernel(const T* __res
                                                                     int* __restrict__ slow_count) {
   mc_codes_block<T, FIXUP, NG, PADDED>(blockIdx.x, gridDim.x, preds, target, n, C, ld, mode, ignore_index, has_ignore, codes, n_pad,
                                        confmat, err, record_mode, slow_rows, slow_count);
+}
+
+// Persistent, software-pipelined row pass (speculated mode; the FIXUP launch stays the one-tile-per-block kernel):
+// a grid of ~2 blocks per CU, each looping over its tiles.  Once a tile's codes sit in the LDS image, the NEXT tile's
+// loads (64 KiB per block at C = 1000) are issued before the image is stored, so HBM reads stay in flight through the
+// store phase (the compute registers are dead by then: no extra VGPRs; prefetching before the compute instead needs
+// ~150 VGPRs and spills at 4 waves per SIMD).  Tile order stays XCD-aware: block b runs on XCD b % 8 and walks that
+// XCD's contiguous tile run with stride grid / 8.  Same codes, confusion matrix, rare-row lists and mode verdict as
+// mc_codes_kernel.
+template <typename T, int NG, bool SOFTMAX, bool PADDED>
+__device__ __forceinline__ void persist_row_loop(const T* __restrict__ preds, const int64_t* __restrict__ target, int64_t n, int C, int ld,
+                                                 int64_t ignore_index, bool has_ignore, uint32_t* __restrict__ codes, int64_t n_pad,
+                                                 int64_t* __restrict__ confmat, int* __restrict__ err, bool record_mode, SlowRows slow,
+                                                 uint32_t* __restrict__ s_tile, bool& saw_bad) {
+  const int64_t ntiles = (n + kTileRows - 1) / kTileRows;
+  const int64_t per_xcd = (ntiles + 7) / 8;
+  const int64_t base = (blockIdx.x % 8) * per_xcd, stride = gridDim.x / 8;
+  const int64_t kend = min(per_xcd, ntiles - base);  // this XCD's tiles: [base, base + kend)
+  int64_t k = blockIdx.x / 8;
+  RowLoads<NG> L;
+  if (k < kend) row_tile_load<T, NG>(preds, target, n, ld, base + k, L);
+  for (; k < kend; k += stride) {
+    row_tile_compute<T, NG, SOFTMAX, false, PADDED>(L, n, C, ld, ignore_index, has_ignore, confmat, err, record_mode, saw_bad, slow, s_tile,
+                                                    base + k);
+    __syncthreads();
+    if (k + stride < kend) row_tile_load<T, NG>(preds, target, n, ld, base + k + stride, L);  // in flight during the store phase
+    store_tile<NG>(s_tile, codes, C, n_pad, base + k);
+    __syncthreads();  // the image is rewritten by the next tile
+  }
+}
+
+template <typename T, int NG, bool PADDED>
+__global__ void __launch_bounds__(kRowThreads, 4) mc_codes_persist_kernel(const T* __restrict__ preds, const int64_t* __restrict__ target,
+                                                                           int64_t n, int C, int ld, int* __restrict__ mode,
+                                                                           int64_t ignore_index, bool has_ignore,
+                                                                           uint32_t* __restrict__ codes, int64_t n_pad,
+                                                                           int64_t* __restrict__ confmat, int* __restrict__ err,
+                                                                           bool record_mode, int* __restrict__ slow_rows,
+                                                                           int* __restrict__ slow_count) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_tile[];  // [512 * NG][kSlots]
+  const SlowRows slow{slow_rows, slow_count};
+  bool saw_bad = false;
+  if (mode[0] != 0)
+    persist_row_loop<T, NG, true, PADDED>(preds, target, n, C, ld, ignore_index, has_ignore, codes, n_pad, confmat, err, record_mode, slow,
+                                          s_tile, saw_bad);
+  else
+    persist_row_loop<T, NG, false, PADDED>(preds, target, n, C, ld, ignore_index, has_ignore, codes, n_pad, confmat, err, record_mode, slow,
+                                           s_tile, saw_bad);
+  if (record_mode && __syncthreads_or(saw_bad) && threadIdx.x == 0 &&
+      __hip_atomic_load(mode + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
+    __hip_atomic_store(mode + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Multilabel row pass: the same tile / LDS image / class-major scratch as the multiclass row pass, but every element

@@ -1,0 +1,209 @@
+// Host (CPU) twins of the multiclass pair-stream kernels for small CPU batches (BASELINE config 1: MulticlassAccuracy,
+// 5 classes, batch 10, gloo).  The reference's CPU update is ~10 ATen calls per batch (unique for validation, argmax,
+// bincount of t * C + p, reshape, diag, three sums, four in-place adds) plus a module __setattr__ per state.  Here ONE
+// dispatcher call does the eager value check, the arg-max and the in-place accumulation:
+//
+//   mc_stats_host   : tp / fp / tn / fn (per class, or micro totals) += counts of the (target, arg-max) pairs
+//   mc_confmat_host : confmat[t, p] += 1
+//
+// Semantics = the eager PyTorch paths in ops/classification.py (rows whose target is the ignore index or outside
+// [0, C), or whose label pred is outside [0, C), are dropped) and the reference's validation rule
+// (reference functional/classification/stat_scores.py:307-314): more distinct target values than C (+1 with an
+// ignore index), or more distinct integer preds than C, is an error.  The op validates FIRST and accumulates only when
+// the batch passes; it returns {passed, distinct targets, distinct preds} and the caller raises the reference's error
+// text.  torch.argmax semantics: the first maximum, a NaN counts as the maximum (first NaN wins).
+#include <ATen/ATen.h>
+#include <ATen/Dispatch.h>
+#include <torch/library.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <vector>
+
+namespace tmx {
+namespace {
+
+// distinct values of an int64 stream: bitmap over [0, C] (C = an ignore-index slot may sit outside), sorted vector for
+// the rest (rare: out-of-range values)
+struct DistinctCounter {
+  std::vector<uint8_t> seen;
+  std::vector<int64_t> other;
+  int64_t count = 0;
+  explicit DistinctCounter(int64_t C) : seen(static_cast<size_t>(C), 0) {}
+  void add(int64_t v) {
+    if (v >= 0 && v < static_cast<int64_t>(seen.size())) {
+      if (!seen[v]) {
+        seen[v] = 1;
+        ++count;
+      }
+    } else {
+      other.push_back(v);
+    }
+  }
+  int64_t total() {
+    std::sort(other.begin(), other.end());
+    return count + static_cast<int64_t>(std::unique(other.begin(), other.end()) - other.begin());
+  }
+};
+
+template <typename T>
+inline float to_float(T v) {
+  return static_cast<float>(v);
+}
+
+// labels of the batch: arg-max of float rows [M, C] or the integer preds [M]; int64 out
+void labels_of(const at::Tensor& preds, int64_t C, std::vector<int64_t>& out) {
+  if (preds.is_floating_point()) {
+    TORCH_CHECK(preds.dim() == 2 && preds.size(1) == C, "mc host op: float preds must be [M, C]");
+    const at::Tensor p = preds.contiguous();
+    const int64_t M = p.size(0);
+    out.resize(static_cast<size_t>(M));
+    AT_DISPATCH_FLOATING_TYPES_AND2(at::kHalf, at::kBFloat16, p.scalar_type(), "mc_labels_host", [&] {
+      const scalar_t* x = p.data_ptr<scalar_t>();
+      for (int64_t r = 0; r < M; ++r) {
+        const scalar_t* row = x + r * C;
+        int64_t best = 0;
+        float bv = to_float(row[0]);
+        if (!std::isnan(bv)) {
+          for (int64_t c = 1; c < C; ++c) {
+            const float v = to_float(row[c]);
+            if (std::isnan(v)) {
+              best = c;
+              break;
+            }
+            if (v > bv) {
+              bv = v;
+              best = c;
+            }
+          }
+        }
+        out[static_cast<size_t>(r)] = best;
+      }
+    });
+  } else {
+    const at::Tensor p = preds.reshape(-1).to(at::kLong).contiguous();
+    const int64_t* x = p.data_ptr<int64_t>();
+    out.assign(x, x + p.numel());
+  }
+}
+
+void targets_of(const at::Tensor& target, std::vector<int64_t>& out) {
+  const at::Tensor t = target.reshape(-1).to(at::kLong).contiguous();
+  const int64_t* x = t.data_ptr<int64_t>();
+  out.assign(x, x + t.numel());
+}
+
+// {passed, distinct targets, distinct integer preds (0 for float preds)}
+std::vector<int64_t> validate(const std::vector<int64_t>& t, const std::vector<int64_t>& p, bool float_preds, int64_t C,
+                              bool has_ignore) {
+  DistinctCounter dt(C + 1);
+  for (int64_t v : t) dt.add(v);
+  const int64_t nt = dt.total();
+  int64_t np = 0;
+  if (!float_preds) {
+    DistinctCounter dp(C);
+    for (int64_t v : p) dp.add(v);
+    np = dp.total();
+  }
+  const bool ok = nt <= (has_ignore ? C + 1 : C) && (float_preds || np <= C);
+  return {ok ? 1 : 0, nt, np};
+}
+
+void check_state(const at::Tensor& s, const char* what) {
+  TORCH_CHECK(s.device().is_cpu() && s.scalar_type() == at::kLong && s.is_contiguous(), what, " must be a contiguous CPU int64 tensor");
+}
+
+}  // namespace
+
+std::vector<int64_t> mc_stats_host(const at::Tensor& preds, const at::Tensor& target, int64_t C, at::Tensor& tp, at::Tensor& fp,
+                                   at::Tensor& tn, at::Tensor& fn, int64_t ignore_index, bool has_ignore, bool micro,
+                                   bool validate_values) {
+  TORCH_CHECK(C >= 1, "mc_stats_host: num_classes must be positive");
+  for (const at::Tensor* s : {&tp, &fp, &tn, &fn}) check_state(*s, "mc_stats_host: state");
+  TORCH_CHECK(tp.numel() == (micro ? 1 : C) && fp.numel() == tp.numel() && tn.numel() == tp.numel() && fn.numel() == tp.numel(),
+              "mc_stats_host: states must hold ", micro ? 1 : C, " counters");
+  std::vector<int64_t> p, t;
+  labels_of(preds, C, p);
+  targets_of(target, t);
+  TORCH_CHECK(p.size() == t.size(), "mc_stats_host: preds rows and targets differ in count");
+  std::vector<int64_t> res{1, 0, 0};
+  if (validate_values) {
+    res = validate(t, p, preds.is_floating_point(), C, has_ignore);
+    if (!res[0]) return res;
+  }
+  int64_t* TP = tp.data_ptr<int64_t>();
+  int64_t* FP = fp.data_ptr<int64_t>();
+  int64_t* TN = tn.data_ptr<int64_t>();
+  int64_t* FN = fn.data_ptr<int64_t>();
+  if (micro) {
+    int64_t n = 0, hit = 0;
+    for (size_t i = 0; i < t.size(); ++i) {
+      const int64_t tv = t[i], pv = p[i];
+      if ((has_ignore && tv == ignore_index) || tv < 0 || tv >= C || pv < 0 || pv >= C) continue;
+      ++n;
+      hit += tv == pv;
+    }
+    TP[0] += hit;
+    FP[0] += n - hit;
+    FN[0] += n - hit;
+    TN[0] += C * n - (hit + 2 * (n - hit));
+    return res;
+  }
+  // per class: tp_c, fp_c (predicted c, wrong), fn_c (true c, missed); tn_c = n - tp_c - fp_c - fn_c
+  int64_t n = 0;
+  std::vector<int64_t> dtp(static_cast<size_t>(C), 0), dfp(static_cast<size_t>(C), 0), dfn(static_cast<size_t>(C), 0);
+  for (size_t i = 0; i < t.size(); ++i) {
+    const int64_t tv = t[i], pv = p[i];
+    if ((has_ignore && tv == ignore_index) || tv < 0 || tv >= C || pv < 0 || pv >= C) continue;
+    ++n;
+    if (tv == pv) {
+      ++dtp[tv];
+    } else {
+      ++dfp[pv];
+      ++dfn[tv];
+    }
+  }
+  for (int64_t c = 0; c < C; ++c) {
+    TP[c] += dtp[c];
+    FP[c] += dfp[c];
+    FN[c] += dfn[c];
+    TN[c] += n - dtp[c] - dfp[c] - dfn[c];
+  }
+  return res;
+}
+
+std::vector<int64_t> mc_confmat_host(const at::Tensor& preds, const at::Tensor& target, at::Tensor& confmat, int64_t ignore_index,
+                                     bool has_ignore, bool validate_values) {
+  check_state(confmat, "mc_confmat_host: confmat");
+  TORCH_CHECK(confmat.dim() == 2 && confmat.size(0) == confmat.size(1), "mc_confmat_host: confmat must be [C, C]");
+  const int64_t C = confmat.size(0);
+  std::vector<int64_t> p, t;
+  labels_of(preds, C, p);
+  targets_of(target, t);
+  TORCH_CHECK(p.size() == t.size(), "mc_confmat_host: preds rows and targets differ in count");
+  std::vector<int64_t> res{1, 0, 0};
+  if (validate_values) {
+    res = validate(t, p, preds.is_floating_point(), C, has_ignore);
+    if (!res[0]) return res;
+  }
+  int64_t* cm = confmat.data_ptr<int64_t>();
+  for (size_t i = 0; i < t.size(); ++i) {
+    const int64_t tv = t[i], pv = p[i];
+    if ((has_ignore && tv == ignore_index) || tv < 0 || tv >= C || pv < 0 || pv >= C) continue;
+    ++cm[tv * C + pv];
+  }
+  return res;
+}
+
+}  // namespace tmx
+
+TORCH_LIBRARY_FRAGMENT(tmx, m) {
+  m.def("mc_stats_host(Tensor preds, Tensor target, int num_classes, Tensor(a!) tp, Tensor(b!) fp, Tensor(c!) tn, Tensor(d!) fn, int ignore_index, bool has_ignore, bool micro, bool validate) -> int[]");
+  m.def("mc_confmat_host(Tensor preds, Tensor target, Tensor(a!) confmat, int ignore_index, bool has_ignore, bool validate) -> int[]");
+}
+
+TORCH_LIBRARY_IMPL(tmx, CPU, m) {
+  m.impl("mc_stats_host", &tmx::mc_stats_host);
+  m.impl("mc_confmat_host", &tmx::mc_confmat_host);
+}

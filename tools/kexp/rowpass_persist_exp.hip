@@ -1,0 +1,139 @@
+// Persistent, software-pipelined row pass (mc_codes_persist_kernel) vs the one-tile-per-block row pass
+// (mc_codes_kernel) at the headline shape: bit-identical class-major codes / confusion matrix / mode verdict, then
+// timings over 4 rotating 65536 x 1000 bf16 logits batches (bench.py's pool) for several persistent grid sizes,
+// alone and in the full update sequence (row pass, FIXUP no-op, class pass).
+// Build: hipcc -O3 --offload-arch=gfx950 -I csrc tools/kexp/rowpass_persist_exp.hip -o build/rowpass_persist_exp
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "curve_hist_kernels.h"
+
+using namespace tmx;
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP error %s at %s:%d\n", hipGetErrorString(e), __FILE__, __LINE__); exit(1); } } while (0)
+
+__global__ void init_logits(__hip_bfloat16* x, int64_t total, uint32_t seed, int probs) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    uint32_t h = (uint32_t)i * 2654435761u ^ seed;
+    h ^= h >> 15; h *= 2246822519u; h ^= h >> 13; h *= 3266489917u; h ^= h >> 16;
+    uint32_t g = (uint32_t)(i >> 32) * 2654435761u ^ h;
+    g ^= g >> 16; g *= 0x7feb352du; g ^= g >> 15;
+    // sum of 4 uniforms ~ approx normal
+    float u = ((h & 0xFFFF) + (h >> 16) + (g & 0xFFFF) + (g >> 16)) / 65536.f - 2.f;
+    float v = probs ? (float)(h & 0xFFFFFF) / 16777216.f : 1.7f * u;
+    x[i] = __float2bfloat16(v);
+  }
+}
+__global__ void init_target(int64_t* t, int64_t n, int C, uint32_t seed) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    uint32_t h = (uint32_t)i * 2654435761u ^ seed;
+    h ^= h >> 15; h *= 2246822519u; h ^= h >> 13;
+    t[i] = h % C;
+  }
+}
+
+template <typename F>
+float time_us(F f, int iters = 20) {
+  for (int i = 0; i < 3; ++i) f(i);
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
+  CK(hipEventRecord(a));
+  for (int i = 0; i < iters; ++i) f(i);
+  CK(hipEventRecord(b));
+  CK(hipEventSynchronize(b));
+  float ms; CK(hipEventElapsedTime(&ms, a, b));
+  return ms * 1000.f / iters;
+}
+
+int main(int argc, char** argv) {
+  const int64_t N = argc > 1 ? atoll(argv[1]) : 65536;
+  const int C = argc > 2 ? atoi(argv[2]) : 1000;
+  if (C % 8 != 0 || C > 1024 || C <= 512) { printf("{\"error\": \"512 < C <= 1024, C %% 8 == 0\"}\n"); return 1; }
+  hipDeviceProp_t prop;
+  CK(hipGetDeviceProperties(&prop, 0));
+  const int cus = prop.multiProcessorCount;
+  const int64_t n_pad = (N + kTileRows - 1) / kTileRows * kTileRows;
+  const int64_t ntiles = n_pad / kTileRows;
+  const size_t xbytes = (size_t)N * C * 2, cbytes = (size_t)C * n_pad * 2, hbytes = (size_t)C * 2 * kCodes * 8;
+  const int NB = 4;
+  std::vector<__hip_bfloat16*> xs(NB);
+  for (int k = 0; k < NB; ++k) {
+    CK(hipMalloc(&xs[k], xbytes));
+    hipLaunchKernelGGL(init_logits, 4096, 256, 0, 0, xs[k], N * C, 1234u + k, 0);
+  }
+  __hip_bfloat16* xp;
+  CK(hipMalloc(&xp, xbytes));
+  hipLaunchKernelGGL(init_logits, 4096, 256, 0, 0, xp, N * C, 99u, 1);
+  int64_t *t, *cmA, *cmB, *hist;
+  uint32_t *codesA, *codesB;
+  int *modeA, *modeB, *err, *rows, *stateA, *stateB;
+  CK(hipMalloc(&t, N * 8));
+  hipLaunchKernelGGL(init_target, 256, 256, 0, 0, t, N, C, 7u);
+  CK(hipMalloc(&cmA, (size_t)C * C * 8)); CK(hipMalloc(&cmB, (size_t)C * C * 8));
+  CK(hipMalloc(&codesA, cbytes)); CK(hipMalloc(&codesB, cbytes)); CK(hipMalloc(&hist, hbytes));
+  CK(hipMalloc(&modeA, 8)); CK(hipMalloc(&modeB, 8)); CK(hipMalloc(&err, 4)); CK(hipMalloc(&rows, 2 * N * 4));
+  CK(hipMalloc(&stateA, 24)); CK(hipMalloc(&stateB, 24));
+  const int grid1 = (int)((ntiles + 7) / 8 * 8);
+  const size_t shm = (size_t)1024 * kSlots * 4;
+  auto set_mode = [&](int* m, int m0) { int hm[2] = {m0, 0}; CK(hipMemcpy(m, hm, 8, hipMemcpyHostToDevice)); };
+  auto rowA = [&](const __hip_bfloat16* x, bool rec) {
+    hipLaunchKernelGGL((mc_codes_kernel<__hip_bfloat16, false, 2, false>), grid1, kRowThreads, shm, 0, x, t, N, C, C, modeA, -1, false,
+                       codesA, n_pad, cmA, err, rec, rows, stateA);
+  };
+  auto rowB = [&](const __hip_bfloat16* x, bool rec, int grid) {
+    hipLaunchKernelGGL((mc_codes_persist_kernel<__hip_bfloat16, 2, false>), grid, kRowThreads, shm, 0, x, t, N, C, C, modeB, -1, false,
+                       codesB, n_pad, cmB, err, rec, rows, stateB);
+  };
+  auto fix = [&](const __hip_bfloat16* x, int* mode, uint32_t* codes, int64_t* cm, int* state) {
+    hipLaunchKernelGGL((mc_codes_kernel<__hip_bfloat16, true, 2, false>), std::min(grid1, 128), kRowThreads, shm, 0, x, t, N, C, C, mode, -1,
+                       false, codes, n_pad, cm, err, false, rows, state);
+  };
+  auto cls = [&](const __hip_bfloat16* x, int* mode, uint32_t* codes, int* state) {
+    hipLaunchKernelGGL((class_hist_kernel<__hip_bfloat16, false>), C, kClassThreads, kCodes * 4, 0, (const uint16_t*)codes, n_pad, 1, hist,
+                       x, C, t, N, mode, true, rows, state, (int64_t*)nullptr, (int*)nullptr, mode);
+  };
+  std::vector<uint16_t> ha(cbytes / 2), hb(cbytes / 2);
+  std::vector<int64_t> ma(C * C), mb(C * C);
+  printf("{\"N\": %lld, \"C\": %d, \"cus\": %d", (long long)N, C, cus);
+  const int grids[] = {2 * cus, 3 * cus, 4 * cus, grid1};
+  for (int pm = 0; pm < 2; ++pm) {
+    const __hip_bfloat16* x = pm ? xp : xs[0];
+    for (int g : grids) {
+      CK(hipMemset(codesA, 0xAB, cbytes)); CK(hipMemset(codesB, 0xCD, cbytes));
+      CK(hipMemset(cmA, 0, (size_t)C * C * 8)); CK(hipMemset(cmB, 0, (size_t)C * C * 8));
+      CK(hipMemset(stateA, 0, 24)); CK(hipMemset(stateB, 0, 24));
+      set_mode(modeA, pm ? 0 : 1); set_mode(modeB, pm ? 0 : 1);
+      rowA(x, true); rowB(x, true, g);
+      CK(hipDeviceSynchronize());
+      CK(hipMemcpy(ha.data(), codesA, cbytes, hipMemcpyDeviceToHost)); CK(hipMemcpy(hb.data(), codesB, cbytes, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(ma.data(), cmA, (size_t)C * C * 8, hipMemcpyDeviceToHost)); CK(hipMemcpy(mb.data(), cmB, (size_t)C * C * 8, hipMemcpyDeviceToHost));
+      int m1[2], m2[2]; CK(hipMemcpy(m1, modeA, 8, hipMemcpyDeviceToHost)); CK(hipMemcpy(m2, modeB, 8, hipMemcpyDeviceToHost));
+      int64_t cd = 0, md = 0;
+      for (int64_t c = 0; c < C; ++c)
+        for (int64_t r = 0; r < N; ++r) cd += ha[c * n_pad + r] != hb[c * n_pad + r];
+      for (int i = 0; i < C * C; ++i) md += ma[i] != mb[i];
+      printf(", \"check_%s_grid%d\": {\"code_diffs\": %lld, \"confmat_diffs\": %lld, \"verdict\": [%d, %d]}", pm ? "probs" : "logits", g,
+             (long long)cd, (long long)md, m1[1], m2[1]);
+    }
+  }
+  set_mode(modeA, 1); set_mode(modeB, 1);
+  CK(hipMemset(stateA, 0, 24)); CK(hipMemset(stateB, 0, 24));
+  const float tA = time_us([&](int i) { rowA(xs[i % NB], true); });
+  printf(", \"rowpass_tile_per_block_us\": %.2f", tA);
+  for (int g : grids) {
+    const float tB = time_us([&](int i) { rowB(xs[i % NB], true, g); });
+    printf(", \"rowpass_persist_grid%d_us\": %.2f", g, tB);
+  }
+  const float sA = time_us([&](int i) { rowA(xs[i % NB], true); fix(xs[i % NB], modeA, codesA, cmA, stateA); cls(xs[i % NB], modeA, codesA, stateA); });
+  printf(", \"update_seq_tile_per_block_us\": %.2f", sA);
+  for (int g : grids) {
+    const float sB = time_us([&](int i) { rowB(xs[i % NB], true, g); fix(xs[i % NB], modeB, codesB, cmB, stateB); cls(xs[i % NB], modeB, codesB, stateB); });
+    printf(", \"update_seq_persist_grid%d_us\": %.2f", g, sB);
+  }
+  const float cl = time_us([&](int i) { cls(xs[i % NB], modeA, codesA, stateA); });
+  printf(", \"class_pass_us\": %.2f}\n", cl);
+  CK(hipDeviceSynchronize());
+  return 0;
+}

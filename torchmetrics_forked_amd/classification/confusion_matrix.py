@@ -141,6 +141,11 @@ class MulticlassConfusionMatrix(_ConfmatPlot, Metric):
             p, t = _multiclass_pairs_view(preds, target, self.num_classes)
             cls_ops.mc_confmat_update(p, t, self.confmat, self.ignore_index, err_t, err_p)
             return
+        if self.confmat.dtype == torch.long and cls_ops.host_native(preds, target, self.confmat):
+            self._validate(preds, target, check_values=False)
+            p, t = _multiclass_pairs_view(preds, target, self.num_classes)
+            cls_ops.mc_confmat_host(p, t, self.confmat, self.ignore_index, self.validate_args)
+            return
         self._validate(preds, target)
         self.confmat += _multiclass_confusion_matrix_update(preds, target, self.num_classes, self.ignore_index)
 

@@ -54,6 +54,10 @@ def samples_scores(preds: Tensor, labels: Tensor, valid: Optional[Tensor] = None
     if preds.ndim == 1:
         preds, labels = preds.unsqueeze(1), labels.unsqueeze(1)
         valid = valid.unsqueeze(1) if valid is not None else None
+    if preds.device.type == "cpu" and preds.is_floating_point() and ops.load():
+        # host op: per-column radix sort + one tie-group scan (csrc/host_curve.cpp), columns in parallel
+        out = torch.ops.tmx.curve_scores_host(preds.detach(), labels, valid)
+        return out[:, 0], out[:, 1], out[:, 2], out[:, 3]
     n, C = preds.shape
     p = preds.float() if preds.dtype in HIST_DTYPES else preds
     lab = labels.to(torch.float64)

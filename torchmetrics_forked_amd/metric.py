@@ -65,6 +65,8 @@ from torchmetrics_forked_amd.utilities.plot import _AX_TYPE, _PLOT_OUT_TYPE, plo
 from torchmetrics_forked_amd.utilities.prints import rank_zero_warn
 from torchmetrics_forked_amd.utilities.validation import DeferredChecks, host_checks, make_sink
 
+_PLAIN_ATTR_TYPES = frozenset({Tensor, int, float, bool, str, type(None), tuple, list, dict, StateArena})
+
 _STR_REDUCTIONS = {
     "sum": dim_zero_sum,
     "mean": dim_zero_mean,
@@ -711,6 +713,13 @@ class Metric(Module, ABC):
     def __setattr__(self, name: str, value: Any) -> None:
         if name in _CONST_ATTRS:
             raise RuntimeError(f"Can't change const `{name}`.")
+        # Fast path for rebinding an existing plain attribute (states, counters, flags) to a plain value: nn.Module's
+        # __setattr__ would only reach object.__setattr__ after its Parameter / Module / buffer checks (~8 us per call,
+        # dozens of calls per forward).  Parameters, modules and buffers live in their own dicts, never in __dict__, and
+        # the exact-type test keeps Parameter (a Tensor subclass) and every Module on the full path.
+        if type(value) in _PLAIN_ATTR_TYPES and name in self.__dict__:
+            object.__setattr__(self, name, value)
+            return
         super().__setattr__(name, value)
 
     # dtype casts are no-ops unless routed through set_dtype (reference metric.py:729-760)

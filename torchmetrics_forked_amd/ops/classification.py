@@ -22,6 +22,48 @@ def range_flag(x: Tensor) -> Tensor:
     return (~((x >= 0) & (x <= 1))).any().reshape(1).int()
 
 
+def host_native(*ts: Optional[Tensor]) -> bool:
+    """True when the host (CPU) twins of the pair-stream kernels apply: every tensor on the CPU and the native library
+    loaded (``csrc/host_classification.cpp``; ``TMX_DISABLE_NATIVE=1`` forces the eager path)."""
+    return all(t is None or t.device.type == "cpu" for t in ts) and ops.load()
+
+
+def raise_unique_counts(res: List[int], num_classes: int, has_ignore: bool) -> None:
+    """The reference's eager value check (``functional/classification/stat_scores.py:307-314``) from the distinct
+    counts a host op returned (it accumulated nothing when the batch failed)."""
+    if res[0]:
+        return
+    limit = num_classes + 1 if has_ignore else num_classes
+    if res[1] > limit:
+        raise RuntimeError(
+            "Detected more unique values in `target` than `num_classes`. Expected only"
+            f" {limit} but found {res[1]} in `target`."
+        )
+    raise RuntimeError(
+        "Detected more unique values in `preds` than `num_classes`. Expected only"
+        f" {num_classes} but found {res[2]} in `preds`."
+    )
+
+
+def mc_stats_host(
+    preds: Tensor, target: Tensor, num_classes: int, states: Tuple[Tensor, Tensor, Tensor, Tensor], ignore_index: Optional[int],
+    micro: bool, validate: bool,
+) -> None:
+    """CPU: value check + arg-max + in-place tp / fp / tn / fn accumulation in ONE native call (``mc_stats_host``)."""
+    res = torch.ops.tmx.mc_stats_host(
+        preds.detach(), target, num_classes, *states, -1 if ignore_index is None else ignore_index, ignore_index is not None, micro, validate
+    )
+    raise_unique_counts(res, num_classes, ignore_index is not None)
+
+
+def mc_confmat_host(preds: Tensor, target: Tensor, confmat: Tensor, ignore_index: Optional[int], validate: bool) -> None:
+    """CPU: value check + arg-max + ``confmat[t, p] += 1`` in ONE native call (``mc_confmat_host``)."""
+    res = torch.ops.tmx.mc_confmat_host(
+        preds.detach(), target, confmat, -1 if ignore_index is None else ignore_index, ignore_index is not None, validate
+    )
+    raise_unique_counts(res, confmat.shape[0], ignore_index is not None)
+
+
 def mc_confmat_update(
     preds: Tensor,
     target: Tensor,

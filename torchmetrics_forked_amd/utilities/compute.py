@@ -23,7 +23,7 @@ def _safe_divide(num: Tensor, denom: Tensor) -> Tensor:
 
     NOTE: like the reference (``utilities/compute.py:46-55``) ``denom`` is modified in place.
     """
-    denom[denom == 0.0] = 1
+    denom.masked_fill_(denom == 0.0, 1)  # in place, as the reference's boolean-index assignment (one kernel)
     num = num if num.is_floating_point() else num.float()
     denom = denom if denom.is_floating_point() else denom.float()
     return num / denom
@@ -40,7 +40,7 @@ def _adjust_weights_safe_divide(
     else:
         weights = torch.ones_like(score)
         if not multilabel:
-            weights[tp + fp + fn == 0] = 0.0
+            weights.masked_fill_(tp + fp + fn == 0, 0.0)
     return _safe_divide(weights * score, weights.sum(-1, keepdim=True)).sum(-1)
 
 
