@@ -1461,14 +1461,14 @@ void launch_row_pass(const T* p, const int64_t* target, int64_t n, int C, int ld
 template <typename T>
 void launch_class_pass(const uint32_t* cptr, int64_t n, int C, int ld, const T* p, const int64_t* target, const int* bmode,
                        bool speculative, const int* srows, int* state, int64_t* hist, int64_t* cm, int* code_range,
-                       int* roll_mode = nullptr) {
+                       int* roll_mode = nullptr, int64_t* batch_hist = nullptr, int* batch_range = nullptr) {
   const int64_t n_pad = (n + kTileRows - 1) / kTileRows * kTileRows;
   // row splits only when there are too few classes to fill the chip (exclusive-owner flush when splits == 1)
   int splits = 1;
   while ((int64_t)C * splits < 512 && n_pad / (8 * (splits * 2)) >= 1024) splits *= 2;
   hipLaunchKernelGGL((class_hist_kernel<T, false>), C * splits, kClassThreads, kCodes * sizeof(uint32_t), stream(),
                      reinterpret_cast<const uint16_t*>(cptr), n_pad, splits, hist, p, ld, target, n, bmode, speculative,
-                     srows, state, cm, code_range, roll_mode);
+                     srows, state, cm, code_range, roll_mode, batch_hist, batch_range);
   TMX_LAUNCH_CHECK();
 }
 
@@ -1507,7 +1507,7 @@ at::Tensor codes_scratch(const at::TensorOptions& opts, int64_t elems) {
 template <typename T, bool PADDED>
 void launch_two_pass(const T* p, const int64_t* target, int64_t n, int C, int ld, int* mode, int* state, bool speculative,
                      int64_t ignore_index, bool has_ignore, int64_t* hist, int64_t* cm, int* err, const at::TensorOptions& opts,
-                     int* code_range) {
+                     int* code_range, int64_t* batch_hist = nullptr, int* batch_range = nullptr) {
   const int64_t n_pad = (n + kTileRows - 1) / kTileRows * kTileRows;
   auto codes = codes_scratch(opts, (int64_t)C * n_pad);
   auto slow_rows = at::empty({2 * n}, opts.dtype(at::kInt));
@@ -1515,7 +1515,8 @@ void launch_two_pass(const T* p, const int64_t* target, int64_t n, int C, int ld
   int* srows = slow_rows.data_ptr<int>();
   // single stream: the class pass reads the (used, real) pair straight from ``mode`` and its last workgroup rolls it
   launch_row_pass<T, PADDED>(p, target, n, C, ld, mode, state, speculative, ignore_index, has_ignore, cm, err, cptr, srows, true);
-  launch_class_pass<T>(cptr, n, C, ld, p, target, mode, speculative, srows, state, hist, cm, code_range, speculative ? mode : nullptr);
+  launch_class_pass<T>(cptr, n, C, ld, p, target, mode, speculative, srows, state, hist, cm, code_range, speculative ? mode : nullptr,
+                       batch_hist, batch_range);
 }
 
 // The row pass alone into caller-owned scratch (class-major codes + rare-row list): the per-element code pin of
@@ -1637,12 +1638,52 @@ __global__ void __launch_bounds__(kBinThreads) binary_hist_kernel(const T* __res
 
 // hist: int64 [C, 2, kCodes] updated in place.
 // task 0 = multiclass (preds [N, C], target [N]); task 1 = binary/multilabel (preds/target [N, L, ...]).
+void curve_hist_merge_launch(int64_t* dst, int* dst_range, const int64_t* src, const int* src_range, int C);
+
+// ``batch_hist`` / ``batch_range`` (optional, forward()): the batch's own histogram and code range, zero / empty before
+// the call, are produced beside the accumulated ones.  The two-pass routes flush both from the class pass; every other
+// route counts into the batch histogram and one merge launch adds its occupied range into ``hist``.
+void curve_hist_update_impl(const at::Tensor& preds_, const at::Tensor& target_, at::Tensor& hist, int64_t task, int64_t ignore_index,
+                            bool has_ignore, c10::optional<at::Tensor> confmat, c10::optional<at::Tensor> norm_flag,
+                            c10::optional<at::Tensor> err_flag, c10::optional<at::Tensor> mode_state, c10::optional<at::Tensor> code_range,
+                            int64_t* batch_hist, int* batch_range, bool& dual);
+
 void curve_hist_update(const at::Tensor& preds_, const at::Tensor& target_, at::Tensor& hist, int64_t task,
                        int64_t ignore_index, bool has_ignore, c10::optional<at::Tensor> confmat,
                        c10::optional<at::Tensor> norm_flag, c10::optional<at::Tensor> err_flag,
-                       c10::optional<at::Tensor> mode_state, c10::optional<at::Tensor> code_range) {
+                       c10::optional<at::Tensor> mode_state, c10::optional<at::Tensor> code_range,
+                       c10::optional<at::Tensor> batch_hist, c10::optional<at::Tensor> batch_range) {
   TORCH_CHECK(hist.is_contiguous() && hist.scalar_type() == at::kLong && hist.dim() == 3 && hist.size(1) == 2 &&
               hist.size(2) == kCodes, "hist must be int64 [C, 2, 16384]");
+  if (!batch_hist.has_value()) {
+    bool dual = false;
+    curve_hist_update_impl(preds_, target_, hist, task, ignore_index, has_ignore, confmat, norm_flag, err_flag, mode_state, code_range,
+                           nullptr, nullptr, dual);
+    return;
+  }
+  TORCH_CHECK(batch_range.has_value(), "curve_hist_update: batch_hist needs batch_range");
+  TORCH_CHECK(batch_hist->is_contiguous() && batch_hist->sizes() == hist.sizes() && batch_hist->scalar_type() == at::kLong &&
+              batch_hist->device() == hist.device(), "batch_hist must be int64 like hist");
+  TORCH_CHECK(batch_range->scalar_type() == at::kInt && batch_range->numel() == 2 * hist.size(0) && batch_range->is_contiguous() &&
+              batch_range->device() == hist.device(), "batch_range must be int32[C, 2] on the histogram's device");
+  // dual-flush routes write both histograms; the others are run on the batch histogram (+ its range) and merged
+  bool dual = true;
+  curve_hist_update_impl(preds_, target_, hist, task, ignore_index, has_ignore, confmat, norm_flag, err_flag, mode_state, code_range,
+                         batch_hist->data_ptr<int64_t>(), batch_range->data_ptr<int>(), dual);
+  if (!dual) {
+    curve_hist_update_impl(preds_, target_, *batch_hist, task, ignore_index, has_ignore, confmat, norm_flag, err_flag, mode_state,
+                           batch_range, nullptr, nullptr, dual);
+    curve_hist_merge_launch(hist.data_ptr<int64_t>(), code_range.has_value() ? code_range->data_ptr<int>() : nullptr,
+                            batch_hist->data_ptr<int64_t>(), batch_range->data_ptr<int>(), static_cast<int>(hist.size(0)));
+  }
+}
+
+// ``dual`` in: the caller asks for the batch histogram (batch_hist / batch_range non-null); out: false when this route
+// cannot write it and nothing was done (the caller reruns on the batch histogram and merges).
+void curve_hist_update_impl(const at::Tensor& preds_, const at::Tensor& target_, at::Tensor& hist, int64_t task, int64_t ignore_index,
+                            bool has_ignore, c10::optional<at::Tensor> confmat, c10::optional<at::Tensor> norm_flag,
+                            c10::optional<at::Tensor> err_flag, c10::optional<at::Tensor> mode_state, c10::optional<at::Tensor> code_range,
+                            int64_t* batch_hist, int* batch_range, bool& dual) {
   // code_range (int32[C, 2], optional): the occupied code range [lo, hi] of each class of ``hist``.  The two-pass routes widen it
   // in the class pass; every other route (rare shapes) marks it as the full range, so it is always conservative.
   int* crange = nullptr;
@@ -1669,6 +1710,18 @@ void curve_hist_update(const at::Tensor& preds_, const at::Tensor& target_, at::
   // two-pass multiclass route for C <= 1024; rows are padded to a multiple of 8 classes when C % 8 != 0 (one copy)
   const bool two_pass_ok = task == 0 && C <= 8 * 2 * kWave &&
                            (C % 8 != 0 || (reinterpret_cast<uintptr_t>(preds.data_ptr()) & 15) == 0);
+  if (batch_hist != nullptr) {
+    static const bool small_off_b = std::getenv("TMX_CURVE_SMALL_OFF") != nullptr;
+    const bool small_route = task == 0 && !small_off_b && C <= kSmallVpt * 16 && (reinterpret_cast<uintptr_t>(preds.data_ptr()) & 15) == 0;
+    const bool ml_route = task == 1 && C != 1 && C % 8 == 0 && C <= 8 * 2 * kWave && target.dim() >= 1 && target.numel() == target.size(0) * C &&
+                          (reinterpret_cast<uintptr_t>(preds.data_ptr()) & 15) == 0 && (reinterpret_cast<uintptr_t>(target.data_ptr()) & 15) == 0;
+    const bool dual_route = (task == 0 && two_pass_ok && !small_route) || ml_route;
+    if (!dual_route) {
+      dual = false;
+      range_tracked = true;  // nothing counted: the range stays as it is
+      return;
+    }
+  }
   // speculative normalisation mode (persistent int32[8] per metric: mode[2], rare-row counts[2], ticket) replaces the
   // range pre-pass; the class pass leaves the counts at zero for the next batch
   const bool speculative = two_pass_ok && mode_state.has_value() && !norm_flag.has_value();
@@ -1712,11 +1765,11 @@ void curve_hist_update(const at::Tensor& preds_, const at::Tensor& target_, at::
           const at::Tensor padded = at::constant_pad_nd(preds.view({n, C}), {0, ld - C}, 0).contiguous();
           launch_two_pass<scalar_t, true>(reinterpret_cast<const scalar_t*>(padded.data_ptr()), target.data_ptr<int64_t>(), n, C,
                                           ld, flag.data_ptr<int>(), state.data_ptr<int>(), speculative, ignore_index, has_ignore,
-                                          hist.data_ptr<int64_t>(), cm, err, preds.options(), crange);
+                                          hist.data_ptr<int64_t>(), cm, err, preds.options(), crange, batch_hist, batch_range);
         } else {
           launch_two_pass<scalar_t, false>(p, target.data_ptr<int64_t>(), n, C, C, flag.data_ptr<int>(), state.data_ptr<int>(),
                                            speculative, ignore_index, has_ignore, hist.data_ptr<int64_t>(), cm, err, preds.options(),
-                                           crange);
+                                           crange, batch_hist, batch_range);
         }
         range_tracked = true;
         return;
@@ -1774,7 +1827,8 @@ void curve_hist_update(const at::Tensor& preds_, const at::Tensor& target_, at::
         hipLaunchKernelGGL((class_hist_kernel<scalar_t, true>), C * splits, kClassThreads, kCodes * sizeof(uint32_t), stream(),
                            reinterpret_cast<const uint16_t*>(cptr), n_pad, splits, hist.data_ptr<int64_t>(), p, C,
                            target.data_ptr<int64_t>(), N, flag.data_ptr<int>(), false, static_cast<const int*>(nullptr),
-                           state.data_ptr<int>(), static_cast<int64_t*>(nullptr), crange, static_cast<int*>(nullptr));
+                           state.data_ptr<int>(), static_cast<int64_t*>(nullptr), crange, static_cast<int*>(nullptr), batch_hist,
+                           batch_range);
         range_tracked = true;
         return;
       }
@@ -1783,6 +1837,63 @@ void curve_hist_update(const at::Tensor& preds_, const at::Tensor& target_, at::
                          hist.data_ptr<int64_t>(), err);
     }
   });
+  TMX_LAUNCH_CHECK();
+}
+
+// forward()'s batch histogram: ``dst[c, :, lo..hi] += src[c, :, lo..hi]`` over the source's occupied range per class
+// (and the destination range widened), or -- curve_hist_zero -- ``src`` zeroed over that range and the range emptied,
+// so the scratch is ready for the next batch.  One 256-thread workgroup per (class, 4096-code slice): grid.y slices.
+constexpr int kMergeThreads = 256;
+constexpr int kMergeSlice = 4096;
+__global__ void __launch_bounds__(kMergeThreads) curve_hist_merge_kernel(int64_t* __restrict__ dst, int* __restrict__ dst_range,
+                                                                         int64_t* __restrict__ src, int* __restrict__ src_range, bool zero) {
+  const int c = blockIdx.x;
+  const int lo = max(src_range[2 * c], 0), hi = min(src_range[2 * c + 1], kCodes - 1);
+  const int s0 = lo + blockIdx.y * kMergeSlice, s1 = min(hi + 1, s0 + kMergeSlice);
+  for (int h = 0; h < 2; ++h) {
+    int64_t* sp = src + ((int64_t)c * 2 + h) * kCodes;
+    int64_t* dp = dst != nullptr ? dst + ((int64_t)c * 2 + h) * kCodes : nullptr;
+    for (int i = s0 + threadIdx.x; i < s1; i += kMergeThreads) {
+      const int64_t v = sp[i];
+      if (v == 0) continue;
+      if (zero) sp[i] = 0;
+      else dp[i] += v;
+    }
+  }
+  if (blockIdx.y == 0 && threadIdx.x == 0 && hi >= lo) {
+    if (!zero && dst_range != nullptr) {
+      atomicMin(dst_range + 2 * c, lo);
+      atomicMax(dst_range + 2 * c + 1, hi);
+    }
+  }
+}
+
+__global__ void curve_range_reset_kernel(int* __restrict__ range, int C) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c < C) {
+    range[2 * c] = kCodes;
+    range[2 * c + 1] = -1;
+  }
+}
+
+void curve_hist_merge_launch(int64_t* dst, int* dst_range, const int64_t* src, const int* src_range, int C) {
+  if (C == 0) return;
+  hipLaunchKernelGGL(curve_hist_merge_kernel, dim3(C, kCodes / kMergeSlice), kMergeThreads, 0, stream(), dst, dst_range,
+                     const_cast<int64_t*>(src), const_cast<int*>(src_range), false);
+  TMX_LAUNCH_CHECK();
+}
+
+void curve_hist_zero(at::Tensor& src, at::Tensor& src_range) {
+  TORCH_CHECK(src.is_contiguous() && src.scalar_type() == at::kLong && src.dim() == 3 && src.size(1) == 2 && src.size(2) == kCodes,
+              "curve_hist_zero: hist must be int64 [C, 2, 16384]");
+  TORCH_CHECK(src_range.scalar_type() == at::kInt && src_range.numel() == 2 * src.size(0) && src_range.is_contiguous() &&
+              src_range.device() == src.device(), "curve_hist_zero: range must be int32[C, 2] on the histogram's device");
+  const int C = static_cast<int>(src.size(0));
+  if (C == 0) return;
+  hipLaunchKernelGGL(curve_hist_merge_kernel, dim3(C, kCodes / kMergeSlice), kMergeThreads, 0, stream(), static_cast<int64_t*>(nullptr),
+                     static_cast<int*>(nullptr), src.data_ptr<int64_t>(), src_range.data_ptr<int>(), true);
+  TMX_LAUNCH_CHECK();
+  hipLaunchKernelGGL(curve_range_reset_kernel, (C + 255) / 256, 256, 0, stream(), src_range.data_ptr<int>(), C);
   TMX_LAUNCH_CHECK();
 }
 
@@ -1936,6 +2047,11 @@ __global__ void __launch_bounds__(kSumThreads) curve_summary_kernel(const double
     summary[5] = t[10] > 0 ? t[6] / t[10] : NAN;
     summary[6] = t[8] > 0 ? t[7] / t[8] : NAN;
     summary[7] = t[11] > 0 ? t[9] / t[11] : NAN;
+    // float32 copies of the 8 values in the buffer's tail (4 doubles): the metric's float32 result is a view, not a
+    // conversion launch
+    float* s32 = reinterpret_cast<float*>(summary + 8);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s32[i] = static_cast<float>(summary[i]);
   }
 }
 
@@ -1960,7 +2076,7 @@ at::Tensor curve_hist_reduce(const at::Tensor& hist_, c10::optional<at::Tensor> 
 at::Tensor curve_summary(const at::Tensor& scores_) {
   auto scores = scores_.contiguous();
   TORCH_CHECK(scores.scalar_type() == at::kDouble && scores.dim() == 2 && scores.size(1) == 4, "curve_summary: scores must be float64 [C, 4]");
-  auto summary = at::empty({8}, scores.options());
+  auto summary = at::empty({12}, scores.options());  // [0, 8) float64 values, [8, 12) the same as 8 float32
   hipLaunchKernelGGL(curve_summary_kernel, 1, kSumThreads, 0, stream(), scores.data_ptr<double>(),
                      static_cast<int>(scores.size(0)), summary.data_ptr<double>());
   TMX_LAUNCH_CHECK();
@@ -2602,7 +2718,8 @@ TORCH_LIBRARY_FRAGMENT(tmx, m) {
   m.def("mc_stat_scores_update(Tensor preds, Tensor target, int num_classes, Tensor(a!) tp, Tensor(b!) fp, Tensor(c!) tn, Tensor(d!) fn, Tensor(e!) ticket, int ignore_index, bool has_ignore, bool micro, Tensor(f!)? err_t=None, Tensor(g!)? err_p=None) -> ()");
   m.def("binary_stats_fused(Tensor preds, Tensor target, Tensor(a!) tp, Tensor(b!) fp, Tensor(c!) tn, Tensor(d!) fn, Tensor(e!) scratch, int num_labels, float threshold, int ignore_index, bool has_ignore, Tensor(f!)? err_t=None, Tensor(g!)? err_p=None) -> ()");
   m.def("binary_stats_update(Tensor preds, Tensor target, Tensor(a!) counts, int num_labels, float threshold, int ignore_index, bool has_ignore) -> ()");
-  m.def("curve_hist_update(Tensor preds, Tensor target, Tensor(a!) hist, int task, int ignore_index, bool has_ignore, Tensor(b!)? confmat, Tensor? norm_flag, Tensor(c!)? err_flag, Tensor(d!)? mode_state, Tensor(e!)? code_range=None) -> ()");
+  m.def("curve_hist_update(Tensor preds, Tensor target, Tensor(a!) hist, int task, int ignore_index, bool has_ignore, Tensor(b!)? confmat, Tensor? norm_flag, Tensor(c!)? err_flag, Tensor(d!)? mode_state, Tensor(e!)? code_range=None, Tensor(f!)? batch_hist=None, Tensor(g!)? batch_range=None) -> ()");
+  m.def("curve_hist_zero(Tensor(a!) hist, Tensor(b!) code_range) -> ()");
   m.def("curve_hist_reduce(Tensor hist, Tensor? code_range=None) -> Tensor");
   m.def("curve_summary(Tensor scores) -> Tensor");
   m.def("curve_mc_rowpass(Tensor preds, Tensor target, Tensor(a!) mode, Tensor(b!) state, Tensor(c!) codes, Tensor(d!) slow_rows, int ignore_index, bool has_ignore, Tensor(e!)? confmat, Tensor(f!)? err_flag) -> ()");
@@ -2620,6 +2737,7 @@ TORCH_LIBRARY_IMPL(tmx, CUDA, m) {
   m.impl("binary_stats_update", &tmx::binary_stats_update);
   m.impl("binary_stats_fused", &tmx::binary_stats_fused);
   m.impl("curve_hist_update", &tmx::curve_hist_update);
+  m.impl("curve_hist_zero", &tmx::curve_hist_zero);
   m.impl("curve_hist_reduce", &tmx::curve_hist_reduce);
   m.impl("curve_summary", &tmx::curve_summary);
   m.impl("curve_mc_rowpass", &tmx::curve_mc_rowpass);

@@ -593,57 +593,6 @@ __global__ void __launch_bounds__(kRowThreads, 4) mc_codes_kernel(const T* __res
                                        confmat, err, record_mode, slow_rows, slow_count);
 }
 
-// Persistent, software-pipelined row pass (speculated mode; the FIXUP launch stays the one-tile-per-block kernel):
-// a grid of ~2 blocks per CU, each looping over its tiles.  Once a tile's codes sit in the LDS image, the NEXT tile's
-// loads (64 KiB per block at C = 1000) are issued before the image is stored, so HBM reads stay in flight through the
-// store phase (the compute registers are dead by then: no extra VGPRs; prefetching before the compute instead needs
-// ~150 VGPRs and spills at 4 waves per SIMD).  Tile order stays XCD-aware: block b runs on XCD b % 8 and walks that
-// XCD's contiguous tile run with stride grid / 8.  Same codes, confusion matrix, rare-row lists and mode verdict as
-// mc_codes_kernel.
-template <typename T, int NG, bool SOFTMAX, bool PADDED>
-__device__ __forceinline__ void persist_row_loop(const T* __restrict__ preds, const int64_t* __restrict__ target, int64_t n, int C, int ld,
-                                                 int64_t ignore_index, bool has_ignore, uint32_t* __restrict__ codes, int64_t n_pad,
-                                                 int64_t* __restrict__ confmat, int* __restrict__ err, bool record_mode, SlowRows slow,
-                                                 uint32_t* __restrict__ s_tile, bool& saw_bad) {
-  const int64_t ntiles = (n + kTileRows - 1) / kTileRows;
-  const int64_t per_xcd = (ntiles + 7) / 8;
-  const int64_t base = (blockIdx.x % 8) * per_xcd, stride = gridDim.x / 8;
-  const int64_t kend = min(per_xcd, ntiles - base);  // this XCD's tiles: [base, base + kend)
-  int64_t k = blockIdx.x / 8;
-  RowLoads<NG> L;
-  if (k < kend) row_tile_load<T, NG>(preds, target, n, ld, base + k, L);
-  for (; k < kend; k += stride) {
-    row_tile_compute<T, NG, SOFTMAX, false, PADDED>(L, n, C, ld, ignore_index, has_ignore, confmat, err, record_mode, saw_bad, slow, s_tile,
-                                                    base + k);
-    __syncthreads();
-    if (k + stride < kend) row_tile_load<T, NG>(preds, target, n, ld, base + k + stride, L);  // in flight during the store phase
-    store_tile<NG>(s_tile, codes, C, n_pad, base + k);
-    __syncthreads();  // the image is rewritten by the next tile
-  }
-}
-
-template <typename T, int NG, bool PADDED>
-__global__ void __launch_bounds__(kRowThreads, 4) mc_codes_persist_kernel(const T* __restrict__ preds, const int64_t* __restrict__ target,
-                                                                           int64_t n, int C, int ld, int* __restrict__ mode,
-                                                                           int64_t ignore_index, bool has_ignore,
-                                                                           uint32_t* __restrict__ codes, int64_t n_pad,
-                                                                           int64_t* __restrict__ confmat, int* __restrict__ err,
-                                                                           bool record_mode, int* __restrict__ slow_rows,
-                                                                           int* __restrict__ slow_count) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t s_tile[];  // [512 * NG][kSlots]
-  const SlowRows slow{slow_rows, slow_count};
-  bool saw_bad = false;
-  if (mode[0] != 0)
-    persist_row_loop<T, NG, true, PADDED>(preds, target, n, C, ld, ignore_index, has_ignore, codes, n_pad, confmat, err, record_mode, slow,
-                                          s_tile, saw_bad);
-  else
-    persist_row_loop<T, NG, false, PADDED>(preds, target, n, C, ld, ignore_index, has_ignore, codes, n_pad, confmat, err, record_mode, slow,
-                                           s_tile, saw_bad);
-  if (record_mode && __syncthreads_or(saw_bad) && threadIdx.x == 0 &&
-      __hip_atomic_load(mode + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
-    __hip_atomic_store(mode + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 // Multilabel row pass: the same tile / LDS image / class-major scratch as the multiclass row pass, but every element
 // is its own binary problem — code = RNE16(sigmoid(x)) (torch's 1 / (1 + exp(-x)) in fp32) or the raw score when the
 // batch is already in [0, 1] (the range pre-pass decides, as in the reference), flags from the element's own target
@@ -754,9 +703,13 @@ constexpr int kClassUnroll = TMX_CLASS_UNROLL;
 constexpr int kTrashBin = kCodes - 1;  // no valid 16-bit score in [0, 1] maps here (bf16 <= 0x3F80, fp16 <= 0x3C00)
 constexpr int64_t kClassChunk = 65528;  // rows per LDS flush: a 16-bit half never overflows (multiple of 8)
 
+// ``bneg`` / ``bpos`` (optional): the batch histogram of a forward() call, flushed beside the accumulated one (its bins
+// are zero before the batch): a plain store when ``bstore`` (the block's only writer of those bins so far), else atomics.
 template <bool PACKED, int NT = kClassThreads>
 __device__ __forceinline__ void class_flush(uint32_t* __restrict__ s_h, int64_t* __restrict__ neg_hist,
-                                            int64_t* __restrict__ pos_hist, bool exclusive, int& lo, int& hi) {
+                                            int64_t* __restrict__ pos_hist, bool exclusive, int& lo, int& hi,
+                                            int64_t* __restrict__ bneg = nullptr, int64_t* __restrict__ bpos = nullptr,
+                                            bool bstore = false) {
   for (int i = threadIdx.x; i < kCodes; i += NT) {
     const uint32_t w = i == kTrashBin ? 0u : s_h[i];  // the trash bin holds skipped codes (non-PACKED pass)
     if (w) {
@@ -769,6 +722,15 @@ __device__ __forceinline__ void class_flush(uint32_t* __restrict__ s_h, int64_t*
       } else {
         if (neg) atomic_add_i64(neg_hist + i, neg);
         if (pos) atomic_add_i64(pos_hist + i, pos);
+      }
+      if (bneg != nullptr) {
+        if (bstore) {
+          if (neg) bneg[i] = neg;
+          if (pos) bpos[i] = pos;
+        } else {
+          if (neg) atomic_add_i64(bneg + i, neg);
+          if (pos) atomic_add_i64(bpos + i, pos);
+        }
       }
       s_h[i] = 0u;
     }
@@ -817,7 +779,8 @@ __device__ __forceinline__ void class_hist_block(int64_t vb, int64_t vgrid, cons
                                                  const int64_t* __restrict__ target, int64_t n, const int* __restrict__ bmode,
                                                  bool speculative, const int* __restrict__ slow_rows, int* __restrict__ state,
                                                  int64_t* __restrict__ confmat, int* __restrict__ code_range, int* __restrict__ roll_mode,
-                                                 uint32_t* __restrict__ partial = nullptr, int* __restrict__ prange = nullptr) {
+                                                 uint32_t* __restrict__ partial = nullptr, int* __restrict__ prange = nullptr,
+                                                 int64_t* __restrict__ batch_hist = nullptr, int* __restrict__ batch_range = nullptr) {
   extern __shared__ __attribute__((aligned(16))) uint32_t s_h[];  // [kCodes]: neg, or neg (lo 16) | pos (hi 16)
   __shared__ int s_info[4];
   int lo = kCodes, hi = -1;  // occupied code range this thread touched (compute() then scans only that range)
@@ -834,6 +797,9 @@ __device__ __forceinline__ void class_hist_block(int64_t vb, int64_t vgrid, cons
   __syncthreads();
   int64_t* neg_hist = hist + ((int64_t)c * 2) * kCodes;
   int64_t* pos_hist = hist + ((int64_t)c * 2 + 1) * kCodes;
+  int64_t* bneg = batch_hist != nullptr ? batch_hist + ((int64_t)c * 2) * kCodes : nullptr;
+  int64_t* bpos = batch_hist != nullptr ? batch_hist + ((int64_t)c * 2 + 1) * kCodes : nullptr;
+  bool bfirst = true;  // no flush of this block has written the batch bins yet
   const bool exclusive = splits == 1;
   const uint4* col = reinterpret_cast<const uint4*>(codes + (int64_t)c * n_pad);
   const int64_t nv = n_pad / 8;
@@ -875,6 +841,7 @@ __device__ __forceinline__ void class_hist_block(int64_t vb, int64_t vgrid, cons
               if ((x & 0xC000u) == 0x4000u) {
                 atomicSub(&s_h[x & 0x3FFFu], 1u);
                 atomic_add_i64(pos_hist + (x & 0x3FFFu), 1);
+                if (bpos != nullptr) atomic_add_i64(bpos + (x & 0x3FFFu), 1);
                 lo = min(lo, (int)(x & 0x3FFFu));
                 hi = max(hi, (int)(x & 0x3FFFu));
               }
@@ -885,7 +852,8 @@ __device__ __forceinline__ void class_hist_block(int64_t vb, int64_t vgrid, cons
     }
     if (ce < v1) {  // more rows than one chunk: flush before a 16-bit half can overflow
       __syncthreads();
-      class_flush<PACKED, NT>(s_h, neg_hist, pos_hist, exclusive, lo, hi);
+      class_flush<PACKED, NT>(s_h, neg_hist, pos_hist, exclusive, lo, hi, bneg, bpos, exclusive && bfirst);
+      bfirst = false;
       __syncthreads();
     }
   }
@@ -905,6 +873,7 @@ __device__ __forceinline__ void class_hist_block(int64_t vb, int64_t vgrid, cons
       hi = max(hi, (int)code);
       if (target[r] == c) atomic_add_i64(pos_hist + code, 1);
       else atomic_add_i64(neg_hist + code, 1);
+      if (bneg != nullptr) atomic_add_i64((target[r] == c ? bpos : bneg) + code, 1);
     }
   }
   if (confmat != nullptr && threadIdx.x < kWave) {
@@ -931,17 +900,23 @@ __device__ __forceinline__ void class_hist_block(int64_t vb, int64_t vgrid, cons
   __syncthreads();
   // rare-row codes went to the int64 bins by atomics: then the last flush must be atomic too
   if (partial != nullptr) class_store_partial<NT>(s_h, partial + vb * kCodes, prange + 2 * vb, lo, hi);
-  else class_flush<PACKED, NT>(s_h, neg_hist, pos_hist, exclusive && n0 + n1 == 0, lo, hi);
+  else class_flush<PACKED, NT>(s_h, neg_hist, pos_hist, exclusive && n0 + n1 == 0, lo, hi, bneg, bpos, exclusive && bfirst && n0 + n1 == 0);
   // partial mode: class_partial_reduce_kernel derives the class ranges from prange and resets / rolls the state
   // (no per-block global atomics on the same few words — with few classes hundreds of blocks share each class);
   // only rare-row codes (tracked in lo / hi here, not in the partial histogram) still go through atomics
   if (partial != nullptr && n0 + n1 == 0) return;
-  if (code_range != nullptr) {  // per-class running range [C][2]: one min / max per wave, no block barrier
+  if (code_range != nullptr || batch_range != nullptr) {  // per-class running range [C][2]: one min / max per wave
     lo = wave_min_i32(lo);
     hi = wave_max_i32(hi);
     if ((threadIdx.x & (kWave - 1)) == 0 && hi >= 0) {
-      atomicMin(code_range + 2 * c, lo);
-      atomicMax(code_range + 2 * c + 1, hi);
+      if (code_range != nullptr) {
+        atomicMin(code_range + 2 * c, lo);
+        atomicMax(code_range + 2 * c + 1, hi);
+      }
+      if (batch_range != nullptr) {
+        atomicMin(batch_range + 2 * c, lo);
+        atomicMax(batch_range + 2 * c + 1, hi);
+      }
     }
   }
   if (partial != nullptr) return;
@@ -968,9 +943,10 @@ __global__ void __launch_bounds__(kClassThreads) class_hist_kernel(const uint16_
                                                                    const int* __restrict__ bmode, bool speculative,
                                                                    const int* __restrict__ slow_rows, int* __restrict__ state,
                                                                    int64_t* __restrict__ confmat, int* __restrict__ code_range,
-                                                                   int* __restrict__ roll_mode) {
+                                                                   int* __restrict__ roll_mode, int64_t* __restrict__ batch_hist = nullptr,
+                                                                   int* __restrict__ batch_range = nullptr) {
   class_hist_block<T, PACKED, kClassThreads>(blockIdx.x, gridDim.x, codes, n_pad, splits, hist, preds, ld, target, n, bmode, speculative,
-                                             slow_rows, state, confmat, code_range, roll_mode);
+                                             slow_rows, state, confmat, code_range, roll_mode, nullptr, nullptr, batch_hist, batch_range);
 }
 
 // Small-class class pass: packed LDS histogram per (class, split), partial flush (class_store_partial).

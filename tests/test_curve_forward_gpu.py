@@ -1,0 +1,93 @@
+"""``forward`` of exact-histogram curve metrics on the GPU (batch-sink route): the class pass flushes the batch's counts
+into a per-metric scratch histogram beside the accumulated one, the batch value is reduced from the scratch and the
+scratch is zeroed again -- no parked state, no reset, no dense ``glob + local``.
+
+Checked against the update + compute path on every route: multiclass two-pass (C = 1000 / 520, the headline shape
+family, with ignore_index, NaN rows and probability batches), the small-class route (C = 10: batch counts merged by
+one launch), multilabel (aligned class pass) and binary (its own kernel + merge), single metrics and a fused
+MetricCollection: every forward value equals a fresh metric's update + compute on that batch, and the accumulated
+histogram, code range, confusion matrix and final compute equal a metric that only saw update() calls."""
+import pytest
+import torch
+
+import torchmetrics_forked_amd as tm
+
+pytestmark = pytest.mark.gpu
+
+
+def _batches(kind, C, n, k, seed=3):
+    g = torch.Generator().manual_seed(seed)
+    out = []
+    for i in range(k):
+        if kind == "binary":
+            x = torch.randn(n, generator=g)
+            t = torch.randint(0, 2, (n,), generator=g)
+        elif kind == "multilabel":
+            x = torch.randn(n, C, generator=g)
+            t = torch.randint(0, 2, (n, C), generator=g)
+        else:
+            x = torch.randn(n, C, generator=g) * 2
+            if i == 2:
+                x = x.softmax(1)  # a probability batch between logits batches (mode flip)
+            t = torch.randint(0, C, (n,), generator=g)
+            if i == 3:
+                x[5, 7] = float("nan")  # a rare NaN row
+                t[::11] = -1  # ignored rows
+        out.append((x.bfloat16().cuda(), t.cuda()))
+    return out
+
+
+def _make(kind, C, **kw):
+    if kind == "binary":
+        return tm.classification.BinaryAUROC(**kw)
+    if kind == "multilabel":
+        return tm.classification.MultilabelAUROC(num_labels=C, average=None, **kw)
+    return tm.classification.MulticlassAUROC(num_classes=C, average=None, ignore_index=-1, **kw)
+
+
+@pytest.mark.parametrize("kind,C,n", [("multiclass", 1000, 4096 + 37), ("multiclass", 520, 3000), ("multiclass", 10, 5000),
+                                      ("multilabel", 64, 2048), ("multilabel", 24, 999), ("binary", 1, 70000)])
+def test_curve_forward_matches_update_compute(kind, C, n):
+    batches = _batches(kind, C, n, 6)
+    fwd = _make(kind, C).cuda()
+    upd = _make(kind, C).cuda()
+    for i, (x, t) in enumerate(batches):
+        val = fwd(x, t)
+        # the first forward on a fresh metric takes the reference's park / reset route, later ones the batch sink
+        assert ("_batch_bufs" in fwd.__dict__) == (i > 0)
+        single = _make(kind, C).cuda()
+        single.update(x, t)
+        torch.testing.assert_close(val, single.compute(), rtol=0, atol=0, equal_nan=True, msg=f"batch {i}")
+        upd.update(x, t)
+    assert torch.equal(fwd.score_hist, upd.score_hist)
+    if kind == "multiclass" and C >= 512:
+        assert torch.equal(fwd._tracked_range(), upd._tracked_range())
+    torch.testing.assert_close(fwd.compute(), upd.compute(), rtol=0, atol=0, equal_nan=True)
+    sc = fwd.__dict__["_batch_bufs"]
+    assert int(sc[0].abs().sum()) == 0  # the scratch is zero again between forwards
+    assert bool((sc[1][:, 0] == 16384).all()) and bool((sc[1][:, 1] == -1).all())
+
+
+def test_fused_collection_forward_batch_sink():
+    C, n = 1000, 8192
+    batches = _batches("multiclass", C, n, 5)
+
+    def coll():
+        return tm.MetricCollection({
+            "auroc": tm.classification.MulticlassAUROC(num_classes=C, ignore_index=-1),
+            "ap": tm.classification.MulticlassAveragePrecision(num_classes=C, ignore_index=-1),
+            "cm": tm.classification.MulticlassConfusionMatrix(num_classes=C, ignore_index=-1),
+        }).cuda()
+
+    a, b = coll(), coll()
+    for x, t in batches:
+        out = a(x, t)
+        one = coll()
+        one.update(x, t)
+        ref = one.compute()
+        for k in out:
+            torch.testing.assert_close(out[k], ref[k], rtol=0, atol=0, msg=k)
+        b.update(x, t)
+    fa, fb = a.compute(), b.compute()
+    for k in fa:
+        torch.testing.assert_close(fa[k], fb[k], rtol=0, atol=0, msg=k)

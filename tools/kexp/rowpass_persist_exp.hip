@@ -1,4 +1,5 @@
-// Persistent, software-pipelined row pass (mc_codes_persist_kernel) vs the one-tile-per-block row pass
+// Persistent, software-pipelined row pass (mc_codes_persist_kernel, defined here: measured slower, not adopted) vs the
+// one-tile-per-block row pass
 // (mc_codes_kernel) at the headline shape: bit-identical class-major codes / confusion matrix / mode verdict, then
 // timings over 4 rotating 65536 x 1000 bf16 logits batches (bench.py's pool) for several persistent grid sizes,
 // alone and in the full update sequence (row pass, FIXUP no-op, class pass).
@@ -11,6 +12,60 @@
 #include "curve_hist_kernels.h"
 
 using namespace tmx;
+
+namespace tmx {
+// Persistent, software-pipelined row pass (speculated mode; the FIXUP launch stays the one-tile-per-block kernel):
+// a grid of ~2 blocks per CU, each looping over its tiles.  Once a tile's codes sit in the LDS image, the NEXT tile's
+// loads (64 KiB per block at C = 1000) are issued before the image is stored, so HBM reads stay in flight through the
+// store phase (the compute registers are dead by then: no extra VGPRs; prefetching before the compute instead needs
+// ~150 VGPRs and spills at 4 waves per SIMD).  Tile order stays XCD-aware: block b runs on XCD b % 8 and walks that
+// XCD's contiguous tile run with stride grid / 8.  Same codes, confusion matrix, rare-row lists and mode verdict as
+// mc_codes_kernel.
+template <typename T, int NG, bool SOFTMAX, bool PADDED>
+__device__ __forceinline__ void persist_row_loop(const T* __restrict__ preds, const int64_t* __restrict__ target, int64_t n, int C, int ld,
+                                                 int64_t ignore_index, bool has_ignore, uint32_t* __restrict__ codes, int64_t n_pad,
+                                                 int64_t* __restrict__ confmat, int* __restrict__ err, bool record_mode, SlowRows slow,
+                                                 uint32_t* __restrict__ s_tile, bool& saw_bad) {
+  const int64_t ntiles = (n + kTileRows - 1) / kTileRows;
+  const int64_t per_xcd = (ntiles + 7) / 8;
+  const int64_t base = (blockIdx.x % 8) * per_xcd, stride = gridDim.x / 8;
+  const int64_t kend = min(per_xcd, ntiles - base);  // this XCD's tiles: [base, base + kend)
+  int64_t k = blockIdx.x / 8;
+  RowLoads<NG> L;
+  if (k < kend) row_tile_load<T, NG>(preds, target, n, ld, base + k, L);
+  for (; k < kend; k += stride) {
+    row_tile_compute<T, NG, SOFTMAX, false, PADDED>(L, n, C, ld, ignore_index, has_ignore, confmat, err, record_mode, saw_bad, slow, s_tile,
+                                                    base + k);
+    __syncthreads();
+    if (k + stride < kend) row_tile_load<T, NG>(preds, target, n, ld, base + k + stride, L);  // in flight during the store phase
+    store_tile<NG>(s_tile, codes, C, n_pad, base + k);
+    __syncthreads();  // the image is rewritten by the next tile
+  }
+}
+
+template <typename T, int NG, bool PADDED>
+__global__ void __launch_bounds__(kRowThreads, 4) mc_codes_persist_kernel(const T* __restrict__ preds, const int64_t* __restrict__ target,
+                                                                           int64_t n, int C, int ld, int* __restrict__ mode,
+                                                                           int64_t ignore_index, bool has_ignore,
+                                                                           uint32_t* __restrict__ codes, int64_t n_pad,
+                                                                           int64_t* __restrict__ confmat, int* __restrict__ err,
+                                                                           bool record_mode, int* __restrict__ slow_rows,
+                                                                           int* __restrict__ slow_count) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_tile[];  // [512 * NG][kSlots]
+  const SlowRows slow{slow_rows, slow_count};
+  bool saw_bad = false;
+  if (mode[0] != 0)
+    persist_row_loop<T, NG, true, PADDED>(preds, target, n, C, ld, ignore_index, has_ignore, codes, n_pad, confmat, err, record_mode, slow,
+                                          s_tile, saw_bad);
+  else
+    persist_row_loop<T, NG, false, PADDED>(preds, target, n, C, ld, ignore_index, has_ignore, codes, n_pad, confmat, err, record_mode, slow,
+                                           s_tile, saw_bad);
+  if (record_mode && __syncthreads_or(saw_bad) && threadIdx.x == 0 &&
+      __hip_atomic_load(mode + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
+    __hip_atomic_store(mode + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+}  // namespace tmx
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP error %s at %s:%d\n", hipGetErrorString(e), __FILE__, __LINE__); exit(1); } } while (0)
 

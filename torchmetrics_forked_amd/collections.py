@@ -57,7 +57,9 @@ class MetricCollection(ModuleDict):
     # ------------------------------------------------------------------------------------------- update
     @torch.jit.unused
     def forward(self, *args: Any, **kwargs: Any) -> Dict[str, Any]:
-        return self._compute_and_reduce("forward", *args, **kwargs)
+        # every member's batch value registers its host checks with one block: one device->host read per forward
+        with host_checks():
+            return self._compute_and_reduce("forward", *args, **kwargs)
 
     def _leaders(self) -> List[str]:
         if self._groups_checked:

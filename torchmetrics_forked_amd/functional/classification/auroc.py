@@ -70,7 +70,9 @@ def _reduce_auroc(
 
     if summary is not None:
         defer_host_check(summary[2 + col], _warn)
-        return summary[4 + 2 * col + (average == "weighted")].to(res.dtype)
+        i = 4 + 2 * col + (average == "weighted")
+        v32 = cls_ops.summary_f32(summary, i) if res.dtype == torch.float32 else None
+        return v32 if v32 is not None else summary[i].to(res.dtype)
     nan = torch.isnan(res)
     defer_host_check(nan.any(), _warn)
     if average == "macro":
@@ -153,6 +155,9 @@ def auroc_compute(
     sc = _exact_scores(state, task, num, ignore_index)
     auc, _, P, N = sc
     _warn_degenerate(P, N, sc.summary)
+    if task != "binary" and average in ("macro", "weighted") and sc.summary is not None:
+        # the class average comes from the native summary: no per-class conversions
+        return _reduce_auroc(auc[:0].to(torch.float32), average, None, summary=sc.summary, col=0)
     res = auc.to(torch.float32)
     if task == "binary":
         return res[0]

@@ -42,6 +42,8 @@ def average_precision_compute(
         return _reduce_auroc(res, average, state[1][0, :, 1, :].sum(-1))
     sc = _exact_scores(state, task, num, ignore_index)
     _, ap, P, _ = sc
+    if task != "binary" and average in ("macro", "weighted") and sc.summary is not None:
+        return _reduce_auroc(ap[:0].to(torch.float32), average, None, summary=sc.summary, col=1)
     res = ap.to(torch.float32)
     if task == "binary":
         return res[0]

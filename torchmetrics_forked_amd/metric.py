@@ -268,12 +268,11 @@ class Metric(Module, ABC):
             return self._forward_cache
         # the batch value's compute checks (and clears) only the batch's deferred flags; the ones accumulated by
         # earlier update() calls are kept for the user's compute()
-        snap = self._deferred.snapshot()
-        self._deferred.clear()
+        snap = self._deferred.take()
         try:
             self._forward_cache = (self._forward_full_state_update if full else self._forward_reduce_state_update)(*args, **kwargs)
         finally:
-            self._deferred.restore(snap)
+            self._deferred.give_back(snap)
         return self._forward_cache
 
     def _enter_batch_mode(self) -> bool:
@@ -345,8 +344,7 @@ class Metric(Module, ABC):
         self._join_side_work()
         snap_def = None
         if self._deferred is not None:
-            snap_def = self._deferred.snapshot()
-            self._deferred.clear()
+            snap_def = self._deferred.take()
         count = self._update_count
         glob = self.metric_state
         saved = self._enter_batch_mode()
@@ -382,7 +380,7 @@ class Metric(Module, ABC):
         self._cache = None
         self._leave_batch_mode(saved)
         if snap_def is not None:
-            self._deferred.restore(snap_def)
+            self._deferred.give_back(snap_def)
 
     def _step_sync_end(self, ctx: Tuple[Any, ...]) -> Any:
         """Second half: wait for this metric's collectives, compute the synced batch value, restore the global state."""
@@ -407,8 +405,7 @@ class Metric(Module, ABC):
         fresh batch state; the caller then updates this metric (possibly through a fused collection kernel)."""
         snap_def = None
         if self._deferred is not None:
-            snap_def = self._deferred.snapshot()
-            self._deferred.clear()
+            snap_def = self._deferred.take()
         snapshot = self.metric_state
         count = self._update_count
         self.reset()
@@ -426,7 +423,7 @@ class Metric(Module, ABC):
             self._leave_batch_mode(saved)
         finally:
             if snap_def is not None:
-                self._deferred.restore(snap_def)
+                self._deferred.give_back(snap_def)
         self._forward_cache = batch_val
         return batch_val
 
@@ -702,7 +699,7 @@ class Metric(Module, ABC):
 
     def __getstate__(self) -> Dict[str, Any]:
         self._join_side_work()
-        return {k: v for k, v in self.__dict__.items() if k not in ("update", "compute", "_update_signature", "_hist_spare")}
+        return {k: v for k, v in self.__dict__.items() if k not in ("update", "compute", "_update_signature", "_hist_spare", "_batch_bufs", "_batch_sink", "_batch_view")}
 
     def __setstate__(self, state: Dict[str, Any]) -> None:
         self.__dict__.update(state)

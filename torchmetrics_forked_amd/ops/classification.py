@@ -208,8 +208,12 @@ def curve_hist_update(
     err_flag: Optional[Tensor] = None,
     mode_state: Optional[Tensor] = None,
     code_range: Optional[Tensor] = None,
+    batch: Optional[Tuple[Tensor, Tensor]] = None,
 ) -> None:
     """Accumulate the exact 16-bit score histogram ``hist[C, 2, 16384]`` (see csrc/classification.hip).
+
+    ``batch`` (GPU, ``forward``): a zeroed scratch histogram and its empty code range that receive this batch's own
+    counts beside ``hist`` (the class pass flushes both), so the batch value needs no parked state, reset or merge.
 
     ``code_range`` (int32[C, 2] on the GPU, optional) is widened per class to cover every code this batch touched, so
     :func:`curve_hist_reduce` and the histogram collectives can skip the never-occupied codes.
@@ -227,9 +231,12 @@ def curve_hist_update(
         norm = None if (mode_state is not None and task == "multiclass") else _norm_flag(preds, target, task, ignore_index)
         torch.ops.tmx.curve_hist_update(
             preds, target, hist, tcode, -1 if ignore_index is None else ignore_index, ignore_index is not None, confmat,
-            norm, err_flag, mode_state, code_range,
+            norm, err_flag, mode_state, code_range, batch[0] if batch is not None else None,
+            batch[1] if batch is not None else None,
         )
         return
+    if batch is not None:
+        raise RuntimeError("curve_hist_update: the batch histogram is a GPU-only route")
     C = hist.shape[0]
     if task == "multiclass":
         t = target.reshape(-1).long()
@@ -265,6 +272,11 @@ def curve_hist_update(
     hist += torch.bincount(flat.reshape(-1), minlength=hist.numel()).reshape(hist.shape)
 
 
+def curve_hist_zero(hist: Tensor, code_range: Tensor) -> None:
+    """Zero ``hist`` over each class's occupied ``code_range`` and empty the range (forward's batch scratch)."""
+    torch.ops.tmx.curve_hist_zero(hist, code_range)
+
+
 def curve_hist_reduce(hist: Tensor, code_range: Optional[Tensor] = None) -> Tensor:
     """float64 ``[C, 4]`` = (auroc, average_precision, n_pos, n_neg) per class, from ``hist[C, 2, K]``.
 
@@ -284,9 +296,17 @@ def curve_hist_reduce(hist: Tensor, code_range: Optional[Tensor] = None) -> Tens
     return torch.stack([auroc, ap, P, N], dim=1)
 
 
+def summary_f32(summary: Tensor, i: int) -> Optional[Tensor]:
+    """float32 view of value ``i`` of a native ``curve_summary`` buffer (None for the 8-value host form)."""
+    if summary.numel() < 12:
+        return None
+    return summary[8:12].view(torch.float32)[i]
+
+
 def curve_summary(scores: Tensor) -> Tensor:
     """float64[8] from ``curve_hist_reduce``'s ``[C, 4]``: (any N<=0, any P<=0, any AUROC NaN, any AP NaN, macro AUROC,
-    weighted AUROC, macro AP, weighted AP) with NaN classes ignored and weights = P (one native launch on the GPU)."""
+    weighted AUROC, macro AP, weighted AP) with NaN classes ignored and weights = P (one native launch on the GPU).
+    The native buffer is float64[12]: its tail holds the same 8 values as float32 (``summary_f32``)."""
     if ops.use_native(scores):
         return torch.ops.tmx.curve_summary(scores.contiguous())
     a, ap, P, N = scores.double().unbind(1)

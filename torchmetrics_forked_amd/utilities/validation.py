@@ -37,20 +37,24 @@ class HostCheckBatch:
     A ``MetricCollection.compute`` opens the outer block, so a whole collection pays one read."""
 
     def __init__(self) -> None:
-        self._items: List[Tuple[Tensor, Callable[[List[int]], None], bool]] = []
+        # (flag tensors, callback over their concatenated values, is-error, consume: zero the flags once read)
+        self._items: List[Tuple[List[Tensor], Callable[[List[int]], None], bool, bool]] = []
         self._on_error: List[Callable[[], None]] = []
         self._on_abandon: List[Callable[[], None]] = []
 
     def add(self, flags: Tensor, callback: Callable[[List[int]], None], error: bool = False) -> None:
-        self._items.append((flags.reshape(-1).to(torch.int32), callback, error))
+        self._items.append(([flags], callback, error, False))
+
+    def add_many(self, flags: List[Tensor], callback: Callable[[List[int]], None], error: bool = False, consume: bool = False) -> None:
+        """Several flags read together; ``consume`` zeroes them in the same read (DeferredChecks.check)."""
+        self._items.append((list(flags), callback, error, consume))
 
     def on_error(self, fn: Callable[[], None]) -> None:
         """Run ``fn`` if an error callback raises (e.g. drop a cached compute value)."""
         self._on_error.append(fn)
 
     def on_abandon(self, fn: Callable[[], None]) -> None:
-        """Run ``fn`` if the block ends by an exception before resolving (e.g. put consumed device flags back, so the
-        next compute still raises for the invalid inputs)."""
+        """Run ``fn`` if the block ends by an exception before resolving."""
         self._on_abandon.append(fn)
 
     def abandon(self) -> None:
@@ -59,32 +63,49 @@ class HostCheckBatch:
         for fn in fns:
             fn()
 
+    @staticmethod
+    def _read(items: List[Tuple[List[Tensor], Callable[[List[int]], None], bool, bool]]) -> List[int]:
+        """Every flag's elements as ints, in order, in ONE device read; consumed flags are zeroed by that read."""
+        flat = [(t, consume) for ts, _, _, consume in items for t in ts]
+        devs = {t.device for t, _ in flat}
+        if len(devs) == 1 and next(iter(devs)).type == "cuda":
+            if _native():  # one native gather kernel + one copy into pinned memory (csrc/flags.hip)
+                return torch.ops.tmx.gather_flags([t for t, _ in flat], [int(c) for _, c in flat]).tolist()
+        vals = torch.cat([t.reshape(-1).to(torch.int32).cpu() for t, _ in flat]).tolist()
+        for t, consume in flat:
+            if consume:
+                t.zero_()
+        return vals
+
     def resolve(self) -> None:
         self._on_abandon = []
         items, self._items = self._items, []
         on_error, self._on_error = self._on_error, []
         if not items:
             return
-        devs = {t.device for t, _, _ in items}
-        if len(devs) == 1:
-            vals = torch.cat([t for t, _, _ in items]).tolist()  # the one host read
-        else:
-            vals = torch.cat([t.cpu() for t, _, _ in items]).tolist()
+        vals = self._read(items)
         chunks, off = [], 0
-        for t, _, _ in items:
-            chunks.append(vals[off : off + t.numel()])
-            off += t.numel()
+        for ts, _, _, _ in items:
+            n = sum(t.numel() for t in ts)
+            chunks.append(vals[off : off + n])
+            off += n
         try:
-            for (_, cb, err), v in zip(items, chunks):
+            for (_, cb, err, _), v in zip(items, chunks):
                 if err:
                     cb(v)
         except Exception:
             for fn in on_error:
                 fn()
             raise
-        for (_, cb, err), v in zip(items, chunks):
+        for (_, cb, err, _), v in zip(items, chunks):
             if not err:
                 cb(v)
+
+
+def _native() -> bool:
+    from torchmetrics_forked_amd import ops
+
+    return ops.load()
 
 
 _HOST = threading.local()
@@ -170,13 +191,7 @@ class DeferredChecks:
         if not self._flags:
             return
         keys = list(self._flags.keys())
-        devs = {self._flags[k].device for k in keys}
-        if len(devs) == 1:
-            snap = torch.cat([self._flags[k].reshape(1).to(torch.int32) for k in keys])
-        else:
-            snap = torch.cat([self._flags[k].reshape(1).to(torch.int32).cpu() for k in keys])
-        for k in keys:
-            self._flags[k].zero_()
+        flags = [self._flags[k] for k in keys]
         warn_keys = [k for k in keys if issubclass(k[0], Warning)]
 
         def _raise(vals: List[int]) -> None:
@@ -191,18 +206,30 @@ class DeferredChecks:
 
         batch = current_host_checks()
         if batch is None:
-            vals = snap.tolist()  # one host sync
+            vals = HostCheckBatch._read([(flags, _raise, True, True)])  # one host sync; the flags are cleared
             _warn(vals)
             _raise(vals)
             return
+        # snapshot + clear on the device now (one native kernel for all flags; later work -- a forward's restore of the
+        # accumulated flags -- must not leak into this check), read with the block's other checks at its end
+        devs = {f.device for f in flags}
+        if len(devs) == 1 and flags[0].is_cuda and _native():
+            snap = torch.ops.tmx.gather_flags_device(flags, [1] * len(flags))
+        else:
+            snap = torch.cat([f.reshape(-1).to(torch.int32) for f in flags])
+            snap = snap.cpu() if len(devs) > 1 else snap
+            for f in flags:
+                f.zero_()
         batch.add(snap, _raise, error=True)
         if warn_keys:
             batch.add(snap, _warn, error=False)
-        flags = [self._flags[k] for k in keys]
 
         def _put_back() -> None:  # the block raised before reading: the flags still owe their exception
-            for i, f in enumerate(flags):
-                f.bitwise_or_(snap[i].to(f.device, f.dtype).reshape(f.shape))
+            off = 0
+            for f in flags:
+                n = f.numel()
+                f.bitwise_or_(snap[off : off + n].to(f.device, f.dtype).reshape(f.shape))
+                off += n
 
         batch.on_abandon(_put_back)
 
@@ -223,6 +250,40 @@ class DeferredChecks:
                 self._flags[k] = f
             else:
                 cur.bitwise_or_(f)
+
+    def take(self) -> Optional[Tuple[List[Tuple[Type[Exception], str]], Tensor]]:
+        """Snapshot AND clear every flag in one launch (GPU flags; ``snapshot()`` + ``clear()`` otherwise): what
+        ``forward`` parks while its batch compute checks only the batch's own flags.  ``give_back`` ORs it in again."""
+        if not self._flags:
+            return None
+        keys = list(self._flags.keys())
+        flags = [self._flags[k] for k in keys]
+        if len({f.device for f in flags}) == 1 and flags[0].is_cuda and all(f.is_contiguous() for f in flags) and _native():
+            return keys, torch.ops.tmx.gather_flags_device(flags, [1] * len(flags))
+        snap = self.snapshot()
+        self.clear()
+        return keys, snap  # type: ignore[return-value]
+
+    def give_back(self, taken: Optional[Tuple[List[Tuple[Type[Exception], str]], Any]]) -> None:
+        if taken is None:
+            return
+        keys, snap = taken
+        if isinstance(snap, dict):
+            self.restore(snap)
+            return
+        cur = [self._flags.get(k) for k in keys]
+        if all(c is not None and c.device == snap.device and c.is_contiguous() for c in cur) and _native():
+            torch.ops.tmx.or_flags(cur, snap)
+            return
+        off = 0
+        for k, c in zip(keys, cur):  # the flag set changed meanwhile (a new device): per-flag restore
+            n = 1 if c is None else c.numel()
+            piece = snap[off : off + n]
+            off += n
+            if c is None or c.device != snap.device:
+                self._flags[k] = piece.clone()
+            else:
+                c.bitwise_or_(piece.to(c.dtype).reshape(c.shape))
 
 
 def make_sink(t: Tensor) -> Optional[DeferredChecks]:
