@@ -32,6 +32,7 @@
 #include "common.h"
 
 #include <map>
+#include <tuple>
 #include <mutex>
 #include "curve_hist_kernels.h"
 
@@ -1466,7 +1467,8 @@ void launch_class_pass(const uint32_t* cptr, int64_t n, int C, int ld, const T* 
   // row splits only when there are too few classes to fill the chip (exclusive-owner flush when splits == 1)
   int splits = 1;
   while ((int64_t)C * splits < 512 && n_pad / (8 * (splits * 2)) >= 1024) splits *= 2;
-  hipLaunchKernelGGL((class_hist_kernel<T, false>), C * splits, kClassThreads, kCodes * sizeof(uint32_t), stream(),
+  // 16-bit-packed LDS histogram, 512-thread workgroups, four per CU (csrc/curve_hist_kernels.h class_hist_u16_kernel)
+  hipLaunchKernelGGL((class_hist_u16_kernel<T>), C * splits, kClassThreadsU16, kCodes / 2 * sizeof(uint32_t), stream(),
                      reinterpret_cast<const uint16_t*>(cptr), n_pad, splits, hist, p, ld, target, n, bmode, speculative,
                      srows, state, cm, code_range, roll_mode, batch_hist, batch_range);
   TMX_LAUNCH_CHECK();
@@ -1476,22 +1478,24 @@ void launch_class_pass(const uint32_t* cptr, int64_t n, int C, int ld, const T* 
 // from the caching allocator per update it was re-allocated (hipMalloc, ~200 us of host time) on the first update after
 // a compute(), whose temporaries had split the cached block (tools/alloc_probe.py).  Work on one stream is ordered, so
 // one buffer per stream is race-free.  Under HIP-graph capture the allocator is used (the graph's private pool).
-at::Tensor codes_scratch(const at::TensorOptions& opts, int64_t elems) {
+// ``kind`` 0: int16 class-major codes, 1: int32 rare-row lists (one cache entry per (device, stream, kind)).
+at::Tensor stream_scratch(const at::TensorOptions& opts, int64_t elems, int kind) {
+  const auto dt = kind == 0 ? at::kShort : at::kInt;
   hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
   TMX_CHECK_HIP(hipStreamIsCapturing(stream(), &cap));
-  if (cap != hipStreamCaptureStatusNone) return at::empty({elems}, opts.dtype(at::kShort));
+  if (cap != hipStreamCaptureStatusNone) return at::empty({elems}, opts.dtype(dt));
   // At most kMaxScratch (device, stream) entries, least recently used evicted: a buffer goes back to the caching
   // allocator, which only hands it out again on the stream it was allocated on (stream-ordered, so safe).
-  constexpr size_t kMaxScratch = 4;
+  constexpr size_t kMaxScratch = 8;
   struct Entry {
     at::Tensor t;
     uint64_t used;
   };
   static std::mutex mu;
   static uint64_t tick = 0;
-  static auto* cache = new std::map<std::pair<int, hipStream_t>, Entry>();  // leaked: no teardown-order issue
+  static auto* cache = new std::map<std::tuple<int, hipStream_t, int>, Entry>();  // leaked: no teardown-order issue
   std::lock_guard<std::mutex> lock(mu);
-  const std::pair<int, hipStream_t> key{static_cast<int>(opts.device().index()), stream()};
+  const std::tuple<int, hipStream_t, int> key{static_cast<int>(opts.device().index()), stream(), kind};
   if (cache->find(key) == cache->end() && cache->size() >= kMaxScratch) {
     auto lru = cache->begin();
     for (auto it = cache->begin(); it != cache->end(); ++it)
@@ -1500,9 +1504,11 @@ at::Tensor codes_scratch(const at::TensorOptions& opts, int64_t elems) {
   }
   Entry& e = (*cache)[key];
   e.used = ++tick;
-  if (!e.t.defined() || e.t.numel() < elems) e.t = at::empty({elems}, opts.dtype(at::kShort));
+  if (!e.t.defined() || e.t.numel() < elems) e.t = at::empty({elems}, opts.dtype(dt));
   return e.t.narrow(0, 0, elems);
 }
+
+at::Tensor codes_scratch(const at::TensorOptions& opts, int64_t elems) { return stream_scratch(opts, elems, 0); }
 
 template <typename T, bool PADDED>
 void launch_two_pass(const T* p, const int64_t* target, int64_t n, int C, int ld, int* mode, int* state, bool speculative,
@@ -1510,7 +1516,7 @@ void launch_two_pass(const T* p, const int64_t* target, int64_t n, int C, int ld
                      int* code_range, int64_t* batch_hist = nullptr, int* batch_range = nullptr) {
   const int64_t n_pad = (n + kTileRows - 1) / kTileRows * kTileRows;
   auto codes = codes_scratch(opts, (int64_t)C * n_pad);
-  auto slow_rows = at::empty({2 * n}, opts.dtype(at::kInt));
+  auto slow_rows = stream_scratch(opts, 2 * n, 1);  // written before read (counts live in the state word)
   uint32_t* cptr = reinterpret_cast<uint32_t*>(codes.data_ptr());
   int* srows = slow_rows.data_ptr<int>();
   // single stream: the class pass reads the (used, real) pair straight from ``mode`` and its last workgroup rolls it

@@ -5,10 +5,11 @@
 //   * prep     — every (segment = class / label, sample) score becomes an order key whose ascending order is the
 //                DESCENDING score order (NaN first, -0.0 == +0.0), with a one-byte payload: bit 0 = positive label,
 //                bit 1 = ignored sample.  Multiclass labels come from target == class (no one-hot tensor).
-//   * sort     — LSD radix, 8-bit digits (4 passes for fp32 keys, 8 for fp64), each pass = tile histograms ->
-//                segmented exclusive scan -> scatter.  A tile is 4096 keys of ONE segment (256 threads x 16);
-//                the scatter ranks stably per wave: 64 consecutive keys per round, digit groups by 8 ballots, a
-//                running count per (wave, digit) in LDS, then a prefix over the 4 waves — deterministic.
+//   * sort     — LSD radix, 8-bit digits (4 passes for fp32 keys, 8 for fp64), each pass = tile histograms (tile-major,
+//                one 1-KiB row per tile) -> digit offsets by a chunked column scan -> scatter.  A tile is 4096 keys of
+//                ONE segment (256 threads x 16); the scatter ranks stably per wave: 64 consecutive keys per round,
+//                digit groups by 8 ballots, a running count per (wave, digit) in LDS, then a prefix over the 4 waves —
+//                deterministic.
 //   * reduce   — per tile: cumulative positive / negative weights (tile sums scanned per segment), tie-group ends
 //                where the next key differs, the previous group end's cumulative counts by a block scan (and a
 //                binary search when a tie group spans tiles); AUROC trapezoid and AP step terms summed in fp64,
@@ -58,41 +59,109 @@ template <> struct KeyOf<double> {
 };
 
 // ---------------------------------------------------------------------------------------------------------- prep
-// Scores of one chunk: element (s, r) at p[s * ss + r * rs], r < n_k, written to keys[s][off + r].
+// Scores of one chunk: element (s, r) at p[s * ss + r * rs], r < n_k, written to keys[s][off + r].  Grid (x, y) =
+// (row blocks, segments): the segment comes from blockIdx.y, so no 64-bit divide / modulo per element.
 // task 0 (multiclass): label = target[off + r] == s, ignored when == ignore_index;  task 1 (per element): target is
 // row-major [n, S]: label = t == 1, ignored when t == ignore_index.
 template <typename T>
-__global__ void rs_prep_kernel(const T* __restrict__ p, int64_t ss, int64_t rs, int64_t n_k, int64_t off, int S, int64_t n,
-                               const int64_t* __restrict__ target, int task, int64_t ignore_index, bool has_ignore,
-                               typename KeyOf<T>::type* __restrict__ keys, uint8_t* __restrict__ pay) {
-  const int64_t total = (int64_t)S * n_k;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-    const int s = static_cast<int>(i / n_k);
-    const int64_t r = i % n_k;
+__global__ void __launch_bounds__(256) rs_prep_kernel(const T* __restrict__ p, int64_t ss, int64_t rs, int64_t n_k, int64_t off, int S,
+                                                      int64_t n, const int64_t* __restrict__ target, int task, int64_t ignore_index,
+                                                      bool has_ignore, typename KeyOf<T>::type* __restrict__ keys, uint8_t* __restrict__ pay) {
+  const int s = blockIdx.y;
+  const T* ps = p + (int64_t)s * ss;
+  typename KeyOf<T>::type* ks = keys + (int64_t)s * n + off;
+  uint8_t* qs = pay + (int64_t)s * n + off;
+  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n_k; r += (int64_t)gridDim.x * blockDim.x) {
     const int64_t row = off + r;
     const int64_t t = task == 0 ? target[row] : target[row * S + s];
     const bool ign = has_ignore && t == ignore_index;
     const bool pos = task == 0 ? (t == s) : (t == 1);
-    keys[(int64_t)s * n + row] = KeyOf<T>::desc(p[s * ss + r * rs]);
-    pay[(int64_t)s * n + row] = static_cast<uint8_t>((pos && !ign ? 1 : 0) | (ign ? 2 : 0));
+    ks[r] = KeyOf<T>::desc(ps[r * rs]);
+    qs[r] = static_cast<uint8_t>((pos && !ign ? 1 : 0) | (ign ? 2 : 0));
   }
 }
 
 // ----------------------------------------------------------------------------------------------- sort: histograms
-// hist layout [S][256][T] (digit-major per segment): the scan of a segment is then one contiguous run.
+// Tile digit counts, TILE-major [S][T][256]: the 256 counts of a tile are one contiguous 1-KiB store (the previous
+// digit-major [S][256][T] layout wrote them with stride T: 256 scattered 4-B stores per tile).
 template <typename KT>
 __global__ void __launch_bounds__(kRsThreads) rs_hist_kernel(const KT* __restrict__ keys, int64_t n, int T, int shift, uint32_t* __restrict__ hist) {
   __shared__ uint32_t h[4][kRsBins];
-  const int s = blockIdx.x / T, t = blockIdx.x % T;
+  const int s = blockIdx.y, t = blockIdx.x;
   const int wave = threadIdx.x / kWave;
   for (int i = threadIdx.x; i < 4 * kRsBins; i += kRsThreads) (&h[0][0])[i] = 0u;
   __syncthreads();
   const int64_t base = (int64_t)s * n + (int64_t)t * kRsTile;
-  const int64_t len = min<int64_t>(kRsTile, n - (int64_t)t * kRsTile);
+  const int len = static_cast<int>(min<int64_t>(kRsTile, n - (int64_t)t * kRsTile));
+#pragma unroll 4
   for (int i = threadIdx.x; i < len; i += kRsThreads) atomicAdd(&h[wave][(keys[base + i] >> shift) & 0xFF], 1u);
   __syncthreads();
   const uint32_t c = h[0][threadIdx.x] + h[1][threadIdx.x] + h[2][threadIdx.x] + h[3][threadIdx.x];
-  hist[((int64_t)s * kRsBins + threadIdx.x) * T + t] = c;
+  hist[((int64_t)s * T + t) * kRsBins + threadIdx.x] = c;
+}
+
+// Digit offsets of every (segment, tile) from the tile-major counts, in two launches (thread = digit throughout, so
+// every access is a coalesced 1-KiB row):
+//   rs_scan_tiles  — per (segment, chunk of 64 tiles): each digit's counts replaced in place by their exclusive prefix
+//                    within the chunk; the chunk's per-digit totals to ctot[S][chunks][256];
+//   rs_scan_chunks — per segment: ctot replaced by its exclusive prefix over chunks, and base[S][256] = exclusive
+//                    prefix of the segment's digit totals over digits.
+// A key of digit d in tile t of segment s then starts at base[s][d] + ctot[s][t / 64][d] + hist[s][t][d].
+constexpr int kRsChunkTiles = 64;
+__global__ void __launch_bounds__(kRsBins) rs_scan_tiles_kernel(uint32_t* __restrict__ hist, int T, uint32_t* __restrict__ ctot, int nchunks) {
+  const int s = blockIdx.y, c = blockIdx.x, d = threadIdx.x;
+  const int t0 = c * kRsChunkTiles, t1 = min(T, t0 + kRsChunkTiles);
+  uint32_t* h = hist + (int64_t)s * T * kRsBins + d;
+  uint32_t run = 0;
+  int t = t0;
+  for (; t + 8 <= t1; t += 8) {  // 8 independent loads in flight per thread
+    uint32_t v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = h[(int64_t)(t + k) * kRsBins];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      h[(int64_t)(t + k) * kRsBins] = run;
+      run += v[k];
+    }
+  }
+  for (; t < t1; ++t) {
+    const uint32_t v = h[(int64_t)t * kRsBins];
+    h[(int64_t)t * kRsBins] = run;
+    run += v;
+  }
+  ctot[((int64_t)s * nchunks + c) * kRsBins + d] = run;
+}
+
+__global__ void __launch_bounds__(kRsBins) rs_scan_chunks_kernel(uint32_t* __restrict__ ctot, int nchunks, uint32_t* __restrict__ base) {
+  __shared__ uint32_t part[kRsBins];
+  const int s = blockIdx.x, d = threadIdx.x;
+  uint32_t* c = ctot + (int64_t)s * nchunks * kRsBins + d;
+  uint32_t run = 0;
+  int k = 0;
+  for (; k + 16 <= nchunks; k += 16) {  // 16 independent loads in flight, then the running sum (a serial load ->
+    uint32_t v[16];                     // store chain over the chunks took 16.6 us at 64 chunks)
+#pragma unroll
+    for (int u = 0; u < 16; ++u) v[u] = c[(int64_t)(k + u) * kRsBins];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      c[(int64_t)(k + u) * kRsBins] = run;
+      run += v[u];
+    }
+  }
+  for (; k < nchunks; ++k) {
+    const uint32_t v = c[(int64_t)k * kRsBins];
+    c[(int64_t)k * kRsBins] = run;
+    run += v;
+  }
+  part[d] = run;  // the segment's total of digit d
+  __syncthreads();
+  for (int off = 1; off < kRsBins; off <<= 1) {  // inclusive scan over the 256 digit totals
+    const uint32_t x = d >= off ? part[d - off] : 0u;
+    __syncthreads();
+    part[d] += x;
+    __syncthreads();
+  }
+  base[(int64_t)s * kRsBins + d] = d ? part[d - 1] : 0u;
 }
 
 // ------------------------------------------------------------------------------- segmented exclusive scan (u32)
@@ -170,40 +239,42 @@ inline void seg_exclusive_scan(uint32_t* a, int S, int64_t L, uint32_t* csum, in
 
 // ----------------------------------------------------------------------------------------------- sort: scatter
 // Wave w ranks tile keys [w * 1024, w * 1024 + 1024) in 16 rounds of 64 consecutive keys; equal-digit lanes of a
-// round are found with 8 ballots; cnt[w][d] is the wave's running count of digit d.  The tile is then reordered by
-// digit in LDS (stable) and written out in digit runs: consecutive threads store consecutive addresses of a run
-// (a direct scatter would touch up to 64 cache lines per store instruction).
+// round are found with 8 ballots; cnt[w][d] is the wave's running count of digit d (measured: issuing every round's
+// count update as a returning LDS atomic + lane shuffle instead ran 183 vs 68 us per pass at 16.7M keys).  The tile
+// is then reordered by digit in LDS (stable) and written out in digit runs: consecutive threads store consecutive
+// addresses of a run (a direct scatter would touch up to 64 cache lines per store instruction).
 template <typename KT>
 __global__ void __launch_bounds__(kRsThreads) rs_scatter_kernel(const KT* __restrict__ kin, const uint8_t* __restrict__ pin,
                                                                  KT* __restrict__ kout, uint8_t* __restrict__ pout, int64_t n, int T,
-                                                                 int shift, const uint32_t* __restrict__ hist, const uint32_t* __restrict__ csum,
-                                                                 int64_t L, int cps) {
+                                                                 int shift, const uint32_t* __restrict__ hist, const uint32_t* __restrict__ ctot,
+                                                                 int nchunks, const uint32_t* __restrict__ base) {
   __shared__ uint32_t cnt[4][kRsBins];
   __shared__ uint32_t gbase[kRsBins];   // destination of the tile's first key of digit d (segment-relative)
   __shared__ uint32_t lstart[kRsBins];  // first tile position of digit d after the local reorder
   __shared__ KT s_key[kRsTile];
   __shared__ uint8_t s_pay[kRsTile];
-  const int s = blockIdx.x / T, t = blockIdx.x % T;
+  const int s = blockIdx.y, t = blockIdx.x;
   const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
   for (int i = threadIdx.x; i < 4 * kRsBins; i += kRsThreads) (&cnt[0][0])[i] = 0u;
-  gbase[threadIdx.x] = seg_scanned(hist, csum, L, cps, s, (int64_t)threadIdx.x * T + t);
+  gbase[threadIdx.x] = base[(int64_t)s * kRsBins + threadIdx.x] + ctot[((int64_t)s * nchunks + t / kRsChunkTiles) * kRsBins + threadIdx.x] +
+                       hist[((int64_t)s * T + t) * kRsBins + threadIdx.x];
   __syncthreads();
   const int64_t seg0 = (int64_t)s * n;
   const int64_t tb = (int64_t)t * kRsTile;
-  const int64_t len = min<int64_t>(kRsTile, n - tb);
+  const int len = static_cast<int>(min<int64_t>(kRsTile, n - tb));
   KT key[kRsItems];
   uint8_t pay[kRsItems];
   uint32_t rank[kRsItems];
 #pragma unroll
   for (int k = 0; k < kRsItems; ++k) {
-    const int64_t i = (int64_t)wave * (kRsTile / 4) + k * kWave + lane;
+    const int i = wave * (kRsTile / 4) + k * kWave + lane;
     const bool ok = i < len;
     key[k] = ok ? kin[seg0 + tb + i] : KT(0);
     pay[k] = ok ? pin[seg0 + tb + i] : uint8_t(0);
   }
 #pragma unroll
   for (int k = 0; k < kRsItems; ++k) {
-    const int64_t i = (int64_t)wave * (kRsTile / 4) + k * kWave + lane;
+    const int i = wave * (kRsTile / 4) + k * kWave + lane;
     const bool ok = i < len;
     const uint32_t d = static_cast<uint32_t>((key[k] >> shift) & 0xFF);
     uint64_t match = __ballot(ok);
@@ -265,7 +336,7 @@ template <typename KT>
 __global__ void __launch_bounds__(kRsThreads) rs_tile_sums_kernel(const KT* __restrict__ keys, const uint8_t* __restrict__ pay, int64_t n, int T,
                                                                    uint32_t* __restrict__ pos_t, uint32_t* __restrict__ neg_t,
                                                                    uint32_t* __restrict__ end_t) {
-  const int s = blockIdx.x / T, t = blockIdx.x % T;
+  const int s = blockIdx.y, t = blockIdx.x;
   const int64_t seg0 = (int64_t)s * n, tb = (int64_t)t * kRsTile;
   const int64_t len = min<int64_t>(kRsTile, n - tb);
   uint32_t p = 0, q = 0, e = 0;
@@ -302,7 +373,7 @@ __global__ void __launch_bounds__(kRsThreads) rs_reduce_kernel(const KT* __restr
                                                                 RsScan ps, RsScan qs, RsScan es, double* __restrict__ part,
                                                                 float* __restrict__ pt_fps, float* __restrict__ pt_tps, T* __restrict__ pt_thr,
                                                                 const int64_t* __restrict__ pt_base) {
-  const int s = blockIdx.x / Tt, t = blockIdx.x % Tt;
+  const int s = blockIdx.y, t = blockIdx.x;
   const int64_t seg0 = (int64_t)s * n, tb = (int64_t)t * kRsTile;
   const int64_t len = min<int64_t>(kRsTile, n - tb);
   __shared__ uint32_t sp[kRsThreads], sq[kRsThreads], se[kRsThreads];
@@ -509,10 +580,11 @@ std::vector<at::Tensor> curve_sorted(const std::vector<at::Tensor>& chunks, cons
   if (n == 0 || S == 0) {
     return {out};
   }
+  // positions within a segment are 32-bit; the tile-sum scans of the reduce allow 2^31 / 4096 tiles per segment
+  TORCH_CHECK(n < (int64_t{1} << 31), "curve_sorted: more than 2^31 - 1 samples per class");
+  TORCH_CHECK(S <= 65535, "curve_sorted: more than 65535 classes / labels in one call");
   const int Tt = static_cast<int>((n + kRsTile - 1) / kRsTile);
-  TORCH_CHECK((int64_t)Tt <= (int64_t)kScanChunk * 4096 / kRsBins, "curve_sorted: more than 2^25 samples per class");
-  const int64_t L = (int64_t)kRsBins * Tt;
-  const int cps_h = static_cast<int>((L + kScanChunk - 1) / kScanChunk);
+  const int nchunks = (Tt + kRsChunkTiles - 1) / kRsChunkTiles;
   const int cps_t = (Tt + kScanChunk - 1) / kScanChunk;
   std::vector<at::Tensor> res;
   AT_DISPATCH_FLOATING_TYPES(dt, "curve_sorted", [&] {
@@ -529,22 +601,30 @@ std::vector<at::Tensor> curve_sorted(const std::vector<at::Tensor>& chunks, cons
     for (const auto& c : chunks) {
       const int64_t nk = c.size(1);
       if (nk > 0) {
-        hipLaunchKernelGGL(rs_prep_kernel<T>, grid_for((int64_t)S * nk, 256, 4096), 256, 0, stream(), c.data_ptr<T>(), c.stride(0),
-                           c.stride(1), nk, off, S, n, target.data_ptr<int64_t>(), static_cast<int>(task), ignore_index, has_ignore, ka, pa);
+        const dim3 pgrid(static_cast<unsigned>(std::min<int64_t>((nk + 255) / 256, std::max<int64_t>(1, 8192 / S))), static_cast<unsigned>(S));
+        hipLaunchKernelGGL(rs_prep_kernel<T>, pgrid, 256, 0, stream(), c.data_ptr<T>(), c.stride(0), c.stride(1), nk, off, S, n,
+                           target.data_ptr<int64_t>(), static_cast<int>(task), ignore_index, has_ignore, ka, pa);
         TMX_LAUNCH_CHECK();
       }
       off += nk;
     }
-    auto hist = at::empty({L * S}, opts.dtype(at::kInt));
-    auto csum = at::empty({(int64_t)S * cps_h}, opts.dtype(at::kInt));
+    auto hist = at::empty({(int64_t)S * Tt * kRsBins}, opts.dtype(at::kInt));
+    auto ctot = at::empty({(int64_t)S * nchunks * kRsBins}, opts.dtype(at::kInt));
+    auto dbase = at::empty({(int64_t)S * kRsBins}, opts.dtype(at::kInt));
     uint32_t* h = reinterpret_cast<uint32_t*>(hist.data_ptr());
-    uint32_t* cs = reinterpret_cast<uint32_t*>(csum.data_ptr());
+    uint32_t* ct = reinterpret_cast<uint32_t*>(ctot.data_ptr());
+    uint32_t* db = reinterpret_cast<uint32_t*>(dbase.data_ptr());
     const int passes = static_cast<int>(sizeof(KT));
+    const dim3 tgrid(static_cast<unsigned>(Tt), static_cast<unsigned>(S));
     for (int pss = 0; pss < passes; ++pss) {
-      hipLaunchKernelGGL(rs_hist_kernel<KT>, S * Tt, kRsThreads, 0, stream(), ka, n, Tt, 8 * pss, h);
+      hipLaunchKernelGGL(rs_hist_kernel<KT>, tgrid, kRsThreads, 0, stream(), ka, n, Tt, 8 * pss, h);
       TMX_LAUNCH_CHECK();
-      seg_exclusive_scan(h, S, L, cs, cps_h);
-      hipLaunchKernelGGL(rs_scatter_kernel<KT>, S * Tt, kRsThreads, 0, stream(), ka, pa, kb, pb, n, Tt, 8 * pss, h, cs, L, cps_h);
+      hipLaunchKernelGGL(rs_scan_tiles_kernel, dim3(static_cast<unsigned>(nchunks), static_cast<unsigned>(S)), kRsBins, 0, stream(), h, Tt,
+                         ct, nchunks);
+      TMX_LAUNCH_CHECK();
+      hipLaunchKernelGGL(rs_scan_chunks_kernel, S, kRsBins, 0, stream(), ct, nchunks, db);
+      TMX_LAUNCH_CHECK();
+      hipLaunchKernelGGL(rs_scatter_kernel<KT>, tgrid, kRsThreads, 0, stream(), ka, pa, kb, pb, n, Tt, 8 * pss, h, ct, nchunks, db);
       TMX_LAUNCH_CHECK();
       std::swap(ka, kb);
       std::swap(pa, pb);
@@ -557,7 +637,7 @@ std::vector<at::Tensor> curve_sorted(const std::vector<at::Tensor>& chunks, cons
     uint32_t* sc = reinterpret_cast<uint32_t*>(scs.data_ptr());
     uint32_t* la = reinterpret_cast<uint32_t*>(last.data_ptr());
     uint32_t *pos_t = su, *neg_t = su + (int64_t)S * Tt, *end_t = su + 2 * (int64_t)S * Tt;
-    hipLaunchKernelGGL(rs_tile_sums_kernel<KT>, S * Tt, kRsThreads, 0, stream(), ka, pa, n, Tt, pos_t, neg_t, end_t);
+    hipLaunchKernelGGL(rs_tile_sums_kernel<KT>, tgrid, kRsThreads, 0, stream(), ka, pa, n, Tt, pos_t, neg_t, end_t);
     TMX_LAUNCH_CHECK();
     // the totals need the last tile's own sums (the scan is exclusive)
     hipLaunchKernelGGL(rs_copy_last_kernel, (S + 255) / 256, 256, 0, stream(), pos_t, Tt, la, S);
@@ -588,7 +668,7 @@ std::vector<at::Tensor> curve_sorted(const std::vector<at::Tensor>& chunks, cons
       th = thr.data_ptr<T>();
       bp = base.data_ptr<int64_t>();
     }
-    hipLaunchKernelGGL((rs_reduce_kernel<T, KT>), S * Tt, kRsThreads, 0, stream(), ka, pa, n, Tt, ps, qs, es, part.data_ptr<double>(),
+    hipLaunchKernelGGL((rs_reduce_kernel<T, KT>), tgrid, kRsThreads, 0, stream(), ka, pa, n, Tt, ps, qs, es, part.data_ptr<double>(),
                        fp, tp, th, bp);
     TMX_LAUNCH_CHECK();
     hipLaunchKernelGGL(rs_final_kernel, S, 256, 0, stream(), part.data_ptr<double>(), Tt, ps, qs, la, la + S, out.data_ptr<double>());

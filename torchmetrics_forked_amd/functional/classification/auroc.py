@@ -59,7 +59,7 @@ def _reduce_auroc(
     native ``summary`` (column ``col``: 0 = AUROC, 1 = AP) the averages and the flag come from it directly."""
     if average is None or average == "none":
         return res
-    if average not in ("macro", "weighted") or (average == "weighted" and weights is None):
+    if average not in ("macro", "weighted") or (average == "weighted" and weights is None and summary is None):
         raise ValueError("Received an incompatible combinations of inputs to make reduction.")
 
     def _warn(v: List[int]) -> None:
