@@ -91,3 +91,33 @@ def test_fused_collection_forward_batch_sink():
     fa, fb = a.compute(), b.compute()
     for k in fa:
         torch.testing.assert_close(fa[k], fb[k], rtol=0, atol=0, msg=k)
+
+
+def test_gpu_forward_does_not_synchronise_and_defers_checks():
+    """A GPU forward neither reads device flags nor waits for the device: an invalid target in a forward batch raises
+    at the next compute() (the update-time deferral extended to forward), and the degenerate-class warnings of a
+    forward batch are emitted by that compute."""
+    import warnings
+
+    C = 16
+    m = tm.classification.MulticlassAUROC(num_classes=C).cuda()
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(256, C, generator=g).bfloat16().cuda()
+    t = torch.randint(0, C, (256,), generator=g).cuda()
+    m.update(x, t)  # the state exists: later forwards take the batch-sink route
+    bad = t.clone()
+    bad[3] = C + 5  # outside [0, C)
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")  # nothing may be read (and warned) during the forward itself
+        m(x, bad)
+    with pytest.raises(RuntimeError):
+        m.compute()
+    # a batch without positives of some class: its warning comes with the next compute, not with the forward
+    m2 = tm.classification.MulticlassAUROC(num_classes=C).cuda()
+    m2.update(x, t)
+    few = torch.zeros_like(t)  # only class 0 present in this batch
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")
+        m2(x, few)
+    with pytest.warns(UserWarning):
+        m2.compute()

@@ -26,6 +26,9 @@ for s in "$@"; do
     prof) run prof 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o headline --output-format csv -- python3 bench.py --steps 20 --warmup 5 ;;
     radix) run radix 300 python tools/radix_curve_bench.py; tail -1 "$OUT/radix.log" ;;
     radixprof) run radixprof 300 rocprofv3 --kernel-trace --stats -d "$OUT/radixprof" -o radix --output-format csv -- python3 tools/radix_curve_bench.py ;;
+    imgprof) run imgprof 900 rocprofv3 --kernel-trace --stats -d "$OUT/imgprof" -o image --output-format csv -- python3 bench.py --config image --steps 1 --warmup 1; tail -2 "$OUT/imgprof.log" ;;
+    bertprof) run bertprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/bertprof" -o bert --output-format csv -- python3 bench.py --config bert --steps 2 --warmup 1; tail -2 "$OUT/bertprof.log" ;;
+    mapbench) run mapbench 600 python bench.py --config map --steps 5 --warmup 1; tail -1 "$OUT/mapbench.log" ;;
     *) echo "unknown step $s" ;;
   esac
 done

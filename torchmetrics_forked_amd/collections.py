@@ -28,7 +28,7 @@ from torchmetrics_forked_amd.parallel.sync import PendingSyncMany, sync_states_m
 from torchmetrics_forked_amd.utilities.data import _flatten_dict, allclose
 from torchmetrics_forked_amd.utilities.plot import _AX_TYPE, _PLOT_OUT_TYPE, plot_single_or_multi_val
 from torchmetrics_forked_amd.utilities.prints import rank_zero_warn
-from torchmetrics_forked_amd.utilities.validation import host_checks
+from torchmetrics_forked_amd.utilities.validation import forward_scope, host_checks
 
 
 class MetricCollection(ModuleDict):
@@ -58,7 +58,7 @@ class MetricCollection(ModuleDict):
     @torch.jit.unused
     def forward(self, *args: Any, **kwargs: Any) -> Dict[str, Any]:
         # every member's batch value registers its host checks with one block: one device->host read per forward
-        with host_checks():
+        with forward_scope(), host_checks():
             return self._compute_and_reduce("forward", *args, **kwargs)
 
     def _leaders(self) -> List[str]:

@@ -81,6 +81,22 @@ class HostCheckBatch:
         self._on_abandon = []
         items, self._items = self._items, []
         on_error, self._on_error = self._on_error, []
+        if _in_forward() and items and all(not err for _, _, err, _ in items) and all(
+            t.is_cuda for ts, _, _, _ in items for t in ts
+        ):
+            # a forward on the GPU does not wait for the device: its warning flags are read with the next compute's
+            # checks (errors of a forward batch stay in the metric's deferred flags, see DeferredChecks.check)
+            pend = _pending()
+            pend.extend(items)
+            if len(pend) <= _MAX_PENDING:
+                return
+            items = list(pend)
+            pend.clear()
+        elif not _in_forward():
+            pend = _pending()
+            if pend:  # warnings parked by earlier forwards are read (and emitted) now, before this block's own
+                items = list(pend) + items
+                pend.clear()
         if not items:
             return
         vals = self._read(items)
@@ -109,6 +125,14 @@ def _native() -> bool:
 
 
 _HOST = threading.local()
+_MAX_PENDING = 256  # parked forward warning checks before one synchronous read flushes them
+
+
+def _pending() -> List[Tuple[List[Tensor], Callable[[List[int]], None], bool, bool]]:
+    p = getattr(_HOST, "pending", None)
+    if p is None:
+        p = _HOST.pending = []
+    return p
 
 
 def _batch_stack() -> List[HostCheckBatch]:
@@ -116,6 +140,21 @@ def _batch_stack() -> List[HostCheckBatch]:
     if st is None:
         st = _HOST.stack = []
     return st
+
+
+@contextmanager
+def forward_scope() -> Iterator[None]:
+    """Marks a ``forward``: its batch compute's flag checks must snapshot the flags at once (the accumulated flags are
+    OR-ed back before the block's single read); a plain ``compute`` lets that read consume them instead (no kernel)."""
+    _HOST.forward_depth = getattr(_HOST, "forward_depth", 0) + 1
+    try:
+        yield
+    finally:
+        _HOST.forward_depth -= 1
+
+
+def _in_forward() -> bool:
+    return getattr(_HOST, "forward_depth", 0) > 0
 
 
 def current_host_checks() -> Optional[HostCheckBatch]:
@@ -210,9 +249,20 @@ class DeferredChecks:
             _warn(vals)
             _raise(vals)
             return
-        # snapshot + clear on the device now (one native kernel for all flags; later work -- a forward's restore of the
-        # accumulated flags -- must not leak into this check), read with the block's other checks at its end
         devs = {f.device for f in flags}
+        if _in_forward() and len(devs) == 1 and flags[0].is_cuda:
+            # forward on the GPU: no host read now -- the batch's error flags stay set; the forward ORs the accumulated
+            # flags back and the next compute() raises (the update-time deferral, extended to forward's batch value)
+            return
+        if not _in_forward() and len(devs) == 1 and flags[0].is_cuda and _native():
+            # compute(): the block's single read returns these flags and clears them (no snapshot kernel; an abandoned
+            # block -- an exception before the read -- leaves them set, so the next compute still raises)
+            batch.add_many(flags, _raise, error=True, consume=True)
+            if warn_keys:
+                batch.add_many(flags, _warn, error=False)
+            return
+        # forward(): snapshot + clear on the device now (one native kernel for all flags) -- the forward ORs the
+        # accumulated flags back before the block's read, and they must not leak into this batch's check
         if len(devs) == 1 and flags[0].is_cuda and _native():
             snap = torch.ops.tmx.gather_flags_device(flags, [1] * len(flags))
         else:
