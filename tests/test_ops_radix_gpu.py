@@ -28,7 +28,7 @@ def _scores(n, S, dtype, ties, gen):
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
 @pytest.mark.parametrize("ties", [False, True])
-@pytest.mark.parametrize("n", [1, 4095, 4097, 100_003])
+@pytest.mark.parametrize("n", [1, 4095, 4097, 100_003, 4_300_003])  # the last: > 1024 tiles (two chunks of the tile-sum scan)
 def test_sorted_binary_matches_cpu(dtype, ties, n):
     gen = torch.Generator().manual_seed(n)
     p = _scores(n, 1, dtype, ties, gen).reshape(-1)

@@ -25,6 +25,10 @@ for s in "$@"; do
     bench50) run bench50 120 python bench.py --steps 50 --warmup 5; tail -1 "$OUT/bench50.log" ;;
     prof) run prof 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o headline --output-format csv -- python3 bench.py --steps 20 --warmup 5 ;;
     radix) run radix 300 python tools/radix_curve_bench.py; tail -1 "$OUT/radix.log" ;;
+    radixab) for r in 1 2; do
+               TMX_NATIVE_LIB=$PWD/build/ab_radix/_tmx_native.so run radix_old_$r 300 python tools/radix_curve_bench.py; tail -1 "$OUT/radix_old_$r.log"
+               run radix_new_$r 300 python tools/radix_curve_bench.py; tail -1 "$OUT/radix_new_$r.log"; done ;;
+    radixtest) run radixtest 300 python -u -m pytest tests/test_ops_radix_gpu.py tests/test_binary_samples_gpu.py -x -q --timeout 120 --timeout-method thread; tail -2 "$OUT/radixtest.log" ;;
     radixprof) run radixprof 300 rocprofv3 --kernel-trace --stats -d "$OUT/radixprof" -o radix --output-format csv -- python3 tools/radix_curve_bench.py ;;
     imgprof) run imgprof 900 rocprofv3 --kernel-trace --stats -d "$OUT/imgprof" -o image --output-format csv -- python3 bench.py --config image --steps 1 --warmup 1; tail -2 "$OUT/imgprof.log" ;;
     bertprof) run bertprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/bertprof" -o bert --output-format csv -- python3 bench.py --config bert --steps 2 --warmup 1; tail -2 "$OUT/bertprof.log" ;;

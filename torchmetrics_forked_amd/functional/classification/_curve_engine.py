@@ -211,6 +211,8 @@ def anchored_scores(
         pos_rows = None  # sorted below, only when the anchored route is taken
     else:
         p2 = preds.reshape(-1, 1) if task == "binary" else preds
+        if task == "binary" and cls_ops.count_exceeds(target, 1, cls_ops.ANCHOR_MAX_POS) > cls_ops.ANCHOR_MAX_POS:
+            return None  # decided by a capped count (stops reading once past the cap): no [N] compare + reduce
         lab = (target.reshape(p2.shape) == 1).t()
         C = p2.shape[1]
         counts = lab.sum(1)  # the positions of the positives only when the anchored route is taken (below)

@@ -412,6 +412,20 @@ def anchored_scores(cols: List[Tensor], pos_off: Tensor, pos_rows: Tensor, max_p
     return torch.ops.tmx.anchored_curve_scores(cols, pos_off, pos_rows, int(max_pos))
 
 
+def binary_samples_format(preds: Tensor, target: Tensor, err_flag: Optional[Tensor]) -> Tensor:
+    """GPU fp32 / fp64 binary samples (csrc/binary_samples.hip): scores flattened, sigmoid applied iff any is outside
+    [0, 1] (decided on device); ``err_flag`` (int32[1]) ORed with 1 when a target value is not 0 / 1."""
+    return torch.ops.tmx.binary_samples_format(preds, target, err_flag)
+
+
+def count_exceeds(target: Tensor, value: int, cap: int) -> int:
+    """Host int: the number of ``target == value`` when it is at most ``cap``, else some number > ``cap`` (the GPU
+    count stops reading once it passes the cap).  One 8-byte device-to-host read."""
+    if target.is_cuda and ops.use_native(target):
+        return int(torch.ops.tmx.count_eq_capped(target, int(value), int(cap)))
+    return int((target == value).sum())
+
+
 def curve_sorted(chunks: List[Tensor], target: Tensor, task: int, ignore_index: Optional[int], want_points: bool) -> List[Tensor]:
     """fp32 / fp64 curve scores by the hand-written segmented radix sort + fused tie-group scan (csrc/radix.hip).
 
