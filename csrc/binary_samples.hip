@@ -163,7 +163,8 @@ __global__ void __launch_bounds__(256) count_eq_kernel(const TT* __restrict__ t,
 template <typename TT>
 static void count_eq_launch(const TT* t, int64_t n, TT value, int64_t cap, unsigned long long* c) {
   const int64_t head = std::min<int64_t>(n, 65536);
-  hipLaunchKernelGGL(count_eq_kernel<TT>, 1, 256, 0, stream(), t, head, value, -1ll, c);
+  // 32 probe blocks (one block walking 64K int64 serially took 34 us: latency, not bandwidth)
+  hipLaunchKernelGGL(count_eq_kernel<TT>, static_cast<int>(std::min<int64_t>(32, (head + 2047) / 2048)), 256, 0, stream(), t, head, value, -1ll, c);
   if (n > head) {
     const int grid = grid_for(std::max<int64_t>((n - head + 3) / 4, 1), 256, 2048);
     hipLaunchKernelGGL(count_eq_kernel<TT>, grid, 256, 0, stream(), t + head, n - head, value, static_cast<long long>(cap), c);

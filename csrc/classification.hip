@@ -99,7 +99,9 @@ at::Tensor range_flag(const at::Tensor& x_) {
     // after one flag read; probabilities (all in range) are read once in full, without any atomics
     const float4* xv = reinterpret_cast<const float4*>(x.data_ptr<float>());
     const int64_t head = std::min<int64_t>(nvec, 16384);
-    hipLaunchKernelGGL(range_flag_f32_kernel, 1, block, 0, stream(), xv, head, tail, ntail, flag.data_ptr<int>());
+    // 16 probe blocks: one block reading the 256-KiB head alone took 20 us (latency-bound) on in-range data
+    hipLaunchKernelGGL(range_flag_f32_kernel, static_cast<int>(std::min<int64_t>(16, (head + 1023) / 1024)), block, 0, stream(), xv, head, tail,
+                       ntail, flag.data_ptr<int>());
     if (nvec > head) {
       const int grid = grid_for(std::max<int64_t>((nvec - head + 3) / 4, 1), block, 2048);
       hipLaunchKernelGGL(range_flag_f32_kernel, grid, block, 0, stream(), xv + head, nvec - head, tail, 0, flag.data_ptr<int>());

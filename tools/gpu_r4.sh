@@ -16,6 +16,7 @@ run() {  # run <name> <seconds> <cmd...>; stdout+stderr -> $OUT/<name>.log
 for s in "$@"; do
   case $s in
     u16) run u16 60 ./build/classpass_u16_exp; cat "$OUT/u16.log" ;;
+    gather) run gather 60 ./build/gather_class_exp; cat "$OUT/gather.log" ;;
     host) run host 120 python tools/host_overhead_probe.py ;;
     suite) run pytest_gpu 800 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread; tail -3 "$OUT/pytest_gpu.log" ;;
     smoke) run smoke 200 python -u -c "import __graft_entry__ as g; g.smoke()"; tail -1 "$OUT/smoke.log" ;;
