@@ -1481,11 +1481,11 @@ void launch_class_pass(const uint32_t* cptr, int64_t n, int C, int ld, const T* 
 // a compute(), whose temporaries had split the cached block (tools/alloc_probe.py).  Work on one stream is ordered, so
 // one buffer per stream is race-free.  Under HIP-graph capture the allocator is used (the graph's private pool).
 // ``kind`` 0: int16 class-major codes, 1: int32 rare-row lists (one cache entry per (device, stream, kind)).
-at::Tensor stream_scratch(const at::TensorOptions& opts, int64_t elems, int kind) {
+// ``capturing``: the caller's hipStreamIsCapturing verdict (one runtime query per update, not one per buffer).  The
+// returned tensor is the whole cached buffer (no narrow() view per call): callers take its data pointer.
+at::Tensor stream_scratch(const at::TensorOptions& opts, int64_t elems, int kind, bool capturing) {
   const auto dt = kind == 0 ? at::kShort : at::kInt;
-  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-  TMX_CHECK_HIP(hipStreamIsCapturing(stream(), &cap));
-  if (cap != hipStreamCaptureStatusNone) return at::empty({elems}, opts.dtype(dt));
+  if (capturing) return at::empty({elems}, opts.dtype(dt));
   // At most kMaxScratch (device, stream) entries, least recently used evicted: a buffer goes back to the caching
   // allocator, which only hands it out again on the stream it was allocated on (stream-ordered, so safe).
   constexpr size_t kMaxScratch = 8;
@@ -1507,18 +1507,23 @@ at::Tensor stream_scratch(const at::TensorOptions& opts, int64_t elems, int kind
   Entry& e = (*cache)[key];
   e.used = ++tick;
   if (!e.t.defined() || e.t.numel() < elems) e.t = at::empty({elems}, opts.dtype(dt));
-  return e.t.narrow(0, 0, elems);
+  return e.t;
 }
 
-at::Tensor codes_scratch(const at::TensorOptions& opts, int64_t elems) { return stream_scratch(opts, elems, 0); }
+static bool stream_capturing() {
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  TMX_CHECK_HIP(hipStreamIsCapturing(stream(), &cap));
+  return cap != hipStreamCaptureStatusNone;
+}
 
 template <typename T, bool PADDED>
 void launch_two_pass(const T* p, const int64_t* target, int64_t n, int C, int ld, int* mode, int* state, bool speculative,
                      int64_t ignore_index, bool has_ignore, int64_t* hist, int64_t* cm, int* err, const at::TensorOptions& opts,
                      int* code_range, int64_t* batch_hist = nullptr, int* batch_range = nullptr) {
   const int64_t n_pad = (n + kTileRows - 1) / kTileRows * kTileRows;
-  auto codes = codes_scratch(opts, (int64_t)C * n_pad);
-  auto slow_rows = stream_scratch(opts, 2 * n, 1);  // written before read (counts live in the state word)
+  const bool capturing = stream_capturing();
+  const auto codes = stream_scratch(opts, (int64_t)C * n_pad, 0, capturing);
+  const auto slow_rows = stream_scratch(opts, 2 * n, 1, capturing);  // written before read (counts live in the state word)
   uint32_t* cptr = reinterpret_cast<uint32_t*>(codes.data_ptr());
   int* srows = slow_rows.data_ptr<int>();
   // single stream: the class pass reads the (used, real) pair straight from ``mode`` and its last workgroup rolls it
@@ -1711,8 +1716,9 @@ void curve_hist_update_impl(const at::Tensor& preds_, const at::Tensor& target_,
       }
     }
   } range_guard{code_range, range_tracked};
-  auto preds = preds_.contiguous();
-  auto target = target_.contiguous().to(at::kLong);
+  // no dispatcher round trips for inputs that are already contiguous int64 (the hot path: ~1 us of host time each)
+  const at::Tensor preds = preds_.is_contiguous() ? preds_ : preds_.contiguous();
+  const at::Tensor target = target_.is_contiguous() && target_.scalar_type() == at::kLong ? target_ : target_.contiguous().to(at::kLong);
   const int C = static_cast<int>(hist.size(0));
   const int block = 256;
   // two-pass multiclass route for C <= 1024; rows are padded to a multiple of 8 classes when C % 8 != 0 (one copy)
@@ -1734,14 +1740,18 @@ void curve_hist_update_impl(const at::Tensor& preds_, const at::Tensor& target_,
   // range pre-pass; the class pass leaves the counts at zero for the next batch
   const bool speculative = two_pass_ok && mode_state.has_value() && !norm_flag.has_value();
   at::Tensor flag, state;
+  int* state_ptr = nullptr;
   if (speculative) {
     TORCH_CHECK(mode_state->scalar_type() == at::kInt && mode_state->numel() >= 8 && mode_state->is_contiguous(),
                 "mode_state must be int32[>= 8]");
     flag = *mode_state;
-    state = mode_state->narrow(0, 2, 6);
+    state_ptr = mode_state->data_ptr<int>() + 2;  // [2:8] of the persistent word (no narrow() view per call)
   } else {
     flag = norm_flag.has_value() ? norm_flag->to(at::kInt).contiguous() : range_flag(preds);
-    if (two_pass_ok) state = at::zeros({6}, preds.options().dtype(at::kInt));
+    if (two_pass_ok) {
+      state = at::zeros({6}, preds.options().dtype(at::kInt));
+      state_ptr = state.data_ptr<int>();
+    }
   }
   int64_t* cm = nullptr;
   if (confmat.has_value()) {
@@ -1762,7 +1772,7 @@ void curve_hist_update_impl(const at::Tensor& preds_, const at::Tensor& target_,
       static const bool small_off = std::getenv("TMX_CURVE_SMALL_OFF") != nullptr;  // A/B against the tile row pass
       const bool small_ok = !small_off && C <= kSmallVpt * 16 && (reinterpret_cast<uintptr_t>(preds.data_ptr()) & 15) == 0;
       if (small_ok) {
-        launch_small_two_pass<scalar_t>(p, target.data_ptr<int64_t>(), n, C, flag.data_ptr<int>(), state.data_ptr<int>(), speculative,
+        launch_small_two_pass<scalar_t>(p, target.data_ptr<int64_t>(), n, C, flag.data_ptr<int>(), state_ptr, speculative,
                                         ignore_index, has_ignore, hist.data_ptr<int64_t>(), cm, err, preds.options(), crange);
         range_tracked = true;
         return;
@@ -1772,10 +1782,10 @@ void curve_hist_update_impl(const at::Tensor& preds_, const at::Tensor& target_,
           const int ld = (C + 7) / 8 * 8;
           const at::Tensor padded = at::constant_pad_nd(preds.view({n, C}), {0, ld - C}, 0).contiguous();
           launch_two_pass<scalar_t, true>(reinterpret_cast<const scalar_t*>(padded.data_ptr()), target.data_ptr<int64_t>(), n, C,
-                                          ld, flag.data_ptr<int>(), state.data_ptr<int>(), speculative, ignore_index, has_ignore,
+                                          ld, flag.data_ptr<int>(), state_ptr, speculative, ignore_index, has_ignore,
                                           hist.data_ptr<int64_t>(), cm, err, preds.options(), crange, batch_hist, batch_range);
         } else {
-          launch_two_pass<scalar_t, false>(p, target.data_ptr<int64_t>(), n, C, C, flag.data_ptr<int>(), state.data_ptr<int>(),
+          launch_two_pass<scalar_t, false>(p, target.data_ptr<int64_t>(), n, C, C, flag.data_ptr<int>(), state_ptr,
                                            speculative, ignore_index, has_ignore, hist.data_ptr<int64_t>(), cm, err, preds.options(),
                                            crange, batch_hist, batch_range);
         }

@@ -42,6 +42,10 @@ def main() -> None:
         "MulticlassConfusionMatrix_C10": (lambda: tm.MulticlassConfusionMatrix(num_classes=10), mc(10)),
         "BinaryAUROC": (lambda: tm.BinaryAUROC(), (torch.rand(4096, device=dev).bfloat16(), torch.randint(0, 2, (4096,), device=dev))),
         "MeanSquaredError": (lambda: tm.MeanSquaredError(), (torch.randn(4096, device=dev), torch.randn(4096, device=dev))),
+        "Collection_AUROC_ConfMat_C1000": (
+            lambda: tm.MetricCollection({"auroc": tm.MulticlassAUROC(num_classes=1000), "confmat": tm.MulticlassConfusionMatrix(num_classes=1000)}),
+            mc(1000, 256),
+        ),
     }
     out = {}
     for name, (make, batch) in cases.items():
@@ -70,6 +74,22 @@ def main() -> None:
     s = io.StringIO()
     pstats.Stats(prof, stream=s).sort_stats("tottime").print_stats(18)
     out["profile_MulticlassAUROC_C10"] = [ln for ln in s.getvalue().splitlines() if ln.strip()][:30]
+    # host time per update by op / runtime call (torch.profiler, CPU self time): the headline collection
+    coll = cases["Collection_AUROC_ConfMat_C1000"][0]().to(dev)
+    batch = cases["Collection_AUROC_ConfMat_C1000"][1]
+    for _ in range(20):
+        coll.update(*batch)
+    torch.cuda.synchronize(dev)
+    K = 200
+    with torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CPU, torch.profiler.ProfilerActivity.CUDA]) as prof2:
+        for _ in range(K):
+            coll.update(*batch)
+        torch.cuda.synchronize(dev)
+    rows = []
+    for ka in prof2.key_averages():
+        if ka.self_cpu_time_total > 0:
+            rows.append((ka.key[:70], round(ka.count / K, 2), round(ka.self_cpu_time_total / K, 2)))
+    out["collection_host_us_per_update_by_op"] = sorted(rows, key=lambda r: -r[2])[:20]
     print(json.dumps(out), flush=True)
 
 

@@ -24,6 +24,10 @@ _loaded: Optional[bool] = None
 _error: Optional[str] = None
 
 
+# read once at import (A/B switch for whole processes); use_native runs on every update's hot path
+_DISABLED = os.environ.get("TMX_DISABLE_NATIVE", "0") == "1"
+
+
 def load() -> bool:
     """Load the native library once; returns True on success."""
     global _loaded, _error
@@ -68,12 +72,14 @@ def use_native(t: torch.Tensor, *others: Optional[torch.Tensor]) -> bool:
     host scalars excepted): a HIP kernel handed a host pointer faults the GPU instead of raising, so the device error
     torch itself would give is raised here, before any launch."""
     if t.is_cuda:
+        dev = t.device
         for o in others:
-            if isinstance(o, torch.Tensor) and o.device != t.device and not (o.device.type == "cpu" and o.dim() == 0):
-                raise _device_error(t.device, o.device)
-        if os.environ.get("TMX_DISABLE_NATIVE", "0") == "1":
+            if o is not None and o.device != dev and not (o.device.type == "cpu" and o.dim() == 0):
+                raise _device_error(dev, o.device)
+        if _DISABLED:
             return False
-        require(t)
+        if not _loaded:
+            require(t)
         return True
     for o in others:
         if isinstance(o, torch.Tensor) and o.is_cuda:
