@@ -45,13 +45,31 @@ def main() -> None:
         best = None
         for rep in range(3):
             torch.cuda.synchronize(dev)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             t0 = time.perf_counter()
+            e0.record()
+            for i in range(args.steps):
+                out = step(*pool[i % 4])
+            e1.record()
+            t_enq = time.perf_counter()
+            torch.cuda.synchronize(dev)
+            dt = (time.perf_counter() - t0) / args.steps
+            if best is None or dt < best:
+                best = dt
+                res[f"{mode}_host_enqueue_us"] = round((t_enq - t0) / args.steps * 1e6, 1)
+                res[f"{mode}_gpu_span_us"] = round(e0.elapsed_time(e1) / args.steps * 1e3, 1)
+        res[f"{mode}_ms"] = round(best * 1e3, 4)
+        # device kernels per step (profiler; GPU time by kernel)
+        with torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CPU, torch.profiler.ProfilerActivity.CUDA]) as prof:
             for i in range(args.steps):
                 out = step(*pool[i % 4])
             torch.cuda.synchronize(dev)
-            dt = (time.perf_counter() - t0) / args.steps
-            best = dt if best is None else min(best, dt)
-        res[f"{mode}_ms"] = round(best * 1e3, 4)
+        kern = [(ka.key[:60], round(ka.count / args.steps, 2), round(ka.device_time_total / args.steps, 1))
+                for ka in prof.key_averages() if ka.device_time_total > 0 and ka.self_device_time_total > 0]
+        res[f"{mode}_device_us_per_step"] = sorted(kern, key=lambda k: -k[2])[:14]
+        host = [(ka.key[:60], round(ka.count / args.steps, 2), round(ka.self_cpu_time_total / args.steps, 1))
+                for ka in prof.key_averages() if ka.self_cpu_time_total > 0]
+        res[f"{mode}_host_us_per_step"] = sorted(host, key=lambda k: -k[2])[:14]
         if mode == "forward":
             res["last_batch_auroc"] = float(out["auroc"])
     res["forward_over_update"] = round(res["forward_ms"] / res["update_ms"], 3)

@@ -17,6 +17,8 @@ for s in "$@"; do
   case $s in
     u16) run u16 60 ./build/classpass_u16_exp; cat "$OUT/u16.log" ;;
     gather) run gather 60 ./build/gather_class_exp; cat "$OUT/gather.log" ;;
+    pipe) run pipe 90 ./build/classpass_pipe_exp; cat "$OUT/pipe.log" ;;
+    wpat) run wpat 60 ./build/write_pattern_exp; cat "$OUT/wpat.log" ;;
     host) run host 120 python tools/host_overhead_probe.py ;;
     suite) run pytest_gpu 800 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread; tail -3 "$OUT/pytest_gpu.log" ;;
     smoke) run smoke 200 python -u -c "import __graft_entry__ as g; g.smoke()"; tail -1 "$OUT/smoke.log" ;;

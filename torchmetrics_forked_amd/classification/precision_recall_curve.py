@@ -304,7 +304,7 @@ class _CurveMetric(Metric):
             return super()._fused_forward_begin()
         snap_def = None
         if self._deferred is not None:
-            snap_def = self._deferred.take()
+            snap_def = self._deferred.take_for_forward()
         count = self._update_count
         saved = self._enter_batch_mode()
         self.__dict__["_batch_sink"] = self._batch_scratch()

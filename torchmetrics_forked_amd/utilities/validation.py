@@ -314,6 +314,19 @@ class DeferredChecks:
         self.clear()
         return keys, snap  # type: ignore[return-value]
 
+    def take_for_forward(self) -> Optional[Tuple[List[Tuple[Type[Exception], str]], Tensor]]:
+        """``take()`` as ``forward`` needs it: a GPU forward's batch compute never reads device flags (``check``
+        returns at once under :func:`forward_scope`), so there is nothing to park -- no snapshot and no OR-back
+        launch (2 x 2 launches per forward of a two-metric collection).  Elsewhere: ``take()``."""
+        if not self._flags:
+            return None
+        if _in_forward() and _native():
+            flags = list(self._flags.values())
+            dev = flags[0].device
+            if dev.type == "cuda" and all(f.device == dev for f in flags):
+                return None
+        return self.take()
+
     def give_back(self, taken: Optional[Tuple[List[Tuple[Type[Exception], str]], Any]]) -> None:
         if taken is None:
             return
