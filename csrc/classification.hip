@@ -100,8 +100,8 @@ at::Tensor range_flag(const at::Tensor& x_) {
     const float4* xv = reinterpret_cast<const float4*>(x.data_ptr<float>());
     const int64_t head = std::min<int64_t>(nvec, 16384);
     // 16 probe blocks: one block reading the 256-KiB head alone took 20 us (latency-bound) on in-range data
-    hipLaunchKernelGGL(range_flag_f32_kernel, static_cast<int>(std::min<int64_t>(16, (head + 1023) / 1024)), block, 0, stream(), xv, head, tail,
-                       ntail, flag.data_ptr<int>());
+    hipLaunchKernelGGL(range_flag_f32_kernel, static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(16, (head + 1023) / 1024))), block, 0,
+                       stream(), xv, head, tail, ntail, flag.data_ptr<int>());  // >= 1 block: it also checks the < 4-element tail
     if (nvec > head) {
       const int grid = grid_for(std::max<int64_t>((nvec - head + 3) / 4, 1), block, 2048);
       hipLaunchKernelGGL(range_flag_f32_kernel, grid, block, 0, stream(), xv + head, nvec - head, tail, 0, flag.data_ptr<int>());
@@ -1202,163 +1202,15 @@ __global__ void __launch_bounds__(256) curve_hist_mc_kernel(const T* __restrict_
 //   3. codes go through an LDS image [C][64] to the class-major scratch as 128-B class segments.
 // The FIXUP instance redoes the codes of a mis-speculated batch (mode[0] != mode[1]); the class pass is shared.
 // ---------------------------------------------------------------------------------------------------------
-constexpr int kSmallRows = 64;
-constexpr int kSmallVpt = 16;
-constexpr int kSmallCmMax = 64;  // LDS-privatised confusion matrix up to 64 x 64 (16 KiB)
-
-template <typename T, int TL, bool FIXUP>
-__global__ void __launch_bounds__(kSmallRows * TL) mc_codes_small_kernel(
-    const T* __restrict__ preds, const int64_t* __restrict__ target, int64_t n, int C, int* __restrict__ mode, int64_t ignore_index,
-    bool has_ignore, uint16_t* __restrict__ codes, int64_t n_pad, int64_t* __restrict__ confmat, int* __restrict__ err,
-    bool record_mode, int* __restrict__ slow_rows, int* __restrict__ slow_count, uint32_t* __restrict__ pcm) {
-  extern __shared__ __attribute__((aligned(16))) uint16_t s_small[];  // staging [64][C], then image [C][64]; cm [C][C]
-  int use_mode;
-  if constexpr (FIXUP) {
-    const int m0 = mode[0], m1 = mode[1];
-    if (m0 == m1) return;
-    use_mode = m1;
-  } else {
-    use_mode = mode[0];
-  }
-  // C <= 64: the confusion matrix is privatised in LDS (at C = 2 every row's atomic hit one of 4 global words)
-  uint32_t* s_cm = reinterpret_cast<uint32_t*>(s_small + kSmallRows * C);
-  const bool lds_cm = !FIXUP && confmat != nullptr && C <= kSmallCmMax;
-  if (lds_cm)
-    for (int i = threadIdx.x; i < C * C; i += kSmallRows * TL) s_cm[i] = 0u;
-  const int64_t ntiles = n_pad / kSmallRows;
-  bool bad = false;
-  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-  __syncthreads();  // previous tile's class segments were read from the image
-  const int64_t r0 = tile * kSmallRows;
-  const int rows = static_cast<int>(min<int64_t>(kSmallRows, n - r0));
-  // 1. stage the block's scores (byte range [r0 C, (r0 + rows) C) x 2; r0 C x 2 is a multiple of 128 B)
-  {
-    const int64_t nelem = (int64_t)rows * C;
-    const uint16_t* src = reinterpret_cast<const uint16_t*>(preds) + r0 * C;
-    const int nvec = static_cast<int>(nelem / 8);
-    for (int i = threadIdx.x; i < nvec; i += kSmallRows * TL)
-      reinterpret_cast<uint4*>(s_small)[i] = reinterpret_cast<const uint4*>(src)[i];
-    for (int i = nvec * 8 + threadIdx.x; i < nelem; i += kSmallRows * TL) s_small[i] = src[i];
-  }
-  __syncthreads();
-  const int q = threadIdx.x % TL, lr = threadIdx.x / TL;  // lane within the row, row within the block
-  const int64_t r = r0 + lr;
-  const int cb = q * kSmallVpt;
-  const bool in_rows = lr < rows;
-  float v[kSmallVpt];
-  uint16_t raw[kSmallVpt];
-#pragma unroll
-  for (int j = 0; j < kSmallVpt; ++j) {
-    const int c = cb + j;
-    const bool ok = in_rows && c < C;
-    raw[j] = ok ? s_small[lr * C + c] : (uint16_t)0;
-    v[j] = ok ? to_f32<T>(*reinterpret_cast<const T*>(&raw[j])) : -INFINITY;
-  }
-  const int64_t t = in_rows ? target[r] : -1;
-  const bool valid = in_rows && !(has_ignore && t == ignore_index);
-  // row statistics over the TL lanes of the row (xor shuffles stay inside aligned groups of TL lanes)
-  float mx = -INFINITY, mn = INFINITY, sum = 0.f;
-#pragma unroll
-  for (int j = 0; j < kSmallVpt; ++j) {
-    if (cb + j < C) {
-      mx = __builtin_fmaxf(mx, v[j]);
-      mn = __builtin_fminf(mn, v[j]);
-      sum += v[j];
-    }
-  }
-#pragma unroll
-  for (int off = 1; off < TL; off <<= 1) {
-    mx = __builtin_fmaxf(mx, __shfl_xor(mx, off, kWave));
-    mn = __builtin_fminf(mn, __shfl_xor(mn, off, kWave));
-    sum += __shfl_xor(sum, off, kWave);
-  }
-  bool fin = __builtin_isfinite(mx);
-  // arg-max of a finite row: the first class holding the maximum
-  int am = C;
-#pragma unroll
-  for (int j = kSmallVpt - 1; j >= 0; --j)
-    if (cb + j < C && v[j] == mx) am = cb + j;
-#pragma unroll
-  for (int off = 1; off < TL; off <<= 1) am = min(am, __shfl_xor(am, off, kWave));
-  float s = 0.f, inv = 0.f;
-  if (use_mode != 0) {
-    float acc = 0.f;
-#pragma unroll
-    for (int j = 0; j < kSmallVpt; ++j) {
-      v[j] = cb + j < C ? exp_nonpos(v[j] - mx) : 0.f;
-      acc += v[j];
-    }
-#pragma unroll
-    for (int off = 1; off < TL; off <<= 1) acc += __shfl_xor(acc, off, kWave);
-    s = acc;
-    inv = 1.f / s;
-    fin = fin && s == s;
-  } else {
-    fin = fin && __builtin_isfinite(sum);
-  }
-  const bool slow = valid && !fin;
-  const bool keep = valid && fin;
-  // 3. codes into the image [C][64] (the staging area is free once every lane holds its values)
-  __syncthreads();
-#pragma unroll
-  for (int j = 0; j < kSmallVpt; ++j) {
-    const int c = cb + j;
-    if (!in_rows || c >= C) continue;
-    uint32_t code = 0x8000u;
-    if (keep) {
-      const uint32_t b = use_mode != 0 ? (rne_word<T>(div_rn(v[j], s, inv)) >> 16) : (uint32_t)raw[j];
-      code = raw_code<T>(b);
-      if (c == t && !(code & 0x8000u)) code |= 0x4000u;
-    }
-    s_small[c * kSmallRows + lr] = static_cast<uint16_t>(code);
-  }
-  if (lr >= rows && q == 0) {  // padding rows of the last block: skipped codes
-    for (int c = 0; c < C; ++c) s_small[c * kSmallRows + lr] = 0x8000u;
-  }
-  if (q == 0 && in_rows) {
-    if constexpr (!FIXUP) {
-      if (confmat != nullptr && keep && t >= 0 && t < C && am < C) {
-        if (lds_cm) atomicAdd(s_cm + t * C + am, 1u);
-        else atomic_add_i64(confmat + t * C + am, 1);
-      }
-      if (err != nullptr && valid && (t < 0 || t >= C)) atomicOr(err, 1);
-    }
-    if (slow) {
-      const int list = FIXUP ? 1 : 0;
-      slow_rows[list * n + atomicAdd(slow_count + list, 1)] = static_cast<int>(r);
-    }
-  }
-  if (!FIXUP && record_mode && q == 0) bad = bad || slow || (valid && (mx > 1.f || mn < 0.f));
-  __syncthreads();
-  // class segments: C rows of 64 codes = 8 x 16 B each
-  for (int i = threadIdx.x; i < C * 8; i += kSmallRows * TL) {
-    const int c = i >> 3, k = i & 7;
-    reinterpret_cast<uint4*>(codes + (int64_t)c * n_pad + r0)[k] = reinterpret_cast<const uint4*>(s_small + c * kSmallRows)[k];
-  }
-  }  // tiles
-  if (lds_cm) {  // per-block partial (summed by class_partial_reduce_kernel), else atomics on the few cells
-    __syncthreads();
-    if (pcm != nullptr)
-      for (int i = threadIdx.x; i < C * C; i += kSmallRows * TL) pcm[(int64_t)blockIdx.x * C * C + i] = s_cm[i];
-    else
-      for (int i = threadIdx.x; i < C * C; i += kSmallRows * TL)
-        if (s_cm[i]) atomic_add_i64(confmat + i, s_cm[i]);
-  }
-  if constexpr (!FIXUP) {
-    if (record_mode && __syncthreads_or(bad) && threadIdx.x == 0 &&
-        __hip_atomic_load(mode + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
-      __hip_atomic_store(mode + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
 template <typename T, bool FIXUP>
 void launch_small_rows(int TL, int grid, const T* p, const int64_t* target, int64_t n, int C, int* mode, int64_t ignore_index, bool has_ignore,
-                       uint16_t* codes, int64_t n_pad, int64_t* cm, int* err, bool rec, int* srows, int* scount, uint32_t* pcm) {
+                       uint16_t* codes, int64_t n_pad, int64_t* cm, int* err, bool rec, int* srows, int* scount, uint32_t* pcm,
+                       float4* row_stats = nullptr) {
   const size_t shm = (size_t)kSmallRows * C * sizeof(uint16_t) + (C <= kSmallCmMax ? (size_t)C * C * sizeof(uint32_t) : 0);
 #define TMX_SMALL_CASE(TLV)                                                                                                     \
   case TLV:                                                                                                                      \
     hipLaunchKernelGGL((mc_codes_small_kernel<T, TLV, FIXUP>), grid, kSmallRows * TLV, shm, stream(), p, target, n, C, mode,   \
-                       ignore_index, has_ignore, codes, n_pad, cm, err, rec, srows, scount, pcm);                                 \
+                       ignore_index, has_ignore, codes, n_pad, cm, err, rec, srows, scount, pcm, row_stats);                      \
     break;
   switch (TL) {
     TMX_SMALL_CASE(1) TMX_SMALL_CASE(2) TMX_SMALL_CASE(4) TMX_SMALL_CASE(8) TMX_SMALL_CASE(16)
@@ -1367,6 +1219,9 @@ void launch_small_rows(int TL, int grid, const T* p, const int64_t* target, int6
 #undef TMX_SMALL_CASE
   TMX_LAUNCH_CHECK();
 }
+
+at::Tensor stream_scratch(const at::TensorOptions& opts, int64_t elems, int kind, bool capturing);
+static bool stream_capturing();
 
 // Small-class two-pass route: small row pass (+ FIXUP), then the shared class pass (which finishes rare rows and
 // rolls the speculation).  Codes are class-major [C][n_pad], n_pad = 64-row blocks.
@@ -1386,17 +1241,19 @@ void launch_small_two_pass(const T* p, const int64_t* target, int64_t n, int C, 
   const int grid = static_cast<int>(std::min<int64_t>(ntiles, std::max(256, grid_cap / TL)));
   // confusion-matrix partials per block (C <= 32: at most 4 MiB), summed by the reduce launch: no same-cell atomics
   const bool use_pcm = cm != nullptr && C <= 32;
-  auto pcm_t = use_pcm ? at::empty({(int64_t)grid * C * C}, opts.dtype(at::kInt)) : at::Tensor();
-  uint32_t* pcm = use_pcm ? reinterpret_cast<uint32_t*>(pcm_t.data_ptr<int>()) : nullptr;
-  auto codes = at::empty({(int64_t)C * n_pad}, opts.dtype(at::kShort));
-  auto slow_rows = at::empty({2 * n}, opts.dtype(at::kInt));
+  // per-stream cached scratch (no allocator round trips per update); stream order keeps consecutive updates apart
+  const bool capturing = stream_capturing();
+  const auto pcm_t = use_pcm ? stream_scratch(opts, (int64_t)grid * C * C, 3, capturing) : at::Tensor();
+  uint32_t* pcm = use_pcm ? reinterpret_cast<uint32_t*>(pcm_t.data_ptr()) : nullptr;
+  const auto codes = stream_scratch(opts, (int64_t)C * n_pad, 0, capturing);
+  const auto slow_rows = stream_scratch(opts, 2 * n, 1, capturing);
+  // per-row softmax statistics: a mispredicted batch is refit by the class pass (no FIXUP launch)
+  const auto stats = speculative ? stream_scratch(opts, 4 * n, 2, capturing) : at::Tensor();
+  float4* rstats = speculative ? reinterpret_cast<float4*>(stats.data_ptr()) : nullptr;
   uint16_t* cptr = reinterpret_cast<uint16_t*>(codes.data_ptr());
   int* srows = slow_rows.data_ptr<int>();
   launch_small_rows<T, false>(TL, grid, p, target, n, C, mode, ignore_index, has_ignore, cptr, n_pad, cm, err, speculative, srows, state,
-                              pcm);
-  if (speculative)
-    launch_small_rows<T, true>(TL, std::min(grid, 1024), p, target, n, C, mode, ignore_index, has_ignore, cptr, n_pad, cm, err, false,
-                               srows, state, nullptr);
+                              pcm, rstats);
   // Class pass: packed LDS histogram per (class, row split) — with few classes 1 / C of the codes are positives —
   // and a partial flush (plain stores of the occupied range, then one reduce launch) instead of global int64 atomics:
   // every split of a class hits the same few thousand bins.  Splits: enough (class, split) blocks to fill the chip,
@@ -1409,12 +1266,12 @@ void launch_small_two_pass(const T* p, const int64_t* target, int64_t n, int C, 
   while ((int64_t)C * splits < 32 && nv / (splits * 2) >= 1024) splits *= 2;
   static const int forced_splits = [] { const char* v = std::getenv("TMX_SMALL_SPLITS"); return v ? std::atoi(v) : 0; }();
   if (forced_splits > 0) splits = forced_splits;  // experiment knob (tools/mc_small_probe.py sweeps)
-  auto partial = at::empty({(int64_t)C * splits * kCodes}, opts.dtype(at::kInt));
-  auto prange = at::empty({(int64_t)C * splits * 2}, opts.dtype(at::kInt));
-  uint32_t* pp = reinterpret_cast<uint32_t*>(partial.data_ptr<int>());
+  const auto partial = stream_scratch(opts, (int64_t)C * splits * kCodes, 4, capturing);
+  const auto prange = stream_scratch(opts, (int64_t)C * splits * 2, 5, capturing);
+  uint32_t* pp = reinterpret_cast<uint32_t*>(partial.data_ptr());
   hipLaunchKernelGGL((class_hist_partial_kernel<T>), C * splits, kClassThreads, kCodes * sizeof(uint32_t), stream(), cptr, n_pad, splits,
                      hist, p, C, target, n, mode, speculative, srows, state, cm, code_range, speculative ? mode : nullptr, pp,
-                     prange.data_ptr<int>());
+                     reinterpret_cast<int*>(prange.data_ptr()), rstats);
   TMX_LAUNCH_CHECK();
   const int pcm_slices = use_pcm ? std::max(1, std::min(64, grid / 256)) : 0;
   hipLaunchKernelGGL(class_partial_reduce_kernel, dim3(kCodes / 256 + 1 + pcm_slices, C), 256, 0, stream(), pp, prange.data_ptr<int>(),
@@ -1427,27 +1284,29 @@ void launch_small_two_pass(const T* p, const int64_t* target, int64_t n, int C, 
 template <typename T, bool PADDED>
 void launch_row_pass(const T* p, const int64_t* target, int64_t n, int C, int ld, int* mode, int* state, bool speculative,
                      int64_t ignore_index, bool has_ignore, int64_t* cm, int* err, uint32_t* cptr, int* srows,
-                     bool roll_in_class_pass = false) {
+                     bool roll_in_class_pass = false, float4* row_stats = nullptr) {
   TORCH_CHECK(n < (int64_t{1} << 31), "curve_hist_update: more than 2^31 rows in one batch");
   const int64_t n_pad = (n + kTileRows - 1) / kTileRows * kTileRows;
   const int64_t ntiles = n_pad / kTileRows;
   const int grid = static_cast<int>((ntiles + 7) / 8 * 8);  // one block per tile (XCD-aware order inside)
   const int fixup_grid = std::min(grid, 128);                // exits at once unless the speculation was wrong
   const size_t shm = (size_t)512 * (C > 512 ? 2 : 1) * kSlots * sizeof(uint32_t);  // 32 / 64 KiB -> 2 blocks per CU
+  // with row_stats the class pass refits a mispredicted batch itself: no FIXUP launch
+  const bool fixup = speculative && row_stats == nullptr;
   if (C > 512) {
     hipLaunchKernelGGL((mc_codes_kernel<T, false, 2, PADDED>), grid, kRowThreads, shm, stream(), p, target, n, C, ld, mode, ignore_index,
-                       has_ignore, cptr, n_pad, cm, err, speculative, srows, state);
+                       has_ignore, cptr, n_pad, cm, err, speculative, srows, state, row_stats);
     TMX_LAUNCH_CHECK();
-    if (speculative) {
+    if (fixup) {
       hipLaunchKernelGGL((mc_codes_kernel<T, true, 2, PADDED>), fixup_grid, kRowThreads, shm, stream(), p, target, n, C, ld, mode,
                          ignore_index, has_ignore, cptr, n_pad, cm, err, false, srows, state);
       TMX_LAUNCH_CHECK();
     }
   } else {
     hipLaunchKernelGGL((mc_codes_kernel<T, false, 1, PADDED>), grid, kRowThreads, shm, stream(), p, target, n, C, ld, mode, ignore_index,
-                       has_ignore, cptr, n_pad, cm, err, speculative, srows, state);
+                       has_ignore, cptr, n_pad, cm, err, speculative, srows, state, row_stats);
     TMX_LAUNCH_CHECK();
-    if (speculative) {
+    if (fixup) {
       hipLaunchKernelGGL((mc_codes_kernel<T, true, 1, PADDED>), fixup_grid, kRowThreads, shm, stream(), p, target, n, C, ld, mode,
                          ignore_index, has_ignore, cptr, n_pad, cm, err, false, srows, state);
       TMX_LAUNCH_CHECK();
@@ -1464,7 +1323,8 @@ void launch_row_pass(const T* p, const int64_t* target, int64_t n, int C, int ld
 template <typename T>
 void launch_class_pass(const uint32_t* cptr, int64_t n, int C, int ld, const T* p, const int64_t* target, const int* bmode,
                        bool speculative, const int* srows, int* state, int64_t* hist, int64_t* cm, int* code_range,
-                       int* roll_mode = nullptr, int64_t* batch_hist = nullptr, int* batch_range = nullptr) {
+                       int* roll_mode = nullptr, int64_t* batch_hist = nullptr, int* batch_range = nullptr,
+                       const float4* row_stats = nullptr) {
   const int64_t n_pad = (n + kTileRows - 1) / kTileRows * kTileRows;
   // row splits only when there are too few classes to fill the chip (exclusive-owner flush when splits == 1)
   int splits = 1;
@@ -1472,7 +1332,7 @@ void launch_class_pass(const uint32_t* cptr, int64_t n, int C, int ld, const T* 
   // 16-bit-packed LDS histogram, 512-thread workgroups, four per CU (csrc/curve_hist_kernels.h class_hist_u16_kernel)
   hipLaunchKernelGGL((class_hist_u16_kernel<T>), C * splits, kClassThreadsU16, kCodes / 2 * sizeof(uint32_t), stream(),
                      reinterpret_cast<const uint16_t*>(cptr), n_pad, splits, hist, p, ld, target, n, bmode, speculative,
-                     srows, state, cm, code_range, roll_mode, batch_hist, batch_range);
+                     srows, state, cm, code_range, roll_mode, batch_hist, batch_range, row_stats);
   TMX_LAUNCH_CHECK();
 }
 
@@ -1480,15 +1340,17 @@ void launch_class_pass(const uint32_t* cptr, int64_t n, int C, int ld, const T* 
 // from the caching allocator per update it was re-allocated (hipMalloc, ~200 us of host time) on the first update after
 // a compute(), whose temporaries had split the cached block (tools/alloc_probe.py).  Work on one stream is ordered, so
 // one buffer per stream is race-free.  Under HIP-graph capture the allocator is used (the graph's private pool).
-// ``kind`` 0: int16 class-major codes, 1: int32 rare-row lists (one cache entry per (device, stream, kind)).
+// ``kind`` 0: int16 class-major codes, 1: int32 rare-row lists, 2: float per-row softmax statistics, 3-5: the
+// small-class route's int32 confusion-matrix partials, partial histograms and their ranges (one cache entry per
+// (device, stream, kind)).
 // ``capturing``: the caller's hipStreamIsCapturing verdict (one runtime query per update, not one per buffer).  The
 // returned tensor is the whole cached buffer (no narrow() view per call): callers take its data pointer.
 at::Tensor stream_scratch(const at::TensorOptions& opts, int64_t elems, int kind, bool capturing) {
-  const auto dt = kind == 0 ? at::kShort : at::kInt;
+  const auto dt = kind == 0 ? at::kShort : (kind == 2 ? at::kFloat : at::kInt);
   if (capturing) return at::empty({elems}, opts.dtype(dt));
   // At most kMaxScratch (device, stream) entries, least recently used evicted: a buffer goes back to the caching
   // allocator, which only hands it out again on the stream it was allocated on (stream-ordered, so safe).
-  constexpr size_t kMaxScratch = 8;
+  constexpr size_t kMaxScratch = 32;
   struct Entry {
     at::Tensor t;
     uint64_t used;
@@ -1524,12 +1386,15 @@ void launch_two_pass(const T* p, const int64_t* target, int64_t n, int C, int ld
   const bool capturing = stream_capturing();
   const auto codes = stream_scratch(opts, (int64_t)C * n_pad, 0, capturing);
   const auto slow_rows = stream_scratch(opts, 2 * n, 1, capturing);  // written before read (counts live in the state word)
+  // per-row softmax statistics (float4 per row, 1 MiB at 65536 rows): the class pass refits a mispredicted batch
+  const auto stats = speculative ? stream_scratch(opts, 4 * n, 2, capturing) : at::Tensor();
+  float4* rstats = speculative ? reinterpret_cast<float4*>(stats.data_ptr()) : nullptr;
   uint32_t* cptr = reinterpret_cast<uint32_t*>(codes.data_ptr());
   int* srows = slow_rows.data_ptr<int>();
   // single stream: the class pass reads the (used, real) pair straight from ``mode`` and its last workgroup rolls it
-  launch_row_pass<T, PADDED>(p, target, n, C, ld, mode, state, speculative, ignore_index, has_ignore, cm, err, cptr, srows, true);
+  launch_row_pass<T, PADDED>(p, target, n, C, ld, mode, state, speculative, ignore_index, has_ignore, cm, err, cptr, srows, true, rstats);
   launch_class_pass<T>(cptr, n, C, ld, p, target, mode, speculative, srows, state, hist, cm, code_range, speculative ? mode : nullptr,
-                       batch_hist, batch_range);
+                       batch_hist, batch_range, rstats);
 }
 
 // The row pass alone into caller-owned scratch (class-major codes + rare-row list): the per-element code pin of

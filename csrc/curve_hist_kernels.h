@@ -412,7 +412,8 @@ __device__ __forceinline__ void row_tile_load(const T* __restrict__ preds, const
 template <typename T, int NG, bool SOFTMAX, bool FIXUP, bool PADDED>
 __device__ __forceinline__ void row_tile_compute(const RowLoads<NG>& L, int64_t n, int C, int ld, int64_t ignore_index, bool has_ignore,
                                                  int64_t* __restrict__ confmat, int* __restrict__ err, bool rec, bool& saw_bad,
-                                                 SlowRows slow, uint32_t* __restrict__ s_tile, int64_t tile) {
+                                                 SlowRows slow, uint32_t* __restrict__ s_tile, int64_t tile,
+                                                 float4* __restrict__ row_stats = nullptr) {
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = threadIdx.x / kWave;
   const int nvec = ld / 8;
@@ -467,6 +468,21 @@ __device__ __forceinline__ void row_tile_compute(const RowLoads<NG>& L, int64_t 
     } else {
       fa = fa && __builtin_isfinite(wave_sum_uniform(ra.sum));
       fb = fb && __builtin_isfinite(wave_sum_uniform(rb.sum));
+      if (row_stats != nullptr) {  // the softmax statistics too, so the class pass can refit a mispredicted batch
+        f32x2 acc = {0.f, 0.f};
+        const f32x2 mx2 = {ra.mx, rb.mx};
+#pragma unroll
+        for (int j = 0; j < 8 * NG; ++j) acc = acc + exp_nonpos2(f32x2{ra.v[j], rb.v[j]} - mx2);
+        sa = wave_sum_uniform(acc.x);
+        sb = wave_sum_uniform(acc.y);
+      }
+    }
+    if (row_stats != nullptr && lane == 0) {
+      // per row: {max, exp-sum, flags (bit 0 = counted row, bit 1 = finite softmax)} for the class pass's refit
+      // of a batch whose speculated normalisation mode was wrong (class_hist_block)
+      const bool sfa = __builtin_isfinite(ra.mx) && sa == sa, sfb = __builtin_isfinite(rb.mx) && sb == sb;
+      if (r0 < n) row_stats[r0] = make_float4(ra.mx, sa, __uint_as_float((va ? 1u : 0u) | (sfa ? 2u : 0u)), 0.f);
+      if (r0 + 1 < n) row_stats[r0 + 1] = make_float4(rb.mx, sb, __uint_as_float((vb ? 1u : 0u) | (sfb ? 2u : 0u)), 0.f);
     }
     const bool slow_a = va && !fa, slow_b = vb && !fb;
     if (rec && !saw_bad) {
@@ -519,10 +535,11 @@ template <typename T, int NG, bool SOFTMAX, bool FIXUP, bool PADDED>
 __device__ __forceinline__ void row_tile(const T* __restrict__ preds, const int64_t* __restrict__ target, int64_t n, int C, int ld,
                                           int64_t ignore_index, bool has_ignore, uint32_t* __restrict__ codes, int64_t n_pad,
                                           int64_t* __restrict__ confmat, int* __restrict__ err, bool rec, bool& saw_bad,
-                                          SlowRows slow, uint32_t* __restrict__ s_tile, int64_t tile) {
+                                          SlowRows slow, uint32_t* __restrict__ s_tile, int64_t tile, float4* __restrict__ row_stats) {
   RowLoads<NG> L;
   row_tile_load<T, NG>(preds, target, n, ld, tile, L);
-  row_tile_compute<T, NG, SOFTMAX, FIXUP, PADDED>(L, n, C, ld, ignore_index, has_ignore, confmat, err, rec, saw_bad, slow, s_tile, tile);
+  row_tile_compute<T, NG, SOFTMAX, FIXUP, PADDED>(L, n, C, ld, ignore_index, has_ignore, confmat, err, rec, saw_bad, slow, s_tile, tile,
+                                                  row_stats);
   __syncthreads();
   store_tile<NG>(s_tile, codes, C, n_pad, tile);
 }
@@ -538,7 +555,7 @@ __device__ __forceinline__ void mc_codes_block(int64_t vb, int64_t vgrid, const 
                                                int64_t n, int C, int ld, int* __restrict__ mode, int64_t ignore_index, bool has_ignore,
                                                uint32_t* __restrict__ codes, int64_t n_pad, int64_t* __restrict__ confmat,
                                                int* __restrict__ err, bool record_mode, int* __restrict__ slow_rows,
-                                               int* __restrict__ slow_count) {
+                                               int* __restrict__ slow_count, float4* __restrict__ row_stats) {
   extern __shared__ __attribute__((aligned(16))) uint32_t s_tile[];  // [512 * NG][kSlots]
   int use_mode;
   if constexpr (FIXUP) {
@@ -562,9 +579,11 @@ __device__ __forceinline__ void mc_codes_block(int64_t vb, int64_t vgrid, const 
     const int64_t tile = (b % 8) * per_xcd + b / 8;
     if (tile >= ntiles) return;
     if (use_mode != 0)
-      row_tile<T, NG, true, FIXUP, PADDED>(preds, target, n, C, ld, ignore_index, has_ignore, codes, n_pad, confmat, err, rec, saw_bad, slow, s_tile, tile);
+      row_tile<T, NG, true, FIXUP, PADDED>(preds, target, n, C, ld, ignore_index, has_ignore, codes, n_pad, confmat, err, rec, saw_bad, slow, s_tile, tile,
+                                           row_stats);
     else
-      row_tile<T, NG, false, FIXUP, PADDED>(preds, target, n, C, ld, ignore_index, has_ignore, codes, n_pad, confmat, err, rec, saw_bad, slow, s_tile, tile);
+      row_tile<T, NG, false, FIXUP, PADDED>(preds, target, n, C, ld, ignore_index, has_ignore, codes, n_pad, confmat, err, rec, saw_bad, slow, s_tile, tile,
+                                            row_stats);
   };
   if constexpr (FIXUP) {  // rare: blocks stride over the tiles (small grid, cheap early exit)
     for (int64_t b = vb; b < per_xcd * 8; b += vgrid) {
@@ -588,9 +607,9 @@ __global__ void __launch_bounds__(kRowThreads, 4) mc_codes_kernel(const T* __res
                                                                     uint32_t* __restrict__ codes, int64_t n_pad,
                                                                     int64_t* __restrict__ confmat, int* __restrict__ err,
                                                                     bool record_mode, int* __restrict__ slow_rows,
-                                                                    int* __restrict__ slow_count) {
+                                                                    int* __restrict__ slow_count, float4* __restrict__ row_stats = nullptr) {
   mc_codes_block<T, FIXUP, NG, PADDED>(blockIdx.x, gridDim.x, preds, target, n, C, ld, mode, ignore_index, has_ignore, codes, n_pad,
-                                       confmat, err, record_mode, slow_rows, slow_count);
+                                       confmat, err, record_mode, slow_rows, slow_count, row_stats);
 }
 
 // Multilabel row pass: the same tile / LDS image / class-major scratch as the multiclass row pass, but every element
@@ -737,6 +756,13 @@ __device__ __forceinline__ void class_flush(uint32_t* __restrict__ s_h, int64_t*
   }
 }
 
+// 16-bit-packed LDS histogram layout: bin b lives in word (b mod 8192), low half for b < 8192, high half above.  Softmax
+// codes cluster in a few binades (bins ~14000-16256), so consecutive codes land in consecutive words -- different LDS
+// banks -- instead of sharing one word (the b >> 1 layout put every second pair of lanes on the same address, and
+// same-address atomics serialise like bank conflicts).  The trash bin 16383 stays the high half of the last word.
+__device__ __forceinline__ uint32_t u16_word(uint32_t bin) { return bin & (kCodes / 2 - 1); }
+__device__ __forceinline__ uint32_t u16_one(uint32_t bin) { return 1u << ((bin >> (kCodeBits - 1)) << 4); }
+
 // Flush of the 16-bit-packed multiclass histogram (two bins per u32 word; the trash bin is the high half of the last
 // word): negatives only (positives went straight to global), same exclusive / atomic and batch-histogram rules.
 template <int NT>
@@ -750,7 +776,7 @@ __device__ __forceinline__ void class_flush_u16(uint32_t* __restrict__ s_w, int6
       for (int h = 0; h < 2; ++h) {
         const uint32_t cnt = h ? (v >> 16) : (v & 0xFFFFu);
         if (!cnt) continue;
-        const int i = 2 * w + h;
+        const int i = w + h * (kCodes / 2);
         lo = min(lo, i);
         hi = max(hi, i);
         if (exclusive) neg_hist[i] += cnt;
@@ -808,7 +834,8 @@ __device__ __forceinline__ void class_hist_block(int64_t vb, int64_t vgrid, cons
                                                  bool speculative, const int* __restrict__ slow_rows, int* __restrict__ state,
                                                  int64_t* __restrict__ confmat, int* __restrict__ code_range, int* __restrict__ roll_mode,
                                                  uint32_t* __restrict__ partial = nullptr, int* __restrict__ prange = nullptr,
-                                                 int64_t* __restrict__ batch_hist = nullptr, int* __restrict__ batch_range = nullptr) {
+                                                 int64_t* __restrict__ batch_hist = nullptr, int* __restrict__ batch_range = nullptr,
+                                                 const float4* __restrict__ row_stats = nullptr) {
   static_assert(!(PACKED && U16), "the 16-bit-packed histogram is the multiclass form");
   // [kCodes]: neg, or neg (lo 16) | pos (hi 16) (PACKED); U16: [kCodes / 2] words holding bins 2w (lo) and 2w + 1 (hi)
   extern __shared__ __attribute__((aligned(16))) uint32_t s_h[];
@@ -836,6 +863,43 @@ __device__ __forceinline__ void class_hist_block(int64_t vb, int64_t vgrid, cons
   const int64_t per = (nv + splits - 1) / splits;
   const int64_t v0 = sp * per, v1 = v0 + per < nv ? v0 + per : nv;
   constexpr int64_t kChunkV = (PACKED || U16) ? kClassChunk / 8 : (int64_t{1} << 62);
+  // Refit (multiclass routes, no FIXUP launch): when the speculated normalisation mode of this batch was wrong
+  // (rare: the first batch of a metric, or inputs switching between logits and probabilities) the codes were written
+  // in the wrong mode, and this class's codes are rebuilt from the scores themselves with the row pass's per-row
+  // softmax statistics -- the same instruction sequence as the row pass (exp_nonpos2, div_rn2, pack_rne2), so the
+  // same bits.  A strided gather (~0.3 ms for the whole batch) instead of a FIXUP launch on every update (4.5 us).
+  const bool refit = speculative && row_stats != nullptr && s_info[0] != s_info[1];
+  if (refit) {
+    // rewrite this class's own slice of the code scratch (rows [8 v0, 8 v1) of class c belong to this workgroup
+    // alone), then count it with the normal loop below
+    const int m1 = s_info[1];
+    uint16_t* ccol = const_cast<uint16_t*>(codes) + (int64_t)c * n_pad;
+    for (int64_t r = v0 * 8 + threadIdx.x; r < v1 * 8; r += NT) {
+      uint32_t code = 0x8000u;
+      if (r < n) {
+        const float4 st = row_stats[r];
+        const uint32_t fl = __float_as_uint(st.z);
+        const T xv = preds[r * ld + c];
+        if (m1 != 0) {
+          if ((fl & 3u) == 3u) {  // counted row with a finite softmax (NaN / inf rows: every code skipped)
+            const float inv = 1.f / st.y;
+            if constexpr (PACKED) {  // small-class route: its row pass's scalar sequence (exp_nonpos, div_rn, rne_word)
+              code = raw_code<T>(rne_word<T>(div_rn(exp_nonpos(to_f32<T>(xv) - st.x), st.y, inv)) >> 16);
+            } else {  // tile route: the packed pair sequence of row_tile_compute
+              const f32x2 e = exp_nonpos2(f32x2{to_f32<T>(xv) - st.x, 0.f});
+              code = pack_rne2<T>(div_rn2(f32x2{e.x, 0.f}, f32x2{st.y, 1.f}, f32x2{inv, 1.f})) & 0xFFFFu;
+            }
+          }
+        } else if (fl & 1u) {
+          code = raw_code<T>(bits16<T>(xv));
+        }
+        if (!(code & 0x8000u) && target[r] == c) code |= 0x4000u;
+      }
+      ccol[r] = static_cast<uint16_t>(code);
+    }
+    __threadfence();  // the rewritten codes are read back by other waves of this workgroup
+    __syncthreads();
+  }
   for (int64_t cb = v0; cb < v1; cb += kChunkV) {
     const int64_t ce = cb + kChunkV < v1 ? cb + kChunkV : v1;
     for (int64_t v = cb + threadIdx.x; v < ce; v += kClassUnroll * NT) {
@@ -862,7 +926,7 @@ __device__ __forceinline__ void class_hist_block(int64_t vb, int64_t vgrid, cons
           for (int k = 0; k < 8; ++k) {
             const uint32_t x = (k & 1) ? (parts[k >> 1] >> 16) : (parts[k >> 1] & 0xFFFFu);
             const uint32_t bin = (x & 0x8000u) ? (uint32_t)kTrashBin : (x & 0x3FFFu);
-            if constexpr (U16) atomicAdd(&s_h[bin >> 1], 1u << ((bin & 1u) << 4));
+            if constexpr (U16) atomicAdd(&s_h[u16_word(bin)], u16_one(bin));
             else atomicAdd(&s_h[bin], 1u);
           }
           const uint32_t anypos = (parts[0] | parts[1] | parts[2] | parts[3]) & 0x40004000u;
@@ -871,7 +935,7 @@ __device__ __forceinline__ void class_hist_block(int64_t vb, int64_t vgrid, cons
             for (int k = 0; k < 8; ++k) {
               const uint32_t x = (k & 1) ? (parts[k >> 1] >> 16) : (parts[k >> 1] & 0xFFFFu);
               if ((x & 0xC000u) == 0x4000u) {
-                if constexpr (U16) atomicSub(&s_h[(x & 0x3FFFu) >> 1], 1u << ((x & 1u) << 4));
+                if constexpr (U16) atomicSub(&s_h[u16_word(x & 0x3FFFu)], u16_one(x & 0x3FFFu));
                 else atomicSub(&s_h[x & 0x3FFFu], 1u);
                 atomic_add_i64(pos_hist + (x & 0x3FFFu), 1);
                 if (bpos != nullptr) atomic_add_i64(bpos + (x & 0x3FFFu), 1);
@@ -998,10 +1062,10 @@ __global__ void __launch_bounds__(kClassThreadsU16) class_hist_u16_kernel(const 
                                                                          const int* __restrict__ slow_rows, int* __restrict__ state,
                                                                          int64_t* __restrict__ confmat, int* __restrict__ code_range,
                                                                          int* __restrict__ roll_mode, int64_t* __restrict__ batch_hist,
-                                                                         int* __restrict__ batch_range) {
+                                                                         int* __restrict__ batch_range, const float4* __restrict__ row_stats = nullptr) {
   class_hist_block<T, false, kClassThreadsU16, true>(blockIdx.x, gridDim.x, codes, n_pad, splits, hist, preds, ld, target, n, bmode,
                                                      speculative, slow_rows, state, confmat, code_range, roll_mode, nullptr, nullptr,
-                                                     batch_hist, batch_range);
+                                                     batch_hist, batch_range, row_stats);
 }
 
 // Small-class class pass: packed LDS histogram per (class, split), partial flush (class_store_partial).
@@ -1010,9 +1074,9 @@ __global__ void __launch_bounds__(kClassThreads) class_hist_partial_kernel(
     const uint16_t* __restrict__ codes, int64_t n_pad, int splits, int64_t* __restrict__ hist, const T* __restrict__ preds, int ld,
     const int64_t* __restrict__ target, int64_t n, const int* __restrict__ bmode, bool speculative, const int* __restrict__ slow_rows,
     int* __restrict__ state, int64_t* __restrict__ confmat, int* __restrict__ code_range, int* __restrict__ roll_mode,
-    uint32_t* __restrict__ partial, int* __restrict__ prange) {
+    uint32_t* __restrict__ partial, int* __restrict__ prange, const float4* __restrict__ row_stats = nullptr) {
   class_hist_block<T, true, kClassThreads>(blockIdx.x, gridDim.x, codes, n_pad, splits, hist, preds, ld, target, n, bmode, speculative,
-                                           slow_rows, state, confmat, code_range, roll_mode, partial, prange);
+                                           slow_rows, state, confmat, code_range, roll_mode, partial, prange, nullptr, nullptr, row_stats);
 }
 
 // Sum of the splits' partial packed words per (class, bin) into the int64 histogram: one owner thread per bin, so a
@@ -1095,6 +1159,168 @@ __global__ void mode_roll_kernel(int* __restrict__ mode, int* __restrict__ bmode
   bmode[1] = m1;
   mode[0] = m1;
   mode[1] = 0;
+}
+
+
+// ---- small-class row pass (C <= 256): see classification.hip launch_small_two_pass
+constexpr int kSmallRows = 64;
+constexpr int kSmallVpt = 16;
+constexpr int kSmallCmMax = 64;  // LDS-privatised confusion matrix up to 64 x 64 (16 KiB)
+
+template <typename T, int TL, bool FIXUP>
+__global__ void __launch_bounds__(kSmallRows * TL) mc_codes_small_kernel(
+    const T* __restrict__ preds, const int64_t* __restrict__ target, int64_t n, int C, int* __restrict__ mode, int64_t ignore_index,
+    bool has_ignore, uint16_t* __restrict__ codes, int64_t n_pad, int64_t* __restrict__ confmat, int* __restrict__ err,
+    bool record_mode, int* __restrict__ slow_rows, int* __restrict__ slow_count, uint32_t* __restrict__ pcm,
+    float4* __restrict__ row_stats = nullptr) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t s_small[];  // staging [64][C], then image [C][64]; cm [C][C]
+  int use_mode;
+  if constexpr (FIXUP) {
+    const int m0 = mode[0], m1 = mode[1];
+    if (m0 == m1) return;
+    use_mode = m1;
+  } else {
+    use_mode = mode[0];
+  }
+  // C <= 64: the confusion matrix is privatised in LDS (at C = 2 every row's atomic hit one of 4 global words)
+  uint32_t* s_cm = reinterpret_cast<uint32_t*>(s_small + kSmallRows * C);
+  const bool lds_cm = !FIXUP && confmat != nullptr && C <= kSmallCmMax;
+  if (lds_cm)
+    for (int i = threadIdx.x; i < C * C; i += kSmallRows * TL) s_cm[i] = 0u;
+  const int64_t ntiles = n_pad / kSmallRows;
+  bool bad = false;
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+  __syncthreads();  // previous tile's class segments were read from the image
+  const int64_t r0 = tile * kSmallRows;
+  const int rows = static_cast<int>(min<int64_t>(kSmallRows, n - r0));
+  // 1. stage the block's scores (byte range [r0 C, (r0 + rows) C) x 2; r0 C x 2 is a multiple of 128 B)
+  {
+    const int64_t nelem = (int64_t)rows * C;
+    const uint16_t* src = reinterpret_cast<const uint16_t*>(preds) + r0 * C;
+    const int nvec = static_cast<int>(nelem / 8);
+    for (int i = threadIdx.x; i < nvec; i += kSmallRows * TL)
+      reinterpret_cast<uint4*>(s_small)[i] = reinterpret_cast<const uint4*>(src)[i];
+    for (int i = nvec * 8 + threadIdx.x; i < nelem; i += kSmallRows * TL) s_small[i] = src[i];
+  }
+  __syncthreads();
+  const int q = threadIdx.x % TL, lr = threadIdx.x / TL;  // lane within the row, row within the block
+  const int64_t r = r0 + lr;
+  const int cb = q * kSmallVpt;
+  const bool in_rows = lr < rows;
+  float v[kSmallVpt];
+  uint16_t raw[kSmallVpt];
+#pragma unroll
+  for (int j = 0; j < kSmallVpt; ++j) {
+    const int c = cb + j;
+    const bool ok = in_rows && c < C;
+    raw[j] = ok ? s_small[lr * C + c] : (uint16_t)0;
+    v[j] = ok ? to_f32<T>(*reinterpret_cast<const T*>(&raw[j])) : -INFINITY;
+  }
+  const int64_t t = in_rows ? target[r] : -1;
+  const bool valid = in_rows && !(has_ignore && t == ignore_index);
+  // row statistics over the TL lanes of the row (xor shuffles stay inside aligned groups of TL lanes)
+  float mx = -INFINITY, mn = INFINITY, sum = 0.f;
+#pragma unroll
+  for (int j = 0; j < kSmallVpt; ++j) {
+    if (cb + j < C) {
+      mx = __builtin_fmaxf(mx, v[j]);
+      mn = __builtin_fminf(mn, v[j]);
+      sum += v[j];
+    }
+  }
+#pragma unroll
+  for (int off = 1; off < TL; off <<= 1) {
+    mx = __builtin_fmaxf(mx, __shfl_xor(mx, off, kWave));
+    mn = __builtin_fminf(mn, __shfl_xor(mn, off, kWave));
+    sum += __shfl_xor(sum, off, kWave);
+  }
+  bool fin = __builtin_isfinite(mx);
+  // arg-max of a finite row: the first class holding the maximum
+  int am = C;
+#pragma unroll
+  for (int j = kSmallVpt - 1; j >= 0; --j)
+    if (cb + j < C && v[j] == mx) am = cb + j;
+#pragma unroll
+  for (int off = 1; off < TL; off <<= 1) am = min(am, __shfl_xor(am, off, kWave));
+  float s = 0.f, inv = 0.f;
+  if (use_mode != 0) {
+    float acc = 0.f;
+#pragma unroll
+    for (int j = 0; j < kSmallVpt; ++j) {
+      v[j] = cb + j < C ? exp_nonpos(v[j] - mx) : 0.f;
+      acc += v[j];
+    }
+#pragma unroll
+    for (int off = 1; off < TL; off <<= 1) acc += __shfl_xor(acc, off, kWave);
+    s = acc;
+    inv = 1.f / s;
+    fin = fin && s == s;
+  } else {
+    fin = fin && __builtin_isfinite(sum);
+    if (row_stats != nullptr) {  // softmax statistics for the class pass's refit of a mispredicted batch
+      float acc = 0.f;
+#pragma unroll
+      for (int j = 0; j < kSmallVpt; ++j) acc += cb + j < C ? exp_nonpos(v[j] - mx) : 0.f;
+#pragma unroll
+      for (int off = 1; off < TL; off <<= 1) acc += __shfl_xor(acc, off, kWave);
+      s = acc;
+    }
+  }
+  if (row_stats != nullptr && q == 0 && in_rows && !FIXUP)
+    row_stats[r] = make_float4(mx, s, __uint_as_float((valid ? 1u : 0u) | (__builtin_isfinite(mx) && s == s ? 2u : 0u)), 0.f);
+  const bool slow = valid && !fin;
+  const bool keep = valid && fin;
+  // 3. codes into the image [C][64] (the staging area is free once every lane holds its values)
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kSmallVpt; ++j) {
+    const int c = cb + j;
+    if (!in_rows || c >= C) continue;
+    uint32_t code = 0x8000u;
+    if (keep) {
+      const uint32_t b = use_mode != 0 ? (rne_word<T>(div_rn(v[j], s, inv)) >> 16) : (uint32_t)raw[j];
+      code = raw_code<T>(b);
+      if (c == t && !(code & 0x8000u)) code |= 0x4000u;
+    }
+    s_small[c * kSmallRows + lr] = static_cast<uint16_t>(code);
+  }
+  if (lr >= rows && q == 0) {  // padding rows of the last block: skipped codes
+    for (int c = 0; c < C; ++c) s_small[c * kSmallRows + lr] = 0x8000u;
+  }
+  if (q == 0 && in_rows) {
+    if constexpr (!FIXUP) {
+      if (confmat != nullptr && keep && t >= 0 && t < C && am < C) {
+        if (lds_cm) atomicAdd(s_cm + t * C + am, 1u);
+        else atomic_add_i64(confmat + t * C + am, 1);
+      }
+      if (err != nullptr && valid && (t < 0 || t >= C)) atomicOr(err, 1);
+    }
+    if (slow) {
+      const int list = FIXUP ? 1 : 0;
+      slow_rows[list * n + atomicAdd(slow_count + list, 1)] = static_cast<int>(r);
+    }
+  }
+  if (!FIXUP && record_mode && q == 0) bad = bad || slow || (valid && (mx > 1.f || mn < 0.f));
+  __syncthreads();
+  // class segments: C rows of 64 codes = 8 x 16 B each
+  for (int i = threadIdx.x; i < C * 8; i += kSmallRows * TL) {
+    const int c = i >> 3, k = i & 7;
+    reinterpret_cast<uint4*>(codes + (int64_t)c * n_pad + r0)[k] = reinterpret_cast<const uint4*>(s_small + c * kSmallRows)[k];
+  }
+  }  // tiles
+  if (lds_cm) {  // per-block partial (summed by class_partial_reduce_kernel), else atomics on the few cells
+    __syncthreads();
+    if (pcm != nullptr)
+      for (int i = threadIdx.x; i < C * C; i += kSmallRows * TL) pcm[(int64_t)blockIdx.x * C * C + i] = s_cm[i];
+    else
+      for (int i = threadIdx.x; i < C * C; i += kSmallRows * TL)
+        if (s_cm[i]) atomic_add_i64(confmat + i, s_cm[i]);
+  }
+  if constexpr (!FIXUP) {
+    if (record_mode && __syncthreads_or(bad) && threadIdx.x == 0 &&
+        __hip_atomic_load(mode + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
+      __hip_atomic_store(mode + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 

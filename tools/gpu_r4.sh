@@ -19,6 +19,7 @@ for s in "$@"; do
     gather) run gather 60 ./build/gather_class_exp; cat "$OUT/gather.log" ;;
     pipe) run pipe 90 ./build/classpass_pipe_exp; cat "$OUT/pipe.log" ;;
     wpat) run wpat 60 ./build/write_pattern_exp; cat "$OUT/wpat.log" ;;
+    small) run small 60 ./build/small_rowpass_exp; cat "$OUT/small.log" ;;
     host) run host 120 python tools/host_overhead_probe.py ;;
     suite) run pytest_gpu 800 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread; tail -3 "$OUT/pytest_gpu.log" ;;
     smoke) run smoke 200 python -u -c "import __graft_entry__ as g; g.smoke()"; tail -1 "$OUT/smoke.log" ;;

@@ -74,6 +74,21 @@ def main() -> None:
     s = io.StringIO()
     pstats.Stats(prof, stream=s).sort_stats("tottime").print_stats(18)
     out["profile_MulticlassAUROC_C10"] = [ln for ln in s.getvalue().splitlines() if ln.strip()][:30]
+    # Python time of the headline collection's update (cProfile, own time per function)
+    coll = cases["Collection_AUROC_ConfMat_C1000"][0]().to(dev)
+    batch = cases["Collection_AUROC_ConfMat_C1000"][1]
+    for _ in range(20):
+        coll.update(*batch)
+    torch.cuda.synchronize(dev)
+    prof = cProfile.Profile()
+    prof.enable()
+    for _ in range(500):
+        coll.update(*batch)
+    prof.disable()
+    torch.cuda.synchronize(dev)
+    s = io.StringIO()
+    pstats.Stats(prof, stream=s).sort_stats("tottime").print_stats(25)
+    out["profile_Collection_C1000"] = [ln for ln in s.getvalue().splitlines() if ln.strip()][:36]
     # host time per update by op / runtime call (torch.profiler, CPU self time): the headline collection
     coll = cases["Collection_AUROC_ConfMat_C1000"][0]().to(dev)
     batch = cases["Collection_AUROC_ConfMat_C1000"][1]

@@ -20,7 +20,17 @@ import torch
 from torch import Tensor
 
 
+_ENV_DATA = getattr(os.environ, "_data", None)  # CPython's backing dict: one plain lookup, kept in sync by os.environ[...]
+_ENV_KEY = os.fsencode("TMX_VALIDATION") if _ENV_DATA is not None and any(isinstance(k, bytes) for k in list(_ENV_DATA)[:1]) else "TMX_VALIDATION"
+
+
 def validation_mode() -> str:
+    """``TMX_VALIDATION`` (read on every update: the sink choice follows runtime changes of the variable)."""
+    if _ENV_DATA is not None:
+        v = _ENV_DATA.get(_ENV_KEY)
+        if v is None:
+            return "auto"
+        return os.fsdecode(v) if isinstance(v, bytes) else v
     return os.environ.get("TMX_VALIDATION", "auto")
 
 
