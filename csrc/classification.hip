@@ -1212,10 +1212,24 @@ void launch_small_rows(int TL, int grid, const T* p, const int64_t* target, int6
     hipLaunchKernelGGL((mc_codes_small_kernel<T, TLV, FIXUP>), grid, kSmallRows * TLV, shm, stream(), p, target, n, C, mode,   \
                        ignore_index, has_ignore, codes, n_pad, cm, err, rec, srows, scount, pcm, row_stats);                      \
     break;
-  switch (TL) {
-    TMX_SMALL_CASE(1) TMX_SMALL_CASE(2) TMX_SMALL_CASE(4) TMX_SMALL_CASE(8) TMX_SMALL_CASE(16)
-    default: TORCH_CHECK(false, "mc_codes_small: unsupported lanes per row");
+#define TMX_SMALL_CC(CCV)                                                                                                      \
+  case CCV:                                                                                                                      \
+    hipLaunchKernelGGL((mc_codes_small_kernel<T, 1, FIXUP, CCV>), grid, kSmallRows, shm, stream(), p, target, n, C, mode,       \
+                       ignore_index, has_ignore, codes, n_pad, cm, err, rec, srows, scount, pcm, row_stats);                      \
+    break;
+  if (TL == 1 && C >= 2 && C <= 16) {  // compile-time class count (no masked value slots)
+    switch (C) {
+      TMX_SMALL_CC(2) TMX_SMALL_CC(3) TMX_SMALL_CC(4) TMX_SMALL_CC(5) TMX_SMALL_CC(6) TMX_SMALL_CC(7) TMX_SMALL_CC(8) TMX_SMALL_CC(9)
+      TMX_SMALL_CC(10) TMX_SMALL_CC(11) TMX_SMALL_CC(12) TMX_SMALL_CC(13) TMX_SMALL_CC(14) TMX_SMALL_CC(15) TMX_SMALL_CC(16)
+      default: break;
+    }
+  } else {
+    switch (TL) {
+      TMX_SMALL_CASE(1) TMX_SMALL_CASE(2) TMX_SMALL_CASE(4) TMX_SMALL_CASE(8) TMX_SMALL_CASE(16)
+      default: TORCH_CHECK(false, "mc_codes_small: unsupported lanes per row");
+    }
   }
+#undef TMX_SMALL_CC
 #undef TMX_SMALL_CASE
   TMX_LAUNCH_CHECK();
 }

@@ -1167,12 +1167,16 @@ constexpr int kSmallRows = 64;
 constexpr int kSmallVpt = 16;
 constexpr int kSmallCmMax = 64;  // LDS-privatised confusion matrix up to 64 x 64 (16 KiB)
 
-template <typename T, int TL, bool FIXUP>
+// CC > 0: the class count as a compile-time constant (C <= 16, one lane per row): the per-lane loops lose their
+// runtime class masks (at C = 10 the generic form ran 6 of 16 slots masked, 82 VGPRs and 69 SGPR spills).
+template <typename T, int TL, bool FIXUP, int CC = 0>
 __global__ void __launch_bounds__(kSmallRows * TL) mc_codes_small_kernel(
-    const T* __restrict__ preds, const int64_t* __restrict__ target, int64_t n, int C, int* __restrict__ mode, int64_t ignore_index,
+    const T* __restrict__ preds, const int64_t* __restrict__ target, int64_t n, int C_arg, int* __restrict__ mode, int64_t ignore_index,
     bool has_ignore, uint16_t* __restrict__ codes, int64_t n_pad, int64_t* __restrict__ confmat, int* __restrict__ err,
     bool record_mode, int* __restrict__ slow_rows, int* __restrict__ slow_count, uint32_t* __restrict__ pcm,
     float4* __restrict__ row_stats = nullptr) {
+  const int C = CC > 0 ? CC : C_arg;
+  constexpr int kVpt = CC > 0 ? CC : kSmallVpt;  // value slots per lane
   extern __shared__ __attribute__((aligned(16))) uint16_t s_small[];  // staging [64][C], then image [C][64]; cm [C][C]
   int use_mode;
   if constexpr (FIXUP) {
@@ -1205,12 +1209,12 @@ __global__ void __launch_bounds__(kSmallRows * TL) mc_codes_small_kernel(
   __syncthreads();
   const int q = threadIdx.x % TL, lr = threadIdx.x / TL;  // lane within the row, row within the block
   const int64_t r = r0 + lr;
-  const int cb = q * kSmallVpt;
+  const int cb = q * kVpt;
   const bool in_rows = lr < rows;
-  float v[kSmallVpt];
-  uint16_t raw[kSmallVpt];
+  float v[kVpt];
+  uint16_t raw[kVpt];
 #pragma unroll
-  for (int j = 0; j < kSmallVpt; ++j) {
+  for (int j = 0; j < kVpt; ++j) {
     const int c = cb + j;
     const bool ok = in_rows && c < C;
     raw[j] = ok ? s_small[lr * C + c] : (uint16_t)0;
@@ -1221,7 +1225,7 @@ __global__ void __launch_bounds__(kSmallRows * TL) mc_codes_small_kernel(
   // row statistics over the TL lanes of the row (xor shuffles stay inside aligned groups of TL lanes)
   float mx = -INFINITY, mn = INFINITY, sum = 0.f;
 #pragma unroll
-  for (int j = 0; j < kSmallVpt; ++j) {
+  for (int j = 0; j < kVpt; ++j) {
     if (cb + j < C) {
       mx = __builtin_fmaxf(mx, v[j]);
       mn = __builtin_fminf(mn, v[j]);
@@ -1238,7 +1242,7 @@ __global__ void __launch_bounds__(kSmallRows * TL) mc_codes_small_kernel(
   // arg-max of a finite row: the first class holding the maximum
   int am = C;
 #pragma unroll
-  for (int j = kSmallVpt - 1; j >= 0; --j)
+  for (int j = kVpt - 1; j >= 0; --j)
     if (cb + j < C && v[j] == mx) am = cb + j;
 #pragma unroll
   for (int off = 1; off < TL; off <<= 1) am = min(am, __shfl_xor(am, off, kWave));
@@ -1246,7 +1250,7 @@ __global__ void __launch_bounds__(kSmallRows * TL) mc_codes_small_kernel(
   if (use_mode != 0) {
     float acc = 0.f;
 #pragma unroll
-    for (int j = 0; j < kSmallVpt; ++j) {
+    for (int j = 0; j < kVpt; ++j) {
       v[j] = cb + j < C ? exp_nonpos(v[j] - mx) : 0.f;
       acc += v[j];
     }
@@ -1260,7 +1264,7 @@ __global__ void __launch_bounds__(kSmallRows * TL) mc_codes_small_kernel(
     if (row_stats != nullptr) {  // softmax statistics for the class pass's refit of a mispredicted batch
       float acc = 0.f;
 #pragma unroll
-      for (int j = 0; j < kSmallVpt; ++j) acc += cb + j < C ? exp_nonpos(v[j] - mx) : 0.f;
+      for (int j = 0; j < kVpt; ++j) acc += cb + j < C ? exp_nonpos(v[j] - mx) : 0.f;
 #pragma unroll
       for (int off = 1; off < TL; off <<= 1) acc += __shfl_xor(acc, off, kWave);
       s = acc;
@@ -1273,7 +1277,7 @@ __global__ void __launch_bounds__(kSmallRows * TL) mc_codes_small_kernel(
   // 3. codes into the image [C][64] (the staging area is free once every lane holds its values)
   __syncthreads();
 #pragma unroll
-  for (int j = 0; j < kSmallVpt; ++j) {
+  for (int j = 0; j < kVpt; ++j) {
     const int c = cb + j;
     if (!in_rows || c >= C) continue;
     uint32_t code = 0x8000u;

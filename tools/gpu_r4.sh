@@ -29,6 +29,8 @@ for s in "$@"; do
     bench50) run bench50 120 python bench.py --steps 50 --warmup 5; tail -1 "$OUT/bench50.log" ;;
     prof) run prof 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o headline --output-format csv -- python3 bench.py --steps 20 --warmup 5 ;;
     radix) run radix 300 python tools/radix_curve_bench.py; tail -1 "$OUT/radix.log" ;;
+    smallprobe) run smallprobe 240 python tools/mc_small_probe.py; tail -1 "$OUT/smallprobe.log" ;;
+    smallprof) PROBE_SMALL_ONLY=1 run smallprof 300 rocprofv3 --kernel-trace --stats -d "$OUT/smallprof" -o small --output-format csv -- python3 tools/mc_small_probe.py ;;
     radixab) for r in 1 2; do
                TMX_NATIVE_LIB=$PWD/build/ab_radix/_tmx_native.so run radix_old_$r 300 python tools/radix_curve_bench.py; tail -1 "$OUT/radix_old_$r.log"
                run radix_new_$r 300 python tools/radix_curve_bench.py; tail -1 "$OUT/radix_new_$r.log"; done ;;

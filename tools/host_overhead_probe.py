@@ -89,6 +89,19 @@ def main() -> None:
     s = io.StringIO()
     pstats.Stats(prof, stream=s).sort_stats("tottime").print_stats(25)
     out["profile_Collection_C1000"] = [ln for ln in s.getvalue().splitlines() if ln.strip()][:36]
+    # Python time of the headline collection's compute() (cProfile over 30 computes, 4 updates before each)
+    prof = cProfile.Profile()
+    for _ in range(30):
+        for _ in range(4):
+            coll.update(*batch)
+        torch.cuda.synchronize(dev)
+        prof.enable()
+        coll.compute()
+        prof.disable()
+        coll.reset()
+    s = io.StringIO()
+    pstats.Stats(prof, stream=s).sort_stats("tottime").print_stats(30)
+    out["profile_Collection_compute"] = [ln for ln in s.getvalue().splitlines() if ln.strip()][:40]
     # host time per update by op / runtime call (torch.profiler, CPU self time): the headline collection
     coll = cases["Collection_AUROC_ConfMat_C1000"][0]().to(dev)
     batch = cases["Collection_AUROC_ConfMat_C1000"][1]

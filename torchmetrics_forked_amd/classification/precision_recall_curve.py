@@ -228,10 +228,11 @@ class _CurveMetric(Metric):
                     batch=batch,
                 )
             elif self._task == "multiclass":
-                p = torch.movedim(preds, 1, -1).reshape(-1, self._num)
+                # [N, C] inputs (the common case) go through as they are: no movedim / reshape views per update
+                p = preds if preds.ndim == 2 else torch.movedim(preds, 1, -1).reshape(-1, self._num)
                 cls_ops.curve_hist_update(
-                    p, target.reshape(-1), hist, "multiclass", ii, confmat_out, err_flag, self._mode_state(p), code_range=rng,
-                    batch=batch,
+                    p, target if target.ndim == 1 else target.reshape(-1), hist, "multiclass", ii, confmat_out, err_flag,
+                    self._mode_state(p), code_range=rng, batch=batch,
                 )
             else:
                 cls_ops.curve_hist_update(preds, target, hist, "multilabel", ii, err_flag=err_flag, code_range=rng, batch=batch)

@@ -225,7 +225,9 @@ def curve_hist_update(
     if preds.dtype not in (torch.bfloat16, torch.float16):
         raise TypeError(f"curve_hist_update expects bf16/fp16 scores, got {preds.dtype}")
     tcode = 0 if task == "multiclass" else 1
-    if ops.use_native(target, preds, hist, confmat, err_flag, mode_state, code_range):
+    # device checks for the caller-supplied tensors; mode_state / code_range / err_flag are made by the metric on the
+    # inputs' device
+    if ops.use_native(target, preds, hist, confmat):
         # with a persistent ``mode_state`` (int32[8]) the multiclass kernel speculates the softmax decision and
         # records the real one in-pass (no separate range pass, ignore-aware); otherwise a pre-pass flag is used
         norm = None if (mode_state is not None and task == "multiclass") else _norm_flag(preds, target, task, ignore_index)
