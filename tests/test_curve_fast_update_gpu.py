@@ -1,0 +1,98 @@
+"""Steady-state fast path of the multiclass exact-histogram update (``MulticlassPrecisionRecallCurve._fast_hist_update``):
+after the first GPU update the next ones call the native op directly.  Results must equal the full path's (fast path
+disabled by clearing the cache before every update) through resets, forward, state_dict round trips, ignore_index,
+softmax / probability switches, and deferred target-range errors."""
+import pytest
+import torch
+
+import torchmetrics_forked_amd as tm
+from torchmetrics_forked_amd import ops
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_native(device):
+    ops.require()
+
+
+def _batches(C, n=2048, k=6, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    out = []
+    for i in range(k):
+        x = torch.randn(n, C, generator=g) * 2
+        if i in (2, 3):
+            x = x.softmax(1)  # probability batches in the middle: the speculation flips twice
+        t = torch.randint(0, C, (n,), generator=g)
+        t[::17] = -1
+        out.append((x.bfloat16().cuda(), t.cuda()))
+    return out
+
+
+def _slow(m):
+    m.__dict__["_fast_update"] = None
+
+
+@pytest.mark.parametrize("cls", [tm.MulticlassAUROC, tm.MulticlassAveragePrecision])
+@pytest.mark.parametrize("C", [10, 1000])
+def test_fast_path_matches_full_path(cls, C):
+    kw = dict(num_classes=C, ignore_index=-1)
+    fast, slow = cls(**kw).cuda(), cls(**kw).cuda()
+    for x, t in _batches(C):
+        fast.update(x, t)
+        _slow(slow)
+        slow.update(x, t)
+    assert fast.__dict__.get("_fast_update") is not None  # armed
+    torch.testing.assert_close(fast.compute(), slow.compute(), rtol=0, atol=0)
+    assert torch.equal(fast.score_hist, slow.score_hist)
+    # reset + more updates
+    fast.reset()
+    slow.reset()
+    for x, t in _batches(C, seed=1)[:3]:
+        fast.update(x, t)
+        _slow(slow)
+        slow.update(x, t)
+    torch.testing.assert_close(fast.compute(), slow.compute(), rtol=0, atol=0)
+    # forward in between (batch histogram route) then plain updates again
+    x, t = _batches(C, seed=2)[0]
+    bf, bs = fast(x, t), slow(x, t)
+    torch.testing.assert_close(bf, bs, rtol=0, atol=0)
+    x, t = _batches(C, seed=3)[1]
+    fast.update(x, t)
+    _slow(slow)
+    slow.update(x, t)
+    torch.testing.assert_close(fast.compute(), slow.compute(), rtol=0, atol=0)
+    # state_dict round trip into a fresh metric, then updates
+    fresh = cls(**kw).cuda()
+    fresh.persistent(True)
+    fast.persistent(True)
+    fresh.load_state_dict(fast.state_dict())
+    fresh.update(x, t)
+    fresh.update(x, t)
+    fast.update(x, t)
+    fast.update(x, t)
+    torch.testing.assert_close(fresh.compute(), fast.compute(), rtol=0, atol=0)
+
+
+def test_fast_path_defers_target_errors():
+    m = tm.MulticlassAUROC(num_classes=10).cuda()
+    x, t = _batches(10)[0]
+    t = t.clamp(min=0)
+    m.update(x, t)
+    m.update(x, t)  # fast path
+    bad = t.clone()
+    bad[5] = 10
+    m.update(x, bad)  # fast path: the kernel flags the out-of-range target
+    with pytest.raises(RuntimeError):
+        m.compute()
+
+
+def test_fast_path_shape_checks_still_raise():
+    m = tm.MulticlassAUROC(num_classes=10).cuda()
+    x, t = _batches(10)[0]
+    t = t.clamp(min=0)
+    m.update(x, t)
+    with pytest.raises(ValueError):
+        m.update(x[:, :9], t)  # wrong class count: full path, reference error
+    with pytest.raises(ValueError):
+        m.update(x, t.float())  # float target

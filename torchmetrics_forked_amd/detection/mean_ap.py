@@ -79,7 +79,7 @@ class MeanAveragePrecision(Metric):
     warn_on_many_detections: bool = True
 
     # host-side evaluation caches (segm IoU blocks, class-sharded flat states): not module state, invisible to script
-    __jit_ignored_attributes__: ClassVar[List[str]] = ["device", "_segm_cache", "_shard_flat"]
+    __jit_ignored_attributes__: ClassVar[List[str]] = ["device", "_fast_update", "_segm_cache", "_shard_flat"]
 
     def __init__(
         self,

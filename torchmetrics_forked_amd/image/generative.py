@@ -330,7 +330,7 @@ class LearnedPerceptualImagePatchSimilarity(Metric):
     full_state_update: bool = False
     plot_lower_bound: float = 0.0
     plot_upper_bound: float = 1.0
-    __jit_ignored_attributes__: ClassVar[List[str]] = ["net"]
+    __jit_ignored_attributes__: ClassVar[List[str]] = ["device", "_fast_update", "net"]
 
     def __init__(self, net_type: Literal["vgg", "alex", "squeeze"] = "alex", reduction: Literal["sum", "mean"] = "mean",
                  normalize: bool = False, model_path: Optional[str] = None, backbone_weights: Optional[str] = None,

@@ -106,7 +106,7 @@ class Metric(Module, ABC):
             ``TMX_SYNC_TIMEOUT`` environment variable, else unbounded as in the reference).
     """
 
-    __jit_ignored_attributes__: ClassVar[List[str]] = ["device"]
+    __jit_ignored_attributes__: ClassVar[List[str]] = ["device", "_fast_update"]
     __jit_unused_properties__: ClassVar[List[str]] = [
         "is_differentiable",
         "higher_is_better",
@@ -715,7 +715,7 @@ class Metric(Module, ABC):
 
     def __getstate__(self) -> Dict[str, Any]:
         self._join_side_work()
-        return {k: v for k, v in self.__dict__.items() if k not in ("update", "compute", "_update_signature", "_hist_spare", "_batch_bufs", "_batch_sink", "_batch_view")}
+        return {k: v for k, v in self.__dict__.items() if k not in ("update", "compute", "_update_signature", "_hist_spare", "_batch_bufs", "_batch_sink", "_batch_view", "_fast_update")}
 
     def __setstate__(self, state: Dict[str, Any]) -> None:
         self.__dict__.update(state)
