@@ -22,10 +22,10 @@ def _batch(N, C, probs, dtype, seed):
     x = torch.randn(N, C, generator=g) * 2
     if probs:
         x = x.softmax(1)
-    x[5::97, 3] = float("nan")
+    x[5::97, min(3, C - 1)] = float("nan")
     x[11::131, C // 2] = float("inf")
     x[17::211] = float("-inf")
-    x[23::53, 0] = x[23::53, 2] = 0.75 if probs else 9.0
+    x[23::53, 0] = x[23::53, min(2, C - 1)] = 0.75 if probs else 9.0
     t = torch.randint(0, C, (N,), generator=g)
     t[::19] = -1  # ignored rows
     return x.to(dtype).cuda(), t.cuda()
@@ -82,3 +82,15 @@ def test_refit_rows_beyond_one_chunk(C):
     bad = _run(x, t, speculated=0)
     assert torch.equal(good[0], bad[0]) and torch.equal(good[2], bad[2])
     assert good[0].sum().item() == N * C
+
+
+def test_small_route_error_flag_with_mode_word():
+    x, t = _batch(5000, 10, False, torch.bfloat16, seed=5)
+    t = t.clamp(min=0)
+    t[17] = 12
+    hist = torch.zeros(10, 2, K.N_CODES, dtype=torch.long, device="cuda")
+    mode = torch.zeros(8, dtype=torch.int32, device="cuda")
+    err = torch.zeros(1, dtype=torch.int32, device="cuda")
+    K.curve_hist_update(x, t, hist, "multiclass", None, None, err, mode, None)
+    torch.cuda.synchronize()
+    assert int(err) == 1
