@@ -262,14 +262,116 @@ void pearson_update(const at::Tensor& preds_in, const at::Tensor& target_in, at:
   TMX_LAUNCH_CHECK();
 }
 
+
+// Sum-state update in place (MSE / MAE / ... update: ``state += sums[chan].to(out) ; total += n``): the batch's
+// per-block partials are reduced in a fixed order (as in pearson_merge_kernel) and added into up to four state
+// tensors and the int64 sample counter by ONE small launch -- replacing the ATen partial.sum, select, dtype cast and
+// two in-place adds (five launches and their host cost per update).  Rounding follows the eager ops: the fp64 sum is
+// cast to the inputs' dtype O, then added in promote(S, O) and stored as the state dtype S.
+constexpr int kAccMax = 4;
+struct AccArgs {
+  void* state[kAccMax];
+  int32_t chan[kAccMax];
+  int32_t s_double[kAccMax];  // state dtype: 1 = float64, 0 = float32
+  int32_t count;
+};
+
+template <typename O>
+__global__ __launch_bounds__(256) void regression_accumulate_kernel(const double* __restrict__ partial, int64_t G, int D, AccArgs a,
+                                                                    int64_t* __restrict__ total, int64_t n_add) {
+  const int d = blockIdx.x;
+  __shared__ double red[kAccMax][256];
+  double v[kAccMax] = {0.0, 0.0, 0.0, 0.0};
+  for (int64_t g = threadIdx.x; g < G; g += blockDim.x)
+#pragma unroll
+    for (int i = 0; i < kAccMax; ++i)
+      if (i < a.count) v[i] += partial[(g * kRegCh + a.chan[i]) * D + d];
+#pragma unroll
+  for (int i = 0; i < kAccMax; ++i) red[i][threadIdx.x] = v[i];
+  __syncthreads();
+  for (int w = blockDim.x / 2; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w)
+#pragma unroll
+      for (int i = 0; i < kAccMax; ++i) red[i][threadIdx.x] += red[i][threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x != 0) return;
+  for (int i = 0; i < a.count; ++i) {
+    const O inc = static_cast<O>(red[i][0]);
+    if (a.s_double[i]) {
+      double* st = static_cast<double*>(a.state[i]);
+      st[d] = st[d] + static_cast<double>(inc);
+    } else {
+      float* st = static_cast<float*>(a.state[i]);
+      if constexpr (sizeof(O) == 8) st[d] = static_cast<float>(static_cast<double>(st[d]) + inc);
+      else st[d] = st[d] + inc;
+    }
+  }
+  if (d == 0 && total != nullptr) total[0] += n_add;
+}
+
+void regression_accumulate(const at::Tensor& preds_in, const at::Tensor& target_in, int64_t op, double param, c10::IntArrayRef chans,
+                           at::TensorList states, const c10::optional<at::Tensor>& total, int64_t n_add) {
+  TORCH_CHECK(preds_in.sizes() == target_in.sizes() && preds_in.dim() == 2, "regression_accumulate: expected matching [N, D] inputs");
+  TORCH_CHECK(preds_in.scalar_type() == target_in.scalar_type() &&
+                  (preds_in.scalar_type() == at::kFloat || preds_in.scalar_type() == at::kDouble),
+              "regression_accumulate: float32 / float64 inputs of one dtype");
+  TORCH_CHECK(op >= 0 && op <= kOpTweedie, "regression_accumulate: unknown op ", op);
+  TORCH_CHECK(chans.size() == states.size() && !states.empty() && states.size() <= kAccMax, "regression_accumulate: 1-4 states");
+  const int64_t N = preds_in.size(0), D64 = preds_in.size(1);
+  TORCH_CHECK(D64 >= 1 && D64 <= (1 << 20), "regression_accumulate: unsupported column count ", D64);
+  AccArgs a{};
+  a.count = static_cast<int32_t>(states.size());
+  for (size_t i = 0; i < states.size(); ++i) {
+    const at::Tensor& st = states[i];
+    TORCH_CHECK(st.is_cuda() && st.device() == preds_in.device() && st.is_contiguous() && st.numel() == D64 &&
+                    (st.scalar_type() == at::kFloat || st.scalar_type() == at::kDouble),
+                "regression_accumulate: states must be contiguous float32/float64 [D] on the inputs' device");
+    TORCH_CHECK(chans[i] >= 0 && chans[i] < kRegCh, "regression_accumulate: channel out of range");
+    a.state[i] = st.data_ptr();
+    a.chan[i] = static_cast<int32_t>(chans[i]);
+    a.s_double[i] = st.scalar_type() == at::kDouble;
+  }
+  int64_t* tot = nullptr;
+  if (total.has_value()) {
+    TORCH_CHECK(total->is_cuda() && total->device() == preds_in.device() && total->scalar_type() == at::kLong && total->numel() == 1,
+                "regression_accumulate: total must be one int64 on the inputs' device");
+    tot = total->data_ptr<int64_t>();
+  }
+  const at::DeviceGuard guard(preds_in.device());
+  if (N == 0) {  // nothing to add but the (zero) count
+    return;
+  }
+  auto preds = preds_in.contiguous();
+  auto target = target_in.contiguous();
+  const int D = static_cast<int>(D64);
+  const int tiles = (D + kWave - 1) / kWave;
+  const int W0 = std::min(kWave, D);
+  const int rows_per_block = 4 * (kWave / W0);
+  const int64_t gx = std::min<int64_t>((N + rows_per_block - 1) / rows_per_block, std::max<int64_t>(1, 2048 / tiles));
+  auto partial = at::empty({gx, kRegCh, D64}, preds.options().dtype(at::kDouble));
+  dim3 grid(static_cast<unsigned>(gx), static_cast<unsigned>(tiles));
+  TMX_DISPATCH_FLOAT(preds.scalar_type(), "regression_accumulate", [&] {
+    launch_regression_sums<scalar_t>(preds, target, N, D, static_cast<int>(op), param, partial, grid);
+  });
+  TMX_LAUNCH_CHECK();
+  if (preds.scalar_type() == at::kFloat)
+    hipLaunchKernelGGL(regression_accumulate_kernel<float>, D, 256, 0, stream(), partial.data_ptr<double>(), gx, D, a, tot, n_add);
+  else
+    hipLaunchKernelGGL(regression_accumulate_kernel<double>, D, 256, 0, stream(), partial.data_ptr<double>(), gx, D, a, tot, n_add);
+  TMX_LAUNCH_CHECK();
+}
+
 }  // namespace tmx
 
 TORCH_LIBRARY_FRAGMENT(tmx, m) {
   m.def("regression_sums(Tensor preds, Tensor target, int op, float param) -> Tensor");
   m.def("pearson_update(Tensor preds, Tensor target, Tensor(a!) mean_x, Tensor(b!) mean_y, Tensor(c!) var_x, Tensor(d!) var_y, Tensor(e!) corr_xy, Tensor(f!) n_total) -> ()");
+  m.def("regression_accumulate(Tensor preds, Tensor target, int op, float param, int[] chans, Tensor(a!)[] states, Tensor(b!)? total, int n_add) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(tmx, CUDA, m) {
   m.impl("regression_sums", &tmx::regression_sums);
   m.impl("pearson_update", &tmx::pearson_update);
+  m.impl("regression_accumulate", &tmx::regression_accumulate);
 }

@@ -6,7 +6,7 @@ native kernel is mandatory; the eager implementation below is the CPU path and t
 tests.  Callers use the fused path only when no autograd graph is needed (``fused_ok``), so differentiable
 functional calls keep exact PyTorch semantics.
 """
-from typing import Optional
+from typing import Optional, List
 
 import torch
 from torch import Tensor
@@ -68,3 +68,28 @@ def regression_sums(preds: Tensor, target: Tensor, op: int = OP_NONE, param: flo
     d = p - t
     chans = [p, t, p * p, t * t, p * t, d * d, d.abs(), _eager_op(op, p, t, param)]
     return torch.stack([c.double().sum(0) for c in chans])
+
+
+CH_SQ, CH_ABS = 5, 6  # channels of regression_sums: sum of squared / absolute differences
+
+
+def accumulate(preds: Tensor, target: Tensor, op: int, param: float, chans: List[int], states: List[Tensor], total: Optional[Tensor],
+               n_add: int) -> bool:
+    """``states[i] += sums[chans[i]]`` (cast to the inputs' dtype, as the eager update) and ``total += n_add`` in place,
+    one map-reduce launch + one tiny fold launch (csrc/regression.hip ``regression_accumulate``).  ``preds`` /
+    ``target``: ``[N]`` or ``[N, D]``.  Returns False (nothing done) when the eager path must run: CPU, autograd,
+    16-bit or mixed input dtypes, or states that are not contiguous float32 / float64 ``[D]`` on the inputs' device."""
+    if not fused_ok(preds, target) or preds.dtype != target.dtype or preds.dtype not in (torch.float32, torch.float64):
+        return False
+    if preds.ndim == 1:
+        preds, target = preds.unsqueeze(1), target.unsqueeze(1)
+    elif preds.ndim != 2:
+        return False
+    dev, D = preds.device, preds.shape[1]
+    for st in states:
+        if st.device != dev or not st.is_contiguous() or st.numel() != D or st.dtype not in (torch.float32, torch.float64):
+            return False
+    if total is not None and (total.device != dev or total.dtype != torch.long or total.numel() != 1):
+        return False
+    torch.ops.tmx.regression_accumulate(preds, target, int(op), float(param), list(chans), list(states), total, int(n_add))
+    return True
