@@ -1492,7 +1492,7 @@ template <typename T>
 __global__ void __launch_bounds__(kBinThreads) binary_hist_kernel(const T* __restrict__ preds, const int64_t* __restrict__ target,
                                                                   int64_t total, const int* __restrict__ sigmoid_flag,
                                                                   int64_t ignore_index, bool has_ignore, int64_t* __restrict__ hist,
-                                                                  int* __restrict__ err) {
+                                                                  int* __restrict__ err, int* __restrict__ code_range = nullptr) {
   extern __shared__ __attribute__((aligned(16))) uint32_t s_h[];  // [2][kCodes]: negatives, positives
   bool bad = false;
   uint4* s4 = reinterpret_cast<uint4*>(s_h);
@@ -1522,9 +1522,23 @@ __global__ void __launch_bounds__(kBinThreads) binary_hist_kernel(const T* __res
   }
   if (bad && err) atomicOr(err, 1);
   __syncthreads();
+  int lo = kCodes, hi = -1;  // occupied code range (compute() reads only [lo, hi]): tracked here, no host-side fill
   for (int i = threadIdx.x; i < 2 * kCodes; i += kBinThreads) {
     const uint32_t cnt = s_h[i];
-    if (cnt) atomic_add_i64(hist + i, cnt);
+    if (cnt) {
+      atomic_add_i64(hist + i, cnt);
+      const int b = i & (kCodes - 1);
+      lo = min(lo, b);
+      hi = max(hi, b);
+    }
+  }
+  if (code_range != nullptr) {
+    lo = wave_min_i32(lo);
+    hi = wave_max_i32(hi);
+    if ((threadIdx.x & (kWave - 1)) == 0 && hi >= 0) {
+      atomicMin(code_range, lo);
+      atomicMax(code_range + 1, hi);
+    }
   }
 }
 
@@ -1701,7 +1715,8 @@ void curve_hist_update_impl(const at::Tensor& preds_, const at::Tensor& target_,
         const int grid = static_cast<int>(std::min<int64_t>(256, (total + 8 * kBinThreads - 1) / (8 * kBinThreads)));
         hipLaunchKernelGGL(binary_hist_kernel<scalar_t>, std::max(grid, 1), kBinThreads, 2 * kCodes * sizeof(uint32_t), stream(), p,
                            target.data_ptr<int64_t>(), total, flag.data_ptr<int>(), ignore_index, has_ignore,
-                           hist.data_ptr<int64_t>(), err);
+                           hist.data_ptr<int64_t>(), err, crange);
+        range_tracked = crange != nullptr;
         return;
       }
       if (S == 1 && C % 8 == 0 && C <= 8 * 2 * kWave && aligned) {

@@ -96,3 +96,32 @@ def test_fast_path_shape_checks_still_raise():
         m.update(x[:, :9], t)  # wrong class count: full path, reference error
     with pytest.raises(ValueError):
         m.update(x, t.float())  # float target
+
+
+@pytest.mark.parametrize("cls", [tm.BinaryAUROC, tm.BinaryAveragePrecision])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_fast_path_binary_matches_full_path(cls, dtype):
+    g = torch.Generator().manual_seed(4)
+    fast, slow = cls().cuda(), cls().cuda()
+    batches = []
+    for i in range(5):
+        x = torch.randn(100_003, generator=g) * 3
+        if i == 2:
+            x = x.sigmoid()  # probability batch: the per-batch sigmoid decision flips
+        batches.append((x.to(dtype).cuda(), torch.randint(0, 2, (100_003,), generator=g).cuda()))
+    for x, t in batches:
+        fast.update(x, t)
+        _slow(slow)
+        slow.update(x, t)
+    assert fast.__dict__.get("_fast_update") is not None
+    torch.testing.assert_close(fast.compute(), slow.compute(), rtol=0, atol=0)
+    assert torch.equal(fast.score_hist, slow.score_hist)
+    # the binary kernel tracks the occupied code range itself: compute reads only that range
+    lo, hi = (int(v) for v in fast._code_range.view(-1)[:2])
+    occ = (fast.score_hist[0].sum(0) > 0).nonzero().view(-1)
+    assert lo == int(occ.min()) and hi == int(occ.max())
+    bad = batches[0][1].clone()
+    bad[7] = 3
+    fast.update(batches[0][0], bad)
+    with pytest.raises(RuntimeError):
+        fast.compute()

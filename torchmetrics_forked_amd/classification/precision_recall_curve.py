@@ -270,6 +270,59 @@ class _CurveMetric(Metric):
         self.preds.append(st[1])
         self.target.append(st[2])
 
+    # ---- steady-state GPU update: one native call ----------------------------------------------------------------
+    # After an update took the exact-histogram route on the GPU, the next ones with the same kind of inputs skip the
+    # generic plumbing (sink / route / range / mode-word lookups, ~10 us of Python) and call the native op directly.
+    # Every cached object is re-validated by identity per call (a reset, load_state_dict, .to(), sync or a forward's
+    # batch histogram replaces it and falls back to the full path, which re-arms); the host-side shape / dtype checks
+    # of the reference's validation are kept inline, the target value check stays in the kernel (deferred flag).
+    # multiclass: [N, C] scores, [N] targets; binary (no ignore_index): scores and targets of one shape.
+    def _arm_fast_update(self, preds: Tensor, target: Tensor) -> None:
+        hist = self.score_hist if self.thresholds is None else None
+        ok = (
+            isinstance(hist, Tensor) and hist.is_cuda and hist.numel() > 0 and preds.is_cuda
+            and preds.dtype in eng.HIST_DTYPES and self._range_hist is hist and self._code_range is not None
+            and self._rows_bound is not None and (not self.validate_args or self._deferred is not None)
+        )
+        if ok and self._task == "multiclass":
+            ok = preds.ndim == 2 and target.ndim == 1 and "_spec_mode" in self.__dict__
+        elif ok and self._task == "binary":
+            ok = self.ignore_index is None
+        else:
+            ok = False
+        self.__dict__["_fast_update"] = (hist, preds.dtype, preds.get_device()) if ok else None
+
+    def _fast_hist_update(self, preds: Tensor, target: Tensor) -> bool:
+        fast = self.__dict__.get("_fast_update")
+        if fast is None:
+            return False
+        hist, dtype, dev = fast
+        d = self.__dict__
+        if (
+            self.score_hist is not hist or d.get("_batch_sink") is not None or self._range_hist is not hist
+            or type(preds) is not Tensor or type(target) is not Tensor or preds.dtype is not dtype
+            or preds.get_device() != dev or target.get_device() != dev or target.is_floating_point() or self._rows_bound is None
+        ):
+            return False
+        multiclass = self._task == "multiclass"
+        if multiclass:
+            if preds.ndim != 2 or target.ndim != 1 or preds.shape[0] != target.shape[0] or preds.shape[1] != self._num:
+                return False
+        elif preds.shape != target.shape:
+            return False
+        err = None
+        if self.validate_args:
+            if validation_mode() == "eager":
+                return False
+            err = self._deferred.flag(RuntimeError, TARGET_RANGE_MSG if multiclass else BINARY_TARGET_MSG, hist.device)
+        ii = self.ignore_index
+        torch.ops.tmx.curve_hist_update(
+            preds, target, hist, 0 if multiclass else 1, -1 if ii is None else ii, ii is not None, None, None, err,
+            d["_spec_mode"] if multiclass else None, self._code_range, None, None,
+        )
+        d["_rows_bound"] = self._rows_bound + (preds.shape[0] if multiclass else preds.numel())
+        return True
+
     # ---- forward on the exact histogram (GPU) -----------------------------------------------------------------------
     # The reference's reduce-state forward parks the global state, resets, updates a fresh state, computes and merges
     # (metric.py:352-390): for a [C, 2, 16384] int64 histogram that is a 262 MB zero-filled allocation plus a dense
@@ -566,6 +619,8 @@ class BinaryPrecisionRecallCurve(_CurveMetric):
         self._init_curve_states(1, thresholds)
 
     def update(self, preds: Tensor, target: Tensor) -> None:
+        if self._fast_hist_update(preds, target):
+            return
         err = None
         if self.validate_args:
             sink = self._validation_sink(target)
@@ -573,6 +628,7 @@ class BinaryPrecisionRecallCurve(_CurveMetric):
             _binary_precision_recall_curve_tensor_validation(preds, target, self.ignore_index, sink, check_values=not in_kernel)
             err = sink.flag(RuntimeError, BINARY_TARGET_MSG, target.device) if in_kernel else None
         self._curve_update(preds, target, err_flag=err)
+        self._arm_fast_update(preds, target)
 
     def compute(self) -> Tuple[Tensor, Tensor, Tensor]:
         return precision_recall_curve_compute(self._curve_state(), "binary", 1, self.thresholds)
@@ -626,48 +682,6 @@ class MulticlassPrecisionRecallCurve(_CurveMetric):
         err = self._validate_fused(preds, target)
         self._curve_update(preds, target, err_flag=err)
         self._arm_fast_update(preds, target)
-
-    # ---- steady-state GPU update: one native call ----------------------------------------------------------------
-    # After an update took the exact-histogram route on the GPU, the next ones with the same kind of inputs skip the
-    # generic plumbing (sink / route / range / mode-word lookups, ~10 us of Python) and call the native op directly.
-    # Every cached object is re-validated by identity per call (a reset, load_state_dict, .to(), sync or a forward's
-    # batch histogram replaces it and falls back to the full path, which re-arms); the host-side shape / dtype checks
-    # of the reference's validation are kept inline, the target value check stays in the kernel (deferred flag).
-    def _arm_fast_update(self, preds: Tensor, target: Tensor) -> None:
-        hist = self.score_hist if self.thresholds is None else None
-        ok = (
-            isinstance(hist, Tensor) and hist.is_cuda and hist.numel() > 0 and preds.is_cuda and preds.ndim == 2
-            and target.ndim == 1 and preds.dtype in eng.HIST_DTYPES and self._range_hist is hist
-            and self._code_range is not None and self._rows_bound is not None and "_spec_mode" in self.__dict__
-            and (not self.validate_args or self._deferred is not None)
-        )
-        self.__dict__["_fast_update"] = (hist, preds.dtype, preds.get_device()) if ok else None
-
-    def _fast_hist_update(self, preds: Tensor, target: Tensor) -> bool:
-        fast = self.__dict__.get("_fast_update")
-        if fast is None:
-            return False
-        hist, dtype, dev = fast
-        d = self.__dict__
-        if (
-            self.score_hist is not hist or d.get("_batch_sink") is not None or self._range_hist is not hist
-            or type(preds) is not Tensor or type(target) is not Tensor or preds.dtype is not dtype or preds.ndim != 2
-            or target.ndim != 1 or preds.get_device() != dev or target.get_device() != dev or target.is_floating_point()
-            or preds.shape[0] != target.shape[0] or preds.shape[1] != self._num or self._rows_bound is None
-        ):
-            return False
-        err = None
-        if self.validate_args:
-            if validation_mode() == "eager":
-                return False
-            err = self._deferred.flag(RuntimeError, TARGET_RANGE_MSG, hist.device)
-        ii = self.ignore_index
-        torch.ops.tmx.curve_hist_update(
-            preds, target, hist, 0, -1 if ii is None else ii, ii is not None, None, None, err, d["_spec_mode"], self._code_range,
-            None, None,
-        )
-        d["_rows_bound"] = self._rows_bound + preds.shape[0]
-        return True
 
     def compute(self) -> Union[Tuple[Tensor, Tensor, Tensor], Tuple[List[Tensor], List[Tensor], List[Tensor]]]:
         return precision_recall_curve_compute(
