@@ -81,16 +81,9 @@ static int32_t flag_dtype(at::ScalarType t) {
 
 // flags: device tensors on one device (any shape); zero[i]: clear flags[i] after reading it (contiguous flags only).
 // Device int32 tensor with every flag's elements in order; one launch per 48 flags, no host synchronisation.
-at::Tensor gather_flags_device(at::TensorList flags, c10::IntArrayRef zero) {
-  TORCH_CHECK(flags.size() == zero.size(), "gather_flags: one zero entry per flag");
-  TORCH_CHECK(!flags.empty(), "gather_flags: no flags");
-  int64_t total = 0;
-  for (const at::Tensor& f : flags) total += f.numel();
+// One launch per 48 flags: every flag's elements, in order, as int32 at out (device-visible memory).
+static void launch_gather(at::TensorList flags, c10::IntArrayRef zero, int64_t total, int32_t* out) {
   const at::Device dev = flags[0].device();
-  TORCH_CHECK(dev.is_cuda(), "gather_flags: device tensors only");
-  const c10::DeviceGuard guard(dev);
-  auto out = at::empty({total}, at::TensorOptions().dtype(at::kInt).device(dev));
-  if (total == 0) return out;
   std::vector<at::Tensor> keep;  // contiguous views (a non-contiguous flag is read from a copy; it is never cleared then)
   keep.reserve(flags.size());
   int64_t off = 0;
@@ -112,9 +105,24 @@ at::Tensor gather_flags_device(at::TensorList flags, c10::IntArrayRef zero) {
       off += f.numel();
       ++i;
     }
-    hipLaunchKernelGGL(gather_flags_kernel, 1, kWave, 0, stream(), args, static_cast<int32_t>(total), out.data_ptr<int32_t>());
+    hipLaunchKernelGGL(gather_flags_kernel, 1, kWave, 0, stream(), args, static_cast<int32_t>(total), out);
     TMX_LAUNCH_CHECK();
   }
+}
+
+// flags: device tensors on one device (any shape); zero[i]: clear flags[i] after reading it (contiguous flags only).
+// Device int32 tensor with every flag's elements in order; one launch per 48 flags, no host synchronisation.
+at::Tensor gather_flags_device(at::TensorList flags, c10::IntArrayRef zero) {
+  TORCH_CHECK(flags.size() == zero.size(), "gather_flags: one zero entry per flag");
+  TORCH_CHECK(!flags.empty(), "gather_flags: no flags");
+  int64_t total = 0;
+  for (const at::Tensor& f : flags) total += f.numel();
+  const at::Device dev = flags[0].device();
+  TORCH_CHECK(dev.is_cuda(), "gather_flags: device tensors only");
+  const c10::DeviceGuard guard(dev);
+  auto out = at::empty({total}, at::TensorOptions().dtype(at::kInt).device(dev));
+  if (total == 0) return out;
+  launch_gather(flags, zero, total, out.data_ptr<int32_t>());
   return out;
 }
 
@@ -165,16 +173,26 @@ void or_flags(at::TensorList flags, const at::Tensor& src) {
   }
 }
 
-// The same gather, then one copy into pinned host memory and a stream synchronisation: a CPU int32 tensor.
+// The same gather written straight into pinned host memory (mapped into the device's address space: no separate
+// device->host copy launch), then a stream synchronisation: a CPU int32 tensor.  Falls back to a device buffer + copy
+// when the pinned block has no device mapping.
 at::Tensor gather_flags(at::TensorList flags, c10::IntArrayRef zero) {
   int64_t total = 0;
   for (const at::Tensor& f : flags) total += f.numel();
   auto host = at::empty({total}, at::TensorOptions().dtype(at::kInt).pinned_memory(true));
   if (total == 0) return host;
-  const at::Tensor out = gather_flags_device(flags, zero);
-  const c10::DeviceGuard guard(out.device());
-  TMX_CHECK_HIP(hipMemcpyAsync(host.data_ptr<int32_t>(), out.data_ptr<int32_t>(), total * sizeof(int32_t), hipMemcpyDeviceToHost,
-                               stream()));
+  TORCH_CHECK(flags.size() == zero.size(), "gather_flags: one zero entry per flag");
+  TORCH_CHECK(flags[0].is_cuda(), "gather_flags: device tensors only");
+  const c10::DeviceGuard guard(flags[0].device());
+  void* dptr = nullptr;
+  if (hipHostGetDevicePointer(&dptr, host.data_ptr(), 0) == hipSuccess && dptr != nullptr) {
+    launch_gather(flags, zero, total, static_cast<int32_t*>(dptr));
+  } else {
+    (void)hipGetLastError();  // clear the failed lookup
+    const at::Tensor out = gather_flags_device(flags, zero);
+    TMX_CHECK_HIP(hipMemcpyAsync(host.data_ptr<int32_t>(), out.data_ptr<int32_t>(), total * sizeof(int32_t), hipMemcpyDeviceToHost,
+                                 stream()));
+  }
   TMX_CHECK_HIP(hipStreamSynchronize(stream()));
   return host;
 }

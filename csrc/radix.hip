@@ -182,16 +182,16 @@ __global__ void __launch_bounds__(kRsBins) rs_scan_chunks_kernel(uint32_t* __res
 // count update as a returning LDS atomic + lane shuffle instead ran 183 vs 68 us per pass at 16.7M keys).  The tile
 // is then reordered by digit in LDS (stable) and written out in digit runs: consecutive threads store consecutive
 // addresses of a run (a direct scatter would touch up to 64 cache lines per store instruction).
-template <typename KT>
-__global__ void __launch_bounds__(kRsThreads) rs_scatter_kernel(const KT* __restrict__ kin, const uint8_t* __restrict__ pin,
-                                                                 KT* __restrict__ kout, uint8_t* __restrict__ pout, int64_t n, int T,
+template <typename KT, typename PT>
+__global__ void __launch_bounds__(kRsThreads) rs_scatter_kernel(const KT* __restrict__ kin, const PT* __restrict__ pin,
+                                                                 KT* __restrict__ kout, PT* __restrict__ pout, int64_t n, int T,
                                                                  int shift, const uint32_t* __restrict__ hist, const uint32_t* __restrict__ ctot,
                                                                  int nchunks, const uint32_t* __restrict__ base) {
   __shared__ uint32_t cnt[4][kRsBins];
   __shared__ uint32_t gbase[kRsBins];   // destination of the tile's first key of digit d (segment-relative)
   __shared__ uint32_t lstart[kRsBins];  // first tile position of digit d after the local reorder
   __shared__ KT s_key[kRsTile];
-  __shared__ uint8_t s_pay[kRsTile];
+  __shared__ PT s_pay[kRsTile];
   const int s = blockIdx.y, t = blockIdx.x;
   const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
   for (int i = threadIdx.x; i < 4 * kRsBins; i += kRsThreads) (&cnt[0][0])[i] = 0u;
@@ -202,14 +202,14 @@ __global__ void __launch_bounds__(kRsThreads) rs_scatter_kernel(const KT* __rest
   const int64_t tb = (int64_t)t * kRsTile;
   const int len = static_cast<int>(min<int64_t>(kRsTile, n - tb));
   KT key[kRsItems];
-  uint8_t pay[kRsItems];
+  PT pay[kRsItems];
   uint32_t rank[kRsItems];
 #pragma unroll
   for (int k = 0; k < kRsItems; ++k) {
     const int i = wave * (kRsTile / 4) + k * kWave + lane;
     const bool ok = i < len;
     key[k] = ok ? kin[seg0 + tb + i] : KT(0);
-    pay[k] = ok ? pin[seg0 + tb + i] : uint8_t(0);
+    pay[k] = ok ? pin[seg0 + tb + i] : PT(0);
   }
 #pragma unroll
   for (int k = 0; k < kRsItems; ++k) {
@@ -535,6 +535,34 @@ __global__ void __launch_bounds__(256) rs_final_kernel(const double* __restrict_
   out[4 * s + 3] = N;
 }
 
+// The LSD passes over [S][n] keys with payloads: per 8-bit digit, tile histograms -> two scans -> stable scatter.
+// On return ka / pa point at the sorted keys / payloads (the buffers ping-pong, one swap per pass).
+template <typename KT, typename PT>
+void rs_sort_passes(KT*& ka, KT*& kb, PT*& pa, PT*& pb, int64_t n, int S, int Tt, const at::TensorOptions& opts) {
+  const int nchunks = (Tt + kRsChunkTiles - 1) / kRsChunkTiles;
+  auto hist = at::empty({(int64_t)S * Tt * kRsBins}, opts.dtype(at::kInt));
+  auto ctot = at::empty({(int64_t)S * nchunks * kRsBins}, opts.dtype(at::kInt));
+  auto dbase = at::empty({(int64_t)S * kRsBins}, opts.dtype(at::kInt));
+  uint32_t* h = reinterpret_cast<uint32_t*>(hist.data_ptr());
+  uint32_t* ct = reinterpret_cast<uint32_t*>(ctot.data_ptr());
+  uint32_t* db = reinterpret_cast<uint32_t*>(dbase.data_ptr());
+  const int passes = static_cast<int>(sizeof(KT));
+  const dim3 tgrid(static_cast<unsigned>(Tt), static_cast<unsigned>(S));
+  for (int pss = 0; pss < passes; ++pss) {
+    hipLaunchKernelGGL(rs_hist_kernel<KT>, tgrid, kRsThreads, 0, stream(), ka, n, Tt, 8 * pss, h);
+    TMX_LAUNCH_CHECK();
+    hipLaunchKernelGGL(rs_scan_tiles_kernel, dim3(static_cast<unsigned>(nchunks), static_cast<unsigned>(S)), kRsBins, 0, stream(), h, Tt,
+                       ct, nchunks);
+    TMX_LAUNCH_CHECK();
+    hipLaunchKernelGGL(rs_scan_chunks_kernel, S, kRsBins, 0, stream(), ct, nchunks, db);
+    TMX_LAUNCH_CHECK();
+    hipLaunchKernelGGL((rs_scatter_kernel<KT, PT>), tgrid, kRsThreads, 0, stream(), ka, pa, kb, pb, n, Tt, 8 * pss, h, ct, nchunks, db);
+    TMX_LAUNCH_CHECK();
+    std::swap(ka, kb);
+    std::swap(pa, pb);
+  }
+}
+
 // --------------------------------------------------------------------------------------------------- host op
 // chunks: score tensors whose element (s, r) is at data + s * stride(0) + r * stride(1) (class-major [S, n_k] views of
 // the curve state's chunks, or row-major [n, S] via .t()); target int64 ([n] multiclass, [n, S] per-element).
@@ -563,7 +591,6 @@ std::vector<at::Tensor> curve_sorted(const std::vector<at::Tensor>& chunks, cons
   TORCH_CHECK(n < (int64_t{1} << 31), "curve_sorted: more than 2^31 - 1 samples per class");
   TORCH_CHECK(S <= 65535, "curve_sorted: more than 65535 classes / labels in one call");
   const int Tt = static_cast<int>((n + kRsTile - 1) / kRsTile);
-  const int nchunks = (Tt + kRsChunkTiles - 1) / kRsChunkTiles;
   std::vector<at::Tensor> res;
   AT_DISPATCH_FLOATING_TYPES(dt, "curve_sorted", [&] {
     using T = scalar_t;
@@ -586,27 +613,8 @@ std::vector<at::Tensor> curve_sorted(const std::vector<at::Tensor>& chunks, cons
       }
       off += nk;
     }
-    auto hist = at::empty({(int64_t)S * Tt * kRsBins}, opts.dtype(at::kInt));
-    auto ctot = at::empty({(int64_t)S * nchunks * kRsBins}, opts.dtype(at::kInt));
-    auto dbase = at::empty({(int64_t)S * kRsBins}, opts.dtype(at::kInt));
-    uint32_t* h = reinterpret_cast<uint32_t*>(hist.data_ptr());
-    uint32_t* ct = reinterpret_cast<uint32_t*>(ctot.data_ptr());
-    uint32_t* db = reinterpret_cast<uint32_t*>(dbase.data_ptr());
-    const int passes = static_cast<int>(sizeof(KT));
+    rs_sort_passes<KT, uint8_t>(ka, kb, pa, pb, n, S, Tt, opts);
     const dim3 tgrid(static_cast<unsigned>(Tt), static_cast<unsigned>(S));
-    for (int pss = 0; pss < passes; ++pss) {
-      hipLaunchKernelGGL(rs_hist_kernel<KT>, tgrid, kRsThreads, 0, stream(), ka, n, Tt, 8 * pss, h);
-      TMX_LAUNCH_CHECK();
-      hipLaunchKernelGGL(rs_scan_tiles_kernel, dim3(static_cast<unsigned>(nchunks), static_cast<unsigned>(S)), kRsBins, 0, stream(), h, Tt,
-                         ct, nchunks);
-      TMX_LAUNCH_CHECK();
-      hipLaunchKernelGGL(rs_scan_chunks_kernel, S, kRsBins, 0, stream(), ct, nchunks, db);
-      TMX_LAUNCH_CHECK();
-      hipLaunchKernelGGL(rs_scatter_kernel<KT>, tgrid, kRsThreads, 0, stream(), ka, pa, kb, pb, n, Tt, 8 * pss, h, ct, nchunks, db);
-      TMX_LAUNCH_CHECK();
-      std::swap(ka, kb);
-      std::swap(pa, pb);
-    }
     // tile sums -> scans -> fused reduce
     auto sums = at::empty({3 * (int64_t)S * Tt}, opts.dtype(at::kInt));
     auto tots = at::empty({3 * (int64_t)S}, opts.dtype(at::kInt));
@@ -652,10 +660,113 @@ std::vector<at::Tensor> curve_sorted(const std::vector<at::Tensor>& chunks, cons
   return res;
 }
 
+// ------------------------------------------------------------------------------------------- general stable sort
+// tmx::radix_sort — stable sort of every row of a [S, n] tensor (fp32 / fp64 / int32 / int64) along its last dim with
+// the same LSD passes, payload = the element's position in its row (torch.sort(x, dim=-1, stable=True) semantics:
+// NaN last ascending / first descending, -0.0 == +0.0, equal keys keep their input order in both directions).  Used
+// by the sample-sharded ranking (parallel/sample_sort.py), Spearman / Kendall ranks and the grouped retrieval order
+// instead of ATen's sort (reference ranks with torch.sort, TF/functional/regression/
+// spearman.py:23-55).  The values are gathered from the input by the sorted positions (bit-exact, NaN payloads and
+// signed zeros preserved).
+template <typename T> struct SortKey;
+template <> struct SortKey<float> {
+  using type = uint32_t;
+  __device__ static uint32_t asc(float f) {
+    if (f != f) return 0xFFFFFFFFu;  // every NaN after +inf
+    const uint32_t b = __float_as_uint(f == 0.f ? 0.f : f);
+    return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+  }
+};
+template <> struct SortKey<double> {
+  using type = uint64_t;
+  __device__ static uint64_t asc(double f) {
+    if (f != f) return ~0ull;
+    const uint64_t b = static_cast<uint64_t>(__double_as_longlong(f == 0.0 ? 0.0 : f));
+    return (b >> 63) ? ~b : (b | (1ull << 63));
+  }
+};
+template <> struct SortKey<int32_t> {
+  using type = uint32_t;
+  __device__ static uint32_t asc(int32_t v) { return static_cast<uint32_t>(v) ^ 0x80000000u; }
+};
+template <> struct SortKey<int64_t> {
+  using type = uint64_t;
+  __device__ static uint64_t asc(int64_t v) { return static_cast<uint64_t>(v) ^ (1ull << 63); }
+};
+
+template <typename T>
+__global__ void __launch_bounds__(256) sort_prep_kernel(const T* __restrict__ x, int64_t n, bool desc,
+                                                        typename SortKey<T>::type* __restrict__ keys, uint32_t* __restrict__ pos) {
+  const int64_t s0 = (int64_t)blockIdx.y * n;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const typename SortKey<T>::type k = SortKey<T>::asc(x[s0 + i]);
+    keys[s0 + i] = desc ? ~k : k;
+    pos[s0 + i] = static_cast<uint32_t>(i);
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) sort_final_kernel(const T* __restrict__ x, const uint32_t* __restrict__ pos, int64_t n,
+                                                         T* __restrict__ vals, int64_t* __restrict__ idx) {
+  const int64_t s0 = (int64_t)blockIdx.y * n;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t j = pos[s0 + i];
+    vals[s0 + i] = x[s0 + j];
+    idx[s0 + i] = j;
+  }
+}
+
+template <typename T>
+void radix_sort_impl(const at::Tensor& x, int S, int64_t n, bool desc, at::Tensor& vals, at::Tensor& idx) {
+  using KT = typename SortKey<T>::type;
+  auto opts = x.options();
+  const auto kdt = sizeof(KT) == 4 ? at::kInt : at::kLong;
+  auto k0 = at::empty({(int64_t)S * n}, opts.dtype(kdt)), k1 = at::empty({(int64_t)S * n}, opts.dtype(kdt));
+  auto p0 = at::empty({(int64_t)S * n}, opts.dtype(at::kInt)), p1 = at::empty({(int64_t)S * n}, opts.dtype(at::kInt));
+  KT* ka = reinterpret_cast<KT*>(k0.data_ptr());
+  KT* kb = reinterpret_cast<KT*>(k1.data_ptr());
+  uint32_t* pa = reinterpret_cast<uint32_t*>(p0.data_ptr());
+  uint32_t* pb = reinterpret_cast<uint32_t*>(p1.data_ptr());
+  const dim3 grid(static_cast<unsigned>(std::min<int64_t>((n + 255) / 256, std::max<int64_t>(1, 8192 / S))), static_cast<unsigned>(S));
+  hipLaunchKernelGGL(sort_prep_kernel<T>, grid, 256, 0, stream(), x.data_ptr<T>(), n, desc, ka, pa);
+  TMX_LAUNCH_CHECK();
+  const int Tt = static_cast<int>((n + kRsTile - 1) / kRsTile);
+  rs_sort_passes<KT, uint32_t>(ka, kb, pa, pb, n, S, Tt, opts);
+  hipLaunchKernelGGL(sort_final_kernel<T>, grid, 256, 0, stream(), x.data_ptr<T>(), pa, n, vals.data_ptr<T>(), idx.data_ptr<int64_t>());
+  TMX_LAUNCH_CHECK();
+}
+
+// x: [n] or [S, n] on the GPU; returns (values, int64 indices) of the same shape.
+std::vector<at::Tensor> radix_sort(const at::Tensor& x_, bool descending) {
+  TORCH_CHECK(x_.is_cuda() && (x_.dim() == 1 || x_.dim() == 2), "radix_sort: a 1-D or 2-D GPU tensor (sorted along the last dim)");
+  const at::ScalarType dt = x_.scalar_type();
+  TORCH_CHECK(dt == at::kFloat || dt == at::kDouble || dt == at::kInt || dt == at::kLong, "radix_sort: float32 / float64 / int32 / int64");
+  const c10::DeviceGuard guard(x_.device());
+  auto x = x_.contiguous();
+  const int S = x.dim() == 2 ? static_cast<int>(x.size(0)) : 1;
+  const int64_t n = x.size(-1);
+  TORCH_CHECK(n < (int64_t{1} << 31), "radix_sort: more than 2^31 - 1 elements per row");
+  TORCH_CHECK(S <= 65535, "radix_sort: more than 65535 rows in one call");
+  auto vals = at::empty_like(x);
+  auto idx = at::empty(x.sizes(), x.options().dtype(at::kLong));
+  if (n == 0 || S == 0) return {vals, idx};
+  switch (dt) {
+    case at::kFloat: radix_sort_impl<float>(x, S, n, descending, vals, idx); break;
+    case at::kDouble: radix_sort_impl<double>(x, S, n, descending, vals, idx); break;
+    case at::kInt: radix_sort_impl<int32_t>(x, S, n, descending, vals, idx); break;
+    default: radix_sort_impl<int64_t>(x, S, n, descending, vals, idx); break;
+  }
+  return {vals, idx};
+}
+
 }  // namespace tmx
 
 TORCH_LIBRARY_FRAGMENT(tmx, m) {
   m.def("curve_sorted(Tensor[] chunks, Tensor target, int task, int ignore_index, bool has_ignore, bool want_points) -> Tensor[]");
+  m.def("radix_sort(Tensor x, bool descending) -> Tensor[]");
 }
 
-TORCH_LIBRARY_IMPL(tmx, CUDA, m) { m.impl("curve_sorted", &tmx::curve_sorted); }
+TORCH_LIBRARY_IMPL(tmx, CUDA, m) {
+  m.impl("curve_sorted", &tmx::curve_sorted);
+  m.impl("radix_sort", &tmx::radix_sort);
+}

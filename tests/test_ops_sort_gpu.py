@@ -1,0 +1,76 @@
+"""``tmx::radix_sort`` (csrc/radix.hip, ops/sort.py) against ``torch.sort(..., stable=True)`` on the host: identical
+indices (stability included) and bit-identical values for fp32 / fp64 / int32 / int64, ascending and descending,
+ties, NaN, +-inf, signed zeros, 1-D and row-batched 2-D inputs, tile edges (4096 keys per tile)."""
+import pytest
+import torch
+
+from torchmetrics_forked_amd import ops
+from torchmetrics_forked_amd.ops.sort import sort
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_native(device):
+    ops.require()
+
+
+def _data(n, dtype, seed, rows=None):
+    g = torch.Generator().manual_seed(seed)
+    shape = (n,) if rows is None else (rows, n)
+    if dtype.is_floating_point:
+        x = (torch.randn(shape, generator=g, dtype=torch.float64) * 100).round() / 4  # many ties
+        x = x.to(dtype)
+        flat = x.view(-1)
+        if flat.numel() > 20:
+            flat[3::97] = float("nan")
+            flat[5::89] = float("inf")
+            flat[7::83] = float("-inf")
+            flat[11::79] = -0.0
+            flat[13::73] = 0.0
+    else:
+        x = torch.randint(-(1 << 20), 1 << 20, shape, generator=g, dtype=dtype)
+        flat = x.view(-1)
+        if flat.numel() > 20:
+            flat[::5] = 7  # long tie run
+            flat[1::101] = torch.iinfo(dtype).min
+            flat[2::103] = torch.iinfo(dtype).max
+    return x
+
+
+def _check(x, descending):
+    v, i = sort(x.cuda(), descending)
+    ref = torch.sort(x, dim=-1, descending=descending, stable=True)
+    assert i.dtype == torch.int64 and v.dtype == x.dtype
+    assert torch.equal(i.cpu(), ref.indices)
+    # bit-identical values (NaN payloads and signed zeros included)
+    bits = torch.int64 if x.element_size() == 8 else torch.int32
+    assert torch.equal(v.cpu().view(bits), ref.values.view(bits))
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64, torch.int32, torch.int64])
+@pytest.mark.parametrize("n", [0, 1, 5, 4095, 4096, 4097, 100_003])
+@pytest.mark.parametrize("descending", [False, True])
+def test_radix_sort_matches_stable_torch_sort(dtype, n, descending):
+    _check(_data(n, dtype, seed=n + 3), descending)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.int64])
+def test_radix_sort_rows(dtype):
+    _check(_data(9001, dtype, seed=1, rows=7), False)
+    _check(_data(9001, dtype, seed=2, rows=7), True)
+
+
+def test_radix_sort_large():
+    _check(_data(3_000_017, torch.float32, seed=9), False)
+
+
+def test_ranking_paths_use_native_sort():
+    """Spearman / Kendall on the GPU (native sort + rank kernels) equal their host values."""
+    from torchmetrics_forked_amd.functional.regression import kendall_rank_corrcoef, spearman_corrcoef
+
+    g = torch.Generator().manual_seed(0)
+    p = (torch.randn(20_000, generator=g) * 10).round()
+    t = p * 0.5 + (torch.randn(20_000, generator=g) * 10).round()
+    torch.testing.assert_close(spearman_corrcoef(p.cuda(), t.cuda()).cpu(), spearman_corrcoef(p, t), rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(kendall_rank_corrcoef(p.cuda(), t.cuda()).cpu(), kendall_rank_corrcoef(p, t), rtol=1e-5, atol=1e-6)

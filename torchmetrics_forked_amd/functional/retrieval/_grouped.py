@@ -17,6 +17,7 @@ import torch
 from torch import Tensor
 
 from torchmetrics_forked_amd import ops
+from torchmetrics_forked_amd.ops.sort import argsort as _argsort
 
 
 class Grouped:
@@ -32,8 +33,8 @@ class Grouped:
             _, gid = torch.unique(indexes, return_inverse=True)
             self.Q = int(gid.max()) + 1 if n else 0
         key = preds if sort_key is None else sort_key
-        o1 = torch.sort(key, descending=True, stable=True).indices
-        o2 = torch.sort(gid[o1], stable=True).indices
+        o1 = _argsort(key, descending=True)
+        o2 = _argsort(gid[o1])
         order = o1[o2]
         self.order = order
         self.gid = gid[order]

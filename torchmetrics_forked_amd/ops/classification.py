@@ -298,6 +298,15 @@ def curve_hist_reduce(hist: Tensor, code_range: Optional[Tensor] = None) -> Tens
     return torch.stack([auroc, ap, P, N], dim=1)
 
 
+def curve_hist_scores(hist: Tensor, code_range: Optional[Tensor] = None) -> Tuple[Tensor, Optional[Tensor]]:
+    """(``curve_hist_reduce`` scores ``[C, 4]``, native ``curve_summary`` buffer or None on the host) -- on the GPU one
+    launch: the reduce's last class block folds the summary."""
+    if ops.use_native(hist, code_range):
+        sc, summ = torch.ops.tmx.curve_hist_scores(hist, code_range)
+        return sc, summ
+    return curve_hist_reduce(hist, code_range), None
+
+
 def summary_f32(summary: Tensor, i: int) -> Optional[Tensor]:
     """float32 view of value ``i`` of a native ``curve_summary`` buffer (None for the 8-value host form)."""
     if summary.numel() < 12:

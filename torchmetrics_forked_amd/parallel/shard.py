@@ -22,6 +22,7 @@ import torch.distributed as dist
 from torch import Tensor
 
 from torchmetrics_forked_amd.parallel.sync import _collective, _comm_device, _world
+from torchmetrics_forked_amd.ops.sort import argsort as _argsort
 
 _DTYPES: Tuple[torch.dtype, ...] = (
     torch.float64, torch.float32, torch.float16, torch.bfloat16, torch.int64, torch.int32, torch.int16, torch.int8,
@@ -71,7 +72,7 @@ def exchange_rows(
             raise RuntimeError(f"sharded compute: ranks hold column {j} with different dtypes / shapes; cast the inputs to one dtype")
         dtypes.append(_DTYPES[codes.pop()] if codes else torch.float32)
         widths.append(wids.pop() if wids else 1)
-    order = torch.sort(owner.reshape(-1).long().to(dev), stable=True).indices if n_local else None
+    order = _argsort(owner.reshape(-1).long().to(dev)) if n_local else None
     out: List[Tensor] = []
     for j, c in enumerate(columns):
         trail: Tuple[int, ...] = tuple(c.shape[1:]) if c is not None and c.dim() > 1 else ((widths[j],) if widths[j] != 1 else ())
