@@ -176,6 +176,42 @@ __global__ void __launch_bounds__(kRsBins) rs_scan_chunks_kernel(uint32_t* __res
   base[(int64_t)s * kRsBins + d] = d ? part[d - 1] : 0u;
 }
 
+// Both scans in one launch when a segment has a single chunk (<= 64 tiles = 262,144 keys): per segment, the tile scan
+// of every digit, chunk offsets 0, and the digit prefix (two launches fewer per pass for small sorts).
+__global__ void __launch_bounds__(kRsBins) rs_scan_single_kernel(uint32_t* __restrict__ hist, int T, uint32_t* __restrict__ ctot,
+                                                                  uint32_t* __restrict__ base) {
+  __shared__ uint32_t part[kRsBins];
+  const int s = blockIdx.x, d = threadIdx.x;
+  uint32_t* h = hist + (int64_t)s * T * kRsBins + d;
+  uint32_t run = 0;
+  int t = 0;
+  for (; t + 8 <= T; t += 8) {
+    uint32_t v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = h[(int64_t)(t + k) * kRsBins];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      h[(int64_t)(t + k) * kRsBins] = run;
+      run += v[k];
+    }
+  }
+  for (; t < T; ++t) {
+    const uint32_t v = h[(int64_t)t * kRsBins];
+    h[(int64_t)t * kRsBins] = run;
+    run += v;
+  }
+  ctot[(int64_t)s * kRsBins + d] = 0u;
+  part[d] = run;
+  __syncthreads();
+  for (int off = 1; off < kRsBins; off <<= 1) {
+    const uint32_t x = d >= off ? part[d - off] : 0u;
+    __syncthreads();
+    part[d] += x;
+    __syncthreads();
+  }
+  base[(int64_t)s * kRsBins + d] = d ? part[d - 1] : 0u;
+}
+
 // ----------------------------------------------------------------------------------------------- sort: scatter
 // Wave w ranks tile keys [w * 1024, w * 1024 + 1024) in 16 rounds of 64 consecutive keys; equal-digit lanes of a
 // round are found with 8 ballots; cnt[w][d] is the wave's running count of digit d (measured: issuing every round's
@@ -537,8 +573,10 @@ __global__ void __launch_bounds__(256) rs_final_kernel(const double* __restrict_
 
 // The LSD passes over [S][n] keys with payloads: per 8-bit digit, tile histograms -> two scans -> stable scatter.
 // On return ka / pa point at the sorted keys / payloads (the buffers ping-pong, one swap per pass).
+// skip: bit p set -> digit p is the same in every key (known from the keys' AND / OR): that pass is a no-op and is not
+// launched.
 template <typename KT, typename PT>
-void rs_sort_passes(KT*& ka, KT*& kb, PT*& pa, PT*& pb, int64_t n, int S, int Tt, const at::TensorOptions& opts) {
+void rs_sort_passes(KT*& ka, KT*& kb, PT*& pa, PT*& pb, int64_t n, int S, int Tt, const at::TensorOptions& opts, uint32_t skip = 0u) {
   const int nchunks = (Tt + kRsChunkTiles - 1) / kRsChunkTiles;
   auto hist = at::empty({(int64_t)S * Tt * kRsBins}, opts.dtype(at::kInt));
   auto ctot = at::empty({(int64_t)S * nchunks * kRsBins}, opts.dtype(at::kInt));
@@ -549,13 +587,19 @@ void rs_sort_passes(KT*& ka, KT*& kb, PT*& pa, PT*& pb, int64_t n, int S, int Tt
   const int passes = static_cast<int>(sizeof(KT));
   const dim3 tgrid(static_cast<unsigned>(Tt), static_cast<unsigned>(S));
   for (int pss = 0; pss < passes; ++pss) {
+    if ((skip >> pss) & 1u) continue;
     hipLaunchKernelGGL(rs_hist_kernel<KT>, tgrid, kRsThreads, 0, stream(), ka, n, Tt, 8 * pss, h);
     TMX_LAUNCH_CHECK();
-    hipLaunchKernelGGL(rs_scan_tiles_kernel, dim3(static_cast<unsigned>(nchunks), static_cast<unsigned>(S)), kRsBins, 0, stream(), h, Tt,
-                       ct, nchunks);
-    TMX_LAUNCH_CHECK();
-    hipLaunchKernelGGL(rs_scan_chunks_kernel, S, kRsBins, 0, stream(), ct, nchunks, db);
-    TMX_LAUNCH_CHECK();
+    if (nchunks == 1) {
+      hipLaunchKernelGGL(rs_scan_single_kernel, S, kRsBins, 0, stream(), h, Tt, ct, db);
+      TMX_LAUNCH_CHECK();
+    } else {
+      hipLaunchKernelGGL(rs_scan_tiles_kernel, dim3(static_cast<unsigned>(nchunks), static_cast<unsigned>(S)), kRsBins, 0, stream(), h,
+                         Tt, ct, nchunks);
+      TMX_LAUNCH_CHECK();
+      hipLaunchKernelGGL(rs_scan_chunks_kernel, S, kRsBins, 0, stream(), ct, nchunks, db);
+      TMX_LAUNCH_CHECK();
+    }
     hipLaunchKernelGGL((rs_scatter_kernel<KT, PT>), tgrid, kRsThreads, 0, stream(), ka, pa, kb, pb, n, Tt, 8 * pss, h, ct, nchunks, db);
     TMX_LAUNCH_CHECK();
     std::swap(ka, kb);
@@ -694,24 +738,69 @@ template <> struct SortKey<int64_t> {
   __device__ static uint64_t asc(int64_t v) { return static_cast<uint64_t>(v) ^ (1ull << 63); }
 };
 
+// bits (optional): per block {AND, OR} of the keys it wrote, [gridDim.y][gridDim.x][2] -- the host skips the passes
+// of digits that are equal in every key (e.g. int64 labels in [0, 1000): 2 passes of 8).
 template <typename T>
 __global__ void __launch_bounds__(256) sort_prep_kernel(const T* __restrict__ x, int64_t n, bool desc,
-                                                        typename SortKey<T>::type* __restrict__ keys, uint32_t* __restrict__ pos) {
+                                                        typename SortKey<T>::type* __restrict__ keys, uint32_t* __restrict__ pos,
+                                                        typename SortKey<T>::type* __restrict__ bits) {
+  using KT = typename SortKey<T>::type;
   const int64_t s0 = (int64_t)blockIdx.y * n;
+  KT a = ~KT(0), o = KT(0);
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const typename SortKey<T>::type k = SortKey<T>::asc(x[s0 + i]);
-    keys[s0 + i] = desc ? ~k : k;
+    const KT k0 = SortKey<T>::asc(x[s0 + i]);
+    const KT k = desc ? ~k0 : k0;
+    keys[s0 + i] = k;
     pos[s0 + i] = static_cast<uint32_t>(i);
+    a &= k;
+    o |= k;
+  }
+  if (bits == nullptr) return;
+  __shared__ KT s_a[256 / kWave], s_o[256 / kWave];
+#pragma unroll
+  for (int off = kWave / 2; off > 0; off >>= 1) {
+    a &= __shfl_xor(a, off, kWave);
+    o |= __shfl_xor(o, off, kWave);
+  }
+  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+  if (lane == 0) { s_a[wave] = a; s_o[wave] = o; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < 256 / kWave; ++w) { a &= s_a[w]; o |= s_o[w]; }
+    const int64_t b = (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
+    bits[2 * b] = a;
+    bits[2 * b + 1] = o;
   }
 }
 
+// Values straight from the sorted keys (sequential reads; a gather x[pos] is one random cache line per element:
+// 144 us at 16.7M fp32).  Only keys that do not determine the bits -- NaN (any payload) and zero (either sign) -- read
+// the input element.
+template <typename T> struct KeyDecode {
+  using KT = typename SortKey<T>::type;
+  __device__ static bool exact(KT) { return true; }
+  __device__ static T value(KT k) { return static_cast<T>(k ^ (KT(1) << (8 * sizeof(KT) - 1))); }
+};
+template <> struct KeyDecode<float> {
+  __device__ static bool exact(uint32_t k) { return k != 0xFFFFFFFFu && k != 0x80000000u; }
+  __device__ static float value(uint32_t k) { return __uint_as_float((k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k); }
+};
+template <> struct KeyDecode<double> {
+  __device__ static bool exact(uint64_t k) { return k != ~0ull && k != (1ull << 63); }
+  __device__ static double value(uint64_t k) {
+    return __longlong_as_double(static_cast<long long>((k >> 63) ? (k & ~(1ull << 63)) : ~k));
+  }
+};
+
 template <typename T>
-__global__ void __launch_bounds__(256) sort_final_kernel(const T* __restrict__ x, const uint32_t* __restrict__ pos, int64_t n,
-                                                         T* __restrict__ vals, int64_t* __restrict__ idx) {
+__global__ void __launch_bounds__(256) sort_final_kernel(const T* __restrict__ x, const typename SortKey<T>::type* __restrict__ keys,
+                                                         const uint32_t* __restrict__ pos, int64_t n, bool desc, T* __restrict__ vals,
+                                                         int64_t* __restrict__ idx) {
   const int64_t s0 = (int64_t)blockIdx.y * n;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const uint32_t j = pos[s0 + i];
-    vals[s0 + i] = x[s0 + j];
+    const typename SortKey<T>::type k = desc ? ~keys[s0 + i] : keys[s0 + i];
+    vals[s0 + i] = KeyDecode<T>::exact(k) ? KeyDecode<T>::value(k) : x[s0 + j];
     idx[s0 + i] = j;
   }
 }
@@ -728,11 +817,31 @@ void radix_sort_impl(const at::Tensor& x, int S, int64_t n, bool desc, at::Tenso
   uint32_t* pa = reinterpret_cast<uint32_t*>(p0.data_ptr());
   uint32_t* pb = reinterpret_cast<uint32_t*>(p1.data_ptr());
   const dim3 grid(static_cast<unsigned>(std::min<int64_t>((n + 255) / 256, std::max<int64_t>(1, 8192 / S))), static_cast<unsigned>(S));
-  hipLaunchKernelGGL(sort_prep_kernel<T>, grid, 256, 0, stream(), x.data_ptr<T>(), n, desc, ka, pa);
+  // Large integer sorts read the keys' AND / OR back (one small synchronising copy) and skip constant digits (labels,
+  // ids: a few varying bytes); float keys, fewer than 2^18 keys and graph capture run every pass (measured: the probe
+  // costs ~30 us and random floats vary in every byte).
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  TMX_CHECK_HIP(hipStreamIsCapturing(stream(), &cap));
+  const bool probe = std::is_integral<T>::value && (int64_t)S * n >= (int64_t{1} << 18) && cap == hipStreamCaptureStatusNone;
+  at::Tensor bits;
+  if (probe) bits = at::empty({(int64_t)grid.x * grid.y * 2}, opts.dtype(kdt));
+  hipLaunchKernelGGL(sort_prep_kernel<T>, grid, 256, 0, stream(), x.data_ptr<T>(), n, desc, ka, pa,
+                     probe ? reinterpret_cast<KT*>(bits.data_ptr()) : static_cast<KT*>(nullptr));
   TMX_LAUNCH_CHECK();
+  uint32_t skip = 0u;
+  if (probe) {
+    const at::Tensor hb = bits.cpu();
+    const KT* hv = reinterpret_cast<const KT*>(hb.data_ptr());
+    KT a = ~KT(0), o = KT(0);
+    for (int64_t i = 0; i < hb.numel(); i += 2) { a &= hv[i]; o |= hv[i + 1]; }
+    const KT varying = a ^ o;
+    for (int p = 0; p < static_cast<int>(sizeof(KT)); ++p)
+      if (((varying >> (8 * p)) & KT(0xFF)) == KT(0)) skip |= 1u << p;
+  }
   const int Tt = static_cast<int>((n + kRsTile - 1) / kRsTile);
-  rs_sort_passes<KT, uint32_t>(ka, kb, pa, pb, n, S, Tt, opts);
-  hipLaunchKernelGGL(sort_final_kernel<T>, grid, 256, 0, stream(), x.data_ptr<T>(), pa, n, vals.data_ptr<T>(), idx.data_ptr<int64_t>());
+  rs_sort_passes<KT, uint32_t>(ka, kb, pa, pb, n, S, Tt, opts, skip);
+  hipLaunchKernelGGL(sort_final_kernel<T>, grid, 256, 0, stream(), x.data_ptr<T>(), ka, pa, n, desc, vals.data_ptr<T>(),
+                     idx.data_ptr<int64_t>());
   TMX_LAUNCH_CHECK();
 }
 

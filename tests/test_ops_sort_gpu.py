@@ -74,3 +74,16 @@ def test_ranking_paths_use_native_sort():
     t = p * 0.5 + (torch.randn(20_000, generator=g) * 10).round()
     torch.testing.assert_close(spearman_corrcoef(p.cuda(), t.cuda()).cpu(), spearman_corrcoef(p, t), rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(kendall_rank_corrcoef(p.cuda(), t.cuda()).cpu(), kendall_rank_corrcoef(p, t), rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("descending", [False, True])
+def test_radix_sort_constant_digit_passes_skipped(descending):
+    """>= 2^18 keys: digits equal in every key are not sorted on (labels in a small range, constants, rows)."""
+    g = torch.Generator().manual_seed(5)
+    _check(torch.randint(0, 1000, (300_001,), generator=g), descending)  # 2 of 8 int64 digits vary
+    _check(torch.randint(-3, 3, (300_001,), generator=g, dtype=torch.int32), descending)  # sign flips every byte
+    _check(torch.full((270_000,), 7, dtype=torch.int64), descending)  # every pass skipped: identity order
+    _check(torch.full((270_000,), 0.5, dtype=torch.float32), descending)
+    _check(torch.randint(0, 300, (4, 70_001), generator=g), descending)
+    x = torch.rand(400_000, generator=g) * 0.25 + 0.5  # one exponent (float keys: every pass runs)
+    _check(x, descending)

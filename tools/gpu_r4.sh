@@ -21,6 +21,8 @@ for s in "$@"; do
     wpat) run wpat 60 ./build/write_pattern_exp; cat "$OUT/wpat.log" ;;
     small) run small 60 ./build/small_rowpass_exp; cat "$OUT/small.log" ;;
     host) run host 120 python tools/host_overhead_probe.py ;;
+    sort) run sort 180 python tools/sort_bench.py; tail -1 "$OUT/sort.log" ;;
+    sortprof) run sortprof 300 rocprofv3 --kernel-trace --stats -d "$OUT/sortprof" -o sort --output-format csv -- python3 tools/sort_bench.py ;;
     suite) run pytest_gpu 800 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread; tail -3 "$OUT/pytest_gpu.log" ;;
     smoke) run smoke 200 python -u -c "import __graft_entry__ as g; g.smoke()"; tail -1 "$OUT/smoke.log" ;;
     fwd) run forward_bench 120 python tools/forward_bench.py; tail -1 "$OUT/forward_bench.log" ;;
