@@ -760,6 +760,9 @@ __device__ __forceinline__ void class_flush(uint32_t* __restrict__ s_h, int64_t*
 // codes cluster in a few binades (bins ~14000-16256), so consecutive codes land in consecutive words -- different LDS
 // banks -- instead of sharing one word (the b >> 1 layout put every second pair of lanes on the same address, and
 // same-address atomics serialise like bank conflicts).  The trash bin 16383 stays the high half of the last word.
+#ifndef TMX_FLUSH_RMW
+#define TMX_FLUSH_RMW 0
+#endif
 __device__ __forceinline__ uint32_t u16_word(uint32_t bin) { return bin & (kCodes / 2 - 1); }
 __device__ __forceinline__ uint32_t u16_one(uint32_t bin) { return 1u << ((bin >> (kCodeBits - 1)) << 4); }
 
@@ -779,8 +782,14 @@ __device__ __forceinline__ void class_flush_u16(uint32_t* __restrict__ s_w, int6
         const int i = w + h * (kCodes / 2);
         lo = min(lo, i);
         hi = max(hi, i);
+#if TMX_FLUSH_RMW
         if (exclusive) neg_hist[i] += cnt;
         else atomic_add_i64(neg_hist + i, cnt);
+#else
+        // a non-returning atomic even when this block owns the class: the plain += waited on a global load per bin
+        (void)exclusive;
+        atomic_add_i64(neg_hist + i, cnt);
+#endif
         if (bneg != nullptr) {
           if (bstore) bneg[i] = cnt;
           else atomic_add_i64(bneg + i, cnt);

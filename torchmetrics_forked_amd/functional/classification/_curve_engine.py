@@ -24,6 +24,7 @@ from torch import Tensor
 
 from torchmetrics_forked_amd import ops
 from torchmetrics_forked_amd.ops import classification as cls_ops
+from torchmetrics_forked_amd.ops.sort import argsort as _argsort, sort as _sort
 
 N_CODES = cls_ops.N_CODES
 HIST_DTYPES = (torch.bfloat16, torch.float16)
@@ -222,7 +223,7 @@ def anchored_scores(
     if max_pos > cls_ops.ANCHOR_MAX_POS:
         return None
     if pos_rows is None:
-        pos_rows = torch.sort(t, stable=True)[1] if task == "multiclass" else lab.nonzero(as_tuple=True)[1]
+        pos_rows = _argsort(t) if task == "multiclass" else lab.nonzero(as_tuple=True)[1]
     pos_off = torch.zeros(C + 1, dtype=torch.long, device=sample.device)
     pos_off[1:] = counts.cumsum(0)
     if cols is None:
@@ -253,8 +254,7 @@ def hist_curve_points(hist: Tensor, dtype: torch.dtype) -> List[Tuple[Tensor, Te
 def samples_curve_points(preds: Tensor, labels: Tensor) -> Tuple[Tensor, Tensor, Tensor]:
     """(fps, tps, thresholds) for a single 1-D problem (reference ``_binary_clf_curve`` semantics)."""
     with torch.no_grad():
-        order = torch.argsort(preds, descending=True)
-        sp = preds[order]
+        sp, order = _sort(preds, descending=True) if preds.dim() == 1 else torch.sort(preds, descending=True)
         sl = labels[order].to(torch.long)
         distinct = torch.where(sp[1:] - sp[:-1])[0]
         thr_idx = torch.nn.functional.pad(distinct, [0, 1], value=sl.size(0) - 1)
@@ -270,7 +270,7 @@ def samples_curve_points_columns(preds: Tensor, labels: Tensor) -> List[Tuple[Te
     does not matter; one host read sizes the per-class outputs."""
     with torch.no_grad():
         cols = preds.t().contiguous()
-        sv, order = torch.sort(cols, dim=1, descending=True)
+        sv, order = _sort(cols, descending=True)
         sl = torch.gather(labels.t().to(torch.float32), 1, order)
         tps = torch.cumsum(sl, dim=1)
         n = cols.shape[1]
