@@ -721,6 +721,10 @@ constexpr int kClassThreads = 1024;
 constexpr int kClassUnroll = TMX_CLASS_UNROLL;
 constexpr int kTrashBin = kCodes - 1;  // no valid 16-bit score in [0, 1] maps here (bf16 <= 0x3F80, fp16 <= 0x3C00)
 constexpr int64_t kClassChunk = 65528;  // rows per LDS flush: a 16-bit half never overflows (multiple of 8)
+// The u16 multiclass pass (split-half layout) counts whole 65536-row chunks: a half can only wrap when all 65536 codes
+// of a chunk are one negative code, which the chunk's all-equal test catches and books directly (a 65528-row chunk
+// left an 8-row tail and a second flush per class at the headline's 65536 rows: 41 -> 36 us).
+constexpr int64_t kClassChunkU16 = 65536;
 
 // ``bneg`` / ``bpos`` (optional): the batch histogram of a forward() call, flushed beside the accumulated one (its bins
 // are zero before the batch): a plain store when ``bstore`` (the block's only writer of those bins so far), else atomics.
@@ -871,7 +875,7 @@ __device__ __forceinline__ void class_hist_block(int64_t vb, int64_t vgrid, cons
   const int64_t nv = n_pad / 8;
   const int64_t per = (nv + splits - 1) / splits;
   const int64_t v0 = sp * per, v1 = v0 + per < nv ? v0 + per : nv;
-  constexpr int64_t kChunkV = (PACKED || U16) ? kClassChunk / 8 : (int64_t{1} << 62);
+  constexpr int64_t kChunkV = U16 ? kClassChunkU16 / 8 : (PACKED ? kClassChunk / 8 : (int64_t{1} << 62));
   // Refit (multiclass routes, no FIXUP launch): when the speculated normalisation mode of this batch was wrong
   // (rare: the first batch of a metric, or inputs switching between logits and probabilities) the codes were written
   // in the wrong mode, and this class's codes are rebuilt from the scores themselves with the row pass's per-row
@@ -911,11 +915,24 @@ __device__ __forceinline__ void class_hist_block(int64_t vb, int64_t vgrid, cons
   }
   for (int64_t cb = v0; cb < v1; cb += kChunkV) {
     const int64_t ce = cb + kChunkV < v1 ? cb + kChunkV : v1;
+    // U16, full 65536-row chunk: OR of every code's difference from the chunk's first code (all equal -> a half may
+    // have wrapped, fixed below); a partial chunk cannot reach 65536 in one bin
+    static_assert(!U16 || (kClassChunkU16 / 8) % (kClassUnroll * NT) == 0, "a full u16 chunk has no padding vectors");
+    const bool full = U16 && ce - cb == kChunkV;
+    uint32_t ref2 = 0u, diff = 0u;
+    if (full) {
+      const uint32_t r0 = col[cb].x & 0xFFFFu;
+      ref2 = r0 | (r0 << 16);
+    }
     for (int64_t v = cb + threadIdx.x; v < ce; v += kClassUnroll * NT) {
       uint4 w[kClassUnroll];
 #pragma unroll
       for (int u = 0; u < kClassUnroll; ++u)
         w[u] = (v + u * NT < ce) ? col[v + u * NT] : make_uint4(0x80008000u, 0x80008000u, 0x80008000u, 0x80008000u);
+      if (full) {
+#pragma unroll
+        for (int u = 0; u < kClassUnroll; ++u) diff |= ((w[u].x ^ ref2) | (w[u].y ^ ref2)) | ((w[u].z ^ ref2) | (w[u].w ^ ref2));
+      }
 #pragma unroll
       for (int u = 0; u < kClassUnroll; ++u) {
         const uint32_t parts[4] = {w[u].x, w[u].y, w[u].z, w[u].w};
@@ -953,6 +970,22 @@ __device__ __forceinline__ void class_hist_block(int64_t vb, int64_t vgrid, cons
               }
             }
           }
+        }
+      }
+    }
+    if constexpr (U16) {
+      if (full && !__syncthreads_or(diff != 0u)) {
+        // every code of the chunk is ref2's: a negative code's count 65536 wrapped its 16-bit half (low half: carried
+        // 1 into the high half; high half: carried out) -- undo it in LDS and book the count directly.  Positives
+        // (added then subtracted) and the trash bin are exact modulo 2^32.
+        const uint32_t x = ref2 & 0xFFFFu;
+        if (threadIdx.x == 0 && (x & 0xC000u) == 0u) {
+          const uint32_t bin = x & 0x3FFFu;
+          if (!(bin >> (kCodeBits - 1))) s_h[u16_word(bin)] -= 0x10000u;
+          atomic_add_i64(neg_hist + bin, kChunkV * 8);
+          if (bneg != nullptr) atomic_add_i64(bneg + bin, kChunkV * 8);
+          lo = min(lo, (int)bin);
+          hi = max(hi, (int)bin);
         }
       }
     }

@@ -94,3 +94,29 @@ def test_small_route_error_flag_with_mode_word():
     K.curve_hist_update(x, t, hist, "multiclass", None, None, err, mode, None)
     torch.cuda.synchronize()
     assert int(err) == 1
+
+
+@pytest.mark.parametrize("N", [65536, 65544, 131072])
+def test_u16_full_chunk_single_code_columns(N):
+    """Tile route, whole 65536-row chunks: a class whose every code is one negative value would wrap its 16-bit LDS
+    half (low-half and high-half bins), an all-positive identical column is exact modulo 2^32 -- the histogram must
+    equal the host bincount in every case."""
+    C = 520
+    g = torch.Generator().manual_seed(N)
+    x = torch.rand(N, C, generator=g) * 0.9 + 0.05  # probabilities: raw-score codes (bf16 bits)
+    x[:, 3] = 1e-20  # code < 8192: low half of its LDS word
+    x[:, 5] = 0.25  # code >= 8192: high half
+    x[:, 7] = 0.125
+    t = torch.full((N,), 7, dtype=torch.long)  # every row positive for class 7, negative for 3 and 5
+    t[N // 2 :: 3] = torch.randint(8, C, (len(range(N // 2, N, 3)),), generator=g)
+    xb = x.bfloat16()
+    hist, _, _, mode = _run(xb.cuda(), t.cuda(), speculated=0)
+    assert int(mode[0]) == 0
+    codes = xb.view(torch.int16).long() & 0xFFFF
+    for c in (3, 5, 7, 8, 519):
+        pos = t == c
+        ref_neg = torch.bincount(codes[~pos, c], minlength=K.N_CODES)
+        ref_pos = torch.bincount(codes[pos, c], minlength=K.N_CODES)
+        assert torch.equal(hist[c, 0].cpu(), ref_neg), c
+        assert torch.equal(hist[c, 1].cpu(), ref_pos), c
+    assert int(hist.sum()) == N * C
