@@ -213,40 +213,13 @@ __global__ void __launch_bounds__(kRsBins) rs_scan_single_kernel(uint32_t* __res
 }
 
 // ----------------------------------------------------------------------------------------------- sort: scatter
-// Wave w ranks tile keys [w * 1024, w * 1024 + 1024) in 16 rounds of 64 consecutive keys; equal-digit lanes of a
-// round are found with 8 ballots; cnt[w][d] is the wave's running count of digit d (measured: issuing every round's
-// count update as a returning LDS atomic + lane shuffle instead ran 183 vs 68 us per pass at 16.7M keys).  The tile
-// is then reordered by digit in LDS (stable) and written out in digit runs: consecutive threads store consecutive
-// addresses of a run (a direct scatter would touch up to 64 cache lines per store instruction).
-template <typename KT, typename PT>
-__global__ void __launch_bounds__(kRsThreads) rs_scatter_kernel(const KT* __restrict__ kin, const PT* __restrict__ pin,
-                                                                 KT* __restrict__ kout, PT* __restrict__ pout, int64_t n, int T,
-                                                                 int shift, const uint32_t* __restrict__ hist, const uint32_t* __restrict__ ctot,
-                                                                 int nchunks, const uint32_t* __restrict__ base) {
-  __shared__ uint32_t cnt[4][kRsBins];
-  __shared__ uint32_t gbase[kRsBins];   // destination of the tile's first key of digit d (segment-relative)
-  __shared__ uint32_t lstart[kRsBins];  // first tile position of digit d after the local reorder
-  __shared__ KT s_key[kRsTile];
-  __shared__ PT s_pay[kRsTile];
-  const int s = blockIdx.y, t = blockIdx.x;
+// Stable in-tile ranking of one digit: key k of wave w, round r is tile element w * 1024 + r * 64 + lane (elements
+// >= len take no part: rank 0xFFFFFFFF).  On return, rank[k] + cnt[w][d] + lstart[d] is the element's position in the
+// tile reordered stably by digit d (cnt: per-wave exclusive prefix of each digit; lstart: exclusive prefix over digits).
+template <typename KT>
+__device__ __forceinline__ void rs_rank_tile(const KT (&key)[kRsItems], int len, int shift, uint32_t (*cnt)[kRsBins], uint32_t* lstart,
+                                             uint32_t (&rank)[kRsItems]) {
   const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
-  for (int i = threadIdx.x; i < 4 * kRsBins; i += kRsThreads) (&cnt[0][0])[i] = 0u;
-  gbase[threadIdx.x] = base[(int64_t)s * kRsBins + threadIdx.x] + ctot[((int64_t)s * nchunks + t / kRsChunkTiles) * kRsBins + threadIdx.x] +
-                       hist[((int64_t)s * T + t) * kRsBins + threadIdx.x];
-  __syncthreads();
-  const int64_t seg0 = (int64_t)s * n;
-  const int64_t tb = (int64_t)t * kRsTile;
-  const int len = static_cast<int>(min<int64_t>(kRsTile, n - tb));
-  KT key[kRsItems];
-  PT pay[kRsItems];
-  uint32_t rank[kRsItems];
-#pragma unroll
-  for (int k = 0; k < kRsItems; ++k) {
-    const int i = wave * (kRsTile / 4) + k * kWave + lane;
-    const bool ok = i < len;
-    key[k] = ok ? kin[seg0 + tb + i] : KT(0);
-    pay[k] = ok ? pin[seg0 + tb + i] : PT(0);
-  }
 #pragma unroll
   for (int k = 0; k < kRsItems; ++k) {
     const int i = wave * (kRsTile / 4) + k * kWave + lane;
@@ -287,6 +260,43 @@ __global__ void __launch_bounds__(kRsThreads) rs_scatter_kernel(const KT* __rest
   __syncthreads();
   lstart[threadIdx.x] = my_excl;
   __syncthreads();
+}
+
+// Wave w ranks tile keys [w * 1024, w * 1024 + 1024) in 16 rounds of 64 consecutive keys; equal-digit lanes of a
+// round are found with 8 ballots; cnt[w][d] is the wave's running count of digit d (measured: issuing every round's
+// count update as a returning LDS atomic + lane shuffle instead ran 183 vs 68 us per pass at 16.7M keys).  The tile
+// is then reordered by digit in LDS (stable) and written out in digit runs: consecutive threads store consecutive
+// addresses of a run (a direct scatter would touch up to 64 cache lines per store instruction).
+template <typename KT, typename PT>
+__global__ void __launch_bounds__(kRsThreads) rs_scatter_kernel(const KT* __restrict__ kin, const PT* __restrict__ pin,
+                                                                 KT* __restrict__ kout, PT* __restrict__ pout, int64_t n, int T,
+                                                                 int shift, const uint32_t* __restrict__ hist, const uint32_t* __restrict__ ctot,
+                                                                 int nchunks, const uint32_t* __restrict__ base) {
+  __shared__ uint32_t cnt[4][kRsBins];
+  __shared__ uint32_t gbase[kRsBins];   // destination of the tile's first key of digit d (segment-relative)
+  __shared__ uint32_t lstart[kRsBins];  // first tile position of digit d after the local reorder
+  __shared__ KT s_key[kRsTile];
+  __shared__ PT s_pay[kRsTile];
+  const int s = blockIdx.y, t = blockIdx.x;
+  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+  for (int i = threadIdx.x; i < 4 * kRsBins; i += kRsThreads) (&cnt[0][0])[i] = 0u;
+  gbase[threadIdx.x] = base[(int64_t)s * kRsBins + threadIdx.x] + ctot[((int64_t)s * nchunks + t / kRsChunkTiles) * kRsBins + threadIdx.x] +
+                       hist[((int64_t)s * T + t) * kRsBins + threadIdx.x];
+  __syncthreads();
+  const int64_t seg0 = (int64_t)s * n;
+  const int64_t tb = (int64_t)t * kRsTile;
+  const int len = static_cast<int>(min<int64_t>(kRsTile, n - tb));
+  KT key[kRsItems];
+  PT pay[kRsItems];
+  uint32_t rank[kRsItems];
+#pragma unroll
+  for (int k = 0; k < kRsItems; ++k) {
+    const int i = wave * (kRsTile / 4) + k * kWave + lane;
+    const bool ok = i < len;
+    key[k] = ok ? kin[seg0 + tb + i] : KT(0);
+    pay[k] = ok ? pin[seg0 + tb + i] : PT(0);
+  }
+  rs_rank_tile<KT>(key, len, shift, cnt, lstart, rank);
 #pragma unroll
   for (int k = 0; k < kRsItems; ++k) {
     if (rank[k] == 0xFFFFFFFFu) continue;
@@ -710,8 +720,8 @@ std::vector<at::Tensor> curve_sorted(const std::vector<at::Tensor>& chunks, cons
 // NaN last ascending / first descending, -0.0 == +0.0, equal keys keep their input order in both directions).  Used
 // by the sample-sharded ranking (parallel/sample_sort.py), Spearman / Kendall ranks and the grouped retrieval order
 // instead of ATen's sort (reference ranks with torch.sort, TF/functional/regression/
-// spearman.py:23-55).  The values are gathered from the input by the sorted positions (bit-exact, NaN payloads and
-// signed zeros preserved).
+// spearman.py:23-55).  The values are decoded from the sorted keys (bit-exact: NaN and zero keys read the input
+// element, so NaN payloads and signed zeros are preserved).
 template <typename T> struct SortKey;
 template <> struct SortKey<float> {
   using type = uint32_t;
@@ -805,9 +815,87 @@ __global__ void __launch_bounds__(256) sort_final_kernel(const T* __restrict__ x
   }
 }
 
+// Rows of at most one tile (n <= 4096): the whole sort of a row in one workgroup -- key prep, every pass ranked in
+// registers (rs_rank_tile) and reordered through LDS, digits equal in every key of the row skipped (block AND / OR),
+// values decoded at the end.  One launch instead of prep + final + 4 per pass.
+template <typename T>
+__global__ void __launch_bounds__(kRsThreads) sort_tile_kernel(const T* __restrict__ x, int64_t n, bool desc, T* __restrict__ vals,
+                                                               int64_t* __restrict__ idx) {
+  using KT = typename SortKey<T>::type;
+  __shared__ uint32_t cnt[4][kRsBins];
+  __shared__ uint32_t lstart[kRsBins];
+  __shared__ KT s_key[kRsTile];
+  __shared__ uint32_t s_pos[kRsTile];
+  __shared__ KT s_and[kRsThreads / kWave], s_or[kRsThreads / kWave];
+  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+  const int64_t s0 = (int64_t)blockIdx.x * n;
+  const int len = static_cast<int>(n);
+  KT key[kRsItems];
+  uint32_t pos[kRsItems], rank[kRsItems];
+  KT a = ~KT(0), o = KT(0);
+#pragma unroll
+  for (int k = 0; k < kRsItems; ++k) {
+    const int i = wave * (kRsTile / 4) + k * kWave + lane;
+    const bool ok = i < len;
+    const KT k0 = ok ? SortKey<T>::asc(x[s0 + i]) : KT(0);
+    key[k] = desc ? ~k0 : k0;
+    pos[k] = static_cast<uint32_t>(i);
+    if (ok) { a &= key[k]; o |= key[k]; }
+  }
+#pragma unroll
+  for (int off = kWave / 2; off > 0; off >>= 1) {
+    a &= __shfl_xor(a, off, kWave);
+    o |= __shfl_xor(o, off, kWave);
+  }
+  if (lane == 0) { s_and[wave] = a; s_or[wave] = o; }
+  __syncthreads();
+  KT varying = KT(0);
+  {
+    KT ba = ~KT(0), bo = KT(0);
+#pragma unroll
+    for (int w = 0; w < kRsThreads / kWave; ++w) { ba &= s_and[w]; bo |= s_or[w]; }
+    varying = ba ^ bo;
+  }
+  for (int shift = 0; shift < 8 * static_cast<int>(sizeof(KT)); shift += 8) {
+    if (((varying >> shift) & KT(0xFF)) == KT(0)) continue;  // block-uniform
+    for (int i = threadIdx.x; i < 4 * kRsBins; i += kRsThreads) (&cnt[0][0])[i] = 0u;
+    __syncthreads();
+    rs_rank_tile<KT>(key, len, shift, cnt, lstart, rank);
+#pragma unroll
+    for (int k = 0; k < kRsItems; ++k) {
+      if (rank[k] == 0xFFFFFFFFu) continue;
+      const uint32_t d = static_cast<uint32_t>((key[k] >> shift) & 0xFF);
+      const uint32_t lp = lstart[d] + cnt[wave][d] + rank[k];
+      s_key[lp] = key[k];
+      s_pos[lp] = pos[k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kRsItems; ++k) {  // the reordered row, read back in the ranking's element order
+      const int i = wave * (kRsTile / 4) + k * kWave + lane;
+      if (i < len) { key[k] = s_key[i]; pos[k] = s_pos[i]; }
+    }
+    __syncthreads();  // cnt / lstart / s_key are rewritten by the next pass
+  }
+#pragma unroll
+  for (int k = 0; k < kRsItems; ++k) {
+    const int i = wave * (kRsTile / 4) + k * kWave + lane;
+    if (i >= len) continue;
+    const KT kk = desc ? ~key[k] : key[k];
+    vals[s0 + i] = KeyDecode<T>::exact(kk) ? KeyDecode<T>::value(kk) : x[s0 + pos[k]];
+    idx[s0 + i] = pos[k];
+  }
+}
+
 template <typename T>
 void radix_sort_impl(const at::Tensor& x, int S, int64_t n, bool desc, at::Tensor& vals, at::Tensor& idx) {
   using KT = typename SortKey<T>::type;
+  if (n <= kRsTile) {  // one workgroup per row, one launch
+    hipLaunchKernelGGL(sort_tile_kernel<T>, S, kRsThreads, 0, stream(), x.data_ptr<T>(), n, desc, vals.data_ptr<T>(),
+                       idx.data_ptr<int64_t>());
+    TMX_LAUNCH_CHECK();
+    return;
+  }
   auto opts = x.options();
   const auto kdt = sizeof(KT) == 4 ? at::kInt : at::kLong;
   auto k0 = at::empty({(int64_t)S * n}, opts.dtype(kdt)), k1 = at::empty({(int64_t)S * n}, opts.dtype(kdt));

@@ -87,3 +87,14 @@ def test_radix_sort_constant_digit_passes_skipped(descending):
     _check(torch.randint(0, 300, (4, 70_001), generator=g), descending)
     x = torch.rand(400_000, generator=g) * 0.25 + 0.5  # one exponent (float keys: every pass runs)
     _check(x, descending)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64, torch.int32, torch.int64])
+@pytest.mark.parametrize("descending", [False, True])
+def test_radix_sort_single_tile_rows(dtype, descending):
+    """Rows of <= 4096 keys take the one-workgroup kernel (all passes in LDS, per-row constant digits skipped)."""
+    _check(_data(4000, dtype, seed=21, rows=7), descending)
+    _check(_data(1, dtype, seed=22, rows=3), descending)
+    _check(_data(257, dtype, seed=23, rows=64), descending)
+    const = torch.full((5, 300), 3, dtype=dtype)
+    _check(const, descending)

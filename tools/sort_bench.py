@@ -26,6 +26,8 @@ def main() -> None:
         "i32_4M": torch.randint(-(1 << 30), 1 << 30, (1 << 22,), device=dev, generator=g, dtype=torch.int32),
         "f32_rows_64x262144": torch.randn(64, 1 << 18, device=dev, generator=g),
         "f32_64K": torch.randn(1 << 16, device=dev, generator=g),
+        "f32_4K": torch.randn(4096, device=dev, generator=g),
+        "f32_rows_256x2048": torch.randn(256, 2048, device=dev, generator=g),
     }
 
     def med_ms(fn, reps=15):
