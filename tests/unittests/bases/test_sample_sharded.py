@@ -102,3 +102,13 @@ def test_kendall_cross_range_counting_single_process():
     brute = int(((y[:, None] > y[None, :]) & (xr[:, None] < xr[None, :])).sum())
     assert _greater_in_lower_ranges(y, xr, 4) == brute
     assert int(_count_inversions(torch.tensor([3.0, 1.0, 2.0]))) == 2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("check", [check_rank_metrics, check_clustering_metrics])
+def test_sample_sharded_gpu_states_gloo(check):
+    """The same checks with the samples on cuda:0 (two ranks share the one GPU, collectives over gloo): the sharded
+    ranks sort through the in-tree radix sort (ops/sort.py) on the device."""
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    run_multirank(check, 2, "gloo_cuda", timeout=300)
