@@ -1179,17 +1179,32 @@ __global__ void __launch_bounds__(256) class_partial_reduce_kernel(const uint32_
   }
   const int i = blockIdx.x * 256 + threadIdx.x;
   uint64_t neg = 0, pos = 0;
-  for (int s = 0; s < splits; ++s) {
-    const int64_t b = (int64_t)c * splits + s;
-    const int lo = prange[2 * b], hi = prange[2 * b + 1];
-    if (i >= lo && i <= hi) {
+  const int64_t b0 = (int64_t)c * splits;
+  int s = 0;
+  for (; s + 8 <= splits; s += 8) {  // 8 splits' words requested before any is summed (one latency, not 8)
+    uint32_t w[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int64_t b = b0 + s + u;
+      w[u] = (i >= prange[2 * b] && i <= prange[2 * b + 1]) ? partial[b * kCodes + i] : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      neg += w[u] & 0xFFFFu;
+      pos += w[u] >> 16;
+    }
+  }
+  for (; s < splits; ++s) {
+    const int64_t b = b0 + s;
+    if (i >= prange[2 * b] && i <= prange[2 * b + 1]) {
       const uint32_t w = partial[b * kCodes + i];
       neg += w & 0xFFFFu;
       pos += w >> 16;
     }
   }
-  if (neg) hist[(int64_t)c * 2 * kCodes + i] += static_cast<int64_t>(neg);
-  if (pos) hist[((int64_t)c * 2 + 1) * kCodes + i] += static_cast<int64_t>(pos);
+  // one owner per bin; non-returning atomics instead of a read-modify-write that waits on a global load
+  if (neg) atomic_add_i64(hist + (int64_t)c * 2 * kCodes + i, static_cast<int64_t>(neg));
+  if (pos) atomic_add_i64(hist + ((int64_t)c * 2 + 1) * kCodes + i, static_cast<int64_t>(pos));
 }
 
 // Speculation roll, one thread, in row-pass stream order right after the FIXUP launch (standalone row pass only; the
