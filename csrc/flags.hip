@@ -52,12 +52,15 @@ __device__ __forceinline__ void flag_clear(const FlagDesc& f, int j) {
 
 // one wave: lane l walks the flat element list with stride 64; a flag shared by two descriptors (two metrics attached
 // to one kernel-written word) is read by both before any clear: all reads, a wave barrier, then the clears
-__global__ void __launch_bounds__(kWave) gather_flags_kernel(FlagArgs args, int32_t total, int32_t* __restrict__ out) {
-  for (int k = 0; k < args.n; ++k) {
-    const FlagDesc& f = args.d[k];
-    for (int j = threadIdx.x; j < f.numel; j += kWave) out[f.out_off + j] = flag_value(f, j);
+// (read == 0: a clear-only launch, issued after every read launch when the descriptors span several launches)
+__global__ void __launch_bounds__(kWave) gather_flags_kernel(FlagArgs args, int32_t read, int32_t* __restrict__ out) {
+  if (read) {
+    for (int k = 0; k < args.n; ++k) {
+      const FlagDesc& f = args.d[k];
+      for (int j = threadIdx.x; j < f.numel; j += kWave) out[f.out_off + j] = flag_value(f, j);
+    }
+    __syncthreads();
   }
-  __syncthreads();
   for (int k = 0; k < args.n; ++k) {
     const FlagDesc& f = args.d[k];
     if (!f.zero) continue;
@@ -81,11 +84,16 @@ static int32_t flag_dtype(at::ScalarType t) {
 
 // flags: device tensors on one device (any shape); zero[i]: clear flags[i] after reading it (contiguous flags only).
 // Device int32 tensor with every flag's elements in order; one launch per 48 flags, no host synchronisation.
-// One launch per 48 flags: every flag's elements, in order, as int32 at out (device-visible memory).
+// One launch per 48 flags: every flag's elements, in order, as int32 at out (device-visible memory).  A flag tensor
+// may appear twice (two metrics attached to one kernel-written word, or one sink registered for its errors and its
+// warnings): within one launch the kernel reads before it clears; when the list spans several launches, the read
+// launches clear nothing and clear-only launches follow them, so no descriptor sees a flag another one consumed.
 static void launch_gather(at::TensorList flags, c10::IntArrayRef zero, int64_t total, int32_t* out) {
   const at::Device dev = flags[0].device();
   std::vector<at::Tensor> keep;  // contiguous views (a non-contiguous flag is read from a copy; it is never cleared then)
   keep.reserve(flags.size());
+  const bool split = flags.size() > static_cast<size_t>(kMaxFlagDescs);
+  std::vector<FlagArgs> clears;
   int64_t off = 0;
   size_t i = 0;
   while (i < flags.size()) {
@@ -105,7 +113,16 @@ static void launch_gather(at::TensorList flags, c10::IntArrayRef zero, int64_t t
       off += f.numel();
       ++i;
     }
-    hipLaunchKernelGGL(gather_flags_kernel, 1, kWave, 0, stream(), args, static_cast<int32_t>(total), out);
+    if (split) {
+      clears.push_back(args);
+      for (int k = 0; k < args.n; ++k) args.d[k].zero = 0;
+    }
+    hipLaunchKernelGGL(gather_flags_kernel, 1, kWave, 0, stream(), args, 1, out);
+    TMX_LAUNCH_CHECK();
+  }
+  (void)total;
+  for (const FlagArgs& c : clears) {
+    hipLaunchKernelGGL(gather_flags_kernel, 1, kWave, 0, stream(), c, 0, out);
     TMX_LAUNCH_CHECK();
   }
 }

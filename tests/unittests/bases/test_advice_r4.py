@@ -1,0 +1,201 @@
+"""Round-4 advisor findings.
+
+* A GPU ``forward`` keeps the deferred input flags accumulated by earlier ``update`` calls: the forward paths'
+  internal ``reset()`` must not clear them (``DeferredChecks.take_for_forward`` holds them in place), for reduce-state,
+  full-state, fused-collection and ``dist_sync_on_step`` forwards.
+* ``Metric.forward(dist_sync_on_step=True)`` on 2 gloo ranks: global state, synced batch value and surviving flags.
+* A flag list longer than one gather launch still reads every duplicate before it is cleared.
+* ``validation_mode()`` follows ``TMX_VALIDATION`` whatever the environment looked like at import.
+"""
+import pytest
+import torch
+
+from tests.helpers.multirank import run_multirank
+
+
+def _mc_batch(seed, n=64, c=5, bad=False, device="cpu"):
+    g = torch.Generator().manual_seed(seed)
+    p = torch.randn(n, c, generator=g)
+    t = torch.randint(0, c, (n,), generator=g)
+    if bad:
+        t[3] = c + 2  # out of range: a deferred RuntimeError
+    return p.to(device), t.to(device)
+
+
+def _bin_batch(seed, n=64, bad=False, device="cpu"):
+    g = torch.Generator().manual_seed(seed)
+    p = torch.rand(n, generator=g)
+    t = torch.randint(0, 2, (n,), generator=g)
+    if bad:
+        t[3] = 2  # not binary: a deferred RuntimeError
+    return p.to(device), t.to(device)
+
+
+def _make(kind, **kw):
+    from torchmetrics_forked_amd.classification import BinaryAccuracy, MulticlassAccuracy, MulticlassConfusionMatrix
+
+    if kind == "binary":
+        return BinaryAccuracy(**kw)
+    if kind == "binary_full":
+
+        class _FullBin(BinaryAccuracy):
+            full_state_update = True
+
+        return _FullBin(**kw)
+
+    if kind == "reduce":
+        return MulticlassAccuracy(num_classes=5, **kw)
+    if kind == "full":
+
+        class _FullAcc(MulticlassAccuracy):
+            full_state_update = True
+
+        return _FullAcc(num_classes=5, **kw)
+    if kind == "confmat":
+        return MulticlassConfusionMatrix(num_classes=5, **kw)
+    raise ValueError(kind)
+
+
+def _flags_survive(kind, device):
+    m = _make(kind).to(device)
+    twin = _make(kind).to(device)
+    batch = _bin_batch if kind.startswith("binary") else _mc_batch
+    bad = batch(0, bad=True, device=device)
+    good = [batch(s, device=device) for s in (1, 2)]
+    m.update(*bad)
+    twin.update(*bad)
+    for b in good:
+        m(*b)  # valid batches through forward
+        twin.update(*b)
+    with pytest.raises(RuntimeError):
+        m.compute()
+    with pytest.raises(RuntimeError):
+        twin.compute()
+    # the raise consumed the flags; the accumulated states are the same as the update-only twin's
+    torch.testing.assert_close(m.compute(), twin.compute())
+
+
+def test_deferred_flags_survive_forward_cpu_deferred(monkeypatch):
+    monkeypatch.setenv("TMX_VALIDATION", "deferred")
+    for kind in ("binary", "binary_full"):
+        _flags_survive(kind, "cpu")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["reduce", "full", "confmat", "binary", "binary_full"])
+def test_deferred_flags_survive_forward_gpu(kind):
+    _flags_survive(kind, "cuda")
+
+
+@pytest.mark.gpu
+def test_deferred_flags_survive_collection_forward_gpu():
+    from torchmetrics_forked_amd import MetricCollection
+    from torchmetrics_forked_amd.classification import MulticlassAccuracy, MulticlassF1Score
+
+    mk = lambda: MetricCollection({"acc": MulticlassAccuracy(num_classes=5), "f1": MulticlassF1Score(num_classes=5)}).cuda()  # noqa: E731
+    coll, twin = mk(), mk()
+    bad = _mc_batch(0, bad=True, device="cuda")
+    coll.update(*bad)
+    twin.update(*bad)
+    for s in (1, 2):
+        b = _mc_batch(s, device="cuda")
+        coll(*b)
+        twin.update(*b)
+    with pytest.raises(RuntimeError):
+        coll.compute()
+    with pytest.raises(RuntimeError):
+        twin.compute()
+    got, ref = coll.compute(), twin.compute()
+    for k in ref:
+        torch.testing.assert_close(got[k], ref[k])
+
+
+@pytest.mark.gpu
+def test_bad_forward_batch_raises_at_compute_gpu():
+    """GPU forward defers its own batch's range check to the next compute (no host read inside forward)."""
+    m = _make("reduce").cuda()
+    m(*_mc_batch(1, device="cuda"))
+    m(*_mc_batch(0, bad=True, device="cuda"))
+    with pytest.raises(RuntimeError):
+        m.compute()
+
+
+# ---- dist_sync_on_step forward, 2 ranks ------------------------------------------------------------------------
+def check_step_sync_forward_flags(rank, world, device):
+    import os
+
+    from torchmetrics_forked_amd.functional.classification import binary_accuracy
+    from torchmetrics_forked_amd.utilities.distributed import gather_all_tensors
+
+    os.environ["TMX_VALIDATION"] = "deferred"
+    m = _make("binary", dist_sync_on_step=True).to(device)
+    twin = _make("binary").to(device)
+    bad = _bin_batch(10 + rank, bad=True, device=device)
+    m.update(*bad)
+    twin.update(*bad)
+    for step in range(2):
+        p, t = _bin_batch(100 * rank + step, n=32 + 8 * rank, device=device)
+        val = m(p, t)
+        twin.update(p, t)
+        # the batch value is the synced one: accuracy over every rank's batch
+        ps, ts = gather_all_tensors(p), gather_all_tensors(t)
+        ref = binary_accuracy(torch.cat(ps), torch.cat(ts))
+        torch.testing.assert_close(val, ref)
+    # the flags of the bad update() survived both forwards
+    with pytest.raises(RuntimeError):
+        m.compute()
+    with pytest.raises(RuntimeError):
+        twin.compute()
+    # global state equals the update-only twin's (local states, before any sync)
+    for name in m._defaults:
+        torch.testing.assert_close(getattr(m, name), getattr(twin, name))
+
+
+def test_step_sync_forward_flags_gloo():
+    run_multirank(check_step_sync_forward_flags, 2, "gloo")
+
+
+@pytest.mark.gpu
+def test_step_sync_forward_flags_gloo_cuda():
+    run_multirank(check_step_sync_forward_flags, 2, "gloo_cuda")
+
+
+# ---- flags gathered over several launches --------------------------------------------------------------------------
+@pytest.mark.gpu
+def test_gather_flags_duplicates_across_launches():
+    from torchmetrics_forked_amd import ops
+
+    assert ops.load()
+    flags = [torch.full((1,), i % 3, dtype=torch.int32, device="cuda") for i in range(60)]
+    lst = flags + flags  # every flag twice: first copy in launch 1/2, second in launch 2/3
+    vals = torch.ops.tmx.gather_flags(lst, [1] * len(lst)).tolist()
+    assert vals == [i % 3 for i in range(60)] * 2
+    assert all(int(f.item()) == 0 for f in flags)
+
+
+@pytest.mark.gpu
+def test_deferred_checks_warn_and_raise_one_read_gpu():
+    """compute()'s device branch: a sink with an error and a warning flag registers its flags once; the warning is
+    emitted from the values the consuming read returned (and the flags are cleared)."""
+    from torchmetrics_forked_amd.utilities.validation import DeferredChecks, host_checks
+
+    d = DeferredChecks()
+    w = d.flag(UserWarning, "deferred warning", torch.device("cuda"))
+    w.fill_(1)
+    with pytest.warns(UserWarning, match="deferred warning"), host_checks():
+        d.check()
+    assert int(w.item()) == 0
+    e = d.flag(ValueError, "deferred error", torch.device("cuda"))
+    e.fill_(1)
+    w.fill_(1)
+    with pytest.raises(ValueError, match="deferred error"), host_checks():
+        d.check()
+
+
+def test_validation_mode_follows_env(monkeypatch):
+    from torchmetrics_forked_amd.utilities.validation import validation_mode
+
+    monkeypatch.delenv("TMX_VALIDATION", raising=False)
+    assert validation_mode() == "auto"
+    monkeypatch.setenv("TMX_VALIDATION", "eager")
+    assert validation_mode() == "eager"

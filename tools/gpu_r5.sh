@@ -1,0 +1,44 @@
+#!/bin/bash
+# Round-5 GPU session steps (one MI355X).  Each step has its own time limit; a step that times out, aborts or
+# faults (exit 124 / 134 / 137 / 139) ends the script, any other failure is recorded and the next step runs.
+#   usage (from the container): gpurun --timeout 1100 -- bash tools/gpu_r5.sh <out-subdir> step [step ...]
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out/${1:-r5}; shift; mkdir -p "$OUT"; export TMPDIR=/tmp
+run() {  # run <name> <seconds> <cmd...>; stdout+stderr -> $OUT/<name>.log
+  local name=$1 secs=$2; shift 2
+  timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "step $name rc=$rc"
+  case $rc in 124|134|137|139) echo "fatal rc=$rc in $name: stopping"; exit $rc ;; esac
+  return 0
+}
+for s in "$@"; do
+  case $s in
+    tests) run tests 400 python -u -m pytest ${TMX_TESTS:-tests/unittests/bases/test_advice_r4.py} -m gpu -x -q --timeout 120 --timeout-method thread; tail -3 "$OUT/tests.log" ;;
+    kexp) run kexp 120 ./build/kexp_r5/${TMX_KEXP:-exp}; cat "$OUT/kexp.log" ;;
+    host) run host 120 python tools/host_overhead_probe.py ;;
+    sort) run sort 180 python tools/sort_bench.py; tail -1 "$OUT/sort.log" ;;
+    sortprof) run sortprof 300 rocprofv3 --kernel-trace --stats -d "$OUT/sortprof" -o sort --output-format csv -- python3 tools/sort_bench.py ;;
+    suite) run pytest_gpu 800 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread; tail -3 "$OUT/pytest_gpu.log" ;;
+    smoke) run smoke 200 python -u -c "import __graft_entry__ as g; g.smoke()"; tail -1 "$OUT/smoke.log" ;;
+    fwd) run forward_bench 120 python tools/forward_bench.py; tail -1 "$OUT/forward_bench.log" ;;
+    window) run window 120 python tools/window_probe.py ;;
+    bench) for i in 1 2; do run bench20_$i 120 python bench.py --steps 20 --warmup 5; tail -1 "$OUT/bench20_$i.log"; done ;;
+    bench50) run bench50 120 python bench.py --steps 50 --warmup 5; tail -1 "$OUT/bench50.log" ;;
+    prof) run prof 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o headline --output-format csv -- python3 bench.py --steps 20 --warmup 5 ;;
+    radix) run radix 300 python tools/radix_curve_bench.py; tail -1 "$OUT/radix.log" ;;
+    smallprobe) run smallprobe 240 python tools/mc_small_probe.py; tail -1 "$OUT/smallprobe.log" ;;
+    smallprof) PROBE_SMALL_ONLY=1 run smallprof 300 rocprofv3 --kernel-trace --stats -d "$OUT/smallprof" -o small --output-format csv -- python3 tools/mc_small_probe.py ;;
+    radixab) for r in 1 2; do
+               TMX_NATIVE_LIB=$PWD/build/ab_radix/_tmx_native.so run radix_old_$r 300 python tools/radix_curve_bench.py; tail -1 "$OUT/radix_old_$r.log"
+               run radix_new_$r 300 python tools/radix_curve_bench.py; tail -1 "$OUT/radix_new_$r.log"; done ;;
+    radixtest) run radixtest 300 python -u -m pytest tests/test_ops_radix_gpu.py tests/test_binary_samples_gpu.py -x -q --timeout 120 --timeout-method thread; tail -2 "$OUT/radixtest.log" ;;
+    radixprof) run radixprof 300 rocprofv3 --kernel-trace --stats -d "$OUT/radixprof" -o radix --output-format csv -- python3 tools/radix_curve_bench.py ;;
+    imgprof) run imgprof 900 rocprofv3 --kernel-trace --stats -d "$OUT/imgprof" -o image --output-format csv -- python3 bench.py --config image --steps 1 --warmup 1; tail -2 "$OUT/imgprof.log" ;;
+    bertprof) run bertprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/bertprof" -o bert --output-format csv -- python3 bench.py --config bert --steps 2 --warmup 1; tail -2 "$OUT/bertprof.log" ;;
+    mapbench) run mapbench 600 python bench.py --config map --steps 5 --warmup 1; tail -1 "$OUT/mapbench.log" ;;
+    *) echo "unknown step $s" ;;
+  esac
+done
+echo "session done"

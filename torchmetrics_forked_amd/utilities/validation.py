@@ -21,7 +21,10 @@ from torch import Tensor
 
 
 _ENV_DATA = getattr(os.environ, "_data", None)  # CPython's backing dict: one plain lookup, kept in sync by os.environ[...]
-_ENV_KEY = os.fsencode("TMX_VALIDATION") if _ENV_DATA is not None and any(isinstance(k, bytes) for k in list(_ENV_DATA)[:1]) else "TMX_VALIDATION"
+_encodekey = getattr(os.environ, "encodekey", None)  # the key type the backing dict uses (bytes on POSIX, str on Windows)
+_ENV_KEY = _encodekey("TMX_VALIDATION") if _ENV_DATA is not None and _encodekey is not None else "TMX_VALIDATION"
+if _ENV_DATA is not None and _encodekey is None:
+    _ENV_DATA = None
 
 
 def validation_mode() -> str:
@@ -91,20 +94,23 @@ class HostCheckBatch:
         self._on_abandon = []
         items, self._items = self._items, []
         on_error, self._on_error = self._on_error, []
-        if _in_forward() and items and all(not err for _, _, err, _ in items) and all(
+        in_forward = _in_forward()
+        if in_forward and items and all(not err for _, _, err, _ in items) and all(
             t.is_cuda for ts, _, _, _ in items for t in ts
         ):
-            # a forward on the GPU does not wait for the device: its warning flags are read with the next compute's
-            # checks (errors of a forward batch stay in the metric's deferred flags, see DeferredChecks.check)
+            # a forward on the GPU does not wait for the device: its warning flags are read with the next read of any
+            # block -- a compute, or a forward that reads error flags anyway (errors of a forward batch stay in the
+            # metric's deferred flags, see DeferredChecks.check).  Documented deviation: such batch-value warnings
+            # (e.g. "no positive samples") surface late, at most _MAX_PENDING forwards after their batch.
             pend = _pending()
             pend.extend(items)
             if len(pend) <= _MAX_PENDING:
                 return
             items = list(pend)
             pend.clear()
-        elif not _in_forward():
+        else:
             pend = _pending()
-            if pend:  # warnings parked by earlier forwards are read (and emitted) now, before this block's own
+            if pend and (items or not in_forward):  # warnings parked by earlier forwards ride on this block's read
                 items = list(pend) + items
                 pend.clear()
         if not items:
@@ -135,7 +141,7 @@ def _native() -> bool:
 
 
 _HOST = threading.local()
-_MAX_PENDING = 256  # parked forward warning checks before one synchronous read flushes them
+_MAX_PENDING = 32  # parked forward warning checks before one synchronous read flushes them
 
 
 def _pending() -> List[Tuple[List[Tensor], Callable[[List[int]], None], bool, bool]]:
@@ -212,6 +218,7 @@ class DeferredChecks:
 
     def __init__(self) -> None:
         self._flags: Dict[Tuple[Type[Exception], str], Tensor] = {}
+        self._held = 0  # > 0 inside a GPU forward that keeps its accumulated flags in place (take_for_forward)
 
     def add(self, bad: Tensor, exc: Type[Exception], message: str) -> None:
         key = (exc, message)
@@ -266,10 +273,20 @@ class DeferredChecks:
             return
         if not _in_forward() and len(devs) == 1 and flags[0].is_cuda and _native():
             # compute(): the block's single read returns these flags and clears them (no snapshot kernel; an abandoned
-            # block -- an exception before the read -- leaves them set, so the next compute still raises)
-            batch.add_many(flags, _raise, error=True, consume=True)
-            if warn_keys:
-                batch.add_many(flags, _warn, error=False)
+            # block -- an exception before the read -- leaves them set, so the next compute still raises).  Each flag
+            # is registered once: the warnings reuse the values the error callback received (registering the flags a
+            # second time would let the consuming read clear them before the warning read sees them)
+            if not warn_keys:
+                batch.add_many(flags, _raise, error=True, consume=True)
+                return
+            seen: List[List[int]] = []
+
+            def _raise_keep(vals: List[int]) -> None:
+                seen.append(vals)
+                _raise(vals)
+
+            batch.add_many(flags, _raise_keep, error=True, consume=True)
+            batch.add_many([], lambda _v: _warn(seen[0]) if seen else None, error=False)
             return
         # forward(): snapshot + clear on the device now (one native kernel for all flags) -- the forward ORs the
         # accumulated flags back before the block's read, and they must not leak into this batch's check
@@ -294,6 +311,10 @@ class DeferredChecks:
         batch.on_abandon(_put_back)
 
     def clear(self) -> None:
+        if getattr(self, "_held", 0) > 0 and _in_forward():
+            # a GPU forward's internal reset(): the accumulated flags stay where they are (nothing was parked), the
+            # batch's own flags join them -- both are owed to the next compute()
+            return
         for f in self._flags.values():
             f.zero_()
 
@@ -334,11 +355,16 @@ class DeferredChecks:
             flags = list(self._flags.values())
             dev = flags[0].device
             if dev.type == "cuda" and all(f.device == dev for f in flags):
-                return None
+                # nothing is parked, so the forward's internal reset() must not clear them either: hold until give_back
+                self._held = getattr(self, "_held", 0) + 1
+                return _HOLD  # type: ignore[return-value]
         return self.take()
 
     def give_back(self, taken: Optional[Tuple[List[Tuple[Type[Exception], str]], Any]]) -> None:
         if taken is None:
+            return
+        if taken is _HOLD:
+            self._held = max(0, getattr(self, "_held", 0) - 1)
             return
         keys, snap = taken
         if isinstance(snap, dict):
@@ -357,6 +383,9 @@ class DeferredChecks:
                 self._flags[k] = piece.clone()
             else:
                 c.bitwise_or_(piece.to(c.dtype).reshape(c.shape))
+
+
+_HOLD = ("held",)  # take_for_forward's token: flags kept in place (and reset() does not clear them) until give_back
 
 
 def make_sink(t: Tensor) -> Optional[DeferredChecks]:
