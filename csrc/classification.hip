@@ -1343,7 +1343,16 @@ void launch_class_pass(const uint32_t* cptr, int64_t n, int C, int ld, const T* 
   // row splits only when there are too few classes to fill the chip (exclusive-owner flush when splits == 1)
   int splits = 1;
   while ((int64_t)C * splits < 512 && n_pad / (8 * (splits * 2)) >= 1024) splits *= 2;
-  // 16-bit-packed LDS histogram, 512-thread workgroups, four per CU (csrc/curve_hist_kernels.h class_hist_u16_kernel)
+  // windowed u32 LDS histogram, 512-thread workgroups, four per CU (csrc/curve_hist_kernels.h class_hist_hi_kernel;
+  // TMX_CLASS_PASS_U16=1 selects the round-4 16-bit-packed form for A/B runs)
+  static const bool u16 = [] { const char* v = std::getenv("TMX_CLASS_PASS_U16"); return v != nullptr && v[0] == '1'; }();
+  if (!u16) {
+    hipLaunchKernelGGL((class_hist_hi_kernel<T>), C * splits, kClassThreadsU16, kHiLdsBytes, stream(),
+                       reinterpret_cast<const uint16_t*>(cptr), n_pad, splits, hist, p, ld, target, n, bmode, speculative,
+                       srows, state, cm, code_range, roll_mode, batch_hist, batch_range, row_stats);
+    TMX_LAUNCH_CHECK();
+    return;
+  }
   hipLaunchKernelGGL((class_hist_u16_kernel<T>), C * splits, kClassThreadsU16, kCodes / 2 * sizeof(uint32_t), stream(),
                      reinterpret_cast<const uint16_t*>(cptr), n_pad, splits, hist, p, ld, target, n, bmode, speculative,
                      srows, state, cm, code_range, roll_mode, batch_hist, batch_range, row_stats);

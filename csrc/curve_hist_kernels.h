@@ -2,6 +2,8 @@
 // ablation harness tools/kexp/curve_hist_exp.hip).  See classification.hip for the op-level documentation.
 #pragma once
 
+#include <type_traits>
+
 #include "device_common.h"
 
 namespace tmx {
@@ -531,15 +533,219 @@ __device__ __forceinline__ void row_tile_compute(const RowLoads<NG>& L, int64_t 
   }
 }
 
-template <typename T, int NG, bool SOFTMAX, bool FIXUP, bool PADDED>
+// ---- softmax row tile, lean form (round 5) ----------------------------------------------------------------------------
+// The same codes, bit for bit, as row_tile_compute<SOFTMAX> with about 40 % fewer VALU instructions per element
+// (profiles/pmc_headline_r4.json: the row pass issued ~22 VALU instructions per logit and was VALU-bound):
+//  * the two rows of a pair are unpacked straight into (row a, row b) register pairs, so every v_pk_* operand is
+//    already adjacent (no v_mov to build pairs);
+//  * padding lanes hold duplicates of the row's last vector (the clamped loads), which change neither a maximum, a
+//    minimum, nor the arg-max (the lowest lane wins ties); only the exp-sum must skip them: the lane sum is taken
+//    before the padding group is added (one select per row instead of one per element);
+//  * exp: when every element of the pair is within 86 of its row maximum (ballot, wave-uniform) the clamp is a no-op,
+//    rint(ph) is (ph + 1.5 2^23) - 1.5 2^23 (RNE for |ph| < 2^22) and ldexp(r, e) = bits(r) + (e << 23) exactly (r in
+//    [0.7, 1.42], 126 + e >= 2: normal), where e << 23 is the low bits of (ph + 1.5 2^23) shifted by 23 -- one
+//    v_lshl_add_u32 for v_rndne + v_cvt_i32 + v_ldexp.  Otherwise (a gap > 86, -inf, or a row that is not finite) the
+//    pair takes exp_nonpos2, the reference sequence;
+//  * the row minimum is only compared (ballots), never wave-reduced; the probability-mode witnesses are tested only
+//    while the block has not seen one (``rec && !saw_bad``), as before.
+__device__ __forceinline__ f32x2 exp_nonpos2_narrow(f32x2 x) {
+#pragma clang fp contract(off)
+  const float hi_s = __uint_as_float(0x3fb8aa3bu), lo_s = __uint_as_float(0x32a5705fu), magic = 12582912.f;
+  const f32x2 log2e_hi = {hi_s, hi_s}, log2e_lo = {lo_s, lo_s}, m2 = {magic, magic};
+  const f32x2 ph = x * log2e_hi;
+  f32x2 pl = __builtin_elementwise_fma(x, log2e_hi, -ph);
+  const f32x2 s = ph + m2;  // low bits: rint(ph)
+  const f32x2 e = s - m2;   // rint(ph), exact
+  pl = __builtin_elementwise_fma(x, log2e_lo, pl);
+  const f32x2 t = (ph - e) + pl;
+  const uint32_t ra = __float_as_uint(__builtin_amdgcn_exp2f(t.x)), rb = __float_as_uint(__builtin_amdgcn_exp2f(t.y));
+  return f32x2{__uint_as_float(ra + (__float_as_uint(s.x) << 23)), __uint_as_float(rb + (__float_as_uint(s.y) << 23))};
+}
+
+template <typename T, int NG>
+__device__ __forceinline__ void unpack_pair(const uint4& wa, const uint4& wb, f32x2* P) {
+  float a[8], b[8];
+  unpack8<T>(wa, a);
+  unpack8<T>(wb, b);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) P[j] = f32x2{a[j], b[j]};
+}
+
+__device__ __forceinline__ float max8(const float* v) {
+  return __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaxf(v[0], v[1]), __builtin_fmaxf(v[2], v[3])),
+                         __builtin_fmaxf(__builtin_fmaxf(v[4], v[5]), __builtin_fmaxf(v[6], v[7])));
+}
+__device__ __forceinline__ float min8(const float* v) {
+  return __builtin_fminf(__builtin_fminf(__builtin_fminf(v[0], v[1]), __builtin_fminf(v[2], v[3])),
+                         __builtin_fminf(__builtin_fminf(v[4], v[5]), __builtin_fminf(v[6], v[7])));
+}
+
+template <typename T, int NG>
+__device__ __forceinline__ void row_tile_softmax_lean(const RowLoads<NG>& L, int64_t n, int C, int ld, int64_t ignore_index,
+                                                      bool has_ignore, int64_t* __restrict__ confmat, int* __restrict__ err, bool rec,
+                                                      bool& saw_bad, SlowRows slow, uint32_t* __restrict__ s_tile, int64_t tile,
+                                                      float4* __restrict__ row_stats) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wave = threadIdx.x / kWave;
+  const int nvec = ld / 8;
+  const bool lo_ok = lane < nvec, hi_ok = lane + kWave < nvec;
+  auto row0_of = [&](int pp) -> int64_t { return tile * kTileRows + 2 * (wave + pp * kRowWaves); };
+  const int64_t tv = L.tv;
+  auto target_of = [&](int i) -> int64_t {
+    const uint64_t u = static_cast<uint64_t>(tv);
+    const uint32_t lo = __builtin_amdgcn_readlane(static_cast<uint32_t>(u), i);
+    const uint32_t hi = __builtin_amdgcn_readlane(static_cast<uint32_t>(u >> 32), i);
+    return static_cast<int64_t>((static_cast<uint64_t>(hi) << 32) | lo);
+  };
+  int64_t tt[4];
+  int am[4];
+  bool keepv[4], slowv[4], validv[4];
+#pragma unroll
+  for (int pp = 0; pp < 2; ++pp) {
+    const int p = wave + pp * kRowWaves;
+    const int64_t r0 = row0_of(pp);
+    const int64_t ta = target_of(2 * pp), tb = target_of(2 * pp + 1);
+    const bool va = r0 < n && !(has_ignore && ta == ignore_index);
+    const bool vb = r0 + 1 < n && !(has_ignore && tb == ignore_index);
+    f32x2 P[8 * NG];
+    float mlo_a, mlo_b, mhi_a = -INFINITY, mhi_b = -INFINITY, mn_a, mn_b;
+    {
+      float a[8], b[8];
+      unpack8<T>(L.raw[pp][0][0], a);
+      unpack8<T>(L.raw[pp][1][0], b);
+      mlo_a = max8(a);
+      mlo_b = max8(b);
+      mn_a = min8(a);
+      mn_b = min8(b);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) P[j] = f32x2{a[j], b[j]};
+    }
+    if constexpr (NG == 2) {
+      float a[8], b[8];
+      unpack8<T>(L.raw[pp][0][1], a);
+      unpack8<T>(L.raw[pp][1][1], b);
+      mhi_a = max8(a);
+      mhi_b = max8(b);
+      mn_a = __builtin_fminf(mn_a, min8(a));
+      mn_b = __builtin_fminf(mn_b, min8(b));
+#pragma unroll
+      for (int j = 0; j < 8; ++j) P[8 + j] = f32x2{a[j], b[j]};
+    }
+    const float mxa = wave_max_uniform(__builtin_fmaxf(mlo_a, mhi_a));
+    const float mxb = wave_max_uniform(__builtin_fmaxf(mlo_b, mhi_b));
+    // arg-max (row_argmax on the pair layout): lowest lane of the lowest group holding the maximum, lowest slot
+    auto argmax = [&](float mlo, float mhi, float mx, bool second) -> int {
+      const uint64_t blo = __ballot(mlo == mx);
+      const int g = blo != 0 ? 0 : 1;
+      const uint64_t bm = blo != 0 ? blo : __ballot(mhi == mx);
+      const int Ln = __builtin_ctzll(bm | (1ull << 63));
+      int k = 7;
+      if (NG == 1 || g == 0) {
+#pragma unroll
+        for (int j = 6; j >= 0; --j)
+          if ((__ballot((second ? P[j].y : P[j].x) == mx) >> Ln) & 1ull) k = j;
+      } else {
+#pragma unroll
+        for (int j = 6; j >= 0; --j)
+          if ((__ballot((second ? P[8 * (NG - 1) + j].y : P[8 * (NG - 1) + j].x) == mx) >> Ln) & 1ull) k = j;
+      }
+      return 512 * g + 8 * Ln + k;
+    };
+    const int ama = argmax(mlo_a, mhi_a, mxa, false), amb = argmax(mlo_b, mhi_b, mxb, true);
+    bool fa = __builtin_isfinite(mxa), fb = __builtin_isfinite(mxb);
+    // exp(x - max): the lean sequence when every element of both rows is within 86 of its maximum (wave-uniform)
+    const bool narrow = __ballot(!(mxa - mn_a <= 86.f && mxb - mn_b <= 86.f)) == 0;
+    const f32x2 mx2 = {mxa, mxb};
+    f32x2 acc = {0.f, 0.f}, acc_lo = {0.f, 0.f};
+    if (narrow) {
+#pragma unroll
+      for (int j = 0; j < 8 * NG; ++j) {
+        P[j] = exp_nonpos2_narrow(P[j] - mx2);
+        acc = acc + P[j];
+        if (j == 7) acc_lo = acc;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8 * NG; ++j) {
+        P[j] = exp_nonpos2(P[j] - mx2);
+        acc = acc + P[j];
+        if (j == 7) acc_lo = acc;
+      }
+    }
+    // padding lanes: the group-1 duplicates (NG == 2) or the whole lane (NG == 1) add nothing to the exp-sum
+    if constexpr (NG == 2) acc = hi_ok ? acc : acc_lo;
+    else acc = lo_ok ? acc : f32x2{0.f, 0.f};
+    const float sa = wave_sum_uniform(acc.x), sb = wave_sum_uniform(acc.y);
+    const float ia = 1.f / sa, ib = 1.f / sb;
+    fa = fa && sa == sa;
+    fb = fb && sb == sb;
+    if (row_stats != nullptr && lane == 0) {
+      const bool sfa = __builtin_isfinite(mxa) && sa == sa, sfb = __builtin_isfinite(mxb) && sb == sb;
+      if (r0 < n) row_stats[r0] = make_float4(mxa, sa, __uint_as_float((va ? 1u : 0u) | (sfa ? 2u : 0u)), 0.f);
+      if (r0 + 1 < n) row_stats[r0 + 1] = make_float4(mxb, sb, __uint_as_float((vb ? 1u : 0u) | (sfb ? 2u : 0u)), 0.f);
+    }
+    const bool slow_a = va && !fa, slow_b = vb && !fb;
+    if (rec && !saw_bad) {
+      saw_bad = slow_a || slow_b || (va && mxa > 1.f) || (vb && mxb > 1.f);
+      if (!saw_bad && (va || vb)) {
+        // lanes past the row's vectors hold duplicates: a duplicate's minimum is a real element's
+        saw_bad = __ballot((va && mn_a < 0.f) || (vb && mn_b < 0.f)) != 0;
+      }
+    }
+    const bool ka = va && fa, kb = vb && fb;
+    const f32x2 s2 = {sa, sb}, i2 = {ia, ib};
+    if (ka && kb) {  // wave-uniform: both rows counted (the common case) -- no mask
+#pragma unroll
+      for (int j = 0; j < 8 * NG; ++j) {
+        const int c = 512 * (j >> 3) + 8 * lane + (j & 7);
+        s_tile[c * kSlots + (p ^ (lane & (kSlots - 1)))] = pack_rne2<T>(div_rn2(P[j], s2, i2));
+      }
+    } else {
+      const uint32_t keep = (ka ? 0x0000FFFFu : 0u) | (kb ? 0xFFFF0000u : 0u);
+      const uint32_t setm = ~keep & 0x80008000u;
+#pragma unroll
+      for (int j = 0; j < 8 * NG; ++j) {
+        const int c = 512 * (j >> 3) + 8 * lane + (j & 7);
+        s_tile[c * kSlots + (p ^ (lane & (kSlots - 1)))] = (pack_rne2<T>(div_rn2(P[j], s2, i2)) & keep) | setm;
+      }
+    }
+    if (lane == 0) {
+      if (ka && ta >= 0 && ta < C) atomicOr(&s_tile[ta * kSlots + (p ^ ((int)(ta >> 3) & (kSlots - 1)))], 0x00004000u);
+      if (kb && tb >= 0 && tb < C) atomicOr(&s_tile[tb * kSlots + (p ^ ((int)(tb >> 3) & (kSlots - 1)))], 0x40000000u);
+    }
+    tt[2 * pp] = ta; tt[2 * pp + 1] = tb;
+    am[2 * pp] = ama; am[2 * pp + 1] = amb;
+    keepv[2 * pp] = ka; keepv[2 * pp + 1] = kb;
+    slowv[2 * pp] = slow_a; slowv[2 * pp + 1] = slow_b;
+    validv[2 * pp] = va; validv[2 * pp + 1] = vb;
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int64_t t = tt[i];
+      if (confmat != nullptr && keepv[i] && t >= 0 && t < C && am[i] < C) atomic_add_i64(confmat + t * C + am[i], 1);
+      if (err != nullptr && validv[i] && (t < 0 || t >= C)) atomicOr(err, 1);
+      if (slowv[i]) slow.rows[atomicAdd(slow.count, 1)] = static_cast<int>(row0_of(i >> 1) + (i & 1));
+    }
+  }
+}
+
+#ifndef TMX_ROWPASS_LEAN
+#define TMX_ROWPASS_LEAN 1
+#endif
+
+template <typename T, int NG, bool SOFTMAX, bool FIXUP, bool PADDED, bool LEAN = (TMX_ROWPASS_LEAN != 0)>
 __device__ __forceinline__ void row_tile(const T* __restrict__ preds, const int64_t* __restrict__ target, int64_t n, int C, int ld,
                                           int64_t ignore_index, bool has_ignore, uint32_t* __restrict__ codes, int64_t n_pad,
                                           int64_t* __restrict__ confmat, int* __restrict__ err, bool rec, bool& saw_bad,
                                           SlowRows slow, uint32_t* __restrict__ s_tile, int64_t tile, float4* __restrict__ row_stats) {
   RowLoads<NG> L;
   row_tile_load<T, NG>(preds, target, n, ld, tile, L);
-  row_tile_compute<T, NG, SOFTMAX, FIXUP, PADDED>(L, n, C, ld, ignore_index, has_ignore, confmat, err, rec, saw_bad, slow, s_tile, tile,
-                                                  row_stats);
+  if constexpr (LEAN && SOFTMAX && !FIXUP && !PADDED)
+    row_tile_softmax_lean<T, NG>(L, n, C, ld, ignore_index, has_ignore, confmat, err, rec, saw_bad, slow, s_tile, tile, row_stats);
+  else
+    row_tile_compute<T, NG, SOFTMAX, FIXUP, PADDED>(L, n, C, ld, ignore_index, has_ignore, confmat, err, rec, saw_bad, slow, s_tile, tile,
+                                                    row_stats);
   __syncthreads();
   store_tile<NG>(s_tile, codes, C, n_pad, tile);
 }
@@ -1108,6 +1314,297 @@ __global__ void __launch_bounds__(kClassThreadsU16) class_hist_u16_kernel(const 
   class_hist_block<T, false, kClassThreadsU16, true>(blockIdx.x, gridDim.x, codes, n_pad, splits, hist, preds, ld, target, n, bmode,
                                                      speculative, slow_rows, state, confmat, code_range, roll_mode, nullptr, nullptr,
                                                      batch_hist, batch_range, row_stats);
+}
+
+// ---- multiclass class pass, windowed u32 form (round 5) ------------------------------------------------------------
+// class_hist_u16_kernel spent ~12 VALU instructions per code (unpack one 16-bit code, route skip codes to the trash bin,
+// split the bin into a u16 word and a half, test every code for the positive flag; profiles/pmc_headline_r4.json) and
+// with that VALU the pass ran at ~55 % of the read floor; without any of its atomics it still took 36 of its 43 us
+// (profiles/kexp_classpass_r5.json).  Here the histogram is one u32 word per bin of a window of 8192 codes, so a count
+// is a constant 1 at a byte offset computed for two codes at once:
+//   y = min(max(code, 8190), 16382)   (v_pk_max_u16 + v_pk_min_u16: both codes of a dword)
+//   offset = 4 y - 32760              (one v_mad_u32_u16 per code, the 16-bit half selected by op_sel)
+// Word 0 collects every code <= 8190 (the low bucket: scores below 2^-63, rare), words 1..8190 are bins 8191..16380,
+// word 8191 (bin 16381, above every bf16 / fp16 score in [0, 1]: 16256 / 15360) collects skip codes (bit 15) AND positives (bit 14),
+// which are booked straight into the int64 positive bins under a wave-uniform test of the whole 16-B vector (1 / C of
+// the codes).  A block whose low bucket is not empty re-reads its codes once and counts the window [0, 8190] the same
+// way (y = min(code, 8191), word 8191 the trash): exact for any input, one extra pass only for classes holding
+// probabilities below 2^-63 (logit gaps above ~43).  Per code: ~2.5 VALU instructions and one ds_add_u32.
+constexpr int kHiBase = kCodes / 2 - 2;                     // 8190: word 0 = the low bucket
+constexpr int kHiWords = kCodes / 2;                        // 8192 words: bins 8191..16381 at words 1..8191
+constexpr int kHiTrash = kHiBase + kHiWords - 1;            // 16381: skip codes and positives (word 8191)
+constexpr size_t kHiLdsBytes = (size_t)kHiWords * 4;        // exactly 32 KiB (no other LDS object): the workgroup fits
+                                                            // beside two 64-KiB row-pass workgroups on a 160-KiB CU
+#ifndef TMX_HI_UNROLL
+#define TMX_HI_UNROLL 4
+#endif
+constexpr int kHiUnroll = TMX_HI_UNROLL;  // 16-B code vectors per thread per step (two steps' worth in registers)
+
+typedef unsigned short hi_u16x2 __attribute__((ext_vector_type(2)));
+
+// count the codes of one 16-B vector into the window (LOW: the [0, 8190] re-pass) -- positives are returned as a
+// bit mask (0x40004000 bits of any dword) for the caller's wave-uniform test
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+
+// LDS word at byte offset ``off`` of the dynamic allocation (which starts at LDS address 0 in these kernels: no static
+// __shared__ object precedes it), counted by one ds_add_u32 with no base-address arithmetic
+#ifndef TMX_CLASS_ABL
+#define TMX_CLASS_ABL 0  // kernel-harness ablation (tools/kexp): 1 = no LDS count atomics.  Always 0 in the library.
+#endif
+__device__ uint32_t g_abl_sink;
+__device__ __forceinline__ void lds_inc(uint32_t off) {
+#if TMX_CLASS_ABL & 1
+  if (off == 0xFFFFFFFFu) g_abl_sink = off;
+#else
+  __hip_atomic_fetch_add(reinterpret_cast<lds_u32*>(static_cast<size_t>(off)), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#endif
+}
+
+// count the codes of one 16-B vector into the window (LOW: the [0, 8190] re-pass): per dword a saturating v_pk_sub_u16
+// and a v_pk_min_u16 give both codes' window indices, two SDWA shifts their byte offsets
+template <bool LOW>
+__device__ __forceinline__ void hi_count4(const uint4& v) {
+  const uint32_t parts[4] = {v.x, v.y, v.z, v.w};
+  uint32_t idx[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    hi_u16x2 c = __builtin_bit_cast(hi_u16x2, parts[k]);
+    if constexpr (LOW) c = __builtin_elementwise_min(c, (hi_u16x2){kHiBase + 1, kHiBase + 1});
+    else c = __builtin_elementwise_min(__builtin_elementwise_sub_sat(c, (hi_u16x2){kHiBase, kHiBase}),
+                                       (hi_u16x2){kHiTrash - kHiBase, kHiTrash - kHiBase});
+    idx[k] = __builtin_bit_cast(uint32_t, c);
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    lds_inc((idx[k] & 0xFFFFu) << 2);
+    lds_inc((idx[k] >> 16) << 2);
+  }
+}
+
+template <typename T, int NT>
+__device__ __forceinline__ void class_hist_hi_block(int64_t vb, int64_t vgrid, const uint16_t* __restrict__ codes, int64_t n_pad, int splits,
+                                                    int64_t* __restrict__ hist, const T* __restrict__ preds, int ld,
+                                                    const int64_t* __restrict__ target, int64_t n, const int* __restrict__ bmode,
+                                                    bool speculative, const int* __restrict__ slow_rows, int* __restrict__ state,
+                                                    int64_t* __restrict__ confmat, int* __restrict__ code_range, int* __restrict__ roll_mode,
+                                                    int64_t* __restrict__ batch_hist, int* __restrict__ batch_range,
+                                                    const float4* __restrict__ row_stats) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_h[];  // [kHiWords] words, at LDS address 0
+  int lo = kCodes, hi = -1;
+  const int C = static_cast<int>(vgrid / splits);
+  const int c = static_cast<int>(vb / splits), sp = static_cast<int>(vb % splits);
+  // the row-pass kernels of this batch are complete (stream order); read before this block's ticket (below), so before
+  // the last block resets the state words
+  const int info_m0 = bmode[0], info_m1 = speculative ? bmode[1] : bmode[0];
+  const int info_n0 = state[0], info_n1 = state[1];
+  uint4* s4 = reinterpret_cast<uint4*>(s_h);
+  for (int i = threadIdx.x; i < kHiWords / 4; i += NT) s4[i] = make_uint4(0, 0, 0, 0);
+  __syncthreads();
+  int64_t* neg_hist = hist + ((int64_t)c * 2) * kCodes;
+  int64_t* pos_hist = hist + ((int64_t)c * 2 + 1) * kCodes;
+  int64_t* bneg = batch_hist != nullptr ? batch_hist + ((int64_t)c * 2) * kCodes : nullptr;
+  int64_t* bpos = batch_hist != nullptr ? batch_hist + ((int64_t)c * 2 + 1) * kCodes : nullptr;
+  const uint4* col = reinterpret_cast<const uint4*>(codes + (int64_t)c * n_pad);
+  const int64_t nv = n_pad / 8;
+  const int64_t per = (nv + splits - 1) / splits;
+  const int64_t v0 = sp * per, v1 = v0 + per < nv ? v0 + per : nv;
+  // refit of a mis-speculated batch (the class_hist_block sequence): this class's codes rebuilt from the scores
+  if (speculative && row_stats != nullptr && info_m0 != info_m1) {
+    const int m1 = info_m1;
+    uint16_t* ccol = const_cast<uint16_t*>(codes) + (int64_t)c * n_pad;
+    for (int64_t r = v0 * 8 + threadIdx.x; r < v1 * 8; r += NT) {
+      uint32_t code = 0x8000u;
+      if (r < n) {
+        const float4 st = row_stats[r];
+        const uint32_t fl = __float_as_uint(st.z);
+        const T xv = preds[r * ld + c];
+        if (m1 != 0) {
+          if ((fl & 3u) == 3u) {
+            const float inv = 1.f / st.y;
+            const f32x2 e = exp_nonpos2(f32x2{to_f32<T>(xv) - st.x, 0.f});
+            code = pack_rne2<T>(div_rn2(f32x2{e.x, 0.f}, f32x2{st.y, 1.f}, f32x2{inv, 1.f})) & 0xFFFFu;
+          }
+        } else if (fl & 1u) {
+          code = raw_code<T>(bits16<T>(xv));
+        }
+        if (!(code & 0x8000u) && target[r] == c) code |= 0x4000u;
+      }
+      ccol[r] = static_cast<uint16_t>(code);
+    }
+    __threadfence();
+    __syncthreads();
+  }
+  // positives of one vector: int64 bins directly (and the batch bins), range tracked here
+  auto book_pos = [&](const uint4& v) {
+    const uint32_t parts[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const uint32_t x = (k & 1) ? (parts[k >> 1] >> 16) : (parts[k >> 1] & 0xFFFFu);
+      if ((x & 0xC000u) == 0x4000u) {
+        const uint32_t bin = x & 0x3FFFu;
+        atomic_add_i64(pos_hist + bin, 1);
+        if (bpos != nullptr) atomic_add_i64(bpos + bin, 1);
+        lo = min(lo, (int)bin);
+        hi = max(hi, (int)bin);
+      }
+    }
+  };
+  // Loads run one step ahead (register double buffer of kHiUnroll vectors): the next step's loads are in flight while
+  // this step is counted, so a workgroup streams instead of alternating load and count phases.  EXACT: the slice is a
+  // whole number of steps (65536-row classes: 4 steps of 4 vectors per thread), no bounds tests.
+  constexpr int64_t kStep = (int64_t)kHiUnroll * NT;
+  auto count_step = [&](const uint4 (&w)[kHiUnroll]) {
+#pragma unroll
+    for (int u = 0; u < kHiUnroll; ++u) {
+      hi_count4<false>(w[u]);
+      const uint32_t anypos = ((w[u].x | w[u].y) | (w[u].z | w[u].w)) & 0x40004000u;
+      if (__builtin_expect(__ballot(anypos != 0) != 0, 0) && anypos != 0) book_pos(w[u]);
+    }
+  };
+  auto stream = [&](auto exact_tag) {
+    constexpr bool EXACT = decltype(exact_tag)::value;
+    auto load = [&](uint4 (&w)[kHiUnroll], int64_t cb) {
+#pragma unroll
+      for (int u = 0; u < kHiUnroll; ++u) {
+        const int64_t v = cb + threadIdx.x + u * NT;
+        if constexpr (EXACT) w[u] = col[v];
+        else w[u] = v < v1 ? col[v] : make_uint4(0x80008000u, 0x80008000u, 0x80008000u, 0x80008000u);
+      }
+    };
+    uint4 a[kHiUnroll], b[kHiUnroll];
+    if (v0 >= v1) return;
+    load(a, v0);
+    for (int64_t cb = v0; cb < v1; cb += 2 * kStep) {
+      const bool more1 = cb + kStep < v1, more2 = cb + 2 * kStep < v1;  // block-uniform
+      if (more1) load(b, cb + kStep);
+      count_step(a);
+      if (!more1) break;
+      if (more2) load(a, cb + 2 * kStep);
+      count_step(b);
+    }
+  };
+  if ((v1 - v0) % kStep == 0) stream(std::true_type{});
+  else stream(std::false_type{});
+  __syncthreads();
+  const bool low = s_h[0] != 0u;  // block-uniform
+  // rare rows (usually none): before the flushes, which then go by atomics when there are any
+  const int m0 = info_m0, m1 = info_m1;
+  const bool fixed = speculative && m0 != m1;
+  const int64_t n0 = info_n0, n1 = info_n1;
+  if (sp == 0) {
+    for (int64_t i = threadIdx.x; i < n0 + n1; i += NT) {
+      const int lst = i < n0 ? 0 : 1;
+      if (lst == 0 && fixed) continue;
+      const int64_t r = slow_rows[lst * n + (lst == 0 ? i : i - n0)];
+      if ((lst == 1 ? m1 : m0) != 0) continue;
+      const uint32_t code = raw_code<T>(bits16<T>(preds[r * ld + c]));
+      if (code & 0x8000u) continue;
+      lo = min(lo, (int)code);
+      hi = max(hi, (int)code);
+      if (target[r] == c) atomic_add_i64(pos_hist + code, 1);
+      else atomic_add_i64(neg_hist + code, 1);
+      if (bneg != nullptr) atomic_add_i64((target[r] == c ? bpos : bneg) + code, 1);
+    }
+  }
+  if (confmat != nullptr && threadIdx.x < kWave) {
+    const int lane = threadIdx.x;
+    for (int64_t i = vb; i < n0; i += vgrid) {
+      const int64_t r = slow_rows[i];
+      const int64_t t = target[r];
+      if (t < 0 || t >= C) continue;
+      const T* row = preds + r * ld;
+      float best = -INFINITY;
+      int bi = C, first_nan = C;
+      for (int cc = lane; cc < C; cc += kWave) {
+        const float v = to_f32<T>(row[cc]);
+        if (v != v) first_nan = min(first_nan, cc);
+        else if (bi == C || v > best) { best = v; bi = cc; }
+      }
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) first_nan = min(first_nan, __shfl_xor(first_nan, off, kWave));
+      wave_argmax(best, bi);
+      const int am = first_nan < C ? first_nan : bi;
+      if (lane == 0 && am < C) atomic_add_i64(confmat + t * C + am, 1);
+    }
+  }
+  const bool bstore = splits == 1 && n0 + n1 == 0;  // this block is the only writer of its batch bins
+  // flush of the upper window: words 1..8190 = bins 8191..16380 (word 0: the low bucket, word 8191: trash)
+  for (int w = 1 + threadIdx.x; w < kHiWords - 1; w += NT) {
+    const uint32_t cnt = s_h[w];
+    if (cnt) {
+      const int i = w + kHiBase;
+      lo = min(lo, i);
+      hi = max(hi, i);
+      atomic_add_i64(neg_hist + i, cnt);
+      if (bneg != nullptr) {
+        if (bstore) bneg[i] = cnt;
+        else atomic_add_i64(bneg + i, cnt);
+      }
+    }
+  }
+  if (low) {  // codes <= 8190 (probabilities below 2^-63): one more pass over this slice, window [0, 8190]
+    __syncthreads();
+    for (int i = threadIdx.x; i < kHiWords / 4; i += NT) s4[i] = make_uint4(0, 0, 0, 0);
+    __syncthreads();
+    for (int64_t cb = v0; cb < v1; cb += kStep) {
+#pragma unroll
+      for (int u = 0; u < kHiUnroll; ++u) {
+        const int64_t v = cb + threadIdx.x + u * NT;
+        if (v < v1) hi_count4<true>(col[v]);
+      }
+    }
+    __syncthreads();
+    for (int w = threadIdx.x; w <= kHiBase; w += NT) {
+      const uint32_t cnt = s_h[w];
+      if (cnt) {
+        lo = min(lo, w);
+        hi = max(hi, w);
+        atomic_add_i64(neg_hist + w, cnt);
+        if (bneg != nullptr) {
+          if (bstore) bneg[w] = cnt;
+          else atomic_add_i64(bneg + w, cnt);
+        }
+      }
+    }
+  }
+  if (code_range != nullptr || batch_range != nullptr) {
+    lo = wave_min_i32(lo);
+    hi = wave_max_i32(hi);
+    if ((threadIdx.x & (kWave - 1)) == 0 && hi >= 0) {
+      if (code_range != nullptr) {
+        atomicMin(code_range + 2 * c, lo);
+        atomicMax(code_range + 2 * c + 1, hi);
+      }
+      if (batch_range != nullptr) {
+        atomicMin(batch_range + 2 * c, lo);
+        atomicMax(batch_range + 2 * c + 1, hi);
+      }
+    }
+  }
+  if (threadIdx.x == 0) {  // last workgroup: reset the batch state words and roll the speculation (class_hist_block)
+    if (__hip_atomic_fetch_add(state + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)vgrid - 1) {
+      state[0] = state[1] = 0;
+      state[2] = 0;
+      if (roll_mode != nullptr) {
+        const int mr = roll_mode[1];
+        roll_mode[0] = mr;
+        roll_mode[1] = 0;
+      }
+    }
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(kClassThreadsU16) class_hist_hi_kernel(const uint16_t* __restrict__ codes, int64_t n_pad, int splits,
+                                                                        int64_t* __restrict__ hist, const T* __restrict__ preds, int ld,
+                                                                        const int64_t* __restrict__ target, int64_t n,
+                                                                        const int* __restrict__ bmode, bool speculative,
+                                                                        const int* __restrict__ slow_rows, int* __restrict__ state,
+                                                                        int64_t* __restrict__ confmat, int* __restrict__ code_range,
+                                                                        int* __restrict__ roll_mode, int64_t* __restrict__ batch_hist,
+                                                                        int* __restrict__ batch_range, const float4* __restrict__ row_stats = nullptr) {
+  class_hist_hi_block<T, kClassThreadsU16>(blockIdx.x, gridDim.x, codes, n_pad, splits, hist, preds, ld, target, n, bmode, speculative,
+                                           slow_rows, state, confmat, code_range, roll_mode, batch_hist, batch_range, row_stats);
 }
 
 // Small-class class pass: packed LDS histogram per (class, split), partial flush (class_store_partial).

@@ -17,6 +17,8 @@ for s in "$@"; do
   case $s in
     tests) run tests 400 python -u -m pytest ${TMX_TESTS:-tests/unittests/bases/test_advice_r4.py} -m gpu -x -q --timeout 120 --timeout-method thread; tail -3 "$OUT/tests.log" ;;
     kexp) run kexp 120 ./build/kexp_r5/${TMX_KEXP:-exp}; cat "$OUT/kexp.log" ;;
+    kexpmulti) for k in ${TMX_KEXP}; do run kexp_$k 120 ./build/kexp_r5/$k; echo "$k: $(tail -c 400 $OUT/kexp_$k.log)"; done ;;
+    kexppmc) run kexppmc 120 rocprofv3 --kernel-trace --pmc ${TMX_PMC:-SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU} -d "$OUT/kexppmc" -o pmc --output-format csv -- ./build/kexp_r5/${TMX_KEXP:-exp} ;;
     host) run host 120 python tools/host_overhead_probe.py ;;
     sort) run sort 180 python tools/sort_bench.py; tail -1 "$OUT/sort.log" ;;
     sortprof) run sortprof 300 rocprofv3 --kernel-trace --stats -d "$OUT/sortprof" -o sort --output-format csv -- python3 tools/sort_bench.py ;;

@@ -1,0 +1,156 @@
+// Row pass A/B (round 5): production softmax row tile (row_tile_compute) vs the lean form (row_tile_softmax_lean).
+// Same grid / LDS image / store; the lean form must produce the same class-major codes, confusion matrix, rare-row
+// list and per-row statistics bit for bit.  Cases: randn logits (narrow rows), logits x 40 (gaps > 86: the exact
+// exp path), NaN / +-inf / all -inf rows, ignore_index rows, C = 1000 (two class groups) and C = 256 (one group).
+// Build: hipcc -O3 --offload-arch=gfx950 -I csrc tools/kexp/rowpass_lean_exp.hip -o build/kexp_r5/rowpass_lean_exp
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "curve_hist_kernels.h"
+
+using namespace tmx;
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP error %s at %s:%d\n", hipGetErrorString(e), __FILE__, __LINE__); exit(1); } } while (0)
+
+static uint16_t f2bf(float f) { uint32_t u; memcpy(&u, &f, 4); u += 0x7FFF + ((u >> 16) & 1); return (uint16_t)(u >> 16); }
+
+template <bool LEAN, int NG>
+__global__ void __launch_bounds__(kRowThreads, 4) rp_kernel(const __hip_bfloat16* __restrict__ preds, const int64_t* __restrict__ target,
+                                                            int64_t n, int C, int use_mode, int64_t ignore_index, bool has_ignore,
+                                                            uint32_t* __restrict__ codes, int64_t n_pad, int64_t* __restrict__ confmat,
+                                                            int* __restrict__ err, int* __restrict__ slow_rows, int* __restrict__ slow_count,
+                                                            float4* __restrict__ row_stats, int* __restrict__ verdict) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_tile[];
+  const int64_t ntiles = (n + kTileRows - 1) / kTileRows;
+  const int64_t per_xcd = (ntiles + 7) / 8;
+  const int64_t b = blockIdx.x;
+  const int64_t tile = (b % 8) * per_xcd + b / 8;
+  bool saw_bad = false;
+  const SlowRows slow{slow_rows, slow_count};
+  if (tile < ntiles) {
+    if (use_mode)
+      row_tile<__hip_bfloat16, NG, true, false, false, LEAN>(preds, target, n, C, C, ignore_index, has_ignore, codes, n_pad, confmat, err,
+                                                            true, saw_bad, slow, s_tile, tile, row_stats);
+    else
+      row_tile<__hip_bfloat16, NG, false, false, false, LEAN>(preds, target, n, C, C, ignore_index, has_ignore, codes, n_pad, confmat, err,
+                                                             true, saw_bad, slow, s_tile, tile, row_stats);
+  }
+  if (__syncthreads_or(saw_bad) && threadIdx.x == 0) atomicOr(verdict, 1);
+}
+
+template <typename F>
+float time_us(F f, int iters = 50) {
+  for (int i = 0; i < 5; ++i) f();
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
+  CK(hipEventRecord(a));
+  for (int i = 0; i < iters; ++i) f();
+  CK(hipEventRecord(b));
+  CK(hipEventSynchronize(b));
+  float ms; CK(hipEventElapsedTime(&ms, a, b));
+  return ms * 1000.f / iters;
+}
+
+struct Bufs {
+  uint32_t* codes; int64_t* cm; int* err; int* rows; int* cnt; float4* stats; int* verdict;
+};
+
+template <int NG>
+static void launch(bool lean, const __hip_bfloat16* x, const int64_t* t, int64_t N, int C, int ign, const Bufs& B, int64_t n_pad) {
+  const int64_t ntiles = n_pad / kTileRows;
+  const int grid = (int)((ntiles + 7) / 8 * 8);
+  const size_t shm = (size_t)512 * NG * kSlots * 4;
+  if (lean)
+    hipLaunchKernelGGL((rp_kernel<true, NG>), grid, kRowThreads, shm, 0, x, t, N, C, 1, -100, ign != 0, B.codes, n_pad, B.cm, B.err, B.rows,
+                       B.cnt, B.stats, B.verdict);
+  else
+    hipLaunchKernelGGL((rp_kernel<false, NG>), grid, kRowThreads, shm, 0, x, t, N, C, 1, -100, ign != 0, B.codes, n_pad, B.cm, B.err, B.rows,
+                       B.cnt, B.stats, B.verdict);
+}
+
+int main(int argc, char** argv) {
+  const int64_t N = argc > 1 ? atoll(argv[1]) : 65536;
+  const int64_t n_pad = (N + kTileRows - 1) / kTileRows * kTileRows;
+  printf("{\"N\": %lld", (long long)N);
+  int64_t total_bad = 0;
+  for (int C : {1000, 256}) {
+    const int NG = C > 512 ? 2 : 1;
+    std::vector<uint16_t> h(N * C);
+    std::vector<int64_t> ht(N), hti(N);
+    srand(7 + C);
+    for (int64_t i = 0; i < N * C; ++i) {
+      float u1 = (rand() + 1.f) / (RAND_MAX + 2.f), u2 = (rand() + 1.f) / (RAND_MAX + 2.f);
+      h[i] = f2bf(2.f * sqrtf(-2.f * logf(u1)) * cosf(6.2831853f * u2));
+    }
+    for (int64_t i = 0; i < N; ++i) { ht[i] = rand() % C; hti[i] = (i % 7 == 3) ? -100 : ht[i]; }
+    std::vector<uint16_t> hw = h, hn = h;
+    for (int64_t i = 0; i < N * C; ++i) { float v; uint32_t u = (uint32_t)h[i] << 16; memcpy(&v, &u, 4); hw[i] = f2bf(v * 40.f); }
+    for (int64_t r = 5; r < N; r += 997) hn[r * C + (r % C)] = 0x7FC0;                          // NaN
+    for (int64_t r = 11; r < N; r += 1999) hn[r * C + ((r * 7) % C)] = 0x7F80;                  // +inf
+    for (int64_t r = 13; r < N; r += 29) hn[r * C + ((r * 3) % C)] = 0xFF80;                    // one -inf (finite max)
+    for (int64_t r = 17; r < N; r += 4001) for (int c = 0; c < C; ++c) hn[r * C + c] = 0xFF80;  // all -inf
+    for (int64_t r = 23; r < N; r += 503) hn[r * C + 3] = hn[r * C + 1] = 0x4300;               // tie at the max (128.0)
+    for (int64_t r = 31; r < N; r += 61) hn[r * C + ((r * 5) % C)] = 0x42C8;                    // one logit 100: gap > 86
+    __hip_bfloat16* dx; int64_t *dt, *dti;
+    const size_t xbytes = (size_t)N * C * 2, cbytes = (size_t)C * n_pad * 2;
+    CK(hipMalloc(&dx, xbytes)); CK(hipMalloc(&dt, N * 8)); CK(hipMalloc(&dti, N * 8));
+    CK(hipMemcpy(dt, ht.data(), N * 8, hipMemcpyHostToDevice)); CK(hipMemcpy(dti, hti.data(), N * 8, hipMemcpyHostToDevice));
+    Bufs B[2];
+    for (auto& b : B) {
+      CK(hipMalloc(&b.codes, cbytes)); CK(hipMalloc(&b.cm, (size_t)C * C * 8)); CK(hipMalloc(&b.err, 4)); CK(hipMalloc(&b.rows, 2 * N * 4));
+      CK(hipMalloc(&b.cnt, 8)); CK(hipMalloc(&b.stats, N * 16)); CK(hipMalloc(&b.verdict, 4));
+    }
+    struct Case { const char* name; const std::vector<uint16_t>* x; bool ign; };
+    Case cases[] = {{"randn", &h, false}, {"wide_x40", &hw, false}, {"special_rows", &hn, false}, {"special_ignore", &hn, true}};
+    for (const Case& cs : cases) {
+      CK(hipMemcpy(dx, cs.x->data(), xbytes, hipMemcpyHostToDevice));
+      for (int v = 0; v < 2; ++v) {
+        CK(hipMemset(B[v].codes, 0xAB, cbytes)); CK(hipMemset(B[v].cm, 0, (size_t)C * C * 8)); CK(hipMemset(B[v].err, 0, 4));
+        CK(hipMemset(B[v].cnt, 0, 8)); CK(hipMemset(B[v].stats, 0, N * 16)); CK(hipMemset(B[v].verdict, 0, 4));
+        if (NG == 2) launch<2>(v == 1, dx, cs.ign ? dti : dt, N, C, cs.ign, B[v], n_pad);
+        else launch<1>(v == 1, dx, cs.ign ? dti : dt, N, C, cs.ign, B[v], n_pad);
+      }
+      CK(hipDeviceSynchronize());
+      std::vector<uint16_t> c0(cbytes / 2), c1(cbytes / 2);
+      std::vector<int64_t> m0(C * C), m1(C * C);
+      std::vector<float> s0(N * 4), s1(N * 4);
+      int cnt[2][2], vd[2];
+      CK(hipMemcpy(c0.data(), B[0].codes, cbytes, hipMemcpyDeviceToHost)); CK(hipMemcpy(c1.data(), B[1].codes, cbytes, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(m0.data(), B[0].cm, (size_t)C * C * 8, hipMemcpyDeviceToHost)); CK(hipMemcpy(m1.data(), B[1].cm, (size_t)C * C * 8, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(s0.data(), B[0].stats, N * 16, hipMemcpyDeviceToHost)); CK(hipMemcpy(s1.data(), B[1].stats, N * 16, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(cnt[0], B[0].cnt, 8, hipMemcpyDeviceToHost)); CK(hipMemcpy(cnt[1], B[1].cnt, 8, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(&vd[0], B[0].verdict, 4, hipMemcpyDeviceToHost)); CK(hipMemcpy(&vd[1], B[1].verdict, 4, hipMemcpyDeviceToHost));
+      std::vector<int> r0(cnt[0][0]), r1(cnt[1][0]);
+      if (!r0.empty()) CK(hipMemcpy(r0.data(), B[0].rows, r0.size() * 4, hipMemcpyDeviceToHost));
+      if (!r1.empty()) CK(hipMemcpy(r1.data(), B[1].rows, r1.size() * 4, hipMemcpyDeviceToHost));
+      std::sort(r0.begin(), r0.end()); std::sort(r1.begin(), r1.end());
+      int64_t code_diff = 0, cm_diff = 0, stat_diff = 0;
+      for (int c = 0; c < C; ++c)
+        for (int64_t r = 0; r < N; ++r) code_diff += c0[c * n_pad + r] != c1[c * n_pad + r];
+      for (int64_t i = 0; i < (int64_t)C * C; ++i) cm_diff += m0[i] != m1[i];
+      for (int64_t i = 0; i < N * 4; ++i) stat_diff += memcmp(&s0[i], &s1[i], 4) != 0;
+      const bool rows_same = r0 == r1;
+      total_bad += code_diff + cm_diff + stat_diff + !rows_same + (vd[0] != vd[1]);
+      printf(", \"C%d_%s\": {\"code_diffs\": %lld, \"confmat_diffs\": %lld, \"stat_diffs\": %lld, \"slow_rows\": [%zu, %zu], \"rows_same\": %s, "
+             "\"verdict\": [%d, %d]}",
+             C, cs.name, (long long)code_diff, (long long)cm_diff, (long long)stat_diff, r0.size(), r1.size(), rows_same ? "true" : "false",
+             vd[0], vd[1]);
+    }
+    // timing: randn logits (production grid, statistics on)
+    CK(hipMemcpy(dx, h.data(), xbytes, hipMemcpyHostToDevice));
+    float tp = 0, tl = 0;
+    for (int rep = 0; rep < 3; ++rep) {  // interleaved reps: clock drift hits both arms
+      tp += time_us([&] { if (NG == 2) launch<2>(false, dx, dt, N, C, 0, B[0], n_pad); else launch<1>(false, dx, dt, N, C, 0, B[0], n_pad); });
+      tl += time_us([&] { if (NG == 2) launch<2>(true, dx, dt, N, C, 0, B[1], n_pad); else launch<1>(true, dx, dt, N, C, 0, B[1], n_pad); });
+    }
+    printf(", \"C%d_us\": {\"production\": %.2f, \"lean\": %.2f}", C, tp / 3, tl / 3);
+    CK(hipFree(dx)); CK(hipFree(dt)); CK(hipFree(dti));
+    for (auto& b : B) { CK(hipFree(b.codes)); CK(hipFree(b.cm)); CK(hipFree(b.err)); CK(hipFree(b.rows)); CK(hipFree(b.cnt)); CK(hipFree(b.stats)); CK(hipFree(b.verdict)); }
+  }
+  printf(", \"all_identical\": %s}\n", total_bad == 0 ? "true" : "false");
+  return total_bad == 0 ? 0 : 3;
+}
