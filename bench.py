@@ -10,7 +10,7 @@ reported.  ``value`` = world_size * K / max_rank_seconds (whole-job aggregate, w
 
 Usage::
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config auroc|map|image|bert]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config auroc|map|image|bert|plumbing]
 
 * ``--gpus 1`` (default): one process.
 * ``--gpus N`` without ``WORLD_SIZE`` in the environment: this process launches ``torch.distributed.run`` with N
@@ -19,7 +19,9 @@ Usage::
   (``nccl`` backend) when a GPU is visible, gloo on CPU-only hosts.
 
 Secondary BASELINE configs (``--config map|image|bert``) are implemented in ``tools/config_bench.py`` and print one
-JSON line in the same format.
+JSON line in the same format.  ``--config plumbing`` is BASELINE config 1 (``MulticlassAccuracy(num_classes=5)``,
+batch 10, CPU, 2 gloo ranks, one thread each): ``tools/plumbing_bench.py`` times K ``update`` calls + one ``compute``
+and, on a second line, K ``forward`` calls + one ``compute`` (``--impl ref`` there runs the unmodified reference).
 """
 import argparse
 import json
@@ -78,7 +80,7 @@ def _parse(argv: list) -> argparse.Namespace:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", default="auroc", choices=["auroc", "map", "image", "bert"])
+    ap.add_argument("--config", default="auroc", choices=["auroc", "map", "image", "bert", "plumbing"])
     ap.add_argument("--num-classes", type=int, default=1000)
     ap.add_argument("--batch", type=int, default=65536)
     ap.add_argument("--pool", type=int, default=4, help="distinct synthetic batches cycled through")
@@ -216,9 +218,37 @@ def _worker(args: argparse.Namespace) -> None:
         dist.destroy_process_group()
 
 
+def _plumbing(args: argparse.Namespace) -> None:
+    """BASELINE config 1 on the CPU: 2 gloo ranks (spawned here; no GPU is touched), update and forward modes."""
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "tools"))
+    import contextlib
+    import io
+
+    import plumbing_bench
+
+    steps = args.steps if args.steps != 50 else 2000  # the default K of the GPU configs is too short a CPU window
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        plumbing_bench.main(["--impl", "tmx", "--mode", "both", "--steps", str(steps), "--warmup", str(max(args.warmup, 50)), "--world", "2"])
+    for line in buf.getvalue().splitlines():
+        r = json.loads(line)
+        out = {
+            "metric": r["metric"], "value": r["value"], "unit": "updates/s", "n_gpus": 0, "n_ranks": r["n_ranks"],
+            "steps": r["steps"], "warmup": r["warmup"], "ms_per_step": round(r["us_per_step_incl_compute"] / 1000.0, 5),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": r["data"],
+            "config": {"model": "MulticlassAccuracy(num_classes=5)", "global_batch": 10 * r["n_ranks"], "seq_len": 1,
+                       "parallelism": "gloo dp2 (CPU)"},
+            "us_per_step_loop_only": r["us_per_step_loop_only"], "compute_incl_sync_us": r["compute_incl_sync_us"],
+        }
+        print(json.dumps(out), flush=True)
+
+
 def main() -> None:
     argv = sys.argv[1:]
     args = _parse(argv)
+    if args.config == "plumbing":
+        _plumbing(args)
+        return
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         # launcher: N ranks as a child process group; this process never initialises the GPU
         sys.exit(_launch_ranks(args.gpus, argv))

@@ -1298,7 +1298,7 @@ void launch_small_two_pass(const T* p, const int64_t* target, int64_t n, int C, 
 template <typename T, bool PADDED>
 void launch_row_pass(const T* p, const int64_t* target, int64_t n, int C, int ld, int* mode, int* state, bool speculative,
                      int64_t ignore_index, bool has_ignore, int64_t* cm, int* err, uint32_t* cptr, int* srows,
-                     bool roll_in_class_pass = false, float4* row_stats = nullptr) {
+                     bool roll_in_class_pass = false, float4* row_stats = nullptr, PosSink pos = PosSink{}) {
   TORCH_CHECK(n < (int64_t{1} << 31), "curve_hist_update: more than 2^31 rows in one batch");
   const int64_t n_pad = (n + kTileRows - 1) / kTileRows * kTileRows;
   const int64_t ntiles = n_pad / kTileRows;
@@ -1307,9 +1307,10 @@ void launch_row_pass(const T* p, const int64_t* target, int64_t n, int C, int ld
   const size_t shm = (size_t)512 * (C > 512 ? 2 : 1) * kSlots * sizeof(uint32_t);  // 32 / 64 KiB -> 2 blocks per CU
   // with row_stats the class pass refits a mispredicted batch itself: no FIXUP launch
   const bool fixup = speculative && row_stats == nullptr;
+  TORCH_CHECK(!fixup || pos.hist == nullptr, "curve row pass: positive booking needs the refit route (row statistics)");
   if (C > 512) {
     hipLaunchKernelGGL((mc_codes_kernel<T, false, 2, PADDED>), grid, kRowThreads, shm, stream(), p, target, n, C, ld, mode, ignore_index,
-                       has_ignore, cptr, n_pad, cm, err, speculative, srows, state, row_stats);
+                       has_ignore, cptr, n_pad, cm, err, speculative, srows, state, row_stats, pos);
     TMX_LAUNCH_CHECK();
     if (fixup) {
       hipLaunchKernelGGL((mc_codes_kernel<T, true, 2, PADDED>), fixup_grid, kRowThreads, shm, stream(), p, target, n, C, ld, mode,
@@ -1318,7 +1319,7 @@ void launch_row_pass(const T* p, const int64_t* target, int64_t n, int C, int ld
     }
   } else {
     hipLaunchKernelGGL((mc_codes_kernel<T, false, 1, PADDED>), grid, kRowThreads, shm, stream(), p, target, n, C, ld, mode, ignore_index,
-                       has_ignore, cptr, n_pad, cm, err, speculative, srows, state, row_stats);
+                       has_ignore, cptr, n_pad, cm, err, speculative, srows, state, row_stats, pos);
     TMX_LAUNCH_CHECK();
     if (fixup) {
       hipLaunchKernelGGL((mc_codes_kernel<T, true, 1, PADDED>), fixup_grid, kRowThreads, shm, stream(), p, target, n, C, ld, mode,
@@ -1332,27 +1333,33 @@ void launch_row_pass(const T* p, const int64_t* target, int64_t n, int C, int ld
   }
 }
 
+// TMX_CLASS_PASS_U16=1: the round-4 class pass (16-bit-packed LDS bins, positives flagged in the codes) for A/B runs
+static bool class_pass_u16() {
+  static const bool u16 = [] { const char* v = std::getenv("TMX_CLASS_PASS_U16"); return v != nullptr && v[0] == '1'; }();
+  return u16;
+}
+
 // Class pass of the multiclass two-pass route.  ``bmode`` = the batch's (used, real) mode pair (state + 3 after a
-// speculative row pass, else the pre-pass flag with speculative = false).
+// speculative row pass, else the pre-pass flag with speculative = false).  ``pos_booked``: the row pass booked the
+// positives itself (PosSink) and left their codes skipped.
 template <typename T>
 void launch_class_pass(const uint32_t* cptr, int64_t n, int C, int ld, const T* p, const int64_t* target, const int* bmode,
                        bool speculative, const int* srows, int* state, int64_t* hist, int64_t* cm, int* code_range,
                        int* roll_mode = nullptr, int64_t* batch_hist = nullptr, int* batch_range = nullptr,
-                       const float4* row_stats = nullptr) {
+                       const float4* row_stats = nullptr, bool pos_booked = false) {
   const int64_t n_pad = (n + kTileRows - 1) / kTileRows * kTileRows;
   // row splits only when there are too few classes to fill the chip (exclusive-owner flush when splits == 1)
   int splits = 1;
   while ((int64_t)C * splits < 512 && n_pad / (8 * (splits * 2)) >= 1024) splits *= 2;
-  // windowed u32 LDS histogram, 512-thread workgroups, four per CU (csrc/curve_hist_kernels.h class_hist_hi_kernel;
-  // TMX_CLASS_PASS_U16=1 selects the round-4 16-bit-packed form for A/B runs)
-  static const bool u16 = [] { const char* v = std::getenv("TMX_CLASS_PASS_U16"); return v != nullptr && v[0] == '1'; }();
-  if (!u16) {
+  // windowed u32 LDS histogram, 512-thread workgroups, four per CU (csrc/curve_hist_kernels.h class_hist_hi_kernel)
+  if (!class_pass_u16()) {
     hipLaunchKernelGGL((class_hist_hi_kernel<T>), C * splits, kClassThreadsU16, kHiLdsBytes, stream(),
                        reinterpret_cast<const uint16_t*>(cptr), n_pad, splits, hist, p, ld, target, n, bmode, speculative,
-                       srows, state, cm, code_range, roll_mode, batch_hist, batch_range, row_stats);
+                       srows, state, cm, code_range, roll_mode, batch_hist, batch_range, row_stats, pos_booked);
     TMX_LAUNCH_CHECK();
     return;
   }
+  TORCH_CHECK(!pos_booked, "curve class pass: the u16 form needs positives flagged in the codes");
   hipLaunchKernelGGL((class_hist_u16_kernel<T>), C * splits, kClassThreadsU16, kCodes / 2 * sizeof(uint32_t), stream(),
                      reinterpret_cast<const uint16_t*>(cptr), n_pad, splits, hist, p, ld, target, n, bmode, speculative,
                      srows, state, cm, code_range, roll_mode, batch_hist, batch_range, row_stats);
@@ -1415,9 +1422,13 @@ void launch_two_pass(const T* p, const int64_t* target, int64_t n, int C, int ld
   uint32_t* cptr = reinterpret_cast<uint32_t*>(codes.data_ptr());
   int* srows = slow_rows.data_ptr<int>();
   // single stream: the class pass reads the (used, real) pair straight from ``mode`` and its last workgroup rolls it
-  launch_row_pass<T, PADDED>(p, target, n, C, ld, mode, state, speculative, ignore_index, has_ignore, cm, err, cptr, srows, true, rstats);
+  // the row pass books each row's positive itself (class pass: negatives only)
+  const bool book = !class_pass_u16() && (rstats != nullptr || !speculative);
+  const PosSink pos = book ? PosSink{hist, batch_hist, code_range, batch_range} : PosSink{};
+  launch_row_pass<T, PADDED>(p, target, n, C, ld, mode, state, speculative, ignore_index, has_ignore, cm, err, cptr, srows, true, rstats,
+                             pos);
   launch_class_pass<T>(cptr, n, C, ld, p, target, mode, speculative, srows, state, hist, cm, code_range, speculative ? mode : nullptr,
-                       batch_hist, batch_range, rstats);
+                       batch_hist, batch_range, rstats, book);
 }
 
 // The row pass alone into caller-owned scratch (class-major codes + rare-row list): the per-element code pin of

@@ -409,13 +409,74 @@ __device__ __forceinline__ void row_tile_load(const T* __restrict__ preds, const
     }
 }
 
+// Positive booking by the row pass (round 5).  The row pass knows each row's positive (its target); instead of
+// flagging it with bit 14 for the class pass to find (a test of every code there: ~40 % of the class pass's 16-B vectors
+// carry one at C = 1000), lane i < 4 of each wave marks its row's positive skipped in the LDS image (a returning
+// ds_or) and books the code into the int64 positive bins of the target class and its code range (no-return atomics;
+// the tile's barrier waits for LDS only, so nothing waits for them).  Values kept alive across the barrier, or range
+// words prefetched at the tile's start, cost ~5 us at this kernel's 128-VGPR edge (profiles/kexp_headline_r5.json).
+// The booked code goes to row_stats[r].w (code | 0x10000; 0 = none) so the class pass can take it back when it refits
+// a mis-speculated batch.  hist == nullptr: the bit-14 flag as before (test op, FIXUP route, u16 pass).
+struct PosSink {
+  int64_t* hist;    // [C][2][kCodes]: the positive half of class t is hist + (2 t + 1) kCodes
+  int64_t* bhist;   // forward()'s batch histogram or nullptr
+  int* range;       // [C][2] occupied code range of hist (nullptr: not tracked)
+  int* brange;      // [C][2] of bhist
+};
+
+struct PosTake {  // lane i < 4: row i of the wave's four rows
+  int64_t r, t;
+  uint32_t code;  // code | 0x10000 when booked
+  int lo, hi, blo, bhi;
+};
+
+// before the tile's barrier (the wave's own image writes are done): mark the positive skipped, keep its code
+__device__ __forceinline__ void pos_take(PosTake& pt, uint32_t* __restrict__ s_tile, const bool (&keepv)[4], const int64_t (&tt)[4], int C,
+                                         int wave, int64_t row00, int64_t n) {
+  const int lane = threadIdx.x & (kWave - 1);
+  if (lane >= 4) return;
+  const bool k = lane == 0 ? keepv[0] : lane == 1 ? keepv[1] : lane == 2 ? keepv[2] : keepv[3];
+  const int64_t t = lane == 0 ? tt[0] : lane == 1 ? tt[1] : lane == 2 ? tt[2] : tt[3];
+  const int p = wave + (lane >> 1) * kRowWaves;
+  const int half = lane & 1;
+  const int64_t r = row00 + 2 * (int64_t)(lane >> 1) * kRowWaves + half;
+  if (r >= n || !k || t < 0 || t >= C) return;
+  const int idx = (int)t * kSlots + (p ^ ((int)(t >> 3) & (kSlots - 1)));
+  const uint32_t code = (atomicOr(&s_tile[idx], 0x8000u << (16 * half)) >> (16 * half)) & 0xFFFFu;
+  pt.r = r;
+  if (!(code & 0x8000u)) pt.code = code | 0x10000u;  // an out-of-range score (probability mode) counts nowhere
+}
+
+// after the tile's barrier and store: the global side of the booking
+#ifndef TMX_POS_ABL
+#define TMX_POS_ABL 0  // kernel-harness ablation (tools/kexp): 1 no global booking, 2 no range words, 4 no row_stats word,
+                       // 8 no bin atomic.  0 in the library.
+#endif
+__device__ __forceinline__ void pos_book(const PosTake& pt, const PosSink& pos, float4* __restrict__ row_stats) {
+  if (pos.hist == nullptr || (threadIdx.x & (kWave - 1)) >= 4 || !(pt.code & 0x10000u)) return;
+  if (TMX_POS_ABL & 1) return;
+  const int64_t t = pt.t;
+  const int code = static_cast<int>(pt.code & 0xFFFFu);
+  if (!(TMX_POS_ABL & 8)) atomic_add_i64(pos.hist + (2 * t + 1) * kCodes + code, 1);
+  if (pos.bhist != nullptr) atomic_add_i64(pos.bhist + (2 * t + 1) * kCodes + code, 1);
+  if (pos.range != nullptr && !(TMX_POS_ABL & 2)) {
+    if (code < pt.lo) atomicMin(pos.range + 2 * t, code);
+    if (code > pt.hi) atomicMax(pos.range + 2 * t + 1, code);
+  }
+  if (pos.brange != nullptr) {
+    if (code < pt.blo) atomicMin(pos.brange + 2 * t, code);
+    if (code > pt.bhi) atomicMax(pos.brange + 2 * t + 1, code);
+  }
+  if (row_stats != nullptr && !(TMX_POS_ABL & 4)) reinterpret_cast<uint32_t*>(row_stats + pt.r)[3] = pt.code;
+}
+
 // Compute half of a tile: codes into the LDS image, confusion matrix / error / rare-row side effects.  The caller
 // stores the image (after a barrier).
 template <typename T, int NG, bool SOFTMAX, bool FIXUP, bool PADDED>
 __device__ __forceinline__ void row_tile_compute(const RowLoads<NG>& L, int64_t n, int C, int ld, int64_t ignore_index, bool has_ignore,
                                                  int64_t* __restrict__ confmat, int* __restrict__ err, bool rec, bool& saw_bad,
                                                  SlowRows slow, uint32_t* __restrict__ s_tile, int64_t tile,
-                                                 float4* __restrict__ row_stats = nullptr) {
+                                                 float4* __restrict__ row_stats, const PosSink& pos, PosTake& ptake) {
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = threadIdx.x / kWave;
   const int nvec = ld / 8;
@@ -433,6 +494,7 @@ __device__ __forceinline__ void row_tile_compute(const RowLoads<NG>& L, int64_t 
   int64_t tt[4];
   int am[4];
   bool keepv[4], slowv[4], validv[4];
+  ptake = PosTake{-1, tv, 0u, kCodes, -1, kCodes, -1};
 #pragma unroll
   for (int pp = 0; pp < 2; ++pp) {
     const int p = wave + pp * kRowWaves;
@@ -508,7 +570,7 @@ __device__ __forceinline__ void row_tile_compute(const RowLoads<NG>& L, int64_t 
       const int c = 512 * (j >> 3) + 8 * lane + (j & 7);
       s_tile[c * kSlots + (p ^ (lane & (kSlots - 1)))] = (packed & keep) | setm;
     }
-    if (lane == 0) {
+    if (lane == 0 && pos.hist == nullptr) {
       if (ka && ta >= 0 && ta < C) atomicOr(&s_tile[ta * kSlots + (p ^ ((int)(ta >> 3) & (kSlots - 1)))], 0x00004000u);
       if (kb && tb >= 0 && tb < C) atomicOr(&s_tile[tb * kSlots + (p ^ ((int)(tb >> 3) & (kSlots - 1)))], 0x40000000u);
     }
@@ -517,6 +579,10 @@ __device__ __forceinline__ void row_tile_compute(const RowLoads<NG>& L, int64_t 
     keepv[2 * pp] = ka; keepv[2 * pp + 1] = kb;
     slowv[2 * pp] = slow_a; slowv[2 * pp + 1] = slow_b;
     validv[2 * pp] = va; validv[2 * pp + 1] = vb;
+  }
+  if (pos.hist != nullptr) {
+    pos_take(ptake, s_tile, keepv, tt, C, wave, row0_of(0), n);
+    pos_book(ptake, pos, row_stats);
   }
   // global side effects after every load has been consumed
   if (lane == 0) {
@@ -584,7 +650,7 @@ template <typename T, int NG>
 __device__ __forceinline__ void row_tile_softmax_lean(const RowLoads<NG>& L, int64_t n, int C, int ld, int64_t ignore_index,
                                                       bool has_ignore, int64_t* __restrict__ confmat, int* __restrict__ err, bool rec,
                                                       bool& saw_bad, SlowRows slow, uint32_t* __restrict__ s_tile, int64_t tile,
-                                                      float4* __restrict__ row_stats) {
+                                                      float4* __restrict__ row_stats, const PosSink& pos, PosTake& ptake) {
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = threadIdx.x / kWave;
   const int nvec = ld / 8;
@@ -600,6 +666,7 @@ __device__ __forceinline__ void row_tile_softmax_lean(const RowLoads<NG>& L, int
   int64_t tt[4];
   int am[4];
   bool keepv[4], slowv[4], validv[4];
+  ptake = PosTake{-1, tv, 0u, kCodes, -1, kCodes, -1};
 #pragma unroll
   for (int pp = 0; pp < 2; ++pp) {
     const int p = wave + pp * kRowWaves;
@@ -709,7 +776,7 @@ __device__ __forceinline__ void row_tile_softmax_lean(const RowLoads<NG>& L, int
         s_tile[c * kSlots + (p ^ (lane & (kSlots - 1)))] = (pack_rne2<T>(div_rn2(P[j], s2, i2)) & keep) | setm;
       }
     }
-    if (lane == 0) {
+    if (lane == 0 && pos.hist == nullptr) {
       if (ka && ta >= 0 && ta < C) atomicOr(&s_tile[ta * kSlots + (p ^ ((int)(ta >> 3) & (kSlots - 1)))], 0x00004000u);
       if (kb && tb >= 0 && tb < C) atomicOr(&s_tile[tb * kSlots + (p ^ ((int)(tb >> 3) & (kSlots - 1)))], 0x40000000u);
     }
@@ -718,6 +785,10 @@ __device__ __forceinline__ void row_tile_softmax_lean(const RowLoads<NG>& L, int
     keepv[2 * pp] = ka; keepv[2 * pp + 1] = kb;
     slowv[2 * pp] = slow_a; slowv[2 * pp + 1] = slow_b;
     validv[2 * pp] = va; validv[2 * pp + 1] = vb;
+  }
+  if (pos.hist != nullptr) {
+    pos_take(ptake, s_tile, keepv, tt, C, wave, row0_of(0), n);
+    pos_book(ptake, pos, row_stats);
   }
   if (lane == 0) {
 #pragma unroll
@@ -734,19 +805,32 @@ __device__ __forceinline__ void row_tile_softmax_lean(const RowLoads<NG>& L, int
 #define TMX_ROWPASS_LEAN 1
 #endif
 
+#ifndef TMX_ROW_RAW_BARRIER
+#define TMX_ROW_RAW_BARRIER 0  // measured: no difference (profiles/kexp_headline_r5.json)
+#endif
+
 template <typename T, int NG, bool SOFTMAX, bool FIXUP, bool PADDED, bool LEAN = (TMX_ROWPASS_LEAN != 0)>
 __device__ __forceinline__ void row_tile(const T* __restrict__ preds, const int64_t* __restrict__ target, int64_t n, int C, int ld,
                                           int64_t ignore_index, bool has_ignore, uint32_t* __restrict__ codes, int64_t n_pad,
                                           int64_t* __restrict__ confmat, int* __restrict__ err, bool rec, bool& saw_bad,
-                                          SlowRows slow, uint32_t* __restrict__ s_tile, int64_t tile, float4* __restrict__ row_stats) {
+                                          SlowRows slow, uint32_t* __restrict__ s_tile, int64_t tile, float4* __restrict__ row_stats,
+                                          PosSink pos = PosSink{}) {
   RowLoads<NG> L;
   row_tile_load<T, NG>(preds, target, n, ld, tile, L);
+  PosTake ptake;
+  if constexpr (FIXUP) pos = PosSink{};
   if constexpr (LEAN && SOFTMAX && !FIXUP && !PADDED)
-    row_tile_softmax_lean<T, NG>(L, n, C, ld, ignore_index, has_ignore, confmat, err, rec, saw_bad, slow, s_tile, tile, row_stats);
+    row_tile_softmax_lean<T, NG>(L, n, C, ld, ignore_index, has_ignore, confmat, err, rec, saw_bad, slow, s_tile, tile, row_stats, pos, ptake);
   else
     row_tile_compute<T, NG, SOFTMAX, FIXUP, PADDED>(L, n, C, ld, ignore_index, has_ignore, confmat, err, rec, saw_bad, slow, s_tile, tile,
-                                                    row_stats);
+                                                    row_stats, pos, ptake);
+  // the image is complete once every wave's LDS writes are: a bare s_barrier after lgkmcnt(0).  __syncthreads() would
+  // also wait (vmcnt(0)) for the global atomics just issued (confusion matrix, positive bins), ~1-2 us per tile
+#if TMX_ROW_RAW_BARRIER
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#else
   __syncthreads();
+#endif
   store_tile<NG>(s_tile, codes, C, n_pad, tile);
 }
 
@@ -761,7 +845,8 @@ __device__ __forceinline__ void mc_codes_block(int64_t vb, int64_t vgrid, const 
                                                int64_t n, int C, int ld, int* __restrict__ mode, int64_t ignore_index, bool has_ignore,
                                                uint32_t* __restrict__ codes, int64_t n_pad, int64_t* __restrict__ confmat,
                                                int* __restrict__ err, bool record_mode, int* __restrict__ slow_rows,
-                                               int* __restrict__ slow_count, float4* __restrict__ row_stats) {
+                                               int* __restrict__ slow_count, float4* __restrict__ row_stats,
+                                               PosSink pos = PosSink{}) {
   extern __shared__ __attribute__((aligned(16))) uint32_t s_tile[];  // [512 * NG][kSlots]
   int use_mode;
   if constexpr (FIXUP) {
@@ -786,10 +871,10 @@ __device__ __forceinline__ void mc_codes_block(int64_t vb, int64_t vgrid, const 
     if (tile >= ntiles) return;
     if (use_mode != 0)
       row_tile<T, NG, true, FIXUP, PADDED>(preds, target, n, C, ld, ignore_index, has_ignore, codes, n_pad, confmat, err, rec, saw_bad, slow, s_tile, tile,
-                                           row_stats);
+                                           row_stats, pos);
     else
       row_tile<T, NG, false, FIXUP, PADDED>(preds, target, n, C, ld, ignore_index, has_ignore, codes, n_pad, confmat, err, rec, saw_bad, slow, s_tile, tile,
-                                            row_stats);
+                                            row_stats, pos);
   };
   if constexpr (FIXUP) {  // rare: blocks stride over the tiles (small grid, cheap early exit)
     for (int64_t b = vb; b < per_xcd * 8; b += vgrid) {
@@ -813,9 +898,10 @@ __global__ void __launch_bounds__(kRowThreads, 4) mc_codes_kernel(const T* __res
                                                                     uint32_t* __restrict__ codes, int64_t n_pad,
                                                                     int64_t* __restrict__ confmat, int* __restrict__ err,
                                                                     bool record_mode, int* __restrict__ slow_rows,
-                                                                    int* __restrict__ slow_count, float4* __restrict__ row_stats = nullptr) {
+                                                                    int* __restrict__ slow_count, float4* __restrict__ row_stats = nullptr,
+                                                                    PosSink pos = PosSink{}) {
   mc_codes_block<T, FIXUP, NG, PADDED>(blockIdx.x, gridDim.x, preds, target, n, C, ld, mode, ignore_index, has_ignore, codes, n_pad,
-                                       confmat, err, record_mode, slow_rows, slow_count, row_stats);
+                                       confmat, err, record_mode, slow_rows, slow_count, row_stats, pos);
 }
 
 // Multilabel row pass: the same tile / LDS image / class-major scratch as the multiclass row pass, but every element
@@ -1381,6 +1467,22 @@ __device__ __forceinline__ void hi_count4(const uint4& v) {
   }
 }
 
+// Last workgroup of a class-pass launch: reset the batch state words and roll the speculation (every workgroup read
+// them before its ticket; class_hist_block)
+__device__ __forceinline__ void class_hi_ticket(int* __restrict__ state, int* __restrict__ roll_mode, int64_t vgrid) {
+  if (threadIdx.x == 0) {
+    if (__hip_atomic_fetch_add(state + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)vgrid - 1) {
+      state[0] = state[1] = 0;
+      state[2] = 0;
+      if (roll_mode != nullptr) {
+        const int mr = roll_mode[1];
+        roll_mode[0] = mr;
+        roll_mode[1] = 0;
+      }
+    }
+  }
+}
+
 template <typename T, int NT>
 __device__ __forceinline__ void class_hist_hi_block(int64_t vb, int64_t vgrid, const uint16_t* __restrict__ codes, int64_t n_pad, int splits,
                                                     int64_t* __restrict__ hist, const T* __restrict__ preds, int ld,
@@ -1388,7 +1490,7 @@ __device__ __forceinline__ void class_hist_hi_block(int64_t vb, int64_t vgrid, c
                                                     bool speculative, const int* __restrict__ slow_rows, int* __restrict__ state,
                                                     int64_t* __restrict__ confmat, int* __restrict__ code_range, int* __restrict__ roll_mode,
                                                     int64_t* __restrict__ batch_hist, int* __restrict__ batch_range,
-                                                    const float4* __restrict__ row_stats) {
+                                                    const float4* __restrict__ row_stats, bool pos_booked) {
   extern __shared__ __attribute__((aligned(16))) uint32_t s_h[];  // [kHiWords] words, at LDS address 0
   int lo = kCodes, hi = -1;
   const int C = static_cast<int>(vgrid / splits);
@@ -1427,7 +1529,26 @@ __device__ __forceinline__ void class_hist_hi_block(int64_t vb, int64_t vgrid, c
         } else if (fl & 1u) {
           code = raw_code<T>(bits16<T>(xv));
         }
-        if (!(code & 0x8000u) && target[r] == c) code |= 0x4000u;
+        if (target[r] == c) {
+          if (pos_booked) {
+            // the row pass booked this row's positive with the mis-speculated mode's code: take it back, book the
+            // refit code, and leave the code skipped for the count below
+            const uint32_t booked = __float_as_uint(st.w);
+            if (booked & 0x10000u) {
+              atomic_add_i64(pos_hist + (booked & 0xFFFFu), -1);
+              if (bpos != nullptr) atomic_add_i64(bpos + (booked & 0xFFFFu), -1);
+            }
+            if (!(code & 0x8000u)) {
+              atomic_add_i64(pos_hist + code, 1);
+              if (bpos != nullptr) atomic_add_i64(bpos + code, 1);
+              lo = min(lo, (int)code);
+              hi = max(hi, (int)code);
+              code = 0x8000u;
+            }
+          } else if (!(code & 0x8000u)) {
+            code |= 0x4000u;
+          }
+        }
       }
       ccol[r] = static_cast<uint16_t>(code);
     }
@@ -1453,16 +1574,20 @@ __device__ __forceinline__ void class_hist_hi_block(int64_t vb, int64_t vgrid, c
   // this step is counted, so a workgroup streams instead of alternating load and count phases.  EXACT: the slice is a
   // whole number of steps (65536-row classes: 4 steps of 4 vectors per thread), no bounds tests.
   constexpr int64_t kStep = (int64_t)kHiUnroll * NT;
-  auto count_step = [&](const uint4 (&w)[kHiUnroll]) {
-#pragma unroll
-    for (int u = 0; u < kHiUnroll; ++u) {
-      hi_count4<false>(w[u]);
-      const uint32_t anypos = ((w[u].x | w[u].y) | (w[u].z | w[u].w)) & 0x40004000u;
-      if (__builtin_expect(__ballot(anypos != 0) != 0, 0) && anypos != 0) book_pos(w[u]);
-    }
-  };
-  auto stream = [&](auto exact_tag) {
+  // pos_booked: the row pass booked every positive and left its code skipped -- no per-vector positive test here
+  auto stream = [&](auto exact_tag, auto booked_tag) {
     constexpr bool EXACT = decltype(exact_tag)::value;
+    constexpr bool BOOKED = decltype(booked_tag)::value;
+    auto count_step = [&](const uint4 (&w)[kHiUnroll]) {
+#pragma unroll
+      for (int u = 0; u < kHiUnroll; ++u) {
+        hi_count4<false>(w[u]);
+        if constexpr (!BOOKED) {
+          const uint32_t anypos = ((w[u].x | w[u].y) | (w[u].z | w[u].w)) & 0x40004000u;
+          if (__builtin_expect(__ballot(anypos != 0) != 0, 0) && anypos != 0) book_pos(w[u]);
+        }
+      }
+    };
     auto load = [&](uint4 (&w)[kHiUnroll], int64_t cb) {
 #pragma unroll
       for (int u = 0; u < kHiUnroll; ++u) {
@@ -1483,8 +1608,14 @@ __device__ __forceinline__ void class_hist_hi_block(int64_t vb, int64_t vgrid, c
       count_step(b);
     }
   };
-  if ((v1 - v0) % kStep == 0) stream(std::true_type{});
-  else stream(std::false_type{});
+  const bool exact = (v1 - v0) % kStep == 0;
+  if (pos_booked) {
+    if (exact) stream(std::true_type{}, std::true_type{});
+    else stream(std::false_type{}, std::true_type{});
+  } else {
+    if (exact) stream(std::true_type{}, std::false_type{});
+    else stream(std::false_type{}, std::false_type{});
+  }
   __syncthreads();
   const bool low = s_h[0] != 0u;  // block-uniform
   // rare rows (usually none): before the flushes, which then go by atomics when there are any
@@ -1581,30 +1712,24 @@ __device__ __forceinline__ void class_hist_hi_block(int64_t vb, int64_t vgrid, c
       }
     }
   }
-  if (threadIdx.x == 0) {  // last workgroup: reset the batch state words and roll the speculation (class_hist_block)
-    if (__hip_atomic_fetch_add(state + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)vgrid - 1) {
-      state[0] = state[1] = 0;
-      state[2] = 0;
-      if (roll_mode != nullptr) {
-        const int mr = roll_mode[1];
-        roll_mode[0] = mr;
-        roll_mode[1] = 0;
-      }
-    }
-  }
+  class_hi_ticket(state, roll_mode, vgrid);
 }
 
+// amdgpu_waves_per_eu(8): eight waves per SIMD (four workgroups per CU, all 1000 classes of the headline in one round);
+// without it the compiler spent 106 SGPRs and the occupancy fell to 7 waves -- 3 workgroups per CU, a second round for
+// the last 232 classes (47 vs 31 us)
 template <typename T>
-__global__ void __launch_bounds__(kClassThreadsU16) class_hist_hi_kernel(const uint16_t* __restrict__ codes, int64_t n_pad, int splits,
+__global__ void __launch_bounds__(kClassThreadsU16) __attribute__((amdgpu_waves_per_eu(8))) class_hist_hi_kernel(const uint16_t* __restrict__ codes, int64_t n_pad, int splits,
                                                                         int64_t* __restrict__ hist, const T* __restrict__ preds, int ld,
                                                                         const int64_t* __restrict__ target, int64_t n,
                                                                         const int* __restrict__ bmode, bool speculative,
                                                                         const int* __restrict__ slow_rows, int* __restrict__ state,
                                                                         int64_t* __restrict__ confmat, int* __restrict__ code_range,
                                                                         int* __restrict__ roll_mode, int64_t* __restrict__ batch_hist,
-                                                                        int* __restrict__ batch_range, const float4* __restrict__ row_stats = nullptr) {
+                                                                        int* __restrict__ batch_range, const float4* __restrict__ row_stats = nullptr,
+                                                                        bool pos_booked = false) {
   class_hist_hi_block<T, kClassThreadsU16>(blockIdx.x, gridDim.x, codes, n_pad, splits, hist, preds, ld, target, n, bmode, speculative,
-                                           slow_rows, state, confmat, code_range, roll_mode, batch_hist, batch_range, row_stats);
+                                           slow_rows, state, confmat, code_range, roll_mode, batch_hist, batch_range, row_stats, pos_booked);
 }
 
 // Small-class class pass: packed LDS histogram per (class, split), partial flush (class_store_partial).

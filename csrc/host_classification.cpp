@@ -196,14 +196,120 @@ std::vector<int64_t> mc_confmat_host(const at::Tensor& preds, const at::Tensor& 
   return res;
 }
 
+
+// ---------------------------------------------------------------------------------------------------------------
+// stat_reduce_host: the final reduction of every (tp, fp, tn, fn) metric -- accuracy, precision, recall, F-beta,
+// specificity, Hamming distance -- for CPU int64 states in ONE call (functional/classification/_stat_family.py).
+// The Python chain (sums, _safe_divide, _adjust_weights_safe_divide) is ~15 ATen calls of a few microseconds each on
+// [C]-sized tensors; at BASELINE config 1 (5 classes, batch 10) it was the largest part of a CPU forward().  Same
+// float32 operations in the same order as that chain (int64 sums, int64 -> float32 casts, a denominator of 0 read as 1,
+// F-beta's (1 + b2) tp + b2 fn + fp in float32), except the final sum over classes of macro / weighted averages, which is
+// accumulated in double and rounded once (ATen's vectorised float32 sum may differ in the last bit).
+//   kind: 0 accuracy, 1 precision, 2 recall, 3 fbeta, 4 specificity, 5 hamming
+//   average: 0 binary (elementwise), 1 micro, 2 macro, 3 weighted, 4 none (elementwise)
+// States [C] (global) or [N, C] (samplewise: reductions over the last dim), or any shape for binary.
+namespace {
+
+#pragma clang fp contract(off)
+inline float sdiv(float num, float den) { return num / (den == 0.f ? 1.f : den); }
+
+inline float stat_score(int kind, bool elementwise_acc, bool multilabel, int64_t tp, int64_t fp, int64_t tn, int64_t fn, float k1, float b2) {
+  switch (kind) {
+    case 0:
+    case 5: {
+      const float s = (elementwise_acc || multilabel) ? sdiv(static_cast<float>(tp + tn), static_cast<float>(tp + tn + fp + fn))
+                                                      : sdiv(static_cast<float>(tp), static_cast<float>(tp + fn));
+      return kind == 0 ? s : 1.f - s;
+    }
+    case 1: return sdiv(static_cast<float>(tp), static_cast<float>(tp + fp));
+    case 2: return sdiv(static_cast<float>(tp), static_cast<float>(tp + fn));
+    case 3: {
+      const float num = k1 * static_cast<float>(tp);
+      const float den = (num + b2 * static_cast<float>(fn)) + static_cast<float>(fp);
+      return sdiv(num, den);
+    }
+    default: return sdiv(static_cast<float>(tn), static_cast<float>(tn + fp));
+  }
+}
+
+}  // namespace
+
+at::Tensor stat_reduce_host(const at::Tensor& tp_t, const at::Tensor& fp_t, const at::Tensor& tn_t, const at::Tensor& fn_t, int64_t kind,
+                            int64_t average, bool multilabel, double beta) {
+  TORCH_CHECK(kind >= 0 && kind <= 5 && average >= 0 && average <= 4, "stat_reduce_host: bad kind / average");
+  for (const at::Tensor* t : {&tp_t, &fp_t, &tn_t, &fn_t})
+    TORCH_CHECK(t->device().is_cpu() && t->scalar_type() == at::kLong && t->sizes() == tp_t.sizes(),
+                "stat_reduce_host: int64 CPU states of one shape");
+  const at::Tensor tp = tp_t.contiguous(), fp = fp_t.contiguous(), tn = tn_t.contiguous(), fn = fn_t.contiguous();
+  const int64_t* a = tp.data_ptr<int64_t>();
+  const int64_t* b = fp.data_ptr<int64_t>();
+  const int64_t* c = tn.data_ptr<int64_t>();
+  const int64_t* d = fn.data_ptr<int64_t>();
+  const double b2d = beta * beta;
+  const float k1 = static_cast<float>(1.0 + b2d), b2 = static_cast<float>(b2d);
+  const auto fopt = at::TensorOptions().dtype(at::kFloat);
+  if (average == 0 || average == 4) {  // elementwise
+    at::Tensor out = at::empty(tp.sizes(), fopt);
+    float* o = out.data_ptr<float>();
+    const int64_t n = tp.numel();
+    for (int64_t i = 0; i < n; ++i) o[i] = stat_score(static_cast<int>(kind), average == 0, multilabel, a[i], b[i], c[i], d[i], k1, b2);
+    return out;
+  }
+  TORCH_CHECK(tp.dim() <= 2, "stat_reduce_host: micro / macro / weighted need [], [C] or [N, C] states");
+  const int64_t C = tp.dim() == 0 ? 1 : tp.size(-1), R = tp.dim() == 2 ? tp.size(0) : 1;
+  at::Tensor out = tp.dim() == 2 ? at::empty({R}, fopt) : at::empty({}, fopt);
+  float* o = out.data_ptr<float>();
+  for (int64_t r = 0; r < R; ++r) {
+    const int64_t* ar = a + r * C;
+    const int64_t* br = b + r * C;
+    const int64_t* cr = c + r * C;
+    const int64_t* dr = d + r * C;
+    if (average == 1) {  // micro: int64 totals, then the elementwise formula
+      int64_t st[4] = {0, 0, 0, 0};
+      for (int64_t i = 0; i < C; ++i) {
+        st[0] += ar[i];
+        st[1] += br[i];
+        st[2] += cr[i];
+        st[3] += dr[i];
+      }
+      o[r] = stat_score(static_cast<int>(kind), false, multilabel, st[0], st[1], st[2], st[3], k1, b2);
+      continue;
+    }
+    // macro / weighted: _adjust_weights_safe_divide(score, average, multilabel, tp, fp, fn)
+    double acc = 0.0;
+    if (average == 3) {
+      int64_t ws = 0;
+      for (int64_t i = 0; i < C; ++i) ws += ar[i] + dr[i];
+      const float den = static_cast<float>(ws == 0 ? 1 : ws);
+      for (int64_t i = 0; i < C; ++i) {
+        const float sc = stat_score(static_cast<int>(kind), false, multilabel, ar[i], br[i], cr[i], dr[i], k1, b2);
+        acc += static_cast<double>((static_cast<float>(ar[i] + dr[i]) * sc) / den);
+      }
+    } else {
+      float wsum = 0.f;
+      for (int64_t i = 0; i < C; ++i) wsum += (multilabel || ar[i] + br[i] + dr[i] != 0) ? 1.f : 0.f;
+      const float den = wsum == 0.f ? 1.f : wsum;
+      for (int64_t i = 0; i < C; ++i) {
+        const float w = (multilabel || ar[i] + br[i] + dr[i] != 0) ? 1.f : 0.f;
+        const float sc = stat_score(static_cast<int>(kind), false, multilabel, ar[i], br[i], cr[i], dr[i], k1, b2);
+        acc += static_cast<double>((w * sc) / den);
+      }
+    }
+    o[r] = static_cast<float>(acc);
+  }
+  return out;
+}
+
 }  // namespace tmx
 
 TORCH_LIBRARY_FRAGMENT(tmx, m) {
   m.def("mc_stats_host(Tensor preds, Tensor target, int num_classes, Tensor(a!) tp, Tensor(b!) fp, Tensor(c!) tn, Tensor(d!) fn, int ignore_index, bool has_ignore, bool micro, bool validate) -> int[]");
   m.def("mc_confmat_host(Tensor preds, Tensor target, Tensor(a!) confmat, int ignore_index, bool has_ignore, bool validate) -> int[]");
+  m.def("stat_reduce_host(Tensor tp, Tensor fp, Tensor tn, Tensor fn, int kind, int average, bool multilabel, float beta) -> Tensor");
 }
 
 TORCH_LIBRARY_IMPL(tmx, CPU, m) {
   m.impl("mc_stats_host", &tmx::mc_stats_host);
   m.impl("mc_confmat_host", &tmx::mc_confmat_host);
+  m.impl("stat_reduce_host", &tmx::stat_reduce_host);
 }

@@ -78,6 +78,7 @@ def test_binary_stats(L, dtype, logits):
 @pytest.mark.parametrize("probs", [False, True])
 def test_curve_hist_multiclass(C, dtype, probs):
     N = 3000
+    torch.manual_seed(1000 * C + (dtype == torch.float16) * 10 + int(probs))  # the moved-code count is data dependent
     x = torch.randn(N, C)
     preds = (x.softmax(1) if probs else x).to(dtype)
     target = torch.randint(0, C, (N,))

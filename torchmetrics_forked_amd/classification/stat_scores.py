@@ -56,7 +56,12 @@ class _AbstractStatScores(Metric):
     def _int64_states(self) -> bool:
         """The native kernels count into int64 states; after ``set_dtype`` (which, as in the reference, casts every
         state) the generic update path takes over."""
-        return all(isinstance(getattr(self, n), Tensor) and getattr(self, n).dtype == torch.long for n in ("tp", "fp", "tn", "fn"))
+        d = self.__dict__
+        for n in ("tp", "fp", "tn", "fn"):
+            v = d.get(n)
+            if not isinstance(v, Tensor) or v.dtype != torch.long:
+                return False
+        return True
 
     def _scratch(self, numel: int, device: torch.device) -> Tensor:
         """Zero int64 scratch of the fused GPU kernels (left at zero by every launch; not a metric state)."""
@@ -210,7 +215,7 @@ class MulticlassStatScores(_AbstractStatScores):
         if self.multidim_average != "global" or self.top_k != 1 or not self._int64_states():
             return False
         if not ops.use_native(target):
-            if not cls_ops.host_native(preds, target, self.tp):
+            if not (preds.is_cpu and target.is_cpu and self.tp.is_cpu and ops.load()):  # cls_ops.host_native, inlined
                 return False
             # CPU (gloo / plumbing): shape checks here, value check + arg-max + accumulation in one host call
             if self.validate_args:

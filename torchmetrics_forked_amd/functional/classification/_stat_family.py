@@ -30,11 +30,45 @@ from torchmetrics_forked_amd.utilities.enums import ClassificationTask
 Reducer = Callable[..., Tensor]
 
 
+_AVG_CODE = {"binary": 0, "micro": 1, "macro": 2, "weighted": 3, "none": 4, None: 4}
+
+
+def _host_reduce(kind: int, tp: Tensor, fp: Tensor, tn: Tensor, fn: Tensor, average: Optional[str], multidim_average: str,
+                 multilabel: bool, beta: float = 1.0) -> Optional[Tensor]:
+    """CPU int64 states: the whole reduction in one native call (csrc/host_classification.cpp ``stat_reduce_host``);
+    ``None`` when it does not apply (device tensors, float states, autograd, no native library)."""
+    if tp.is_cuda or tp.dtype != torch.long or average not in _AVG_CODE or tp.requires_grad:
+        return None
+    if average not in ("binary", "none", None):
+        glob = multidim_average == "global"
+        if not ((glob and tp.ndim == 1) or (not glob and tp.ndim == 2) or (glob and tp.ndim == 0 and average == "micro")):
+            return None
+    if not _native_loaded():
+        return None
+    if not (fp.dtype == tn.dtype == fn.dtype == torch.long and not (fp.is_cuda or tn.is_cuda or fn.is_cuda)):
+        return None
+    return torch.ops.tmx.stat_reduce_host(tp, fp, tn, fn, kind, _AVG_CODE[average], multilabel, float(beta))
+
+
+_NATIVE = []
+
+
+def _native_loaded() -> bool:
+    if not _NATIVE:
+        from torchmetrics_forked_amd import ops
+
+        _NATIVE.append(bool(ops.load()))
+    return _NATIVE[0]
+
+
 def _sum_micro(x: Tensor, multidim_average: str) -> Tensor:
     return x.sum(dim=0 if multidim_average == "global" else 1)
 
 
 def _accuracy_reduce(tp, fp, tn, fn, average, multidim_average="global", multilabel=False) -> Tensor:  # noqa: ANN001
+    r = _host_reduce(0, tp, fp, tn, fn, average, multidim_average, multilabel)
+    if r is not None:
+        return r
     if average == "binary":
         return _safe_divide(tp + tn, tp + tn + fp + fn)
     if average == "micro":
@@ -48,6 +82,9 @@ def _accuracy_reduce(tp, fp, tn, fn, average, multidim_average="global", multila
 
 
 def _precision_recall_reduce(stat, tp, fp, tn, fn, average, multidim_average="global", multilabel=False) -> Tensor:  # noqa: ANN001
+    r = _host_reduce(1 if stat == "precision" else 2, tp, fp, tn, fn, average, multidim_average, multilabel)
+    if r is not None:
+        return r
     other = fp if stat == "precision" else fn
     if average == "binary":
         return _safe_divide(tp, tp + other)
@@ -59,6 +96,9 @@ def _precision_recall_reduce(stat, tp, fp, tn, fn, average, multidim_average="gl
 
 
 def _fbeta_reduce(tp, fp, tn, fn, beta, average, multidim_average="global", multilabel=False) -> Tensor:  # noqa: ANN001
+    r = _host_reduce(3, tp, fp, tn, fn, average, multidim_average, multilabel, beta)
+    if r is not None:
+        return r
     b2 = beta**2
 
     def f(tp_: Tensor, fp_: Tensor, fn_: Tensor) -> Tensor:
@@ -72,6 +112,9 @@ def _fbeta_reduce(tp, fp, tn, fn, beta, average, multidim_average="global", mult
 
 
 def _specificity_reduce(tp, fp, tn, fn, average, multidim_average="global", multilabel=False) -> Tensor:  # noqa: ANN001
+    r = _host_reduce(4, tp, fp, tn, fn, average, multidim_average, multilabel)
+    if r is not None:
+        return r
     if average == "binary":
         return _safe_divide(tn, tn + fp)
     if average == "micro":
@@ -81,6 +124,9 @@ def _specificity_reduce(tp, fp, tn, fn, average, multidim_average="global", mult
 
 
 def _hamming_distance_reduce(tp, fp, tn, fn, average, multidim_average="global", multilabel=False) -> Tensor:  # noqa: ANN001
+    r = _host_reduce(5, tp, fp, tn, fn, average, multidim_average, multilabel)
+    if r is not None:
+        return r
     if average == "binary":
         return 1 - _safe_divide(tp + tn, tp + fp + tn + fn)
     if average == "micro":

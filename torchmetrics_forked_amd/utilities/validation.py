@@ -169,6 +169,15 @@ def forward_scope() -> Iterator[None]:
         _HOST.forward_depth -= 1
 
 
+def enter_forward() -> None:
+    """forward_scope()'s entry, for callers that use try / finally instead of a context manager."""
+    _HOST.forward_depth = getattr(_HOST, "forward_depth", 0) + 1
+
+
+def leave_forward() -> None:
+    _HOST.forward_depth -= 1
+
+
 def _in_forward() -> bool:
     return getattr(_HOST, "forward_depth", 0) > 0
 
