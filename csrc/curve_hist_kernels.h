@@ -637,13 +637,17 @@ __device__ __forceinline__ void unpack_pair(const uint4& wa, const uint4& wb, f3
   for (int j = 0; j < 8; ++j) P[j] = f32x2{a[j], b[j]};
 }
 
+// IEEE 754-2019 maximum (v_maximum3_f32): a NaN row's maximum is NaN -- not finite, so the row takes the rare-row path
+// exactly as with fmaxf's NaN-dropping maximum (whose NaN exp-sum marked it)
 __device__ __forceinline__ float max8(const float* v) {
-  return __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaxf(v[0], v[1]), __builtin_fmaxf(v[2], v[3])),
-                         __builtin_fmaxf(__builtin_fmaxf(v[4], v[5]), __builtin_fmaxf(v[6], v[7])));
+  auto m = [](float a, float b) { return __builtin_elementwise_maximum(a, b); };
+  return m(m(m(v[0], v[1]), m(v[2], v[3])), m(m(v[4], v[5]), m(v[6], v[7])));
 }
+// IEEE 754-2019 minimum (NaN-propagating; gfx950 v_minimum3_f32): fminf's sNaN quieting made the compiler canonicalise
+// every element first (v_max x, x).  A NaN minimum fails the narrow test below, which is the safe direction.
 __device__ __forceinline__ float min8(const float* v) {
-  return __builtin_fminf(__builtin_fminf(__builtin_fminf(v[0], v[1]), __builtin_fminf(v[2], v[3])),
-                         __builtin_fminf(__builtin_fminf(v[4], v[5]), __builtin_fminf(v[6], v[7])));
+  auto m = [](float a, float b) { return __builtin_elementwise_minimum(a, b); };
+  return m(m(m(v[0], v[1]), m(v[2], v[3])), m(m(v[4], v[5]), m(v[6], v[7])));
 }
 
 template <typename T, int NG>

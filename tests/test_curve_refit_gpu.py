@@ -93,7 +93,8 @@ def test_refit_rows_beyond_one_chunk(C):
     t = torch.randint(0, C, (N,), generator=g).cuda()
     good = _run(x, t, speculated=1)
     bad = _run(x, t, speculated=0)
-    assert torch.equal(good[0], bad[0]) and torch.equal(good[2], bad[2])
+    assert torch.equal(good[0], bad[0])
+    _range_covers(bad[2], good[2], C)
     assert good[0].sum().item() == N * C
 
 
