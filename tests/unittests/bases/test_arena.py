@@ -180,3 +180,63 @@ def test_adopt_takes_the_buffer_without_touching_the_source():
     b.append(torch.tensor([9.0]))
     assert len(a) == 1 and torch.equal(a.cat(), torch.arange(4.0))  # the source never sees b's appends
     assert torch.equal(b.cat(), torch.tensor([0.0, 1, 2, 3, 9]))
+
+
+def _check_runs(a):
+    """pieces() / item_rows() agree with the items whatever the run state."""
+    items = list(a)
+    if items:
+        assert torch.equal(torch.cat(a.pieces()), _plain_cat(items))
+    assert a.item_rows() == [1 if t.ndim == 0 else t.shape[0] for t in items]
+
+
+@pytest.mark.parametrize("tail", [(), (4,)])
+def test_extend_rows_records_runs_and_matches_items(tail):
+    g = torch.Generator().manual_seed(3)
+    a = StateArena()
+    ref = []
+    for step in range(6):
+        sizes = [int(v) for v in torch.randint(0, 5, (7,), generator=g)]
+        flat = torch.randn((sum(sizes), *tail), generator=g)
+        a.extend_rows(flat, sizes)
+        ref.extend(t.clone() for t in torch.split(flat, sizes))
+        if step % 2:
+            a.append(torch.randn((2, *tail), generator=g))
+            ref.append(a[-1].clone())
+        assert len(a) == len(ref)
+        assert all(torch.equal(x, y) for x, y in zip(a, ref))
+        _check_runs(a)
+        assert len(a.pieces()) < len(a)  # runs, not items
+        if step == 3:
+            out = a.cat()  # compaction: the runs collapse to the buffer
+            assert torch.equal(out, _plain_cat(ref))
+            assert len(a.pieces()) == 1
+    # appends into the buffer's free tail after compaction keep the runs exact
+    a.cat()
+    flat = torch.randn((3, *tail), generator=g)
+    a.extend_rows(flat, [1, 2])
+    ref.extend(t.clone() for t in torch.split(flat, [1, 2]))
+    _check_runs(a)
+    assert torch.equal(a.cat(), _plain_cat(ref))
+
+
+def test_runs_are_dropped_by_mutation_and_copies_stay_exact():
+    a = StateArena()
+    a.extend_rows(torch.arange(6.0), [2, 4])
+    a.append(torch.tensor(7.0))
+    _check_runs(a)
+    b = deepcopy(a)
+    _check_runs(b)
+    a[0] = torch.tensor([9.0, 9.0])
+    assert a._runs is None
+    _check_runs(a)
+    a.truncate(1)
+    _check_runs(a)
+    a.clear()
+    a.extend_rows(torch.ones(3), [3])
+    _check_runs(a)
+    c = StateArena.adopt(b)
+    _check_runs(c)
+    d = pickle.loads(pickle.dumps(b))
+    _check_runs(d)
+    assert torch.equal(torch.cat(d.pieces()), torch.cat(b.pieces()))

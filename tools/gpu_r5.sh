@@ -16,7 +16,8 @@ run() {  # run <name> <seconds> <cmd...>; stdout+stderr -> $OUT/<name>.log
 for s in "$@"; do
   case $s in
     tests) run tests 400 python -u -m pytest ${TMX_TESTS:-tests/unittests/bases/test_advice_r4.py} -m gpu -x -q --timeout 120 --timeout-method thread; tail -3 "$OUT/tests.log" ;;
-    kexp) run kexp 120 ./build/kexp_r5/${TMX_KEXP:-exp}; cat "$OUT/kexp.log" ;;
+    kexp) run kexp 120 ./build/kexp_r5/${TMX_KEXP:-exp} ${TMX_KEXP_ARGS:-}; cat "$OUT/kexp.log" ;;
+    synclat) for b in 200 1000 1500 3000; do run synclat_$b 120 ./build/kexp_r5/sync_latency_exp 50 $b; cat "$OUT/synclat_$b.log"; done ;;
     kexpmulti) for k in ${TMX_KEXP}; do run kexp_$k 120 ./build/kexp_r5/$k; echo "$k: $(tail -c 400 $OUT/kexp_$k.log)"; done ;;
     kexppmc) run kexppmc 120 rocprofv3 --kernel-trace --pmc ${TMX_PMC:-SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU} -d "$OUT/kexppmc" -o pmc --output-format csv -- ./build/kexp_r5/${TMX_KEXP:-exp} ;;
     host) run host 120 python tools/host_overhead_probe.py ;;
@@ -26,6 +27,9 @@ for s in "$@"; do
     smoke) run smoke 200 python -u -c "import __graft_entry__ as g; g.smoke()"; tail -1 "$OUT/smoke.log" ;;
     fwd) run forward_bench 120 python tools/forward_bench.py; tail -1 "$OUT/forward_bench.log" ;;
     window) run window 120 python tools/window_probe.py ;;
+    wsplit) run wsplit 180 python tools/window_split_probe.py; cat "$OUT/wsplit.log" ;;
+    fwprof) run fwprof 200 rocprofv3 --kernel-trace -d "$OUT/fwprof" -o fw --output-format csv -- python3 tools/first_window_probe.py base; tail -1 "$OUT/fwprof.log" ;;
+    firstwin) for r in 1 2 3; do for v in ${TMX_FW_VARIANTS:-base spin double inplace}; do run fw_${v}_$r 60 python tools/first_window_probe.py $v; tail -1 "$OUT/fw_${v}_$r.log"; done; done ;;
     bench) for i in 1 2; do run bench20_$i 120 python bench.py --steps 20 --warmup 5; tail -1 "$OUT/bench20_$i.log"; done ;;
     bench50) run bench50 120 python bench.py --steps 50 --warmup 5; tail -1 "$OUT/bench50.log" ;;
     prof) run prof 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o headline --output-format csv -- python3 bench.py --steps 20 --warmup 5 ;;
@@ -39,7 +43,10 @@ for s in "$@"; do
     radixprof) run radixprof 300 rocprofv3 --kernel-trace --stats -d "$OUT/radixprof" -o radix --output-format csv -- python3 tools/radix_curve_bench.py ;;
     imgprof) run imgprof 900 rocprofv3 --kernel-trace --stats -d "$OUT/imgprof" -o image --output-format csv -- python3 bench.py --config image --steps 1 --warmup 1; tail -2 "$OUT/imgprof.log" ;;
     bertprof) run bertprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/bertprof" -o bert --output-format csv -- python3 bench.py --config bert --steps 2 --warmup 1; tail -2 "$OUT/bertprof.log" ;;
+    mapcprof) run mapcprof 300 python tools/map_profile.py; head -c 600 "$OUT/mapcprof.log" ;;
     mapbench) run mapbench 600 python bench.py --config map --steps 5 --warmup 1; tail -1 "$OUT/mapbench.log" ;;
+    mapprof) run mapprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/mapprof" -o map --output-format csv -- python3 bench.py --config map --steps 5 --warmup 1; tail -1 "$OUT/mapprof.log" ;;
+    sweep) run sweep 300 python tools/class_count_sweep.py; tail -3 "$OUT/sweep.log" ;;
     *) echo "unknown step $s" ;;
   esac
 done

@@ -145,6 +145,8 @@ class MetricCollection(ModuleDict):
         """Point every group member's states at the leader's (or deep-copy them when ``copy``)."""
         if not self._state_is_copy:
             for cg in self._groups.values():
+                if len(cg) == 1:  # a singleton group has no members to point at its leader
+                    continue
                 m0 = getattr(self, cg[0])
                 for name in cg[1:]:
                     mi = getattr(self, name)

@@ -134,9 +134,16 @@ class HostCheckBatch:
                 cb(v)
 
 
-def _native() -> bool:
-    from torchmetrics_forked_amd import ops
+_OPS = None
 
+
+def _native() -> bool:
+    global _OPS
+    ops = _OPS
+    if ops is None:  # bound once: a function-level import costs ~2 us per call on the compute path
+        from torchmetrics_forked_amd import ops
+
+        _OPS = ops
     return ops.load()
 
 
