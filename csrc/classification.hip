@@ -1206,11 +1206,17 @@ template <typename T, bool FIXUP>
 void launch_small_rows(int TL, int grid, const T* p, const int64_t* target, int64_t n, int C, int* mode, int64_t ignore_index, bool has_ignore,
                        uint16_t* codes, int64_t n_pad, int64_t* cm, int* err, bool rec, int* srows, int* scount, uint32_t* pcm,
                        float4* row_stats = nullptr) {
-  const size_t shm = (size_t)kSmallRows * C * sizeof(uint16_t) + (C <= kSmallCmMax ? (size_t)C * C * sizeof(uint32_t) : 0);
+  const size_t shm = (size_t)kSmallRows * ((C + 1) & ~1) * sizeof(uint16_t) + (C <= kSmallCmMax ? (size_t)C * C * sizeof(uint32_t) : 0);
+  // 16-B aligned rows (C % 8 == 0, aligned base): scores straight into registers, no LDS staging
+  const bool direct = C % 8 == 0 && (reinterpret_cast<uintptr_t>(p) & 15) == 0;
 #define TMX_SMALL_CASE(TLV)                                                                                                     \
   case TLV:                                                                                                                      \
-    hipLaunchKernelGGL((mc_codes_small_kernel<T, TLV, FIXUP>), grid, kSmallRows * TLV, shm, stream(), p, target, n, C, mode,   \
-                       ignore_index, has_ignore, codes, n_pad, cm, err, rec, srows, scount, pcm, row_stats);                      \
+    if (direct)                                                                                                                  \
+      hipLaunchKernelGGL((mc_codes_small_kernel<T, TLV, FIXUP, 0, true>), grid, kSmallRows * TLV, shm, stream(), p, target, n,  \
+                         C, mode, ignore_index, has_ignore, codes, n_pad, cm, err, rec, srows, scount, pcm, row_stats);            \
+    else                                                                                                                         \
+      hipLaunchKernelGGL((mc_codes_small_kernel<T, TLV, FIXUP>), grid, kSmallRows * TLV, shm, stream(), p, target, n, C, mode, \
+                         ignore_index, has_ignore, codes, n_pad, cm, err, rec, srows, scount, pcm, row_stats);                    \
     break;
 #define TMX_SMALL_CC(CCV)                                                                                                      \
   case CCV:                                                                                                                      \
@@ -1242,7 +1248,7 @@ static bool stream_capturing();
 template <typename T>
 void launch_small_two_pass(const T* p, const int64_t* target, int64_t n, int C, int* mode, int* state, bool speculative,
                            int64_t ignore_index, bool has_ignore, int64_t* hist, int64_t* cm, int* err, const at::TensorOptions& opts,
-                           int* code_range) {
+                           int* code_range, int64_t* batch_hist = nullptr, int* batch_range = nullptr) {
   TORCH_CHECK(n < (int64_t{1} << 31), "curve_hist_update: more than 2^31 rows in one batch");
   const int64_t n_pad = (n + kSmallRows - 1) / kSmallRows * kSmallRows;
   const int64_t ntiles = n_pad / kSmallRows;
@@ -1253,8 +1259,13 @@ void launch_small_two_pass(const T* p, const int64_t* target, int64_t n, int C, 
   // the row pass latency-bound, 40 us for 1M x 10 bf16)
   static const int grid_cap = [] { const char* v = std::getenv("TMX_SMALL_GRID"); return v ? std::atoi(v) : 8192; }();
   const int grid = static_cast<int>(std::min<int64_t>(ntiles, std::max(256, grid_cap / TL)));
-  // confusion-matrix partials per block (C <= 32: at most 4 MiB), summed by the reduce launch: no same-cell atomics
-  const bool use_pcm = cm != nullptr && C <= 32;
+  // class pass: the windowed u32 LDS histogram of the headline route (class_hist_hi_kernel) for C > 16 -- the
+  // packed partial-flush pass + reduce launch took 48 + 12 us at C = 256 x 262,144 against ~30 us for the same bytes
+  // at C = 1000; C <= 16 keeps the partial pass (few classes: every split of a class hits the same few thousand bins)
+  static const bool hi_off = std::getenv("TMX_SMALL_CLASS_PARTIAL") != nullptr;  // A/B knob
+  const bool hi_pass = C > 16 && !hi_off;
+  // confusion-matrix partials per block (C <= 64: at most 16 MiB), summed by a reduce launch: no same-cell atomics
+  const bool use_pcm = cm != nullptr && C <= (hi_pass ? kSmallCmMax : 32);
   // per-stream cached scratch (no allocator round trips per update); stream order keeps consecutive updates apart
   const bool capturing = stream_capturing();
   const auto pcm_t = use_pcm ? stream_scratch(opts, (int64_t)grid * C * C, 3, capturing) : at::Tensor();
@@ -1268,6 +1279,22 @@ void launch_small_two_pass(const T* p, const int64_t* target, int64_t n, int C, 
   int* srows = slow_rows.data_ptr<int>();
   launch_small_rows<T, false>(TL, grid, p, target, n, C, mode, ignore_index, has_ignore, cptr, n_pad, cm, err, speculative, srows, state,
                               pcm, rstats);
+  const int pcm_slices = use_pcm ? std::max(1, std::min(64, grid / 256)) : 0;
+  if (hi_pass) {
+    // enough (class, split) workgroups for four per CU on every CU; at least 2048 rows per split
+    int hsplits = 1;
+    while ((int64_t)C * hsplits < 1024 && n_pad / (hsplits * 2) >= 2048) hsplits *= 2;
+    hipLaunchKernelGGL((class_hist_hi_kernel<T>), C * hsplits, kClassThreadsU16, kHiLdsBytes, stream(), cptr, n_pad, hsplits, hist, p, C,
+                       target, n, mode, speculative, srows, state, cm, code_range, speculative ? mode : nullptr, batch_hist, batch_range,
+                       rstats, false);
+    TMX_LAUNCH_CHECK();
+    if (use_pcm) {
+      hipLaunchKernelGGL(class_partial_reduce_kernel, dim3(pcm_slices, C), 256, 0, stream(), nullptr, nullptr, 0, hist, nullptr, nullptr,
+                         nullptr, pcm, grid, cm, C, pcm_slices, kCodes / 256 + 1);
+      TMX_LAUNCH_CHECK();
+    }
+    return;
+  }
   // Class pass: packed LDS histogram per (class, row split) — with few classes 1 / C of the codes are positives —
   // and a partial flush (plain stores of the occupied range, then one reduce launch) instead of global int64 atomics:
   // every split of a class hits the same few thousand bins.  Splits: enough (class, split) blocks to fill the chip,
@@ -1287,7 +1314,6 @@ void launch_small_two_pass(const T* p, const int64_t* target, int64_t n, int C, 
                      hist, p, C, target, n, mode, speculative, srows, state, cm, code_range, speculative ? mode : nullptr, pp,
                      reinterpret_cast<int*>(prange.data_ptr()), rstats);
   TMX_LAUNCH_CHECK();
-  const int pcm_slices = use_pcm ? std::max(1, std::min(64, grid / 256)) : 0;
   hipLaunchKernelGGL(class_partial_reduce_kernel, dim3(kCodes / 256 + 1 + pcm_slices, C), 256, 0, stream(), pp, prange.data_ptr<int>(),
                      splits, hist, code_range, state, speculative ? mode : nullptr, pcm, grid, cm, C, pcm_slices);
   TMX_LAUNCH_CHECK();
@@ -1634,15 +1660,18 @@ void curve_hist_update_impl(const at::Tensor& preds_, const at::Tensor& target_,
   const at::Tensor target = target_.is_contiguous() && target_.scalar_type() == at::kLong ? target_ : target_.contiguous().to(at::kLong);
   const int C = static_cast<int>(hist.size(0));
   const int block = 256;
-  // two-pass multiclass route for C <= 1024; rows are padded to a multiple of 8 classes when C % 8 != 0 (one copy)
+  // two-pass multiclass route for C <= 1024 (C % 8 != 0: rows read in place at stride C, unaligned loads)
   const bool two_pass_ok = task == 0 && C <= 8 * 2 * kWave &&
                            (C % 8 != 0 || (reinterpret_cast<uintptr_t>(preds.data_ptr()) & 15) == 0);
   if (batch_hist != nullptr) {
     static const bool small_off_b = std::getenv("TMX_CURVE_SMALL_OFF") != nullptr;
     const bool small_route = task == 0 && !small_off_b && C <= kSmallVpt * 16 && (reinterpret_cast<uintptr_t>(preds.data_ptr()) & 15) == 0;
+    // the small route's windowed class pass (C > 16) fills the batch histogram too
+    static const bool small_partial = std::getenv("TMX_SMALL_CLASS_PARTIAL") != nullptr;
+    const bool small_dual = small_route && C > 16 && !small_partial;
     const bool ml_route = task == 1 && C != 1 && C % 8 == 0 && C <= 8 * 2 * kWave && target.dim() >= 1 && target.numel() == target.size(0) * C &&
                           (reinterpret_cast<uintptr_t>(preds.data_ptr()) & 15) == 0 && (reinterpret_cast<uintptr_t>(target.data_ptr()) & 15) == 0;
-    const bool dual_route = (task == 0 && two_pass_ok && !small_route) || ml_route;
+    const bool dual_route = (task == 0 && two_pass_ok && !small_route) || small_dual || ml_route;
     if (!dual_route) {
       dual = false;
       range_tracked = true;  // nothing counted: the range stays as it is
@@ -1686,17 +1715,18 @@ void curve_hist_update_impl(const at::Tensor& preds_, const at::Tensor& target_,
       const bool small_ok = !small_off && C <= kSmallVpt * 16 && (reinterpret_cast<uintptr_t>(preds.data_ptr()) & 15) == 0;
       if (small_ok) {
         launch_small_two_pass<scalar_t>(p, target.data_ptr<int64_t>(), n, C, flag.data_ptr<int>(), state_ptr, speculative,
-                                        ignore_index, has_ignore, hist.data_ptr<int64_t>(), cm, err, preds.options(), crange);
+                                        ignore_index, has_ignore, hist.data_ptr<int64_t>(), cm, err, preds.options(), crange,
+                                        batch_hist, batch_range);
         range_tracked = true;
         return;
       }
       if (two_pass_ok) {
         if (C % 8 != 0) {
-          const int ld = (C + 7) / 8 * 8;
-          const at::Tensor padded = at::constant_pad_nd(preds.view({n, C}), {0, ld - C}, 0).contiguous();
-          launch_two_pass<scalar_t, true>(reinterpret_cast<const scalar_t*>(padded.data_ptr()), target.data_ptr<int64_t>(), n, C,
-                                          ld, flag.data_ptr<int>(), state_ptr, speculative, ignore_index, has_ignore,
-                                          hist.data_ptr<int64_t>(), cm, err, preds.options(), crange, batch_hist, batch_range);
+          // rows at stride C read in place with 2-byte-aligned 16-B loads (row_tile_load UNALIGNED); round 4 padded
+          // every row to a multiple of 8 with a copy (48 us + 18 us of fill at 65,536 x 1001)
+          launch_two_pass<scalar_t, true>(p, target.data_ptr<int64_t>(), n, C, C, flag.data_ptr<int>(), state_ptr, speculative,
+                                          ignore_index, has_ignore, hist.data_ptr<int64_t>(), cm, err, preds.options(), crange, batch_hist,
+                                          batch_range);
         } else {
           launch_two_pass<scalar_t, false>(p, target.data_ptr<int64_t>(), n, C, C, flag.data_ptr<int>(), state_ptr,
                                            speculative, ignore_index, has_ignore, hist.data_ptr<int64_t>(), cm, err, preds.options(),

@@ -226,6 +226,12 @@ template <> __device__ __forceinline__ uint32_t pack_rne2<__half>(f32x2 q) {
   return __builtin_amdgcn_perm(rne_word<__half>(q.y), rne_word<__half>(q.x), 0x07060302u);
 }
 
+// the 16-bit pattern of a score widened to fp32 (exact: bf16 / fp16 -> fp32 is lossless; NaN payloads may be
+// quietened for fp16, and every NaN pattern is a skip code anyway)
+template <typename T> __device__ __forceinline__ uint32_t half_bits(float f);
+template <> __device__ __forceinline__ uint32_t half_bits<__hip_bfloat16>(float f) { return __float_as_uint(f) >> 16; }
+template <> __device__ __forceinline__ uint32_t half_bits<__half>(float f) { return bits16<__half>(__float2half(f)); }
+
 // 16-bit code of a raw score pattern: -0.0 -> 0, [0, 1] -> itself, anything else (negative, > 1, inf, NaN) -> skip
 template <typename T> __device__ __forceinline__ uint32_t raw_code(uint32_t b) {
   return b == 0x8000u ? 0u : (b <= RangeBits<T>::one ? b : 0x8000u);
@@ -388,12 +394,43 @@ struct RowLoads {
   int64_t tv;
 };
 
-template <typename T, int NG>
+// UNALIGNED (C % 8 != 0, rows at stride C: round 5, no padding copy): a row starts 2 ((r C) % 8) bytes past a 16-B
+// boundary; its 16-B vectors are loaded at the row's own addresses (gfx950 global loads take any 2-byte alignment at
+// full speed: tools/kexp/unaligned_load_exp.hip, 0 wrong elements, 47.5 vs 47.4 us per 131 MB sweep).  The row's last
+// vector is partial: its slots past the row (the next row's first scores) take the value of its slot 0, a real score of
+// the row, so maxima, minima and the arg-max (lowest slot wins) are unchanged; the exp-sum skips them.  The last vector
+// of the last row is assembled from 16-bit loads that stop at the tensor's end.
+template <typename T>
+__device__ __forceinline__ uint4 load_row_vec_unaligned(const T* __restrict__ preds, int64_t e0, int rem, int64_t total) {
+  const uint16_t* p = reinterpret_cast<const uint16_t*>(preds);
+  uint4 w;
+  if (e0 + 8 <= total) {
+    w = stream_load16(reinterpret_cast<const uint4*>(p + e0));
+  } else {
+    uint32_t d[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t lo = e0 + 2 * k < total ? p[e0 + 2 * k] : 0u, hi = e0 + 2 * k + 1 < total ? p[e0 + 2 * k + 1] : 0u;
+      d[k] = lo | (hi << 16);
+    }
+    w = make_uint4(d[0], d[1], d[2], d[3]);
+  }
+  if (rem < 8) {  // partial vector: slots >= rem repeat slot 0
+    const uint32_t s0 = w.x & 0xFFFFu, d0 = s0 | (s0 << 16);
+    auto fix = [&](uint32_t dw, int k) -> uint32_t {
+      return 2 * k + 1 < rem ? dw : (2 * k < rem ? ((dw & 0xFFFFu) | (s0 << 16)) : d0);
+    };
+    w = make_uint4(fix(w.x, 0), fix(w.y, 1), fix(w.z, 2), fix(w.w, 3));
+  }
+  return w;
+}
+
+template <typename T, int NG, bool UNALIGNED = false>
 __device__ __forceinline__ void row_tile_load(const T* __restrict__ preds, const int64_t* __restrict__ target, int64_t n, int ld,
                                               int64_t tile, RowLoads<NG>& L) {
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = threadIdx.x / kWave;
-  const int nvec = ld / 8;
+  const int nvec = UNALIGNED ? (ld + 7) / 8 : ld / 8;
   const bool lo_ok = lane < nvec, hi_ok = lane + kWave < nvec;
   const int lq = lo_ok ? lane : nvec - 1;  // clamped: every load stays inside its row
   const int hq = hi_ok ? lane + kWave : nvec - 1;
@@ -403,9 +440,16 @@ __device__ __forceinline__ void row_tile_load(const T* __restrict__ preds, const
   for (int pp = 0; pp < 2; ++pp)
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      const uint4* row = reinterpret_cast<const uint4*>(preds + min(row0_of(pp) + h, n - 1) * ld);
-      L.raw[pp][h][0] = stream_load16(row + lq);
-      if constexpr (NG == 2) L.raw[pp][h][1] = stream_load16(row + hq);
+      if constexpr (UNALIGNED) {
+        const int64_t base = min(row0_of(pp) + h, n - 1) * ld, total = n * ld;
+        L.raw[pp][h][0] = load_row_vec_unaligned<T>(preds, base + 8 * lq, lq == nvec - 1 ? ld - 8 * lq : 8, total);
+        if constexpr (NG == 2)
+          L.raw[pp][h][1] = load_row_vec_unaligned<T>(preds, base + 8 * hq, hq == nvec - 1 ? ld - 8 * hq : 8, total);
+      } else {
+        const uint4* row = reinterpret_cast<const uint4*>(preds + min(row0_of(pp) + h, n - 1) * ld);
+        L.raw[pp][h][0] = stream_load16(row + lq);
+        if constexpr (NG == 2) L.raw[pp][h][1] = stream_load16(row + hq);
+      }
     }
 }
 
@@ -479,7 +523,7 @@ __device__ __forceinline__ void row_tile_compute(const RowLoads<NG>& L, int64_t 
                                                  float4* __restrict__ row_stats, const PosSink& pos, PosTake& ptake) {
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = threadIdx.x / kWave;
-  const int nvec = ld / 8;
+  const int nvec = PADDED ? (ld + 7) / 8 : ld / 8;
   const int nlo = min(max(C - 8 * lane, 0), 8), nhi = min(max(C - 8 * (lane + kWave), 0), 8);
   const bool lo_ok = lane < nvec, hi_ok = lane + kWave < nvec;
   auto row0_of = [&](int pp) -> int64_t { return tile * kTileRows + 2 * (wave + pp * kRowWaves); };
@@ -650,15 +694,18 @@ __device__ __forceinline__ float min8(const float* v) {
   return m(m(m(v[0], v[1]), m(v[2], v[3])), m(m(v[4], v[5]), m(v[6], v[7])));
 }
 
-template <typename T, int NG>
+template <typename T, int NG, bool UNALIGNED = false>
 __device__ __forceinline__ void row_tile_softmax_lean(const RowLoads<NG>& L, int64_t n, int C, int ld, int64_t ignore_index,
                                                       bool has_ignore, int64_t* __restrict__ confmat, int* __restrict__ err, bool rec,
                                                       bool& saw_bad, SlowRows slow, uint32_t* __restrict__ s_tile, int64_t tile,
                                                       float4* __restrict__ row_stats, const PosSink& pos, PosTake& ptake) {
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = threadIdx.x / kWave;
-  const int nvec = ld / 8;
+  const int nvec = UNALIGNED ? (ld + 7) / 8 : ld / 8;
   const bool lo_ok = lane < nvec, hi_ok = lane + kWave < nvec;
+  // UNALIGNED: the lane holding the row's partial last vector counts only its first ``rem`` slots in the exp-sum
+  const int rem = ld - 8 * (nvec - 1);
+  const int cut_lo = UNALIGNED && lane == nvec - 1 ? rem : 8, cut_hi = UNALIGNED && lane + kWave == nvec - 1 ? rem : 8;
   auto row0_of = [&](int pp) -> int64_t { return tile * kTileRows + 2 * (wave + pp * kRowWaves); };
   const int64_t tv = L.tv;
   auto target_of = [&](int i) -> int64_t {
@@ -728,18 +775,22 @@ __device__ __forceinline__ void row_tile_softmax_lean(const RowLoads<NG>& L, int
     const bool narrow = __ballot(!(mxa - mn_a <= 86.f && mxb - mn_b <= 86.f)) == 0;
     const f32x2 mx2 = {mxa, mxb};
     f32x2 acc = {0.f, 0.f}, acc_lo = {0.f, 0.f};
+    auto counted = [&](int j) -> f32x2 {
+      if constexpr (UNALIGNED) return (j & 7) < (j < 8 ? cut_lo : cut_hi) ? P[j] : f32x2{0.f, 0.f};
+      else return P[j];
+    };
     if (narrow) {
 #pragma unroll
       for (int j = 0; j < 8 * NG; ++j) {
         P[j] = exp_nonpos2_narrow(P[j] - mx2);
-        acc = acc + P[j];
+        acc = acc + counted(j);
         if (j == 7) acc_lo = acc;
       }
     } else {
 #pragma unroll
       for (int j = 0; j < 8 * NG; ++j) {
         P[j] = exp_nonpos2(P[j] - mx2);
-        acc = acc + P[j];
+        acc = acc + counted(j);
         if (j == 7) acc_lo = acc;
       }
     }
@@ -820,11 +871,12 @@ __device__ __forceinline__ void row_tile(const T* __restrict__ preds, const int6
                                           SlowRows slow, uint32_t* __restrict__ s_tile, int64_t tile, float4* __restrict__ row_stats,
                                           PosSink pos = PosSink{}) {
   RowLoads<NG> L;
-  row_tile_load<T, NG>(preds, target, n, ld, tile, L);
+  row_tile_load<T, NG, PADDED>(preds, target, n, ld, tile, L);  // PADDED: rows of C % 8 != 0 scores at stride C
   PosTake ptake;
   if constexpr (FIXUP) pos = PosSink{};
-  if constexpr (LEAN && SOFTMAX && !FIXUP && !PADDED)
-    row_tile_softmax_lean<T, NG>(L, n, C, ld, ignore_index, has_ignore, confmat, err, rec, saw_bad, slow, s_tile, tile, row_stats, pos, ptake);
+  if constexpr (LEAN && SOFTMAX && !FIXUP)
+    row_tile_softmax_lean<T, NG, PADDED>(L, n, C, ld, ignore_index, has_ignore, confmat, err, rec, saw_bad, slow, s_tile, tile, row_stats, pos,
+                                         ptake);
   else
     row_tile_compute<T, NG, SOFTMAX, FIXUP, PADDED>(L, n, C, ld, ignore_index, has_ignore, confmat, err, rec, saw_bad, slow, s_tile, tile,
                                                     row_stats, pos, ptake);
@@ -1192,12 +1244,9 @@ __device__ __forceinline__ void class_hist_block(int64_t vb, int64_t vgrid, cons
         if (m1 != 0) {
           if ((fl & 3u) == 3u) {  // counted row with a finite softmax (NaN / inf rows: every code skipped)
             const float inv = 1.f / st.y;
-            if constexpr (PACKED) {  // small-class route: its row pass's scalar sequence (exp_nonpos, div_rn, rne_word)
-              code = raw_code<T>(rne_word<T>(div_rn(exp_nonpos(to_f32<T>(xv) - st.x), st.y, inv)) >> 16);
-            } else {  // tile route: the packed pair sequence of row_tile_compute
-              const f32x2 e = exp_nonpos2(f32x2{to_f32<T>(xv) - st.x, 0.f});
-              code = pack_rne2<T>(div_rn2(f32x2{e.x, 0.f}, f32x2{st.y, 1.f}, f32x2{inv, 1.f})) & 0xFFFFu;
-            }
+            // the packed pair sequence of both row passes (row_tile_compute / mc_codes_small_kernel, round 5)
+            const f32x2 e = exp_nonpos2(f32x2{to_f32<T>(xv) - st.x, 0.f});
+            code = pack_rne2<T>(div_rn2(f32x2{e.x, 0.f}, f32x2{st.y, 1.f}, f32x2{inv, 1.f})) & 0xFFFFu;
           }
         } else if (fl & 1u) {
           code = raw_code<T>(bits16<T>(xv));
@@ -1756,14 +1805,16 @@ __global__ void __launch_bounds__(256) class_partial_reduce_kernel(const uint32_
                                                                    int splits, int64_t* __restrict__ hist, int* __restrict__ code_range,
                                                                    int* __restrict__ state, int* __restrict__ roll_mode,
                                                                    const uint32_t* __restrict__ pcm, int pcm_blocks,
-                                                                   int64_t* __restrict__ confmat, int C, int pcm_slices) {
+                                                                   int64_t* __restrict__ confmat, int C, int pcm_slices,
+                                                                   int x_base = 0) {
   const int c = blockIdx.y;
-  if (blockIdx.x > kCodes / 256) {
+  const int bx = static_cast<int>(blockIdx.x) + x_base;  // x_base = kCodes / 256 + 1: the confusion-matrix blocks only
+  if (bx > kCodes / 256) {
     // confusion-matrix row c: slice p of the row pass's per-block partials, 256 / C thread groups stride over the
     // slice's blocks, an LDS fold per cell, one int64 atomic per (slice, cell) — a serial loop over thousands of
     // partials per cell was the reduce launch's cost
     __shared__ uint64_t s_acc[256];
-    const int p = blockIdx.x - (kCodes / 256 + 1);
+    const int p = bx - (kCodes / 256 + 1);
     const int G = 256 / C, cell = threadIdx.x % C, g = threadIdx.x / C;
     const int per = (pcm_blocks + pcm_slices - 1) / pcm_slices;
     const int b0 = p * per, b1 = min(pcm_blocks, b0 + per);
@@ -1779,7 +1830,7 @@ __global__ void __launch_bounds__(256) class_partial_reduce_kernel(const uint32_
     }
     return;
   }
-  if (blockIdx.x == kCodes / 256) {
+  if (bx == kCodes / 256) {
     if (threadIdx.x == 0 && code_range != nullptr) {
       int lo = kCodes, hi = -1;
       for (int s = 0; s < splits; ++s) {
@@ -1803,7 +1854,7 @@ __global__ void __launch_bounds__(256) class_partial_reduce_kernel(const uint32_
     }
     return;
   }
-  const int i = blockIdx.x * 256 + threadIdx.x;
+  const int i = bx * 256 + threadIdx.x;
   uint64_t neg = 0, pos = 0;
   const int64_t b0 = (int64_t)c * splits;
   int s = 0;
@@ -1850,17 +1901,75 @@ constexpr int kSmallRows = 64;
 constexpr int kSmallVpt = 16;
 constexpr int kSmallCmMax = 64;  // LDS-privatised confusion matrix up to 64 x 64 (16 KiB)
 
+// Reductions over aligned groups of TL lanes (TL <= 16) by DPP (quad_perm xor 1, xor 2, row_half_mirror, row_mirror:
+// after the first two steps a quad is uniform, so the mirrors pair exactly as xor 4 / xor 8 would -- the same values,
+// the same fp32 additions as an xor butterfly) -- no LDS round trip and no per-offset address register, which the
+// __shfl_xor form (ds_bpermute) hoisted out of the tile loop: ~20 VGPRs of the small row pass's 126.
+template <int TL> __device__ __forceinline__ float grp_max(float v) {
+  if constexpr (TL > 1) v = __builtin_fmaxf(v, dpp_f32<0xB1>(v, v));
+  if constexpr (TL > 2) v = __builtin_fmaxf(v, dpp_f32<0x4E>(v, v));
+  if constexpr (TL > 4) v = __builtin_fmaxf(v, dpp_f32<0x141>(v, v));
+  if constexpr (TL > 8) v = __builtin_fmaxf(v, dpp_f32<0x140>(v, v));
+  return v;
+}
+template <int TL> __device__ __forceinline__ float grp_min(float v) {
+  if constexpr (TL > 1) v = __builtin_fminf(v, dpp_f32<0xB1>(v, v));
+  if constexpr (TL > 2) v = __builtin_fminf(v, dpp_f32<0x4E>(v, v));
+  if constexpr (TL > 4) v = __builtin_fminf(v, dpp_f32<0x141>(v, v));
+  if constexpr (TL > 8) v = __builtin_fminf(v, dpp_f32<0x140>(v, v));
+  return v;
+}
+template <int TL> __device__ __forceinline__ float grp_sum(float v) {
+  if constexpr (TL > 1) v += dpp_f32<0xB1>(v, v);
+  if constexpr (TL > 2) v += dpp_f32<0x4E>(v, v);
+  if constexpr (TL > 4) v += dpp_f32<0x141>(v, v);
+  if constexpr (TL > 8) v += dpp_f32<0x140>(v, v);
+  return v;
+}
+template <int TL> __device__ __forceinline__ int grp_min_i32(int v) {
+  if constexpr (TL > 1) v = min(v, dpp_i32<0xB1>(v, v));
+  if constexpr (TL > 2) v = min(v, dpp_i32<0x4E>(v, v));
+  if constexpr (TL > 4) v = min(v, dpp_i32<0x141>(v, v));
+  if constexpr (TL > 8) v = min(v, dpp_i32<0x140>(v, v));
+  return v;
+}
+// value of lane ^ M (M < 32): ds_swizzle in bitmask mode (and 0x1F, xor M), no address register
+template <int M> __device__ __forceinline__ uint32_t swz_xor(uint32_t v) {
+  return static_cast<uint32_t>(__builtin_amdgcn_ds_swizzle(static_cast<int>(v), 0x1F | (M << 10)));
+}
+
 // CC > 0: the class count as a compile-time constant (C <= 16, one lane per row): the per-lane loops lose their
 // runtime class masks (at C = 10 the generic form ran 6 of 16 slots masked, 82 VGPRs and 69 SGPR spills).
-template <typename T, int TL, bool FIXUP, int CC = 0>
-__global__ void __launch_bounds__(kSmallRows * TL) mc_codes_small_kernel(
+// DIRECT (C % 8 == 0, 16-B aligned scores): every lane loads its 16 scores straight into registers (two 16-B loads;
+// a row's lanes and consecutive rows are contiguous, so a wave reads one contiguous run) -- no LDS staging.
+// Otherwise the block's scores are staged into LDS with 16-B loads and each lane reads its 16 from there.
+// Image (round 5): the codes of row pair (2k, 2k+1) and class c are packed into one dword (the lane of the even row
+// swaps halves with its partner lane of the odd row: the even lane then holds the even classes of both rows, the odd
+// lane the odd classes) at dword c * 32 + ((k + rot(c)) & 31), rot(c) = (c >> 4) * (32 / TL): for one store
+// instruction the 64 lanes' (class parity, rotated pair slot) are 64 distinct banks.  The round-4 image took one
+// 16-bit write per code at c * 64 + row -- a TL-way bank conflict per store (all lanes of a row 2 KiB apart) on top
+// of the two-lanes-per-dword one: the row pass of C = 256 x 262,144 ran 171 us against 59 us for C = 1000 x 65,536.
+#ifndef TMX_SMALL_WPE
+#define TMX_SMALL_WPE 0
+#endif
+#if TMX_SMALL_WPE > 0
+#define TMX_SMALL_WPE_ATTR __attribute__((amdgpu_waves_per_eu(TMX_SMALL_WPE)))
+#else
+#define TMX_SMALL_WPE_ATTR
+#endif
+template <typename T, int TL, bool FIXUP, int CC = 0, bool DIRECT = false>
+__global__ void __launch_bounds__(kSmallRows * TL) TMX_SMALL_WPE_ATTR mc_codes_small_kernel(
     const T* __restrict__ preds, const int64_t* __restrict__ target, int64_t n, int C_arg, int* __restrict__ mode, int64_t ignore_index,
     bool has_ignore, uint16_t* __restrict__ codes, int64_t n_pad, int64_t* __restrict__ confmat, int* __restrict__ err,
     bool record_mode, int* __restrict__ slow_rows, int* __restrict__ slow_count, uint32_t* __restrict__ pcm,
     float4* __restrict__ row_stats = nullptr) {
   const int C = CC > 0 ? CC : C_arg;
   constexpr int kVpt = CC > 0 ? CC : kSmallVpt;  // value slots per lane
-  extern __shared__ __attribute__((aligned(16))) uint16_t s_small[];  // staging [64][C], then image [C][64]; cm [C][C]
+  constexpr int kPairs = (kVpt + 1) / 2;
+  constexpr int kRot = 32 / TL;
+  static_assert(!DIRECT || kVpt == kSmallVpt, "direct loads take 16 scores per lane");
+  extern __shared__ __attribute__((aligned(16))) uint16_t s_small[];  // staging [64][C] / image [C][32 dwords]; cm [C][C]
+  uint32_t* s_img = reinterpret_cast<uint32_t*>(s_small);
   int use_mode;
   if constexpr (FIXUP) {
     const int m0 = mode[0], m1 = mode[1];
@@ -1870,109 +1979,156 @@ __global__ void __launch_bounds__(kSmallRows * TL) mc_codes_small_kernel(
     use_mode = mode[0];
   }
   // C <= 64: the confusion matrix is privatised in LDS (at C = 2 every row's atomic hit one of 4 global words)
-  uint32_t* s_cm = reinterpret_cast<uint32_t*>(s_small + kSmallRows * C);
+  uint32_t* s_cm = reinterpret_cast<uint32_t*>(s_small + kSmallRows * ((C + 1) & ~1));
   const bool lds_cm = !FIXUP && confmat != nullptr && C <= kSmallCmMax;
   if (lds_cm)
     for (int i = threadIdx.x; i < C * C; i += kSmallRows * TL) s_cm[i] = 0u;
   const int64_t ntiles = n_pad / kSmallRows;
   bool bad = false;
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+  // lane -> (row, class chunk), opaque per tile: loop-invariant per-slot class indices, slot masks and image addresses
+  // hoisted out of the tile loop held ~40 VGPRs and ~30 SGPR spills (the loop body needs ~60 registers)
+  int lane_id = static_cast<int>(threadIdx.x);
+  asm volatile("" : "+v"(lane_id));
+  const int q = lane_id % TL, lr = lane_id / TL;  // lane within the row, row within the block
+  const int cb = q * kVpt;
   __syncthreads();  // previous tile's class segments were read from the image
   const int64_t r0 = tile * kSmallRows;
   const int rows = static_cast<int>(min<int64_t>(kSmallRows, n - r0));
-  // 1. stage the block's scores (byte range [r0 C, (r0 + rows) C) x 2; r0 C x 2 is a multiple of 128 B)
-  {
-    const int64_t nelem = (int64_t)rows * C;
-    const uint16_t* src = reinterpret_cast<const uint16_t*>(preds) + r0 * C;
-    const int nvec = static_cast<int>(nelem / 8);
-    for (int i = threadIdx.x; i < nvec; i += kSmallRows * TL)
-      reinterpret_cast<uint4*>(s_small)[i] = reinterpret_cast<const uint4*>(src)[i];
-    for (int i = nvec * 8 + threadIdx.x; i < nelem; i += kSmallRows * TL) s_small[i] = src[i];
-  }
-  __syncthreads();
-  const int q = threadIdx.x % TL, lr = threadIdx.x / TL;  // lane within the row, row within the block
   const int64_t r = r0 + lr;
-  const int cb = q * kVpt;
   const bool in_rows = lr < rows;
-  float v[kVpt];
-  uint16_t raw[kVpt];
+  // the lane's slots as packed fp32 pairs (2p, 2p + 1); slots past the class count (and rows past n) hold -inf
+  f32x2 P[kPairs];
+  if constexpr (DIRECT) {
+    uint4 w[2] = {make_uint4(0u, 0u, 0u, 0u), make_uint4(0u, 0u, 0u, 0u)};
+    const uint4* src = reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(preds) + r * C + cb);
+    const bool ok0 = in_rows && cb < C, ok1 = in_rows && cb + 8 < C;
+    if (ok0) w[0] = stream_load16(src);
+    if (ok1) w[1] = stream_load16(src + 1);
+    float u[16];
+    unpack8<T>(w[0], u);
+    unpack8<T>(w[1], u + 8);
 #pragma unroll
-  for (int j = 0; j < kVpt; ++j) {
-    const int c = cb + j;
-    const bool ok = in_rows && c < C;
-    raw[j] = ok ? s_small[lr * C + c] : (uint16_t)0;
-    v[j] = ok ? to_f32<T>(*reinterpret_cast<const T*>(&raw[j])) : -INFINITY;
+    for (int p = 0; p < kPairs; ++p)
+      P[p] = f32x2{(p < 4 ? ok0 : ok1) ? u[2 * p] : -INFINITY, (p < 4 ? ok0 : ok1) ? u[2 * p + 1] : -INFINITY};
+  } else {
+    // 1. stage the block's scores (byte range [r0 C, (r0 + rows) C) x 2; r0 C x 2 is a multiple of 128 B)
+    {
+      const int64_t nelem = (int64_t)rows * C;
+      const uint16_t* src = reinterpret_cast<const uint16_t*>(preds) + r0 * C;
+      const int nvec = static_cast<int>(nelem / 8);
+      for (int i = threadIdx.x; i < nvec; i += kSmallRows * TL)
+        reinterpret_cast<uint4*>(s_small)[i] = reinterpret_cast<const uint4*>(src)[i];
+      for (int i = nvec * 8 + threadIdx.x; i < nelem; i += kSmallRows * TL) s_small[i] = src[i];
+    }
+    __syncthreads();
+    auto at = [&](int j) -> float {
+      const int c = cb + j;
+      return (j < kVpt && in_rows && c < C) ? to_f32<T>(*reinterpret_cast<const T*>(&s_small[lr * C + c])) : -INFINITY;
+    };
+#pragma unroll
+    for (int p = 0; p < kPairs; ++p) P[p] = f32x2{at(2 * p), at(2 * p + 1)};
   }
   const int64_t t = in_rows ? target[r] : -1;
   const bool valid = in_rows && !(has_ignore && t == ignore_index);
   // row statistics over the TL lanes of the row (xor shuffles stay inside aligned groups of TL lanes)
+  // (masked slots are -inf: neutral for the maximum; excluded from the minimum and the sum)
   float mx = -INFINITY, mn = INFINITY, sum = 0.f;
 #pragma unroll
   for (int j = 0; j < kVpt; ++j) {
+    const float x = (j & 1) ? P[j >> 1].y : P[j >> 1].x;
+    mx = __builtin_fmaxf(mx, x);
     if (cb + j < C) {
-      mx = __builtin_fmaxf(mx, v[j]);
-      mn = __builtin_fminf(mn, v[j]);
-      sum += v[j];
+      mn = __builtin_fminf(mn, x);
+      sum += x;
     }
   }
-#pragma unroll
-  for (int off = 1; off < TL; off <<= 1) {
-    mx = __builtin_fmaxf(mx, __shfl_xor(mx, off, kWave));
-    mn = __builtin_fminf(mn, __shfl_xor(mn, off, kWave));
-    sum += __shfl_xor(sum, off, kWave);
-  }
+  mx = grp_max<TL>(mx);
+  mn = grp_min<TL>(mn);
+  sum = grp_sum<TL>(sum);
   bool fin = __builtin_isfinite(mx);
   // arg-max of a finite row: the first class holding the maximum
   int am = C;
 #pragma unroll
   for (int j = kVpt - 1; j >= 0; --j)
-    if (cb + j < C && v[j] == mx) am = cb + j;
-#pragma unroll
-  for (int off = 1; off < TL; off <<= 1) am = min(am, __shfl_xor(am, off, kWave));
+    if (cb + j < C && ((j & 1) ? P[j >> 1].y : P[j >> 1].x) == mx) am = cb + j;
+  am = grp_min_i32<TL>(am);
+  // exp / quotient / rounding on the packed pairs (round 5): v_pk_* and v_cvt_pk_bf16_f32 -- per component exactly
+  // the scalar sequences (exp_nonpos, div_rn, RNE), bit for bit.  Slots past the class count exist only in the last
+  // lanes of a row when C % 16 != 0 (wave-uniform test).
+  const bool masked = (CC > 0 ? (kVpt & 1) != 0 : C % kSmallVpt != 0);
   float s = 0.f, inv = 0.f;
-  if (use_mode != 0) {
-    float acc = 0.f;
+  // exp(x - max) of the slots and their row sum; the exps replace the scores in P only in softmax mode (probability
+  // mode keeps the scores: they are the codes, the sum only feeds the class pass's refit statistics)
+  auto exp_sum = [&](bool store) -> float {
+    const f32x2 m2 = {mx, mx};
+    // every valid element of every row of the wave within 86 of its maximum: the lean exp (exp_nonpos2_narrow)
+    const bool narrow = __ballot(!(mx - mn <= 86.f)) == 0;
+    f32x2 acc = {0.f, 0.f};
 #pragma unroll
-    for (int j = 0; j < kVpt; ++j) {
-      v[j] = cb + j < C ? exp_nonpos(v[j] - mx) : 0.f;
-      acc += v[j];
+    for (int p = 0; p < kPairs; ++p) {
+      f32x2 e = narrow ? exp_nonpos2_narrow(P[p] - m2) : exp_nonpos2(P[p] - m2);
+      if (masked) {
+        e.x = cb + 2 * p < C ? e.x : 0.f;
+        e.y = cb + 2 * p + 1 < C ? e.y : 0.f;
+      }
+      acc = acc + e;
+      if (store) P[p] = e;
     }
-#pragma unroll
-    for (int off = 1; off < TL; off <<= 1) acc += __shfl_xor(acc, off, kWave);
-    s = acc;
+    return grp_sum<TL>(acc.x + acc.y);
+  };
+  // softmax statistics: the codes in softmax mode, the class pass's refit of a mispredicted batch otherwise
+  if (use_mode != 0 || row_stats != nullptr) s = exp_sum(use_mode != 0);
+  if (use_mode != 0) {
     inv = 1.f / s;
     fin = fin && s == s;
   } else {
     fin = fin && __builtin_isfinite(sum);
-    if (row_stats != nullptr) {  // softmax statistics for the class pass's refit of a mispredicted batch
-      float acc = 0.f;
-#pragma unroll
-      for (int j = 0; j < kVpt; ++j) acc += cb + j < C ? exp_nonpos(v[j] - mx) : 0.f;
-#pragma unroll
-      for (int off = 1; off < TL; off <<= 1) acc += __shfl_xor(acc, off, kWave);
-      s = acc;
-    }
   }
   if (row_stats != nullptr && q == 0 && in_rows && !FIXUP)
     row_stats[r] = make_float4(mx, s, __uint_as_float((valid ? 1u : 0u) | (__builtin_isfinite(mx) && s == s ? 2u : 0u)), 0.f);
   const bool slow = valid && !fin;
   const bool keep = valid && fin;
-  // 3. codes into the image [C][64] (the staging area is free once every lane holds its values)
+  // 3. codes into the image (the staging area is free once every lane holds its values): pack class pairs, swap
+  //    halves with the partner row's lane, one dword per (class, row pair)
+  uint32_t word[kPairs];
+  const int tl = static_cast<int>(t) - cb;  // the positive's slot in this lane (any value when t is not here)
+  const uint32_t tflag = 0x4000u << (16 * (tl & 1));
+  if (keep && use_mode != 0) {  // softmax codes: quotients in [0, 1] are their own codes
+    const f32x2 s2 = {s, s}, i2 = {inv, inv};
+#pragma unroll
+    for (int p = 0; p < kPairs; ++p) {
+      const uint32_t w2 = pack_rne2<T>(div_rn2(P[p], s2, i2));
+      word[p] = w2 | ((tl >> 1) == p && tl >= 0 ? tflag : 0u);
+    }
+  } else {
+#pragma unroll
+    for (int p = 0; p < kPairs; ++p) {
+      uint32_t cw[2];
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int j = 2 * p + e;
+        const int c = cb + j;
+        uint32_t code = 0x8000u;  // padding rows / absent classes: skipped
+        if (j < kVpt && keep && c < C) {
+          code = raw_code<T>(half_bits<T>(e ? P[p].y : P[p].x));
+          if (c == t && !(code & 0x8000u)) code |= 0x4000u;
+        }
+        cw[e] = code;
+      }
+      word[p] = cw[0] | (cw[1] << 16);
+    }
+  }
+  const bool odd_row = (lr & 1) != 0;
+  const int k = lr >> 1;
   __syncthreads();
 #pragma unroll
-  for (int j = 0; j < kVpt; ++j) {
-    const int c = cb + j;
-    if (!in_rows || c >= C) continue;
-    uint32_t code = 0x8000u;
-    if (keep) {
-      const uint32_t b = use_mode != 0 ? (rne_word<T>(div_rn(v[j], s, inv)) >> 16) : (uint32_t)raw[j];
-      code = raw_code<T>(b);
-      if (c == t && !(code & 0x8000u)) code |= 0x4000u;
-    }
-    s_small[c * kSmallRows + lr] = static_cast<uint16_t>(code);
-  }
-  if (lr >= rows && q == 0) {  // padding rows of the last block: skipped codes
-    for (int c = 0; c < C; ++c) s_small[c * kSmallRows + lr] = 0x8000u;
+  for (int p = 0; p < kPairs; ++p) {
+    const uint32_t other = swz_xor<TL>(word[p]);  // the partner row's (even, odd) class pair
+    // even row lane: class cb + 2p of rows (2k, 2k+1); odd row lane: class cb + 2p + 1 of rows (2k, 2k+1)
+    const uint32_t packed = odd_row ? ((other >> 16) | (word[p] & 0xFFFF0000u)) : ((word[p] & 0xFFFFu) | (other << 16));
+    const int c = cb + 2 * p + (odd_row ? 1 : 0);
+    if (2 * p + (odd_row ? 1 : 0) < kVpt && c < C) s_img[c * 32 + ((k + (c >> 4) * kRot) & 31)] = packed;
   }
   if (q == 0 && in_rows) {
     if constexpr (!FIXUP) {
@@ -1989,10 +2145,13 @@ __global__ void __launch_bounds__(kSmallRows * TL) mc_codes_small_kernel(
   }
   if (!FIXUP && record_mode && q == 0) bad = bad || slow || (valid && (mx > 1.f || mn < 0.f));
   __syncthreads();
-  // class segments: C rows of 64 codes = 8 x 16 B each
+  // class segments: C rows of 64 codes = 8 x 16 B each (4 rotated dwords = two 8-B LDS reads: rot(c) is even)
   for (int i = threadIdx.x; i < C * 8; i += kSmallRows * TL) {
-    const int c = i >> 3, k = i & 7;
-    reinterpret_cast<uint4*>(codes + (int64_t)c * n_pad + r0)[k] = reinterpret_cast<const uint4*>(s_small + c * kSmallRows)[k];
+    const int c = i >> 3, m = i & 7;
+    const int base = c * 32, rot = (4 * m + (c >> 4) * kRot) & 31;
+    const uint2 a = *reinterpret_cast<const uint2*>(s_img + base + rot);
+    const uint2 b = *reinterpret_cast<const uint2*>(s_img + base + ((rot + 2) & 31));
+    reinterpret_cast<uint4*>(codes + (int64_t)c * n_pad + r0)[m] = make_uint4(a.x, a.y, b.x, b.y);
   }
   }  // tiles
   if (lds_cm) {  // per-block partial (summed by class_partial_reduce_kernel), else atomics on the few cells

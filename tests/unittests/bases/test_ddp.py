@@ -307,3 +307,31 @@ def test_sync_timeout_kwarg_validation():
         with pytest.raises(ValueError, match="sync_timeout"):
             SumMetric(sync_timeout=bad)
     assert SumMetric(sync_timeout=2.5).sync_timeout == 2.5
+
+
+def _owned_buffer_reuse_worker(rank, world):
+    """The sharded sync keeps its owned-class histogram buffer across syncs and clears only the previous code
+    window: computes over resets whose code ranges do not overlap (high codes, then low codes, then both) match the
+    replicated metric each time, and the buffer is reused."""
+    from torchmetrics_forked_amd.classification import MulticlassAUROC
+
+    g = torch.Generator().manual_seed(40 + rank)
+    ok = True
+    sharded = MulticlassAUROC(num_classes=5, average="none", sharded_compute=True)
+    plain = MulticlassAUROC(num_classes=5, average="none")
+    bufs = []
+    for lo, width in ((0.9, 0.1), (0.0, 0.05), (0.0, 1.0)):
+        sharded.reset()
+        plain.reset()
+        for _ in range(2):
+            p = (lo + torch.rand(32, 5, generator=g) * width).bfloat16()
+            t = torch.randint(0, 5, (32,), generator=g)
+            sharded.update(p, t)
+            plain.update(p, t)
+        ok &= bool(torch.allclose(sharded.compute(), plain.compute(), atol=1e-7, equal_nan=True))
+        bufs.append(sharded.__dict__["_owned_buf"][0].data_ptr())
+    return ok and len(set(bufs)) == 1
+
+
+def test_sharded_owned_buffer_reuse():
+    assert all(run_ddp(_owned_buffer_reuse_worker))

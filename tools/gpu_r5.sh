@@ -35,6 +35,15 @@ for s in "$@"; do
     prof) run prof 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o headline --output-format csv -- python3 bench.py --steps 20 --warmup 5 ;;
     radix) run radix 300 python tools/radix_curve_bench.py; tail -1 "$OUT/radix.log" ;;
     smallprobe) run smallprobe 240 python tools/mc_small_probe.py; tail -1 "$OUT/smallprobe.log" ;;
+    smallab) export PROBE_CONFIGS=${PROBE_CONFIGS:-64:1048576,100:262144,104:262144,256:262144,1000:65536,1001:65536}
+             run smallab_on 240 python tools/mc_small_probe.py; tail -1 "$OUT/smallab_on.log"
+             TMX_CURVE_SMALL_OFF=1 run smallab_off 240 python tools/mc_small_probe.py; tail -1 "$OUT/smallab_off.log"
+             run smallab_prof_on 300 rocprofv3 --kernel-trace --stats -d "$OUT/smallab_prof_on" -o on --output-format csv -- python3 tools/mc_small_probe.py
+             TMX_CURVE_SMALL_OFF=1 run smallab_prof_off 300 rocprofv3 --kernel-trace --stats -d "$OUT/smallab_prof_off" -o off --output-format csv -- python3 tools/mc_small_probe.py ;;
+    abprobe) export PROBE_CONFIGS=${PROBE_CONFIGS:-64:1048576,100:262144,104:262144,256:262144,10:1048576}
+             for v in default ${TMX_AB_VARIANTS:-}; do
+               if [ $v = default ]; then unset TMX_NATIVE_LIB; else export TMX_NATIVE_LIB=$PWD/build/ab/$v/_tmx_native.so; fi
+               run abprobe_$v 240 python tools/mc_small_probe.py; echo "$v: $(tail -1 $OUT/abprobe_$v.log)"; done; unset TMX_NATIVE_LIB ;;
     smallprof) PROBE_SMALL_ONLY=1 run smallprof 300 rocprofv3 --kernel-trace --stats -d "$OUT/smallprof" -o small --output-format csv -- python3 tools/mc_small_probe.py ;;
     radixab) for r in 1 2; do
                TMX_NATIVE_LIB=$PWD/build/ab_radix/_tmx_native.so run radix_old_$r 300 python tools/radix_curve_bench.py; tail -1 "$OUT/radix_old_$r.log"

@@ -30,6 +30,8 @@ CONFIGS = ((2, 1 << 20), (10, 1 << 20), (16, 1 << 20), (64, 1 << 20), (100, 1 <<
            (1000, 1 << 16), (1001, 1 << 16))
 if os.environ.get("PROBE_SMALL_ONLY"):
     CONFIGS = CONFIGS[:4]
+if os.environ.get("PROBE_CONFIGS"):  # "C:N,C:N,..."
+    CONFIGS = tuple(tuple(int(v) for v in cn.split(":")) for cn in os.environ["PROBE_CONFIGS"].split(","))
 for C, N in CONFIGS:
     p = torch.randn(N, C, device=dev).bfloat16()
     t = torch.randint(0, C, (N,), device=dev)

@@ -809,7 +809,7 @@ class Metric(Module, ABC):
 
     def __getstate__(self) -> Dict[str, Any]:
         self._join_side_work()
-        return {k: v for k, v in self.__dict__.items() if k not in ("update", "compute", "_update_signature", "_hist_spare", "_batch_bufs", "_batch_sink", "_batch_view", "_fast_update", "_sum_fwd", "_sum_fwd_defaults", "_tensor_states")}
+        return {k: v for k, v in self.__dict__.items() if k not in ("update", "compute", "_update_signature", "_hist_spare", "_batch_bufs", "_batch_sink", "_batch_view", "_fast_update", "_sum_fwd", "_sum_fwd_defaults", "_tensor_states", "_owned_buf")}
 
     def __setstate__(self, state: Dict[str, Any]) -> None:
         self.__dict__.update(state)
