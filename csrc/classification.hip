@@ -1259,11 +1259,12 @@ void launch_small_two_pass(const T* p, const int64_t* target, int64_t n, int C, 
   // the row pass latency-bound, 40 us for 1M x 10 bf16)
   static const int grid_cap = [] { const char* v = std::getenv("TMX_SMALL_GRID"); return v ? std::atoi(v) : 8192; }();
   const int grid = static_cast<int>(std::min<int64_t>(ntiles, std::max(256, grid_cap / TL)));
-  // class pass: the windowed u32 LDS histogram of the headline route (class_hist_hi_kernel) for C > 16 -- the
-  // packed partial-flush pass + reduce launch took 48 + 12 us at C = 256 x 262,144 against ~30 us for the same bytes
-  // at C = 1000; C <= 16 keeps the partial pass (few classes: every split of a class hits the same few thousand bins)
-  static const bool hi_off = std::getenv("TMX_SMALL_CLASS_PARTIAL") != nullptr;  // A/B knob
-  const bool hi_pass = C > 16 && !hi_off;
+  // class pass: the packed partial-flush pass + reduce launch.  The windowed u32 pass of the headline route
+  // (class_hist_hi_kernel; opt-in TMX_SMALL_CLASS_HI=1, C > 16) measured slower here: 127 / 95 / 50 us at C = 64 x 1M,
+  // 100 x 262k, 256 x 262k against 51 / 22 / 48 us (few classes concentrate the codes on few bins: LDS atomic
+  // contention in its window), gpurun_out r5ar
+  static const bool hi_on = std::getenv("TMX_SMALL_CLASS_HI") != nullptr;
+  const bool hi_pass = C > 16 && hi_on;
   // confusion-matrix partials per block (C <= 64: at most 16 MiB), summed by a reduce launch: no same-cell atomics
   const bool use_pcm = cm != nullptr && C <= (hi_pass ? kSmallCmMax : 32);
   // per-stream cached scratch (no allocator round trips per update); stream order keeps consecutive updates apart
@@ -1667,8 +1668,8 @@ void curve_hist_update_impl(const at::Tensor& preds_, const at::Tensor& target_,
     static const bool small_off_b = std::getenv("TMX_CURVE_SMALL_OFF") != nullptr;
     const bool small_route = task == 0 && !small_off_b && C <= kSmallVpt * 16 && (reinterpret_cast<uintptr_t>(preds.data_ptr()) & 15) == 0;
     // the small route's windowed class pass (C > 16) fills the batch histogram too
-    static const bool small_partial = std::getenv("TMX_SMALL_CLASS_PARTIAL") != nullptr;
-    const bool small_dual = small_route && C > 16 && !small_partial;
+    static const bool small_hi = std::getenv("TMX_SMALL_CLASS_HI") != nullptr;
+    const bool small_dual = small_route && C > 16 && small_hi;
     const bool ml_route = task == 1 && C != 1 && C % 8 == 0 && C <= 8 * 2 * kWave && target.dim() >= 1 && target.numel() == target.size(0) * C &&
                           (reinterpret_cast<uintptr_t>(preds.data_ptr()) & 15) == 0 && (reinterpret_cast<uintptr_t>(target.data_ptr()) & 15) == 0;
     const bool dual_route = (task == 0 && two_pass_ok && !small_route) || small_dual || ml_route;

@@ -395,34 +395,37 @@ struct RowLoads {
 };
 
 // UNALIGNED (C % 8 != 0, rows at stride C: round 5, no padding copy): a row starts 2 ((r C) % 8) bytes past a 16-B
-// boundary; its 16-B vectors are loaded at the row's own addresses (gfx950 global loads take any 2-byte alignment at
-// full speed: tools/kexp/unaligned_load_exp.hip, 0 wrong elements, 47.5 vs 47.4 us per 131 MB sweep).  The row's last
-// vector is partial: its slots past the row (the next row's first scores) take the value of its slot 0, a real score of
-// the row, so maxima, minima and the arg-max (lowest slot wins) are unchanged; the exp-sum skips them.  The last vector
-// of the last row is assembled from 16-bit loads that stop at the tensor's end.
-template <typename T>
-__device__ __forceinline__ uint4 load_row_vec_unaligned(const T* __restrict__ preds, int64_t e0, int rem, int64_t total) {
-  const uint16_t* p = reinterpret_cast<const uint16_t*>(preds);
-  uint4 w;
-  if (e0 + 8 <= total) {
-    w = stream_load16(reinterpret_cast<const uint4*>(p + e0));
-  } else {
-    uint32_t d[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const uint32_t lo = e0 + 2 * k < total ? p[e0 + 2 * k] : 0u, hi = e0 + 2 * k + 1 < total ? p[e0 + 2 * k + 1] : 0u;
-      d[k] = lo | (hi << 16);
-    }
-    w = make_uint4(d[0], d[1], d[2], d[3]);
+// boundary; its full 16-B vectors are loaded at the row's own addresses (gfx950 global loads take any 2-byte
+// alignment: tools/kexp/unaligned_load_exp.hip, 0 wrong elements; tools/kexp/unaligned_bw_exp.hip, 4.8 vs 5.5 TB/s
+// streaming).  The row's last, partial vector is loaded as the 16 B that END at the row's end -- always inside the
+// tensor, the last row included -- and rotated by R = 8 - rem slots into place: slots [0, rem) hold the row's last
+// rem scores, slots [rem, 8) the R scores before them (real scores of the row, so maxima, minima and the arg-max --
+// lowest lane wins -- are unchanged; the exp-sum skips them).  Lanes past the row's vectors load vector 0.
+__device__ __forceinline__ uint4 rotate_slots(uint4 w, int R) {  // slot k <- slot (k + R) mod 8, R wave-uniform
+  uint32_t d[4] = {w.x, w.y, w.z, w.w};
+  if (R & 4) {  // 2 dwords
+    const uint32_t t0 = d[0], t1 = d[1];
+    d[0] = d[2]; d[1] = d[3]; d[2] = t0; d[3] = t1;
   }
-  if (rem < 8) {  // partial vector: slots >= rem repeat slot 0
-    const uint32_t s0 = w.x & 0xFFFFu, d0 = s0 | (s0 << 16);
-    auto fix = [&](uint32_t dw, int k) -> uint32_t {
-      return 2 * k + 1 < rem ? dw : (2 * k < rem ? ((dw & 0xFFFFu) | (s0 << 16)) : d0);
-    };
-    w = make_uint4(fix(w.x, 0), fix(w.y, 1), fix(w.z, 2), fix(w.w, 3));
+  if (R & 2) {  // 1 dword
+    const uint32_t t0 = d[0];
+    d[0] = d[1]; d[1] = d[2]; d[2] = d[3]; d[3] = t0;
   }
-  return w;
+  if (R & 1) {  // 2 bytes: dword k = high half of d[k], low half of d[k + 1]
+    const uint32_t t0 = d[0];
+    d[0] = __builtin_amdgcn_alignbyte(d[1], d[0], 2);
+    d[1] = __builtin_amdgcn_alignbyte(d[2], d[1], 2);
+    d[2] = __builtin_amdgcn_alignbyte(d[3], d[2], 2);
+    d[3] = __builtin_amdgcn_alignbyte(t0, d[3], 2);
+  }
+  return make_uint4(d[0], d[1], d[2], d[3]);
+}
+// the row's vectors as loaded by row_tile_load<UNALIGNED>, with the partial vector (last group) rotated into place
+template <int NG>
+__device__ __forceinline__ void realign_partial(uint4 (&w)[2], int ld) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int nvec = (ld + 7) / 8;
+  if (lane + kWave * (NG - 1) == nvec - 1) w[NG - 1] = rotate_slots(w[NG - 1], 8 * nvec - ld);
 }
 
 template <typename T, int NG, bool UNALIGNED = false>
@@ -432,8 +435,8 @@ __device__ __forceinline__ void row_tile_load(const T* __restrict__ preds, const
   const int wave = threadIdx.x / kWave;
   const int nvec = UNALIGNED ? (ld + 7) / 8 : ld / 8;
   const bool lo_ok = lane < nvec, hi_ok = lane + kWave < nvec;
-  const int lq = lo_ok ? lane : nvec - 1;  // clamped: every load stays inside its row
-  const int hq = hi_ok ? lane + kWave : nvec - 1;
+  const int lq = lo_ok ? lane : (UNALIGNED ? 0 : nvec - 1);  // clamped: every load stays inside its row
+  const int hq = hi_ok ? lane + kWave : (UNALIGNED ? 0 : nvec - 1);
   auto row0_of = [&](int pp) -> int64_t { return tile * kTileRows + 2 * (wave + pp * kRowWaves); };
   L.tv = target[min(row0_of((lane & 3) >> 1) + (lane & 1), n - 1)];
 #pragma unroll
@@ -441,10 +444,22 @@ __device__ __forceinline__ void row_tile_load(const T* __restrict__ preds, const
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       if constexpr (UNALIGNED) {
-        const int64_t base = min(row0_of(pp) + h, n - 1) * ld, total = n * ld;
-        L.raw[pp][h][0] = load_row_vec_unaligned<T>(preds, base + 8 * lq, lq == nvec - 1 ? ld - 8 * lq : 8, total);
-        if constexpr (NG == 2)
-          L.raw[pp][h][1] = load_row_vec_unaligned<T>(preds, base + 8 * hq, hq == nvec - 1 ? ld - 8 * hq : 8, total);
+#ifdef TMX_UNALIGNED_TIMING_HACK  // timing experiment only (wrong data): the same loads at 16-B aligned addresses
+        const uint16_t* row = reinterpret_cast<const uint16_t*>(preds) + (min(row0_of(pp) + h, n - 1) * ld & ~int64_t{7});
+#else
+        const uint16_t* row = reinterpret_cast<const uint16_t*>(preds) + min(row0_of(pp) + h, n - 1) * ld;
+#endif
+        const int R = 8 * nvec - ld;  // 1..7
+        // the partial vector lives in the last group: NG == 2 -> the hi group (nvec > 64), NG == 1 -> the lo group
+        // (the rotation waits until the vector is consumed -- realign_partial -- so every load is in flight first:
+        // rotating here stalled the next rows' loads on this one, +7 us per 65,536 x 1001 row pass)
+        if constexpr (NG == 2) {
+          L.raw[pp][h][0] = stream_load16(reinterpret_cast<const uint4*>(row + 8 * lq));
+          L.raw[pp][h][1] = stream_load16(reinterpret_cast<const uint4*>(row + (hq == nvec - 1 ? ld - 8 : 8 * hq)));
+        } else {
+          L.raw[pp][h][0] = stream_load16(reinterpret_cast<const uint4*>(row + (lq == nvec - 1 ? ld - 8 : 8 * lq)));
+        }
+        (void)R;
       } else {
         const uint4* row = reinterpret_cast<const uint4*>(preds + min(row0_of(pp) + h, n - 1) * ld);
         L.raw[pp][h][0] = stream_load16(row + lq);
@@ -547,12 +562,16 @@ __device__ __forceinline__ void row_tile_compute(const RowLoads<NG>& L, int64_t 
     const bool va = r0 < n && !(has_ignore && ta == ignore_index);
     const bool vb = r0 + 1 < n && !(has_ignore && tb == ignore_index);
     RowStat<NG> ra, rb;
+    // the row pair's vectors (PADDED = UNALIGNED rows: the partial vector rotated into place)
+    uint4 wa[2] = {raw[pp][0][0], raw[pp][0][1]}, wb[2] = {raw[pp][1][0], raw[pp][1][1]};
     if constexpr (PADDED) {
-      row_stat_padded<T, NG>(raw[pp][0], nlo, nhi, ra);
-      row_stat_padded<T, NG>(raw[pp][1], nlo, nhi, rb);
+      realign_partial<NG>(wa, ld);
+      realign_partial<NG>(wb, ld);
+      row_stat_padded<T, NG>(wa, nlo, nhi, ra);
+      row_stat_padded<T, NG>(wb, nlo, nhi, rb);
     } else {
-      row_stat<T, NG>(raw[pp][0], lo_ok, hi_ok, ra);
-      row_stat<T, NG>(raw[pp][1], lo_ok, hi_ok, rb);
+      row_stat<T, NG>(wa, lo_ok, hi_ok, ra);
+      row_stat<T, NG>(wb, lo_ok, hi_ok, rb);
     }
     bool fa = __builtin_isfinite(ra.mx), fb = __builtin_isfinite(rb.mx);
     const int ama = row_argmax<NG>(ra), amb = row_argmax<NG>(rb);
@@ -607,8 +626,8 @@ __device__ __forceinline__ void row_tile_compute(const RowLoads<NG>& L, int64_t 
       if constexpr (SOFTMAX) {
         packed = pack_rne2<T>(div_rn2(f32x2{ra.v[j], rb.v[j]}, f32x2{sa, sb}, f32x2{ia, ib}));
       } else {
-        const uint32_t ca = raw_code<T>(raw_bits<T>(raw[pp][0][j >> 3], j & 7));
-        const uint32_t cb = raw_code<T>(raw_bits<T>(raw[pp][1][j >> 3], j & 7));
+        const uint32_t ca = raw_code<T>(raw_bits<T>(wa[j >> 3], j & 7));
+        const uint32_t cb = raw_code<T>(raw_bits<T>(wb[j >> 3], j & 7));
         packed = ca | (cb << 16);
       }
       const int c = 512 * (j >> 3) + 8 * lane + (j & 7);
@@ -727,10 +746,15 @@ __device__ __forceinline__ void row_tile_softmax_lean(const RowLoads<NG>& L, int
     const bool vb = r0 + 1 < n && !(has_ignore && tb == ignore_index);
     f32x2 P[8 * NG];
     float mlo_a, mlo_b, mhi_a = -INFINITY, mhi_b = -INFINITY, mn_a, mn_b;
+    uint4 wa[2] = {L.raw[pp][0][0], L.raw[pp][0][1]}, wb[2] = {L.raw[pp][1][0], L.raw[pp][1][1]};
+    if constexpr (UNALIGNED) {
+      realign_partial<NG>(wa, ld);
+      realign_partial<NG>(wb, ld);
+    }
     {
       float a[8], b[8];
-      unpack8<T>(L.raw[pp][0][0], a);
-      unpack8<T>(L.raw[pp][1][0], b);
+      unpack8<T>(wa[0], a);
+      unpack8<T>(wb[0], b);
       mlo_a = max8(a);
       mlo_b = max8(b);
       mn_a = min8(a);
@@ -740,8 +764,8 @@ __device__ __forceinline__ void row_tile_softmax_lean(const RowLoads<NG>& L, int
     }
     if constexpr (NG == 2) {
       float a[8], b[8];
-      unpack8<T>(L.raw[pp][0][1], a);
-      unpack8<T>(L.raw[pp][1][1], b);
+      unpack8<T>(wa[1], a);
+      unpack8<T>(wb[1], b);
       mhi_a = max8(a);
       mhi_b = max8(b);
       mn_a = __builtin_fminf(mn_a, min8(a));
@@ -775,9 +799,19 @@ __device__ __forceinline__ void row_tile_softmax_lean(const RowLoads<NG>& L, int
     const bool narrow = __ballot(!(mxa - mn_a <= 86.f && mxb - mn_b <= 86.f)) == 0;
     const f32x2 mx2 = {mxa, mxb};
     f32x2 acc = {0.f, 0.f}, acc_lo = {0.f, 0.f};
+    // the partial vector sits in the last class group (nvec - 1 >= 64 when NG == 2): scale its slots by 0 / 1
     auto counted = [&](int j) -> f32x2 {
-      if constexpr (UNALIGNED) return (j & 7) < (j < 8 ? cut_lo : cut_hi) ? P[j] : f32x2{0.f, 0.f};
-      else return P[j];
+      if constexpr (UNALIGNED
+#ifdef TMX_UNALIGNED_NOMASK_HACK  // timing experiment only
+                    && false
+#endif
+      ) {
+        if (j >= 8 * (NG - 1)) {
+          const float m = (j & 7) < (NG == 2 ? cut_hi : cut_lo) ? 1.f : 0.f;
+          return P[j] * f32x2{m, m};
+        }
+      }
+      return P[j];
     };
     if (narrow) {
 #pragma unroll

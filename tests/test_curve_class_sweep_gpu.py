@@ -4,7 +4,7 @@ the one built from ATen's GPU softmax of the same logits, the fused confusion ma
 from the histogram vs the sort-based computation on ATen's scores.
 
 Routes covered: the small-class row pass (C <= 256: DIRECT 16-B loads for C % 8 == 0, LDS staging otherwise) with
-the partial class pass (C <= 16) or the windowed class pass (C > 16); the tile row pass with rows read in place at
+the partial class pass; the tile row pass with rows read in place at
 stride C for C % 8 != 0 (UNALIGNED, no padding copy: C = 300, 999, 1001); and the round-4 u16 class pass
 (``TMX_CLASS_PASS_U16=1``, whole 65,536-row chunks whose 16-bit counters can wrap) in a child process.
 The row pass sums exp(x - max) in a different fp32 order than ATen's softmax, so a quotient within an ulp of a 16-bit

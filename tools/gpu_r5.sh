@@ -44,6 +44,9 @@ for s in "$@"; do
              for v in default ${TMX_AB_VARIANTS:-}; do
                if [ $v = default ]; then unset TMX_NATIVE_LIB; else export TMX_NATIVE_LIB=$PWD/build/ab/$v/_tmx_native.so; fi
                run abprobe_$v 240 python tools/mc_small_probe.py; echo "$v: $(tail -1 $OUT/abprobe_$v.log)"; done; unset TMX_NATIVE_LIB ;;
+    abprof) export PROBE_CONFIGS=${PROBE_CONFIGS:-64:1048576,100:262144,104:262144,256:262144,10:1048576,1000:65536,1001:65536}
+            run abprof 300 rocprofv3 --kernel-trace --stats -d "$OUT/abprof" -o ab --output-format csv -- python3 tools/mc_small_probe.py ;;
+    abpmc) run abpmc 200 rocprofv3 --kernel-trace --pmc ${TMX_PMC:-SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU} -d "$OUT/abpmc" -o pmc --output-format csv -- python3 tools/mc_small_probe.py ;;
     smallprof) PROBE_SMALL_ONLY=1 run smallprof 300 rocprofv3 --kernel-trace --stats -d "$OUT/smallprof" -o small --output-format csv -- python3 tools/mc_small_probe.py ;;
     radixab) for r in 1 2; do
                TMX_NATIVE_LIB=$PWD/build/ab_radix/_tmx_native.so run radix_old_$r 300 python tools/radix_curve_bench.py; tail -1 "$OUT/radix_old_$r.log"
