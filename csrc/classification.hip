@@ -1202,6 +1202,56 @@ __global__ void __launch_bounds__(256) curve_hist_mc_kernel(const T* __restrict_
 //   3. codes go through an LDS image [C][64] to the class-major scratch as 128-B class segments.
 // The FIXUP instance redoes the codes of a mis-speculated batch (mode[0] != mode[1]); the class pass is shared.
 // ---------------------------------------------------------------------------------------------------------
+// The small-class row kernel instance launch_small_rows runs for (TL, C, direct), as a function pointer (occupancy).
+template <typename T, bool FIXUP>
+static const void* small_rows_kernel(int TL, int C, bool direct) {
+#define TMX_SK(...) reinterpret_cast<const void*>(&mc_codes_small_kernel<__VA_ARGS__>)
+  if (TL == 1 && C >= 2 && C <= 16) {
+    switch (C) {
+      case 2: return TMX_SK(T, 1, FIXUP, 2);   case 3: return TMX_SK(T, 1, FIXUP, 3);   case 4: return TMX_SK(T, 1, FIXUP, 4);
+      case 5: return TMX_SK(T, 1, FIXUP, 5);   case 6: return TMX_SK(T, 1, FIXUP, 6);   case 7: return TMX_SK(T, 1, FIXUP, 7);
+      case 8: return TMX_SK(T, 1, FIXUP, 8);   case 9: return TMX_SK(T, 1, FIXUP, 9);   case 10: return TMX_SK(T, 1, FIXUP, 10);
+      case 11: return TMX_SK(T, 1, FIXUP, 11); case 12: return TMX_SK(T, 1, FIXUP, 12); case 13: return TMX_SK(T, 1, FIXUP, 13);
+      case 14: return TMX_SK(T, 1, FIXUP, 14); case 15: return TMX_SK(T, 1, FIXUP, 15); default: return TMX_SK(T, 1, FIXUP, 16);
+    }
+  }
+  switch (TL) {
+    case 1: return direct ? TMX_SK(T, 1, FIXUP, 0, true) : TMX_SK(T, 1, FIXUP);
+    case 2: return direct ? TMX_SK(T, 2, FIXUP, 0, true) : TMX_SK(T, 2, FIXUP);
+    case 4: return direct ? TMX_SK(T, 4, FIXUP, 0, true) : TMX_SK(T, 4, FIXUP);
+    case 8: return direct ? TMX_SK(T, 8, FIXUP, 0, true) : TMX_SK(T, 8, FIXUP);
+    default: return direct ? TMX_SK(T, 16, FIXUP, 0, true) : TMX_SK(T, 16, FIXUP);
+  }
+#undef TMX_SK
+}
+
+// Blocks of the small-class row pass: every resident slot on every CU once (blocks loop over 64-row tiles).  A
+// fixed 8192 / TL-block grid left a partial second round at C = 64 (TL = 4: 2048 blocks over 1280 resident slots --
+// a third of the chip idle for half the kernel).
+template <typename T>
+static int small_rows_grid(int TL, int C, bool direct, size_t shm, int64_t ntiles) {
+  static std::mutex mu;
+  static std::map<std::tuple<const void*, size_t, int>, int> cache;
+  const void* k = small_rows_kernel<T, false>(TL, C, direct);
+  int dev = 0;
+  TMX_CHECK_HIP(hipGetDevice(&dev));
+  int per_cu = 0;
+  {
+    std::lock_guard<std::mutex> lock(mu);
+    auto it = cache.find({k, shm, dev});
+    if (it == cache.end()) {
+      int nb = 0, cus = 0;
+      TMX_CHECK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, kSmallRows * TL, shm));
+      TMX_CHECK_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+      it = cache.emplace(std::make_tuple(k, shm, dev), std::max(1, nb) * std::max(1, cus)).first;
+    }
+    per_cu = it->second;
+  }
+  static const int grid_cap = [] { const char* v = std::getenv("TMX_SMALL_GRID"); return v ? std::atoi(v) : 0; }();  // A/B knob
+  const int64_t want = grid_cap > 0 ? grid_cap / TL : per_cu;
+  return static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(ntiles, want)));
+}
+
 template <typename T, bool FIXUP>
 void launch_small_rows(int TL, int grid, const T* p, const int64_t* target, int64_t n, int C, int* mode, int64_t ignore_index, bool has_ignore,
                        uint16_t* codes, int64_t n_pad, int64_t* cm, int* err, bool rec, int* srows, int* scount, uint32_t* pcm,
@@ -1257,8 +1307,8 @@ void launch_small_two_pass(const T* p, const int64_t* target, int64_t n, int C, 
   // a block loops over 64-row tiles: ~8-16 waves per CU in flight, and one LDS confusion-matrix flush per block
   // (8192 / TL blocks: up to 32 waves per CU — at 2048 / TL the one-wave blocks of C <= 16 left the CUs at 8 waves and
   // the row pass latency-bound, 40 us for 1M x 10 bf16)
-  static const int grid_cap = [] { const char* v = std::getenv("TMX_SMALL_GRID"); return v ? std::atoi(v) : 8192; }();
-  const int grid = static_cast<int>(std::min<int64_t>(ntiles, std::max(256, grid_cap / TL)));
+  const size_t shm = (size_t)kSmallRows * ((C + 1) & ~1) * sizeof(uint16_t) + (C <= kSmallCmMax ? (size_t)C * C * sizeof(uint32_t) : 0);
+  const int grid = small_rows_grid<T>(TL, C, C % 8 == 0 && (reinterpret_cast<uintptr_t>(p) & 15) == 0, shm, ntiles);
   // class pass: the packed partial-flush pass + reduce launch.  The windowed u32 pass of the headline route
   // (class_hist_hi_kernel; opt-in TMX_SMALL_CLASS_HI=1, C > 16) measured slower here: 127 / 95 / 50 us at C = 64 x 1M,
   // 100 x 262k, 256 x 262k against 51 / 22 / 48 us (few classes concentrate the codes on few bins: LDS atomic

@@ -2019,6 +2019,28 @@ __global__ void __launch_bounds__(kSmallRows * TL) TMX_SMALL_WPE_ATTR mc_codes_s
     for (int i = threadIdx.x; i < C * C; i += kSmallRows * TL) s_cm[i] = 0u;
   const int64_t ntiles = n_pad / kSmallRows;
   bool bad = false;
+  // DIRECT: the next tile's scores (and targets) are loaded into registers before this tile is processed, and the
+  // tile's barriers wait for LDS only (s_waitcnt lgkmcnt(0); s_barrier): __syncthreads() also drains vmcnt, which
+  // would wait for the prefetch.  The image is the only block-shared state, so the LDS-only barrier is sufficient.
+  auto lds_barrier = [&]() {
+    if constexpr (DIRECT) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else __syncthreads();
+  };
+  uint4 nxt[2] = {make_uint4(0u, 0u, 0u, 0u), make_uint4(0u, 0u, 0u, 0u)};
+  int64_t nxt_t = -1;
+  auto prefetch = [&](int64_t tl_) {
+    const int lid = static_cast<int>(threadIdx.x);
+    const int q_ = lid % TL, lr_ = lid / TL, cb_ = q_ * kVpt;
+    const int64_t rr = tl_ * kSmallRows + lr_;
+    const bool inr = tl_ < ntiles && rr < n;
+    const uint4* src = reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(preds) + rr * C + cb_);
+    nxt[0] = make_uint4(0u, 0u, 0u, 0u);
+    nxt[1] = make_uint4(0u, 0u, 0u, 0u);
+    if (inr && cb_ < C) nxt[0] = stream_load16(src);
+    if (inr && cb_ + 8 < C) nxt[1] = stream_load16(src + 1);
+    nxt_t = inr ? target[rr] : -1;
+  };
+  if constexpr (DIRECT) prefetch(blockIdx.x);
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
   // lane -> (row, class chunk), opaque per tile: loop-invariant per-slot class indices, slot masks and image addresses
   // hoisted out of the tile loop held ~40 VGPRs and ~30 SGPR spills (the loop body needs ~60 registers)
@@ -2026,19 +2048,19 @@ __global__ void __launch_bounds__(kSmallRows * TL) TMX_SMALL_WPE_ATTR mc_codes_s
   asm volatile("" : "+v"(lane_id));
   const int q = lane_id % TL, lr = lane_id / TL;  // lane within the row, row within the block
   const int cb = q * kVpt;
-  __syncthreads();  // previous tile's class segments were read from the image
+  lds_barrier();  // previous tile's class segments were read from the image
   const int64_t r0 = tile * kSmallRows;
   const int rows = static_cast<int>(min<int64_t>(kSmallRows, n - r0));
   const int64_t r = r0 + lr;
   const bool in_rows = lr < rows;
   // the lane's slots as packed fp32 pairs (2p, 2p + 1); slots past the class count (and rows past n) hold -inf
   f32x2 P[kPairs];
+  int64_t t_pref = -1;
   if constexpr (DIRECT) {
-    uint4 w[2] = {make_uint4(0u, 0u, 0u, 0u), make_uint4(0u, 0u, 0u, 0u)};
-    const uint4* src = reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(preds) + r * C + cb);
+    const uint4 w[2] = {nxt[0], nxt[1]};
+    t_pref = nxt_t;
+    prefetch(tile + gridDim.x);  // in flight while this tile is processed
     const bool ok0 = in_rows && cb < C, ok1 = in_rows && cb + 8 < C;
-    if (ok0) w[0] = stream_load16(src);
-    if (ok1) w[1] = stream_load16(src + 1);
     float u[16];
     unpack8<T>(w[0], u);
     unpack8<T>(w[1], u + 8);
@@ -2063,34 +2085,49 @@ __global__ void __launch_bounds__(kSmallRows * TL) TMX_SMALL_WPE_ATTR mc_codes_s
 #pragma unroll
     for (int p = 0; p < kPairs; ++p) P[p] = f32x2{at(2 * p), at(2 * p + 1)};
   }
-  const int64_t t = in_rows ? target[r] : -1;
+  const int64_t t = DIRECT ? t_pref : (in_rows ? target[r] : -1);
   const bool valid = in_rows && !(has_ignore && t == ignore_index);
   // row statistics over the TL lanes of the row (xor shuffles stay inside aligned groups of TL lanes)
-  // (masked slots are -inf: neutral for the maximum; excluded from the minimum and the sum)
-  float mx = -INFINITY, mn = INFINITY, sum = 0.f;
+  // (masked slots are -inf: neutral for the maximum; excluded from the minimum and the sum).  Slots past the class
+  // count exist only in the last lanes of a row when C % 16 != 0 (wave-uniform): otherwise the trees run unmasked.
+  const bool masked = (CC > 0 ? (kVpt & 1) != 0 : C % kSmallVpt != 0);
+  auto slot = [&](int j) -> float { return (j & 1) ? P[j >> 1].y : P[j >> 1].x; };
+  float mx, mn;
+  if (!masked) {
+    float a[kVpt], b[kVpt];
 #pragma unroll
-  for (int j = 0; j < kVpt; ++j) {
-    const float x = (j & 1) ? P[j >> 1].y : P[j >> 1].x;
-    mx = __builtin_fmaxf(mx, x);
-    if (cb + j < C) {
-      mn = __builtin_fminf(mn, x);
-      sum += x;
+    for (int j = 0; j < kVpt; ++j) a[j] = b[j] = slot(j);
+#pragma unroll
+    for (int w = 1; w < kVpt; w *= 2)  // balanced trees (v_max3 / v_min3 after the compiler's folding)
+#pragma unroll
+      for (int j = 0; j + w < kVpt; j += 2 * w) {
+        a[j] = __builtin_fmaxf(a[j], a[j + w]);
+        b[j] = __builtin_fminf(b[j], b[j + w]);
+      }
+    mx = a[0];
+    mn = b[0];
+  } else {
+    mx = -INFINITY;
+    mn = INFINITY;
+#pragma unroll
+    for (int j = 0; j < kVpt; ++j) {
+      mx = __builtin_fmaxf(mx, slot(j));
+      if (cb + j < C) mn = __builtin_fminf(mn, slot(j));
     }
   }
   mx = grp_max<TL>(mx);
   mn = grp_min<TL>(mn);
-  sum = grp_sum<TL>(sum);
   bool fin = __builtin_isfinite(mx);
-  // arg-max of a finite row: the first class holding the maximum
+  // arg-max of a finite row (the first class holding the maximum): only for the fused confusion matrix
   int am = C;
+  if (!FIXUP && confmat != nullptr) {
 #pragma unroll
-  for (int j = kVpt - 1; j >= 0; --j)
-    if (cb + j < C && ((j & 1) ? P[j >> 1].y : P[j >> 1].x) == mx) am = cb + j;
-  am = grp_min_i32<TL>(am);
+    for (int j = kVpt - 1; j >= 0; --j)
+      if (cb + j < C && slot(j) == mx) am = cb + j;
+    am = grp_min_i32<TL>(am);
+  }
   // exp / quotient / rounding on the packed pairs (round 5): v_pk_* and v_cvt_pk_bf16_f32 -- per component exactly
-  // the scalar sequences (exp_nonpos, div_rn, RNE), bit for bit.  Slots past the class count exist only in the last
-  // lanes of a row when C % 16 != 0 (wave-uniform test).
-  const bool masked = (CC > 0 ? (kVpt & 1) != 0 : C % kSmallVpt != 0);
+  // the scalar sequences (exp_nonpos, div_rn, RNE), bit for bit
   float s = 0.f, inv = 0.f;
   // exp(x - max) of the slots and their row sum; the exps replace the scores in P only in softmax mode (probability
   // mode keeps the scores: they are the codes, the sum only feeds the class pass's refit statistics)
@@ -2117,7 +2154,11 @@ __global__ void __launch_bounds__(kSmallRows * TL) TMX_SMALL_WPE_ATTR mc_codes_s
     inv = 1.f / s;
     fin = fin && s == s;
   } else {
-    fin = fin && __builtin_isfinite(sum);
+    float sum = 0.f;  // probability mode: a row is counted when its scores' sum is finite (no NaN / inf)
+#pragma unroll
+    for (int j = 0; j < kVpt; ++j)
+      if (cb + j < C) sum += slot(j);
+    fin = fin && __builtin_isfinite(grp_sum<TL>(sum));
   }
   if (row_stats != nullptr && q == 0 && in_rows && !FIXUP)
     row_stats[r] = make_float4(mx, s, __uint_as_float((valid ? 1u : 0u) | (__builtin_isfinite(mx) && s == s ? 2u : 0u)), 0.f);
@@ -2126,14 +2167,18 @@ __global__ void __launch_bounds__(kSmallRows * TL) TMX_SMALL_WPE_ATTR mc_codes_s
   // 3. codes into the image (the staging area is free once every lane holds its values): pack class pairs, swap
   //    halves with the partner row's lane, one dword per (class, row pair)
   uint32_t word[kPairs];
-  const int tl = static_cast<int>(t) - cb;  // the positive's slot in this lane (any value when t is not here)
-  const uint32_t tflag = 0x4000u << (16 * (tl & 1));
-  if (keep && use_mode != 0) {  // softmax codes: quotients in [0, 1] are their own codes
+  // softmax codes (quotients in [0, 1] are their own codes, never skipped): the positive's bit 14 is set after the
+  // image is written, by one LDS OR per row (below) instead of a compare + select per slot pair
+  // (one lane per row -- TL == 1 -- keeps the per-pair select: 64 LDS ORs per wave cost more than its few pairs)
+  const bool or_positive = TL > 1 && keep && use_mode != 0;
+  if (keep && use_mode != 0) {
     const f32x2 s2 = {s, s}, i2 = {inv, inv};
+    const int tl = static_cast<int>(t) - cb;  // the positive's slot in this lane (any value when t is not here)
+    const uint32_t tflag = TL > 1 ? 0u : 0x4000u << (16 * (tl & 1));
 #pragma unroll
     for (int p = 0; p < kPairs; ++p) {
-      const uint32_t w2 = pack_rne2<T>(div_rn2(P[p], s2, i2));
-      word[p] = w2 | ((tl >> 1) == p && tl >= 0 ? tflag : 0u);
+      word[p] = pack_rne2<T>(div_rn2(P[p], s2, i2));
+      if constexpr (TL == 1) word[p] |= ((tl >> 1) == p && tl >= 0 ? tflag : 0u);
     }
   } else {
 #pragma unroll
@@ -2155,15 +2200,21 @@ __global__ void __launch_bounds__(kSmallRows * TL) TMX_SMALL_WPE_ATTR mc_codes_s
   }
   const bool odd_row = (lr & 1) != 0;
   const int k = lr >> 1;
-  __syncthreads();
+  if constexpr (!DIRECT) __syncthreads();  // every lane has read its scores from the staging area (the image's space)
+  // this lane's image dwords: class cb + 2p + odd at dword (cb + 2p + odd) * 32 + ((k + q * kRot) & 31) -- one base
+  // address, the pairs at immediate offsets of 64 dwords
+  uint32_t* img = s_img + (cb + (odd_row ? 1 : 0)) * 32 + ((k + q * kRot) & 31);
 #pragma unroll
   for (int p = 0; p < kPairs; ++p) {
     const uint32_t other = swz_xor<TL>(word[p]);  // the partner row's (even, odd) class pair
     // even row lane: class cb + 2p of rows (2k, 2k+1); odd row lane: class cb + 2p + 1 of rows (2k, 2k+1)
     const uint32_t packed = odd_row ? ((other >> 16) | (word[p] & 0xFFFF0000u)) : ((word[p] & 0xFFFFu) | (other << 16));
-    const int c = cb + 2 * p + (odd_row ? 1 : 0);
-    if (2 * p + (odd_row ? 1 : 0) < kVpt && c < C) s_img[c * 32 + ((k + (c >> 4) * kRot) & 31)] = packed;
+    if (2 * p + (odd_row ? 1 : 0) < kVpt && cb + 2 * p + (odd_row ? 1 : 0) < C) img[64 * p] = packed;
   }
+  // the positive of a softmax row: bit 14 of its half of dword (t, k), after that dword's write (same wave: LDS
+  // operations of one wave complete in order)
+  if (q == 0 && or_positive && t >= 0 && t < C)
+    atomicOr(&s_img[static_cast<int>(t) * 32 + ((k + static_cast<int>(t >> 4) * kRot) & 31)], 0x4000u << (16 * (lr & 1)));
   if (q == 0 && in_rows) {
     if constexpr (!FIXUP) {
       if (confmat != nullptr && keep && t >= 0 && t < C && am < C) {
@@ -2178,7 +2229,7 @@ __global__ void __launch_bounds__(kSmallRows * TL) TMX_SMALL_WPE_ATTR mc_codes_s
     }
   }
   if (!FIXUP && record_mode && q == 0) bad = bad || slow || (valid && (mx > 1.f || mn < 0.f));
-  __syncthreads();
+  lds_barrier();
   // class segments: C rows of 64 codes = 8 x 16 B each (4 rotated dwords = two 8-B LDS reads: rot(c) is even)
   for (int i = threadIdx.x; i < C * 8; i += kSmallRows * TL) {
     const int c = i >> 3, m = i & 7;
