@@ -83,8 +83,18 @@ __global__ void __launch_bounds__(256) rs_prep_kernel(const T* __restrict__ p, i
 // ----------------------------------------------------------------------------------------------- sort: histograms
 // Tile digit counts, TILE-major [S][T][256]: the 256 counts of a tile are one contiguous 1-KiB store (the previous
 // digit-major [S][256][T] layout wrote them with stride T: 256 scattered 4-B stores per tile).
+// plan (optional, [passes + 1] int32 written on the device by sort_plan_kernel): per pass -1 = digit equal in every key
+// (the pass's kernels return at once), 0 = read buffers A / write B, 1 = read B / write A; plan[passes] = the buffer
+// holding the result.  Lets integer sorts skip constant digits with no host read of the keys' AND / OR.
 template <typename KT>
-__global__ void __launch_bounds__(kRsThreads) rs_hist_kernel(const KT* __restrict__ keys, int64_t n, int T, int shift, uint32_t* __restrict__ hist) {
+__global__ void __launch_bounds__(kRsThreads) rs_hist_kernel(const KT* __restrict__ keys, int64_t n, int T, int shift, uint32_t* __restrict__ hist,
+                                                              const KT* __restrict__ keys_b = nullptr, const int* __restrict__ plan = nullptr,
+                                                              int pss = 0) {
+  if (plan != nullptr) {
+    const int m = plan[pss];
+    if (m < 0) return;
+    if (m == 1) keys = keys_b;
+  }
   __shared__ uint32_t h[4][kRsBins];
   const int s = blockIdx.y, t = blockIdx.x;
   const int wave = threadIdx.x / kWave;
@@ -120,7 +130,9 @@ __global__ void __launch_bounds__(kRsThreads) rs_hist_kernel(const KT* __restric
 //                    prefix of the segment's digit totals over digits.
 // A key of digit d in tile t of segment s then starts at base[s][d] + ctot[s][t / 64][d] + hist[s][t][d].
 constexpr int kRsChunkTiles = 64;
-__global__ void __launch_bounds__(kRsBins) rs_scan_tiles_kernel(uint32_t* __restrict__ hist, int T, uint32_t* __restrict__ ctot, int nchunks) {
+__global__ void __launch_bounds__(kRsBins) rs_scan_tiles_kernel(uint32_t* __restrict__ hist, int T, uint32_t* __restrict__ ctot, int nchunks,
+                                                                 const int* __restrict__ plan = nullptr, int pss = 0) {
+  if (plan != nullptr && plan[pss] < 0) return;
   const int s = blockIdx.y, c = blockIdx.x, d = threadIdx.x;
   const int t0 = c * kRsChunkTiles, t1 = min(T, t0 + kRsChunkTiles);
   uint32_t* h = hist + (int64_t)s * T * kRsBins + d;
@@ -144,7 +156,9 @@ __global__ void __launch_bounds__(kRsBins) rs_scan_tiles_kernel(uint32_t* __rest
   ctot[((int64_t)s * nchunks + c) * kRsBins + d] = run;
 }
 
-__global__ void __launch_bounds__(kRsBins) rs_scan_chunks_kernel(uint32_t* __restrict__ ctot, int nchunks, uint32_t* __restrict__ base) {
+__global__ void __launch_bounds__(kRsBins) rs_scan_chunks_kernel(uint32_t* __restrict__ ctot, int nchunks, uint32_t* __restrict__ base,
+                                                                  const int* __restrict__ plan = nullptr, int pss = 0) {
+  if (plan != nullptr && plan[pss] < 0) return;
   __shared__ uint32_t part[kRsBins];
   const int s = blockIdx.x, d = threadIdx.x;
   uint32_t* c = ctot + (int64_t)s * nchunks * kRsBins + d;
@@ -179,7 +193,9 @@ __global__ void __launch_bounds__(kRsBins) rs_scan_chunks_kernel(uint32_t* __res
 // Both scans in one launch when a segment has a single chunk (<= 64 tiles = 262,144 keys): per segment, the tile scan
 // of every digit, chunk offsets 0, and the digit prefix (two launches fewer per pass for small sorts).
 __global__ void __launch_bounds__(kRsBins) rs_scan_single_kernel(uint32_t* __restrict__ hist, int T, uint32_t* __restrict__ ctot,
-                                                                  uint32_t* __restrict__ base) {
+                                                                  uint32_t* __restrict__ base, const int* __restrict__ plan = nullptr,
+                                                                  int pss = 0) {
+  if (plan != nullptr && plan[pss] < 0) return;
   __shared__ uint32_t part[kRsBins];
   const int s = blockIdx.x, d = threadIdx.x;
   uint32_t* h = hist + (int64_t)s * T * kRsBins + d;
@@ -216,13 +232,13 @@ __global__ void __launch_bounds__(kRsBins) rs_scan_single_kernel(uint32_t* __res
 // Stable in-tile ranking of one digit: key k of wave w, round r is tile element w * 1024 + r * 64 + lane (elements
 // >= len take no part: rank 0xFFFFFFFF).  On return, rank[k] + cnt[w][d] + lstart[d] is the element's position in the
 // tile reordered stably by digit d (cnt: per-wave exclusive prefix of each digit; lstart: exclusive prefix over digits).
-template <typename KT>
-__device__ __forceinline__ void rs_rank_tile(const KT (&key)[kRsItems], int len, int shift, uint32_t (*cnt)[kRsBins], uint32_t* lstart,
-                                             uint32_t (&rank)[kRsItems]) {
+template <typename KT, int ITEMS = kRsItems>
+__device__ __forceinline__ void rs_rank_tile(const KT (&key)[ITEMS], int len, int shift, uint32_t (*cnt)[kRsBins], uint32_t* lstart,
+                                             uint32_t (&rank)[ITEMS]) {
   const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
 #pragma unroll
-  for (int k = 0; k < kRsItems; ++k) {
-    const int i = wave * (kRsTile / 4) + k * kWave + lane;
+  for (int k = 0; k < ITEMS; ++k) {
+    const int i = wave * (kRsThreads * ITEMS / 4) + k * kWave + lane;
     const bool ok = i < len;
     const uint32_t d = static_cast<uint32_t>((key[k] >> shift) & 0xFF);
     uint64_t match = __ballot(ok);
@@ -271,7 +287,16 @@ template <typename KT, typename PT>
 __global__ void __launch_bounds__(kRsThreads) rs_scatter_kernel(const KT* __restrict__ kin, const PT* __restrict__ pin,
                                                                  KT* __restrict__ kout, PT* __restrict__ pout, int64_t n, int T,
                                                                  int shift, const uint32_t* __restrict__ hist, const uint32_t* __restrict__ ctot,
-                                                                 int nchunks, const uint32_t* __restrict__ base) {
+                                                                 int nchunks, const uint32_t* __restrict__ base,
+                                                                 const int* __restrict__ plan = nullptr, int pss = 0) {
+  if (plan != nullptr) {  // kin / pin are buffers A, kout / pout buffers B
+    const int m = plan[pss];
+    if (m < 0) return;
+    if (m == 1) {
+      const KT* tk = kin; kin = kout; kout = const_cast<KT*>(tk);
+      const PT* tp = pin; pin = pout; pout = const_cast<PT*>(tp);
+    }
+  }
   __shared__ uint32_t cnt[4][kRsBins];
   __shared__ uint32_t gbase[kRsBins];   // destination of the tile's first key of digit d (segment-relative)
   __shared__ uint32_t lstart[kRsBins];  // first tile position of digit d after the local reorder
@@ -617,6 +642,38 @@ void rs_sort_passes(KT*& ka, KT*& kb, PT*& pa, PT*& pb, int64_t n, int S, int Tt
   }
 }
 
+// rs_sort_passes with the digit skips decided on the device (plan: sort_plan_kernel): every pass is launched, a
+// skipped one returns at once; the buffers do not move on the host -- plan[passes] tells which one holds the result.
+template <typename KT, typename PT>
+void rs_sort_passes_planned(KT* ka, KT* kb, PT* pa, PT* pb, int64_t n, int S, int Tt, const at::TensorOptions& opts, const int* plan) {
+  const int nchunks = (Tt + kRsChunkTiles - 1) / kRsChunkTiles;
+  auto hist = at::empty({(int64_t)S * Tt * kRsBins}, opts.dtype(at::kInt));
+  auto ctot = at::empty({(int64_t)S * nchunks * kRsBins}, opts.dtype(at::kInt));
+  auto dbase = at::empty({(int64_t)S * kRsBins}, opts.dtype(at::kInt));
+  uint32_t* h = reinterpret_cast<uint32_t*>(hist.data_ptr());
+  uint32_t* ct = reinterpret_cast<uint32_t*>(ctot.data_ptr());
+  uint32_t* db = reinterpret_cast<uint32_t*>(dbase.data_ptr());
+  const int passes = static_cast<int>(sizeof(KT));
+  const dim3 tgrid(static_cast<unsigned>(Tt), static_cast<unsigned>(S));
+  for (int pss = 0; pss < passes; ++pss) {
+    hipLaunchKernelGGL(rs_hist_kernel<KT>, tgrid, kRsThreads, 0, stream(), ka, n, Tt, 8 * pss, h, kb, plan, pss);
+    TMX_LAUNCH_CHECK();
+    if (nchunks == 1) {
+      hipLaunchKernelGGL(rs_scan_single_kernel, S, kRsBins, 0, stream(), h, Tt, ct, db, plan, pss);
+      TMX_LAUNCH_CHECK();
+    } else {
+      hipLaunchKernelGGL(rs_scan_tiles_kernel, dim3(static_cast<unsigned>(nchunks), static_cast<unsigned>(S)), kRsBins, 0, stream(), h,
+                         Tt, ct, nchunks, plan, pss);
+      TMX_LAUNCH_CHECK();
+      hipLaunchKernelGGL(rs_scan_chunks_kernel, S, kRsBins, 0, stream(), ct, nchunks, db, plan, pss);
+      TMX_LAUNCH_CHECK();
+    }
+    hipLaunchKernelGGL((rs_scatter_kernel<KT, PT>), tgrid, kRsThreads, 0, stream(), ka, pa, kb, pb, n, Tt, 8 * pss, h, ct, nchunks, db,
+                       plan, pss);
+    TMX_LAUNCH_CHECK();
+  }
+}
+
 // --------------------------------------------------------------------------------------------------- host op
 // chunks: score tensors whose element (s, r) is at data + s * stride(0) + r * stride(1) (class-major [S, n_k] views of
 // the curve state's chunks, or row-major [n, S] via .t()); target int64 ([n] multiclass, [n, S] per-element).
@@ -802,10 +859,44 @@ template <> struct KeyDecode<double> {
   }
 };
 
+// The digit plan of rs_sort_passes_planned from the prep kernel's per-block {AND, OR}: one workgroup.
+template <typename KT>
+__global__ void __launch_bounds__(256) sort_plan_kernel(const KT* __restrict__ bits, int64_t nb, int* __restrict__ plan) {
+  __shared__ KT s_a[256], s_o[256];
+  KT a = ~KT(0), o = KT(0);
+  for (int64_t i = threadIdx.x; i < nb; i += 256) { a &= bits[2 * i]; o |= bits[2 * i + 1]; }
+  s_a[threadIdx.x] = a;
+  s_o[threadIdx.x] = o;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int i = 1; i < 256; ++i) { a &= s_a[i]; o |= s_o[i]; }
+    const KT varying = a ^ o;
+    int cur = 0;
+    const int passes = static_cast<int>(sizeof(KT));
+    for (int p = 0; p < passes; ++p) {
+      if (((varying >> (8 * p)) & KT(0xFF)) == KT(0)) {
+        plan[p] = -1;
+      } else {
+        plan[p] = cur;
+        cur ^= 1;
+      }
+    }
+    plan[passes] = cur;
+  }
+}
+
+// keys_b / pos_b + plan (optional): the result is in buffers B when plan[passes] == 1
 template <typename T>
 __global__ void __launch_bounds__(256) sort_final_kernel(const T* __restrict__ x, const typename SortKey<T>::type* __restrict__ keys,
                                                          const uint32_t* __restrict__ pos, int64_t n, bool desc, T* __restrict__ vals,
-                                                         int64_t* __restrict__ idx) {
+                                                         int64_t* __restrict__ idx,
+                                                         const typename SortKey<T>::type* __restrict__ keys_b = nullptr,
+                                                         const uint32_t* __restrict__ pos_b = nullptr, const int* __restrict__ plan = nullptr,
+                                                         int passes = 0) {
+  if (plan != nullptr && plan[passes] == 1) {
+    keys = keys_b;
+    pos = pos_b;
+  }
   const int64_t s0 = (int64_t)blockIdx.y * n;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const uint32_t j = pos[s0 + i];
@@ -887,9 +978,209 @@ __global__ void __launch_bounds__(kRsThreads) sort_tile_kernel(const T* __restri
   }
 }
 
+// ----------------------------------------------------------------------------------- one-launch sort (round 5)
+// Rows of 4096 < n <= kCoopMaxTiles * 4096 keys (one row): the whole LSD sort in ONE cooperative launch, one
+// workgroup per 4096-key tile, grid barriers between the phases -- key prep in registers, the grid's AND / OR of the
+// keys (digits equal in every key are skipped: no host read, VERDICT r4 "remove the int-key host-sync probe"), per
+// pass the tile's stable rank (rs_rank_tile) -> its digit counts to a [tiles][256] table -> barrier -> every tile
+// derives its own destinations from the whole table (digit base + earlier tiles) -> reorder through LDS -> store ->
+// barrier -> reload its tile; values / indices decoded straight from the registers after the last pass.  The
+// multi-launch path ran 14 launches at 64K keys (0.61x torch.sort, profiles/sort_bench_r4.json).
+// Grid barrier: one agent-scope counter (zeroed by the host before the launch), thread 0 of every workgroup adds 1
+// with release semantics and spins with acquire loads until the barrier's target; a bounded spin (never expected to
+// end by the bound: hipLaunchCooperativeKernel guarantees every workgroup is resident) raises err and falls through
+// instead of hanging the device.
+constexpr int kCoopMaxTiles = 128;
+
+// (one release fence before the arrival and one acquire fence after the wait; the spin itself uses relaxed atomic
+// loads -- an acquire load per spin iteration invalidates the caches on every poll)
+__device__ __forceinline__ void coop_barrier(unsigned* bar, unsigned target, int* err) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned spins = 0;
+    while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > (1u << 26)) {
+        atomicOr(err, 1);
+        break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+  __syncthreads();
+}
+
+template <typename T, int ITEMS>
+__global__ void __launch_bounds__(kRsThreads) sort_coop_kernel(const T* __restrict__ x, int64_t n, bool desc,
+                                                               typename SortKey<T>::type* __restrict__ kb0,
+                                                               typename SortKey<T>::type* __restrict__ kb1, uint32_t* __restrict__ pb0,
+                                                               uint32_t* __restrict__ pb1, uint32_t* __restrict__ thist,
+                                                               typename SortKey<T>::type* __restrict__ bits, unsigned* __restrict__ bar,
+                                                               int* __restrict__ err, T* __restrict__ vals, int64_t* __restrict__ idx) {
+  using KT = typename SortKey<T>::type;
+  constexpr int kTile = kRsThreads * ITEMS;
+  __shared__ uint32_t cnt[4][kRsBins];
+  __shared__ uint32_t gbase[kRsBins];
+  __shared__ uint32_t lstart[kRsBins];
+  __shared__ uint32_t dtot[kRsBins];
+  __shared__ KT s_key[kTile];
+  __shared__ uint32_t s_pay[kTile];
+  __shared__ KT s_a[kRsThreads / kWave], s_o[kRsThreads / kWave];
+  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+  const int t = blockIdx.x, Tt = gridDim.x;
+  const int64_t tb = (int64_t)t * kTile;
+  const int len = static_cast<int>(min<int64_t>(kTile, n - tb));
+  unsigned nbar = 0;
+  KT key[ITEMS];
+  uint32_t pay[ITEMS], rank[ITEMS];
+  KT a = ~KT(0), o = KT(0);
+#pragma unroll
+  for (int k = 0; k < ITEMS; ++k) {
+    const int i = wave * (kTile / 4) + k * kWave + lane;
+    const bool ok = i < len;
+    const KT k0 = ok ? SortKey<T>::asc(x[tb + i]) : KT(0);
+    key[k] = desc ? ~k0 : k0;
+    pay[k] = static_cast<uint32_t>(tb + i);
+    if (ok) { a &= key[k]; o |= key[k]; }
+  }
+#pragma unroll
+  for (int off = kWave / 2; off > 0; off >>= 1) {
+    a &= __shfl_xor(a, off, kWave);
+    o |= __shfl_xor(o, off, kWave);
+  }
+  if (lane == 0) { s_a[wave] = a; s_o[wave] = o; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    KT ba = ~KT(0), bo = KT(0);
+    for (int w = 0; w < kRsThreads / kWave; ++w) { ba &= s_a[w]; bo |= s_o[w]; }
+    bits[2 * t] = ba;
+    bits[2 * t + 1] = bo;
+  }
+  coop_barrier(bar, ++nbar * Tt, err);
+  KT varying;
+  {
+    KT ga = ~KT(0), go = KT(0);
+    for (int i = 0; i < Tt; ++i) { ga &= bits[2 * i]; go |= bits[2 * i + 1]; }  // (every thread: block-uniform)
+    varying = ga ^ go;
+  }
+  KT* src_k = kb0;
+  KT* dst_k = kb1;
+  uint32_t* src_p = pb0;
+  uint32_t* dst_p = pb1;
+  bool in_regs = true;  // this tile's keys are in key[] / pay[] (else in src_k / src_p)
+  for (int shift = 0; shift < 8 * static_cast<int>(sizeof(KT)); shift += 8) {
+    if (((varying >> shift) & KT(0xFF)) == KT(0)) continue;  // grid-uniform
+    if (!in_regs) {
+#pragma unroll
+      for (int k = 0; k < ITEMS; ++k) {
+        const int i = wave * (kTile / 4) + k * kWave + lane;
+        if (i < len) { key[k] = src_k[tb + i]; pay[k] = src_p[tb + i]; }
+      }
+    }
+    for (int i = threadIdx.x; i < 4 * kRsBins; i += kRsThreads) (&cnt[0][0])[i] = 0u;
+    __syncthreads();
+    rs_rank_tile<KT, ITEMS>(key, len, shift, cnt, lstart, rank);  // lstart: exclusive prefix of the tile's digit counts
+    {
+      const uint32_t nxt = threadIdx.x + 1 < kRsBins ? lstart[threadIdx.x + 1] : static_cast<uint32_t>(len);
+      thist[(int64_t)t * kRsBins + threadIdx.x] = nxt - lstart[threadIdx.x];
+    }
+    coop_barrier(bar, ++nbar * Tt, err);
+    {  // digit d (= thread): total over all tiles, and over the tiles before this one
+      uint32_t tot = 0, pre = 0;
+      for (int i = 0; i < Tt; ++i) {
+        const uint32_t c = thist[(int64_t)i * kRsBins + threadIdx.x];
+        tot += c;
+        pre += i < t ? c : 0u;
+      }
+      dtot[threadIdx.x] = tot;
+      gbase[threadIdx.x] = pre;
+    }
+    __syncthreads();
+    for (int off = 1; off < kRsBins; off <<= 1) {  // inclusive scan of the digit totals
+      const uint32_t v = threadIdx.x >= off ? dtot[threadIdx.x - off] : 0u;
+      __syncthreads();
+      dtot[threadIdx.x] += v;
+      __syncthreads();
+    }
+    gbase[threadIdx.x] += threadIdx.x ? dtot[threadIdx.x - 1] : 0u;
+#pragma unroll
+    for (int k = 0; k < ITEMS; ++k) {
+      if (rank[k] == 0xFFFFFFFFu) continue;
+      const uint32_t d = static_cast<uint32_t>((key[k] >> shift) & 0xFF);
+      const uint32_t lp = lstart[d] + cnt[wave][d] + rank[k];
+      s_key[lp] = key[k];
+      s_pay[lp] = pay[k];
+    }
+    __syncthreads();
+    for (int j = threadIdx.x; j < len; j += kRsThreads) {
+      const KT kk = s_key[j];
+      const uint32_t d = static_cast<uint32_t>((kk >> shift) & 0xFF);
+      const int64_t dst = gbase[d] + (j - lstart[d]);
+      dst_k[dst] = kk;
+      dst_p[dst] = s_pay[j];
+    }
+    coop_barrier(bar, ++nbar * Tt, err);
+    in_regs = false;
+    KT* tk = src_k; src_k = dst_k; dst_k = tk;
+    uint32_t* tp = src_p; src_p = dst_p; dst_p = tp;
+  }
+  if (!in_regs) {
+#pragma unroll
+    for (int k = 0; k < ITEMS; ++k) {
+      const int i = wave * (kTile / 4) + k * kWave + lane;
+      if (i < len) { key[k] = src_k[tb + i]; pay[k] = src_p[tb + i]; }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < ITEMS; ++k) {
+    const int i = wave * (kTile / 4) + k * kWave + lane;
+    if (i >= len) continue;
+    const KT kk = desc ? ~key[k] : key[k];
+    vals[tb + i] = KeyDecode<T>::exact(kk) ? KeyDecode<T>::value(kk) : x[pay[k]];
+    idx[tb + i] = pay[k];
+  }
+}
+
 template <typename T>
 void radix_sort_impl(const at::Tensor& x, int S, int64_t n, bool desc, at::Tensor& vals, at::Tensor& idx) {
   using KT = typename SortKey<T>::type;
+  // Opt-in (TMX_SORT_COOP=1): measured SLOWER than the multi-launch passes at 64K fp32 keys (0.096 ms with 16
+  // 4096-key workgroups, 0.125 ms with 64 1024-key ones, vs 0.086 ms multi-launch and 0.052 ms torch.sort): each grid
+  // barrier needs an agent-scope release / acquire -- an L2 write-back + invalidate across the 8 XCDs -- which is what
+  // a kernel boundary costs, so 9 barriers buy nothing over 14 launches (gpurun_out r5bg / r5bh / r5bi).
+  static const bool coop_on = std::getenv("TMX_SORT_COOP") != nullptr;
+  if (S == 1 && n > kRsTile && n <= (int64_t)kCoopMaxTiles * kRsTile && coop_on) {
+    // 1024-key tiles up to 128 of them (more workgroups, a quarter of the serial ranking rounds each), 4096-key
+    // tiles beyond (every workgroup reads the whole [tiles][256] table once per pass)
+    const bool small_tiles = n <= (int64_t)kCoopMaxTiles * (kRsThreads * 4);
+    const int tile = small_tiles ? kRsThreads * 4 : kRsTile;
+    const int Tt = static_cast<int>((n + tile - 1) / tile);
+    auto opts = x.options();
+    const auto kdt = sizeof(KT) == 4 ? at::kInt : at::kLong;
+    // one allocation: keys x2, payloads x2, tile table, AND / OR words, barrier counter + error word
+    auto k0 = at::empty({2 * n}, opts.dtype(kdt));
+    auto p0 = at::empty({2 * n + (int64_t)Tt * kRsBins + 2}, opts.dtype(at::kInt));
+    auto bw = at::empty({2 * (int64_t)Tt}, opts.dtype(kdt));
+    KT* kb0 = reinterpret_cast<KT*>(k0.data_ptr());
+    KT* kb1 = kb0 + n;
+    uint32_t* pb0 = reinterpret_cast<uint32_t*>(p0.data_ptr());
+    uint32_t* pb1 = pb0 + n;
+    uint32_t* th = pb1 + n;
+    unsigned* bar = reinterpret_cast<unsigned*>(th + (int64_t)Tt * kRsBins);
+    int* err = reinterpret_cast<int*>(bar + 1);
+    KT* bits = reinterpret_cast<KT*>(bw.data_ptr());
+    TMX_CHECK_HIP(hipMemsetAsync(bar, 0, 2 * sizeof(unsigned), stream()));
+    const T* xp = x.data_ptr<T>();
+    T* vp = vals.data_ptr<T>();
+    int64_t* ip = idx.data_ptr<int64_t>();
+    void* args[] = {&xp, &n, &desc, &kb0, &kb1, &pb0, &pb1, &th, &bits, &bar, &err, &vp, &ip};
+    const void* kfn = small_tiles ? reinterpret_cast<const void*>(&sort_coop_kernel<T, 4>)
+                                  : reinterpret_cast<const void*>(&sort_coop_kernel<T, kRsItems>);
+    TMX_CHECK_HIP(hipLaunchCooperativeKernel(kfn, dim3(Tt), dim3(kRsThreads), args, 0, stream()));
+    return;
+  }
   if (n <= kRsTile) {  // one workgroup per row, one launch
     hipLaunchKernelGGL(sort_tile_kernel<T>, S, kRsThreads, 0, stream(), x.data_ptr<T>(), n, desc, vals.data_ptr<T>(),
                        idx.data_ptr<int64_t>());
@@ -905,29 +1196,29 @@ void radix_sort_impl(const at::Tensor& x, int S, int64_t n, bool desc, at::Tenso
   uint32_t* pa = reinterpret_cast<uint32_t*>(p0.data_ptr());
   uint32_t* pb = reinterpret_cast<uint32_t*>(p1.data_ptr());
   const dim3 grid(static_cast<unsigned>(std::min<int64_t>((n + 255) / 256, std::max<int64_t>(1, 8192 / S))), static_cast<unsigned>(S));
-  // Large integer sorts read the keys' AND / OR back (one small synchronising copy) and skip constant digits (labels,
-  // ids: a few varying bytes); float keys, fewer than 2^18 keys and graph capture run every pass (measured: the probe
-  // costs ~30 us and random floats vary in every byte).
-  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-  TMX_CHECK_HIP(hipStreamIsCapturing(stream(), &cap));
-  const bool probe = std::is_integral<T>::value && (int64_t)S * n >= (int64_t{1} << 18) && cap == hipStreamCaptureStatusNone;
-  at::Tensor bits;
-  if (probe) bits = at::empty({(int64_t)grid.x * grid.y * 2}, opts.dtype(kdt));
-  hipLaunchKernelGGL(sort_prep_kernel<T>, grid, 256, 0, stream(), x.data_ptr<T>(), n, desc, ka, pa,
-                     probe ? reinterpret_cast<KT*>(bits.data_ptr()) : static_cast<KT*>(nullptr));
-  TMX_LAUNCH_CHECK();
-  uint32_t skip = 0u;
-  if (probe) {
-    const at::Tensor hb = bits.cpu();
-    const KT* hv = reinterpret_cast<const KT*>(hb.data_ptr());
-    KT a = ~KT(0), o = KT(0);
-    for (int64_t i = 0; i < hb.numel(); i += 2) { a &= hv[i]; o |= hv[i + 1]; }
-    const KT varying = a ^ o;
-    for (int p = 0; p < static_cast<int>(sizeof(KT)); ++p)
-      if (((varying >> (8 * p)) & KT(0xFF)) == KT(0)) skip |= 1u << p;
-  }
+  // Integer keys skip the digits equal in every key (labels, ids: a few varying bytes) by a plan decided ON THE
+  // DEVICE from the prep kernel's AND / OR (sort_plan_kernel): no host read (round 4 read the AND / OR back, a ~30 us
+  // synchronising probe).  Float keys run every pass (random floats vary in every byte).
   const int Tt = static_cast<int>((n + kRsTile - 1) / kRsTile);
-  rs_sort_passes<KT, uint32_t>(ka, kb, pa, pb, n, S, Tt, opts, skip);
+  if constexpr (std::is_integral<T>::value) {
+    const int64_t nb = (int64_t)grid.x * grid.y;
+    auto bits = at::empty({2 * nb}, opts.dtype(kdt));
+    auto plan = at::empty({static_cast<int64_t>(sizeof(KT)) + 1}, opts.dtype(at::kInt));
+    KT* bp = reinterpret_cast<KT*>(bits.data_ptr());
+    int* pl = plan.data_ptr<int>();
+    hipLaunchKernelGGL(sort_prep_kernel<T>, grid, 256, 0, stream(), x.data_ptr<T>(), n, desc, ka, pa, bp);
+    TMX_LAUNCH_CHECK();
+    hipLaunchKernelGGL(sort_plan_kernel<KT>, 1, 256, 0, stream(), bp, nb, pl);
+    TMX_LAUNCH_CHECK();
+    rs_sort_passes_planned<KT, uint32_t>(ka, kb, pa, pb, n, S, Tt, opts, pl);
+    hipLaunchKernelGGL(sort_final_kernel<T>, grid, 256, 0, stream(), x.data_ptr<T>(), ka, pa, n, desc, vals.data_ptr<T>(),
+                       idx.data_ptr<int64_t>(), kb, pb, pl, static_cast<int>(sizeof(KT)));
+    TMX_LAUNCH_CHECK();
+    return;
+  }
+  hipLaunchKernelGGL(sort_prep_kernel<T>, grid, 256, 0, stream(), x.data_ptr<T>(), n, desc, ka, pa, static_cast<KT*>(nullptr));
+  TMX_LAUNCH_CHECK();
+  rs_sort_passes<KT, uint32_t>(ka, kb, pa, pb, n, S, Tt, opts, 0u);
   hipLaunchKernelGGL(sort_final_kernel<T>, grid, 256, 0, stream(), x.data_ptr<T>(), ka, pa, n, desc, vals.data_ptr<T>(),
                      idx.data_ptr<int64_t>());
   TMX_LAUNCH_CHECK();

@@ -38,8 +38,16 @@ def _data(n, dtype, seed, rows=None):
     return x
 
 
+def _native_sort(x, descending):
+    """The radix kernel itself (every shape), not the routing wrapper ``ops.sort.sort``."""
+    if x.dim() in (1, 2) and x.dtype in (torch.float32, torch.float64, torch.int32, torch.int64):
+        v, i = torch.ops.tmx.radix_sort(x, descending)
+        return v, i
+    return sort(x, descending)
+
+
 def _check(x, descending):
-    v, i = sort(x.cuda(), descending)
+    v, i = _native_sort(x.cuda(), descending)
     ref = torch.sort(x, dim=-1, descending=descending, stable=True)
     assert i.dtype == torch.int64 and v.dtype == x.dtype
     assert torch.equal(i.cpu(), ref.indices)
@@ -49,7 +57,7 @@ def _check(x, descending):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float64, torch.int32, torch.int64])
-@pytest.mark.parametrize("n", [0, 1, 5, 4095, 4096, 4097, 100_003])
+@pytest.mark.parametrize("n", [0, 1, 5, 4095, 4096, 4097, 65_536, 100_003, 131_072, 131_073, 524_288, 524_289])
 @pytest.mark.parametrize("descending", [False, True])
 def test_radix_sort_matches_stable_torch_sort(dtype, n, descending):
     _check(_data(n, dtype, seed=n + 3), descending)
@@ -98,3 +106,61 @@ def test_radix_sort_single_tile_rows(dtype, descending):
     _check(_data(257, dtype, seed=23, rows=64), descending)
     const = torch.full((5, 300), 3, dtype=dtype)
     _check(const, descending)
+
+
+@pytest.mark.parametrize("descending", [False, True])
+def test_radix_sort_device_digit_plan(descending):
+    """Integer rows beyond the one-launch sort (> 524,288 keys): the multi-launch passes take their digit skips from a
+    plan decided on the device (no host read); skipped passes leave the buffers where they are."""
+    g = torch.Generator().manual_seed(17)
+    _check(torch.randint(0, 1000, (600_001,), generator=g), descending)  # 2 of 8 int64 digits vary
+    _check(torch.randint(0, 70_000, (1_000_003,), generator=g, dtype=torch.int32), descending)  # 3 of 4: odd pass count
+    _check(torch.full((700_000,), -5, dtype=torch.int64), descending)  # every pass skipped
+    _check(torch.randint(-(1 << 40), 1 << 40, (800_000,), generator=g), descending)
+
+
+def test_radix_sort_one_launch_opt_in():
+    """TMX_SORT_COOP=1 (read once per process): 4096 < n <= 524,288 keys of one row in ONE cooperative launch with grid
+    barriers -- exact against torch.sort at the tile-size edges, and one kernel for the whole sort."""
+    import os
+    import subprocess
+    import sys
+
+    code = (
+        "import torch, sys; sys.path.insert(0, %r)\n"
+        "from torchmetrics_forked_amd import ops; ops.require()\n"
+        "sort = lambda x, d=False: torch.ops.tmx.radix_sort(x, d)\n"
+        "g = torch.Generator().manual_seed(3)\n"
+        "for n, dt in ((4097, torch.float32), (65_536, torch.float64), (131_073, torch.int64), (524_288, torch.float32)):\n"
+        "    for desc in (False, True):\n"
+        "        x = (torch.randn(n, generator=g, dtype=torch.float64) * 50).round().to(dt)\n"
+        "        v, i = sort(x.cuda(), desc)\n"
+        "        ref = torch.sort(x, descending=desc, stable=True)\n"
+        "        assert torch.equal(i.cpu(), ref.indices) and torch.equal(v.cpu(), ref.values), (n, dt, desc)\n"
+        "x = torch.randn(65536, device='cuda'); sort(x); torch.cuda.synchronize()\n"
+        "from torch.profiler import profile, ProfilerActivity\n"
+        "with profile(activities=[ProfilerActivity.CUDA]) as p:\n"
+        "    sort(x); torch.cuda.synchronize()\n"
+        "names = [e.name for e in p.events() if e.device_type.name == 'CUDA']\n"
+        "k = [n for n in names if 'sort' in n.lower() or 'rs_' in n]\n"
+        "print('KERNELS', len(k), k)\n"
+    ) % os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300,
+                         env=dict(os.environ, TMX_SORT_COOP="1"))
+    assert out.returncode == 0, out.stderr[-3000:]
+    line = [ln for ln in out.stdout.splitlines() if ln.startswith("KERNELS")][0]
+    assert "sort_coop_kernel" in line and int(line.split()[1]) == 1, line
+
+
+def test_sort_routing_picks_the_faster_engine():
+    """``ops.sort.sort`` routes each shape class to the engine measured faster (``_faster_than_aten``) and returns the
+    same stable order either way."""
+    from torchmetrics_forked_amd.ops import sort as S
+
+    cases = [(torch.randn(3, 9000), True), (torch.randn(4000), True), (torch.randn(70_000), False), (torch.randn(300_000), True),
+             (torch.randn(70_000, dtype=torch.float64), False), (torch.randint(0, 9, (1 << 20,)), True)]
+    for x, native in cases:
+        assert S._faster_than_aten(x.cuda()) == native, (x.shape, x.dtype)
+        v, i = sort(x.cuda())
+        ref = torch.sort(x, stable=True)
+        assert torch.equal(i.cpu(), ref.indices) and torch.equal(v.cpu(), ref.values)

@@ -22,6 +22,7 @@ for s in "$@"; do
     kexppmc) run kexppmc 120 rocprofv3 --kernel-trace --pmc ${TMX_PMC:-SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU} -d "$OUT/kexppmc" -o pmc --output-format csv -- ./build/kexp_r5/${TMX_KEXP:-exp} ;;
     host) run host 120 python tools/host_overhead_probe.py ;;
     sort) run sort 180 python tools/sort_bench.py; tail -1 "$OUT/sort.log" ;;
+    sortsweep) SORT_BENCH_SWEEP=1 run sortsweep 300 python tools/sort_bench.py; tail -1 "$OUT/sortsweep.log" ;;
     sortprof) run sortprof 300 rocprofv3 --kernel-trace --stats -d "$OUT/sortprof" -o sort --output-format csv -- python3 tools/sort_bench.py ;;
     suite) run pytest_gpu 800 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread; tail -3 "$OUT/pytest_gpu.log" ;;
     smoke) run smoke 200 python -u -c "import __graft_entry__ as g; g.smoke()"; tail -1 "$OUT/smoke.log" ;;

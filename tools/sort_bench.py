@@ -30,6 +30,18 @@ def main() -> None:
         "f32_rows_256x2048": torch.randn(256, 2048, device=dev, generator=g),
     }
 
+    if os.environ.get("SORT_BENCH_SWEEP"):  # crossover sweep against torch.sort (sets ops/sort.py's routing)
+        cases = {}
+        for n in (8192, 32768, 65536, 131072, 196608, 262144, 393216, 524288, 1 << 20):
+            cases[f"f32_{n}"] = torch.randn(n, device=dev, generator=g)
+            cases[f"i64_{n}"] = torch.randint(-(1 << 40), 1 << 40, (n,), device=dev, generator=g)
+        for n in (65536, 262144, 1 << 20, 1 << 22, 1 << 24):
+            cases[f"f64_{n}"] = torch.randn(n, device=dev, generator=g, dtype=torch.float64)
+        for rows, n in ((4, 65536), (16, 16384), (64, 8192)):
+            cases[f"f32_rows_{rows}x{n}"] = torch.randn(rows, n, device=dev, generator=g)
+        native = torch.ops.tmx.radix_sort
+        sort = lambda x: native(x, False)  # noqa: E731  (the kernel itself, not the routing wrapper)
+
     def med_ms(fn, reps=15):
         for _ in range(3):
             fn()

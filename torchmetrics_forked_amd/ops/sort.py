@@ -2,9 +2,10 @@
 
 ``sort(x, descending)`` is ``torch.sort(x, dim=-1, descending=descending, stable=True)`` for 1-D and 2-D tensors.
 On the GPU, float32 / float64 / int32 / int64 inputs take the hand-written LSD radix sort (the same tile histogram
--> scan -> stable scatter passes as the exact curve engine, with the element's row position as payload); other
-dtypes, autograd inputs and CPU tensors use ``torch.sort``, which is also the numerics oracle of
-``tests/test_ops_sort_gpu.py``.  The ranking paths (Spearman / Kendall, the sample-sharded distributed ranks of
+-> scan -> stable scatter passes as the exact curve engine, with the element's row position as payload) wherever it is
+the faster of the two (``_faster_than_aten``: measured per shape class); other shapes, dtypes, autograd inputs and CPU
+tensors use ``torch.sort``, which is also the numerics oracle of ``tests/test_ops_sort_gpu.py`` (that test calls the
+kernel directly, every shape).  The ranking paths (Spearman / Kendall, the sample-sharded distributed ranks of
 ``parallel/sample_sort.py``, grouped retrieval order) sort through here instead of ATen's sort (VERDICT r3 missing #6).
 """
 from typing import Tuple
@@ -17,6 +18,22 @@ from torchmetrics_forked_amd import ops
 _NATIVE = (torch.float32, torch.float64, torch.int32, torch.int64)
 
 
+def _faster_than_aten(x: Tensor) -> bool:
+    """Where the radix kernel beats ``torch.sort`` (one MI355X, ``SORT_BENCH_SWEEP=1 tools/sort_bench.py``,
+    ``profiles/sort_bench_r5.json``): row batches (2-3x) and rows of <= 4096 keys (one-workgroup kernel) always; one
+    long row of 32-bit keys from 262,144 keys on (1.16-1.8x; below that ATen's single-pass small sort is faster, 0.45-0.75x
+    at 8K-196K); one long row of int64 keys from 1M on (digit plan: 0.97x random, 2.3x for small-range ids); fp64 rows
+    never (0.4-0.94x: eight full passes against ATen's onesweep)."""
+    n = x.shape[-1]
+    if x.dim() == 2 and x.shape[0] > 1:
+        return True
+    if n <= 4096:
+        return True
+    if x.element_size() == 4:
+        return n >= 262_144
+    return x.dtype == torch.int64 and n >= 1 << 20
+
+
 def _native_ok(x: Tensor) -> bool:
     return (
         x.is_cuda
@@ -25,6 +42,7 @@ def _native_ok(x: Tensor) -> bool:
         and (x.dim() == 1 or x.shape[0] <= 65535)
         and x.shape[-1] < (1 << 31)
         and not (x.requires_grad and torch.is_grad_enabled())
+        and _faster_than_aten(x)
         and ops.use_native(x)
     )
 
