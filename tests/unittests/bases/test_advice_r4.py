@@ -199,3 +199,27 @@ def test_validation_mode_follows_env(monkeypatch):
     assert validation_mode() == "auto"
     monkeypatch.setenv("TMX_VALIDATION", "eager")
     assert validation_mode() == "eager"
+
+
+def test_forward_batch_state_reuse_keeps_returned_values():
+    """forward() reuses the previous batch's zero-defaulted sum states (one foreach_zero_ instead of copying the
+    defaults) unless the batch value aliases them: values returned by earlier forwards never change, and the
+    accumulated state equals plain updates."""
+    import torchmetrics_forked_amd as tm
+
+    g = torch.Generator().manual_seed(4)
+    batches = [(torch.randn(12, 5, generator=g), torch.randint(0, 5, (12,), generator=g)) for _ in range(4)]
+    for cls in (tm.classification.MulticlassAccuracy, tm.classification.MulticlassConfusionMatrix, tm.classification.MulticlassF1Score):
+        m, ref = cls(num_classes=5), cls(num_classes=5)
+        outs, clones = [], []
+        for p, t in batches:
+            v = m(p, t)
+            outs.append(v)
+            clones.append(v.clone())
+            ref.update(p, t)
+        for v, c in zip(outs, clones):
+            assert torch.equal(v, c), cls.__name__
+        for p, (v, _) in zip(batches, zip(outs, clones)):
+            one = cls(num_classes=5)
+            assert torch.equal(one(*p), v)
+        assert torch.equal(m.compute(), ref.compute())

@@ -337,6 +337,8 @@ class Metric(Module, ABC):
         names = tuple(self._defaults) if ok else ()
         d["_sum_fwd"] = names
         d["_sum_fwd_defaults"] = [self._defaults[n] for n in names]
+        d["_sum_fwd_zero"] = all(not bool(self._defaults[n].any()) for n in names)
+        d["_sum_fwd_scratch"] = None
         return names or None
 
     def _forward_full_state_update(self, *args: Any, **kwargs: Any) -> Any:
@@ -369,7 +371,11 @@ class Metric(Module, ABC):
             glob = None
         if glob is not None:
             defaults = d["_sum_fwd_defaults"]
-            if defaults[0].device == glob[0].device:  # states and defaults move together (_apply)
+            scratch = d.get("_sum_fwd_scratch")
+            if scratch is not None and scratch[0].device == glob[0].device:
+                fresh = scratch  # the previous forward's batch states, unaliased: zeroed in one call (zero defaults)
+                torch._foreach_zero_(fresh)
+            elif defaults[0].device == glob[0].device:  # states and defaults move together (_apply)
                 fresh = torch._foreach_add(defaults, 0)  # one call: a fresh copy of every default
             else:
                 fresh = [dv.detach().clone().to(g.device) for dv, g in zip(defaults, glob)]
@@ -387,10 +393,16 @@ class Metric(Module, ABC):
             self.update(*args, **kwargs)
             batch_val = self.compute()
             d["_update_count"] = count + 1
+            batch = [d[n] for n in names]  # (an update may have rebound a state rather than added into it)
             with torch.no_grad():
-                merged = torch._foreach_add(glob, [d[n] for n in names])
-            for n, m in zip(names, merged):
-                d[n] = m
+                # in place, as update() itself accumulates (the fused stat-score / confusion-matrix updates add into
+                # the state tensors): one foreach call, no new global tensors
+                torch._foreach_add_(glob, batch)
+            for n, g in zip(names, glob):
+                d[n] = g
+            # keep the batch states for the next forward when they are zero-defaulted and the batch value does not
+            # alias them (a confusion matrix's compute returns its state)
+            d["_sum_fwd_scratch"] = batch if d["_sum_fwd_zero"] and not _aliases(batch_val, batch) else None
             self._leave_batch_mode(saved)
             return batch_val
         snapshot = self.metric_state
@@ -809,7 +821,7 @@ class Metric(Module, ABC):
 
     def __getstate__(self) -> Dict[str, Any]:
         self._join_side_work()
-        return {k: v for k, v in self.__dict__.items() if k not in ("update", "compute", "_update_signature", "_hist_spare", "_batch_bufs", "_batch_sink", "_batch_view", "_fast_update", "_sum_fwd", "_sum_fwd_defaults", "_tensor_states", "_owned_buf")}
+        return {k: v for k, v in self.__dict__.items() if k not in ("update", "compute", "_update_signature", "_hist_spare", "_batch_bufs", "_batch_sink", "_batch_view", "_fast_update", "_sum_fwd", "_sum_fwd_defaults", "_sum_fwd_scratch", "_tensor_states", "_owned_buf")}
 
     def __setstate__(self, state: Dict[str, Any]) -> None:
         self.__dict__.update(state)
@@ -851,7 +863,7 @@ class Metric(Module, ABC):
 
     def _apply(self, fn: Callable, exclude_state: Sequence[str] = "") -> Module:
         self._join_side_work()
-        for k in ("_sum_fwd", "_sum_fwd_defaults"):  # forward's cached defaults follow the new device / dtype
+        for k in ("_sum_fwd", "_sum_fwd_defaults", "_sum_fwd_scratch"):  # forward's caches follow the new device / dtype
             self.__dict__.pop(k, None)
         this = super()._apply(fn)
         fs = str(fn)
@@ -1117,6 +1129,19 @@ class CompositionalMetric(Metric):
 
     def _wrap_compute(self, compute: Callable) -> Callable:
         return compute
+
+
+def _aliases(value: Any, tensors: List[Tensor]) -> bool:
+    """True if any tensor in ``value`` (a tensor, or a flat dict / tuple / list of them) shares storage with one of
+    ``tensors``."""
+    ptrs = {t.untyped_storage().data_ptr() for t in tensors}
+    items = value.values() if isinstance(value, dict) else (value if isinstance(value, (tuple, list)) else (value,))
+    for v in items:
+        if isinstance(v, Tensor) and v.untyped_storage().data_ptr() in ptrs:
+            return True
+        if not isinstance(v, Tensor) and not isinstance(v, (int, float, bool, type(None))):
+            return True  # nested structure: be conservative
+    return False
 
 
 class _MetricPendingSync:
