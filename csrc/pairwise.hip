@@ -1,4 +1,4 @@
-// Pairwise L1 / Lp distance matrices for gfx950.
+// Pairwise distance / similarity matrices for gfx950: L1 / Lp (VALU) and the GEMM forms (MFMA).
 //
 // out[i, j] = (Σ_k |x[i,k] - y[j,k]|^p)^(1/p)   (p == 1: Manhattan, no root)
 //
@@ -120,8 +120,232 @@ at::Tensor pairwise_lp(const at::Tensor& x_in, const at::Tensor& y_in, double p,
   return out;
 }
 
+// ------------------------------------------------------------------------------ GEMM forms: linear / cosine / euclidean
+// out[i, j] = epilogue(x[i] . y[j]) in one kernel (reference ``functional/pairwise/{linear,cosine,euclidean}.py``):
+//   linear     x . y                                (fp32 accumulation for fp32 / bf16 / fp16, fp64 for fp64)
+//   cosine     x . y * (1/|x|) * (1/|y|)            (the reference normalises the rows first, then runs the GEMM)
+//   euclidean  sqrt(T(|x|^2 + |y|^2 - 2 x . y))     (fp64 throughout, as the reference's upcast; rounded to the input
+//                                                    dtype before the root, diagonal zeroed before the root)
+// The reference runs 4-12 separate ATen kernels and, for euclidean, round-trips the N x M matrix through HBM in fp64
+// five times.  Here one 64 x 64 output tile per 256-thread workgroup: 64-row slices of x and y (32 deep for fp32
+// accumulation, 16 for fp64) are converted to the accumulation type on the way into LDS (k-major rows padded to 80
+// elements: the four 16-lane groups of a fragment read land in disjoint bank ranges), double-buffered with the next
+// slice in registers during the MFMAs; each wave owns a 32 x 32 block (2 x 2 MFMA tiles: v_mfma_f32_16x16x4_f32,
+// exact fp32 products, or v_mfma_f64_16x16x4_f64).  Row norms are summed from the staging registers (no extra pass),
+// the epilogue runs on the accumulators and writes the input dtype once.  Tile ids are remapped so that consecutive
+// ids (same x rows) share an XCD and its L2.
+enum PgMode : int { kPgLinear = 0, kPgCosine = 1, kPgEuclid = 2 };
+constexpr int kPgT = 64, kPgPad = 16, kPgThreads = 256;
+// slice depth: 32 (fp32) / 16 (fp64) -- 40 KiB of double-buffered LDS either way, three workgroups per CU
+template <typename Acc> constexpr int pg_k() { return std::is_same<Acc, double>::value ? 16 : 32; }
+
+template <typename Acc> struct PgMma;
+template <> struct PgMma<float> {
+  typedef float V __attribute__((ext_vector_type(4)));
+  static __device__ __forceinline__ V mma(float a, float b, V c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
+  static __device__ __forceinline__ int row(int lane, int r) { return (lane >> 4) * 4 + r; }
+};
+template <> struct PgMma<double> {
+  typedef double V __attribute__((ext_vector_type(4)));
+  static __device__ __forceinline__ V mma(double a, double b, V c) { return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0); }
+  static __device__ __forceinline__ int row(int lane, int r) { return (lane >> 4) + 4 * r; }  // f64 C/D map
+};
+
+template <typename T, typename Acc> __device__ __forceinline__ Acc pg_in(T v) {
+  if constexpr (std::is_same<T, double>::value) return static_cast<Acc>(v);
+  else return static_cast<Acc>(to_f32<T>(v));
+}
+// Acc -> output dtype the way ATen's ``.to`` does (double -> float -> 16-bit: c10 rounds through float)
+template <typename T, typename Acc> __device__ __forceinline__ T pg_out(Acc v) {
+  if constexpr (std::is_same<T, double>::value) return static_cast<double>(v);
+  else if constexpr (std::is_same<T, float>::value) return static_cast<float>(v);
+  else if constexpr (std::is_same<T, __hip_bfloat16>::value) return __float2bfloat16(static_cast<float>(v));
+  else return __float2half(static_cast<float>(v));
+}
+template <typename T> __device__ __forceinline__ T pg_sqrt(T v) {
+  if constexpr (std::is_same<T, double>::value) return sqrt(v);
+  else if constexpr (std::is_same<T, float>::value) return sqrtf(v);
+  else return pg_out<T, float>(sqrtf(to_f32<T>(v)));
+}
+
+// KPT consecutive elements of one row into Acc registers: whole-vector loads when VEC (D % KPT == 0, rows aligned
+// to the vector: host check)
+template <typename T, typename Acc, int KPT, bool VEC>
+__device__ __forceinline__ void pg_load(const T* __restrict__ p, int64_t row, int64_t nrows, int64_t k, int64_t D, Acc (&v)[KPT]) {
+  if constexpr (VEC) {
+    constexpr int kBytes = KPT * static_cast<int>(sizeof(T));
+    constexpr int kVec = kBytes < 16 ? kBytes : 16;
+    using W = typename std::conditional<kVec == 16, uint4, uint2>::type;
+    constexpr int kPer = kVec / static_cast<int>(sizeof(T));
+    if (row < nrows && k < D) {
+      const W* q = reinterpret_cast<const W*>(p + row * D + k);
+#pragma unroll
+      for (int c = 0; c < KPT / kPer; ++c) {
+        const W w = q[c];
+        const T* e = reinterpret_cast<const T*>(&w);
+#pragma unroll
+        for (int i = 0; i < kPer; ++i) v[c * kPer + i] = pg_in<T, Acc>(e[i]);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < KPT; ++i) v[i] = Acc(0);
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < KPT; ++i) v[i] = (row < nrows && k + i < D) ? pg_in<T, Acc>(p[row * D + k + i]) : Acc(0);
+  }
+}
+
+template <typename T, typename Acc, int MODE, bool VEC>
+__global__ __launch_bounds__(kPgThreads) void pairwise_gemm_kernel(const T* __restrict__ x, const T* __restrict__ y, int64_t N, int64_t M,
+                                                                   int64_t D, int tiles_n, bool zero_diag, T* __restrict__ out) {
+  using Mma = PgMma<Acc>;
+  constexpr int kPgK = pg_k<Acc>(), KPT = kPgK / 4;
+  __shared__ Acc xs[2][kPgK][kPgT + kPgPad];
+  __shared__ Acc ys[2][kPgK][kPgT + kPgPad];
+  __shared__ Acc nrm[2][kPgT];
+  const int64_t nwg = gridDim.x, orig = blockIdx.x, xcd = orig % 8, q = nwg / 8, rr = nwg % 8;
+  const int64_t id = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
+  const int64_t row0 = (id / tiles_n) * kPgT, col0 = (id % tiles_n) * kPgT;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 1, wc = wave & 1;
+  const int sr = tid >> 2, sk = (tid & 3) * KPT;  // staging: row sr, k [sk, sk + KPT) of the slice
+  Acc rx[KPT], ry[KPT];
+  Acc px = Acc(0), py = Acc(0);
+  auto load = [&](int64_t k0) {
+    pg_load<T, Acc, KPT, VEC>(x, row0 + sr, N, k0 + sk, D, rx);
+    pg_load<T, Acc, KPT, VEC>(y, col0 + sr, M, k0 + sk, D, ry);
+    if constexpr (MODE != kPgLinear) {
+#pragma unroll
+      for (int i = 0; i < KPT; ++i) {
+        px = fma(rx[i], rx[i], px);
+        py = fma(ry[i], ry[i], py);
+      }
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < KPT; ++i) {
+      xs[buf][sk + i][sr] = rx[i];
+      ys[buf][sk + i][sr] = ry[i];
+    }
+  };
+  typename Mma::V acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = typename Mma::V{0, 0, 0, 0};
+  const int nk = static_cast<int>((D + kPgK - 1) / kPgK);
+  load(0);
+  store(0);
+  __syncthreads();
+  const int fr = lane & 15, fk = lane >> 4;
+  for (int s = 0; s < nk; ++s) {
+    const int buf = s & 1;
+    if (s + 1 < nk) load(static_cast<int64_t>(s + 1) * kPgK);
+#pragma unroll
+    for (int kk = 0; kk < kPgK; kk += 4) {
+      Acc a[2], b[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        a[i] = xs[buf][kk + fk][wr * 32 + 16 * i + fr];
+        b[i] = ys[buf][kk + fk][wc * 32 + 16 * i + fr];
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = Mma::mma(a[i], b[j], acc[i][j]);
+    }
+    if (s + 1 < nk) store(buf ^ 1);  // that buffer was last read before the previous barrier
+    __syncthreads();
+  }
+  if constexpr (MODE != kPgLinear) {
+    // four consecutive lanes share a staging row
+    px += __shfl_xor(px, 1, kWave);
+    px += __shfl_xor(px, 2, kWave);
+    py += __shfl_xor(py, 1, kWave);
+    py += __shfl_xor(py, 2, kWave);
+    if ((tid & 3) == 0) {  // cosine keeps reciprocal norms: the epilogue is two multiplies per output
+      nrm[0][sr] = MODE == kPgCosine ? Acc(1) / sqrt(px) : px;
+      nrm[1][sr] = MODE == kPgCosine ? Acc(1) / sqrt(py) : py;
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int lr = wr * 32 + 16 * i + Mma::row(lane, r), lc = wc * 32 + 16 * j + fr;
+        const int64_t gi = row0 + lr, gj = col0 + lc;
+        if (gi >= N || gj >= M) continue;
+        const Acc v = acc[i][j][r];
+        T res;
+        if constexpr (MODE == kPgLinear) {
+          res = pg_out<T, Acc>(v);
+          if (zero_diag && gi == gj) res = pg_out<T, Acc>(Acc(0));
+        } else if constexpr (MODE == kPgCosine) {
+          res = pg_out<T, Acc>(v * nrm[0][lr] * nrm[1][lc]);
+          if (zero_diag && gi == gj) res = pg_out<T, Acc>(Acc(0));
+        } else {
+          T d = pg_out<T, Acc>((nrm[0][lr] + nrm[1][lc]) - Acc(2) * v);
+          if (zero_diag && gi == gj) d = pg_out<T, Acc>(Acc(0));
+          res = pg_sqrt<T>(d);
+        }
+        out[gi * M + gj] = res;
+      }
+}
+
+template <typename T, typename Acc, int MODE>
+void launch_pairwise_gemm(const at::Tensor& x, const at::Tensor& y, at::Tensor& out, bool zero_diag) {
+  const int64_t N = x.size(0), M = y.size(0), D = x.size(1);
+  const int64_t tiles_m = (N + kPgT - 1) / kPgT, tiles_n = (M + kPgT - 1) / kPgT;
+  const int64_t nwg = tiles_m * tiles_n;
+  TORCH_CHECK(nwg < (int64_t(1) << 31) && tiles_n < (int64_t(1) << 31), "pairwise_gemm: output too large");
+  const auto* xp = reinterpret_cast<const T*>(x.data_ptr());
+  const auto* yp = reinterpret_cast<const T*>(y.data_ptr());
+  auto* op = reinterpret_cast<T*>(out.data_ptr());
+  constexpr int kpt = pg_k<Acc>() / 4, align = kpt * sizeof(T) < 16 ? kpt * sizeof(T) : 16;
+  const bool vec = D % kpt == 0 && reinterpret_cast<uintptr_t>(xp) % align == 0 && reinterpret_cast<uintptr_t>(yp) % align == 0;
+  if (vec)
+    hipLaunchKernelGGL((pairwise_gemm_kernel<T, Acc, MODE, true>), dim3(static_cast<unsigned>(nwg)), kPgThreads, 0, stream(), xp, yp, N, M, D,
+                       static_cast<int>(tiles_n), zero_diag, op);
+  else
+    hipLaunchKernelGGL((pairwise_gemm_kernel<T, Acc, MODE, false>), dim3(static_cast<unsigned>(nwg)), kPgThreads, 0, stream(), xp, yp, N, M, D,
+                       static_cast<int>(tiles_n), zero_diag, op);
+}
+
+// [N, M] in the input dtype; mode 0 linear, 1 cosine, 2 euclidean (fp64 accumulation, as the reference)
+at::Tensor pairwise_gemm(const at::Tensor& x_in, const at::Tensor& y_in, int64_t mode, bool zero_diag) {
+  TORCH_CHECK(x_in.is_cuda() && y_in.is_cuda(), "pairwise_gemm: expected GPU tensors");
+  TORCH_CHECK(x_in.dim() == 2 && y_in.dim() == 2 && x_in.size(1) == y_in.size(1), "pairwise_gemm: expected [N,d] and [M,d]");
+  TORCH_CHECK(x_in.scalar_type() == y_in.scalar_type(), "pairwise_gemm: dtype mismatch");
+  TORCH_CHECK(mode >= kPgLinear && mode <= kPgEuclid, "pairwise_gemm: bad mode");
+  const at::DeviceGuard guard(x_in.device());
+  auto x = x_in.contiguous();
+  auto y = y_in.contiguous();
+  auto out = at::empty({x.size(0), y.size(0)}, x.options());
+  if (x.size(0) == 0 || y.size(0) == 0) return out;
+  TMX_DISPATCH_FLOAT(x.scalar_type(), "pairwise_gemm", [&] {
+    constexpr bool kF64 = std::is_same<scalar_t, double>::value;
+    using AccLC = typename std::conditional<kF64, double, float>::type;
+    if (mode == kPgLinear) launch_pairwise_gemm<scalar_t, AccLC, kPgLinear>(x, y, out, zero_diag);
+    else if (mode == kPgCosine) launch_pairwise_gemm<scalar_t, AccLC, kPgCosine>(x, y, out, zero_diag);
+    else launch_pairwise_gemm<scalar_t, double, kPgEuclid>(x, y, out, zero_diag);
+  });
+  TMX_LAUNCH_CHECK();
+  return out;
+}
+
 }  // namespace tmx
 
-TORCH_LIBRARY_FRAGMENT(tmx, m) { m.def("pairwise_lp(Tensor x, Tensor y, float p, bool fp64_acc) -> Tensor"); }
+TORCH_LIBRARY_FRAGMENT(tmx, m) {
+  m.def("pairwise_lp(Tensor x, Tensor y, float p, bool fp64_acc) -> Tensor");
+  m.def("pairwise_gemm(Tensor x, Tensor y, int mode, bool zero_diag) -> Tensor");
+}
 
-TORCH_LIBRARY_IMPL(tmx, CUDA, m) { m.impl("pairwise_lp", &tmx::pairwise_lp); }
+TORCH_LIBRARY_IMPL(tmx, CUDA, m) {
+  m.impl("pairwise_lp", &tmx::pairwise_lp);
+  m.impl("pairwise_gemm", &tmx::pairwise_gemm);
+}

@@ -1,15 +1,20 @@
-"""Pairwise Euclidean distance (API parity: reference ``functional/pairwise/euclidean.py``): fp64 GEMM
-identity ‖x‖² + ‖y‖² − 2·x·yᵀ (fp64 MFMA on gfx950), like the reference."""
+"""Pairwise Euclidean distance (API parity: reference ``functional/pairwise/euclidean.py``).  GPU: one fused MFMA
+kernel (``csrc/pairwise.hip`` ``pairwise_gemm``: fp64 dot products and norms, the reference's cast / zero-diagonal /
+root epilogue in registers) where measured faster; otherwise the reference's fp64 GEMM identity
+‖x‖² + ‖y‖² − 2·x·yᵀ on ATen."""
 from typing import Optional
 
 import torch
 from torch import Tensor
 from typing_extensions import Literal
 
-from torchmetrics_forked_amd.functional.pairwise.helpers import _check_input, _reduce_distance_matrix
+from torchmetrics_forked_amd.functional.pairwise.helpers import _check_input, _native_gemm, _reduce_distance_matrix
 
 
 def _pairwise_euclidean_distance_update(x: Tensor, y: Optional[Tensor] = None, zero_diagonal: Optional[bool] = None) -> Tensor:
+    fused = _native_gemm(x, y, "euclidean", zero_diagonal)
+    if fused is not None:
+        return fused
     x, y, zero_diagonal = _check_input(x, y, zero_diagonal)
     orig = x.dtype
     x, y = x.to(torch.float64), y.to(torch.float64)

@@ -1,14 +1,19 @@
-"""Pairwise linear (dot-product) similarity (API parity: reference ``functional/pairwise/linear.py``)."""
+"""Pairwise linear (dot-product) similarity (API parity: reference ``functional/pairwise/linear.py``).  GPU: the fused
+MFMA kernel (``csrc/pairwise.hip`` ``pairwise_gemm``, diagonal zeroed in the epilogue) for launch-bound shapes,
+hipBLASLt beyond."""
 from typing import Optional
 
 from torch import Tensor
 from typing_extensions import Literal
 
-from torchmetrics_forked_amd.functional.pairwise.helpers import _check_input, _reduce_distance_matrix
+from torchmetrics_forked_amd.functional.pairwise.helpers import _check_input, _native_gemm, _reduce_distance_matrix
 from torchmetrics_forked_amd.utilities.compute import _safe_matmul
 
 
 def _pairwise_linear_similarity_update(x: Tensor, y: Optional[Tensor] = None, zero_diagonal: Optional[bool] = None) -> Tensor:
+    fused = _native_gemm(x, y, "linear", zero_diagonal)
+    if fused is not None:
+        return fused
     x, y, zero_diagonal = _check_input(x, y, zero_diagonal)
     distance = _safe_matmul(x, y)
     if zero_diagonal:
