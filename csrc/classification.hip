@@ -1243,6 +1243,10 @@ static int small_rows_grid(int TL, int C, bool direct, size_t shm, int64_t ntile
       int nb = 0, cus = 0;
       TMX_CHECK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, kSmallRows * TL, shm));
       TMX_CHECK_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+      // one lane per row (TL = 1, C <= 16: single-wave blocks): at most 16 blocks per CU -- the 32 resident slots of
+      // the occupancy query measured slower (C = 10 / 2 / 16 at 1M rows: 0.043 / 0.047 / 0.052 ms with 4096 blocks
+      // against 0.055-0.059 / 0.062 / 0.054 with 8192; tools/small_grid_sweep.sh, profiles/small_class_sweep_r5.json)
+      if (TL == 1) nb = std::min(nb, 16);
       it = cache.emplace(std::make_tuple(k, shm, dev), std::max(1, nb) * std::max(1, cus)).first;
     }
     per_cu = it->second;
