@@ -297,6 +297,143 @@ __global__ __launch_bounds__(kPgThreads) void pairwise_gemm_kernel(const T* __re
       }
 }
 
+// 16-bit inputs, linear / cosine, large outputs: 128 x 128 tiles on v_mfma_f32_16x16x32_{bf16,f16} (exact 16-bit
+// products, fp32 accumulation -- what the f32 MFMA path above computes, at 16x its rate).  Four waves, each a 64 x 64
+// block of 4 x 4 MFMA tiles; 64-deep K slices of both operands staged row-major in LDS (rows padded to 72 elements:
+// the 16 lanes of each ds_read_b128 group land on distinct bank quads), double-buffered with the next slice in
+// registers.  Cosine scales by reciprocal fp32 row norms taken by one ATen reduction per operand.
+constexpr int kPhT = 128, kPhK = 64, kPhLd = kPhK + 8, kPhThreads = 256;
+typedef short ph_frag8 __attribute__((ext_vector_type(8)));
+typedef float ph_acc4 __attribute__((ext_vector_type(4)));
+
+template <typename T>
+__device__ __forceinline__ ph_acc4 ph_mma(ph_frag8 a, ph_frag8 b, ph_acc4 c) {
+  if constexpr (std::is_same<T, __hip_bfloat16>::value) return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+  else return __builtin_amdgcn_mfma_f32_16x16x32_f16(reinterpret_cast<__attribute__((ext_vector_type(8))) _Float16&>(a),
+                                                      reinterpret_cast<__attribute__((ext_vector_type(8))) _Float16&>(b), c, 0, 0, 0);
+}
+
+template <typename T, int MODE, bool VEC>
+__global__ __launch_bounds__(kPhThreads) void pairwise_gemm_h16_kernel(const T* __restrict__ x, const T* __restrict__ y, int64_t N, int64_t M,
+                                                                       int64_t D, int tiles_n, bool zero_diag, T* __restrict__ out,
+                                                                       const float* __restrict__ xnorm, const float* __restrict__ ynorm) {
+  __shared__ __attribute__((aligned(16))) short lds[2][2][kPhT * kPhLd];  // [buffer][x | y][row * kPhLd + k]
+  __shared__ float nrm[2][kPhT];
+  const int64_t nwg = gridDim.x, orig = blockIdx.x, xcd = orig % 8, q = nwg / 8, rr = nwg % 8;
+  const int64_t id = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
+  const int64_t row0 = (id / tiles_n) * kPhT, col0 = (id % tiles_n) * kPhT;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 1, wc = wave & 1;
+  // staging chunk i (< 4): row (tid >> 3) + 32 i, elements [8 (tid & 7), + 8) of the slice
+  ph_frag8 rx[4], ry[4];
+  auto ld8 = [&](const T* __restrict__ p, int64_t row, int64_t nrows, int64_t k) -> ph_frag8 {
+    ph_frag8 v = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (row < nrows) {
+      if constexpr (VEC) {
+        if (k < D) v = *reinterpret_cast<const ph_frag8*>(p + row * D + k);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (k + e < D) v[e] = reinterpret_cast<const short*>(p)[row * D + k + e];
+      }
+    }
+    return v;
+  };
+  auto load = [&](int64_t k0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = (tid >> 3) + 32 * i;
+      const int64_t k = k0 + 8 * (tid & 7);
+      rx[i] = ld8(x, row0 + r, N, k);
+      ry[i] = ld8(y, col0 + r, M, k);
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = (tid >> 3) + 32 * i, kk = 8 * (tid & 7);
+      *reinterpret_cast<ph_frag8*>(&lds[buf][0][r * kPhLd + kk]) = rx[i];
+      *reinterpret_cast<ph_frag8*>(&lds[buf][1][r * kPhLd + kk]) = ry[i];
+    }
+  };
+  ph_acc4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = ph_acc4{0.f, 0.f, 0.f, 0.f};
+  const int nk = static_cast<int>((D + kPhK - 1) / kPhK);
+  load(0);
+  store(0);
+  __syncthreads();
+  const int fr = lane & 15, fk = 8 * (lane >> 4);
+  for (int s = 0; s < nk; ++s) {
+    const int buf = s & 1;
+    if (s + 1 < nk) load(static_cast<int64_t>(s + 1) * kPhK);
+    const short* A = lds[buf][0];
+    const short* B = lds[buf][1];
+#pragma unroll
+    for (int kh = 0; kh < kPhK; kh += 32) {
+      ph_frag8 af[4], bf[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        af[i] = *reinterpret_cast<const ph_frag8*>(A + (wr * 64 + 16 * i + fr) * kPhLd + kh + fk);
+        bf[i] = *reinterpret_cast<const ph_frag8*>(B + (wc * 64 + 16 * i + fr) * kPhLd + kh + fk);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = ph_mma<T>(af[i], bf[j], acc[i][j]);
+    }
+    if (s + 1 < nk) store(buf ^ 1);
+    __syncthreads();
+  }
+  if constexpr (MODE == kPgCosine) {  // reciprocal row norms of the tile (fp32 norms of the inputs, from the host op)
+    const int64_t g = tid < kPhT ? row0 + tid : col0 + (tid - kPhT);
+    const float nv = tid < kPhT ? (g < N ? xnorm[g] : 1.f) : (g < M ? ynorm[g] : 1.f);
+    nrm[tid >> 7][tid & 127] = 1.f / nv;
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int lr = wr * 64 + 16 * i + (lane >> 4) * 4 + r, lc = wc * 64 + 16 * j + fr;
+        const int64_t gi = row0 + lr, gj = col0 + lc;
+        if (gi >= N || gj >= M) continue;
+        float v = acc[i][j][r];
+        if constexpr (MODE == kPgCosine) v = v * nrm[0][lr] * nrm[1][lc];
+        if (zero_diag && gi == gj) v = 0.f;
+        out[gi * M + gj] = pg_out<T, float>(v);
+      }
+}
+
+template <typename T, int MODE>
+void launch_pairwise_gemm_h16(const at::Tensor& x, const at::Tensor& y, at::Tensor& out, bool zero_diag) {
+  const int64_t N = x.size(0), M = y.size(0), D = x.size(1);
+  const int64_t tiles_m = (N + kPhT - 1) / kPhT, tiles_n = (M + kPhT - 1) / kPhT, nwg = tiles_m * tiles_n;
+  TORCH_CHECK(nwg < (int64_t(1) << 31), "pairwise_gemm: output too large");
+  const auto* xp = reinterpret_cast<const T*>(x.data_ptr());
+  const auto* yp = reinterpret_cast<const T*>(y.data_ptr());
+  auto* op = reinterpret_cast<T*>(out.data_ptr());
+  const bool vec = D % 8 == 0 && reinterpret_cast<uintptr_t>(xp) % 16 == 0 && reinterpret_cast<uintptr_t>(yp) % 16 == 0;
+  // cosine: fp32 row norms by one ATen reduction per operand (vector_norm accumulates 16-bit inputs in fp32)
+  at::Tensor xn, yn;
+  if (MODE == kPgCosine) {
+    xn = at::linalg_vector_norm(x, 2, at::IntArrayRef{1}, false, at::kFloat);
+    yn = at::linalg_vector_norm(y, 2, at::IntArrayRef{1}, false, at::kFloat);
+  }
+  const float* xnp = MODE == kPgCosine ? xn.data_ptr<float>() : nullptr;
+  const float* ynp = MODE == kPgCosine ? yn.data_ptr<float>() : nullptr;
+  if (vec)
+    hipLaunchKernelGGL((pairwise_gemm_h16_kernel<T, MODE, true>), dim3(static_cast<unsigned>(nwg)), kPhThreads, 0, stream(), xp, yp, N, M,
+                       D, static_cast<int>(tiles_n), zero_diag, op, xnp, ynp);
+  else
+    hipLaunchKernelGGL((pairwise_gemm_h16_kernel<T, MODE, false>), dim3(static_cast<unsigned>(nwg)), kPhThreads, 0, stream(), xp, yp, N, M,
+                       D, static_cast<int>(tiles_n), zero_diag, op, xnp, ynp);
+}
+
 template <typename T, typename Acc, int MODE>
 void launch_pairwise_gemm(const at::Tensor& x, const at::Tensor& y, at::Tensor& out, bool zero_diag) {
   const int64_t N = x.size(0), M = y.size(0), D = x.size(1);
@@ -316,6 +453,154 @@ void launch_pairwise_gemm(const at::Tensor& x, const at::Tensor& y, at::Tensor& 
                        static_cast<int>(tiles_n), zero_diag, op);
 }
 
+// ------------------------------------------------------------------------------- FID moments
+// gram += xᵀx and colsum += Σ_b x[b] in fp64 for a feature batch x [B, F] of any float dtype (reference
+// ``image/fid.py``: ``features.double()``, ``sum(dim=0)`` and ``cov_sum.addmm(features.t(), features)`` -- a converted
+// copy, a new F x F fp64 matrix per update and both triangles computed).  Here one launch, in place: only the tiles
+// with tm <= tn of the 64 x 64 tiling are computed (the Gram is symmetric), each by one workgroup on
+// v_mfma_f64_16x16x4_f64 from 16-deep batch slices converted to fp64 on the way into LDS (the batch dimension is the
+// GEMM's K; the staging layout is the k-major one of the pairwise kernel, reached with row-contiguous loads).  An
+// off-diagonal tile adds itself at (tm, tn) and, transposed through LDS for coalesced rows, at (tn, tm); diagonal tiles
+// also fold their feature sums.  Every Gram element has exactly one writer: plain read-modify-writes, no atomics.
+template <typename T, bool VEC>
+__global__ __launch_bounds__(kPgThreads) void fid_gram_kernel(const T* __restrict__ x, int64_t B, int64_t F, int tiles,
+                                                              double* __restrict__ gram, double* __restrict__ colsum) {
+  using Mma = PgMma<double>;
+  constexpr int K = 16, kLd = kPgT + kPgPad, kTld = kPgT + 1;
+  static_assert(2 * 2 * K * kLd >= kPgT * kTld, "the transpose tile reuses the staging buffers");
+  __shared__ double buf[2 * 2 * K * kLd];
+  __shared__ double csum[kPgThreads / kWave][kPgT];
+  auto xs = [&](int b, int k, int r) -> double& { return buf[((b * 2 + 0) * K + k) * kLd + r]; };
+  auto ys = [&](int b, int k, int r) -> double& { return buf[((b * 2 + 1) * K + k) * kLd + r]; };
+  const int64_t nwg = gridDim.x, orig = blockIdx.x, xcd = orig % 8, q = nwg / 8, rr = nwg % 8;
+  int64_t id = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
+  int tm = 0;
+  while (id >= tiles - tm) {  // upper-triangular row tm holds tiles - tm tiles (tiles <= 64 for F <= 4096)
+    id -= tiles - tm;
+    ++tm;
+  }
+  const int tn = tm + static_cast<int>(id);
+  const int64_t f0 = static_cast<int64_t>(tm) * kPgT, g0 = static_cast<int64_t>(tn) * kPgT;
+  const bool diag = tm == tn;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 1, wc = wave & 1;
+  const int sb = tid >> 4, sf = 4 * (tid & 15);  // staging: batch row sb of the slice, features [sf, sf + 4)
+  double ra[4], rb[4], cs[4] = {0.0, 0.0, 0.0, 0.0};
+  auto load = [&](int64_t b0) {
+    pg_load<T, double, 4, VEC>(x, b0 + sb, B, f0 + sf, F, ra);
+    pg_load<T, double, 4, VEC>(x, b0 + sb, B, g0 + sf, F, rb);
+    if (diag) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) cs[e] += ra[e];
+    }
+  };
+  auto store = [&](int b) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      xs(b, sb, sf + e) = ra[e];
+      ys(b, sb, sf + e) = rb[e];
+    }
+  };
+  typename Mma::V acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = typename Mma::V{0, 0, 0, 0};
+  const int nk = static_cast<int>((B + K - 1) / K);
+  load(0);
+  store(0);
+  __syncthreads();
+  const int fr = lane & 15, fk = lane >> 4;
+  for (int s = 0; s < nk; ++s) {
+    const int b = s & 1;
+    if (s + 1 < nk) load(static_cast<int64_t>(s + 1) * K);
+#pragma unroll
+    for (int kk = 0; kk < K; kk += 4) {
+      double a[2], c[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        a[i] = xs(b, kk + fk, wr * 32 + 16 * i + fr);
+        c[i] = ys(b, kk + fk, wc * 32 + 16 * i + fr);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = Mma::mma(a[i], c[j], acc[i][j]);
+    }
+    if (s + 1 < nk) store(b ^ 1);
+    __syncthreads();
+  }
+  // (tm, tn): rows f0 + lr, columns g0 + lc; off-diagonal tiles stage the block for the mirrored (tn, tm) rows
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int lr = wr * 32 + 16 * i + Mma::row(lane, r), lc = wc * 32 + 16 * j + fr;
+        const double v = acc[i][j][r];
+        if (f0 + lr < F && g0 + lc < F) gram[(f0 + lr) * F + g0 + lc] += v;
+        if (!diag) buf[lc * kTld + lr] = v;  // transposed: row lc of the mirrored block
+      }
+  if (!diag) {
+    __syncthreads();
+    for (int e = tid; e < kPgT * kPgT; e += kPgThreads) {
+      const int r = e / kPgT, c = e % kPgT;
+      if (g0 + r < F && f0 + c < F) gram[(g0 + r) * F + f0 + c] += buf[r * kTld + c];
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {  // the 16 lanes of a wave sharing sf are 16 apart
+      cs[e] += __shfl_xor(cs[e], 16, kWave);
+      cs[e] += __shfl_xor(cs[e], 32, kWave);
+    }
+    if (lane < 16) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) csum[wave][sf + e] = cs[e];
+    }
+    __syncthreads();
+    if (tid < kPgT && f0 + tid < F) {
+      double t = 0.0;
+#pragma unroll
+      for (int w = 0; w < kPgThreads / kWave; ++w) t += csum[w][tid];
+      colsum[f0 + tid] += t;
+    }
+  }
+}
+
+template <typename T>
+void launch_fid_gram(const at::Tensor& x, at::Tensor& gram, at::Tensor& colsum) {
+  const int64_t B = x.size(0), F = x.size(1);
+  const int tiles = static_cast<int>((F + kPgT - 1) / kPgT);
+  const int64_t nwg = static_cast<int64_t>(tiles) * (tiles + 1) / 2;
+  const auto* xp = reinterpret_cast<const T*>(x.data_ptr());
+  constexpr int align = 4 * sizeof(T) < 16 ? 4 * sizeof(T) : 16;
+  const bool vec = F % 4 == 0 && reinterpret_cast<uintptr_t>(xp) % align == 0;
+  if (vec)
+    hipLaunchKernelGGL((fid_gram_kernel<T, true>), dim3(static_cast<unsigned>(nwg)), kPgThreads, 0, stream(), xp, B, F, tiles,
+                       gram.data_ptr<double>(), colsum.data_ptr<double>());
+  else
+    hipLaunchKernelGGL((fid_gram_kernel<T, false>), dim3(static_cast<unsigned>(nwg)), kPgThreads, 0, stream(), xp, B, F, tiles,
+                       gram.data_ptr<double>(), colsum.data_ptr<double>());
+}
+
+// gram [F, F] += xᵀx, colsum [F] += Σ_b x[b] (fp64 states; x [B, F] fp32 / fp64 / bf16 / fp16)
+void fid_gram_update(const at::Tensor& x_in, at::Tensor gram, at::Tensor colsum) {
+  TORCH_CHECK(x_in.is_cuda() && gram.is_cuda() && colsum.is_cuda(), "fid_gram_update: expected GPU tensors");
+  TORCH_CHECK(x_in.dim() == 2, "fid_gram_update: expected features [B, F]");
+  const int64_t F = x_in.size(1);
+  TORCH_CHECK(gram.scalar_type() == at::kDouble && colsum.scalar_type() == at::kDouble, "fid_gram_update: fp64 states expected");
+  TORCH_CHECK(gram.dim() == 2 && gram.size(0) == F && gram.size(1) == F && gram.is_contiguous(), "fid_gram_update: gram must be a contiguous [F, F]");
+  TORCH_CHECK(colsum.dim() == 1 && colsum.size(0) == F && colsum.is_contiguous(), "fid_gram_update: colsum must be a contiguous [F]");
+  TORCH_CHECK(F <= 4096 * 4, "fid_gram_update: too many features");
+  TORCH_CHECK(x_in.device() == gram.device() && x_in.device() == colsum.device(), "fid_gram_update: device mismatch");
+  const at::DeviceGuard guard(x_in.device());
+  if (x_in.size(0) == 0 || F == 0) return;
+  auto x = x_in.contiguous();
+  TMX_DISPATCH_FLOAT(x.scalar_type(), "fid_gram_update", [&] { launch_fid_gram<scalar_t>(x, gram, colsum); });
+  TMX_LAUNCH_CHECK();
+}
+
 // [N, M] in the input dtype; mode 0 linear, 1 cosine, 2 euclidean (fp64 accumulation, as the reference)
 at::Tensor pairwise_gemm(const at::Tensor& x_in, const at::Tensor& y_in, int64_t mode, bool zero_diag) {
   TORCH_CHECK(x_in.is_cuda() && y_in.is_cuda(), "pairwise_gemm: expected GPU tensors");
@@ -330,6 +615,16 @@ at::Tensor pairwise_gemm(const at::Tensor& x_in, const at::Tensor& y_in, int64_t
   TMX_DISPATCH_FLOAT(x.scalar_type(), "pairwise_gemm", [&] {
     constexpr bool kF64 = std::is_same<scalar_t, double>::value;
     using AccLC = typename std::conditional<kF64, double, float>::type;
+    constexpr bool kH16 = std::is_same<scalar_t, __hip_bfloat16>::value || std::is_same<scalar_t, __half>::value;
+    // 16-bit linear / cosine with at least 256 128 x 128 tiles: the 16-bit MFMA kernel
+    const bool h16 = kH16 && mode != kPgEuclid && ((x.size(0) + kPhT - 1) / kPhT) * ((y.size(0) + kPhT - 1) / kPhT) >= 256;
+    if constexpr (kH16) {
+      if (h16) {
+        if (mode == kPgLinear) launch_pairwise_gemm_h16<scalar_t, kPgLinear>(x, y, out, zero_diag);
+        else launch_pairwise_gemm_h16<scalar_t, kPgCosine>(x, y, out, zero_diag);
+        return;
+      }
+    }
     if (mode == kPgLinear) launch_pairwise_gemm<scalar_t, AccLC, kPgLinear>(x, y, out, zero_diag);
     else if (mode == kPgCosine) launch_pairwise_gemm<scalar_t, AccLC, kPgCosine>(x, y, out, zero_diag);
     else launch_pairwise_gemm<scalar_t, double, kPgEuclid>(x, y, out, zero_diag);
@@ -343,9 +638,11 @@ at::Tensor pairwise_gemm(const at::Tensor& x_in, const at::Tensor& y_in, int64_t
 TORCH_LIBRARY_FRAGMENT(tmx, m) {
   m.def("pairwise_lp(Tensor x, Tensor y, float p, bool fp64_acc) -> Tensor");
   m.def("pairwise_gemm(Tensor x, Tensor y, int mode, bool zero_diag) -> Tensor");
+  m.def("fid_gram_update(Tensor x, Tensor(a!) gram, Tensor(b!) colsum) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(tmx, CUDA, m) {
   m.impl("pairwise_lp", &tmx::pairwise_lp);
   m.impl("pairwise_gemm", &tmx::pairwise_gemm);
+  m.impl("fid_gram_update", &tmx::fid_gram_update);
 }

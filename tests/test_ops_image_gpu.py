@@ -125,3 +125,52 @@ def test_fused_ssim_psnr_collection(shape):
     assert torch.allclose(out["ssim"].cpu(), sep[0].compute().cpu(), atol=1e-6)
     assert torch.allclose(out["psnr"].cpu(), sep[1].compute().cpu(), atol=1e-4)
     assert int(coll["psnr"].total) == int(sep[1].total)
+
+
+@pytest.mark.parametrize("shape", [(256, 2048), (37, 100), (5, 64), (1, 3), (200, 130)])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64, torch.bfloat16])
+def test_fid_gram_update_vs_fp64(shape, dtype):
+    """Fused FID moments (``fid_gram_update``: upper tiles mirrored, feature sums on the diagonal tiles) against the
+    fp64 torch reference ``x.double().T @ x.double()`` / ``sum``, accumulated over two updates."""
+    g = torch.Generator().manual_seed(sum(shape))
+    x = torch.randn(*shape, generator=g).to(dtype).cuda()
+    F = shape[1]
+    gram = torch.zeros(F, F, dtype=torch.float64, device="cuda")
+    colsum = torch.zeros(F, dtype=torch.float64, device="cuda")
+    for _ in range(2):
+        torch.ops.tmx.fid_gram_update(x, gram, colsum)
+    xd = x.double()
+    torch.testing.assert_close(gram, 2 * xd.T @ xd, rtol=1e-12, atol=1e-10)
+    torch.testing.assert_close(colsum, 2 * xd.sum(0), rtol=1e-12, atol=1e-10)
+    assert torch.equal(gram, gram.T)
+
+
+def test_fid_metric_fused_moments_match_cpu():
+    """FrechetInceptionDistance with a small feature extractor: GPU (fused moments) vs CPU (double + sum + addmm)."""
+    from torchmetrics_forked_amd.image import FrechetInceptionDistance
+
+    class Feat(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            g = torch.Generator().manual_seed(0)
+            self.register_buffer("w", torch.randn(3 * 4, 320, generator=g))
+
+        def forward(self, x):
+            x = torch.nn.functional.adaptive_avg_pool2d(x.float(), 2).flatten(1)
+            return torch.tanh(x / 128.0 - 1.0) @ self.w
+
+    g = torch.Generator().manual_seed(1)
+    real = torch.randint(0, 256, (40, 3, 32, 32), generator=g, dtype=torch.uint8)
+    fake = torch.randint(0, 200, (40, 3, 32, 32), generator=g, dtype=torch.uint8)
+    from torchmetrics_forked_amd.image.generative import _fused_moments
+
+    assert _fused_moments(torch.zeros(2, 320, device="cuda"), torch.zeros(320, 320, dtype=torch.float64, device="cuda"),
+                          torch.zeros(320, dtype=torch.float64, device="cuda"))
+    vals = []
+    for dev in ("cuda", "cpu"):
+        m = FrechetInceptionDistance(feature=Feat()).to(dev)
+        for i in range(2):
+            m.update(real[20 * i:20 * (i + 1)].to(dev), real=True)
+            m.update(fake[20 * i:20 * (i + 1)].to(dev), real=False)
+        vals.append(m.compute().cpu())
+    torch.testing.assert_close(vals[0], vals[1], rtol=1e-6, atol=1e-6)

@@ -113,4 +113,20 @@ def test_routing_sends_deep_or_large_products_to_the_library():
     assert helpers._fused_wins("euclidean", torch.float32, 8192, 8192, 512)
     assert not helpers._fused_wins("euclidean", torch.float32, 4096, 4096, 2048)
     assert helpers._fused_wins("linear", torch.float32, 1000, 1000, 128)
-    assert not helpers._fused_wins("cosine", torch.bfloat16, 4096, 4096, 512)
+    assert helpers._fused_wins("cosine", torch.bfloat16, 4096, 4096, 512)  # 16-bit MFMA tiles
+    assert not helpers._fused_wins("cosine", torch.bfloat16, 8192, 8192, 256)
+    assert not helpers._fused_wins("linear", torch.bfloat16, 1000, 1000, 1024)
+
+
+@pytest.mark.parametrize("D", [64, 100])
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_pairwise_gemm_16bit_mfma_tiles(D, mode, dtype):
+    """>= 256 128 x 128 output tiles of 16-bit linear / cosine take the v_mfma_f32_16x16x32 kernel (D = 100: the
+    element-wise staging path)."""
+    g = torch.Generator().manual_seed(D + mode)
+    x = torch.randn(2048, D, generator=g).to(dtype).cuda()
+    y = torch.randn(2100, D, generator=g).to(dtype).cuda()
+    for zd in (False, True):
+        out = torch.ops.tmx.pairwise_gemm(x, y, mode, zd)
+        torch.testing.assert_close(out.double(), _ref(mode, x, y, zd).double(), rtol=1e-2, atol=1e-2 * (D ** 0.5 if mode == 0 else 1))

@@ -33,12 +33,15 @@ def _fused_wins(mode: str, dtype: torch.dtype, n: int, m: int, d: int) -> bool:
     Euclidean: the kernel keeps the reference's fp64 N x M chain (five HBM round trips) out of memory and wins at every
     measured shape up to d = 512 (1.3-4.2x) and up to 2^31 work at d = 1024; deeper, rocBLAS's dgemm out-runs the
     kernel's fp64 MFMA loop.  Linear / cosine are a plain library GEMM plus a diagonal fill / row normalisation: the
-    kernel wins while the launches dominate, hipBLASLt beyond -- much earlier for 16-bit inputs, which it runs on
-    bf16 / fp16 MFMA at 16x the fp32 MFMA rate the kernel uses."""
+    kernel wins while the launches dominate, hipBLASLt beyond.  16-bit inputs with at least 256 128 x 128 output tiles
+    run on the kernel's bf16 / fp16 MFMA tiles (1.1-3.3x over hipBLASLt + the epilogue up to 2^33 work); smaller
+    outputs take its fp32 MFMA tiles, which win only while the launches dominate."""
     work = n * m * d
     if mode == "euclidean":
         return d <= 512 or work <= (1 << 31)
     if dtype in (torch.bfloat16, torch.float16):
+        if ((n + 127) // 128) * ((m + 127) // 128) >= 256:  # the kernel's 16-bit MFMA tiles (csrc: kPhT)
+            return work <= (1 << 33)
         return work <= (1 << 29) and d <= (256 if mode == "linear" else 1024)
     return work < (1 << 32) and d <= (512 if mode == "linear" else 1024)
 
