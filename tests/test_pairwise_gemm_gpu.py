@@ -114,7 +114,7 @@ def test_routing_sends_deep_or_large_products_to_the_library():
     assert not helpers._fused_wins("euclidean", torch.float32, 4096, 4096, 2048)
     assert helpers._fused_wins("linear", torch.float32, 1000, 1000, 128)
     assert helpers._fused_wins("cosine", torch.bfloat16, 4096, 4096, 512)  # 16-bit MFMA tiles
-    assert not helpers._fused_wins("cosine", torch.bfloat16, 8192, 8192, 256)
+    assert not helpers._fused_wins("cosine", torch.bfloat16, 8192, 8192, 64)
     assert not helpers._fused_wins("linear", torch.bfloat16, 1000, 1000, 1024)
 
 

@@ -34,14 +34,14 @@ def _fused_wins(mode: str, dtype: torch.dtype, n: int, m: int, d: int) -> bool:
     measured shape up to d = 512 (1.3-4.2x) and up to 2^31 work at d = 1024; deeper, rocBLAS's dgemm out-runs the
     kernel's fp64 MFMA loop.  Linear / cosine are a plain library GEMM plus a diagonal fill / row normalisation: the
     kernel wins while the launches dominate, hipBLASLt beyond.  16-bit inputs with at least 256 128 x 128 output tiles
-    run on the kernel's bf16 / fp16 MFMA tiles (1.1-3.3x over hipBLASLt + the epilogue up to 2^33 work); smaller
-    outputs take its fp32 MFMA tiles, which win only while the launches dominate."""
+    run on the kernel's bf16 / fp16 MFMA tiles (1.0-3.3x over hipBLASLt + the epilogue up to 2^33 work and 2^25
+    outputs); smaller outputs take its fp32 MFMA tiles, which win only while the launches dominate."""
     work = n * m * d
     if mode == "euclidean":
         return d <= 512 or work <= (1 << 31)
     if dtype in (torch.bfloat16, torch.float16):
         if ((n + 127) // 128) * ((m + 127) // 128) >= 256:  # the kernel's 16-bit MFMA tiles (csrc: kPhT)
-            return work <= (1 << 33)
+            return work <= (1 << 33) and n * m <= (1 << 25)
         return work <= (1 << 29) and d <= (256 if mode == "linear" else 1024)
     return work < (1 << 32) and d <= (512 if mode == "linear" else 1024)
 
