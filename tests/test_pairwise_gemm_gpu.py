@@ -116,6 +116,8 @@ def test_routing_sends_deep_or_large_products_to_the_library():
     assert helpers._fused_wins("cosine", torch.bfloat16, 4096, 4096, 512)  # 16-bit MFMA tiles
     assert not helpers._fused_wins("cosine", torch.bfloat16, 8192, 8192, 64)
     assert not helpers._fused_wins("linear", torch.bfloat16, 1000, 1000, 1024)
+    assert not helpers._fused_wins("linear", torch.float64, 1000, 1000, 128)
+    assert helpers._fused_wins("cosine", torch.float64, 1000, 1000, 128)
 
 
 @pytest.mark.parametrize("D", [64, 100])

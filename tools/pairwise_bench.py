@@ -39,7 +39,8 @@ def main() -> None:
 
     res = {}
     for (n, m, d) in shapes:
-        for dtype in (torch.float32, torch.bfloat16):
+        dtypes = [getattr(torch, t) for t in os.environ.get("PW_DTYPES", "float32,bfloat16").split(",")]
+        for dtype in dtypes:
             x = torch.randn(n, d, device="cuda").to(dtype)
             y = torch.randn(m, d, device="cuda").to(dtype)
             for name, fn in fns.items():

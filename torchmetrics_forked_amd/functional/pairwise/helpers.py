@@ -39,6 +39,8 @@ def _fused_wins(mode: str, dtype: torch.dtype, n: int, m: int, d: int) -> bool:
     work = n * m * d
     if mode == "euclidean":
         return d <= 512 or work <= (1 << 31)
+    if dtype == torch.float64:  # rocBLAS's dgemm beats the fp64 MFMA loop on the plain product
+        return mode == "cosine" and work <= (1 << 29) and d <= 256
     if dtype in (torch.bfloat16, torch.float16):
         if ((n + 127) // 128) * ((m + 127) // 128) >= 256:  # the kernel's 16-bit MFMA tiles (csrc: kPhT)
             return work <= (1 << 33) and n * m <= (1 << 25)
