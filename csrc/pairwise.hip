@@ -485,20 +485,22 @@ __global__ __launch_bounds__(kPgThreads) void fid_gram_kernel(const T* __restric
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 1, wc = wave & 1;
   const int sb = tid >> 4, sf = 4 * (tid & 15);  // staging: batch row sb of the slice, features [sf, sf + 4)
-  double ra[4], rb[4], cs[4] = {0.0, 0.0, 0.0, 0.0};
-  auto load = [&](int64_t b0) {
-    pg_load<T, double, 4, VEC>(x, b0 + sb, B, f0 + sf, F, ra);
-    pg_load<T, double, 4, VEC>(x, b0 + sb, B, g0 + sf, F, rb);
+  // two register sets: slices s + 1 and s + 2 are in flight while slice s is multiplied (a batch of a few hundred
+  // rows is only ~16 slices, and one slice of prefetch left each slice waiting on its loads)
+  double ra[2][4], rb[2][4], cs[4] = {0.0, 0.0, 0.0, 0.0};
+  auto load = [&](int64_t b0, double (&pa)[4], double (&pb)[4]) {
+    pg_load<T, double, 4, VEC>(x, b0 + sb, B, f0 + sf, F, pa);
+    pg_load<T, double, 4, VEC>(x, b0 + sb, B, g0 + sf, F, pb);
     if (diag) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) cs[e] += ra[e];
+      for (int e = 0; e < 4; ++e) cs[e] += pa[e];
     }
   };
-  auto store = [&](int b) {
+  auto store = [&](int b, const double (&pa)[4], const double (&pb)[4]) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      xs(b, sb, sf + e) = ra[e];
-      ys(b, sb, sf + e) = rb[e];
+      xs(b, sb, sf + e) = pa[e];
+      ys(b, sb, sf + e) = pb[e];
     }
   };
   typename Mma::V acc[2][2];
@@ -507,13 +509,15 @@ __global__ __launch_bounds__(kPgThreads) void fid_gram_kernel(const T* __restric
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = typename Mma::V{0, 0, 0, 0};
   const int nk = static_cast<int>((B + K - 1) / K);
-  load(0);
-  store(0);
+  load(0, ra[0], rb[0]);
+  store(0, ra[0], rb[0]);
+  if (nk > 1) load(K, ra[1], rb[1]);
   __syncthreads();
   const int fr = lane & 15, fk = lane >> 4;
-  for (int s = 0; s < nk; ++s) {
+  auto step = [&](int s, double (&na)[4], double (&nb)[4], const double (&sa)[4], const double (&sb2)[4]) {
+    // na / nb: the set that held slice s (already in LDS) takes slice s + 2; sa / sb2 hold slice s + 1
     const int b = s & 1;
-    if (s + 1 < nk) load(static_cast<int64_t>(s + 1) * K);
+    if (s + 2 < nk) load(static_cast<int64_t>(s + 2) * K, na, nb);
 #pragma unroll
     for (int kk = 0; kk < K; kk += 4) {
       double a[2], c[2];
@@ -527,8 +531,12 @@ __global__ __launch_bounds__(kPgThreads) void fid_gram_kernel(const T* __restric
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = Mma::mma(a[i], c[j], acc[i][j]);
     }
-    if (s + 1 < nk) store(b ^ 1);
+    if (s + 1 < nk) store(b ^ 1, sa, sb2);
     __syncthreads();
+  };
+  for (int s = 0; s < nk; s += 2) {
+    step(s, ra[0], rb[0], ra[1], rb[1]);
+    if (s + 1 < nk) step(s + 1, ra[1], rb[1], ra[0], rb[0]);
   }
   // (tm, tn): rows f0 + lr, columns g0 + lc; off-diagonal tiles stage the block for the mirrored (tn, tm) rows
 #pragma unroll
