@@ -210,24 +210,25 @@ __global__ __launch_bounds__(kPgThreads) void pairwise_gemm_kernel(const T* __re
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 1, wc = wave & 1;
   const int sr = tid >> 2, sk = (tid & 3) * KPT;  // staging: row sr, k [sk, sk + KPT) of the slice
-  Acc rx[KPT], ry[KPT];
+  // two register sets: slices s + 1 and s + 2 in flight while slice s is multiplied
+  Acc rx[2][KPT], ry[2][KPT];
   Acc px = Acc(0), py = Acc(0);
-  auto load = [&](int64_t k0) {
-    pg_load<T, Acc, KPT, VEC>(x, row0 + sr, N, k0 + sk, D, rx);
-    pg_load<T, Acc, KPT, VEC>(y, col0 + sr, M, k0 + sk, D, ry);
+  auto load = [&](int64_t k0, Acc (&qx)[KPT], Acc (&qy)[KPT]) {
+    pg_load<T, Acc, KPT, VEC>(x, row0 + sr, N, k0 + sk, D, qx);
+    pg_load<T, Acc, KPT, VEC>(y, col0 + sr, M, k0 + sk, D, qy);
     if constexpr (MODE != kPgLinear) {
 #pragma unroll
       for (int i = 0; i < KPT; ++i) {
-        px = fma(rx[i], rx[i], px);
-        py = fma(ry[i], ry[i], py);
+        px = fma(qx[i], qx[i], px);
+        py = fma(qy[i], qy[i], py);
       }
     }
   };
-  auto store = [&](int buf) {
+  auto store = [&](int buf, const Acc (&qx)[KPT], const Acc (&qy)[KPT]) {
 #pragma unroll
     for (int i = 0; i < KPT; ++i) {
-      xs[buf][sk + i][sr] = rx[i];
-      ys[buf][sk + i][sr] = ry[i];
+      xs[buf][sk + i][sr] = qx[i];
+      ys[buf][sk + i][sr] = qy[i];
     }
   };
   typename Mma::V acc[2][2];
@@ -236,13 +237,15 @@ __global__ __launch_bounds__(kPgThreads) void pairwise_gemm_kernel(const T* __re
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = typename Mma::V{0, 0, 0, 0};
   const int nk = static_cast<int>((D + kPgK - 1) / kPgK);
-  load(0);
-  store(0);
+  load(0, rx[0], ry[0]);
+  store(0, rx[0], ry[0]);
+  if (nk > 1) load(kPgK, rx[1], ry[1]);
   __syncthreads();
   const int fr = lane & 15, fk = lane >> 4;
-  for (int s = 0; s < nk; ++s) {
+  // nx / ny: the set that held slice s (already in LDS) takes slice s + 2; sx / sy hold slice s + 1
+  auto step = [&](int s, Acc (&nx)[KPT], Acc (&ny)[KPT], const Acc (&sx)[KPT], const Acc (&sy)[KPT]) {
     const int buf = s & 1;
-    if (s + 1 < nk) load(static_cast<int64_t>(s + 1) * kPgK);
+    if (s + 2 < nk) load(static_cast<int64_t>(s + 2) * kPgK, nx, ny);
 #pragma unroll
     for (int kk = 0; kk < kPgK; kk += 4) {
       Acc a[2], b[2];
@@ -256,8 +259,12 @@ __global__ __launch_bounds__(kPgThreads) void pairwise_gemm_kernel(const T* __re
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = Mma::mma(a[i], b[j], acc[i][j]);
     }
-    if (s + 1 < nk) store(buf ^ 1);  // that buffer was last read before the previous barrier
+    if (s + 1 < nk) store(buf ^ 1, sx, sy);  // that buffer was last read before the previous barrier
     __syncthreads();
+  };
+  for (int s = 0; s < nk; s += 2) {
+    step(s, rx[0], ry[0], rx[1], ry[1]);
+    if (s + 1 < nk) step(s + 1, rx[1], ry[1], rx[0], ry[0]);
   }
   if constexpr (MODE != kPgLinear) {
     // four consecutive lanes share a staging row

@@ -110,7 +110,7 @@ def test_autograd_and_mixed_dtypes_take_the_aten_path():
 def test_routing_sends_deep_or_large_products_to_the_library():
     from torchmetrics_forked_amd.functional.pairwise import helpers
 
-    assert helpers._fused_wins("euclidean", torch.float32, 8192, 8192, 512)
+    assert helpers._fused_wins("euclidean", torch.float32, 8192, 8192, 1024)
     assert not helpers._fused_wins("euclidean", torch.float32, 4096, 4096, 2048)
     assert helpers._fused_wins("linear", torch.float32, 1000, 1000, 128)
     assert helpers._fused_wins("cosine", torch.bfloat16, 4096, 4096, 512)  # 16-bit MFMA tiles

@@ -31,14 +31,13 @@ _FUSED = True  # False: always the ATen composition; "force": always the kernel 
 def _fused_wins(mode: str, dtype: torch.dtype, n: int, m: int, d: int) -> bool:
     """Measured routing (``tools/pairwise_bench.py``, ``profiles/pairwise_gemm_r5.json``; work = n * m * d).
     Euclidean: the kernel keeps the reference's fp64 N x M chain (five HBM round trips) out of memory and wins at every
-    measured shape up to d = 512 (1.3-4.2x) and up to 2^31 work at d = 1024; deeper, rocBLAS's dgemm out-runs the
-    kernel's fp64 MFMA loop.  Linear / cosine are a plain library GEMM plus a diagonal fill / row normalisation: the
+    measured shape up to d = 1024 (1.05-4.2x); deeper, rocBLAS's dgemm out-runs the kernel's fp64 MFMA loop.  Linear / cosine are a plain library GEMM plus a diagonal fill / row normalisation: the
     kernel wins while the launches dominate, hipBLASLt beyond.  16-bit inputs with at least 256 128 x 128 output tiles
     run on the kernel's bf16 / fp16 MFMA tiles (1.0-3.3x over hipBLASLt + the epilogue up to 2^33 work and 2^25
     outputs); smaller outputs take its fp32 MFMA tiles, which win only while the launches dominate."""
     work = n * m * d
     if mode == "euclidean":
-        return d <= 512 or work <= (1 << 31)
+        return d <= 1024 or work <= (1 << 31)
     if dtype == torch.float64:  # rocBLAS's dgemm beats the fp64 MFMA loop on the plain product
         return mode == "cosine" and work <= (1 << 29) and d <= 256
     if dtype in (torch.bfloat16, torch.float16):
