@@ -402,7 +402,15 @@ class Metric(Module, ABC):
                 d[n] = g
             # keep the batch states for the next forward when they are zero-defaulted and the batch value does not
             # alias them (a confusion matrix's compute returns its state)
-            d["_sum_fwd_scratch"] = batch if d["_sum_fwd_zero"] and not _aliases(batch_val, batch) else None
+            if d["_sum_fwd_zero"]:
+                # the storage addresses of a reused scratch are known from the previous forward
+                ptrs = d.get("_sum_fwd_ptrs") if fresh is scratch and all(a is b for a, b in zip(batch, fresh)) else None
+                if ptrs is None:
+                    ptrs = {t.untyped_storage().data_ptr() for t in batch}
+                d["_sum_fwd_ptrs"] = ptrs
+                d["_sum_fwd_scratch"] = None if _aliases(batch_val, ptrs) else batch
+            else:
+                d["_sum_fwd_scratch"] = None
             self._leave_batch_mode(saved)
             return batch_val
         snapshot = self.metric_state
@@ -821,7 +829,7 @@ class Metric(Module, ABC):
 
     def __getstate__(self) -> Dict[str, Any]:
         self._join_side_work()
-        return {k: v for k, v in self.__dict__.items() if k not in ("update", "compute", "_update_signature", "_hist_spare", "_batch_bufs", "_batch_sink", "_batch_view", "_fast_update", "_sum_fwd", "_sum_fwd_defaults", "_sum_fwd_scratch", "_tensor_states", "_owned_buf")}
+        return {k: v for k, v in self.__dict__.items() if k not in ("update", "compute", "_update_signature", "_hist_spare", "_batch_bufs", "_batch_sink", "_batch_view", "_fast_update", "_sum_fwd", "_sum_fwd_defaults", "_sum_fwd_scratch", "_sum_fwd_ptrs", "_tensor_states", "_owned_buf")}
 
     def __setstate__(self, state: Dict[str, Any]) -> None:
         self.__dict__.update(state)
@@ -863,7 +871,7 @@ class Metric(Module, ABC):
 
     def _apply(self, fn: Callable, exclude_state: Sequence[str] = "") -> Module:
         self._join_side_work()
-        for k in ("_sum_fwd", "_sum_fwd_defaults", "_sum_fwd_scratch"):  # forward's caches follow the new device / dtype
+        for k in ("_sum_fwd", "_sum_fwd_defaults", "_sum_fwd_scratch", "_sum_fwd_ptrs"):  # forward's caches follow the new device / dtype
             self.__dict__.pop(k, None)
         this = super()._apply(fn)
         fs = str(fn)
@@ -1131,10 +1139,11 @@ class CompositionalMetric(Metric):
         return compute
 
 
-def _aliases(value: Any, tensors: List[Tensor]) -> bool:
+def _aliases(value: Any, ptrs: Any) -> bool:
     """True if any tensor in ``value`` (a tensor, or a flat dict / tuple / list of them) shares storage with one of
-    ``tensors``."""
-    ptrs = {t.untyped_storage().data_ptr() for t in tensors}
+    the storages at ``ptrs`` (storage data pointers; a list of tensors is converted)."""
+    if isinstance(ptrs, list):
+        ptrs = {t.untyped_storage().data_ptr() for t in ptrs}
     items = value.values() if isinstance(value, dict) else (value if isinstance(value, (tuple, list)) else (value,))
     for v in items:
         if isinstance(v, Tensor) and v.untyped_storage().data_ptr() in ptrs:
