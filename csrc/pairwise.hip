@@ -460,6 +460,149 @@ void launch_pairwise_gemm(const at::Tensor& x, const at::Tensor& y, at::Tensor& 
                        static_cast<int>(tiles_n), zero_diag, op);
 }
 
+// ------------------------------------------------------------------------------- KID polynomial MMD sums (K20)
+// One launch per subset of the reference's ``poly_mmd`` (``image/kid.py``: three GEMMs f @ gᵀ, then
+// (· gamma + coef) ** degree, diagonal and full sums -- about twenty kernels and three m x m matrices per subset).
+// Here the three products (real·real, fake·fake, real·fake) are tiles of one grid; rows are gathered through the
+// subset index vectors while they are staged (no subset copies), and each tile's epilogue raises its dot products to
+// the polynomial and folds them (diagonal left out of the two self terms) into one fp64 atomic per workgroup.
+template <typename T, typename Acc, bool VEC>
+__global__ __launch_bounds__(kPgThreads) void kid_poly_kernel(const T* __restrict__ real, const T* __restrict__ fake,
+                                                              const int64_t* __restrict__ idx_r, const int64_t* __restrict__ idx_f,
+                                                              int64_t m, int64_t D, int tiles, int degree, double gamma, double coef,
+                                                              double* __restrict__ sums) {
+  using Mma = PgMma<Acc>;
+  constexpr int kPgK = pg_k<Acc>(), KPT = kPgK / 4;
+  __shared__ Acc xs[2][kPgK][kPgT + kPgPad];
+  __shared__ Acc ys[2][kPgK][kPgT + kPgPad];
+  __shared__ double red[kPgThreads / kWave];
+  const int64_t per = static_cast<int64_t>(tiles) * tiles;
+  const int prob = static_cast<int>(blockIdx.x / per);  // 0: real x real, 1: fake x fake, 2: real x fake
+  const int64_t t = blockIdx.x % per;
+  const int64_t row0 = (t / tiles) * kPgT, col0 = (t % tiles) * kPgT;
+  const T* A = prob == 1 ? fake : real;
+  const T* B = prob == 0 ? real : fake;
+  const int64_t* ia = prob == 1 ? idx_f : idx_r;
+  const int64_t* ib = prob == 0 ? idx_r : idx_f;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 1, wc = wave & 1;
+  const int sr = tid >> 2, sk = (tid & 3) * KPT;
+  const int64_t ra_row = row0 + sr < m ? ia[row0 + sr] : 0, rb_row = col0 + sr < m ? ib[col0 + sr] : 0;
+  Acc rx[KPT], ry[KPT];
+  auto load = [&](int64_t k0) {
+    // a row outside the subset (row0 + sr >= m) loads zeros: nrows = 0 masks it
+    pg_load<T, Acc, KPT, VEC>(A, ra_row, row0 + sr < m ? ra_row + 1 : 0, k0 + sk, D, rx);
+    pg_load<T, Acc, KPT, VEC>(B, rb_row, col0 + sr < m ? rb_row + 1 : 0, k0 + sk, D, ry);
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < KPT; ++i) {
+      xs[buf][sk + i][sr] = rx[i];
+      ys[buf][sk + i][sr] = ry[i];
+    }
+  };
+  typename Mma::V acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = typename Mma::V{0, 0, 0, 0};
+  const int nk = static_cast<int>((D + kPgK - 1) / kPgK);
+  load(0);
+  store(0);
+  __syncthreads();
+  const int fr = lane & 15, fk = lane >> 4;
+  for (int s = 0; s < nk; ++s) {
+    const int buf = s & 1;
+    if (s + 1 < nk) load(static_cast<int64_t>(s + 1) * kPgK);
+#pragma unroll
+    for (int kk = 0; kk < kPgK; kk += 4) {
+      Acc a[2], b[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        a[i] = xs[buf][kk + fk][wr * 32 + 16 * i + fr];
+        b[i] = ys[buf][kk + fk][wc * 32 + 16 * i + fr];
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = Mma::mma(a[i], b[j], acc[i][j]);
+    }
+    if (s + 1 < nk) store(buf ^ 1);
+    __syncthreads();
+  }
+  const Acc g = static_cast<Acc>(gamma), c0 = static_cast<Acc>(coef);
+  double part = 0.0;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t gi = row0 + wr * 32 + 16 * i + Mma::row(lane, r), gj = col0 + wc * 32 + 16 * j + fr;
+        if (gi >= m || gj >= m || (prob < 2 && gi == gj)) continue;
+        const Acc base = acc[i][j][r] * g + c0;  // the reference's (f @ gᵀ * gamma + coef)
+        Acc p = base;
+        for (int e = 1; e < degree; ++e) p = p * base;  // ** degree (integer degree >= 1)
+        part += static_cast<double>(p);
+      }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) part += __shfl_xor(part, off, kWave);
+  if (lane == 0) red[wave] = part;
+  __syncthreads();
+  if (tid == 0) {
+    double tot = 0.0;
+#pragma unroll
+    for (int w = 0; w < kPgThreads / kWave; ++w) tot += red[w];
+    atomicAdd(sums + prob, tot);
+  }
+}
+
+// [3] fp64: Σ_{i != j} k(r_i, r_j), Σ_{i != j} k(f_i, f_j), Σ k(r_i, f_j) over the subsets real[idx_r], fake[idx_f]
+at::Tensor kid_poly_sums(const at::Tensor& real_in, const at::Tensor& fake_in, const at::Tensor& idx_r_in, const at::Tensor& idx_f_in,
+                         int64_t degree, double gamma, double coef) {
+  TORCH_CHECK(real_in.is_cuda() && fake_in.is_cuda(), "kid_poly_sums: expected GPU features");
+  TORCH_CHECK(real_in.dim() == 2 && fake_in.dim() == 2 && real_in.size(1) == fake_in.size(1), "kid_poly_sums: expected [n, d] features");
+  TORCH_CHECK(real_in.scalar_type() == fake_in.scalar_type(), "kid_poly_sums: dtype mismatch");
+  TORCH_CHECK(idx_r_in.numel() == idx_f_in.numel(), "kid_poly_sums: subsets of different sizes");
+  TORCH_CHECK(degree >= 1, "kid_poly_sums: degree must be >= 1");
+  const at::DeviceGuard guard(real_in.device());
+  auto real = real_in.contiguous();
+  auto fake = fake_in.contiguous();
+  // the kernel gathers rows through the indices: bounds are checked on the host before any launch (a device index
+  // costs one synchronising copy; KernelInceptionDistance passes host randperm slices, as the reference draws them)
+  const at::Tensor hr = idx_r_in.to(at::kCPU, at::kLong).contiguous(), hf = idx_f_in.to(at::kCPU, at::kLong).contiguous();
+  if (hr.numel() > 0) {
+    TORCH_CHECK(hr.min().item<int64_t>() >= 0 && hr.max().item<int64_t>() < real_in.size(0), "kid_poly_sums: real subset index out of range");
+    TORCH_CHECK(hf.min().item<int64_t>() >= 0 && hf.max().item<int64_t>() < fake_in.size(0), "kid_poly_sums: fake subset index out of range");
+  }
+  auto idx_r = hr.to(real.device());
+  auto idx_f = hf.to(real.device());
+  auto sums = at::zeros({3}, real.options().dtype(at::kDouble));
+  const int64_t m = idx_r.numel(), D = real.size(1);
+  if (m == 0 || D == 0) return sums;
+  const int tiles = static_cast<int>((m + kPgT - 1) / kPgT);
+  const int64_t nwg = 3 * static_cast<int64_t>(tiles) * tiles;
+  TORCH_CHECK(nwg < (int64_t(1) << 31), "kid_poly_sums: subset too large");
+  TMX_DISPATCH_FLOAT(real.scalar_type(), "kid_poly_sums", [&] {
+    constexpr bool kF64 = std::is_same<scalar_t, double>::value;
+    using Acc = typename std::conditional<kF64, double, float>::type;
+    constexpr int kpt = pg_k<Acc>() / 4, align = kpt * sizeof(scalar_t) < 16 ? kpt * sizeof(scalar_t) : 16;
+    const auto* rp = reinterpret_cast<const scalar_t*>(real.data_ptr());
+    const auto* fp = reinterpret_cast<const scalar_t*>(fake.data_ptr());
+    const bool vec = D % kpt == 0 && reinterpret_cast<uintptr_t>(rp) % align == 0 && reinterpret_cast<uintptr_t>(fp) % align == 0;
+    if (vec)
+      hipLaunchKernelGGL((kid_poly_kernel<scalar_t, Acc, true>), dim3(static_cast<unsigned>(nwg)), kPgThreads, 0, stream(), rp, fp,
+                         idx_r.data_ptr<int64_t>(), idx_f.data_ptr<int64_t>(), m, D, tiles, static_cast<int>(degree), gamma, coef,
+                         sums.data_ptr<double>());
+    else
+      hipLaunchKernelGGL((kid_poly_kernel<scalar_t, Acc, false>), dim3(static_cast<unsigned>(nwg)), kPgThreads, 0, stream(), rp, fp,
+                         idx_r.data_ptr<int64_t>(), idx_f.data_ptr<int64_t>(), m, D, tiles, static_cast<int>(degree), gamma, coef,
+                         sums.data_ptr<double>());
+  });
+  TMX_LAUNCH_CHECK();
+  return sums;
+}
+
 // ------------------------------------------------------------------------------- FID moments
 // gram += xᵀx and colsum += Σ_b x[b] in fp64 for a feature batch x [B, F] of any float dtype (reference
 // ``image/fid.py``: ``features.double()``, ``sum(dim=0)`` and ``cov_sum.addmm(features.t(), features)`` -- a converted
@@ -654,10 +797,12 @@ TORCH_LIBRARY_FRAGMENT(tmx, m) {
   m.def("pairwise_lp(Tensor x, Tensor y, float p, bool fp64_acc) -> Tensor");
   m.def("pairwise_gemm(Tensor x, Tensor y, int mode, bool zero_diag) -> Tensor");
   m.def("fid_gram_update(Tensor x, Tensor(a!) gram, Tensor(b!) colsum) -> ()");
+  m.def("kid_poly_sums(Tensor real, Tensor fake, Tensor idx_r, Tensor idx_f, int degree, float gamma, float coef) -> Tensor");
 }
 
 TORCH_LIBRARY_IMPL(tmx, CUDA, m) {
   m.impl("pairwise_lp", &tmx::pairwise_lp);
   m.impl("pairwise_gemm", &tmx::pairwise_gemm);
   m.impl("fid_gram_update", &tmx::fid_gram_update);
+  m.impl("kid_poly_sums", &tmx::kid_poly_sums);
 }

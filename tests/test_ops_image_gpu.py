@@ -174,3 +174,52 @@ def test_fid_metric_fused_moments_match_cpu():
             m.update(fake[20 * i:20 * (i + 1)].to(dev), real=False)
         vals.append(m.compute().cpu())
     torch.testing.assert_close(vals[0], vals[1], rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
+@pytest.mark.parametrize(("n", "m", "d", "degree"), [(300, 100, 64, 3), (150, 150, 37, 2), (90, 65, 130, 1)])
+def test_kid_poly_sums_vs_torch(dtype, n, m, d, degree):
+    """Fused KID subset sums (``kid_poly_sums``) against the reference's poly_kernel / maximum_mean_discrepancy terms on
+    the gathered subsets, in fp64."""
+    g = torch.Generator().manual_seed(n + m + d)
+    real = torch.randn(n, d, generator=g).to(dtype).cuda()
+    fake = (torch.randn(n + 7, d, generator=g) + 0.3).to(dtype).cuda()
+    ir, jf = torch.randperm(n, generator=g)[:m], torch.randperm(n + 7, generator=g)[:m]
+    gamma, coef = 1.0 / d, 1.0
+    sums = torch.ops.tmx.kid_poly_sums(real, fake, ir, jf, degree, gamma, coef)
+    a, b = real.double()[ir.cuda()], fake.double()[jf.cuda()]
+    k = lambda x, y: (x @ y.T * gamma + coef) ** degree  # noqa: E731
+    kxx, kyy, kxy = k(a, a), k(b, b), k(a, b)
+    ref = torch.stack([kxx.sum() - kxx.diag().sum(), kyy.sum() - kyy.diag().sum(), kxy.sum()])
+    tol = 1e-10 if dtype == torch.float64 else 2e-5
+    torch.testing.assert_close(sums, ref, rtol=tol, atol=tol * m * m)
+    with pytest.raises(RuntimeError, match="out of range"):
+        torch.ops.tmx.kid_poly_sums(real, fake, torch.tensor([0, n]), torch.tensor([0, 1]), degree, gamma, coef)
+
+
+def test_kid_metric_fused_matches_cpu():
+    """KernelInceptionDistance compute on the GPU (fused subset sums) vs the CPU reference path, same randperm draws."""
+    from torchmetrics_forked_amd.image import KernelInceptionDistance
+
+    class Feat(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            g = torch.Generator().manual_seed(0)
+            self.register_buffer("w", torch.randn(3 * 4, 70, generator=g))
+
+        def forward(self, x):
+            x = torch.nn.functional.adaptive_avg_pool2d(x.float(), 2).flatten(1)
+            return torch.tanh(x / 128.0 - 1.0) @ self.w
+
+    g = torch.Generator().manual_seed(1)
+    real = torch.randint(0, 256, (120, 3, 16, 16), generator=g, dtype=torch.uint8)
+    fake = torch.randint(0, 200, (110, 3, 16, 16), generator=g, dtype=torch.uint8)
+    out = []
+    for dev in ("cuda", "cpu"):
+        m = KernelInceptionDistance(feature=Feat(), subsets=5, subset_size=100).to(dev)
+        m.update(real.to(dev), real=True)
+        m.update(fake.to(dev), real=False)
+        torch.manual_seed(123)
+        out.append([v.cpu() for v in m.compute()])
+    torch.testing.assert_close(out[0][0], out[1][0], rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(out[0][1], out[1][1], rtol=1e-3, atol=1e-5)

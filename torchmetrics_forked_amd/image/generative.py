@@ -219,10 +219,23 @@ class KernelInceptionDistance(Metric):
         if fake.shape[0] < self.subset_size:
             raise ValueError("Argument `subset_size` should be smaller than the number of samples")
         scores = []
-        for _ in range(self.subsets):
-            f_real = real[torch.randperm(real.shape[0])[: self.subset_size]]
-            f_fake = fake[torch.randperm(fake.shape[0])[: self.subset_size]]
-            scores.append(poly_mmd(f_real, f_fake, self.degree, self.gamma, self.coef))
+        if (real.is_cuda and real.is_floating_point() and real.dtype == fake.dtype and real.dim() == 2 and fake.dim() == 2
+                and ops.use_native(real, fake)):
+            # one fused launch per subset (csrc/pairwise.hip kid_poly_sums: the three polynomial-kernel sums, rows
+            # gathered through the subset indices); the subsets come from the same host randperm draws, in the same
+            # order, as the reference's loop
+            m = self.subset_size
+            gamma = self.gamma if self.gamma is not None else 1.0 / real.shape[1]
+            for _ in range(self.subsets):
+                ir = torch.randperm(real.shape[0])[:m]
+                jf = torch.randperm(fake.shape[0])[:m]
+                sums = torch.ops.tmx.kid_poly_sums(real, fake, ir, jf, int(self.degree), float(gamma), float(self.coef))
+                scores.append(((sums[0] + sums[1]) / (m * (m - 1)) - 2 * sums[2] / m**2).to(real.dtype))
+        else:
+            for _ in range(self.subsets):
+                f_real = real[torch.randperm(real.shape[0])[: self.subset_size]]
+                f_fake = fake[torch.randperm(fake.shape[0])[: self.subset_size]]
+                scores.append(poly_mmd(f_real, f_fake, self.degree, self.gamma, self.coef))
         scores_t = torch.stack(scores)
         return scores_t.mean(), scores_t.std(unbiased=False)
 
