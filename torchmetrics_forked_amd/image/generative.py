@@ -5,7 +5,8 @@ FID keeps the reference's fp64 ``sum`` states (feature sum + Gram ``XᵀX``), so
 GPU the update is one fused in-place launch (``fid_gram_update``: fp64 MFMA over the upper tiles, mirrored, plus the
 feature sums, from the raw features -- no fp64 copy, no new F x F matrix).  ``trace(sqrtm(Σ1·Σ2))`` is evaluated through the symmetric
 form ``√Σ1·Σ2·√Σ1`` with two symmetric eigensolvers (``eigh``), which stays on the GPU, instead of the general
-non-symmetric ``eigvals`` of the reference (same eigenvalues)."""
+non-symmetric ``eigvals`` of the reference (same eigenvalues).  KID's compute runs one fused launch per subset
+(``kid_poly_sums``: the three polynomial-kernel sums of ``poly_mmd`` with the subset rows gathered in the kernel)."""
 from copy import deepcopy
 from typing import Any, ClassVar, List, Optional, Sequence, Tuple, Union
 
