@@ -477,13 +477,15 @@ __global__ __launch_bounds__(kPgThreads) void kid_poly_kernel(const T* __restric
   __shared__ Acc ys[2][kPgK][kPgT + kPgPad];
   __shared__ double red[kPgThreads / kWave];
   const int64_t per = static_cast<int64_t>(tiles) * tiles;
-  const int prob = static_cast<int>(blockIdx.x / per);  // 0: real x real, 1: fake x fake, 2: real x fake
+  const int64_t sub = blockIdx.x / (3 * per);  // subset
+  const int prob = static_cast<int>((blockIdx.x / per) % 3);  // 0: real x real, 1: fake x fake, 2: real x fake
   const int64_t t = blockIdx.x % per;
   const int64_t row0 = (t / tiles) * kPgT, col0 = (t % tiles) * kPgT;
   const T* A = prob == 1 ? fake : real;
   const T* B = prob == 0 ? real : fake;
-  const int64_t* ia = prob == 1 ? idx_f : idx_r;
-  const int64_t* ib = prob == 0 ? idx_r : idx_f;
+  const int64_t* ia = (prob == 1 ? idx_f : idx_r) + sub * m;
+  const int64_t* ib = (prob == 0 ? idx_r : idx_f) + sub * m;
+  sums += 3 * sub;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 1, wc = wave & 1;
   const int sr = tid >> 2, sk = (tid & 3) * KPT;
@@ -557,13 +559,13 @@ __global__ __launch_bounds__(kPgThreads) void kid_poly_kernel(const T* __restric
   }
 }
 
-// [3] fp64: Σ_{i != j} k(r_i, r_j), Σ_{i != j} k(f_i, f_j), Σ k(r_i, f_j) over the subsets real[idx_r], fake[idx_f]
+// [S, 3] fp64 per subset s: Σ_{i != j} k(r_i, r_j), Σ_{i != j} k(f_i, f_j), Σ k(r_i, f_j) over real[idx_r[s]],
+// fake[idx_f[s]] (idx [S, m], or [m] for one subset -> [3]); every subset in one launch
 at::Tensor kid_poly_sums(const at::Tensor& real_in, const at::Tensor& fake_in, const at::Tensor& idx_r_in, const at::Tensor& idx_f_in,
                          int64_t degree, double gamma, double coef) {
   TORCH_CHECK(real_in.is_cuda() && fake_in.is_cuda(), "kid_poly_sums: expected GPU features");
   TORCH_CHECK(real_in.dim() == 2 && fake_in.dim() == 2 && real_in.size(1) == fake_in.size(1), "kid_poly_sums: expected [n, d] features");
   TORCH_CHECK(real_in.scalar_type() == fake_in.scalar_type(), "kid_poly_sums: dtype mismatch");
-  TORCH_CHECK(idx_r_in.numel() == idx_f_in.numel(), "kid_poly_sums: subsets of different sizes");
   TORCH_CHECK(degree >= 1, "kid_poly_sums: degree must be >= 1");
   const at::DeviceGuard guard(real_in.device());
   auto real = real_in.contiguous();
@@ -577,11 +579,13 @@ at::Tensor kid_poly_sums(const at::Tensor& real_in, const at::Tensor& fake_in, c
   }
   auto idx_r = hr.to(real.device());
   auto idx_f = hf.to(real.device());
-  auto sums = at::zeros({3}, real.options().dtype(at::kDouble));
-  const int64_t m = idx_r.numel(), D = real.size(1);
-  if (m == 0 || D == 0) return sums;
+  TORCH_CHECK(idx_r_in.dim() <= 2 && idx_r_in.sizes() == idx_f_in.sizes(), "kid_poly_sums: index shapes differ");
+  const bool batched = idx_r_in.dim() == 2;
+  const int64_t S = batched ? idx_r_in.size(0) : 1, m = batched ? idx_r_in.size(1) : idx_r_in.numel(), D = real.size(1);
+  auto sums = at::zeros(batched ? at::IntArrayRef{S, 3} : at::IntArrayRef{3}, real.options().dtype(at::kDouble));
+  if (m == 0 || D == 0 || S == 0) return sums;
   const int tiles = static_cast<int>((m + kPgT - 1) / kPgT);
-  const int64_t nwg = 3 * static_cast<int64_t>(tiles) * tiles;
+  const int64_t nwg = 3 * S * static_cast<int64_t>(tiles) * tiles;
   TORCH_CHECK(nwg < (int64_t(1) << 31), "kid_poly_sums: subset too large");
   TMX_DISPATCH_FLOAT(real.scalar_type(), "kid_poly_sums", [&] {
     constexpr bool kF64 = std::is_same<scalar_t, double>::value;

@@ -193,6 +193,13 @@ def test_kid_poly_sums_vs_torch(dtype, n, m, d, degree):
     ref = torch.stack([kxx.sum() - kxx.diag().sum(), kyy.sum() - kyy.diag().sum(), kxy.sum()])
     tol = 1e-10 if dtype == torch.float64 else 2e-5
     torch.testing.assert_close(sums, ref, rtol=tol, atol=tol * m * m)
+    # several subsets in one launch: row s equals the single-subset call on subset s
+    ir2 = torch.stack([ir, torch.randperm(n, generator=g)[:m]])
+    jf2 = torch.stack([jf, torch.randperm(n + 7, generator=g)[:m]])
+    many = torch.ops.tmx.kid_poly_sums(real, fake, ir2, jf2, degree, gamma, coef)
+    assert many.shape == (2, 3)
+    torch.testing.assert_close(many[0], sums, rtol=1e-12, atol=0)
+    torch.testing.assert_close(many[1], torch.ops.tmx.kid_poly_sums(real, fake, ir2[1], jf2[1], degree, gamma, coef), rtol=1e-12, atol=0)
     with pytest.raises(RuntimeError, match="out of range"):
         torch.ops.tmx.kid_poly_sums(real, fake, torch.tensor([0, n]), torch.tensor([0, 1]), degree, gamma, coef)
 

@@ -20,12 +20,10 @@ def main() -> None:
     m, subsets = 1000, 100
 
     def fused():
-        out = []
-        for _ in range(subsets):
-            ir, jf = torch.randperm(2000)[:m], torch.randperm(2000)[:m]
-            s = torch.ops.tmx.kid_poly_sums(real, fake, ir, jf, 3, 1.0 / 2048, 1.0)
-            out.append((s[0] + s[1]) / (m * (m - 1)) - 2 * s[2] / m**2)
-        return torch.stack(out).mean()
+        draws = [(torch.randperm(2000)[:m], torch.randperm(2000)[:m]) for _ in range(subsets)]
+        s = torch.ops.tmx.kid_poly_sums(real, fake, torch.stack([d[0] for d in draws]), torch.stack([d[1] for d in draws]),
+                                        3, 1.0 / 2048, 1.0)
+        return ((s[:, 0] + s[:, 1]) / (m * (m - 1)) - 2 * s[:, 2] / m**2).mean()
 
     def composed():
         out = []

@@ -5,7 +5,7 @@ FID keeps the reference's fp64 ``sum`` states (feature sum + Gram ``XᵀX``), so
 GPU the update is one fused in-place launch (``fid_gram_update``: fp64 MFMA over the upper tiles, mirrored, plus the
 feature sums, from the raw features -- no fp64 copy, no new F x F matrix).  ``trace(sqrtm(Σ1·Σ2))`` is evaluated through the symmetric
 form ``√Σ1·Σ2·√Σ1`` with two symmetric eigensolvers (``eigh``), which stays on the GPU, instead of the general
-non-symmetric ``eigvals`` of the reference (same eigenvalues).  KID's compute runs one fused launch per subset
+non-symmetric ``eigvals`` of the reference (same eigenvalues).  KID's compute runs every subset in one fused launch
 (``kid_poly_sums``: the three polynomial-kernel sums of ``poly_mmd`` with the subset rows gathered in the kernel)."""
 from copy import deepcopy
 from typing import Any, ClassVar, List, Optional, Sequence, Tuple, Union
@@ -222,16 +222,16 @@ class KernelInceptionDistance(Metric):
         scores = []
         if (real.is_cuda and real.is_floating_point() and real.dtype == fake.dtype and real.dim() == 2 and fake.dim() == 2
                 and ops.use_native(real, fake)):
-            # one fused launch per subset (csrc/pairwise.hip kid_poly_sums: the three polynomial-kernel sums, rows
-            # gathered through the subset indices); the subsets come from the same host randperm draws, in the same
-            # order, as the reference's loop
+            # every subset in one fused launch (csrc/pairwise.hip kid_poly_sums: the three polynomial-kernel sums per
+            # subset, rows gathered through the subset indices); the subsets are the same host randperm draws, in the
+            # same order, as the reference's loop
             m = self.subset_size
             gamma = self.gamma if self.gamma is not None else 1.0 / real.shape[1]
-            for _ in range(self.subsets):
-                ir = torch.randperm(real.shape[0])[:m]
-                jf = torch.randperm(fake.shape[0])[:m]
-                sums = torch.ops.tmx.kid_poly_sums(real, fake, ir, jf, int(self.degree), float(gamma), float(self.coef))
-                scores.append(((sums[0] + sums[1]) / (m * (m - 1)) - 2 * sums[2] / m**2).to(real.dtype))
+            draws = [(torch.randperm(real.shape[0])[:m], torch.randperm(fake.shape[0])[:m]) for _ in range(self.subsets)]
+            ir = torch.stack([d[0] for d in draws])
+            jf = torch.stack([d[1] for d in draws])
+            sums = torch.ops.tmx.kid_poly_sums(real, fake, ir, jf, int(self.degree), float(gamma), float(self.coef))
+            scores = list(((sums[:, 0] + sums[:, 1]) / (m * (m - 1)) - 2 * sums[:, 2] / m**2).to(real.dtype))
         else:
             for _ in range(self.subsets):
                 f_real = real[torch.randperm(real.shape[0])[: self.subset_size]]
