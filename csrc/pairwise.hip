@@ -134,7 +134,7 @@ at::Tensor pairwise_lp(const at::Tensor& x_in, const at::Tensor& y_in, double p,
 // exact fp32 products, or v_mfma_f64_16x16x4_f64).  Row norms are summed from the staging registers (no extra pass),
 // the epilogue runs on the accumulators and writes the input dtype once.  Tile ids are remapped so that consecutive
 // ids (same x rows) share an XCD and its L2.
-enum PgMode : int { kPgLinear = 0, kPgCosine = 1, kPgEuclid = 2 };
+enum PgMode : int { kPgLinear = 0, kPgCosine = 1, kPgEuclid = 2, kPgAbsCosMax = 3 };  // 3: MiFID's row max |cos|
 constexpr int kPgT = 64, kPgPad = 16, kPgThreads = 256;
 // slice depth: 32 (fp32) / 16 (fp64) -- 40 KiB of double-buffered LDS either way, three workgroups per CU
 template <typename Acc> constexpr int pg_k() { return std::is_same<Acc, double>::value ? 16 : 32; }
@@ -198,7 +198,8 @@ __device__ __forceinline__ void pg_load(const T* __restrict__ p, int64_t row, in
 
 template <typename T, typename Acc, int MODE, bool VEC>
 __global__ __launch_bounds__(kPgThreads) void pairwise_gemm_kernel(const T* __restrict__ x, const T* __restrict__ y, int64_t N, int64_t M,
-                                                                   int64_t D, int tiles_n, bool zero_diag, T* __restrict__ out) {
+                                                                   int64_t D, int tiles_n, bool zero_diag, T* __restrict__ out,
+                                                                   void* __restrict__ rowmax = nullptr) {
   using Mma = PgMma<Acc>;
   constexpr int kPgK = pg_k<Acc>(), KPT = kPgK / 4;
   __shared__ Acc xs[2][kPgK][kPgT + kPgPad];
@@ -273,10 +274,32 @@ __global__ __launch_bounds__(kPgThreads) void pairwise_gemm_kernel(const T* __re
     py += __shfl_xor(py, 1, kWave);
     py += __shfl_xor(py, 2, kWave);
     if ((tid & 3) == 0) {  // cosine keeps reciprocal norms: the epilogue is two multiplies per output
-      nrm[0][sr] = MODE == kPgCosine ? Acc(1) / sqrt(px) : px;
-      nrm[1][sr] = MODE == kPgCosine ? Acc(1) / sqrt(py) : py;
+      nrm[0][sr] = MODE == kPgCosine || MODE == kPgAbsCosMax ? Acc(1) / sqrt(px) : px;
+      nrm[1][sr] = MODE == kPgCosine || MODE == kPgAbsCosMax ? Acc(1) / sqrt(py) : py;
     }
     __syncthreads();
+  }
+  if constexpr (MODE == kPgAbsCosMax) {
+    // row maxima of |cos|: the lane's two columns, then the 16 lanes of a row (col = lane & 15 in both C/D maps),
+    // one order-preserving integer atomicMax per (row, wave) -- non-negative floats order as their bit patterns
+    using Bits = typename std::conditional<std::is_same<Acc, double>::value, unsigned long long, unsigned int>::type;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int lr = wr * 32 + 16 * i + Mma::row(lane, r);
+        const int64_t gi = row0 + lr;
+        Acc mv = Acc(-1);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int lc = wc * 32 + 16 * j + fr;
+          if (gi < N && col0 + lc < M) mv = fmax(mv, fabs(acc[i][j][r] * nrm[0][lr] * nrm[1][lc]));
+        }
+#pragma unroll
+        for (int off = 1; off < 16; off <<= 1) mv = fmax(mv, __shfl_xor(mv, off, kWave));
+        if (fr == 0 && gi < N && mv >= Acc(0)) atomicMax(reinterpret_cast<Bits*>(rowmax) + gi, __builtin_bit_cast(Bits, mv));
+      }
+    return;
   }
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -763,6 +786,40 @@ void fid_gram_update(const at::Tensor& x_in, at::Tensor gram, at::Tensor colsum)
   TMX_LAUNCH_CHECK();
 }
 
+// MiFID's memorization term: for every row of x the largest |cos| against the rows of y (fp32, fp64 for fp64 inputs),
+// without the N x M similarity matrix (reference ``image/mifid.py``: normalise, n1 @ n2ᵀ, abs, min of 1 - |cos|)
+at::Tensor pairwise_abs_cos_rowmax(const at::Tensor& x_in, const at::Tensor& y_in) {
+  TORCH_CHECK(x_in.is_cuda() && y_in.is_cuda(), "pairwise_abs_cos_rowmax: expected GPU tensors");
+  TORCH_CHECK(x_in.dim() == 2 && y_in.dim() == 2 && x_in.size(1) == y_in.size(1), "pairwise_abs_cos_rowmax: expected [N,d] and [M,d]");
+  TORCH_CHECK(x_in.scalar_type() == y_in.scalar_type(), "pairwise_abs_cos_rowmax: dtype mismatch");
+  TORCH_CHECK(y_in.size(0) > 0 && x_in.size(1) > 0, "pairwise_abs_cos_rowmax: empty operand");
+  const at::DeviceGuard guard(x_in.device());
+  auto x = x_in.contiguous();
+  auto y = y_in.contiguous();
+  const bool f64 = x.scalar_type() == at::kDouble;
+  auto out = at::zeros({x.size(0)}, x.options().dtype(f64 ? at::kDouble : at::kFloat));
+  if (x.size(0) == 0) return out;
+  const int64_t N = x.size(0), M = y.size(0), D = x.size(1);
+  const int64_t tiles_m = (N + kPgT - 1) / kPgT, tiles_n = (M + kPgT - 1) / kPgT, nwg = tiles_m * tiles_n;
+  TORCH_CHECK(nwg < (int64_t(1) << 31), "pairwise_abs_cos_rowmax: too large");
+  TMX_DISPATCH_FLOAT(x.scalar_type(), "pairwise_abs_cos_rowmax", [&] {
+    constexpr bool kF64 = std::is_same<scalar_t, double>::value;
+    using Acc = typename std::conditional<kF64, double, float>::type;
+    constexpr int kpt = pg_k<Acc>() / 4, align = kpt * sizeof(scalar_t) < 16 ? kpt * sizeof(scalar_t) : 16;
+    const auto* xp = reinterpret_cast<const scalar_t*>(x.data_ptr());
+    const auto* yp = reinterpret_cast<const scalar_t*>(y.data_ptr());
+    const bool vec = D % kpt == 0 && reinterpret_cast<uintptr_t>(xp) % align == 0 && reinterpret_cast<uintptr_t>(yp) % align == 0;
+    if (vec)
+      hipLaunchKernelGGL((pairwise_gemm_kernel<scalar_t, Acc, kPgAbsCosMax, true>), dim3(static_cast<unsigned>(nwg)), kPgThreads, 0, stream(),
+                         xp, yp, N, M, D, static_cast<int>(tiles_n), false, static_cast<scalar_t*>(nullptr), out.data_ptr());
+    else
+      hipLaunchKernelGGL((pairwise_gemm_kernel<scalar_t, Acc, kPgAbsCosMax, false>), dim3(static_cast<unsigned>(nwg)), kPgThreads, 0, stream(),
+                         xp, yp, N, M, D, static_cast<int>(tiles_n), false, static_cast<scalar_t*>(nullptr), out.data_ptr());
+  });
+  TMX_LAUNCH_CHECK();
+  return out;
+}
+
 // [N, M] in the input dtype; mode 0 linear, 1 cosine, 2 euclidean (fp64 accumulation, as the reference)
 at::Tensor pairwise_gemm(const at::Tensor& x_in, const at::Tensor& y_in, int64_t mode, bool zero_diag) {
   TORCH_CHECK(x_in.is_cuda() && y_in.is_cuda(), "pairwise_gemm: expected GPU tensors");
@@ -801,6 +858,7 @@ TORCH_LIBRARY_FRAGMENT(tmx, m) {
   m.def("pairwise_lp(Tensor x, Tensor y, float p, bool fp64_acc) -> Tensor");
   m.def("pairwise_gemm(Tensor x, Tensor y, int mode, bool zero_diag) -> Tensor");
   m.def("fid_gram_update(Tensor x, Tensor(a!) gram, Tensor(b!) colsum) -> ()");
+  m.def("pairwise_abs_cos_rowmax(Tensor x, Tensor y) -> Tensor");
   m.def("kid_poly_sums(Tensor real, Tensor fake, Tensor idx_r, Tensor idx_f, int degree, float gamma, float coef) -> Tensor");
 }
 
@@ -809,4 +867,5 @@ TORCH_LIBRARY_IMPL(tmx, CUDA, m) {
   m.impl("pairwise_gemm", &tmx::pairwise_gemm);
   m.impl("fid_gram_update", &tmx::fid_gram_update);
   m.impl("kid_poly_sums", &tmx::kid_poly_sums);
+  m.impl("pairwise_abs_cos_rowmax", &tmx::pairwise_abs_cos_rowmax);
 }

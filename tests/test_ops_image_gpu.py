@@ -230,3 +230,31 @@ def test_kid_metric_fused_matches_cpu():
         out.append([v.cpu() for v in m.compute()])
     torch.testing.assert_close(out[0][0], out[1][0], rtol=1e-4, atol=1e-5)
     torch.testing.assert_close(out[0][1], out[1][1], rtol=1e-3, atol=1e-5)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64, torch.bfloat16])
+@pytest.mark.parametrize(("n", "m", "d"), [(300, 200, 64), (70, 130, 33), (1, 5, 8), (257, 64, 100)])
+def test_pairwise_abs_cos_rowmax_vs_torch(dtype, n, m, d):
+    """MiFID's memorization term: row maxima of |cos| from the fused kernel vs the normalise / matmul / abs / max
+    composition in fp64."""
+    g = torch.Generator().manual_seed(n + m + d)
+    x = torch.randn(n, d, generator=g).to(dtype).cuda()
+    y = torch.randn(m, d, generator=g).to(dtype).cuda()
+    got = torch.ops.tmx.pairwise_abs_cos_rowmax(x, y)
+    xd, yd = x.double(), y.double()
+    ref = ((xd / xd.norm(dim=1, keepdim=True)) @ (yd / yd.norm(dim=1, keepdim=True)).T).abs().max(dim=1).values
+    tol = 1e-12 if dtype == torch.float64 else 2e-6
+    torch.testing.assert_close(got.double(), ref, rtol=tol, atol=tol)
+
+
+def test_mifid_cosine_distance_fused_matches_cpu():
+    from torchmetrics_forked_amd.image.generative import _compute_cosine_distance
+
+    g = torch.Generator().manual_seed(3)
+    a = torch.randn(500, 96, generator=g)
+    b = a[:400] + 0.05 * torch.randn(400, 96, generator=g)  # near-duplicates: a small memorization distance
+    a[7] = 0.0  # a zero-sum row is dropped on both paths
+    for eps in (0.1, 0.5):
+        gpu = _compute_cosine_distance(a.cuda(), b.cuda(), eps).cpu()
+        cpu = _compute_cosine_distance(a, b, eps)
+        torch.testing.assert_close(gpu, cpu, rtol=1e-5, atol=1e-6)
