@@ -22,6 +22,7 @@ for s in "$@"; do
     kexppmc) run kexppmc 120 rocprofv3 --kernel-trace --pmc ${TMX_PMC:-SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU} -d "$OUT/kexppmc" -o pmc --output-format csv -- ./build/kexp_r5/${TMX_KEXP:-exp} ;;
     host) run host 120 python tools/host_overhead_probe.py ;;
     fidprof) run fidprof 200 rocprofv3 --kernel-trace --stats -d "$OUT/fidprof" -o fid --output-format csv -- python3 tools/fid_gram_bench.py ;;
+    mifid) run mifid_bench 200 python tools/mifid_bench.py; tail -1 "$OUT/mifid_bench.log" ;;
     kid) run kid_bench 200 python tools/kid_bench.py; tail -1 "$OUT/kid_bench.log" ;;
     fidg) run fid_gram_bench 200 python tools/fid_gram_bench.py; tail -1 "$OUT/fid_gram_bench.log" ;;
     pw) run pairwise_bench 300 python tools/pairwise_bench.py; tail -1 "$OUT/pairwise_bench.log" ;;

@@ -293,11 +293,23 @@ class InceptionScore(Metric):
         return self._plot(val, ax)
 
 
+def _rowmax_fused_wins(f1: Tensor, f2: Tensor) -> bool:
+    """The fused row-max kernel multiplies on fp32 (fp64) MFMA tiles: it wins while the launches and the N x M
+    round trips dominate, hipBLASLt's GEMM beyond (10,000 x 10,000 x 2048 fp32: 4.7 vs 3.9 ms,
+    ``profiles/mifid_rowmax_r5.json``) -- the pairwise cosine crossover."""
+    work = f1.shape[0] * f2.shape[0] * f1.shape[1]
+    if f1.dtype == torch.float64:
+        return work <= (1 << 29) and f1.shape[1] <= 256
+    if f1.dtype in (torch.bfloat16, torch.float16):
+        return work <= (1 << 29)
+    return work < (1 << 32) and f1.shape[1] <= 1024
+
+
 def _compute_cosine_distance(features1: Tensor, features2: Tensor, cosine_distance_eps: float = 0.1) -> Tensor:
     f1 = features1[torch.sum(features1, dim=1) != 0]
     f2 = features2[torch.sum(features2, dim=1) != 0]
     if (f1.is_cuda and f1.is_floating_point() and f1.dtype == f2.dtype and f1.dim() == 2 and f2.shape[0] > 0
-            and f1.shape[1] > 0 and ops.use_native(f1, f2)):
+            and f1.shape[1] > 0 and _rowmax_fused_wins(f1, f2) and ops.use_native(f1, f2)):
         # one fused launch: the row maxima of |cos| without the N x M similarity matrix (csrc/pairwise.hip)
         mean_min_d = torch.mean(1.0 - torch.ops.tmx.pairwise_abs_cos_rowmax(f1, f2)).to(f1.dtype)
     else:
