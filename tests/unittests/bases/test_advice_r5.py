@@ -1,0 +1,103 @@
+"""Round-5 advisor findings.
+
+* The sum-state forward fast path merges the batch state out of place: members of a compute group share the leader's
+  state tensors, so an in-place merge counted each forward batch once per member.
+* The out-of-place merge keeps the reference's type promotion (``global + local``).
+* FID feature widths above the fused Gram kernel's limit take the ATen path.
+* The fused MiFID row maximum propagates NaN like the reference's ``min``.
+* The batched mAP update refuses columns with mixed dtypes.
+"""
+import pytest
+import torch
+
+from torchmetrics_forked_amd import MetricCollection
+from torchmetrics_forked_amd.classification import BinaryPrecision, BinaryRecall, BinaryF1Score
+from torchmetrics_forked_amd.regression import MeanSquaredError, MeanAbsoluteError
+
+
+def _bin(seed, n=50):
+    g = torch.Generator().manual_seed(seed)
+    return torch.rand(n, generator=g), torch.randint(0, 2, (n,), generator=g)
+
+
+@pytest.mark.parametrize("groups", [True, [["p", "r", "f"]]])
+def test_compute_group_forward_counts_each_batch_once(groups):
+    coll = MetricCollection({"p": BinaryPrecision(), "r": BinaryRecall(), "f": BinaryF1Score()}, compute_groups=groups)
+    ref = {"p": BinaryPrecision(), "r": BinaryRecall(), "f": BinaryF1Score()}
+    for s in range(5):
+        p, t = _bin(s)
+        out = coll(p, t)
+        for k, m in ref.items():
+            torch.testing.assert_close(out[k], m(p, t))
+    res = coll.compute()
+    for k, m in ref.items():
+        torch.testing.assert_close(res[k], m.compute())
+
+
+def test_compute_group_forward_regression_after_merge():
+    coll = MetricCollection([MeanSquaredError(), MeanAbsoluteError()], compute_groups=True)
+    mse, mae = MeanSquaredError(), MeanAbsoluteError()
+    g = torch.Generator().manual_seed(0)
+    x, y = torch.randn(40, generator=g), torch.randn(40, generator=g)
+    coll.update(x, y)
+    mse.update(x, y)
+    mae.update(x, y)
+    for s in range(4):
+        x, y = torch.randn(40, generator=g), torch.randn(40, generator=g)
+        coll(x, y)
+        mse(x, y)
+        mae(x, y)
+    res = coll.compute()
+    torch.testing.assert_close(res["MeanSquaredError"], mse.compute())
+    torch.testing.assert_close(res["MeanAbsoluteError"], mae.compute())
+
+
+def test_forward_merge_promotes_like_reference():
+    from torchmetrics_forked_amd import Metric
+
+    class Promote(Metric):
+        full_state_update = False
+
+        def __init__(self):
+            super().__init__()
+            self.add_state("s", torch.tensor(0), dist_reduce_fx="sum")
+
+        def update(self, x):
+            self.s = self.s + x.sum()  # rebinds the int64 state to float
+
+        def compute(self):
+            return self.s
+
+    m = Promote()
+    m(torch.tensor([1.5, 2.0]))
+    out = m(torch.tensor([0.25]))
+    assert out.dtype == torch.float32
+    torch.testing.assert_close(m.compute(), torch.tensor(3.75))
+
+
+def test_fid_wide_features_route_to_aten():
+    from torchmetrics_forked_amd.image import generative
+
+    cond = generative._gram_kernel_ok
+    assert not cond(torch.empty(4, 16385))
+    assert not cond(torch.empty(4, 128))
+    assert cond(torch.empty(4, 2048))
+    assert cond(torch.empty(4, 16384))
+
+
+def test_map_batched_update_refuses_mixed_dtypes():
+    from torchmetrics_forked_amd.detection import MeanAveragePrecision
+
+    m = MeanAveragePrecision()
+    preds = [
+        {"boxes": torch.tensor([[0.0, 0.0, 10.0, 10.0]]), "scores": torch.tensor([0.9]), "labels": torch.tensor([1], dtype=torch.int32)},
+        {"boxes": torch.tensor([[5.0, 5.0, 20.0, 20.0]]), "scores": torch.tensor([0.8]), "labels": torch.tensor([1])},
+    ]
+    target = [
+        {"boxes": torch.tensor([[0.0, 0.0, 10.0, 10.0]]), "labels": torch.tensor([1])},
+        {"boxes": torch.tensor([[5.0, 5.0, 20.0, 20.0]]), "labels": torch.tensor([1])},
+    ]
+    assert m._update_batched(preds, target) is False
+    m.update(preds, target)
+    assert m.detection_labels[0].dtype == torch.int32
+    assert m.detection_labels[1].dtype == torch.int64

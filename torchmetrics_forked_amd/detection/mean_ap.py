@@ -196,6 +196,10 @@ class MeanAveragePrecision(Metric):
             gn = [t.shape[0] for t in gl]
             if dn != [t.shape[0] for t in db] or dn != [t.shape[0] for t in ds] or gn != [t.shape[0] for t in gb] or 0 in dn or 0 in gn:
                 return False
+            # one dtype per column: a concatenation would promote mixed images, where the per-image path (and the
+            # reference) keeps each image's own tensors
+            if any(len({t.dtype for t in col}) != 1 for col in (db, ds, dl, gb, gl)):
+                return False
             flats = [torch.cat(col) for col in (db, ds, dl, gb, gl)]
             crowd = torch.cat([t["iscrowd"] for t in target]) if n_crowd else None
             area = torch.cat([t["area"] for t in target]) if n_area else None

@@ -44,11 +44,19 @@ def _sqrtm_psd(mat: Tensor) -> Tensor:
     return (v * w.clamp(min=0).sqrt().unsqueeze(0)) @ v.T
 
 
+_GRAM_MAX_FEATURES = 16384  # csrc/pairwise.hip fid_gram_update's TORCH_CHECK
+
+
+def _gram_kernel_ok(features: Tensor) -> bool:
+    """Feature widths the fused Gram kernel takes: below 256 the triangle holds too few 64 x 64 tiles to fill the GPU
+    (0.8x at 512 x 192 fp32), above 16384 the kernel refuses the width."""
+    return features.dim() == 2 and 256 <= features.shape[1] <= _GRAM_MAX_FEATURES
+
+
 def _fused_moments(features: Tensor, gram: Tensor, fsum: Tensor) -> bool:
     """``csrc/pairwise.hip`` ``fid_gram_update`` for GPU float features into contiguous fp64 states on their device
     (``profiles/fid_gram_r5.json``); otherwise the reference's ``double()`` + ``sum`` + ``addmm``."""
-    # (below 256 features the triangle holds too few 64 x 64 tiles to fill the GPU: 0.8x at 512 x 192 fp32)
-    return (features.is_cuda and features.is_floating_point() and features.dim() == 2 and features.shape[1] >= 256
+    return (features.is_cuda and features.is_floating_point() and _gram_kernel_ok(features)
             and gram.dtype == torch.float64
             and fsum.dtype == torch.float64 and gram.device == features.device and fsum.device == features.device
             and gram.is_contiguous() and fsum.is_contiguous() and ops.use_native(features, gram, fsum))
@@ -221,10 +229,12 @@ class KernelInceptionDistance(Metric):
             raise ValueError("Argument `subset_size` should be smaller than the number of samples")
         scores = []
         if (real.is_cuda and real.is_floating_point() and real.dtype == fake.dtype and real.dim() == 2 and fake.dim() == 2
-                and ops.use_native(real, fake)):
+                and not torch.are_deterministic_algorithms_enabled() and ops.use_native(real, fake)):
             # every subset in one fused launch (csrc/pairwise.hip kid_poly_sums: the three polynomial-kernel sums per
             # subset, rows gathered through the subset indices); the subsets are the same host randperm draws, in the
-            # same order, as the reference's loop
+            # same order, as the reference's loop.  The per-workgroup partials are combined by fp64 atomics, so the
+            # last bits of a score can differ between runs (the reference's reduction order is fixed); under
+            # torch.use_deterministic_algorithms(True) the reference's loop runs instead
             m = self.subset_size
             gamma = self.gamma if self.gamma is not None else 1.0 / real.shape[1]
             draws = [(torch.randperm(real.shape[0])[:m], torch.randperm(fake.shape[0])[:m]) for _ in range(self.subsets)]
@@ -312,6 +322,10 @@ def _compute_cosine_distance(features1: Tensor, features2: Tensor, cosine_distan
             and f1.shape[1] > 0 and _rowmax_fused_wins(f1, f2) and ops.use_native(f1, f2)):
         # one fused launch: the row maxima of |cos| without the N x M similarity matrix (csrc/pairwise.hip)
         mean_min_d = torch.mean(1.0 - torch.ops.tmx.pairwise_abs_cos_rowmax(f1, f2)).to(f1.dtype)
+        # the kernel's fmax skips NaN cosines; the reference's ``min`` propagates them (any non-finite feature makes a
+        # NaN row or column): restore that without a host sync
+        finite = torch.isfinite(f1).all() & torch.isfinite(f2).all()
+        mean_min_d = torch.where(finite, mean_min_d, torch.full_like(mean_min_d, float("nan")))
     else:
         n1 = f1 / torch.norm(f1, dim=1, keepdim=True)
         n2 = f2 / torch.norm(f2, dim=1, keepdim=True)

@@ -395,9 +395,10 @@ class Metric(Module, ABC):
             d["_update_count"] = count + 1
             batch = [d[n] for n in names]  # (an update may have rebound a state rather than added into it)
             with torch.no_grad():
-                # in place, as update() itself accumulates (the fused stat-score / confusion-matrix updates add into
-                # the state tensors): one foreach call, no new global tensors
-                torch._foreach_add_(glob, batch)
+                # out of place, as the reference's ``global + local`` (metric.py:_reduce_states): a compute group's
+                # members share the leader's state tensors, so an in-place merge would add each batch once per member;
+                # the new tensors also take the reference's type promotion (int64 state + float batch -> float)
+                glob = torch._foreach_add(glob, batch)
             for n, g in zip(names, glob):
                 d[n] = g
             # keep the batch states for the next forward when they are zero-defaulted and the batch value does not
