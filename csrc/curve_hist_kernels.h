@@ -226,6 +226,60 @@ template <> __device__ __forceinline__ uint32_t pack_rne2<__half>(f32x2 q) {
   return __builtin_amdgcn_perm(rne_word<__half>(q.y), rne_word<__half>(q.x), 0x07060302u);
 }
 
+// exp_nonpos2 for pairs of rows whose every element is within 86 of its maximum (see row_tile_softmax_lean)
+__device__ __forceinline__ f32x2 exp_nonpos2_narrow(f32x2 x) {
+#pragma clang fp contract(off)
+  const float hi_s = __uint_as_float(0x3fb8aa3bu), lo_s = __uint_as_float(0x32a5705fu), magic = 12582912.f;
+  const f32x2 log2e_hi = {hi_s, hi_s}, log2e_lo = {lo_s, lo_s}, m2 = {magic, magic};
+  const f32x2 ph = x * log2e_hi;
+  f32x2 pl = __builtin_elementwise_fma(x, log2e_hi, -ph);
+  const f32x2 s = ph + m2;  // low bits: rint(ph)
+  const f32x2 e = s - m2;   // rint(ph), exact
+  pl = __builtin_elementwise_fma(x, log2e_lo, pl);
+  const f32x2 t = (ph - e) + pl;
+  const uint32_t ra = __float_as_uint(__builtin_amdgcn_exp2f(t.x)), rb = __float_as_uint(__builtin_amdgcn_exp2f(t.y));
+  return f32x2{__uint_as_float(ra + (__float_as_uint(s.x) << 23)), __uint_as_float(rb + (__float_as_uint(s.y) << 23))};
+}
+
+// ---- fast softmax with verified quotients (round 6) -----------------------------------------------------------------
+// A softmax code is DEFINED as RNE16(div_rn(exp_nonpos(x - max), s)): the correctly rounded quotient of expf's exact
+// instruction sequence (what ATen's softmax stores before its 16-bit rounding) by the row sum s.  Since round 6 s is
+// the fixed-order sum of FAST exponentials e_f(x) = v_exp_f32(fma(x, log2e, -RN(max log2e))) -- one fma and one
+// v_exp per element instead of the 9-instruction exact sequence; it differs from the sum of exact exps in the last
+// bits only (the fp32 summation order already differs from ATen's).  The refit and every row pass store and reuse
+// the same s (row_stats), so all routes still produce the same codes for one batch.
+// The quotient of the common case (bf16, every element within 86 of its row maximum) is taken FAST and VERIFIED:
+// with r = 1 / s (correctly rounded), the exact quotient lies in [e_f r (1 - eps), e_f r (1 + eps)] where
+//   |t_f - d log2e| <= 2^-24 log2e (3 |d| + |max|)        (t_f = fma(x, L, -RN(max L)), L = RN(log2e), d = x - max)
+//   -> |e_f / exp(d) - 1| <= 2^-24 (3 |d| + |max|) + v_exp_f32's 1 ulp, |exp_nonpos(d) / exp(d) - 1| <= 1 ulp,
+//      |r s - 1| <= 2^-24, the roundings of r (1 -+ eps) <= 2^-24 each,
+// so eps = 2^-24 (3 (max - lane min) + |max| + 16) bounds it with room to spare.  RNE16 and fp32 rounding are
+// monotone: when RNE16(fl(e_f r_lo)) == RNE16(fl(e_f r_hi)) the exact quotient rounds to that same code.  Otherwise
+// (about 1e-3 of the bf16 elements of randn logits) the whole wave recomputes that element pair with the exact
+// sequence (a wave-uniform branch).  Per element: fma, v_exp, two multiplies, a conversion and a compare, against
+// the exact sequence's ~14 instructions.  fp16 keeps the exact quotient (its 10-bit codes put 8x as many rounding
+// boundaries in the window).
+constexpr float kLog2eF = 1.44269502163f;  // RN(log2 e) = 0x3fb8aa3b
+__device__ __forceinline__ f32x2 exp_fast2(f32x2 x, f32x2 nml) {
+  const f32x2 t = __builtin_elementwise_fma(x, f32x2{kLog2eF, kLog2eF}, nml);
+  return f32x2{__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)};
+}
+__device__ __forceinline__ float fast_nml(float mx) { return -(mx * kLog2eF); }
+// relative half-width of the verification interval (see above); lane_min: the smallest element this lane holds
+__device__ __forceinline__ float fast_eps(float mx, float lane_min) {
+  return (3.f * (mx - lane_min) + __builtin_fabsf(mx) + 16.f) * 5.9604645e-8f;
+}
+template <typename T> struct FastQuot : std::false_type {};
+template <> struct FastQuot<__hip_bfloat16> : std::true_type {};
+// the code pair of (x.x, x.y): fast and verified, or exact for the whole wave when any lane's pair is undecided
+template <typename T>
+__device__ __forceinline__ uint32_t fast_code2(f32x2 x, f32x2 nml, f32x2 rlo, f32x2 rhi, f32x2 mx2, f32x2 s2, f32x2 i2) {
+  const f32x2 e = exp_fast2(x, nml);
+  const uint32_t lo = pack_rne2<T>(e * rlo), hi = pack_rne2<T>(e * rhi);
+  if (__ballot(lo != hi) == 0) return lo;
+  return pack_rne2<T>(div_rn2(exp_nonpos2_narrow(x - mx2), s2, i2));
+}
+
 // the 16-bit pattern of a score widened to fp32 (exact: bf16 / fp16 -> fp32 is lossless; NaN payloads may be
 // quietened for fp16, and every NaN pattern is a skip code anyway)
 template <typename T> __device__ __forceinline__ uint32_t half_bits(float f);
@@ -576,15 +630,17 @@ __device__ __forceinline__ void row_tile_compute(const RowLoads<NG>& L, int64_t 
     bool fa = __builtin_isfinite(ra.mx), fb = __builtin_isfinite(rb.mx);
     const int ama = row_argmax<NG>(ra), amb = row_argmax<NG>(rb);
     float sa = 0.f, sb = 0.f, ia = 0.f, ib = 0.f;
+    const f32x2 nml = {fast_nml(ra.mx), fast_nml(rb.mx)};
     if constexpr (SOFTMAX) {
       f32x2 acc = {0.f, 0.f};
       const f32x2 mx2 = {ra.mx, rb.mx};
 #pragma unroll
       for (int j = 0; j < 8 * NG; ++j) {
-        const f32x2 e = exp_nonpos2(f32x2{ra.v[j], rb.v[j]} - mx2);
-        ra.v[j] = e.x;
-        rb.v[j] = e.y;
-        acc = acc + e;  // per row: the same sequential fp32 order as before
+        // the row sums of the fast exps, in the lean form's order (padding slots hold -inf: exp2(-inf) adds +0)
+        acc = acc + exp_fast2(f32x2{ra.v[j], rb.v[j]}, nml);
+        const f32x2 ex = exp_nonpos2(f32x2{ra.v[j], rb.v[j]} - mx2);  // exact exps for the quotients
+        ra.v[j] = ex.x;
+        rb.v[j] = ex.y;
       }
       sa = wave_sum_uniform(acc.x);
       sb = wave_sum_uniform(acc.y);
@@ -597,9 +653,8 @@ __device__ __forceinline__ void row_tile_compute(const RowLoads<NG>& L, int64_t 
       fb = fb && __builtin_isfinite(wave_sum_uniform(rb.sum));
       if (row_stats != nullptr) {  // the softmax statistics too, so the class pass can refit a mispredicted batch
         f32x2 acc = {0.f, 0.f};
-        const f32x2 mx2 = {ra.mx, rb.mx};
 #pragma unroll
-        for (int j = 0; j < 8 * NG; ++j) acc = acc + exp_nonpos2(f32x2{ra.v[j], rb.v[j]} - mx2);
+        for (int j = 0; j < 8 * NG; ++j) acc = acc + exp_fast2(f32x2{ra.v[j], rb.v[j]}, nml);
         sa = wave_sum_uniform(acc.x);
         sb = wave_sum_uniform(acc.y);
       }
@@ -677,19 +732,6 @@ __device__ __forceinline__ void row_tile_compute(const RowLoads<NG>& L, int64_t 
 //    pair takes exp_nonpos2, the reference sequence;
 //  * the row minimum is only compared (ballots), never wave-reduced; the probability-mode witnesses are tested only
 //    while the block has not seen one (``rec && !saw_bad``), as before.
-__device__ __forceinline__ f32x2 exp_nonpos2_narrow(f32x2 x) {
-#pragma clang fp contract(off)
-  const float hi_s = __uint_as_float(0x3fb8aa3bu), lo_s = __uint_as_float(0x32a5705fu), magic = 12582912.f;
-  const f32x2 log2e_hi = {hi_s, hi_s}, log2e_lo = {lo_s, lo_s}, m2 = {magic, magic};
-  const f32x2 ph = x * log2e_hi;
-  f32x2 pl = __builtin_elementwise_fma(x, log2e_hi, -ph);
-  const f32x2 s = ph + m2;  // low bits: rint(ph)
-  const f32x2 e = s - m2;   // rint(ph), exact
-  pl = __builtin_elementwise_fma(x, log2e_lo, pl);
-  const f32x2 t = (ph - e) + pl;
-  const uint32_t ra = __float_as_uint(__builtin_amdgcn_exp2f(t.x)), rb = __float_as_uint(__builtin_amdgcn_exp2f(t.y));
-  return f32x2{__uint_as_float(ra + (__float_as_uint(s.x) << 23)), __uint_as_float(rb + (__float_as_uint(s.y) << 23))};
-}
 
 template <typename T, int NG>
 __device__ __forceinline__ void unpack_pair(const uint4& wa, const uint4& wb, f32x2* P) {
@@ -798,9 +840,10 @@ __device__ __forceinline__ void row_tile_softmax_lean(const RowLoads<NG>& L, int
     // exp(x - max): the lean sequence when every element of both rows is within 86 of its maximum (wave-uniform)
     const bool narrow = __ballot(!(mxa - mn_a <= 86.f && mxb - mn_b <= 86.f)) == 0;
     const f32x2 mx2 = {mxa, mxb};
+    const f32x2 nml = {fast_nml(mxa), fast_nml(mxb)};
     f32x2 acc = {0.f, 0.f}, acc_lo = {0.f, 0.f};
     // the partial vector sits in the last class group (nvec - 1 >= 64 when NG == 2): scale its slots by 0 / 1
-    auto counted = [&](int j) -> f32x2 {
+    auto counted = [&](f32x2 e, int j) -> f32x2 {
       if constexpr (UNALIGNED
 #ifdef TMX_UNALIGNED_NOMASK_HACK  // timing experiment only
                     && false
@@ -808,25 +851,16 @@ __device__ __forceinline__ void row_tile_softmax_lean(const RowLoads<NG>& L, int
       ) {
         if (j >= 8 * (NG - 1)) {
           const float m = (j & 7) < (NG == 2 ? cut_hi : cut_lo) ? 1.f : 0.f;
-          return P[j] * f32x2{m, m};
+          return e * f32x2{m, m};
         }
       }
-      return P[j];
+      return e;
     };
-    if (narrow) {
+    // the row sums of the fast exps (the scores stay in P for the quotients)
 #pragma unroll
-      for (int j = 0; j < 8 * NG; ++j) {
-        P[j] = exp_nonpos2_narrow(P[j] - mx2);
-        acc = acc + counted(j);
-        if (j == 7) acc_lo = acc;
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8 * NG; ++j) {
-        P[j] = exp_nonpos2(P[j] - mx2);
-        acc = acc + counted(j);
-        if (j == 7) acc_lo = acc;
-      }
+    for (int j = 0; j < 8 * NG; ++j) {
+      acc = acc + counted(exp_fast2(P[j], nml), j);
+      if (j == 7) acc_lo = acc;
     }
     // padding lanes: the group-1 duplicates (NG == 2) or the whole lane (NG == 1) add nothing to the exp-sum
     if constexpr (NG == 2) acc = hi_ok ? acc : acc_lo;
@@ -850,11 +884,19 @@ __device__ __forceinline__ void row_tile_softmax_lean(const RowLoads<NG>& L, int
     }
     const bool ka = va && fa, kb = vb && fb;
     const f32x2 s2 = {sa, sb}, i2 = {ia, ib};
+    // the pair's codes: fast and verified (bf16, narrow rows), else the exact definition
+    const bool fast = FastQuot<T>::value && narrow;
+    const float ea = fast_eps(mxa, mn_a), eb = fast_eps(mxb, mn_b);
+    const f32x2 rlo = {ia - ia * ea, ib - ib * eb}, rhi = {ia + ia * ea, ib + ib * eb};
+    auto code_pair = [&](int j) -> uint32_t {
+      if (fast) return fast_code2<T>(P[j], nml, rlo, rhi, mx2, s2, i2);
+      return pack_rne2<T>(div_rn2(exp_nonpos2(P[j] - mx2), s2, i2));
+    };
     if (ka && kb) {  // wave-uniform: both rows counted (the common case) -- no mask
 #pragma unroll
       for (int j = 0; j < 8 * NG; ++j) {
         const int c = 512 * (j >> 3) + 8 * lane + (j & 7);
-        s_tile[c * kSlots + (p ^ (lane & (kSlots - 1)))] = pack_rne2<T>(div_rn2(P[j], s2, i2));
+        s_tile[c * kSlots + (p ^ (lane & (kSlots - 1)))] = code_pair(j);
       }
     } else {
       const uint32_t keep = (ka ? 0x0000FFFFu : 0u) | (kb ? 0xFFFF0000u : 0u);
@@ -862,7 +904,7 @@ __device__ __forceinline__ void row_tile_softmax_lean(const RowLoads<NG>& L, int
 #pragma unroll
       for (int j = 0; j < 8 * NG; ++j) {
         const int c = 512 * (j >> 3) + 8 * lane + (j & 7);
-        s_tile[c * kSlots + (p ^ (lane & (kSlots - 1)))] = (pack_rne2<T>(div_rn2(P[j], s2, i2)) & keep) | setm;
+        s_tile[c * kSlots + (p ^ (lane & (kSlots - 1)))] = (code_pair(j) & keep) | setm;
       }
     }
     if (lane == 0 && pos.hist == nullptr) {
@@ -2131,25 +2173,26 @@ __global__ void __launch_bounds__(kSmallRows * TL) TMX_SMALL_WPE_ATTR mc_codes_s
   float s = 0.f, inv = 0.f;
   // exp(x - max) of the slots and their row sum; the exps replace the scores in P only in softmax mode (probability
   // mode keeps the scores: they are the codes, the sum only feeds the class pass's refit statistics)
-  auto exp_sum = [&](bool store) -> float {
-    const f32x2 m2 = {mx, mx};
-    // every valid element of every row of the wave within 86 of its maximum: the lean exp (exp_nonpos2_narrow)
-    const bool narrow = __ballot(!(mx - mn <= 86.f)) == 0;
+  // round 6: the row sum of the fast exps (csrc/curve_hist_kernels.h fast_code2); the scores stay in P
+  const f32x2 m2 = {mx, mx};
+  const f32x2 nml = {fast_nml(mx), fast_nml(mx)};
+  // every valid element of every row of the wave within 86 of its maximum: verified fast quotients (bf16)
+  const bool narrow = __ballot(!(mx - mn <= 86.f)) == 0;
+  auto exp_sum = [&]() -> float {
     f32x2 acc = {0.f, 0.f};
 #pragma unroll
     for (int p = 0; p < kPairs; ++p) {
-      f32x2 e = narrow ? exp_nonpos2_narrow(P[p] - m2) : exp_nonpos2(P[p] - m2);
+      f32x2 e = exp_fast2(P[p], nml);
       if (masked) {
         e.x = cb + 2 * p < C ? e.x : 0.f;
         e.y = cb + 2 * p + 1 < C ? e.y : 0.f;
       }
       acc = acc + e;
-      if (store) P[p] = e;
     }
     return grp_sum<TL>(acc.x + acc.y);
   };
   // softmax statistics: the codes in softmax mode, the class pass's refit of a mispredicted batch otherwise
-  if (use_mode != 0 || row_stats != nullptr) s = exp_sum(use_mode != 0);
+  if (use_mode != 0 || row_stats != nullptr) s = exp_sum();
   if (use_mode != 0) {
     inv = 1.f / s;
     fin = fin && s == s;
@@ -2175,9 +2218,12 @@ __global__ void __launch_bounds__(kSmallRows * TL) TMX_SMALL_WPE_ATTR mc_codes_s
     const f32x2 s2 = {s, s}, i2 = {inv, inv};
     const int tl = static_cast<int>(t) - cb;  // the positive's slot in this lane (any value when t is not here)
     const uint32_t tflag = TL > 1 ? 0u : 0x4000u << (16 * (tl & 1));
+    const bool fast = FastQuot<T>::value && narrow;
+    const float eps = fast_eps(mx, mn);  // (the row minimum bounds this lane's elements too)
+    const f32x2 rlo = {inv - inv * eps, inv - inv * eps}, rhi = {inv + inv * eps, inv + inv * eps};
 #pragma unroll
     for (int p = 0; p < kPairs; ++p) {
-      word[p] = pack_rne2<T>(div_rn2(P[p], s2, i2));
+      word[p] = fast ? fast_code2<T>(P[p], nml, rlo, rhi, m2, s2, i2) : pack_rne2<T>(div_rn2(exp_nonpos2(P[p] - m2), s2, i2));
       if constexpr (TL == 1) word[p] |= ((tl >> 1) == p && tl >= 0 ? tflag : 0u);
     }
   } else {

@@ -12,12 +12,12 @@
 // sensitivity terms of each valid window are reduced per block (wave shuffles + LDS) into one fp64 partial per
 // (plane, block) — the output image is never materialised.
 #include "common.h"
+#include "ssim_kernels.h"
 
 #include <cstdlib>
 
 namespace tmx {
 
-constexpr int kSsimThreads = 256;
 constexpr int kRowsPerBlock = 64;
 
 template <typename T> __device__ __forceinline__ float ld_f(const T* p, int64_t i) { return to_f32<T>(p[i]); }
@@ -141,190 +141,6 @@ __global__ __launch_bounds__(kSsimThreads) void ssim_valid_kernel(const T* __res
   }
 }
 
-// ------------------------------------------------------------------------------------------------------------
-// fp32, W % 4 == 0, 16-B aligned planes (the common case): the same valid-window algorithm, restructured for
-// throughput (the one-row-per-barrier kernel above ran at 0.78 TB/s on 256 x 3 x 1024^2):
-//   * KS input rows are staged per barrier, prefetched into registers with 16-B loads while the previous group is
-//     computed (one barrier per KS rows instead of per row);
-//   * (p, t) are interleaved in LDS as float2, so one 8-B LDS read feeds both images, and the moment arithmetic runs
-//     on packed fp32 pairs (v_pk_mul / v_pk_add / v_pk_fma): (mu_p, mu_t) and (E[pp], E[tt]) share instructions,
-//     ~4 instructions per horizontal tap and 3 per vertical tap instead of 7 and 5;
-//   * strips of kRowsV2 output rows per block halve the KS - 1 halo rows' share of the reads.
-typedef float f2 __attribute__((ext_vector_type(2)));
-constexpr int kRowsV2 = 128;
-
-// SSE (fused PSNR of a MetricCollection{SSIM, PSNR}): every input pixel is owned by exactly one block (rows
-// [y0, y0 + kRowsV2) and columns [x0, x0 + 256), the last strip / column block up to H / W), and its (p - t)^2 is
-// added while the block stages it anyway: PSNR needs no second pass over the two images.
-template <int KS, bool SSE>
-__global__ __launch_bounds__(kSsimThreads, 2) void ssim_v2_kernel(const float* __restrict__ preds, const float* __restrict__ target,
-                                                                int H, int W, const float* __restrict__ wx,
-                                                                const float* __restrict__ wy, const float* __restrict__ consts,
-                                                                double* __restrict__ partial_sim, double* __restrict__ partial_cs,
-                                                                double* __restrict__ partial_sse) {
-  constexpr int kSeg4 = (kSsimThreads + KS - 1 + 3) / 4;   // float4 columns per staged row segment
-  constexpr int kSegF = kSeg4 * 4;
-  constexpr int kItems = KS * kSeg4;                       // (row, column quad) items per group
-  constexpr int kPer = (kItems + kSsimThreads - 1) / kSsimThreads;
-  __shared__ f2 s_pt[2][KS][kSegF];
-  __shared__ double red[3][kSsimThreads / kWave];
-
-  const int Hv = H - KS + 1, Wv = W - KS + 1;
-  const int64_t plane = blockIdx.z;
-  const int x0 = blockIdx.x * kSsimThreads;
-  const int y0 = blockIdx.y * kRowsV2;
-  const int tid = threadIdx.x;
-  const float* P = preds + plane * static_cast<int64_t>(H) * W;
-  const float* Tt = target + plane * static_cast<int64_t>(H) * W;
-  const float c1 = consts[0], c2 = consts[1];
-  f2 wx2[KS], wy2[KS];  // weights pre-splatted into packed pairs (no per-tap register moves)
-#pragma unroll
-  for (int k = 0; k < KS; ++k) {
-    wx2[k] = f2{wx[k], wx[k]};
-    wy2[k] = f2{wy[k], wy[k]};
-  }
-  const int out_rows = min(kRowsV2, Hv - y0);
-  const int in_rows = out_rows + KS - 1;
-  const bool col_ok = (x0 + tid) < Wv;
-
-  float4 pre_p[kPer], pre_t[kPer];
-  auto fetch = [&](int g) {  // group g = input rows y0 + g KS .. + KS - 1 into registers
-#pragma unroll
-    for (int i = 0; i < kPer; ++i) {
-      const int e = tid + i * kSsimThreads;
-      const int r = e / kSeg4, q = e % kSeg4;
-      const int y = y0 + g * KS + r, x = x0 + 4 * q;
-      const bool ok = e < kItems && g * KS + r < in_rows && x < W;  // W % 4 == 0: a quad is all in or all out
-      const int64_t o = static_cast<int64_t>(y) * W + x;
-      pre_p[i] = ok ? *reinterpret_cast<const float4*>(P + o) : make_float4(0.f, 0.f, 0.f, 0.f);
-      pre_t[i] = ok ? *reinterpret_cast<const float4*>(Tt + o) : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-  };
-  auto store = [&](int buf) {
-#pragma unroll
-    for (int i = 0; i < kPer; ++i) {
-      const int e = tid + i * kSsimThreads;
-      if (e < kItems) {
-        const int r = e / kSeg4, q = e % kSeg4;
-        f2* d = &s_pt[buf][r][4 * q];
-        d[0] = f2{pre_p[i].x, pre_t[i].x};
-        d[1] = f2{pre_p[i].y, pre_t[i].y};
-        d[2] = f2{pre_p[i].z, pre_t[i].z};
-        d[3] = f2{pre_p[i].w, pre_t[i].w};
-      }
-    }
-  };
-
-  // ring of horizontal sums for the last KS rows: (mu_p, mu_t), (E[pp], E[tt]) packed, E[pt] scalar
-  f2 rm[KS], rq[KS];
-  float rx[KS];
-#pragma unroll
-  for (int k = 0; k < KS; ++k) {
-    rm[k] = f2{0.f, 0.f};
-    rq[k] = f2{0.f, 0.f};
-    rx[k] = 0.f;
-  }
-  double acc_sim = 0.0, acc_cs = 0.0, acc_sse = 0.0;
-  float f_sim = 0.f, f_cs = 0.f, f_sse = 0.f;
-  // owned input pixels (SSE): rows r < own_rows, this thread's column, plus columns 256 .. for the last column block
-  const bool last_x = blockIdx.x == gridDim.x - 1, last_y = blockIdx.y == gridDim.y - 1;
-  const int own_rows = last_y ? in_rows : out_rows;
-  const bool own_col = x0 + tid < W && (last_x || tid < kSsimThreads);
-  const bool own_col2 = last_x && tid < KS - 1 && x0 + kSsimThreads + tid < W;
-  const int groups = (in_rows + KS - 1) / KS;
-  if (groups > 0) {
-    fetch(0);
-    store(0);
-  }
-  __syncthreads();
-  for (int g = 0; g < groups; ++g) {
-    const int buf = g & 1;
-    if (g + 1 < groups) fetch(g + 1);  // in flight during this group's arithmetic
-#pragma unroll
-    for (int j = 0; j < KS; ++j) {
-      const int r = g * KS + j;
-      if (r < in_rows) {  // block-uniform
-        f2 hm = f2{0.f, 0.f}, hq = f2{0.f, 0.f};
-        float hx = 0.f;
-#pragma unroll
-        for (int k = 0; k < KS; ++k) {
-          const f2 v = s_pt[buf][j][tid + k];
-          const f2 wv = wx2[k] * v;                        // (w p, w t)
-          hm += wv;
-          hq = __builtin_elementwise_fma(wv, v, hq);       // (w p p, w t t)
-          hx = fmaf(wv.x, v.y, hx);                        // w p t
-        }
-        rm[j] = hm;
-        rq[j] = hq;
-        rx[j] = hx;
-        if constexpr (SSE) {
-          if (r < own_rows) {
-            if (own_col) {
-              const f2 v = s_pt[buf][j][tid];
-              const float d = v.x - v.y;
-              f_sse = fmaf(d, d, f_sse);
-            }
-            if (own_col2) {
-              const f2 v = s_pt[buf][j][kSsimThreads + tid];
-              const float d = v.x - v.y;
-              f_sse = fmaf(d, d, f_sse);
-            }
-          }
-        }
-        if (r >= KS - 1 && col_ok) {
-          f2 m01 = f2{0.f, 0.f}, m23 = f2{0.f, 0.f};
-          float m4 = 0.f;
-#pragma unroll
-          for (int k = 0; k < KS; ++k) {
-            const int slot = (j + 1 + k) % KS;  // oldest first
-            m01 = __builtin_elementwise_fma(wy2[k], rm[slot], m01);
-            m23 = __builtin_elementwise_fma(wy2[k], rq[slot], m23);
-            m4 = fmaf(wy2[k].x, rx[slot], m4);
-          }
-          const float mu_pp = m01.x * m01.x, mu_tt = m01.y * m01.y, mu_pt = m01.x * m01.y;
-          const float upper = 2.f * (m4 - mu_pt) + c2;
-          const float lower = (m23.x - mu_pp) + (m23.y - mu_tt) + c2;
-          // hardware reciprocals (1 ulp) instead of two IEEE divisions (~10 instructions each)
-          const float cs = upper * __builtin_amdgcn_rcpf(lower);
-          const float sim = (2.f * mu_pt + c1) * cs * __builtin_amdgcn_rcpf(mu_pp + mu_tt + c1);
-          f_sim += sim;  // <= kRowsV2 terms per thread in fp32, folded into fp64 per group
-          f_cs += cs;
-        }
-      }
-    }
-    acc_sim += static_cast<double>(f_sim);
-    acc_cs += static_cast<double>(f_cs);
-    acc_sse += static_cast<double>(f_sse);
-    f_sim = f_cs = f_sse = 0.f;
-    if (g + 1 < groups) {
-      store(buf ^ 1);  // the other buffer was last read in group g - 1, before the previous barrier
-      __syncthreads();
-    }
-  }
-  acc_sim = wave_sum(acc_sim);
-  acc_cs = wave_sum(acc_cs);
-  if constexpr (SSE) acc_sse = wave_sum(acc_sse);
-  const int wave = tid / kWave, lane = tid & (kWave - 1);
-  if (lane == 0) {
-    red[0][wave] = acc_sim;
-    red[1][wave] = acc_cs;
-    red[2][wave] = acc_sse;
-  }
-  __syncthreads();
-  if (tid == 0) {
-    double s = 0.0, c = 0.0, e = 0.0;
-    for (int w = 0; w < kSsimThreads / kWave; ++w) {
-      s += red[0][w];
-      c += red[1][w];
-      e += red[2][w];
-    }
-    const int64_t idx = (plane * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
-    partial_sim[idx] = s;
-    partial_cs[idx] = c;
-    if constexpr (SSE) partial_sse[idx] = e;
-  }
-}
-
 template <typename T, int KS>
 void launch_ssim(const at::Tensor& p, const at::Tensor& t, const at::Tensor& wx, const at::Tensor& wy,
                  const at::Tensor& consts, at::Tensor& ps, at::Tensor& pc, dim3 grid, int H, int W) {
@@ -335,17 +151,19 @@ void launch_ssim(const at::Tensor& p, const at::Tensor& t, const at::Tensor& wx,
 
 template <int KS>
 void launch_ssim_v2(const at::Tensor& p, const at::Tensor& t, const at::Tensor& wx, const at::Tensor& wy, const at::Tensor& consts,
-                    at::Tensor& ps, at::Tensor& pc, double* pe, dim3 grid, int H, int W) {
+                    at::Tensor& ps, at::Tensor& pc, double* pe, dim3 grid, int H, int W, const int* run_if = nullptr) {
   if (pe != nullptr)
     hipLaunchKernelGGL((ssim_v2_kernel<KS, true>), grid, kSsimThreads, 0, stream(), p.data_ptr<float>(), t.data_ptr<float>(), H, W,
-                       wx.data_ptr<float>(), wy.data_ptr<float>(), consts.data_ptr<float>(), ps.data_ptr<double>(), pc.data_ptr<double>(), pe);
+                       wx.data_ptr<float>(), wy.data_ptr<float>(), consts.data_ptr<float>(), ps.data_ptr<double>(), pc.data_ptr<double>(), pe,
+                       run_if);
   else
     hipLaunchKernelGGL((ssim_v2_kernel<KS, false>), grid, kSsimThreads, 0, stream(), p.data_ptr<float>(), t.data_ptr<float>(), H, W,
                        wx.data_ptr<float>(), wy.data_ptr<float>(), consts.data_ptr<float>(), ps.data_ptr<double>(), pc.data_ptr<double>(),
-                       nullptr);
+                       nullptr, run_if);
 }
 
-// preds/target [P, H, W] planes (P = B*C); wx/wy fp32 [KS] window weights; consts fp32 [2] = (c1, c2) on device.
+// preds/target [P, H, W] planes (P = B*C); wx/wy fp32 [KS] window weights; consts fp32 [2] = (c1, c2) on device, or
+// [3] = (c1, c2, data range): the matrix-core kernel (wx == wy).
 // Returns fp64 [2, P]: per-plane sums of SSIM and contrast sensitivity over all valid windows.
 at::Tensor ssim_sums(const at::Tensor& preds_in, const at::Tensor& target_in, const at::Tensor& wx_in,
                      const at::Tensor& wy_in, const at::Tensor& consts_in, bool with_sse) {
@@ -375,6 +193,43 @@ at::Tensor ssim_sums(const at::Tensor& preds_in, const at::Tensor& target_in, co
   auto pc = at::empty({P, static_cast<int64_t>(grid.y) * grid.x}, opts);
   auto pe_t = with_sse && v2 ? at::empty({P, static_cast<int64_t>(grid.y) * grid.x}, opts) : at::Tensor();
   double* pe = with_sse && v2 ? pe_t.data_ptr<double>() : nullptr;
+  // round 6: the matrix-core kernel (csrc/ssim_kernels.h ssim_mfma_kernel) when the caller passes the data range
+  // (consts = c1, c2, D), with ssim_v2_kernel as its device-side fallback for out-of-range data
+  static const bool mfma_off = std::getenv("TMX_SSIM_V2") != nullptr;  // A/B knob (tools/ssim_bench.py)
+  if (v2 && !mfma_off && consts.numel() >= 3 && KS <= 17) {
+    constexpr int kStrip = 256;
+    const int ntx = static_cast<int>((Wv + 15) / 16);
+    dim3 mgrid(static_cast<unsigned>((ntx + kSsimMfmaWaves - 1) / kSsimMfmaWaves), static_cast<unsigned>((Hv + kStrip - 1) / kStrip),
+               static_cast<unsigned>(P));
+    const int64_t nparts = static_cast<int64_t>(mgrid.y) * ntx;
+    auto ms = at::empty({P, nparts}, opts), mc = at::empty({P, nparts}, opts);
+    auto me = with_sse ? at::empty({P, nparts}, opts) : at::Tensor();
+    auto flag = at::zeros({1}, p.options().dtype(at::kInt));
+    if (with_sse)
+      hipLaunchKernelGGL((ssim_mfma_kernel<true>), mgrid, kSsimMfmaWaves * kWave, 0, stream(), p.data_ptr<float>(), t.data_ptr<float>(),
+                         (int)H, (int)W, (int)KS, kStrip, wx.data_ptr<float>(), consts.data_ptr<float>(), ms.data_ptr<double>(),
+                         mc.data_ptr<double>(), me.data_ptr<double>(), flag.data_ptr<int>());
+    else
+      hipLaunchKernelGGL((ssim_mfma_kernel<false>), mgrid, kSsimMfmaWaves * kWave, 0, stream(), p.data_ptr<float>(), t.data_ptr<float>(),
+                         (int)H, (int)W, (int)KS, kStrip, wx.data_ptr<float>(), consts.data_ptr<float>(), ms.data_ptr<double>(),
+                         mc.data_ptr<double>(), nullptr, flag.data_ptr<int>());
+    TMX_LAUNCH_CHECK();
+    // the fallback launch: every workgroup exits at its first load unless the kernel above flagged the batch
+    switch (KS) {
+      case 3: launch_ssim_v2<3>(p, t, wx, wy, consts, ps, pc, pe, grid, H, W, flag.data_ptr<int>()); break;
+      case 5: launch_ssim_v2<5>(p, t, wx, wy, consts, ps, pc, pe, grid, H, W, flag.data_ptr<int>()); break;
+      case 7: launch_ssim_v2<7>(p, t, wx, wy, consts, ps, pc, pe, grid, H, W, flag.data_ptr<int>()); break;
+      case 9: launch_ssim_v2<9>(p, t, wx, wy, consts, ps, pc, pe, grid, H, W, flag.data_ptr<int>()); break;
+      case 11: launch_ssim_v2<11>(p, t, wx, wy, consts, ps, pc, pe, grid, H, W, flag.data_ptr<int>()); break;
+      case 13: launch_ssim_v2<13>(p, t, wx, wy, consts, ps, pc, pe, grid, H, W, flag.data_ptr<int>()); break;
+      default: launch_ssim_v2<15>(p, t, wx, wy, consts, ps, pc, pe, grid, H, W, flag.data_ptr<int>()); break;
+    }
+    TMX_LAUNCH_CHECK();
+    auto use_v2 = flag.gt(0);
+    auto fast = with_sse ? at::stack({ms.sum(1), mc.sum(1), me.sum(1)}) : at::stack({ms.sum(1), mc.sum(1)});
+    auto slow = with_sse ? at::stack({ps.sum(1), pc.sum(1), pe_t.sum(1)}) : at::stack({ps.sum(1), pc.sum(1)});
+    return at::where(use_v2, slow, fast);
+  }
   if (v2) {
     switch (KS) {
       case 3: launch_ssim_v2<3>(p, t, wx, wy, consts, ps, pc, pe, grid, H, W); break;

@@ -1,4 +1,4 @@
-// Row pass A/B (round 5): production softmax row tile (row_tile_compute) vs the lean form (row_tile_softmax_lean).
+// Row pass A/B (round 5; round 6: the lean form's fast verified quotients vs the production form's exact ones): production softmax row tile (row_tile_compute) vs the lean form (row_tile_softmax_lean).
 // Same grid / LDS image / store; the lean form must produce the same class-major codes, confusion matrix, rare-row
 // list and per-row statistics bit for bit.  Cases: randn logits (narrow rows), logits x 40 (gaps > 86: the exact
 // exp path), NaN / +-inf / all -inf rows, ignore_index rows, C = 1000 (two class groups) and C = 256 (one group).
@@ -87,8 +87,11 @@ int main(int argc, char** argv) {
       h[i] = f2bf(2.f * sqrtf(-2.f * logf(u1)) * cosf(6.2831853f * u2));
     }
     for (int64_t i = 0; i < N; ++i) { ht[i] = rand() % C; hti[i] = (i % 7 == 3) ? -100 : ht[i]; }
-    std::vector<uint16_t> hw = h, hn = h;
+    std::vector<uint16_t> hw = h, hn = h, h5 = h, hs = h;
     for (int64_t i = 0; i < N * C; ++i) { float v; uint32_t u = (uint32_t)h[i] << 16; memcpy(&v, &u, 4); hw[i] = f2bf(v * 40.f); }
+    // round 6 (fast verified quotients): wide but narrow rows (range ~64: the largest verification window) and
+    // near-uniform rows (every quotient close to 1 / C)
+    for (int64_t i = 0; i < N * C; ++i) { float v; uint32_t u = (uint32_t)h[i] << 16; memcpy(&v, &u, 4); h5[i] = f2bf(v * 5.f); hs[i] = f2bf(v * 0.01f + 3.f); }
     for (int64_t r = 5; r < N; r += 997) hn[r * C + (r % C)] = 0x7FC0;                          // NaN
     for (int64_t r = 11; r < N; r += 1999) hn[r * C + ((r * 7) % C)] = 0x7F80;                  // +inf
     for (int64_t r = 13; r < N; r += 29) hn[r * C + ((r * 3) % C)] = 0xFF80;                    // one -inf (finite max)
@@ -105,7 +108,8 @@ int main(int argc, char** argv) {
       CK(hipMalloc(&b.cnt, 8)); CK(hipMalloc(&b.stats, N * 16)); CK(hipMalloc(&b.verdict, 4));
     }
     struct Case { const char* name; const std::vector<uint16_t>* x; bool ign; };
-    Case cases[] = {{"randn", &h, false}, {"wide_x40", &hw, false}, {"special_rows", &hn, false}, {"special_ignore", &hn, true}};
+    Case cases[] = {{"randn", &h, false}, {"wide_x40", &hw, false}, {"special_rows", &hn, false}, {"special_ignore", &hn, true},
+                     {"narrow_x5", &h5, false}, {"near_uniform", &hs, false}};
     for (const Case& cs : cases) {
       CK(hipMemcpy(dx, cs.x->data(), xbytes, hipMemcpyHostToDevice));
       for (int v = 0; v < 2; ++v) {

@@ -1,0 +1,140 @@
+// SSIM window A/B (round 6): the matrix-core kernel (ssim_mfma_kernel) vs the fp32 VALU kernel (ssim_v2_kernel) on
+// the same planes -- per-plane SSIM / CS / SSE sums and their difference, fallback flag, and timing at the BASELINE
+// config-4 shape (256 x 3 x 1024^2 fp32, 11-tap gaussian, sigma 1.5).
+// Build: hipcc -O3 --offload-arch=gfx950 -I csrc tools/kexp/ssim_mfma_exp.hip -o build/kexp_r6/ssim_mfma_exp
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#include "ssim_kernels.h"
+
+using namespace tmx;
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP error %s at %s:%d\n", hipGetErrorString(e), __FILE__, __LINE__); exit(1); } } while (0)
+
+// deterministic images: kind 0 uniform [0, 1); 1 smooth (low-variance gradients + small noise); 2 [0, 255) ints;
+// 3 out of range (x 10 of the stated data range: the MFMA kernel must flag its fallback)
+__global__ void fill(float* p, float* t, int64_t n, int W, int kind, uint32_t seed) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    uint32_t h = (uint32_t)i * 2654435761u ^ seed;
+    h ^= h >> 15; h *= 2246822519u; h ^= h >> 13; h *= 3266489917u; h ^= h >> 16;
+    const float u = (h >> 8) * (1.f / 16777216.f);
+    uint32_t k = h * 747796405u + 2891336453u;
+    k ^= k >> 16;
+    const float v = (k >> 8) * (1.f / 16777216.f);
+    const int x = (int)(i % W), y = (int)((i / W) % 1024);
+    float a, b;
+    if (kind == 0) { a = u; b = 0.7f * u + 0.3f * v; }
+    else if (kind == 1) { a = 0.4f + 0.1f * sinf(x * 0.01f) * cosf(y * 0.013f) + 0.01f * u; b = a + 0.005f * (v - 0.5f); }
+    else if (kind == 2) { a = floorf(u * 255.f); b = floorf((0.8f * u + 0.2f * v) * 255.f); }
+    else { a = 10.f * u; b = 10.f * v; }
+    p[i] = a;
+    t[i] = b;
+  }
+}
+
+template <typename F>
+float time_ms(F f, int iters) {
+  f();
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
+  CK(hipEventRecord(a));
+  for (int i = 0; i < iters; ++i) f();
+  CK(hipEventRecord(b));
+  CK(hipEventSynchronize(b));
+  float ms; CK(hipEventElapsedTime(&ms, a, b));
+  return ms / iters;
+}
+
+static std::vector<float> gaussian(int ks, float sigma) {
+  std::vector<float> w(ks);
+  float s = 0.f;
+  for (int i = 0; i < ks; ++i) { const float d = i - (ks - 1) / 2.f; w[i] = expf(-(d * d) / (2.f * sigma * sigma)); s += w[i]; }
+  for (auto& x : w) x /= s;
+  return w;
+}
+
+struct Result { std::vector<double> sim, cs, sse; int flag; float ms; };
+
+template <int KS>
+Result run(bool mfma, const float* p, const float* t, int P, int H, int W, const float* dw, const float* dc, bool timed) {
+  Result r;
+  const int Hv = H - KS + 1, Wv = W - KS + 1;
+  int* flag; CK(hipMalloc(&flag, 4)); CK(hipMemset(flag, 0, 4));
+  double *ds, *dcs, *de;
+  int64_t nparts;
+  dim3 grid;
+  if (mfma) {
+    const int strip = 256, ntx = (Wv + 15) / 16;
+    grid = dim3((ntx + kSsimMfmaWaves - 1) / kSsimMfmaWaves, (Hv + strip - 1) / strip, P);
+    nparts = (int64_t)grid.y * ntx;
+  } else {
+    grid = dim3((Wv + kSsimThreads - 1) / kSsimThreads, (Hv + kRowsV2 - 1) / kRowsV2, P);
+    nparts = (int64_t)grid.y * grid.x;
+  }
+  CK(hipMalloc(&ds, P * nparts * 8)); CK(hipMalloc(&dcs, P * nparts * 8)); CK(hipMalloc(&de, P * nparts * 8));
+  auto launch = [&] {
+    if (mfma)
+      hipLaunchKernelGGL((ssim_mfma_kernel<true>), grid, kSsimMfmaWaves * kWave, 0, 0, p, t, H, W, KS, 256, dw, dc, ds, dcs, de, flag);
+    else
+      hipLaunchKernelGGL((ssim_v2_kernel<KS, true>), grid, kSsimThreads, 0, 0, p, t, H, W, dw, dw, dc, ds, dcs, de, nullptr);
+  };
+  launch();
+  CK(hipDeviceSynchronize());
+  std::vector<double> hs(P * nparts), hc(P * nparts), he(P * nparts);
+  CK(hipMemcpy(hs.data(), ds, hs.size() * 8, hipMemcpyDeviceToHost));
+  CK(hipMemcpy(hc.data(), dcs, hc.size() * 8, hipMemcpyDeviceToHost));
+  CK(hipMemcpy(he.data(), de, he.size() * 8, hipMemcpyDeviceToHost));
+  CK(hipMemcpy(&r.flag, flag, 4, hipMemcpyDeviceToHost));
+  r.sim.assign(P, 0.0); r.cs.assign(P, 0.0); r.sse.assign(P, 0.0);
+  for (int pl = 0; pl < P; ++pl)
+    for (int64_t k = 0; k < nparts; ++k) { r.sim[pl] += hs[pl * nparts + k]; r.cs[pl] += hc[pl * nparts + k]; r.sse[pl] += he[pl * nparts + k]; }
+  r.ms = timed ? time_ms(launch, 5) : 0.f;
+  CK(hipFree(ds)); CK(hipFree(dcs)); CK(hipFree(de)); CK(hipFree(flag));
+  return r;
+}
+
+template <int KS>
+bool compare(const char* name, int P, int H, int W, int kind, bool timed) {
+  const int64_t n = (int64_t)P * H * W;
+  float *p, *t, *dw, *dc;
+  CK(hipMalloc(&p, n * 4)); CK(hipMalloc(&t, n * 4)); CK(hipMalloc(&dw, KS * 4)); CK(hipMalloc(&dc, 12));
+  hipLaunchKernelGGL(fill, 4096, 256, 0, 0, p, t, n, W, kind, 12345u + kind);
+  const std::vector<float> w = gaussian(KS, 1.5f);
+  const float D = kind == 2 ? 255.f : 1.f;
+  const float c[3] = {(0.01f * D) * (0.01f * D), (0.03f * D) * (0.03f * D), D};
+  CK(hipMemcpy(dw, w.data(), KS * 4, hipMemcpyHostToDevice)); CK(hipMemcpy(dc, c, 12, hipMemcpyHostToDevice));
+  const Result a = run<KS>(false, p, t, P, H, W, dw, dc, timed), b = run<KS>(true, p, t, P, H, W, dw, dc, timed);
+  const double nv = (double)(H - KS + 1) * (W - KS + 1);
+  double dmax = 0.0, cmax = 0.0, emax = 0.0, mean_a = 0.0, mean_b = 0.0;
+  for (int pl = 0; pl < P; ++pl) {
+    dmax = fmax(dmax, fabs(a.sim[pl] - b.sim[pl]) / nv);
+    cmax = fmax(cmax, fabs(a.cs[pl] - b.cs[pl]) / nv);
+    emax = fmax(emax, fabs(a.sse[pl] - b.sse[pl]) / fmax(1e-30, fabs(a.sse[pl])));
+    mean_a += a.sim[pl] / nv / P;
+    mean_b += b.sim[pl] / nv / P;
+  }
+  const bool ok = kind == 3 ? b.flag == 1 : (b.flag == 0 && dmax <= 1e-6 && cmax <= 1e-6 && emax <= 1e-9);
+  printf(", \"%s_KS%d\": {\"P\": %d, \"H\": %d, \"W\": %d, \"ssim_v2\": %.9f, \"ssim_mfma\": %.9f, \"max_plane_ssim_diff\": %.3g, "
+         "\"max_plane_cs_diff\": %.3g, \"max_plane_sse_rel_diff\": %.3g, \"fallback_flag\": %d, \"v2_ms\": %.3f, \"mfma_ms\": %.3f, \"ok\": %s}",
+         name, KS, P, H, W, mean_a, mean_b, dmax, cmax, emax, b.flag, a.ms, b.ms, ok ? "true" : "false");
+  CK(hipFree(p)); CK(hipFree(t)); CK(hipFree(dw)); CK(hipFree(dc));
+  return ok;
+}
+
+int main() {
+  printf("{\"bench\": \"ssim_mfma_exp\"");
+  bool ok = true;
+  ok &= compare<11>("uniform_odd", 5, 257, 300, 0, false);
+  ok &= compare<11>("smooth_odd", 3, 129, 1020, 1, false);
+  ok &= compare<11>("u8_range", 4, 300, 516, 2, false);
+  ok &= compare<7>("uniform_ks7", 3, 100, 128, 0, false);
+  ok &= compare<3>("uniform_ks3", 3, 64, 64, 0, false);
+  ok &= compare<15>("uniform_ks15", 2, 211, 260, 0, false);
+  ok &= compare<11>("out_of_range", 2, 64, 64, 3, false);
+  ok &= compare<11>("config4", 768, 1024, 1024, 0, true);
+  ok &= compare<11>("config4_smooth", 768, 1024, 1024, 1, true);
+  printf(", \"all_ok\": %s}\n", ok ? "true" : "false");
+  return ok ? 0 : 3;
+}

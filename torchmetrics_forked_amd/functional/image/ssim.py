@@ -116,8 +116,9 @@ def _ssim_update(
         else:
             w1 = torch.full((window[0],), 1.0 / window[0], dtype=torch.float32, device=device)
         # fill kernels for Python-float constants (a pageable host-to-device copy would block the host)
+        # (c1, c2, data range): the range sets the matrix-core kernel's exact power-of-two operand scaling
         consts = torch.stack([c.to(device, torch.float32) if isinstance(c, torch.Tensor) else torch.full((), float(c), device=device)
-                              for c in (c1, c2)])
+                              for c in (c1, c2, data_range)])
         b, c, h, w = preds.shape
         sums = torch.ops.tmx.ssim_sums(preds.reshape(b * c, h, w), target.reshape(b * c, h, w), w1, w1, consts, sse_out is not None)
         if sse_out is not None:
