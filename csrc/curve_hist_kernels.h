@@ -244,40 +244,42 @@ __device__ __forceinline__ f32x2 exp_nonpos2_narrow(f32x2 x) {
 // ---- fast softmax with verified quotients (round 6) -----------------------------------------------------------------
 // A softmax code is DEFINED as RNE16(div_rn(exp_nonpos(x - max), s)): the correctly rounded quotient of expf's exact
 // instruction sequence (what ATen's softmax stores before its 16-bit rounding) by the row sum s.  Since round 6 s is
-// the fixed-order sum of FAST exponentials e_f(x) = v_exp_f32(fma(x, log2e, -RN(max log2e))) -- one fma and one
-// v_exp per element instead of the 9-instruction exact sequence; it differs from the sum of exact exps in the last
-// bits only (the fp32 summation order already differs from ATen's).  The refit and every row pass store and reuse
-// the same s (row_stats), so all routes still produce the same codes for one batch.
+// the fixed-order sum of FAST exponentials e_f(x) = v_exp_f32(RN(RN(x - max) L)), L = RN(log2 e) -- one multiply and
+// one v_exp per element instead of the 9-instruction exact sequence.  e_f(max) = 1 exactly (as ATen's exp(0)); the
+// other terms differ from expf's in the last bits only (the fp32 summation order already differs from ATen's).  The
+// class pass's refit reads s from row_stats, so every route produces the same codes for one batch.
 // The quotient of the common case (bf16, every element within 86 of its row maximum) is taken FAST and VERIFIED:
-// with r = 1 / s (correctly rounded), the exact quotient lies in [e_f r (1 - eps), e_f r (1 + eps)] where
-//   |t_f - d log2e| <= 2^-24 log2e (3 |d| + |max|)        (t_f = fma(x, L, -RN(max L)), L = RN(log2e), d = x - max)
-//   -> |e_f / exp(d) - 1| <= 2^-24 (3 |d| + |max|) + v_exp_f32's 1 ulp, |exp_nonpos(d) / exp(d) - 1| <= 1 ulp,
-//      |r s - 1| <= 2^-24, the roundings of r (1 -+ eps) <= 2^-24 each,
-// so eps = 2^-24 (3 (max - lane min) + |max| + 16) bounds it with room to spare.  RNE16 and fp32 rounding are
-// monotone: when RNE16(fl(e_f r_lo)) == RNE16(fl(e_f r_hi)) the exact quotient rounds to that same code.  Otherwise
-// (about 1e-3 of the bf16 elements of randn logits) the whole wave recomputes that element pair with the exact
-// sequence (a wave-uniform branch).  Per element: fma, v_exp, two multiplies, a conversion and a compare, against
-// the exact sequence's ~14 instructions.  fp16 keeps the exact quotient (its 10-bit codes put 8x as many rounding
-// boundaries in the window).
+// with r = 1 / s (correctly rounded) and d = RN(x - max), the exact quotient lies in [e_f r (1 - eps), e_f r (1 + eps)]:
+//   |RN(d L) - d log2e| <= 2^-23 |d| log2e -> |e_f / 2^(d log2e) - 1| <= 2^-23 |d| + v_exp_f32's 1 ulp,
+//   |exp_nonpos(d) / exp(d) - 1| <= 1 ulp, |r s - 1| <= 2^-24, and the roundings of r (1 -+ eps) <= 2^-24 each,
+// so eps = 2^-24 (2 (max - lane min) + 12) bounds it with room to spare.  RNE16 and fp32 rounding are monotone: when
+// RNE16(fl(e_f r_lo)) == RNE16(fl(e_f r_hi)) the exact quotient rounds to that same code.  The element pairs where any
+// lane is undecided (~7 % of the pair slots of randn logits at C = 1000, 1e-3 of the elements) are collected in a
+// wave-uniform bit mask and recomputed with the exact sequence after the pass, patching the LDS image.  Per element
+// pair: sum pass sub, mul, 2 v_exp, add; quotient pass 2 mul, 2 conversions, 1 compare -- against ~17 instructions
+// for the exact exp + correctly rounded division.  fp16 keeps the exact quotient (its 10-bit codes put 8x as many
+// rounding boundaries in the window).
 constexpr float kLog2eF = 1.44269502163f;  // RN(log2 e) = 0x3fb8aa3b
-__device__ __forceinline__ f32x2 exp_fast2(f32x2 x, f32x2 nml) {
-  const f32x2 t = __builtin_elementwise_fma(x, f32x2{kLog2eF, kLog2eF}, nml);
+__device__ __forceinline__ f32x2 exp_fast2(f32x2 d) {  // d = x - max (<= 0, -inf or NaN)
+  const f32x2 t = d * f32x2{kLog2eF, kLog2eF};
   return f32x2{__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)};
 }
-__device__ __forceinline__ float fast_nml(float mx) { return -(mx * kLog2eF); }
 // relative half-width of the verification interval (see above); lane_min: the smallest element this lane holds
-__device__ __forceinline__ float fast_eps(float mx, float lane_min) {
-  return (3.f * (mx - lane_min) + __builtin_fabsf(mx) + 16.f) * 5.9604645e-8f;
-}
+__device__ __forceinline__ float fast_eps(float mx, float lane_min) { return (2.f * (mx - lane_min) + 12.f) * 5.9604645e-8f; }
 template <typename T> struct FastQuot : std::false_type {};
 template <> struct FastQuot<__hip_bfloat16> : std::true_type {};
-// the code pair of (x.x, x.y): fast and verified, or exact for the whole wave when any lane's pair is undecided
+// the code pair of (e.x, e.y) from the fast exps, and whether either could round differently from the definition
 template <typename T>
-__device__ __forceinline__ uint32_t fast_code2(f32x2 x, f32x2 nml, f32x2 rlo, f32x2 rhi, f32x2 mx2, f32x2 s2, f32x2 i2) {
-  const f32x2 e = exp_fast2(x, nml);
+__device__ __forceinline__ uint32_t fast_code2(f32x2 e, f32x2 rlo, f32x2 rhi, bool& undecided) {
   const uint32_t lo = pack_rne2<T>(e * rlo), hi = pack_rne2<T>(e * rhi);
-  if (__ballot(lo != hi) == 0) return lo;
-  return pack_rne2<T>(div_rn2(exp_nonpos2_narrow(x - mx2), s2, i2));
+  undecided = lo != hi;
+  return lo;
+}
+// the definition, for the exact paths and the fallback
+template <typename T>
+__device__ __forceinline__ uint32_t exact_code2(f32x2 x, f32x2 mx2, f32x2 s2, f32x2 i2, bool narrow) {
+  const f32x2 d = x - mx2;
+  return pack_rne2<T>(div_rn2(narrow ? exp_nonpos2_narrow(d) : exp_nonpos2(d), s2, i2));
 }
 
 // the 16-bit pattern of a score widened to fp32 (exact: bf16 / fp16 -> fp32 is lossless; NaN payloads may be
@@ -630,18 +632,13 @@ __device__ __forceinline__ void row_tile_compute(const RowLoads<NG>& L, int64_t 
     bool fa = __builtin_isfinite(ra.mx), fb = __builtin_isfinite(rb.mx);
     const int ama = row_argmax<NG>(ra), amb = row_argmax<NG>(rb);
     float sa = 0.f, sb = 0.f, ia = 0.f, ib = 0.f;
-    const f32x2 nml = {fast_nml(ra.mx), fast_nml(rb.mx)};
     if constexpr (SOFTMAX) {
       f32x2 acc = {0.f, 0.f};
       const f32x2 mx2 = {ra.mx, rb.mx};
+      // the row sums of the fast exps, in the lean form's order (padding slots hold -inf: exp2(-inf) adds +0); the
+      // quotients below take the exact exps (the definition)
 #pragma unroll
-      for (int j = 0; j < 8 * NG; ++j) {
-        // the row sums of the fast exps, in the lean form's order (padding slots hold -inf: exp2(-inf) adds +0)
-        acc = acc + exp_fast2(f32x2{ra.v[j], rb.v[j]}, nml);
-        const f32x2 ex = exp_nonpos2(f32x2{ra.v[j], rb.v[j]} - mx2);  // exact exps for the quotients
-        ra.v[j] = ex.x;
-        rb.v[j] = ex.y;
-      }
+      for (int j = 0; j < 8 * NG; ++j) acc = acc + exp_fast2(f32x2{ra.v[j], rb.v[j]} - mx2);
       sa = wave_sum_uniform(acc.x);
       sb = wave_sum_uniform(acc.y);
       ia = 1.f / sa;
@@ -653,8 +650,9 @@ __device__ __forceinline__ void row_tile_compute(const RowLoads<NG>& L, int64_t 
       fb = fb && __builtin_isfinite(wave_sum_uniform(rb.sum));
       if (row_stats != nullptr) {  // the softmax statistics too, so the class pass can refit a mispredicted batch
         f32x2 acc = {0.f, 0.f};
+        const f32x2 mx2 = {ra.mx, rb.mx};
 #pragma unroll
-        for (int j = 0; j < 8 * NG; ++j) acc = acc + exp_fast2(f32x2{ra.v[j], rb.v[j]}, nml);
+        for (int j = 0; j < 8 * NG; ++j) acc = acc + exp_fast2(f32x2{ra.v[j], rb.v[j]} - mx2);
         sa = wave_sum_uniform(acc.x);
         sb = wave_sum_uniform(acc.y);
       }
@@ -679,7 +677,7 @@ __device__ __forceinline__ void row_tile_compute(const RowLoads<NG>& L, int64_t 
     for (int j = 0; j < 8 * NG; ++j) {
       uint32_t packed;
       if constexpr (SOFTMAX) {
-        packed = pack_rne2<T>(div_rn2(f32x2{ra.v[j], rb.v[j]}, f32x2{sa, sb}, f32x2{ia, ib}));
+        packed = exact_code2<T>(f32x2{ra.v[j], rb.v[j]}, f32x2{ra.mx, rb.mx}, f32x2{sa, sb}, f32x2{ia, ib}, false);
       } else {
         const uint32_t ca = raw_code<T>(raw_bits<T>(wa[j >> 3], j & 7));
         const uint32_t cb = raw_code<T>(raw_bits<T>(wb[j >> 3], j & 7));
@@ -840,7 +838,6 @@ __device__ __forceinline__ void row_tile_softmax_lean(const RowLoads<NG>& L, int
     // exp(x - max): the lean sequence when every element of both rows is within 86 of its maximum (wave-uniform)
     const bool narrow = __ballot(!(mxa - mn_a <= 86.f && mxb - mn_b <= 86.f)) == 0;
     const f32x2 mx2 = {mxa, mxb};
-    const f32x2 nml = {fast_nml(mxa), fast_nml(mxb)};
     f32x2 acc = {0.f, 0.f}, acc_lo = {0.f, 0.f};
     // the partial vector sits in the last class group (nvec - 1 >= 64 when NG == 2): scale its slots by 0 / 1
     auto counted = [&](f32x2 e, int j) -> f32x2 {
@@ -856,10 +853,11 @@ __device__ __forceinline__ void row_tile_softmax_lean(const RowLoads<NG>& L, int
       }
       return e;
     };
-    // the row sums of the fast exps (the scores stay in P for the quotients)
+    // the row sums of the fast exps, which replace the scores in P (wa / wb keep the raw scores for the exact paths)
 #pragma unroll
     for (int j = 0; j < 8 * NG; ++j) {
-      acc = acc + counted(exp_fast2(P[j], nml), j);
+      P[j] = exp_fast2(P[j] - mx2);
+      acc = acc + counted(P[j], j);
       if (j == 7) acc_lo = acc;
     }
     // padding lanes: the group-1 duplicates (NG == 2) or the whole lane (NG == 1) add nothing to the exp-sum
@@ -884,28 +882,36 @@ __device__ __forceinline__ void row_tile_softmax_lean(const RowLoads<NG>& L, int
     }
     const bool ka = va && fa, kb = vb && fb;
     const f32x2 s2 = {sa, sb}, i2 = {ia, ib};
-    // the pair's codes: fast and verified (bf16, narrow rows), else the exact definition
+    // the pair's codes: fast and verified (bf16, narrow rows), else the exact definition from the raw scores
     const bool fast = FastQuot<T>::value && narrow;
     const float ea = fast_eps(mxa, mn_a), eb = fast_eps(mxb, mn_b);
     const f32x2 rlo = {ia - ia * ea, ib - ib * eb}, rhi = {ia + ia * ea, ib + ib * eb};
-    auto code_pair = [&](int j) -> uint32_t {
-      if (fast) return fast_code2<T>(P[j], nml, rlo, rhi, mx2, s2, i2);
-      return pack_rne2<T>(div_rn2(exp_nonpos2(P[j] - mx2), s2, i2));
+    const uint32_t keep = (ka ? 0x0000FFFFu : 0u) | (kb ? 0xFFFF0000u : 0u);
+    const uint32_t setm = ~keep & 0x80008000u;
+    auto raw_pair = [&](int j) -> f32x2 {  // the scores of slot j of both rows (the exact paths: rare)
+      const uint16_t a = raw_bits<T>(wa[j >> 3], j & 7), b = raw_bits<T>(wb[j >> 3], j & 7);
+      return f32x2{to_f32<T>(__builtin_bit_cast(T, a)), to_f32<T>(__builtin_bit_cast(T, b))};
     };
-    if (ka && kb) {  // wave-uniform: both rows counted (the common case) -- no mask
+    auto put = [&](int j, uint32_t code) {
+      const int c = 512 * (j >> 3) + 8 * lane + (j & 7);
+      s_tile[c * kSlots + (p ^ (lane & (kSlots - 1)))] = (code & keep) | setm;
+    };
+    if (fast) {
+      uint32_t redo = 0;  // wave-uniform: slot j has an undecided pair in some lane
 #pragma unroll
       for (int j = 0; j < 8 * NG; ++j) {
-        const int c = 512 * (j >> 3) + 8 * lane + (j & 7);
-        s_tile[c * kSlots + (p ^ (lane & (kSlots - 1)))] = code_pair(j);
+        bool und;
+        put(j, fast_code2<T>(P[j], rlo, rhi, und));
+        redo |= (__ballot(und) != 0 ? 1u : 0u) << j;
+      }
+      if (redo != 0) {  // rare: the undecided slots from the definition (same wave, same lanes: LDS order holds)
+#pragma unroll
+        for (int j = 0; j < 8 * NG; ++j)
+          if ((redo >> j) & 1u) put(j, exact_code2<T>(raw_pair(j), mx2, s2, i2, true));
       }
     } else {
-      const uint32_t keep = (ka ? 0x0000FFFFu : 0u) | (kb ? 0xFFFF0000u : 0u);
-      const uint32_t setm = ~keep & 0x80008000u;
 #pragma unroll
-      for (int j = 0; j < 8 * NG; ++j) {
-        const int c = 512 * (j >> 3) + 8 * lane + (j & 7);
-        s_tile[c * kSlots + (p ^ (lane & (kSlots - 1)))] = (code_pair(j) & keep) | setm;
-      }
+      for (int j = 0; j < 8 * NG; ++j) put(j, exact_code2<T>(raw_pair(j), mx2, s2, i2, narrow));
     }
     if (lane == 0 && pos.hist == nullptr) {
       if (ka && ta >= 0 && ta < C) atomicOr(&s_tile[ta * kSlots + (p ^ ((int)(ta >> 3) & (kSlots - 1)))], 0x00004000u);
@@ -2175,14 +2181,13 @@ __global__ void __launch_bounds__(kSmallRows * TL) TMX_SMALL_WPE_ATTR mc_codes_s
   // mode keeps the scores: they are the codes, the sum only feeds the class pass's refit statistics)
   // round 6: the row sum of the fast exps (csrc/curve_hist_kernels.h fast_code2); the scores stay in P
   const f32x2 m2 = {mx, mx};
-  const f32x2 nml = {fast_nml(mx), fast_nml(mx)};
   // every valid element of every row of the wave within 86 of its maximum: verified fast quotients (bf16)
   const bool narrow = __ballot(!(mx - mn <= 86.f)) == 0;
   auto exp_sum = [&]() -> float {
     f32x2 acc = {0.f, 0.f};
 #pragma unroll
     for (int p = 0; p < kPairs; ++p) {
-      f32x2 e = exp_fast2(P[p], nml);
+      f32x2 e = exp_fast2(P[p] - m2);
       if (masked) {
         e.x = cb + 2 * p < C ? e.x : 0.f;
         e.y = cb + 2 * p + 1 < C ? e.y : 0.f;
@@ -2223,7 +2228,13 @@ __global__ void __launch_bounds__(kSmallRows * TL) TMX_SMALL_WPE_ATTR mc_codes_s
     const f32x2 rlo = {inv - inv * eps, inv - inv * eps}, rhi = {inv + inv * eps, inv + inv * eps};
 #pragma unroll
     for (int p = 0; p < kPairs; ++p) {
-      word[p] = fast ? fast_code2<T>(P[p], nml, rlo, rhi, m2, s2, i2) : pack_rne2<T>(div_rn2(exp_nonpos2(P[p] - m2), s2, i2));
+      if (fast) {
+        bool und;
+        word[p] = fast_code2<T>(exp_fast2(P[p] - m2), rlo, rhi, und);
+        if (__ballot(und) != 0) word[p] = exact_code2<T>(P[p], m2, s2, i2, true);
+      } else {
+        word[p] = exact_code2<T>(P[p], m2, s2, i2, false);
+      }
       if constexpr (TL == 1) word[p] |= ((tl >> 1) == p && tl >= 0 ? tflag : 0u);
     }
   } else {

@@ -258,3 +258,45 @@ def test_mifid_cosine_distance_fused_matches_cpu():
         gpu = _compute_cosine_distance(a.cuda(), b.cuda(), eps).cpu()
         cpu = _compute_cosine_distance(a, b, eps)
         torch.testing.assert_close(gpu, cpu, rtol=1e-5, atol=1e-6)
+
+
+def _ssim_raw(p, t, ks, consts, sse=True):
+    w = torch.exp(-((torch.arange(ks, dtype=torch.float32) - (ks - 1) / 2) ** 2) / (2 * 1.5**2))
+    w = (w / w.sum()).cuda()
+    return torch.ops.tmx.ssim_sums(p, t, w, w, consts.cuda(), sse)
+
+
+@pytest.mark.parametrize("shape", [(5, 257, 300), (3, 129, 1020), (2, 64, 64), (4, 1024, 1024), (1, 40, 2052)])
+@pytest.mark.parametrize("ks", [3, 7, 11, 15])
+@pytest.mark.parametrize("rng", [1.0, 255.0])
+def test_ssim_mfma_vs_fp32_kernel(shape, ks, rng):
+    """Round 6: the matrix-core SSIM kernel (fp16-split banded products, consts = c1, c2, data range) against the fp32
+    VALU kernel (consts = c1, c2) on the same planes: per-plane mean SSIM / CS within 1e-6, SSE equal."""
+    g = torch.Generator(device="cuda").manual_seed(sum(shape) + ks)
+    t = torch.rand(*shape, device="cuda", generator=g) * rng
+    p = (t + 0.1 * rng * torch.randn(*shape, device="cuda", generator=g)).clamp(0, rng)
+    if rng == 255.0:
+        p, t = p.round(), t.round()
+    c = torch.tensor([(0.01 * rng) ** 2, (0.03 * rng) ** 2, rng])
+    fast = _ssim_raw(p, t, ks, c)
+    ref = _ssim_raw(p, t, ks, c[:2])
+    nv = (shape[1] - ks + 1) * (shape[2] - ks + 1)
+    torch.testing.assert_close(fast[:2] / nv, ref[:2] / nv, rtol=0, atol=1e-6)
+    torch.testing.assert_close(fast[2], ref[2], rtol=1e-12, atol=0)
+
+
+@pytest.mark.parametrize("bad", ["range", "nan", "inf"])
+def test_ssim_mfma_falls_back_on_device(bad):
+    """Data outside the kernel's fp16 operand range (here 10x the stated data range), NaN or inf: the fallback launch of
+    the fp32 kernel runs on the device (no host synchronisation) and its sums are returned, bit for bit."""
+    g = torch.Generator(device="cuda").manual_seed(5)
+    t = torch.rand(3, 100, 128, device="cuda", generator=g)
+    p = t.clone()
+    if bad == "range":
+        p = p * 10
+    else:
+        p[1, 50, 60] = float("nan") if bad == "nan" else float("inf")
+    c = torch.tensor([1e-4, 9e-4, 1.0])
+    fast = _ssim_raw(p, t, 11, c)
+    ref = _ssim_raw(p, t, 11, c[:2])
+    torch.testing.assert_close(fast, ref, rtol=0, atol=0, equal_nan=True)

@@ -101,3 +101,37 @@ def test_map_batched_update_refuses_mixed_dtypes():
     m.update(preds, target)
     assert m.detection_labels[0].dtype == torch.int32
     assert m.detection_labels[1].dtype == torch.int64
+
+
+def test_map_batched_update_views_and_lazy_items_match_per_image_path():
+    """Round 6: a batch whose per-image tensors are rows of one batch tensor is concatenated without a copy
+    (csrc/rows_host.cpp cat_rows), the per-image items stay lazy until used, and compute / state_dict equal the
+    per-image path's."""
+    from torchmetrics_forked_amd import ops
+    from torchmetrics_forked_amd.detection import MeanAveragePrecision
+
+    g = torch.Generator().manual_seed(3)
+    n, k = 6, 5
+    xy = torch.rand(n, k, 2, generator=g) * 50
+    boxes = torch.cat([xy, xy + 5 + torch.rand(n, k, 2, generator=g) * 20], -1)
+    scores = torch.rand(n, k, generator=g)
+    labels = torch.randint(0, 3, (n, k), generator=g)
+    preds = [{"boxes": boxes[i], "scores": scores[i], "labels": labels[i]} for i in range(n)]
+    target = [{"boxes": boxes[i] + 1, "labels": labels[i]} for i in range(n)]
+    a, b = MeanAveragePrecision(), MeanAveragePrecision()
+    assert a._update_batched(preds, target)
+    if ops.load():
+        assert a.detection_scores.pieces()[0].untyped_storage().data_ptr() == scores.untyped_storage().data_ptr()
+        assert list.__len__(a.detection_scores) == 0 and len(a.detection_scores) == n
+    for p, t in zip(preds, target):
+        b.update([p], [t])
+    ra, rb = a.compute(), b.compute()
+    for key in rb:
+        torch.testing.assert_close(ra[key], rb[key])
+    sa, sb = a.state_dict(), b.state_dict()
+    assert set(sa) == set(sb)
+    a.persistent(True)
+    b.persistent(True)
+    sa, sb = a.state_dict(), b.state_dict()
+    for key in sb:
+        assert len(sa[key]) == len(sb[key]) and all(torch.equal(x, y) for x, y in zip(sa[key], sb[key]))

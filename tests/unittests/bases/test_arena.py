@@ -240,3 +240,39 @@ def test_runs_are_dropped_by_mutation_and_copies_stay_exact():
     d = pickle.loads(pickle.dumps(b))
     _check_runs(d)
     assert torch.equal(torch.cat(d.pieces()), torch.cat(b.pieces()))
+
+
+def test_lazy_runs_materialise_on_first_item_access():
+    """Round 6: extend_rows(lazy=True) records runs without per-item views; len / pieces / item_rows / cat work from
+    the runs, any item access or mutation materialises every item in order, pickles hold the per-item tensors."""
+    import pickle
+
+    from torchmetrics_forked_amd.utilities.arena import StateArena
+
+    a = StateArena()
+    f1, f2 = torch.arange(12.0).reshape(6, 2), torch.arange(12.0, 20.0).reshape(4, 2)
+    a.extend_rows(f1, [2, 4], lazy=True)
+    a.extend_rows(f2, [1, 3], lazy=True)
+    assert len(a) == 4 and bool(a) and list.__len__(a) == 0
+    assert [p.shape[0] for p in a.pieces()] == [6, 4] and a.item_rows() == [2, 4, 1, 3]
+    torch.testing.assert_close(a.cat(), torch.cat([f1, f2]))
+    assert list.__len__(a) == 0  # cat kept them pending
+    back = pickle.loads(pickle.dumps(a))
+    assert [t.shape[0] for t in back] == [2, 4, 1, 3]
+    assert torch.equal(a[2], f2[:1]) and list.__len__(a) == 4
+    a.append(torch.ones(5, 2))
+    assert len(a) == 5 and a.item_rows()[-1] == 5
+    torch.testing.assert_close(torch.cat(list(a)), torch.cat([f1, f2, torch.ones(5, 2)]))
+
+
+def test_lazy_runs_only_while_nothing_is_materialised():
+    from torchmetrics_forked_amd.utilities.arena import StateArena
+
+    a = StateArena()
+    a.append(torch.zeros(3))
+    a.extend_rows(torch.arange(4.0), [1, 3], lazy=True)  # items exist already: eager
+    assert list.__len__(a) == 3 and len(a) == 3
+    b = StateArena()
+    b.extend_rows(torch.arange(4.0), [1, 3], lazy=True)
+    b.extend_rows(torch.arange(2.0), [2], lazy=True)
+    assert [t.tolist() for t in b] == [[0.0], [1.0, 2.0, 3.0], [0.0, 1.0]]

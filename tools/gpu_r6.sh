@@ -67,6 +67,8 @@ for s in "$@"; do
     mapprof) run mapprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/mapprof" -o map --output-format csv -- python3 bench.py --config map --steps 5 --warmup 1; tail -1 "$OUT/mapprof.log" ;;
     sweep) run sweep 300 python tools/class_count_sweep.py; tail -3 "$OUT/sweep.log" ;;
     pmc) run pmc 200 rocprofv3 --kernel-trace --pmc ${TMX_PMC:-SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU} -d "$OUT/pmc" -o pmc --output-format csv -- python3 bench.py --steps 5 --warmup 2; tail -1 "$OUT/pmc.log" ;;
+    wtrace) run wtrace 200 python tools/window_trace.py; tail -c 3000 "$OUT/wtrace.log" ;;
+    fwdbench) run fwdbench 200 python tools/forward_bench.py; tail -c 1500 "$OUT/fwdbench.log" ;;
     *) echo "unknown step $s" ;;
   esac
 done

@@ -73,15 +73,27 @@ def run_rank(impl: str, mode: str, steps: int, warmup: int, world: int, rank: in
     t0 = time.perf_counter()
     for i in range(steps):
         step(*pool[i % 64])
-    t_upd = time.perf_counter() - t0
+    t1 = time.perf_counter()
     res = metric.compute()
+    t2 = time.perf_counter()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    t = torch.tensor([elapsed, t_upd], dtype=torch.float64)
+    # per-rank pieces, reduced separately (round 6): a rank whose loop finishes early waits inside compute()'s
+    # collective for the slow one -- that wait is the loop skew, not compute work.  compute_own_s = this rank's
+    # compute() call minus the time it spent waiting for the slowest rank's loop to end.
+    upd, comp = t1 - t0, t2 - t1
+    t = torch.tensor([elapsed, upd, upd, comp], dtype=torch.float64)
     if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return {"elapsed": float(t[0]), "update_s": float(t[1]), "value_result": float(res)}
+        tmax, tmin = t.clone(), t.clone()
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        dist.all_reduce(tmin, op=dist.ReduceOp.MIN)
+        wait = float(tmax[1]) - upd  # how long this rank's compute waited for the slowest loop (lower bound)
+        own = torch.tensor([max(comp - wait, 0.0)], dtype=torch.float64)
+        dist.all_reduce(own, op=dist.ReduceOp.MAX)
+        return {"elapsed": float(tmax[0]), "update_s": float(tmax[1]), "update_min_s": float(tmin[2]), "compute_s": float(tmax[3]),
+                "compute_own_s": float(own[0]), "value_result": float(res)}
+    return {"elapsed": elapsed, "update_s": upd, "update_min_s": upd, "compute_s": comp, "compute_own_s": comp, "value_result": float(res)}
 
 
 def _report(impl: str, mode: str, steps: int, warmup: int, world: int, r: dict) -> dict:
@@ -97,6 +109,9 @@ def _report(impl: str, mode: str, steps: int, warmup: int, world: int, r: dict) 
         "us_per_step_incl_compute": round(1e6 * r["elapsed"] / steps, 2),
         "us_per_step_loop_only": round(1e6 * r["update_s"] / steps, 2),
         "compute_incl_sync_us": round(1e6 * (r["elapsed"] - r["update_s"]), 1),
+        "compute_call_us_max_rank": round(1e6 * r["compute_s"], 1),
+        "compute_own_us": round(1e6 * r["compute_own_s"], 1),
+        "loop_skew_us": round(1e6 * (r["update_s"] - r["update_min_s"]), 1),
         "result": r["value_result"],
         "threads_per_rank": 1,
         "data": "synthetic fp32 logits [10, 5] + int64 labels, 64-batch pool per rank",

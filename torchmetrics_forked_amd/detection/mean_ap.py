@@ -183,26 +183,39 @@ class MeanAveragePrecision(Metric):
         if not all(isinstance(st, StateArena) for st in states):
             return False
         try:
-            db = [p["boxes"] for p in preds]
-            ds = [p["scores"] for p in preds]
-            dl = [p["labels"] for p in preds]
-            gb = [t["boxes"] for t in target]
-            gl = [t["labels"] for t in target]
+            cols = ([p["boxes"] for p in preds], [p["scores"] for p in preds], [p["labels"] for p in preds],
+                    [t["boxes"] for t in target], [t["labels"] for t in target])
             n_crowd = sum("iscrowd" in t for t in target)
             n_area = sum("area" in t for t in target)
             if n_crowd not in (0, len(target)) or n_area not in (0, len(target)):
                 return False
-            dn = [t.shape[0] for t in dl]  # (Tensor.__len__ is a Python-level method: 5x the cost of .shape)
-            gn = [t.shape[0] for t in gl]
-            if dn != [t.shape[0] for t in db] or dn != [t.shape[0] for t in ds] or gn != [t.shape[0] for t in gb] or 0 in dn or 0 in gn:
-                return False
-            # one dtype per column: a concatenation would promote mixed images, where the per-image path (and the
-            # reference) keeps each image's own tensors
-            if any(len({t.dtype for t in col}) != 1 for col in (db, ds, dl, gb, gl)):
-                return False
-            flats = [torch.cat(col) for col in (db, ds, dl, gb, gl)]
-            crowd = torch.cat([t["iscrowd"] for t in target]) if n_crowd else None
-            area = torch.cat([t["area"] for t in target]) if n_area else None
+            extra = ([t["iscrowd"] for t in target] if n_crowd else None, [t["area"] for t in target] if n_area else None)
+            if ops.load():
+                # one C++ pass per column: every item of one dtype / device / shape, row counts, and the concatenation
+                # (a view when the items are consecutive rows of one batch tensor) -- csrc/rows_host.cpp cat_rows
+                res = [torch.ops.tmx.cat_rows(col, w) for col, w in zip(cols, (4, 0, 0, 4, 0))]
+                res_x = [torch.ops.tmx.cat_rows(col, 0) if col is not None else None for col in extra]
+                if any(r[1].numel() == 0 for r in res) or any(r is not None and r[1].numel() == 0 for r in res_x):
+                    return False
+                dn, gn = res[2][1].tolist(), res[4][1].tolist()
+                if (dn != res[0][1].tolist() or dn != res[1][1].tolist() or gn != res[3][1].tolist()
+                        or any(r is not None and r[1].tolist() != gn for r in res_x)):
+                    return False
+                flats = [r[0] for r in res]
+                crowd, area = (r[0] if r is not None else None for r in res_x)
+            else:
+                db, ds, dl, gb, gl = cols
+                dn = [t.shape[0] for t in dl]  # (Tensor.__len__ is a Python-level method: 5x the cost of .shape)
+                gn = [t.shape[0] for t in gl]
+                if dn != [t.shape[0] for t in db] or dn != [t.shape[0] for t in ds] or gn != [t.shape[0] for t in gb] or 0 in dn or 0 in gn:
+                    return False
+                # one dtype per column: a concatenation would promote mixed images, where the per-image path (and the
+                # reference) keeps each image's own tensors
+                if any(len({t.dtype for t in col}) != 1 for col in cols):
+                    return False
+                flats = [torch.cat(col) for col in cols]
+                crowd = torch.cat(extra[0]) if n_crowd else None
+                area = torch.cat(extra[1]) if n_area else None
         except (KeyError, TypeError, RuntimeError, ValueError, IndexError, AttributeError):
             return False
         det_box, det_score, det_label, gt_box, gt_label = flats
@@ -217,13 +230,14 @@ class MeanAveragePrecision(Metric):
             area = torch.zeros_like(gt_label)
         if self.warn_on_many_detections and max(dn) > self.max_detection_thresholds[-1]:
             _warning_on_too_many_detections(self.max_detection_thresholds[-1])
-        self.detection_box.extend_rows(box_convert(det_box, in_fmt=self.box_format, out_fmt="xywh"), dn)
-        self.detection_scores.extend_rows(det_score, dn)
-        self.detection_labels.extend_rows(det_label, dn)
-        self.groundtruth_box.extend_rows(box_convert(gt_box, in_fmt=self.box_format, out_fmt="xywh"), gn)
-        self.groundtruth_labels.extend_rows(gt_label, gn)
-        self.groundtruth_crowds.extend_rows(crowd, gn)
-        self.groundtruth_area.extend_rows(area, gn)
+        # lazy runs: the per-image items are views created at their first use (state_dict, list access), not here
+        self.detection_box.extend_rows(box_convert(det_box, in_fmt=self.box_format, out_fmt="xywh"), dn, lazy=True)
+        self.detection_scores.extend_rows(det_score, dn, lazy=True)
+        self.detection_labels.extend_rows(det_label, dn, lazy=True)
+        self.groundtruth_box.extend_rows(box_convert(gt_box, in_fmt=self.box_format, out_fmt="xywh"), gn, lazy=True)
+        self.groundtruth_labels.extend_rows(gt_label, gn, lazy=True)
+        self.groundtruth_crowds.extend_rows(crowd, gn, lazy=True)
+        self.groundtruth_area.extend_rows(area, gn, lazy=True)
         return True
 
     def _convert_boxes(self, boxes: List[Tensor]) -> List[Tensor]:
@@ -268,7 +282,7 @@ class MeanAveragePrecision(Metric):
     def _get_classes(self) -> List:
         if len(self.detection_labels) > 0 or len(self.groundtruth_labels) > 0:
             parts = [
-                self._flat_cached(lst, sum(_item_sizes(lst)), torch.long, lst[0].device)
+                self._flat_cached(lst, sum(_item_sizes(lst)), torch.long, _first(lst).device)
                 for lst in (self.detection_labels, self.groundtruth_labels)
                 if len(lst)
             ]
@@ -301,7 +315,7 @@ class MeanAveragePrecision(Metric):
         thresholds; anything else (and CPU states) takes the host evaluator ``tmx::coco_evaluate``."""
         if not self.groundtruth_labels and not self.detection_labels:
             return False
-        sample = (self.detection_labels or self.groundtruth_labels)[0]
+        sample = _first(self.detection_labels or self.groundtruth_labels)
         if not (sample.is_cuda and ops.use_native(sample)):
             return False
         return self._gpu_eligible_params()
@@ -336,7 +350,7 @@ class MeanAveragePrecision(Metric):
     def _evaluate_gpu(self, i_type: str, average: str, classes: List[int]) -> _EvalResult:
         """Flatten the per-image states on the device and run ``tmx::coco_evaluate_gpu`` (csrc/coco_match.hip):
         matching and accumulation never leave the GPU; one small host read sizes the IoU export."""
-        dev = (self.detection_labels or self.groundtruth_labels)[0].device
+        dev = _first(self.detection_labels or self.groundtruth_labels).device
         num_images = len(self.groundtruth_labels)
         det_sizes = _item_sizes(self.detection_labels)
         gt_sizes = _item_sizes(self.groundtruth_labels)
@@ -857,9 +871,14 @@ def _flat_rows(lst: List[Tensor], n: int, dtype: torch.dtype, dev: torch.device,
 
 def _item_sizes(lst: List[Tensor]) -> List[int]:
     """``numel`` of every per-image item (the arena's run records when it has them: no per-item tensor call)."""
-    if isinstance(lst, StateArena) and lst._runs is not None and all(t.ndim == 1 for t in lst[:1]):
+    if isinstance(lst, StateArena) and lst._runs is not None and (not lst._runs or lst._runs[0][0].ndim == 1):
         return lst.item_rows()
     return [t.numel() for t in lst]
+
+
+def _first(lst: List[Tensor]) -> Tensor:
+    """The first per-image item's tensor (a run of a lazy arena: same device and dtype, no item materialised)."""
+    return lst.first_piece() if isinstance(lst, StateArena) else lst[0]
 
 
 def _pack_rle_states(states: List[Tuple[Tuple[Tuple[int, int], bytes], ...]], device: torch.device) -> List[Tensor]:

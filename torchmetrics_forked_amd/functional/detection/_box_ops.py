@@ -30,9 +30,10 @@ def box_convert(boxes: Tensor, in_fmt: str, out_fmt: str) -> Tensor:
         raise ValueError(f"Unsupported box format {in_fmt}")
     if out_fmt == "xyxy":
         return xyxy
+    if out_fmt == "xywh":  # (two kernels instead of unbind + two subtractions + stack; the same values)
+        lo = xyxy[..., :2]
+        return torch.cat([lo, xyxy[..., 2:] - lo], dim=-1)
     x0, y0, x1, y1 = xyxy.unbind(-1)
-    if out_fmt == "xywh":
-        return torch.stack([x0, y0, x1 - x0, y1 - y0], dim=-1)
     if out_fmt == "cxcywh":
         return torch.stack([(x0 + x1) / 2, (y0 + y1) / 2, x1 - x0, y1 - y0], dim=-1)
     raise ValueError(f"Unsupported box format {out_fmt}")

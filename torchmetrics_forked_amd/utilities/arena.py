@@ -21,6 +21,13 @@ previous capacity.  Over any sequence of appends and reads every sample is copie
   item is covered by runs, ``pieces()`` hands consumers the run tensors instead of the items (5 pieces to concatenate
   instead of 2,560 per-image views for MeanAveragePrecision after five 512-image updates) and ``item_rows()`` the
   per-item row counts without touching the items.
+* ``extend_rows(flat, sizes, lazy=True)`` on an arena without materialised items (round 6) records the run WITHOUT
+  creating its per-item views (3,584 Python tensor objects per 512-image detection update, ~0.9 ms of host time):
+  the items are materialised -- split views of the runs -- at the first access that needs them (indexing, iteration,
+  any mutation, pickling, ``state_dict``), while ``len()``, ``pieces()``, ``item_rows()`` and ``cat()`` work from the
+  runs.  Until then the list storage underneath is empty: C-level readers that bypass the Python protocol (e.g.
+  ``torch.cat(state)`` on the raw list) see no items -- the package's consumers go through ``dim_zero_cat`` /
+  ``pieces()``.
 * ``cat()`` returns a view of the state; internal consumers treat it as read-only, as they treat a tensor state.
   ``Metric.compute`` copies any result that aliases an arena buffer before handing it to the user (the reference's
   ``dim_zero_cat`` always returns a fresh ``torch.cat``).
@@ -35,7 +42,7 @@ from torch import Tensor
 class StateArena(list):
     """A list of tensors with a lazily compacted, growable backing buffer (see module docstring)."""
 
-    __slots__ = ("_buf", "_rows", "_covered", "clean", "_runs")
+    __slots__ = ("_buf", "_rows", "_covered", "clean", "_runs", "_pend", "_npend")
 
     def __init__(self, items: Iterable[Any] = ()) -> None:
         super().__init__(items)
@@ -47,7 +54,77 @@ class StateArena(list):
         self.clean = 0
         # (flat [rows, *tail] tensor, per-item row counts) per appended batch, in item order; None once an item is
         # not covered (constructed from items, or mutated other than by append / extend)
-        self._runs: Optional[List[Tuple[Tensor, List[int]]]] = None if len(self) else []
+        self._runs: Optional[List[Tuple[Tensor, List[int]]]] = None if list.__len__(self) else []
+        # runs recorded by extend_rows(lazy=True) whose items are not materialised yet (the list storage is empty then)
+        self._pend: List[Tuple[Tensor, List[int]]] = []
+        self._npend = 0
+
+    # ------------------------------------------------------------------------------------------ lazy items
+    def _materialize(self) -> None:
+        """Create the pending runs' items (split views), in order, after which the list storage holds every item."""
+        if self._npend:
+            pend, self._pend, self._npend = self._pend, [], 0
+            for flat, sizes in pend:
+                list.extend(self, torch.split(flat, sizes))
+
+    def __len__(self) -> int:
+        return list.__len__(self) + self._npend
+
+    def __bool__(self) -> bool:
+        return self._npend > 0 or list.__len__(self) > 0
+
+    def __getitem__(self, i: Any) -> Any:
+        self._materialize()
+        return list.__getitem__(self, i)
+
+    def __iter__(self):  # type: ignore[override]
+        self._materialize()
+        return list.__iter__(self)
+
+    def __reversed__(self):  # type: ignore[override]
+        self._materialize()
+        return list.__reversed__(self)
+
+    def __contains__(self, x: Any) -> bool:
+        self._materialize()
+        return list.__contains__(self, x)
+
+    def __repr__(self) -> str:
+        self._materialize()
+        return list.__repr__(self)
+
+    def __eq__(self, other: Any) -> bool:  # type: ignore[override]
+        self._materialize()
+        if isinstance(other, StateArena):
+            other._materialize()
+        return list.__eq__(self, other)
+
+    def __ne__(self, other: Any) -> bool:  # type: ignore[override]
+        return not self.__eq__(other)
+
+    __hash__ = None  # type: ignore[assignment]
+
+    def __add__(self, other: Any) -> List[Any]:  # type: ignore[override]
+        self._materialize()
+        return list.__add__(self, other)
+
+    def __mul__(self, n: Any) -> List[Any]:  # type: ignore[override]
+        self._materialize()
+        return list.__mul__(self, n)
+
+    __rmul__ = __mul__
+
+    def index(self, *args: Any) -> int:  # type: ignore[override]
+        self._materialize()
+        return list.index(self, *args)
+
+    def count(self, x: Any) -> int:  # type: ignore[override]
+        self._materialize()
+        return list.count(self, x)
+
+    def copy(self) -> List[Any]:  # type: ignore[override]
+        self._materialize()
+        return list.copy(self)
 
     # ---------------------------------------------------------------------------------------------- helpers
     @staticmethod
@@ -80,6 +157,7 @@ class StateArena(list):
 
     # ------------------------------------------------------------------------------------------ list protocol
     def append(self, t: Any) -> None:  # type: ignore[override]
+        self._materialize()
         self._append(t)
         runs = self._runs
         if runs is not None:
@@ -101,15 +179,23 @@ class StateArena(list):
             super().append(t)
 
     def extend(self, items: Iterable[Any]) -> None:  # type: ignore[override]
+        self._materialize()
         if self._buf is None and self._runs is None:  # plain-list mode: nothing to copy into, nothing to record
             list.extend(self, items)
             return
         for t in items:
             self.append(t)
 
-    def extend_rows(self, flat: Tensor, sizes: List[int]) -> None:
+    def extend_rows(self, flat: Tensor, sizes: List[int], lazy: bool = False) -> None:
         """Append ``torch.split(flat, sizes)`` (items of ``sizes[i]`` rows each) and record them as one run: one copy
-        into the buffer's free tail when it has room, else the split views themselves (zero-copy)."""
+        into the buffer's free tail when it has room, else the split views themselves (zero-copy).  ``lazy``: while
+        no item is materialised, only record the run (the items are created at their first use)."""
+        if lazy and self._runs is not None and list.__len__(self) == 0 and self._buf is None:
+            self._pend.append((flat, list(sizes)))
+            self._npend += len(sizes)
+            self._runs.append((flat, list(sizes)))
+            return
+        self._materialize()
         if self._covered == len(self) and self._fits(flat):
             rows = flat.shape[0]
             dst = self._buf[self._rows : self._rows + rows]  # type: ignore[index]
@@ -125,9 +211,15 @@ class StateArena(list):
         """Tensors whose dim-0 concatenation equals the items' (0-d items as 1 row): the run tensors while every
         item is covered by a run, else the items."""
         runs = self._runs
-        if runs is not None and len(runs) < len(self):
+        if runs is not None and (self._npend or len(runs) < len(self)):
             return [f for f, _ in runs]
         return [t.unsqueeze(0) if isinstance(t, Tensor) and t.ndim == 0 else t for t in self]
+
+    def first_piece(self) -> Any:
+        """The first run tensor (or item) without materialising pending items: device / dtype probes."""
+        if self._runs:
+            return self._runs[0][0]
+        return self[0]
 
     def item_rows(self) -> List[int]:
         """Rows per item (``numel`` of 1-d items), from the runs' records when every item is covered."""
@@ -147,6 +239,7 @@ class StateArena(list):
         base = getattr(list, name)
 
         def method(self: "StateArena", *args: Any, **kwargs: Any) -> Any:
+            self._materialize()
             self._drop()
             self.clean = 0
             self._runs = None if name != "clear" else []
@@ -170,6 +263,7 @@ class StateArena(list):
         """A new arena with ``other``'s items that takes over its buffer (and free tail); ``other`` keeps its items
         (views of the untouched prefix) but no longer appends into that buffer, so a list that is still shared
         elsewhere is never extended behind its holders' backs."""
+        other._materialize()
         out = cls(other)
         out.clean = other.clean
         if other._runs is not None:
@@ -181,6 +275,7 @@ class StateArena(list):
 
     def truncate(self, k: int) -> None:
         """Drop the items from ``k`` on, keeping the buffer (and its free tail) when it covers the first ``k``."""
+        self._materialize()
         k = max(0, min(k, len(self)))
         self.clean = min(self.clean, k)
         if k < len(self):
@@ -199,6 +294,15 @@ class StateArena(list):
             raise ValueError("No samples to concatenate")
         if self._buf is not None and self._covered == len(self):
             return self._buf[: self._rows]
+        if self._npend and list.__len__(self) == 0:
+            # every item still pending: compact the runs, and keep the items pending as views of the new buffer
+            runs = self._runs or self._pend
+            flats = [f for f, _ in runs]
+            sizes = [k for _, sz in runs for k in sz]
+            buf = flats[0] if len(flats) == 1 else torch.cat(flats, dim=0)
+            self._pend = [(buf, sizes)]
+            self._runs = [(buf, list(sizes))]
+            return buf
         if not self._compactable():
             return torch.cat([t.unsqueeze(0) if t.ndim == 0 else t for t in self], dim=0)
         first = self[0]
@@ -234,12 +338,14 @@ class StateArena(list):
     # ------------------------------------------------------------------------------- copies and serialisation
     def compact_items(self) -> List[Any]:
         """Independent copies of the items (checkpoints hold one storage per item, as the reference's lists)."""
+        self._materialize()
         return [t.detach().clone() if isinstance(t, Tensor) else deepcopy(t) for t in self]
 
     def __reduce_ex__(self, protocol: int) -> Any:
         return (StateArena, (self.compact_items(),))
 
     def __deepcopy__(self, memo: dict) -> "StateArena":
+        self._materialize()
         out = StateArena()
         if self._buf is not None and self._covered == len(self) and all(not t.requires_grad for t in self):
             buf = self._buf.clone()
