@@ -1933,6 +1933,9 @@ __device__ __forceinline__ long long shfl_up_i64(long long v, int off) {
   return (static_cast<long long>(hi) << 32) | static_cast<unsigned int>(lo);
 }
 
+// CLEAR (forward()'s batch histogram, round 6): every read segment is zeroed behind the read and the class's range
+// emptied, so the scratch is ready for the next batch without the separate zero + range-reset launches.
+template <bool CLEAR = false>
 __global__ void __launch_bounds__(kRedThreads) curve_hist_reduce_kernel(const int64_t* __restrict__ hist,
                                                                          const int* __restrict__ code_range,
                                                                          double* __restrict__ out) {
@@ -1964,6 +1967,15 @@ __global__ void __launch_bounds__(kRedThreads) curve_hist_reduce_kernel(const in
           const longlong2 a = posv[v], b = negv[v];
           p[kRedPer - 1 - 2 * v] = a.x; p[kRedPer - 2 - 2 * v] = a.y;
           n[kRedPer - 1 - 2 * v] = b.x; n[kRedPer - 2 - 2 * v] = b.y;
+        }
+        if constexpr (CLEAR) {  // (codes of the aligned segment outside [lo, hi] are zero already)
+          longlong2* pw = const_cast<longlong2*>(posv);
+          longlong2* nw = const_cast<longlong2*>(negv);
+#pragma unroll
+          for (int v = 0; v < kRedPer / 2; ++v) {
+            pw[v] = make_longlong2(0, 0);
+            nw[v] = make_longlong2(0, 0);
+          }
         }
       } else {
 #pragma unroll
@@ -2013,6 +2025,11 @@ __global__ void __launch_bounds__(kRedThreads) curve_hist_reduce_kernel(const in
     out[c * 4 + 1] = P > 0 ? b / (double)P : NAN;
     out[c * 4 + 2] = (double)P;
     out[c * 4 + 3] = (double)N;
+    if constexpr (CLEAR) {  // every thread read lo / hi at the start (the barrier above orders this after them)
+      int* cr = const_cast<int*>(code_range);
+      cr[2 * c] = K;
+      cr[2 * c + 1] = -1;
+    }
   }
 }
 
@@ -2076,7 +2093,8 @@ __global__ void __launch_bounds__(kSumThreads) curve_summary_kernel(const double
   curve_summary_block(sc, C, summary);
 }
 
-at::Tensor curve_hist_reduce(const at::Tensor& hist_, c10::optional<at::Tensor> code_range) {
+at::Tensor curve_hist_reduce_impl(const at::Tensor& hist_, c10::optional<at::Tensor> code_range, bool clear) {
+  TORCH_CHECK(!clear || (hist_.is_contiguous() && code_range.has_value()), "curve_hist_reduce: clear needs a contiguous histogram and its range");
   auto hist = hist_.contiguous();
   TORCH_CHECK(hist.scalar_type() == at::kLong && hist.dim() == 3 && hist.size(1) == 2 && hist.size(2) == kCodes,
               "curve_hist_reduce: hist must be int64 [C, 2, 16384]");
@@ -2089,9 +2107,16 @@ at::Tensor curve_hist_reduce(const at::Tensor& hist_, c10::optional<at::Tensor> 
   const int C = static_cast<int>(hist.size(0));
   auto out = at::empty({C, 4}, hist.options().dtype(at::kDouble));
   if (C == 0) return out;
-  hipLaunchKernelGGL(curve_hist_reduce_kernel, C, kRedThreads, 0, stream(), hist.data_ptr<int64_t>(), cr, out.data_ptr<double>());
+  if (clear)
+    hipLaunchKernelGGL(curve_hist_reduce_kernel<true>, C, kRedThreads, 0, stream(), hist.data_ptr<int64_t>(), cr, out.data_ptr<double>());
+  else
+    hipLaunchKernelGGL(curve_hist_reduce_kernel<false>, C, kRedThreads, 0, stream(), hist.data_ptr<int64_t>(), cr, out.data_ptr<double>());
   TMX_LAUNCH_CHECK();
   return out;
+}
+
+at::Tensor curve_hist_reduce(const at::Tensor& hist, c10::optional<at::Tensor> code_range) {
+  return curve_hist_reduce_impl(hist, code_range, false);
 }
 
 at::Tensor curve_summary(const at::Tensor& scores_);
@@ -2100,8 +2125,8 @@ at::Tensor curve_summary(const at::Tensor& scores_);
 // the reduce's last class block (device-wide completion counter) measured 33.7 us against 12.4 + 5.1 us -- every
 // block's agent-scope release fence has to write back its XCD's L2 (tests/test_compute_fused_gpu.py keeps the op's
 // contract; README round 4).
-std::vector<at::Tensor> curve_hist_scores(const at::Tensor& hist, c10::optional<at::Tensor> code_range) {
-  auto sc = curve_hist_reduce(hist, code_range);
+std::vector<at::Tensor> curve_hist_scores(const at::Tensor& hist, c10::optional<at::Tensor> code_range, bool clear) {
+  auto sc = curve_hist_reduce_impl(hist, code_range, clear);
   return {sc, curve_summary(sc)};
 }
 
@@ -2754,7 +2779,7 @@ TORCH_LIBRARY_FRAGMENT(tmx, m) {
   m.def("curve_hist_zero(Tensor(a!) hist, Tensor(b!) code_range) -> ()");
   m.def("curve_hist_reduce(Tensor hist, Tensor? code_range=None) -> Tensor");
   m.def("curve_summary(Tensor scores) -> Tensor");
-  m.def("curve_hist_scores(Tensor hist, Tensor? code_range=None) -> Tensor[]");
+  m.def("curve_hist_scores(Tensor(a!) hist, Tensor(b!)? code_range=None, bool clear=False) -> Tensor[]");
   m.def("curve_mc_rowpass(Tensor preds, Tensor target, Tensor(a!) mode, Tensor(b!) state, Tensor(c!) codes, Tensor(d!) slow_rows, int ignore_index, bool has_ignore, Tensor(e!)? confmat, Tensor(f!)? err_flag) -> ()");
   m.def("binned_curve_update(Tensor preds, Tensor target, Tensor thresholds, Tensor(a!) confmat, int task, int ignore_index, bool has_ignore, Tensor? norm_flag, Tensor(b!)? err_flag=None) -> ()");
   m.def("ce_bins_update(Tensor conf, Tensor acc, Tensor boundaries, Tensor(a!) bins) -> ()");

@@ -250,9 +250,10 @@ __device__ __forceinline__ f32x2 exp_nonpos2_narrow(f32x2 x) {
 // class pass's refit reads s from row_stats, so every route produces the same codes for one batch.
 // The quotient of the common case (bf16, every element within 86 of its row maximum) is taken FAST and VERIFIED:
 // with r = 1 / s (correctly rounded) and d = RN(x - max), the exact quotient lies in [e_f r (1 - eps), e_f r (1 + eps)]:
-//   |RN(d L) - d log2e| <= 2^-23 |d| log2e -> |e_f / 2^(d log2e) - 1| <= 2^-23 |d| + v_exp_f32's 1 ulp,
+//   |RN(d L) - d log2e| <= 2^-24 |d| log2e (1 + 0.24)   (RN(d L) and L = log2e (1 + 0.24 2^-24))
+//     -> |e_f / exp(d) - 1| <= 1.24 2^-24 |d| + v_exp_f32's 1 ulp (2^-23),
 //   |exp_nonpos(d) / exp(d) - 1| <= 1 ulp, |r s - 1| <= 2^-24, and the roundings of r (1 -+ eps) <= 2^-24 each,
-// so eps = 2^-24 (2 (max - lane min) + 12) bounds it with room to spare.  RNE16 and fp32 rounding are monotone: when
+// so eps = 2^-24 (1.25 (max - lane min) + 8) bounds it (the ulp terms in units of 2^-24: 2 + 2 + 1 + 1).  RNE16 and fp32 rounding are monotone: when
 // RNE16(fl(e_f r_lo)) == RNE16(fl(e_f r_hi)) the exact quotient rounds to that same code.  The element pairs where any
 // lane is undecided (~7 % of the pair slots of randn logits at C = 1000, 1e-3 of the elements) are collected in a
 // wave-uniform bit mask and recomputed with the exact sequence after the pass, patching the LDS image.  Per element
@@ -260,12 +261,15 @@ __device__ __forceinline__ f32x2 exp_nonpos2_narrow(f32x2 x) {
 // for the exact exp + correctly rounded division.  fp16 keeps the exact quotient (its 10-bit codes put 8x as many
 // rounding boundaries in the window).
 constexpr float kLog2eF = 1.44269502163f;  // RN(log2 e) = 0x3fb8aa3b
+#ifndef TMX_FASTQ_RELOAD
+#define TMX_FASTQ_RELOAD 1  // the fallback re-reads the scores (1) or keeps the raw vectors in registers (0)
+#endif
 __device__ __forceinline__ f32x2 exp_fast2(f32x2 d) {  // d = x - max (<= 0, -inf or NaN)
   const f32x2 t = d * f32x2{kLog2eF, kLog2eF};
   return f32x2{__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)};
 }
 // relative half-width of the verification interval (see above); lane_min: the smallest element this lane holds
-__device__ __forceinline__ float fast_eps(float mx, float lane_min) { return (2.f * (mx - lane_min) + 12.f) * 5.9604645e-8f; }
+__device__ __forceinline__ float fast_eps(float mx, float lane_min) { return (1.25f * (mx - lane_min) + 8.f) * 5.9604645e-8f; }
 template <typename T> struct FastQuot : std::false_type {};
 template <> struct FastQuot<__hip_bfloat16> : std::true_type {};
 // the code pair of (e.x, e.y) from the fast exps, and whether either could round differently from the definition
@@ -635,10 +639,16 @@ __device__ __forceinline__ void row_tile_compute(const RowLoads<NG>& L, int64_t 
     if constexpr (SOFTMAX) {
       f32x2 acc = {0.f, 0.f};
       const f32x2 mx2 = {ra.mx, rb.mx};
-      // the row sums of the fast exps, in the lean form's order (padding slots hold -inf: exp2(-inf) adds +0); the
-      // quotients below take the exact exps (the definition)
+      // the row sums of the fast exps, in the lean form's order (padding slots hold -inf: exp2(-inf) adds +0); then
+      // the exact exps (the definition's numerators) replace the scores
 #pragma unroll
-      for (int j = 0; j < 8 * NG; ++j) acc = acc + exp_fast2(f32x2{ra.v[j], rb.v[j]} - mx2);
+      for (int j = 0; j < 8 * NG; ++j) {
+        const f32x2 d = f32x2{ra.v[j], rb.v[j]} - mx2;
+        acc = acc + exp_fast2(d);
+        const f32x2 e = exp_nonpos2(d);
+        ra.v[j] = e.x;
+        rb.v[j] = e.y;
+      }
       sa = wave_sum_uniform(acc.x);
       sb = wave_sum_uniform(acc.y);
       ia = 1.f / sa;
@@ -677,7 +687,7 @@ __device__ __forceinline__ void row_tile_compute(const RowLoads<NG>& L, int64_t 
     for (int j = 0; j < 8 * NG; ++j) {
       uint32_t packed;
       if constexpr (SOFTMAX) {
-        packed = exact_code2<T>(f32x2{ra.v[j], rb.v[j]}, f32x2{ra.mx, rb.mx}, f32x2{sa, sb}, f32x2{ia, ib}, false);
+        packed = pack_rne2<T>(div_rn2(f32x2{ra.v[j], rb.v[j]}, f32x2{sa, sb}, f32x2{ia, ib}));
       } else {
         const uint32_t ca = raw_code<T>(raw_bits<T>(wa[j >> 3], j & 7));
         const uint32_t cb = raw_code<T>(raw_bits<T>(wb[j >> 3], j & 7));
@@ -754,7 +764,7 @@ __device__ __forceinline__ float min8(const float* v) {
 }
 
 template <typename T, int NG, bool UNALIGNED = false>
-__device__ __forceinline__ void row_tile_softmax_lean(const RowLoads<NG>& L, int64_t n, int C, int ld, int64_t ignore_index,
+__device__ __forceinline__ void row_tile_softmax_lean(const T* __restrict__ preds, const RowLoads<NG>& L, int64_t n, int C, int ld, int64_t ignore_index,
                                                       bool has_ignore, int64_t* __restrict__ confmat, int* __restrict__ err, bool rec,
                                                       bool& saw_bad, SlowRows slow, uint32_t* __restrict__ s_tile, int64_t tile,
                                                       float4* __restrict__ row_stats, const PosSink& pos, PosTake& ptake) {
@@ -853,12 +863,22 @@ __device__ __forceinline__ void row_tile_softmax_lean(const RowLoads<NG>& L, int
       }
       return e;
     };
-    // the row sums of the fast exps, which replace the scores in P (wa / wb keep the raw scores for the exact paths)
+    // the row sums of the fast exps; on the fast path (bf16, narrow rows) the exps replace the scores in P, otherwise
+    // P keeps the scores for the exact quotients
+    const bool fast = FastQuot<T>::value && narrow;
+    if (fast) {
 #pragma unroll
-    for (int j = 0; j < 8 * NG; ++j) {
-      P[j] = exp_fast2(P[j] - mx2);
-      acc = acc + counted(P[j], j);
-      if (j == 7) acc_lo = acc;
+      for (int j = 0; j < 8 * NG; ++j) {
+        P[j] = exp_fast2(P[j] - mx2);
+        acc = acc + counted(P[j], j);
+        if (j == 7) acc_lo = acc;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8 * NG; ++j) {
+        acc = acc + counted(exp_fast2(P[j] - mx2), j);
+        if (j == 7) acc_lo = acc;
+      }
     }
     // padding lanes: the group-1 duplicates (NG == 2) or the whole lane (NG == 1) add nothing to the exp-sum
     if constexpr (NG == 2) acc = hi_ok ? acc : acc_lo;
@@ -882,8 +902,7 @@ __device__ __forceinline__ void row_tile_softmax_lean(const RowLoads<NG>& L, int
     }
     const bool ka = va && fa, kb = vb && fb;
     const f32x2 s2 = {sa, sb}, i2 = {ia, ib};
-    // the pair's codes: fast and verified (bf16, narrow rows), else the exact definition from the raw scores
-    const bool fast = FastQuot<T>::value && narrow;
+    // the pair's codes: fast and verified (bf16, narrow rows), else the exact definition from the scores
     const float ea = fast_eps(mxa, mn_a), eb = fast_eps(mxb, mn_b);
     const f32x2 rlo = {ia - ia * ea, ib - ib * eb}, rhi = {ia + ia * ea, ib + ib * eb};
     const uint32_t keep = (ka ? 0x0000FFFFu : 0u) | (kb ? 0xFFFF0000u : 0u);
@@ -905,13 +924,25 @@ __device__ __forceinline__ void row_tile_softmax_lean(const RowLoads<NG>& L, int
         redo |= (__ballot(und) != 0 ? 1u : 0u) << j;
       }
       if (redo != 0) {  // rare: the undecided slots from the definition (same wave, same lanes: LDS order holds)
+        if constexpr (TMX_FASTQ_RELOAD && !UNALIGNED) {
+          // the scores again from memory (the pass's own reads: cache hits) instead of holding them in 16 VGPRs
+          const int lq = lo_ok ? lane : nvec - 1, hq = hi_ok ? lane + kWave : nvec - 1;
+          const uint4* ra = reinterpret_cast<const uint4*>(preds + min(r0, n - 1) * ld);
+          const uint4* rb = reinterpret_cast<const uint4*>(preds + min(r0 + 1, n - 1) * ld);
+          wa[0] = ra[lq];
+          wb[0] = rb[lq];
+          if constexpr (NG == 2) {
+            wa[1] = ra[hq];
+            wb[1] = rb[hq];
+          }
+        }
 #pragma unroll
         for (int j = 0; j < 8 * NG; ++j)
           if ((redo >> j) & 1u) put(j, exact_code2<T>(raw_pair(j), mx2, s2, i2, true));
       }
     } else {
 #pragma unroll
-      for (int j = 0; j < 8 * NG; ++j) put(j, exact_code2<T>(raw_pair(j), mx2, s2, i2, narrow));
+      for (int j = 0; j < 8 * NG; ++j) put(j, exact_code2<T>(P[j], mx2, s2, i2, narrow));
     }
     if (lane == 0 && pos.hist == nullptr) {
       if (ka && ta >= 0 && ta < C) atomicOr(&s_tile[ta * kSlots + (p ^ ((int)(ta >> 3) & (kSlots - 1)))], 0x00004000u);
@@ -957,7 +988,7 @@ __device__ __forceinline__ void row_tile(const T* __restrict__ preds, const int6
   PosTake ptake;
   if constexpr (FIXUP) pos = PosSink{};
   if constexpr (LEAN && SOFTMAX && !FIXUP)
-    row_tile_softmax_lean<T, NG, PADDED>(L, n, C, ld, ignore_index, has_ignore, confmat, err, rec, saw_bad, slow, s_tile, tile, row_stats, pos,
+    row_tile_softmax_lean<T, NG, PADDED>(preds, L, n, C, ld, ignore_index, has_ignore, confmat, err, rec, saw_bad, slow, s_tile, tile, row_stats, pos,
                                          ptake);
   else
     row_tile_compute<T, NG, SOFTMAX, FIXUP, PADDED>(L, n, C, ld, ignore_index, has_ignore, confmat, err, rec, saw_bad, slow, s_tile, tile,

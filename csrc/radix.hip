@@ -1143,6 +1143,219 @@ __global__ void __launch_bounds__(kRsThreads) sort_coop_kernel(const T* __restri
   }
 }
 
+// ----------------------------------------------------------------------------------- onesweep passes (round 6)
+// Rows of 4096 < n <= kOsMax keys (one row): one launch for every digit histogram of every pass plus the keys'
+// AND / OR (os_hist_kernel), then ONE launch per 8-bit pass (os_pass_kernel): each workgroup takes the next 4096-key
+// tile (a dynamic tile id: a tile only ever waits for tiles taken before it, so the chain always drains), ranks it
+// stably (rs_rank_tile), publishes its per-digit counts and resolves its per-digit offsets by a decoupled look-back
+// over the earlier tiles' published words -- {2-bit state, 30-bit count} in one 32-bit word, stored and polled with
+// agent-scope atomics, so no payload needs ordering -- and scatters through LDS in digit runs.  The first executed pass
+// reads the input and builds the keys, the last writes the values and int64 indices; passes of digits equal in every
+// key exit at once (decided on the device from the AND / OR: no host read).  Replaces prep + (histogram, scan(s),
+// scatter) per pass + final: 6 launches for fp32 / int32 instead of 11-14 (profiles/sort_bench_r5.json: the
+// multi-launch path was launch-bound below 262K keys, 0.45-0.75x torch.sort).
+constexpr int64_t kOsMax = int64_t{1} << 22;
+constexpr uint32_t kOsAgg = 1u << 30, kOsInc = 2u << 30, kOsVal = (1u << 30) - 1u;
+
+template <typename T>
+__global__ void __launch_bounds__(256) os_hist_kernel(const T* __restrict__ x, int64_t n, bool desc, uint32_t* __restrict__ ghist,
+                                                      typename SortKey<T>::type* __restrict__ andor) {
+  using KT = typename SortKey<T>::type;
+  constexpr int P = static_cast<int>(sizeof(KT));
+  __shared__ uint32_t h[P * kRsBins];
+  for (int i = threadIdx.x; i < P * kRsBins; i += 256) h[i] = 0u;
+  __syncthreads();
+  KT na = KT(0), o = KT(0);  // (NOT of the AND, so both words OR into zeroed memory)
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const KT k0 = SortKey<T>::asc(x[i]);
+    const KT k = desc ? ~k0 : k0;
+    na |= ~k;
+    o |= k;
+#pragma unroll
+    for (int p = 0; p < P; ++p) atomicAdd(&h[p * kRsBins + static_cast<int>((k >> (8 * p)) & 0xFF)], 1u);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < P * kRsBins; i += 256)
+    if (h[i]) atomicAdd(&ghist[i], h[i]);
+#pragma unroll
+  for (int off = kWave / 2; off > 0; off >>= 1) {
+    na |= __shfl_xor(na, off, kWave);
+    o |= __shfl_xor(o, off, kWave);
+  }
+  if ((threadIdx.x & (kWave - 1)) == 0) {
+    atomicOr(&andor[0], na);
+    atomicOr(&andor[1], o);
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(kRsThreads) os_pass_kernel(const T* __restrict__ x, typename SortKey<T>::type* __restrict__ kb0,
+                                                               typename SortKey<T>::type* __restrict__ kb1, uint32_t* __restrict__ pb0,
+                                                               uint32_t* __restrict__ pb1, T* __restrict__ vals, int64_t* __restrict__ idx,
+                                                               int64_t n, bool desc, int pass, const uint32_t* __restrict__ ghist,
+                                                               uint32_t* __restrict__ status, unsigned* __restrict__ ctr,
+                                                               const typename SortKey<T>::type* __restrict__ andor, int* __restrict__ err) {
+  using KT = typename SortKey<T>::type;
+  constexpr int P = static_cast<int>(sizeof(KT));
+  __shared__ uint32_t cnt[4][kRsBins];
+  __shared__ uint32_t lstart[kRsBins];
+  __shared__ uint32_t gb[kRsBins];
+  __shared__ KT s_key[kRsTile];
+  __shared__ uint32_t s_pay[kRsTile];
+  __shared__ unsigned s_t;
+  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+  const int Tt = static_cast<int>((n + kRsTile - 1) / kRsTile);
+  // the plan: which digits vary (written by os_hist_kernel, complete at this launch's start)
+  const KT varying = static_cast<KT>(~andor[0]) ^ andor[1];
+  if (varying == KT(0)) {  // every key equal: the stable order is the input order (pass 0 writes it)
+    if (pass == 0)
+      for (int64_t i = blockIdx.x * (int64_t)kRsThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kRsThreads) {
+        vals[i] = x[i];
+        idx[i] = i;
+      }
+    return;
+  }
+  if (((varying >> (8 * pass)) & KT(0xFF)) == KT(0)) return;
+  int k_index = 0, n_exec = 0;
+#pragma unroll
+  for (int p = 0; p < P; ++p)
+    if (((varying >> (8 * p)) & KT(0xFF)) != KT(0)) {
+      k_index += p < pass ? 1 : 0;
+      ++n_exec;
+    }
+  const bool first = k_index == 0, last = k_index == n_exec - 1;
+  const KT* kin = (k_index & 1) ? kb0 : kb1;  // executed pass k reads buffer (k - 1) % 2 and writes buffer k % 2
+  const uint32_t* pin = (k_index & 1) ? pb0 : pb1;
+  KT* kout = (k_index & 1) ? kb1 : kb0;
+  uint32_t* pout = (k_index & 1) ? pb1 : pb0;
+  if (threadIdx.x == 0) s_t = atomicAdd(&ctr[pass], 1u);
+  __syncthreads();
+  const int t = static_cast<int>(s_t);
+  const int64_t tb = (int64_t)t * kRsTile;
+  const int len = static_cast<int>(min<int64_t>(kRsTile, n - tb));
+  KT key[kRsItems];
+  uint32_t pay[kRsItems], rank[kRsItems];
+#pragma unroll
+  for (int k = 0; k < kRsItems; ++k) {
+    const int i = wave * (kRsTile / 4) + k * kWave + lane;
+    if (i < len) {
+      if (first) {
+        const KT k0 = SortKey<T>::asc(x[tb + i]);
+        key[k] = desc ? ~k0 : k0;
+        pay[k] = static_cast<uint32_t>(tb + i);
+      } else {
+        key[k] = kin[tb + i];
+        pay[k] = pin[tb + i];
+      }
+    } else {
+      key[k] = KT(0);
+      pay[k] = 0u;
+    }
+  }
+  for (int i = threadIdx.x; i < 4 * kRsBins; i += kRsThreads) (&cnt[0][0])[i] = 0u;
+  __syncthreads();
+  const int shift = 8 * pass;
+  rs_rank_tile<KT>(key, len, shift, cnt, lstart, rank);
+  // this tile's count of digit d (thread d), published; the earlier tiles' total by look-back
+  const int d = threadIdx.x;
+  const uint32_t c = (d + 1 < kRsBins ? lstart[d + 1] : static_cast<uint32_t>(len)) - lstart[d];
+  uint32_t* st = status + ((int64_t)pass * Tt) * kRsBins;
+  uint32_t excl = 0;
+  if (t == 0) {
+    __hip_atomic_store(&st[d], kOsInc | c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    __hip_atomic_store(&st[(int64_t)t * kRsBins + d], kOsAgg | c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int j = t - 1;
+    unsigned spins = 0;
+    while (j >= 0) {
+      const uint32_t v = __hip_atomic_load(&st[(int64_t)j * kRsBins + d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t state = v >> 30;
+      if (state == 0u) {  // tile j has not published yet (it was taken earlier: it is running)
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > (1u << 24)) {  // never expected; bounded so a fault cannot hang the device
+          atomicOr(err, 1);
+          break;
+        }
+        continue;
+      }
+      excl += v & kOsVal;
+      if (state == 2u) break;
+      --j;
+    }
+    __hip_atomic_store(&st[(int64_t)t * kRsBins + d], kOsInc | (excl + c), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  // global position of digit d's first key of this tile: keys of smaller digits (all tiles) + this digit in earlier tiles
+  gb[d] = ghist[pass * kRsBins + d];
+  __syncthreads();
+  for (int off = 1; off < kRsBins; off <<= 1) {  // inclusive scan of the global digit totals
+    const uint32_t v = d >= off ? gb[d - off] : 0u;
+    __syncthreads();
+    gb[d] += v;
+    __syncthreads();
+  }
+  const uint32_t base = (d ? gb[d - 1] : 0u) + excl;
+  __syncthreads();
+  gb[d] = base;
+#pragma unroll
+  for (int k = 0; k < kRsItems; ++k) {
+    if (rank[k] == 0xFFFFFFFFu) continue;
+    const uint32_t dk = static_cast<uint32_t>((key[k] >> shift) & 0xFF);
+    const uint32_t lp = lstart[dk] + cnt[wave][dk] + rank[k];
+    s_key[lp] = key[k];
+    s_pay[lp] = pay[k];
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < len; j += kRsThreads) {  // digit runs: consecutive threads, consecutive addresses
+    const KT kk = s_key[j];
+    const uint32_t dk = static_cast<uint32_t>((kk >> shift) & 0xFF);
+    const int64_t dst = gb[dk] + (j - lstart[dk]);
+    const uint32_t pj = s_pay[j];
+    if (last) {
+      const KT kd = desc ? ~kk : kk;
+      vals[dst] = KeyDecode<T>::exact(kd) ? KeyDecode<T>::value(kd) : x[pj];
+      idx[dst] = pj;
+    } else {
+      kout[dst] = kk;
+      pout[dst] = pj;
+    }
+  }
+}
+
+template <typename T>
+void radix_sort_onesweep(const at::Tensor& x, int64_t n, bool desc, at::Tensor& vals, at::Tensor& idx) {
+  using KT = typename SortKey<T>::type;
+  constexpr int P = static_cast<int>(sizeof(KT));
+  const int Tt = static_cast<int>((n + kRsTile - 1) / kRsTile);
+  auto opts = x.options();
+  const auto kdt = sizeof(KT) == 4 ? at::kInt : at::kLong;
+  auto keys = at::empty({2 * n}, opts.dtype(kdt));
+  auto pays = at::empty({2 * n}, opts.dtype(at::kInt));
+  // zeroed scratch: digit totals [P][256] | tile status [P][Tt][256] | tile counters [P] + error word | AND / OR
+  const int64_t words = (int64_t)P * kRsBins + (int64_t)P * Tt * kRsBins + P + 1;
+  const int64_t kt_words = 2 * static_cast<int64_t>(sizeof(KT)) / 4;
+  auto scratch = at::empty({words + kt_words + 1}, opts.dtype(at::kInt));  // (+1: 8-B alignment of the AND / OR)
+  uint32_t* sp = reinterpret_cast<uint32_t*>(scratch.data_ptr());
+  TMX_CHECK_HIP(hipMemsetAsync(sp, 0, (words + kt_words + 1) * 4, stream()));
+  uint32_t* ghist = sp;
+  uint32_t* status = ghist + P * kRsBins;
+  unsigned* ctr = status + (int64_t)P * Tt * kRsBins;
+  int* err = reinterpret_cast<int*>(ctr + P);
+  uintptr_t ao = reinterpret_cast<uintptr_t>(err + 1);
+  ao = (ao + 7) & ~uintptr_t(7);
+  KT* andor = reinterpret_cast<KT*>(ao);
+  KT* kb0 = reinterpret_cast<KT*>(keys.data_ptr());
+  uint32_t* pb0 = reinterpret_cast<uint32_t*>(pays.data_ptr());
+  const T* xp = x.data_ptr<T>();
+  const int hgrid = static_cast<int>(std::min<int64_t>((n + 1023) / 1024, 512));
+  hipLaunchKernelGGL(os_hist_kernel<T>, hgrid, 256, 0, stream(), xp, n, desc, ghist, andor);
+  TMX_LAUNCH_CHECK();
+  for (int p = 0; p < P; ++p) {
+    hipLaunchKernelGGL(os_pass_kernel<T>, Tt, kRsThreads, 0, stream(), xp, kb0, kb0 + n, pb0, pb0 + n, vals.data_ptr<T>(),
+                       idx.data_ptr<int64_t>(), n, desc, p, ghist, status, ctr, andor, err);
+    TMX_LAUNCH_CHECK();
+  }
+}
+
 template <typename T>
 void radix_sort_impl(const at::Tensor& x, int S, int64_t n, bool desc, at::Tensor& vals, at::Tensor& idx) {
   using KT = typename SortKey<T>::type;
@@ -1179,6 +1392,11 @@ void radix_sort_impl(const at::Tensor& x, int S, int64_t n, bool desc, at::Tenso
     const void* kfn = small_tiles ? reinterpret_cast<const void*>(&sort_coop_kernel<T, 4>)
                                   : reinterpret_cast<const void*>(&sort_coop_kernel<T, kRsItems>);
     TMX_CHECK_HIP(hipLaunchCooperativeKernel(kfn, dim3(Tt), dim3(kRsThreads), args, 0, stream()));
+    return;
+  }
+  static const bool os_off = std::getenv("TMX_SORT_ONESWEEP_OFF") != nullptr;  // A/B knob (tools/sort_bench.py)
+  if (S == 1 && n > kRsTile && n <= kOsMax && !os_off) {
+    radix_sort_onesweep<T>(x, n, desc, vals, idx);
     return;
   }
   if (n <= kRsTile) {  // one workgroup per row, one launch

@@ -297,7 +297,8 @@ __global__ __launch_bounds__(kSsimMfmaWaves * kWave) void ssim_mfma_kernel(
   // this lane's input vectors of band b: row oy0 + 16 b + i16, columns c0 + 8 g .. + 7 (W % 4 == 0: whole float4s)
   const int xc = c0 + 8 * g;
   const bool x_ok0 = xc < W, x_ok1 = xc + 4 < W;
-  float4 np0, np1, nt0, nt1;
+  float4 np0, np1, nt0, nt1;  // band b + 2 in flight (fetch)
+  float4 cp0, cp1, ct0, ct1;  // band b + 1 (arrived or arriving)
   // every lane loads (a masked lane reads the plane's first vector) and zeroes what lies outside the image: no
   // divergent loads, no stack temporaries for the selects
   auto ld = [](const float* base, int64_t o, bool ok) -> float4 {
@@ -325,11 +326,16 @@ __global__ __launch_bounds__(kSsimMfmaWaves * kWave) void ssim_mfma_kernel(
   uint32_t prev_hi[5][2], prev_lo[5][2];  // h of the previous band, split (the vertical product's first 16 K slots)
   double acc_sim = 0.0, acc_cs = 0.0, acc_sse = 0.0;
   bool bad = false;
+  // two bands in flight: a band's loads are issued two band computations (~1.5 us) before its use -- one was not
+  // enough to cover the HBM latency at three waves per SIMD
   fetch(0);
+  cp0 = np0; cp1 = np1; ct0 = nt0; ct1 = nt1;
+  fetch(1);
   for (int b = 0; b < nb; ++b) {
-    const float p[8] = {np0.x, np0.y, np0.z, np0.w, np1.x, np1.y, np1.z, np1.w};
-    const float t[8] = {nt0.x, nt0.y, nt0.z, nt0.w, nt1.x, nt1.y, nt1.z, nt1.w};
-    if (b + 1 < nb) fetch(b + 1);  // in flight while this band is computed
+    const float p[8] = {cp0.x, cp0.y, cp0.z, cp0.w, cp1.x, cp1.y, cp1.z, cp1.w};
+    const float t[8] = {ct0.x, ct0.y, ct0.z, ct0.w, ct1.x, ct1.y, ct1.z, ct1.w};
+    cp0 = np0; cp1 = np1; ct0 = nt0; ct1 = nt1;
+    if (b + 2 < nb) fetch(b + 2);
     float f_sse = 0.f;
     if constexpr (SSE) {
       const int y = oy0 + 16 * b + i16;

@@ -164,3 +164,25 @@ def test_sort_routing_picks_the_faster_engine():
         v, i = sort(x.cuda())
         ref = torch.sort(x, stable=True)
         assert torch.equal(i.cpu(), ref.indices) and torch.equal(v.cpu(), ref.values)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64, torch.int32, torch.int64])
+@pytest.mark.parametrize("descending", [False, True])
+@pytest.mark.parametrize("kind", ["equal", "narrow", "two_values", "huge"])
+def test_radix_sort_onesweep_edge_cases(dtype, descending, kind):
+    """Round 6 one-sweep path (4096 < n <= 4M keys, one row): every key equal (no pass executes: identity order),
+    keys with constant high digits (passes skipped on the device), two distinct values (one executed pass), and the
+    largest routed size."""
+    n = {"equal": 10_000, "narrow": 70_001, "two_values": 4_097, "huge": 1 << 22}[kind]
+    g = torch.Generator().manual_seed(n)
+    if kind == "equal":
+        x = torch.full((n,), 3, dtype=dtype)
+    elif kind == "narrow":
+        x = torch.randint(0, 200, (n,), generator=g).to(dtype)
+        if dtype.is_floating_point:
+            x = x / 8 + 1.0  # few varying mantissa bits, constant exponent
+    elif kind == "two_values":
+        x = torch.randint(0, 2, (n,), generator=g).to(dtype)
+    else:
+        x = _data(n, dtype, 17)
+    _check(x, descending)

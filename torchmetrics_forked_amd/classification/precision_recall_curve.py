@@ -386,12 +386,13 @@ class _CurveMetric(Metric):
             return super()._fused_forward_end(ctx)
         _, count, saved, snap_def = ctx
         self.__dict__["_batch_view"] = True
+        cleared = self.__dict__["_batch_cleared"] = [False]
         try:
             batch_val = self.compute()
         finally:
             self.__dict__["_batch_view"] = False
             sink = self.__dict__.pop("_batch_sink", None)
-            if sink is not None:
+            if sink is not None and not cleared[0]:
                 cls_ops.curve_hist_zero(*sink)
             self._update_count = count + 1
             self._leave_batch_mode(saved)
@@ -630,7 +631,8 @@ class _CurveMetric(Metric):
             return ("binned", cm)
         if self.__dict__.get("_batch_view") and self.__dict__.get("_batch_sink") is not None:
             bh, br = self.__dict__["_batch_sink"]
-            return ("hist", bh, self._hist_dtype or torch.bfloat16, br)
+            # (the one-element marker: a consumer that reduces AND clears the scratch sets it -- no zero launches after)
+            return ("hist", bh, self._hist_dtype or torch.bfloat16, br, self.__dict__.setdefault("_batch_cleared", [False]))
         if isinstance(self.score_hist, Tensor) and self.score_hist.numel() > 0:
             return ("hist", self.score_hist, self._hist_dtype or torch.bfloat16, self._tracked_range())
         if lazy and isinstance(self.preds, list) and self.preds:

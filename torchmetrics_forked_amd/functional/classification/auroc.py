@@ -107,7 +107,7 @@ def _warn_degenerate(P: Tensor, N: Tensor, summary: Optional[Tensor] = None) -> 
 def _exact_scores(state: CurveState, task: str, num: int, ignore_index: Optional[int]) -> ExactScores:
     """(auroc, ap, P, N) per class for hist / samples states (``.summary`` set on the native histogram path)."""
     if state[0] == "hist":
-        sc, summ = cls_ops.curve_hist_scores(state[1], state[3] if len(state) > 3 else None)
+        sc, summ = cls_ops.curve_hist_scores(state[1], state[3] if len(state) > 3 else None, state[4] if len(state) > 4 else None)
         return ExactScores.of(sc[:, 0], sc[:, 1], sc[:, 2], sc[:, 3], summ)
     preds, target = state[1], state[2]
     anchored = eng.anchored_scores(preds, target, task, num, ignore_index)

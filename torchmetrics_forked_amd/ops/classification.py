@@ -298,10 +298,15 @@ def curve_hist_reduce(hist: Tensor, code_range: Optional[Tensor] = None) -> Tens
     return torch.stack([auroc, ap, P, N], dim=1)
 
 
-def curve_hist_scores(hist: Tensor, code_range: Optional[Tensor] = None) -> Tuple[Tensor, Optional[Tensor]]:
-    """(``curve_hist_reduce`` scores ``[C, 4]``, native ``curve_summary`` buffer or None on the host) -- on the GPU one
-    launch: the reduce's last class block folds the summary."""
+def curve_hist_scores(hist: Tensor, code_range: Optional[Tensor] = None, clear: Optional[list] = None) -> Tuple[Tensor, Optional[Tensor]]:
+    """(``curve_hist_reduce`` scores ``[C, 4]``, native ``curve_summary`` buffer or None on the host) -- on the GPU two
+    launches (reduce, summary).  ``clear`` (forward()'s batch histogram: a one-element list): the reduce also zeroes
+    what it read and empties the code range, and ``clear[0]`` is set True so the caller skips ``curve_hist_zero``."""
     if ops.use_native(hist, code_range):
+        if clear is not None and code_range is not None and hist.is_contiguous():
+            sc, summ = torch.ops.tmx.curve_hist_scores(hist, code_range, True)
+            clear[0] = True
+            return sc, summ
         sc, summ = torch.ops.tmx.curve_hist_scores(hist, code_range)
         return sc, summ
     return curve_hist_reduce(hist, code_range), None
