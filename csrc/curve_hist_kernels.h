@@ -264,6 +264,9 @@ constexpr float kLog2eF = 1.44269502163f;  // RN(log2 e) = 0x3fb8aa3b
 #ifndef TMX_FASTQ_RELOAD
 #define TMX_FASTQ_RELOAD 1  // the fallback re-reads the scores (1) or keeps the raw vectors in registers (0)
 #endif
+#ifndef TMX_FASTQ_RECOMPUTE
+#define TMX_FASTQ_RECOMPUTE 0  // 1: P keeps the scores and the quotient pass recomputes the fast exps (no reload)
+#endif
 __device__ __forceinline__ f32x2 exp_fast2(f32x2 d) {  // d = x - max (<= 0, -inf or NaN)
   const f32x2 t = d * f32x2{kLog2eF, kLog2eF};
   return f32x2{__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)};
@@ -866,7 +869,7 @@ __device__ __forceinline__ void row_tile_softmax_lean(const T* __restrict__ pred
     // the row sums of the fast exps; on the fast path (bf16, narrow rows) the exps replace the scores in P, otherwise
     // P keeps the scores for the exact quotients
     const bool fast = FastQuot<T>::value && narrow;
-    if (fast) {
+    if (fast && !TMX_FASTQ_RECOMPUTE) {
 #pragma unroll
       for (int j = 0; j < 8 * NG; ++j) {
         P[j] = exp_fast2(P[j] - mx2);
@@ -920,10 +923,18 @@ __device__ __forceinline__ void row_tile_softmax_lean(const T* __restrict__ pred
 #pragma unroll
       for (int j = 0; j < 8 * NG; ++j) {
         bool und;
-        put(j, fast_code2<T>(P[j], rlo, rhi, und));
+        put(j, fast_code2<T>(TMX_FASTQ_RECOMPUTE ? exp_fast2(P[j] - mx2) : P[j], rlo, rhi, und));
         redo |= (__ballot(und) != 0 ? 1u : 0u) << j;
       }
+#ifdef TMX_FASTQ_NO_REDO  // timing experiment only: codes may differ from the definition
+      redo = 0;
+#endif
       if (redo != 0) {  // rare: the undecided slots from the definition (same wave, same lanes: LDS order holds)
+        if constexpr (TMX_FASTQ_RECOMPUTE) {
+#pragma unroll
+          for (int j = 0; j < 8 * NG; ++j)
+            if ((redo >> j) & 1u) put(j, exact_code2<T>(P[j], mx2, s2, i2, true));
+        } else {
         if constexpr (TMX_FASTQ_RELOAD && !UNALIGNED) {
           // the scores again from memory (the pass's own reads: cache hits) instead of holding them in 16 VGPRs
           const int lq = lo_ok ? lane : nvec - 1, hq = hi_ok ? lane + kWave : nvec - 1;
@@ -939,6 +950,7 @@ __device__ __forceinline__ void row_tile_softmax_lean(const T* __restrict__ pred
 #pragma unroll
         for (int j = 0; j < 8 * NG; ++j)
           if ((redo >> j) & 1u) put(j, exact_code2<T>(raw_pair(j), mx2, s2, i2, true));
+        }
       }
     } else {
 #pragma unroll

@@ -199,12 +199,14 @@ __device__ __forceinline__ void pg_load(const T* __restrict__ p, int64_t row, in
 template <typename T, typename Acc, int MODE, bool VEC>
 __global__ __launch_bounds__(kPgThreads) void pairwise_gemm_kernel(const T* __restrict__ x, const T* __restrict__ y, int64_t N, int64_t M,
                                                                    int64_t D, int tiles_n, bool zero_diag, T* __restrict__ out,
-                                                                   void* __restrict__ rowmax = nullptr) {
+                                                                   void* __restrict__ rowmax = nullptr,
+                                                                   const int* __restrict__ run_if = nullptr) {
   using Mma = PgMma<Acc>;
   constexpr int kPgK = pg_k<Acc>(), KPT = kPgK / 4;
   __shared__ Acc xs[2][kPgK][kPgT + kPgPad];
   __shared__ Acc ys[2][kPgK][kPgT + kPgPad];
   __shared__ Acc nrm[2][kPgT];
+  if (run_if != nullptr && *run_if == 0) return;  // device-side fallback launch (x3 route, non-finite inputs)
   const int64_t nwg = gridDim.x, orig = blockIdx.x, xcd = orig % 8, q = nwg / 8, rr = nwg % 8;
   const int64_t id = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
   const int64_t row0 = (id / tiles_n) * kPgT, col0 = (id % tiles_n) * kPgT;
@@ -462,6 +464,214 @@ void launch_pairwise_gemm_h16(const at::Tensor& x, const at::Tensor& y, at::Tens
   else
     hipLaunchKernelGGL((pairwise_gemm_h16_kernel<T, MODE, false>), dim3(static_cast<unsigned>(nwg)), kPhThreads, 0, stream(), xp, yp, N, M,
                        D, static_cast<int>(tiles_n), zero_diag, op, xnp, ynp);
+}
+
+// ------------------------------------------------------------------------------------ fp32 on f16 matrix cores (x3)
+// fp32 linear / cosine / MiFID row max at large shapes.  gfx950's fp32 MFMA rate is a sixteenth of its f16 rate, and
+// hipBLASLt's fp32 GEMM reaches ~110 TFLOP/s there.  Here every fp32 row is split into two f16 planes: t = x·2^s
+// (s per row: the row max lands in [2^14, 2^15), so nothing overflows and the planes stay normal for every element
+// within 2^-18 of the row max), hi = f16(t), lo = f16(t - hi): hi + lo carries 22 of t's 24 bits.  The dot product
+// is hi·hi + hi·lo + lo·hi (three v_mfma_f32_16x16x32_f16 per fragment, exact f16 products, fp32 accumulation);
+// the dropped lo·lo term is below 2^-22 of |x||y| -- under fp32's own rounding of a K-deep sum.  The split runs once
+// per operand (x3_split_kernel: packed [row][k/32][hi 32 | lo 32] planes, the same bytes as the fp32 input) and the
+// GEMM reuses the 16-bit kernel's 128 x 128 tiles: one 64-element LDS row slice holds 32 k of both planes.
+// Output: ldexp(acc, -(s_x + s_y)) (linear) or acc · f_x · f_y with f = 1 / |t| (cosine / |cos| row max).
+// Non-finite rows (inf / NaN) set a flag; linear mode then reruns the exact fp32 MFMA kernel on device (its run_if).
+constexpr int kX3K = 32;  // real k per slice (64 halves: hi | lo)
+
+__global__ __launch_bounds__(256) void x3_split_kernel(const float* __restrict__ x, const float* __restrict__ y, int64_t N, int64_t Np,
+                                                       int64_t M, int64_t D, int64_t Dp, __half* __restrict__ px, __half* __restrict__ py,
+                                                       int* __restrict__ shift, float* __restrict__ finv, int* __restrict__ nonfinite) {
+  const int lane = threadIdx.x & 63;
+  const int64_t grow = blockIdx.x * 4 + (threadIdx.x >> 6);  // rows [0, Np) of x, then [Np, Np + Mp) of y
+  const bool is_x = grow < Np;
+  const int64_t row = is_x ? grow : grow - Np, nrows = is_x ? N : M;
+  const float* __restrict__ src = is_x ? x : y;
+  __half* __restrict__ dst = (is_x ? px : py) + row * 2 * Dp;
+  float mx = 0.f;
+  if (row < nrows)
+    for (int64_t k = lane; k < D; k += 64) mx = fmaxf(mx, fabsf(src[row * D + k]));
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) mx = fmaxf(mx, __shfl_xor(mx, off, kWave));
+  const bool fin = mx <= 3.4028235e38f;  // false for inf and NaN (fmaxf drops NaN: checked below per element)
+  int e = 0;
+  if (fin && mx > 0.f) frexpf(mx, &e);
+  const int s = fin && mx > 0.f ? 15 - e : 0;
+  float ss = 0.f;
+  bool bad = !fin;
+  for (int64_t k = lane; k < Dp; k += 64) {
+    const float v = (row < nrows && k < D) ? src[row * D + k] : 0.f;
+    bad |= v != v;
+    const float t = ldexpf(v, s);
+    const __half h = __float2half_rn(t);
+    const __half l = __float2half_rn(t - __half2float(h));
+    ss = fmaf(t, t, ss);
+    dst[(k >> 5) * 64 + (k & 31)] = h;
+    dst[(k >> 5) * 64 + 32 + (k & 31)] = l;
+  }
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) ss += __shfl_xor(ss, off, kWave);
+  const bool any_bad = __any(bad);
+  if (lane == 0) {
+    shift[grow] = s;
+    finv[grow] = 1.f / sqrtf(ss);
+    if (any_bad && row < nrows) nonfinite[0] = 1;
+  }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kPhThreads, 2) void pairwise_gemm_x3_kernel(const __half* __restrict__ x, const __half* __restrict__ y, int64_t N,
+                                                                         int64_t M, int64_t Dp, int tiles_n, bool zero_diag,
+                                                                         float* __restrict__ out, const int* __restrict__ xs_shift,
+                                                                         const int* __restrict__ ys_shift, const float* __restrict__ xs_f,
+                                                                         const float* __restrict__ ys_f) {
+  __shared__ __attribute__((aligned(16))) short lds[2][2][kPhT * kPhLd];  // [buffer][x | y][row * kPhLd + (hi 32 | lo 32)]
+  __shared__ float fac[2][kPhT];
+  __shared__ int sh[2][kPhT];
+  const int64_t nwg = gridDim.x, orig = blockIdx.x, xcd = orig % 8, q = nwg / 8, rr = nwg % 8;
+  const int64_t id = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
+  const int64_t row0 = (id / tiles_n) * kPhT, col0 = (id % tiles_n) * kPhT;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 1, wc = wave & 1;
+  const int64_t ld = 2 * Dp;  // halves per packed row; rows are padded to the tile (zeros), so no bounds checks
+  ph_frag8 rx[4], ry[4];
+  auto load = [&](int64_t s) {  // slice s: 64 halves = 128 B per row, 8 lanes per row
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = (tid >> 3) + 32 * i;
+      const int64_t off = s * 64 + 8 * (tid & 7);
+      rx[i] = *reinterpret_cast<const ph_frag8*>(x + (row0 + r) * ld + off);
+      ry[i] = *reinterpret_cast<const ph_frag8*>(y + (col0 + r) * ld + off);
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = (tid >> 3) + 32 * i, kk = 8 * (tid & 7);
+      *reinterpret_cast<ph_frag8*>(&lds[buf][0][r * kPhLd + kk]) = rx[i];
+      *reinterpret_cast<ph_frag8*>(&lds[buf][1][r * kPhLd + kk]) = ry[i];
+    }
+  };
+  ph_acc4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = ph_acc4{0.f, 0.f, 0.f, 0.f};
+  const int nk = static_cast<int>(Dp / kX3K);
+  load(0);
+  store(0);
+  __syncthreads();
+  const int fr = lane & 15, fk = 8 * (lane >> 4);
+  for (int s = 0; s < nk; ++s) {
+    const int buf = s & 1;
+    if (s + 1 < nk) load(s + 1);
+    const short* A = lds[buf][0];
+    const short* B = lds[buf][1];
+    ph_frag8 ah[4], al[4], bh[4], bl[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      ah[i] = *reinterpret_cast<const ph_frag8*>(A + (wr * 64 + 16 * i + fr) * kPhLd + fk);
+      bh[i] = *reinterpret_cast<const ph_frag8*>(B + (wc * 64 + 16 * i + fr) * kPhLd + fk);
+      al[i] = *reinterpret_cast<const ph_frag8*>(A + (wr * 64 + 16 * i + fr) * kPhLd + 32 + fk);
+      bl[i] = *reinterpret_cast<const ph_frag8*>(B + (wc * 64 + 16 * i + fr) * kPhLd + 32 + fk);
+    }
+    // the small terms first: hi·lo and lo·hi, then hi·hi (16 independent accumulators between reuses)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = ph_mma<__half>(ah[i], bl[j], acc[i][j]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = ph_mma<__half>(al[i], bh[j], acc[i][j]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = ph_mma<__half>(ah[i], bh[j], acc[i][j]);
+    if (s + 1 < nk) store(buf ^ 1);
+    __syncthreads();
+  }
+  {
+    const int64_t g = tid < kPhT ? row0 + tid : col0 + (tid - kPhT);
+    fac[tid >> 7][tid & 127] = tid < kPhT ? xs_f[g] : ys_f[g];
+    sh[tid >> 7][tid & 127] = tid < kPhT ? xs_shift[g] : ys_shift[g];
+    __syncthreads();
+  }
+  if constexpr (MODE == kPgAbsCosMax) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int lr = wr * 64 + 16 * i + (lane >> 4) * 4 + r;
+        const int64_t gi = row0 + lr;
+        float mv = -1.f;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int lc = wc * 64 + 16 * j + fr;
+          if (col0 + lc < M) mv = fmaxf(mv, fabsf(acc[i][j][r] * fac[0][lr] * fac[1][lc]));
+        }
+#pragma unroll
+        for (int off = 1; off < 16; off <<= 1) mv = fmaxf(mv, __shfl_xor(mv, off, kWave));
+        if (fr == 0 && gi < N && mv >= 0.f) atomicMax(reinterpret_cast<unsigned int*>(out) + gi, __float_as_uint(mv));
+      }
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int lr = wr * 64 + 16 * i + (lane >> 4) * 4 + r, lc = wc * 64 + 16 * j + fr;
+        const int64_t gi = row0 + lr, gj = col0 + lc;
+        if (gi >= N || gj >= M) continue;
+        float v = acc[i][j][r];
+        if constexpr (MODE == kPgCosine) v = v * fac[0][lr] * fac[1][lc];
+        else v = ldexpf(v, -(sh[0][lr] + sh[1][lc]));
+        if (zero_diag && gi == gj) v = 0.f;
+        out[gi * M + gj] = v;
+      }
+}
+
+// x3 route: fp32, >= 256 128 x 128 output tiles (the host decides; see pairwise_gemm / pairwise_abs_cos_rowmax)
+inline bool x3_eligible(const at::Tensor& x, const at::Tensor& y) {
+  return x.scalar_type() == at::kFloat && ((x.size(0) + kPhT - 1) / kPhT) * ((y.size(0) + kPhT - 1) / kPhT) >= 256 &&
+         !std::getenv("TMX_PAIRWISE_X3_OFF");
+}
+
+// out: [N, M] fp32 (linear / cosine) or [N] row maxima (kPgAbsCosMax, zero-initialised)
+template <int MODE>
+void launch_pairwise_gemm_x3(const at::Tensor& x, const at::Tensor& y, at::Tensor& out, bool zero_diag) {
+  const int64_t N = x.size(0), M = y.size(0), D = x.size(1);
+  const int64_t Np = (N + kPhT - 1) / kPhT * kPhT, Mp = (M + kPhT - 1) / kPhT * kPhT, Dp = (D + kX3K - 1) / kX3K * kX3K;
+  const int64_t tiles_n = Mp / kPhT, nwg = (Np / kPhT) * tiles_n;
+  TORCH_CHECK(nwg < (int64_t(1) << 31), "pairwise_gemm: output too large");
+  auto px = at::empty({Np, 2 * Dp}, x.options().dtype(at::kHalf));
+  auto py = at::empty({Mp, 2 * Dp}, x.options().dtype(at::kHalf));
+  auto shift = at::empty({Np + Mp}, x.options().dtype(at::kInt));
+  auto finv = at::empty({Np + Mp}, x.options());
+  auto flag = at::zeros({1}, x.options().dtype(at::kInt));
+  const float* xp = x.data_ptr<float>();
+  const float* yp = y.data_ptr<float>();
+  hipLaunchKernelGGL(x3_split_kernel, dim3(static_cast<unsigned>((Np + Mp) / 4)), 256, 0, stream(), xp, yp, N, Np, M, D, Dp,
+                     reinterpret_cast<__half*>(px.data_ptr()), reinterpret_cast<__half*>(py.data_ptr()), shift.data_ptr<int>(),
+                     finv.data_ptr<float>(), flag.data_ptr<int>());
+  const int* shp = shift.data_ptr<int>();
+  const float* fp = finv.data_ptr<float>();
+  hipLaunchKernelGGL((pairwise_gemm_x3_kernel<MODE>), dim3(static_cast<unsigned>(nwg)), kPhThreads, 0, stream(),
+                     reinterpret_cast<const __half*>(px.data_ptr()), reinterpret_cast<const __half*>(py.data_ptr()), N, M, Dp,
+                     static_cast<int>(tiles_n), zero_diag, out.data_ptr<float>(), shp, shp + Np, fp, fp + Np);
+  if constexpr (MODE == kPgLinear) {
+    // inf / NaN inputs: the exact fp32 kernel redoes the product on device (a no-op grid otherwise)
+    const int64_t t64 = (M + kPgT - 1) / kPgT, nwg64 = ((N + kPgT - 1) / kPgT) * t64;
+    const bool vec = D % 8 == 0 && reinterpret_cast<uintptr_t>(xp) % 16 == 0 && reinterpret_cast<uintptr_t>(yp) % 16 == 0;
+    if (vec)
+      hipLaunchKernelGGL((pairwise_gemm_kernel<float, float, kPgLinear, true>), dim3(static_cast<unsigned>(nwg64)), kPgThreads, 0, stream(),
+                         xp, yp, N, M, D, static_cast<int>(t64), zero_diag, out.data_ptr<float>(), nullptr, flag.data_ptr<int>());
+    else
+      hipLaunchKernelGGL((pairwise_gemm_kernel<float, float, kPgLinear, false>), dim3(static_cast<unsigned>(nwg64)), kPgThreads, 0, stream(),
+                         xp, yp, N, M, D, static_cast<int>(t64), zero_diag, out.data_ptr<float>(), nullptr, flag.data_ptr<int>());
+  }
 }
 
 template <typename T, typename Acc, int MODE>
@@ -802,6 +1012,11 @@ at::Tensor pairwise_abs_cos_rowmax(const at::Tensor& x_in, const at::Tensor& y_i
   const int64_t N = x.size(0), M = y.size(0), D = x.size(1);
   const int64_t tiles_m = (N + kPgT - 1) / kPgT, tiles_n = (M + kPgT - 1) / kPgT, nwg = tiles_m * tiles_n;
   TORCH_CHECK(nwg < (int64_t(1) << 31), "pairwise_abs_cos_rowmax: too large");
+  if (x3_eligible(x, y)) {  // fp32 at large shapes: the f16-split matrix-core route
+    launch_pairwise_gemm_x3<kPgAbsCosMax>(x, y, out, false);
+    TMX_LAUNCH_CHECK();
+    return out;
+  }
   TMX_DISPATCH_FLOAT(x.scalar_type(), "pairwise_abs_cos_rowmax", [&] {
     constexpr bool kF64 = std::is_same<scalar_t, double>::value;
     using Acc = typename std::conditional<kF64, double, float>::type;
@@ -841,6 +1056,13 @@ at::Tensor pairwise_gemm(const at::Tensor& x_in, const at::Tensor& y_in, int64_t
       if (h16) {
         if (mode == kPgLinear) launch_pairwise_gemm_h16<scalar_t, kPgLinear>(x, y, out, zero_diag);
         else launch_pairwise_gemm_h16<scalar_t, kPgCosine>(x, y, out, zero_diag);
+        return;
+      }
+    }
+    if constexpr (std::is_same<scalar_t, float>::value) {
+      if (mode != kPgEuclid && x3_eligible(x, y)) {  // fp32 at large shapes: the f16-split matrix-core route
+        if (mode == kPgLinear) launch_pairwise_gemm_x3<kPgLinear>(x, y, out, zero_diag);
+        else launch_pairwise_gemm_x3<kPgCosine>(x, y, out, zero_diag);
         return;
       }
     }

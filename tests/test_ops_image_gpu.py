@@ -271,7 +271,7 @@ def _ssim_raw(p, t, ks, consts, sse=True):
 @pytest.mark.parametrize("rng", [1.0, 255.0])
 def test_ssim_mfma_vs_fp32_kernel(shape, ks, rng):
     """Round 6: the matrix-core SSIM kernel (fp16-split banded products, consts = c1, c2, data range) against the fp32
-    VALU kernel (consts = c1, c2) on the same planes: per-plane mean SSIM / CS within 1e-6, SSE equal."""
+    VALU kernel (consts = c1, c2) on the same planes: per-plane mean SSIM / CS within 1e-6, SSE to fp64 summation order."""
     g = torch.Generator(device="cuda").manual_seed(sum(shape) + ks)
     t = torch.rand(*shape, device="cuda", generator=g) * rng
     p = (t + 0.1 * rng * torch.randn(*shape, device="cuda", generator=g)).clamp(0, rng)
@@ -282,7 +282,7 @@ def test_ssim_mfma_vs_fp32_kernel(shape, ks, rng):
     ref = _ssim_raw(p, t, ks, c[:2])
     nv = (shape[1] - ks + 1) * (shape[2] - ks + 1)
     torch.testing.assert_close(fast[:2] / nv, ref[:2] / nv, rtol=0, atol=1e-6)
-    torch.testing.assert_close(fast[2], ref[2], rtol=1e-12, atol=0)
+    torch.testing.assert_close(fast[2], ref[2], rtol=1e-8, atol=0)  # fp64 sums of the same fp32 squares, another tile order
 
 
 @pytest.mark.parametrize("bad", ["range", "nan", "inf"])

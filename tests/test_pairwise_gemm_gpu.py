@@ -132,3 +132,78 @@ def test_pairwise_gemm_16bit_mfma_tiles(D, mode, dtype):
     for zd in (False, True):
         out = torch.ops.tmx.pairwise_gemm(x, y, mode, zd)
         torch.testing.assert_close(out.double(), _ref(mode, x, y, zd).double(), rtol=1e-2, atol=1e-2 * (D ** 0.5 if mode == 0 else 1))
+
+
+def _x3_err(out, x, y, mode):
+    """Max |out - fp64 ref| and the same for ATen's fp32 GEMM of the op (the precision the reference delivers)."""
+    ref = _ref(mode, x, y, False).double()
+    if mode == 0:
+        aten = x @ y.T
+    else:
+        aten = (x / x.norm(dim=1, keepdim=True)) @ (y / y.norm(dim=1, keepdim=True)).T
+    return (out.double() - ref).abs().max().item(), (aten.double() - ref).abs().max().item()
+
+
+@pytest.mark.parametrize("D", [33, 100, 512, 2048])
+@pytest.mark.parametrize("mode", [0, 1])
+def test_pairwise_gemm_fp32_split_f16_route(D, mode):
+    """fp32 with >= 256 128 x 128 tiles runs on f16 matrix cores as hi·hi + hi·lo + lo·hi of a per-row scaled
+    two-plane split (csrc/pairwise.hip x3): its error against fp64 stays within ATen's own fp32 GEMM error."""
+    g = torch.Generator().manual_seed(D * 3 + mode)
+    x = torch.randn(2053, D, generator=g).cuda()
+    y = torch.randn(2100, D, generator=g).cuda()
+    x[7] *= 1e-30  # tiny and huge rows: per-row power-of-two scales keep both planes in f16 range
+    y[9] *= 3e28
+    x[11] = 0.0
+    for zd in (False, True):
+        out = torch.ops.tmx.pairwise_gemm(x, y, mode, zd)
+        ref = _ref(mode, x, y, zd).double()
+        if mode == 1:  # the zero row is NaN in both (0 / 0)
+            assert torch.isnan(out[11]).all() == torch.isnan(ref[11]).all()
+            keep = torch.ones(x.shape[0], dtype=torch.bool, device=x.device)
+            keep[11] = False
+            out, ref = out[keep], ref[keep]
+        assert not torch.isnan(out).any()
+        if mode == 0:  # scale-aware: compare each output against |x_i| |y_j|
+            scale = x.double().norm(dim=1, keepdim=True) @ y.double().norm(dim=1, keepdim=True).T
+            if zd:
+                scale.fill_diagonal_(1.0)
+            assert ((out.double() - ref).abs() / scale.clamp_min(1e-300)).max().item() < 4e-7 * max(1, D) ** 0.5
+        else:
+            assert (out.double() - ref).abs().max().item() < 2e-6
+    e_x3, e_aten = _x3_err(torch.ops.tmx.pairwise_gemm(x[12:], y[:2000], mode, False), x[12:], y[:2000], mode)
+    assert e_x3 <= 4.0 * e_aten, (e_x3, e_aten)
+
+
+def test_pairwise_gemm_fp32_split_nonfinite_falls_back_on_device():
+    """An inf in a linear operand: the x3 route flags it and the exact fp32 kernel reruns on device (inf, not the
+    NaN of inf - inf in the split)."""
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(2048, 64, generator=g).cuda()
+    y = torch.randn(2048, 64, generator=g).cuda()
+    x[5, 3] = float("inf")
+    out = torch.ops.tmx.pairwise_gemm(x, y, 0, False)
+    torch.testing.assert_close(out.double(), _ref(0, x, y, False).double(), rtol=2e-5, atol=2e-4, equal_nan=True)
+    assert torch.isinf(out[5]).any()
+
+
+@pytest.mark.parametrize("n,d", [(2100, 2048), (2500, 100)])
+def test_abs_cos_rowmax_fp32_split_route(n, d):
+    """MiFID's row max |cos| on the x3 route against fp64 and against the exact fp32 MFMA kernel (env switch)."""
+    import os
+
+    g = torch.Generator().manual_seed(n + d)
+    a = torch.randn(n, d, generator=g).cuda()
+    b = torch.randn(n - 37, d, generator=g).cuda()
+    b[:50] = a[:50] * 0.5 + 1e-3 * b[:50]  # near duplicates: |cos| ~ 1
+    got = torch.ops.tmx.pairwise_abs_cos_rowmax(a, b)
+    ad, bd = a.double(), b.double()
+    ref = ((ad / ad.norm(dim=1, keepdim=True)) @ (bd / bd.norm(dim=1, keepdim=True)).T).abs().max(dim=1).values
+    assert (got.double() - ref).abs().max().item() < 1e-6
+    os.environ["TMX_PAIRWISE_X3_OFF"] = "1"
+    try:
+        exact = torch.ops.tmx.pairwise_abs_cos_rowmax(a, b)
+    finally:
+        del os.environ["TMX_PAIRWISE_X3_OFF"]
+    assert (got - exact).abs().max().item() < 1e-6
+    assert abs((1 - got).mean().item() - (1 - exact).mean().item()) < 1e-7

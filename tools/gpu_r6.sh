@@ -69,6 +69,8 @@ for s in "$@"; do
     pmc) run pmc 200 rocprofv3 --kernel-trace --pmc ${TMX_PMC:-SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU} -d "$OUT/pmc" -o pmc --output-format csv -- python3 bench.py --steps 5 --warmup 2; tail -1 "$OUT/pmc.log" ;;
     wtrace) run wtrace 200 python tools/window_trace.py; tail -c 3000 "$OUT/wtrace.log" ;;
     fwdbench) run fwdbench 200 python tools/forward_bench.py; tail -c 1500 "$OUT/fwdbench.log" ;;
+    ccprobe) for v in base spin; do run ccprobe_$v 200 python tools/compute_cost_probe.py $v; tail -c 700 "$OUT/ccprobe_$v.log"; echo; done ;;
+    pwx3) PW_SHAPES=${PW_SHAPES:-4096:4096:512,2048:2048:2048,8192:8192:256,10000:10000:2048,16384:2048:1024} PW_DTYPES=float32 PW_MODES=linear,cosine run pwx3 300 python tools/pairwise_bench.py; tail -1 "$OUT/pwx3.log" ;;
     *) echo "unknown step $s" ;;
   esac
 done

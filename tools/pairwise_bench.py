@@ -18,6 +18,8 @@ def main() -> None:
     ops.require()
     fns = {"linear": FP.pairwise_linear_similarity, "cosine": FP.pairwise_cosine_similarity,
            "euclidean": FP.pairwise_euclidean_distance}
+    if os.environ.get("PW_MODES"):  # e.g. "linear,cosine"
+        fns = {k: v for k, v in fns.items() if k in os.environ["PW_MODES"].split(",")}
     shapes = [(1000, 1000, 128), (4096, 4096, 512), (8192, 8192, 256), (16384, 2048, 1024), (2048, 2048, 4096)]
     if os.environ.get("PW_SHAPES"):  # "N:M:D,N:M:D,..." (crossover sweeps for the routing in functional/pairwise/helpers.py)
         shapes = [tuple(int(v) for v in t.split(":")) for t in os.environ["PW_SHAPES"].split(",")]
