@@ -34,7 +34,8 @@ def _fused_wins(mode: str, dtype: torch.dtype, n: int, m: int, d: int) -> bool:
     measured shape up to d = 1024 (1.05-4.2x); deeper, rocBLAS's dgemm out-runs the kernel's fp64 MFMA loop.  Linear / cosine are a plain library GEMM plus a diagonal fill / row normalisation: the
     kernel wins while the launches dominate, hipBLASLt beyond.  16-bit inputs with at least 256 128 x 128 output tiles
     run on the kernel's bf16 / fp16 MFMA tiles (1.0-3.3x over hipBLASLt + the epilogue up to 2^33 work and 2^25
-    outputs); smaller outputs take its fp32 MFMA tiles, which win only while the launches dominate."""
+    outputs); smaller outputs take its fp32 MFMA tiles, which win only while the launches dominate.  fp32 with at least
+    256 128 x 128 tiles runs on the f16-split matrix-core route at every depth."""
     work = n * m * d
     if mode == "euclidean":
         return d <= 1024 or work <= (1 << 31)
@@ -44,6 +45,10 @@ def _fused_wins(mode: str, dtype: torch.dtype, n: int, m: int, d: int) -> bool:
         if ((n + 127) // 128) * ((m + 127) // 128) >= 256:  # the kernel's 16-bit MFMA tiles (csrc: kPhT)
             return work <= (1 << 33) and n * m <= (1 << 25)
         return work <= (1 << 29) and d <= (256 if mode == "linear" else 1024)
+    if ((n + 127) // 128) * ((m + 127) // 128) >= 256:
+        # fp32 on f16 matrix cores (csrc/pairwise.hip x3: two-plane split, three products): 1.45-2.4x over hipBLASLt's
+        # fp32 GEMM from 2048^2 x 2048 to 10,000^2 x 2048 (profiles/pairwise_gemm_r6.json)
+        return True
     return work < (1 << 32) and d <= (512 if mode == "linear" else 1024)
 
 

@@ -304,11 +304,12 @@ class InceptionScore(Metric):
 
 
 def _rowmax_fused_wins(f1: Tensor, f2: Tensor) -> bool:
-    """The fused row-max kernel multiplies on fp32 (fp64) MFMA tiles: it wins while the launches and the N x M
-    round trips dominate, hipBLASLt's GEMM beyond (10,000 x 10,000 x 2048 fp32: 4.7 vs 3.9 ms,
-    ``profiles/mifid_rowmax_r5.json``) -- the pairwise cosine crossover."""
+    """The fused row-max kernel: fp32 with >= 256 128 x 128 tiles runs on f16 matrix cores (a two-plane split of
+    every fp32 row, three products; 2.4x over normalise + hipBLASLt matmul + min at 10,000 x 10,000 x 2048); smaller
+    fp32 / fp64 products take its exact fp32 / fp64 MFMA tiles while the launches and the N x M round trips dominate."""
     work = f1.shape[0] * f2.shape[0] * f1.shape[1]
-    if f1.dtype == torch.float64:
+    if f1.dtype == torch.float32 and ((f1.shape[0] + 127) // 128) * ((f2.shape[0] + 127) // 128) >= 256:
+        return True  # the f16-split matrix-core route (10,000^2 x 2048: 1.64 vs 3.87 ms, profiles/mifid_rowmax_r6.json)
         return work <= (1 << 29) and f1.shape[1] <= 256
     if f1.dtype in (torch.bfloat16, torch.float16):
         return work <= (1 << 29)
