@@ -6,7 +6,10 @@
 //
 // Pipeline (all on the metric's device; ATen is only used for the stable orderings):
 //   1. detections ordered by (image, class, score desc, input row) with two stable sorts; rank within the
-//      (image, class) pair; rows past maxDets[-1] dropped.  Ground truth ordered by (image, class, input row).
+//      (image, class) pair; rows past maxDets[-1] stay in the arrays but are never matched (each pair's detection
+//      count is clamped to maxDets[-1]) nor accumulated (maxDet clamped likewise) -- no data-dependent compaction,
+//      so no host synchronisation.  Ground truth ordered by (image, class, input row).  The (image, class) pairs are
+//      the dense grid image * K + class (no unique() and its host read) unless an IoU export needs sizes anyway.
 //   2. coco_match_kernel: one wave per (image, class) pair.  Lane l owns one (IoU threshold t, area range a)
 //      combination (l = t * A + a, so T * A <= 64) and runs the sequential greedy match of that combination:
 //      non-ignored ground truth first, crowd boxes re-matchable, ties resolved to the later ground truth exactly
@@ -22,7 +25,8 @@
 //      np.searchsorted(rc, thr, side="left") finds, computed with the same double arithmetic.
 //
 // Limits of the GPU path (the caller falls back to the C++ evaluator beyond them): T * A <= 64,
-// <= 1024 ground-truth boxes per (image, class) pair, <= 256 recall thresholds.
+// <= 1024 ground-truth boxes per (image, class) pair (a device flag, output 5, read with the caller's results),
+// <= 256 recall thresholds.
 #include "common.h"
 
 #include <limits>
@@ -77,6 +81,7 @@ __global__ __launch_bounds__(kCocoMatchWaves * kWave) void coco_match_kernel(
   const int64_t d0 = pairs.det_start[p], nd = pairs.det_count[p];
   const int64_t g0 = pairs.gt_start[p], ng = pairs.gt_count[p];
   const int64_t k = pairs.cls[p];
+  if (ng > kCocoMaxGt) return;  // beyond the LDS bitsets: flagged by the host op (the caller reruns on the host)
 
   auto iou_of = [&](int64_t d, int64_t g) -> double {
     if (custom) {
@@ -275,7 +280,7 @@ at::Tensor stable_order(const at::Tensor& key, bool descending) {
 // Same contract as the host op tmx::coco_evaluate (coco_eval.cpp), except that class labels come in already
 // mapped to class indices (det_cls / gt_cls in [0, K)), every tensor lives on the GPU, and iou_index lists only
 // the (image, class) pairs that hold a detection or a ground truth.
-std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor> coco_evaluate_gpu(
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor> coco_evaluate_gpu(
     const at::Tensor& det_boxes_, const at::Tensor& det_scores_, const at::Tensor& det_cls_, const at::Tensor& det_img_,
     const at::Tensor& det_area_, const at::Tensor& gt_boxes_, const at::Tensor& gt_cls_, const at::Tensor& gt_img_,
     const at::Tensor& gt_crowd_, const at::Tensor& gt_area_, int64_t K, int64_t num_images, const at::Tensor& iou_thrs_,
@@ -294,19 +299,21 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor> coco_eval
   const auto gt_crowd = i64(gt_crowd_);
   const auto iou_thrs = f64(iou_thrs_), rec_thrs = f64(rec_thrs_), area_rng = f64(area_rng_).reshape({-1, 2});
   const auto max_dets_cpu = max_dets_.to(at::kCPU, at::kLong).contiguous();
-  const auto max_dets = max_dets_cpu.to(dev);
-  const int64_t T = iou_thrs.numel(), R = rec_thrs.numel(), M = max_dets.numel(), A = area_rng.size(0);
+  const int64_t T = iou_thrs.numel(), R = rec_thrs.numel(), M = max_dets_cpu.numel(), A = area_rng.size(0);
   TORCH_CHECK(T > 0 && R > 0 && M > 0 && A > 0, "coco_evaluate_gpu: empty parameter list");
   TORCH_CHECK(T * A <= 64, "coco_evaluate_gpu: at most 64 (IoU threshold, area range) combinations");
   TORCH_CHECK(R <= kCocoMaxRec, "coco_evaluate_gpu: at most ", kCocoMaxRec, " recall thresholds");
   const int64_t max_det_last = max_dets_cpu.data_ptr<int64_t>()[M - 1];
+  // pycocotools truncates each (image, class) list at maxDets[-1] before accumulating every maxDet
+  const auto max_dets = max_dets_cpu.clamp_max(max_det_last).to(dev);
   const bool custom = img_iou_.has_value() && img_iou_->defined();
 
   auto precision = at::full({T, R, K, A, M}, -1.0, det_scores.options());
   auto recall = at::full({T, K, A, M}, -1.0, det_scores.options());
   auto scores_out = at::full({T, R, K, A, M}, -1.0, det_scores.options());
   auto lopt = det_cls.options();
-  if (K == 0) return {precision, recall, scores_out, at::zeros({0}, det_scores.options()), at::zeros({0, 5}, lopt)};
+  auto overflow = at::zeros({1}, lopt);
+  if (K == 0) return {precision, recall, scores_out, at::zeros({0}, det_scores.options()), at::zeros({0, 5}, lopt), overflow};
 
   // ---- 1. orderings ------------------------------------------------------------------------------------
   const auto det_pair = det_img * K + det_cls;
@@ -314,29 +321,33 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor> coco_eval
   order = order.index_select(0, stable_order(det_pair.index_select(0, order), false));
   const auto det_pair_sorted = det_pair.index_select(0, order);
   const auto first_of_pair = at::searchsorted(det_pair_sorted, det_pair_sorted, /*out_int32=*/false, /*right=*/false);
-  const auto rank_all = at::arange(det_pair_sorted.numel(), lopt) - first_of_pair;
-  const auto keep = at::nonzero(rank_all < max_det_last).reshape({-1});
-  const auto dsel = order.index_select(0, keep);  // kept detections in (image, class, rank) order
-  const auto d_pair = det_pair_sorted.index_select(0, keep);
-  const auto d_rank = rank_all.index_select(0, keep).to(at::kInt);
+  const auto d_rank = (at::arange(det_pair_sorted.numel(), lopt) - first_of_pair).to(at::kInt);
+  const auto& dsel = order;  // every detection in (image, class, rank) order
+  const auto& d_pair = det_pair_sorted;
   const auto gorder = stable_order(gt_img * K + gt_cls, false);
   const auto g_pair = (gt_img * K + gt_cls).index_select(0, gorder);
 
-  const auto pair_keys = std::get<0>(at::_unique(at::cat({d_pair, g_pair}), /*sorted=*/true));
+  // pairs: the dense (image, class) grid -- its size is known on the host -- unless an IoU export (which needs its
+  // total size on the host anyway) or a very large grid asks for the occupied pairs only
+  const bool dense = !export_iou && num_images * K <= (int64_t(1) << 22);
+  const auto pair_keys = dense ? at::arange(num_images * K, lopt) : std::get<0>(at::_unique(at::cat({d_pair, g_pair}), /*sorted=*/true));
   const int64_t P = pair_keys.numel();
   const auto det_start = at::searchsorted(d_pair, pair_keys, false, false);
-  const auto det_count = at::searchsorted(d_pair, pair_keys, false, true) - det_start;
+  const auto det_count = (at::searchsorted(d_pair, pair_keys, false, true) - det_start).clamp_max(max_det_last);
   const auto gt_start = at::searchsorted(g_pair, pair_keys, false, false);
   const auto gt_count = at::searchsorted(g_pair, pair_keys, false, true) - gt_start;
   const auto pair_cls = pair_keys.remainder(K);
   const auto pair_img = pair_keys.div(K, "floor");
   const auto pair_cells = det_count * gt_count;
   const auto iou_off = pair_cells.cumsum(0) - pair_cells;
-  // one host read for both the export size and the per-pair ground-truth limit
-  const auto host = at::stack({P ? pair_cells.sum() : at::zeros({}, lopt), P ? gt_count.max() : at::zeros({}, lopt)}).cpu();
-  const int64_t total_cells = host.data_ptr<int64_t>()[0];
-  TORCH_CHECK(host.data_ptr<int64_t>()[1] <= kCocoMaxGt, "coco_evaluate_gpu: more than ", kCocoMaxGt,
-              " ground-truth boxes of one class in one image");
+  if (P > 0) overflow = (gt_count.max() > kCocoMaxGt).to(at::kLong).reshape({1});
+  int64_t total_cells = 0;
+  if (export_iou && P > 0) {  // one host read: the export size and the per-pair ground-truth limit
+    const auto host = at::stack({pair_cells.sum(), gt_count.max()}).cpu();
+    total_cells = host.data_ptr<int64_t>()[0];
+    TORCH_CHECK(host.data_ptr<int64_t>()[1] <= kCocoMaxGt, "coco_evaluate_gpu: more than ", kCocoMaxGt,
+                " ground-truth boxes of one class in one image");
+  }
 
   const auto sd_box = det_boxes.index_select(0, dsel).contiguous();
   const auto sd_area = det_area.index_select(0, dsel).contiguous();
@@ -397,7 +408,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor> coco_eval
   TMX_LAUNCH_CHECK();
 
   auto iou_index = at::stack({pair_img, pair_cls, det_count, gt_count, iou_off}, 1);
-  return {precision, recall, scores_out, iou_values, iou_index};
+  return {precision, recall, scores_out, iou_values, iou_index, overflow};
 }
 
 }  // namespace tmx
@@ -408,7 +419,7 @@ TORCH_LIBRARY_FRAGMENT(tmx, m) {
       "Tensor gt_boxes, Tensor gt_cls, Tensor gt_img, Tensor gt_crowd, Tensor gt_area, int num_classes, "
       "int num_images, Tensor iou_thrs, Tensor rec_thrs, Tensor max_dets, Tensor area_rng, Tensor? img_iou, "
       "Tensor? img_iou_offsets, Tensor? det_local, Tensor? gt_local, Tensor? img_ng, bool export_iou) "
-      "-> (Tensor, Tensor, Tensor, Tensor, Tensor)");
+      "-> (Tensor, Tensor, Tensor, Tensor, Tensor, Tensor)");
 }
 
 TORCH_LIBRARY_IMPL(tmx, CUDA, m) { m.impl("coco_evaluate_gpu", &tmx::coco_evaluate_gpu); }

@@ -207,31 +207,38 @@ __global__ __launch_bounds__(kSsimThreads, 2) void ssim_v2_kernel(const float* _
 // tile and of the current one as its 8 K slots; Ay is built in that K order): no LDS round trip, no lane movement.
 // Exactness: every fp32 operand is split into two fp16 halves, x = hi + lo with hi = RNE16(x), lo = RNE16(x - hi)
 // (|x - hi - lo| <= 2^-23 |x|, unbiased), and each product is hi.hi + hi.lo + lo.hi with fp32 accumulation (the
-// omitted lo.lo is below 2^-22 of a term): the five window moments agree with the fp32 VALU kernel to ~1e-7 relative.
+// omitted lo.lo is below 2^-22 of a term): the window moments agree with the fp32 VALU kernel to ~1e-7 relative.
+// Four moments, not five: SSIM reads E[p^2] and E[t^2] only through their sum, so one window of (p^2 + t^2) serves.
 // fp16's range is met by exact power-of-two scaling: scores are multiplied by alpha = 2^(7 - ceil(log2 data_range)),
 // squares by alpha^2 / 256 and the weights by 64, so every fp16 operand stays below 2^13.5 and above the subnormals
 // for all but values 2^-21 below the window's largest; SSIM is evaluated in those scaled units with c1, c2 scaled
-// alike (SSIM is invariant to the common scale).  A lane that meets a scaled score above 2^7.5 (data outside
-// [-2.8 data_range, 2.8 data_range]) or a NaN / inf sets ``fallback``: the op then runs ssim_v2_kernel for the batch
+// alike (SSIM is invariant to the common scale).  A lane that meets a pixel pair with p^2 + t^2 above 2^15 in scaled
+// units (|(p, t)| beyond 1.41-2.8 data_range, depending on how far data_range is below a power of two) or a NaN / inf
+// sets ``fallback``: the op then runs ssim_v2_kernel for the batch
 // (a launch that exits at once otherwise) and takes its sums -- no host synchronisation either way.
-// The five moments per band and lane cost ~25 VALU per input value (scaling, squares, fp16 splits) and 30 MFMAs per
-// 256 output pixels; the fp32 VALU kernel above spends ~107 VALU instructions per output pixel on the taps.
+// The kernel is VALU-issue bound (SQ_ACTIVE_INST_VALU ~90 % of the wave time, profiles/ssim_mfma_pmc_r6.json): per
+// band and lane the work is the scaling / products (packed fp32, two columns per instruction), the fp16 splits
+// (three instructions per pair), 24 MFMAs and a packed epilogue over two output rows at a time; interior bands load
+// without the edge selects.
 typedef _Float16 h8_t __attribute__((ext_vector_type(8)));
 typedef float f4_t __attribute__((ext_vector_type(4)));
 typedef uint32_t u4_t __attribute__((ext_vector_type(4)));
 typedef uint32_t u2_t __attribute__((ext_vector_type(2)));
 constexpr int kSsimMfmaWaves = 4;    // independent waves (column tiles) per workgroup
-constexpr float kSsimMfmaBound = 181.f;  // 2^7.5: largest scaled score the fp16 operands take
+constexpr float kSsimMfmaQBound = 128.f;  // (p^2 + t^2) / 256 in scaled units: |p|, |t| <= 2^7.5 for the fp16 operands
 
-// two fp32 values -> (hi pair, lo pair) of packed fp16
+// two fp32 values -> (hi pair, lo pair) of packed fp16: hi = v_cvt_pk_f16_f32 (RNE), lo = RNE16(x - hi) by
+// v_fma_mix{lo,hi}_f16 reading hi's f16 halves directly (the fma's exact x - hi, one rounding to f16): three
+// instructions per pair instead of five (convert back, packed subtract, convert)
 __device__ __forceinline__ void split_pair(float a, float b, uint32_t& hi, uint32_t& lo) {
   typedef float f2x __attribute__((ext_vector_type(2)));
   typedef _Float16 h2x __attribute__((ext_vector_type(2)));
-  const h2x h = __builtin_convertvector(f2x{a, b}, h2x);  // v_cvt_pk_f16_f32 (RNE)
-  const f2x hf = __builtin_convertvector(h, f2x);
-  const h2x l = __builtin_convertvector(f2x{a, b} - hf, h2x);  // a - hi is exact in fp32
+  const h2x h = __builtin_convertvector(f2x{a, b}, h2x);
   hi = __builtin_bit_cast(uint32_t, h);
-  lo = __builtin_bit_cast(uint32_t, l);
+  uint32_t l;
+  asm("v_fma_mixlo_f16 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]" : "=v"(l) : "v"(hi), "v"(a));
+  asm("v_fma_mixhi_f16 %0, -%1, 1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "+v"(l) : "v"(hi), "v"(b));
+  lo = l;
 }
 template <int N>
 __device__ __forceinline__ void split_n(const float* v, uint32_t* hi, uint32_t* lo) {
@@ -276,23 +283,28 @@ __global__ __launch_bounds__(kSsimMfmaWaves * kWave) void ssim_mfma_kernel(
   const float c1 = consts[0] * U2, c2 = consts[1] * U2;
 
   // band operands (constants of the launch): Bx[x][c] = 64 w[x - c] for lane (c = i16, x = 8 g + j);
-  // Ay[i][r] = 64 w[r - i] for lane (i = i16, K slot 8 g + j = h row r(g, j)), r(g, j) = j < 4 ? 4 g + j : 16 + 4 g + j - 4
-  uint32_t bxh[4], bxl[4], ayh[4], ayl[4];
+  // Ay[i][r] = 64 w[r - i] for lane (i = i16, K slot 8 g + j = h row r(g, j)).  The vertical B operand is one
+  // 4-register tuple per moment whose halves alternate roles band by band (no register moves): even bands write the
+  // new h rows into the upper half (K order previous | current, r(g, j) = j < 4 ? 4 g + j : 16 + 4 g + j - 4), odd
+  // bands into the lower half (current | previous, the second Ay)
+  uint32_t bxh[4], bxl[4], ayh[2][4], ayl[2][4];
   {
-    float bx[8], ay[8];
+    float bx[8], ay0[8], ay1[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int dx = 8 * g + j - i16;
       bx[j] = dx >= 0 && dx < KS ? 64.f * w[dx] : 0.f;
-      const int r = j < 4 ? 4 * g + j : 16 + 4 * g + (j - 4);
-      const int dy = r - i16;
-      ay[j] = dy >= 0 && dy < KS ? 64.f * w[dy] : 0.f;
+      const int r0 = j < 4 ? 4 * g + j : 16 + 4 * g + (j - 4), r1 = j < 4 ? 16 + 4 * g + j : 4 * g + (j - 4);
+      ay0[j] = r0 - i16 >= 0 && r0 - i16 < KS ? 64.f * w[r0 - i16] : 0.f;
+      ay1[j] = r1 - i16 >= 0 && r1 - i16 < KS ? 64.f * w[r1 - i16] : 0.f;
     }
     split_n<8>(bx, bxh, bxl);
-    split_n<8>(ay, ayh, ayl);
+    split_n<8>(ay0, ayh[0], ayl[0]);
+    split_n<8>(ay1, ayh[1], ayl[1]);
   }
   const h8_t BXH = as_h8(bxh[0], bxh[1], bxh[2], bxh[3]), BXL = as_h8(bxl[0], bxl[1], bxl[2], bxl[3]);
-  const h8_t AYH = as_h8(ayh[0], ayh[1], ayh[2], ayh[3]), AYL = as_h8(ayl[0], ayl[1], ayl[2], ayl[3]);
+  const h8_t AYH[2] = {as_h8(ayh[0][0], ayh[0][1], ayh[0][2], ayh[0][3]), as_h8(ayh[1][0], ayh[1][1], ayh[1][2], ayh[1][3])};
+  const h8_t AYL[2] = {as_h8(ayl[0][0], ayl[0][1], ayl[0][2], ayl[0][3]), as_h8(ayl[1][0], ayl[1][1], ayl[1][2], ayl[1][3])};
 
   // this lane's input vectors of band b: row oy0 + 16 b + i16, columns c0 + 8 g .. + 7 (W % 4 == 0: whole float4s)
   const int xc = c0 + 8 * g;
@@ -309,10 +321,18 @@ __global__ __launch_bounds__(kSsimMfmaWaves * kWave) void ssim_mfma_kernel(
     v.w = ok ? v.w : 0.f;
     return v;
   };
+  const bool cols_in = c0 + 32 <= W;  // every lane's 8 columns inside the image (wave-uniform)
   auto fetch = [&](int b) {
     const int y = oy0 + 16 * b + i16;
-    const bool y_ok = y < H && b < nb;
     const int64_t o = static_cast<int64_t>(y) * W + xc;
+    if (cols_in && oy0 + 16 * b + 16 <= H && b < nb) {  // interior band (uniform): plain loads, no selects
+      np0 = *reinterpret_cast<const float4*>(Pp + o);
+      np1 = *reinterpret_cast<const float4*>(Pp + o + 4);
+      nt0 = *reinterpret_cast<const float4*>(Tp + o);
+      nt1 = *reinterpret_cast<const float4*>(Tp + o + 4);
+      return;
+    }
+    const bool y_ok = y < H && b < nb;
     np0 = ld(Pp, o, y_ok && x_ok0);
     np1 = ld(Pp, o + 4, y_ok && x_ok1);
     nt0 = ld(Tp, o, y_ok && x_ok0);
@@ -323,86 +343,107 @@ __global__ __launch_bounds__(kSsimMfmaWaves * kWave) void ssim_mfma_kernel(
   const int own_row_end = last_strip ? H : oy0 + strip;
   const bool own_lo = g < 2 || last_tile;
 
-  uint32_t prev_hi[5][2], prev_lo[5][2];  // h of the previous band, split (the vertical product's first 16 K slots)
+  u4_t vh[4], vl[4];  // per moment: the vertical B operand (h rows of two bands, split), halves alternating
   double acc_sim = 0.0, acc_cs = 0.0, acc_sse = 0.0;
   bool bad = false;
-  // two bands in flight: a band's loads are issued two band computations (~1.5 us) before its use -- one was not
-  // enough to cover the HBM latency at three waves per SIMD
+  const f2 c1v = {c1, c1}, c2v = {c2, c2};
+  // two bands in flight: a band's loads are issued two band computations before its use -- one was not enough to
+  // cover the HBM latency at three waves per SIMD
   fetch(0);
   cp0 = np0; cp1 = np1; ct0 = nt0; ct1 = nt1;
   fetch(1);
-  for (int b = 0; b < nb; ++b) {
-    const float p[8] = {cp0.x, cp0.y, cp0.z, cp0.w, cp1.x, cp1.y, cp1.z, cp1.w};
-    const float t[8] = {ct0.x, ct0.y, ct0.z, ct0.w, ct1.x, ct1.y, ct1.z, ct1.w};
+  auto band = [&](const int b, auto par_c) {
+    constexpr int par = decltype(par_c)::value;  // b & 1
+    // (p, t) pairs of the lane's 8 columns, packed as f2 {p, t}... -- the packed ops below take two columns at once
+    const f2 P[4] = {f2{cp0.x, cp0.y}, f2{cp0.z, cp0.w}, f2{cp1.x, cp1.y}, f2{cp1.z, cp1.w}};
+    const f2 T[4] = {f2{ct0.x, ct0.y}, f2{ct0.z, ct0.w}, f2{ct1.x, ct1.y}, f2{ct1.z, ct1.w}};
     cp0 = np0; cp1 = np1; ct0 = nt0; ct1 = nt1;
     if (b + 2 < nb) fetch(b + 2);
     float f_sse = 0.f;
     if constexpr (SSE) {
       const int y = oy0 + 16 * b + i16;
       if (own_lo && y < own_row_end && y < H) {
+        f2 e = {0.f, 0.f};
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float d = p[j] - t[j];
-          f_sse = fmaf(d, d, f_sse);  // (zero-filled columns past W add 0)
+        for (int j = 0; j < 4; ++j) {
+          const f2 d = P[j] - T[j];
+          e = __builtin_elementwise_fma(d, d, e);  // (zero-filled columns past W add 0)
         }
+        f_sse = e.x + e.y;
       }
     }
-    // scaled scores and their range check (NaN-propagating maximum: a NaN / inf fails the test)
-    float ps[8], ts[8];
-    float m = 0.f;
+    // scaled scores, their range check (NaN-propagating maximum: a NaN / inf fails it) and the four moment inputs
+    // in scaled units: p, t, (p^2 + t^2) / 256, p t / 256 (SSIM needs E[p^2] + E[t^2] only as a sum)
+    const f2 av = {alpha, alpha}, kv = {0.00390625f, 0.00390625f};
+    f2 ps[4], ts[4], qs[4], rs[4];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      ps[j] = p[j] * alpha;
-      ts[j] = t[j] * alpha;
-      m = __builtin_elementwise_maximum(m, __builtin_elementwise_maximum(__builtin_fabsf(ps[j]), __builtin_fabsf(ts[j])));
+    for (int j = 0; j < 4; ++j) {
+      ps[j] = P[j] * av;
+      ts[j] = T[j] * av;
+      const f2 tk = ts[j] * kv;
+      qs[j] = __builtin_elementwise_fma(ps[j], ps[j] * kv, ts[j] * tk);
+      rs[j] = ps[j] * tk;
     }
-    bad |= !(m <= kSsimMfmaBound);
-    // per moment (p, t, p^2 / 256, t^2 / 256, p t / 256 in scaled units): the horizontal pass of this band, its split,
-    // and the vertical pass for output tile b - 1 (h rows of bands b - 1 and b) -- one moment's values live at a time
-    f4_t v[5];
+    // range check on (p^2 + t^2) / 256 <= 128, i.e. p^2 + t^2 <= 2^15 (so |p|, |t| <= 2^7.5); NaN-propagating
+    // maximum: a NaN / inf fails it
+    auto mx3 = [](float a, float b, float c) { return __builtin_elementwise_maximum(__builtin_elementwise_maximum(a, b), c); };
+    const float m = mx3(mx3(qs[0].x, qs[0].y, qs[1].x), mx3(qs[1].y, qs[2].x, qs[2].y), __builtin_elementwise_maximum(qs[3].x, qs[3].y));
+    bad |= !(m <= kSsimMfmaQBound);
+    // per moment: the horizontal pass of this band, its split, and the vertical pass for output tile b - 1 (h rows of
+    // bands b - 1 and b) -- one moment's values live at a time
+    f4_t v[4];
 #pragma unroll
-    for (int mo = 0; mo < 5; ++mo) {
-      float x[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float a = mo == 0 || mo == 2 || mo == 4 ? ps[j] : ts[j];
-        const float c = mo == 2 ? ps[j] : ts[j];
-        x[j] = mo < 2 ? a : a * (c * 0.00390625f);
-      }
+    for (int mo = 0; mo < 4; ++mo) {
+      const f2* x = mo == 0 ? ps : mo == 1 ? ts : mo == 2 ? qs : rs;
       uint32_t ah[4], al[4];
-      split_n<8>(x, ah, al);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) split_pair(x[j].x, x[j].y, ah[j], al[j]);
       const f4_t hm = mfma3(as_h8(ah[0], ah[1], ah[2], ah[3]), as_h8(al[0], al[1], al[2], al[3]), BXH, BXL, f4_t{0.f, 0.f, 0.f, 0.f});
       uint32_t hh[2], hl[2];
       split_pair(hm[0], hm[1], hh[0], hl[0]);
       split_pair(hm[2], hm[3], hh[1], hl[1]);
+      vh[mo][2 - 2 * par] = hh[0]; vh[mo][3 - 2 * par] = hh[1];
+      vl[mo][2 - 2 * par] = hl[0]; vl[mo][3 - 2 * par] = hl[1];
       if (b > 0)
-        v[mo] = mfma3(AYH, AYL, as_h8(prev_hi[mo][0], prev_hi[mo][1], hh[0], hh[1]), as_h8(prev_lo[mo][0], prev_lo[mo][1], hl[0], hl[1]),
-                      f4_t{0.f, 0.f, 0.f, 0.f});
-      prev_hi[mo][0] = hh[0]; prev_hi[mo][1] = hh[1];
-      prev_lo[mo][0] = hl[0]; prev_lo[mo][1] = hl[1];
+        v[mo] = mfma3(AYH[par], AYL[par], __builtin_bit_cast(h8_t, vh[mo]), __builtin_bit_cast(h8_t, vl[mo]), f4_t{0.f, 0.f, 0.f, 0.f});
     }
-    float f_sim = 0.f, f_cs = 0.f;
+    f2 s_sim = {0.f, 0.f}, s_cs = {0.f, 0.f};
     if (b > 0) {
+      // U-scaled moments: mu = v, E[.] = v * 2^20 (see above); two output rows per packed op
       const int x = c0 + i16;
+      const int ybase = 16 * (b - 1) + 4 * g;  // output row (strip-relative) of r = 0
+      const bool all_ok = c0 + 16 <= Wv && 16 * (b - 1) + 16 <= orows;  // wave-uniform: no masking
+      const f2 e20 = {1048576.f, 1048576.f}, two = {2.f, 2.f};
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int y = oy0 + 16 * (b - 1) + 4 * g + r;
-        // U-scaled moments: mu = v, E[xy] = v * 2^20 (see above)
-        const float mp = v[0][r], mt = v[1][r];
-        const float epp = v[2][r] * 1048576.f, ett = v[3][r] * 1048576.f, ept = v[4][r] * 1048576.f;
-        const float mu_pp = mp * mp, mu_tt = mt * mt, mu_pt = mp * mt;
-        const float upper = 2.f * (ept - mu_pt) + c2;
-        const float lower = (epp - mu_pp) + (ett - mu_tt) + c2;
-        const float cs = upper * __builtin_amdgcn_rcpf(lower);
-        const float sim = (2.f * mu_pt + c1) * cs * __builtin_amdgcn_rcpf(mu_pp + mu_tt + c1);
-        const bool ok = x < Wv && y < oy0 + orows;
-        f_sim += ok ? sim : 0.f;
-        f_cs += ok ? cs : 0.f;
+      for (int h = 0; h < 2; ++h) {
+        const f2 mp = {v[0][2 * h], v[0][2 * h + 1]}, mt = {v[1][2 * h], v[1][2 * h + 1]};
+        const f2 e2 = f2{v[2][2 * h], v[2][2 * h + 1]} * e20, ept = f2{v[3][2 * h], v[3][2 * h + 1]} * e20;
+        const f2 mu_pt = mp * mt;
+        const f2 musum = __builtin_elementwise_fma(mp, mp, mt * mt);
+        const f2 upper = __builtin_elementwise_fma(two, ept - mu_pt, c2v);
+        const f2 lower = (e2 - musum) + c2v;
+        const f2 num1 = __builtin_elementwise_fma(two, mu_pt, c1v);
+        const f2 den1 = musum + c1v;
+        // hardware reciprocals (1 ulp) instead of IEEE divisions
+        const f2 cs = upper * f2{__builtin_amdgcn_rcpf(lower.x), __builtin_amdgcn_rcpf(lower.y)};
+        f2 sim = num1 * cs * f2{__builtin_amdgcn_rcpf(den1.x), __builtin_amdgcn_rcpf(den1.y)};
+        f2 csm = cs;
+        if (!all_ok) {
+          const bool ok0 = x < Wv && ybase + 2 * h < orows, ok1 = x < Wv && ybase + 2 * h + 1 < orows;
+          sim = f2{ok0 ? sim.x : 0.f, ok1 ? sim.y : 0.f};
+          csm = f2{ok0 ? cs.x : 0.f, ok1 ? cs.y : 0.f};
+        }
+        s_sim += sim;
+        s_cs += csm;
       }
     }
-    acc_sim += static_cast<double>(f_sim);
-    acc_cs += static_cast<double>(f_cs);
+    acc_sim += static_cast<double>(s_sim.x + s_sim.y);
+    acc_cs += static_cast<double>(s_cs.x + s_cs.y);
     acc_sse += static_cast<double>(f_sse);
+  };
+  for (int b = 0; b < nb; b += 2) {
+    band(b, std::integral_constant<int, 0>{});
+    if (b + 1 < nb) band(b + 1, std::integral_constant<int, 1>{});
   }
   acc_sim = wave_sum(acc_sim);
   acc_cs = wave_sum(acc_cs);

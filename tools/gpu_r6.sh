@@ -20,6 +20,7 @@ for s in "$@"; do
     synclat) for b in 200 1000 1500 3000; do run synclat_$b 120 ./build/kexp_r6/sync_latency_exp 50 $b; cat "$OUT/synclat_$b.log"; done ;;
     kexpmulti) for k in ${TMX_KEXP}; do run kexp_$k 120 ./build/kexp_r6/$k; echo "$k: $(tail -c 400 $OUT/kexp_$k.log)"; done ;;
     kexppmc) run kexppmc 120 rocprofv3 --kernel-trace --pmc ${TMX_PMC:-SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU} -d "$OUT/kexppmc" -o pmc --output-format csv -- ./build/kexp_r6/${TMX_KEXP:-exp} ;;
+    kexppmcmulti) for k in ${TMX_KEXP}; do run kexppmc_$k 120 rocprofv3 --kernel-trace --pmc ${TMX_PMC:-SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU} -d "$OUT/kexppmc_$k" -o pmc --output-format csv -- ./build/kexp_r6/$k; done ;;
     host) run host 120 python tools/host_overhead_probe.py ;;
     fidprof) run fidprof 200 rocprofv3 --kernel-trace --stats -d "$OUT/fidprof" -o fid --output-format csv -- python3 tools/fid_gram_bench.py ;;
     mifid) run mifid_bench 200 python tools/mifid_bench.py; tail -1 "$OUT/mifid_bench.log" ;;

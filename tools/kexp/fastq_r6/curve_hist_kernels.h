@@ -226,6 +226,72 @@ template <> __device__ __forceinline__ uint32_t pack_rne2<__half>(f32x2 q) {
   return __builtin_amdgcn_perm(rne_word<__half>(q.y), rne_word<__half>(q.x), 0x07060302u);
 }
 
+// exp_nonpos2 for pairs of rows whose every element is within 86 of its maximum (see row_tile_softmax_lean)
+__device__ __forceinline__ f32x2 exp_nonpos2_narrow(f32x2 x) {
+#pragma clang fp contract(off)
+  const float hi_s = __uint_as_float(0x3fb8aa3bu), lo_s = __uint_as_float(0x32a5705fu), magic = 12582912.f;
+  const f32x2 log2e_hi = {hi_s, hi_s}, log2e_lo = {lo_s, lo_s}, m2 = {magic, magic};
+  const f32x2 ph = x * log2e_hi;
+  f32x2 pl = __builtin_elementwise_fma(x, log2e_hi, -ph);
+  const f32x2 s = ph + m2;  // low bits: rint(ph)
+  const f32x2 e = s - m2;   // rint(ph), exact
+  pl = __builtin_elementwise_fma(x, log2e_lo, pl);
+  const f32x2 t = (ph - e) + pl;
+  const uint32_t ra = __float_as_uint(__builtin_amdgcn_exp2f(t.x)), rb = __float_as_uint(__builtin_amdgcn_exp2f(t.y));
+  return f32x2{__uint_as_float(ra + (__float_as_uint(s.x) << 23)), __uint_as_float(rb + (__float_as_uint(s.y) << 23))};
+}
+
+// ---- fast softmax with verified quotients (round 6) -----------------------------------------------------------------
+// A softmax code is DEFINED as RNE16(div_rn(exp_nonpos(x - max), s)): the correctly rounded quotient of expf's exact
+// instruction sequence (what ATen's softmax stores before its 16-bit rounding) by the row sum s.  Since round 6 s is
+// the fixed-order sum of FAST exponentials e_f(x) = v_exp_f32(RN(RN(x - max) L)), L = RN(log2 e) -- one multiply and
+// one v_exp per element instead of the 9-instruction exact sequence.  e_f(max) = 1 exactly (as ATen's exp(0)); the
+// other terms differ from expf's in the last bits only (the fp32 summation order already differs from ATen's).  The
+// class pass's refit reads s from row_stats, so every route produces the same codes for one batch.
+// The quotient of the common case (bf16, every element within 86 of its row maximum) is taken FAST and VERIFIED:
+// with r = 1 / s (correctly rounded) and d = RN(x - max), the exact quotient lies in [e_f r (1 - eps), e_f r (1 + eps)]:
+//   |RN(d L) - d log2e| <= 2^-24 |d| log2e (1 + 0.24)   (RN(d L) and L = log2e (1 + 0.24 2^-24))
+//     -> |e_f / exp(d) - 1| <= 1.24 2^-24 |d| + v_exp_f32's 1 ulp (2^-23),
+//   |exp_nonpos(d) / exp(d) - 1| <= 1 ulp, |r s - 1| <= 2^-24, and the roundings of r (1 -+ eps) <= 2^-24 each,
+// so eps = 2^-24 (1.25 (max - lane min) + 8) bounds it (the ulp terms in units of 2^-24: 2 + 2 + 1 + 1).  RNE16 and fp32 rounding are monotone: when
+// RNE16(fl(e_f r_lo)) == RNE16(fl(e_f r_hi)) the exact quotient rounds to that same code.  The element pairs where any
+// lane is undecided (~7 % of the pair slots of randn logits at C = 1000, 1e-3 of the elements) are collected in a
+// wave-uniform bit mask and recomputed with the exact sequence after the pass, patching the LDS image.  Per element
+// pair: sum pass sub, mul, 2 v_exp, add; quotient pass 2 mul, 2 conversions, 1 compare -- against ~17 instructions
+// for the exact exp + correctly rounded division.  fp16 keeps the exact quotient (its 10-bit codes put 8x as many
+// rounding boundaries in the window).
+constexpr float kLog2eF = 1.44269502163f;  // RN(log2 e) = 0x3fb8aa3b
+#ifndef TMX_FASTQ_RELOAD
+#define TMX_FASTQ_RELOAD 1  // the fallback re-reads the scores (1) or keeps the raw vectors in registers (0)
+#endif
+#ifndef TMX_FASTQ_RECOMPUTE
+#define TMX_FASTQ_RECOMPUTE 0  // 1: P keeps the scores and the quotient pass recomputes the fast exps (no reload)
+#endif
+#ifndef TMX_FASTQ_LDS
+#define TMX_FASTQ_LDS 0  // 1: each wave parks its raw rows in the (not yet written) LDS image; codes wait in registers
+#endif
+__device__ __forceinline__ f32x2 exp_fast2(f32x2 d) {  // d = x - max (<= 0, -inf or NaN)
+  const f32x2 t = d * f32x2{kLog2eF, kLog2eF};
+  return f32x2{__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)};
+}
+// relative half-width of the verification interval (see above); lane_min: the smallest element this lane holds
+__device__ __forceinline__ float fast_eps(float mx, float lane_min) { return (1.25f * (mx - lane_min) + 8.f) * 5.9604645e-8f; }
+template <typename T> struct FastQuot : std::false_type {};
+template <> struct FastQuot<__hip_bfloat16> : std::true_type {};
+// the code pair of (e.x, e.y) from the fast exps, and whether either could round differently from the definition
+template <typename T>
+__device__ __forceinline__ uint32_t fast_code2(f32x2 e, f32x2 rlo, f32x2 rhi, bool& undecided) {
+  const uint32_t lo = pack_rne2<T>(e * rlo), hi = pack_rne2<T>(e * rhi);
+  undecided = lo != hi;
+  return lo;
+}
+// the definition, for the exact paths and the fallback
+template <typename T>
+__device__ __forceinline__ uint32_t exact_code2(f32x2 x, f32x2 mx2, f32x2 s2, f32x2 i2, bool narrow) {
+  const f32x2 d = x - mx2;
+  return pack_rne2<T>(div_rn2(narrow ? exp_nonpos2_narrow(d) : exp_nonpos2(d), s2, i2));
+}
+
 // the 16-bit pattern of a score widened to fp32 (exact: bf16 / fp16 -> fp32 is lossless; NaN payloads may be
 // quietened for fp16, and every NaN pattern is a skip code anyway)
 template <typename T> __device__ __forceinline__ uint32_t half_bits(float f);
@@ -579,12 +645,15 @@ __device__ __forceinline__ void row_tile_compute(const RowLoads<NG>& L, int64_t 
     if constexpr (SOFTMAX) {
       f32x2 acc = {0.f, 0.f};
       const f32x2 mx2 = {ra.mx, rb.mx};
+      // the row sums of the fast exps, in the lean form's order (padding slots hold -inf: exp2(-inf) adds +0); then
+      // the exact exps (the definition's numerators) replace the scores
 #pragma unroll
       for (int j = 0; j < 8 * NG; ++j) {
-        const f32x2 e = exp_nonpos2(f32x2{ra.v[j], rb.v[j]} - mx2);
+        const f32x2 d = f32x2{ra.v[j], rb.v[j]} - mx2;
+        acc = acc + exp_fast2(d);
+        const f32x2 e = exp_nonpos2(d);
         ra.v[j] = e.x;
         rb.v[j] = e.y;
-        acc = acc + e;  // per row: the same sequential fp32 order as before
       }
       sa = wave_sum_uniform(acc.x);
       sb = wave_sum_uniform(acc.y);
@@ -599,7 +668,7 @@ __device__ __forceinline__ void row_tile_compute(const RowLoads<NG>& L, int64_t 
         f32x2 acc = {0.f, 0.f};
         const f32x2 mx2 = {ra.mx, rb.mx};
 #pragma unroll
-        for (int j = 0; j < 8 * NG; ++j) acc = acc + exp_nonpos2(f32x2{ra.v[j], rb.v[j]} - mx2);
+        for (int j = 0; j < 8 * NG; ++j) acc = acc + exp_fast2(f32x2{ra.v[j], rb.v[j]} - mx2);
         sa = wave_sum_uniform(acc.x);
         sb = wave_sum_uniform(acc.y);
       }
@@ -677,19 +746,6 @@ __device__ __forceinline__ void row_tile_compute(const RowLoads<NG>& L, int64_t 
 //    pair takes exp_nonpos2, the reference sequence;
 //  * the row minimum is only compared (ballots), never wave-reduced; the probability-mode witnesses are tested only
 //    while the block has not seen one (``rec && !saw_bad``), as before.
-__device__ __forceinline__ f32x2 exp_nonpos2_narrow(f32x2 x) {
-#pragma clang fp contract(off)
-  const float hi_s = __uint_as_float(0x3fb8aa3bu), lo_s = __uint_as_float(0x32a5705fu), magic = 12582912.f;
-  const f32x2 log2e_hi = {hi_s, hi_s}, log2e_lo = {lo_s, lo_s}, m2 = {magic, magic};
-  const f32x2 ph = x * log2e_hi;
-  f32x2 pl = __builtin_elementwise_fma(x, log2e_hi, -ph);
-  const f32x2 s = ph + m2;  // low bits: rint(ph)
-  const f32x2 e = s - m2;   // rint(ph), exact
-  pl = __builtin_elementwise_fma(x, log2e_lo, pl);
-  const f32x2 t = (ph - e) + pl;
-  const uint32_t ra = __float_as_uint(__builtin_amdgcn_exp2f(t.x)), rb = __float_as_uint(__builtin_amdgcn_exp2f(t.y));
-  return f32x2{__uint_as_float(ra + (__float_as_uint(s.x) << 23)), __uint_as_float(rb + (__float_as_uint(s.y) << 23))};
-}
 
 template <typename T, int NG>
 __device__ __forceinline__ void unpack_pair(const uint4& wa, const uint4& wb, f32x2* P) {
@@ -714,7 +770,7 @@ __device__ __forceinline__ float min8(const float* v) {
 }
 
 template <typename T, int NG, bool UNALIGNED = false>
-__device__ __forceinline__ void row_tile_softmax_lean(const RowLoads<NG>& L, int64_t n, int C, int ld, int64_t ignore_index,
+__device__ __forceinline__ void row_tile_softmax_lean(const T* __restrict__ preds, const RowLoads<NG>& L, int64_t n, int C, int ld, int64_t ignore_index,
                                                       bool has_ignore, int64_t* __restrict__ confmat, int* __restrict__ err, bool rec,
                                                       bool& saw_bad, SlowRows slow, uint32_t* __restrict__ s_tile, int64_t tile,
                                                       float4* __restrict__ row_stats, const PosSink& pos, PosTake& ptake) {
@@ -737,6 +793,14 @@ __device__ __forceinline__ void row_tile_softmax_lean(const RowLoads<NG>& L, int
   int am[4];
   bool keepv[4], slowv[4], validv[4];
   ptake = PosTake{-1, tv, 0u, kCodes, -1, kCodes, -1};
+#if TMX_FASTQ_LDS
+  // the fallback's scores: every wave parks its four rows in the LDS image region ([row in tile][group][lane] 16-B
+  // vectors, exactly the image's size), which nobody writes until the barrier after the pair loop -- the codes wait
+  // in registers (cv) meanwhile, so an undecided slot re-reads its scores from LDS instead of global memory
+  static_assert(kTileRows * kWave * 16 == 512 * kSlots * 4, "raw rows must fit the code image");
+  uint32_t cv[2][8 * NG];
+  uint4* const raw_lds = reinterpret_cast<uint4*>(s_tile);
+#endif
 #pragma unroll
   for (int pp = 0; pp < 2; ++pp) {
     const int p = wave + pp * kRowWaves;
@@ -751,6 +815,13 @@ __device__ __forceinline__ void row_tile_softmax_lean(const RowLoads<NG>& L, int
       realign_partial<NG>(wa, ld);
       realign_partial<NG>(wb, ld);
     }
+#if TMX_FASTQ_LDS
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      raw_lds[((2 * p) * NG + g) * kWave + lane] = wa[g];
+      raw_lds[((2 * p + 1) * NG + g) * kWave + lane] = wb[g];
+    }
+#endif
     {
       float a[8], b[8];
       unpack8<T>(wa[0], a);
@@ -800,7 +871,7 @@ __device__ __forceinline__ void row_tile_softmax_lean(const RowLoads<NG>& L, int
     const f32x2 mx2 = {mxa, mxb};
     f32x2 acc = {0.f, 0.f}, acc_lo = {0.f, 0.f};
     // the partial vector sits in the last class group (nvec - 1 >= 64 when NG == 2): scale its slots by 0 / 1
-    auto counted = [&](int j) -> f32x2 {
+    auto counted = [&](f32x2 e, int j) -> f32x2 {
       if constexpr (UNALIGNED
 #ifdef TMX_UNALIGNED_NOMASK_HACK  // timing experiment only
                     && false
@@ -808,23 +879,25 @@ __device__ __forceinline__ void row_tile_softmax_lean(const RowLoads<NG>& L, int
       ) {
         if (j >= 8 * (NG - 1)) {
           const float m = (j & 7) < (NG == 2 ? cut_hi : cut_lo) ? 1.f : 0.f;
-          return P[j] * f32x2{m, m};
+          return e * f32x2{m, m};
         }
       }
-      return P[j];
+      return e;
     };
-    if (narrow) {
+    // the row sums of the fast exps; on the fast path (bf16, narrow rows) the exps replace the scores in P, otherwise
+    // P keeps the scores for the exact quotients
+    const bool fast = FastQuot<T>::value && narrow;
+    if (fast && !TMX_FASTQ_RECOMPUTE) {
 #pragma unroll
       for (int j = 0; j < 8 * NG; ++j) {
-        P[j] = exp_nonpos2_narrow(P[j] - mx2);
-        acc = acc + counted(j);
+        P[j] = exp_fast2(P[j] - mx2);
+        acc = acc + counted(P[j], j);
         if (j == 7) acc_lo = acc;
       }
     } else {
 #pragma unroll
       for (int j = 0; j < 8 * NG; ++j) {
-        P[j] = exp_nonpos2(P[j] - mx2);
-        acc = acc + counted(j);
+        acc = acc + counted(exp_fast2(P[j] - mx2), j);
         if (j == 7) acc_lo = acc;
       }
     }
@@ -850,22 +923,71 @@ __device__ __forceinline__ void row_tile_softmax_lean(const RowLoads<NG>& L, int
     }
     const bool ka = va && fa, kb = vb && fb;
     const f32x2 s2 = {sa, sb}, i2 = {ia, ib};
-    if (ka && kb) {  // wave-uniform: both rows counted (the common case) -- no mask
+    // the pair's codes: fast and verified (bf16, narrow rows), else the exact definition from the scores
+    const float ea = fast_eps(mxa, mn_a), eb = fast_eps(mxb, mn_b);
+    const f32x2 rlo = {ia - ia * ea, ib - ib * eb}, rhi = {ia + ia * ea, ib + ib * eb};
+    const uint32_t keep = (ka ? 0x0000FFFFu : 0u) | (kb ? 0xFFFF0000u : 0u);
+    const uint32_t setm = ~keep & 0x80008000u;
+    auto raw_pair = [&](int j) -> f32x2 {  // the scores of slot j of both rows (the exact paths: rare)
+      const uint16_t a = raw_bits<T>(wa[j >> 3], j & 7), b = raw_bits<T>(wb[j >> 3], j & 7);
+      return f32x2{to_f32<T>(__builtin_bit_cast(T, a)), to_f32<T>(__builtin_bit_cast(T, b))};
+    };
+    auto put = [&](int j, uint32_t code) {
+#if TMX_FASTQ_LDS
+      cv[pp][j] = (code & keep) | setm;
+#else
+      const int c = 512 * (j >> 3) + 8 * lane + (j & 7);
+      s_tile[c * kSlots + (p ^ (lane & (kSlots - 1)))] = (code & keep) | setm;
+#endif
+    };
+    if (fast) {
+      uint32_t redo = 0;  // wave-uniform: slot j has an undecided pair in some lane
 #pragma unroll
       for (int j = 0; j < 8 * NG; ++j) {
-        const int c = 512 * (j >> 3) + 8 * lane + (j & 7);
-        s_tile[c * kSlots + (p ^ (lane & (kSlots - 1)))] = pack_rne2<T>(div_rn2(P[j], s2, i2));
+        bool und;
+        put(j, fast_code2<T>(TMX_FASTQ_RECOMPUTE ? exp_fast2(P[j] - mx2) : P[j], rlo, rhi, und));
+        redo |= (__ballot(und) != 0 ? 1u : 0u) << j;
+      }
+#ifdef TMX_FASTQ_NO_REDO  // timing experiment only: codes may differ from the definition
+      redo = 0;
+#endif
+      if (redo != 0) {  // rare: the undecided slots from the definition (same wave, same lanes: LDS order holds)
+        if constexpr (TMX_FASTQ_RECOMPUTE) {
+#pragma unroll
+          for (int j = 0; j < 8 * NG; ++j)
+            if ((redo >> j) & 1u) put(j, exact_code2<T>(P[j], mx2, s2, i2, true));
+        } else {
+#if TMX_FASTQ_LDS
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+          wa[g] = raw_lds[((2 * p) * NG + g) * kWave + lane];
+          wb[g] = raw_lds[((2 * p + 1) * NG + g) * kWave + lane];
+        }
+        if constexpr (false) {
+#else
+        if constexpr (TMX_FASTQ_RELOAD && !UNALIGNED) {
+#endif
+          // the scores again from memory (the pass's own reads: cache hits) instead of holding them in 16 VGPRs
+          const int lq = lo_ok ? lane : nvec - 1, hq = hi_ok ? lane + kWave : nvec - 1;
+          const uint4* ra = reinterpret_cast<const uint4*>(preds + min(r0, n - 1) * ld);
+          const uint4* rb = reinterpret_cast<const uint4*>(preds + min(r0 + 1, n - 1) * ld);
+          wa[0] = ra[lq];
+          wb[0] = rb[lq];
+          if constexpr (NG == 2) {
+            wa[1] = ra[hq];
+            wb[1] = rb[hq];
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < 8 * NG; ++j)
+          if ((redo >> j) & 1u) put(j, exact_code2<T>(raw_pair(j), mx2, s2, i2, true));
+        }
       }
     } else {
-      const uint32_t keep = (ka ? 0x0000FFFFu : 0u) | (kb ? 0xFFFF0000u : 0u);
-      const uint32_t setm = ~keep & 0x80008000u;
 #pragma unroll
-      for (int j = 0; j < 8 * NG; ++j) {
-        const int c = 512 * (j >> 3) + 8 * lane + (j & 7);
-        s_tile[c * kSlots + (p ^ (lane & (kSlots - 1)))] = (pack_rne2<T>(div_rn2(P[j], s2, i2)) & keep) | setm;
-      }
+      for (int j = 0; j < 8 * NG; ++j) put(j, exact_code2<T>(P[j], mx2, s2, i2, narrow));
     }
-    if (lane == 0 && pos.hist == nullptr) {
+    if (!TMX_FASTQ_LDS && lane == 0 && pos.hist == nullptr) {
       if (ka && ta >= 0 && ta < C) atomicOr(&s_tile[ta * kSlots + (p ^ ((int)(ta >> 3) & (kSlots - 1)))], 0x00004000u);
       if (kb && tb >= 0 && tb < C) atomicOr(&s_tile[tb * kSlots + (p ^ ((int)(tb >> 3) & (kSlots - 1)))], 0x40000000u);
     }
@@ -875,6 +997,23 @@ __device__ __forceinline__ void row_tile_softmax_lean(const RowLoads<NG>& L, int
     slowv[2 * pp] = slow_a; slowv[2 * pp + 1] = slow_b;
     validv[2 * pp] = va; validv[2 * pp + 1] = vb;
   }
+#if TMX_FASTQ_LDS
+  __syncthreads();  // every wave is done with its parked rows: the image may overwrite them
+#pragma unroll
+  for (int pp = 0; pp < 2; ++pp) {
+    const int p = wave + pp * kRowWaves;
+#pragma unroll
+    for (int j = 0; j < 8 * NG; ++j) {
+      const int c = 512 * (j >> 3) + 8 * lane + (j & 7);
+      s_tile[c * kSlots + (p ^ (lane & (kSlots - 1)))] = cv[pp][j];
+    }
+    if (lane == 0 && pos.hist == nullptr) {
+      const int64_t ta = tt[2 * pp], tb = tt[2 * pp + 1];
+      if (keepv[2 * pp] && ta >= 0 && ta < C) atomicOr(&s_tile[ta * kSlots + (p ^ ((int)(ta >> 3) & (kSlots - 1)))], 0x00004000u);
+      if (keepv[2 * pp + 1] && tb >= 0 && tb < C) atomicOr(&s_tile[tb * kSlots + (p ^ ((int)(tb >> 3) & (kSlots - 1)))], 0x40000000u);
+    }
+  }
+#endif
   if (pos.hist != nullptr) {
     pos_take(ptake, s_tile, keepv, tt, C, wave, row0_of(0), n);
     pos_book(ptake, pos, row_stats);
@@ -909,7 +1048,7 @@ __device__ __forceinline__ void row_tile(const T* __restrict__ preds, const int6
   PosTake ptake;
   if constexpr (FIXUP) pos = PosSink{};
   if constexpr (LEAN && SOFTMAX && !FIXUP)
-    row_tile_softmax_lean<T, NG, PADDED>(L, n, C, ld, ignore_index, has_ignore, confmat, err, rec, saw_bad, slow, s_tile, tile, row_stats, pos,
+    row_tile_softmax_lean<T, NG, PADDED>(preds, L, n, C, ld, ignore_index, has_ignore, confmat, err, rec, saw_bad, slow, s_tile, tile, row_stats, pos,
                                          ptake);
   else
     row_tile_compute<T, NG, SOFTMAX, FIXUP, PADDED>(L, n, C, ld, ignore_index, has_ignore, confmat, err, rec, saw_bad, slow, s_tile, tile,
@@ -2131,25 +2270,25 @@ __global__ void __launch_bounds__(kSmallRows * TL) TMX_SMALL_WPE_ATTR mc_codes_s
   float s = 0.f, inv = 0.f;
   // exp(x - max) of the slots and their row sum; the exps replace the scores in P only in softmax mode (probability
   // mode keeps the scores: they are the codes, the sum only feeds the class pass's refit statistics)
-  auto exp_sum = [&](bool store) -> float {
-    const f32x2 m2 = {mx, mx};
-    // every valid element of every row of the wave within 86 of its maximum: the lean exp (exp_nonpos2_narrow)
-    const bool narrow = __ballot(!(mx - mn <= 86.f)) == 0;
+  // round 6: the row sum of the fast exps (csrc/curve_hist_kernels.h fast_code2); the scores stay in P
+  const f32x2 m2 = {mx, mx};
+  // every valid element of every row of the wave within 86 of its maximum: verified fast quotients (bf16)
+  const bool narrow = __ballot(!(mx - mn <= 86.f)) == 0;
+  auto exp_sum = [&]() -> float {
     f32x2 acc = {0.f, 0.f};
 #pragma unroll
     for (int p = 0; p < kPairs; ++p) {
-      f32x2 e = narrow ? exp_nonpos2_narrow(P[p] - m2) : exp_nonpos2(P[p] - m2);
+      f32x2 e = exp_fast2(P[p] - m2);
       if (masked) {
         e.x = cb + 2 * p < C ? e.x : 0.f;
         e.y = cb + 2 * p + 1 < C ? e.y : 0.f;
       }
       acc = acc + e;
-      if (store) P[p] = e;
     }
     return grp_sum<TL>(acc.x + acc.y);
   };
   // softmax statistics: the codes in softmax mode, the class pass's refit of a mispredicted batch otherwise
-  if (use_mode != 0 || row_stats != nullptr) s = exp_sum(use_mode != 0);
+  if (use_mode != 0 || row_stats != nullptr) s = exp_sum();
   if (use_mode != 0) {
     inv = 1.f / s;
     fin = fin && s == s;
@@ -2175,9 +2314,18 @@ __global__ void __launch_bounds__(kSmallRows * TL) TMX_SMALL_WPE_ATTR mc_codes_s
     const f32x2 s2 = {s, s}, i2 = {inv, inv};
     const int tl = static_cast<int>(t) - cb;  // the positive's slot in this lane (any value when t is not here)
     const uint32_t tflag = TL > 1 ? 0u : 0x4000u << (16 * (tl & 1));
+    const bool fast = FastQuot<T>::value && narrow;
+    const float eps = fast_eps(mx, mn);  // (the row minimum bounds this lane's elements too)
+    const f32x2 rlo = {inv - inv * eps, inv - inv * eps}, rhi = {inv + inv * eps, inv + inv * eps};
 #pragma unroll
     for (int p = 0; p < kPairs; ++p) {
-      word[p] = pack_rne2<T>(div_rn2(P[p], s2, i2));
+      if (fast) {
+        bool und;
+        word[p] = fast_code2<T>(exp_fast2(P[p] - m2), rlo, rhi, und);
+        if (__ballot(und) != 0) word[p] = exact_code2<T>(P[p], m2, s2, i2, true);
+      } else {
+        word[p] = exact_code2<T>(P[p], m2, s2, i2, false);
+      }
       if constexpr (TL == 1) word[p] |= ((tl >> 1) == p && tl >= 0 ? tflag : 0u);
     }
   } else {

@@ -1,7 +1,7 @@
 // SSIM window A/B (round 6): the matrix-core kernel (ssim_mfma_kernel) vs the fp32 VALU kernel (ssim_v2_kernel) on
 // the same planes -- per-plane SSIM / CS / SSE sums and their difference, fallback flag, and timing at the BASELINE
 // config-4 shape (256 x 3 x 1024^2 fp32, 11-tap gaussian, sigma 1.5).
-// Build: hipcc -O3 --offload-arch=gfx950 -I csrc tools/kexp/ssim_mfma_exp.hip -o build/kexp_r6/ssim_mfma_exp
+// Build: hipcc -O3 --offload-arch=gfx950 -mllvm -amdgpu-mfma-vgpr-form=1 -I csrc tools/kexp/ssim_mfma_exp.hip -o build/kexp_r6/ssim_mfma_exp
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>

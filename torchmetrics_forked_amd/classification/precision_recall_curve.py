@@ -39,7 +39,7 @@ from torchmetrics_forked_amd.parallel.sync import _collective, sync_states
 from torchmetrics_forked_amd.utilities.distributed import gather_all_tensors
 from torchmetrics_forked_amd import ops
 from torchmetrics_forked_amd.ops import classification as cls_ops
-from torchmetrics_forked_amd.utilities.data import dim_zero_cat
+from torchmetrics_forked_amd.utilities.data import dim_zero_cat, dim_zero_sum
 from torchmetrics_forked_amd.utilities.validation import validation_mode
 from torchmetrics_forked_amd.utilities.enums import ClassificationTask
 from torchmetrics_forked_amd.utilities.plot import _AX_TYPE, _PLOT_OUT_TYPE, plot_curve
@@ -607,17 +607,35 @@ class _CurveMetric(Metric):
             shard = full.new_empty(per, *full.shape[1:])
             _collective(dist.reduce_scatter_tensor, shard, full.contiguous(), op=dist.ReduceOp.SUM,
                         what="reduce_scatter(score_hist)", group=group)
-            others = {k: v for k, v in self.metric_state.items() if k != "score_hist"}
-            for name, val in sync_states(others, self._reductions, group=group).items():
-                setattr(self, name, val)
+            self._sync_fixed_states([k for k in self._defaults if k != "score_hist"], group)
             first = rank * per
             owned = max(0, min(per, c - first))
             self.score_hist = shard[:owned]
             self._set_range(self.score_hist, rng_all[first : first + owned].contiguous(), None)
             self._shard_info = (first, owned, per, group)
             return
-        Metric._sync_dist(self, None, group)
+        self._sync_fixed_states(list(self._defaults), group)
         self._set_range(self.score_hist, rng_all.to(torch.int32).contiguous(), None)
+
+    def _sync_fixed_states(self, names: List[str], group: Optional[Any]) -> None:
+        """The sync-free path's remaining states: a sum-reduced tensor (the same shape on every rank) is one in-place
+        SUM all-reduce of a copy (the pre-sync value stays in the unsync cache); an empty list state stays empty (the
+        sync-free contract: every rank holds histograms, so no rank has list samples).  Anything else goes through the
+        generic gather, which may read sizes on the host."""
+        rest = {}
+        for name in names:
+            val = getattr(self, name)
+            if isinstance(val, Tensor) and self._reductions[name] is dim_zero_sum:
+                out = val.clone()
+                _collective(dist.all_reduce, out, op=dist.ReduceOp.SUM, what=f"all_reduce({name})", group=group)
+                setattr(self, name, out)
+            elif isinstance(val, list) and len(val) == 0:
+                continue
+            else:
+                rest[name] = val
+        if rest:
+            for name, val in sync_states(rest, self._reductions, group=group).items():
+                setattr(self, name, val)
 
     # ------------------------------------------------------------------------------------------- compute
     def _colmajor_ok(self, preds: Tensor) -> bool:

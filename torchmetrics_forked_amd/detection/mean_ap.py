@@ -46,13 +46,26 @@ _STAT_NAMES = (
 
 
 class _EvalResult:
-    __slots__ = ("precision", "recall", "iou_values", "iou_index", "cat_ids", "num_images")
+    __slots__ = ("precision", "recall", "iou_values", "iou_index", "cat_ids", "num_images", "overflow")
 
     def __init__(self, precision: Tensor, recall: Tensor, iou_values: Tensor, iou_index: Tensor, cat_ids: List[int],
-                 num_images: int):
+                 num_images: int, overflow: Optional[Tensor] = None):
         self.precision, self.recall, self.iou_values, self.iou_index, self.cat_ids, self.num_images = (
             precision, recall, iou_values, iou_index, cat_ids, num_images,
         )
+        # device flag of the GPU evaluator: a (image, class) pair past its ground-truth limit (the tables are then
+        # invalid and the host evaluator reruns; read together with the summary tables, no extra synchronisation)
+        self.overflow = overflow
+
+
+def _h2d(values: Sequence[Any], dtype: torch.dtype, dev: torch.device) -> Tensor:
+    """A host list as a device tensor without a stream synchronisation: ``torch.tensor(..., device=cuda)`` copies
+    from pageable memory, which waits for the stream; this stages through (cached) pinned memory and copies
+    asynchronously."""
+    t = torch.tensor(values, dtype=dtype)
+    if dev.type != "cuda":
+        return t
+    return t.pin_memory().to(dev, non_blocking=True)
 
 
 class MeanAveragePrecision(Metric):
@@ -359,12 +372,9 @@ class MeanAveragePrecision(Metric):
         def flat(lst: List[Tensor], n: int, dtype: torch.dtype, width: int = 0) -> Tensor:
             return self._flat_cached(lst, n, dtype, dev, width)
 
-        det_img = torch.repeat_interleave(
-            torch.arange(len(det_sizes), device=dev), torch.tensor(det_sizes, device=dev), output_size=n_det
-        )
-        gt_img = torch.repeat_interleave(
-            torch.arange(num_images, device=dev), torch.tensor(gt_sizes, device=dev), output_size=n_gt
-        )
+        det_sz, gt_sz = _h2d(det_sizes, torch.long, dev), _h2d(gt_sizes, torch.long, dev)
+        det_img = torch.repeat_interleave(torch.arange(len(det_sizes), device=dev), det_sz, output_size=n_det)
+        gt_img = torch.repeat_interleave(torch.arange(num_images, device=dev), gt_sz, output_size=n_gt)
         det_labels = flat(self.detection_labels, n_det, torch.long)
         gt_labels = flat(self.groundtruth_labels, n_gt, torch.long)
         det_scores = flat(self.detection_scores, n_det, torch.float64)
@@ -375,7 +385,7 @@ class MeanAveragePrecision(Metric):
             det_cls, gt_cls = torch.zeros_like(det_labels), torch.zeros_like(gt_labels)
         else:
             cat_ids = list(classes)
-            cats = torch.tensor(cat_ids, dtype=torch.long, device=dev)
+            cats = _h2d(cat_ids, torch.long, dev)
             det_cls = torch.searchsorted(cats, det_labels)
             gt_cls = torch.searchsorted(cats, gt_labels)
 
@@ -395,8 +405,8 @@ class MeanAveragePrecision(Metric):
         img_iou = img_off = det_local = gt_local = img_ng = None
         if i_type == "segm":
             img_iou, img_off = seg_iou, seg_off
-            img_ng = torch.tensor(gt_sizes, dtype=torch.long, device=dev)
-            det_first = torch.tensor(det_sizes, device=dev).cumsum(0) - torch.tensor(det_sizes, device=dev)
+            img_ng = gt_sz
+            det_first = det_sz.cumsum(0) - det_sz
             gt_first = img_ng.cumsum(0) - img_ng
             det_local = torch.arange(n_det, device=dev) - det_first[det_img]
             gt_local = torch.arange(n_gt, device=dev) - gt_first[gt_img]
@@ -406,13 +416,16 @@ class MeanAveragePrecision(Metric):
                 det_boxes, det_scores, det_cls, det_area = det_boxes[keep], det_scores[keep], det_cls[keep], det_area[keep]
                 det_img, det_local = det_img[keep], det_local[keep]
 
-        prec, rec, _scores, iou_values, iou_index = torch.ops.tmx.coco_evaluate_gpu(
+        prec, rec, _scores, iou_values, iou_index, overflow = torch.ops.tmx.coco_evaluate_gpu(
             det_boxes, det_scores, det_cls, det_img, det_area, gt_boxes, gt_cls, gt_img, gt_crowd, gt_area,
             len(cat_ids), num_images, *self._eval_params(dev),
             img_iou, img_off, det_local, gt_local, img_ng, self.extended_summary,
         )
-        # precision / recall stay on the device (summarised there, copied only for extended_summary)
-        return _EvalResult(prec, rec, iou_values.cpu(), iou_index.cpu(), cat_ids, num_images)
+        # precision / recall stay on the device (summarised there, copied only for extended_summary); the IoU export
+        # exists only for extended_summary (empty otherwise: no copy)
+        if self.extended_summary:
+            iou_values, iou_index = iou_values.cpu(), iou_index.cpu()
+        return _EvalResult(prec, rec, iou_values, iou_index, cat_ids, num_images, overflow)
 
     _param_cache: Optional[Tuple[Any, Tuple[Tensor, ...]]] = None
 
@@ -607,13 +620,15 @@ class MeanAveragePrecision(Metric):
             torch.tensor(_AREA_RANGES, dtype=torch.float64, device=dev),
         )
         cats = torch.tensor(classes, dtype=torch.long, device=dev)
-        if dev.type == "cuda" and ops.use_native(f["det_scores"]) and self._gpu_eligible_params():
-            prec, rec, _, _, _ = torch.ops.tmx.coco_evaluate_gpu(
+        gpu_ok = dev.type == "cuda" and ops.use_native(f["det_scores"]) and self._gpu_eligible_params()
+        if gpu_ok:
+            prec, rec, _, _, _, overflow = torch.ops.tmx.coco_evaluate_gpu(
                 f["det_boxes"], f["det_scores"], torch.searchsorted(cats, f["det_labels"]), f["det_img"], det_area,
                 f["gt_boxes"], torch.searchsorted(cats, f["gt_labels"]), f["gt_img"], f["gt_crowd"], gt_area,
                 len(classes), f["num_images"], *args, None, None, None, None, None, False,
             )
-        else:
+            gpu_ok = not bool(overflow.item())  # (this path reads its tables on the host below anyway)
+        if not gpu_ok:
             prec, rec, _, _, _ = torch.ops.tmx.coco_evaluate(
                 f["det_boxes"].cpu(), f["det_scores"].cpu(), f["det_labels"].cpu(), f["det_img"].cpu(), det_area.cpu(),
                 f["gt_boxes"].cpu(), f["gt_labels"].cpu(), f["gt_img"].cpu(), f["gt_crowd"].cpu(), gt_area.cpu(),
@@ -624,7 +639,7 @@ class MeanAveragePrecision(Metric):
         empty = torch.zeros(0)
         return _EvalResult(prec, rec, empty, torch.zeros(0, 5, dtype=torch.long), list(classes), f["num_images"])
 
-    def _summary_tables(self, precision: Tensor, recall: Tensor) -> np.ndarray:
+    def _summary_tables(self, precision: Tensor, recall: Tensor, overflow: Optional[Tensor] = None) -> Optional[np.ndarray]:
         """Sums and counts of the valid (``> -1``) entries of ``precision [T,R,K,A,M]`` (summed over R) and ``recall
         [T,K,A,M]``, as one host array ``[4, T, K, A, M]``: a few reductions where the tables live (the device, for the
         GPU evaluator) and ONE small copy, instead of copying both tables and slicing them twelve times per summary."""
@@ -634,7 +649,11 @@ class MeanAveragePrecision(Metric):
             torch.where(vp, precision, 0.0).sum(1, dtype=torch.float64), vp.sum(1, dtype=torch.float64),
             torch.where(vr, recall, 0.0).to(torch.float64), vr.to(torch.float64),
         ])
-        return tab.cpu().numpy()
+        if overflow is None:
+            return tab.cpu().numpy()
+        # the GPU evaluator's overflow flag travels in the same copy; None = the tables are invalid
+        both = torch.cat([tab.reshape(-1), overflow.to(torch.float64).reshape(-1)]).cpu().numpy()
+        return None if both[-1] != 0 else both[:-1].reshape(tab.shape)
 
     def _summarize_tables(self, tab: np.ndarray, k: Optional[int] = None) -> List[float]:
         """COCO ``summarize()`` statistics (all classes, or class index ``k``) from ``_summary_tables``: each statistic
@@ -704,7 +723,10 @@ class MeanAveragePrecision(Metric):
         for i_type in self.iou_type:
             prefix = "" if len(self.iou_type) == 1 else f"{i_type}_"
             ev = self._evaluate_sharded(classes) if sharded else self._evaluate(i_type, self.average, classes)
-            tab = self._summary_tables(ev.precision, ev.recall)
+            tab = self._summary_tables(ev.precision, ev.recall, ev.overflow)
+            if tab is None:  # > 1024 ground truths of one class in one image: the host evaluator
+                ev = self._evaluate_host(i_type, self.average, classes)
+                tab = self._summary_tables(ev.precision, ev.recall)
             result.update(self._coco_stats_to_tensor_dict(self._summarize_tables(tab), prefix))
             if self.extended_summary:
                 result[f"{prefix}ious"] = self._ious_dict(ev)
@@ -713,7 +735,10 @@ class MeanAveragePrecision(Metric):
             if self.class_metrics:
                 if self.average == "micro":
                     ev = self._evaluate(i_type, "macro", classes)
-                    tab = self._summary_tables(ev.precision, ev.recall)
+                    tab = self._summary_tables(ev.precision, ev.recall, ev.overflow)
+                    if tab is None:
+                        ev = self._evaluate_host(i_type, "macro", classes)
+                        tab = self._summary_tables(ev.precision, ev.recall)
                 map_pc, mar_pc = [], []
                 for k in range(len(classes)):
                     st = self._summarize_tables(tab, k)

@@ -65,6 +65,15 @@ def _common_flags() -> List[str]:
     ]
 
 
+# per-source extra flags: image.hip's SSIM kernel keeps its MFMA accumulators in VGPRs (the AGPR form read every
+# result back with one v_accvgpr_read per value: ~50 extra VALU instructions per band of its VALU-bound loop)
+_EXTRA_FLAGS = {"image.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]}
+
+
+def _flags_for(src: Path) -> List[str]:
+    return [*_common_flags(), *_EXTRA_FLAGS.get(src.name, [])]
+
+
 def sources() -> List[Path]:
     return sorted([*CSRC.glob("*.hip"), *CSRC.glob("*.cpp")])
 
@@ -116,7 +125,7 @@ def _compile(src: Path, digest: str, manifest: dict, force: bool) -> "tuple[Path
     obj = BUILD_DIR / (src.name + ".o")
     if not force and obj.exists() and manifest.get(src.name) == digest:
         return obj, False
-    cmd = [_hipcc(), *_common_flags(), "-c", str(src), "-o", str(obj)]
+    cmd = [_hipcc(), *_flags_for(src), "-c", str(src), "-o", str(obj)]
     proc = subprocess.run(cmd, capture_output=True, text=True)
     if proc.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src.name}:\n{' '.join(cmd)}\n{proc.stdout}\n{proc.stderr}")
@@ -128,7 +137,7 @@ def build(jobs: int = 8, force: bool = False, verbose: bool = True) -> Path:
     BUILD_DIR.mkdir(parents=True, exist_ok=True)
     srcs = sources()
     flags, headers = _common_flags(), _headers_digest()
-    digests = {s.name: source_digest(s, flags, headers) for s in srcs}
+    digests = {s.name: source_digest(s, [*flags, *_EXTRA_FLAGS.get(s.name, [])], headers) for s in srcs}
     manifest = _load_manifest()
     with ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
         results = list(ex.map(lambda s: _compile(s, digests[s.name], manifest, force), srcs))
