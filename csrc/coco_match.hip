@@ -277,6 +277,37 @@ at::Tensor stable_order(const at::Tensor& key, bool descending) {
 
 }  // namespace
 
+// (major ascending, fp32 score descending) as ONE int64 key: major << 32 | ~orderkey(score), where orderkey maps fp32
+// bits to an ascending uint32 (negatives bit-flipped, positives with the sign bit set).  One stable radix sort on it is
+// the reference's stable mergesort by score followed by the stable sort by major -- two merge sorts on doubles before.
+__global__ void coco_key_kernel(const int64_t* __restrict__ major, const float* __restrict__ score, int64_t n, int64_t* __restrict__ key) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float f = score[i];
+  // -0 sorts with +0 and every NaN with the positive quiet NaN (torch's sort: NaN above +inf), as the double sort did
+  const uint32_t u = f != f ? 0x7FC00000u : (f == 0.f ? 0u : __float_as_uint(f));
+  const uint32_t k = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+  key[i] = static_cast<int64_t>((static_cast<uint64_t>(major[i]) << 32) | static_cast<uint64_t>(~k));
+}
+
+namespace {
+
+// stable order by (major asc, score desc); scores exactly representable in fp32 (fp32 / fp16 / bf16 inputs)
+at::Tensor major_score_order(const at::Tensor& major, const at::Tensor& score32) {
+  const int64_t n = major.numel();
+  auto key = at::empty({n}, major.options());
+  if (n > 0) {
+    const auto mj = major.contiguous();
+    const auto sc = score32.contiguous();
+    hipLaunchKernelGGL(coco_key_kernel, dim3(static_cast<unsigned>((n + 255) / 256)), 256, 0, stream(), mj.data_ptr<int64_t>(),
+                       sc.data_ptr<float>(), n, key.data_ptr<int64_t>());
+    TMX_LAUNCH_CHECK();
+  }
+  return stable_order(key, false);
+}
+
+}  // namespace
+
 // Same contract as the host op tmx::coco_evaluate (coco_eval.cpp), except that class labels come in already
 // mapped to class indices (det_cls / gt_cls in [0, K)), every tensor lives on the GPU, and iou_index lists only
 // the (image, class) pairs that hold a detection or a ground truth.
@@ -317,8 +348,17 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tenso
 
   // ---- 1. orderings ------------------------------------------------------------------------------------
   const auto det_pair = det_img * K + det_cls;
-  at::Tensor order = stable_order(det_scores, /*descending=*/true);
-  order = order.index_select(0, stable_order(det_pair.index_select(0, order), false));
+  // fp32-exact scores (fp32 / fp16 / bf16 inputs; pair index < 2^31): one radix sort on a composite key
+  const bool key32 = (det_scores_.scalar_type() == at::kFloat || det_scores_.scalar_type() == at::kHalf ||
+                      det_scores_.scalar_type() == at::kBFloat16) && num_images * K < (int64_t(1) << 31);
+  const auto det_score32 = key32 ? det_scores_.to(dev, at::kFloat).contiguous() : at::Tensor();
+  at::Tensor order;
+  if (key32) {
+    order = major_score_order(det_pair, det_score32);
+  } else {
+    order = stable_order(det_scores, /*descending=*/true);
+    order = order.index_select(0, stable_order(det_pair.index_select(0, order), false));
+  }
   const auto det_pair_sorted = det_pair.index_select(0, order);
   const auto first_of_pair = at::searchsorted(det_pair_sorted, det_pair_sorted, /*out_int32=*/false, /*right=*/false);
   const auto d_rank = (at::arange(det_pair_sorted.numel(), lopt) - first_of_pair).to(at::kInt);
@@ -389,8 +429,13 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tenso
 
   // ---- 3. accumulate order: (class, score desc, image, rank) ------------------------------------------
   const auto d_cls = d_pair.remainder(K);
-  at::Tensor acc = stable_order(sd_score, true);
-  acc = acc.index_select(0, stable_order(d_cls.index_select(0, acc), false));
+  at::Tensor acc;
+  if (key32) {
+    acc = major_score_order(d_cls, det_score32.index_select(0, dsel));
+  } else {
+    acc = stable_order(sd_score, true);
+    acc = acc.index_select(0, stable_order(d_cls.index_select(0, acc), false));
+  }
   const auto a_rank = d_rank.index_select(0, acc).contiguous();
   const auto a_matched = matched.index_select(0, acc).contiguous();
   const auto a_ignored = ignored.index_select(0, acc).contiguous();

@@ -208,12 +208,17 @@ def _coco_inputs(seed, n_img, n_cls, max_det_img, max_gt_img, tie_scores):
     dict(seed=3, n_img=7, n_cls=2, max_det_img=0, max_gt_img=5, tie_scores=False, max_dets=[1, 10, 100]),
     dict(seed=4, n_img=9, n_cls=2, max_det_img=12, max_gt_img=0, tie_scores=False, max_dets=[1, 10, 100]),
 ])
-def test_coco_evaluate_gpu_matches_host(cfg):
+@pytest.mark.parametrize("score_dtype", [torch.float64, torch.float32])
+def test_coco_evaluate_gpu_matches_host(cfg, score_dtype):
     """Device matcher + accumulator (csrc/coco_match.hip) against the host evaluator (coco_eval.cpp): precision,
-    recall, score tables and exported IoUs are bit-identical (same double arithmetic)."""
+    recall, score tables and exported IoUs are bit-identical (same double arithmetic).  fp32 scores take the
+    composite-key radix orderings, fp64 the two stable sorts."""
     from torchmetrics_forked_amd.detection.mean_ap import _AREA_RANGES
 
     x = _coco_inputs(cfg["seed"], cfg["n_img"], cfg["n_cls"], cfg["max_det_img"], cfg["max_gt_img"], cfg["tie_scores"])
+    x["det_scores"] = x["det_scores"].to(score_dtype)
+    if score_dtype == torch.float32 and x["det_scores"].numel() > 3:
+        x["det_scores"][:3] = torch.tensor([0.0, -0.0, 0.5])  # signed zeros tie
     cats = torch.cat([x["det_labels"], x["gt_labels"]]).unique()
     iou_thr = torch.linspace(0.5, 0.95, 10, dtype=torch.float64)
     rec_thr = torch.linspace(0.0, 1.0, 101, dtype=torch.float64)
