@@ -1935,10 +1935,13 @@ __device__ __forceinline__ long long shfl_up_i64(long long v, int off) {
 
 // CLEAR (forward()'s batch histogram, round 6): every read segment is zeroed behind the read and the class's range
 // emptied, so the scratch is ready for the next batch without the separate zero + range-reset launches.
+__device__ __forceinline__ void curve_summary_block(const double* __restrict__ sc, int C, double* __restrict__ summary);
+
 template <bool CLEAR = false>
 __global__ void __launch_bounds__(kRedThreads) curve_hist_reduce_kernel(const int64_t* __restrict__ hist,
                                                                          const int* __restrict__ code_range,
-                                                                         double* __restrict__ out) {
+                                                                         double* __restrict__ out, int* __restrict__ done = nullptr,
+                                                                         double* __restrict__ summary = nullptr) {
   constexpr int K = kCodes;
   constexpr int kWaves = kRedThreads / kWave;
   const int c = blockIdx.x;
@@ -2029,6 +2032,21 @@ __global__ void __launch_bounds__(kRedThreads) curve_hist_reduce_kernel(const in
       int* cr = const_cast<int*>(code_range);
       cr[2 * c] = K;
       cr[2 * c + 1] = -1;
+    }
+  }
+  if (summary != nullptr) {
+    // the last block to finish folds every class's scores into the summary (no second launch): release this
+    // block's row of ``out``, count it, and the block that completes the count acquires all rows
+    __shared__ bool s_last;
+    if (tid == 0) {
+      __threadfence();
+      s_last = atomicAdd(done, 1) == static_cast<int>(gridDim.x) - 1;
+    }
+    __syncthreads();
+    if (s_last) {
+      __threadfence();
+      curve_summary_block(out, static_cast<int>(gridDim.x), summary);
+      if (tid == 0) *done = 0;  // ready for the next launch (stream order)
     }
   }
 }
@@ -2125,9 +2143,165 @@ at::Tensor curve_summary(const at::Tensor& scores_);
 // the reduce's last class block (device-wide completion counter) measured 33.7 us against 12.4 + 5.1 us -- every
 // block's agent-scope release fence has to write back its XCD's L2 (tests/test_compute_fused_gpu.py keeps the op's
 // contract; README round 4).
-std::vector<at::Tensor> curve_hist_scores(const at::Tensor& hist, c10::optional<at::Tensor> code_range, bool clear) {
-  auto sc = curve_hist_reduce_impl(hist, code_range, clear);
-  return {sc, curve_summary(sc)};
+// Wave-per-class form of the reduce (round 6): one 64-lane wave per class, four classes per 256-thread block, no LDS
+// and no block barriers in the scan -- the block form spends most of its ~13 us on the latency of its two barriers
+// per 4096-code chunk with ~70 of 256 threads holding codes (a class's occupied range is ~1-2k codes).  Lane l owns
+// kRedWavePer consecutive codes of a 64 * kRedWavePer chunk, walked from the top code down with carried prefix
+// counts; the per-element arithmetic (area of the trapezoids, precision at each positive) is the block form's.
+constexpr int kRedWavePer = 16;
+constexpr int kRedWaveChunk = kWave * kRedWavePer;
+constexpr int kRedWaveClasses = kRedThreads / kWave;
+
+template <bool CLEAR = false>
+__global__ void __launch_bounds__(kRedThreads) curve_hist_reduce_wave_kernel(const int64_t* __restrict__ hist, const int* __restrict__ code_range,
+                                                                              double* __restrict__ out, int C, int* __restrict__ done,
+                                                                              double* __restrict__ summary) {
+  constexpr int K = kCodes;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int c = blockIdx.x * kRedWaveClasses + static_cast<int>(threadIdx.x / kWave);
+  if (c < C) {
+    int lo = 0, hi = K - 1;
+    if (code_range != nullptr) {
+      lo = max(code_range[2 * c], 0);
+      hi = min(code_range[2 * c + 1], K - 1);
+    }
+    const int64_t* negh = hist + ((int64_t)c * 2 + 0) * K;
+    const int64_t* posh = hist + ((int64_t)c * 2 + 1) * K;
+    long long carry_p = 0, carry_n = 0;
+    double area = 0.0, ap_sum = 0.0;
+    if (hi >= lo) {
+      const int top = hi | (kRedWavePer - 1), bottom = lo & ~(kRedWavePer - 1);
+      for (int chunk_top = top; chunk_top >= bottom; chunk_top -= kRedWaveChunk) {
+        const int seg_hi = chunk_top - kRedWavePer * lane;
+        long long p[kRedWavePer], n[kRedWavePer];  // index i = i-th highest owned code
+        if (seg_hi >= bottom) {
+          const longlong2* negv = reinterpret_cast<const longlong2*>(negh + (seg_hi - (kRedWavePer - 1)));
+          const longlong2* posv = reinterpret_cast<const longlong2*>(posh + (seg_hi - (kRedWavePer - 1)));
+#pragma unroll
+          for (int v = 0; v < kRedWavePer / 2; ++v) {
+            const longlong2 a = posv[v], b = negv[v];
+            p[kRedWavePer - 1 - 2 * v] = a.x; p[kRedWavePer - 2 - 2 * v] = a.y;
+            n[kRedWavePer - 1 - 2 * v] = b.x; n[kRedWavePer - 2 - 2 * v] = b.y;
+          }
+          if constexpr (CLEAR) {  // (codes of the aligned segment outside [lo, hi] are zero already)
+            longlong2* pw = const_cast<longlong2*>(posv);
+            longlong2* nw = const_cast<longlong2*>(negv);
+#pragma unroll
+            for (int v = 0; v < kRedWavePer / 2; ++v) {
+              pw[v] = make_longlong2(0, 0);
+              nw[v] = make_longlong2(0, 0);
+            }
+          }
+        } else {
+#pragma unroll
+          for (int i = 0; i < kRedWavePer; ++i) p[i] = n[i] = 0;
+        }
+        long long sp = 0, sn = 0;
+#pragma unroll
+        for (int i = 0; i < kRedWavePer; ++i) { sp += p[i]; sn += n[i]; }
+        long long ip = sp, in = sn;  // inclusive wave scan in lane order (= descending code order)
+#pragma unroll
+        for (int off = 1; off < kWave; off <<= 1) {
+          const long long tp = shfl_up_i64(ip, off), tn = shfl_up_i64(in, off);
+          if (lane >= off) { ip += tp; in += tn; }
+        }
+        long long tp = carry_p + ip - sp, fp = carry_n + in - sn;  // positives / negatives above this lane
+#pragma unroll
+        for (int i = 0; i < kRedWavePer; ++i) {
+          const long long pk = p[i], nk = n[i];
+          tp += pk;
+          fp += nk;
+          area += (double)nk * (double)(2 * (tp - pk) + pk);
+          if (pk) ap_sum += (double)pk * ((double)tp / (double)(tp + fp));
+        }
+        carry_p += __shfl(ip, kWave - 1, kWave);
+        carry_n += __shfl(in, kWave - 1, kWave);
+      }
+    }
+    area = wave_sum(area);
+    ap_sum = wave_sum(ap_sum);
+    if (lane == 0) {
+      const long long P = carry_p, N = carry_n;
+      out[c * 4 + 0] = (P > 0 && N > 0) ? area / (2.0 * (double)P * (double)N) : 0.0;
+      out[c * 4 + 1] = P > 0 ? ap_sum / (double)P : NAN;
+      out[c * 4 + 2] = (double)P;
+      out[c * 4 + 3] = (double)N;
+      if constexpr (CLEAR) {  // every lane read lo / hi at the start (program order within the wave)
+        int* cr = const_cast<int*>(code_range);
+        cr[2 * c] = K;
+        cr[2 * c + 1] = -1;
+      }
+    }
+  }
+  if (summary != nullptr) {  // the last block folds the summary (see curve_hist_reduce_kernel)
+    __shared__ bool s_last;
+    __syncthreads();  // every wave's row of ``out`` is written
+    if (threadIdx.x == 0) {
+      __threadfence();
+      s_last = atomicAdd(done, 1) == static_cast<int>(gridDim.x) - 1;
+    }
+    __syncthreads();
+    if (s_last) {
+      __threadfence();
+      curve_summary_block(out, C, summary);
+      if (threadIdx.x == 0) *done = 0;
+    }
+  }
+}
+
+// a zero-initialised int per (device, stream) for the reduce's last-block count (each launch leaves it at zero again;
+// launches on one stream are ordered, so they never share it concurrently)
+static int* reduce_done_counter(const at::Device& dev) {
+  static std::mutex mu;
+  static std::map<std::pair<int, hipStream_t>, at::Tensor> counters;
+  std::lock_guard<std::mutex> lock(mu);
+  const auto key = std::make_pair(static_cast<int>(dev.index()), stream());
+  auto it = counters.find(key);
+  if (it == counters.end()) it = counters.emplace(key, at::zeros({1}, at::TensorOptions().dtype(at::kInt).device(dev))).first;
+  return it->second.data_ptr<int>();
+}
+
+// scores [C, 4] and the summary [12] in ONE launch (the last reduce block folds the summary)
+std::vector<at::Tensor> curve_hist_scores(const at::Tensor& hist_, c10::optional<at::Tensor> code_range, bool clear) {
+  TORCH_CHECK(!clear || (hist_.is_contiguous() && code_range.has_value()), "curve_hist_reduce: clear needs a contiguous histogram and its range");
+  auto hist = hist_.contiguous();
+  TORCH_CHECK(hist.scalar_type() == at::kLong && hist.dim() == 3 && hist.size(1) == 2 && hist.size(2) == kCodes,
+              "curve_hist_reduce: hist must be int64 [C, 2, 16384]");
+  const int* cr = nullptr;
+  if (code_range.has_value()) {
+    TORCH_CHECK(code_range->scalar_type() == at::kInt && code_range->numel() == 2 * hist.size(0) && code_range->is_contiguous() &&
+                code_range->device() == hist.device(), "code_range must be int32[C, 2] on the histogram's device");
+    cr = code_range->data_ptr<int>();
+  }
+  const int C = static_cast<int>(hist.size(0));
+  auto out = at::empty({C, 4}, hist.options().dtype(at::kDouble));
+  if (C == 0) return {out, curve_summary(out)};
+  auto summary = at::empty({12}, out.options());
+  int* done = reduce_done_counter(hist.device());
+  // wave-per-class form for compute()'s reduce (22 vs 31 us with the summary, tools/reduce_bench.py), the block form for
+  // forward()'s clearing one (28 vs 22 us: the wave form's zeroing stores serialise behind its loads);
+  // profiles/reduce_bench_r6.json.  TMX_REDUCE_FORM=block|wave forces one form.
+  static const char* form = std::getenv("TMX_REDUCE_FORM");
+  const bool wave_form = form != nullptr ? std::string(form) == "wave" : !clear;
+  if (wave_form) {
+    const unsigned blocks = static_cast<unsigned>((C + kRedWaveClasses - 1) / kRedWaveClasses);
+    if (clear)
+      hipLaunchKernelGGL(curve_hist_reduce_wave_kernel<true>, blocks, kRedThreads, 0, stream(), hist.data_ptr<int64_t>(), cr,
+                         out.data_ptr<double>(), C, done, summary.data_ptr<double>());
+    else
+      hipLaunchKernelGGL(curve_hist_reduce_wave_kernel<false>, blocks, kRedThreads, 0, stream(), hist.data_ptr<int64_t>(), cr,
+                         out.data_ptr<double>(), C, done, summary.data_ptr<double>());
+    TMX_LAUNCH_CHECK();
+    return {out, summary};
+  }
+  if (clear)
+    hipLaunchKernelGGL(curve_hist_reduce_kernel<true>, C, kRedThreads, 0, stream(), hist.data_ptr<int64_t>(), cr, out.data_ptr<double>(), done,
+                       summary.data_ptr<double>());
+  else
+    hipLaunchKernelGGL(curve_hist_reduce_kernel<false>, C, kRedThreads, 0, stream(), hist.data_ptr<int64_t>(), cr, out.data_ptr<double>(), done,
+                       summary.data_ptr<double>());
+  TMX_LAUNCH_CHECK();
+  return {out, summary};
 }
 
 at::Tensor curve_summary(const at::Tensor& scores_) {

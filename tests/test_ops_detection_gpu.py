@@ -337,3 +337,16 @@ def test_panoptic_segment_keys_kernel_paths(big_ids):
     torch.testing.assert_close(mg.compute().cpu(), mc.compute(), atol=1e-12, rtol=0)
     keys = torch.ops.tmx.panoptic_segment_keys(p.reshape(3, -1, 2).cuda(), t.reshape(3, -1, 2).cuda(), torch.tensor([0, 1, 6, 7]).cuda(), torch.tensor([0, 1, 2, 3, 4]).cuda())
     assert int(keys[2].item()) == int(big_ids)
+
+
+def test_upload_i64_pinned_staging():
+    """tmx::upload_i64: host int64 -> device through the reused pinned buffer, back-to-back calls of growing size (the
+    buffer is reused only after the previous copy completed)."""
+    like = torch.zeros(1, device="cuda")
+    outs = []
+    for n in (0, 5, 1000, 70000, 3):
+        h = torch.arange(n, dtype=torch.long) * 7 - 3
+        d = torch.ops.tmx.upload_i64(h, like)
+        outs.append((h, d))
+    for h, d in outs:
+        assert d.is_cuda and d.dtype == torch.long and torch.equal(d.cpu(), h)

@@ -60,10 +60,15 @@ class _EvalResult:
         self.overflow = overflow
 
 
-def _h2d_many(lists: Sequence[Sequence[int]], dev: torch.device) -> List[Tensor]:
-    """Several host int lists as int64 device tensors in ONE host-to-device copy (each ``torch.tensor(..., device=)``
-    is a ~20 us pageable copy on the host's critical path; staging through fresh pinned memory costs more)."""
-    flat = torch.tensor([v for lst in lists for v in lst], dtype=torch.long, device=dev)
+def _h2d_many(lists: Sequence[Sequence[int]], like: Tensor) -> List[Tensor]:
+    """Several host int lists as int64 tensors on ``like``'s device in ONE asynchronous copy through a reused pinned
+    buffer (``tmx::upload_i64``): a ``torch.tensor(..., device=cuda)`` copy from pageable memory waits for every
+    kernel queued before it, and fresh pinned memory per call costs more than the copy."""
+    flat = torch.tensor([v for lst in lists for v in lst], dtype=torch.long)
+    if like.is_cuda and ops.load():
+        flat = torch.ops.tmx.upload_i64(flat, like)
+    else:
+        flat = flat.to(like.device)
     return list(flat.split([len(lst) for lst in lists]))
 
 
@@ -296,7 +301,10 @@ class MeanAveragePrecision(Metric):
                 for lst in (self.detection_labels, self.groundtruth_labels)
                 if len(lst)
             ]
-            return torch.cat(parts).unique().cpu().tolist()
+            uniq = torch.cat(parts).unique()
+            self.__dict__["_classes_dev"] = uniq  # the evaluator's sorted class ids, without a host round trip
+            return uniq.cpu().tolist()
+        self.__dict__["_classes_dev"] = None
         return []
 
     _flat_cache: Optional[Dict[Tuple[int, torch.dtype, str, int], Tensor]] = None
@@ -369,7 +377,10 @@ class MeanAveragePrecision(Metric):
         def flat(lst: List[Tensor], n: int, dtype: torch.dtype, width: int = 0) -> Tensor:
             return self._flat_cached(lst, n, dtype, dev, width)
 
-        det_sz, gt_sz, cats = _h2d_many([det_sizes, gt_sizes, [] if average == "micro" else classes], dev)
+        det_sz, gt_sz = _h2d_many([det_sizes, gt_sizes], _first(self.detection_labels or self.groundtruth_labels))
+        cats = self.__dict__.get("_classes_dev")
+        if average != "micro" and (cats is None or cats.numel() != len(classes) or cats.device != dev):
+            cats = torch.tensor(classes, dtype=torch.long, device=dev)
         det_img = torch.repeat_interleave(torch.arange(len(det_sizes), device=dev), det_sz, output_size=n_det)
         gt_img = torch.repeat_interleave(torch.arange(num_images, device=dev), gt_sz, output_size=n_gt)
         det_labels = flat(self.detection_labels, n_det, torch.long)
@@ -717,6 +728,7 @@ class MeanAveragePrecision(Metric):
         finally:
             self._segm_cache = None
             self._flat_cache = None
+            self.__dict__["_classes_dev"] = None
 
     def _compute(self) -> dict:
         sharded = self._shard_flat is not None

@@ -257,6 +257,10 @@ class Metric(Module, ABC):
         self._defaults[name] = deepcopy(default)
         self._persistent[name] = persistent
         self._reductions[name] = fx
+        # an all-zero tensor default (decided here, while it is still a host / freshly built tensor) resets by a fill,
+        # not by a device copy of the default: half the memory traffic for large states (a 1000 x 1000 confusion matrix)
+        zd = self.__dict__.setdefault("_zero_default", {})
+        zd[name] = isinstance(default, Tensor) and default.device.type == "cpu" and default.numel() > 0 and not bool(default.any())
 
     # ---------------------------------------------------------------------------------------------- forward
     @torch.jit.unused
@@ -813,11 +817,15 @@ class Metric(Module, ABC):
         self._update_count = 0
         self._forward_cache = None
         self._computed = None
+        zero = self.__dict__.get("_zero_default", {})
         for name, default in self._defaults.items():
             if isinstance(default, Tensor):
                 current = getattr(self, name)
                 dev = current.device if isinstance(current, Tensor) else default.device
-                setattr(self, name, default.detach().clone().to(dev))
+                if zero.get(name):
+                    setattr(self, name, torch.zeros(default.shape, dtype=default.dtype, device=dev))
+                else:
+                    setattr(self, name, default.detach().clone().to(dev))
             else:
                 setattr(self, name, StateArena())
         self._cache = None
