@@ -2282,7 +2282,7 @@ std::vector<at::Tensor> curve_hist_scores(const at::Tensor& hist_, c10::optional
   // forward()'s clearing one (28 vs 22 us: the wave form's zeroing stores serialise behind its loads);
   // profiles/reduce_bench_r6.json.  TMX_REDUCE_FORM=block|wave forces one form.
   static const char* form = std::getenv("TMX_REDUCE_FORM");
-  const bool wave_form = form != nullptr ? std::string(form) == "wave" : !clear;
+  const bool wave_form = !clear && (form == nullptr || std::string(form) == "wave");
   if (wave_form) {
     const unsigned blocks = static_cast<unsigned>((C + kRedWaveClasses - 1) / kRedWaveClasses);
     if (clear)
@@ -2294,10 +2294,14 @@ std::vector<at::Tensor> curve_hist_scores(const at::Tensor& hist_, c10::optional
     TMX_LAUNCH_CHECK();
     return {out, summary};
   }
-  if (clear)
-    hipLaunchKernelGGL(curve_hist_reduce_kernel<true>, C, kRedThreads, 0, stream(), hist.data_ptr<int64_t>(), cr, out.data_ptr<double>(), done,
-                       summary.data_ptr<double>());
-  else
+  if (clear) {
+    // forward's clearing reduce keeps the summary as its own launch: the last-block fold needs a device-scope release
+    // per block (an L2 write-back), which behind 18 MB of zeroing stores cost 57 vs 17 + 5 us (profiles/reduce_bench_r6.json)
+    hipLaunchKernelGGL(curve_hist_reduce_kernel<true>, C, kRedThreads, 0, stream(), hist.data_ptr<int64_t>(), cr, out.data_ptr<double>(),
+                       nullptr, nullptr);
+    TMX_LAUNCH_CHECK();
+    return {out, curve_summary(out)};
+  } else
     hipLaunchKernelGGL(curve_hist_reduce_kernel<false>, C, kRedThreads, 0, stream(), hist.data_ptr<int64_t>(), cr, out.data_ptr<double>(), done,
                        summary.data_ptr<double>());
   TMX_LAUNCH_CHECK();

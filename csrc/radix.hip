@@ -1188,7 +1188,7 @@ __global__ void __launch_bounds__(256) os_hist_kernel(const T* __restrict__ x, i
   }
 }
 
-template <typename T>
+template <typename T, int ITEMS = kRsItems>
 __global__ void __launch_bounds__(kRsThreads) os_pass_kernel(const T* __restrict__ x, typename SortKey<T>::type* __restrict__ kb0,
                                                                typename SortKey<T>::type* __restrict__ kb1, uint32_t* __restrict__ pb0,
                                                                uint32_t* __restrict__ pb1, T* __restrict__ vals, int64_t* __restrict__ idx,
@@ -1197,14 +1197,15 @@ __global__ void __launch_bounds__(kRsThreads) os_pass_kernel(const T* __restrict
                                                                const typename SortKey<T>::type* __restrict__ andor, int* __restrict__ err) {
   using KT = typename SortKey<T>::type;
   constexpr int P = static_cast<int>(sizeof(KT));
+  constexpr int TILE = kRsThreads * ITEMS;
   __shared__ uint32_t cnt[4][kRsBins];
   __shared__ uint32_t lstart[kRsBins];
   __shared__ uint32_t gb[kRsBins];
-  __shared__ KT s_key[kRsTile];
-  __shared__ uint32_t s_pay[kRsTile];
+  __shared__ KT s_key[TILE];
+  __shared__ uint32_t s_pay[TILE];
   __shared__ unsigned s_t;
   const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
-  const int Tt = static_cast<int>((n + kRsTile - 1) / kRsTile);
+  const int Tt = static_cast<int>((n + TILE - 1) / TILE);
   // the plan: which digits vary (written by os_hist_kernel, complete at this launch's start)
   const KT varying = static_cast<KT>(~andor[0]) ^ andor[1];
   if (varying == KT(0)) {  // every key equal: the stable order is the input order (pass 0 writes it)
@@ -1231,13 +1232,13 @@ __global__ void __launch_bounds__(kRsThreads) os_pass_kernel(const T* __restrict
   if (threadIdx.x == 0) s_t = atomicAdd(&ctr[pass], 1u);
   __syncthreads();
   const int t = static_cast<int>(s_t);
-  const int64_t tb = (int64_t)t * kRsTile;
-  const int len = static_cast<int>(min<int64_t>(kRsTile, n - tb));
-  KT key[kRsItems];
-  uint32_t pay[kRsItems], rank[kRsItems];
+  const int64_t tb = (int64_t)t * TILE;
+  const int len = static_cast<int>(min<int64_t>(TILE, n - tb));
+  KT key[ITEMS];
+  uint32_t pay[ITEMS], rank[ITEMS];
 #pragma unroll
-  for (int k = 0; k < kRsItems; ++k) {
-    const int i = wave * (kRsTile / 4) + k * kWave + lane;
+  for (int k = 0; k < ITEMS; ++k) {
+    const int i = wave * (TILE / 4) + k * kWave + lane;
     if (i < len) {
       if (first) {
         const KT k0 = SortKey<T>::asc(x[tb + i]);
@@ -1255,7 +1256,7 @@ __global__ void __launch_bounds__(kRsThreads) os_pass_kernel(const T* __restrict
   for (int i = threadIdx.x; i < 4 * kRsBins; i += kRsThreads) (&cnt[0][0])[i] = 0u;
   __syncthreads();
   const int shift = 8 * pass;
-  rs_rank_tile<KT>(key, len, shift, cnt, lstart, rank);
+  rs_rank_tile<KT, ITEMS>(key, len, shift, cnt, lstart, rank);
   // this tile's count of digit d (thread d), published; the earlier tiles' total by look-back
   const int d = threadIdx.x;
   const uint32_t c = (d + 1 < kRsBins ? lstart[d + 1] : static_cast<uint32_t>(len)) - lstart[d];
@@ -1297,7 +1298,7 @@ __global__ void __launch_bounds__(kRsThreads) os_pass_kernel(const T* __restrict
   __syncthreads();
   gb[d] = base;
 #pragma unroll
-  for (int k = 0; k < kRsItems; ++k) {
+  for (int k = 0; k < ITEMS; ++k) {
     if (rank[k] == 0xFFFFFFFFu) continue;
     const uint32_t dk = static_cast<uint32_t>((key[k] >> shift) & 0xFF);
     const uint32_t lp = lstart[dk] + cnt[wave][dk] + rank[k];
@@ -1321,11 +1322,12 @@ __global__ void __launch_bounds__(kRsThreads) os_pass_kernel(const T* __restrict
   }
 }
 
-template <typename T>
-void radix_sort_onesweep(const at::Tensor& x, int64_t n, bool desc, at::Tensor& vals, at::Tensor& idx) {
+template <typename T, int ITEMS>
+void radix_sort_onesweep_t(const at::Tensor& x, int64_t n, bool desc, at::Tensor& vals, at::Tensor& idx) {
   using KT = typename SortKey<T>::type;
   constexpr int P = static_cast<int>(sizeof(KT));
-  const int Tt = static_cast<int>((n + kRsTile - 1) / kRsTile);
+  constexpr int TILE = kRsThreads * ITEMS;
+  const int Tt = static_cast<int>((n + TILE - 1) / TILE);
   auto opts = x.options();
   const auto kdt = sizeof(KT) == 4 ? at::kInt : at::kLong;
   auto keys = at::empty({2 * n}, opts.dtype(kdt));
@@ -1350,10 +1352,22 @@ void radix_sort_onesweep(const at::Tensor& x, int64_t n, bool desc, at::Tensor& 
   hipLaunchKernelGGL(os_hist_kernel<T>, hgrid, 256, 0, stream(), xp, n, desc, ghist, andor);
   TMX_LAUNCH_CHECK();
   for (int p = 0; p < P; ++p) {
-    hipLaunchKernelGGL(os_pass_kernel<T>, Tt, kRsThreads, 0, stream(), xp, kb0, kb0 + n, pb0, pb0 + n, vals.data_ptr<T>(),
+    hipLaunchKernelGGL((os_pass_kernel<T, ITEMS>), Tt, kRsThreads, 0, stream(), xp, kb0, kb0 + n, pb0, pb0 + n, vals.data_ptr<T>(),
                        idx.data_ptr<int64_t>(), n, desc, p, ghist, status, ctr, andor, err);
     TMX_LAUNCH_CHECK();
   }
+}
+
+// tile size by row length: 1024-key tiles (4 per thread) keep >= 64 workgroups per pass on short rows, where a pass
+// over 16 4096-key tiles is one workgroup's latency; 4096-key tiles amortise the look-back on long rows
+// (TMX_OS_ITEMS=4|8|16 forces one; tools/sort_bench.py)
+template <typename T>
+void radix_sort_onesweep(const at::Tensor& x, int64_t n, bool desc, at::Tensor& vals, at::Tensor& idx) {
+  static const int forced = std::getenv("TMX_OS_ITEMS") ? std::atoi(std::getenv("TMX_OS_ITEMS")) : 0;
+  const int items = forced ? forced : (n <= (int64_t(1) << 18) ? 4 : n <= (int64_t(1) << 20) ? 8 : 16);
+  if (items == 4) radix_sort_onesweep_t<T, 4>(x, n, desc, vals, idx);
+  else if (items == 8) radix_sort_onesweep_t<T, 8>(x, n, desc, vals, idx);
+  else radix_sort_onesweep_t<T, 16>(x, n, desc, vals, idx);
 }
 
 template <typename T>

@@ -225,6 +225,9 @@ typedef float f4_t __attribute__((ext_vector_type(4)));
 typedef uint32_t u4_t __attribute__((ext_vector_type(4)));
 typedef uint32_t u2_t __attribute__((ext_vector_type(2)));
 constexpr int kSsimMfmaWaves = 4;    // independent waves (column tiles) per workgroup
+#ifndef TMX_SSIM_DEPTH
+#define TMX_SSIM_DEPTH 1  // input bands in flight per wave: 1 (128 VGPRs, 4 waves / SIMD) measured 2.44-2.52 vs 2.69-2.75 ms for 2
+#endif
 constexpr float kSsimMfmaQBound = 128.f;  // (p^2 + t^2) / 256 in scaled units: |p|, |t| <= 2^7.5 for the fp16 operands
 
 // two fp32 values -> (hi pair, lo pair) of packed fp16: hi = v_cvt_pk_f16_f32 (RNE), lo = RNE16(x - hi) by
@@ -347,18 +350,28 @@ __global__ __launch_bounds__(kSsimMfmaWaves * kWave) void ssim_mfma_kernel(
   double acc_sim = 0.0, acc_cs = 0.0, acc_sse = 0.0;
   bool bad = false;
   const f2 c1v = {c1, c1}, c2v = {c2, c2};
-  // two bands in flight: a band's loads are issued two band computations before its use -- one was not enough to
-  // cover the HBM latency at three waves per SIMD
+#if TMX_SSIM_DEPTH == 2
+  // two bands in flight: a band's loads are issued two band computations before its use
   fetch(0);
   cp0 = np0; cp1 = np1; ct0 = nt0; ct1 = nt1;
   fetch(1);
+#else
+  // one band in flight (16 fewer VGPRs: 4 waves per SIMD instead of 3)
+  fetch(0);
+#endif
   auto band = [&](const int b, auto par_c) {
     constexpr int par = decltype(par_c)::value;  // b & 1
     // (p, t) pairs of the lane's 8 columns, packed as f2 {p, t}... -- the packed ops below take two columns at once
+#if TMX_SSIM_DEPTH == 2
     const f2 P[4] = {f2{cp0.x, cp0.y}, f2{cp0.z, cp0.w}, f2{cp1.x, cp1.y}, f2{cp1.z, cp1.w}};
     const f2 T[4] = {f2{ct0.x, ct0.y}, f2{ct0.z, ct0.w}, f2{ct1.x, ct1.y}, f2{ct1.z, ct1.w}};
     cp0 = np0; cp1 = np1; ct0 = nt0; ct1 = nt1;
     if (b + 2 < nb) fetch(b + 2);
+#else
+    const f2 P[4] = {f2{np0.x, np0.y}, f2{np0.z, np0.w}, f2{np1.x, np1.y}, f2{np1.z, np1.w}};
+    const f2 T[4] = {f2{nt0.x, nt0.y}, f2{nt0.z, nt0.w}, f2{nt1.x, nt1.y}, f2{nt1.z, nt1.w}};
+    if (b + 1 < nb) fetch(b + 1);
+#endif
     float f_sse = 0.f;
     if constexpr (SSE) {
       const int y = oy0 + 16 * b + i16;
