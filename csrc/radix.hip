@@ -1358,13 +1358,14 @@ void radix_sort_onesweep_t(const at::Tensor& x, int64_t n, bool desc, at::Tensor
   }
 }
 
-// tile size by row length: 1024-key tiles (4 per thread) keep >= 64 workgroups per pass on short rows, where a pass
-// over 16 4096-key tiles is one workgroup's latency; 4096-key tiles amortise the look-back on long rows
-// (TMX_OS_ITEMS=4|8|16 forces one; tools/sort_bench.py)
+// tile size by row length: 1024-key tiles (4 per thread) keep >= 8 workgroups per pass on short rows, where a pass
+// over a few 4096-key tiles is one workgroup's latency (fp32 8K keys: 0.043 vs 0.061 ms); 2048-key tiles from 256K,
+// 4096-key tiles above 1M keys amortise the look-back (profiles/sort_bench_r6.json items sweep; TMX_OS_ITEMS=4|8|16
+// forces one)
 template <typename T>
 void radix_sort_onesweep(const at::Tensor& x, int64_t n, bool desc, at::Tensor& vals, at::Tensor& idx) {
   static const int forced = std::getenv("TMX_OS_ITEMS") ? std::atoi(std::getenv("TMX_OS_ITEMS")) : 0;
-  const int items = forced ? forced : (n <= (int64_t(1) << 18) ? 4 : n <= (int64_t(1) << 20) ? 8 : 16);
+  const int items = forced ? forced : (n < (int64_t(1) << 18) ? 4 : n <= (int64_t(1) << 20) ? 8 : 16);
   if (items == 4) radix_sort_onesweep_t<T, 4>(x, n, desc, vals, idx);
   else if (items == 8) radix_sort_onesweep_t<T, 8>(x, n, desc, vals, idx);
   else radix_sort_onesweep_t<T, 16>(x, n, desc, vals, idx);

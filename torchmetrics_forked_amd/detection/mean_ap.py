@@ -211,10 +211,12 @@ class MeanAveragePrecision(Metric):
                 res_x = [torch.ops.tmx.cat_rows(col, 0) if col is not None else None for col in extra]
                 if any(r[1].numel() == 0 for r in res) or any(r is not None and r[1].numel() == 0 for r in res_x):
                     return False
-                dn, gn = res[2][1].tolist(), res[4][1].tolist()
-                if (dn != res[0][1].tolist() or dn != res[1][1].tolist() or gn != res[3][1].tolist()
-                        or any(r is not None and r[1].tolist() != gn for r in res_x)):
+                # row counts compared as host int64 tensors (torch.equal), listed once
+                eq = torch.equal
+                if (not eq(res[2][1], res[0][1]) or not eq(res[2][1], res[1][1]) or not eq(res[4][1], res[3][1])
+                        or any(r is not None and not eq(r[1], res[4][1]) for r in res_x)):
                     return False
+                dn, gn = res[2][1].tolist(), res[4][1].tolist()
                 flats = [r[0] for r in res]
                 crowd, area = (r[0] if r is not None else None for r in res_x)
             else:
@@ -234,15 +236,15 @@ class MeanAveragePrecision(Metric):
         except (KeyError, TypeError, RuntimeError, ValueError, IndexError, AttributeError):
             return False
         det_box, det_score, det_label, gt_box, gt_label = flats
-        n_det, n_gt = sum(dn), sum(gn)
+        n_det, n_gt = det_label.shape[0], gt_label.shape[0]
         if (det_box.shape != (n_det, 4) or gt_box.shape != (n_gt, 4) or det_score.shape != (n_det,) or det_label.shape != (n_det,)
                 or gt_label.shape != (n_gt,) or (crowd is not None and crowd.shape != (n_gt,)) or (area is not None and area.shape != (n_gt,))
                 or len({t.device for t in (*flats, *(c for c in (crowd, area) if c is not None))}) != 1):
             return False
-        if crowd is None:
-            crowd = torch.zeros_like(gt_label)
-        if area is None:
-            area = torch.zeros_like(gt_label)
+        if crowd is None or area is None:  # absent columns share one zero buffer (read-only state runs)
+            zero = torch.zeros_like(gt_label)
+            crowd = zero if crowd is None else crowd
+            area = zero if area is None else area
         if self.warn_on_many_detections and max(dn) > self.max_detection_thresholds[-1]:
             _warning_on_too_many_detections(self.max_detection_thresholds[-1])
         # lazy runs: the per-image items are views created at their first use (state_dict, list access), not here

@@ -191,9 +191,10 @@ class StateArena(list):
         into the buffer's free tail when it has room, else the split views themselves (zero-copy).  ``lazy``: while
         no item is materialised, only record the run (the items are created at their first use)."""
         if lazy and self._runs is not None and list.__len__(self) == 0 and self._buf is None:
-            self._pend.append((flat, list(sizes)))
-            self._npend += len(sizes)
-            self._runs.append((flat, list(sizes)))
+            sz = list(sizes)  # one private copy, shared by the pending record and the run (neither is mutated)
+            self._pend.append((flat, sz))
+            self._npend += len(sz)
+            self._runs.append((flat, sz))
             return
         self._materialize()
         if self._covered == len(self) and self._fits(flat):
