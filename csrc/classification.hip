@@ -2111,38 +2111,6 @@ __global__ void __launch_bounds__(kSumThreads) curve_summary_kernel(const double
   curve_summary_block(sc, C, summary);
 }
 
-at::Tensor curve_hist_reduce_impl(const at::Tensor& hist_, c10::optional<at::Tensor> code_range, bool clear) {
-  TORCH_CHECK(!clear || (hist_.is_contiguous() && code_range.has_value()), "curve_hist_reduce: clear needs a contiguous histogram and its range");
-  auto hist = hist_.contiguous();
-  TORCH_CHECK(hist.scalar_type() == at::kLong && hist.dim() == 3 && hist.size(1) == 2 && hist.size(2) == kCodes,
-              "curve_hist_reduce: hist must be int64 [C, 2, 16384]");
-  const int* cr = nullptr;
-  if (code_range.has_value()) {
-    TORCH_CHECK(code_range->scalar_type() == at::kInt && code_range->numel() == 2 * hist.size(0) && code_range->is_contiguous() &&
-                code_range->device() == hist.device(), "code_range must be int32[C, 2] on the histogram's device");
-    cr = code_range->data_ptr<int>();
-  }
-  const int C = static_cast<int>(hist.size(0));
-  auto out = at::empty({C, 4}, hist.options().dtype(at::kDouble));
-  if (C == 0) return out;
-  if (clear)
-    hipLaunchKernelGGL(curve_hist_reduce_kernel<true>, C, kRedThreads, 0, stream(), hist.data_ptr<int64_t>(), cr, out.data_ptr<double>());
-  else
-    hipLaunchKernelGGL(curve_hist_reduce_kernel<false>, C, kRedThreads, 0, stream(), hist.data_ptr<int64_t>(), cr, out.data_ptr<double>());
-  TMX_LAUNCH_CHECK();
-  return out;
-}
-
-at::Tensor curve_hist_reduce(const at::Tensor& hist, c10::optional<at::Tensor> code_range) {
-  return curve_hist_reduce_impl(hist, code_range, false);
-}
-
-at::Tensor curve_summary(const at::Tensor& scores_);
-
-// curve_hist_reduce + curve_summary: (scores [C, 4], summary float64[12]).  Two launches: folding the summary into
-// the reduce's last class block (device-wide completion counter) measured 33.7 us against 12.4 + 5.1 us -- every
-// block's agent-scope release fence has to write back its XCD's L2 (tests/test_compute_fused_gpu.py keeps the op's
-// contract; README round 4).
 // Wave-per-class form of the reduce (round 6): one 64-lane wave per class, four classes per 256-thread block, no LDS
 // and no block barriers in the scan -- the block form spends most of its ~13 us on the latency of its two barriers
 // per 4096-code chunk with ~70 of 256 threads holding codes (a class's occupied range is ~1-2k codes).  Lane l owns
@@ -2249,6 +2217,43 @@ __global__ void __launch_bounds__(kRedThreads) curve_hist_reduce_wave_kernel(con
   }
 }
 
+at::Tensor curve_hist_reduce_impl(const at::Tensor& hist_, c10::optional<at::Tensor> code_range, bool clear) {
+  TORCH_CHECK(!clear || (hist_.is_contiguous() && code_range.has_value()), "curve_hist_reduce: clear needs a contiguous histogram and its range");
+  auto hist = hist_.contiguous();
+  TORCH_CHECK(hist.scalar_type() == at::kLong && hist.dim() == 3 && hist.size(1) == 2 && hist.size(2) == kCodes,
+              "curve_hist_reduce: hist must be int64 [C, 2, 16384]");
+  const int* cr = nullptr;
+  if (code_range.has_value()) {
+    TORCH_CHECK(code_range->scalar_type() == at::kInt && code_range->numel() == 2 * hist.size(0) && code_range->is_contiguous() &&
+                code_range->device() == hist.device(), "code_range must be int32[C, 2] on the histogram's device");
+    cr = code_range->data_ptr<int>();
+  }
+  const int C = static_cast<int>(hist.size(0));
+  auto out = at::empty({C, 4}, hist.options().dtype(at::kDouble));
+  if (C == 0) return out;
+  static const char* form = std::getenv("TMX_REDUCE_FORM");
+  if (!clear && (form == nullptr || std::string(form) == "wave")) {  // the same form as curve_hist_scores (bitwise)
+    hipLaunchKernelGGL(curve_hist_reduce_wave_kernel<false>, static_cast<unsigned>((C + kRedWaveClasses - 1) / kRedWaveClasses), kRedThreads, 0,
+                       stream(), hist.data_ptr<int64_t>(), cr, out.data_ptr<double>(), C, nullptr, nullptr);
+  } else if (clear) {
+    hipLaunchKernelGGL(curve_hist_reduce_kernel<true>, C, kRedThreads, 0, stream(), hist.data_ptr<int64_t>(), cr, out.data_ptr<double>());
+  } else {
+    hipLaunchKernelGGL(curve_hist_reduce_kernel<false>, C, kRedThreads, 0, stream(), hist.data_ptr<int64_t>(), cr, out.data_ptr<double>());
+  }
+  TMX_LAUNCH_CHECK();
+  return out;
+}
+
+at::Tensor curve_hist_reduce(const at::Tensor& hist, c10::optional<at::Tensor> code_range) {
+  return curve_hist_reduce_impl(hist, code_range, false);
+}
+
+at::Tensor curve_summary(const at::Tensor& scores_);
+
+// curve_hist_reduce + curve_summary: (scores [C, 4], summary float64[12]).  Two launches: folding the summary into
+// the reduce's last class block (device-wide completion counter) measured 33.7 us against 12.4 + 5.1 us -- every
+// block's agent-scope release fence has to write back its XCD's L2 (tests/test_compute_fused_gpu.py keeps the op's
+// contract; README round 4).
 // a zero-initialised int per (device, stream) for the reduce's last-block count (each launch leaves it at zero again;
 // launches on one stream are ordered, so they never share it concurrently)
 static int* reduce_done_counter(const at::Device& dev) {

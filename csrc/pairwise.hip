@@ -519,45 +519,49 @@ __global__ __launch_bounds__(256) void x3_split_kernel(const float* __restrict__
   }
 }
 
-template <int MODE>
-__global__ __launch_bounds__(kPhThreads, 2) void pairwise_gemm_x3_kernel(const __half* __restrict__ x, const __half* __restrict__ y, int64_t N,
-                                                                         int64_t M, int64_t Dp, int tiles_n, bool zero_diag,
-                                                                         float* __restrict__ out, const int* __restrict__ xs_shift,
-                                                                         const int* __restrict__ ys_shift, const float* __restrict__ xs_f,
-                                                                         const float* __restrict__ ys_f) {
-  __shared__ __attribute__((aligned(16))) short lds[2][2][kPhT * kPhLd];  // [buffer][x | y][row * kPhLd + (hi 32 | lo 32)]
-  __shared__ float fac[2][kPhT];
-  __shared__ int sh[2][kPhT];
-  const int64_t nwg = gridDim.x, orig = blockIdx.x, xcd = orig % 8, q = nwg / 8, rr = nwg % 8;
-  const int64_t id = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
-  const int64_t row0 = (id / tiles_n) * kPhT, col0 = (id % tiles_n) * kPhT;
+// The x3 tile core shared by the pairwise forms, MiFID's row max and KID's polynomial sums: a 128 x 128 block of
+// packed-plane dot products on 4 waves (64 x 64 each, 4 x 4 MFMA tiles).  ``xrow(r)`` / ``yrow(r)`` give the packed row
+// of tile row r (nullptr: a zero row -- KID's gathered subsets end mid-tile); slices of 32 k (64 halves) are double-
+// buffered through LDS with the next slice in registers.
+typedef __half X3Lds[2][2][kPhT * kPhLd];
+template <bool ZERO_ROWS, typename RowA, typename RowB>
+__device__ __forceinline__ void x3_tile_core(RowA xrow, RowB yrow, int nk, X3Lds& lds, ph_acc4 (&acc)[4][4]) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 1, wc = wave & 1;
-  const int64_t ld = 2 * Dp;  // halves per packed row; rows are padded to the tile (zeros), so no bounds checks
+  const __half* xr[4];
+  const __half* yr[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    xr[i] = xrow((tid >> 3) + 32 * i);
+    yr[i] = yrow((tid >> 3) + 32 * i);
+  }
   ph_frag8 rx[4], ry[4];
   auto load = [&](int64_t s) {  // slice s: 64 halves = 128 B per row, 8 lanes per row
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int r = (tid >> 3) + 32 * i;
       const int64_t off = s * 64 + 8 * (tid & 7);
-      rx[i] = *reinterpret_cast<const ph_frag8*>(x + (row0 + r) * ld + off);
-      ry[i] = *reinterpret_cast<const ph_frag8*>(y + (col0 + r) * ld + off);
+      if constexpr (ZERO_ROWS) {
+        const ph_frag8 z = {0, 0, 0, 0, 0, 0, 0, 0};
+        rx[i] = xr[i] != nullptr ? *reinterpret_cast<const ph_frag8*>(xr[i] + off) : z;
+        ry[i] = yr[i] != nullptr ? *reinterpret_cast<const ph_frag8*>(yr[i] + off) : z;
+      } else {
+        rx[i] = *reinterpret_cast<const ph_frag8*>(xr[i] + off);
+        ry[i] = *reinterpret_cast<const ph_frag8*>(yr[i] + off);
+      }
     }
   };
   auto store = [&](int buf) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int r = (tid >> 3) + 32 * i, kk = 8 * (tid & 7);
-      *reinterpret_cast<ph_frag8*>(&lds[buf][0][r * kPhLd + kk]) = rx[i];
-      *reinterpret_cast<ph_frag8*>(&lds[buf][1][r * kPhLd + kk]) = ry[i];
+      *reinterpret_cast<ph_frag8*>(reinterpret_cast<short*>(lds[buf][0]) + r * kPhLd + kk) = rx[i];
+      *reinterpret_cast<ph_frag8*>(reinterpret_cast<short*>(lds[buf][1]) + r * kPhLd + kk) = ry[i];
     }
   };
-  ph_acc4 acc[4][4];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = ph_acc4{0.f, 0.f, 0.f, 0.f};
-  const int nk = static_cast<int>(Dp / kX3K);
   load(0);
   store(0);
   __syncthreads();
@@ -565,8 +569,8 @@ __global__ __launch_bounds__(kPhThreads, 2) void pairwise_gemm_x3_kernel(const _
   for (int s = 0; s < nk; ++s) {
     const int buf = s & 1;
     if (s + 1 < nk) load(s + 1);
-    const short* A = lds[buf][0];
-    const short* B = lds[buf][1];
+    const short* A = reinterpret_cast<const short*>(lds[buf][0]);
+    const short* B = reinterpret_cast<const short*>(lds[buf][1]);
     ph_frag8 ah[4], al[4], bh[4], bl[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -591,6 +595,27 @@ __global__ __launch_bounds__(kPhThreads, 2) void pairwise_gemm_x3_kernel(const _
     if (s + 1 < nk) store(buf ^ 1);
     __syncthreads();
   }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kPhThreads, 2) void pairwise_gemm_x3_kernel(const __half* __restrict__ x, const __half* __restrict__ y, int64_t N,
+                                                                         int64_t M, int64_t Dp, int tiles_n, bool zero_diag,
+                                                                         float* __restrict__ out, const int* __restrict__ xs_shift,
+                                                                         const int* __restrict__ ys_shift, const float* __restrict__ xs_f,
+                                                                         const float* __restrict__ ys_f) {
+  __shared__ __attribute__((aligned(16))) X3Lds lds;  // [buffer][x | y][row * kPhLd + (hi 32 | lo 32)]
+  __shared__ float fac[2][kPhT];
+  __shared__ int sh[2][kPhT];
+  const int64_t nwg = gridDim.x, orig = blockIdx.x, xcd = orig % 8, q = nwg / 8, rr = nwg % 8;
+  const int64_t id = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
+  const int64_t row0 = (id / tiles_n) * kPhT, col0 = (id % tiles_n) * kPhT;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 1, wc = wave & 1;
+  const int fr = lane & 15;
+  const int64_t ld = 2 * Dp;  // halves per packed row; rows are padded to the tile (zeros), so no bounds checks
+  ph_acc4 acc[4][4];
+  x3_tile_core<false>([&](int r) { return x + (row0 + r) * ld; }, [&](int r) { return y + (col0 + r) * ld; },
+                      static_cast<int>(Dp / kX3K), lds, acc);
   {
     const int64_t g = tid < kPhT ? row0 + tid : col0 + (tid - kPhT);
     fac[tid >> 7][tid & 127] = tid < kPhT ? xs_f[g] : ys_f[g];
@@ -792,6 +817,68 @@ __global__ __launch_bounds__(kPgThreads) void kid_poly_kernel(const T* __restric
   }
 }
 
+// KID on the x3 core (fp32 features, round 6): the real and fake features are split once (x3_split_kernel), every
+// (subset, product, 128 x 128 tile) block gathers its rows through the subset indices into the shared tile core, and
+// the epilogue raises ldexp(acc, -(s_i + s_j)) * gamma + coef to the degree and folds one fp64 atomic per block.
+__global__ __launch_bounds__(kPhThreads, 2) void kid_poly_x3_kernel(const __half* __restrict__ pr, const __half* __restrict__ pf,
+                                                                    const int* __restrict__ sh_r, const int* __restrict__ sh_f,
+                                                                    const int64_t* __restrict__ idx_r, const int64_t* __restrict__ idx_f,
+                                                                    int64_t m, int64_t Dp, int tiles, int degree, double gamma, double coef,
+                                                                    double* __restrict__ sums) {
+  __shared__ __attribute__((aligned(16))) X3Lds lds;
+  __shared__ int sh[2][kPhT];
+  __shared__ double red[kPhThreads / kWave];
+  const int64_t per = static_cast<int64_t>(tiles) * tiles;
+  const int64_t sub = blockIdx.x / (3 * per);
+  const int prob = static_cast<int>((blockIdx.x / per) % 3);  // 0: real x real, 1: fake x fake, 2: real x fake
+  const int64_t t = blockIdx.x % per;
+  const int64_t row0 = (t / tiles) * kPhT, col0 = (t % tiles) * kPhT;
+  const __half* A = prob == 1 ? pf : pr;
+  const __half* B = prob == 0 ? pr : pf;
+  const int* sa = prob == 1 ? sh_f : sh_r;
+  const int* sb = prob == 0 ? sh_r : sh_f;
+  const int64_t* ia = (prob == 1 ? idx_f : idx_r) + sub * m;
+  const int64_t* ib = (prob == 0 ? idx_r : idx_f) + sub * m;
+  const int64_t ld = 2 * Dp;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 1, wc = wave & 1, fr = lane & 15;
+  ph_acc4 acc[4][4];
+  x3_tile_core<true>([&](int r) -> const __half* { return row0 + r < m ? A + ia[row0 + r] * ld : nullptr; },
+                     [&](int r) -> const __half* { return col0 + r < m ? B + ib[col0 + r] * ld : nullptr; },
+                     static_cast<int>(Dp / kX3K), lds, acc);
+  {
+    const int64_t g = tid < kPhT ? row0 + tid : col0 + (tid - kPhT);
+    sh[tid >> 7][tid & 127] = g < m ? (tid < kPhT ? sa[ia[g]] : sb[ib[g]]) : 0;
+    __syncthreads();
+  }
+  const float gf = static_cast<float>(gamma), cf = static_cast<float>(coef);
+  double part = 0.0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int lr = wr * 64 + 16 * i + (lane >> 4) * 4 + r, lc = wc * 64 + 16 * j + fr;
+        const int64_t gi = row0 + lr, gj = col0 + lc;
+        if (gi >= m || gj >= m || (prob < 2 && gi == gj)) continue;
+        const float base = ldexpf(acc[i][j][r], -(sh[0][lr] + sh[1][lc])) * gf + cf;  // (f @ gᵀ * gamma + coef)
+        float p = base;
+        for (int e = 1; e < degree; ++e) p = p * base;
+        part += static_cast<double>(p);
+      }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) part += __shfl_xor(part, off, kWave);
+  if (lane == 0) red[wave] = part;
+  __syncthreads();
+  if (tid == 0) {
+    double tot = 0.0;
+#pragma unroll
+    for (int w = 0; w < kPhThreads / kWave; ++w) tot += red[w];
+    atomicAdd(sums + 3 * sub + prob, tot);
+  }
+}
+
 // [S, 3] fp64 per subset s: Σ_{i != j} k(r_i, r_j), Σ_{i != j} k(f_i, f_j), Σ k(r_i, f_j) over real[idx_r[s]],
 // fake[idx_f[s]] (idx [S, m], or [m] for one subset -> [3]); every subset in one launch
 at::Tensor kid_poly_sums(const at::Tensor& real_in, const at::Tensor& fake_in, const at::Tensor& idx_r_in, const at::Tensor& idx_f_in,
@@ -817,6 +904,29 @@ at::Tensor kid_poly_sums(const at::Tensor& real_in, const at::Tensor& fake_in, c
   const int64_t S = batched ? idx_r_in.size(0) : 1, m = batched ? idx_r_in.size(1) : idx_r_in.numel(), D = real.size(1);
   auto sums = at::zeros(batched ? at::IntArrayRef{S, 3} : at::IntArrayRef{3}, real.options().dtype(at::kDouble));
   if (m == 0 || D == 0 || S == 0) return sums;
+  if (real.scalar_type() == at::kFloat && D >= 256 && !std::getenv("TMX_PAIRWISE_X3_OFF")) {
+    // fp32 Inception-depth features: the x3 route (both feature sets split once, 128 x 128 tiles)
+    const int64_t Nr = real.size(0), Nf = fake.size(0), Dp = (D + kX3K - 1) / kX3K * kX3K;
+    const int64_t Nrp = (Nr + 3) / 4 * 4, Nfp = (Nf + 3) / 4 * 4;
+    auto pr = at::empty({Nrp, 2 * Dp}, real.options().dtype(at::kHalf));
+    auto pf = at::empty({Nfp, 2 * Dp}, real.options().dtype(at::kHalf));
+    auto shift = at::empty({Nrp + Nfp}, real.options().dtype(at::kInt));
+    auto finv = at::empty({Nrp + Nfp}, real.options());
+    auto flag = at::zeros({1}, real.options().dtype(at::kInt));
+    hipLaunchKernelGGL(x3_split_kernel, dim3(static_cast<unsigned>((Nrp + Nfp) / 4)), 256, 0, stream(), real.data_ptr<float>(),
+                       fake.data_ptr<float>(), Nr, Nrp, Nf, D, Dp, reinterpret_cast<__half*>(pr.data_ptr()),
+                       reinterpret_cast<__half*>(pf.data_ptr()), shift.data_ptr<int>(), finv.data_ptr<float>(), flag.data_ptr<int>());
+    TMX_LAUNCH_CHECK();
+    const int tiles = static_cast<int>((m + kPhT - 1) / kPhT);
+    const int64_t nwg = 3 * S * static_cast<int64_t>(tiles) * tiles;
+    TORCH_CHECK(nwg < (int64_t(1) << 31), "kid_poly_sums: subset too large");
+    hipLaunchKernelGGL(kid_poly_x3_kernel, dim3(static_cast<unsigned>(nwg)), kPhThreads, 0, stream(),
+                       reinterpret_cast<const __half*>(pr.data_ptr()), reinterpret_cast<const __half*>(pf.data_ptr()), shift.data_ptr<int>(),
+                       shift.data_ptr<int>() + Nrp, idx_r.data_ptr<int64_t>(), idx_f.data_ptr<int64_t>(), m, Dp, tiles, static_cast<int>(degree),
+                       gamma, coef, sums.data_ptr<double>());
+    TMX_LAUNCH_CHECK();
+    return sums;
+  }
   const int tiles = static_cast<int>((m + kPgT - 1) / kPgT);
   const int64_t nwg = 3 * S * static_cast<int64_t>(tiles) * tiles;
   TORCH_CHECK(nwg < (int64_t(1) << 31), "kid_poly_sums: subset too large");

@@ -204,6 +204,26 @@ def test_kid_poly_sums_vs_torch(dtype, n, m, d, degree):
         torch.ops.tmx.kid_poly_sums(real, fake, torch.tensor([0, n]), torch.tensor([0, 1]), degree, gamma, coef)
 
 
+@pytest.mark.parametrize(("m", "d", "degree"), [(1000, 2048, 3), (300, 257, 2)])
+def test_kid_poly_sums_fp32_split_route(m, d, degree):
+    """fp32 features of Inception depth take the f16-split matrix-core route (csrc/pairwise.hip kid_poly_x3_kernel:
+    features split once, subset rows gathered into the shared x3 tile core); the three sums against fp64."""
+    g = torch.Generator().manual_seed(m + d)
+    real = torch.rand(m + 50, d, generator=g).cuda()
+    fake = (torch.rand(m + 20, d, generator=g) * 1.1).cuda()
+    ir, jf = torch.randperm(m + 50, generator=g)[:m], torch.randperm(m + 20, generator=g)[:m]
+    gamma, coef = 1.0 / d, 1.0
+    sums = torch.ops.tmx.kid_poly_sums(real, fake, ir, jf, degree, gamma, coef)
+    a, b = real.double()[ir.cuda()], fake.double()[jf.cuda()]
+    k = lambda x, y: (x @ y.T * gamma + coef) ** degree  # noqa: E731
+    kxx, kyy, kxy = k(a, a), k(b, b), k(a, b)
+    ref = torch.stack([kxx.sum() - kxx.diag().sum(), kyy.sum() - kyy.diag().sum(), kxy.sum()])
+    torch.testing.assert_close(sums, ref, rtol=2e-6, atol=0)
+    # the MMD the metric forms from them (reference kid.py maximum_mean_discrepancy) to ~1e-6 of its scale
+    mmd = lambda s: s[0] / (m * (m - 1)) + s[1] / (m * (m - 1)) - 2 * s[2] / (m * m)  # noqa: E731
+    assert abs(float(mmd(sums)) - float(mmd(ref))) < 1e-5 * float(ref[2] / (m * m))
+
+
 def test_kid_metric_fused_matches_cpu():
     """KernelInceptionDistance compute on the GPU (fused subset sums) vs the CPU reference path, same randperm draws."""
     from torchmetrics_forked_amd.image import KernelInceptionDistance

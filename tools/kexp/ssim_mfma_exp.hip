@@ -60,13 +60,14 @@ struct Result { std::vector<double> sim, cs, sse; int flag; float ms; };
 template <int KS>
 Result run(bool mfma, const float* p, const float* t, int P, int H, int W, const float* dw, const float* dc, bool timed) {
   Result r;
+  static const int strip = getenv("TMX_SSIM_STRIP") ? atoi(getenv("TMX_SSIM_STRIP")) : 256;
   const int Hv = H - KS + 1, Wv = W - KS + 1;
   int* flag; CK(hipMalloc(&flag, 4)); CK(hipMemset(flag, 0, 4));
   double *ds, *dcs, *de;
   int64_t nparts;
   dim3 grid;
   if (mfma) {
-    const int strip = 256, ntx = (Wv + 15) / 16;
+    const int ntx = (Wv + 15) / 16;
     grid = dim3((ntx + kSsimMfmaWaves - 1) / kSsimMfmaWaves, (Hv + strip - 1) / strip, P);
     nparts = (int64_t)grid.y * ntx;
   } else {
@@ -76,7 +77,7 @@ Result run(bool mfma, const float* p, const float* t, int P, int H, int W, const
   CK(hipMalloc(&ds, P * nparts * 8)); CK(hipMalloc(&dcs, P * nparts * 8)); CK(hipMalloc(&de, P * nparts * 8));
   auto launch = [&] {
     if (mfma)
-      hipLaunchKernelGGL((ssim_mfma_kernel<true>), grid, kSsimMfmaWaves * kWave, 0, 0, p, t, H, W, KS, 256, dw, dc, ds, dcs, de, flag);
+      hipLaunchKernelGGL((ssim_mfma_kernel<true>), grid, kSsimMfmaWaves * kWave, 0, 0, p, t, H, W, KS, strip, dw, dc, ds, dcs, de, flag);
     else
       hipLaunchKernelGGL((ssim_v2_kernel<KS, true>), grid, kSsimThreads, 0, 0, p, t, H, W, dw, dw, dc, ds, dcs, de, nullptr);
   };

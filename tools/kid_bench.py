@@ -1,5 +1,5 @@
-"""KernelInceptionDistance compute on one GPU: fused per-subset sums (kid_poly_sums) vs the reference's poly_mmd
-composition, 2000 real / 2000 fake Inception-2048 features (synthetic), 100 subsets of 1000.  One JSON line (ms)."""
+"""KernelInceptionDistance compute on one GPU: fused per-subset sums (kid_poly_sums: the f16-split matrix-core route for fp32,
+and with it switched off the round-5 fp32 MFMA kernel) vs the reference's poly_mmd composition, 2000 real / 2000 fake Inception-2048 features (synthetic), 100 subsets of 1000.  One JSON line (ms)."""
 import json
 import os
 import sys
@@ -33,8 +33,15 @@ def main() -> None:
             out.append(G.poly_mmd(a, b, 3, None, 1.0))
         return torch.stack(out).mean()
 
+    def fused_exact():  # the fp32-MFMA kernel (round 5), the x3 route switched off
+        os.environ["TMX_PAIRWISE_X3_OFF"] = "1"
+        try:
+            return fused()
+        finally:
+            del os.environ["TMX_PAIRWISE_X3_OFF"]
+
     res = {}
-    for name, fn in (("fused", fused), ("composed", composed)):
+    for name, fn in (("fused", fused), ("fused_fp32_mfma", fused_exact), ("composed", composed)):
         fn()
         torch.cuda.synchronize()
         ts = []
