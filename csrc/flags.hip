@@ -214,9 +214,32 @@ at::Tensor gather_flags(at::TensorList flags, c10::IntArrayRef zero) {
   return host;
 }
 
+// gather_flags without the synchronisation: the caller records an event after it and reads the pinned result once the
+// event has completed (forward()'s parked warning flags: no pipeline drain every few dozen forwards)
+at::Tensor gather_flags_async(at::TensorList flags, c10::IntArrayRef zero) {
+  int64_t total = 0;
+  for (const at::Tensor& f : flags) total += f.numel();
+  auto host = at::empty({total}, at::TensorOptions().dtype(at::kInt).pinned_memory(true));
+  if (total == 0) return host;
+  TORCH_CHECK(flags.size() == zero.size(), "gather_flags_async: one zero entry per flag");
+  TORCH_CHECK(flags[0].is_cuda(), "gather_flags_async: device tensors only");
+  const c10::DeviceGuard guard(flags[0].device());
+  void* dptr = nullptr;
+  if (hipHostGetDevicePointer(&dptr, host.data_ptr(), 0) == hipSuccess && dptr != nullptr) {
+    launch_gather(flags, zero, total, static_cast<int32_t*>(dptr));
+  } else {
+    (void)hipGetLastError();
+    const at::Tensor out = gather_flags_device(flags, zero);
+    TMX_CHECK_HIP(hipMemcpyAsync(host.data_ptr<int32_t>(), out.data_ptr<int32_t>(), total * sizeof(int32_t), hipMemcpyDeviceToHost,
+                                 stream()));
+  }
+  return host;
+}
+
 }  // namespace tmx
 
 TORCH_LIBRARY_FRAGMENT(tmx, m) {
+  m.def("gather_flags_async(Tensor[] flags, int[] zero) -> Tensor");
   m.def("gather_flags(Tensor[] flags, int[] zero) -> Tensor");
   m.def("gather_flags_device(Tensor[] flags, int[] zero) -> Tensor");
   m.def("or_flags(Tensor(a!)[] flags, Tensor src) -> ()");
@@ -224,6 +247,7 @@ TORCH_LIBRARY_FRAGMENT(tmx, m) {
 
 TORCH_LIBRARY_IMPL(tmx, CUDA, m) {
   m.impl("gather_flags", &tmx::gather_flags);
+  m.impl("gather_flags_async", &tmx::gather_flags_async);
   m.impl("gather_flags_device", &tmx::gather_flags_device);
   m.impl("or_flags", &tmx::or_flags);
 }

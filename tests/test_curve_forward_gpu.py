@@ -121,3 +121,31 @@ def test_gpu_forward_does_not_synchronise_and_defers_checks():
         m2(x, few)
     with pytest.warns(UserWarning):
         m2.compute()
+
+
+def test_parked_forward_warnings_flush_without_synchronising():
+    """Past the parked limit, forward's warning flags are gathered into pinned memory behind an event (no stream
+    synchronisation inside forward); every batch's warning is still delivered, at the latest by compute()."""
+    import warnings
+
+    from torchmetrics_forked_amd.utilities import validation
+
+    C = 16
+    m = tm.classification.MulticlassAUROC(num_classes=C).cuda()
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(256, C, generator=g).bfloat16().cuda()
+    t = torch.randint(0, C, (256,), generator=g).cuda()
+    m.update(x, t)
+    few = torch.zeros_like(t)  # classes 1.. have no positives in these batches: one warning check per forward
+    n_fwd = 3 * validation._MAX_PENDING
+    with warnings.catch_warnings(record=True) as rec:
+        warnings.simplefilter("always")
+        torch.cuda.set_sync_debug_mode("error")
+        try:
+            for _ in range(n_fwd):
+                m(x, few)
+        finally:
+            torch.cuda.set_sync_debug_mode("default")
+        m.compute()
+    assert not validation._inflight()
+    assert sum(issubclass(w.category, UserWarning) for w in rec) >= n_fwd  # one degenerate-class warning per batch

@@ -74,6 +74,8 @@ for s in "$@"; do
     pwx3) PW_SHAPES=${PW_SHAPES:-4096:4096:512,2048:2048:2048,8192:8192:256,10000:10000:2048,16384:2048:1024} PW_DTYPES=float32 PW_MODES=linear,cosine run pwx3 300 python tools/pairwise_bench.py; tail -1 "$OUT/pwx3.log" ;;
     sortitems) for it in 4 8 16; do TMX_OS_ITEMS=$it SORT_BENCH_SWEEP=1 run sortsweep_items$it 300 python tools/sort_bench.py; tail -c 600 "$OUT/sortsweep_items$it.log"; echo; done ;;
     ssimstrip) for st in 256 512 1024; do TMX_SSIM_STRIP=$st run ssim_strip$st 120 ./build/kexp_r6/ssim_mfma_exp; echo "strip $st: $(grep -o '"config4_KS11[^}]*}' $OUT/ssim_strip$st.log | grep -o '"mfma_ms[^,]*')"; done ;;
+    ssimbench) run ssimbench 300 python tools/ssim_bench.py; tail -1 "$OUT/ssimbench.log" ;;
+    ssimprof) run ssimprof 300 rocprofv3 --kernel-trace --stats -d "$OUT/ssimprof" -o ssim --output-format csv -- python3 tools/ssim_bench.py ;;
     reduce) run reduce 200 python tools/reduce_bench.py; tail -1 "$OUT/reduce.log" ;;
     *) echo "unknown step $s" ;;
   esac

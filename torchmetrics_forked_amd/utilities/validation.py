@@ -104,11 +104,15 @@ class HostCheckBatch:
             # (e.g. "no positive samples") surface late, at most _MAX_PENDING forwards after their batch.
             pend = _pending()
             pend.extend(items)
+            _drain_inflight(block=False)
             if len(pend) <= _MAX_PENDING:
                 return
             items = list(pend)
             pend.clear()
+            if _read_async(items):  # gathered into pinned memory behind an event: read at a later resolve
+                return
         else:
+            _drain_inflight(block=True)
             pend = _pending()
             if pend and (items or not in_forward):  # warnings parked by earlier forwards ride on this block's read
                 items = list(pend) + items
@@ -148,7 +152,47 @@ def _native() -> bool:
 
 
 _HOST = threading.local()
-_MAX_PENDING = 32  # parked forward warning checks before one synchronous read flushes them
+_MAX_PENDING = 32  # parked forward warning checks before one read flushes them (asynchronously on the GPU)
+
+
+def _inflight() -> List[Tuple[List[Tuple[List[Tensor], Callable[[List[int]], None], bool, bool]], Tensor, Any]]:
+    q = getattr(_HOST, "inflight", None)
+    if q is None:
+        q = _HOST.inflight = []
+    return q
+
+
+def _read_async(items: List[Tuple[List[Tensor], Callable[[List[int]], None], bool, bool]]) -> bool:
+    """Start one gather of the parked forward flags into pinned host memory without waiting for the device (an
+    event marks its completion); False when the flags are not all on one GPU with the native library loaded."""
+    flat = [(t, consume) for ts, _, _, consume in items for t in ts]
+    devs = {t.device for t, _ in flat}
+    if not (len(devs) == 1 and next(iter(devs)).type == "cuda" and _native()):
+        return False
+    host = torch.ops.tmx.gather_flags_async([t for t, _ in flat], [int(c) for _, c in flat])
+    ev = torch.cuda.Event()
+    ev.record()
+    _inflight().append((items, host, ev))
+    return True
+
+
+def _drain_inflight(block: bool) -> None:
+    """Run the callbacks of completed asynchronous flag reads (all of them when ``block``), in issue order."""
+    q = _inflight()
+    while q:
+        items, host, ev = q[0]
+        if not block:
+            if not ev.query():
+                return
+        else:
+            ev.synchronize()
+        q.pop(0)
+        vals = host.tolist()
+        off = 0
+        for ts, cb, _, _ in items:
+            n = sum(t.numel() for t in ts)
+            cb(vals[off : off + n])
+            off += n
 
 
 def _pending() -> List[Tuple[List[Tensor], Callable[[List[int]], None], bool, bool]]:
