@@ -197,8 +197,9 @@ at::Tensor ssim_sums(const at::Tensor& preds_in, const at::Tensor& target_in, co
   // (consts = c1, c2, D), with ssim_v2_kernel as its device-side fallback for out-of-range data
   static const bool mfma_off = std::getenv("TMX_SSIM_V2") != nullptr;  // A/B knob (tools/ssim_bench.py)
   if (v2 && !mfma_off && consts.numel() >= 3 && KS <= 17) {
-    // output rows per workgroup strip (a multiple of 16; each strip re-reads a KS - 1 halo band)
-    static const int kStrip = std::getenv("TMX_SSIM_STRIP") ? std::max(16, std::atoi(std::getenv("TMX_SSIM_STRIP")) / 16 * 16) : 256;
+    // output rows per workgroup strip (a multiple of 16; each strip re-reads a KS - 1 halo band); 1024 measured fastest
+    // of 256 / 512 / 1024 on the 1080p bench config (2.48 / 2.35 / 2.32 ms, tools/kexp/ssim_mfma_exp.hip)
+    static const int kStrip = std::getenv("TMX_SSIM_STRIP") ? std::max(16, std::atoi(std::getenv("TMX_SSIM_STRIP")) / 16 * 16) : 1024;
     const int ntx = static_cast<int>((Wv + 15) / 16);
     dim3 mgrid(static_cast<unsigned>((ntx + kSsimMfmaWaves - 1) / kSsimMfmaWaves), static_cast<unsigned>((Hv + kStrip - 1) / kStrip),
                static_cast<unsigned>(P));

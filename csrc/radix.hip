@@ -1159,7 +1159,8 @@ constexpr uint32_t kOsAgg = 1u << 30, kOsInc = 2u << 30, kOsVal = (1u << 30) - 1
 
 template <typename T>
 __global__ void __launch_bounds__(256) os_hist_kernel(const T* __restrict__ x, int64_t n, bool desc, uint32_t* __restrict__ ghist,
-                                                      typename SortKey<T>::type* __restrict__ andor) {
+                                                      typename SortKey<T>::type* __restrict__ andor, unsigned* __restrict__ done,
+                                                      uint32_t* __restrict__ gpre) {
   using KT = typename SortKey<T>::type;
   constexpr int P = static_cast<int>(sizeof(KT));
   __shared__ uint32_t h[P * kRsBins];
@@ -1186,13 +1187,36 @@ __global__ void __launch_bounds__(256) os_hist_kernel(const T* __restrict__ x, i
     atomicOr(&andor[0], na);
     atomicOr(&andor[1], o);
   }
+  // the last block turns the digit totals into exclusive prefixes per pass (gpre), once -- every tile of every pass
+  // read its pass's 256 totals and scanned them itself before (8 barrier rounds per tile and pass)
+  __shared__ bool s_last;
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) s_last = atomicAdd(done, 1u) == gridDim.x - 1;
+  __syncthreads();
+  if (!s_last) return;
+  __threadfence();
+  __shared__ uint32_t sc[kRsBins];
+  for (int p = 0; p < P; ++p) {
+    const uint32_t v = __hip_atomic_load(&ghist[p * kRsBins + threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    sc[threadIdx.x] = v;
+    __syncthreads();
+    for (int off = 1; off < kRsBins; off <<= 1) {
+      const uint32_t t = threadIdx.x >= off ? sc[threadIdx.x - off] : 0u;
+      __syncthreads();
+      sc[threadIdx.x] += t;
+      __syncthreads();
+    }
+    gpre[p * kRsBins + threadIdx.x] = sc[threadIdx.x] - v;  // exclusive
+    __syncthreads();
+  }
 }
 
 template <typename T, int ITEMS = kRsItems>
 __global__ void __launch_bounds__(kRsThreads) os_pass_kernel(const T* __restrict__ x, typename SortKey<T>::type* __restrict__ kb0,
                                                                typename SortKey<T>::type* __restrict__ kb1, uint32_t* __restrict__ pb0,
                                                                uint32_t* __restrict__ pb1, T* __restrict__ vals, int64_t* __restrict__ idx,
-                                                               int64_t n, bool desc, int pass, const uint32_t* __restrict__ ghist,
+                                                               int64_t n, bool desc, int pass, const uint32_t* __restrict__ gpre,
                                                                uint32_t* __restrict__ status, unsigned* __restrict__ ctr,
                                                                const typename SortKey<T>::type* __restrict__ andor, int* __restrict__ err) {
   using KT = typename SortKey<T>::type;
@@ -1285,18 +1309,9 @@ __global__ void __launch_bounds__(kRsThreads) os_pass_kernel(const T* __restrict
     }
     __hip_atomic_store(&st[(int64_t)t * kRsBins + d], kOsInc | (excl + c), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  // global position of digit d's first key of this tile: keys of smaller digits (all tiles) + this digit in earlier tiles
-  gb[d] = ghist[pass * kRsBins + d];
-  __syncthreads();
-  for (int off = 1; off < kRsBins; off <<= 1) {  // inclusive scan of the global digit totals
-    const uint32_t v = d >= off ? gb[d - off] : 0u;
-    __syncthreads();
-    gb[d] += v;
-    __syncthreads();
-  }
-  const uint32_t base = (d ? gb[d - 1] : 0u) + excl;
-  __syncthreads();
-  gb[d] = base;
+  // global position of digit d's first key of this tile: keys of smaller digits (all tiles, prefix from os_hist_kernel)
+  // + this digit in earlier tiles
+  gb[d] = gpre[pass * kRsBins + d] + excl;
 #pragma unroll
   for (int k = 0; k < ITEMS; ++k) {
     if (rank[k] == 0xFFFFFFFFu) continue;
@@ -1322,6 +1337,132 @@ __global__ void __launch_bounds__(kRsThreads) os_pass_kernel(const T* __restrict
   }
 }
 
+// Rows of 4097..16384 32-bit keys / ..8192 64-bit keys: the whole sort of a row in ONE 1024-thread workgroup (16
+// waves; ITEMS keys per lane in registers, the reorder buffer in LDS: 16384 x (4 + 4) B or 8192 x (8 + 4) B of the
+// 160 KB) -- the onesweep path ran 1 + P launches of <= 16 tiles there, each pass bound by launch + look-back latency
+// (profiles/sort_bench_r6.json: 0.36-0.9x torch.sort at 8K keys).  Per pass: 9-ballot ranking per 64-key round, the
+// 16 waves' digit counts prefixed by the 256 digit threads, the digit totals scanned with wave shuffles (3 barriers
+// instead of rs_rank_tile's 18), reorder through LDS, read back in element order.  Digits constant in the row skipped.
+template <typename T>
+struct SortBlockCfg {
+  static constexpr int kItems = sizeof(typename SortKey<T>::type) == 4 ? 16 : 8;
+  static constexpr int kThreads = 1024;
+  static constexpr int kTile = kThreads * kItems;
+};
+
+template <typename T>
+__global__ void __launch_bounds__(1024) sort_block_kernel(const T* __restrict__ x, int64_t n, bool desc, T* __restrict__ vals,
+                                                          int64_t* __restrict__ idx) {
+  using KT = typename SortKey<T>::type;
+  constexpr int ITEMS = SortBlockCfg<T>::kItems, NT = SortBlockCfg<T>::kThreads, NW = NT / kWave, TILE = SortBlockCfg<T>::kTile;
+  constexpr int PER = ITEMS * kWave;  // keys per wave
+  __shared__ uint32_t cnt[NW][kRsBins];
+  __shared__ uint32_t lstart[kRsBins];
+  __shared__ uint32_t wsum[kRsBins / kWave];
+  __shared__ KT s_key[TILE];
+  __shared__ uint32_t s_pos[TILE];
+  __shared__ KT s_and[NW], s_or[NW];
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
+  const int64_t s0 = (int64_t)blockIdx.x * n;
+  const int len = static_cast<int>(n);
+  KT key[ITEMS];
+  uint32_t pos[ITEMS], rank[ITEMS];
+  KT a = ~KT(0), o = KT(0);
+#pragma unroll
+  for (int k = 0; k < ITEMS; ++k) {
+    const int i = wave * PER + k * kWave + lane;
+    const bool ok = i < len;
+    const KT k0 = ok ? SortKey<T>::asc(x[s0 + i]) : KT(0);
+    key[k] = desc ? ~k0 : k0;
+    pos[k] = static_cast<uint32_t>(i);
+    if (ok) { a &= key[k]; o |= key[k]; }
+  }
+#pragma unroll
+  for (int off = kWave / 2; off > 0; off >>= 1) {
+    a &= __shfl_xor(a, off, kWave);
+    o |= __shfl_xor(o, off, kWave);
+  }
+  if (lane == 0) { s_and[wave] = a; s_or[wave] = o; }
+  __syncthreads();
+  KT varying;
+  {
+    KT ba = ~KT(0), bo = KT(0);
+#pragma unroll
+    for (int w = 0; w < NW; ++w) { ba &= s_and[w]; bo |= s_or[w]; }
+    varying = ba ^ bo;
+  }
+  for (int shift = 0; shift < 8 * static_cast<int>(sizeof(KT)); shift += 8) {
+    if (((varying >> shift) & KT(0xFF)) == KT(0)) continue;  // block-uniform
+    for (int i = tid; i < NW * kRsBins; i += NT) (&cnt[0][0])[i] = 0u;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < ITEMS; ++k) {  // stable ranking within the wave: round k = keys wave * PER + k * 64 + lane
+      const int i = wave * PER + k * kWave + lane;
+      const bool ok = i < len;
+      const uint32_t d = static_cast<uint32_t>((key[k] >> shift) & 0xFF);
+      uint64_t match = __ballot(ok);
+#pragma unroll
+      for (int b = 0; b < 8; ++b) {
+        const uint64_t bal = __ballot((d >> b) & 1u);
+        match &= ((d >> b) & 1u) ? bal : ~bal;
+      }
+      const uint64_t lower = match & ((1ull << lane) - 1ull);
+      const uint32_t before = cnt[wave][d];
+      rank[k] = ok ? before + static_cast<uint32_t>(__popcll(lower)) : 0xFFFFFFFFu;
+      if (ok && lower == 0ull) cnt[wave][d] = before + static_cast<uint32_t>(__popcll(match));
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the next round reads what this one wrote
+    }
+    __syncthreads();
+    uint32_t excl = 0;
+    if (tid < kRsBins) {  // digit d = tid: prefix over the waves, then the digit totals scanned (4 whole waves)
+      uint32_t run = 0;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) {
+        const uint32_t c = cnt[w][tid];
+        cnt[w][tid] = run;
+        run += c;
+      }
+      uint32_t sc = run;
+#pragma unroll
+      for (int off = 1; off < kWave; off <<= 1) {
+        const uint32_t t = __shfl_up(sc, off, kWave);
+        if (lane >= off) sc += t;
+      }
+      if (lane == kWave - 1) wsum[wave] = sc;
+      excl = sc - run;
+    }
+    __syncthreads();
+    if (tid < kRsBins) {
+      for (int w = 0; w < wave; ++w) excl += wsum[w];
+      lstart[tid] = excl;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < ITEMS; ++k) {
+      if (rank[k] == 0xFFFFFFFFu) continue;
+      const uint32_t d = static_cast<uint32_t>((key[k] >> shift) & 0xFF);
+      const uint32_t lp = lstart[d] + cnt[wave][d] + rank[k];
+      s_key[lp] = key[k];
+      s_pos[lp] = pos[k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < ITEMS; ++k) {  // the reordered row, read back in the ranking's element order
+      const int i = wave * PER + k * kWave + lane;
+      if (i < len) { key[k] = s_key[i]; pos[k] = s_pos[i]; }
+    }
+    __syncthreads();  // cnt / lstart / s_key are rewritten by the next pass
+  }
+#pragma unroll
+  for (int k = 0; k < ITEMS; ++k) {
+    const int i = wave * PER + k * kWave + lane;
+    if (i >= len) continue;
+    const KT kk = desc ? ~key[k] : key[k];
+    vals[s0 + i] = KeyDecode<T>::exact(kk) ? KeyDecode<T>::value(kk) : x[s0 + pos[k]];
+    idx[s0 + i] = pos[k];
+  }
+}
+
 template <typename T, int ITEMS>
 void radix_sort_onesweep_t(const at::Tensor& x, int64_t n, bool desc, at::Tensor& vals, at::Tensor& idx) {
   using KT = typename SortKey<T>::type;
@@ -1333,7 +1474,7 @@ void radix_sort_onesweep_t(const at::Tensor& x, int64_t n, bool desc, at::Tensor
   auto keys = at::empty({2 * n}, opts.dtype(kdt));
   auto pays = at::empty({2 * n}, opts.dtype(at::kInt));
   // zeroed scratch: digit totals [P][256] | tile status [P][Tt][256] | tile counters [P] + error word | AND / OR
-  const int64_t words = (int64_t)P * kRsBins + (int64_t)P * Tt * kRsBins + P + 1;
+  const int64_t words = (int64_t)P * kRsBins + (int64_t)P * Tt * kRsBins + P + 1 + 1 + (int64_t)P * kRsBins;
   const int64_t kt_words = 2 * static_cast<int64_t>(sizeof(KT)) / 4;
   auto scratch = at::empty({words + kt_words + 1}, opts.dtype(at::kInt));  // (+1: 8-B alignment of the AND / OR)
   uint32_t* sp = reinterpret_cast<uint32_t*>(scratch.data_ptr());
@@ -1342,18 +1483,20 @@ void radix_sort_onesweep_t(const at::Tensor& x, int64_t n, bool desc, at::Tensor
   uint32_t* status = ghist + P * kRsBins;
   unsigned* ctr = status + (int64_t)P * Tt * kRsBins;
   int* err = reinterpret_cast<int*>(ctr + P);
-  uintptr_t ao = reinterpret_cast<uintptr_t>(err + 1);
+  unsigned* hdone = reinterpret_cast<unsigned*>(err + 1);
+  uint32_t* gpre = hdone + 1;
+  uintptr_t ao = reinterpret_cast<uintptr_t>(gpre + P * kRsBins);
   ao = (ao + 7) & ~uintptr_t(7);
   KT* andor = reinterpret_cast<KT*>(ao);
   KT* kb0 = reinterpret_cast<KT*>(keys.data_ptr());
   uint32_t* pb0 = reinterpret_cast<uint32_t*>(pays.data_ptr());
   const T* xp = x.data_ptr<T>();
   const int hgrid = static_cast<int>(std::min<int64_t>((n + 1023) / 1024, 512));
-  hipLaunchKernelGGL(os_hist_kernel<T>, hgrid, 256, 0, stream(), xp, n, desc, ghist, andor);
+  hipLaunchKernelGGL(os_hist_kernel<T>, hgrid, 256, 0, stream(), xp, n, desc, ghist, andor, hdone, gpre);
   TMX_LAUNCH_CHECK();
   for (int p = 0; p < P; ++p) {
     hipLaunchKernelGGL((os_pass_kernel<T, ITEMS>), Tt, kRsThreads, 0, stream(), xp, kb0, kb0 + n, pb0, pb0 + n, vals.data_ptr<T>(),
-                       idx.data_ptr<int64_t>(), n, desc, p, ghist, status, ctr, andor, err);
+                       idx.data_ptr<int64_t>(), n, desc, p, gpre, status, ctr, andor, err);
     TMX_LAUNCH_CHECK();
   }
 }
@@ -1407,6 +1550,13 @@ void radix_sort_impl(const at::Tensor& x, int S, int64_t n, bool desc, at::Tenso
     const void* kfn = small_tiles ? reinterpret_cast<const void*>(&sort_coop_kernel<T, 4>)
                                   : reinterpret_cast<const void*>(&sort_coop_kernel<T, kRsItems>);
     TMX_CHECK_HIP(hipLaunchCooperativeKernel(kfn, dim3(Tt), dim3(kRsThreads), args, 0, stream()));
+    return;
+  }
+  static const bool blk_off = std::getenv("TMX_SORT_BLOCK_OFF") != nullptr;  // A/B knob (tools/sort_bench.py)
+  if (n > kRsTile && n <= SortBlockCfg<T>::kTile && !blk_off) {  // one 1024-thread workgroup per row, one launch
+    hipLaunchKernelGGL(sort_block_kernel<T>, S, SortBlockCfg<T>::kThreads, 0, stream(), x.data_ptr<T>(), n, desc, vals.data_ptr<T>(),
+                       idx.data_ptr<int64_t>());
+    TMX_LAUNCH_CHECK();
     return;
   }
   static const bool os_off = std::getenv("TMX_SORT_ONESWEEP_OFF") != nullptr;  // A/B knob (tools/sort_bench.py)

@@ -1,6 +1,7 @@
 """``tmx::radix_sort`` (csrc/radix.hip, ops/sort.py) against ``torch.sort(..., stable=True)`` on the host: identical
 indices (stability included) and bit-identical values for fp32 / fp64 / int32 / int64, ascending and descending,
-ties, NaN, +-inf, signed zeros, 1-D and row-batched 2-D inputs, tile edges (4096 keys per tile)."""
+ties, NaN, +-inf, signed zeros, 1-D and row-batched 2-D inputs, tile edges (4096 keys per tile), the one-workgroup row kernels' limits (4096;
+16384 32-bit / 8192 64-bit keys)."""
 import pytest
 import torch
 
@@ -57,7 +58,7 @@ def _check(x, descending):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float64, torch.int32, torch.int64])
-@pytest.mark.parametrize("n", [0, 1, 5, 4095, 4096, 4097, 65_536, 100_003, 131_072, 131_073, 524_288, 524_289])
+@pytest.mark.parametrize("n", [0, 1, 5, 4095, 4096, 4097, 8192, 8193, 12_345, 16_384, 16_385, 65_536, 100_003, 131_072, 131_073, 524_288, 524_289])
 @pytest.mark.parametrize("descending", [False, True])
 def test_radix_sort_matches_stable_torch_sort(dtype, n, descending):
     _check(_data(n, dtype, seed=n + 3), descending)
@@ -67,6 +68,7 @@ def test_radix_sort_matches_stable_torch_sort(dtype, n, descending):
 def test_radix_sort_rows(dtype):
     _check(_data(9001, dtype, seed=1, rows=7), False)
     _check(_data(9001, dtype, seed=2, rows=7), True)
+    _check(_data(8000, dtype, seed=3, rows=5), True)  # one 1024-thread workgroup per row (sort_block_kernel) for both
 
 
 def test_radix_sort_large():

@@ -105,7 +105,7 @@ def test_map_batched_update_refuses_mixed_dtypes():
 
 def test_map_batched_update_views_and_lazy_items_match_per_image_path():
     """Round 6: a batch whose per-image tensors are rows of one batch tensor is concatenated without a copy
-    (csrc/rows_host.cpp cat_rows), the per-image items stay lazy until used, and compute / state_dict equal the
+    (csrc/py_columns.cpp cat_dict_columns), the per-image items stay lazy until used, and compute / state_dict equal the
     per-image path's."""
     from torchmetrics_forked_amd import ops
     from torchmetrics_forked_amd.detection import MeanAveragePrecision

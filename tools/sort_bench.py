@@ -32,7 +32,7 @@ def main() -> None:
 
     if os.environ.get("SORT_BENCH_SWEEP"):  # crossover sweep against torch.sort (sets ops/sort.py's routing)
         cases = {}
-        for n in (8192, 32768, 65536, 131072, 196608, 262144, 393216, 524288, 1 << 20):
+        for n in (8192, 16384, 32768, 65536, 131072, 196608, 262144, 393216, 524288, 1 << 20):
             cases[f"f32_{n}"] = torch.randn(n, device=dev, generator=g)
             cases[f"i64_{n}"] = torch.randint(-(1 << 40), 1 << 40, (n,), device=dev, generator=g)
         for n in (65536, 262144, 1 << 20, 1 << 22, 1 << 24):

@@ -200,26 +200,23 @@ class MeanAveragePrecision(Metric):
         if not all(isinstance(st, StateArena) for st in states):
             return False
         try:
-            # C-level column extraction (map + itemgetter: ~2x a comprehension per 512-image batch)
-            cols = (list(map(_BOXES, preds)), list(map(_SCORES, preds)), list(map(_LABELS, preds)),
-                    list(map(_BOXES, target)), list(map(_LABELS, target)))
-            extra = (_optional_col(target, "iscrowd"), _optional_col(target, "area"))
-            if ops.load():
-                # one C++ pass per column: every item of one dtype / device / shape, row counts, and the concatenation
-                # (a view when the items are consecutive rows of one batch tensor) -- csrc/rows_host.cpp cat_rows
-                res = [torch.ops.tmx.cat_rows(col, w) for col, w in zip(cols, (4, 0, 0, 4, 0))]
-                res_x = [torch.ops.tmx.cat_rows(col, 0) if col is not None else None for col in extra]
-                if any(r[1].numel() == 0 for r in res) or any(r is not None and r[1].numel() == 0 for r in res_x):
+            pym = ops.py_module()
+            if pym is not None:
+                # one C pass per list straight over the dicts (csrc/py_columns.cpp): per column one dtype / device /
+                # shape, equal row counts across an item's columns, and the concatenation (a view when the items are
+                # consecutive rows of one batch tensor); a torch.ops call would box every tensor of each column list
+                rp = pym.cat_dict_columns(preds, _PRED_KEYS, _PRED_WIDTHS)
+                rt = pym.cat_dict_columns(target, _GT_KEYS, _GT_WIDTHS) if rp is not None else None
+                if rt is None:
                     return False
-                # row counts compared as host int64 tensors (torch.equal), listed once
-                eq = torch.equal
-                if (not eq(res[2][1], res[0][1]) or not eq(res[2][1], res[1][1]) or not eq(res[4][1], res[3][1])
-                        or any(r is not None and not eq(r[1], res[4][1]) for r in res_x)):
-                    return False
-                dn, gn = res[2][1].tolist(), res[4][1].tolist()
-                flats = [r[0] for r in res]
-                crowd, area = (r[0] if r is not None else None for r in res_x)
+                (flats, dn), (gcols, gn) = rp, rt
+                flats = [*flats, gcols[0], gcols[1]]
+                crowd, area = gcols[2], gcols[3]
             else:
+                # C-level column extraction (map + itemgetter: ~2x a comprehension per 512-image batch)
+                cols = (list(map(_BOXES, preds)), list(map(_SCORES, preds)), list(map(_LABELS, preds)),
+                        list(map(_BOXES, target)), list(map(_LABELS, target)))
+                extra = (_optional_col(target, "iscrowd"), _optional_col(target, "area"))
                 n_crowd, n_area = extra[0] is not None, extra[1] is not None
                 db, ds, dl, gb, gl = cols
                 dn = [t.shape[0] for t in dl]  # (Tensor.__len__ is a Python-level method: 5x the cost of .shape)
@@ -911,6 +908,10 @@ def _flat_rows(lst: List[Tensor], n: int, dtype: torch.dtype, dev: torch.device,
 
 
 _BOXES, _SCORES, _LABELS = operator.itemgetter("boxes"), operator.itemgetter("scores"), operator.itemgetter("labels")
+
+
+_PRED_KEYS, _PRED_WIDTHS = ("boxes", "scores", "labels"), (4, 0, 0)
+_GT_KEYS, _GT_WIDTHS = ("boxes", "labels", "iscrowd", "area"), (4, 0, -1, -1)  # (-1: optional 1-d column)
 
 
 def _optional_col(items: List[Dict[str, Tensor]], key: str) -> Optional[List[Tensor]]:

@@ -54,6 +54,23 @@ def available() -> bool:
     return load()
 
 
+_py_mod: Optional[object] = None
+
+
+def py_module() -> Optional[object]:
+    """The library's CPython entry point (``csrc/py_columns.cpp``: host helpers that read Python containers in C,
+    where a ``torch.ops`` call would box every tensor of a list); ``None`` when the library is not loaded."""
+    global _py_mod
+    if _py_mod is None and load():
+        import importlib.util
+
+        spec = importlib.util.spec_from_file_location("_tmx_native", str(_LIB))
+        mod = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mod)
+        _py_mod = mod
+    return _py_mod
+
+
 def require(tensor: Optional[torch.Tensor] = None) -> None:
     """Raise unless the native library is loaded (called on every GPU code path)."""
     if not load():

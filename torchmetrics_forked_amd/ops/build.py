@@ -18,6 +18,7 @@ import os
 import shutil
 import subprocess
 import sys
+import sysconfig
 from concurrent.futures import ThreadPoolExecutor
 from pathlib import Path
 from typing import List
@@ -67,7 +68,8 @@ def _common_flags() -> List[str]:
 
 # per-source extra flags: image.hip's SSIM kernel keeps its MFMA accumulators in VGPRs (the AGPR form read every
 # result back with one v_accvgpr_read per value: ~50 extra VALU instructions per band of its VALU-bound loop)
-_EXTRA_FLAGS = {"image.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]}
+# py_columns.cpp is the library's CPython entry point (``ops.py_module()``): Python headers, libtorch_python at link
+_EXTRA_FLAGS = {"image.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"], "py_columns.cpp": [f"-I{sysconfig.get_paths()['include']}"]}
 
 
 def _flags_for(src: Path) -> List[str]:
@@ -165,6 +167,7 @@ def build(jobs: int = 8, force: bool = False, verbose: bool = True) -> Path:
         "-ltorch",
         "-ltorch_cpu",
         "-ltorch_hip",
+        "-ltorch_python",
         f"-Wl,-rpath,{lib}",
         "-o",
         str(tmp),
