@@ -1337,15 +1337,15 @@ __global__ void __launch_bounds__(kRsThreads) os_pass_kernel(const T* __restrict
   }
 }
 
-// Rows of 4097..16384 32-bit keys / ..8192 64-bit keys: the whole sort of a row in ONE 1024-thread workgroup (16
-// waves; ITEMS keys per lane in registers, the reorder buffer in LDS: 16384 x (4 + 4) B or 8192 x (8 + 4) B of the
-// 160 KB) -- the onesweep path ran 1 + P launches of <= 16 tiles there, each pass bound by launch + look-back latency
-// (profiles/sort_bench_r6.json: 0.36-0.9x torch.sort at 8K keys).  Per pass: 9-ballot ranking per 64-key round, the
+// Rows of 4097..8192 keys: the whole sort of a row in ONE 1024-thread workgroup (16 waves; 8 keys per lane in
+// registers, the reorder buffer in LDS: 8192 x (8 + 4) B of the 160 KB at most) -- the onesweep path ran 1 + P
+// launches of <= 8 tiles there, each pass bound by launch + look-back latency (profiles/sort_bench_r6.json: 0.54-0.9x
+// torch.sort at 8K keys).  Per pass: 9-ballot ranking per 64-key round, the
 // 16 waves' digit counts prefixed by the 256 digit threads, the digit totals scanned with wave shuffles (3 barriers
 // instead of rs_rank_tile's 18), reorder through LDS, read back in element order.  Digits constant in the row skipped.
 template <typename T>
 struct SortBlockCfg {
-  static constexpr int kItems = sizeof(typename SortKey<T>::type) == 4 ? 16 : 8;
+  static constexpr int kItems = 8;  // (16 keys per lane spilled 23 / 825 VGPRs for fp32 / int32 at 1024 threads)
   static constexpr int kThreads = 1024;
   static constexpr int kTile = kThreads * kItems;
 };
