@@ -1159,8 +1159,7 @@ constexpr uint32_t kOsAgg = 1u << 30, kOsInc = 2u << 30, kOsVal = (1u << 30) - 1
 
 template <typename T>
 __global__ void __launch_bounds__(256) os_hist_kernel(const T* __restrict__ x, int64_t n, bool desc, uint32_t* __restrict__ ghist,
-                                                      typename SortKey<T>::type* __restrict__ andor, unsigned* __restrict__ done,
-                                                      uint32_t* __restrict__ gpre) {
+                                                      typename SortKey<T>::type* __restrict__ andor) {
   using KT = typename SortKey<T>::type;
   constexpr int P = static_cast<int>(sizeof(KT));
   __shared__ uint32_t h[P * kRsBins];
@@ -1187,36 +1186,13 @@ __global__ void __launch_bounds__(256) os_hist_kernel(const T* __restrict__ x, i
     atomicOr(&andor[0], na);
     atomicOr(&andor[1], o);
   }
-  // the last block turns the digit totals into exclusive prefixes per pass (gpre), once -- every tile of every pass
-  // read its pass's 256 totals and scanned them itself before (8 barrier rounds per tile and pass)
-  __shared__ bool s_last;
-  __threadfence();
-  __syncthreads();
-  if (threadIdx.x == 0) s_last = atomicAdd(done, 1u) == gridDim.x - 1;
-  __syncthreads();
-  if (!s_last) return;
-  __threadfence();
-  __shared__ uint32_t sc[kRsBins];
-  for (int p = 0; p < P; ++p) {
-    const uint32_t v = __hip_atomic_load(&ghist[p * kRsBins + threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    sc[threadIdx.x] = v;
-    __syncthreads();
-    for (int off = 1; off < kRsBins; off <<= 1) {
-      const uint32_t t = threadIdx.x >= off ? sc[threadIdx.x - off] : 0u;
-      __syncthreads();
-      sc[threadIdx.x] += t;
-      __syncthreads();
-    }
-    gpre[p * kRsBins + threadIdx.x] = sc[threadIdx.x] - v;  // exclusive
-    __syncthreads();
-  }
 }
 
 template <typename T, int ITEMS = kRsItems>
 __global__ void __launch_bounds__(kRsThreads) os_pass_kernel(const T* __restrict__ x, typename SortKey<T>::type* __restrict__ kb0,
                                                                typename SortKey<T>::type* __restrict__ kb1, uint32_t* __restrict__ pb0,
                                                                uint32_t* __restrict__ pb1, T* __restrict__ vals, int64_t* __restrict__ idx,
-                                                               int64_t n, bool desc, int pass, const uint32_t* __restrict__ gpre,
+                                                               int64_t n, bool desc, int pass, const uint32_t* __restrict__ ghist,
                                                                uint32_t* __restrict__ status, unsigned* __restrict__ ctr,
                                                                const typename SortKey<T>::type* __restrict__ andor, int* __restrict__ err) {
   using KT = typename SortKey<T>::type;
@@ -1309,9 +1285,18 @@ __global__ void __launch_bounds__(kRsThreads) os_pass_kernel(const T* __restrict
     }
     __hip_atomic_store(&st[(int64_t)t * kRsBins + d], kOsInc | (excl + c), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  // global position of digit d's first key of this tile: keys of smaller digits (all tiles, prefix from os_hist_kernel)
-  // + this digit in earlier tiles
-  gb[d] = gpre[pass * kRsBins + d] + excl;
+  // global position of digit d's first key of this tile: keys of smaller digits (all tiles) + this digit in earlier tiles
+  gb[d] = ghist[pass * kRsBins + d];
+  __syncthreads();
+  for (int off = 1; off < kRsBins; off <<= 1) {  // inclusive scan of the global digit totals
+    const uint32_t v = d >= off ? gb[d - off] : 0u;
+    __syncthreads();
+    gb[d] += v;
+    __syncthreads();
+  }
+  const uint32_t base = (d ? gb[d - 1] : 0u) + excl;
+  __syncthreads();
+  gb[d] = base;
 #pragma unroll
   for (int k = 0; k < ITEMS; ++k) {
     if (rank[k] == 0xFFFFFFFFu) continue;
@@ -1474,7 +1459,7 @@ void radix_sort_onesweep_t(const at::Tensor& x, int64_t n, bool desc, at::Tensor
   auto keys = at::empty({2 * n}, opts.dtype(kdt));
   auto pays = at::empty({2 * n}, opts.dtype(at::kInt));
   // zeroed scratch: digit totals [P][256] | tile status [P][Tt][256] | tile counters [P] + error word | AND / OR
-  const int64_t words = (int64_t)P * kRsBins + (int64_t)P * Tt * kRsBins + P + 1 + 1 + (int64_t)P * kRsBins;
+  const int64_t words = (int64_t)P * kRsBins + (int64_t)P * Tt * kRsBins + P + 1;
   const int64_t kt_words = 2 * static_cast<int64_t>(sizeof(KT)) / 4;
   auto scratch = at::empty({words + kt_words + 1}, opts.dtype(at::kInt));  // (+1: 8-B alignment of the AND / OR)
   uint32_t* sp = reinterpret_cast<uint32_t*>(scratch.data_ptr());
@@ -1483,20 +1468,18 @@ void radix_sort_onesweep_t(const at::Tensor& x, int64_t n, bool desc, at::Tensor
   uint32_t* status = ghist + P * kRsBins;
   unsigned* ctr = status + (int64_t)P * Tt * kRsBins;
   int* err = reinterpret_cast<int*>(ctr + P);
-  unsigned* hdone = reinterpret_cast<unsigned*>(err + 1);
-  uint32_t* gpre = hdone + 1;
-  uintptr_t ao = reinterpret_cast<uintptr_t>(gpre + P * kRsBins);
+  uintptr_t ao = reinterpret_cast<uintptr_t>(err + 1);
   ao = (ao + 7) & ~uintptr_t(7);
   KT* andor = reinterpret_cast<KT*>(ao);
   KT* kb0 = reinterpret_cast<KT*>(keys.data_ptr());
   uint32_t* pb0 = reinterpret_cast<uint32_t*>(pays.data_ptr());
   const T* xp = x.data_ptr<T>();
   const int hgrid = static_cast<int>(std::min<int64_t>((n + 1023) / 1024, 512));
-  hipLaunchKernelGGL(os_hist_kernel<T>, hgrid, 256, 0, stream(), xp, n, desc, ghist, andor, hdone, gpre);
+  hipLaunchKernelGGL(os_hist_kernel<T>, hgrid, 256, 0, stream(), xp, n, desc, ghist, andor);
   TMX_LAUNCH_CHECK();
   for (int p = 0; p < P; ++p) {
     hipLaunchKernelGGL((os_pass_kernel<T, ITEMS>), Tt, kRsThreads, 0, stream(), xp, kb0, kb0 + n, pb0, pb0 + n, vals.data_ptr<T>(),
-                       idx.data_ptr<int64_t>(), n, desc, p, gpre, status, ctr, andor, err);
+                       idx.data_ptr<int64_t>(), n, desc, p, ghist, status, ctr, andor, err);
     TMX_LAUNCH_CHECK();
   }
 }

@@ -5,7 +5,6 @@ forward).  Complements tools/forward_bench.py (device timeline) for the host-enq
     python tools/forward_cprof.py
 """
 import cProfile
-import io
 import os
 import pstats
 import sys
@@ -28,19 +27,34 @@ def main() -> None:
         coll(*pool[i % 4])
     torch.cuda.synchronize(dev)
     steps = 50
+    import time
+
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(steps):
+        coll(*pool[i % 4])
+    t1 = time.perf_counter()
+    torch.cuda.synchronize(dev)
+    t_upd = time.perf_counter()
+    for i in range(steps):
+        coll.update(*pool[i % 4])
+    t_upd1 = time.perf_counter()
+    torch.cuda.synchronize(dev)
+    print(f"host enqueue without profiler: forward {1e6 * (t1 - t0) / steps:.1f} us, update {1e6 * (t_upd1 - t_upd) / steps:.1f} us "
+          "(queue-bound once the device falls behind: compare the two)")
     pr = cProfile.Profile()
     pr.enable()
     for i in range(steps):
         coll(*pool[i % 4])
     pr.disable()
     torch.cuda.synchronize(dev)
-    for key in ("cumulative", "tottime"):
-        s = io.StringIO()
-        st = pstats.Stats(pr, stream=s).sort_stats(key)
-        st.print_stats(35)
-        print(f"--- forward: by {key} (totals over {steps} forwards)")
-        print(s.getvalue()[:9000])
-
+    st = pstats.Stats(pr).stats
+    print(f"--- forward: by cumulative (us per forward, cProfile on), {sum(v[1] for v in st.values()) / steps:.0f} calls per forward")
+    for ct, tt, nc, k in sorted(((v[3], v[2], v[1], k) for k, v in st.items()), reverse=True)[:45]:
+        print(f"{1e6 * ct / steps:10.1f} {1e6 * tt / steps:10.1f} {nc:8d} {os.path.basename(k[0])}:{k[1]}({k[2]})")
+    print("--- forward: by self time")
+    for tt, ct, nc, k in sorted(((v[2], v[3], v[1], k) for k, v in st.items()), reverse=True)[:45]:
+        print(f"{1e6 * tt / steps:10.1f} {1e6 * ct / steps:10.1f} {nc:8d} {os.path.basename(k[0])}:{k[1]}({k[2]})")
 
 if __name__ == "__main__":
     main()

@@ -755,9 +755,12 @@ class Metric(Module, ABC):
             with host_checks() as batch:
                 if self._deferred is not None:
                     self._deferred.check()
-                with _range(f"tmx/{self.__class__.__name__}.compute"), self.sync_context(
-                    dist_sync_fn=self.dist_sync_fn, should_sync=self._to_sync, should_unsync=self._should_unsync
-                ):
+                if _PROFILE or d["_is_synced"] or (d["_to_sync"] and self._distributed_on()):
+                    with _range(f"tmx/{self.__class__.__name__}.compute"), self.sync_context(
+                        dist_sync_fn=self.dist_sync_fn, should_sync=self._to_sync, should_unsync=self._should_unsync
+                    ):
+                        value = self._unalias(_squeeze_if_scalar(compute(*args, **kwargs)))
+                else:  # nothing to sync or unsync (sync_context would return at once): no generator context per compute
                     value = self._unalias(_squeeze_if_scalar(compute(*args, **kwargs)))
                 if self.compute_with_cache:
                     self._computed = value
@@ -765,6 +768,11 @@ class Metric(Module, ABC):
             return value
 
         return wrapped_func
+
+    def _distributed_on(self) -> bool:
+        """``sync``'s own test (``distributed_available_fn``, no override): would a sync reach a collective?"""
+        fn = self.distributed_available_fn
+        return bool(fn()) if callable(fn) else False
 
     def _drop_computed(self) -> None:
         self._computed = None
