@@ -176,6 +176,10 @@ def _worker(args: argparse.Namespace) -> None:
     for i in range(args.steps):
         coll.update(*pool[i % args.pool])
     if use_cuda:
+        # (diagnostic split only: the updates' side-stream work -- the curve update lanes -- is joined into this stream
+        # so the event closes the update share; compute would join it first anyway, the total is unaffected)
+        for m in coll.values(copy_state=False):
+            m._join_side_work()
         ev_upd.record()
     res = coll.compute()
     sync()

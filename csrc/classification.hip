@@ -1859,7 +1859,8 @@ void curve_hist_update_impl(const at::Tensor& preds_, const at::Tensor& target_,
 
 // forward()'s batch histogram: ``dst[c, :, lo..hi] += src[c, :, lo..hi]`` over the source's occupied range per class
 // (and the destination range widened), or -- curve_hist_zero -- ``src`` zeroed over that range and the range emptied,
-// so the scratch is ready for the next batch.  One 256-thread workgroup per (class, 4096-code slice): grid.y slices.
+// so the scratch is ready for the next batch, or -- curve_hist_drain -- both in one pass (the update lanes' join).
+// One 256-thread workgroup per (class, 4096-code slice): grid.y slices.
 constexpr int kMergeThreads = 256;
 constexpr int kMergeSlice = 4096;
 __global__ void __launch_bounds__(kMergeThreads) curve_hist_merge_kernel(int64_t* __restrict__ dst, int* __restrict__ dst_range,
@@ -1873,12 +1874,12 @@ __global__ void __launch_bounds__(kMergeThreads) curve_hist_merge_kernel(int64_t
     for (int i = s0 + threadIdx.x; i < s1; i += kMergeThreads) {
       const int64_t v = sp[i];
       if (v == 0) continue;
+      if (dp != nullptr) dp[i] += v;
       if (zero) sp[i] = 0;
-      else dp[i] += v;
     }
   }
   if (blockIdx.y == 0 && threadIdx.x == 0 && hi >= lo) {
-    if (!zero && dst_range != nullptr) {
+    if (dst_range != nullptr) {
       atomicMin(dst_range + 2 * c, lo);
       atomicMax(dst_range + 2 * c + 1, hi);
     }
@@ -1909,6 +1910,24 @@ void curve_hist_zero(at::Tensor& src, at::Tensor& src_range) {
   if (C == 0) return;
   hipLaunchKernelGGL(curve_hist_merge_kernel, dim3(C, kCodes / kMergeSlice), kMergeThreads, 0, stream(), static_cast<int64_t*>(nullptr),
                      static_cast<int*>(nullptr), src.data_ptr<int64_t>(), src_range.data_ptr<int>(), true);
+  TMX_LAUNCH_CHECK();
+  hipLaunchKernelGGL(curve_range_reset_kernel, (C + 255) / 256, 256, 0, stream(), src_range.data_ptr<int>(), C);
+  TMX_LAUNCH_CHECK();
+}
+
+// The update lanes' join (classification/precision_recall_curve.py ``_join_lanes``): ``src`` (lane 1's histogram) added
+// into ``dst`` (the metric's) over src's occupied range per class, dst's range widened, src zeroed and its range emptied.
+void curve_hist_drain(at::Tensor& dst, at::Tensor& dst_range, at::Tensor& src, at::Tensor& src_range) {
+  TORCH_CHECK(src.is_contiguous() && src.scalar_type() == at::kLong && src.dim() == 3 && src.size(1) == 2 && src.size(2) == kCodes &&
+              dst.is_contiguous() && dst.sizes() == src.sizes() && dst.scalar_type() == at::kLong && dst.device() == src.device(),
+              "curve_hist_drain: two int64 [C, 2, 16384] histograms on one device");
+  for (const at::Tensor* r : {&src_range, &dst_range})
+    TORCH_CHECK(r->scalar_type() == at::kInt && r->numel() == 2 * src.size(0) && r->is_contiguous() && r->device() == src.device(),
+                "curve_hist_drain: ranges must be int32[C, 2] on the histograms' device");
+  const int C = static_cast<int>(src.size(0));
+  if (C == 0) return;
+  hipLaunchKernelGGL(curve_hist_merge_kernel, dim3(C, kCodes / kMergeSlice), kMergeThreads, 0, stream(), dst.data_ptr<int64_t>(),
+                     dst_range.data_ptr<int>(), src.data_ptr<int64_t>(), src_range.data_ptr<int>(), true);
   TMX_LAUNCH_CHECK();
   hipLaunchKernelGGL(curve_range_reset_kernel, (C + 255) / 256, 256, 0, stream(), src_range.data_ptr<int>(), C);
   TMX_LAUNCH_CHECK();
@@ -2960,6 +2979,7 @@ TORCH_LIBRARY_FRAGMENT(tmx, m) {
   m.def("binary_stats_update(Tensor preds, Tensor target, Tensor(a!) counts, int num_labels, float threshold, int ignore_index, bool has_ignore) -> ()");
   m.def("curve_hist_update(Tensor preds, Tensor target, Tensor(a!) hist, int task, int ignore_index, bool has_ignore, Tensor(b!)? confmat, Tensor? norm_flag, Tensor(c!)? err_flag, Tensor(d!)? mode_state, Tensor(e!)? code_range=None, Tensor(f!)? batch_hist=None, Tensor(g!)? batch_range=None) -> ()");
   m.def("curve_hist_zero(Tensor(a!) hist, Tensor(b!) code_range) -> ()");
+  m.def("curve_hist_drain(Tensor(a!) dst, Tensor(b!) dst_range, Tensor(c!) src, Tensor(d!) src_range) -> ()");
   m.def("curve_hist_reduce(Tensor hist, Tensor? code_range=None) -> Tensor");
   m.def("curve_summary(Tensor scores) -> Tensor");
   m.def("curve_hist_scores(Tensor(a!) hist, Tensor(b!)? code_range=None, bool clear=False) -> Tensor[]");
@@ -2979,6 +2999,7 @@ TORCH_LIBRARY_IMPL(tmx, CUDA, m) {
   m.impl("binary_stats_fused", &tmx::binary_stats_fused);
   m.impl("curve_hist_update", &tmx::curve_hist_update);
   m.impl("curve_hist_zero", &tmx::curve_hist_zero);
+  m.impl("curve_hist_drain", &tmx::curve_hist_drain);
   m.impl("curve_hist_reduce", &tmx::curve_hist_reduce);
   m.impl("curve_summary", &tmx::curve_summary);
   m.impl("curve_hist_scores", &tmx::curve_hist_scores);

@@ -1,0 +1,115 @@
+"""Update lanes of the multiclass exact-histogram curve metrics (classification/precision_recall_curve.py
+``_lane_update``): consecutive batches alternate between two side streams with private histograms, joined and drained
+at every state consumer.  Every result must equal the single-stream path (``_LANES_ON`` off) bit for bit: histograms,
+AUROC / AP values, the fused confusion matrix, forward values, state_dict, reset (the code range must cover every
+occupied code)."""
+import pytest
+import torch
+
+import torchmetrics_forked_amd as tm
+from torchmetrics_forked_amd import ops
+from torchmetrics_forked_amd.classification import precision_recall_curve as prc
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_native(device):
+    ops.require()
+
+
+def _batches(n, c, k, seed=0, probs_at=()):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    out = []
+    for i in range(k):
+        x = torch.randn(n, c, device="cuda", generator=g) * 3
+        if i in probs_at:  # probabilities: the speculated softmax decision flips for this batch
+            x = x.softmax(-1)
+        out.append((x.bfloat16(), torch.randint(0, c, (n,), device="cuda", generator=g)))
+    return out
+
+
+def _run(make, batches, lanes, monkeypatch, after=None):
+    monkeypatch.setattr(prc, "_LANES_ON", lanes)
+    m = make().cuda()
+    for p, t in batches:
+        m.update(p, t)
+    if after is not None:
+        after(m)
+    return m
+
+
+@pytest.mark.parametrize("c", [512, 1000])
+def test_lanes_match_single_stream(c, monkeypatch):
+    n = (1 << 22) // c + 64
+    bs = _batches(n, c, 5, seed=c, probs_at=(3,))
+    mk = lambda: tm.MulticlassAUROC(num_classes=c)  # noqa: E731
+    ref = _run(mk, bs, False, monkeypatch)
+    got = _run(mk, bs, True, monkeypatch)
+    assert "_lanes" in got.__dict__ and got.__dict__["_lanes"].dirty  # lane 1 holds batches 2 and 4
+    a_ref, a_got = ref.compute(), got.compute()
+    assert torch.equal(a_ref, a_got)
+    assert torch.equal(ref.metric_state["score_hist"], got.metric_state["score_hist"])
+    # the code range is a superset of the occupied codes (a mispredicted softmax decision may widen it before the
+    # refit): it must cover every occupied code; lanes speculate from their own history, so the supersets may differ
+    h, rng = got.metric_state["score_hist"], got._tracked_range()
+    occ = h.amax(1) > 0
+    idx = torch.arange(h.shape[-1], device=h.device)
+    assert bool((~occ | ((idx >= rng[:, :1]) & (idx <= rng[:, 1:]))).all())
+    # more updates after a compute: lanes restart at lane 0 and keep matching
+    more = _batches(n, c, 3, seed=c + 1)
+    for p, t in more:
+        ref.update(p, t)
+        got.update(p, t)
+    assert torch.equal(ref.compute(), got.compute())
+    assert torch.equal(ref.state_dict()["score_hist"], got.state_dict()["score_hist"])
+
+
+def test_lanes_fused_collection_and_forward(monkeypatch):
+    c = 1000
+    n = 8192
+    bs = _batches(n, c, 4, seed=5)
+
+    def mk():
+        return tm.MetricCollection({"auroc": tm.MulticlassAUROC(num_classes=c), "cm": tm.MulticlassConfusionMatrix(num_classes=c)})
+
+    res = {}
+    for lanes in (False, True):
+        monkeypatch.setattr(prc, "_LANES_ON", lanes)
+        coll = mk().cuda()
+        for p, t in bs[:3]:
+            coll.update(p, t)
+        fwd = coll(*bs[3])  # forward after lane updates: joins first, batch values from the batch alone
+        out = coll.compute()
+        res[lanes] = (fwd, out, coll["auroc"].metric_state["score_hist"].clone())
+        if lanes:
+            assert "_lanes" in coll["auroc"].__dict__
+    (f0, o0, h0), (f1, o1, h1) = res[False], res[True]
+    for k in f0:
+        assert torch.equal(f0[k], f1[k]), k
+    for k in o0:
+        assert torch.equal(o0[k], o1[k]), k
+    assert torch.equal(h0, h1)
+
+
+def test_lanes_reset_and_reload(monkeypatch):
+    c = 1000
+    n = 8192
+    bs = _batches(n, c, 3, seed=9)
+    mk = lambda: tm.MulticlassAveragePrecision(num_classes=c)  # noqa: E731
+    ref = _run(mk, bs, False, monkeypatch)
+    got = _run(mk, bs, True, monkeypatch)
+    sd = got.state_dict()
+    assert torch.equal(sd["score_hist"], ref.state_dict()["score_hist"])
+    got.reset()
+    ref.reset()
+    for p, t in bs[1:]:
+        ref.update(p, t)
+        got.update(p, t)
+    assert torch.equal(ref.compute(), got.compute())
+    # a state loaded over pending lane work replaces it (the lanes drain into the replaced histogram first)
+    got.update(*bs[0])
+    got.update(*bs[0])
+    got.load_state_dict(sd)
+    fresh = _run(mk, bs, False, monkeypatch)
+    assert torch.equal(got.compute(), fresh.compute())

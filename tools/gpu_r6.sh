@@ -76,6 +76,7 @@ for s in "$@"; do
     ssimstrip) for st in 256 512 1024; do TMX_SSIM_STRIP=$st run ssim_strip$st 120 ./build/kexp_r6/ssim_mfma_exp; echo "strip $st: $(grep -o '"config4_KS11[^}]*}' $OUT/ssim_strip$st.log | grep -o '"mfma_ms[^,]*')"; done ;;
     ssimbench) run ssimbench 300 python tools/ssim_bench.py; tail -1 "$OUT/ssimbench.log" ;;
     ssimprof) run ssimprof 300 rocprofv3 --kernel-trace --stats -d "$OUT/ssimprof" -o ssim --output-format csv -- python3 tools/ssim_bench.py ;;
+    overlap) run overlap 120 python tools/overlap_probe.py; tail -1 "$OUT/overlap.log" ;;
     fwdcprof) run fwdcprof 200 python tools/forward_cprof.py; head -c 4000 "$OUT/fwdcprof.log" ;;
     reduce) run reduce 200 python tools/reduce_bench.py; tail -1 "$OUT/reduce.log" ;;
     *) echo "unknown step $s" ;;

@@ -64,7 +64,8 @@ def _h2d_many(lists: Sequence[Sequence[int]], like: Tensor) -> List[Tensor]:
     """Several host int lists as int64 tensors on ``like``'s device in ONE asynchronous copy through a reused pinned
     buffer (``tmx::upload_i64``): a ``torch.tensor(..., device=cuda)`` copy from pageable memory waits for every
     kernel queued before it, and fresh pinned memory per call costs more than the copy."""
-    flat = torch.tensor([v for lst in lists for v in lst], dtype=torch.long)
+    # (np.fromiter over a chain: 2.6x a list comprehension + torch.tensor for 6K ints)
+    flat = torch.from_numpy(np.fromiter(itertools.chain.from_iterable(lists), dtype=np.int64, count=sum(map(len, lists))))
     if like.is_cuda and ops.load():
         flat = torch.ops.tmx.upload_i64(flat, like)
     else:
@@ -300,7 +301,18 @@ class MeanAveragePrecision(Metric):
                 for lst in (self.detection_labels, self.groundtruth_labels)
                 if len(lst)
             ]
-            uniq = torch.cat(parts).unique()
+            lab = torch.cat(parts)
+            if lab.is_cuda and ops.load():
+                # class ids in [0, 65536): a presence map (one scatter, one 64 KiB read) instead of torch.unique's sort +
+                # size synchronisation; the ids go back to the device through the pinned staging buffer
+                present = torch.zeros(_CLASS_MAP + 1, dtype=torch.uint8, device=lab.device)
+                present[torch.where((lab >= 0) & (lab < _CLASS_MAP), lab, _CLASS_MAP)] = 1
+                host = present.cpu().numpy()
+                if not host[-1]:
+                    ids = np.flatnonzero(host[:-1])
+                    self.__dict__["_classes_dev"] = torch.ops.tmx.upload_i64(torch.from_numpy(ids.astype(np.int64)), lab)
+                    return ids.tolist()
+            uniq = lab.unique()
             self.__dict__["_classes_dev"] = uniq  # the evaluator's sorted class ids, without a host round trip
             return uniq.cpu().tolist()
         self.__dict__["_classes_dev"] = None
@@ -910,6 +922,7 @@ def _flat_rows(lst: List[Tensor], n: int, dtype: torch.dtype, dev: torch.device,
 _BOXES, _SCORES, _LABELS = operator.itemgetter("boxes"), operator.itemgetter("scores"), operator.itemgetter("labels")
 
 
+_CLASS_MAP = 1 << 16  # class ids below this are found with a presence map (_get_classes)
 _PRED_KEYS, _PRED_WIDTHS = ("boxes", "scores", "labels"), (4, 0, 0)
 _GT_KEYS, _GT_WIDTHS = ("boxes", "labels", "iscrowd", "area"), (4, 0, -1, -1)  # (-1: optional 1-d column)
 

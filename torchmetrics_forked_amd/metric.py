@@ -510,6 +510,7 @@ class Metric(Module, ABC):
     def _fused_forward_begin(self) -> Tuple[Any, ...]:
         """First half of ``_forward_reduce_state_update``: park the global state (and deferred flags), start a
         fresh batch state; the caller then updates this metric (possibly through a fused collection kernel)."""
+        self._join_side_work()
         snap_def = None
         if self._deferred is not None:
             snap_def = self._deferred.take_for_forward()
@@ -846,7 +847,7 @@ class Metric(Module, ABC):
 
     def __getstate__(self) -> Dict[str, Any]:
         self._join_side_work()
-        return {k: v for k, v in self.__dict__.items() if k not in ("update", "compute", "_update_signature", "_hist_spare", "_batch_bufs", "_batch_sink", "_batch_view", "_fast_update", "_sum_fwd", "_sum_fwd_defaults", "_sum_fwd_scratch", "_sum_fwd_ptrs", "_tensor_states", "_owned_buf")}
+        return {k: v for k, v in self.__dict__.items() if k not in ("update", "compute", "_update_signature", "_hist_spare", "_batch_bufs", "_batch_sink", "_batch_view", "_fast_update", "_sum_fwd", "_sum_fwd_defaults", "_sum_fwd_scratch", "_sum_fwd_ptrs", "_tensor_states", "_owned_buf", "_lanes")}
 
     def __setstate__(self, state: Dict[str, Any]) -> None:
         self.__dict__.update(state)
@@ -953,6 +954,7 @@ class Metric(Module, ABC):
         unexpected_keys: List[str],
         error_msgs: List[str],
     ) -> None:
+        self._join_side_work()  # pending state work lands in the states being replaced, not in the loaded ones
         for key in self._defaults:
             name = prefix + key
             if name in state_dict:

@@ -141,7 +141,13 @@ class _MulticlassScoresPlan:
             d["_computed"] = None
             d["_update_count"] += 1
         if curve is not None:
-            curve._curve_update(preds, target, confmat_out=delta, err_flag=err)
+            # update lanes (side streams) only when no fold runs after the pass on the caller's stream
+            curve._curve_update(preds, target, confmat_out=delta, err_flag=err, lanes_ok=direct)
+            join = curve.__dict__.get("_side_event")
+            if join is not None:  # the confusion-matrix state is written on the curve's lanes: its consumers join them
+                for cm in confmats:
+                    if cm.__dict__.get("_side_event") is None:
+                        cm.__dict__["_side_event"] = join
         else:
             from torchmetrics_forked_amd.ops import classification as cls_ops
 

@@ -20,14 +20,15 @@ _NATIVE = (torch.float32, torch.float64, torch.int32, torch.int64)
 
 def _faster_than_aten(x: Tensor) -> bool:
     """Where the radix kernel beats ``torch.sort`` (one MI355X, ``SORT_BENCH_SWEEP=1 tools/sort_bench.py``,
-    ``profiles/sort_bench_r5.json``): row batches (2-3x) and rows of <= 4096 keys (one-workgroup kernel) always; one
-    long row of 32-bit keys from 262,144 keys on (1.16-1.8x; below that ATen's single-pass small sort is faster, 0.45-0.75x
-    at 8K-196K); one long row of int64 keys from 1M on (digit plan: 0.97x random, 2.3x for small-range ids); fp64 rows
-    never (0.4-0.94x: eight full passes against ATen's onesweep)."""
+    ``profiles/sort_bench_r5.json`` / ``_r6.json``): row batches (2.3-8.4x) and rows of <= 4096 keys (one-workgroup
+    kernel) always; one row of <= 8192 32-bit keys (the 1024-thread one-workgroup kernel, 1.09x); one long row of 32-bit
+    keys from 262,144 keys on (1.2-1.34x; between, the onesweep passes are latency-bound, 0.81-0.92x); one long row of
+    int64 keys from 1M on (digit plan: 0.8-0.97x random, 2.3x for small-range ids); fp64 rows never (0.57-0.95x: eight
+    full passes against ATen's onesweep)."""
     n = x.shape[-1]
     if x.dim() == 2 and x.shape[0] > 1:
         return True
-    if n <= 4096:
+    if n <= 4096 or (n <= 8192 and x.element_size() == 4):
         return True
     if x.element_size() == 4:
         return n >= 262_144

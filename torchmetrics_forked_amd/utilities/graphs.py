@@ -96,6 +96,8 @@ class GraphedUpdate:
             for _ in range(max(warmup, 1)):  # first updates may create lazy buffers / flags / compute groups
                 metric.update(*self._static_args, **self._static_kwargs)
         torch.cuda.current_stream(device).wait_stream(side)
+        for m in self._members:  # work the warm-up left on other streams (curve update lanes) lands before the roll-back
+            m._join_side_work()
 
         # the state tensors the warm-up left are the ones the graph accumulates into (a fresh collection may merge
         # its compute groups' states during its first update, so states can be rebound here, not during capture)
