@@ -62,7 +62,7 @@ def test_lanes_match_single_stream(c, monkeypatch):
         ref.update(p, t)
         got.update(p, t)
     assert torch.equal(ref.compute(), got.compute())
-    assert torch.equal(ref.state_dict()["score_hist"], got.state_dict()["score_hist"])
+    assert torch.equal(ref.metric_state["score_hist"], got.metric_state["score_hist"])
 
 
 def test_lanes_fused_collection_and_forward(monkeypatch):
@@ -99,7 +99,9 @@ def test_lanes_reset_and_reload(monkeypatch):
     mk = lambda: tm.MulticlassAveragePrecision(num_classes=c)  # noqa: E731
     ref = _run(mk, bs, False, monkeypatch)
     got = _run(mk, bs, True, monkeypatch)
-    sd = got.state_dict()
+    got.persistent(True)
+    ref.persistent(True)
+    sd = got.state_dict()  # joins the lanes: the saved histogram holds all three batches
     assert torch.equal(sd["score_hist"], ref.state_dict()["score_hist"])
     got.reset()
     ref.reset()
