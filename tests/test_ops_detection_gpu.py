@@ -245,6 +245,79 @@ def test_coco_evaluate_gpu_matches_host(cfg, score_dtype):
         assert torch.equal(hmap[key], dmap[key]), key
 
 
+@pytest.mark.parametrize("cfg", [
+    dict(seed=0, n_img=40, n_cls=6, max_det_img=30, max_gt_img=12, tie_scores=False, max_dets=[1, 10, 100]),
+    dict(seed=1, n_img=25, n_cls=3, max_det_img=260, max_gt_img=70, tie_scores=True, max_dets=[1, 10, 100]),
+    dict(seed=2, n_img=60, n_cls=10, max_det_img=15, max_gt_img=6, tie_scores=True, max_dets=[2, 5, 300]),
+    dict(seed=3, n_img=7, n_cls=2, max_det_img=0, max_gt_img=5, tie_scores=False, max_dets=[1, 10, 100]),
+    dict(seed=4, n_img=9, n_cls=2, max_det_img=12, max_gt_img=0, tie_scores=False, max_dets=[1, 10, 100]),
+    dict(seed=5, n_img=6, n_cls=4, max_det_img=256, max_gt_img=256, tie_scores=True, max_dets=[1, 10, 100]),
+])
+@pytest.mark.parametrize("score_dtype", [torch.float32, torch.bfloat16])
+def test_coco_evaluate_gpu_img_matches_host(cfg, score_dtype):
+    """Per-image route (one workgroup per image ranks, orders and matches its rows; csrc/coco_match.hip
+    coco_image_match_kernel) against the host evaluator: precision, recall and score tables bit-identical."""
+    from torchmetrics_forked_amd.detection.mean_ap import _AREA_RANGES
+
+    x = _coco_inputs(cfg["seed"], cfg["n_img"], cfg["n_cls"], cfg["max_det_img"], cfg["max_gt_img"], cfg["tie_scores"])
+    x["det_scores"] = x["det_scores"].to(score_dtype)
+    if x["det_scores"].numel() > 3:
+        x["det_scores"][:3] = torch.tensor([0.0, -0.0, 0.5], dtype=score_dtype)  # signed zeros tie
+    cats = torch.cat([x["det_labels"], x["gt_labels"]]).unique()
+    iou_thr = torch.linspace(0.5, 0.95, 10, dtype=torch.float64)
+    rec_thr = torch.linspace(0.0, 1.0, 101, dtype=torch.float64)
+    max_dets = torch.tensor(cfg["max_dets"], dtype=torch.long)
+    area = torch.tensor(_AREA_RANGES, dtype=torch.float64)
+    host = torch.ops.tmx.coco_evaluate(
+        x["det_boxes"], x["det_scores"].double(), x["det_labels"], x["det_img"], x["det_area"], x["gt_boxes"],
+        x["gt_labels"], x["gt_img"], x["gt_crowd"], x["gt_area"], cats, cfg["n_img"], iou_thr, rec_thr, max_dets, area,
+        None, None)
+    offs = lambda img: torch.cat([torch.zeros(1, dtype=torch.long),
+                                  torch.bincount(img, minlength=cfg["n_img"]).cumsum(0)])
+    c = lambda t: t.cuda()
+    dev = torch.ops.tmx.coco_evaluate_gpu_img(
+        c(x["det_boxes"]), c(x["det_scores"]), c(torch.searchsorted(cats, x["det_labels"])), c(x["det_area"]),
+        c(offs(x["det_img"])), c(x["gt_boxes"]), c(torch.searchsorted(cats, x["gt_labels"])), c(x["gt_crowd"]),
+        c(x["gt_area"]), c(offs(x["gt_img"])), cats.numel(), c(iou_thr), c(rec_thr), max_dets, c(area))
+    if cfg["max_det_img"] > 256:  # past the per-image LDS tables: flagged (the module then takes another route)
+        assert int(dev[3]) == 1 or x["det_img"].bincount().max() <= 256
+        return
+    assert int(dev[3]) == 0
+    for name, h, d in zip(("precision", "recall", "scores"), host[:3], dev[:3]):
+        assert torch.equal(h, d.cpu()), (name, (h - d.cpu()).abs().max())
+
+
+def test_map_module_img_route_equals_grid_route(monkeypatch):
+    """Module level, bbox, no extended summary: the per-image route and the (image, class)-grid route give identical
+    results (macro with class metrics, and micro)."""
+    import torchmetrics_forked_amd.detection.mean_ap as mod
+    from torchmetrics_forked_amd.detection import MeanAveragePrecision
+
+    g = torch.Generator().manual_seed(11)
+    preds, target = [], []
+    for _ in range(30):
+        ng = int(torch.randint(0, 25, (1,), generator=g))
+        gt = _boxes(ng, g) if ng else torch.zeros(0, 4)
+        nd = int(torch.randint(0, 140, (1,), generator=g))
+        det = (gt[torch.randint(0, ng, (nd,), generator=g)] if ng else _boxes(nd, g)) + torch.randn(nd, 4, generator=g) * 9
+        det[:, 2:] = torch.maximum(det[:, 2:], det[:, :2] + 1)
+        preds.append({"boxes": det, "scores": (torch.rand(nd, generator=g) * 32).floor() / 32,
+                      "labels": torch.randint(0, 7, (nd,), generator=g)})
+        target.append({"boxes": gt, "labels": torch.randint(0, 7, (ng,), generator=g),
+                       "iscrowd": (torch.rand(ng, generator=g) < 0.1).long()})
+    batch = _to((preds, target), "cuda")
+    for avg in ("macro", "micro"):
+        out = []
+        for route in (True, False):
+            monkeypatch.setattr(mod, "_IMG_ROUTE", route)
+            m = MeanAveragePrecision(class_metrics=True, average=avg).cuda()
+            m.warn_on_many_detections = False
+            m.update(*batch)
+            out.append(m.compute())
+        for k in out[1]:
+            torch.testing.assert_close(out[0][k].cpu(), out[1][k].cpu(), atol=0, rtol=0, msg=k)
+
+
 def test_map_module_gpu_many_dets_crowds_matches_cpu():
     """Module level: crowd ground truth, supplied areas, > max_det detections, extended summary and micro average."""
     from torchmetrics_forked_amd.detection import MeanAveragePrecision
@@ -350,3 +423,19 @@ def test_upload_i64_pinned_staging():
         outs.append((h, d))
     for h, d in outs:
         assert d.is_cuda and d.dtype == torch.long and torch.equal(d.cpu(), h)
+
+
+@pytest.mark.parametrize("labels", [[], [0], [3, 3, 1, 65535, 7, 1], list(range(0, 65536, 97)), [5, -1], [70000, 2]])
+def test_class_presence_bitmap_and_ids(labels):
+    """tmx::class_presence: the bitmap's set bits and the compacted device ids are torch.unique of the labels; a
+    label outside [0, 65536) sets the flag word."""
+    import numpy as np
+
+    lab = torch.tensor(labels, dtype=torch.long, device="cuda")
+    bm, ids = torch.ops.tmx.class_presence(lab)
+    words = bm.numpy().view(np.uint32)
+    inside = sorted({v for v in labels if 0 <= v < 65536})
+    assert bool(words[-1]) == any(not 0 <= v < 65536 for v in labels)
+    got = [32 * w + b for w in np.flatnonzero(words[:-1]) for b in range(32) if (int(words[w]) >> b) & 1]
+    assert got == inside
+    assert ids[: len(inside)].cpu().tolist() == inside

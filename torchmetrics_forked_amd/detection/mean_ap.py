@@ -19,6 +19,7 @@ is not one of the labels).
 """
 import itertools
 import json
+import os
 import operator
 from typing import ClassVar, Any, Dict, List, Literal, Optional, Sequence, Tuple, Union
 
@@ -303,14 +304,15 @@ class MeanAveragePrecision(Metric):
             ]
             lab = torch.cat(parts)
             if lab.is_cuda and ops.load():
-                # class ids in [0, 65536): a presence map (one scatter, one 64 KiB read) instead of torch.unique's sort +
-                # size synchronisation; the ids go back to the device through the pinned staging buffer
-                present = torch.zeros(_CLASS_MAP + 1, dtype=torch.uint8, device=lab.device)
-                present[torch.where((lab >= 0) & (lab < _CLASS_MAP), lab, _CLASS_MAP)] = 1
-                host = present.cpu().numpy()
-                if not host[-1]:
-                    ids = np.flatnonzero(host[:-1])
-                    self.__dict__["_classes_dev"] = torch.ops.tmx.upload_i64(torch.from_numpy(ids.astype(np.int64)), lab)
+                # class ids in [0, 65536): a presence bitmap (8 KiB read into pinned memory) and the present ids compacted
+                # on the device (tmx::class_presence) instead of torch.unique's sort + size synchronisation
+                bm, ids_dev = torch.ops.tmx.class_presence(lab)
+                words = bm.numpy().view(np.uint32)
+                if not words[-1]:
+                    nz = np.flatnonzero(words[:-1])
+                    bits = np.unpackbits(words[nz].view(np.uint8), bitorder="little").reshape(-1, 32).view(bool)
+                    ids = (nz[:, None] * 32 + np.arange(32))[bits]
+                    self.__dict__["_classes_dev"] = ids_dev[: ids.size]
                     return ids.tolist()
             uniq = lab.unique()
             self.__dict__["_classes_dev"] = uniq  # the evaluator's sorted class ids, without a host round trip
@@ -388,10 +390,16 @@ class MeanAveragePrecision(Metric):
         def flat(lst: List[Tensor], n: int, dtype: torch.dtype, width: int = 0) -> Tensor:
             return self._flat_cached(lst, n, dtype, dev, width)
 
-        det_sz, gt_sz = _h2d_many([det_sizes, gt_sizes], _first(self.detection_labels or self.groundtruth_labels))
         cats = self.__dict__.get("_classes_dev")
         if average != "micro" and (cats is None or cats.numel() != len(classes) or cats.device != dev):
             cats = torch.tensor(classes, dtype=torch.long, device=dev)
+        if (
+            i_type == "bbox" and "segm" not in self.iou_type and not self.extended_summary and _IMG_ROUTE
+            and len(det_sizes) == num_images and max(det_sizes, default=0) <= _IMG_ROUTE_ROWS
+            and max(gt_sizes, default=0) <= _IMG_ROUTE_ROWS and _score_dtype(self.detection_scores) == torch.float32
+        ):
+            return self._evaluate_gpu_img(average, classes, cats, det_sizes, gt_sizes, n_det, n_gt, flat)
+        det_sz, gt_sz = _h2d_many([det_sizes, gt_sizes], _first(self.detection_labels or self.groundtruth_labels))
         det_img = torch.repeat_interleave(torch.arange(len(det_sizes), device=dev), det_sz, output_size=n_det)
         gt_img = torch.repeat_interleave(torch.arange(num_images, device=dev), gt_sz, output_size=n_gt)
         det_labels = flat(self.detection_labels, n_det, torch.long)
@@ -446,6 +454,41 @@ class MeanAveragePrecision(Metric):
         if self.extended_summary:
             iou_values, iou_index = iou_values.cpu(), iou_index.cpu()
         return _EvalResult(prec, rec, iou_values, iou_index, cat_ids, num_images, overflow)
+
+    def _evaluate_gpu_img(self, average: str, classes: List[int], cats: Optional[Tensor], det_sizes: List[int],
+                          gt_sizes: List[int], n_det: int, n_gt: int, flat: Any) -> _EvalResult:
+        """bbox evaluation on the per-image route (``tmx::coco_evaluate_gpu_img``): one workgroup per image orders,
+        ranks and matches its own rows, so no global sort by (image, class), no (image, class) grid lookups and no
+        row gathers run before the accumulate step; the image offsets come from the host-held item sizes."""
+        like = _first(self.detection_labels or self.groundtruth_labels)
+        nd1 = len(det_sizes) + 1
+        off = np.fromiter(itertools.chain((0,), det_sizes, (0,), gt_sizes), dtype=np.int64, count=nd1 + len(gt_sizes) + 1)
+        np.cumsum(off[:nd1], out=off[:nd1])
+        np.cumsum(off[nd1:], out=off[nd1:])
+        off_t = torch.from_numpy(off)
+        off_t = torch.ops.tmx.upload_i64(off_t, like) if like.is_cuda and ops.load() else off_t.to(like.device)
+        det_labels = flat(self.detection_labels, n_det, torch.long)
+        gt_labels = flat(self.groundtruth_labels, n_gt, torch.long)
+        det_scores = flat(self.detection_scores, n_det, torch.float32)
+        gt_crowd = flat(self.groundtruth_crowds, n_gt, torch.long)
+        gt_area = flat(self.groundtruth_area, n_gt, torch.float64)
+        det_boxes = flat(self.detection_box, n_det, torch.float64, 4)
+        gt_boxes = flat(self.groundtruth_box, n_gt, torch.float64, 4)
+        if average == "micro":
+            cat_ids = [0] if classes else []
+            det_cls, gt_cls = torch.zeros_like(det_labels), torch.zeros_like(gt_labels)
+        else:
+            cat_ids = list(classes)
+            det_cls = torch.searchsorted(cats, det_labels)
+            gt_cls = torch.searchsorted(cats, gt_labels)
+        det_area = det_boxes[:, 2] * det_boxes[:, 3]
+        gt_area = torch.where(gt_area > 0, gt_area, gt_boxes[:, 2] * gt_boxes[:, 3])
+        prec, rec, _scores, overflow = torch.ops.tmx.coco_evaluate_gpu_img(
+            det_boxes, det_scores, det_cls, det_area, off_t[:nd1], gt_boxes, gt_cls, gt_crowd, gt_area, off_t[nd1:],
+            len(cat_ids), *self._eval_params(det_scores.device),
+        )
+        empty = torch.zeros(0, dtype=torch.float64)
+        return _EvalResult(prec, rec, empty, torch.zeros(0, 5, dtype=torch.long), cat_ids, len(gt_sizes), overflow)
 
     _param_cache: Optional[Tuple[Any, Tuple[Tensor, ...]]] = None
 
@@ -923,6 +966,10 @@ _BOXES, _SCORES, _LABELS = operator.itemgetter("boxes"), operator.itemgetter("sc
 
 
 _CLASS_MAP = 1 << 16  # class ids below this are found with a presence map (_get_classes)
+# bbox evaluation on the per-image route (tmx::coco_evaluate_gpu_img) when every image holds at most this many
+# detections and ground truths; TMX_MAP_IMG_ROUTE=0 keeps the (image, class)-grid evaluator
+_IMG_ROUTE_ROWS = 256
+_IMG_ROUTE = os.environ.get("TMX_MAP_IMG_ROUTE", "1") != "0"
 _PRED_KEYS, _PRED_WIDTHS = ("boxes", "scores", "labels"), (4, 0, 0)
 _GT_KEYS, _GT_WIDTHS = ("boxes", "labels", "iscrowd", "area"), (4, 0, -1, -1)  # (-1: optional 1-d column)
 
