@@ -294,9 +294,8 @@ __global__ __launch_bounds__(kImgThreads) void coco_image_match_kernel(
     const double* __restrict__ gbox, const int64_t* __restrict__ gcls, const int64_t* __restrict__ gcrowd,
     const double* __restrict__ garea, const double* __restrict__ iou_thr, int T, const double* __restrict__ area_rng,
     int A, int64_t max_det_last, int32_t* __restrict__ rank_out, uint64_t* __restrict__ matched_out,
-    uint64_t* __restrict__ ignored_out, int64_t* __restrict__ npig, int64_t* __restrict__ overflow) {
-  __shared__ uint32_t s_okey[kImgMaxRows];
-  __shared__ int32_t s_dcls[kImgMaxRows];
+    uint64_t* __restrict__ ignored_out, int64_t* __restrict__ overflow, int probe) {
+  __shared__ uint64_t s_dkey[kImgMaxRows];  // class << 32 | ~score key: ascending = (class, score desc)
   __shared__ int16_t s_dord[kImgMaxRows];  // image-local detection at each (class, score desc, row) position
   __shared__ int32_t s_gcls[kImgMaxRows];
   __shared__ int16_t s_gord[kImgMaxRows];  // image-local ground truth at each (class, row) position
@@ -319,8 +318,7 @@ __global__ __launch_bounds__(kImgThreads) void coco_image_match_kernel(
   }
   if (tid == 0) s_nrun = 0;
   for (int i = tid; i < nd; i += kImgThreads) {
-    s_okey[i] = coco_score_okey(dscore[d0 + i]);
-    s_dcls[i] = static_cast<int32_t>(dcls[d0 + i]);
+    s_dkey[i] = (static_cast<uint64_t>(dcls[d0 + i]) << 32) | static_cast<uint64_t>(~coco_score_okey(dscore[d0 + i]));
     const double* b = dbox + 4 * (d0 + i);
     s_dbox[i] = make_double4(b[0], b[1], b[2], b[3]);
     s_darea[i] = darea[d0 + i];
@@ -333,32 +331,16 @@ __global__ __launch_bounds__(kImgThreads) void coco_image_match_kernel(
     s_gcrowd[i] = gcrowd[g0 + i] != 0;
   }
   __syncthreads();
-  for (int i = tid; i < nd; i += kImgThreads) {  // (LDS broadcast reads: every lane reads entry j together)
-    const int ci = s_dcls[i];
-    const uint32_t ki = s_okey[i];
-    int below = 0, same = 0, cnt = 0;
+  // position of each detection in (class, score desc, row) order: one 64-bit key per row (class above the inverted
+  // score key), an all-pairs count with one LDS broadcast read per pair
+  for (int i = tid; i < nd && !(probe & 2); i += kImgThreads) {
+    const uint64_t ki = s_dkey[i];
+    int pos = 0;
     for (int j = 0; j < nd; ++j) {
-      const int cj = s_dcls[j];
-      const uint32_t kj = s_okey[j];
-      below += cj < ci;
-      cnt += cj == ci;
-      same += cj == ci && (kj > ki || (kj == ki && j < i));
+      const uint64_t kj = s_dkey[j];
+      pos += kj < ki || (kj == ki && j < i);
     }
-    s_dord[below + same] = static_cast<int16_t>(i);
-    if (same == 0) {  // head of its class run: the run's descriptor
-      int gb = 0, gc = 0;
-      for (int h = 0; h < ng; ++h) {
-        const int ch = s_gcls[h];
-        gb += ch < ci;
-        gc += ch == ci;
-      }
-      s_run[atomicAdd(&s_nrun, 1)] = make_int4(below, cnt, gb, gc);
-    }
-    rank_out[d0 + i] = same;
-    if (same >= max_det_last) {  // past maxDets[-1] in its pair: never matched nor accumulated
-      matched_out[d0 + i] = 0ull;
-      ignored_out[d0 + i] = 0ull;
-    }
+    s_dord[pos] = static_cast<int16_t>(i);
   }
   for (int g = tid; g < ng; g += kImgThreads) {
     const int cg = s_gcls[g];
@@ -368,10 +350,30 @@ __global__ __launch_bounds__(kImgThreads) void coco_image_match_kernel(
       pos += ch < cg || (ch == cg && h < g);
     }
     s_gord[pos] = static_cast<int16_t>(g);
-    if (!s_gcrowd[g]) {  // non-ignored ground truth per (class, area)
-      const double ar = s_garea[g];
-      for (int a = 0; a < A; ++a)
-        if (!(ar < area_rng[2 * a] || ar > area_rng[2 * a + 1])) atomic_add_i64(npig + static_cast<int64_t>(cg) * A + a, 1);
+  }
+  __syncthreads();
+  // rank within the (image, class) pair = distance to the class run's head; heads write the run descriptors
+  for (int p = tid; p < nd && !(probe & 2); p += kImgThreads) {
+    const int i = s_dord[p];
+    const uint32_t c = static_cast<uint32_t>(s_dkey[i] >> 32);
+    int head = p;
+    while (head > 0 && static_cast<uint32_t>(s_dkey[s_dord[head - 1]] >> 32) == c) --head;
+    const int rk = p - head;
+    if (rk == 0) {
+      int cnt = 1;
+      while (p + cnt < nd && static_cast<uint32_t>(s_dkey[s_dord[p + cnt]] >> 32) == c) ++cnt;
+      int gb = 0, gc = 0;
+      for (int h = 0; h < ng; ++h) {
+        const uint32_t ch = static_cast<uint32_t>(s_gcls[h]);
+        gb += ch < c;
+        gc += ch == c;
+      }
+      s_run[atomicAdd(&s_nrun, 1)] = make_int4(p, cnt, gb, gc);
+    }
+    rank_out[d0 + i] = rk;
+    if (rk >= max_det_last) {  // past maxDets[-1] in its pair: never matched nor accumulated
+      matched_out[d0 + i] = 0ull;
+      ignored_out[d0 + i] = 0ull;
     }
   }
   __syncthreads();
@@ -426,8 +428,39 @@ __global__ __launch_bounds__(kImgThreads) void coco_image_match_kernel(
       }
     }
   };
-  const int nrun = s_nrun;
+  const int nrun = (probe & 4) ? 0 : s_nrun;
   for (int r = wave; r < nrun; r += kImgWaves) match_run(s_run[r]);
+}
+
+// non-ignored ground truth per (class, area): npig[k * A + a].  Each workgroup counts into LDS (K * A <= 8192 bins)
+// and flushes its non-zero bins (a global atomic per ground truth serialises on the few hot bins of COCO-80 data)
+constexpr int kNpigLdsBins = 8192;
+
+__global__ __launch_bounds__(256) void coco_npig_kernel(const int64_t* __restrict__ gcls, const int64_t* __restrict__ gcrowd,
+                                                        const double* __restrict__ garea, int64_t n,
+                                                        const double* __restrict__ area_rng, int A, int bins, bool lds,
+                                                        int64_t* __restrict__ npig) {
+  extern __shared__ unsigned np_lds[];
+  if (lds) {
+    for (int b = threadIdx.x; b < bins; b += blockDim.x) np_lds[b] = 0u;
+    __syncthreads();
+  }
+  for (int64_t g = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; g < n;
+       g += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    if (gcrowd[g] != 0) continue;
+    const double ar = garea[g];
+    const int64_t base = gcls[g] * A;
+    for (int a = 0; a < A; ++a) {
+      if (ar < area_rng[2 * a] || ar > area_rng[2 * a + 1]) continue;
+      if (lds) atomicAdd(np_lds + base + a, 1u);
+      else atomic_add_i64(npig + base + a, 1);
+    }
+  }
+  if (lds) {
+    __syncthreads();
+    for (int b = threadIdx.x; b < bins; b += blockDim.x)
+      if (np_lds[b]) atomic_add_i64(npig + b, static_cast<long long>(np_lds[b]));
+  }
 }
 
 // step 3's arrays in accumulate order (one launch for the four gathers) and the class segment starts seg[K + 1]
@@ -775,13 +808,25 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> coco_evaluate_gpu_img
   uint64_t* a_ignored = reinterpret_cast<uint64_t*>(w + 5 * n);
   int64_t* seg = w + 6 * n;
   auto a_score = at::empty({n}, fopt);
+  // TMX_COCO_IMG_PROBE (timing probe only, tools/coco_img_probe.py; wrong tables): bit 0 skips the ground-truth
+  // counts, bit 1 the rank pass, bit 2 the matching
+  const char* probe_env = std::getenv("TMX_COCO_IMG_PROBE");
+  const int probe = probe_env != nullptr ? std::atoi(probe_env) : 0;
   if (I > 0) {
     coco_image_match_kernel<<<static_cast<unsigned>(I), kImgThreads, 0, stream()>>>(
         det_off.data_ptr<int64_t>(), gt_off.data_ptr<int64_t>(), det_boxes.data_ptr<double>(), score32.data_ptr<float>(),
         det_cls.data_ptr<int64_t>(), det_area.data_ptr<double>(), gt_boxes.data_ptr<double>(), gt_cls.data_ptr<int64_t>(),
         gt_crowd.data_ptr<int64_t>(), gt_area.data_ptr<double>(), iou_thrs.data_ptr<double>(), static_cast<int>(T),
-        area_rng.data_ptr<double>(), static_cast<int>(A), max_det_last, rank, matched, ignored, npig.data_ptr<int64_t>(),
-        overflow.data_ptr<int64_t>());
+        area_rng.data_ptr<double>(), static_cast<int>(A), max_det_last, rank, matched, ignored, overflow.data_ptr<int64_t>(), probe);
+    TMX_LAUNCH_CHECK();
+  }
+  const int64_t n_gt = gt_cls.numel();
+  if (n_gt > 0 && !(probe & 1)) {
+    const bool lds = K * A <= kNpigLdsBins;
+    const int blocks = static_cast<int>(std::min<int64_t>((n_gt + 511) / 512, 256));
+    coco_npig_kernel<<<blocks, 256, lds ? sizeof(unsigned) * K * A : 0, stream()>>>(
+        gt_cls.data_ptr<int64_t>(), gt_crowd.data_ptr<int64_t>(), gt_area.data_ptr<double>(), n_gt,
+        area_rng.data_ptr<double>(), static_cast<int>(A), static_cast<int>(K * A), lds, npig.data_ptr<int64_t>());
     TMX_LAUNCH_CHECK();
   }
   if (n == 0) {

@@ -1,0 +1,8 @@
+# per-image COCO route: detection GPU tests, op-part probe, mAP bench (each step time-limited)
+set -u
+cd "$GRAFT_REPO_ROOT"; O=gpurun_out/${1:-r7e}; mkdir -p $O; export TMPDIR=/tmp
+timeout -k 10 300 python -u -m pytest tests/test_ops_detection_gpu.py -x -q --timeout 120 --timeout-method thread > $O/det.log 2>&1; rc=$?; tail -1 $O/det.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 200 python -u tools/coco_img_probe.py > $O/probe.log 2>&1 || exit $?
+tail -n 1 $O/probe.log
+timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $O/prof -o p --output-format csv -- python3 tools/coco_img_probe.py > $O/prof.log 2>&1 || exit $?
+for i in 1 2; do timeout -k 10 300 python bench.py --config map --steps 5 --warmup 1 > $O/mapbench_$i.log 2>&1 || exit $?; tail -n 1 $O/mapbench_$i.log | cut -c1-60; done
