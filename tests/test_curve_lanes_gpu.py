@@ -39,7 +39,7 @@ def _run(make, batches, lanes, monkeypatch, after=None):
     return m
 
 
-@pytest.mark.parametrize("c", [512, 1000])
+@pytest.mark.parametrize("c", [2, 10, 64, 100, 256, 512, 1000, 1001])  # small-class, tile and odd-width routes
 def test_lanes_match_single_stream(c, monkeypatch):
     n = (1 << 22) // c + 64
     bs = _batches(n, c, 5, seed=c, probs_at=(3,))
