@@ -46,7 +46,10 @@ def test_lanes_match_single_stream(c, monkeypatch):
     mk = lambda: tm.MulticlassAUROC(num_classes=c)  # noqa: E731
     ref = _run(mk, bs, False, monkeypatch)
     got = _run(mk, bs, True, monkeypatch)
-    assert "_lanes" in got.__dict__ and got.__dict__["_lanes"].dirty  # lane 1 holds batches 2 and 4
+    if c < prc._LANE_MIN_CLASSES:  # small-class route: single stream
+        assert got.__dict__.get("_lanes") is None
+    else:
+        assert "_lanes" in got.__dict__ and got.__dict__["_lanes"].dirty  # lane 1 holds batches 2 and 4
     a_ref, a_got = ref.compute(), got.compute()
     assert torch.equal(a_ref, a_got)
     assert torch.equal(ref.metric_state["score_hist"], got.metric_state["score_hist"])

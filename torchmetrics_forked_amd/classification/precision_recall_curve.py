@@ -49,6 +49,9 @@ _SYNC_FREE = os.environ.get("TMX_CURVE_SYNC_FREE", "0") not in ("", "0")
 # update lanes (multiclass exact histogram on the GPU, see _CurveMetric._lane_update): on unless TMX_CURVE_LANES=0
 _LANES_ON = os.environ.get("TMX_CURVE_LANES", "1") != "0"
 _LANE_MIN_ELEMS = 1 << 22  # smaller batches: stream hand-offs cost more than the overlap gains
+# the small-class route (C <= 256: one-lane / few-lane rows, csrc/classification.hip) gains nothing from the lanes and
+# pays their host hand-offs: C = 10 x 1M 0.060 vs 0.040 ms, C = 64 x 1M 0.161 vs 0.149 (gpurun r7l, tools/gpu_r7f.sh)
+_LANE_MIN_CLASSES = 257
 _LANE_MAX_HIST_BYTES = 4 << 30  # the second lane's histogram (2 C 16384 int64) is allocated only up to this size
 
 
@@ -324,6 +327,7 @@ class _CurveMetric(Metric):
     def _lanes_for(self, p: Tensor, hist: Tensor, rng: Optional[Tensor], batch: Any, lanes_ok: bool) -> Optional[_Lanes]:
         if not (
             _LANES_ON and lanes_ok and batch is None and rng is not None and hist.is_cuda and p.numel() >= _LANE_MIN_ELEMS
+            and p.shape[-1] >= _LANE_MIN_CLASSES
             and hist.numel() * 8 <= _LANE_MAX_HIST_BYTES and self._range_hist is hist
             and not torch.cuda.is_current_stream_capturing()
         ):
@@ -424,7 +428,7 @@ class _CurveMetric(Metric):
         if multiclass:
             if preds.ndim != 2 or target.ndim != 1 or preds.shape[0] != target.shape[0] or preds.shape[1] != self._num:
                 return False
-            if _LANES_ON and preds.numel() >= _LANE_MIN_ELEMS:
+            if _LANES_ON and preds.numel() >= _LANE_MIN_ELEMS and preds.shape[1] >= _LANE_MIN_CLASSES:
                 return False  # the update lanes take it (_lane_update)
         if d.get("_side_event") is not None:
             self._join_side_work()
