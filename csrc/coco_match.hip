@@ -29,6 +29,7 @@
 // <= 256 recall thresholds.
 #include "common.h"
 
+#include <algorithm>
 #include <limits>
 
 namespace tmx {
@@ -178,7 +179,15 @@ __global__ __launch_bounds__(1024) void coco_accumulate_kernel(
   const int a = static_cast<int>(q % A); q /= A;
   const int k = static_cast<int>(q);
   const int64_t npig = npig_all[k * A + a];
-  if (npig == 0) return;  // stays -1 (no ground truth for this class / area); (k, a) is workgroup-uniform
+  if (npig == 0) {  // no ground truth for this class / area: -1 everywhere ((k, a) is workgroup-uniform)
+    for (int r = lane; r < R; r += kWave) {
+      const int64_t idx = (((static_cast<int64_t>(t) * R + r) * K + k) * A + a) * M + m;
+      prec_out[idx] = -1.0;
+      score_out[idx] = -1.0;
+    }
+    if (lane == 0) rec_out[((static_cast<int64_t>(t) * K + k) * A + a) * M + m] = -1.0;
+    return;
+  }
   const int64_t s = seg[k], e = seg[k + 1];
   const int bit = t * A + a;
   const int64_t maxd = max_dets[m];
@@ -321,13 +330,14 @@ __global__ __launch_bounds__(kImgThreads) void coco_image_match_kernel(
     s_dkey[i] = (static_cast<uint64_t>(dcls[d0 + i]) << 32) | static_cast<uint64_t>(~coco_score_okey(dscore[d0 + i]));
     const double* b = dbox + 4 * (d0 + i);
     s_dbox[i] = make_double4(b[0], b[1], b[2], b[3]);
-    s_darea[i] = darea[d0 + i];
+    s_darea[i] = b[2] * b[3];  // (bbox route: the detection's area is its box area)
   }
   for (int i = tid; i < ng; i += kImgThreads) {
     s_gcls[i] = static_cast<int32_t>(gcls[g0 + i]);
     const double* b = gbox + 4 * (g0 + i);
     s_gbox[i] = make_double4(b[0], b[1], b[2], b[3]);
-    s_garea[i] = garea[g0 + i];
+    const double ga = garea[g0 + i];
+    s_garea[i] = ga > 0 ? ga : b[2] * b[3];  // supplied area, else the box's
     s_gcrowd[i] = gcrowd[g0 + i] != 0;
   }
   __syncthreads();
@@ -437,7 +447,7 @@ __global__ __launch_bounds__(kImgThreads) void coco_image_match_kernel(
 constexpr int kNpigLdsBins = 8192;
 
 __global__ __launch_bounds__(256) void coco_npig_kernel(const int64_t* __restrict__ gcls, const int64_t* __restrict__ gcrowd,
-                                                        const double* __restrict__ garea, int64_t n,
+                                                        const double* __restrict__ garea, const double* __restrict__ gbox, int64_t n,
                                                         const double* __restrict__ area_rng, int A, int bins, bool lds,
                                                         int64_t* __restrict__ npig) {
   extern __shared__ unsigned np_lds[];
@@ -448,7 +458,8 @@ __global__ __launch_bounds__(256) void coco_npig_kernel(const int64_t* __restric
   for (int64_t g = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; g < n;
        g += static_cast<int64_t>(gridDim.x) * blockDim.x) {
     if (gcrowd[g] != 0) continue;
-    const double ar = garea[g];
+    const double ga = garea[g];
+    const double ar = ga > 0 ? ga : gbox[4 * g + 2] * gbox[4 * g + 3];
     const int64_t base = gcls[g] * A;
     for (int a = 0; a < A; ++a) {
       if (ar < area_rng[2 * a] || ar > area_rng[2 * a + 1]) continue;
@@ -613,9 +624,10 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tenso
   const auto max_dets = max_dets_cpu.clamp_max(max_det_last).to(dev);
   const bool custom = img_iou_.has_value() && img_iou_->defined();
 
-  auto precision = at::full({T, R, K, A, M}, -1.0, det_scores.options());
-  auto recall = at::full({T, K, A, M}, -1.0, det_scores.options());
-  auto scores_out = at::full({T, R, K, A, M}, -1.0, det_scores.options());
+  // every entry is written by the accumulate kernel (-1 where a class / area has no ground truth)
+  auto precision = at::empty({T, R, K, A, M}, det_scores.options());
+  auto recall = at::empty({T, K, A, M}, det_scores.options());
+  auto scores_out = at::empty({T, R, K, A, M}, det_scores.options());
   auto lopt = det_cls.options();
   auto overflow = at::zeros({1}, lopt);
   if (K == 0) return {precision, recall, scores_out, at::zeros({0}, det_scores.options()), at::zeros({0, 5}, lopt), overflow};
@@ -759,10 +771,10 @@ std::tuple<at::Tensor, at::Tensor> class_presence(const at::Tensor& labels) {
 // tables as coco_evaluate_gpu, plus a device flag (output 4) set when an image holds more rows than that (the tables
 // are then invalid).
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> coco_evaluate_gpu_img(
-    const at::Tensor& det_boxes_, const at::Tensor& det_scores_, const at::Tensor& det_cls_, const at::Tensor& det_area_,
-    const at::Tensor& det_off_, const at::Tensor& gt_boxes_, const at::Tensor& gt_cls_, const at::Tensor& gt_crowd_,
-    const at::Tensor& gt_area_, const at::Tensor& gt_off_, int64_t K, const at::Tensor& iou_thrs_,
-    const at::Tensor& rec_thrs_, const at::Tensor& max_dets_, const at::Tensor& area_rng_) {
+    const at::Tensor& det_boxes_, const at::Tensor& det_scores_, const at::Tensor& det_cls_, const at::Tensor& det_off_,
+    const at::Tensor& gt_boxes_, const at::Tensor& gt_cls_, const at::Tensor& gt_crowd_, const at::Tensor& gt_area_,
+    const at::Tensor& gt_off_, int64_t K, const at::Tensor& iou_thrs_, const at::Tensor& rec_thrs_,
+    const at::Tensor& max_dets_, const c10::optional<at::Tensor>& max_dets_dev_, const at::Tensor& area_rng_) {
   TORCH_CHECK(det_scores_.is_cuda(), "coco_evaluate_gpu_img: expected GPU tensors");
   const auto st = det_scores_.scalar_type();
   TORCH_CHECK(st == at::kFloat || st == at::kHalf || st == at::kBFloat16, "coco_evaluate_gpu_img: fp32-exact scores only");
@@ -770,7 +782,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> coco_evaluate_gpu_img
   const auto dev = det_scores_.device();
   auto f64 = [&](const at::Tensor& t) { return t.to(dev, at::kDouble).contiguous(); };
   auto i64 = [&](const at::Tensor& t) { return t.to(dev, at::kLong).contiguous(); };
-  const auto det_boxes = f64(det_boxes_).reshape({-1, 4}), det_area = f64(det_area_);
+  const auto det_boxes = f64(det_boxes_).reshape({-1, 4});
   const auto gt_boxes = f64(gt_boxes_).reshape({-1, 4}), gt_area = f64(gt_area_);
   const auto det_cls = i64(det_cls_), gt_cls = i64(gt_cls_), gt_crowd = i64(gt_crowd_);
   const auto det_off = i64(det_off_), gt_off = i64(gt_off_);
@@ -783,16 +795,22 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> coco_evaluate_gpu_img
   TORCH_CHECK(T * A <= 64, "coco_evaluate_gpu_img: at most 64 (IoU threshold, area range) combinations");
   TORCH_CHECK(R <= kCocoMaxRec, "coco_evaluate_gpu_img: at most ", kCocoMaxRec, " recall thresholds");
   TORCH_CHECK(I >= 0 && gt_off.numel() == I + 1, "coco_evaluate_gpu_img: det_off / gt_off must both hold I + 1 offsets");
-  TORCH_CHECK(det_boxes.size(0) == n && score32.numel() == n && det_area.numel() == n,
+  TORCH_CHECK(det_boxes.size(0) == n && score32.numel() == n,
               "coco_evaluate_gpu_img: detection columns differ in length");
   TORCH_CHECK(gt_boxes.size(0) == gt_cls.numel() && gt_crowd.numel() == gt_cls.numel() && gt_area.numel() == gt_cls.numel(),
               "coco_evaluate_gpu_img: ground-truth columns differ in length");
   const int64_t max_det_last = max_dets_cpu.data_ptr<int64_t>()[M - 1];
-  const auto max_dets = max_dets_cpu.clamp_max(max_det_last).to(dev);
+  // (a device copy of the thresholds from the caller's cache avoids a pageable host-to-device copy per call; the
+  // clamp to maxDets[-1] is the identity for the sorted thresholds the module passes)
+  const bool dev_md = max_dets_dev_.has_value() && max_dets_dev_->defined() && max_dets_dev_->is_cuda() &&
+                      max_dets_dev_->scalar_type() == at::kLong && max_dets_dev_->numel() == M &&
+                      std::is_sorted(max_dets_cpu.data_ptr<int64_t>(), max_dets_cpu.data_ptr<int64_t>() + M);
+  const auto max_dets = dev_md ? max_dets_dev_->contiguous() : max_dets_cpu.clamp_max(max_det_last).to(dev);
   const auto fopt = det_boxes.options();
-  auto precision = at::full({T, R, K, A, M}, -1.0, fopt);
-  auto recall = at::full({T, K, A, M}, -1.0, fopt);
-  auto scores_out = at::full({T, R, K, A, M}, -1.0, fopt);
+  // every entry is written by the accumulate kernel (-1 where a class / area has no ground truth)
+  auto precision = at::empty({T, R, K, A, M}, fopt);
+  auto recall = at::empty({T, K, A, M}, fopt);
+  auto scores_out = at::empty({T, R, K, A, M}, fopt);
   const auto lopt = det_cls.options();
   auto overflow = at::zeros({1}, lopt);
   if (K == 0) return {precision, recall, scores_out, overflow};
@@ -815,7 +833,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> coco_evaluate_gpu_img
   if (I > 0) {
     coco_image_match_kernel<<<static_cast<unsigned>(I), kImgThreads, 0, stream()>>>(
         det_off.data_ptr<int64_t>(), gt_off.data_ptr<int64_t>(), det_boxes.data_ptr<double>(), score32.data_ptr<float>(),
-        det_cls.data_ptr<int64_t>(), det_area.data_ptr<double>(), gt_boxes.data_ptr<double>(), gt_cls.data_ptr<int64_t>(),
+        det_cls.data_ptr<int64_t>(), nullptr, gt_boxes.data_ptr<double>(), gt_cls.data_ptr<int64_t>(),
         gt_crowd.data_ptr<int64_t>(), gt_area.data_ptr<double>(), iou_thrs.data_ptr<double>(), static_cast<int>(T),
         area_rng.data_ptr<double>(), static_cast<int>(A), max_det_last, rank, matched, ignored, overflow.data_ptr<int64_t>(), probe);
     TMX_LAUNCH_CHECK();
@@ -825,7 +843,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> coco_evaluate_gpu_img
     const bool lds = K * A <= kNpigLdsBins;
     const int blocks = static_cast<int>(std::min<int64_t>((n_gt + 511) / 512, 256));
     coco_npig_kernel<<<blocks, 256, lds ? sizeof(unsigned) * K * A : 0, stream()>>>(
-        gt_cls.data_ptr<int64_t>(), gt_crowd.data_ptr<int64_t>(), gt_area.data_ptr<double>(), n_gt,
+        gt_cls.data_ptr<int64_t>(), gt_crowd.data_ptr<int64_t>(), gt_area.data_ptr<double>(), gt_boxes.data_ptr<double>(), n_gt,
         area_rng.data_ptr<double>(), static_cast<int>(A), static_cast<int>(K * A), lds, npig.data_ptr<int64_t>());
     TMX_LAUNCH_CHECK();
   }
@@ -857,9 +875,9 @@ TORCH_LIBRARY_FRAGMENT(tmx, m) {
       "Tensor? img_iou_offsets, Tensor? det_local, Tensor? gt_local, Tensor? img_ng, bool export_iou) "
       "-> (Tensor, Tensor, Tensor, Tensor, Tensor, Tensor)");
   m.def(
-      "coco_evaluate_gpu_img(Tensor det_boxes, Tensor det_scores, Tensor det_cls, Tensor det_area, Tensor det_off, "
+      "coco_evaluate_gpu_img(Tensor det_boxes, Tensor det_scores, Tensor det_cls, Tensor det_off, "
       "Tensor gt_boxes, Tensor gt_cls, Tensor gt_crowd, Tensor gt_area, Tensor gt_off, int num_classes, "
-      "Tensor iou_thrs, Tensor rec_thrs, Tensor max_dets, Tensor area_rng) -> (Tensor, Tensor, Tensor, Tensor)");
+      "Tensor iou_thrs, Tensor rec_thrs, Tensor max_dets, Tensor? max_dets_dev, Tensor area_rng) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("class_presence(Tensor labels) -> (Tensor, Tensor)");
 }
 

@@ -22,11 +22,11 @@ det = torch.cat([gt + torch.randn(I, G, 4, device=dev, generator=g) * 6,
                  torch.cat([torch.rand(I, D - G, 2, device=dev, generator=g) * 500,
                             torch.rand(I, D - G, 2, device=dev, generator=g) * 150 + 4], -1)], 1).abs() + 1
 args = (det.reshape(-1, 4).double(), torch.rand(I * D, device=dev, generator=g), torch.randint(0, K, (I * D,), device=dev, generator=g),
-        (det[..., 2] * det[..., 3]).reshape(-1).double(), torch.arange(0, I * D + 1, D, device=dev),
+        torch.arange(0, I * D + 1, D, device=dev),
         gt.reshape(-1, 4).double(), torch.randint(0, K, (I * G,), device=dev, generator=g), torch.zeros(I * G, dtype=torch.long, device=dev),
         (gt[..., 2] * gt[..., 3]).reshape(-1).double(), torch.arange(0, I * G + 1, G, device=dev), K,
         torch.linspace(0.5, 0.95, 10, dtype=torch.float64, device=dev), torch.linspace(0, 1, 101, dtype=torch.float64, device=dev),
-        torch.tensor([1, 10, 100]), torch.tensor(_AREA_RANGES, dtype=torch.float64, device=dev))
+        torch.tensor([1, 10, 100]), torch.tensor([1, 10, 100], device=dev), torch.tensor(_AREA_RANGES, dtype=torch.float64, device=dev))
 
 
 def med_us(reps=15):

@@ -481,11 +481,11 @@ class MeanAveragePrecision(Metric):
             cat_ids = list(classes)
             det_cls = torch.searchsorted(cats, det_labels)
             gt_cls = torch.searchsorted(cats, gt_labels)
-        det_area = det_boxes[:, 2] * det_boxes[:, 3]
-        gt_area = torch.where(gt_area > 0, gt_area, gt_boxes[:, 2] * gt_boxes[:, 3])
+        # (areas: the kernel takes box areas for detections and the supplied ground-truth area where > 0, else the box's)
+        iou_thr, rec_thr, max_dets, area_rng = self._eval_params(det_scores.device)
         prec, rec, _scores, overflow = torch.ops.tmx.coco_evaluate_gpu_img(
-            det_boxes, det_scores, det_cls, det_area, off_t[:nd1], gt_boxes, gt_cls, gt_crowd, gt_area, off_t[nd1:],
-            len(cat_ids), *self._eval_params(det_scores.device),
+            det_boxes, det_scores, det_cls, off_t[:nd1], gt_boxes, gt_cls, gt_crowd, gt_area, off_t[nd1:],
+            len(cat_ids), iou_thr, rec_thr, max_dets, self._param_cache[2], area_rng,
         )
         empty = torch.zeros(0, dtype=torch.float64)
         return _EvalResult(prec, rec, empty, torch.zeros(0, 5, dtype=torch.long), cat_ids, len(gt_sizes), overflow)
@@ -498,12 +498,13 @@ class MeanAveragePrecision(Metric):
         key = (str(dev), tuple(self.iou_thresholds), tuple(self.rec_thresholds), tuple(self.max_detection_thresholds))
         cached = self._param_cache
         if cached is None or cached[0] != key:
+            md = torch.tensor(self.max_detection_thresholds, dtype=torch.long)
             cached = self._param_cache = (key, (
                 torch.tensor(self.iou_thresholds, dtype=torch.float64, device=dev),
                 torch.tensor(self.rec_thresholds, dtype=torch.float64, device=dev),
-                torch.tensor(self.max_detection_thresholds, dtype=torch.long),
+                md,
                 torch.tensor(_AREA_RANGES, dtype=torch.float64, device=dev),
-            ))
+            ), md.to(dev))  # (+ a device copy of the thresholds for the per-image route)
         return cached[1]
 
     def _evaluate_host(self, i_type: str, average: str, classes: List[int]) -> _EvalResult:
