@@ -544,6 +544,31 @@ __global__ __launch_bounds__(1024) void class_compact_kernel(const uint32_t* __r
   }
 }
 
+// COCO summary tables for MeanAveragePrecision._summarize_tables: per (t, k, a, m) cell the sum and count of the valid
+// (> -1) precisions over the recall thresholds, and the recall with its validity -- [4][T][K][A][M] fp64 -- plus the
+// evaluator's overflow flag as the last word: one launch and one copy into pinned memory instead of ~10 ATen ops.
+__global__ void coco_summary_kernel(const double* __restrict__ prec, const double* __restrict__ rec, int64_t T, int64_t kam,
+                                    int R, const int64_t* __restrict__ overflow, double* __restrict__ out) {
+  const int64_t cells = T * kam;
+  const int64_t c = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (c == 0) out[4 * cells] = overflow != nullptr ? static_cast<double>(overflow[0]) : 0.0;
+  if (c >= cells) return;
+  const int64_t t = c / kam, j = c % kam;
+  double s = 0.0, n = 0.0;
+  for (int r = 0; r < R; ++r) {
+    const double p = prec[(t * R + r) * kam + j];
+    if (p > -1) {
+      s += p;
+      n += 1.0;
+    }
+  }
+  const double rv = rec[c];
+  out[c] = s;
+  out[cells + c] = n;
+  out[2 * cells + c] = rv > -1 ? rv : 0.0;
+  out[3 * cells + c] = rv > -1 ? 1.0 : 0.0;
+}
+
 // ------------------------------------------------------------------------------------------------ host side
 namespace {
 
@@ -742,6 +767,29 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tenso
   return {precision, recall, scores_out, iou_values, iou_index, overflow};
 }
 
+// precision [T, R, K, A, M], recall [T, K, A, M] (fp64, device) -> host (pinned) fp64 [4 T K A M + 1]: the summary
+// tables, then the overflow flag (0 without one); synchronises the stream (the caller reads the result at once)
+at::Tensor coco_summary_tables(const at::Tensor& precision, const at::Tensor& recall, const c10::optional<at::Tensor>& overflow) {
+  TORCH_CHECK(precision.is_cuda() && precision.dim() == 5 && recall.dim() == 4, "coco_summary_tables: expected GPU [T,R,K,A,M] / [T,K,A,M]");
+  const c10::DeviceGuard guard(precision.device());
+  const auto p = precision.to(at::kDouble).contiguous(), r = recall.to(at::kDouble).contiguous();
+  const int64_t T = p.size(0), R = p.size(1), kam = p.size(2) * p.size(3) * p.size(4);
+  TORCH_CHECK(r.numel() == T * kam, "coco_summary_tables: recall does not match precision");
+  const int64_t cells = T * kam;
+  auto dev_out = at::empty({4 * cells + 1}, p.options());
+  const bool has_ov = overflow.has_value() && overflow->defined();
+  const auto ov = has_ov ? overflow->to(at::kLong).contiguous() : at::Tensor();
+  coco_summary_kernel<<<static_cast<unsigned>(std::max<int64_t>(1, (cells + 255) / 256)), 256, 0, stream()>>>(
+      p.data_ptr<double>(), r.data_ptr<double>(), T, kam, static_cast<int>(R), has_ov ? ov.data_ptr<int64_t>() : nullptr,
+      dev_out.data_ptr<double>());
+  TMX_LAUNCH_CHECK();
+  auto host = at::empty({4 * cells + 1}, at::TensorOptions().dtype(at::kDouble).pinned_memory(true));
+  TMX_CHECK_HIP(hipMemcpyAsync(host.data_ptr<double>(), dev_out.data_ptr<double>(), sizeof(double) * (4 * cells + 1),
+                               hipMemcpyDeviceToHost, stream()));
+  TMX_CHECK_HIP(hipStreamSynchronize(stream()));
+  return host;
+}
+
 // (host bitmap [kClassWords + 1] int32 in pinned memory, read after this op's stream synchronisation; device ids
 // [32 * kClassWords] int64 whose first popcount(bitmap) entries are the present ids, ascending)
 std::tuple<at::Tensor, at::Tensor> class_presence(const at::Tensor& labels) {
@@ -879,10 +927,12 @@ TORCH_LIBRARY_FRAGMENT(tmx, m) {
       "Tensor gt_boxes, Tensor gt_cls, Tensor gt_crowd, Tensor gt_area, Tensor gt_off, int num_classes, "
       "Tensor iou_thrs, Tensor rec_thrs, Tensor max_dets, Tensor? max_dets_dev, Tensor area_rng) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("class_presence(Tensor labels) -> (Tensor, Tensor)");
+  m.def("coco_summary_tables(Tensor precision, Tensor recall, Tensor? overflow) -> Tensor");
 }
 
 TORCH_LIBRARY_IMPL(tmx, CUDA, m) {
   m.impl("coco_evaluate_gpu", &tmx::coco_evaluate_gpu);
   m.impl("coco_evaluate_gpu_img", &tmx::coco_evaluate_gpu_img);
   m.impl("class_presence", &tmx::class_presence);
+  m.impl("coco_summary_tables", &tmx::coco_summary_tables);
 }

@@ -707,6 +707,12 @@ class MeanAveragePrecision(Metric):
         """Sums and counts of the valid (``> -1``) entries of ``precision [T,R,K,A,M]`` (summed over R) and ``recall
         [T,K,A,M]``, as one host array ``[4, T, K, A, M]``: a few reductions where the tables live (the device, for the
         GPU evaluator) and ONE small copy, instead of copying both tables and slicing them twelve times per summary."""
+        if precision.is_cuda and precision.dim() == 5 and ops.load():  # one kernel + one pinned copy (tmx::coco_summary_tables)
+            both = torch.ops.tmx.coco_summary_tables(precision, recall, overflow).numpy()
+            if both[-1] != 0:
+                return None
+            t, _, k, a, m = precision.shape
+            return both[:-1].reshape(4, t, k, a, m)
         vp = precision > -1
         vr = recall > -1
         tab = torch.stack([
