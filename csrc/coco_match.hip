@@ -30,6 +30,7 @@
 #include "common.h"
 
 #include <algorithm>
+#include <climits>
 #include <limits>
 
 namespace tmx {
@@ -213,7 +214,12 @@ __global__ __launch_bounds__(1024) void coco_accumulate_kernel(
   __syncthreads();
 
   const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);  // lanes <= this one
-  int64_t nd = 0, tp_run = 0, fp_run = 0, first = -1;
+  // 32-bit counts (a class segment holds < 2^31 rows: checked by the host) -- the TP branch is the kernel's VALU bill:
+  // int64 -> double conversions and an int64 division for the bucket guess cost dozens of instructions each
+  const int maxd32 = static_cast<int>(min(maxd, static_cast<int64_t>(INT_MAX)));
+  const double guess_scale = static_cast<double>(R - 1) / static_cast<double>(npig);
+  int nd = 0, tp_run = 0, fp_run = 0;
+  int64_t first = -1;
   for (int64_t base = s; base < e; base += kAccBatch * kWave) {
     bool in[kAccBatch];
     int32_t rk[kAccBatch];
@@ -228,7 +234,7 @@ __global__ __launch_bounds__(1024) void coco_accumulate_kernel(
     }
 #pragma unroll
     for (int u = 0; u < kAccBatch; ++u) {
-      const bool valid = in[u] && rk[u] < maxd;
+      const bool valid = in[u] && rk[u] < maxd32;
       const bool m1 = (mt[u] >> bit) & 1ull, i1 = (ig[u] >> bit) & 1ull;
       const bool tp = valid && m1 && !i1;
       const uint64_t vb = __ballot(valid), tb = __ballot(tp), fb = __ballot(valid && !m1 && !i1);
@@ -236,12 +242,13 @@ __global__ __launch_bounds__(1024) void coco_accumulate_kernel(
       nd += __builtin_popcountll(vb);
       if (tb) {  // (wave-uniform) this chunk holds TPs: their precisions, bucketed by TP count
         if (tp) {
-          const int64_t tp_sum = tp_run + __builtin_popcountll(tb & upto);
-          const int64_t fp_sum = fp_run + __builtin_popcountll(fb & upto);
-          const double prec = static_cast<double>(tp_sum) / (static_cast<double>(fp_sum) + static_cast<double>(tp_sum) + eps);
+          const int tp_sum = tp_run + __builtin_popcountll(tb & upto);
+          const int fp_sum = fp_run + __builtin_popcountll(fb & upto);
+          const double tpd = static_cast<double>(tp_sum);
+          const double prec = tpd / (static_cast<double>(fp_sum) + tpd + eps);
           // upper_bound(ctab, tp_sum): start where evenly spaced thresholds would put it, then walk (a step or
           // two for the usual linspace; a dependent binary search was the kernel's longest latency chain)
-          int lo_r = static_cast<int>(min(static_cast<int64_t>(R), tp_sum * (R - 1) / npig + 1));
+          int lo_r = min(R, static_cast<int>(tpd * guess_scale) + 1);
           while (lo_r < R && ctab[lo_r] <= tp_sum) ++lo_r;
           while (lo_r > 0 && ctab[lo_r - 1] > tp_sum) --lo_r;
           if (lo_r > 0) {
@@ -754,6 +761,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tenso
   const auto seg = at::searchsorted(d_cls.index_select(0, acc).contiguous(), at::arange(K + 1, lopt), false, false);
 
   // ---- 4. accumulate -----------------------------------------------------------------------------------
+  TORCH_CHECK(det_scores.numel() < (int64_t(1) << 31), "COCO evaluator: at most 2^31 - 1 detections");
   const int64_t combos = K * A * M * T;
   coco_accumulate_kernel<<<static_cast<unsigned>(combos / acc_wpb(T)), acc_wpb(T) * kWave, acc_lds_bytes(T, R), stream()>>>(
       seg.data_ptr<int64_t>(), static_cast<int>(K), static_cast<int>(A), static_cast<int>(M), static_cast<int>(T),
@@ -904,6 +912,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> coco_evaluate_gpu_img
         score32.data_ptr<float>(), a_rank, a_matched, a_ignored, a_score.data_ptr<double>(), seg);
     TMX_LAUNCH_CHECK();
   }
+  TORCH_CHECK(n < (int64_t(1) << 31), "coco_evaluate_gpu_img: at most 2^31 - 1 detections");
   const int64_t combos = K * A * M * T;
   coco_accumulate_kernel<<<static_cast<unsigned>(combos / acc_wpb(T)), acc_wpb(T) * kWave, acc_lds_bytes(T, R), stream()>>>(
       seg, static_cast<int>(K), static_cast<int>(A), static_cast<int>(M), static_cast<int>(T), static_cast<int>(R),
