@@ -24,6 +24,11 @@
 //      threshold at the detection where the prefix TP first reaches ceil(thr * npig) - the same element
 //      np.searchsorted(rc, thr, side="left") finds, computed with the same double arithmetic.
 //
+// Per-image route (bbox IoU, fp32-exact scores, <= 256 detections and ground truths per image: the module's default
+// for COCO-style data, tmx::coco_evaluate_gpu_img): steps 1-2 run as one workgroup per image (coco_image_match_kernel:
+// rows staged in LDS, ordered and ranked by 64-bit keys, class runs matched by the image's waves), non-ignored
+// ground-truth counts come from an LDS-aggregated kernel, and step 3 sorts the detection rows directly.
+//
 // Limits of the GPU path (the caller falls back to the C++ evaluator beyond them): T * A <= 64,
 // <= 1024 ground-truth boxes per (image, class) pair (a device flag, output 5, read with the caller's results),
 // <= 256 recall thresholds.
@@ -306,9 +311,9 @@ __device__ __forceinline__ uint32_t coco_score_okey(float f) {  // fp32 bits -> 
 
 __global__ __launch_bounds__(kImgThreads) void coco_image_match_kernel(
     const int64_t* __restrict__ det_off, const int64_t* __restrict__ gt_off, const double* __restrict__ dbox,
-    const float* __restrict__ dscore, const int64_t* __restrict__ dcls, const double* __restrict__ darea,
-    const double* __restrict__ gbox, const int64_t* __restrict__ gcls, const int64_t* __restrict__ gcrowd,
-    const double* __restrict__ garea, const double* __restrict__ iou_thr, int T, const double* __restrict__ area_rng,
+    const float* __restrict__ dscore, const int64_t* __restrict__ dcls, const double* __restrict__ gbox,
+    const int64_t* __restrict__ gcls, const int64_t* __restrict__ gcrowd, const double* __restrict__ garea,
+    const double* __restrict__ iou_thr, int T, const double* __restrict__ area_rng,
     int A, int64_t max_det_last, int32_t* __restrict__ rank_out, uint64_t* __restrict__ matched_out,
     uint64_t* __restrict__ ignored_out, int64_t* __restrict__ overflow, int probe) {
   __shared__ uint64_t s_dkey[kImgMaxRows];  // class << 32 | ~score key: ascending = (class, score desc)
@@ -889,7 +894,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> coco_evaluate_gpu_img
   if (I > 0) {
     coco_image_match_kernel<<<static_cast<unsigned>(I), kImgThreads, 0, stream()>>>(
         det_off.data_ptr<int64_t>(), gt_off.data_ptr<int64_t>(), det_boxes.data_ptr<double>(), score32.data_ptr<float>(),
-        det_cls.data_ptr<int64_t>(), nullptr, gt_boxes.data_ptr<double>(), gt_cls.data_ptr<int64_t>(),
+        det_cls.data_ptr<int64_t>(), gt_boxes.data_ptr<double>(), gt_cls.data_ptr<int64_t>(),
         gt_crowd.data_ptr<int64_t>(), gt_area.data_ptr<double>(), iou_thrs.data_ptr<double>(), static_cast<int>(T),
         area_rng.data_ptr<double>(), static_cast<int>(A), max_det_last, rank, matched, ignored, overflow.data_ptr<int64_t>(), probe);
     TMX_LAUNCH_CHECK();
