@@ -518,3 +518,24 @@ def test_map_ddp_matches_single_process():
     for res in got:
         for k, v in exp.items():
             np.testing.assert_allclose(np.asarray(res[k], dtype=np.float64), v.double().numpy(), atol=1e-6, err_msg=k)
+
+
+@pytest.mark.parametrize("backend", ["pycocotools", "faster_coco_eval"])
+@pytest.mark.parametrize("md", [[1, 10, 100], [1, 10, 50], [5]])
+def test_map_per_class_stats_vectorised_equal_loop(backend, md):
+    """class_metrics: the per-class map / mar_100 of all classes at once (``_per_class_stats``) equal the per-class
+    ``_summarize_tables(tab, k)`` statistics they replace (float32 outputs)."""
+    import numpy as np
+
+    from torchmetrics_forked_amd.detection import MeanAveragePrecision
+
+    rng = np.random.default_rng(len(md))
+    m = MeanAveragePrecision(backend=backend, max_detection_thresholds=md)
+    T, K, A, M = 10, 17, 4, len(md)
+    tab = rng.random((4, T, K, A, M)) * 5
+    tab[1] = np.floor(tab[1])
+    tab[1][rng.random((T, K, A, M)) < 0.3] = 0
+    tab[3] = (tab[3] > 2.5).astype(float)
+    got_map, got_mar = m._per_class_stats(tab)
+    assert torch.equal(got_map, torch.tensor([m._summarize_tables(tab, k)[0] for k in range(K)], dtype=torch.float32))
+    assert torch.equal(got_mar, torch.tensor([m._summarize_tables(tab, k)[8] for k in range(K)], dtype=torch.float32))

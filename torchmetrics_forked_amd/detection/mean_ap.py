@@ -761,6 +761,24 @@ class MeanAveragePrecision(Metric):
             stat(False, area=3, max_det=last),
         ]
 
+    def _per_class_stats(self, tab: np.ndarray) -> Tuple[Tensor, Tensor]:
+        """``map`` (stats[0]) and ``mar_100`` (stats[8]) of every class at once from ``_summary_tables``: the same
+        selections as ``_summarize_tables(tab, k)`` reduced over the IoU thresholds / maxDets axes for all classes in two
+        numpy reductions each, instead of twelve statistics per class in a Python loop (10 ms at 80 classes)."""
+        md = self.max_detection_thresholds
+        last = md[2] if len(md) > 2 else md[-1]
+        first_map = 100 if self.backend == "pycocotools" else md[-1]
+
+        def per_class(base: int, max_det: int) -> Tensor:
+            mind = [i for i, m in enumerate(md) if m == max_det]
+            sub = tab[base : base + 2, :, :, 0][..., mind]  # [2, T, K, len(mind)]
+            total, count = sub[0].sum(axis=(0, 2)), sub[1].sum(axis=(0, 2))
+            with np.errstate(divide="ignore", invalid="ignore"):
+                val = np.where(count > 0, total / np.where(count > 0, count, 1.0), -1.0)
+            return torch.from_numpy(val.astype(np.float32))
+
+        return per_class(0, first_map), per_class(2, last)
+
     def _summarize(self, precision: Tensor, recall: Tensor) -> List[float]:
         """COCO ``summarize()`` statistics from accumulated ``precision [T,R,K,A,M]`` / ``recall [T,K,A,M]``."""
         return self._summarize_tables(self._summary_tables(precision, recall))
@@ -814,13 +832,7 @@ class MeanAveragePrecision(Metric):
                     if tab is None:
                         ev = self._evaluate_host(i_type, "macro", classes)
                         tab = self._summary_tables(ev.precision, ev.recall)
-                map_pc, mar_pc = [], []
-                for k in range(len(classes)):
-                    st = self._summarize_tables(tab, k)
-                    map_pc.append(st[0])
-                    mar_pc.append(st[8])
-                map_pc_t = torch.tensor(map_pc, dtype=torch.float32)
-                mar_pc_t = torch.tensor(mar_pc, dtype=torch.float32)
+                map_pc_t, mar_pc_t = self._per_class_stats(tab)
             else:
                 map_pc_t = torch.tensor([-1], dtype=torch.float32)
                 mar_pc_t = torch.tensor([-1], dtype=torch.float32)
