@@ -311,6 +311,44 @@ __global__ __launch_bounds__(kLpipsThreads) void lpips_head_kernel(const T* __re
   }
 }
 
+// channels_last feature maps ([B][H·W][C] in memory, what a channels_last trunk produces): the same sums, each thread
+// walking its pixel's C contiguous channels (no layout copy of the feature maps before the head)
+template <typename T>
+__global__ __launch_bounds__(kLpipsThreads) void lpips_head_nhwc_kernel(const T* __restrict__ f0, const T* __restrict__ f1,
+                                                                        const float* __restrict__ w, int C, int64_t HW,
+                                                                        double* __restrict__ partial) {
+  const int64_t b = blockIdx.y;
+  const int64_t s = static_cast<int64_t>(blockIdx.x) * kLpipsThreads + threadIdx.x;
+  double v = 0.0;
+  if (s < HW) {
+    const T* p0 = f0 + (b * HW + s) * C;
+    const T* p1 = f1 + (b * HW + s) * C;
+    float n0 = 0.f, n1 = 0.f, s00 = 0.f, s11 = 0.f, s01 = 0.f;
+    for (int c = 0; c < C; ++c) {
+      const float x = to_f32<T>(p0[c]);
+      const float y = to_f32<T>(p1[c]);
+      const float wc = w[c];
+      n0 = fmaf(x, x, n0);
+      n1 = fmaf(y, y, n1);
+      s00 = fmaf(wc * x, x, s00);
+      s11 = fmaf(wc * y, y, s11);
+      s01 = fmaf(wc * x, y, s01);
+    }
+    const float a2 = 1e-8f + n0, b2 = 1e-8f + n1;
+    v = static_cast<double>(s00 / a2 + s11 / b2 - 2.f * s01 / (sqrtf(a2) * sqrtf(b2)));
+  }
+  v = wave_sum(v);
+  __shared__ double red[kLpipsThreads / kWave];
+  const int wave = threadIdx.x / kWave;
+  if ((threadIdx.x & (kWave - 1)) == 0) red[wave] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int i = 0; i < kLpipsThreads / kWave; ++i) t += red[i];
+    partial[b * gridDim.x + blockIdx.x] = t;
+  }
+}
+
 // f0/f1 [B, C, H, W]; w [C] (1×1 conv weight). Returns fp64 [B] spatial means of the weighted normalised distance.
 at::Tensor lpips_head(const at::Tensor& f0_in, const at::Tensor& f1_in, const at::Tensor& w_in) {
   TORCH_CHECK(f0_in.is_cuda() && f1_in.is_cuda(), "lpips_head: expected GPU tensors");
@@ -318,8 +356,11 @@ at::Tensor lpips_head(const at::Tensor& f0_in, const at::Tensor& f1_in, const at
   TORCH_CHECK(f0_in.scalar_type() == f1_in.scalar_type(), "lpips_head: dtype mismatch");
   TORCH_CHECK(w_in.numel() == f0_in.size(1), "lpips_head: weight / channel mismatch");
   const at::DeviceGuard guard(f0_in.device());
-  auto f0 = f0_in.contiguous();
-  auto f1 = f1_in.contiguous();
+  // channels_last inputs (a channels_last trunk) are read in place by the NHWC kernel
+  const bool nhwc = !f0_in.is_contiguous() && f0_in.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                    f1_in.is_contiguous(at::MemoryFormat::ChannelsLast);
+  auto f0 = nhwc ? f0_in : f0_in.contiguous();
+  auto f1 = nhwc ? f1_in : f1_in.contiguous();
   auto w = w_in.reshape(-1).to(at::kFloat).contiguous();
   const int64_t B = f0.size(0), C = f0.size(1), HW = f0.size(2) * f0.size(3);
   auto opts = f0.options().dtype(at::kDouble);
@@ -328,9 +369,14 @@ at::Tensor lpips_head(const at::Tensor& f0_in, const at::Tensor& f1_in, const at
   dim3 grid(static_cast<unsigned>((HW + kLpipsThreads - 1) / kLpipsThreads), static_cast<unsigned>(B));
   auto partial = at::empty({B, static_cast<int64_t>(grid.x)}, opts);
   TMX_DISPATCH_FLOAT(f0.scalar_type(), "lpips_head", [&] {
-    hipLaunchKernelGGL((lpips_head_kernel<scalar_t>), grid, kLpipsThreads, 0, stream(),
-                       reinterpret_cast<const scalar_t*>(f0.data_ptr()), reinterpret_cast<const scalar_t*>(f1.data_ptr()),
-                       w.data_ptr<float>(), static_cast<int>(C), HW, partial.data_ptr<double>());
+    if (nhwc)
+      hipLaunchKernelGGL((lpips_head_nhwc_kernel<scalar_t>), grid, kLpipsThreads, 0, stream(),
+                         reinterpret_cast<const scalar_t*>(f0.data_ptr()), reinterpret_cast<const scalar_t*>(f1.data_ptr()),
+                         w.data_ptr<float>(), static_cast<int>(C), HW, partial.data_ptr<double>());
+    else
+      hipLaunchKernelGGL((lpips_head_kernel<scalar_t>), grid, kLpipsThreads, 0, stream(),
+                         reinterpret_cast<const scalar_t*>(f0.data_ptr()), reinterpret_cast<const scalar_t*>(f1.data_ptr()),
+                         w.data_ptr<float>(), static_cast<int>(C), HW, partial.data_ptr<double>());
   });
   TMX_LAUNCH_CHECK();
   return partial.sum(1) / static_cast<double>(HW);

@@ -27,6 +27,10 @@ _SLICES = {
 }
 _CHANNELS = {"alex": [64, 192, 384, 256, 256], "vgg": [64, 128, 256, 512, 512], "squeeze": [64, 128, 256, 384, 384, 512, 512]}
 _FEATURES = {"alex": alexnet_features, "vgg": vgg16_features, "squeeze": squeezenet1_1_features}
+# channels_last trunk on the fused GPU path: opt-in (TMX_LPIPS_CHANNELS_LAST=1).  The VGG16 trunk alone is faster in
+# channels_last (16 x 3 x 1024^2: 92.6 vs 101.1 ms, tools/lpips_layout_probe.py) but BASELINE config 4 end to end is
+# slower (0.250 vs 0.304 updates/s, gpurun r7v: the NHWC head and the input conversions cost more than MIOpen saves)
+_CHANNELS_LAST = os.environ.get("TMX_LPIPS_CHANNELS_LAST", "0") == "1"
 # LPIPS v0.1 linear heads (``tools/convert_lpips_heads.py`` from the reference's lpips_models/*.pth): the default for
 # ``pretrained=True``, as in the reference (``functional/image/lpips.py:318-325``)
 _HEADS_FILE = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))), "models", "lpips_heads.safetensors")
@@ -181,9 +185,17 @@ class _LPIPS(nn.Module):
         x0, x1 = self.scaling_layer(in0), self.scaling_layer(in1)
         if self.resize is not None:
             x0, x1 = _resize_tensor(x0, size=self.resize), _resize_tensor(x1, size=self.resize)
-        outs0, outs1 = self.net(x0), self.net(x1)
         grad = torch.is_grad_enabled() and (in0.requires_grad or in1.requires_grad or any(p.requires_grad for p in self.parameters()))
-        fused = (not self.spatial) and outs0[0].is_cuda and not grad and not self.training and ops.use_native(outs0[0])
+        fused = (not self.spatial) and x0.is_cuda and not grad and not self.training and ops.use_native(x0)
+        if fused and _CHANNELS_LAST and x0.dim() == 4:
+            # (opt-in, see _CHANNELS_LAST) channels_last trunk: MIOpen's NHWC convolutions without its layout
+            # transposes; the head reads the channels_last feature maps in place (tmx::lpips_head)
+            if not self.__dict__.get("_trunk_cl"):
+                self.net.to(memory_format=torch.channels_last)
+                self.__dict__["_trunk_cl"] = True
+            x0 = x0.contiguous(memory_format=torch.channels_last)
+            x1 = x1.contiguous(memory_format=torch.channels_last)
+        outs0, outs1 = self.net(x0), self.net(x1)
         res = []
         for kk in range(self.L):
             if fused:
