@@ -349,6 +349,56 @@ __global__ __launch_bounds__(kLpipsThreads) void lpips_head_nhwc_kernel(const T*
   }
 }
 
+// channels_last, C % 4 == 0, 16-B aligned: four threads per pixel read adjacent float4s of its channel row (a wave covers
+// 16 pixels x 64 B per load instead of 64 pixels x 4 B at stride C), then two xor-shuffle steps combine the four
+// partial sums.  (The per-thread walk above ran at 9.4 ms per call on VGG16's first tap: gpurun r7w.)
+constexpr int kLpipsPixPerBlock = kLpipsThreads / 4;
+
+__global__ __launch_bounds__(kLpipsThreads) void lpips_head_nhwc4_kernel(const float* __restrict__ f0, const float* __restrict__ f1,
+                                                                         const float* __restrict__ w, int C, int64_t HW,
+                                                                         double* __restrict__ partial) {
+  const int64_t b = blockIdx.y;
+  const int q = threadIdx.x & 3;
+  const int64_t s = static_cast<int64_t>(blockIdx.x) * kLpipsPixPerBlock + (threadIdx.x >> 2);
+  float n0 = 0.f, n1 = 0.f, s00 = 0.f, s11 = 0.f, s01 = 0.f;
+  if (s < HW) {
+    const float4* p0 = reinterpret_cast<const float4*>(f0 + (b * HW + s) * C);
+    const float4* p1 = reinterpret_cast<const float4*>(f1 + (b * HW + s) * C);
+    const float4* w4 = reinterpret_cast<const float4*>(w);
+    for (int k = q; k < C / 4; k += 4) {
+      const float4 x = p0[k], y = p1[k], wc = w4[k];
+      n0 = fmaf(x.x, x.x, fmaf(x.y, x.y, fmaf(x.z, x.z, fmaf(x.w, x.w, n0))));
+      n1 = fmaf(y.x, y.x, fmaf(y.y, y.y, fmaf(y.z, y.z, fmaf(y.w, y.w, n1))));
+      s00 = fmaf(wc.x * x.x, x.x, fmaf(wc.y * x.y, x.y, fmaf(wc.z * x.z, x.z, fmaf(wc.w * x.w, x.w, s00))));
+      s11 = fmaf(wc.x * y.x, y.x, fmaf(wc.y * y.y, y.y, fmaf(wc.z * y.z, y.z, fmaf(wc.w * y.w, y.w, s11))));
+      s01 = fmaf(wc.x * x.x, y.x, fmaf(wc.y * x.y, y.y, fmaf(wc.z * x.z, y.z, fmaf(wc.w * x.w, y.w, s01))));
+    }
+  }
+#pragma unroll
+  for (int off = 1; off < 4; off <<= 1) {  // (every lane takes part: the shuffles stay uniform)
+    n0 += __shfl_xor(n0, off, 4);
+    n1 += __shfl_xor(n1, off, 4);
+    s00 += __shfl_xor(s00, off, 4);
+    s11 += __shfl_xor(s11, off, 4);
+    s01 += __shfl_xor(s01, off, 4);
+  }
+  double v = 0.0;
+  if (q == 0 && s < HW) {
+    const float a2 = 1e-8f + n0, b2 = 1e-8f + n1;
+    v = static_cast<double>(s00 / a2 + s11 / b2 - 2.f * s01 / (sqrtf(a2) * sqrtf(b2)));
+  }
+  v = wave_sum(v);
+  __shared__ double red[kLpipsThreads / kWave];
+  const int wave = threadIdx.x / kWave;
+  if ((threadIdx.x & (kWave - 1)) == 0) red[wave] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int i = 0; i < kLpipsThreads / kWave; ++i) t += red[i];
+    partial[b * gridDim.x + blockIdx.x] = t;
+  }
+}
+
 // f0/f1 [B, C, H, W]; w [C] (1×1 conv weight). Returns fp64 [B] spatial means of the weighted normalised distance.
 at::Tensor lpips_head(const at::Tensor& f0_in, const at::Tensor& f1_in, const at::Tensor& w_in) {
   TORCH_CHECK(f0_in.is_cuda() && f1_in.is_cuda(), "lpips_head: expected GPU tensors");
@@ -366,8 +416,17 @@ at::Tensor lpips_head(const at::Tensor& f0_in, const at::Tensor& f1_in, const at
   auto opts = f0.options().dtype(at::kDouble);
   if (B == 0 || HW == 0) return at::zeros({B}, opts);
   TORCH_CHECK(B <= 65535, "lpips_head: batch too large for one launch");
-  dim3 grid(static_cast<unsigned>((HW + kLpipsThreads - 1) / kLpipsThreads), static_cast<unsigned>(B));
+  const bool nhwc4 = nhwc && f0.scalar_type() == at::kFloat && C % 4 == 0 &&
+                     (reinterpret_cast<uintptr_t>(f0.data_ptr()) & 15) == 0 && (reinterpret_cast<uintptr_t>(f1.data_ptr()) & 15) == 0;
+  const int64_t per_block = nhwc4 ? kLpipsPixPerBlock : kLpipsThreads;
+  dim3 grid(static_cast<unsigned>((HW + per_block - 1) / per_block), static_cast<unsigned>(B));
   auto partial = at::empty({B, static_cast<int64_t>(grid.x)}, opts);
+  if (nhwc4) {  // (w is a fresh contiguous fp32 tensor: 16-B aligned)
+    hipLaunchKernelGGL(lpips_head_nhwc4_kernel, grid, kLpipsThreads, 0, stream(), f0.data_ptr<float>(), f1.data_ptr<float>(),
+                       w.data_ptr<float>(), static_cast<int>(C), HW, partial.data_ptr<double>());
+    TMX_LAUNCH_CHECK();
+    return partial.sum(1) / static_cast<double>(HW);
+  }
   TMX_DISPATCH_FLOAT(f0.scalar_type(), "lpips_head", [&] {
     if (nhwc)
       hipLaunchKernelGGL((lpips_head_nhwc_kernel<scalar_t>), grid, kLpipsThreads, 0, stream(),

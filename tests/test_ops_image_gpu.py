@@ -87,10 +87,11 @@ def test_lpips_fused_head_vs_eager(net, dtype):
             eager = (((_normalize_tensor(f0.float()) - _normalize_tensor(f1.float())) ** 2) * w.view(1, -1, 1, 1)).sum(1).mean((1, 2))
             tol = 1e-5 if dtype == torch.float32 else 1e-4
             assert torch.allclose(fused, eager.double().float(), rtol=1e-4, atol=tol), (fused, eager)
-            # channels_last feature maps: the NHWC kernel reads them in place, same sums (same per-pixel order)
+            # channels_last feature maps: the NHWC kernels read them in place (fp32 with C % 4 == 0: four threads per
+            # pixel, another summation order)
             cl = torch.ops.tmx.lpips_head(f0.contiguous(memory_format=torch.channels_last),
                                           f1.contiguous(memory_format=torch.channels_last), w).float()
-            assert torch.equal(cl, fused), (cl, fused)
+            assert torch.allclose(cl, fused, rtol=1e-5, atol=1e-7), (cl, fused)
         val = lp(a, b)
     assert val.shape == (3, 1, 1, 1) and torch.isfinite(val).all()
 

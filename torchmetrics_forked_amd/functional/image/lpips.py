@@ -27,10 +27,11 @@ _SLICES = {
 }
 _CHANNELS = {"alex": [64, 192, 384, 256, 256], "vgg": [64, 128, 256, 512, 512], "squeeze": [64, 128, 256, 384, 384, 512, 512]}
 _FEATURES = {"alex": alexnet_features, "vgg": vgg16_features, "squeeze": squeezenet1_1_features}
-# channels_last trunk on the fused GPU path: opt-in (TMX_LPIPS_CHANNELS_LAST=1).  The VGG16 trunk alone is faster in
-# channels_last (16 x 3 x 1024^2: 92.6 vs 101.1 ms, tools/lpips_layout_probe.py) but BASELINE config 4 end to end is
-# slower (0.250 vs 0.304 updates/s, gpurun r7v: the NHWC head and the input conversions cost more than MIOpen saves)
-_CHANNELS_LAST = os.environ.get("TMX_LPIPS_CHANNELS_LAST", "0") == "1"
+# channels_last trunk on the fused GPU path (TMX_LPIPS_CHANNELS_LAST=0 keeps NCHW): MIOpen's NHWC convolutions run
+# without its layout transposes (VGG16 trunk, 16 x 3 x 1024^2: 92.6 vs 101.1 ms, tools/lpips_layout_probe.py) and the
+# head reads the channels_last maps in place with four threads per pixel; BASELINE config 4: 0.329 vs 0.303 updates/s
+# (gpurun r7x; the first NHWC head, one thread per pixel, lost: 0.250, r7v / r7w)
+_CHANNELS_LAST = os.environ.get("TMX_LPIPS_CHANNELS_LAST", "1") != "0"
 # LPIPS v0.1 linear heads (``tools/convert_lpips_heads.py`` from the reference's lpips_models/*.pth): the default for
 # ``pretrained=True``, as in the reference (``functional/image/lpips.py:318-325``)
 _HEADS_FILE = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))), "models", "lpips_heads.safetensors")
@@ -188,8 +189,8 @@ class _LPIPS(nn.Module):
         grad = torch.is_grad_enabled() and (in0.requires_grad or in1.requires_grad or any(p.requires_grad for p in self.parameters()))
         fused = (not self.spatial) and x0.is_cuda and not grad and not self.training and ops.use_native(x0)
         if fused and _CHANNELS_LAST and x0.dim() == 4:
-            # (opt-in, see _CHANNELS_LAST) channels_last trunk: MIOpen's NHWC convolutions without its layout
-            # transposes; the head reads the channels_last feature maps in place (tmx::lpips_head)
+            # channels_last trunk (see _CHANNELS_LAST): MIOpen's NHWC convolutions without its layout transposes; the
+            # head reads the channels_last feature maps in place (tmx::lpips_head)
             if not self.__dict__.get("_trunk_cl"):
                 self.net.to(memory_format=torch.channels_last)
                 self.__dict__["_trunk_cl"] = True
